@@ -1,0 +1,348 @@
+// hipps — dense flat-buffer kernels: wire cast/pack, rank-ordered aggregate, fused optimizers.
+//
+// Reference parity:
+//   K4  d_p = sum(grads)               ps.py:176       -> k_aggregate (fixed rank order, fp32 acc)
+//   K5  SGD wd/momentum/nesterov/update ps.py:197-214  -> k_sgd   (one pass, fused with K4)
+//   K6  Adam (reference eps placement)  ps.py:217-261  -> k_adam  (one pass, fused with K4)
+//   K1/K2/K3 host staging + float cast  mpi_comms.py:32-58 -> k_convert (device-resident wire)
+//
+// All kernels are HBM-bound streams: 16-byte (fp32x4) or 8-byte (bf16x4) vector accesses per
+// lane, grid capped at 8 blocks/CU with a grid-stride loop (cdna_hip_programming.md G11/G13).
+#include "common.h"
+
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+namespace hipps {
+
+// ------------------------------------------------------------------------------------------
+// element ops (scalar form; the vector loops apply them lane-wise).  fmaf mirrors ATen's
+// add_(alpha, other) == fma(other, alpha, self) so results track torch to ~1 ulp.
+// ------------------------------------------------------------------------------------------
+struct SgdHp {
+  float lr, wd, mom, damp;
+  int nesterov, first;
+};
+
+__device__ __forceinline__ float sgd1(float& p, float& b, float d, const SgdHp& h, bool has_buf) {
+  if (h.wd != 0.f) d = fmaf(h.wd, p, d);
+  if (h.mom != 0.f && has_buf) {
+    b = h.first ? d : fmaf(1.f - h.damp, d, b * h.mom);
+    d = h.nesterov ? fmaf(h.mom, b, d) : b;
+  }
+  p = fmaf(-h.lr, d, p);
+  return p;
+}
+
+struct AdamHp {
+  float lr, b1, b2, eps, wd, step_size, bc2_sqrt;
+  int amsgrad, torch_mode;
+};
+
+__device__ __forceinline__ float adam1(float& p, float& m, float& v, float* vmax, float g, const AdamHp& h) {
+  if (h.wd != 0.f) g = fmaf(h.wd, p, g);
+  m = fmaf(1.f - h.b1, g, m * h.b1);
+  v = fmaf((1.f - h.b2) * g, g, v * h.b2);
+  float vv = v;
+  if (h.amsgrad) {
+    vv = fmaxf(*vmax, v);
+    *vmax = vv;
+  }
+  // reference (ps.py:255): denom = sqrt(v) + eps, step_size = lr*sqrt(bc2)/bc1
+  // torch   (>=1.0)       : denom = sqrt(v)/sqrt(bc2) + eps, step_size = lr/bc1
+  float denom = h.torch_mode ? (sqrtf(vv) / h.bc2_sqrt + h.eps) : (sqrtf(vv) + h.eps);
+  p = fmaf(-h.step_size, m / denom, p);
+  return p;
+}
+
+template <typename T>
+__device__ __forceinline__ float4 sum_slots4(const SlotPtrs& g, int W, int64_t i, float gscale) {
+  float4 d = Vec4<T>::load(reinterpret_cast<const T*>(g.p[0]), i);
+  for (int w = 1; w < W; ++w) {  // fixed rank order -> bitwise identical on every rank
+    float4 s = Vec4<T>::load(reinterpret_cast<const T*>(g.p[w]), i);
+    d.x += s.x; d.y += s.y; d.z += s.z; d.w += s.w;
+  }
+  if (gscale != 1.f) { d.x *= gscale; d.y *= gscale; d.z *= gscale; d.w *= gscale; }
+  return d;
+}
+template <typename T>
+__device__ __forceinline__ float sum_slots1(const SlotPtrs& g, int W, int64_t i, float gscale) {
+  float d = Vec4<T>::load1(reinterpret_cast<const T*>(g.p[0]), i);
+  for (int w = 1; w < W; ++w) d += Vec4<T>::load1(reinterpret_cast<const T*>(g.p[w]), i);
+  return gscale != 1.f ? d * gscale : d;
+}
+
+__device__ __forceinline__ void pub_store4(void* pub, int pub_mode, int64_t i, float4 v) {
+  if (pub_mode == 1) Vec4<float>::store(reinterpret_cast<float*>(pub), i, v);
+  else if (pub_mode == 2) Vec4<uint16_t>::store(reinterpret_cast<uint16_t*>(pub), i, v);
+}
+__device__ __forceinline__ void pub_store1(void* pub, int pub_mode, int64_t i, float v) {
+  if (pub_mode == 1) reinterpret_cast<float*>(pub)[i] = v;
+  else if (pub_mode == 2) reinterpret_cast<uint16_t*>(pub)[i] = f32_to_bf16(v);
+}
+
+// ------------------------------------------------------------------------------------------
+// k_aggregate: acc = (accumulate ? acc : 0) + gscale * sum_w slot_w
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_aggregate(SlotPtrs g, int W, float gscale, float* __restrict__ acc,
+                                                      int64_t n, int accumulate) {
+  const int64_t nv = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+    const int64_t i = v << 2;
+    float4 d = sum_slots4<T>(g, W, i, gscale);
+    if (accumulate) {
+      float4 a = Vec4<float>::load(acc, i);
+      d.x += a.x; d.y += a.y; d.z += a.z; d.w += a.w;
+    }
+    Vec4<float>::store(acc, i, d);
+  }
+  if (blockIdx.x == 0) {
+    for (int64_t i = (nv << 2) + threadIdx.x; i < n; i += blockDim.x) {
+      float d = sum_slots1<T>(g, W, i, gscale);
+      acc[i] = accumulate ? acc[i] + d : d;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_convert: dst(Tout) = scale * src(Tin)   (f32->bf16 wire pack, bf16->f32 unpack, copies)
+// ------------------------------------------------------------------------------------------
+template <typename Tin, typename Tout>
+__global__ __launch_bounds__(kBlock) void k_convert(const Tin* __restrict__ src, Tout* __restrict__ dst, int64_t n,
+                                                    float scale) {
+  const int64_t nv = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+    const int64_t i = v << 2;
+    float4 d = Vec4<Tin>::load(src, i);
+    if (scale != 1.f) { d.x *= scale; d.y *= scale; d.z *= scale; d.w *= scale; }
+    Vec4<Tout>::store(dst, i, d);
+  }
+  if (blockIdx.x == 0) {
+    for (int64_t i = (nv << 2) + threadIdx.x; i < n; i += blockDim.x)
+      Vec4<Tout>::store1(dst, i, Vec4<Tin>::load1(src, i) * scale);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_sgd: decode + sum_W + weight decay + momentum/nesterov + update + publish, one pass.
+// zero_src: when the gradient source is a single fp32 accumulator, clear it in the same pass
+// (the async PS re-arms its accumulator without a separate memset).
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_sgd(SlotPtrs g, int W, float gscale, float* __restrict__ p,
+                                                float* __restrict__ buf, void* __restrict__ pub, int pub_mode,
+                                                int zero_src, int64_t n, SgdHp h) {
+  const bool has_buf = buf != nullptr;
+  const int64_t nv = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+    const int64_t i = v << 2;
+    float4 d = sum_slots4<T>(g, W, i, gscale);
+    if (zero_src) Vec4<float>::store((float*)g.p[0], i, make_float4(0.f, 0.f, 0.f, 0.f));
+    float4 pv = Vec4<float>::load(p, i);
+    float4 b = has_buf && !h.first ? Vec4<float>::load(buf, i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    sgd1(pv.x, b.x, d.x, h, has_buf);
+    sgd1(pv.y, b.y, d.y, h, has_buf);
+    sgd1(pv.z, b.z, d.z, h, has_buf);
+    sgd1(pv.w, b.w, d.w, h, has_buf);
+    Vec4<float>::store(p, i, pv);
+    if (has_buf && h.mom != 0.f) Vec4<float>::store(buf, i, b);
+    pub_store4(pub, pub_mode, i, pv);
+  }
+  if (blockIdx.x == 0) {
+    for (int64_t i = (nv << 2) + threadIdx.x; i < n; i += blockDim.x) {
+      float d = sum_slots1<T>(g, W, i, gscale);
+      if (zero_src) ((float*)g.p[0])[i] = 0.f;
+      float pv = p[i];
+      float b = has_buf && !h.first ? buf[i] : 0.f;
+      sgd1(pv, b, d, h, has_buf);
+      p[i] = pv;
+      if (has_buf && h.mom != 0.f) buf[i] = b;
+      pub_store1(pub, pub_mode, i, pv);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_adam(SlotPtrs g, int W, float gscale, float* __restrict__ p,
+                                                 float* __restrict__ m, float* __restrict__ vv,
+                                                 float* __restrict__ vmax, void* __restrict__ pub, int pub_mode,
+                                                 int zero_src, int64_t n, AdamHp h) {
+  const int64_t nv = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
+  float dummy = 0.f;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+    const int64_t i = v << 2;
+    float4 d = sum_slots4<T>(g, W, i, gscale);
+    if (zero_src) Vec4<float>::store((float*)g.p[0], i, make_float4(0.f, 0.f, 0.f, 0.f));
+    float4 pv = Vec4<float>::load(p, i), mv = Vec4<float>::load(m, i), sv = Vec4<float>::load(vv, i);
+    float4 xv = h.amsgrad ? Vec4<float>::load(vmax, i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    adam1(pv.x, mv.x, sv.x, &xv.x, d.x, h);
+    adam1(pv.y, mv.y, sv.y, &xv.y, d.y, h);
+    adam1(pv.z, mv.z, sv.z, &xv.z, d.z, h);
+    adam1(pv.w, mv.w, sv.w, &xv.w, d.w, h);
+    Vec4<float>::store(p, i, pv);
+    Vec4<float>::store(m, i, mv);
+    Vec4<float>::store(vv, i, sv);
+    if (h.amsgrad) Vec4<float>::store(vmax, i, xv);
+    pub_store4(pub, pub_mode, i, pv);
+  }
+  if (blockIdx.x == 0) {
+    for (int64_t i = (nv << 2) + threadIdx.x; i < n; i += blockDim.x) {
+      float d = sum_slots1<T>(g, W, i, gscale);
+      if (zero_src) ((float*)g.p[0])[i] = 0.f;
+      float pv = p[i], mv = m[i], sv = vv[i];
+      float* xp = h.amsgrad ? &vmax[i] : &dummy;
+      adam1(pv, mv, sv, xp, d, h);
+      p[i] = pv; m[i] = mv; vv[i] = sv;
+      pub_store1(pub, pub_mode, i, pv);
+    }
+  }
+}
+
+// ==========================================================================================
+// host launchers
+// ==========================================================================================
+namespace {
+
+void check_dev(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a device (HIP) tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+enum class WireT { F32, BF16 };
+
+WireT wire_of(const at::Tensor& t) {
+  if (t.scalar_type() == at::kFloat) return WireT::F32;
+  if (t.scalar_type() == at::kBFloat16) return WireT::BF16;
+  TORCH_CHECK(false, "wire dtype must be float32 or bfloat16, got ", t.scalar_type());
+}
+
+SlotPtrs make_slots(const std::vector<at::Tensor>& slots, int64_t n, WireT& wt) {
+  TORCH_CHECK(!slots.empty() && (int)slots.size() <= kMaxSlots, "1..", kMaxSlots, " gradient sources required");
+  SlotPtrs s{};
+  wt = wire_of(slots[0]);
+  for (size_t w = 0; w < slots.size(); ++w) {
+    check_dev(slots[w], "grad source");
+    TORCH_CHECK(wire_of(slots[w]) == wt, "all gradient sources must share one dtype");
+    TORCH_CHECK(slots[w].numel() == n, "gradient source ", w, " has ", slots[w].numel(), " elements, expected ", n);
+    s.p[w] = slots[w].data_ptr();
+  }
+  return s;
+}
+
+int pub_mode_of(const c10::optional<at::Tensor>& pub, int64_t n) {
+  if (!pub.has_value() || !pub->defined()) return 0;
+  check_dev(*pub, "publish");
+  TORCH_CHECK(pub->numel() == n, "publish buffer size mismatch");
+  return wire_of(*pub) == WireT::F32 ? 1 : 2;
+}
+
+}  // namespace
+
+void aggregate(const std::vector<at::Tensor>& slots, at::Tensor acc, double gscale, bool accumulate) {
+  check_dev(acc, "acc");
+  TORCH_CHECK(acc.scalar_type() == at::kFloat, "acc must be float32");
+  const int64_t n = acc.numel();
+  WireT wt;
+  SlotPtrs s = make_slots(slots, n, wt);
+  auto stream = c10::hip::getCurrentHIPStream();
+  const int grid = grid_for(n >> 2);
+  if (wt == WireT::F32)
+    hipLaunchKernelGGL(k_aggregate<float>, grid, kBlock, 0, stream, s, (int)slots.size(), (float)gscale,
+                       acc.data_ptr<float>(), n, (int)accumulate);
+  else
+    hipLaunchKernelGGL(k_aggregate<uint16_t>, grid, kBlock, 0, stream, s, (int)slots.size(), (float)gscale,
+                       acc.data_ptr<float>(), n, (int)accumulate);
+}
+
+void convert(at::Tensor src, at::Tensor dst, double scale) {
+  check_dev(src, "src");
+  check_dev(dst, "dst");
+  const int64_t n = src.numel();
+  TORCH_CHECK(dst.numel() == n, "convert size mismatch");
+  auto stream = c10::hip::getCurrentHIPStream();
+  const int grid = grid_for(n >> 2);
+  const WireT a = wire_of(src), b = wire_of(dst);
+  const float sc = (float)scale;
+  if (a == WireT::F32 && b == WireT::BF16)
+    hipLaunchKernelGGL((k_convert<float, uint16_t>), grid, kBlock, 0, stream, src.data_ptr<float>(),
+                       (uint16_t*)dst.data_ptr(), n, sc);
+  else if (a == WireT::BF16 && b == WireT::F32)
+    hipLaunchKernelGGL((k_convert<uint16_t, float>), grid, kBlock, 0, stream, (const uint16_t*)src.data_ptr(),
+                       dst.data_ptr<float>(), n, sc);
+  else if (a == WireT::F32 && b == WireT::F32)
+    hipLaunchKernelGGL((k_convert<float, float>), grid, kBlock, 0, stream, src.data_ptr<float>(),
+                       dst.data_ptr<float>(), n, sc);
+  else
+    hipLaunchKernelGGL((k_convert<uint16_t, uint16_t>), grid, kBlock, 0, stream, (const uint16_t*)src.data_ptr(),
+                       (uint16_t*)dst.data_ptr(), n, sc);
+}
+
+void sgd_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p, c10::optional<at::Tensor> buf,
+              c10::optional<at::Tensor> pub, bool zero_src, double lr, double wd, double momentum, double dampening,
+              bool nesterov, bool first) {
+  check_dev(p, "param");
+  TORCH_CHECK(p.scalar_type() == at::kFloat, "param master must be float32");
+  const int64_t n = p.numel();
+  WireT wt;
+  SlotPtrs s = make_slots(grads, n, wt);
+  float* bp = nullptr;
+  if (buf.has_value() && buf->defined()) {
+    check_dev(*buf, "momentum_buffer");
+    TORCH_CHECK(buf->numel() == n && buf->scalar_type() == at::kFloat, "momentum buffer mismatch");
+    bp = buf->data_ptr<float>();
+  }
+  TORCH_CHECK(momentum == 0.0 || bp != nullptr, "momentum != 0 requires a momentum buffer");
+  TORCH_CHECK(!zero_src || (grads.size() == 1 && wt == WireT::F32), "zero_src needs a single fp32 source");
+  const int pm = pub_mode_of(pub, n);
+  void* pp = pm ? pub->data_ptr() : nullptr;
+  SgdHp h{(float)lr, (float)wd, (float)momentum, (float)dampening, (int)nesterov, (int)first};
+  auto stream = c10::hip::getCurrentHIPStream();
+  const int grid = grid_for(n >> 2);
+  if (wt == WireT::F32)
+    hipLaunchKernelGGL(k_sgd<float>, grid, kBlock, 0, stream, s, (int)grads.size(), (float)gscale,
+                       p.data_ptr<float>(), bp, pp, pm, (int)zero_src, n, h);
+  else
+    hipLaunchKernelGGL(k_sgd<uint16_t>, grid, kBlock, 0, stream, s, (int)grads.size(), (float)gscale,
+                       p.data_ptr<float>(), bp, pp, pm, (int)zero_src, n, h);
+}
+
+void adam_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p, at::Tensor exp_avg,
+               at::Tensor exp_avg_sq, c10::optional<at::Tensor> max_exp_avg_sq, c10::optional<at::Tensor> pub,
+               bool zero_src, double lr, double beta1, double beta2, double eps, double wd, int64_t step,
+               bool amsgrad, bool torch_mode) {
+  check_dev(p, "param");
+  check_dev(exp_avg, "exp_avg");
+  check_dev(exp_avg_sq, "exp_avg_sq");
+  const int64_t n = p.numel();
+  TORCH_CHECK(exp_avg.numel() == n && exp_avg_sq.numel() == n, "adam state size mismatch");
+  WireT wt;
+  SlotPtrs s = make_slots(grads, n, wt);
+  float* xp = nullptr;
+  if (amsgrad) {
+    TORCH_CHECK(max_exp_avg_sq.has_value() && max_exp_avg_sq->defined(), "amsgrad needs max_exp_avg_sq");
+    check_dev(*max_exp_avg_sq, "max_exp_avg_sq");
+    xp = max_exp_avg_sq->data_ptr<float>();
+  }
+  TORCH_CHECK(!zero_src || (grads.size() == 1 && wt == WireT::F32), "zero_src needs a single fp32 source");
+  const int pm = pub_mode_of(pub, n);
+  void* pp = pm ? pub->data_ptr() : nullptr;
+  const double bc1 = 1.0 - std::pow(beta1, (double)step), bc2 = 1.0 - std::pow(beta2, (double)step);
+  const double step_size = torch_mode ? lr / bc1 : lr * std::sqrt(bc2) / bc1;
+  AdamHp h{(float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, (float)step_size, (float)std::sqrt(bc2),
+           (int)amsgrad, (int)torch_mode};
+  auto stream = c10::hip::getCurrentHIPStream();
+  const int grid = grid_for(n >> 2);
+  if (wt == WireT::F32)
+    hipLaunchKernelGGL(k_adam<float>, grid, kBlock, 0, stream, s, (int)grads.size(), (float)gscale,
+                       p.data_ptr<float>(), exp_avg.data_ptr<float>(), exp_avg_sq.data_ptr<float>(), xp, pp, pm,
+                       (int)zero_src, n, h);
+  else
+    hipLaunchKernelGGL(k_adam<uint16_t>, grid, kBlock, 0, stream, s, (int)grads.size(), (float)gscale,
+                       p.data_ptr<float>(), exp_avg.data_ptr<float>(), exp_avg_sq.data_ptr<float>(), xp, pp, pm,
+                       (int)zero_src, n, h);
+}
+
+}  // namespace hipps

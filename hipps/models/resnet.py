@@ -1,0 +1,118 @@
+"""ResNet-50 (and family) for the synthetic-ImageNet async-PS benchmark.
+
+The reference has no model zoo (SURVEY.md §1 "Missing layers"); BASELINE.json names
+"ResNet-50 synthetic-ImageNet async PS (AsySG-InCon) bf16" as the headline config, so the
+framework ships its own ResNet definition (random init, no checkpoints, no torchvision).
+
+MI355X notes: convolutions go to MIOpen (library path), run channels_last in bf16 under
+autocast; parameters stay fp32 so the PS keeps an exact fp32 master copy and the wire codec
+decides the transport precision.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def _conv(cin, cout, k, stride=1, groups=1):
+    return nn.Conv2d(cin, cout, k, stride=stride, padding=k // 2, groups=groups, bias=False)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin, width, stride=1, downsample=False):
+        super().__init__()
+        cout = width * self.expansion
+        self.conv1 = _conv(cin, width, 1)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = _conv(width, width, 3, stride=stride)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = _conv(width, cout, 1)
+        self.bn3 = nn.BatchNorm2d(cout)
+        self.downsample = None
+        if downsample:
+            self.downsample = nn.Sequential(_conv(cin, cout, 1, stride=stride), nn.BatchNorm2d(cout))
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        y = F.relu(self.bn1(self.conv1(x)), inplace=True)
+        y = F.relu(self.bn2(self.conv2(y)), inplace=True)
+        y = self.bn3(self.conv3(y))
+        return F.relu(y + idt, inplace=True)
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, cin, width, stride=1, downsample=False):
+        super().__init__()
+        self.conv1 = _conv(cin, width, 3, stride=stride)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = _conv(width, width, 3)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.downsample = None
+        if downsample:
+            self.downsample = nn.Sequential(_conv(cin, width, 1, stride=stride), nn.BatchNorm2d(width))
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        y = F.relu(self.bn1(self.conv1(x)), inplace=True)
+        y = self.bn2(self.conv2(y))
+        return F.relu(y + idt, inplace=True)
+
+
+class ResNet(nn.Module):
+    def __init__(self, block, layers, num_classes=1000, width=64, zero_init_residual=True):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        cin = width
+        stages = []
+        for i, n in enumerate(layers):
+            w = width * (2 ** i)
+            blocks = []
+            for j in range(n):
+                stride = 2 if (j == 0 and i > 0) else 1
+                ds = j == 0 and (stride != 1 or cin != w * block.expansion)
+                blocks.append(block(cin, w, stride=stride, downsample=ds))
+                cin = w * block.expansion
+            stages.append(nn.Sequential(*blocks))
+        self.num_stages = len(stages)
+        for i, st in enumerate(stages):
+            setattr(self, f"layer{i + 1}", st)
+        self.fc = nn.Linear(cin, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        if zero_init_residual:
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    nn.init.zeros_(m.bn3.weight)
+                elif isinstance(m, BasicBlock):
+                    nn.init.zeros_(m.bn2.weight)
+
+    def forward(self, x):
+        x = self.maxpool(F.relu(self.bn1(self.conv1(x)), inplace=True))
+        for i in range(self.num_stages):
+            x = getattr(self, f"layer{i + 1}")(x)
+        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        return self.fc(x)
+
+
+def resnet50(num_classes=1000, **kw):
+    return ResNet(Bottleneck, [3, 4, 6, 3], num_classes=num_classes, **kw)
+
+
+def resnet18(num_classes=1000, **kw):
+    return ResNet(BasicBlock, [2, 2, 2, 2], num_classes=num_classes, **kw)
+
+
+def resnet_tiny(num_classes=10, **kw):
+    """A 2-stage toy ResNet for CPU tests (same block code as ResNet-50)."""
+    return ResNet(Bottleneck, [1, 1], num_classes=num_classes, width=8, **kw)
