@@ -1,0 +1,273 @@
+"""Gradient codecs: the reference's pluggable ``code`` object (ps.py:57, 65-66, 94, 165-166).
+
+The reference calls an external ``codings`` package: ``code.encode(grad)`` in a pool thread,
+``pickle`` + ``blosc`` the result on the host, all-gathers the bytes, sets ``code.codes`` and
+calls ``code.decode(c, cuda=...)`` per rank.  Here a codec owns a *fixed device wire layout*
+per flat bucket, so encode is one (or a few) kernel launches writing straight into the comm
+buffer and decode is fused into the PS/optimizer accumulation:
+
+    layout(n)                       -> WireLayout (16-byte aligned fields, static size)
+    encode_into(x, views, state)    -> writes the message for flat f32 gradient x
+    accumulate(msgs, acc, ...)      -> acc (+)= sum_w decode(msg_w), rank order
+    dense_source(views)             -> (fusable codecs) a tensor the fused optimizer reads directly
+
+The reference's object API (``encode(grad) -> code``, ``decode(code, cuda=False)``, ``codes``)
+is kept on top for drop-in use (see :class:`Codec`).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from hipps import ops
+
+ALIGN = 16
+
+
+def _align(x: int, a: int = ALIGN) -> int:
+    return (x + a - 1) // a * a
+
+
+@dataclass(frozen=True)
+class Field:
+    name: str
+    dtype: torch.dtype
+    numel: int
+    offset: int
+
+    @property
+    def nbytes(self) -> int:
+        return self.numel * torch.empty((), dtype=self.dtype).element_size()
+
+
+class WireLayout:
+    """Static byte layout of one message: fields at 16-byte aligned offsets."""
+
+    def __init__(self, fields: Sequence[Tuple[str, torch.dtype, int]]):
+        off = 0
+        fs = []
+        for name, dt, n in fields:
+            off = _align(off)
+            f = Field(name, dt, int(n), off)
+            fs.append(f)
+            off += f.nbytes
+        self.fields: List[Field] = fs
+        self.nbytes = _align(off)
+
+    def views(self, buf: torch.Tensor) -> Dict[str, torch.Tensor]:
+        assert buf.dtype == torch.uint8 and buf.numel() >= self.nbytes, (buf.dtype, buf.numel(), self.nbytes)
+        return {f.name: buf[f.offset:f.offset + f.nbytes].view(f.dtype) for f in self.fields}
+
+    def __repr__(self):
+        return "WireLayout(%s, nbytes=%d)" % (", ".join(f"{f.name}:{f.dtype}x{f.numel}" for f in self.fields),
+                                             self.nbytes)
+
+
+class Codec:
+    """Base codec.  Subclasses define layout/encode_into/accumulate."""
+
+    name = "codec"
+    fusable = False  # True if dense_source() exists (decode == dtype cast)
+    lossless = False
+
+    def __init__(self):
+        self.codes = None  # reference API: engine sets the list of all ranks' codes (ps.py:165)
+        self._seed = 0
+        self._object_state: dict = {}
+
+    # ---- flat-bucket interface -----------------------------------------------------------
+    def layout(self, n: int) -> WireLayout:
+        raise NotImplementedError
+
+    def init_state(self, n: int, device) -> dict:
+        return {}
+
+    def encode_into(self, x: torch.Tensor, views: Dict[str, torch.Tensor], state: dict) -> None:
+        raise NotImplementedError
+
+    def accumulate(self, msgs: Sequence[Dict[str, torch.Tensor]], acc: torch.Tensor, gscale: float = 1.0,
+                   accumulate: bool = False) -> None:
+        raise NotImplementedError
+
+    def dense_source(self, views: Dict[str, torch.Tensor]) -> torch.Tensor:
+        raise NotImplementedError
+
+    def nbytes(self, n: int) -> int:
+        return self.layout(n).nbytes
+
+    # ---- reference object API (ps.py:94, 165-166) ----------------------------------------
+    def encode(self, grad: torch.Tensor, key=None, **kw) -> dict:
+        """Reference object API.  Pass ``key`` (e.g. the parameter name) to keep per-tensor
+        codec state such as error-feedback residuals across calls."""
+        g = grad.detach().reshape(-1).float().contiguous()
+        if g.data_ptr() % ALIGN:
+            g = g.clone()
+        lay = self.layout(g.numel())
+        buf = torch.empty(lay.nbytes, dtype=torch.uint8, device=g.device)
+        views = lay.views(buf)
+        if key is None:
+            st = self.init_state(g.numel(), g.device)
+            st.pop("resid", None)
+        else:
+            st = self._object_state.setdefault(key, self.init_state(g.numel(), g.device))
+        self.encode_into(g, views, st)
+        return {"codec": self.name, "shape": tuple(grad.shape), "n": g.numel(), "buf": buf}
+
+    def decode(self, code: dict, cuda: bool = False) -> torch.Tensor:
+        buf = code["buf"]
+        if cuda and not buf.is_cuda:
+            buf = buf.cuda(non_blocking=True)
+        lay = self.layout(code["n"])
+        acc = torch.empty(code["n"], dtype=torch.float32, device=buf.device)
+        self.accumulate([lay.views(buf)], acc, 1.0, False)
+        return acc.view(code["shape"])
+
+    def next_seed(self) -> int:
+        self._seed += 1
+        return self._seed
+
+
+class Identity(Codec):
+    """Dense pass-through; wire dtype fp32 (exact) or bf16 (2x fewer bytes)."""
+
+    fusable = True
+
+    def __init__(self, wire_dtype: torch.dtype = torch.float32):
+        super().__init__()
+        assert wire_dtype in (torch.float32, torch.bfloat16)
+        self.wire_dtype = wire_dtype
+        self.lossless = wire_dtype == torch.float32
+        self.name = "fp32" if wire_dtype == torch.float32 else "bf16"
+
+    def layout(self, n):
+        return WireLayout([("x", self.wire_dtype, n)])
+
+    def encode_into(self, x, views, state):
+        ops.convert(x, views["x"])
+
+    def accumulate(self, msgs, acc, gscale=1.0, accumulate=False):
+        ops.aggregate([m["x"] for m in msgs], acc, gscale, accumulate)
+
+    def dense_source(self, views):
+        return views["x"]
+
+
+class Int8(Codec):
+    """Per-256-block absmax int8 (QSGD-style), optional stochastic rounding and error feedback."""
+
+    name = "int8"
+
+    def __init__(self, stochastic: bool = False, error_feedback: bool = True):
+        super().__init__()
+        self.stochastic = stochastic
+        self.error_feedback = error_feedback
+
+    def layout(self, n):
+        return WireLayout([("scales", torch.float32, (n + ops.QBLOCK - 1) // ops.QBLOCK), ("q", torch.int8, n)])
+
+    def init_state(self, n, device):
+        return {"resid": torch.zeros(n, dtype=torch.float32, device=device)} if self.error_feedback else {}
+
+    def encode_into(self, x, views, state):
+        ops.q8_encode(x, state.get("resid"), views["q"], views["scales"], self.stochastic, self.next_seed())
+
+    def accumulate(self, msgs, acc, gscale=1.0, accumulate=False):
+        ops.q8_aggregate([m["q"] for m in msgs], [m["scales"] for m in msgs], acc, gscale, accumulate)
+
+
+class TopK(Codec):
+    """Exact magnitude top-k (k = ceil(ratio*n)), ascending int32 indices + f32/bf16 values."""
+
+    name = "topk"
+
+    def __init__(self, ratio: float = 0.01, value_dtype: torch.dtype = torch.float32, error_feedback: bool = True):
+        super().__init__()
+        assert 0 < ratio <= 1
+        self.ratio = ratio
+        self.value_dtype = value_dtype
+        self.error_feedback = error_feedback
+
+    def k_of(self, n: int) -> int:
+        return max(1, min(n, int(math.ceil(self.ratio * n))))
+
+    def layout(self, n):
+        k = self.k_of(n)
+        return WireLayout([("idx", torch.int32, k), ("val", self.value_dtype, k)])
+
+    def init_state(self, n, device):
+        st = {}
+        if self.error_feedback:
+            st["resid"] = torch.zeros(n, dtype=torch.float32, device=device)
+        if device is not None and torch.device(device).type == "cuda":
+            st["ws"] = torch.empty(ops.topk_workspace_bytes(n), dtype=torch.uint8, device=device)
+        return st
+
+    def encode_into(self, x, views, state):
+        ops.topk_encode(x, state.get("resid"), views["idx"].numel(), views["idx"], views["val"], state.get("ws"))
+
+    def accumulate(self, msgs, acc, gscale=1.0, accumulate=False):
+        if not accumulate:
+            acc.zero_()
+        for m in msgs:  # rank order; one message has unique indices
+            ops.topk_accumulate(m["idx"], m["val"], acc, gscale)
+
+
+class TopKInt8(TopK):
+    """Top-k values further quantized to int8 (one scale per 256 selected values)."""
+
+    name = "topk_int8"
+
+    def layout(self, n):
+        k = self.k_of(n)
+        return WireLayout([("idx", torch.int32, k), ("scales", torch.float32, (k + ops.QBLOCK - 1) // ops.QBLOCK),
+                           ("q", torch.int8, k)])
+
+    def init_state(self, n, device):
+        st = super().init_state(n, device)
+        st["vals"] = torch.empty(self.k_of(n), dtype=torch.float32, device=device)
+        return st
+
+    def encode_into(self, x, views, state):
+        resid = state.get("resid")
+        ops.topk_encode(x, resid, views["idx"].numel(), views["idx"], state["vals"], state.get("ws"))
+        ops.q8_encode(state["vals"], None, views["q"], views["scales"], False, 0)
+        if resid is not None:
+            ops.topk_q8_residual(views["idx"], state["vals"], views["q"], views["scales"], resid)
+
+    def accumulate(self, msgs, acc, gscale=1.0, accumulate=False):
+        if not accumulate:
+            acc.zero_()
+        for m in msgs:
+            ops.topk_q8_accumulate(m["idx"], m["q"], m["scales"], acc, gscale)
+
+
+def get_codec(spec) -> Codec:
+    """'fp32' | 'bf16' | 'int8' | 'int8_sr' | 'topk[:ratio]' | 'topk_bf16[:ratio]' | 'topk_int8[:ratio]' | Codec."""
+    if spec is None:
+        return Identity(torch.float32)
+    if isinstance(spec, Codec):
+        return spec
+    name, _, arg = str(spec).partition(":")
+    name = name.lower()
+    if name in ("fp32", "identity", "none"):
+        return Identity(torch.float32)
+    if name == "bf16":
+        return Identity(torch.bfloat16)
+    if name in ("int8", "qsgd"):
+        return Int8(stochastic=False)
+    if name in ("int8_sr", "qsgd_sr"):
+        return Int8(stochastic=True)
+    ratio = float(arg) if arg else 0.01
+    if name == "topk":
+        return TopK(ratio)
+    if name == "topk_bf16":
+        return TopK(ratio, value_dtype=torch.bfloat16)
+    if name == "topk_int8":
+        return TopKInt8(ratio)
+    raise ValueError(f"unknown codec {spec!r}")
+
+
+__all__ = ["Codec", "Identity", "Int8", "TopK", "TopKInt8", "WireLayout", "get_codec"]

@@ -12,6 +12,18 @@ void adam_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p
                at::Tensor exp_avg_sq, c10::optional<at::Tensor> max_exp_avg_sq, c10::optional<at::Tensor> pub,
                bool zero_src, double lr, double beta1, double beta2, double eps, double wd, int64_t step,
                bool amsgrad, bool torch_mode);
+// quant.hip
+void q8_encode(at::Tensor x, c10::optional<at::Tensor> resid, at::Tensor q, at::Tensor scales, bool stochastic,
+               int64_t seed);
+void q8_aggregate(const std::vector<at::Tensor>& qs, const std::vector<at::Tensor>& ss, at::Tensor acc, double gscale,
+                  bool accumulate);
+// topk.hip
+void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::Tensor idx, at::Tensor val,
+                 at::Tensor workspace);
+int64_t topk_workspace_bytes(int64_t n);
+void topk_accumulate(at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale);
+void topk_q8_accumulate(at::Tensor idx, at::Tensor q, at::Tensor scales, at::Tensor acc, double gscale);
+void topk_q8_residual(at::Tensor idx, at::Tensor v, at::Tensor q, at::Tensor scales, at::Tensor resid);
 }  // namespace hipps
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -20,4 +32,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("convert", &hipps::convert, "dst = scale * src with f32/bf16 conversion");
   m.def("sgd_step", &hipps::sgd_step, "fused decode+sum+SGD (reference ps.py:197-214 math)");
   m.def("adam_step", &hipps::adam_step, "fused decode+sum+Adam (reference ps.py:217-261 math)");
+  m.def("q8_encode", &hipps::q8_encode, "per-256-block absmax int8 quantization (+EF, +stochastic)");
+  m.def("q8_aggregate", &hipps::q8_aggregate, "acc (+)= gscale * sum_w dequant(q_w, s_w)");
+  m.def("topk_encode", &hipps::topk_encode, "exact top-k |g| (radix select) -> idx asc, val");
+  m.def("topk_workspace_bytes", &hipps::topk_workspace_bytes);
+  m.def("topk_accumulate", &hipps::topk_accumulate, "acc[idx] += gscale * val");
+  m.def("topk_q8_accumulate", &hipps::topk_q8_accumulate, "acc[idx] += gscale * deq(q)");
+  m.def("topk_q8_residual", &hipps::topk_q8_residual, "EF: r[idx] += v - deq(q)");
 }

@@ -1,0 +1,103 @@
+"""Device-dispatching hipps ops.
+
+Every op takes flat buffers.  HIP tensors run the hand-written gfx950 kernels in
+``hipps/csrc/*.hip`` (and FAIL if the extension is not built); CPU tensors run
+:mod:`hipps.ops.reference`.  Kernels are enqueued on the current HIP stream, so callers pick the
+stream with ``torch.cuda.stream(...)``.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+
+from . import reference as ref
+from ._native import available as native_available  # noqa: F401
+from ._native import native
+
+QBLOCK = ref.QBLOCK
+
+
+def _dev(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def aggregate(slots: Sequence[torch.Tensor], acc: torch.Tensor, gscale: float = 1.0, accumulate: bool = False):
+    """acc (+)= gscale * sum_w slots[w], summed in rank order (reference ps.py:176)."""
+    if _dev(acc):
+        return native().aggregate(list(slots), acc, float(gscale), bool(accumulate))
+    return ref.aggregate(slots, acc, gscale, accumulate)
+
+
+def convert(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0):
+    """dst = scale*src with f32<->bf16 conversion (wire pack / unpack)."""
+    if _dev(src):
+        return native().convert(src, dst, float(scale))
+    return ref.convert(src, dst, scale)
+
+
+def sgd_step(grads: Sequence[torch.Tensor], p: torch.Tensor, buf: Optional[torch.Tensor] = None,
+             pub: Optional[torch.Tensor] = None, zero_src: bool = False, gscale: float = 1.0, lr: float = 0.0,
+             weight_decay: float = 0.0, momentum: float = 0.0, dampening: float = 0.0, nesterov: bool = False,
+             first: bool = False):
+    """Fused decode + sum_W + SGD (reference ps.py:197-214) + optional publish copy."""
+    if _dev(p):
+        return native().sgd_step(list(grads), float(gscale), p, buf, pub, bool(zero_src), float(lr),
+                                 float(weight_decay), float(momentum), float(dampening), bool(nesterov), bool(first))
+    return ref.sgd_step(list(grads), p, buf, pub, zero_src, gscale, lr, weight_decay, momentum, dampening,
+                        nesterov, first)
+
+
+def adam_step(grads: Sequence[torch.Tensor], p: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor,
+              max_exp_avg_sq: Optional[torch.Tensor] = None, pub: Optional[torch.Tensor] = None,
+              zero_src: bool = False, gscale: float = 1.0, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+              weight_decay: float = 0.0, step: int = 1, amsgrad: bool = False, torch_mode: bool = False):
+    """Fused decode + sum_W + Adam (reference ps.py:217-261 eps placement unless torch_mode)."""
+    if _dev(p):
+        return native().adam_step(list(grads), float(gscale), p, exp_avg, exp_avg_sq, max_exp_avg_sq, pub,
+                                  bool(zero_src), float(lr), float(betas[0]), float(betas[1]), float(eps),
+                                  float(weight_decay), int(step), bool(amsgrad), bool(torch_mode))
+    return ref.adam_step(list(grads), p, exp_avg, exp_avg_sq, max_exp_avg_sq, pub, zero_src, gscale, lr, betas, eps,
+                         weight_decay, step, amsgrad, torch_mode)
+
+
+def q8_encode(x, resid, q, scales, stochastic: bool = False, seed: int = 0):
+    if _dev(x):
+        return native().q8_encode(x, resid, q, scales, bool(stochastic), int(seed) & ((1 << 63) - 1))
+    return ref.q8_encode(x, resid, q, scales, stochastic, int(seed) & ((1 << 63) - 1))
+
+
+def q8_aggregate(qs, ss, acc, gscale: float = 1.0, accumulate: bool = False):
+    if _dev(acc):
+        return native().q8_aggregate(list(qs), list(ss), acc, float(gscale), bool(accumulate))
+    return ref.q8_aggregate(qs, ss, acc, gscale, accumulate)
+
+
+def topk_workspace_bytes(n: int) -> int:
+    return native().topk_workspace_bytes(int(n)) if native_available() else ref.topk_workspace_bytes(n)
+
+
+def topk_encode(g, resid, k: int, idx, val, workspace=None):
+    if _dev(g):
+        if workspace is None:
+            workspace = torch.empty(native().topk_workspace_bytes(g.numel()), dtype=torch.uint8, device=g.device)
+        return native().topk_encode(g, resid, int(k), idx, val, workspace)
+    return ref.topk_encode(g, resid, k, idx, val)
+
+
+def topk_accumulate(idx, val, acc, gscale: float = 1.0):
+    if _dev(acc):
+        return native().topk_accumulate(idx, val, acc, float(gscale))
+    return ref.topk_accumulate(idx, val, acc, gscale)
+
+
+def topk_q8_accumulate(idx, q, scales, acc, gscale: float = 1.0):
+    if _dev(acc):
+        return native().topk_q8_accumulate(idx, q, scales, acc, float(gscale))
+    return ref.topk_q8_accumulate(idx, q, scales, acc, gscale)
+
+
+def topk_q8_residual(idx, v, q, scales, resid):
+    if _dev(resid):
+        return native().topk_q8_residual(idx, v, q, scales, resid)
+    return ref.topk_q8_residual(idx, v, q, scales, resid)

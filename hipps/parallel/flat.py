@@ -1,0 +1,202 @@
+"""Flat parameter / gradient store and the bucket plan.
+
+The reference keeps every parameter separate: one hook, one encode task, one pickle, two MPI
+collectives and one optimizer call per tensor (ps.py:63-66, 140-190; 161 tensors for
+ResNet-50).  hipps instead re-homes all parameters of an optimizer into ONE fp32 buffer and all
+gradients into another (``param.data`` / ``param.grad`` become views), so that
+
+  * the optimizer is one fused kernel per param group (not per tensor),
+  * a bucket is a contiguous slice that a codec encodes with one launch,
+  * a dense wire image (identity codec) is a linear copy of the flat buffer, which the fused
+    aggregate+update kernel can read directly.
+
+Every tensor's slot starts on a 16-element boundary (64 B fp32 / 32 B bf16), so every bucket
+and group slice is 16-byte aligned for vector loads.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+ALIGN_ELEMS = 16
+
+
+def _align(n: int, a: int = ALIGN_ELEMS) -> int:
+    return (n + a - 1) // a * a
+
+
+def _is_dense(t: torch.Tensor) -> bool:
+    """Non-overlapping and dense (any dim permutation, e.g. channels_last)."""
+    if t.numel() <= 1:
+        return True
+    dims = sorted([(s, d) for d, s in enumerate(t.stride()) if t.size(d) != 1])
+    expect = 1
+    for s, d in dims:
+        if s != expect:
+            return False
+        expect *= t.size(d)
+    return True
+
+
+@dataclass
+class Slot:
+    name: str
+    param: torch.Tensor
+    offset: int
+    numel: int
+    group: int
+
+
+class FlatStore:
+    """All params of ``groups`` in one flat fp32 buffer; grads in a second one."""
+
+    def __init__(self, groups: Sequence[Sequence[torch.Tensor]], names: Optional[Dict[int, str]] = None,
+                 device=None, dtype=torch.float32):
+        names = names or {}
+        self.slots: List[Slot] = []
+        self.group_ranges: List[Tuple[int, int]] = []
+        off = 0
+        seen = set()
+        for gi, params in enumerate(groups):
+            g0 = off
+            for p in params:
+                if id(p) in seen:
+                    raise ValueError("a parameter appears twice in the optimizer")
+                seen.add(id(p))
+                self.slots.append(Slot(names.get(id(p), f"param{len(self.slots)}"), p, off, p.numel(), gi))
+                off = _align(off + p.numel())
+            self.group_ranges.append((g0, off))
+        self.numel = off
+        if device is None:
+            device = self.slots[0].param.device if self.slots else torch.device("cpu")
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.data = torch.zeros(self.numel, dtype=dtype, device=self.device)
+        self.grad = torch.zeros(self.numel, dtype=dtype, device=self.device)
+        for s in self.slots:
+            p = s.param
+            if p.dtype != dtype:
+                raise TypeError(f"{s.name}: parameter dtype {p.dtype} != flat store dtype {dtype}; keep params fp32 "
+                                "and use autocast for bf16 compute")
+            src = p.data
+            if not _is_dense(src):
+                src = src.contiguous()
+            v = self._view(self.data, s, src)
+            v.copy_(src)
+            p.data = v
+        self.attach_grads()
+
+    @staticmethod
+    def _view(buf: torch.Tensor, s: Slot, like: torch.Tensor) -> torch.Tensor:
+        seg = buf[s.offset:s.offset + s.numel]
+        if like.is_contiguous():
+            return seg.view(like.shape)
+        return seg.as_strided(like.shape, like.stride())
+
+    def param_view(self, buf: torch.Tensor, i: int) -> torch.Tensor:
+        s = self.slots[i]
+        return self._view(buf, s, s.param)
+
+    def attach_grads(self):
+        """(Re)point every ``param.grad`` at its flat slice, salvaging foreign grads."""
+        for s in self.slots:
+            p = s.param
+            v = self._view(self.grad, s, p.data)
+            g = p.grad
+            if g is None or g.data_ptr() != v.data_ptr():
+                if g is not None:
+                    v.copy_(g)
+                p.grad = v
+
+    def grads_attached(self) -> bool:
+        return all(s.param.grad is not None and s.param.grad.data_ptr() ==
+                   self.grad[s.offset:].data_ptr() for s in self.slots)
+
+    def zero_grad(self):
+        self.grad.zero_()
+        self.attach_grads()
+
+    def group_slice(self, buf: torch.Tensor, gi: int) -> torch.Tensor:
+        a, b = self.group_ranges[gi]
+        return buf[a:b]
+
+    def new_buffer(self, dtype=None, zero=True) -> torch.Tensor:
+        f = torch.zeros if zero else torch.empty
+        return f(self.numel, dtype=dtype or self.dtype, device=self.device)
+
+
+@dataclass
+class Bucket:
+    index: int
+    lo: int
+    hi: int
+    slot_ids: List[int]
+    wire_offset: int = 0
+    layout: object = None
+
+    @property
+    def numel(self):
+        return self.hi - self.lo
+
+
+class BucketPlan:
+    """Contiguous flat slices, filled in autograd (reverse registration) order.
+
+    Buckets are ready in ``ready_order`` (the last layers' gradients first) but their messages are
+    laid out in FLAT order inside the wire buffer, so a dense codec's wire buffer is a linear
+    image of the flat gradient.
+    """
+
+    def __init__(self, store: FlatStore, codec, bucket_bytes: int = 64 << 20):
+        self.store = store
+        self.codec = codec
+        cap = max(1, bucket_bytes // store.data.element_size())
+        rev = list(range(len(store.slots)))[::-1]
+        groups: List[List[int]] = []
+        cur: List[int] = []
+        cur_n = 0
+        for i in rev:
+            cur.append(i)
+            cur_n += store.slots[i].numel
+            if cur_n >= cap:
+                groups.append(cur)
+                cur, cur_n = [], 0
+        if cur:
+            groups.append(cur)
+        # flat order: group with lowest offsets first
+        spans = []
+        for ids in groups:
+            lo = min(store.slots[i].offset for i in ids)
+            hi = max(_align(store.slots[i].offset + store.slots[i].numel) for i in ids)
+            spans.append((lo, hi, sorted(ids)))
+        spans.sort()
+        # make spans tile [0, numel) exactly (alignment padding belongs to the preceding bucket)
+        self.buckets: List[Bucket] = []
+        for bi, (lo, hi, ids) in enumerate(spans):
+            nxt = spans[bi + 1][0] if bi + 1 < len(spans) else store.numel
+            self.buckets.append(Bucket(bi, lo if bi else 0, nxt, ids))
+        woff = 0
+        for b in self.buckets:
+            b.layout = codec.layout(b.numel)
+            b.wire_offset = woff
+            woff += b.layout.nbytes
+        self.wire_nbytes = woff
+        self.ready_order = [b.index for b in reversed(self.buckets)]
+        self.slot_bucket = {}
+        for b in self.buckets:
+            for i in b.slot_ids:
+                self.slot_bucket[i] = b.index
+
+    def views(self, wire: torch.Tensor, bi: int):
+        b = self.buckets[bi]
+        return b.layout.views(wire[b.wire_offset:b.wire_offset + b.layout.nbytes])
+
+    def new_wire(self, device=None) -> torch.Tensor:
+        return torch.empty(self.wire_nbytes, dtype=torch.uint8, device=device or self.store.device)
+
+    def dense_image(self, wire: torch.Tensor) -> torch.Tensor:
+        """For fusable (identity) codecs: the whole wire buffer as one flat tensor."""
+        dt = self.buckets[0].layout.fields[0].dtype
+        return wire[: self.wire_nbytes].view(dt)

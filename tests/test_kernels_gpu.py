@@ -1,0 +1,168 @@
+"""GPU numerics: every hipps HIP kernel vs the fp32 PyTorch reference of the same op.
+
+Runs only on an MI355X (marker ``gpu``).  The native extension must be the code path under
+test: the first test asserts ``hipps._C`` is loaded (no silent eager fallback).
+"""
+import pytest
+import torch
+
+from hipps import codecs, ops
+from hipps.ops import _native
+from hipps.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+SIZES = [1, 7, 1000, 4099, 1 << 20]
+
+
+def test_native_extension_loaded():
+    assert _native.available(), "hipps._C must be built and importable on the GPU box"
+    import sys
+
+    assert "hipps._C" in sys.modules
+
+
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("W", [1, 3, 8])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_aggregate(n, W, dt):
+    torch.manual_seed(n + W)
+    slots = [torch.randn(n).to(dt) for _ in range(W)]
+    want = torch.randn(n)
+    got = want.clone().to(DEV)
+    ref.aggregate(slots, want, 0.25, accumulate=True)
+    ops.aggregate([s.to(DEV) for s in slots], got, 0.25, accumulate=True)
+    torch.testing.assert_close(got.cpu(), want, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_convert_bf16_roundtrip_bitexact(n):
+    x = torch.randn(n) * 10
+    x[:1] = float("nan") if n > 3 else x[:1]
+    y = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    ops.convert(x.to(DEV), y)
+    want = x.to(torch.bfloat16)
+    assert torch.equal(y.cpu().view(torch.int16)[~want.isnan()], want.view(torch.int16)[~want.isnan()])
+    assert y.cpu().isnan().sum() == want.isnan().sum()
+    z = torch.empty(n, device=DEV)
+    ops.convert(y, z, 2.0)
+    torch.testing.assert_close(z.cpu(), want.float() * 2, equal_nan=True)
+
+
+@pytest.mark.parametrize("n", [5, 4096, 100003])
+@pytest.mark.parametrize("mom,damp,nesterov,wd", [(0, 0, False, 0), (0.9, 0, False, 1e-4), (0.9, 0.1, True, 1e-4)])
+@pytest.mark.parametrize("W,dt", [(1, torch.float32), (4, torch.bfloat16)])
+def test_sgd_fused(n, mom, damp, nesterov, wd, W, dt):
+    torch.manual_seed(n)
+    p = torch.randn(n)
+    buf = torch.zeros(n)
+    pd, bd = p.to(DEV), buf.to(DEV)
+    pub = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    for t in range(3):
+        grads = [torch.randn(n).to(dt) for _ in range(W)]
+        kw = dict(lr=0.05, weight_decay=wd, momentum=mom, dampening=damp, nesterov=nesterov, first=(t == 0))
+        ref.sgd_step(grads, p, buf if mom else None, None, False, 0.5, **kw)
+        ops.sgd_step([g.to(DEV) for g in grads], pd, bd if mom else None, pub, False, 0.5, **kw)
+    torch.testing.assert_close(pd.cpu(), p, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(pub.cpu().float(), p.to(torch.bfloat16).float(), rtol=1e-2, atol=1e-2)
+    if mom:
+        torch.testing.assert_close(bd.cpu(), buf, rtol=1e-5, atol=1e-6)
+
+
+def test_sgd_zero_src():
+    n = 4099
+    g = torch.randn(n, device=DEV)
+    p = torch.randn(n, device=DEV)
+    p0 = p.clone()
+    ops.sgd_step([g], p, None, None, True, 1.0, lr=0.1)
+    assert g.abs().sum().item() == 0
+    assert not torch.equal(p, p0)
+
+
+@pytest.mark.parametrize("n", [3, 4096, 65537])
+@pytest.mark.parametrize("amsgrad,torch_mode,wd", [(False, False, 0.0), (True, False, 1e-2), (False, True, 0.0)])
+def test_adam_fused(n, amsgrad, torch_mode, wd):
+    torch.manual_seed(n + 1)
+    p, m, v, vm = torch.randn(n), torch.zeros(n), torch.zeros(n), torch.zeros(n)
+    pd, md, vd, vmd = p.to(DEV), m.to(DEV), v.to(DEV), vm.to(DEV)
+    for t in range(1, 4):
+        g = torch.randn(n)
+        kw = dict(lr=1e-2, betas=(0.9, 0.999), eps=1e-8, weight_decay=wd, step=t, amsgrad=amsgrad,
+                  torch_mode=torch_mode)
+        ref.adam_step([g], p, m, v, vm if amsgrad else None, None, False, 1.0, **kw)
+        ops.adam_step([g.to(DEV)], pd, md, vd, vmd if amsgrad else None, None, False, 1.0, **kw)
+    torch.testing.assert_close(pd.cpu(), p, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(vd.cpu(), v, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("n", [1, 255, 256, 1000, 1 << 20])
+@pytest.mark.parametrize("ef,sr", [(False, False), (True, False), (False, True)])
+def test_q8_encode_matches_reference(n, ef, sr):
+    torch.manual_seed(n)
+    x = torch.randn(n) * 3
+    nb = (n + 255) // 256
+    q, s = torch.empty(n, dtype=torch.int8), torch.empty(nb)
+    r = torch.randn(n) * 0.01 if ef else None
+    rd = r.to(DEV) if ef else None
+    qd, sd = torch.empty(n, dtype=torch.int8, device=DEV), torch.empty(nb, device=DEV)
+    ref.q8_encode(x, r, q, s, sr, 99)
+    ops.q8_encode(x.to(DEV), rd, qd, sd, sr, 99)
+    torch.testing.assert_close(sd.cpu(), s, rtol=1e-6, atol=0)
+    mism = (qd.cpu().int() - q.int()).abs()
+    assert mism.max() <= 1 and (mism > 0).float().mean() < 1e-3  # rint tie / fma corner cases only
+    if ef:
+        torch.testing.assert_close(rd.cpu(), r, rtol=0, atol=float(s.max()) * 1.01)
+    acc = torch.zeros(n, device=DEV)
+    ops.q8_aggregate([qd, qd], [sd, sd], acc, 0.5)
+    torch.testing.assert_close(acc.cpu(), ref.q8_dequant(qd.cpu(), sd.cpu()), rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("n,k", [(10, 3), (1000, 10), (4099, 41), (1 << 20, 10486), (3_000_001, 30001)])
+@pytest.mark.parametrize("vdt", [torch.float32, torch.bfloat16])
+def test_topk_exact(n, k, vdt):
+    torch.manual_seed(n)
+    x = torch.randn(n)
+    x[: n // 10] = x[0]  # force many ties at some magnitude
+    idx, val = torch.empty(k, dtype=torch.int32), torch.empty(k, dtype=vdt)
+    ref.topk_encode(x, None, k, idx, val)
+    idd, vd = torch.empty(k, dtype=torch.int32, device=DEV), torch.empty(k, dtype=vdt, device=DEV)
+    ops.topk_encode(x.to(DEV), None, k, idd, vd)
+    assert torch.equal(idd.cpu(), idx)
+    assert torch.equal(vd.cpu(), val)
+    acc = torch.zeros(n, device=DEV)
+    ops.topk_accumulate(idd, vd, acc, 2.0)
+    want = torch.zeros(n)
+    want[idx.long()] = val.float() * 2
+    torch.testing.assert_close(acc.cpu(), want)
+
+
+def test_topk_error_feedback_conserves_mass():
+    n, k = 100_000, 1000
+    g = torch.randn(n, device=DEV)
+    r = torch.randn(n, device=DEV) * 0.1
+    total = g + r
+    idx = torch.empty(k, dtype=torch.int32, device=DEV)
+    val = torch.empty(k, device=DEV)
+    ops.topk_encode(g, r, k, idx, val)
+    acc = torch.zeros(n, device=DEV)
+    ops.topk_accumulate(idx, val, acc)
+    torch.testing.assert_close(acc + r, total, rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("spec", ["fp32", "bf16", "int8", "int8_sr", "topk:0.01", "topk_bf16:0.05", "topk_int8:0.02"])
+def test_codec_gpu_matches_cpu(spec):
+    torch.manual_seed(0)
+    n = 50_000
+    x = torch.randn(n)
+    outs = []
+    for dev in ("cpu", DEV):
+        c = codecs.get_codec(spec)
+        lay = c.layout(n)
+        buf = torch.empty(lay.nbytes, dtype=torch.uint8, device=dev)
+        st = c.init_state(n, dev)
+        c.encode_into(x.to(dev), lay.views(buf), st)
+        acc = torch.zeros(n, device=dev)
+        c.accumulate([lay.views(buf)], acc)
+        outs.append(acc.cpu())
+    tol = 1e-6 if spec in ("fp32", "topk:0.01") else (2e-2 if "int8" in spec else 1e-2)
+    torch.testing.assert_close(outs[1], outs[0], rtol=tol, atol=tol)
