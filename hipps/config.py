@@ -1,0 +1,81 @@
+"""PSConfig: every engine knob in one place.
+
+The reference has only constructor kwargs (ps.py:54-59) and hard-coded constants (pool size
+200 ps.py:85, blosc level 0 mpi_comms.py:18, 32-byte sentinel mpi_comms.py:80, 15 KiB slot floor
+mpi_comms.py:82-83, accumulate count 32 README.md:69).  Here they are fields, filled from
+kwargs, then overridden by ``HIPPS_<FIELD>`` environment variables (e.g. ``HIPPS_MODE=ps_async``,
+``HIPPS_CODEC=topk:0.01``, ``HIPPS_ACCUMULATE=8``).
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+from dataclasses import dataclass, fields
+from typing import Optional
+
+MODES = ("auto", "local", "allgather", "ps_sync", "ps_async")
+
+
+@dataclass
+class PSConfig:
+    # local | allgather (reference ps.py semantics) | ps_sync | ps_async (AsySG-InCon)
+    mode: str = "auto"
+    # codec spec or object; see hipps.codecs.get_codec
+    codec: object = None
+    # async PS: gradients summed per update (README.md:69 uses 32); 0 -> world size
+    accumulate: int = 0
+    # async PS: drop gradients computed on params older than (version - staleness); -1 = never
+    staleness: int = -1
+    # async PS: a worker blocks in irequest_params() when it is more than this many versions behind
+    max_delay: int = 4
+    # bucket size for hook-driven encode overlap
+    bucket_mb: float = 64.0
+    # scale the rank-summed gradient by 1/accumulate (reference sums: ps.py:176)
+    average: bool = False
+    # encode buckets from post-accumulate-grad hooks on a side stream during backward
+    overlap: bool = True
+    # published-parameter wire dtype for PS modes: 'fp32' | 'bf16'
+    param_wire: str = "fp32"
+    # host pickle slow path compression level (mpi_comms.py:18; 0 = framing only)
+    compress_level: int = 0
+    # Adam eps placement: 'reference' (ps.py:255) or 'torch'
+    adam_variant: str = "reference"
+    # all-gather a hash of the posting sequence each step and assert equality (race detector)
+    debug_check_order: bool = False
+    # metrics JSONL path (per rank; '{rank}' is substituted)
+    metrics_path: Optional[str] = None
+
+    @classmethod
+    def from_kwargs(cls, **kw) -> "PSConfig":
+        names = {f.name for f in fields(cls)}
+        cfg = cls(**{k: v for k, v in kw.items() if k in names and v is not None})
+        cfg.apply_env()
+        cfg.validate()
+        return cfg
+
+    def apply_env(self):
+        for f in fields(self):
+            v = os.environ.get("HIPPS_" + f.name.upper())
+            if v is None:
+                continue
+            cur = getattr(self, f.name)
+            if isinstance(cur, bool) or f.type in ("bool",):
+                val = v.lower() in ("1", "true", "yes", "on")
+            elif isinstance(cur, int) and not isinstance(cur, bool):
+                val = int(v)
+            elif isinstance(cur, float):
+                val = float(v)
+            else:
+                val = v
+            setattr(self, f.name, val)
+
+    def validate(self):
+        if self.mode not in MODES:
+            raise ValueError(f"mode must be one of {MODES}, got {self.mode!r}")
+        if self.param_wire not in ("fp32", "bf16"):
+            raise ValueError("param_wire must be 'fp32' or 'bf16'")
+        if self.adam_variant not in ("reference", "torch"):
+            raise ValueError("adam_variant must be 'reference' or 'torch'")
+
+    def replace(self, **kw) -> "PSConfig":
+        return dataclasses.replace(self, **kw)

@@ -1,0 +1,256 @@
+"""Reference-compatible optimizer API: ``MPI_PS``, ``SGD``, ``Adam`` (ps.py:53-261).
+
+Constructor parity with the reference (ps.py:54-59)::
+
+    opt = SGD(model.named_parameters(), model.parameters(), lr=0.1, momentum=0.9,
+              code=codec, cuda=True)
+    loss, data = opt.step()            # (loss, metrics) like ps.py:193
+
+``named_params`` feeds the gradient hooks and names; ``*args`` goes to ``torch.optim`` exactly as
+in the reference MRO (``SGD(MPI_PS, torch.optim.SGD)``).  If ``*args`` is omitted the params are
+taken from ``named_params``.  ``optim`` ('sgd'/'adam') is inferred from the class.
+
+What changed underneath (MI355X design):
+  * parameters/gradients live in one flat fp32 buffer (hipps/parallel/flat.py); ``param.name``
+    is not set (it is read-only on torch >= 2, ps.py:64) -- names are kept in a dict;
+  * the update is ONE fused HIP kernel per param group (decode + sum_W + wd + momentum/Adam +
+    optional publish cast) instead of ~6 eager ops per tensor (ps.py:197-261);
+  * the exchange strategy is a config knob (``mode``): 'allgather' reproduces ps.py:140-190,
+    'ps_sync' and 'ps_async' are the centralized PS of README.md:56-81.
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, Iterable, List, Optional, Tuple
+
+import torch
+
+from . import ops
+from .codecs import get_codec
+from .config import PSConfig
+from .parallel import dist as hdist
+from .parallel.flat import FlatStore
+
+
+class MPI_PS(torch.optim.Optimizer):
+    """Base PS optimizer (ps.py:53).  Subclasses provide ``_update_group``."""
+
+    optim = "base"
+
+    def __init__(self, named_params, *args, names=(), optim=None, code=None, use_mpi=True, cuda=None,
+                 mode=None, config: Optional[PSConfig] = None, accumulate=None, staleness=None, average=None,
+                 bucket_mb=None, overlap=None, param_wire=None, max_delay=None, adam_variant=None,
+                 debug_check_order=None, metrics_path=None, **kwargs):
+        named_params = list(named_params)
+        if named_params and not isinstance(named_params[0], (tuple, list)):
+            named_params = [(f"param{i}", p) for i, p in enumerate(named_params)]
+        if not args:
+            args = ([p for _, p in named_params],)
+        super().__init__(*args, **kwargs)
+        if optim is not None and optim != self.optim and self.optim != "base":
+            raise ValueError(f"optim={optim!r} does not match optimizer class {type(self).__name__}")
+        self.code = code
+        self.use_mpi = use_mpi
+        self.cuda = cuda
+        self.names = list(names)
+        base = config or PSConfig()
+        over = {k: v for k, v in dict(mode=mode, codec=code, accumulate=accumulate, staleness=staleness,
+                                      average=average, bucket_mb=bucket_mb, overlap=overlap, param_wire=param_wire,
+                                      max_delay=max_delay, adam_variant=adam_variant,
+                                      debug_check_order=debug_check_order, metrics_path=metrics_path).items()
+                if v is not None}
+        self.cfg = base.replace(**over)
+        self.cfg.apply_env()
+        self.cfg.validate()
+        self.codec = get_codec(self.cfg.codec)
+        if self.code is None:
+            self.code = self.codec
+        # names: named_params order (the reference sets param.name, ps.py:63-64)
+        self.param_names: Dict[int, str] = {id(p): n for n, p in named_params}
+        groups = [g["params"] for g in self.param_groups]
+        seen = {id(p) for g in groups for p in g}
+        missing = [n for n, p in named_params if id(p) not in seen]
+        if missing:
+            raise ValueError(f"named parameters not in the optimizer's param groups: {missing[:5]}")
+        dev = groups[0][0].device
+        self.world = hdist.current()
+        self.store = FlatStore(groups, self.param_names, device=dev)
+        self._init_state()
+        self.steps = 0
+        self.engine = self._make_engine()
+        self._metrics = None
+        if self.cfg.metrics_path:
+            from .utils.metrics import MetricsWriter
+
+            self._metrics = MetricsWriter(self.cfg.metrics_path, self.world.rank)
+
+    # ------------------------------------------------------------------ engine
+    def _make_engine(self):
+        from .parallel.engine import AllGatherEngine, LocalEngine, PSSyncEngine
+
+        mode = self.cfg.mode
+        if mode == "auto":
+            mode = "allgather" if self.world.size > 1 else "local"
+        self.mode = mode
+        if mode == "local":
+            if self.world.size > 1:
+                raise ValueError("mode='local' with world size > 1")
+            return LocalEngine(self, self.cfg, self.store, self.codec, self.world)
+        if mode == "allgather":
+            return AllGatherEngine(self, self.cfg, self.store, self.codec, self.world)
+        if mode == "ps_sync":
+            return PSSyncEngine(self, self.cfg, self.store, self.codec, self.world)
+        if mode == "ps_async":
+            from .parallel.ps_async import PSAsyncEngine
+
+            return PSAsyncEngine(self, self.cfg, self.store, self.codec, self.world)
+        raise ValueError(mode)
+
+    # ------------------------------------------------------------------ state
+    def _init_state(self):
+        """Flat optimizer state; per-param torch-compatible views in self.state."""
+        self.flat_state: Dict[str, torch.Tensor] = {}
+        self._group_steps = [0] * len(self.param_groups)
+
+    def _ensure_state(self, key: str) -> torch.Tensor:
+        if key not in self.flat_state:
+            buf = self.store.new_buffer()
+            self.flat_state[key] = buf
+            for i, s in enumerate(self.store.slots):
+                self.state[s.param][key] = self.store.param_view(buf, i)
+        return self.flat_state[key]
+
+    def _update_flat(self, sources: List[torch.Tensor], target: torch.Tensor, gscale: float, zero_src: bool = False,
+                     pub: Optional[torch.Tensor] = None):
+        """Apply the optimizer to flat ``target`` from flat gradient ``sources`` (summed)."""
+        for gi, group in enumerate(self.param_groups):
+            a, b = self.store.group_ranges[gi]
+            if b == a:
+                continue
+            self._group_steps[gi] += 1
+            self._update_group(gi, group, [s[a:b] for s in sources], target[a:b], gscale, zero_src,
+                               None if pub is None else pub[a:b])
+
+    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub):
+        raise NotImplementedError
+
+    # ------------------------------------------------------------------ public API
+    @torch.no_grad()
+    def step(self, closure=None):
+        """One exchange + update.  Returns ``(loss, data)`` like the reference (ps.py:193)."""
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        self.steps += 1
+        t0 = time.perf_counter()
+        data = self.engine.step()
+        data["step_time"] = time.perf_counter() - t0
+        if self._metrics is not None:
+            self._metrics.write(self.steps, data)
+        return loss, data
+
+    def zero_grad(self, set_to_none: bool = False):
+        """Zero the flat gradient buffer (grads stay views; set_to_none is ignored on purpose)."""
+        if hasattr(self, "engine"):
+            self.engine.before_zero_grad() if hasattr(self.engine, "before_zero_grad") else None
+        self.store.zero_grad()
+
+    def irequest_params(self):
+        """AsySG-InCon parameter refresh (README.md:63): adopt the newest published params that
+        have arrived, without waiting for the rest (inconsistent read).  No-op in sync modes."""
+        return self.engine.irequest_params()
+
+    def close(self):
+        if getattr(self, "engine", None) is not None:
+            self.engine.close()
+            self.engine = None
+        if self._metrics is not None:
+            self._metrics.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def state_dict(self):
+        sd = super().state_dict()
+        sd["hipps"] = {"steps": self.steps, "group_steps": list(self._group_steps), "mode": self.mode,
+                       "codec": self.codec.name}
+        return sd
+
+    def load_state_dict(self, state_dict):
+        extra = state_dict.get("hipps", {})
+        sd = {k: v for k, v in state_dict.items() if k != "hipps"}
+        # torch's loader replaces per-param tensors; copy them back into our flat buffers
+        super().load_state_dict(sd)
+        keys = {k for st in self.state.values() for k, v in st.items() if torch.is_tensor(v) and v.dim() > 0}
+        for key in sorted(keys):
+            buf = self._ensure_state_nocopy(key)
+            for i, s in enumerate(self.store.slots):
+                t = self.state[s.param].get(key)
+                v = self.store.param_view(buf, i)
+                if t is not None and t.data_ptr() != v.data_ptr():
+                    v.copy_(t)
+                self.state[s.param][key] = v
+        self.steps = extra.get("steps", self.steps)
+        if "group_steps" in extra:
+            self._group_steps = list(extra["group_steps"])
+
+    def _ensure_state_nocopy(self, key):
+        if key not in self.flat_state:
+            self.flat_state[key] = self.store.new_buffer()
+        return self.flat_state[key]
+
+
+class SGD(MPI_PS, torch.optim.SGD):
+    """Reference SGD (ps.py:195-214): wd, momentum (buf = d_p on first step), dampening,
+    nesterov, p -= lr*d_p.  Fused into one kernel per param group."""
+
+    optim = "sgd"
+
+    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub):
+        mom = group.get("momentum", 0) or 0
+        a, b = self.store.group_ranges[gi]
+        buf = self._ensure_state("momentum_buffer")[a:b] if mom else None
+        first = mom and not self._momentum_started(gi)
+        ops.sgd_step(srcs, target, buf, pub, zero_src, gscale, lr=group["lr"],
+                     weight_decay=group.get("weight_decay", 0) or 0, momentum=mom,
+                     dampening=group.get("dampening", 0) or 0, nesterov=bool(group.get("nesterov", False)),
+                     first=bool(first))
+
+    def _momentum_started(self, gi):
+        started = getattr(self, "_mom_started", None)
+        if started is None:
+            started = self._mom_started = set()
+        if gi in started:
+            return True
+        started.add(gi)
+        return False
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        if "momentum_buffer" in self.flat_state:
+            self._mom_started = set(range(len(self.param_groups)))
+
+
+class Adam(MPI_PS, torch.optim.Adam):
+    """Reference Adam (ps.py:217-261): eps added to the un-corrected sqrt(v) unless
+    ``adam_variant='torch'``; amsgrad honoured (the reference never passes it, ps.py:185-186)."""
+
+    optim = "adam"
+
+    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub):
+        a, b = self.store.group_ranges[gi]
+        m = self._ensure_state("exp_avg")[a:b]
+        v = self._ensure_state("exp_avg_sq")[a:b]
+        ams = bool(group.get("amsgrad", False))
+        vm = self._ensure_state("max_exp_avg_sq")[a:b] if ams else None
+        step = self._group_steps[gi]
+        for s in self.store.slots:
+            if s.group == gi:
+                self.state[s.param]["step"] = step
+        ops.adam_step(srcs, target, m, v, vm, pub, zero_src, gscale, lr=group["lr"], betas=group["betas"],
+                      eps=group["eps"], weight_decay=group.get("weight_decay", 0) or 0, step=step, amsgrad=ams,
+                      torch_mode=self.cfg.adam_variant == "torch")

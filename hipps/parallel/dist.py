@@ -1,0 +1,97 @@
+"""Process-group plumbing (replaces the reference's module-level MPI.COMM_WORLD globals,
+mpi_comms.py:11-13 / ps.py:71-73).
+
+One process per GPU; ``torch.distributed`` with backend ``nccl`` (= RCCL over xGMI on ROCm)
+for device tensors or ``gloo`` for CPU plumbing.  Launch with ``python -m hipps.launch`` or
+``torch.distributed.run`` (rendezvous on 127.0.0.1).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class World:
+    rank: int = 0
+    size: int = 1
+    local_rank: int = 0
+    backend: Optional[str] = None
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def distributed(self) -> bool:
+        return self.size > 1
+
+    @property
+    def is_ps(self) -> bool:
+        return self.rank == 0
+
+
+def init_from_env(backend: Optional[str] = None, timeout_s: float = 600.0) -> World:
+    """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* if present; bind rank->GPU."""
+    rank = int(os.environ.get("RANK", "0"))
+    size = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    if use_gpu:
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+    if size > 1 and not dist.is_initialized():
+        be = backend or ("nccl" if use_gpu else "gloo")
+        kw = {}
+        if be == "nccl" and use_gpu:
+            kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
+        dist.init_process_group(be, rank=rank, world_size=size, timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return current()
+
+
+def current() -> World:
+    if dist.is_available() and dist.is_initialized():
+        be = dist.get_backend()
+        dev = torch.device("cuda", torch.cuda.current_device()) if be == "nccl" else torch.device("cpu")
+        return World(dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", dist.get_rank())), be,
+                     dev)
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    return World(0, 1, 0, None, dev)
+
+
+def barrier(world: Optional[World] = None):
+    w = world or current()
+    if w.size > 1:
+        if w.backend == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def all_gather_into(out: torch.Tensor, inp: torch.Tensor, world: World, group=None):
+    """out[W * n] <- concat_w inp_w   (one collective; gloo falls back to list all_gather)."""
+    if world.size == 1:
+        out[: inp.numel()].copy_(inp)
+        return
+    if world.backend == "nccl":
+        dist.all_gather_into_tensor(out, inp, group=group)
+    else:
+        n = inp.numel()
+        dist.all_gather([out[w * n:(w + 1) * n] for w in range(world.size)], inp, group=group)
+
+
+def gather_into(out: Optional[torch.Tensor], inp: torch.Tensor, world: World, dst: int = 0, group=None):
+    """Root receives concat_w inp_w into out (reference igather, mpi_comms.py:60-93)."""
+    if world.size == 1:
+        out[: inp.numel()].copy_(inp)
+        return
+    n = inp.numel()
+    lst = [out[w * n:(w + 1) * n] for w in range(world.size)] if world.rank == dst else None
+    dist.gather(inp, gather_list=lst, dst=dst, group=group)
+
+
+def broadcast(t: torch.Tensor, world: World, src: int = 0, group=None):
+    if world.size > 1:
+        dist.broadcast(t, src=src, group=group)

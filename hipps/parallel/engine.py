@@ -1,0 +1,265 @@
+"""Exchange engines behind ``MPI_PS.step()``.
+
+  LocalEngine      single process: fused decode+update (codec round trip still applied)
+  AllGatherEngine  the reference's implemented algorithm (ps.py:103-193): every rank encodes,
+                   all-gathers every rank's code, decodes + sums in rank order and steps
+                   locally -> bitwise-identical replicas
+  PSSyncEngine     centralized PS (mpi_comms.py:60-133 primitives): gather codes to rank 0,
+                   rank 0 aggregates + steps, broadcasts the parameters
+  PSAsyncEngine    README.md:56-81 AsySG-InCon (hipps/parallel/ps_async.py)
+
+Shared machinery (Engine): the per-bucket encode pipeline.  Buckets are encoded as soon as
+backward has produced them (post-accumulate-grad hooks) on a side HIP stream, so the codec
+overlaps the rest of backward -- the reference encodes in a 200-thread pool but cannot start
+communicating before every tensor is encoded (ps.py:128-132).
+"""
+from __future__ import annotations
+
+import hashlib
+import time
+from typing import Dict, List, Optional
+
+import torch
+
+from .dist import World, all_gather_into, barrier, broadcast, gather_into
+from .flat import BucketPlan, FlatStore
+
+
+class Engine:
+    name = "base"
+
+    def __init__(self, opt, cfg, store: FlatStore, codec, world: World):
+        self.opt = opt
+        self.cfg = cfg
+        self.store = store
+        self.codec = codec
+        self.world = world
+        self.plan = BucketPlan(store, codec, int(cfg.bucket_mb * (1 << 20)))
+        self.cuda = store.device.type == "cuda"
+        self.wire = self.plan.new_wire()
+        self.codec_state = [codec.init_state(b.numel, store.device) for b in self.plan.buckets]
+        self.comm_stream = torch.cuda.Stream(device=store.device) if self.cuda else None
+        self._encoded = [False] * len(self.plan.buckets)
+        self._bucket_count = [0] * len(self.plan.buckets)
+        self._hooks = []
+        self.steps = 0
+        self._order_log: List[str] = []
+        if cfg.overlap:
+            self._register_hooks()
+
+    # ------------------------------------------------------------------ hooks / encode
+    def _register_hooks(self):
+        for i, s in enumerate(self.store.slots):
+            bi = self.plan.slot_bucket[i]
+
+            def hook(p, bi=bi):
+                self._bucket_count[bi] += 1
+                if self._bucket_count[bi] == len(self.plan.buckets[bi].slot_ids) and not self._encoded[bi]:
+                    self.encode_bucket(bi)
+
+            self._hooks.append(s.param.register_post_accumulate_grad_hook(hook))
+
+    def remove_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+    def encode_bucket(self, bi: int):
+        b = self.plan.buckets[bi]
+        g = self.store.grad[b.lo:b.hi]
+        views = self.plan.views(self.wire, bi)
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.store.device))
+            with torch.cuda.stream(self.comm_stream):
+                self.comm_stream.wait_event(ev)
+                self.codec.encode_into(g, views, self.codec_state[bi])
+        else:
+            self.codec.encode_into(g, views, self.codec_state[bi])
+        self._encoded[bi] = True
+        if self.cfg.debug_check_order:
+            self._order_log.append(f"{bi}:{b.numel}:{self.codec.name}")
+
+    def encode_all(self):
+        """Encode every bucket not yet handled by a hook; returns host seconds spent."""
+        t = time.perf_counter()
+        self.store.attach_grads()
+        for bi in self.plan.ready_order:
+            if not self._encoded[bi]:
+                self.encode_bucket(bi)
+        self._encoded = [False] * len(self._encoded)
+        self._bucket_count = [0] * len(self._bucket_count)
+        return time.perf_counter() - t
+
+    def _check_order(self):
+        """Race detector: every rank must post the same exchange sequence."""
+        if not self.cfg.debug_check_order or self.world.size == 1:
+            self._order_log.clear()
+            return
+        import torch.distributed as dist
+
+        h = hashlib.sha1("|".join(sorted(self._order_log)).encode()).hexdigest()
+        self._order_log.clear()
+        hs = [None] * self.world.size
+        dist.all_gather_object(hs, h)
+        if len(set(hs)) != 1:
+            raise RuntimeError(f"exchange order mismatch across ranks: {hs}")
+
+    # ------------------------------------------------------------------ decode / update
+    def _sources_dense(self, images: List[torch.Tensor]) -> List[torch.Tensor]:
+        return images
+
+    def apply(self, wire_msgs: List[torch.Tensor], target: torch.Tensor, pub: Optional[torch.Tensor], gscale: float,
+              scratch: Optional[torch.Tensor] = None):
+        """Decode W wire messages, sum in rank order, apply the optimizer to ``target`` (flat)."""
+        if self.codec.fusable:
+            imgs = [self.plan.dense_image(w) for w in wire_msgs]
+            self.opt._update_flat(imgs, target, gscale, zero_src=False, pub=pub)
+        else:
+            acc = scratch if scratch is not None else torch.empty_like(self.store.grad)
+            for bi, b in enumerate(self.plan.buckets):
+                msgs = [self.plan.views(w, bi) for w in wire_msgs]
+                self.codec.accumulate(msgs, acc[b.lo:b.hi], 1.0, False)
+            self.opt._update_flat([acc], target, gscale, zero_src=False, pub=pub)
+
+    def gscale(self, n: int) -> float:
+        return 1.0 / n if self.cfg.average else 1.0
+
+    def step(self) -> Dict[str, float]:
+        raise NotImplementedError
+
+    def irequest_params(self):
+        return None
+
+    def close(self):
+        self.remove_hooks()
+
+    def bytes_per_step(self) -> Dict[str, int]:
+        return {"grad_bytes_sent": self.plan.wire_nbytes}
+
+
+class LocalEngine(Engine):
+    """World size 1: encode (codec round trip, e.g. to study compression) + fused update."""
+
+    name = "local"
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self._scratch = None if self.codec.fusable else torch.empty_like(self.store.grad)
+        self._bypass = self.codec.fusable and self.codec.lossless
+
+    def encode_bucket(self, bi):
+        if self._bypass:  # fp32 identity: the flat grad IS the message
+            self._encoded[bi] = True
+            return
+        super().encode_bucket(bi)
+
+    def step(self):
+        data = {}
+        data["code_wait"] = self.encode_all()
+        t = time.perf_counter()
+        if self.cuda and not self._bypass:
+            torch.cuda.current_stream(self.store.device).wait_stream(self.comm_stream)
+        if self._bypass:
+            self.opt._update_flat([self.store.grad], self.store.data, 1.0, zero_src=False, pub=None)
+        else:
+            self.apply([self.wire], self.store.data, None, 1.0, self._scratch)
+        data["optim_step_time"] = time.perf_counter() - t
+        data["decode_time"] = 0.0
+        data["comm_wait"] = 0.0
+        data.update(self.bytes_per_step())
+        self.steps += 1
+        return data
+
+
+class AllGatherEngine(Engine):
+    """Reference semantics (ps.py:140-190) with static-size device messages: ONE all-gather of
+    the whole wire buffer per step (no per-tensor size round, M1 removed)."""
+
+    name = "allgather"
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        W = self.world.size
+        self.gathered = torch.empty(W * self.plan.wire_nbytes, dtype=torch.uint8, device=self.store.device)
+        self._scratch = None if self.codec.fusable else torch.empty_like(self.store.grad)
+
+    def step(self):
+        data = {}
+        data["code_wait"] = self.encode_all()
+        self._check_order()
+        t = time.perf_counter()
+        if self.cuda:
+            with torch.cuda.stream(self.comm_stream):
+                all_gather_into(self.gathered, self.wire, self.world)
+            torch.cuda.current_stream(self.store.device).wait_stream(self.comm_stream)
+        else:
+            all_gather_into(self.gathered, self.wire, self.world)
+        data["isend_time"] = data["comm_wait"] = time.perf_counter() - t
+        t = time.perf_counter()
+        n = self.plan.wire_nbytes
+        msgs = [self.gathered[w * n:(w + 1) * n] for w in range(self.world.size)]
+        self.apply(msgs, self.store.data, None, self.gscale(self.world.size), self._scratch)
+        data["optim_step_time"] = time.perf_counter() - t
+        data["decode_time"] = 0.0
+        data.update(self.bytes_per_step())
+        data["grad_bytes_recv"] = n * self.world.size
+        self.steps += 1
+        return data
+
+
+class PSSyncEngine(Engine):
+    """Centralized synchronous PS: gather -> rank-0 aggregate+update -> broadcast params."""
+
+    name = "ps_sync"
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        W = self.world.size
+        dev = self.store.device
+        self.gathered = (torch.empty(W * self.plan.wire_nbytes, dtype=torch.uint8, device=dev)
+                         if self.world.is_ps else torch.empty(self.plan.wire_nbytes, dtype=torch.uint8, device=dev))
+        self._scratch = None if self.codec.fusable else torch.empty_like(self.store.grad)
+        self.pub = None
+        if self.cfg.param_wire == "bf16":
+            self.pub = torch.empty(self.store.numel, dtype=torch.bfloat16, device=dev)
+
+    def step(self):
+        data = {}
+        data["code_wait"] = self.encode_all()
+        t = time.perf_counter()
+        cs = self.comm_stream
+        ctx = torch.cuda.stream(cs) if self.cuda else _null()
+        with ctx:
+            gather_into(self.gathered if self.world.is_ps else None, self.wire, self.world)
+        if self.cuda:
+            torch.cuda.current_stream(self.store.device).wait_stream(cs)
+        data["comm_wait"] = time.perf_counter() - t
+        t = time.perf_counter()
+        if self.world.is_ps:
+            n = self.plan.wire_nbytes
+            msgs = [self.gathered[w * n:(w + 1) * n] for w in range(self.world.size)]
+            self.apply(msgs, self.store.data, self.pub, self.gscale(self.world.size), self._scratch)
+        data["optim_step_time"] = time.perf_counter() - t
+        t = time.perf_counter()
+        # ibroadcast of the parameters (mpi_comms.py:127-133 / README.md:76)
+        if self.pub is not None:
+            broadcast(self.pub, self.world, 0)
+            if not self.world.is_ps:
+                from hipps import ops
+
+                ops.convert(self.pub, self.store.data)
+        else:
+            broadcast(self.store.data, self.world, 0)
+        data["bcast_time"] = time.perf_counter() - t
+        data.update(self.bytes_per_step())
+        self.steps += 1
+        return data
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
