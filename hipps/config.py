@@ -26,8 +26,11 @@ class PSConfig:
     accumulate: int = 0
     # async PS: drop gradients computed on params older than (version - staleness); -1 = never
     staleness: int = -1
-    # async PS: a worker blocks in irequest_params() when it is more than this many versions behind
-    max_delay: int = 4
+    # async PS: a worker blocks in irequest_params() until the published params include all but
+    # its newest `max_delay` gradients (SSP-style bound; 0 = synchronous per worker; -1 = unbounded)
+    max_delay: int = -1
+    # async PS: pull the newest published params at the end of every step() (AsySG-InCon read)
+    auto_pull: bool = True
     # bucket size for hook-driven encode overlap
     bucket_mb: float = 64.0
     # scale the rank-summed gradient by 1/accumulate (reference sums: ps.py:176)

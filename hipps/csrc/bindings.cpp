@@ -24,6 +24,10 @@ int64_t topk_workspace_bytes(int64_t n);
 void topk_accumulate(at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale);
 void topk_q8_accumulate(at::Tensor idx, at::Tensor q, at::Tensor scales, at::Tensor acc, double gscale);
 void topk_q8_residual(at::Tensor idx, at::Tensor v, at::Tensor q, at::Tensor scales, at::Tensor resid);
+namespace rt {
+void bind_control(pybind11::module& m);
+void bind_ipc(pybind11::module& m);
+}  // namespace rt
 }  // namespace hipps
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -39,4 +43,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("topk_accumulate", &hipps::topk_accumulate, "acc[idx] += gscale * val");
   m.def("topk_q8_accumulate", &hipps::topk_q8_accumulate, "acc[idx] += gscale * deq(q)");
   m.def("topk_q8_residual", &hipps::topk_q8_residual, "EF: r[idx] += v - deq(q)");
+  hipps::rt::bind_control(m);
+  hipps::rt::bind_ipc(m);
 }

@@ -1,0 +1,349 @@
+"""Asynchronous parameter server: AsySG-InCon (README.md:56-81, arXiv:1506.08272).
+
+Reference design (pseudo-code only in the reference; ``irequest_params`` never existed in code):
+rank 0 receives gradients from ``MPI.ANY_SOURCE`` until it has 32, sums them, steps, and
+``ibcast``s the parameters; workers ``send`` gradients and read whatever parameters have
+arrived (inconsistent reads).
+
+hipps design (one node, one process per GPU, rank 0 = PS *and* worker 0):
+
+  data plane   one-sided device copies over xGMI into/out of PS-owned HIP-IPC mailboxes
+               (hipps/csrc/runtime/ipc.cpp): worker -> PS gradient slots (2 per worker), PS ->
+               workers published parameter buffers (3, rotating).  Nothing on the PS posts a
+               receive, so no RCCL kernel ever spins waiting for a straggler.
+  control      POSIX-shm doorbells (hipps/csrc/runtime/control.cpp) = the ANY_SOURCE: the PS
+               thread waits on all workers' push sequence words at once.
+  PS loop      a thread on rank 0 with its own HIP stream: decode+accumulate each arriving
+               message (fused codec kernel), after M messages run the fused optimizer kernel on
+               the fp32 master, write the new version into the next publish buffer, then ring
+               the version doorbell -- all stream-ordered, the thread never synchronises.
+  worker       encode (side stream, overlapped with backward) -> copy into its mailbox slot ->
+               doorbell; ``irequest_params()`` adopts the newest published version if one has
+               landed (a D2D copy on the compute stream) and never waits unless ``max_delay`` asks.
+  staleness    ConditionalAccumulator semantics (README.md:33-35): a gradient computed on params
+               older than ``version - staleness`` is dropped (staleness=-1 keeps all).
+
+CPU runs use the same protocol with POSIX-shm mailboxes and the torch reference ops.
+"""
+from __future__ import annotations
+
+import os
+import secrets
+import threading
+import time
+import traceback
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from hipps import ops
+from hipps.ops._native import native
+from .dist import barrier
+from .engine import Engine
+
+TIMEOUT_US = int(float(os.environ.get("HIPPS_TIMEOUT_S", "600")) * 1e6)
+
+
+def _align(x: int, a: int = 256) -> int:
+    return (x + a - 1) // a * a
+
+
+class PSAsyncEngine(Engine):
+    name = "ps_async"
+
+    def __init__(self, opt, cfg, store, codec, world):
+        super().__init__(opt, cfg, store, codec, world)
+        C = native()
+        self.C = C
+        W = world.size
+        self.W = W
+        self.rank = world.rank
+        self.M = cfg.accumulate if cfg.accumulate > 0 else W
+        self.SLOTS = C.ControlBlock.SLOTS
+        self.NPUB = C.ControlBlock.NPUB
+        self.pub_dtype = torch.bfloat16 if cfg.param_wire == "bf16" else torch.float32
+        esz = torch.empty((), dtype=self.pub_dtype).element_size()
+        self.slot_bytes = _align(self.plan.wire_nbytes)
+        self.pub_bytes = _align(store.numel * esz)
+        self.mail_off = 0
+        self.pub_off = W * self.SLOTS * self.slot_bytes
+        total = self.pub_off + self.NPUB * self.pub_bytes
+
+        # ---- rendezvous: rank 0 creates control block + mailboxes, others map them ----------
+        token = secrets.token_hex(6) if self.rank == 0 else None
+        handle = None
+        if self.rank == 0:
+            self.ctl_name = f"/hipps_ctl_{os.getpid()}_{token}"
+            self.mb_name = f"/hipps_mb_{os.getpid()}_{token}"
+            self.ctl = C.ControlBlock(self.ctl_name, W, True)
+            if self.cuda:
+                self.mailbox = C.DeviceMailbox(total)
+                handle = self.mailbox.handle()
+            else:
+                self.mailbox = C.HostMailbox(self.mb_name, total, True)
+        meta = [getattr(self, "ctl_name", None), getattr(self, "mb_name", None), handle]
+        if W > 1:
+            dist.broadcast_object_list(meta, src=0)
+        if self.rank != 0:
+            self.ctl_name, self.mb_name, handle = meta
+            self.ctl = C.ControlBlock(self.ctl_name, W, False)
+            if self.cuda:
+                self.mailbox = C.DeviceMailbox(handle, total)
+            else:
+                self.mailbox = C.HostMailbox(self.mb_name, total, False)
+        barrier(world)
+        if self.rank == 0:  # everyone has mapped: remove the names (no /dev/shm leftovers)
+            self.ctl.unlink()
+            if not self.cuda:
+                self.mailbox.unlink()
+        self.mem = self.mailbox.tensor()
+
+        # ---- PS state on rank 0 ------------------------------------------------------------
+        self.seq = 0
+        self.local_ver = -1
+        self._stats = {"drops": 0, "staleness_sum": 0, "accumulated": 0}
+        self._err: Optional[str] = None
+        self._thread = None
+        self.enc_event = torch.cuda.Event() if self.cuda else None
+        if self.rank == 0:
+            self.master = store.data.detach().clone()
+            self.acc = torch.zeros_like(store.data)
+            self.ps_stream = torch.cuda.Stream(device=store.device) if self.cuda else None
+            self.ver = 0
+            self._publish_initial()
+            self._thread = threading.Thread(target=self._serve_guard, name="hipps-ps", daemon=True)
+            self._thread.start()
+        barrier(world)
+        # every replica starts from the PS's version 0 (ranks may have initialised differently)
+        self.irequest_params(block_for=0)
+        if self.cuda:
+            torch.cuda.current_stream(store.device).synchronize()
+
+    # ------------------------------------------------------------------ memory views
+    def slot_buf(self, rank: int, slot: int) -> torch.Tensor:
+        o = self.mail_off + (rank * self.SLOTS + slot) * self.slot_bytes
+        return self.mem[o:o + self.plan.wire_nbytes]
+
+    def pub_buf(self, b: int) -> torch.Tensor:
+        o = self.pub_off + b * self.pub_bytes
+        esz = torch.empty((), dtype=self.pub_dtype).element_size()
+        return self.mem[o:o + self.store.numel * esz].view(self.pub_dtype)
+
+    # ------------------------------------------------------------------ PS side
+    def _ring(self, stream, field, idx, value):
+        if stream is not None:
+            self.ctl.enqueue_store(stream.cuda_stream, field, idx, value)
+        else:
+            self.ctl.store(field, idx, value)
+
+    def _publish_initial(self):
+        C = self.C
+        pub = self.pub_buf(0)
+        ops.convert(self.master, pub)
+        if self.cuda:
+            torch.cuda.current_stream(self.store.device).synchronize()
+        self.ctl.store(C.F_BUF_VER, 0, 0)
+        self.ctl.store(C.F_PUB_VER, 0, 0)
+
+    def _serve_guard(self):
+        try:
+            if self.cuda:
+                torch.cuda.set_device(self.store.device)
+                with torch.cuda.stream(self.ps_stream):
+                    self._serve()
+                self.ps_stream.synchronize()
+            else:
+                self._serve()
+        except BaseException:
+            self._err = traceback.format_exc()
+            self.ctl.store(self.C.F_ERROR, 0, 1)
+
+    def _serve(self):
+        C, W = self.C, self.W
+        seen = [0] * W
+        pending_incl: List[tuple] = []  # (rank, seq) accumulated since the last update
+        count = 0
+        gscale = 1.0 / self.M if self.cfg.average else 1.0
+        st = self.ps_stream
+        with torch.no_grad():
+            while True:
+                ready = self.ctl.wait_any(seen, 20000)
+                for i in ready:
+                    s_now = self.ctl.load(C.F_PUSH_SEQ, i)
+                    for s in range(seen[i] + 1, s_now + 1):
+                        slot = s % self.SLOTS
+                        pv = self.ctl.load(C.F_PUSH_VER, i * self.SLOTS + slot)
+                        stale = self.ver - pv
+                        if 0 <= self.cfg.staleness < stale:
+                            self._stats["drops"] += 1
+                            self.ctl.fetch_add(C.F_DROPS, 0, 1)
+                            self._ring(st, C.F_ACK_SEQ, i, s)  # stream-ordered: acks stay monotonic
+                            pending_incl.append((i, s))  # counts as handled for max_delay
+                            continue
+                        msg = self.slot_buf(i, slot)
+                        for bi, b in enumerate(self.plan.buckets):
+                            self.codec.accumulate([self.plan.views(msg, bi)], self.acc[b.lo:b.hi], 1.0, True)
+                        self._ring(st, C.F_ACK_SEQ, i, s)
+                        pending_incl.append((i, s))
+                        self._stats["accumulated"] += 1
+                        self._stats["staleness_sum"] += max(0, stale)
+                        count += 1
+                        if count >= self.M:
+                            self._update(pending_incl, gscale)
+                            pending_incl = []
+                            count = 0
+                    seen[i] = s_now
+                if self._should_stop(seen):
+                    break
+
+    def _update(self, included, gscale):
+        C = self.C
+        self.ver += 1
+        b = self.ver % self.NPUB
+        self.ctl.store(C.F_BUF_VER, b, -1)  # readers skip a buffer being rewritten
+        self.opt._update_flat([self.acc], self.master, gscale, zero_src=True, pub=self.pub_buf(b))
+        st = self.ps_stream
+        # order matters: buffer stamp -> version word -> per-worker "included" words, so a worker
+        # that sees its message included also sees a version containing it
+        self._ring(st, C.F_BUF_VER, b, self.ver)
+        self._ring(st, C.F_PUB_VER, 0, self.ver)
+        last = {}
+        for i, s in included:
+            last[i] = max(last.get(i, 0), s)
+        for i, s in last.items():
+            self._ring(st, C.F_INCL_SEQ, i, s)
+        self.ctl.fetch_add(C.F_UPDATES, 0, 1)
+
+    def _should_stop(self, seen):
+        C = self.C
+        if self.ctl.load(C.F_PS_STOP, 0):
+            return True
+        for i in range(self.W):
+            stop = self.ctl.load(C.F_STOP, i)
+            if stop == 0 or seen[i] < stop - 1:
+                return False
+        return True
+
+    # ------------------------------------------------------------------ worker side
+    def _check_error(self):
+        if self.ctl.load(self.C.F_ERROR, 0):
+            msg = self._err or "parameter-server thread failed on rank 0"
+            raise RuntimeError(msg)
+
+    def before_zero_grad(self):
+        # the side-stream encode reads the flat grads: do not zero them under it
+        if self.cuda and self.enc_event is not None:
+            torch.cuda.current_stream(self.store.device).wait_event(self.enc_event)
+
+    def step(self):
+        C = self.C
+        data = {}
+        data["code_wait"] = self.encode_all()
+        self._check_error()
+        self.seq += 1
+        s = self.seq
+        slot = s % self.SLOTS
+        t = time.perf_counter()
+        if s > self.SLOTS:  # slot reuse: message s - SLOTS must have been consumed
+            if not self.ctl.wait_ge(C.F_ACK_SEQ, self.rank, s - self.SLOTS, TIMEOUT_US):
+                self._check_error()
+                raise TimeoutError(f"rank {self.rank}: PS did not consume message {s - self.SLOTS}")
+        data["slot_wait"] = time.perf_counter() - t
+        t = time.perf_counter()
+        dst = self.slot_buf(self.rank, slot)
+        if self.cuda:
+            cs = self.comm_stream
+            self.enc_event.record(cs)
+            with torch.cuda.stream(cs):
+                dst.copy_(self.wire, non_blocking=True)
+            self._ring(cs, C.F_PUSH_VER, self.rank * self.SLOTS + slot, self.local_ver)
+            self._ring(cs, C.F_PUSH_SEQ, self.rank, s)
+        else:
+            dst.copy_(self.wire)
+            self.ctl.store(C.F_PUSH_VER, self.rank * self.SLOTS + slot, self.local_ver)
+            self.ctl.store(C.F_PUSH_SEQ, self.rank, s)
+        data["isend_time"] = time.perf_counter() - t
+        t = time.perf_counter()
+        if self.cfg.auto_pull:
+            data["pulled"] = float(self.irequest_params())
+        data["comm_wait"] = time.perf_counter() - t
+        data["version"] = float(self.local_ver)
+        data["optim_step_time"] = 0.0
+        data["decode_time"] = 0.0
+        data.update(self.bytes_per_step())
+        data["grad_bytes_recv"] = 0
+        data["param_bytes_pulled"] = self.store.numel * torch.empty((), dtype=self.pub_dtype).element_size() \
+            if data.get("pulled") else 0
+        self.steps += 1
+        return data
+
+    def irequest_params(self, block_for: Optional[int] = None) -> bool:
+        """Adopt the newest published parameter version if it has landed (README.md:63).
+
+        ``block_for=v`` waits until version >= v is published.  ``cfg.max_delay >= 0`` waits
+        until the published params include all but the newest ``max_delay`` own gradients."""
+        C = self.C
+        if block_for is not None:
+            if not self.ctl.wait_ge(C.F_PUB_VER, 0, block_for, TIMEOUT_US):
+                self._check_error()
+                raise TimeoutError("no published parameters")
+        if self.cfg.max_delay >= 0 and self.seq - self.cfg.max_delay > 0:
+            need = self.seq - self.cfg.max_delay
+            if not self.ctl.wait_ge(C.F_INCL_SEQ, self.rank, need, TIMEOUT_US):
+                self._check_error()
+                raise TimeoutError(f"rank {self.rank}: params never caught up to message {need}")
+        for _ in range(8):
+            v = self.ctl.load(C.F_PUB_VER, 0)
+            if v <= self.local_ver:
+                return False
+            b = v % self.NPUB
+            if self.ctl.load(C.F_BUF_VER, b) != v:
+                continue  # rewritten under us: re-read the version word
+            src = self.pub_buf(b)
+            if self.pub_dtype == torch.float32:
+                self.store.data.copy_(src, non_blocking=self.cuda)
+            else:
+                ops.convert(src, self.store.data)
+            if not self.cuda and self.ctl.load(C.F_BUF_VER, b) != v:
+                continue  # torn on the host path: retry (seqlock)
+            self.local_ver = v
+            self.ctl.store(C.F_APPLIED_VER, self.rank, v)
+            return True
+        return False
+
+    def ps_stats(self) -> dict:
+        C = self.C
+        d = dict(self._stats)
+        d["updates"] = self.ctl.load(C.F_UPDATES, 0)
+        d["version"] = self.ctl.load(C.F_PUB_VER, 0)
+        return d
+
+    def close(self):
+        if getattr(self, "_closed", False):
+            return
+        self._closed = True
+        super().close()
+        C = self.C
+        try:
+            if self.cuda:
+                torch.cuda.synchronize(self.store.device)
+            self.ctl.store(C.F_STOP, self.rank, self.seq + 1)
+            if self.rank == 0 and self._thread is not None:
+                deadline = time.time() + TIMEOUT_US / 1e6
+                while self._thread.is_alive() and time.time() < deadline:
+                    self._thread.join(timeout=0.5)
+                if self._thread.is_alive():
+                    self.ctl.store(C.F_PS_STOP, 0, 1)
+                    self._thread.join(timeout=10)
+                if self.cuda:
+                    self.ps_stream.synchronize()
+        finally:
+            if self.rank != 0 and self.cuda:
+                self.mailbox.close()
+        if self._err:
+            raise RuntimeError(self._err)
+
+    def final_params(self) -> Optional[torch.Tensor]:
+        """PS master parameters (rank 0 only) after close()."""
+        return self.master if self.rank == 0 else None

@@ -1,0 +1,89 @@
+"""Async PS (AsySG-InCon) protocol tests on CPU: shm control block + shm mailboxes, gloo rendezvous."""
+import pytest
+import torch
+
+from dist_util import run_world
+from test_dist_cpu import _data, _mlp
+
+
+def _train_async(rank, world, steps, codec, accumulate, max_delay, staleness, opt_name="sgd"):
+    import hipps
+
+    m = _mlp()
+    if rank:  # deliberately different init: the PS's version 0 must win
+        torch.manual_seed(100 + rank)
+        for p in m.parameters():
+            p.data.normal_()
+    cls = hipps.SGD if opt_name == "sgd" else hipps.Adam
+    kw = dict(lr=0.05, momentum=0.9) if opt_name == "sgd" else dict(lr=1e-3)
+    opt = cls(m.named_parameters(), mode="ps_async", code=codec, accumulate=accumulate, max_delay=max_delay,
+              staleness=staleness, **kw)
+    init = [p.detach().clone() for p in m.parameters()]
+    losses = []
+    for s in range(steps):
+        x, y = _data(rank, s % 4)
+        opt.zero_grad()
+        loss = torch.nn.functional.cross_entropy(m(x), y)
+        loss.backward()
+        losses.append(loss.item())
+        opt.step()
+    eng = opt.engine
+    opt.close()  # drains: the PS thread exits only after consuming every pushed message
+    stats = eng.ps_stats()
+    master = eng.final_params() if rank == 0 else None
+    return {"init": init, "losses": losses, "stats": stats, "master": master,
+            "params": [p.detach().clone() for p in m.parameters()]}
+
+
+def test_async_single_rank_sync_delay_equals_local():
+    """W=1, M=1, max_delay=0: every step waits for its own update -> identical to local SGD."""
+    import hipps
+    from test_dist_cpu import _simulate
+
+    out = run_world(_train_async, 1, 5, "fp32", 1, 0, -1)
+    want = _simulate(1, 5, "sgd")  # same data for rank 0, steps 0..4 (s % 4 wraps: recompute)
+    # recompute the reference with the same data schedule
+    m = _mlp()
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="local")
+    for s in range(5):
+        x, y = _data(0, s % 4)
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x), y).backward()
+        opt.step()
+    for a, b in zip(out[0]["params"], m.parameters()):
+        torch.testing.assert_close(a, b.detach(), rtol=0, atol=0)
+    assert out[0]["stats"]["updates"] == 5
+
+
+@pytest.mark.parametrize("codec", ["fp32", "bf16", "topk_int8:0.1"])
+def test_async_three_ranks_converges_and_accounts(codec):
+    steps = 12
+    out = run_world(_train_async, 3, steps, codec, 0, -1, -1)
+    st = out[0]["stats"]
+    # every pushed message is accumulated exactly once; M = W = 3
+    assert st["accumulated"] == 3 * steps
+    assert st["updates"] == steps
+    # all replicas adopted the PS's version 0 at start
+    for r in (1, 2):
+        for a, b in zip(out[0]["init"], out[r]["init"]):
+            assert torch.equal(a, b)
+    # training made progress on every worker
+    for r in range(3):
+        L = out[r]["losses"]
+        assert sum(L[-4:]) / 4 < sum(L[:4]) / 4
+    # after close the PS master holds the last version; bounded staleness
+    assert st["staleness_sum"] / st["accumulated"] < 4
+
+
+def test_async_max_delay_zero_three_ranks_is_ssp_synchronous():
+    out = run_world(_train_async, 3, 6, "fp32", 3, 0, -1)
+    st = out[0]["stats"]
+    assert st["updates"] == 6 and st["accumulated"] == 18
+
+
+def test_async_staleness_drop_and_adam():
+    # M=1 with 3 workers: versions advance on every message; staleness=0 drops most laggards
+    out = run_world(_train_async, 3, 6, "fp32", 1, -1, 0, "adam")
+    st = out[0]["stats"]
+    assert st["accumulated"] + st["drops"] == 18
+    assert st["updates"] == st["accumulated"]
