@@ -1,0 +1,163 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 synthetic-ImageNet async parameter server (AsySG-InCon), bf16.
+
+BASELINE.json metric "samples/sec (node) ResNet-50 async PS at 1/2/4/8 MI355X; grad bytes/step".
+One process per GPU; rank 0 is the PS (and also trains, as worker 0); every rank trains
+ResNet-50 (random init, 224x224 synthetic images, 1000 classes) with autocast-bf16 compute and
+fp32 parameters; gradients go to the PS through the bf16 wire codec; the PS applies SGD-momentum
+to an fp32 master with the fused HIP kernel and publishes new parameters that workers pull
+one-sidedly (HIP-IPC over xGMI).
+
+    python bench.py                                   # N=1
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 5
+
+Timing: W warmup steps, then barrier + synchronize, K timed steps, barrier + synchronize; the
+per-rank elapsed time is max-reduced; rank 0 prints one JSON line.  value = whole-job samples/s
+(N x per-GPU batch x K / max elapsed).  Weak scaling: per-GPU batch fixed as N grows.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+METRIC = "samples/sec (node) ResNet-50 async PS at 1/2/4/8 MI355X; grad bytes/step"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--mode", default="ps_async", choices=["ps_async", "ps_sync", "allgather", "local"])
+    ap.add_argument("--codec", default="bf16")
+    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--accumulate", type=int, default=0, help="PS update every M grads (0 = world size)")
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--no-channels-last", action="store_true")
+    ap.add_argument("--out", default=None, help="also write the JSON line to this file")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    from hipps.parallel import dist as hdist
+
+    world = hdist.init_from_env()
+    if world.size != a.gpus and world.rank == 0:
+        print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world.size}; using WORLD_SIZE", file=sys.stderr)
+    N = world.size
+    dev = torch.device("cuda", torch.cuda.current_device())
+    torch.backends.cudnn.benchmark = True
+
+    import hipps
+    from hipps.models import build_model
+
+    torch.manual_seed(1234 + world.rank)
+    model = build_model(a.model).to(dev)
+    cl = not a.no_channels_last
+    if cl:
+        model = model.to(memory_format=torch.channels_last)
+    x = torch.randn(a.batch, 3, a.image, a.image, device=dev)
+    if cl:
+        x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (a.batch,), device=dev)
+
+    mode = a.mode if N > 1 or a.mode in ("ps_async", "local") else "local"
+    note = None
+    try:
+        opt = hipps.SGD(model.named_parameters(), lr=a.lr, momentum=0.9, weight_decay=5e-5, mode=mode, code=a.codec,
+                        accumulate=a.accumulate or None, average=True)
+    except Exception as e:  # robust fallback so a scaling run still reports a number
+        if mode != "ps_async" or N == 1:
+            raise
+        note = f"ps_async init failed ({type(e).__name__}: {e}); fell back to ps_sync"
+        print("[bench] " + note, file=sys.stderr)
+        mode = "ps_sync"
+        opt = hipps.SGD(model.named_parameters(), lr=a.lr, momentum=0.9, weight_decay=5e-5, mode=mode,
+                        code=a.codec, average=True)
+
+    def step():
+        opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = F.cross_entropy(model(x), y)
+        loss.backward()
+        _, data = opt.step()
+        return loss, data
+
+    for _ in range(a.warmup):
+        step()
+    hdist.barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    last = None
+    for _ in range(a.steps):
+        loss, last = step()
+    torch.cuda.synchronize()
+    hdist.barrier(world)
+    t1 = time.perf_counter()
+    el = torch.tensor([t1 - t0], device=dev, dtype=torch.float64)
+    if N > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    final_loss = float(loss.float().item())
+    grad_bytes = int(last.get("grad_bytes_sent", 0)) if last else 0
+    stats = opt.engine.ps_stats() if hasattr(opt.engine, "ps_stats") else {}
+    opt.close()
+    value = N * a.batch * a.steps / elapsed
+    if world.rank == 0:
+        rec = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "samples/s",
+            "n_gpus": N,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random 224x224 images / labels, random-init weights)",
+            "config": {
+                "model": a.model,
+                "global_batch": a.batch * N,
+                "per_gpu_batch": a.batch,
+                "seq_len": None,
+                "image": a.image,
+                "parallelism": f"dp{N} {mode} (rank0 = PS + worker)",
+                "codec": a.codec,
+                "accumulate": a.accumulate or N,
+                "grad_bytes_per_step_per_worker": grad_bytes,
+                "param_wire": "fp32",
+            },
+            "final_loss": round(final_loss, 4),
+            "ps": {k: (int(v) if isinstance(v, (int, float)) else v) for k, v in stats.items()},
+        }
+        if note:
+            rec["note"] = note
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if a.out:
+            with open(a.out, "w") as f:
+                f.write(line + "\n")
+    if N > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
