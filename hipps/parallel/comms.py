@@ -1,0 +1,202 @@
+"""Object-level communication primitives: the reference ``mpi_comms`` API on torch.distributed.
+
+Reference (mpi4py, host bytearrays): ``igather``/``irecv`` (mpi_comms.py:60-117),
+``ibroadcast``/``irecv1`` (:120-133), ``Iallgather`` (:144-174), ``to_mpi``/``to_mpi_v``
+(:135-141).  These are the "generic Python object" slow path the README asks for
+(README.md:23-27): tensors inside objects become numpy, the object is pickled + framed
+(hipps.utils.serialization), and bytes travel as uint8 tensors -- on the HIP device over RCCL
+when the process group is ``nccl``, on the host over gloo otherwise.  Gradients never take this
+path (they use device wire buffers, hipps.parallel.engine / ps_async).
+
+Fixes relative to the reference:
+  * no fixed 10x / 15 KiB slot guess + sentinel (mpi_comms.py:80-85): sizes are all-gathered
+    first (README.md:30-31 option 1) and slots are exactly max(size);
+  * ``irecv(*igather(obj))`` works (the reference's own test passes the 3-tuple and breaks,
+    test_comms.py:11-12);
+  * ``ibroadcast`` does not require every rank to pass an equal-length object (mpi_comms.py:127-133);
+  * counts are int64 (test_iallgather.py uses int16 and overflows above 32 KiB).
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+from typing import Any, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from hipps.utils.serialization import format_for_send, unformat
+
+
+def _world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size(), dist.get_backend()
+    return 0, 1, None
+
+
+def _dev():
+    _, _, be = _world()
+    if be == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+class Request:
+    """mpi4py-style request wrapper (``Wait``/``Test``) around torch Work handles."""
+
+    def __init__(self, works=None, on_done=None):
+        self.works = [w for w in (works or []) if w is not None]
+        self._done = False
+        self._on_done = on_done
+
+    def Wait(self):
+        if not self._done:
+            for w in self.works:
+                w.wait()
+            if self._on_done:
+                self._on_done()
+            self._done = True
+
+    wait = Wait
+
+    def Test(self) -> bool:
+        if self._done:
+            return True
+        if all(w.is_completed() for w in self.works):
+            self.Wait()
+        return self._done
+
+
+def _to_tensor(b: bytes, n: int, dev) -> torch.Tensor:
+    t = torch.zeros(n, dtype=torch.uint8)
+    if b:
+        t[: len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+    return t.to(dev)
+
+
+def _all_sizes(n: int, dev) -> List[int]:
+    rank, W, _ = _world()
+    if W == 1:
+        return [n]
+    t = torch.tensor([n], dtype=torch.int64, device=dev)
+    out = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(W)]
+    dist.all_gather(out, t)
+    return [int(o.item()) for o in out]
+
+
+@dataclass
+class GatherBuffer:
+    recv: Optional[torch.Tensor]
+    sizes: List[int]
+    slot: int
+
+
+def igather(obj, name="", dst: int = 0, level: int = 0):
+    """Gather a Python object to ``dst``.  Returns ``(recv, req, timing)`` (mpi_comms.py:60-93)."""
+    rank, W, _ = _world()
+    dev = _dev()
+    t = [time.time()]
+    packaged, _ = format_for_send(obj, level)
+    t.append(time.time())
+    sizes = _all_sizes(len(packaged), dev)
+    slot = max(sizes)
+    send = _to_tensor(bytes(packaged), slot, dev)
+    recv = torch.empty(W * slot, dtype=torch.uint8, device=dev) if rank == dst else None
+    t.append(time.time())
+    if W == 1:
+        recv.copy_(send)
+        work = None
+    else:
+        lst = [recv[w * slot:(w + 1) * slot] for w in range(W)] if rank == dst else None
+        work = dist.gather(send, gather_list=lst, dst=dst, async_op=True)
+    t.append(time.time())
+    keep = (send,)  # keep the send buffer alive until completion
+    req = Request([work], on_done=lambda: keep)
+    timing = {"pickle_time": t[1] - t[0], "alloc_time": t[2] - t[1], "igather_time": t[3] - t[2],
+              "alloc_bytes": slot, "name": name}
+    return GatherBuffer(recv, sizes, slot), req, timing
+
+
+def irecv(recv: GatherBuffer, req: Request, timing=None, name="", cuda: bool = False, dst: int = 0):
+    """Complete an igather; the root returns the list of W objects, others None (mpi_comms.py:107-117)."""
+    rank, W, _ = _world()
+    req.Wait()
+    if rank != dst:
+        return None
+    host = recv.recv.cpu().numpy().tobytes()
+    return [unformat(host[w * recv.slot: w * recv.slot + recv.sizes[w]], cuda=cuda) for w in range(W)]
+
+
+def ibroadcast(obj, root: int = 0, level: int = 0):
+    """Broadcast ``obj`` from ``root``; every rank gets it, whatever it passed (mpi_comms.py:127-133)."""
+    rank, W, _ = _world()
+    dev = _dev()
+    packaged = bytes(format_for_send(obj, level)[0]) if rank == root else b""
+    n = torch.tensor([len(packaged)], dtype=torch.int64, device=dev)
+    if W > 1:
+        dist.broadcast(n, src=root)
+    buf = _to_tensor(packaged, int(n.item()), dev)
+    work = dist.broadcast(buf, src=root, async_op=True) if W > 1 else None
+    return buf, Request([work])
+
+
+def irecv1(recv: torch.Tensor, req: Request, cuda: bool = False):
+    """Complete an ibroadcast (mpi_comms.py:120-124)."""
+    req.Wait()
+    return unformat(recv.cpu().numpy().tobytes(), cuda=cuda)
+
+
+def to_mpi_v(v, counts, dtype="byte"):
+    """(buffer, (counts, displacements), dtype) — kept for API parity (mpi_comms.py:135-137)."""
+    displacements = [sum(counts[:i]) for i in range(len(counts))]
+    return (v, (list(counts), displacements), dtype)
+
+
+def to_mpi(v, dtype="byte"):
+    return (v, dtype)
+
+
+class Iallgather:
+    """Variable-size all-gather of byte messages: size round, then payload (mpi_comms.py:144-174)."""
+
+    def __init__(self):
+        self.rank, self.size, _ = _world()
+
+    def _get_counts(self, n: int):
+        dev = _dev()
+        t = torch.tensor([n], dtype=torch.int64, device=dev)
+        if self.size == 1:
+            return Request(), [t]
+        out = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(self.size)]
+        work = dist.all_gather(out, t, async_op=True)
+        return Request([work], on_done=lambda: t), out
+
+    def prepare(self, counts):
+        """One async size all-gather per message; returns [(req, counts)]."""
+        return [self._get_counts(int(c)) for c in counts]
+
+    def send(self, send, counts):
+        """Post the payload all-gather; ``counts`` from prepare (waited).  Returns (recv, req, counts)."""
+        cs = [int(c.item()) if torch.is_tensor(c) else int(c) for c in counts]
+        slot = max(cs)
+        dev = _dev()
+        buf = _to_tensor(bytes(send), slot, dev)
+        if self.size == 1:
+            return [buf], Request(), cs
+        recv = [torch.empty(slot, dtype=torch.uint8, device=dev) for _ in range(self.size)]
+        work = dist.all_gather(recv, buf, async_op=True)
+        return recv, Request([work], on_done=lambda: buf), cs
+
+    def recv(self, recv, req, counts, cuda: bool = False):
+        req.Wait()
+        out = []
+        for r, n in zip(recv, counts):
+            out.append(unformat(r[:n].cpu().numpy().tobytes(), cuda=cuda))
+        return out
+
+    def allgather(self, obj, cuda: bool = False, level: int = 0):
+        """Convenience: all ranks get every rank's object."""
+        packaged, _ = format_for_send(obj, level)
+        (req, counts), = self.prepare([len(packaged)])
+        req.Wait()
+        return self.recv(*self.send(packaged, counts), cuda=cuda)
