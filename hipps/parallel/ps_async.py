@@ -54,6 +54,19 @@ class PSAsyncEngine(Engine):
 
     def __init__(self, opt, cfg, store, codec, world):
         super().__init__(opt, cfg, store, codec, world)
+        try:
+            self._setup(opt, cfg, store, codec, world)
+        except BaseException:
+            self.remove_hooks()  # a failed engine must not leave hooks on the model
+            mb = getattr(self, "mailbox", None)
+            if mb is not None:
+                try:
+                    mb.close()
+                except Exception:
+                    pass
+            raise
+
+    def _setup(self, opt, cfg, store, codec, world):
         C = native()
         self.C = C
         W = world.size
@@ -119,6 +132,47 @@ class PSAsyncEngine(Engine):
         self.irequest_params(block_for=0)
         if self.cuda:
             torch.cuda.current_stream(store.device).synchronize()
+        self._self_test()
+
+    def _self_test(self):
+        """Prove both directions of the one-sided transport before training starts: every rank
+        writes a tag into its mailbox slot through the same stream-ordered copy path, the PS checks
+        them, and every rank compares its pulled version-0 params with the PS's checksum.  A broken
+        IPC/xGMI mapping raises here on ALL ranks (so callers can fall back) instead of corrupting
+        training later."""
+        W, dev = self.W, self.store.device
+        tag = torch.full((16,), (self.rank * 7 + 3) % 251, dtype=torch.uint8, device=dev)
+        dst = self.slot_buf(self.rank, 1)[:16]
+        if self.cuda:
+            with torch.cuda.stream(self.comm_stream):
+                dst.copy_(tag, non_blocking=True)
+            self.comm_stream.synchronize()
+        else:
+            dst.copy_(tag)
+        barrier(self.world)
+        ok = True
+        if self.rank == 0:
+            for r in range(W):
+                got = self.slot_buf(r, 1)[:16].cpu()
+                ok &= bool((got == (r * 7 + 3) % 251).all())
+            ck = float(self.pub_buf(0).double().sum())  # what workers actually receive
+        else:
+            ck = None
+        mine = float(self.store.data.double().sum())
+        if W > 1:
+            box = [ok, ck]
+            dist.broadcast_object_list(box, src=0)
+            ok, ck = box
+        else:
+            ck = ck if ck is not None else mine
+        good = ok and abs(mine - ck) <= 1e-6 * max(1.0, abs(ck))
+        flags = [good]
+        if W > 1:
+            flags = [None] * W
+            dist.all_gather_object(flags, good)
+        if not all(flags):
+            raise RuntimeError(f"ps_async transport self-test failed (per-rank ok={flags}); "
+                               "IPC mailbox path unusable on this machine")
 
     # ------------------------------------------------------------------ memory views
     def slot_buf(self, rank: int, slot: int) -> torch.Tensor:
