@@ -24,6 +24,16 @@ int64_t topk_workspace_bytes(int64_t n);
 void topk_accumulate(at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale);
 void topk_q8_accumulate(at::Tensor idx, at::Tensor q, at::Tensor scales, at::Tensor acc, double gscale);
 void topk_q8_residual(at::Tensor idx, at::Tensor v, at::Tensor q, at::Tensor scales, at::Tensor resid);
+// norm.hip
+void bn_forward_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, at::Tensor weight, at::Tensor bias,
+                      c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var, at::Tensor mean,
+                      at::Tensor invstd, at::Tensor scale, at::Tensor shift, int64_t C, double eps, double momentum,
+                      bool relu);
+void bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, at::Tensor scale, at::Tensor shift, int64_t C,
+              bool relu);
+void bn_backward(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> y, int64_t mask_mode, at::Tensor weight,
+                 at::Tensor mean, at::Tensor invstd, at::Tensor scale, at::Tensor shift, at::Tensor dx,
+                 c10::optional<at::Tensor> dres, at::Tensor dweight, at::Tensor dbias, int64_t C);
 namespace rt {
 void bind_control(pybind11::module& m);
 void bind_ipc(pybind11::module& m);
@@ -43,6 +53,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("topk_accumulate", &hipps::topk_accumulate, "acc[idx] += gscale * val");
   m.def("topk_q8_accumulate", &hipps::topk_q8_accumulate, "acc[idx] += gscale * deq(q)");
   m.def("topk_q8_residual", &hipps::topk_q8_residual, "EF: r[idx] += v - deq(q)");
+  m.def("bn_forward_train", &hipps::bn_forward_train, "fused channels-last BN train fwd (+res) (+relu)");
+  m.def("bn_apply", &hipps::bn_apply, "y = act(x*scale + shift (+res))");
+  m.def("bn_backward", &hipps::bn_backward, "fused BN bwd with relu-mask recompute (+dres)");
   hipps::rt::bind_control(m);
   hipps::rt::bind_ipc(m);
 }

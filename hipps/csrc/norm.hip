@@ -1,0 +1,385 @@
+// hipps — fused training BatchNorm (+ residual add) (+ ReLU) for channels-last bf16 activations.
+//
+// Why: on MI355X the ResNet-50 worker step (ps_async, bs256) spends 14.9 ms in MIOpen BatchNorm
+// and 8.5 ms in eager ReLU / add / relu-backward kernels out of 40.7 ms (profiles/
+// bench_n1_steady_kernels.txt): ~20 HBM passes over 5.7 GB of activations.  Fusing the
+// activation into the normalisation and recomputing the ReLU mask in the backward cuts that to
+// ~9 passes.
+//
+// Layout: x is [M, C] with M = N*H*W rows and C contiguous (channels_last), C % 8 == 0,
+// C <= 2048.  Each lane moves 8 channels (16 bytes) per access; a 256-thread workgroup is
+// G = C/8 channel groups x R = 256/G row lanes, so a lane's channel group never changes and its
+// per-channel constants live in registers for the whole grid-stride loop.
+//
+// Forward:  reduce (sum, sumsq per channel; fp32 lanes -> per-WG partials)   1 read
+//           finalize (fp64 combine; mean, invstd, running stats, scale/shift)
+//           apply  y = act(x*scale + shift [+ res])                         1 read (+res) 1 write
+// Backward: reduce (sum dz, sum dz*xhat; dz = dy * relu'(.), mask recomputed from x, or read
+//           from y when a residual was fused)                               2-3 reads
+//           finalize (dgamma, dbeta, dx = a*dz + k1*x + k0 coefficients)
+//           apply  dx (+ dres = dz)                                          2-3 reads 1-2 writes
+// Partials are combined in a fixed order, so results are deterministic run to run.
+#include "common.h"
+
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+namespace hipps {
+
+constexpr int kMaxC = 2048;
+
+__device__ __forceinline__ void load8(const uint16_t* p, float v[8]) {
+  uint4 u = *reinterpret_cast<const uint4*>(p);
+  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+  v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
+  v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+__device__ __forceinline__ void store8(uint16_t* p, const float v[8]) {
+  *reinterpret_cast<uint4*>(p) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                            pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+}
+__device__ __forceinline__ void load8f(const float* p, float v[8]) {
+  float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+enum MaskMode { MASK_NONE = 0, MASK_X = 1, MASK_Y = 2 };
+
+// ---- per-channel reductions -> partial[rb][C] (two arrays) ---------------------------------
+// FWD: a += x, b += x*x.   BWD: dz = dy*mask; a += dz, b += dz*(x-mean)*invstd.
+template <bool BWD>
+__global__ __launch_bounds__(kBlock) void k_bn_reduce(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+                                                      const uint16_t* __restrict__ y, int mask_mode,
+                                                      const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                      const float* __restrict__ scale, const float* __restrict__ shift,
+                                                      int64_t M, int C, int64_t rows_per_wg,
+                                                      float* __restrict__ pa, float* __restrict__ pb) {
+  __shared__ float la[kBlock * 8], lb[kBlock * 8];
+  const int G = C >> 3, R = kBlock / G;
+  const int g = threadIdx.x % G, r = threadIdx.x / G;
+  const int c0 = g * 8;
+  float sa[8], sb[8], mu[8], is[8], sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sa[j] = 0.f; sb[j] = 0.f; }
+  if (BWD) {
+    load8f(mean + c0, mu);
+    load8f(invstd + c0, is);
+    if (mask_mode == MASK_X) { load8f(scale + c0, sc); load8f(shift + c0, sh); }
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_wg;
+  const int64_t r1 = min(M, r0 + rows_per_wg);
+  for (int64_t row = r0 + r; row < r1; row += R) {
+    const int64_t off = row * C + c0;
+    float xv[8];
+    load8(x + off, xv);
+    if (!BWD) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { sa[j] += xv[j]; sb[j] = fmaf(xv[j], xv[j], sb[j]); }
+    } else {
+      float d[8];
+      load8(dy + off, d);
+      if (mask_mode == MASK_Y) {
+        float yv[8];
+        load8(y + off, yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
+      } else if (mask_mode == MASK_X) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = fmaf(xv[j], sc[j], sh[j]) > 0.f ? d[j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sa[j] += d[j];
+        sb[j] = fmaf(d[j], (xv[j] - mu[j]) * is[j], sb[j]);
+      }
+    }
+  }
+  // combine the R row lanes of each channel group through LDS
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { la[r * C + c0 + j] = sa[j]; lb[r * C + c0 + j] = sb[j]; }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += kBlock) {
+    float a = 0.f, b = 0.f;
+    for (int q = 0; q < R; ++q) { a += la[q * C + c]; b += lb[q * C + c]; }
+    pa[(int64_t)blockIdx.x * C + c] = a;
+    pb[(int64_t)blockIdx.x * C + c] = b;
+  }
+}
+
+// Combine partial[rb][C] over rb for 32 channels per workgroup: 256 lanes = 32 channels x 8 row
+// lanes, fp64 accumulation, LDS tree.  (A serial per-channel loop over 512-1024 partials cost
+// 180-270 us per call: profiles/bn_micro_r1.txt.)
+constexpr int kFinCh = 32;
+__device__ __forceinline__ bool combine_partials(const float* __restrict__ pa, const float* __restrict__ pb, int nrb,
+                                                 int C, double& s, double& q) {
+  __shared__ double ls[kBlock], lq[kBlock];
+  const int cl = threadIdx.x % kFinCh, lane = threadIdx.x / kFinCh;  // 8 lanes
+  const int c = blockIdx.x * kFinCh + cl;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int i = lane; i < nrb; i += kBlock / kFinCh) {
+      a += pa[(int64_t)i * C + c];
+      b += pb[(int64_t)i * C + c];
+    }
+  }
+  ls[threadIdx.x] = a;
+  lq[threadIdx.x] = b;
+  __syncthreads();
+  for (int off = kBlock / 2; off >= kFinCh; off >>= 1) {
+    if (threadIdx.x < off) {
+      ls[threadIdx.x] += ls[threadIdx.x + off];
+      lq[threadIdx.x] += lq[threadIdx.x + off];
+    }
+    __syncthreads();
+  }
+  s = ls[cl];
+  q = lq[cl];
+  return lane == 0 && c < C;
+}
+
+// forward finalize: stats + running stats + per-channel scale/shift
+__global__ __launch_bounds__(kBlock) void k_bn_finalize_fwd(const float* __restrict__ pa, const float* __restrict__ pb,
+                                                            int nrb, int C, int64_t M, const float* __restrict__ w,
+                                                            const float* __restrict__ bias, float eps, float momentum,
+                                                            float* __restrict__ running_mean,
+                                                            float* __restrict__ running_var, float* __restrict__ mean,
+                                                            float* __restrict__ invstd, float* __restrict__ scale,
+                                                            float* __restrict__ shift) {
+  double s, q;
+  if (!combine_partials(pa, pb, nrb, C, s, q)) return;
+  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
+  const double m = s / (double)M;
+  double var = q / (double)M - m * m;
+  if (var < 0.0) var = 0.0;
+  const float is = (float)(1.0 / sqrt(var + (double)eps));
+  mean[c] = (float)m;
+  invstd[c] = is;
+  const float wc = w ? w[c] : 1.f, bc = bias ? bias[c] : 0.f;
+  scale[c] = wc * is;
+  shift[c] = bc - (float)m * wc * is;
+  if (running_mean) {
+    const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)m;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+  }
+}
+
+// backward finalize: dgamma, dbeta and dx = a*dz + k1*x + k0 coefficients
+__global__ __launch_bounds__(kBlock) void k_bn_finalize_bwd(const float* __restrict__ pa, const float* __restrict__ pb,
+                                                            int nrb, int C, int64_t M, const float* __restrict__ w,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd, float* __restrict__ dw,
+                                                            float* __restrict__ db, float* __restrict__ ca,
+                                                            float* __restrict__ ck1, float* __restrict__ ck0) {
+  double s, q;
+  if (!combine_partials(pa, pb, nrb, C, s, q)) return;
+  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
+  if (dw) dw[c] = (float)q;
+  if (db) db[c] = (float)s;
+  const double is = invstd[c];
+  const double a = (w ? (double)w[c] : 1.0) * is;
+  const double k1 = -a * is * q / (double)M;
+  const double k0 = -a * s / (double)M - k1 * (double)mean[c];
+  ca[c] = (float)a;
+  ck1[c] = (float)k1;
+  ck0[c] = (float)k0;
+}
+
+// y = act(x*scale + shift [+ res])
+__global__ __launch_bounds__(kBlock) void k_bn_apply_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+                                                         uint16_t* __restrict__ y, const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, int64_t M, int C, int relu) {
+  const int G = C >> 3;
+  const int64_t V = M * (int64_t)G, stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (int)(v0 % G) * 8;  // fixed per lane: stride is a multiple of G
+  float sc[8], sh[8];
+  load8f(scale + c0, sc);
+  load8f(shift + c0, sh);
+  for (int64_t v = v0; v < V; v += stride) {
+    const int64_t off = v * 8;
+    float xv[8];
+    load8(x + off, xv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xv[j] = fmaf(xv[j], sc[j], sh[j]);
+    if (res) {
+      float rv[8];
+      load8(res + off, rv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xv[j] += rv[j];
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xv[j] = fmaxf(xv[j], 0.f);
+    }
+    store8(y + off, xv);
+  }
+}
+
+// dx = a*dz + k1*x + k0, dz = dy * mask;  dres = dz (when a residual was fused)
+__global__ __launch_bounds__(kBlock) void k_bn_apply_bwd(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+                                                         const uint16_t* __restrict__ y, int mask_mode,
+                                                         const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, const float* __restrict__ ca,
+                                                         const float* __restrict__ ck1, const float* __restrict__ ck0,
+                                                         uint16_t* __restrict__ dx, uint16_t* __restrict__ dres,
+                                                         int64_t M, int C) {
+  const int G = C >> 3;
+  const int64_t V = M * (int64_t)G, stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (int)(v0 % G) * 8;
+  float a[8], k1[8], k0[8], sc[8], sh[8];
+  load8f(ca + c0, a);
+  load8f(ck1 + c0, k1);
+  load8f(ck0 + c0, k0);
+  if (mask_mode == MASK_X) { load8f(scale + c0, sc); load8f(shift + c0, sh); }
+  for (int64_t v = v0; v < V; v += stride) {
+    const int64_t off = v * 8;
+    float d[8], xv[8];
+    load8(dy + off, d);
+    load8(x + off, xv);
+    if (mask_mode == MASK_Y) {
+      float yv[8];
+      load8(y + off, yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
+    } else if (mask_mode == MASK_X) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = fmaf(xv[j], sc[j], sh[j]) > 0.f ? d[j] : 0.f;
+    }
+    if (dres) store8(dres + off, d);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = fmaf(a[j], d[j], fmaf(k1[j], xv[j], k0[j]));
+    store8(dx + off, o);
+  }
+}
+
+// ==========================================================================================
+namespace {
+void check_act(const at::Tensor& t, const char* n, int64_t numel) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16, n, " must be a bf16 device tensor");
+  TORCH_CHECK(t.numel() == numel, n, " size mismatch");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, n, " must be 16-byte aligned");
+}
+void check_vec(const at::Tensor& t, const char* n, int C) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == C, n,
+              " must be a contiguous f32 device vector of length C");
+}
+int64_t pick_rows(int64_t M, int C, int& nrb) {
+  const int G = C / 8, R = kBlock / G;
+  const int64_t vec = M * G;
+  int64_t want = vec / (kBlock * 16);  // >= 16 vectors per lane
+  want = std::max<int64_t>(1, std::min<int64_t>(want, 512));
+  int64_t rows = (M + want - 1) / want;
+  rows = (rows + R - 1) / R * R;
+  nrb = (int)((M + rows - 1) / rows);
+  return rows;
+}
+int apply_grid(int64_t M, int C) {
+  const int64_t V = M * (C / 8);
+  return grid_for(V);
+}
+}  // namespace
+
+// x: [M, C] bf16 view (channels-last storage).  Returns nothing; fills y, mean, invstd,
+// scale, shift and updates running stats in place.
+void bn_forward_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, at::Tensor weight, at::Tensor bias,
+                      c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var, at::Tensor mean,
+                      at::Tensor invstd, at::Tensor scale, at::Tensor shift, int64_t C, double eps, double momentum,
+                      bool relu) {
+  TORCH_CHECK(C % 8 == 0 && C <= kMaxC && C >= 8, "fused BN needs C % 8 == 0 and 8 <= C <= 2048");
+  const int64_t M = x.numel() / C;
+  check_act(x, "x", M * C);
+  check_act(y, "y", M * C);
+  const uint16_t* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_act(*res, "residual", M * C);
+    rp = (const uint16_t*)res->data_ptr();
+  }
+  for (auto* t : {&weight, &bias, &mean, &invstd, &scale, &shift}) check_vec(*t, "per-channel vector", (int)C);
+  float* rm = nullptr;
+  float* rv = nullptr;
+  if (running_mean.has_value() && running_mean->defined()) {
+    check_vec(*running_mean, "running_mean", (int)C);
+    check_vec(*running_var, "running_var", (int)C);
+    rm = running_mean->data_ptr<float>();
+    rv = running_var->data_ptr<float>();
+  }
+  int nrb;
+  const int64_t rows = pick_rows(M, (int)C, nrb);
+  auto part = at::empty({2, (int64_t)nrb, C}, weight.options());
+  auto stream = c10::hip::getCurrentHIPStream();
+  hipLaunchKernelGGL(k_bn_reduce<false>, nrb, kBlock, 0, stream, (const uint16_t*)x.data_ptr(), nullptr, nullptr, 0,
+                     nullptr, nullptr, nullptr, nullptr, M, (int)C, rows, part[0].data_ptr<float>(),
+                     part[1].data_ptr<float>());
+  hipLaunchKernelGGL(k_bn_finalize_fwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, part[0].data_ptr<float>(),
+                     part[1].data_ptr<float>(), nrb, (int)C, M, weight.data_ptr<float>(), bias.data_ptr<float>(),
+                     (float)eps, (float)momentum, rm, rv, mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                     scale.data_ptr<float>(), shift.data_ptr<float>());
+  hipLaunchKernelGGL(k_bn_apply_fwd, apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)x.data_ptr(), rp,
+                     (uint16_t*)y.data_ptr(), scale.data_ptr<float>(), shift.data_ptr<float>(), M, (int)C, (int)relu);
+}
+
+// eval / affine-only apply with given scale/shift
+void bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, at::Tensor scale, at::Tensor shift, int64_t C,
+              bool relu) {
+  TORCH_CHECK(C % 8 == 0 && C <= kMaxC, "fused BN needs C % 8 == 0 and C <= 2048");
+  const int64_t M = x.numel() / C;
+  check_act(x, "x", M * C);
+  check_act(y, "y", M * C);
+  const uint16_t* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_act(*res, "residual", M * C);
+    rp = (const uint16_t*)res->data_ptr();
+  }
+  check_vec(scale, "scale", (int)C);
+  check_vec(shift, "shift", (int)C);
+  hipLaunchKernelGGL(k_bn_apply_fwd, apply_grid(M, (int)C), kBlock, 0, c10::hip::getCurrentHIPStream(),
+                     (const uint16_t*)x.data_ptr(), rp, (uint16_t*)y.data_ptr(), scale.data_ptr<float>(),
+                     shift.data_ptr<float>(), M, (int)C, (int)relu);
+}
+
+// returns nothing; writes dx (and dres), dweight, dbias
+void bn_backward(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> y, int64_t mask_mode, at::Tensor weight,
+                 at::Tensor mean, at::Tensor invstd, at::Tensor scale, at::Tensor shift, at::Tensor dx,
+                 c10::optional<at::Tensor> dres, at::Tensor dweight, at::Tensor dbias, int64_t C) {
+  TORCH_CHECK(C % 8 == 0 && C <= kMaxC, "fused BN needs C % 8 == 0 and C <= 2048");
+  const int64_t M = x.numel() / C;
+  check_act(dy, "dy", M * C);
+  check_act(x, "x", M * C);
+  check_act(dx, "dx", M * C);
+  const uint16_t* yp = nullptr;
+  if (mask_mode == MASK_Y) {
+    TORCH_CHECK(y.has_value() && y->defined(), "mask from y needs y");
+    check_act(*y, "y", M * C);
+    yp = (const uint16_t*)y->data_ptr();
+  }
+  uint16_t* drp = nullptr;
+  if (dres.has_value() && dres->defined()) {
+    check_act(*dres, "dres", M * C);
+    drp = (uint16_t*)dres->data_ptr();
+  }
+  for (auto* t : {&weight, &mean, &invstd, &scale, &shift, &dweight, &dbias}) check_vec(*t, "per-channel vector", (int)C);
+  int nrb;
+  const int64_t rows = pick_rows(M, (int)C, nrb);
+  auto part = at::empty({2, (int64_t)nrb, C}, weight.options());
+  auto coef = at::empty({3, C}, weight.options());
+  auto stream = c10::hip::getCurrentHIPStream();
+  hipLaunchKernelGGL(k_bn_reduce<true>, nrb, kBlock, 0, stream, (const uint16_t*)x.data_ptr(),
+                     (const uint16_t*)dy.data_ptr(), yp, (int)mask_mode, mean.data_ptr<float>(),
+                     invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(), M, (int)C, rows,
+                     part[0].data_ptr<float>(), part[1].data_ptr<float>());
+  hipLaunchKernelGGL(k_bn_finalize_bwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, part[0].data_ptr<float>(),
+                     part[1].data_ptr<float>(), nrb, (int)C, M, weight.data_ptr<float>(), mean.data_ptr<float>(),
+                     invstd.data_ptr<float>(), dweight.data_ptr<float>(), dbias.data_ptr<float>(),
+                     coef[0].data_ptr<float>(), coef[1].data_ptr<float>(), coef[2].data_ptr<float>());
+  hipLaunchKernelGGL(k_bn_apply_bwd, apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)dy.data_ptr(),
+                     (const uint16_t*)x.data_ptr(), yp, (int)mask_mode, scale.data_ptr<float>(),
+                     shift.data_ptr<float>(), coef[0].data_ptr<float>(), coef[1].data_ptr<float>(),
+                     coef[2].data_ptr<float>(), (uint16_t*)dx.data_ptr(), drp, M, (int)C);
+}
+
+}  // namespace hipps

@@ -14,6 +14,18 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from hipps.ops.nn import FusedBatchNorm2d
+
+# One switch for the whole zoo: fused BN(+residual)(+ReLU) HIP kernels on channels-last bf16,
+# standard PyTorch elsewhere.  HIPPS_FUSED_BN=0 restores the eager MIOpen path for A/B runs.
+import os as _os
+
+_FUSED = _os.environ.get("HIPPS_FUSED_BN", "1") != "0"
+
+
+def _bn(c, relu=False):
+    return FusedBatchNorm2d(c, relu=relu, fused=_FUSED)
+
 
 def _conv(cin, cout, k, stride=1, groups=1):
     return nn.Conv2d(cin, cout, k, stride=stride, padding=k // 2, groups=groups, bias=False)
@@ -26,21 +38,20 @@ class Bottleneck(nn.Module):
         super().__init__()
         cout = width * self.expansion
         self.conv1 = _conv(cin, width, 1)
-        self.bn1 = nn.BatchNorm2d(width)
+        self.bn1 = _bn(width, relu=True)
         self.conv2 = _conv(width, width, 3, stride=stride)
-        self.bn2 = nn.BatchNorm2d(width)
+        self.bn2 = _bn(width, relu=True)
         self.conv3 = _conv(width, cout, 1)
-        self.bn3 = nn.BatchNorm2d(cout)
+        self.bn3 = _bn(cout, relu=True)  # relu(bn3(conv3) + identity), one fused pass
         self.downsample = None
         if downsample:
-            self.downsample = nn.Sequential(_conv(cin, cout, 1, stride=stride), nn.BatchNorm2d(cout))
+            self.downsample = nn.Sequential(_conv(cin, cout, 1, stride=stride), _bn(cout))
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        y = F.relu(self.bn1(self.conv1(x)), inplace=True)
-        y = F.relu(self.bn2(self.conv2(y)), inplace=True)
-        y = self.bn3(self.conv3(y))
-        return F.relu(y + idt, inplace=True)
+        y = self.bn1(self.conv1(x))
+        y = self.bn2(self.conv2(y))
+        return self.bn3(self.conv3(y), residual=idt)
 
 
 class BasicBlock(nn.Module):
@@ -49,25 +60,24 @@ class BasicBlock(nn.Module):
     def __init__(self, cin, width, stride=1, downsample=False):
         super().__init__()
         self.conv1 = _conv(cin, width, 3, stride=stride)
-        self.bn1 = nn.BatchNorm2d(width)
+        self.bn1 = _bn(width, relu=True)
         self.conv2 = _conv(width, width, 3)
-        self.bn2 = nn.BatchNorm2d(width)
+        self.bn2 = _bn(width, relu=True)
         self.downsample = None
         if downsample:
-            self.downsample = nn.Sequential(_conv(cin, width, 1, stride=stride), nn.BatchNorm2d(width))
+            self.downsample = nn.Sequential(_conv(cin, width, 1, stride=stride), _bn(width))
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        y = F.relu(self.bn1(self.conv1(x)), inplace=True)
-        y = self.bn2(self.conv2(y))
-        return F.relu(y + idt, inplace=True)
+        y = self.bn1(self.conv1(x))
+        return self.bn2(self.conv2(y), residual=idt)
 
 
 class ResNet(nn.Module):
     def __init__(self, block, layers, num_classes=1000, width=64, zero_init_residual=True):
         super().__init__()
         self.conv1 = nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False)
-        self.bn1 = nn.BatchNorm2d(width)
+        self.bn1 = _bn(width, relu=True)
         self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
         cin = width
         stages = []
@@ -98,7 +108,7 @@ class ResNet(nn.Module):
                     nn.init.zeros_(m.bn2.weight)
 
     def forward(self, x):
-        x = self.maxpool(F.relu(self.bn1(self.conv1(x)), inplace=True))
+        x = self.maxpool(self.bn1(self.conv1(x)))
         for i in range(self.num_stages):
             x = getattr(self, f"layer{i + 1}")(x)
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

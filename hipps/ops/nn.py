@@ -1,0 +1,98 @@
+"""Fused model ops backed by hipps HIP kernels.
+
+``FusedBatchNorm2d`` is a drop-in ``nn.BatchNorm2d`` that can also apply a residual add and a
+ReLU in the same pass (``forward(x, residual=None)``).  On a HIP device with a channels-last
+bf16 input (the autocast ResNet path) it runs hipps/csrc/norm.hip: one statistics pass, one
+apply pass, and a backward that recomputes the ReLU mask instead of storing it.  Anything
+else (CPU, fp32, NCHW, odd channel counts, eval with grad) takes the standard PyTorch path, so
+models stay portable and the CPU test suite exercises the same module.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ._native import native
+
+MASK_NONE, MASK_X, MASK_Y = 0, 1, 2
+
+
+class _FusedBNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, res, weight, bias, running_mean, running_var, eps, momentum, relu):
+        C = x.shape[1]
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        f32 = dict(dtype=torch.float32, device=x.device)
+        mean, invstd = torch.empty(C, **f32), torch.empty(C, **f32)
+        scale, shift = torch.empty(C, **f32), torch.empty(C, **f32)
+        native().bn_forward_train(x, res, y, weight, bias, running_mean, running_var, mean, invstd, scale, shift, C,
+                                  float(eps), float(momentum), bool(relu))
+        mode = MASK_NONE if not relu else (MASK_Y if res is not None else MASK_X)
+        ctx.mode, ctx.C, ctx.has_res = mode, C, res is not None
+        ctx.save_for_backward(x, y if mode == MASK_Y else None, weight, mean, invstd, scale, shift)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, weight, mean, invstd, scale, shift = ctx.saved_tensors
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
+        dw = torch.empty_like(weight)
+        db = torch.empty_like(weight)
+        native().bn_backward(dy, x, y, ctx.mode, weight, mean, invstd, scale, shift, dx, dres, dw, db, ctx.C)
+        return dx, dres, dw, db, None, None, None, None, None
+
+
+def fused_bn_act(x, weight, bias, running_mean, running_var, eps=1e-5, momentum=0.1, relu=True, residual=None):
+    """Training-mode BN (+residual) (+ReLU) on a channels-last bf16 HIP tensor."""
+    return _FusedBNAct.apply(x, residual, weight, bias, running_mean, running_var, eps, momentum, relu)
+
+
+class FusedBatchNorm2d(nn.BatchNorm2d):
+    """nn.BatchNorm2d with optional fused residual add and ReLU."""
+
+    def __init__(self, num_features, relu: bool = False, fused: bool = True, **kw):
+        super().__init__(num_features, **kw)
+        self.relu = relu
+        self.fused = fused
+
+    def extra_repr(self):
+        return super().extra_repr() + f", relu={self.relu}, fused={self.fused}"
+
+    def _fast_ok(self, x, residual) -> bool:
+        if not (self.fused and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4):
+            return False
+        C = x.shape[1]
+        if C % 8 or C > 2048 or not self.affine or not x.is_contiguous(memory_format=torch.channels_last):
+            return False
+        if self.training and (not self.track_running_stats or self.momentum is None):
+            return False
+        if residual is not None and (residual.dtype != torch.bfloat16 or residual.shape != x.shape or
+                                     not residual.is_contiguous(memory_format=torch.channels_last)):
+            return False
+        if x.numel() % 16:
+            return False
+        return True
+
+    def forward(self, x, residual=None):
+        if self._fast_ok(x, residual):
+            if self.training:
+                self.num_batches_tracked.add_(1)
+                return fused_bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, self.eps,
+                                    self.momentum, self.relu, residual)
+            if not torch.is_grad_enabled() or not (x.requires_grad or (residual is not None and
+                                                                       residual.requires_grad)):
+                scale = self.weight / torch.sqrt(self.running_var + self.eps)
+                shift = self.bias - self.running_mean * scale
+                y = torch.empty_like(x, memory_format=torch.channels_last)
+                native().bn_apply(x, residual, y, scale.float().contiguous(), shift.float().contiguous(),
+                                  x.shape[1], self.relu)
+                return y
+        y = super().forward(x)
+        if residual is not None:
+            y = y + residual
+        if self.relu:
+            y = F.relu(y)
+        return y

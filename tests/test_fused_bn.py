@@ -1,0 +1,117 @@
+"""Fused BatchNorm(+residual)(+ReLU): CPU fallback parity and GPU kernel numerics vs fp32 torch."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from hipps.ops.nn import FusedBatchNorm2d
+
+
+def _ref(x, res, bn, relu):
+    y = F.batch_norm(x, bn.running_mean, bn.running_var, bn.weight, bn.bias, True, bn.momentum, bn.eps)
+    if res is not None:
+        y = y + res
+    return F.relu(y) if relu else y
+
+
+@pytest.mark.parametrize("relu,residual", [(False, False), (True, False), (True, True)])
+def test_cpu_fallback_matches_batchnorm(relu, residual):
+    torch.manual_seed(0)
+    m = FusedBatchNorm2d(16, relu=relu)
+    ref = torch.nn.BatchNorm2d(16)
+    ref.load_state_dict(m.state_dict(), strict=False)
+    x = torch.randn(4, 16, 5, 5)
+    r = torch.randn(4, 16, 5, 5) if residual else None
+    y = m(x, residual=r)
+    want = ref(x) + (r if residual else 0)
+    want = F.relu(want) if relu else want
+    torch.testing.assert_close(y, want)
+    torch.testing.assert_close(m.running_mean, ref.running_mean)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(8, 64, 56, 56), (4, 256, 14, 14), (16, 2048, 7, 7), (2, 8, 3, 3), (3, 1024, 5, 7)])
+@pytest.mark.parametrize("relu,residual", [(False, False), (True, False), (True, True)])
+def test_gpu_fused_bn_matches_fp32_reference(shape, relu, residual):
+    torch.manual_seed(1)
+    N, C, H, W = shape
+    dev = "cuda"
+    x0 = (torch.randn(shape, device=dev) * 2 + 0.5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    r0 = torch.randn(shape, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last) if residual \
+        else None
+    m = FusedBatchNorm2d(C, relu=relu).to(dev)
+    with torch.no_grad():
+        m.weight.uniform_(0.5, 1.5)
+        m.bias.uniform_(-0.5, 0.5)
+    ref = FusedBatchNorm2d(C, relu=relu, fused=False).to(dev)
+    ref.load_state_dict(m.state_dict())
+    x = x0.clone().requires_grad_(True)
+    r = r0.clone().requires_grad_(True) if residual else None
+    y = m(x, residual=r)
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    xf = x0.float().requires_grad_(True)
+    rf = r0.float().requires_grad_(True) if residual else None
+    yf = ref(xf, residual=rf)
+    torch.testing.assert_close(y.float(), yf, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(m.running_mean, ref.running_mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(m.running_var, ref.running_var, rtol=1e-3, atol=1e-4)
+    g = torch.randn(shape, device=dev)
+    y.backward(g.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+    yf.backward(g.to(torch.bfloat16).float())
+    scale = xf.grad.abs().max().item() + 1e-6
+    torch.testing.assert_close(x.grad.float() / scale, xf.grad / scale, rtol=0, atol=3e-2)
+    torch.testing.assert_close(m.weight.grad, ref.weight.grad, rtol=2e-2, atol=2e-2 * ref.weight.grad.abs().max().item())
+    torch.testing.assert_close(m.bias.grad, ref.bias.grad, rtol=2e-2, atol=2e-2 * ref.bias.grad.abs().max().item())
+    if residual:
+        torch.testing.assert_close(r.grad.float(), rf.grad, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.gpu
+def test_gpu_fused_eval_apply():
+    torch.manual_seed(2)
+    m = FusedBatchNorm2d(64, relu=True).cuda().eval()
+    m.running_mean.uniform_(-1, 1)
+    m.running_var.uniform_(0.5, 2)
+    x = torch.randn(2, 64, 8, 8, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        y = m(x)
+        m.fused = False
+        want = m(x.float())
+    torch.testing.assert_close(y.float(), want, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.gpu
+def test_gpu_resnet_fused_vs_unfused_step():
+    """One autocast step of a small ResNet: the fused-BN model's grads are no further from an fp32
+    reference than the eager bf16 (MIOpen BN) model's grads are."""
+    import copy
+
+    from hipps.models.resnet import ResNet, Bottleneck
+
+    torch.manual_seed(3)
+    base = ResNet(Bottleneck, [1, 1], num_classes=10, width=16, zero_init_residual=False).cuda()
+    base = base.to(memory_format=torch.channels_last)
+    models = {k: copy.deepcopy(base) for k in ("fused", "eager", "fp32")}
+    for k in ("eager", "fp32"):
+        for mod in models[k].modules():
+            if isinstance(mod, FusedBatchNorm2d):
+                mod.fused = False
+    x = torch.randn(32, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (32,), device="cuda")
+    losses = {}
+    for k, m in models.items():
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=(k != "fp32")):
+            loss = F.cross_entropy(m(x), y)
+        loss.backward()
+        losses[k] = loss.item()
+    assert abs(losses["fused"] - losses["fp32"]) < 3e-2
+    ref = dict(models["fp32"].named_parameters())
+    for k in ("fused", "eager"):
+        pass
+    worse = []
+    for (n, pf), pe in zip(models["fused"].named_parameters(), models["eager"].parameters()):
+        g = ref[n].grad
+        ef = (pf.grad - g).norm().item()
+        ee = (pe.grad - g).norm().item()
+        if ef > 1.5 * ee + 1e-3 * g.norm().item() + 1e-6:
+            worse.append((n, ef, ee))
+    assert not worse, worse
