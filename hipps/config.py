@@ -31,6 +31,10 @@ class PSConfig:
     max_delay: int = -1
     # async PS: pull the newest published params at the end of every step() (AsySG-InCon read)
     auto_pull: bool = True
+    # async PS, remote GPU workers: 'prefetch' (side-stream xGMI read, adopted next step) | 'direct'
+    pull: str = "prefetch"
+    # async PS failure detection: a worker silent for this long (no heartbeat, no STOP) is dead
+    dead_after_s: float = 60.0
     # bucket size for hook-driven encode overlap
     bucket_mb: float = 64.0
     # scale the rank-summed gradient by 1/accumulate (reference sums: ps.py:176)
@@ -75,6 +79,8 @@ class PSConfig:
     def validate(self):
         if self.mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}, got {self.mode!r}")
+        if self.pull not in ("prefetch", "direct"):
+            raise ValueError("pull must be 'prefetch' or 'direct'")
         if self.param_wire not in ("fp32", "bf16"):
             raise ValueError("param_wire must be 'fp32' or 'bf16'")
         if self.adam_variant not in ("reference", "torch"):

@@ -1,0 +1,209 @@
+"""Transformer models for BASELINE configs 4 and 5 (random init, synthetic tokens).
+
+  bert-base   BertModel layout (12 x 768, 12 heads, FFN 3072, vocab 30522, 512 positions, pooler)
+              = 109,482,240 params in 199 tensors + a tied-decoder MLM head.
+              Config 4 ("BERT-base async PS, variable-size per-layer grad buckets").
+  llama3-8b   Llama-3 8B (32 x 4096, 32 q / 8 kv heads, SwiGLU 14336, RMSNorm, RoPE theta 5e5,
+              vocab 128256) = 8.03 B params.  Config 5 ("Llama-3 8B pure-DP async PS").
+  *-tiny      same code, small widths, for CPU tests.
+
+Attention is ``F.scaled_dot_product_attention`` (the ROCm flash / mem-efficient kernels); the
+projections and MLPs are plain ``nn.Linear`` (hipBLASLt).  These models exercise the PS engine's
+bucketing/codec/transport at 100 M - 8 B parameters; they are not a kernel showcase.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+# ------------------------------------------------------------------------------------- BERT
+@dataclass
+class BertConfig:
+    vocab: int = 30522
+    hidden: int = 768
+    layers: int = 12
+    heads: int = 12
+    ffn: int = 3072
+    max_pos: int = 512
+    type_vocab: int = 2
+    eps: float = 1e-12
+
+
+class BertLayer(nn.Module):
+    def __init__(self, c: BertConfig):
+        super().__init__()
+        self.heads = c.heads
+        self.q = nn.Linear(c.hidden, c.hidden)
+        self.k = nn.Linear(c.hidden, c.hidden)
+        self.v = nn.Linear(c.hidden, c.hidden)
+        self.attn_out = nn.Linear(c.hidden, c.hidden)
+        self.attn_ln = nn.LayerNorm(c.hidden, eps=c.eps)
+        self.inter = nn.Linear(c.hidden, c.ffn)
+        self.out = nn.Linear(c.ffn, c.hidden)
+        self.out_ln = nn.LayerNorm(c.hidden, eps=c.eps)
+
+    def forward(self, x, mask=None):
+        B, S, D = x.shape
+        h = self.heads
+
+        def split(t):
+            return t.view(B, S, h, D // h).transpose(1, 2)
+
+        a = F.scaled_dot_product_attention(split(self.q(x)), split(self.k(x)), split(self.v(x)), attn_mask=mask)
+        a = a.transpose(1, 2).reshape(B, S, D)
+        x = self.attn_ln(x + self.attn_out(a))
+        return self.out_ln(x + self.out(F.gelu(self.inter(x))))
+
+
+class Bert(nn.Module):
+    def __init__(self, c: BertConfig = BertConfig(), mlm: bool = True):
+        super().__init__()
+        self.c = c
+        self.word = nn.Embedding(c.vocab, c.hidden)
+        self.pos = nn.Embedding(c.max_pos, c.hidden)
+        self.tok_type = nn.Embedding(c.type_vocab, c.hidden)
+        self.emb_ln = nn.LayerNorm(c.hidden, eps=c.eps)
+        self.layers = nn.ModuleList([BertLayer(c) for _ in range(c.layers)])
+        self.pooler = nn.Linear(c.hidden, c.hidden)
+        self.mlm = mlm
+        if mlm:
+            self.mlm_dense = nn.Linear(c.hidden, c.hidden)
+            self.mlm_ln = nn.LayerNorm(c.hidden, eps=c.eps)
+            self.mlm_bias = nn.Parameter(torch.zeros(c.vocab))
+        self.apply(self._init)
+
+    @staticmethod
+    def _init(m):
+        if isinstance(m, (nn.Linear, nn.Embedding)):
+            nn.init.normal_(m.weight, std=0.02)
+        if isinstance(m, nn.Linear) and m.bias is not None:
+            nn.init.zeros_(m.bias)
+
+    def forward(self, ids, labels=None):
+        B, S = ids.shape
+        pos = torch.arange(S, device=ids.device)
+        x = self.word(ids) + self.pos(pos)[None] + self.tok_type(torch.zeros_like(ids))
+        x = self.emb_ln(x)
+        for layer in self.layers:
+            x = layer(x)
+        pooled = torch.tanh(self.pooler(x[:, 0]))
+        if not self.mlm:
+            return x, pooled
+        h = self.mlm_ln(F.gelu(self.mlm_dense(x)))
+        logits = F.linear(h, self.word.weight, self.mlm_bias)  # tied decoder
+        if labels is None:
+            return logits
+        return F.cross_entropy(logits.float().view(-1, logits.shape[-1]), labels.view(-1), ignore_index=-100)
+
+
+# ------------------------------------------------------------------------------------- Llama
+@dataclass
+class LlamaConfig:
+    vocab: int = 128256
+    dim: int = 4096
+    layers: int = 32
+    heads: int = 32
+    kv_heads: int = 8
+    ffn: int = 14336
+    eps: float = 1e-5
+    theta: float = 500000.0
+    max_seq: int = 8192
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, d, eps):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(d))
+        self.eps = eps
+
+    def forward(self, x):
+        xf = x.float()
+        return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.eps)).to(x.dtype) * self.weight.to(x.dtype)
+
+
+def _rope(x, cos, sin):
+    x1, x2 = x[..., ::2], x[..., 1::2]
+    return torch.stack((x1 * cos - x2 * sin, x1 * sin + x2 * cos), dim=-1).flatten(-2)
+
+
+class LlamaBlock(nn.Module):
+    def __init__(self, c: LlamaConfig):
+        super().__init__()
+        self.c = c
+        hd = c.dim // c.heads
+        self.wq = nn.Linear(c.dim, c.heads * hd, bias=False)
+        self.wk = nn.Linear(c.dim, c.kv_heads * hd, bias=False)
+        self.wv = nn.Linear(c.dim, c.kv_heads * hd, bias=False)
+        self.wo = nn.Linear(c.heads * hd, c.dim, bias=False)
+        self.w1 = nn.Linear(c.dim, c.ffn, bias=False)
+        self.w3 = nn.Linear(c.dim, c.ffn, bias=False)
+        self.w2 = nn.Linear(c.ffn, c.dim, bias=False)
+        self.attn_norm = RMSNorm(c.dim, c.eps)
+        self.ffn_norm = RMSNorm(c.dim, c.eps)
+
+    def forward(self, x, cos, sin):
+        B, S, D = x.shape
+        c = self.c
+        hd = D // c.heads
+        h = self.attn_norm(x)
+        q = self.wq(h).view(B, S, c.heads, hd)
+        k = self.wk(h).view(B, S, c.kv_heads, hd)
+        v = self.wv(h).view(B, S, c.kv_heads, hd)
+        q, k = _rope(q, cos, sin), _rope(k, cos, sin)
+        q, k, v = (t.transpose(1, 2) for t in (q, k, v))
+        a = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=c.heads != c.kv_heads)
+        x = x + self.wo(a.transpose(1, 2).reshape(B, S, D))
+        h = self.ffn_norm(x)
+        return x + self.w2(F.silu(self.w1(h)) * self.w3(h))
+
+
+class Llama(nn.Module):
+    def __init__(self, c: LlamaConfig = LlamaConfig()):
+        super().__init__()
+        self.c = c
+        self.tok = nn.Embedding(c.vocab, c.dim)
+        self.blocks = nn.ModuleList([LlamaBlock(c) for _ in range(c.layers)])
+        self.norm = RMSNorm(c.dim, c.eps)
+        self.head = nn.Linear(c.dim, c.vocab, bias=False)
+        for m in self.modules():
+            if isinstance(m, (nn.Linear, nn.Embedding)):
+                nn.init.normal_(m.weight, std=0.02)
+
+    def rope_tables(self, S, device, dtype):
+        hd = self.c.dim // self.c.heads
+        inv = 1.0 / (self.c.theta ** (torch.arange(0, hd, 2, device=device, dtype=torch.float32) / hd))
+        t = torch.arange(S, device=device, dtype=torch.float32)
+        f = torch.outer(t, inv)
+        return f.cos()[None, :, None, :].to(dtype), f.sin()[None, :, None, :].to(dtype)
+
+    def forward(self, ids, labels=None):
+        B, S = ids.shape
+        x = self.tok(ids)
+        dt = torch.get_autocast_dtype("cuda") if (x.is_cuda and torch.is_autocast_enabled()) else x.dtype
+        cos, sin = self.rope_tables(S, ids.device, dt)
+        for b in self.blocks:
+            x = b(x, cos, sin)
+        logits = self.head(self.norm(x))
+        if labels is None:
+            return logits
+        return F.cross_entropy(logits.float().view(-1, logits.shape[-1]), labels.view(-1))
+
+
+def build(name: str, **kw):
+    name = name.lower()
+    if name in ("bert", "bert-base", "bert_base"):
+        return Bert(BertConfig(**kw))
+    if name in ("bert-tiny", "bert_tiny"):
+        return Bert(BertConfig(vocab=512, hidden=64, layers=2, heads=4, ffn=128, max_pos=64, **kw))
+    if name in ("llama3-8b", "llama-3-8b", "llama3_8b"):
+        return Llama(LlamaConfig(**kw))
+    if name in ("llama3-1b", "llama-3.2-1b"):
+        return Llama(LlamaConfig(dim=2048, layers=16, heads=32, kv_heads=8, ffn=8192, **kw))
+    if name in ("llama-tiny", "llama_tiny"):
+        return Llama(LlamaConfig(vocab=512, dim=64, layers=2, heads=4, kv_heads=2, ffn=128, max_seq=128, **kw))
+    raise ValueError(f"unknown transformer {name!r}")

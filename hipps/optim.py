@@ -38,12 +38,20 @@ class MPI_PS(torch.optim.Optimizer):
     optim = "base"
 
     def __init__(self, named_params, *args, names=(), optim=None, code=None, use_mpi=True, cuda=None,
-                 mode=None, config: Optional[PSConfig] = None, accumulate=None, staleness=None, average=None,
-                 bucket_mb=None, overlap=None, param_wire=None, max_delay=None, adam_variant=None,
-                 debug_check_order=None, metrics_path=None, **kwargs):
+                 config: Optional[PSConfig] = None, **kwargs):
+        """``named_params, *args, names, optim, code, use_mpi, cuda`` as in ps.py:54-59; any
+        :class:`PSConfig` field (mode, accumulate, staleness, max_delay, average, bucket_mb, ...)
+        may be passed as a keyword; the rest goes to ``torch.optim`` (lr, momentum, betas, ...)."""
+        import dataclasses
+
         named_params = list(named_params)
         if named_params and not isinstance(named_params[0], (tuple, list)):
             named_params = [(f"param{i}", p) for i, p in enumerate(named_params)]
+        cfg_fields = {f.name for f in dataclasses.fields(PSConfig)}
+        over = {k: kwargs.pop(k) for k in list(kwargs) if k in cfg_fields}
+        over = {k: v for k, v in over.items() if v is not None}
+        if code is not None:
+            over["codec"] = code
         if not args:
             args = ([p for _, p in named_params],)
         super().__init__(*args, **kwargs)
@@ -53,13 +61,7 @@ class MPI_PS(torch.optim.Optimizer):
         self.use_mpi = use_mpi
         self.cuda = cuda
         self.names = list(names)
-        base = config or PSConfig()
-        over = {k: v for k, v in dict(mode=mode, codec=code, accumulate=accumulate, staleness=staleness,
-                                      average=average, bucket_mb=bucket_mb, overlap=overlap, param_wire=param_wire,
-                                      max_delay=max_delay, adam_variant=adam_variant,
-                                      debug_check_order=debug_check_order, metrics_path=metrics_path).items()
-                if v is not None}
-        self.cfg = base.replace(**over)
+        self.cfg = (config or PSConfig()).replace(**over)
         self.cfg.apply_env()
         self.cfg.validate()
         self.codec = get_codec(self.cfg.codec)
@@ -156,10 +158,10 @@ class MPI_PS(torch.optim.Optimizer):
             self.engine.before_zero_grad() if hasattr(self.engine, "before_zero_grad") else None
         self.store.zero_grad()
 
-    def irequest_params(self):
+    def irequest_params(self, **kw):
         """AsySG-InCon parameter refresh (README.md:63): adopt the newest published params that
         have arrived, without waiting for the rest (inconsistent read).  No-op in sync modes."""
-        return self.engine.irequest_params()
+        return self.engine.irequest_params(**kw)
 
     def close(self):
         if getattr(self, "engine", None) is not None:

@@ -128,11 +128,24 @@ class Engine:
     def step(self) -> Dict[str, float]:
         raise NotImplementedError
 
-    def irequest_params(self):
+    def irequest_params(self, **kw):
         return None
 
     def close(self):
         self.remove_hooks()
+
+    def engine_state(self) -> dict:
+        """Codec state (e.g. error-feedback residuals) of this rank, for checkpoints."""
+        if self.cuda:
+            torch.cuda.synchronize(self.store.device)
+        return {"codec_state": [{k: v.detach().cpu() for k, v in st.items() if k != "ws"}
+                                for st in self.codec_state]}
+
+    def load_engine_state(self, d: dict):
+        for st, saved in zip(self.codec_state, d.get("codec_state", [])):
+            for k, v in saved.items():
+                if k in st:
+                    st[k].copy_(v)
 
     def bytes_per_step(self) -> Dict[str, int]:
         return {"grad_bytes_sent": self.plan.wire_nbytes}

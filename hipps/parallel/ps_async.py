@@ -45,6 +45,18 @@ from .engine import Engine
 TIMEOUT_US = int(float(os.environ.get("HIPPS_TIMEOUT_S", "600")) * 1e6)
 
 
+def _parse_fault(spec, rank):
+    """'rank:step:kind[:arg]' -> (kind, arg, step) for this rank, else None."""
+    if not spec:
+        return None
+    for item in spec.split(","):
+        parts = item.split(":")
+        if len(parts) >= 3 and int(parts[0]) == rank:
+            arg = float(parts[3]) if len(parts) > 3 else 0.0
+            return (parts[2], arg, int(parts[1]))
+    return None
+
+
 def _align(x: int, a: int = 256) -> int:
     return (x + a - 1) // a * a
 
@@ -68,6 +80,7 @@ class PSAsyncEngine(Engine):
 
     def _setup(self, opt, cfg, store, codec, world):
         C = native()
+        self._fault = _parse_fault(os.environ.get("HIPPS_FAULT"), world.rank)
         self.C = C
         W = world.size
         self.W = W
@@ -273,11 +286,26 @@ class PSAsyncEngine(Engine):
         C = self.C
         if self.ctl.load(C.F_PS_STOP, 0):
             return True
+        dead = set(self.dead_workers())
         for i in range(self.W):
+            if i in dead:
+                continue  # failure detection: a silent worker does not hold the PS open
             stop = self.ctl.load(C.F_STOP, i)
             if stop == 0 or seen[i] < stop - 1:
                 return False
         return True
+
+    def dead_workers(self) -> List[int]:
+        """Ranks whose heartbeat is older than cfg.dead_after_s and that never said STOP."""
+        C = self.C
+        now = time.monotonic_ns()
+        lim = int(self.cfg.dead_after_s * 1e9)
+        out = []
+        for i in range(self.W):
+            hb = self.ctl.load(C.F_HEARTBEAT, i)
+            if hb and self.ctl.load(C.F_STOP, i) == 0 and now - hb > lim:
+                out.append(i)
+        return out
 
     # ------------------------------------------------------------------ worker side
     def _check_error(self):
@@ -295,6 +323,9 @@ class PSAsyncEngine(Engine):
         data = {}
         data["code_wait"] = self.encode_all()
         self._check_error()
+        if self._fault is not None and self._inject(data):
+            return data
+        self.ctl.heartbeat(self.rank)
         self.seq += 1
         s = self.seq
         slot = s % self.SLOTS
@@ -333,20 +364,44 @@ class PSAsyncEngine(Engine):
         return data
 
     def irequest_params(self, block_for: Optional[int] = None) -> bool:
-        """Adopt the newest published parameter version if it has landed (README.md:63).
+        """Adopt the newest published parameter version that has landed (README.md:63).
 
-        ``block_for=v`` waits until version >= v is published.  ``cfg.max_delay >= 0`` waits
-        until the published params include all but the newest ``max_delay`` own gradients."""
+        Remote workers on a GPU prefetch: the xGMI read of the published buffer runs on a side
+        stream and is adopted (one local copy on the compute stream) at the next call, so the
+        pull overlaps compute instead of stalling the forward pass -- one extra version of
+        staleness, which AsySG-InCon tolerates by design.  ``block_for=v`` waits until version
+        >= v is published and adopts synchronously; ``cfg.max_delay >= 0`` waits until the
+        published params include all but this worker's newest ``max_delay`` gradients."""
         C = self.C
+        sync = block_for is not None
         if block_for is not None:
             if not self.ctl.wait_ge(C.F_PUB_VER, 0, block_for, TIMEOUT_US):
                 self._check_error()
                 raise TimeoutError("no published parameters")
         if self.cfg.max_delay >= 0 and self.seq - self.cfg.max_delay > 0:
             need = self.seq - self.cfg.max_delay
+            sync = True
             if not self.ctl.wait_ge(C.F_INCL_SEQ, self.rank, need, TIMEOUT_US):
                 self._check_error()
                 raise TimeoutError(f"rank {self.rank}: params never caught up to message {need}")
+        if self._use_prefetch() and not sync:
+            return self._prefetch_pull()
+        return self._direct_pull()
+
+    def _use_prefetch(self) -> bool:
+        return self.cuda and self.rank != 0 and self.cfg.pull == "prefetch"
+
+    def _adopt(self, src, v):
+        if src.dtype == self.store.data.dtype:
+            self.store.data.copy_(src, non_blocking=self.cuda)
+        else:
+            ops.convert(src, self.store.data)
+        self.local_ver = v
+        self.ctl.store(self.C.F_APPLIED_VER, self.rank, v)
+
+    def _direct_pull(self) -> bool:
+        C = self.C
+        self._staged = None  # a synchronous adoption supersedes any prefetch in flight
         for _ in range(8):
             v = self.ctl.load(C.F_PUB_VER, 0)
             if v <= self.local_ver:
@@ -355,14 +410,62 @@ class PSAsyncEngine(Engine):
             if self.ctl.load(C.F_BUF_VER, b) != v:
                 continue  # rewritten under us: re-read the version word
             src = self.pub_buf(b)
-            if self.pub_dtype == torch.float32:
-                self.store.data.copy_(src, non_blocking=self.cuda)
-            else:
-                ops.convert(src, self.store.data)
-            if not self.cuda and self.ctl.load(C.F_BUF_VER, b) != v:
+            if self.cuda:
+                self._adopt(src, v)
+                return True
+            tmp = src.clone()
+            if self.ctl.load(C.F_BUF_VER, b) != v:
                 continue  # torn on the host path: retry (seqlock)
-            self.local_ver = v
-            self.ctl.store(C.F_APPLIED_VER, self.rank, v)
+            self._adopt(tmp, v)
+            return True
+        return False
+
+    def _prefetch_pull(self) -> bool:
+        C = self.C
+        adopted = False
+        st = getattr(self, "_staged", None)
+        if st is not None and st[1].query():
+            v, _ = st
+            torch.cuda.current_stream(self.store.device).wait_event(st[1])
+            self._adopt(self._stage_buf, v)
+            self._staged = None
+            adopted = True
+        if getattr(self, "_staged", None) is None:
+            v = self.ctl.load(C.F_PUB_VER, 0)
+            b = v % self.NPUB
+            if v > self.local_ver and self.ctl.load(C.F_BUF_VER, b) == v:
+                if getattr(self, "_stage_buf", None) is None:
+                    self._stage_buf = torch.empty(self.store.numel, dtype=self.pub_dtype, device=self.store.device)
+                    self._pull_stream = torch.cuda.Stream(device=self.store.device)
+                ps = self._pull_stream
+                # the compute stream may still read the staging buffer from the last adoption
+                ps.wait_stream(torch.cuda.current_stream(self.store.device))
+                with torch.cuda.stream(ps):
+                    self._stage_buf.copy_(self.pub_buf(b), non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(ps)
+                self._staged = (v, ev)
+        return adopted
+
+    def _inject(self, data) -> bool:
+        """Fault injection (tests): HIPPS_FAULT='rank:step:kind' with kind in
+        die (stop pushing, never say STOP), slow:<ms> (sleep before pushing), drop (skip one push).
+        Returns True when this step's push is suppressed."""
+        step_no = self.steps + 1
+        kind, arg, at = self._fault
+        if step_no < at:
+            return False
+        if kind == "slow":
+            time.sleep(arg / 1000.0)
+            return False
+        if kind == "drop" and step_no == at:
+            data["dropped_by_fault"] = 1.0
+            self.steps += 1
+            return True
+        if kind == "die":
+            self._dead = True
+            data["dead_by_fault"] = 1.0
+            self.steps += 1
             return True
         return False
 
@@ -382,7 +485,9 @@ class PSAsyncEngine(Engine):
         try:
             if self.cuda:
                 torch.cuda.synchronize(self.store.device)
-            self.ctl.store(C.F_STOP, self.rank, self.seq + 1)
+            self._staged = None
+            if not getattr(self, "_dead", False):
+                self.ctl.store(C.F_STOP, self.rank, self.seq + 1)
             if self.rank == 0 and self._thread is not None:
                 deadline = time.time() + TIMEOUT_US / 1e6
                 while self._thread.is_alive() and time.time() < deadline:
@@ -397,6 +502,43 @@ class PSAsyncEngine(Engine):
                 self.mailbox.close()
         if self._err:
             raise RuntimeError(self._err)
+
+    # ------------------------------------------------------------------ checkpoint support
+    def engine_state(self) -> dict:
+        """PS state (rank 0) + this worker's codec state.  Call between steps."""
+        if self.cuda:
+            torch.cuda.synchronize(self.store.device)
+        d = {"codec_state": [{k: v.detach().cpu() for k, v in st.items() if k != "ws"} for st in self.codec_state],
+             "seq": self.seq, "local_ver": self.local_ver}
+        if self.rank == 0:
+            self.ps_stream.synchronize() if self.cuda else None
+            d.update({"master": self.master.detach().cpu(), "version": self.ver})
+        return d
+
+    def load_engine_state(self, d: dict):
+        """Restore before the first step() after construction (collective: all ranks call)."""
+        for st, saved in zip(self.codec_state, d.get("codec_state", [])):
+            for k, v in saved.items():
+                if k in st:
+                    st[k].copy_(v)
+        if self.rank == 0 and "master" in d:
+            C = self.C
+            if self.steps or self._stats["accumulated"]:
+                raise RuntimeError("load the PS state before training starts")
+            self.master.copy_(d["master"].to(self.master.device))
+            self.ver = int(d["version"])
+            b = self.ver % self.NPUB
+            ops.convert(self.master, self.pub_buf(b))
+            if self.cuda:
+                torch.cuda.current_stream(self.store.device).synchronize()
+            self.ctl.store(C.F_BUF_VER, b, self.ver)
+            self.ctl.store(C.F_PUB_VER, 0, self.ver)
+        barrier(self.world)
+        ver = self.ctl.load(self.C.F_PUB_VER, 0)
+        self.local_ver = -1
+        self.irequest_params(block_for=ver)
+        if self.cuda:
+            torch.cuda.current_stream(self.store.device).synchronize()
 
     def final_params(self) -> Optional[torch.Tensor]:
         """PS master parameters (rank 0 only) after close()."""

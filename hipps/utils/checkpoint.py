@@ -1,0 +1,83 @@
+"""Checkpoint / resume.
+
+The reference has none beyond torch.optim.Optimizer.state_dict() (its per-parameter state keys
+are torch-compatible, ps.py:202-205, 223-234) and never saves ``MPI_PS.steps`` (ps.py:74).
+
+Layout of a checkpoint directory (all files are plain tensors/ints: loadable with
+``torch.load(..., weights_only=True)``):
+  ps.pt          written by rank 0: parameters (the PS master in async mode), flat optimizer
+                 state (momentum / Adam moments), per-group step counts, PS version, metadata
+  rank<r>.pt     written by every rank: its codec state (error-feedback residuals), its worker
+                 sequence numbers and (optionally) the model's buffers (BN running statistics)
+
+``save``/``load`` are collective (every rank calls them).  In ps_async mode ``load`` must run
+after constructing the optimizer and before the first ``step()``: the PS republishes the
+restored master as the current version and every worker adopts it.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+
+from hipps.parallel.dist import barrier, broadcast
+
+
+def _cpu(d):
+    return {k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in d.items()}
+
+
+def save(opt, path: str, model: Optional[torch.nn.Module] = None, extra: Optional[dict] = None) -> None:
+    os.makedirs(path, exist_ok=True)
+    eng = opt.engine
+    rank = opt.world.rank
+    es = eng.engine_state()
+    master = es.pop("master", None)
+    version = es.pop("version", None)
+    mine = {"engine": es}
+    if model is not None:
+        mine["buffers"] = {k: v.detach().cpu() for k, v in model.named_buffers()}
+    torch.save(mine, os.path.join(path, f"rank{rank}.pt"))
+    if rank == 0:
+        params = master if master is not None else opt.store.data.detach().cpu()
+        ps = {"params": params, "flat_state": _cpu(opt.flat_state), "group_steps": list(opt._group_steps),
+              "steps": opt.steps, "mode": opt.mode, "codec": opt.codec.name, "numel": opt.store.numel,
+              "version": -1 if version is None else int(version),
+              "mom_started": sorted(getattr(opt, "_mom_started", set()))}
+        if extra:
+            ps["extra"] = extra
+        torch.save(ps, os.path.join(path, "ps.pt"))
+    barrier(opt.world)
+
+
+def load(opt, path: str, model: Optional[torch.nn.Module] = None) -> dict:
+    ps = torch.load(os.path.join(path, "ps.pt"), map_location="cpu", weights_only=True)
+    if ps["numel"] != opt.store.numel:
+        raise ValueError(f"checkpoint has {ps['numel']} flat elements, optimizer has {opt.store.numel}")
+    for k, v in ps["flat_state"].items():
+        opt._ensure_state(k).copy_(v)
+    opt._group_steps = list(ps["group_steps"])
+    opt.steps = ps["steps"]
+    if ps.get("mom_started"):
+        opt._mom_started = set(ps["mom_started"])
+    rank = opt.world.rank
+    rp = os.path.join(path, f"rank{rank}.pt")
+    mine = torch.load(rp, map_location="cpu", weights_only=True) if os.path.exists(rp) else {"engine": {}}
+    if model is not None and "buffers" in mine:
+        bufs = dict(model.named_buffers())
+        for k, v in mine["buffers"].items():
+            if k in bufs:
+                bufs[k].copy_(v)
+    es = dict(mine.get("engine", {}))
+    if opt.mode == "ps_async":
+        if rank == 0:
+            es["master"] = ps["params"]
+            es["version"] = max(0, ps["version"])
+        opt.engine.load_engine_state(es)
+    else:
+        opt.store.data.copy_(ps["params"].to(opt.store.data.device))
+        broadcast(opt.store.data, opt.world, 0)
+        opt.engine.load_engine_state(es)
+    barrier(opt.world)
+    return ps.get("extra", {})
