@@ -33,6 +33,7 @@ import torch.nn.functional as F  # noqa: E402
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 METRIC = "samples/sec (node) ResNet-50 async PS at 1/2/4/8 MI355X; grad bytes/step"
+TRANSFORMERS = ("bert-base", "bert-tiny", "llama3-8b", "llama3-1b", "llama-tiny")
 
 
 def parse():
@@ -47,6 +48,10 @@ def parse():
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--accumulate", type=int, default=0, help="PS update every M grads (0 = world size)")
     ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--seq", type=int, default=512, help="sequence length (transformer configs)")
+    ap.add_argument("--param-wire", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--momentum", type=float, default=0.9)
+    ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     return ap.parse_args()
@@ -67,33 +72,40 @@ def main():
     from hipps.models import build_model
 
     torch.manual_seed(1234 + world.rank)
+    is_tf = a.model in TRANSFORMERS
     model = build_model(a.model).to(dev)
-    cl = not a.no_channels_last
+    cl = not a.no_channels_last and not is_tf
     if cl:
         model = model.to(memory_format=torch.channels_last)
-    x = torch.randn(a.batch, 3, a.image, a.image, device=dev)
-    if cl:
-        x = x.contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 1000, (a.batch,), device=dev)
+    if is_tf:
+        vocab = model.c.vocab
+        x = torch.randint(0, vocab, (a.batch, a.seq), device=dev)
+        y = torch.randint(0, vocab, (a.batch, a.seq), device=dev)
+    else:
+        x = torch.randn(a.batch, 3, a.image, a.image, device=dev)
+        if cl:
+            x = x.contiguous(memory_format=torch.channels_last)
+        y = torch.randint(0, 1000, (a.batch,), device=dev)
 
     mode = a.mode if N > 1 or a.mode in ("ps_async", "local") else "local"
     note = None
     try:
-        opt = hipps.SGD(model.named_parameters(), lr=a.lr, momentum=0.9, weight_decay=5e-5, mode=mode, code=a.codec,
-                        accumulate=a.accumulate or None, average=True)
+        opt = hipps.SGD(model.named_parameters(), lr=a.lr, momentum=a.momentum, weight_decay=5e-5, mode=mode,
+                        code=a.codec, accumulate=a.accumulate or None, average=True, param_wire=a.param_wire,
+                        bucket_mb=a.bucket_mb)
     except Exception as e:  # robust fallback so a scaling run still reports a number
         if mode != "ps_async" or N == 1:
             raise
         note = f"ps_async init failed ({type(e).__name__}: {e}); fell back to ps_sync"
         print("[bench] " + note, file=sys.stderr)
         mode = "ps_sync"
-        opt = hipps.SGD(model.named_parameters(), lr=a.lr, momentum=0.9, weight_decay=5e-5, mode=mode,
-                        code=a.codec, average=True)
+        opt = hipps.SGD(model.named_parameters(), lr=a.lr, momentum=a.momentum, weight_decay=5e-5, mode=mode,
+                        code=a.codec, average=True, param_wire=a.param_wire, bucket_mb=a.bucket_mb)
 
     def step():
         opt.zero_grad()
         with torch.autocast("cuda", dtype=torch.bfloat16):
-            loss = F.cross_entropy(model(x), y)
+            loss = model(x, y) if is_tf else F.cross_entropy(model(x), y)
         loss.backward()
         _, data = opt.step()
         return loss, data
@@ -115,14 +127,21 @@ def main():
     elapsed = float(el.item())
     final_loss = float(loss.float().item())
     grad_bytes = int(last.get("grad_bytes_sent", 0)) if last else 0
-    stats = opt.engine.ps_stats() if hasattr(opt.engine, "ps_stats") else {}
+    nbuckets = len(opt.engine.plan.buckets)
+    nparams = sum(p.numel() for p in model.parameters())
     opt.close()
-    value = N * a.batch * a.steps / elapsed
+    stats = {}
+    if hasattr(opt, "_last_engine_stats"):
+        stats = opt._last_engine_stats
+    per_sample = a.seq if is_tf else 1
+    value = N * a.batch * per_sample * a.steps / elapsed
     if world.rank == 0:
+        metric = METRIC if a.model == "resnet50" else (
+            f"{'tokens' if is_tf else 'samples'}/sec (node) {a.model} {mode} (secondary BASELINE config)")
         rec = {
-            "metric": METRIC,
+            "metric": metric,
             "value": round(value, 2),
-            "unit": "samples/s",
+            "unit": "tokens/s" if is_tf else "samples/s",
             "n_gpus": N,
             "steps": a.steps,
             "warmup": a.warmup,
@@ -131,18 +150,21 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (random 224x224 images / labels, random-init weights)",
+            "data": ("synthetic (random tokens, random-init weights)" if is_tf else
+                     "synthetic (random 224x224 images / labels, random-init weights)"),
             "config": {
                 "model": a.model,
                 "global_batch": a.batch * N,
                 "per_gpu_batch": a.batch,
-                "seq_len": None,
-                "image": a.image,
+                "seq_len": a.seq if is_tf else None,
+                "image": None if is_tf else a.image,
                 "parallelism": f"dp{N} {mode} (rank0 = PS + worker)",
                 "codec": a.codec,
                 "accumulate": a.accumulate or N,
                 "grad_bytes_per_step_per_worker": grad_bytes,
-                "param_wire": "fp32",
+                "param_wire": a.param_wire,
+                "num_params": nparams,
+                "buckets": nbuckets,
             },
             "final_loss": round(final_loss, 4),
             "ps": {k: (int(v) if isinstance(v, (int, float)) else v) for k, v in stats.items()},

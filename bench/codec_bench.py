@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""Codec microbenchmark: the device counterpart of the reference's serialization notebook.
+
+Reference (Serialization-timing.ipynb): pickle dump / load and zlib compress of an
+n-element float64 payload, n = 10 .. 10^4 (dump min ~32.9 us, load min ~18.8 us at n = 10^4 on
+the author's machine; 18.3 / 10.6 us re-measured on this container's Xeon).  That is the cost
+the reference pays per tensor per rank to put a gradient on the wire (plus D2H/H2D copies).
+
+Here the same job is one device encode (gradient -> wire buffer) and one fused decode-accumulate
+(wire -> fp32 accumulator), timed with HIP events, for each codec, at the notebook sizes and at
+bucket sizes (1 M, 25.6 M = all of ResNet-50).  Also reports wire bytes per element.
+
+    python bench/codec_bench.py [--out profiles/codec_bench.json] [--cpu]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from hipps import codecs  # noqa: E402
+
+SPECS = ["fp32", "bf16", "int8", "int8_sr", "topk:0.01", "topk_bf16:0.01", "topk_int8:0.01"]
+
+
+def timed(fn, dev, iters):
+    for _ in range(3):
+        fn()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(True), torch.cuda.Event(True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) * 1e3 / iters  # us
+    t = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    return (time.perf_counter() - t) * 1e6 / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--sizes", default="10,100,1000,10000,1000000,25557032")
+    a = ap.parse_args()
+    dev = torch.device("cpu" if a.cpu or not torch.cuda.is_available() else "cuda")
+    sizes = [int(s) for s in a.sizes.split(",")]
+    rows = []
+    for n in sizes:
+        x = torch.randn(n, device=dev) * 1e-2
+        for spec in SPECS:
+            c = codecs.get_codec(spec)
+            lay = c.layout(n)
+            buf = torch.empty(lay.nbytes, dtype=torch.uint8, device=dev)
+            views = lay.views(buf)
+            st = c.init_state(n, dev)
+            acc = torch.zeros(n, device=dev)
+            iters = 200 if n <= 1_000_000 else 30
+            if dev.type == "cpu" and n > 1_000_000:
+                iters = 3
+            enc = timed(lambda: c.encode_into(x, views, st), dev, iters)
+            dec = timed(lambda: c.accumulate([views], acc, 1.0, True), dev, iters)
+            row = {"n": n, "codec": spec, "device": dev.type, "encode_us": round(enc, 2), "decode_acc_us": round(dec, 2),
+                   "wire_bytes": lay.nbytes, "bytes_per_elem": round(lay.nbytes / n, 4),
+                   "encode_GBps_in": round(n * 4 / enc / 1e3, 1)}
+            rows.append(row)
+            print(json.dumps(row), flush=True)
+    # reference method for the same payload sizes (host pickle of a float32 numpy array)
+    import pickle
+    import zlib
+
+    for n in sizes[:4]:
+        arr = np.random.randn(n).astype(np.float32)
+        dumps, loads, comp = [], [], []
+        for _ in range(100):
+            t = time.perf_counter()
+            b = pickle.dumps(arr)
+            dumps.append(time.perf_counter() - t)
+            t = time.perf_counter()
+            z = zlib.compress(b, 1)
+            comp.append(time.perf_counter() - t)
+            t = time.perf_counter()
+            pickle.loads(b)
+            loads.append(time.perf_counter() - t)
+        row = {"n": n, "codec": "reference-pickle(host)", "device": "cpu", "encode_us": round(min(dumps) * 1e6, 2),
+               "decode_acc_us": round(min(loads) * 1e6, 2), "zlib1_us_mean": round(float(np.mean(comp)) * 1e6, 1),
+               "wire_bytes": len(b)}
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+    if a.out:
+        os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump(rows, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

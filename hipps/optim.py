@@ -166,6 +166,8 @@ class MPI_PS(torch.optim.Optimizer):
     def close(self):
         if getattr(self, "engine", None) is not None:
             self.engine.close()
+            if hasattr(self.engine, "ps_stats"):
+                self._last_engine_stats = self.engine.ps_stats()  # drained totals after close
             self.engine = None
         if self._metrics is not None:
             self._metrics.close()

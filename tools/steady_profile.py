@@ -1,0 +1,58 @@
+"""Summarize a rocprofv3 kernel trace to steady-state per-step costs.
+
+Steps are delimited by a marker kernel that runs once per optimizer step (default: hipps
+k_sgd); the first `--skip` steps (warmup incl. MIOpen find) are dropped.
+    python tools/steady_profile.py trace.csv out.txt [--marker k_sgd] [--skip 5]
+"""
+import argparse
+import collections
+import csv
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("out")
+    ap.add_argument("--marker", default="k_sgd")
+    ap.add_argument("--skip", type=int, default=5)
+    ap.add_argument("--title", default="")
+    a = ap.parse_args()
+    rows = list(csv.DictReader(open(a.trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    marks = [int(r["Start_Timestamp"]) for r in rows if a.marker in r["Kernel_Name"]]
+    if len(marks) < a.skip + 2:
+        raise SystemExit(f"only {len(marks)} marker kernels")
+    t0, t1 = marks[a.skip], marks[-1]
+    n = len(marks) - 1 - a.skip
+    steady = [r for r in rows if t0 <= int(r["Start_Timestamp"]) < t1]
+    agg = collections.defaultdict(lambda: [0, 0])
+    for r in steady:
+        agg[r["Kernel_Name"]][0] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        agg[r["Kernel_Name"]][1] += 1
+    tot = sum(v[0] for v in agg.values())
+    cat = collections.defaultdict(float)
+    for k, (d, c) in agg.items():
+        if "hipps" in k:
+            key = "hipps-norm" if "k_bn_" in k else "hipps-ps"
+        elif "BatchNorm" in k:
+            key = "miopen-batchnorm"
+        elif any(s in k for s in ("conv", "igemm", "gemm", "Cijk", "xdl")):
+            key = "conv/gemm"
+        elif "elementwise" in k or "Functor" in k:
+            key = "elementwise"
+        else:
+            key = "other"
+        cat[key] += d
+    lines = [a.title, f"steady steps={n} wall/step={(t1 - t0) / n / 1e6:.2f} ms kernel-sum/step={tot / n / 1e6:.2f} ms "
+                      f"launches/step={len(steady) / n:.0f}"]
+    for k, v in sorted(cat.items(), key=lambda x: -x[1]):
+        lines.append(f"  {k:18s} {v / n / 1e6:8.3f} ms/step {100 * v / tot:5.1f}%")
+    lines.append("")
+    for k, (d, c) in sorted(agg.items(), key=lambda x: -x[1][0])[:40]:
+        lines.append(f"{d / n / 1e3:9.1f} us/step calls/step={c / n:6.1f}  {k[:140]}")
+    open(a.out, "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines[:12]))
+
+
+if __name__ == "__main__":
+    main()
