@@ -47,14 +47,35 @@ __device__ __forceinline__ void load8f(const float* p, float v[8]) {
 
 enum MaskMode { MASK_NONE = 0, MASK_X = 1, MASK_Y = 2 };
 
-// ---- per-channel reductions -> partial[rb][C] (two arrays) ---------------------------------
+// ---- per-channel reductions -> partial[c][rb] (channel-major, two arrays) ------------------
 // FWD: a += x, b += x*x.   BWD: dz = dy*mask; a += dz, b += dz*(x-mean)*invstd.
+// Each lane keeps 4 rows (up to 12 x 16 B) in flight before consuming them: one load per
+// iteration left these passes at 3.2-3.9 TB/s (profiles/bench_n1_steady_fusedbn.txt).
+template <bool BWD>
+__device__ __forceinline__ void reduce_row(const float xv[8], const float* d, const float* yv, int mask_mode,
+                                           const float mu[8], const float is[8], const float sc[8],
+                                           const float sh[8], float sa[8], float sb[8]) {
+  if (!BWD) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sa[j] += xv[j]; sb[j] = fmaf(xv[j], xv[j], sb[j]); }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float dz = d[j];
+      if (mask_mode == MASK_Y) dz = yv[j] > 0.f ? dz : 0.f;
+      else if (mask_mode == MASK_X) dz = fmaf(xv[j], sc[j], sh[j]) > 0.f ? dz : 0.f;
+      sa[j] += dz;
+      sb[j] = fmaf(dz, (xv[j] - mu[j]) * is[j], sb[j]);
+    }
+  }
+}
+
 template <bool BWD>
 __global__ __launch_bounds__(kBlock) void k_bn_reduce(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
                                                       const uint16_t* __restrict__ y, int mask_mode,
                                                       const float* __restrict__ mean, const float* __restrict__ invstd,
                                                       const float* __restrict__ scale, const float* __restrict__ shift,
-                                                      int64_t M, int C, int64_t rows_per_wg,
+                                                      int64_t M, int C, int64_t rows_per_wg, int nrb,
                                                       float* __restrict__ pa, float* __restrict__ pb) {
   __shared__ float la[kBlock * 8], lb[kBlock * 8];
   const int G = C >> 3, R = kBlock / G;
@@ -62,39 +83,35 @@ __global__ __launch_bounds__(kBlock) void k_bn_reduce(const uint16_t* __restrict
   const int c0 = g * 8;
   float sa[8], sb[8], mu[8], is[8], sc[8], sh[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { sa[j] = 0.f; sb[j] = 0.f; }
+  for (int j = 0; j < 8; ++j) { sa[j] = 0.f; sb[j] = 0.f; mu[j] = 0.f; is[j] = 0.f; sc[j] = 0.f; sh[j] = 0.f; }
   if (BWD) {
     load8f(mean + c0, mu);
     load8f(invstd + c0, is);
     if (mask_mode == MASK_X) { load8f(scale + c0, sc); load8f(shift + c0, sh); }
   }
+  const bool need_y = BWD && mask_mode == MASK_Y;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_wg;
   const int64_t r1 = min(M, r0 + rows_per_wg);
-  for (int64_t row = r0 + r; row < r1; row += R) {
-    const int64_t off = row * C + c0;
-    float xv[8];
-    load8(x + off, xv);
-    if (!BWD) {
+  int64_t row = r0 + r;
+  for (; row + 3 * (int64_t)R < r1; row += 4 * (int64_t)R) {
+    float xv[4][8], d[4][8], yv[4][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { sa[j] += xv[j]; sb[j] = fmaf(xv[j], xv[j], sb[j]); }
-    } else {
-      float d[8];
-      load8(dy + off, d);
-      if (mask_mode == MASK_Y) {
-        float yv[8];
-        load8(y + off, yv);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
-      } else if (mask_mode == MASK_X) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) d[j] = fmaf(xv[j], sc[j], sh[j]) > 0.f ? d[j] : 0.f;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        sa[j] += d[j];
-        sb[j] = fmaf(d[j], (xv[j] - mu[j]) * is[j], sb[j]);
-      }
+    for (int u = 0; u < 4; ++u) {
+      const int64_t off = (row + u * (int64_t)R) * C + c0;
+      load8(x + off, xv[u]);
+      if (BWD) load8(dy + off, d[u]);
+      if (need_y) load8(y + off, yv[u]);
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) reduce_row<BWD>(xv[u], d[u], yv[u], mask_mode, mu, is, sc, sh, sa, sb);
+  }
+  for (; row < r1; row += R) {
+    const int64_t off = row * C + c0;
+    float xv[8], d[8], yv[8];
+    load8(x + off, xv);
+    if (BWD) load8(dy + off, d);
+    if (need_y) load8(y + off, yv);
+    reduce_row<BWD>(xv, d, yv, mask_mode, mu, is, sc, sh, sa, sb);
   }
   // combine the R row lanes of each channel group through LDS
 #pragma unroll
@@ -103,39 +120,32 @@ __global__ __launch_bounds__(kBlock) void k_bn_reduce(const uint16_t* __restrict
   for (int c = threadIdx.x; c < C; c += kBlock) {
     float a = 0.f, b = 0.f;
     for (int q = 0; q < R; ++q) { a += la[q * C + c]; b += lb[q * C + c]; }
-    pa[(int64_t)blockIdx.x * C + c] = a;
-    pb[(int64_t)blockIdx.x * C + c] = b;
+    pa[(int64_t)c * nrb + blockIdx.x] = a;
+    pb[(int64_t)c * nrb + blockIdx.x] = b;
   }
 }
 
-// Combine partial[rb][C] over rb for 32 channels per workgroup: 256 lanes = 32 channels x 8 row
-// lanes, fp64 accumulation, LDS tree.  (A serial per-channel loop over 512-1024 partials cost
-// 180-270 us per call: profiles/bn_micro_r1.txt.)
-constexpr int kFinCh = 32;
+// Combine partial[c][rb] over rb: one wave per channel (4 channels per workgroup), lanes read
+// consecutive partials (coalesced), fp64 sums, 6-step shuffle tree.  (The first version looped
+// serially per channel: 180-270 us per call, profiles/bn_micro_r1.txt.)
+constexpr int kFinCh = 4;
 __device__ __forceinline__ bool combine_partials(const float* __restrict__ pa, const float* __restrict__ pb, int nrb,
                                                  int C, double& s, double& q) {
-  __shared__ double ls[kBlock], lq[kBlock];
-  const int cl = threadIdx.x % kFinCh, lane = threadIdx.x / kFinCh;  // 8 lanes
-  const int c = blockIdx.x * kFinCh + cl;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * kFinCh + (threadIdx.x >> 6);
   double a = 0.0, b = 0.0;
   if (c < C) {
-    for (int i = lane; i < nrb; i += kBlock / kFinCh) {
-      a += pa[(int64_t)i * C + c];
-      b += pb[(int64_t)i * C + c];
-    }
+    const float* ra = pa + (int64_t)c * nrb;
+    const float* rb = pb + (int64_t)c * nrb;
+    for (int i = lane; i < nrb; i += 64) { a += ra[i]; b += rb[i]; }
   }
-  ls[threadIdx.x] = a;
-  lq[threadIdx.x] = b;
-  __syncthreads();
-  for (int off = kBlock / 2; off >= kFinCh; off >>= 1) {
-    if (threadIdx.x < off) {
-      ls[threadIdx.x] += ls[threadIdx.x + off];
-      lq[threadIdx.x] += lq[threadIdx.x + off];
-    }
-    __syncthreads();
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
   }
-  s = ls[cl];
-  q = lq[cl];
+  s = a;
+  q = b;
   return lane == 0 && c < C;
 }
 
@@ -149,7 +159,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_finalize_fwd(const float* __restr
                                                             float* __restrict__ shift) {
   double s, q;
   if (!combine_partials(pa, pb, nrb, C, s, q)) return;
-  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
+  const int c = blockIdx.x * kFinCh + (threadIdx.x >> 6);
   const double m = s / (double)M;
   double var = q / (double)M - m * m;
   if (var < 0.0) var = 0.0;
@@ -175,7 +185,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_finalize_bwd(const float* __restr
                                                             float* __restrict__ ck1, float* __restrict__ ck0) {
   double s, q;
   if (!combine_partials(pa, pb, nrb, C, s, q)) return;
-  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
+  const int c = blockIdx.x * kFinCh + (threadIdx.x >> 6);
   if (dw) dw[c] = (float)q;
   if (db) db[c] = (float)s;
   const double is = invstd[c];
@@ -231,29 +241,47 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_bwd(const uint16_t* __restr
   const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int c0 = (int)(v0 % G) * 8;
   float a[8], k1[8], k0[8], sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sc[j] = 0.f; sh[j] = 0.f; }
   load8f(ca + c0, a);
   load8f(ck1 + c0, k1);
   load8f(ck0 + c0, k0);
   if (mask_mode == MASK_X) { load8f(scale + c0, sc); load8f(shift + c0, sh); }
-  for (int64_t v = v0; v < V; v += stride) {
-    const int64_t off = v * 8;
-    float d[8], xv[8];
-    load8(dy + off, d);
-    load8(x + off, xv);
-    if (mask_mode == MASK_Y) {
-      float yv[8];
-      load8(y + off, yv);
+  auto body = [&](const float* d_in, const float* xv, const float* yv, int64_t off) {
+    float d[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
-    } else if (mask_mode == MASK_X) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = fmaf(xv[j], sc[j], sh[j]) > 0.f ? d[j] : 0.f;
+    for (int j = 0; j < 8; ++j) {
+      float dz = d_in[j];
+      if (mask_mode == MASK_Y) dz = yv[j] > 0.f ? dz : 0.f;
+      else if (mask_mode == MASK_X) dz = fmaf(xv[j], sc[j], sh[j]) > 0.f ? dz : 0.f;
+      d[j] = dz;
     }
     if (dres) store8(dres + off, d);
     float o[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = fmaf(a[j], d[j], fmaf(k1[j], xv[j], k0[j]));
     store8(dx + off, o);
+  };
+  const bool need_y = mask_mode == MASK_Y;
+  int64_t v = v0;
+  for (; v + stride < V; v += 2 * stride) {  // two vectors in flight per lane
+    float d0[8], x0[8], y0[8], d1[8], x1[8], y1[8];
+    const int64_t o0 = v * 8, o1 = (v + stride) * 8;
+    load8(dy + o0, d0);
+    load8(x + o0, x0);
+    load8(dy + o1, d1);
+    load8(x + o1, x1);
+    if (need_y) { load8(y + o0, y0); load8(y + o1, y1); }
+    body(d0, x0, y0, o0);
+    body(d1, x1, y1, o1);
+  }
+  for (; v < V; v += stride) {
+    float d0[8], x0[8], y0[8];
+    const int64_t o0 = v * 8;
+    load8(dy + o0, d0);
+    load8(x + o0, x0);
+    if (need_y) load8(y + o0, y0);
+    body(d0, x0, y0, o0);
   }
 }
 
@@ -272,7 +300,7 @@ int64_t pick_rows(int64_t M, int C, int& nrb) {
   const int G = C / 8, R = kBlock / G;
   const int64_t vec = M * G;
   int64_t want = vec / (kBlock * 16);  // >= 16 vectors per lane
-  want = std::max<int64_t>(1, std::min<int64_t>(want, 512));
+  want = std::max<int64_t>(1, std::min<int64_t>(want, 1024));
   int64_t rows = (M + want - 1) / want;
   rows = (rows + R - 1) / R * R;
   nrb = (int)((M + rows - 1) / rows);
@@ -310,10 +338,10 @@ void bn_forward_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y,
   }
   int nrb;
   const int64_t rows = pick_rows(M, (int)C, nrb);
-  auto part = at::empty({2, (int64_t)nrb, C}, weight.options());
+  auto part = at::empty({2, C, (int64_t)nrb}, weight.options());
   auto stream = c10::hip::getCurrentHIPStream();
   hipLaunchKernelGGL(k_bn_reduce<false>, nrb, kBlock, 0, stream, (const uint16_t*)x.data_ptr(), nullptr, nullptr, 0,
-                     nullptr, nullptr, nullptr, nullptr, M, (int)C, rows, part[0].data_ptr<float>(),
+                     nullptr, nullptr, nullptr, nullptr, M, (int)C, rows, nrb, part[0].data_ptr<float>(),
                      part[1].data_ptr<float>());
   hipLaunchKernelGGL(k_bn_finalize_fwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, part[0].data_ptr<float>(),
                      part[1].data_ptr<float>(), nrb, (int)C, M, weight.data_ptr<float>(), bias.data_ptr<float>(),
@@ -365,12 +393,12 @@ void bn_backward(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> y, int64
   for (auto* t : {&weight, &mean, &invstd, &scale, &shift, &dweight, &dbias}) check_vec(*t, "per-channel vector", (int)C);
   int nrb;
   const int64_t rows = pick_rows(M, (int)C, nrb);
-  auto part = at::empty({2, (int64_t)nrb, C}, weight.options());
+  auto part = at::empty({2, C, (int64_t)nrb}, weight.options());
   auto coef = at::empty({3, C}, weight.options());
   auto stream = c10::hip::getCurrentHIPStream();
   hipLaunchKernelGGL(k_bn_reduce<true>, nrb, kBlock, 0, stream, (const uint16_t*)x.data_ptr(),
                      (const uint16_t*)dy.data_ptr(), yp, (int)mask_mode, mean.data_ptr<float>(),
-                     invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(), M, (int)C, rows,
+                     invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(), M, (int)C, rows, nrb,
                      part[0].data_ptr<float>(), part[1].data_ptr<float>());
   hipLaunchKernelGGL(k_bn_finalize_bwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, part[0].data_ptr<float>(),
                      part[1].data_ptr<float>(), nrb, (int)C, M, weight.data_ptr<float>(), mean.data_ptr<float>(),

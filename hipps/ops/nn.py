@@ -57,6 +57,16 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
         super().__init__(num_features, **kw)
         self.relu = relu
         self.fused = fused
+        # num_batches_tracked is only read when momentum is None; bumping the device buffer costs
+        # one kernel launch per BN per step (53 per ResNet-50 step), so count on the host and fold
+        # the count in whenever the state is read.
+        self._nbt_pending = 0
+        self.register_state_dict_pre_hook(lambda mod, *a, **k: mod.sync_num_batches_tracked())
+
+    def sync_num_batches_tracked(self):
+        if self._nbt_pending and self.num_batches_tracked is not None:
+            self.num_batches_tracked.add_(self._nbt_pending)
+        self._nbt_pending = 0
 
     def extra_repr(self):
         return super().extra_repr() + f", relu={self.relu}, fused={self.fused}"
@@ -79,7 +89,7 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
     def forward(self, x, residual=None):
         if self._fast_ok(x, residual):
             if self.training:
-                self.num_batches_tracked.add_(1)
+                self._nbt_pending += 1
                 return fused_bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, self.eps,
                                     self.momentum, self.relu, residual)
             if not torch.is_grad_enabled() or not (x.requires_grad or (residual is not None and

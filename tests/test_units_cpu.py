@@ -1,0 +1,99 @@
+"""CPU unit tests: flat store, bucket plan, config, codec layouts, launcher."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.nn as nn
+
+import hipps
+from hipps.codecs import WireLayout, get_codec
+from hipps.config import PSConfig
+from hipps.parallel.flat import BucketPlan, FlatStore
+
+
+def test_flat_store_views_channels_last_and_grads():
+    m = nn.Sequential(nn.Conv2d(3, 8, 3), nn.BatchNorm2d(8), nn.Conv2d(8, 4, 1)).to(memory_format=torch.channels_last)
+    before = [p.detach().clone() for p in m.parameters()]
+    st = FlatStore([list(m.parameters())])
+    for p, b in zip(m.parameters(), before):
+        assert torch.equal(p, b)
+        assert p.data_ptr() >= st.data.data_ptr()
+        assert (p.data_ptr() - st.data.data_ptr()) % 64 == 0  # 16-element aligned slots
+    assert m[0].weight.is_contiguous(memory_format=torch.channels_last)
+    x = torch.randn(2, 3, 8, 8).contiguous(memory_format=torch.channels_last)
+    m(x).sum().backward()
+    assert st.grads_attached()
+    assert st.grad.abs().sum() > 0
+    m.zero_grad(set_to_none=True)  # user drops the views ...
+    st.attach_grads()  # ... and they come back
+    assert st.grads_attached()
+
+
+def test_bucket_plan_tiles_flat_buffer_and_dense_image():
+    m = nn.Sequential(*[nn.Linear(64, 64) for _ in range(6)])
+    st = FlatStore([list(m.parameters())])
+    plan = BucketPlan(st, get_codec("bf16"), bucket_bytes=40_000)
+    assert plan.buckets[0].lo == 0 and plan.buckets[-1].hi == st.numel
+    for a, b in zip(plan.buckets, plan.buckets[1:]):
+        assert a.hi == b.lo
+    assert len(plan.buckets) > 1
+    assert plan.wire_nbytes == st.numel * 2  # dense bf16 image is linear
+    assert plan.ready_order[0] == len(plan.buckets) - 1  # last layers first
+
+
+def test_config_env_override(monkeypatch):
+    monkeypatch.setenv("HIPPS_ACCUMULATE", "7")
+    monkeypatch.setenv("HIPPS_AVERAGE", "1")
+    c = PSConfig.from_kwargs(mode="ps_sync")
+    assert c.accumulate == 7 and c.average is True and c.mode == "ps_sync"
+    with pytest.raises(ValueError):
+        PSConfig.from_kwargs(mode="bogus")
+
+
+def test_codec_layouts_and_bytes():
+    n = 100_000
+    assert get_codec("fp32").nbytes(n) == 400_000
+    assert get_codec("bf16").nbytes(n) == 200_000
+    assert 100_000 + 4 * 391 <= get_codec("int8").nbytes(n) <= 100_000 + 4 * 391 + 32
+    k = 1000
+    assert get_codec("topk:0.01").nbytes(n) == k * 8
+    lay = get_codec("topk_int8:0.01").layout(n)
+    assert lay.nbytes < k * 6
+    for f in lay.fields:
+        assert f.offset % 16 == 0
+    with pytest.raises(ValueError):
+        get_codec("nope")
+
+
+def test_reference_object_api_roundtrip():
+    c = get_codec("topk:0.5")
+    g = torch.randn(4, 5)
+    code = c.encode(g)
+    c.codes = [code]
+    d = c.decode(code)
+    assert d.shape == g.shape
+    nz = d != 0
+    assert nz.sum() == 10 and torch.equal(d[nz], g[nz])
+
+
+def test_optimizer_kwargs_routing():
+    m = nn.Linear(4, 2)
+    opt = hipps.Adam(m.named_parameters(), m.parameters(), lr=1e-3, betas=(0.8, 0.9), accumulate=3, mode="local")
+    assert opt.cfg.accumulate == 3 and opt.param_groups[0]["betas"] == (0.8, 0.9)
+    with pytest.raises(ValueError):
+        hipps.SGD(m.named_parameters(), lr=0.1, optim="adam")
+
+
+def test_launcher_propagates_failure(tmp_path):
+    ok = tmp_path / "ok.py"
+    ok.write_text("import os; print('rank', os.environ['RANK'], os.environ['WORLD_SIZE'])\n")
+    bad = tmp_path / "bad.py"
+    bad.write_text("import os, sys, time\nif os.environ['RANK'] == '1': sys.exit(3)\ntime.sleep(30)\n")
+    r = subprocess.run([sys.executable, "-m", "hipps.launch", "-n", "2", str(ok)], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0 and "[rank1] rank 1 2" in r.stdout
+    r = subprocess.run([sys.executable, "-m", "hipps.launch", "-n", "2", str(bad)], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 3
