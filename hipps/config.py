@@ -41,6 +41,9 @@ class PSConfig:
     average: bool = False
     # encode buckets from post-accumulate-grad hooks on a side stream during backward
     overlap: bool = True
+    # GPU distributed modes: gather autograd-owned grads per bucket with one multi-tensor kernel
+    # instead of accumulating into preset flat-buffer views (161 fewer kernels for ResNet-50)
+    grad_gather: bool = True
     # published-parameter wire dtype for PS modes: 'fp32' | 'bf16'
     param_wire: str = "fp32"
     # host pickle slow path compression level (mpi_comms.py:18; 0 = framing only)

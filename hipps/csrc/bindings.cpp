@@ -5,6 +5,7 @@ namespace hipps {
 // flat.hip
 void aggregate(const std::vector<at::Tensor>& slots, at::Tensor acc, double gscale, bool accumulate);
 void convert(at::Tensor src, at::Tensor dst, double scale);
+void gather_flat(const std::vector<at::Tensor>& srcs, at::Tensor table, at::Tensor dst, double scale);
 void sgd_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p, c10::optional<at::Tensor> buf,
               c10::optional<at::Tensor> pub, bool zero_src, double lr, double wd, double momentum, double dampening,
               bool nesterov, bool first);
@@ -44,6 +45,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hipps native kernels (gfx950) and parameter-server runtime";
   m.def("aggregate", &hipps::aggregate, "acc (+)= gscale * sum_w slots[w] (rank order)");
   m.def("convert", &hipps::convert, "dst = scale * src with f32/bf16 conversion");
+  m.def("gather_flat", &hipps::gather_flat, "multi-tensor gather (+cast) of grads into a flat buffer");
   m.def("sgd_step", &hipps::sgd_step, "fused decode+sum+SGD (reference ps.py:197-214 math)");
   m.def("adam_step", &hipps::adam_step, "fused decode+sum+Adam (reference ps.py:217-261 math)");
   m.def("q8_encode", &hipps::q8_encode, "per-256-block absmax int8 quantization (+EF, +stochastic)");

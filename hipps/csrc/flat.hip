@@ -200,6 +200,37 @@ __global__ __launch_bounds__(kBlock) void k_adam(SlotPtrs g, int W, float gscale
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// k_gather: multi-tensor gather of autograd-owned gradient tensors into a flat destination
+// (fp32 flat gradient or a dense bf16/fp32 wire image), one launch per bucket instead of one
+// accumulate kernel per parameter.  Source pointers travel in the kernel arguments (<= 256
+// tensors per launch); the chunk table (tensor, src offset, dst offset, length) is static and
+// device-resident.
+// ------------------------------------------------------------------------------------------
+constexpr int kGatherMax = 256;
+struct GatherPtrs {
+  const float* p[kGatherMax];
+};
+
+template <typename Tout>
+__global__ __launch_bounds__(kBlock) void k_gather(GatherPtrs src, const int64_t* __restrict__ table, int64_t nchunks,
+                                                   Tout* __restrict__ dst, float scale) {
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t* row = table + c * 4;
+    const float* s = src.p[row[0]] + row[1];
+    Tout* d = dst + row[2];
+    const int64_t len = row[3];
+    const bool vec = ((reinterpret_cast<uintptr_t>(s) & 15) == 0);
+    const int64_t nv = vec ? (len >> 2) : 0;
+    for (int64_t v = threadIdx.x; v < nv; v += blockDim.x) {
+      float4 x = Vec4<float>::load(s, v << 2);
+      if (scale != 1.f) { x.x *= scale; x.y *= scale; x.z *= scale; x.w *= scale; }
+      Vec4<Tout>::store(d, v << 2, x);
+    }
+    for (int64_t i = (nv << 2) + threadIdx.x; i < len; i += blockDim.x) Vec4<Tout>::store1(d, i, s[i] * scale);
+  }
+}
+
 // ==========================================================================================
 // host launchers
 // ==========================================================================================
@@ -278,6 +309,29 @@ void convert(at::Tensor src, at::Tensor dst, double scale) {
   else
     hipLaunchKernelGGL((k_convert<uint16_t, uint16_t>), grid, kBlock, 0, stream, (const uint16_t*)src.data_ptr(),
                        (uint16_t*)dst.data_ptr(), n, sc);
+}
+
+void gather_flat(const std::vector<at::Tensor>& srcs, at::Tensor table, at::Tensor dst, double scale) {
+  TORCH_CHECK(!srcs.empty() && (int)srcs.size() <= kGatherMax, "1..256 source tensors per gather");
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kLong && table.dim() == 2 && table.size(1) == 4,
+              "table must be a device int64 [nchunks, 4]");
+  check_dev(dst, "dst");
+  GatherPtrs p{};
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    TORCH_CHECK(srcs[i].is_cuda() && srcs[i].scalar_type() == at::kFloat, "gather sources must be f32 device tensors");
+    TORCH_CHECK(srcs[i].is_non_overlapping_and_dense(), "gather source must be dense");
+    p.p[i] = srcs[i].data_ptr<float>();
+  }
+  const int64_t nchunks = table.size(0);
+  if (nchunks == 0) return;
+  auto stream = c10::hip::getCurrentHIPStream();
+  const int grid = (int)std::min<int64_t>(nchunks, kMaxGrid);
+  if (wire_of(dst) == WireT::F32)
+    hipLaunchKernelGGL(k_gather<float>, grid, kBlock, 0, stream, p, table.data_ptr<int64_t>(), nchunks,
+                       dst.data_ptr<float>(), (float)scale);
+  else
+    hipLaunchKernelGGL(k_gather<uint16_t>, grid, kBlock, 0, stream, p, table.data_ptr<int64_t>(), nchunks,
+                       (uint16_t*)dst.data_ptr(), (float)scale);
 }
 
 void sgd_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p, c10::optional<at::Tensor> buf,

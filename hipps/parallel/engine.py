@@ -36,7 +36,8 @@ class Engine:
         self.world = world
         self.plan = BucketPlan(store, codec, int(cfg.bucket_mb * (1 << 20)))
         self.cuda = store.device.type == "cuda"
-        self.wire = self.plan.new_wire()
+        # zero-initialised: the 16-element alignment gaps between parameters are never written
+        self.wire = torch.zeros(self.plan.wire_nbytes, dtype=torch.uint8, device=store.device)
         self.codec_state = [codec.init_state(b.numel, store.device) for b in self.plan.buckets]
         self.comm_stream = torch.cuda.Stream(device=store.device) if self.cuda else None
         self._encoded = [False] * len(self.plan.buckets)
@@ -44,8 +45,39 @@ class Engine:
         self._hooks = []
         self.steps = 0
         self._order_log: List[str] = []
+        # 'gather': autograd keeps ownership of p.grad (stolen, no per-parameter accumulate kernel,
+        # no memset) and each bucket is gathered by ONE multi-tensor kernel; 'flat': p.grad are
+        # views of the flat gradient buffer.
+        self.grad_mode = "gather" if (self.cuda and cfg.grad_gather and self.supports_gather) else "flat"
+        if self.grad_mode == "gather":
+            self._build_gather_plan()
+            store.set_grad_mode("gather")
         if cfg.overlap:
             self._register_hooks()
+
+    supports_gather = True
+    GATHER_CHUNK = 8192
+    GATHER_MAX = 256
+
+    def _build_gather_plan(self):
+        """Static per-bucket chunk tables: (tensor index, src offset, dst offset, length)."""
+        dev = self.store.device
+        self._gplan = []
+        zmax = 0
+        for b in self.plan.buckets:
+            groups = []
+            ids = list(b.slot_ids)
+            for g0 in range(0, len(ids), self.GATHER_MAX):
+                gids = ids[g0:g0 + self.GATHER_MAX]
+                rows = []
+                for ti, si in enumerate(gids):
+                    s = self.store.slots[si]
+                    zmax = max(zmax, s.numel)
+                    for off in range(0, s.numel, self.GATHER_CHUNK):
+                        rows.append((ti, off, s.offset - b.lo + off, min(self.GATHER_CHUNK, s.numel - off)))
+                groups.append((gids, torch.tensor(rows, dtype=torch.int64, device=dev).view(-1, 4)))
+            self._gplan.append(groups)
+        self._zeros = torch.zeros(zmax, dtype=self.store.dtype, device=dev)
 
     # ------------------------------------------------------------------ hooks / encode
     def _register_hooks(self):
@@ -64,6 +96,27 @@ class Engine:
             h.remove()
         self._hooks = []
 
+    def _gather_bucket(self, bi: int, views):
+        """Multi-tensor gather of this bucket's autograd gradients (on the comm stream)."""
+        from hipps.ops._native import native
+
+        b = self.plan.buckets[bi]
+        dense = self.codec.fusable
+        dst = views["x"] if dense else self.store.grad[b.lo:b.hi]
+        C = native()
+        for gids, table in self._gplan[bi]:
+            srcs = []
+            for si in gids:
+                p = self.store.slots[si].param
+                g = p.grad
+                if g is None or g.dtype != torch.float32 or not g.is_non_overlapping_and_dense():
+                    g = self._zeros if g is None else g.float().contiguous()
+                else:
+                    g.record_stream(self.comm_stream)  # keep it alive until the gather ran
+                srcs.append(g)
+            C.gather_flat(srcs, table, dst, 1.0)
+        return dense
+
     def encode_bucket(self, bi: int):
         b = self.plan.buckets[bi]
         g = self.store.grad[b.lo:b.hi]
@@ -73,7 +126,10 @@ class Engine:
             ev.record(torch.cuda.current_stream(self.store.device))
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
-                self.codec.encode_into(g, views, self.codec_state[bi])
+                if self.grad_mode == "gather" and self._gather_bucket(bi, views):
+                    pass  # dense codec: the gather already wrote the wire image
+                else:
+                    self.codec.encode_into(g, views, self.codec_state[bi])
         else:
             self.codec.encode_into(g, views, self.codec_state[bi])
         self._encoded[bi] = True
@@ -83,7 +139,8 @@ class Engine:
     def encode_all(self):
         """Encode every bucket not yet handled by a hook; returns host seconds spent."""
         t = time.perf_counter()
-        self.store.attach_grads()
+        if self.grad_mode == "flat":
+            self.store.attach_grads()
         for bi in self.plan.ready_order:
             if not self._encoded[bi]:
                 self.encode_bucket(bi)
@@ -155,6 +212,7 @@ class LocalEngine(Engine):
     """World size 1: encode (codec round trip, e.g. to study compression) + fused update."""
 
     name = "local"
+    supports_gather = False  # the fused update reads the flat gradient directly
 
     def __init__(self, *a, **k):
         super().__init__(*a, **k)

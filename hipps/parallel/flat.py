@@ -75,6 +75,7 @@ class FlatStore:
         self.dtype = dtype
         self.data = torch.zeros(self.numel, dtype=dtype, device=self.device)
         self.grad = torch.zeros(self.numel, dtype=dtype, device=self.device)
+        self.grad_mode = "flat"
         for s in self.slots:
             p = s.param
             if p.dtype != dtype:
@@ -99,8 +100,19 @@ class FlatStore:
         s = self.slots[i]
         return self._view(buf, s, s.param)
 
+    def set_grad_mode(self, mode: str):
+        """'flat': p.grad are views of self.grad; 'gather': autograd owns p.grad (engines gather)."""
+        self.grad_mode = mode
+        if mode == "gather":
+            for s in self.slots:
+                s.param.grad = None
+        else:
+            self.attach_grads()
+
     def attach_grads(self):
         """(Re)point every ``param.grad`` at its flat slice, salvaging foreign grads."""
+        if self.grad_mode == "gather":
+            return
         for s in self.slots:
             p = s.param
             v = self._view(self.grad, s, p.data)
@@ -115,6 +127,10 @@ class FlatStore:
                    self.grad[s.offset:].data_ptr() for s in self.slots)
 
     def zero_grad(self):
+        if self.grad_mode == "gather":
+            for s in self.slots:  # let autograd steal fresh gradients (no memset, no += kernels)
+                s.param.grad = None
+            return
         self.grad.zero_()
         self.attach_grads()
 

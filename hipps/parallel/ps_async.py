@@ -314,8 +314,9 @@ class PSAsyncEngine(Engine):
             raise RuntimeError(msg)
 
     def before_zero_grad(self):
-        # the side-stream encode reads the flat grads: do not zero them under it
-        if self.cuda and self.enc_event is not None:
+        # the side-stream encode reads the flat grads: do not zero them under it (gather mode
+        # keeps autograd's tensors alive through record_stream instead)
+        if self.cuda and self.enc_event is not None and self.grad_mode == "flat":
             torch.cuda.current_stream(self.store.device).wait_event(self.enc_event)
 
     def step(self):

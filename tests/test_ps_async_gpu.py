@@ -93,3 +93,30 @@ def _gpu_resnet(rank, world):
     eng = opt.engine
     opt.close()
     return eng.ps_stats()
+
+
+def _gpu_sync(rank, world, mode, codec):
+    import hipps
+
+    torch.cuda.set_device(0)
+    m = _mlp().cuda()
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode=mode, code=codec)
+    for s in range(4):
+        x, y = _data(rank, s)
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x.cuda()), y.cuda()).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    grad_mode = opt.engine.grad_mode
+    opt.close()
+    return [p.detach().cpu() for p in m.parameters()], grad_mode
+
+
+@pytest.mark.parametrize("mode,codec", [("allgather", "bf16"), ("allgather", "topk:0.1"), ("ps_sync", "fp32")])
+def test_gpu_sync_engines_replicas_identical(mode, codec):
+    """Sync engines on the GPU path (multi-tensor grad gather + fused decode/update), 2 ranks on
+    one device with gloo carrying the device buffers."""
+    out = run_world(_gpu_sync, 2, mode, codec, timeout=300)
+    assert out[0][1] == "gather"
+    for a, b in zip(out[0][0], out[1][0]):
+        assert torch.equal(a, b)
