@@ -22,7 +22,7 @@ from typing import Dict, List, Optional
 import torch
 
 from .dist import World, all_gather_into, barrier, broadcast, gather_into
-from .flat import BucketPlan, FlatStore
+from .flat import BucketPlan, FlatStore, _is_dense
 
 
 class Engine:
@@ -109,7 +109,7 @@ class Engine:
             for si in gids:
                 p = self.store.slots[si].param
                 g = p.grad
-                if g is None or g.dtype != torch.float32 or not g.is_non_overlapping_and_dense():
+                if g is None or g.dtype != torch.float32 or not _is_dense(g):
                     g = self._zeros if g is None else g.float().contiguous()
                 else:
                     g.record_stream(self.comm_stream)  # keep it alive until the gather ran
