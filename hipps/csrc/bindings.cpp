@@ -29,12 +29,13 @@ void topk_q8_residual(at::Tensor idx, at::Tensor v, at::Tensor q, at::Tensor sca
 void bn_forward_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, at::Tensor weight, at::Tensor bias,
                       c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var, at::Tensor mean,
                       at::Tensor invstd, at::Tensor scale, at::Tensor shift, int64_t C, double eps, double momentum,
-                      bool relu);
+                      bool relu, c10::optional<at::Tensor> mask_out);
 void bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, at::Tensor scale, at::Tensor shift, int64_t C,
               bool relu);
 void bn_backward(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> y, int64_t mask_mode, at::Tensor weight,
                  at::Tensor mean, at::Tensor invstd, at::Tensor scale, at::Tensor shift, at::Tensor dx,
-                 c10::optional<at::Tensor> dres, at::Tensor dweight, at::Tensor dbias, int64_t C);
+                 c10::optional<at::Tensor> dres, at::Tensor dweight, at::Tensor dbias, int64_t C,
+                 c10::optional<at::Tensor> mask_in);
 namespace rt {
 void bind_control(pybind11::module& m);
 void bind_ipc(pybind11::module& m);

@@ -45,15 +45,17 @@ __device__ __forceinline__ void load8f(const float* p, float v[8]) {
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
-enum MaskMode { MASK_NONE = 0, MASK_X = 1, MASK_Y = 2 };
+enum MaskMode { MASK_NONE = 0, MASK_X = 1, MASK_Y = 2, MASK_BITS = 3 };
+// MASK_BITS: the forward wrote one byte per 8 channels (bit j = output channel c0+j > 0); the
+// backward reads 1/16 of the bytes that re-reading the bf16 output (MASK_Y) would cost.
 
 // ---- per-channel reductions -> partial[c][rb] (channel-major, two arrays) ------------------
 // FWD: a += x, b += x*x.   BWD: dz = dy*mask; a += dz, b += dz*(x-mean)*invstd.
 // Each lane keeps 4 rows (up to 12 x 16 B) in flight before consuming them: one load per
 // iteration left these passes at 3.2-3.9 TB/s (profiles/bench_n1_steady_fusedbn.txt).
 template <bool BWD>
-__device__ __forceinline__ void reduce_row(const float xv[8], const float* d, const float* yv, int mask_mode,
-                                           const float mu[8], const float is[8], const float sc[8],
+__device__ __forceinline__ void reduce_row(const float xv[8], const float* d, const float* yv, uint32_t mb,
+                                           int mask_mode, const float mu[8], const float is[8], const float sc[8],
                                            const float sh[8], float sa[8], float sb[8]) {
   if (!BWD) {
 #pragma unroll
@@ -62,7 +64,8 @@ __device__ __forceinline__ void reduce_row(const float xv[8], const float* d, co
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float dz = d[j];
-      if (mask_mode == MASK_Y) dz = yv[j] > 0.f ? dz : 0.f;
+      if (mask_mode == MASK_BITS) dz = ((mb >> j) & 1u) ? dz : 0.f;
+      else if (mask_mode == MASK_Y) dz = yv[j] > 0.f ? dz : 0.f;
       else if (mask_mode == MASK_X) dz = fmaf(xv[j], sc[j], sh[j]) > 0.f ? dz : 0.f;
       sa[j] += dz;
       sb[j] = fmaf(dz, (xv[j] - mu[j]) * is[j], sb[j]);
@@ -72,7 +75,8 @@ __device__ __forceinline__ void reduce_row(const float xv[8], const float* d, co
 
 template <bool BWD>
 __global__ __launch_bounds__(kBlock) void k_bn_reduce(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
-                                                      const uint16_t* __restrict__ y, int mask_mode,
+                                                      const uint16_t* __restrict__ y,
+                                                      const uint8_t* __restrict__ mbits, int mask_mode,
                                                       const float* __restrict__ mean, const float* __restrict__ invstd,
                                                       const float* __restrict__ scale, const float* __restrict__ shift,
                                                       int64_t M, int C, int64_t rows_per_wg, int nrb,
@@ -90,20 +94,24 @@ __global__ __launch_bounds__(kBlock) void k_bn_reduce(const uint16_t* __restrict
     if (mask_mode == MASK_X) { load8f(scale + c0, sc); load8f(shift + c0, sh); }
   }
   const bool need_y = BWD && mask_mode == MASK_Y;
+  const bool need_b = BWD && mask_mode == MASK_BITS;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_wg;
   const int64_t r1 = min(M, r0 + rows_per_wg);
   int64_t row = r0 + r;
   for (; row + 3 * (int64_t)R < r1; row += 4 * (int64_t)R) {
     float xv[4][8], d[4][8], yv[4][8];
+    uint32_t mb[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int64_t off = (row + u * (int64_t)R) * C + c0;
+      const int64_t rr = row + u * (int64_t)R;
+      const int64_t off = rr * C + c0;
       load8(x + off, xv[u]);
       if (BWD) load8(dy + off, d[u]);
       if (need_y) load8(y + off, yv[u]);
+      if (need_b) mb[u] = mbits[rr * G + g];
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) reduce_row<BWD>(xv[u], d[u], yv[u], mask_mode, mu, is, sc, sh, sa, sb);
+    for (int u = 0; u < 4; ++u) reduce_row<BWD>(xv[u], d[u], yv[u], mb[u], mask_mode, mu, is, sc, sh, sa, sb);
   }
   for (; row < r1; row += R) {
     const int64_t off = row * C + c0;
@@ -111,7 +119,8 @@ __global__ __launch_bounds__(kBlock) void k_bn_reduce(const uint16_t* __restrict
     load8(x + off, xv);
     if (BWD) load8(dy + off, d);
     if (need_y) load8(y + off, yv);
-    reduce_row<BWD>(xv, d, yv, mask_mode, mu, is, sc, sh, sa, sb);
+    const uint32_t mb = need_b ? (uint32_t)mbits[row * G + g] : 0u;
+    reduce_row<BWD>(xv, d, yv, mb, mask_mode, mu, is, sc, sh, sa, sb);
   }
   // combine the R row lanes of each channel group through LDS
 #pragma unroll
@@ -199,7 +208,8 @@ __global__ __launch_bounds__(kBlock) void k_bn_finalize_bwd(const float* __restr
 
 // y = act(x*scale + shift [+ res])
 __global__ __launch_bounds__(kBlock) void k_bn_apply_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
-                                                         uint16_t* __restrict__ y, const float* __restrict__ scale,
+                                                         uint16_t* __restrict__ y, uint8_t* __restrict__ mbits,
+                                                         const float* __restrict__ scale,
                                                          const float* __restrict__ shift, int64_t M, int C, int relu) {
   const int G = C >> 3;
   const int64_t V = M * (int64_t)G, stride = (int64_t)gridDim.x * blockDim.x;
@@ -225,12 +235,19 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_fwd(const uint16_t* __restr
       for (int j = 0; j < 8; ++j) xv[j] = fmaxf(xv[j], 0.f);
     }
     store8(y + off, xv);
+    if (mbits) {
+      uint32_t b = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b |= (xv[j] > 0.f ? 1u : 0u) << j;
+      mbits[v] = (uint8_t)b;
+    }
   }
 }
 
 // dx = a*dz + k1*x + k0, dz = dy * mask;  dres = dz (when a residual was fused)
 __global__ __launch_bounds__(kBlock) void k_bn_apply_bwd(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
-                                                         const uint16_t* __restrict__ y, int mask_mode,
+                                                         const uint16_t* __restrict__ y,
+                                                         const uint8_t* __restrict__ mbits, int mask_mode,
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ shift, const float* __restrict__ ca,
                                                          const float* __restrict__ ck1, const float* __restrict__ ck0,
@@ -247,12 +264,13 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_bwd(const uint16_t* __restr
   load8f(ck1 + c0, k1);
   load8f(ck0 + c0, k0);
   if (mask_mode == MASK_X) { load8f(scale + c0, sc); load8f(shift + c0, sh); }
-  auto body = [&](const float* d_in, const float* xv, const float* yv, int64_t off) {
+  auto body = [&](const float* d_in, const float* xv, const float* yv, uint32_t mb, int64_t off) {
     float d[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float dz = d_in[j];
-      if (mask_mode == MASK_Y) dz = yv[j] > 0.f ? dz : 0.f;
+      if (mask_mode == MASK_BITS) dz = ((mb >> j) & 1u) ? dz : 0.f;
+      else if (mask_mode == MASK_Y) dz = yv[j] > 0.f ? dz : 0.f;
       else if (mask_mode == MASK_X) dz = fmaf(xv[j], sc[j], sh[j]) > 0.f ? dz : 0.f;
       d[j] = dz;
     }
@@ -262,7 +280,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_bwd(const uint16_t* __restr
     for (int j = 0; j < 8; ++j) o[j] = fmaf(a[j], d[j], fmaf(k1[j], xv[j], k0[j]));
     store8(dx + off, o);
   };
-  const bool need_y = mask_mode == MASK_Y;
+  const bool need_y = mask_mode == MASK_Y, need_b = mask_mode == MASK_BITS;
   int64_t v = v0;
   for (; v + stride < V; v += 2 * stride) {  // two vectors in flight per lane
     float d0[8], x0[8], y0[8], d1[8], x1[8], y1[8];
@@ -272,8 +290,9 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_bwd(const uint16_t* __restr
     load8(dy + o1, d1);
     load8(x + o1, x1);
     if (need_y) { load8(y + o0, y0); load8(y + o1, y1); }
-    body(d0, x0, y0, o0);
-    body(d1, x1, y1, o1);
+    const uint32_t m0 = need_b ? (uint32_t)mbits[v] : 0u, m1 = need_b ? (uint32_t)mbits[v + stride] : 0u;
+    body(d0, x0, y0, m0, o0);
+    body(d1, x1, y1, m1, o1);
   }
   for (; v < V; v += stride) {
     float d0[8], x0[8], y0[8];
@@ -281,7 +300,8 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_bwd(const uint16_t* __restr
     load8(dy + o0, d0);
     load8(x + o0, x0);
     if (need_y) load8(y + o0, y0);
-    body(d0, x0, y0, o0);
+    const uint32_t m0 = need_b ? (uint32_t)mbits[v] : 0u;
+    body(d0, x0, y0, m0, o0);
   }
 }
 
@@ -317,7 +337,7 @@ int apply_grid(int64_t M, int C) {
 void bn_forward_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, at::Tensor weight, at::Tensor bias,
                       c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var, at::Tensor mean,
                       at::Tensor invstd, at::Tensor scale, at::Tensor shift, int64_t C, double eps, double momentum,
-                      bool relu) {
+                      bool relu, c10::optional<at::Tensor> mask_out) {
   TORCH_CHECK(C % 8 == 0 && C <= kMaxC && C >= 8, "fused BN needs C % 8 == 0 and 8 <= C <= 2048");
   const int64_t M = x.numel() / C;
   check_act(x, "x", M * C);
@@ -340,15 +360,22 @@ void bn_forward_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y,
   const int64_t rows = pick_rows(M, (int)C, nrb);
   auto part = at::empty({2, C, (int64_t)nrb}, weight.options());
   auto stream = c10::hip::getCurrentHIPStream();
-  hipLaunchKernelGGL(k_bn_reduce<false>, nrb, kBlock, 0, stream, (const uint16_t*)x.data_ptr(), nullptr, nullptr, 0,
-                     nullptr, nullptr, nullptr, nullptr, M, (int)C, rows, nrb, part[0].data_ptr<float>(),
+  uint8_t* mo = nullptr;
+  if (mask_out.has_value() && mask_out->defined()) {
+    TORCH_CHECK(mask_out->is_cuda() && mask_out->scalar_type() == at::kByte && mask_out->numel() == M * C / 8,
+                "mask_out must be uint8[M*C/8]");
+    mo = (uint8_t*)mask_out->data_ptr();
+  }
+  hipLaunchKernelGGL(k_bn_reduce<false>, nrb, kBlock, 0, stream, (const uint16_t*)x.data_ptr(), nullptr, nullptr,
+                     nullptr, 0, nullptr, nullptr, nullptr, nullptr, M, (int)C, rows, nrb, part[0].data_ptr<float>(),
                      part[1].data_ptr<float>());
   hipLaunchKernelGGL(k_bn_finalize_fwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, part[0].data_ptr<float>(),
                      part[1].data_ptr<float>(), nrb, (int)C, M, weight.data_ptr<float>(), bias.data_ptr<float>(),
                      (float)eps, (float)momentum, rm, rv, mean.data_ptr<float>(), invstd.data_ptr<float>(),
                      scale.data_ptr<float>(), shift.data_ptr<float>());
   hipLaunchKernelGGL(k_bn_apply_fwd, apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)x.data_ptr(), rp,
-                     (uint16_t*)y.data_ptr(), scale.data_ptr<float>(), shift.data_ptr<float>(), M, (int)C, (int)relu);
+                     (uint16_t*)y.data_ptr(), mo, scale.data_ptr<float>(), shift.data_ptr<float>(), M, (int)C,
+                     (int)relu);
 }
 
 // eval / affine-only apply with given scale/shift
@@ -366,14 +393,15 @@ void bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, at::Ten
   check_vec(scale, "scale", (int)C);
   check_vec(shift, "shift", (int)C);
   hipLaunchKernelGGL(k_bn_apply_fwd, apply_grid(M, (int)C), kBlock, 0, c10::hip::getCurrentHIPStream(),
-                     (const uint16_t*)x.data_ptr(), rp, (uint16_t*)y.data_ptr(), scale.data_ptr<float>(),
+                     (const uint16_t*)x.data_ptr(), rp, (uint16_t*)y.data_ptr(), nullptr, scale.data_ptr<float>(),
                      shift.data_ptr<float>(), M, (int)C, (int)relu);
 }
 
 // returns nothing; writes dx (and dres), dweight, dbias
 void bn_backward(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> y, int64_t mask_mode, at::Tensor weight,
                  at::Tensor mean, at::Tensor invstd, at::Tensor scale, at::Tensor shift, at::Tensor dx,
-                 c10::optional<at::Tensor> dres, at::Tensor dweight, at::Tensor dbias, int64_t C) {
+                 c10::optional<at::Tensor> dres, at::Tensor dweight, at::Tensor dbias, int64_t C,
+                 c10::optional<at::Tensor> mask_in) {
   TORCH_CHECK(C % 8 == 0 && C <= kMaxC, "fused BN needs C % 8 == 0 and C <= 2048");
   const int64_t M = x.numel() / C;
   check_act(dy, "dy", M * C);
@@ -384,6 +412,12 @@ void bn_backward(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> y, int64
     TORCH_CHECK(y.has_value() && y->defined(), "mask from y needs y");
     check_act(*y, "y", M * C);
     yp = (const uint16_t*)y->data_ptr();
+  }
+  const uint8_t* mbp = nullptr;
+  if (mask_mode == MASK_BITS) {
+    TORCH_CHECK(mask_in.has_value() && mask_in->defined() && mask_in->scalar_type() == at::kByte &&
+                    mask_in->numel() == M * C / 8, "MASK_BITS needs a uint8[M*C/8] mask");
+    mbp = (const uint8_t*)mask_in->data_ptr();
   }
   uint16_t* drp = nullptr;
   if (dres.has_value() && dres->defined()) {
@@ -397,7 +431,7 @@ void bn_backward(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> y, int64
   auto coef = at::empty({3, C}, weight.options());
   auto stream = c10::hip::getCurrentHIPStream();
   hipLaunchKernelGGL(k_bn_reduce<true>, nrb, kBlock, 0, stream, (const uint16_t*)x.data_ptr(),
-                     (const uint16_t*)dy.data_ptr(), yp, (int)mask_mode, mean.data_ptr<float>(),
+                     (const uint16_t*)dy.data_ptr(), yp, mbp, (int)mask_mode, mean.data_ptr<float>(),
                      invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(), M, (int)C, rows, nrb,
                      part[0].data_ptr<float>(), part[1].data_ptr<float>());
   hipLaunchKernelGGL(k_bn_finalize_bwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, part[0].data_ptr<float>(),
@@ -405,7 +439,7 @@ void bn_backward(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> y, int64
                      invstd.data_ptr<float>(), dweight.data_ptr<float>(), dbias.data_ptr<float>(),
                      coef[0].data_ptr<float>(), coef[1].data_ptr<float>(), coef[2].data_ptr<float>());
   hipLaunchKernelGGL(k_bn_apply_bwd, apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)dy.data_ptr(),
-                     (const uint16_t*)x.data_ptr(), yp, (int)mask_mode, scale.data_ptr<float>(),
+                     (const uint16_t*)x.data_ptr(), yp, mbp, (int)mask_mode, scale.data_ptr<float>(),
                      shift.data_ptr<float>(), coef[0].data_ptr<float>(), coef[1].data_ptr<float>(),
                      coef[2].data_ptr<float>(), (uint16_t*)dx.data_ptr(), drp, M, (int)C);
 }

@@ -15,7 +15,7 @@ import torch.nn.functional as F
 
 from ._native import native
 
-MASK_NONE, MASK_X, MASK_Y = 0, 1, 2
+MASK_NONE, MASK_X, MASK_Y, MASK_BITS = 0, 1, 2, 3
 
 
 class _FusedBNAct(torch.autograd.Function):
@@ -26,22 +26,25 @@ class _FusedBNAct(torch.autograd.Function):
         f32 = dict(dtype=torch.float32, device=x.device)
         mean, invstd = torch.empty(C, **f32), torch.empty(C, **f32)
         scale, shift = torch.empty(C, **f32), torch.empty(C, **f32)
+        # relu(bn(x) + res): the mask depends on res, so keep 1 bit per element instead of
+        # re-reading the bf16 output in the backward
+        mode = MASK_NONE if not relu else (MASK_BITS if res is not None else MASK_X)
+        mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device) if mode == MASK_BITS else None
         native().bn_forward_train(x, res, y, weight, bias, running_mean, running_var, mean, invstd, scale, shift, C,
-                                  float(eps), float(momentum), bool(relu))
-        mode = MASK_NONE if not relu else (MASK_Y if res is not None else MASK_X)
+                                  float(eps), float(momentum), bool(relu), mask)
         ctx.mode, ctx.C, ctx.has_res = mode, C, res is not None
-        ctx.save_for_backward(x, y if mode == MASK_Y else None, weight, mean, invstd, scale, shift)
+        ctx.save_for_backward(x, mask, weight, mean, invstd, scale, shift)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, weight, mean, invstd, scale, shift = ctx.saved_tensors
+        x, mask, weight, mean, invstd, scale, shift = ctx.saved_tensors
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
         dw = torch.empty_like(weight)
         db = torch.empty_like(weight)
-        native().bn_backward(dy, x, y, ctx.mode, weight, mean, invstd, scale, shift, dx, dres, dw, db, ctx.C)
+        native().bn_backward(dy, x, None, ctx.mode, weight, mean, invstd, scale, shift, dx, dres, dw, db, ctx.C, mask)
         return dx, dres, dw, db, None, None, None, None, None
 
 
