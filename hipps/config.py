@@ -35,7 +35,10 @@ class PSConfig:
     pull: str = "prefetch"
     # async PS failure detection: a worker silent for this long (no heartbeat, no STOP) is dead
     dead_after_s: float = 60.0
-    # bucket size for hook-driven encode overlap
+    # async PS mailbox: bucket messages in flight per worker (0 = auto: min(2*buckets, mailbox_mb))
+    mailbox_slots: int = 0
+    mailbox_mb: float = 4096.0
+    # bucket size for hook-driven encode overlap (also the async PS message granularity)
     bucket_mb: float = 64.0
     # scale the rank-summed gradient by 1/accumulate (reference sums: ps.py:176)
     average: bool = False

@@ -38,7 +38,7 @@ namespace rt {
 
 constexpr int64_t kMagic = 0x5350504948ll;  // "HIPPS"
 constexpr int kMaxRanks = 64;
-constexpr int kSlots = 2;  // mailbox slots per worker
+constexpr int kSlots = 64;  // max mailbox slots per worker (bucket messages in flight)
 constexpr int kPub = 3;    // published parameter buffers
 
 struct alignas(64) RankRec {
@@ -180,16 +180,29 @@ class ControlBlock {
   struct StorePayload {
     std::atomic<int64_t>* w;
     int64_t v;
+    std::atomic<int64_t>* w2;  // optional second word, stored after the first
+    int64_t v2;
   };
   static void store_cb(void* arg) {
     auto* p = reinterpret_cast<StorePayload*>(arg);
     p->w->store(p->v, std::memory_order_release);
+    if (p->w2) p->w2->store(p->v2, std::memory_order_release);
     delete p;
   }
 
   // Stream-ordered doorbell: runs after every earlier operation on `stream` has completed.
   void enqueue_store(uint64_t stream, int field, int idx, int64_t value) {
-    auto* p = new StorePayload{word(field, idx), value};
+    auto* p = new StorePayload{word(field, idx), value, nullptr, 0};
+    hipError_t e = hipLaunchHostFunc(reinterpret_cast<hipStream_t>(stream), &ControlBlock::store_cb, p);
+    if (e != hipSuccess) {
+      delete p;
+      throw std::runtime_error(std::string("hipLaunchHostFunc failed: ") + hipGetErrorString(e));
+    }
+  }
+
+  // Two ordered doorbells in one callback (e.g. slot version, then the sequence word).
+  void enqueue_store2(uint64_t stream, int f1, int i1, int64_t v1, int f2, int i2, int64_t v2) {
+    auto* p = new StorePayload{word(f1, i1), v1, word(f2, i2), v2};
     hipError_t e = hipLaunchHostFunc(reinterpret_cast<hipStream_t>(stream), &ControlBlock::store_cb, p);
     if (e != hipSuccess) {
       delete p;
@@ -222,6 +235,7 @@ void bind_control(py::module& m) {
       .def("wait_any", &ControlBlock::wait_any)
       .def("wait_ge", &ControlBlock::wait_ge)
       .def("enqueue_store", &ControlBlock::enqueue_store)
+      .def("enqueue_store2", &ControlBlock::enqueue_store2)
       .def("heartbeat", &ControlBlock::heartbeat)
       .def_property_readonly("world", &ControlBlock::world)
       .def_property_readonly_static("SLOTS", [](py::object) { return kSlots; })

@@ -86,11 +86,18 @@ class PSAsyncEngine(Engine):
         self.W = W
         self.rank = world.rank
         self.M = cfg.accumulate if cfg.accumulate > 0 else W
-        self.SLOTS = C.ControlBlock.SLOTS
+        self.MAXSLOTS = C.ControlBlock.SLOTS  # stride of the per-slot version words
         self.NPUB = C.ControlBlock.NPUB
         self.pub_dtype = torch.bfloat16 if cfg.param_wire == "bf16" else torch.float32
         esz = torch.empty((), dtype=self.pub_dtype).element_size()
-        self.slot_bytes = _align(self.plan.wire_nbytes)
+        # messages are BUCKETS, streamed in ready order; a worker's mailbox holds K of them, so the
+        # PS memory is W*K*max_bucket instead of W*2*model (Llama-3-8B: 8x4x512 MB vs 8x2x16 GB)
+        self.nb = len(self.plan.buckets)
+        self.order = list(self.plan.ready_order)
+        self.slot_bytes = _align(max(b.layout.nbytes for b in self.plan.buckets))
+        K = cfg.mailbox_slots if cfg.mailbox_slots > 0 else min(
+            2 * self.nb, max(2, int(cfg.mailbox_mb * (1 << 20)) // self.slot_bytes))
+        self.SLOTS = max(1, min(K, self.MAXSLOTS))
         self.pub_bytes = _align(store.numel * esz)
         self.mail_off = 0
         self.pub_off = W * self.SLOTS * self.slot_bytes
@@ -127,6 +134,7 @@ class PSAsyncEngine(Engine):
 
         # ---- PS state on rank 0 ------------------------------------------------------------
         self.seq = 0
+        self.step_no = 0
         self.local_ver = -1
         self._stats = {"drops": 0, "staleness_sum": 0, "accumulated": 0}
         self._err: Optional[str] = None
@@ -155,7 +163,7 @@ class PSAsyncEngine(Engine):
         training later."""
         W, dev = self.W, self.store.device
         tag = torch.full((16,), (self.rank * 7 + 3) % 251, dtype=torch.uint8, device=dev)
-        dst = self.slot_buf(self.rank, 1)[:16]
+        dst = self.slot_buf(self.rank, self.SLOTS - 1)[:16]
         if self.cuda:
             with torch.cuda.stream(self.comm_stream):
                 dst.copy_(tag, non_blocking=True)
@@ -166,7 +174,7 @@ class PSAsyncEngine(Engine):
         ok = True
         if self.rank == 0:
             for r in range(W):
-                got = self.slot_buf(r, 1)[:16].cpu()
+                got = self.slot_buf(r, self.SLOTS - 1)[:16].cpu()
                 ok &= bool((got == (r * 7 + 3) % 251).all())
             ck = float(self.pub_buf(0).double().sum())  # what workers actually receive
         else:
@@ -190,7 +198,11 @@ class PSAsyncEngine(Engine):
     # ------------------------------------------------------------------ memory views
     def slot_buf(self, rank: int, slot: int) -> torch.Tensor:
         o = self.mail_off + (rank * self.SLOTS + slot) * self.slot_bytes
-        return self.mem[o:o + self.plan.wire_nbytes]
+        return self.mem[o:o + self.slot_bytes]
+
+    def _bucket_msg(self, bi: int, buf: torch.Tensor):
+        b = self.plan.buckets[bi]
+        return b.layout.views(buf[: b.layout.nbytes])
 
     def pub_buf(self, b: int) -> torch.Tensor:
         o = self.pub_off + b * self.pub_bytes
@@ -227,9 +239,14 @@ class PSAsyncEngine(Engine):
             self.ctl.store(self.C.F_ERROR, 0, 1)
 
     def _serve(self):
-        C, W = self.C, self.W
+        """PS loop.  Message s of worker i is bucket order[(s-1) % nb] of that worker's step
+        (s-1)//nb + 1; a step's first bucket carries the parameter version it was computed on.
+        Counting is in whole worker-steps (M per update, README.md:65-73); every bucket gradient
+        that has arrived is applied exactly once."""
+        C, W, nb = self.C, self.W, self.nb
         seen = [0] * W
-        pending_incl: List[tuple] = []  # (rank, seq) accumulated since the last update
+        dropping = [False] * W
+        pending_incl: List[tuple] = []  # (rank, last seq of a completed step) since the last update
         count = 0
         gscale = 1.0 / self.M if self.cfg.average else 1.0
         st = self.ps_stream
@@ -240,26 +257,31 @@ class PSAsyncEngine(Engine):
                     s_now = self.ctl.load(C.F_PUSH_SEQ, i)
                     for s in range(seen[i] + 1, s_now + 1):
                         slot = s % self.SLOTS
-                        pv = self.ctl.load(C.F_PUSH_VER, i * self.SLOTS + slot)
-                        stale = self.ver - pv
-                        if 0 <= self.cfg.staleness < stale:
-                            self._stats["drops"] += 1
-                            self.ctl.fetch_add(C.F_DROPS, 0, 1)
-                            self._ring(st, C.F_ACK_SEQ, i, s)  # stream-ordered: acks stay monotonic
-                            pending_incl.append((i, s))  # counts as handled for max_delay
-                            continue
-                        msg = self.slot_buf(i, slot)
-                        for bi, b in enumerate(self.plan.buckets):
-                            self.codec.accumulate([self.plan.views(msg, bi)], self.acc[b.lo:b.hi], 1.0, True)
-                        self._ring(st, C.F_ACK_SEQ, i, s)
-                        pending_incl.append((i, s))
-                        self._stats["accumulated"] += 1
-                        self._stats["staleness_sum"] += max(0, stale)
-                        count += 1
-                        if count >= self.M:
-                            self._update(pending_incl, gscale)
-                            pending_incl = []
-                            count = 0
+                        pos = (s - 1) % nb
+                        bi = self.order[pos]
+                        if pos == 0:
+                            pv = self.ctl.load(C.F_PUSH_VER, i * self.MAXSLOTS + slot)
+                            stale = self.ver - pv
+                            dropping[i] = 0 <= self.cfg.staleness < stale
+                            if not dropping[i]:
+                                self._stats["staleness_sum"] += max(0, stale)
+                        if not dropping[i]:
+                            b = self.plan.buckets[bi]
+                            self.codec.accumulate([self._bucket_msg(bi, self.slot_buf(i, slot))],
+                                                  self.acc[b.lo:b.hi], 1.0, True)
+                        self._ring(st, C.F_ACK_SEQ, i, s)  # stream-ordered: acks stay monotonic
+                        if pos == nb - 1:
+                            pending_incl.append((i, s))  # a dropped step still counts for max_delay
+                            if dropping[i]:
+                                self._stats["drops"] += 1
+                                self.ctl.fetch_add(C.F_DROPS, 0, 1)
+                            else:
+                                self._stats["accumulated"] += 1
+                                count += 1
+                                if count >= self.M:
+                                    self._update(pending_incl, gscale)
+                                    pending_incl = []
+                                    count = 0
                     seen[i] = s_now
                 if self._should_stop(seen):
                     break
@@ -327,28 +349,36 @@ class PSAsyncEngine(Engine):
         if self._fault is not None and self._inject(data):
             return data
         self.ctl.heartbeat(self.rank)
-        self.seq += 1
-        s = self.seq
-        slot = s % self.SLOTS
+        t_wait = 0.0
         t = time.perf_counter()
-        if s > self.SLOTS:  # slot reuse: message s - SLOTS must have been consumed
-            if not self.ctl.wait_ge(C.F_ACK_SEQ, self.rank, s - self.SLOTS, TIMEOUT_US):
-                self._check_error()
-                raise TimeoutError(f"rank {self.rank}: PS did not consume message {s - self.SLOTS}")
-        data["slot_wait"] = time.perf_counter() - t
-        t = time.perf_counter()
-        dst = self.slot_buf(self.rank, slot)
         if self.cuda:
-            cs = self.comm_stream
-            self.enc_event.record(cs)
-            with torch.cuda.stream(cs):
-                dst.copy_(self.wire, non_blocking=True)
-            self._ring(cs, C.F_PUSH_VER, self.rank * self.SLOTS + slot, self.local_ver)
-            self._ring(cs, C.F_PUSH_SEQ, self.rank, s)
-        else:
-            dst.copy_(self.wire)
-            self.ctl.store(C.F_PUSH_VER, self.rank * self.SLOTS + slot, self.local_ver)
-            self.ctl.store(C.F_PUSH_SEQ, self.rank, s)
+            self.enc_event.record(self.comm_stream)
+        for pos, bi in enumerate(self.order):
+            self.seq += 1
+            s = self.seq
+            slot = s % self.SLOTS
+            if s > self.SLOTS:  # slot reuse: message s - SLOTS must have been consumed
+                tw = time.perf_counter()
+                if not self.ctl.wait_ge(C.F_ACK_SEQ, self.rank, s - self.SLOTS, TIMEOUT_US):
+                    self._check_error()
+                    raise TimeoutError(f"rank {self.rank}: PS did not consume message {s - self.SLOTS}")
+                t_wait += time.perf_counter() - tw
+            b = self.plan.buckets[bi]
+            src = self.wire[b.wire_offset:b.wire_offset + b.layout.nbytes]
+            dst = self.slot_buf(self.rank, slot)[: b.layout.nbytes]
+            vidx = self.rank * self.MAXSLOTS + slot
+            if self.cuda:
+                cs = self.comm_stream
+                with torch.cuda.stream(cs):
+                    dst.copy_(src, non_blocking=True)
+                self.ctl.enqueue_store2(cs.cuda_stream, C.F_PUSH_VER, vidx, self.local_ver, C.F_PUSH_SEQ,
+                                        self.rank, s)
+            else:
+                dst.copy_(src)
+                self.ctl.store(C.F_PUSH_VER, vidx, self.local_ver)
+                self.ctl.store(C.F_PUSH_SEQ, self.rank, s)
+        self.step_no += 1
+        data["slot_wait"] = t_wait
         data["isend_time"] = time.perf_counter() - t
         t = time.perf_counter()
         if self.cfg.auto_pull:
@@ -379,8 +409,8 @@ class PSAsyncEngine(Engine):
             if not self.ctl.wait_ge(C.F_PUB_VER, 0, block_for, TIMEOUT_US):
                 self._check_error()
                 raise TimeoutError("no published parameters")
-        if self.cfg.max_delay >= 0 and self.seq - self.cfg.max_delay > 0:
-            need = self.seq - self.cfg.max_delay
+        if self.cfg.max_delay >= 0 and self.step_no - self.cfg.max_delay > 0:
+            need = (self.step_no - self.cfg.max_delay) * self.nb  # last message of that step
             sync = True
             if not self.ctl.wait_ge(C.F_INCL_SEQ, self.rank, need, TIMEOUT_US):
                 self._check_error()
@@ -510,7 +540,7 @@ class PSAsyncEngine(Engine):
         if self.cuda:
             torch.cuda.synchronize(self.store.device)
         d = {"codec_state": [{k: v.detach().cpu() for k, v in st.items() if k != "ws"} for st in self.codec_state],
-             "seq": self.seq, "local_ver": self.local_ver}
+             "seq": self.seq, "step_no": self.step_no, "local_ver": self.local_ver}
         if self.rank == 0:
             self.ps_stream.synchronize() if self.cuda else None
             d.update({"master": self.master.detach().cpu(), "version": self.ver})

@@ -6,7 +6,8 @@ from dist_util import run_world
 from test_dist_cpu import _data, _mlp
 
 
-def _train_async(rank, world, steps, codec, accumulate, max_delay, staleness, opt_name="sgd"):
+def _train_async(rank, world, steps, codec, accumulate, max_delay, staleness, opt_name="sgd", bucket_mb=64.0,
+                 slots=0):
     import hipps
 
     m = _mlp()
@@ -17,7 +18,8 @@ def _train_async(rank, world, steps, codec, accumulate, max_delay, staleness, op
     cls = hipps.SGD if opt_name == "sgd" else hipps.Adam
     kw = dict(lr=0.05, momentum=0.9) if opt_name == "sgd" else dict(lr=1e-3)
     opt = cls(m.named_parameters(), mode="ps_async", code=codec, accumulate=accumulate, max_delay=max_delay,
-              staleness=staleness, **kw)
+              staleness=staleness, bucket_mb=bucket_mb, mailbox_slots=slots, **kw)
+    nb = len(opt.engine.plan.buckets)
     init = [p.detach().clone() for p in m.parameters()]
     losses = []
     for s in range(steps):
@@ -31,18 +33,19 @@ def _train_async(rank, world, steps, codec, accumulate, max_delay, staleness, op
     opt.close()  # drains: the PS thread exits only after consuming every pushed message
     stats = eng.ps_stats()
     master = eng.final_params() if rank == 0 else None
-    return {"init": init, "losses": losses, "stats": stats, "master": master,
+    return {"init": init, "losses": losses, "stats": stats, "master": master, "nb": nb,
             "params": [p.detach().clone() for p in m.parameters()]}
 
 
-def test_async_single_rank_sync_delay_equals_local():
-    """W=1, M=1, max_delay=0: every step waits for its own update -> identical to local SGD."""
+@pytest.mark.parametrize("bucket_mb,slots", [(64.0, 0), (0.0005, 2), (0.0005, 1)])
+def test_async_single_rank_sync_delay_equals_local(bucket_mb, slots):
+    """W=1, M=1, max_delay=0: every step waits for its own update -> identical to local SGD, also
+    when each step is streamed as several bucket messages through a 1- or 2-slot mailbox."""
     import hipps
-    from test_dist_cpu import _simulate
 
-    out = run_world(_train_async, 1, 5, "fp32", 1, 0, -1)
-    want = _simulate(1, 5, "sgd")  # same data for rank 0, steps 0..4 (s % 4 wraps: recompute)
-    # recompute the reference with the same data schedule
+    out = run_world(_train_async, 1, 5, "fp32", 1, 0, -1, "sgd", bucket_mb, slots)
+    if bucket_mb < 1:
+        assert out[0]["nb"] >= 3
     m = _mlp()
     opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="local")
     for s in range(5):
@@ -55,10 +58,10 @@ def test_async_single_rank_sync_delay_equals_local():
     assert out[0]["stats"]["updates"] == 5
 
 
-@pytest.mark.parametrize("codec", ["fp32", "bf16", "topk_int8:0.1"])
-def test_async_three_ranks_converges_and_accounts(codec):
+@pytest.mark.parametrize("codec,bucket_mb", [("fp32", 64.0), ("bf16", 0.0005), ("topk_int8:0.1", 0.0005)])
+def test_async_three_ranks_converges_and_accounts(codec, bucket_mb):
     steps = 12
-    out = run_world(_train_async, 3, steps, codec, 0, -1, -1)
+    out = run_world(_train_async, 3, steps, codec, 0, -1, -1, "sgd", bucket_mb, 0)
     st = out[0]["stats"]
     # every pushed message is accumulated exactly once; M = W = 3
     assert st["accumulated"] == 3 * steps
