@@ -121,7 +121,7 @@ def main():
     torch.cuda.synchronize()
     hdist.barrier(world)
     t1 = time.perf_counter()
-    el = torch.tensor([t1 - t0], device=dev, dtype=torch.float64)
+    el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev if world.backend == "nccl" else "cpu")
     if N > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())

@@ -35,15 +35,19 @@ class World:
 
 def init_from_env(backend: Optional[str] = None, timeout_s: float = 600.0) -> World:
     """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* if present; bind rank->GPU."""
+    backend = backend or os.environ.get("HIPPS_BACKEND") or None  # e.g. gloo to rehearse N ranks on 1 GPU
     rank = int(os.environ.get("RANK", "0"))
     size = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    use_gpu = torch.cuda.is_available()
     if use_gpu:
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     if size > 1 and not dist.is_initialized():
         be = backend or ("nccl" if use_gpu else "gloo")
+        if be == "nccl" and torch.cuda.device_count() < size:
+            raise RuntimeError(f"nccl needs one GPU per rank ({size} ranks, {torch.cuda.device_count()} GPUs); "
+                               "set HIPPS_BACKEND=gloo to share a GPU")
         kw = {}
         if be == "nccl" and use_gpu:
             kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
