@@ -244,8 +244,55 @@ class TopKInt8(TopK):
             ops.topk_q8_accumulate(m["idx"], m["q"], m["scales"], acc, gscale)
 
 
+class Threshold(Codec):
+    """Variable-size sparsification: every |g| > tau (ascending indices), at most
+    ceil(max_ratio*n) of them.  The message has a static CAPACITY but a data-dependent COUNT
+    stored in a device-side header that the decode kernel reads -- the "unknown-size" path of
+    README.md:30-31 without a size round trip or a host sync."""
+
+    name = "threshold"
+
+    def __init__(self, tau: float = 1e-3, max_ratio: float = 0.05, value_dtype: torch.dtype = torch.float32,
+                 error_feedback: bool = True):
+        super().__init__()
+        self.tau = float(tau)
+        self.max_ratio = max_ratio
+        self.value_dtype = value_dtype
+        self.error_feedback = error_feedback
+
+    def cap_of(self, n: int) -> int:
+        return max(1, min(n, int(math.ceil(self.max_ratio * n))))
+
+    def layout(self, n):
+        k = self.cap_of(n)
+        return WireLayout([("count", torch.int32, 4), ("idx", torch.int32, k), ("val", self.value_dtype, k)])
+
+    def init_state(self, n, device):
+        st = {}
+        if self.error_feedback:
+            st["resid"] = torch.zeros(n, dtype=torch.float32, device=device)
+        if device is not None and torch.device(device).type == "cuda":
+            st["ws"] = torch.empty(ops.topk_workspace_bytes(n), dtype=torch.uint8, device=device)
+        return st
+
+    def encode_into(self, x, views, state):
+        ops.thresh_encode(x, state.get("resid"), self.tau, views["count"], views["idx"], views["val"], state.get("ws"))
+
+    def accumulate(self, msgs, acc, gscale=1.0, accumulate=False):
+        if not accumulate:
+            acc.zero_()
+        for m in msgs:
+            ops.thresh_accumulate(m["count"], m["idx"], m["val"], acc, gscale)
+
+    @staticmethod
+    def count(views) -> int:
+        """Host read of a message's element count (diagnostics only; forces a sync)."""
+        return int(views["count"][0])
+
+
 def get_codec(spec) -> Codec:
-    """'fp32' | 'bf16' | 'int8' | 'int8_sr' | 'topk[:ratio]' | 'topk_bf16[:ratio]' | 'topk_int8[:ratio]' | Codec."""
+    """'fp32' | 'bf16' | 'int8' | 'int8_sr' | 'topk[:ratio]' | 'topk_bf16[:ratio]' | 'topk_int8[:ratio]' |
+    'threshold[:tau[:max_ratio]]' | Codec instance."""
     if spec is None:
         return Identity(torch.float32)
     if isinstance(spec, Codec):
@@ -260,6 +307,9 @@ def get_codec(spec) -> Codec:
         return Int8(stochastic=False)
     if name in ("int8_sr", "qsgd_sr"):
         return Int8(stochastic=True)
+    if name in ("threshold", "thresh"):
+        tau, _, mr = arg.partition(":")
+        return Threshold(tau=float(tau) if tau else 1e-3, max_ratio=float(mr) if mr else 0.05)
     ratio = float(arg) if arg else 0.01
     if name == "topk":
         return TopK(ratio)
@@ -270,4 +320,4 @@ def get_codec(spec) -> Codec:
     raise ValueError(f"unknown codec {spec!r}")
 
 
-__all__ = ["Codec", "Identity", "Int8", "TopK", "TopKInt8", "WireLayout", "get_codec"]
+__all__ = ["Codec", "Identity", "Int8", "TopK", "TopKInt8", "Threshold", "WireLayout", "get_codec"]

@@ -25,6 +25,9 @@ int64_t topk_workspace_bytes(int64_t n);
 void topk_accumulate(at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale);
 void topk_q8_accumulate(at::Tensor idx, at::Tensor q, at::Tensor scales, at::Tensor acc, double gscale);
 void topk_q8_residual(at::Tensor idx, at::Tensor v, at::Tensor q, at::Tensor scales, at::Tensor resid);
+void thresh_encode(at::Tensor g, c10::optional<at::Tensor> resid, double tau, at::Tensor count, at::Tensor idx,
+                   at::Tensor val, at::Tensor workspace);
+void thresh_accumulate(at::Tensor count, at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale);
 // norm.hip
 void bn_forward_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, at::Tensor weight, at::Tensor bias,
                       c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var, at::Tensor mean,
@@ -56,6 +59,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("topk_accumulate", &hipps::topk_accumulate, "acc[idx] += gscale * val");
   m.def("topk_q8_accumulate", &hipps::topk_q8_accumulate, "acc[idx] += gscale * deq(q)");
   m.def("topk_q8_residual", &hipps::topk_q8_residual, "EF: r[idx] += v - deq(q)");
+  m.def("thresh_encode", &hipps::thresh_encode, "variable-size |x|>tau sparsification, device count header");
+  m.def("thresh_accumulate", &hipps::thresh_accumulate, "acc[idx[:count]] += gscale * val[:count]");
   m.def("bn_forward_train", &hipps::bn_forward_train, "fused channels-last BN train fwd (+res) (+relu)");
   m.def("bn_apply", &hipps::bn_apply, "y = act(x*scale + shift (+res))");
   m.def("bn_backward", &hipps::bn_backward, "fused BN bwd with relu-mask recompute (+dres)");

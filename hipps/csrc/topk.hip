@@ -17,6 +17,9 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
+#include <cmath>
+#include <cstring>
+
 namespace hipps {
 
 constexpr int kHistBins = 2048;
@@ -152,7 +155,8 @@ __global__ __launch_bounds__(kBlock) void k_topk_count(const float* __restrict__
 
 // exclusive scan of both count arrays in place (one workgroup; nchunks ~ n/1024)
 __global__ __launch_bounds__(1024) void k_topk_scan(uint32_t* __restrict__ cgt, uint32_t* __restrict__ ceq,
-                                                    int64_t nchunks) {
+                                                    int64_t nchunks, int32_t* __restrict__ count_out,
+                                                    uint32_t cap) {
   __shared__ uint32_t sg[1024], se[1024];
   __shared__ uint32_t carry_g, carry_e;
   if (threadIdx.x == 0) { carry_g = 0; carry_e = 0; }
@@ -174,6 +178,7 @@ __global__ __launch_bounds__(1024) void k_topk_scan(uint32_t* __restrict__ cgt, 
     if (threadIdx.x == 1023) { carry_g += sg[1023]; carry_e += se[1023]; }
     __syncthreads();
   }
+  if (count_out && threadIdx.x == 0) count_out[0] = (int32_t)(carry_g < cap ? carry_g : cap);
 }
 
 template <typename VT>
@@ -181,7 +186,7 @@ __global__ __launch_bounds__(kBlock) void k_topk_write(const float* __restrict__
                                                        int64_t n, const SelState* __restrict__ st,
                                                        const uint32_t* __restrict__ pgt,
                                                        const uint32_t* __restrict__ peq, int64_t nchunks,
-                                                       int32_t* __restrict__ idx, VT* __restrict__ val) {
+                                                       int32_t* __restrict__ idx, VT* __restrict__ val, uint32_t cap) {
   __shared__ uint32_t wg[4], we[4];
   const uint32_t T = st->prefix, need_eq = st->remaining;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -213,8 +218,8 @@ __global__ __launch_bounds__(kBlock) void k_topk_write(const float* __restrict__
     for (int j = 0; j < 4; ++j) {
       if (i + j >= n) break;
       const bool isgt = k[j] > T, iseq = k[j] == T;
-      if (isgt || (iseq && be < need_eq)) {
-        const uint32_t pos = bg + (be < need_eq ? be : need_eq);
+      const uint32_t pos = bg + (be < need_eq ? be : need_eq);
+      if ((isgt || (iseq && be < need_eq)) && pos < cap) {
         idx[pos] = (int32_t)(i + j);
         Vec4<VT>::store1(val, pos, x[j]);
         if (resid) resid[i + j] = x[j] - Vec4<VT>::load1(val, pos);
@@ -292,13 +297,91 @@ void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::T
   const float* src = rp ? rp : g.data_ptr<float>();
   const int cgrid = (int)std::min<int64_t>(nchunks, kMaxGrid);
   hipLaunchKernelGGL(k_topk_count, cgrid, kBlock, 0, stream, src, n, st, cgt, ceq, nchunks);
-  hipLaunchKernelGGL(k_topk_scan, 1, 1024, 0, stream, cgt, ceq, nchunks);
+  hipLaunchKernelGGL(k_topk_scan, 1, 1024, 0, stream, cgt, ceq, nchunks, nullptr, 0u);
   if (val.scalar_type() == at::kFloat)
     hipLaunchKernelGGL(k_topk_write<float>, cgrid, kBlock, 0, stream, src, rp, n, st, cgt, ceq, nchunks,
-                       idx.data_ptr<int32_t>(), val.data_ptr<float>());
+                       idx.data_ptr<int32_t>(), val.data_ptr<float>(), (uint32_t)k);
   else
     hipLaunchKernelGGL(k_topk_write<uint16_t>, cgrid, kBlock, 0, stream, src, rp, n, st, cgt, ceq, nchunks,
-                       idx.data_ptr<int32_t>(), (uint16_t*)val.data_ptr());
+                       idx.data_ptr<int32_t>(), (uint16_t*)val.data_ptr(), (uint32_t)k);
+}
+
+// ---- threshold sparsification (variable-size message, count in a device header) -----------
+__global__ __launch_bounds__(kBlock) void k_fold(const float* __restrict__ g, float* __restrict__ r, int64_t n) {
+  const int64_t nv = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+    float4 a = *reinterpret_cast<const float4*>(g + 4 * v), b = *reinterpret_cast<const float4*>(r + 4 * v);
+    *reinterpret_cast<float4*>(r + 4 * v) = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = (nv << 2) + threadIdx.x; i < n; i += blockDim.x) r[i] += g[i];
+}
+
+__global__ void k_thresh_init(SelState* __restrict__ st, uint32_t tbits) {
+  if (threadIdx.x == 0) { st->prefix = tbits; st->mask = 0xffffffffu; st->remaining = 0; st->pad = 0; }
+}
+
+template <typename VT>
+__global__ __launch_bounds__(kBlock) void k_scatter_acc_count(const int32_t* __restrict__ idx,
+                                                              const VT* __restrict__ val,
+                                                              const int32_t* __restrict__ count, int64_t cap,
+                                                              float* __restrict__ acc, float gscale) {
+  const int64_t k = min((int64_t)count[0], cap);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < k; j += stride)
+    acc[idx[j]] += gscale * Vec4<VT>::load1(val, j);
+}
+
+// Every |x| > tau (x = g [+ residual]) in ascending index order, at most cap of them; the true
+// count (clamped) goes to count[0] on the device, so decode needs no host round trip.
+void thresh_encode(at::Tensor g, c10::optional<at::Tensor> resid, double tau, at::Tensor count, at::Tensor idx,
+                   at::Tensor val, at::Tensor workspace) {
+  TORCH_CHECK(g.is_cuda() && g.is_contiguous() && g.scalar_type() == at::kFloat, "g: contiguous f32 device tensor");
+  const int64_t n = g.numel(), cap = idx.numel();
+  TORCH_CHECK(val.numel() == cap && count.scalar_type() == at::kInt && count.numel() >= 1, "count/idx/val");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0, "g must be 16-byte aligned");
+  const int64_t nchunks = (n + kChunk - 1) / kChunk;
+  TORCH_CHECK(workspace.numel() * workspace.element_size() >= (int64_t)sizeof(SelState) + 8 * nchunks + 16,
+              "workspace too small");
+  auto stream = c10::hip::getCurrentHIPStream();
+  float* rp = nullptr;
+  if (resid.has_value() && resid->defined()) {
+    TORCH_CHECK(resid->numel() == n && resid->scalar_type() == at::kFloat, "residual");
+    rp = resid->data_ptr<float>();
+    hipLaunchKernelGGL(k_fold, grid_for(n >> 2), kBlock, 0, stream, g.data_ptr<float>(), rp, n);
+  }
+  char* ws = (char*)workspace.data_ptr();
+  SelState* st = reinterpret_cast<SelState*>(ws);
+  uint32_t* cgt = reinterpret_cast<uint32_t*>(ws + sizeof(SelState));
+  uint32_t* ceq = cgt + nchunks;
+  float t = (float)std::fabs(tau);
+  uint32_t tbits;
+  std::memcpy(&tbits, &t, 4);
+  hipLaunchKernelGGL(k_thresh_init, 1, 64, 0, stream, st, tbits);
+  const float* src = rp ? rp : g.data_ptr<float>();
+  const int cgrid = (int)std::min<int64_t>(nchunks, kMaxGrid);
+  hipLaunchKernelGGL(k_topk_count, cgrid, kBlock, 0, stream, src, n, st, cgt, ceq, nchunks);
+  hipLaunchKernelGGL(k_topk_scan, 1, 1024, 0, stream, cgt, ceq, nchunks, count.data_ptr<int32_t>(), (uint32_t)cap);
+  if (val.scalar_type() == at::kFloat)
+    hipLaunchKernelGGL(k_topk_write<float>, cgrid, kBlock, 0, stream, src, rp, n, st, cgt, ceq, nchunks,
+                       idx.data_ptr<int32_t>(), val.data_ptr<float>(), (uint32_t)cap);
+  else
+    hipLaunchKernelGGL(k_topk_write<uint16_t>, cgrid, kBlock, 0, stream, src, rp, n, st, cgt, ceq, nchunks,
+                       idx.data_ptr<int32_t>(), (uint16_t*)val.data_ptr(), (uint32_t)cap);
+}
+
+void thresh_accumulate(at::Tensor count, at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale) {
+  TORCH_CHECK(acc.is_cuda() && acc.scalar_type() == at::kFloat, "acc: f32 device tensor");
+  const int64_t cap = idx.numel();
+  if (cap == 0) return;
+  auto stream = c10::hip::getCurrentHIPStream();
+  if (val.scalar_type() == at::kFloat)
+    hipLaunchKernelGGL(k_scatter_acc_count<float>, grid_for(cap), kBlock, 0, stream, idx.data_ptr<int32_t>(),
+                       val.data_ptr<float>(), count.data_ptr<int32_t>(), cap, acc.data_ptr<float>(), (float)gscale);
+  else
+    hipLaunchKernelGGL(k_scatter_acc_count<uint16_t>, grid_for(cap), kBlock, 0, stream, idx.data_ptr<int32_t>(),
+                       (const uint16_t*)val.data_ptr(), count.data_ptr<int32_t>(), cap, acc.data_ptr<float>(),
+                       (float)gscale);
 }
 
 int64_t topk_workspace_bytes(int64_t n) {

@@ -101,3 +101,18 @@ def topk_q8_residual(idx, v, q, scales, resid):
     if _dev(resid):
         return native().topk_q8_residual(idx, v, q, scales, resid)
     return ref.topk_q8_residual(idx, v, q, scales, resid)
+
+
+def thresh_encode(g, resid, tau: float, count, idx, val, workspace=None):
+    """Variable-size sparsification: |x| > tau, capacity idx.numel(), true count in count[0]."""
+    if _dev(g):
+        if workspace is None:
+            workspace = torch.empty(native().topk_workspace_bytes(g.numel()), dtype=torch.uint8, device=g.device)
+        return native().thresh_encode(g, resid, float(tau), count, idx, val, workspace)
+    return ref.thresh_encode(g, resid, tau, count, idx, val)
+
+
+def thresh_accumulate(count, idx, val, acc, gscale: float = 1.0):
+    if _dev(acc):
+        return native().thresh_accumulate(count, idx, val, acc, float(gscale))
+    return ref.thresh_accumulate(count, idx, val, acc, gscale)

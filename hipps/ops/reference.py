@@ -191,3 +191,24 @@ def topk_q8_residual(idx, v, q, scales, resid):
 
 def topk_workspace_bytes(n: int) -> int:
     return 16
+
+
+def thresh_encode(g, resid, tau, count, idx, val, workspace=None):
+    """Every |x| > tau in ascending index order, at most idx.numel() of them (count in count[0])."""
+    x = _f32(g).clone()
+    if resid is not None:
+        x += resid
+    cap = idx.numel()
+    sel = torch.nonzero(x.abs() > abs(tau)).view(-1)[:cap]
+    count[0] = sel.numel()
+    idx[: sel.numel()] = sel.to(torch.int32)
+    v = x[sel]
+    val[: sel.numel()] = v.to(val.dtype)
+    if resid is not None:
+        resid.copy_(x)
+        resid[sel] = v - val[: sel.numel()].float()
+
+
+def thresh_accumulate(count, idx, val, acc, gscale=1.0):
+    k = min(int(count[0]), idx.numel())
+    acc.index_add_(0, idx[:k].long(), val[:k].float() * gscale)

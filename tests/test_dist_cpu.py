@@ -75,7 +75,7 @@ def test_sync_modes_match_single_process_sum(mode, opt_name):
     assert out[0][1]["grad_bytes_sent"] > 0
 
 
-@pytest.mark.parametrize("codec", ["bf16", "int8", "topk:0.05", "topk_int8:0.05"])
+@pytest.mark.parametrize("codec", ["bf16", "int8", "topk:0.05", "topk_int8:0.05", "threshold:0.01:0.2"])
 def test_allgather_codecs_keep_replicas_identical(codec):
     out = run_world(_train, 2, "allgather", codec, 3, "sgd")
     for a, b in zip(out[0][0], out[1][0]):

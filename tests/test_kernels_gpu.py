@@ -166,3 +166,29 @@ def test_codec_gpu_matches_cpu(spec):
         outs.append(acc.cpu())
     tol = 1e-6 if spec in ("fp32", "topk:0.01") else (2e-2 if "int8" in spec else 1e-2)
     torch.testing.assert_close(outs[1], outs[0], rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("n,tau,ratio", [(1000, 1.0, 0.5), (1 << 20, 2.0, 0.01), (1 << 20, 3.0, 0.5), (4099, 0.0, 0.1)])
+@pytest.mark.parametrize("ef", [False, True])
+def test_threshold_codec_gpu_matches_reference(n, tau, ratio, ef):
+    from hipps.codecs import Threshold
+
+    torch.manual_seed(n)
+    x = torch.randn(n)
+    outs = []
+    for dev in ("cpu", DEV):
+        c = Threshold(tau=tau, max_ratio=ratio, error_feedback=ef)
+        lay = c.layout(n)
+        buf = torch.zeros(lay.nbytes, dtype=torch.uint8, device=dev)
+        v = lay.views(buf)
+        st = c.init_state(n, dev)
+        c.encode_into(x.to(dev), v, st)
+        acc = torch.zeros(n, device=dev)
+        c.accumulate([v], acc, 1.0, True)
+        k = int(v["count"][0])
+        outs.append((k, v["idx"][:k].cpu(), acc.cpu(), st["resid"].cpu() if ef else None))
+    assert outs[0][0] == outs[1][0]
+    assert torch.equal(outs[0][1], outs[1][1])
+    torch.testing.assert_close(outs[1][2], outs[0][2])
+    if ef:
+        torch.testing.assert_close(outs[1][3], outs[0][3])

@@ -164,3 +164,25 @@ def test_uniform01_matches_splitmix_definition():
     u = ref.uniform01(7, np.arange(4, dtype=np.int64))
     assert u.dtype == np.float32 and ((u >= 0) & (u < 1)).all()
     assert len(set(u.tolist())) == 4
+
+
+def test_threshold_codec_variable_size_and_ef():
+    from hipps.codecs import Threshold
+
+    x = torch.tensor([0.5, -3.0, 0.01, 2.0, -0.2, 0.0, 1.0])
+    c = Threshold(tau=0.3, max_ratio=0.5)  # capacity 4
+    lay = c.layout(7)
+    buf = torch.zeros(lay.nbytes, dtype=torch.uint8)
+    v = lay.views(buf)
+    st = c.init_state(7, "cpu")
+    c.encode_into(x, v, st)
+    assert int(v["count"][0]) == 4 and v["idx"].tolist() == [0, 1, 3, 6]
+    acc = torch.zeros(7)
+    c.accumulate([v], acc)
+    torch.testing.assert_close(acc + st["resid"], x)
+    # capacity clamps: a second, denser message keeps the overflow in the residual
+    c2 = Threshold(tau=0.0, max_ratio=2 / 7, error_feedback=False)
+    lay2 = c2.layout(7)
+    v2 = lay2.views(torch.zeros(lay2.nbytes, dtype=torch.uint8))
+    c2.encode_into(x, v2, c2.init_state(7, "cpu"))
+    assert int(v2["count"][0]) == 2 and v2["idx"].tolist() == [0, 1]

@@ -58,7 +58,8 @@ def test_async_single_rank_sync_delay_equals_local(bucket_mb, slots):
     assert out[0]["stats"]["updates"] == 5
 
 
-@pytest.mark.parametrize("codec,bucket_mb", [("fp32", 64.0), ("bf16", 0.0005), ("topk_int8:0.1", 0.0005)])
+@pytest.mark.parametrize("codec,bucket_mb", [("fp32", 64.0), ("bf16", 0.0005), ("topk_int8:0.1", 0.0005),
+                                            ("threshold:0.001:0.3", 0.0005)])
 def test_async_three_ranks_converges_and_accounts(codec, bucket_mb):
     steps = 12
     out = run_world(_train_async, 3, steps, codec, 0, -1, -1, "sgd", bucket_mb, 0)
