@@ -100,7 +100,7 @@ def build(clean: bool = False, verbose: bool = False, jobs: int | None = None) -
     out = ext_path()
     if todo or not os.path.exists(out):
         libs = ["-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip",
-                "-lamdhip64", "-lrccl", "-lrt", "-lpthread"]
+                "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-lrt", "-lpthread"]
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out + ".tmp"] + objs + [
             f"-L{tlib}", "-L/opt/rocm/lib", f"-Wl,-rpath,{tlib}"] + libs
         if verbose:

@@ -55,6 +55,11 @@ class PSConfig:
     adam_variant: str = "reference"
     # all-gather a hash of the posting sequence each step and assert equality (race detector)
     debug_check_order: bool = False
+    # write a 16-byte 0x29 canary after every bucket message (the device analogue of the reference
+    # sentinel, mpi_comms.py:80,101-103) and verify it after encode and after every transfer
+    debug_canary: bool = False
+    # device phase timing with HIP events + roctx ranges (encode_ms / comm_ms / update_ms keys)
+    trace: bool = False
     # metrics JSONL path (per rank; '{rank}' is substituted)
     metrics_path: Optional[str] = None
 

@@ -42,6 +42,7 @@ void bn_backward(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> y, int64
 namespace rt {
 void bind_control(pybind11::module& m);
 void bind_ipc(pybind11::module& m);
+void bind_trace(pybind11::module& m);
 }  // namespace rt
 }  // namespace hipps
 
@@ -66,4 +67,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_backward", &hipps::bn_backward, "fused BN bwd with relu-mask recompute (+dres)");
   hipps::rt::bind_control(m);
   hipps::rt::bind_ipc(m);
+  hipps::rt::bind_trace(m);
 }

@@ -21,6 +21,8 @@ from typing import Dict, List, Optional
 
 import torch
 
+from hipps.utils.tracing import StepTracer
+
 from .dist import World, all_gather_into, barrier, broadcast, gather_into
 from .flat import BucketPlan, FlatStore, _is_dense
 
@@ -34,10 +36,12 @@ class Engine:
         self.store = store
         self.codec = codec
         self.world = world
-        self.plan = BucketPlan(store, codec, int(cfg.bucket_mb * (1 << 20)))
+        self.plan = BucketPlan(store, codec, int(cfg.bucket_mb * (1 << 20)), guard=cfg.debug_canary)
         self.cuda = store.device.type == "cuda"
+        self.tracer = StepTracer(cfg.trace, self.cuda)
         # zero-initialised: the 16-element alignment gaps between parameters are never written
         self.wire = torch.zeros(self.plan.wire_nbytes, dtype=torch.uint8, device=store.device)
+        self.plan.fill_guards(self.wire)
         self.codec_state = [codec.init_state(b.numel, store.device) for b in self.plan.buckets]
         self.comm_stream = torch.cuda.Stream(device=store.device) if self.cuda else None
         self._encoded = [False] * len(self.plan.buckets)
@@ -101,7 +105,7 @@ class Engine:
         from hipps.ops._native import native
 
         b = self.plan.buckets[bi]
-        dense = self.codec.fusable
+        dense = self.codec.fusable  # per-bucket image: guards sit after the layout, not inside
         dst = views["x"] if dense else self.store.grad[b.lo:b.hi]
         C = native()
         for gids, table in self._gplan[bi]:
@@ -126,15 +130,31 @@ class Engine:
             ev.record(torch.cuda.current_stream(self.store.device))
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
-                if self.grad_mode == "gather" and self._gather_bucket(bi, views):
-                    pass  # dense codec: the gather already wrote the wire image
-                else:
-                    self.codec.encode_into(g, views, self.codec_state[bi])
+                with self.tracer.phase("encode", self.comm_stream):
+                    if self.grad_mode == "gather" and self._gather_bucket(bi, views):
+                        pass  # dense codec: the gather already wrote the wire image
+                    else:
+                        self.codec.encode_into(g, views, self.codec_state[bi])
         else:
-            self.codec.encode_into(g, views, self.codec_state[bi])
+            with self.tracer.phase("encode"):
+                self.codec.encode_into(g, views, self.codec_state[bi])
         self._encoded[bi] = True
         if self.cfg.debug_check_order:
             self._order_log.append(f"{bi}:{b.numel}:{self.codec.name}")
+
+    def verify_guards(self, wires: List[torch.Tensor], what: str):
+        """debug_canary: raise if any bucket's 0x29 canary was overwritten (a codec kernel wrote
+        past its layout, or a transfer was truncated/misplaced) -- mpi_comms.py:101-103 analogue.
+        Host sync; debug only."""
+        if not self.plan.guarded:
+            return
+        if self.cuda:
+            torch.cuda.current_stream(self.store.device).wait_stream(self.comm_stream)
+        for r, w in enumerate(wires):
+            bad = self.plan.bad_guards(w)
+            if bool(bad.any()):
+                ids = bad.nonzero().view(-1).tolist()
+                raise RuntimeError(f"wire canary overwritten ({what}, message {r}) in buckets {ids}")
 
     def encode_all(self):
         """Encode every bucket not yet handled by a hook; returns host seconds spent."""
@@ -169,7 +189,7 @@ class Engine:
     def apply(self, wire_msgs: List[torch.Tensor], target: torch.Tensor, pub: Optional[torch.Tensor], gscale: float,
               scratch: Optional[torch.Tensor] = None):
         """Decode W wire messages, sum in rank order, apply the optimizer to ``target`` (flat)."""
-        if self.codec.fusable:
+        if self.plan.dense_ok:
             imgs = [self.plan.dense_image(w) for w in wire_msgs]
             self.opt._update_flat(imgs, target, gscale, zero_src=False, pub=pub)
         else:
@@ -216,8 +236,8 @@ class LocalEngine(Engine):
 
     def __init__(self, *a, **k):
         super().__init__(*a, **k)
-        self._scratch = None if self.codec.fusable else torch.empty_like(self.store.grad)
-        self._bypass = self.codec.fusable and self.codec.lossless
+        self._scratch = None if self.plan.dense_ok else torch.empty_like(self.store.grad)
+        self._bypass = self.plan.dense_ok and self.codec.lossless
 
     def encode_bucket(self, bi):
         if self._bypass:  # fp32 identity: the flat grad IS the message
@@ -231,14 +251,18 @@ class LocalEngine(Engine):
         t = time.perf_counter()
         if self.cuda and not self._bypass:
             torch.cuda.current_stream(self.store.device).wait_stream(self.comm_stream)
-        if self._bypass:
-            self.opt._update_flat([self.store.grad], self.store.data, 1.0, zero_src=False, pub=None)
-        else:
-            self.apply([self.wire], self.store.data, None, 1.0, self._scratch)
+        if not self._bypass:
+            self.verify_guards([self.wire], "encode")
+        with self.tracer.phase("update"):
+            if self._bypass:
+                self.opt._update_flat([self.store.grad], self.store.data, 1.0, zero_src=False, pub=None)
+            else:
+                self.apply([self.wire], self.store.data, None, 1.0, self._scratch)
         data["optim_step_time"] = time.perf_counter() - t
         data["decode_time"] = 0.0
         data["comm_wait"] = 0.0
         data.update(self.bytes_per_step())
+        data.update(self.tracer.collect())
         self.steps += 1
         return data
 
@@ -253,7 +277,7 @@ class AllGatherEngine(Engine):
         super().__init__(*a, **k)
         W = self.world.size
         self.gathered = torch.empty(W * self.plan.wire_nbytes, dtype=torch.uint8, device=self.store.device)
-        self._scratch = None if self.codec.fusable else torch.empty_like(self.store.grad)
+        self._scratch = None if self.plan.dense_ok else torch.empty_like(self.store.grad)
 
     def step(self):
         data = {}
@@ -261,20 +285,24 @@ class AllGatherEngine(Engine):
         self._check_order()
         t = time.perf_counter()
         if self.cuda:
-            with torch.cuda.stream(self.comm_stream):
+            with torch.cuda.stream(self.comm_stream), self.tracer.phase("comm", self.comm_stream):
                 all_gather_into(self.gathered, self.wire, self.world)
             torch.cuda.current_stream(self.store.device).wait_stream(self.comm_stream)
         else:
-            all_gather_into(self.gathered, self.wire, self.world)
+            with self.tracer.phase("comm"):
+                all_gather_into(self.gathered, self.wire, self.world)
         data["isend_time"] = data["comm_wait"] = time.perf_counter() - t
         t = time.perf_counter()
         n = self.plan.wire_nbytes
         msgs = [self.gathered[w * n:(w + 1) * n] for w in range(self.world.size)]
-        self.apply(msgs, self.store.data, None, self.gscale(self.world.size), self._scratch)
+        self.verify_guards(msgs, "allgather")
+        with self.tracer.phase("update"):
+            self.apply(msgs, self.store.data, None, self.gscale(self.world.size), self._scratch)
         data["optim_step_time"] = time.perf_counter() - t
         data["decode_time"] = 0.0
         data.update(self.bytes_per_step())
         data["grad_bytes_recv"] = n * self.world.size
+        data.update(self.tracer.collect())
         self.steps += 1
         return data
 
@@ -290,7 +318,7 @@ class PSSyncEngine(Engine):
         dev = self.store.device
         self.gathered = (torch.empty(W * self.plan.wire_nbytes, dtype=torch.uint8, device=dev)
                          if self.world.is_ps else torch.empty(self.plan.wire_nbytes, dtype=torch.uint8, device=dev))
-        self._scratch = None if self.codec.fusable else torch.empty_like(self.store.grad)
+        self._scratch = None if self.plan.dense_ok else torch.empty_like(self.store.grad)
         self.pub = None
         if self.cfg.param_wire == "bf16":
             self.pub = torch.empty(self.store.numel, dtype=torch.bfloat16, device=dev)
@@ -301,7 +329,8 @@ class PSSyncEngine(Engine):
         t = time.perf_counter()
         cs = self.comm_stream
         ctx = torch.cuda.stream(cs) if self.cuda else _null()
-        with ctx:
+        self.verify_guards([self.wire], "encode")
+        with ctx, self.tracer.phase("comm", cs):
             gather_into(self.gathered if self.world.is_ps else None, self.wire, self.world)
         if self.cuda:
             torch.cuda.current_stream(self.store.device).wait_stream(cs)
@@ -310,20 +339,24 @@ class PSSyncEngine(Engine):
         if self.world.is_ps:
             n = self.plan.wire_nbytes
             msgs = [self.gathered[w * n:(w + 1) * n] for w in range(self.world.size)]
-            self.apply(msgs, self.store.data, self.pub, self.gscale(self.world.size), self._scratch)
+            self.verify_guards(msgs, "gather")
+            with self.tracer.phase("update"):
+                self.apply(msgs, self.store.data, self.pub, self.gscale(self.world.size), self._scratch)
         data["optim_step_time"] = time.perf_counter() - t
         t = time.perf_counter()
         # ibroadcast of the parameters (mpi_comms.py:127-133 / README.md:76)
-        if self.pub is not None:
-            broadcast(self.pub, self.world, 0)
-            if not self.world.is_ps:
-                from hipps import ops
+        with self.tracer.phase("bcast"):
+            if self.pub is not None:
+                broadcast(self.pub, self.world, 0)
+                if not self.world.is_ps:
+                    from hipps import ops
 
-                ops.convert(self.pub, self.store.data)
-        else:
-            broadcast(self.store.data, self.world, 0)
+                    ops.convert(self.pub, self.store.data)
+            else:
+                broadcast(self.store.data, self.world, 0)
         data["bcast_time"] = time.perf_counter() - t
         data.update(self.bytes_per_step())
+        data.update(self.tracer.collect())
         self.steps += 1
         return data
 

@@ -143,6 +143,10 @@ class FlatStore:
         return f(self.numel, dtype=dtype or self.dtype, device=self.device)
 
 
+GUARD_BYTES = 16
+GUARD_BYTE = 0x29  # the reference's sentinel byte (mpi_comms.py:80)
+
+
 @dataclass
 class Bucket:
     index: int
@@ -151,6 +155,7 @@ class Bucket:
     slot_ids: List[int]
     wire_offset: int = 0
     layout: object = None
+    msg_nbytes: int = 0  # layout bytes + canary guard (debug_canary)
 
     @property
     def numel(self):
@@ -165,9 +170,10 @@ class BucketPlan:
     image of the flat gradient.
     """
 
-    def __init__(self, store: FlatStore, codec, bucket_bytes: int = 64 << 20):
+    def __init__(self, store: FlatStore, codec, bucket_bytes: int = 64 << 20, guard: bool = False):
         self.store = store
         self.codec = codec
+        self.guarded = bool(guard)
         cap = max(1, bucket_bytes // store.data.element_size())
         rev = list(range(len(store.slots)))[::-1]
         groups: List[List[int]] = []
@@ -194,11 +200,16 @@ class BucketPlan:
             nxt = spans[bi + 1][0] if bi + 1 < len(spans) else store.numel
             self.buckets.append(Bucket(bi, lo if bi else 0, nxt, ids))
         woff = 0
+        g = GUARD_BYTES if self.guarded else 0
         for b in self.buckets:
             b.layout = codec.layout(b.numel)
             b.wire_offset = woff
-            woff += b.layout.nbytes
+            b.msg_nbytes = b.layout.nbytes + g
+            woff += b.msg_nbytes
         self.wire_nbytes = woff
+        # the whole wire is one dense image of the flat gradient only without guards
+        self.dense_ok = bool(codec.fusable) and not self.guarded
+        self._gidx = {}
         self.ready_order = [b.index for b in reversed(self.buckets)]
         self.slot_bucket = {}
         for b in self.buckets:
@@ -208,6 +219,32 @@ class BucketPlan:
     def views(self, wire: torch.Tensor, bi: int):
         b = self.buckets[bi]
         return b.layout.views(wire[b.wire_offset:b.wire_offset + b.layout.nbytes])
+
+    def message(self, wire: torch.Tensor, bi: int) -> torch.Tensor:
+        """Bucket bi's message bytes (layout + guard) inside a whole-wire buffer."""
+        b = self.buckets[bi]
+        return wire[b.wire_offset:b.wire_offset + b.msg_nbytes]
+
+    def _guard_index(self, device) -> torch.Tensor:
+        key = str(device)
+        if key not in self._gidx:
+            idx = [torch.arange(b.wire_offset + b.layout.nbytes, b.wire_offset + b.msg_nbytes) for b in self.buckets]
+            self._gidx[key] = torch.cat(idx).to(device)
+        return self._gidx[key]
+
+    def fill_guards(self, wire: torch.Tensor):
+        if self.guarded:
+            wire[self._guard_index(wire.device)] = GUARD_BYTE
+
+    def bad_guards(self, wire: torch.Tensor) -> torch.Tensor:
+        """Per-bucket bool (device): canary overwritten in a whole-wire buffer."""
+        g = wire[self._guard_index(wire.device)].view(len(self.buckets), GUARD_BYTES)
+        return (g != GUARD_BYTE).any(dim=1)
+
+    @staticmethod
+    def bad_guard(msg: torch.Tensor, layout_nbytes: int) -> torch.Tensor:
+        """Device bool: canary of ONE message buffer (layout + guard) overwritten."""
+        return (msg[layout_nbytes:layout_nbytes + GUARD_BYTES] != GUARD_BYTE).any()
 
     def new_wire(self, device=None) -> torch.Tensor:
         return torch.empty(self.wire_nbytes, dtype=torch.uint8, device=device or self.store.device)

@@ -94,7 +94,7 @@ class PSAsyncEngine(Engine):
         # PS memory is W*K*max_bucket instead of W*2*model (Llama-3-8B: 8x4x512 MB vs 8x2x16 GB)
         self.nb = len(self.plan.buckets)
         self.order = list(self.plan.ready_order)
-        self.slot_bytes = _align(max(b.layout.nbytes for b in self.plan.buckets))
+        self.slot_bytes = _align(max(b.msg_nbytes for b in self.plan.buckets))
         K = cfg.mailbox_slots if cfg.mailbox_slots > 0 else min(
             2 * self.nb, max(2, int(cfg.mailbox_mb * (1 << 20)) // self.slot_bytes))
         self.SLOTS = max(1, min(K, self.MAXSLOTS))
@@ -204,6 +204,12 @@ class PSAsyncEngine(Engine):
         b = self.plan.buckets[bi]
         return b.layout.views(buf[: b.layout.nbytes])
 
+    def _verify_slot(self, rank: int, slot: int, bi: int, seq: int):
+        """debug_canary on the PS: the pushed message must end in its intact 0x29 guard."""
+        b = self.plan.buckets[bi]
+        if bool(self.plan.bad_guard(self.slot_buf(rank, slot), b.layout.nbytes)):
+            raise RuntimeError(f"mailbox canary overwritten: worker {rank} message {seq} (bucket {bi})")
+
     def pub_buf(self, b: int) -> torch.Tensor:
         o = self.pub_off + b * self.pub_bytes
         esz = torch.empty((), dtype=self.pub_dtype).element_size()
@@ -267,8 +273,11 @@ class PSAsyncEngine(Engine):
                                 self._stats["staleness_sum"] += max(0, stale)
                         if not dropping[i]:
                             b = self.plan.buckets[bi]
-                            self.codec.accumulate([self._bucket_msg(bi, self.slot_buf(i, slot))],
-                                                  self.acc[b.lo:b.hi], 1.0, True)
+                            if self.plan.guarded:
+                                self._verify_slot(i, slot, bi, s)
+                            with self.tracer.phase("ps_accumulate", st):
+                                self.codec.accumulate([self._bucket_msg(bi, self.slot_buf(i, slot))],
+                                                      self.acc[b.lo:b.hi], 1.0, True)
                         self._ring(st, C.F_ACK_SEQ, i, s)  # stream-ordered: acks stay monotonic
                         if pos == nb - 1:
                             pending_incl.append((i, s))  # a dropped step still counts for max_delay
@@ -291,7 +300,8 @@ class PSAsyncEngine(Engine):
         self.ver += 1
         b = self.ver % self.NPUB
         self.ctl.store(C.F_BUF_VER, b, -1)  # readers skip a buffer being rewritten
-        self.opt._update_flat([self.acc], self.master, gscale, zero_src=True, pub=self.pub_buf(b))
+        with self.tracer.phase("ps_update", self.ps_stream):
+            self.opt._update_flat([self.acc], self.master, gscale, zero_src=True, pub=self.pub_buf(b))
         st = self.ps_stream
         # order matters: buffer stamp -> version word -> per-worker "included" words, so a worker
         # that sees its message included also sees a version containing it
@@ -345,6 +355,7 @@ class PSAsyncEngine(Engine):
         C = self.C
         data = {}
         data["code_wait"] = self.encode_all()
+        self.verify_guards([self.wire], "encode")
         self._check_error()
         if self._fault is not None and self._inject(data):
             return data
@@ -364,12 +375,12 @@ class PSAsyncEngine(Engine):
                     raise TimeoutError(f"rank {self.rank}: PS did not consume message {s - self.SLOTS}")
                 t_wait += time.perf_counter() - tw
             b = self.plan.buckets[bi]
-            src = self.wire[b.wire_offset:b.wire_offset + b.layout.nbytes]
-            dst = self.slot_buf(self.rank, slot)[: b.layout.nbytes]
+            src = self.plan.message(self.wire, bi)  # layout (+ canary guard in debug_canary)
+            dst = self.slot_buf(self.rank, slot)[: b.msg_nbytes]
             vidx = self.rank * self.MAXSLOTS + slot
             if self.cuda:
                 cs = self.comm_stream
-                with torch.cuda.stream(cs):
+                with torch.cuda.stream(cs), self.tracer.phase("push", cs):
                     dst.copy_(src, non_blocking=True)
                 self.ctl.enqueue_store2(cs.cuda_stream, C.F_PUSH_VER, vidx, self.local_ver, C.F_PUSH_SEQ,
                                         self.rank, s)
@@ -391,6 +402,7 @@ class PSAsyncEngine(Engine):
         data["grad_bytes_recv"] = 0
         data["param_bytes_pulled"] = self.store.numel * torch.empty((), dtype=self.pub_dtype).element_size() \
             if data.get("pulled") else 0
+        data.update(self.tracer.collect())
         self.steps += 1
         return data
 
