@@ -112,6 +112,11 @@ def main():
 
     for _ in range(a.warmup):
         step()
+    tr = opt.engine.tracer  # HIPPS_TRACE=1: per-phase device ms (HIP events), excluded from warmup
+    if tr.enabled:
+        torch.cuda.synchronize()
+        tr.flush()
+        tr.totals.clear()
     hdist.barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -127,6 +132,10 @@ def main():
     elapsed = float(el.item())
     final_loss = float(loss.float().item())
     grad_bytes = int(last.get("grad_bytes_sent", 0)) if last else 0
+    trace = None
+    if tr.enabled:
+        tr.flush()
+        trace = {k: round(v / a.steps, 4) for k, v in tr.totals.items()}
     nbuckets = len(opt.engine.plan.buckets)
     nparams = sum(p.numel() for p in model.parameters())
     opt.close()
@@ -169,6 +178,8 @@ def main():
             "final_loss": round(final_loss, 4),
             "ps": {k: (int(v) if isinstance(v, (int, float)) else v) for k, v in stats.items()},
         }
+        if trace:
+            rec["trace_device_ms_per_step"] = trace
         if note:
             rec["note"] = note
         line = json.dumps(rec)
