@@ -13,7 +13,7 @@ def test_local_trace_and_canary_gpu(codec):
     m = torch.nn.Sequential(torch.nn.Linear(256, 512), torch.nn.ReLU(), torch.nn.Linear(512, 10)).cuda()
     ref = [p.detach().clone() for p in m.parameters()]
     opt = hipps.SGD(m.named_parameters(), lr=0.05, mode="local", code=codec, trace=True, debug_canary=True,
-                    bucket_mb=0.1)
+                    bucket_mb=0.01)
     assert len(opt.engine.plan.buckets) > 1 and opt.engine.plan.guarded
     keys = {}
     for s in range(4):
