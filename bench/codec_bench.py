@@ -24,7 +24,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from hipps import codecs  # noqa: E402
 
-SPECS = ["fp32", "bf16", "int8", "int8_sr", "topk:0.01", "topk_bf16:0.01", "topk_int8:0.01"]
+SPECS = ["fp32", "bf16", "int8", "int8_sr", "topk:0.01", "topk_bf16:0.01", "topk_int8:0.01", "threshold:0.02:0.05"]
 
 
 def timed(fn, dev, iters):
@@ -93,6 +93,24 @@ def main():
         row = {"n": n, "codec": "reference-pickle(host)", "device": "cpu", "encode_us": round(min(dumps) * 1e6, 2),
                "decode_acc_us": round(min(loads) * 1e6, 2), "zlib1_us_mean": round(float(np.mean(comp)) * 1e6, 1),
                "wire_bytes": len(b)}
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+        try:  # the notebook's other contender (Serialization-timing.ipynb: msgpack dump/load)
+            import msgpack
+        except ImportError:
+            continue
+        payload = arr.tobytes()
+        md, ml = [], []
+        for _ in range(100):
+            t = time.perf_counter()
+            mb = msgpack.packb({"shape": [n], "dtype": "float32", "data": payload})
+            md.append(time.perf_counter() - t)
+            t = time.perf_counter()
+            o = msgpack.unpackb(mb)
+            np.frombuffer(o["data"], dtype=np.float32)
+            ml.append(time.perf_counter() - t)
+        row = {"n": n, "codec": "reference-msgpack(host)", "device": "cpu", "encode_us": round(min(md) * 1e6, 2),
+               "decode_acc_us": round(min(ml) * 1e6, 2), "wire_bytes": len(mb)}
         rows.append(row)
         print(json.dumps(row), flush=True)
     if a.out:

@@ -51,11 +51,13 @@ enum MaskMode { MASK_NONE = 0, MASK_X = 1, MASK_Y = 2, MASK_BITS = 3 };
 
 // ---- per-channel reductions -> partial[c][rb] (channel-major, two arrays) ------------------
 // FWD: a += x, b += x*x.   BWD: dz = dy*mask; a += dz, b += dz*(x-mean)*invstd.
-// Each lane keeps 4 rows (up to 12 x 16 B) in flight before consuming them: one load per
-// iteration left these passes at 3.2-3.9 TB/s (profiles/bench_n1_steady_fusedbn.txt).
-template <bool BWD>
+// Each lane keeps UNR rows (up to 3*UNR x 16 B) in flight before consuming them: one load per
+// iteration left these passes at 3.2-3.9 TB/s (profiles/bench_n1_steady_fusedbn.txt).  The mask
+// mode is a template parameter so each variant only holds the registers it needs (the runtime
+// switch cost 186 VGPRs in the backward = 2 waves/SIMD; profiles/bn_regs.txt).
+template <bool BWD, int MODE>
 __device__ __forceinline__ void reduce_row(const float xv[8], const float* d, const float* yv, uint32_t mb,
-                                           int mask_mode, const float mu[8], const float is[8], const float sc[8],
+                                           const float mu[8], const float is[8], const float sc[8],
                                            const float sh[8], float sa[8], float sb[8]) {
   if (!BWD) {
 #pragma unroll
@@ -64,24 +66,27 @@ __device__ __forceinline__ void reduce_row(const float xv[8], const float* d, co
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float dz = d[j];
-      if (mask_mode == MASK_BITS) dz = ((mb >> j) & 1u) ? dz : 0.f;
-      else if (mask_mode == MASK_Y) dz = yv[j] > 0.f ? dz : 0.f;
-      else if (mask_mode == MASK_X) dz = fmaf(xv[j], sc[j], sh[j]) > 0.f ? dz : 0.f;
+      if (MODE == MASK_BITS) dz = ((mb >> j) & 1u) ? dz : 0.f;
+      else if (MODE == MASK_Y) dz = yv[j] > 0.f ? dz : 0.f;
+      else if (MODE == MASK_X) dz = fmaf(xv[j], sc[j], sh[j]) > 0.f ? dz : 0.f;
       sa[j] += dz;
       sb[j] = fmaf(dz, (xv[j] - mu[j]) * is[j], sb[j]);
     }
   }
 }
 
-template <bool BWD>
+template <bool BWD, int MODE, int UNR>
 __global__ __launch_bounds__(kBlock) void k_bn_reduce(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
                                                       const uint16_t* __restrict__ y,
-                                                      const uint8_t* __restrict__ mbits, int mask_mode,
+                                                      const uint8_t* __restrict__ mbits,
                                                       const float* __restrict__ mean, const float* __restrict__ invstd,
                                                       const float* __restrict__ scale, const float* __restrict__ shift,
                                                       int64_t M, int C, int64_t rows_per_wg, int nrb,
                                                       float* __restrict__ pa, float* __restrict__ pb) {
   __shared__ float la[kBlock * 8], lb[kBlock * 8];
+  constexpr bool need_y = BWD && MODE == MASK_Y;
+  constexpr bool need_b = BWD && MODE == MASK_BITS;
+  constexpr bool need_ss = BWD && MODE == MASK_X;
   const int G = C >> 3, R = kBlock / G;
   const int g = threadIdx.x % G, r = threadIdx.x / G;
   const int c0 = g * 8;
@@ -91,27 +96,26 @@ __global__ __launch_bounds__(kBlock) void k_bn_reduce(const uint16_t* __restrict
   if (BWD) {
     load8f(mean + c0, mu);
     load8f(invstd + c0, is);
-    if (mask_mode == MASK_X) { load8f(scale + c0, sc); load8f(shift + c0, sh); }
+    if (need_ss) { load8f(scale + c0, sc); load8f(shift + c0, sh); }
   }
-  const bool need_y = BWD && mask_mode == MASK_Y;
-  const bool need_b = BWD && mask_mode == MASK_BITS;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_wg;
   const int64_t r1 = min(M, r0 + rows_per_wg);
   int64_t row = r0 + r;
-  for (; row + 3 * (int64_t)R < r1; row += 4 * (int64_t)R) {
-    float xv[4][8], d[4][8], yv[4][8];
-    uint32_t mb[4] = {0u, 0u, 0u, 0u};
+  for (; row + (UNR - 1) * (int64_t)R < r1; row += UNR * (int64_t)R) {
+    float xv[UNR][8], d[BWD ? UNR : 1][8], yv[need_y ? UNR : 1][8];
+    uint32_t mb[UNR];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < UNR; ++u) {
       const int64_t rr = row + u * (int64_t)R;
       const int64_t off = rr * C + c0;
       load8(x + off, xv[u]);
-      if (BWD) load8(dy + off, d[u]);
-      if (need_y) load8(y + off, yv[u]);
-      if (need_b) mb[u] = mbits[rr * G + g];
+      if (BWD) load8(dy + off, d[BWD ? u : 0]);
+      if (need_y) load8(y + off, yv[need_y ? u : 0]);
+      mb[u] = need_b ? (uint32_t)mbits[rr * G + g] : 0u;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) reduce_row<BWD>(xv[u], d[u], yv[u], mb[u], mask_mode, mu, is, sc, sh, sa, sb);
+    for (int u = 0; u < UNR; ++u)
+      reduce_row<BWD, MODE>(xv[u], d[BWD ? u : 0], yv[need_y ? u : 0], mb[u], mu, is, sc, sh, sa, sb);
   }
   for (; row < r1; row += R) {
     const int64_t off = row * C + c0;
@@ -120,7 +124,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_reduce(const uint16_t* __restrict
     if (BWD) load8(dy + off, d);
     if (need_y) load8(y + off, yv);
     const uint32_t mb = need_b ? (uint32_t)mbits[row * G + g] : 0u;
-    reduce_row<BWD>(xv, d, yv, mb, mask_mode, mu, is, sc, sh, sa, sb);
+    reduce_row<BWD, MODE>(xv, d, yv, mb, mu, is, sc, sh, sa, sb);
   }
   // combine the R row lanes of each channel group through LDS
 #pragma unroll
@@ -245,14 +249,16 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_fwd(const uint16_t* __restr
 }
 
 // dx = a*dz + k1*x + k0, dz = dy * mask;  dres = dz (when a residual was fused)
+template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_bn_apply_bwd(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
                                                          const uint16_t* __restrict__ y,
-                                                         const uint8_t* __restrict__ mbits, int mask_mode,
+                                                         const uint8_t* __restrict__ mbits,
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ shift, const float* __restrict__ ca,
                                                          const float* __restrict__ ck1, const float* __restrict__ ck0,
                                                          uint16_t* __restrict__ dx, uint16_t* __restrict__ dres,
                                                          int64_t M, int C) {
+  constexpr int mask_mode = MODE;
   const int G = C >> 3;
   const int64_t V = M * (int64_t)G, stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -280,7 +286,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_bwd(const uint16_t* __restr
     for (int j = 0; j < 8; ++j) o[j] = fmaf(a[j], d[j], fmaf(k1[j], xv[j], k0[j]));
     store8(dx + off, o);
   };
-  const bool need_y = mask_mode == MASK_Y, need_b = mask_mode == MASK_BITS;
+  constexpr bool need_y = mask_mode == MASK_Y, need_b = mask_mode == MASK_BITS;
   int64_t v = v0;
   for (; v + stride < V; v += 2 * stride) {  // two vectors in flight per lane
     float d0[8], x0[8], y0[8], d1[8], x1[8], y1[8];
@@ -366,9 +372,9 @@ void bn_forward_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y,
                 "mask_out must be uint8[M*C/8]");
     mo = (uint8_t*)mask_out->data_ptr();
   }
-  hipLaunchKernelGGL(k_bn_reduce<false>, nrb, kBlock, 0, stream, (const uint16_t*)x.data_ptr(), nullptr, nullptr,
-                     nullptr, 0, nullptr, nullptr, nullptr, nullptr, M, (int)C, rows, nrb, part[0].data_ptr<float>(),
-                     part[1].data_ptr<float>());
+  hipLaunchKernelGGL((k_bn_reduce<false, MASK_NONE, 8>), nrb, kBlock, 0, stream, (const uint16_t*)x.data_ptr(),
+                     nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, (int)C, rows, nrb,
+                     part[0].data_ptr<float>(), part[1].data_ptr<float>());
   hipLaunchKernelGGL(k_bn_finalize_fwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, part[0].data_ptr<float>(),
                      part[1].data_ptr<float>(), nrb, (int)C, M, weight.data_ptr<float>(), bias.data_ptr<float>(),
                      (float)eps, (float)momentum, rm, rv, mean.data_ptr<float>(), invstd.data_ptr<float>(),
@@ -403,6 +409,7 @@ void bn_backward(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> y, int64
                  c10::optional<at::Tensor> dres, at::Tensor dweight, at::Tensor dbias, int64_t C,
                  c10::optional<at::Tensor> mask_in) {
   TORCH_CHECK(C % 8 == 0 && C <= kMaxC, "fused BN needs C % 8 == 0 and C <= 2048");
+  TORCH_CHECK(mask_mode >= MASK_NONE && mask_mode <= MASK_BITS, "bad mask mode");
   const int64_t M = x.numel() / C;
   check_act(dy, "dy", M * C);
   check_act(x, "x", M * C);
@@ -430,18 +437,34 @@ void bn_backward(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> y, int64
   auto part = at::empty({2, C, (int64_t)nrb}, weight.options());
   auto coef = at::empty({3, C}, weight.options());
   auto stream = c10::hip::getCurrentHIPStream();
-  hipLaunchKernelGGL(k_bn_reduce<true>, nrb, kBlock, 0, stream, (const uint16_t*)x.data_ptr(),
-                     (const uint16_t*)dy.data_ptr(), yp, mbp, (int)mask_mode, mean.data_ptr<float>(),
-                     invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(), M, (int)C, rows, nrb,
-                     part[0].data_ptr<float>(), part[1].data_ptr<float>());
+  auto red = [&](auto kern) {
+    hipLaunchKernelGGL(kern, nrb, kBlock, 0, stream, (const uint16_t*)x.data_ptr(), (const uint16_t*)dy.data_ptr(), yp,
+                       mbp, mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
+                       shift.data_ptr<float>(), M, (int)C, rows, nrb, part[0].data_ptr<float>(),
+                       part[1].data_ptr<float>());
+  };
+  switch (mask_mode) {
+    case MASK_NONE: red(k_bn_reduce<true, MASK_NONE, 4>); break;
+    case MASK_X: red(k_bn_reduce<true, MASK_X, 4>); break;
+    case MASK_Y: red(k_bn_reduce<true, MASK_Y, 4>); break;
+    default: red(k_bn_reduce<true, MASK_BITS, 4>); break;
+  }
   hipLaunchKernelGGL(k_bn_finalize_bwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, part[0].data_ptr<float>(),
                      part[1].data_ptr<float>(), nrb, (int)C, M, weight.data_ptr<float>(), mean.data_ptr<float>(),
                      invstd.data_ptr<float>(), dweight.data_ptr<float>(), dbias.data_ptr<float>(),
                      coef[0].data_ptr<float>(), coef[1].data_ptr<float>(), coef[2].data_ptr<float>());
-  hipLaunchKernelGGL(k_bn_apply_bwd, apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)dy.data_ptr(),
-                     (const uint16_t*)x.data_ptr(), yp, mbp, (int)mask_mode, scale.data_ptr<float>(),
-                     shift.data_ptr<float>(), coef[0].data_ptr<float>(), coef[1].data_ptr<float>(),
-                     coef[2].data_ptr<float>(), (uint16_t*)dx.data_ptr(), drp, M, (int)C);
+  auto app = [&](auto kern) {
+    hipLaunchKernelGGL(kern, apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)dy.data_ptr(),
+                       (const uint16_t*)x.data_ptr(), yp, mbp, scale.data_ptr<float>(), shift.data_ptr<float>(),
+                       coef[0].data_ptr<float>(), coef[1].data_ptr<float>(), coef[2].data_ptr<float>(),
+                       (uint16_t*)dx.data_ptr(), drp, M, (int)C);
+  };
+  switch (mask_mode) {
+    case MASK_NONE: app(k_bn_apply_bwd<MASK_NONE>); break;
+    case MASK_X: app(k_bn_apply_bwd<MASK_X>); break;
+    case MASK_Y: app(k_bn_apply_bwd<MASK_Y>); break;
+    default: app(k_bn_apply_bwd<MASK_BITS>); break;
+  }
 }
 
 }  // namespace hipps
