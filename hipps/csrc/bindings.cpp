@@ -39,6 +39,15 @@ void bn_backward(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> y, int64
                  at::Tensor mean, at::Tensor invstd, at::Tensor scale, at::Tensor shift, at::Tensor dx,
                  c10::optional<at::Tensor> dres, at::Tensor dweight, at::Tensor dbias, int64_t C,
                  c10::optional<at::Tensor> mask_in);
+void bn_forward_partials(at::Tensor part, int64_t nrb, at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y,
+                         at::Tensor weight, at::Tensor bias, c10::optional<at::Tensor> running_mean,
+                         c10::optional<at::Tensor> running_var, at::Tensor mean, at::Tensor invstd, at::Tensor scale,
+                         at::Tensor shift, int64_t C, double eps, double momentum, bool relu,
+                         c10::optional<at::Tensor> mask_out);
+// gemm.hip
+int64_t conv1x1_mtiles(int64_t M);
+void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part, int64_t Hi,
+                     int64_t Wi, int64_t stride);
 namespace rt {
 void bind_control(pybind11::module& m);
 void bind_ipc(pybind11::module& m);
@@ -65,6 +74,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_forward_train", &hipps::bn_forward_train, "fused channels-last BN train fwd (+res) (+relu)");
   m.def("bn_apply", &hipps::bn_apply, "y = act(x*scale + shift (+res))");
   m.def("bn_backward", &hipps::bn_backward, "fused BN bwd with relu-mask recompute (+dres)");
+  m.def("bn_forward_partials", &hipps::bn_forward_partials, "BN fwd finalize+apply from producer-reduced partials");
+  m.def("conv1x1_mtiles", &hipps::conv1x1_mtiles);
+  m.def("conv1x1_forward", &hipps::conv1x1_forward, "MFMA 1x1 conv (NHWC GEMM) with fused BN-stats epilogue");
   hipps::rt::bind_control(m);
   hipps::rt::bind_ipc(m);
   hipps::rt::bind_trace(m);

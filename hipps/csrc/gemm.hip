@@ -1,0 +1,264 @@
+// hipps — MFMA 1x1-convolution GEMM for channels-last bf16 activations, with the next
+// BatchNorm's batch statistics fused into the epilogue.
+//
+//   Y[M, N] = X[M, K] · W[N, K]^T      M = images*Ho*Wo rows, K = Cin, N = Cout
+//
+// A 1x1 convolution on NHWC memory is exactly this "NT" GEMM: both operands are K-contiguous,
+// so every MFMA fragment (8 consecutive k of one row, v_mfma_f32_16x16x32_bf16) is ONE 16-byte
+// LDS read.  The epilogue converts the fp32 accumulators to bf16, stages the tile through LDS
+// for full-line 16-byte stores, and (STATS) reduces per-output-channel sum / sum-of-squares of
+// the stored bf16 values into channel-major partials part[c][m_tile] -- the format the fused
+// BatchNorm finalize (norm.hip) consumes.  That removes the BN forward's separate read pass
+// over the convolution output (ResNet-50: 36 of 53 convolutions are 1x1).
+//
+// Tiling: 128 x BN x 64 (BN = 128 or 64), 4 waves (2x2 or 4x1), each wave a 64x64 / 32x64
+// sub-tile of 16x16 MFMA accumulators; two LDS stages with register prefetch (the global loads
+// of k-tile t+1 are in flight during the MFMAs of tile t; one barrier per k-tile).  LDS rows are
+// 128 B with a 16-byte-chunk XOR swizzle (chunk ^= row & 7) so the 16 rows a fragment read
+// touches spread over the banks.  Blocks are remapped so consecutive tiles (the N tiles of one
+// M tile, which share the X rows) land on the same XCD and hit its L2.
+// Strided 1x1 convolutions (ResNet downsample, stride 2) gather their rows in the A loader.
+#include "common.h"
+
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+namespace hipps {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // native vector: HIP uint4 is a struct
+
+constexpr int kGBM = 128, kGBK = 64;
+
+template <int BN> struct GemmCfg;
+template <> struct GemmCfg<128> { static constexpr int WM = 2, WN = 2; };
+template <> struct GemmCfg<64> { static constexpr int WM = 4, WN = 1; };
+
+template <int BN>
+constexpr int gemm_lds_elems() {
+  // max(2 stages of A+B tiles, epilogue tile with 8-element row pad) + stats scratch (floats)
+  constexpr int stage = 2 * (kGBM + BN) * kGBK;
+  constexpr int epi = kGBM * (BN + 8);
+  return (stage > epi ? stage : epi) + 2 * 2 * GemmCfg<BN>::WM * BN;
+}
+
+template <int BN, bool STATS>
+__global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W,
+                                                    uint16_t* __restrict__ Y, float* __restrict__ pa,
+                                                    float* __restrict__ pb, int M, int N, int K, int Ho, int Wo,
+                                                    int Hi, int Wi, int stride, int mtiles, int ntiles) {
+  constexpr int WM = GemmCfg<BN>::WM, WN = GemmCfg<BN>::WN;
+  constexpr int TM = kGBM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int A_CH = kGBM * kGBK / 8 / 256;  // 16-byte chunks per thread per stage
+  constexpr int B_CH = BN * kGBK / 8 / 256;
+  constexpr int STAGE = (kGBM + BN) * kGBK;  // elements
+  constexpr int EP = BN + 8;                 // epilogue row pitch (elements)
+  __shared__ __attribute__((aligned(16))) uint16_t lds[gemm_lds_elems<BN>()];
+
+  // XCD-aware tile order: hardware deals block ids round-robin to the 8 XCDs; give each XCD a
+  // contiguous range of logical tiles so the N tiles of one M tile share an L2.
+  int bid = blockIdx.x;
+  const int nblk = gridDim.x;
+  if ((nblk & 7) == 0) bid = (bid & 7) * (nblk >> 3) + (bid >> 3);
+  const int mt = bid / ntiles, nt = bid - mt * ntiles;
+  const int m0 = mt * kGBM, n0 = nt * BN;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = w / WN, wn = w % WN;
+  const int cchunk = t & 7;  // the 16-byte chunk (k/8) this thread stages, fixed
+
+  // per-thread A source rows (fixed over the K loop); rows past M load zeros
+  int64_t a_off[A_CH];
+  bool a_ok[A_CH];
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    const int row = (t >> 3) + 32 * i;
+    int m = m0 + row;
+    a_ok[i] = m < M;
+    m = a_ok[i] ? m : M - 1;
+    int64_t src = m;
+    if (stride != 1) {
+      const int hw = Ho * Wo;
+      const int img = m / hw, rem = m - img * hw;
+      const int ho = rem / Wo, wo = rem - ho * Wo;
+      src = ((int64_t)img * Hi + (int64_t)ho * stride) * Wi + (int64_t)wo * stride;
+    }
+    a_off[i] = src * K + cchunk * 8;
+  }
+  int64_t b_off[B_CH];
+#pragma unroll
+  for (int i = 0; i < B_CH; ++i) b_off[i] = (int64_t)(n0 + (t >> 3) + 32 * i) * K + cchunk * 8;
+
+  u32x4 ra[A_CH], rb[B_CH];
+  // (macros, not lambdas: a by-reference lambda capture of these arrays put them in scratch)
+#define HIPPS_GLOAD(kt_)                                                        \
+  {                                                                             \
+    const int k0_ = (kt_) * kGBK;                                               \
+    _Pragma("unroll") for (int i = 0; i < A_CH; ++i) {                          \
+      u32x4 v_ = *reinterpret_cast<const u32x4*>(X + a_off[i] + k0_);           \
+      ra[i] = a_ok[i] ? v_ : u32x4{0u, 0u, 0u, 0u};                             \
+    }                                                                           \
+    _Pragma("unroll") for (int i = 0; i < B_CH; ++i) rb[i] =                    \
+        *reinterpret_cast<const u32x4*>(W + b_off[i] + k0_);                    \
+  }
+#define HIPPS_SSTORE(s_)                                                                           \
+  {                                                                                                \
+    uint16_t* base_ = lds + (s_) * STAGE;                                                          \
+    _Pragma("unroll") for (int i = 0; i < A_CH; ++i) {                                             \
+      const int row_ = (t >> 3) + 32 * i;                                                          \
+      *reinterpret_cast<u32x4*>(base_ + row_ * kGBK + ((cchunk ^ (row_ & 7)) << 3)) = ra[i];       \
+    }                                                                                              \
+    _Pragma("unroll") for (int i = 0; i < B_CH; ++i) {                                             \
+      const int row_ = (t >> 3) + 32 * i;                                                          \
+      *reinterpret_cast<u32x4*>(base_ + kGBM * kGBK + row_ * kGBK + ((cchunk ^ (row_ & 7)) << 3)) = \
+          rb[i];                                                                                   \
+    }                                                                                              \
+  }
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int KT = K / kGBK;
+  HIPPS_GLOAD(0);
+  HIPPS_SSTORE(0);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) HIPPS_GLOAD(kt + 1);
+    const uint16_t* As = lds + cur * STAGE;
+    const uint16_t* Bs = As + kGBM * kGBK;
+#pragma unroll
+    for (int ks = 0; ks < kGBK / 32; ++ks) {
+      const int c = ks * 4 + (lane >> 4);
+      bf16x8 a[FM], b[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int row = wm * TM + i * 16 + (lane & 15);
+        a[i] = *reinterpret_cast<const bf16x8*>(As + row * kGBK + ((c ^ (row & 7)) << 3));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = wn * TN + j * 16 + (lane & 15);
+        b[j] = *reinterpret_cast<const bf16x8*>(Bs + row * kGBK + ((c ^ (row & 7)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < KT) HIPPS_SSTORE(cur ^ 1);
+    __syncthreads();
+  }
+
+#undef HIPPS_GLOAD
+#undef HIPPS_SSTORE
+  // ---- epilogue: bf16 tile -> LDS (padded rows), per-channel stats, 16-byte row stores ----
+  // C/D map (16x16x32): column = lane & 15, row = (lane >> 4) * 4 + r.
+  float* st = reinterpret_cast<float*>(lds + (2 * STAGE > kGBM * EP ? 2 * STAGE : kGBM * EP));
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col = wn * TN + j * 16 + (lane & 15);
+    float s = 0.f, q = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+        const uint16_t hb = f32_to_bf16(acc[i][j][r]);
+        lds[row * EP + col] = hb;
+        if (STATS) {
+          const float v = bf16_to_f32(hb);
+          s += v;
+          q = fmaf(v, v, q);
+        }
+      }
+    }
+    if (STATS) {
+      s += __shfl_xor(s, 16, 64);
+      q += __shfl_xor(q, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lane < 16) {
+        st[(wm * BN + col) * 2] = s;
+        st[(wm * BN + col) * 2 + 1] = q;
+      }
+    }
+  }
+  __syncthreads();
+  constexpr int RCH = BN / 8;  // 16-byte chunks per output row
+#pragma unroll
+  for (int i = 0; i < kGBM * RCH / 256; ++i) {
+    const int id = t + 256 * i;
+    const int row = id / RCH, c = id - row * RCH;
+    if (m0 + row < M)
+      *reinterpret_cast<uint4*>(Y + (int64_t)(m0 + row) * N + n0 + c * 8) =
+          *reinterpret_cast<const uint4*>(lds + row * EP + c * 8);
+  }
+  if (STATS && t < BN) {
+    float s = 0.f, q = 0.f;
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+      s += st[(i * BN + t) * 2];
+      q += st[(i * BN + t) * 2 + 1];
+    }
+    pa[(int64_t)(n0 + t) * mtiles + mt] = s;
+    pb[(int64_t)(n0 + t) * mtiles + mt] = q;
+  }
+}
+
+// ==========================================================================================
+int64_t conv1x1_mtiles(int64_t M) { return (M + kGBM - 1) / kGBM; }
+
+// x: [img, Cin, Hi, Wi] channels-last bf16; w: [Cout, Cin(,1,1)] bf16 contiguous;
+// y: [img, Cout, Ho, Wo] channels-last bf16.  part (optional): f32 [2, Cout, mtiles].
+void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part, int64_t Hi,
+                     int64_t Wi, int64_t stride) {
+  TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "conv1x1: device tensors");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
+                  y.scalar_type() == at::kBFloat16, "conv1x1: bf16 tensors");
+  const int64_t N = w.size(0), K = w.numel() / N;
+  TORCH_CHECK(w.is_contiguous(), "conv1x1: weight must be contiguous [Cout, Cin]");
+  TORCH_CHECK(K % kGBK == 0 && N % 64 == 0, "conv1x1: needs Cin % 64 == 0 and Cout % 64 == 0");
+  const int64_t imgs = x.numel() / (K * Hi * Wi);
+  TORCH_CHECK(imgs * K * Hi * Wi == x.numel(), "conv1x1: x size");
+  const int64_t Ho = (Hi - 1) / stride + 1, Wo = (Wi - 1) / stride + 1;
+  const int64_t M = imgs * Ho * Wo;
+  TORCH_CHECK(y.numel() == M * N, "conv1x1: y size");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) || x.dim() != 4, "conv1x1: x must be channels-last");
+  TORCH_CHECK(y.is_contiguous(at::MemoryFormat::ChannelsLast) || y.dim() != 4, "conv1x1: y must be channels-last");
+  for (const at::Tensor* t : {&x, &w, &y})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "conv1x1: 16-byte aligned tensors");
+  TORCH_CHECK(M < (int64_t(1) << 31) && x.numel() < (int64_t(1) << 40), "conv1x1: size");
+  const int64_t mtiles = conv1x1_mtiles(M);
+  const bool bn128 = N % 128 == 0;
+  const int64_t ntiles = N / (bn128 ? 128 : 64);
+  const int64_t nblk = mtiles * ntiles;
+  TORCH_CHECK(nblk < (int64_t(1) << 31), "conv1x1: grid");
+  float *pa = nullptr, *pb = nullptr;
+  if (part.has_value() && part->defined()) {
+    TORCH_CHECK(part->is_cuda() && part->scalar_type() == at::kFloat && part->is_contiguous() &&
+                    part->numel() == 2 * N * mtiles, "conv1x1: part must be f32 [2, Cout, mtiles]");
+    pa = part->data_ptr<float>();
+    pb = pa + N * mtiles;
+  }
+  auto stream = c10::hip::getCurrentHIPStream();
+  const uint16_t* xp = (const uint16_t*)x.data_ptr();
+  const uint16_t* wp = (const uint16_t*)w.data_ptr();
+  uint16_t* yp = (uint16_t*)y.data_ptr();
+#define HIPPS_C1(BNv, ST)                                                                                  \
+  hipLaunchKernelGGL((k_conv1x1_nt<BNv, ST>), (int)nblk, 256, 0, stream, xp, wp, yp, pa, pb, (int)M, (int)N, \
+                     (int)K, (int)Ho, (int)Wo, (int)Hi, (int)Wi, (int)stride, (int)mtiles, (int)ntiles)
+  if (bn128) {
+    if (pa) HIPPS_C1(128, true); else HIPPS_C1(128, false);
+  } else {
+    if (pa) HIPPS_C1(64, true); else HIPPS_C1(64, false);
+  }
+#undef HIPPS_C1
+}
+
+}  // namespace hipps

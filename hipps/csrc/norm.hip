@@ -338,6 +338,24 @@ int apply_grid(int64_t M, int C) {
 }
 }  // namespace
 
+namespace {
+// forward finalize (stats -> running stats, scale/shift) + apply, from channel-major partials
+void finalize_apply_fwd(const at::Tensor& part, int nrb, const at::Tensor& x, const uint16_t* rp, at::Tensor& y,
+                        uint8_t* mo, at::Tensor& weight, at::Tensor& bias, float* rm, float* rv, at::Tensor& mean,
+                        at::Tensor& invstd, at::Tensor& scale, at::Tensor& shift, int64_t M, int64_t C, double eps,
+                        double momentum, bool relu, hipStream_t stream) {
+  const float* pa = part.data_ptr<float>();
+  const float* pb = pa + C * (int64_t)nrb;
+  hipLaunchKernelGGL(k_bn_finalize_fwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, pa, pb, nrb, (int)C, M,
+                     weight.data_ptr<float>(), bias.data_ptr<float>(), (float)eps, (float)momentum, rm, rv,
+                     mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
+                     shift.data_ptr<float>());
+  hipLaunchKernelGGL(k_bn_apply_fwd, apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)x.data_ptr(), rp,
+                     (uint16_t*)y.data_ptr(), mo, scale.data_ptr<float>(), shift.data_ptr<float>(), M, (int)C,
+                     (int)relu);
+}
+}  // namespace
+
 // x: [M, C] bf16 view (channels-last storage).  Returns nothing; fills y, mean, invstd,
 // scale, shift and updates running stats in place.
 void bn_forward_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, at::Tensor weight, at::Tensor bias,
@@ -375,13 +393,8 @@ void bn_forward_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y,
   hipLaunchKernelGGL((k_bn_reduce<false, MASK_NONE, 8>), nrb, kBlock, 0, stream, (const uint16_t*)x.data_ptr(),
                      nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, (int)C, rows, nrb,
                      part[0].data_ptr<float>(), part[1].data_ptr<float>());
-  hipLaunchKernelGGL(k_bn_finalize_fwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, part[0].data_ptr<float>(),
-                     part[1].data_ptr<float>(), nrb, (int)C, M, weight.data_ptr<float>(), bias.data_ptr<float>(),
-                     (float)eps, (float)momentum, rm, rv, mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                     scale.data_ptr<float>(), shift.data_ptr<float>());
-  hipLaunchKernelGGL(k_bn_apply_fwd, apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)x.data_ptr(), rp,
-                     (uint16_t*)y.data_ptr(), mo, scale.data_ptr<float>(), shift.data_ptr<float>(), M, (int)C,
-                     (int)relu);
+  finalize_apply_fwd(part, nrb, x, rp, y, mo, weight, bias, rm, rv, mean, invstd, scale, shift, M, C, eps, momentum,
+                     relu, stream);
 }
 
 // eval / affine-only apply with given scale/shift
@@ -467,4 +480,43 @@ void bn_backward(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> y, int64
   }
 }
 
+}  // namespace hipps
+
+namespace hipps {
+// Forward BN whose batch statistics were already reduced by the producer (conv1x1 epilogue):
+// part = f32 [2, C, nrb] channel-major partial sums / sums of squares.
+void bn_forward_partials(at::Tensor part, int64_t nrb, at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y,
+                         at::Tensor weight, at::Tensor bias, c10::optional<at::Tensor> running_mean,
+                         c10::optional<at::Tensor> running_var, at::Tensor mean, at::Tensor invstd, at::Tensor scale,
+                         at::Tensor shift, int64_t C, double eps, double momentum, bool relu,
+                         c10::optional<at::Tensor> mask_out) {
+  TORCH_CHECK(C % 8 == 0 && C <= kMaxC && C >= 8, "fused BN needs C % 8 == 0 and 8 <= C <= 2048");
+  const int64_t M = x.numel() / C;
+  check_act(x, "x", M * C);
+  check_act(y, "y", M * C);
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.numel() == 2 * C * nrb,
+              "part must be f32 [2, C, nrb]");
+  const uint16_t* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_act(*res, "residual", M * C);
+    rp = (const uint16_t*)res->data_ptr();
+  }
+  for (auto* t : {&weight, &bias, &mean, &invstd, &scale, &shift}) check_vec(*t, "per-channel vector", (int)C);
+  float* rm = nullptr;
+  float* rv = nullptr;
+  if (running_mean.has_value() && running_mean->defined()) {
+    check_vec(*running_mean, "running_mean", (int)C);
+    check_vec(*running_var, "running_var", (int)C);
+    rm = running_mean->data_ptr<float>();
+    rv = running_var->data_ptr<float>();
+  }
+  uint8_t* mo = nullptr;
+  if (mask_out.has_value() && mask_out->defined()) {
+    TORCH_CHECK(mask_out->is_cuda() && mask_out->scalar_type() == at::kByte && mask_out->numel() == M * C / 8,
+                "mask_out must be uint8[M*C/8]");
+    mo = (uint8_t*)mask_out->data_ptr();
+  }
+  finalize_apply_fwd(part, (int)nrb, x, rp, y, mo, weight, bias, rm, rv, mean, invstd, scale, shift, M, C, eps,
+                     momentum, relu, c10::hip::getCurrentHIPStream());
+}
 }  // namespace hipps

@@ -14,13 +14,15 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from hipps.ops.nn import FusedBatchNorm2d
+from hipps.ops.nn import FusedBatchNorm2d, conv_bn
 
 # One switch for the whole zoo: fused BN(+residual)(+ReLU) HIP kernels on channels-last bf16,
 # standard PyTorch elsewhere.  HIPPS_FUSED_BN=0 restores the eager MIOpen path for A/B runs.
 import os as _os
 
 _FUSED = _os.environ.get("HIPPS_FUSED_BN", "1") != "0"
+# 1x1 convolutions feeding a fused BN: MFMA GEMM with the BN statistics in its epilogue
+_FUSED_CONV = _FUSED and _os.environ.get("HIPPS_FUSED_CONV", "1") != "0"
 
 
 def _bn(c, relu=False):
@@ -48,10 +50,11 @@ class Bottleneck(nn.Module):
             self.downsample = nn.Sequential(_conv(cin, cout, 1, stride=stride), _bn(cout))
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
-        y = self.bn1(self.conv1(x))
+        ds = self.downsample
+        idt = x if ds is None else conv_bn(ds[0], ds[1], x, fuse=_FUSED_CONV)
+        y = conv_bn(self.conv1, self.bn1, x, fuse=_FUSED_CONV)
         y = self.bn2(self.conv2(y))
-        return self.bn3(self.conv3(y), residual=idt)
+        return conv_bn(self.conv3, self.bn3, y, residual=idt, fuse=_FUSED_CONV)
 
 
 class BasicBlock(nn.Module):

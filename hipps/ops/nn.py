@@ -1,5 +1,8 @@
 """Fused model ops backed by hipps HIP kernels.
 
+``conv_bn`` runs a 1x1 convolution feeding such a BN as an MFMA GEMM whose epilogue emits the
+BN batch statistics (hipps/csrc/gemm.hip).
+
 ``FusedBatchNorm2d`` is a drop-in ``nn.BatchNorm2d`` that can also apply a residual add and a
 ReLU in the same pass (``forward(x, residual=None)``).  On a HIP device with a channels-last
 bf16 input (the autocast ResNet path) it runs hipps/csrc/norm.hip: one statistics pass, one
@@ -18,9 +21,56 @@ from ._native import native
 MASK_NONE, MASK_X, MASK_Y, MASK_BITS = 0, 1, 2, 3
 
 
+class _Conv1x1(torch.autograd.Function):
+    """1x1 convolution on channels-last bf16 as an MFMA GEMM (hipps/csrc/gemm.hip) that also
+    emits the per-channel batch statistics of its output for the BatchNorm that follows.
+    Backward: MIOpen (aten.convolution_backward) on the saved bf16 input and weight."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride):
+        N, Cin, H, W = x.shape
+        Cout = w.shape[0]
+        Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+        y = torch.empty((N, Cout, Ho, Wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        mt = native().conv1x1_mtiles(N * Ho * Wo)
+        part = torch.empty((2, Cout, mt), dtype=torch.float32, device=x.device)
+        native().conv1x1_forward(x, w.reshape(Cout, Cin), y, part, H, W, stride)
+        ctx.stride = stride
+        ctx.save_for_backward(x, w)
+        ctx.mark_non_differentiable(part)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, dy, _dpart):
+        x, w = ctx.saved_tensors
+        s = ctx.stride
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        need = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False]
+        dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
+                                                        need)
+        return dx, dw, None
+
+
+def conv1x1_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    """Can the MFMA 1x1 path run this convolution on this input?"""
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and
+            x.is_contiguous(memory_format=torch.channels_last)):
+        return False
+    if conv.kernel_size != (1, 1) or conv.padding != (0, 0) or conv.dilation != (1, 1) or conv.groups != 1:
+        return False
+    if conv.bias is not None or conv.stride[0] != conv.stride[1]:
+        return False
+    return conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0
+
+
+def conv1x1_stats(x, weight, stride=1):
+    """(y, part): bf16 1x1 conv output and its [2, Cout, m_tiles] BN partial statistics."""
+    return _Conv1x1.apply(x, weight.to(torch.bfloat16), int(stride))
+
+
 class _FusedBNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, weight, bias, running_mean, running_var, eps, momentum, relu):
+    def forward(ctx, x, res, weight, bias, running_mean, running_var, eps, momentum, relu, part=None):
         C = x.shape[1]
         y = torch.empty_like(x, memory_format=torch.channels_last)
         f32 = dict(dtype=torch.float32, device=x.device)
@@ -30,8 +80,12 @@ class _FusedBNAct(torch.autograd.Function):
         # re-reading the bf16 output in the backward
         mode = MASK_NONE if not relu else (MASK_BITS if res is not None else MASK_X)
         mask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device) if mode == MASK_BITS else None
-        native().bn_forward_train(x, res, y, weight, bias, running_mean, running_var, mean, invstd, scale, shift, C,
-                                  float(eps), float(momentum), bool(relu), mask)
+        if part is not None:  # statistics already reduced by the producing 1x1 conv
+            native().bn_forward_partials(part, part.shape[2], x, res, y, weight, bias, running_mean, running_var,
+                                         mean, invstd, scale, shift, C, float(eps), float(momentum), bool(relu), mask)
+        else:
+            native().bn_forward_train(x, res, y, weight, bias, running_mean, running_var, mean, invstd, scale, shift,
+                                      C, float(eps), float(momentum), bool(relu), mask)
         ctx.mode, ctx.C, ctx.has_res = mode, C, res is not None
         ctx.save_for_backward(x, mask, weight, mean, invstd, scale, shift)
         return y
@@ -45,12 +99,14 @@ class _FusedBNAct(torch.autograd.Function):
         dw = torch.empty_like(weight)
         db = torch.empty_like(weight)
         native().bn_backward(dy, x, None, ctx.mode, weight, mean, invstd, scale, shift, dx, dres, dw, db, ctx.C, mask)
-        return dx, dres, dw, db, None, None, None, None, None
+        return dx, dres, dw, db, None, None, None, None, None, None
 
 
-def fused_bn_act(x, weight, bias, running_mean, running_var, eps=1e-5, momentum=0.1, relu=True, residual=None):
-    """Training-mode BN (+residual) (+ReLU) on a channels-last bf16 HIP tensor."""
-    return _FusedBNAct.apply(x, residual, weight, bias, running_mean, running_var, eps, momentum, relu)
+def fused_bn_act(x, weight, bias, running_mean, running_var, eps=1e-5, momentum=0.1, relu=True, residual=None,
+                 part=None):
+    """Training-mode BN (+residual) (+ReLU) on a channels-last bf16 HIP tensor.  ``part``: the
+    [2, C, nrb] partial statistics when the producer (conv1x1_stats) already reduced them."""
+    return _FusedBNAct.apply(x, residual, weight, bias, running_mean, running_var, eps, momentum, relu, part)
 
 
 class FusedBatchNorm2d(nn.BatchNorm2d):
@@ -89,12 +145,12 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
             return False
         return True
 
-    def forward(self, x, residual=None):
+    def forward(self, x, residual=None, stats=None):
         if self._fast_ok(x, residual):
             if self.training:
                 self._nbt_pending += 1
                 return fused_bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, self.eps,
-                                    self.momentum, self.relu, residual)
+                                    self.momentum, self.relu, residual, stats)
             if not torch.is_grad_enabled() or not (x.requires_grad or (residual is not None and
                                                                        residual.requires_grad)):
                 scale = self.weight / torch.sqrt(self.running_var + self.eps)
@@ -109,3 +165,14 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
         if self.relu:
             y = F.relu(y)
         return y
+
+
+def conv_bn(conv: nn.Conv2d, bn: FusedBatchNorm2d, x, residual=None, fuse: bool = True):
+    """bn(conv(x), residual): a 1x1 conv that feeds a training-mode fused BN runs as the MFMA GEMM
+    with the BN statistics in its epilogue (one fewer pass over the conv output)."""
+    if fuse and bn.training and conv1x1_ok(conv, x):
+        y, part = conv1x1_stats(x, conv.weight, conv.stride[0])
+        if bn._fast_ok(y, residual):
+            return bn(y, residual, stats=part)
+        return bn(y, residual)
+    return bn(conv(x), residual)

@@ -1,4 +1,9 @@
-"""MIOpen 1x1 conv vs hipBLASLt GEMM (channels-last view) for ResNet-50 1x1 shapes, fwd+bwd, bf16."""
+"""Microbenchmark: ResNet-50 1x1 convolutions (bs 256, channels-last bf16), forward.
+
+  miopen        F.conv2d (MIOpen)                        -> y
+  miopen+stats  F.conv2d + the fused-BN statistics pass  (what the unfused path pays)
+  hipps         MFMA GEMM with BN statistics in the epilogue (hipps/csrc/gemm.hip)
+"""
 import json
 import os
 import sys
@@ -8,15 +13,17 @@ import torch.nn.functional as F
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-torch.backends.cudnn.benchmark = True
+from hipps.ops import nn as hnn  # noqa: E402
+from hipps.ops._native import native  # noqa: E402
 
-# (N, Cin, H, W, Cout) for the bottleneck 1x1 convs (stride 1) at bs256
-SHAPES = [(256, 64, 56, 56, 64), (256, 64, 56, 56, 256), (256, 256, 56, 56, 64), (256, 256, 56, 56, 128),
-          (256, 128, 28, 28, 512), (256, 512, 28, 28, 128), (256, 512, 28, 28, 256), (256, 256, 14, 14, 1024),
-          (256, 1024, 14, 14, 256), (256, 1024, 14, 14, 512), (256, 512, 7, 7, 2048), (256, 2048, 7, 7, 512)]
+SHAPES = [  # (Cin, H, Cout, stride) at batch 256
+    (64, 56, 64, 1), (64, 56, 256, 1), (256, 56, 64, 1), (256, 56, 128, 1), (256, 56, 512, 2),
+    (128, 28, 512, 1), (512, 28, 128, 1), (512, 28, 256, 1), (512, 28, 1024, 2),
+    (256, 14, 1024, 1), (1024, 14, 256, 1), (1024, 14, 512, 1), (1024, 14, 2048, 2),
+    (512, 7, 2048, 1), (2048, 7, 512, 1)]
 
 
-def timeit(fn, it=20):
+def timeit(fn, it=30):
     for _ in range(5):
         fn()
     s, e = torch.cuda.Event(True), torch.cuda.Event(True)
@@ -28,55 +35,39 @@ def timeit(fn, it=20):
     return s.elapsed_time(e) / it
 
 
-class GemmConv1x1(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, w):  # x NHWC-contiguous [N,C,H,W] channels_last, w [Co, Ci, 1, 1]
-        N, C, H, W = x.shape
-        x2 = x.permute(0, 2, 3, 1).reshape(-1, C)
-        w2 = w.view(w.shape[0], C)
-        y2 = x2 @ w2.t()
-        ctx.save_for_backward(x2, w2)
-        ctx.shape = (N, H, W)
-        return y2.view(N, H, W, -1).permute(0, 3, 1, 2)
-
-    @staticmethod
-    def backward(ctx, dy):
-        x2, w2 = ctx.saved_tensors
-        N, H, W = ctx.shape
-        dy2 = dy.permute(0, 2, 3, 1).reshape(-1, dy.shape[1])
-        dx = (dy2 @ w2).view(N, H, W, -1).permute(0, 3, 1, 2)
-        dw = (dy2.t() @ x2).view(w2.shape[0], w2.shape[1], 1, 1)
-        return dx, dw
-
-
-tot = {"miopen": 0.0, "gemm": 0.0}
 rows = []
-for N, Ci, H, W, Co in SHAPES:
-    x = torch.randn(N, Ci, H, W, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    w = torch.randn(Co, Ci, 1, 1, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    g = torch.randn(N, Co, H, W, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    xr = x.clone().requires_grad_(True)
-    wr = w.clone().requires_grad_(True)
+for cin, h, cout, st in SHAPES:
+    x = torch.randn(256, cin, h, h, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(cout, cin, 1, 1, device="cuda") / cin ** 0.5).to(torch.bfloat16)
+    ho = (h - 1) // st + 1
+    M = 256 * ho * ho
+    y = torch.empty(256, cout, ho, ho, dtype=torch.bfloat16, device="cuda").contiguous(memory_format=torch.channels_last)
+    mt = native().conv1x1_mtiles(M)
+    part = torch.empty(2, cout, mt, device="cuda")
+    f32 = dict(device="cuda", dtype=torch.float32)
+    bw, bb = torch.ones(cout, **f32), torch.zeros(cout, **f32)
+    rm, rv = torch.zeros(cout, **f32), torch.ones(cout, **f32)
+    mean, inv, sc, sh = (torch.empty(cout, **f32) for _ in range(4))
+    yb = torch.empty_like(y)
 
-    def conv():
-        y = F.conv2d(xr, wr)
-        y.backward(g)
-
-    def gemm():
-        y = GemmConv1x1.apply(xr, wr)
-        y.backward(g)
-
-    # correctness
-    y1 = F.conv2d(x.float(), w.float())
-    y2 = GemmConv1x1.apply(x, w).float()
-    err = ((y1 - y2).abs().max() / y1.abs().max()).item()
-    tc, tg = timeit(conv), timeit(gemm)
-    fl = 3 * 2 * N * H * W * Ci * Co
-    r = {"shape": [N, Ci, H, W, Co], "miopen_ms": round(tc, 3), "gemm_ms": round(tg, 3),
-         "miopen_TF": round(fl / tc / 1e9, 1), "gemm_TF": round(fl / tg / 1e9, 1), "relerr": err}
-    tot["miopen"] += tc
-    tot["gemm"] += tg
+    t_mi = timeit(lambda: F.conv2d(x, w, stride=st))
+    t_mi_bn = timeit(lambda: native().bn_forward_train(F.conv2d(x, w, stride=st), None, yb, bw, bb, rm, rv, mean, inv,
+                                                       sc, sh, cout, 1e-5, 0.1, True, None))
+    t_h = timeit(lambda: native().conv1x1_forward(x, w.view(cout, cin), y, part, h, h, st))
+    t_h_bn = timeit(lambda: (native().conv1x1_forward(x, w.view(cout, cin), y, part, h, h, st),
+                             native().bn_forward_partials(part, mt, y, None, yb, bw, bb, rm, rv, mean, inv, sc, sh,
+                                                          cout, 1e-5, 0.1, True, None)))
+    flops = 2.0 * M * cin * cout
+    byts = (256 * cin * h * h + M * cout) * 2
+    ref = F.conv2d(x, w, stride=st)
+    err = ((y.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
+    r = {"cin": cin, "hw": h, "cout": cout, "stride": st, "miopen_ms": round(t_mi, 4), "hipps_ms": round(t_h, 4),
+         "miopen_plus_bn_ms": round(t_mi_bn, 4), "hipps_plus_bn_ms": round(t_h_bn, 4),
+         "hipps_TFLOPs": round(flops / t_h / 1e9, 1), "hipps_TBps": round(byts / t_h / 1e9, 2),
+         "rel_err": round(err, 5)}
     rows.append(r)
     print(json.dumps(r), flush=True)
-print(json.dumps({"total_ms": tot}))
-json.dump(rows, open(os.path.join(ROOT, "gpurun_out/conv1x1.json"), "w"), indent=1)
+tot = {k: round(sum(r[k] for r in rows), 3) for k in ("miopen_ms", "hipps_ms", "miopen_plus_bn_ms", "hipps_plus_bn_ms")}
+print(json.dumps({"total": tot}))
+os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+json.dump({"rows": rows, "total": tot}, open(os.path.join(ROOT, "gpurun_out/bench_conv1x1.json"), "w"), indent=1)
