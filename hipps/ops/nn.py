@@ -24,7 +24,9 @@ MASK_NONE, MASK_X, MASK_Y, MASK_BITS = 0, 1, 2, 3
 class _Conv1x1(torch.autograd.Function):
     """1x1 convolution on channels-last bf16 as an MFMA GEMM (hipps/csrc/gemm.hip) that also
     emits the per-channel batch statistics of its output for the BatchNorm that follows.
-    Backward: MIOpen (aten.convolution_backward) on the saved bf16 input and weight."""
+    Backward: the input gradient of a stride-1 conv is the same NT GEMM against the transposed
+    weight (dX[M,Cin] = dY[M,Cout] . W[Cout,Cin]); the weight gradient (and strided dgrad)
+    go to MIOpen (aten.convolution_backward)."""
 
     @staticmethod
     def forward(ctx, x, w, stride):
@@ -45,9 +47,17 @@ class _Conv1x1(torch.autograd.Function):
         x, w = ctx.saved_tensors
         s = ctx.stride
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        need = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False]
-        dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
-                                                        need)
+        dx = dw = None
+        own_dx = ctx.needs_input_grad[0] and s == 1
+        need = [ctx.needs_input_grad[0] and not own_dx, ctx.needs_input_grad[1], False]
+        if any(need):
+            dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
+                                                            need)
+        if own_dx:
+            cout, cin = w.shape[0], w.shape[1]
+            wt = w.reshape(cout, cin).t().contiguous()  # [Cin, Cout]: K-contiguous B operand
+            dx = torch.empty_like(x, memory_format=torch.channels_last)
+            native().conv1x1_forward(dy, wt, dx, None, x.shape[2], x.shape[3], 1)
         return dx, dw, None
 
 

@@ -64,13 +64,13 @@ def test_conv_bn_autograd_matches_unfused(residual, stride):
     x0 = _cl(torch.randn(4, cin, 14, 14, device=DEV).to(torch.bfloat16))
     ho = (14 - 1) // stride + 1
     res = _cl(torch.randn(4, cout, ho, ho, device=DEV).to(torch.bfloat16)) if residual else None
+    g = _cl(torch.randn(4, cout, ho, ho, device=DEV).to(torch.bfloat16))
     outs = []
     for fuse, bn in ((True, bn_a), (False, bn_b)):
         conv.zero_grad(set_to_none=True)
         x = x0.clone().requires_grad_(True)
         with torch.autocast("cuda", dtype=torch.bfloat16):
             y = hnn.conv_bn(conv, bn, x, residual=res, fuse=fuse)
-        g = torch.randn_like(y)
         y.backward(g)
         outs.append((y.float(), x.grad.float(), conv.weight.grad.clone(), bn.weight.grad.clone(),
                      bn.running_mean.clone(), bn.running_var.clone()))

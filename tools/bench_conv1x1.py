@@ -57,6 +57,18 @@ for cin, h, cout, st in SHAPES:
     t_h_bn = timeit(lambda: (native().conv1x1_forward(x, w.view(cout, cin), y, part, h, h, st),
                              native().bn_forward_partials(part, mt, y, None, yb, bw, bb, rm, rv, mean, inv, sc, sh,
                                                           cout, 1e-5, 0.1, True, None)))
+    # backward input gradient (stride 1): MIOpen dgrad vs the same GEMM on the transposed weight
+    t_mi_dg = t_h_dg = None
+    if st == 1:
+        dy = torch.randn_like(y)
+        wt = w.view(cout, cin).t().contiguous()
+        dx = torch.empty_like(x)
+        t_mi_dg = timeit(lambda: torch.ops.aten.convolution_backward(dy, x, w, None, [1, 1], [0, 0], [1, 1], False,
+                                                                     [0, 0], 1, [True, False, False]))
+        t_h_dg = timeit(lambda: native().conv1x1_forward(dy, wt, dx, None, h, h, 1))
+        ref_dx = torch.ops.aten.convolution_backward(dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                                     [True, False, False])[0]
+        dg_err = ((dx.float() - ref_dx.float()).abs().max() / ref_dx.float().abs().max()).item()
     flops = 2.0 * M * cin * cout
     byts = (256 * cin * h * h + M * cout) * 2
     ref = F.conv2d(x, w, stride=st)
@@ -64,10 +76,14 @@ for cin, h, cout, st in SHAPES:
     r = {"cin": cin, "hw": h, "cout": cout, "stride": st, "miopen_ms": round(t_mi, 4), "hipps_ms": round(t_h, 4),
          "miopen_plus_bn_ms": round(t_mi_bn, 4), "hipps_plus_bn_ms": round(t_h_bn, 4),
          "hipps_TFLOPs": round(flops / t_h / 1e9, 1), "hipps_TBps": round(byts / t_h / 1e9, 2),
-         "rel_err": round(err, 5)}
+         "rel_err": round(err, 5),
+         "miopen_dgrad_ms": None if t_mi_dg is None else round(t_mi_dg, 4),
+         "hipps_dgrad_ms": None if t_h_dg is None else round(t_h_dg, 4),
+         "dgrad_rel_err": None if t_h_dg is None else round(dg_err, 5)}
     rows.append(r)
     print(json.dumps(r), flush=True)
-tot = {k: round(sum(r[k] for r in rows), 3) for k in ("miopen_ms", "hipps_ms", "miopen_plus_bn_ms", "hipps_plus_bn_ms")}
+tot = {k: round(sum(r[k] or 0 for r in rows), 3) for k in ("miopen_ms", "hipps_ms", "miopen_plus_bn_ms",
+                                                          "hipps_plus_bn_ms", "miopen_dgrad_ms", "hipps_dgrad_ms")}
 print(json.dumps({"total": tot}))
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 json.dump({"rows": rows, "total": tot}, open(os.path.join(ROOT, "gpurun_out/bench_conv1x1.json"), "w"), indent=1)
