@@ -48,6 +48,7 @@ void bn_forward_partials(at::Tensor part, int64_t nrb, at::Tensor x, c10::option
 int64_t conv1x1_mtiles(int64_t M);
 void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part, int64_t Hi,
                      int64_t Wi, int64_t stride);
+void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64_t Wi, int64_t stride);
 namespace rt {
 void bind_control(pybind11::module& m);
 void bind_ipc(pybind11::module& m);
@@ -77,6 +78,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_forward_partials", &hipps::bn_forward_partials, "BN fwd finalize+apply from producer-reduced partials");
   m.def("conv1x1_mtiles", &hipps::conv1x1_mtiles);
   m.def("conv1x1_forward", &hipps::conv1x1_forward, "MFMA 1x1 conv (NHWC GEMM) with fused BN-stats epilogue");
+  m.def("conv1x1_wgrad", &hipps::conv1x1_wgrad, "MFMA 1x1 conv weight gradient (tr_b16 LDS reads, split-M)");
   hipps::rt::bind_control(m);
   hipps::rt::bind_ipc(m);
   hipps::rt::bind_trace(m);

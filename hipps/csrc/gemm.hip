@@ -211,6 +211,147 @@ __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__
   }
 }
 
+
+// ==========================================================================================
+// Weight gradient:  dW[N][K] = sum_m dY[m][N] * X[src(m)][K]   (reduction over the M rows)
+//
+// Both operands arrive M-major (row m, channels contiguous), but an MFMA fragment wants 8
+// consecutive REDUCTION indices (m) per lane.  The tiles are staged row-major in LDS and read
+// back with gfx950's transposing ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses
+// row q / columns 4p..4p+3 and lane i receives column i of the 4 rows -- exactly the 16x16x32
+// A/B lane map (row = lane&15, k = 8*(lane>>4) + j) after two reads (rows +0..3, +4..7).
+// LDS rows are 256 B (128 channels) with the XOR chunk swizzle
+// ch ^ (((row&3)<<2) | ((row>>2)&3)) so the transposed reads spread over the banks.
+// The M range is split into S chunks (S * tiles ~ 2048 blocks); each block writes an fp32
+// partial tile and a second kernel sums the S partials in a fixed order (deterministic).
+constexpr int kWT = 128, kWMS = 64;  // output tile kWT x kWT; m rows per LDS stage
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int wg_off(int row, int ch) {  // byte offset in a [rows][128 x bf16] tile
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+__device__ __forceinline__ bf16x8 tr_frag(const uint8_t* tile, int row0, int col0, int lane) {
+  // rows row0 + 8*(lane>>4) + {0..3, 4..7}, columns col0 .. col0+15 (col0 % 16 == 0)
+  const int il = lane & 15, q = il >> 2, p = il & 3;
+  const int r = row0 + 8 * (lane >> 4) + q;
+  const int ch = (col0 >> 3) + (p >> 1);
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + wg_off(r, ch) + 8 * (p & 1)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + wg_off(r + 4, ch) + 8 * (p & 1)));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+__global__ __launch_bounds__(256) void k_conv1x1_wgrad(const uint16_t* __restrict__ dY, const uint16_t* __restrict__ X,
+                                                       float* __restrict__ part, int M, int N, int K, int Ho, int Wo,
+                                                       int Hi, int Wi, int stride, int chunk, int tn, int tk) {
+  constexpr int TILE = kWMS * kWT;  // elements of one operand tile
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * TILE];  // 2 stages x (dY, X)
+  int bid = blockIdx.x;
+  const int nblk = gridDim.x;
+  if ((nblk & 7) == 0) bid = (bid & 7) * (nblk >> 3) + (bid >> 3);  // M chunk's tiles share an XCD
+  const int tiles = tn * tk;
+  const int sidx = bid / tiles, tile = bid - sidx * tiles;
+  const int n0 = (tile / tk) * kWT, k0 = (tile % tk) * kWT;
+  const int mbeg = sidx * chunk, mend = min(M, mbeg + chunk);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wn = w >> 1, wk = w & 1;  // 2x2 waves, 64x64 each
+  const int ch = t & 15;              // staged 16-byte chunk (8 channels), fixed
+  const bool n_ok = n0 + ch * 8 < N, k_ok = k0 + ch * 8 < K;
+
+  u32x4 ry[4], rx[4];
+#define HIPPS_WLOAD(mb_)                                                                           \
+  {                                                                                                \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                \
+      const int m_ = (mb_) + (t >> 4) + 16 * i;                                                   \
+      const bool ok_ = m_ < mend;                                                                  \
+      const int mc_ = ok_ ? m_ : mbeg;                                                             \
+      int64_t src_ = mc_;                                                                          \
+      if (stride != 1) {                                                                           \
+        const int hw_ = Ho * Wo, img_ = mc_ / hw_, rem_ = mc_ - img_ * hw_;                        \
+        const int ho_ = rem_ / Wo, wo_ = rem_ - ho_ * Wo;                                          \
+        src_ = ((int64_t)img_ * Hi + (int64_t)ho_ * stride) * Wi + (int64_t)wo_ * stride;          \
+      }                                                                                            \
+      const u32x4 vy_ = *reinterpret_cast<const u32x4*>(dY + (int64_t)mc_ * N + (n_ok ? n0 + ch * 8 : 0)); \
+      const u32x4 vx_ = *reinterpret_cast<const u32x4*>(X + src_ * K + (k_ok ? k0 + ch * 8 : 0));  \
+      ry[i] = (ok_ && n_ok) ? vy_ : u32x4{0u, 0u, 0u, 0u};                                         \
+      rx[i] = (ok_ && k_ok) ? vx_ : u32x4{0u, 0u, 0u, 0u};                                         \
+    }                                                                                              \
+  }
+#define HIPPS_WSTORE(s_)                                                                           \
+  {                                                                                                \
+    uint8_t* ty_ = reinterpret_cast<uint8_t*>(lds + (s_) * 2 * TILE);                              \
+    uint8_t* tx_ = ty_ + TILE * 2;                                                                 \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                \
+      const int r_ = (t >> 4) + 16 * i;                                                            \
+      *reinterpret_cast<u32x4*>(ty_ + wg_off(r_, ch)) = ry[i];                                     \
+      *reinterpret_cast<u32x4*>(tx_ + wg_off(r_, ch)) = rx[i];                                     \
+    }                                                                                              \
+  }
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nst = (mend - mbeg + kWMS - 1) / kWMS;
+  HIPPS_WLOAD(mbeg);
+  HIPPS_WSTORE(0);
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int cur = st & 1;
+    if (st + 1 < nst) HIPPS_WLOAD(mbeg + (st + 1) * kWMS);
+    const uint8_t* ty = reinterpret_cast<const uint8_t*>(lds + cur * 2 * TILE);
+    const uint8_t* tx = ty + TILE * 2;
+#pragma unroll
+    for (int ks = 0; ks < kWMS / 32; ++ks) {
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = tr_frag(ty, ks * 32, wn * 64 + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = tr_frag(tx, ks * 32, wk * 64 + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (st + 1 < nst) HIPPS_WSTORE(cur ^ 1);
+    __syncthreads();
+  }
+#undef HIPPS_WLOAD
+#undef HIPPS_WSTORE
+  // D map: column (k) = lane & 15, row (n) = (lane >> 4) * 4 + r
+  float* out = part + (int64_t)sidx * N * K;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + wk * 64 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * 64 + i * 16 + (lane >> 4) * 4 + r;
+        if (n < N && k < K) out[(int64_t)n * K + k] = acc[i][j][r];
+      }
+    }
+}
+
+// dW = sum over the S partial slabs, in slab order (deterministic)
+__global__ __launch_bounds__(kBlock) void k_wgrad_reduce(const float* __restrict__ part, int S, int64_t NK4,
+                                                         float* __restrict__ dw, float scale) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < NK4; i += stride) {
+    float4 a = reinterpret_cast<const float4*>(part)[i];
+    for (int s = 1; s < S; ++s) {
+      const float4 b = reinterpret_cast<const float4*>(part)[(int64_t)s * NK4 + i];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    a.x *= scale; a.y *= scale; a.z *= scale; a.w *= scale;
+    reinterpret_cast<float4*>(dw)[i] = a;
+  }
+}
+
 // ==========================================================================================
 int64_t conv1x1_mtiles(int64_t M) { return (M + kGBM - 1) / kGBM; }
 
@@ -259,6 +400,40 @@ void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
     if (pa) HIPPS_C1(64, true); else HIPPS_C1(64, false);
   }
 #undef HIPPS_C1
+}
+
+
+// dy: [img, Cout, Ho, Wo] channels-last bf16; x: [img, Cin, Hi, Wi] channels-last bf16;
+// dw: f32 [Cout, Cin] (written, not accumulated).
+void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64_t Wi, int64_t stride) {
+  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dw.is_cuda(), "conv1x1_wgrad: device tensors");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 && dw.scalar_type() == at::kFloat,
+              "conv1x1_wgrad: bf16 dy/x, f32 dw");
+  TORCH_CHECK(dw.is_contiguous(), "conv1x1_wgrad: dw contiguous [Cout, Cin]");
+  const int64_t N = dw.size(0), K = dw.numel() / N;
+  TORCH_CHECK(N % 8 == 0 && K % 8 == 0, "conv1x1_wgrad: channels % 8");
+  const int64_t imgs = x.numel() / (K * Hi * Wi);
+  TORCH_CHECK(imgs * K * Hi * Wi == x.numel(), "conv1x1_wgrad: x size");
+  const int64_t Ho = (Hi - 1) / stride + 1, Wo = (Wi - 1) / stride + 1;
+  const int64_t M = imgs * Ho * Wo;
+  TORCH_CHECK(dy.numel() == M * N, "conv1x1_wgrad: dy size");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) || x.dim() != 4, "conv1x1_wgrad: x channels-last");
+  TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) || dy.dim() != 4, "conv1x1_wgrad: dy channels-last");
+  for (const at::Tensor* t : {&x, &dy, &dw})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "conv1x1_wgrad: 16-byte aligned tensors");
+  TORCH_CHECK(M < (int64_t(1) << 31), "conv1x1_wgrad: size");
+  const int64_t tn = (N + kWT - 1) / kWT, tk = (K + kWT - 1) / kWT, tiles = tn * tk;
+  int64_t S = std::max<int64_t>(1, std::min<int64_t>(2048 / tiles, (M + kWMS - 1) / kWMS));
+  int64_t chunk = ((M + S - 1) / S + kWMS - 1) / kWMS * kWMS;
+  S = (M + chunk - 1) / chunk;
+  auto part = at::empty({S, N, K}, dw.options());
+  auto stream = c10::hip::getCurrentHIPStream();
+  hipLaunchKernelGGL(k_conv1x1_wgrad, (int)(S * tiles), 256, 0, stream, (const uint16_t*)dy.data_ptr(),
+                     (const uint16_t*)x.data_ptr(), part.data_ptr<float>(), (int)M, (int)N, (int)K, (int)Ho, (int)Wo,
+                     (int)Hi, (int)Wi, (int)stride, (int)chunk, (int)tn, (int)tk);
+  const int64_t NK4 = N * K / 4;
+  hipLaunchKernelGGL(k_wgrad_reduce, grid_for(NK4), kBlock, 0, stream, part.data_ptr<float>(), (int)S, NK4,
+                     dw.data_ptr<float>(), 1.0f);
 }
 
 }  // namespace hipps

@@ -25,11 +25,14 @@ class _Conv1x1(torch.autograd.Function):
     """1x1 convolution on channels-last bf16 as an MFMA GEMM (hipps/csrc/gemm.hip) that also
     emits the per-channel batch statistics of its output for the BatchNorm that follows.
     Backward: the input gradient of a stride-1 conv is the same NT GEMM against the transposed
-    weight (dX[M,Cin] = dY[M,Cout] . W[Cout,Cin]); the weight gradient (and strided dgrad)
-    go to MIOpen (aten.convolution_backward)."""
+    weight (dX[M,Cin] = dY[M,Cout] . W[Cout,Cin]); the weight gradient is the split-M MFMA
+    reduction with transposing LDS reads (conv1x1_wgrad), written straight into an fp32 grad
+    for an fp32 master weight (no bf16 round trip); strided dgrad goes to MIOpen."""
 
     @staticmethod
-    def forward(ctx, x, w, stride):
+    def forward(ctx, x, w_master, stride):
+        w = w_master if w_master.dtype == torch.bfloat16 else w_master.to(torch.bfloat16)
+        ctx.wdtype = w_master.dtype
         N, Cin, H, W = x.shape
         Cout = w.shape[0]
         Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
@@ -49,10 +52,14 @@ class _Conv1x1(torch.autograd.Function):
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = None
         own_dx = ctx.needs_input_grad[0] and s == 1
-        need = [ctx.needs_input_grad[0] and not own_dx, ctx.needs_input_grad[1], False]
-        if any(need):
-            dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
-                                                            need)
+        if ctx.needs_input_grad[0] and not own_dx:
+            dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
+                                                     [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty(w.shape, dtype=torch.float32, device=w.device)
+            native().conv1x1_wgrad(dy, x, dw.view(w.shape[0], w.shape[1]), x.shape[2], x.shape[3], s)
+            if ctx.wdtype != torch.float32:
+                dw = dw.to(ctx.wdtype)
         if own_dx:
             cout, cin = w.shape[0], w.shape[1]
             wt = w.reshape(cout, cin).t().contiguous()  # [Cin, Cout]: K-contiguous B operand
@@ -75,7 +82,7 @@ def conv1x1_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
 
 def conv1x1_stats(x, weight, stride=1):
     """(y, part): bf16 1x1 conv output and its [2, Cout, m_tiles] BN partial statistics."""
-    return _Conv1x1.apply(x, weight.to(torch.bfloat16), int(stride))
+    return _Conv1x1.apply(x, weight, int(stride))
 
 
 class _FusedBNAct(torch.autograd.Function):

@@ -42,6 +42,20 @@ def test_conv1x1_matches_fp32_conv_and_stats(shape):
     torch.testing.assert_close(part[1].sum(1), (yf * yf).sum(0), rtol=1e-4, atol=1e-2)
 
 
+@pytest.mark.parametrize("shape", SHAPES + [(2, 64, 5, 5, 64, 1), (1, 72, 7, 7, 136, 1)])
+def test_conv1x1_wgrad_matches_fp32(shape):
+    n, cin, h, w, cout, s = shape
+    torch.manual_seed(7 + cin)
+    x = _cl(torch.randn(n, cin, h, w, device=DEV).to(torch.bfloat16))
+    ho = (h - 1) // s + 1
+    dy = _cl(torch.randn(n, cout, ho, ho, device=DEV).to(torch.bfloat16))
+    xs = x.float()[:, :, ::s, ::s]
+    ref = torch.einsum("nchw,nkhw->kc", xs, dy.float())
+    dw = torch.empty(cout, cin, device=DEV)
+    native().conv1x1_wgrad(dy, x, dw, h, w, s)
+    torch.testing.assert_close(dw, ref, rtol=2e-3, atol=2e-3 * (n * ho * ho) ** 0.5)
+
+
 def test_conv1x1_exact_on_integers():
     """Small integers are exact in bf16 and fp32: any row/column/k mix-up shows up exactly."""
     n, cin, h, w, cout = 2, 128, 8, 8, 192
@@ -50,6 +64,10 @@ def test_conv1x1_exact_on_integers():
     wt = torch.randint(-2, 3, (cout, cin, 1, 1), generator=g).float().to(DEV).to(torch.bfloat16)
     y, _ = hnn._Conv1x1.apply(x, wt, 1)
     assert torch.equal(y.float(), F.conv2d(x.float(), wt.float()))
+    dy = _cl(torch.randint(-2, 3, y.shape, generator=g).float().to(DEV).to(torch.bfloat16))
+    dw = torch.empty(cout, cin, device=DEV)
+    native().conv1x1_wgrad(dy, x, dw, h, w, 1)
+    assert torch.equal(dw, torch.einsum("nchw,nkhw->kc", x.float(), dy.float()))
 
 
 @pytest.mark.parametrize("residual", [False, True])

@@ -69,6 +69,14 @@ for cin, h, cout, st in SHAPES:
         ref_dx = torch.ops.aten.convolution_backward(dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
                                                      [True, False, False])[0]
         dg_err = ((dx.float() - ref_dx.float()).abs().max() / ref_dx.float().abs().max()).item()
+    dyw = torch.randn_like(y)
+    dwo = torch.empty(cout, cin, device="cuda")
+    t_mi_wg = timeit(lambda: torch.ops.aten.convolution_backward(dyw, x, w, None, [st, st], [0, 0], [1, 1], False,
+                                                                 [0, 0], 1, [False, True, False]))
+    t_h_wg = timeit(lambda: native().conv1x1_wgrad(dyw, x, dwo, h, h, st))
+    ref_dw = torch.ops.aten.convolution_backward(dyw, x, w, None, [st, st], [0, 0], [1, 1], False, [0, 0], 1,
+                                                 [False, True, False])[1].float().view(cout, cin)
+    wg_err = ((dwo - ref_dw).abs().max() / ref_dw.abs().max()).item()
     flops = 2.0 * M * cin * cout
     byts = (256 * cin * h * h + M * cout) * 2
     ref = F.conv2d(x, w, stride=st)
@@ -79,11 +87,13 @@ for cin, h, cout, st in SHAPES:
          "rel_err": round(err, 5),
          "miopen_dgrad_ms": None if t_mi_dg is None else round(t_mi_dg, 4),
          "hipps_dgrad_ms": None if t_h_dg is None else round(t_h_dg, 4),
-         "dgrad_rel_err": None if t_h_dg is None else round(dg_err, 5)}
+         "dgrad_rel_err": None if t_h_dg is None else round(dg_err, 5),
+         "miopen_wgrad_ms": round(t_mi_wg, 4), "hipps_wgrad_ms": round(t_h_wg, 4), "wgrad_rel_err": round(wg_err, 5)}
     rows.append(r)
     print(json.dumps(r), flush=True)
 tot = {k: round(sum(r[k] or 0 for r in rows), 3) for k in ("miopen_ms", "hipps_ms", "miopen_plus_bn_ms",
-                                                          "hipps_plus_bn_ms", "miopen_dgrad_ms", "hipps_dgrad_ms")}
+                                                          "hipps_plus_bn_ms", "miopen_dgrad_ms", "hipps_dgrad_ms",
+                                                          "miopen_wgrad_ms", "hipps_wgrad_ms")}
 print(json.dumps({"total": tot}))
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 json.dump({"rows": rows, "total": tot}, open(os.path.join(ROOT, "gpurun_out/bench_conv1x1.json"), "w"), indent=1)
