@@ -337,19 +337,50 @@ __global__ __launch_bounds__(256) void k_conv1x1_wgrad(const uint16_t* __restric
     }
 }
 
-// dW = sum over the S partial slabs, in slab order (deterministic)
-__global__ __launch_bounds__(kBlock) void k_wgrad_reduce(const float* __restrict__ part, int S, int64_t NK4,
-                                                         float* __restrict__ dw, float scale) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < NK4; i += stride) {
-    float4 a = reinterpret_cast<const float4*>(part)[i];
-    for (int s = 1; s < S; ++s) {
-      const float4 b = reinterpret_cast<const float4*>(part)[(int64_t)s * NK4 + i];
-      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+// dW = sum of the S partial slabs, deterministic two-level order: group g of G sums slabs
+// [g*S/G, (g+1)*S/G) with 4 independent accumulators (a serial S-long chain per element was
+// latency-bound: ~0.4 ms at S = 2048), then G group sums are added in order.
+__global__ __launch_bounds__(kBlock) void k_wgrad_reduce1(const float* __restrict__ part, int S, int G, int64_t NK4,
+                                                          float* __restrict__ tmp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int g = blockIdx.y;
+  if (i >= NK4) return;
+  const int s0 = (int)((int64_t)g * S / G), s1 = (int)((int64_t)(g + 1) * S / G);
+  const float4* p = reinterpret_cast<const float4*>(part);
+  float4 a[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) a[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  int s = s0;
+  for (; s + 3 < s1; s += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float4 b = p[(int64_t)(s + u) * NK4 + i];
+      a[u].x += b.x; a[u].y += b.y; a[u].z += b.z; a[u].w += b.w;
     }
-    a.x *= scale; a.y *= scale; a.z *= scale; a.w *= scale;
-    reinterpret_cast<float4*>(dw)[i] = a;
   }
+  for (; s < s1; ++s) {
+    const float4 b = p[(int64_t)s * NK4 + i];
+    a[0].x += b.x; a[0].y += b.y; a[0].z += b.z; a[0].w += b.w;
+  }
+  float4 r;
+  r.x = (a[0].x + a[1].x) + (a[2].x + a[3].x);
+  r.y = (a[0].y + a[1].y) + (a[2].y + a[3].y);
+  r.z = (a[0].z + a[1].z) + (a[2].z + a[3].z);
+  r.w = (a[0].w + a[1].w) + (a[2].w + a[3].w);
+  reinterpret_cast<float4*>(tmp)[(int64_t)g * NK4 + i] = r;
+}
+
+__global__ __launch_bounds__(kBlock) void k_wgrad_reduce2(const float* __restrict__ tmp, int G, int64_t NK4,
+                                                          float* __restrict__ dw) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= NK4) return;
+  const float4* p = reinterpret_cast<const float4*>(tmp);
+  float4 a = p[i];
+  for (int g = 1; g < G; ++g) {
+    const float4 b = p[(int64_t)g * NK4 + i];
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  reinterpret_cast<float4*>(dw)[i] = a;
 }
 
 // ==========================================================================================
@@ -432,8 +463,17 @@ void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64
                      (const uint16_t*)x.data_ptr(), part.data_ptr<float>(), (int)M, (int)N, (int)K, (int)Ho, (int)Wo,
                      (int)Hi, (int)Wi, (int)stride, (int)chunk, (int)tn, (int)tk);
   const int64_t NK4 = N * K / 4;
-  hipLaunchKernelGGL(k_wgrad_reduce, grid_for(NK4), kBlock, 0, stream, part.data_ptr<float>(), (int)S, NK4,
-                     dw.data_ptr<float>(), 1.0f);
+  const int G = (int)std::min<int64_t>(S, 32);
+  const int gx = (int)((NK4 + kBlock - 1) / kBlock);
+  if (G == 1) {
+    hipLaunchKernelGGL(k_wgrad_reduce2, gx, kBlock, 0, stream, part.data_ptr<float>(), (int)S, NK4,
+                       dw.data_ptr<float>());
+  } else {
+    auto tmp = at::empty({G, N, K}, dw.options());
+    hipLaunchKernelGGL(k_wgrad_reduce1, dim3(gx, G), kBlock, 0, stream, part.data_ptr<float>(), (int)S, G, NK4,
+                       tmp.data_ptr<float>());
+    hipLaunchKernelGGL(k_wgrad_reduce2, gx, kBlock, 0, stream, tmp.data_ptr<float>(), G, NK4, dw.data_ptr<float>());
+  }
 }
 
 }  // namespace hipps

@@ -18,6 +18,11 @@ import torch.nn.functional as F
 
 from ._native import native
 
+import os as _os
+
+# weight gradient of the MFMA 1x1 path: own split-M kernel (1) or MIOpen (0), for A/B runs
+_OWN_WGRAD = _os.environ.get("HIPPS_CONV_WGRAD", "1") != "0"
+
 MASK_NONE, MASK_X, MASK_Y, MASK_BITS = 0, 1, 2, 3
 
 
@@ -55,7 +60,10 @@ class _Conv1x1(torch.autograd.Function):
         if ctx.needs_input_grad[0] and not own_dx:
             dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
                                                      [True, False, False])[0]
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and not _OWN_WGRAD:
+            dw = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
+                                                     [False, True, False])[1].to(ctx.wdtype)
+        elif ctx.needs_input_grad[1]:
             dw = torch.empty(w.shape, dtype=torch.float32, device=w.device)
             native().conv1x1_wgrad(dy, x, dw.view(w.shape[0], w.shape[1]), x.shape[2], x.shape[3], s)
             if ctx.wdtype != torch.float32:

@@ -10,3 +10,5 @@ timeout -k 10 300 python bench.py --steps 20 --warmup 6 --out gpurun_out/bench_c
 cat gpurun_out/bench_conv.json
 HIPPS_FUSED_CONV=0 timeout -k 10 300 python bench.py --steps 20 --warmup 6 --out gpurun_out/bench_noconv.json > gpurun_out/bench_noconv.log 2>&1 || { echo "bench noconv failed"; tail -40 gpurun_out/bench_noconv.log; exit 1; }
 cat gpurun_out/bench_noconv.json
+HIPPS_CONV_WGRAD=0 timeout -k 10 300 python bench.py --steps 20 --warmup 6 --out gpurun_out/bench_miowgrad.json > gpurun_out/bench_miowgrad.log 2>&1 || { echo "bench miopen-wgrad failed"; tail -40 gpurun_out/bench_miowgrad.log; exit 1; }
+cat gpurun_out/bench_miowgrad.json
