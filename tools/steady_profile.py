@@ -33,7 +33,8 @@ def main():
     cat = collections.defaultdict(float)
     for k, (d, c) in agg.items():
         if "hipps" in k:
-            key = "hipps-norm" if "k_bn_" in k else "hipps-ps"
+            key = ("hipps-norm" if "k_bn_" in k else
+                   "hipps-gemm" if ("conv1x1" in k or "wgrad" in k) else "hipps-ps")
         elif "BatchNorm" in k:
             key = "miopen-batchnorm"
         elif any(s in k for s in ("conv", "igemm", "gemm", "Cijk", "xdl")):
@@ -48,7 +49,7 @@ def main():
     for k, v in sorted(cat.items(), key=lambda x: -x[1]):
         lines.append(f"  {k:18s} {v / n / 1e6:8.3f} ms/step {100 * v / tot:5.1f}%")
     lines.append("")
-    for k, (d, c) in sorted(agg.items(), key=lambda x: -x[1][0])[:40]:
+    for k, (d, c) in sorted(agg.items(), key=lambda x: -x[1][0])[:60]:
         lines.append(f"{d / n / 1e3:9.1f} us/step calls/step={c / n:6.1f}  {k[:140]}")
     open(a.out, "w").write("\n".join(lines) + "\n")
     print("\n".join(lines[:12]))
