@@ -47,7 +47,10 @@ void bn_forward_partials(at::Tensor part, int64_t nrb, at::Tensor x, c10::option
 // gemm.hip
 int64_t conv1x1_mtiles(int64_t M);
 void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part, int64_t Hi,
-                     int64_t Wi, int64_t stride);
+                     int64_t Wi, int64_t stride, c10::optional<at::Tensor> add, c10::optional<at::Tensor> add_mask);
+// pool.hip
+void maxpool3s2_forward(at::Tensor x, at::Tensor y, at::Tensor code);
+void maxpool3s2_backward(at::Tensor dy, at::Tensor code, at::Tensor dx);
 void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64_t Wi, int64_t stride);
 namespace rt {
 void bind_control(pybind11::module& m);
@@ -77,7 +80,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_backward", &hipps::bn_backward, "fused BN bwd with relu-mask recompute (+dres)");
   m.def("bn_forward_partials", &hipps::bn_forward_partials, "BN fwd finalize+apply from producer-reduced partials");
   m.def("conv1x1_mtiles", &hipps::conv1x1_mtiles);
-  m.def("conv1x1_forward", &hipps::conv1x1_forward, "MFMA 1x1 conv (NHWC GEMM) with fused BN-stats epilogue");
+  m.def("conv1x1_forward", &hipps::conv1x1_forward,
+        "MFMA 1x1 conv (NHWC GEMM) with fused BN-stats epilogue and optional (+ add * mask) epilogue",
+        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("part"), pybind11::arg("Hi"),
+        pybind11::arg("Wi"), pybind11::arg("stride"), pybind11::arg("add") = pybind11::none(),
+        pybind11::arg("add_mask") = pybind11::none());
+  m.def("maxpool3s2_forward", &hipps::maxpool3s2_forward, "3x3/s2/p1 max pool, channels-last bf16, 4-bit tap codes");
+  m.def("maxpool3s2_backward", &hipps::maxpool3s2_backward, "3x3/s2/p1 max pool backward (gather form, no atomics)");
   m.def("conv1x1_wgrad", &hipps::conv1x1_wgrad, "MFMA 1x1 conv weight gradient (tr_b16 LDS reads, split-M)");
   hipps::rt::bind_control(m);
   hipps::rt::bind_ipc(m);

@@ -44,11 +44,17 @@ constexpr int gemm_lds_elems() {
   return (stage > epi ? stage : epi) + 2 * 2 * GemmCfg<BN>::WM * BN;
 }
 
+__device__ __forceinline__ uint32_t add_bf16x2(uint32_t a, uint32_t b) {
+  return pack_bf16x2(__uint_as_float(a << 16) + __uint_as_float(b << 16),
+                     __uint_as_float(a & 0xffff0000u) + __uint_as_float(b & 0xffff0000u));
+}
+
 template <int BN, bool STATS>
 __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W,
                                                     uint16_t* __restrict__ Y, float* __restrict__ pa,
-                                                    float* __restrict__ pb, int M, int N, int K, int Ho, int Wo,
-                                                    int Hi, int Wi, int stride, int mtiles, int ntiles) {
+                                                    float* __restrict__ pb, const uint16_t* __restrict__ R,
+                                                    const uint8_t* __restrict__ RM, int M, int N, int K, int Ho,
+                                                    int Wo, int Hi, int Wi, int stride, int mtiles, int ntiles) {
   constexpr int WM = GemmCfg<BN>::WM, WN = GemmCfg<BN>::WN;
   constexpr int TM = kGBM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
@@ -195,9 +201,25 @@ __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__
   for (int i = 0; i < kGBM * RCH / 256; ++i) {
     const int id = t + 256 * i;
     const int row = id / RCH, c = id - row * RCH;
-    if (m0 + row < M)
-      *reinterpret_cast<uint4*>(Y + (int64_t)(m0 + row) * N + n0 + c * 8) =
-          *reinterpret_cast<const uint4*>(lds + row * EP + c * 8);
+    if (m0 + row < M) {
+      const int64_t o = (int64_t)(m0 + row) * N + n0 + c * 8;
+      uint4 v = *reinterpret_cast<const uint4*>(lds + row * EP + c * 8);
+      if (R != nullptr) {  // fused "+ R" (R * ReLU-mask bits): a second gradient path into Y
+        uint4 r = *reinterpret_cast<const uint4*>(R + o);
+        if (RM != nullptr) {  // one mask byte per 8 channels = this 16-byte chunk
+          const uint32_t mb = RM[o >> 3];
+          r.x &= (mb & 1u ? 0xffffu : 0u) | (mb & 2u ? 0xffff0000u : 0u);
+          r.y &= (mb & 4u ? 0xffffu : 0u) | (mb & 8u ? 0xffff0000u : 0u);
+          r.z &= (mb & 16u ? 0xffffu : 0u) | (mb & 32u ? 0xffff0000u : 0u);
+          r.w &= (mb & 64u ? 0xffffu : 0u) | (mb & 128u ? 0xffff0000u : 0u);
+        }
+        v.x = add_bf16x2(v.x, r.x);
+        v.y = add_bf16x2(v.y, r.y);
+        v.z = add_bf16x2(v.z, r.z);
+        v.w = add_bf16x2(v.w, r.w);
+      }
+      *reinterpret_cast<uint4*>(Y + o) = v;
+    }
   }
   if (STATS && t < BN) {
     float s = 0.f, q = 0.f;
@@ -388,8 +410,10 @@ int64_t conv1x1_mtiles(int64_t M) { return (M + kGBM - 1) / kGBM; }
 
 // x: [img, Cin, Hi, Wi] channels-last bf16; w: [Cout, Cin(,1,1)] bf16 contiguous;
 // y: [img, Cout, Ho, Wo] channels-last bf16.  part (optional): f32 [2, Cout, mtiles].
+// add (optional): bf16 shaped like y, added in the epilogue (y = conv(x) + add); add_mask
+// (optional, with add): uint8 [numel/8] ReLU bits, y = conv(x) + add * bit.
 void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part, int64_t Hi,
-                     int64_t Wi, int64_t stride) {
+                     int64_t Wi, int64_t stride, c10::optional<at::Tensor> add, c10::optional<at::Tensor> add_mask) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "conv1x1: device tensors");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
                   y.scalar_type() == at::kBFloat16, "conv1x1: bf16 tensors");
@@ -418,12 +442,27 @@ void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
     pa = part->data_ptr<float>();
     pb = pa + N * mtiles;
   }
+  const uint16_t* rp = nullptr;
+  if (add.has_value() && add->defined()) {
+    TORCH_CHECK(add->is_cuda() && add->scalar_type() == at::kBFloat16 && add->numel() == M * N &&
+                    (add->is_contiguous(at::MemoryFormat::ChannelsLast) || add->dim() != 4) &&
+                    reinterpret_cast<uintptr_t>(add->data_ptr()) % 16 == 0,
+                "conv1x1: add must be a 16-byte aligned channels-last bf16 tensor shaped like y");
+    rp = (const uint16_t*)add->data_ptr();
+  }
+  const uint8_t* mp = nullptr;
+  if (add_mask.has_value() && add_mask->defined()) {
+    TORCH_CHECK(rp != nullptr, "conv1x1: add_mask needs add");
+    TORCH_CHECK(add_mask->is_cuda() && add_mask->scalar_type() == at::kByte && add_mask->is_contiguous() &&
+                    add_mask->numel() == M * N / 8, "conv1x1: add_mask must be uint8[numel(y)/8]");
+    mp = (const uint8_t*)add_mask->data_ptr();
+  }
   auto stream = c10::hip::getCurrentHIPStream();
   const uint16_t* xp = (const uint16_t*)x.data_ptr();
   const uint16_t* wp = (const uint16_t*)w.data_ptr();
   uint16_t* yp = (uint16_t*)y.data_ptr();
 #define HIPPS_C1(BNv, ST)                                                                                  \
-  hipLaunchKernelGGL((k_conv1x1_nt<BNv, ST>), (int)nblk, 256, 0, stream, xp, wp, yp, pa, pb, (int)M, (int)N, \
+  hipLaunchKernelGGL((k_conv1x1_nt<BNv, ST>), (int)nblk, 256, 0, stream, xp, wp, yp, pa, pb, rp, mp, (int)M, (int)N, \
                      (int)K, (int)Ho, (int)Wo, (int)Hi, (int)Wi, (int)stride, (int)mtiles, (int)ntiles)
   if (bn128) {
     if (pa) HIPPS_C1(128, true); else HIPPS_C1(128, false);

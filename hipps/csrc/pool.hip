@@ -1,0 +1,151 @@
+// hipps — 3x3 / stride-2 / pad-1 max pooling for channels-last bf16 activations (the ResNet stem).
+//
+// PyTorch's NHWC max_pool2d backward scatters through int64 indices: 0.62 ms per ResNet-50 step
+// at bs256 (profiles/bench_n1_steady_r1b.txt), the forward 0.26 ms.  Both passes are pure
+// bandwidth (~0.5 GB each), i.e. ~0.1 ms each at HBM speed.
+//
+// forward : one lane = one output pixel x 8 channels (16 B loads/stores).  The argmax is kept as
+//           a 4-bit tap code (kh*3 + kw) per channel, 8 codes in one uint32 per lane: 1/4 of the
+//           output bytes instead of 4x (int64 indices).  Ties and NaNs follow PyTorch's rule
+//           (first maximum in scan order; a NaN always wins), so values and gradients match it.
+// backward: gather form, no atomics: one lane = one input pixel x 8 channels.  With k=3, s=2,
+//           p=1 an input row h lies in the windows oh in [h>>1, (h+1)>>1] (1 or 2 of them), so a
+//           lane checks at most 4 windows' codes and sums the matching dy in fp32.
+#include "common.h"
+
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+namespace hipps {
+
+namespace {
+__device__ __forceinline__ void ld8(const uint16_t* p, float v[8]) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+  v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
+  v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+__device__ __forceinline__ void st8(uint16_t* p, const float v[8]) {
+  *reinterpret_cast<uint4*>(p) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                            pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+}
+}  // namespace
+
+__global__ __launch_bounds__(kBlock) void k_maxpool3s2_fwd(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                           uint32_t* __restrict__ code, int64_t total, int H, int W,
+                                                           int Ho, int Wo, int G) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= total) return;
+  const int g = (int)(v % G);
+  int64_t p = v / G;
+  const int wo = (int)(p % Wo);
+  p /= Wo;
+  const int ho = (int)(p % Ho);
+  const int64_t n = p / Ho;
+  float m[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+  uint32_t c = 0;
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const int h = 2 * ho - 1 + kh;
+    if (h < 0 || h >= H) continue;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int w = 2 * wo - 1 + kw;
+      if (w < 0 || w >= W) continue;
+      float xv[8];
+      ld8(x + (((n * H + h) * W + w) * G + g) * 8, xv);
+      const uint32_t t = (uint32_t)(kh * 3 + kw);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (xv[j] > m[j] || __builtin_isnan(xv[j])) {
+          m[j] = xv[j];
+          c = (c & ~(15u << (4 * j))) | (t << (4 * j));
+        }
+      }
+    }
+  }
+  st8(y + v * 8, m);
+  code[v] = c;
+}
+
+__global__ __launch_bounds__(kBlock) void k_maxpool3s2_bwd(const uint16_t* __restrict__ dy,
+                                                           const uint32_t* __restrict__ code,
+                                                           uint16_t* __restrict__ dx, int64_t total, int H, int W,
+                                                           int Ho, int Wo, int G) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= total) return;
+  const int g = (int)(v % G);
+  int64_t p = v / G;
+  const int w = (int)(p % W);
+  p /= W;
+  const int h = (int)(p % H);
+  const int64_t n = p / H;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  const int oh1 = min((h + 1) >> 1, Ho - 1), ow1 = min((w + 1) >> 1, Wo - 1);
+  for (int oh = h >> 1; oh <= oh1; ++oh) {
+    for (int ow = w >> 1; ow <= ow1; ++ow) {
+      const uint32_t t = (uint32_t)((h - 2 * oh + 1) * 3 + (w - 2 * ow + 1));
+      const int64_t o = ((n * Ho + oh) * Wo + ow) * G + g;
+      const uint32_t c = code[o];
+      float d[8];
+      ld8(dy + o * 8, d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += ((c >> (4 * j)) & 15u) == t ? d[j] : 0.f;
+    }
+  }
+  st8(dx + v * 8, acc);
+}
+
+// x: [N, C, H, W] channels-last bf16 (C % 8 == 0); y: [N, C, Ho, Wo] channels-last bf16;
+// code: int32 [N*Ho*Wo*C/8] (4-bit tap codes).
+void maxpool3s2_forward(at::Tensor x, at::Tensor y, at::Tensor code) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast), "maxpool: x must be channels-last bf16 NCHW");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(C % 8 == 0 && H >= 1 && W >= 1, "maxpool: C % 8 == 0");
+  const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kBFloat16 && y.dim() == 4 && y.size(0) == N && y.size(1) == C &&
+                  y.size(2) == Ho && y.size(3) == Wo && y.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "maxpool: y must be channels-last bf16 [N, C, Ho, Wo]");
+  const int64_t total = N * Ho * Wo * (C / 8);
+  TORCH_CHECK(code.is_cuda() && code.scalar_type() == at::kInt && code.is_contiguous() && code.numel() == total,
+              "maxpool: code must be int32[N*Ho*Wo*C/8]");
+  for (const at::Tensor* t : {&x, &y, &code})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "maxpool: 16-byte aligned tensors");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 40) && (total + kBlock - 1) / kBlock < (int64_t(1) << 31), "maxpool: size");
+  if (total == 0) return;
+  hipLaunchKernelGGL(k_maxpool3s2_fwd, (int)((total + kBlock - 1) / kBlock), kBlock, 0,
+                     c10::hip::getCurrentHIPStream(), (const uint16_t*)x.data_ptr(), (uint16_t*)y.data_ptr(),
+                     (uint32_t*)code.data_ptr(), total, (int)H, (int)W, (int)Ho, (int)Wo, (int)(C / 8));
+}
+
+// dy: [N, C, Ho, Wo] channels-last bf16; dx: [N, C, H, W] channels-last bf16 (fully written).
+void maxpool3s2_backward(at::Tensor dy, at::Tensor code, at::Tensor dx) {
+  TORCH_CHECK(dx.is_cuda() && dx.scalar_type() == at::kBFloat16 && dx.dim() == 4 &&
+                  dx.is_contiguous(at::MemoryFormat::ChannelsLast), "maxpool bwd: dx must be channels-last bf16");
+  const int64_t N = dx.size(0), C = dx.size(1), H = dx.size(2), W = dx.size(3);
+  TORCH_CHECK(C % 8 == 0, "maxpool bwd: C % 8 == 0");
+  const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 && dy.size(0) == N &&
+                  dy.size(1) == C && dy.size(2) == Ho && dy.size(3) == Wo &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast), "maxpool bwd: dy must be channels-last bf16");
+  TORCH_CHECK(code.is_cuda() && code.scalar_type() == at::kInt && code.is_contiguous() &&
+                  code.numel() == N * Ho * Wo * (C / 8), "maxpool bwd: code size");
+  for (const at::Tensor* t : {&dy, &dx, &code})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "maxpool bwd: 16-byte aligned tensors");
+  const int64_t total = N * H * W * (C / 8);
+  TORCH_CHECK(dx.numel() < (int64_t(1) << 40) && (total + kBlock - 1) / kBlock < (int64_t(1) << 31),
+              "maxpool bwd: size");
+  if (total == 0) return;
+  hipLaunchKernelGGL(k_maxpool3s2_bwd, (int)((total + kBlock - 1) / kBlock), kBlock, 0,
+                     c10::hip::getCurrentHIPStream(), (const uint16_t*)dy.data_ptr(), (const uint32_t*)code.data_ptr(),
+                     (uint16_t*)dx.data_ptr(), total, (int)H, (int)W, (int)Ho, (int)Wo, (int)(C / 8));
+}
+
+}  // namespace hipps

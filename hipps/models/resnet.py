@@ -14,7 +14,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from hipps.ops.nn import FusedBatchNorm2d, conv_bn
+from hipps.ops.nn import FusedBatchNorm2d, MaxPool2d, ResidualTap, conv_bn
 
 # One switch for the whole zoo: fused BN(+residual)(+ReLU) HIP kernels on channels-last bf16,
 # standard PyTorch elsewhere.  HIPPS_FUSED_BN=0 restores the eager MIOpen path for A/B runs.
@@ -23,6 +23,10 @@ import os as _os
 _FUSED = _os.environ.get("HIPPS_FUSED_BN", "1") != "0"
 # 1x1 convolutions feeding a fused BN: MFMA GEMM with the BN statistics in its epilogue
 _FUSED_CONV = _FUSED and _os.environ.get("HIPPS_FUSED_CONV", "1") != "0"
+# residual-gradient sums folded into the 1x1 dgrad epilogue (ResidualTap / alias)
+_FUSED_GRAD = _FUSED_CONV and _os.environ.get("HIPPS_FUSED_GRAD", "1") != "0"
+# stem max pool on the hipps kernels
+_FUSED_POOL = _FUSED and _os.environ.get("HIPPS_FUSED_POOL", "1") != "0"
 
 
 def _bn(c, relu=False):
@@ -50,11 +54,24 @@ class Bottleneck(nn.Module):
             self.downsample = nn.Sequential(_conv(cin, cout, 1, stride=stride), _bn(cout))
 
     def forward(self, x):
+        # Gradient of x = conv1's dgrad + the residual path's gradient.  Instead of autograd's add
+        # (read 2, write 1 full-size tensors per block) conv1's dgrad epilogue sums them: the
+        # identity residual's gradient (bn3's dy * ReLU bits) arrives through a ResidualTap, a
+        # downsample branch's input gradient through an alias of x.
         ds = self.downsample
-        idt = x if ds is None else conv_bn(ds[0], ds[1], x, fuse=_FUSED_CONV)
-        y = conv_bn(self.conv1, self.bn1, x, fuse=_FUSED_CONV)
+        if ds is None:
+            tap = ResidualTap() if _FUSED_GRAD else None
+            y = conv_bn(self.conv1, self.bn1, x, fuse=_FUSED_CONV, tap=tap)
+            idt = x
+        else:
+            if _FUSED_GRAD:
+                y, xa = conv_bn(self.conv1, self.bn1, x, fuse=_FUSED_CONV, alias=True)
+            else:
+                y, xa = conv_bn(self.conv1, self.bn1, x, fuse=_FUSED_CONV), x
+            tap = None
+            idt = conv_bn(ds[0], ds[1], xa, fuse=_FUSED_CONV)
         y = self.bn2(self.conv2(y))
-        return conv_bn(self.conv3, self.bn3, y, residual=idt, fuse=_FUSED_CONV)
+        return conv_bn(self.conv3, self.bn3, y, residual=idt, fuse=_FUSED_CONV, res_tap=tap)
 
 
 class BasicBlock(nn.Module):
@@ -81,7 +98,7 @@ class ResNet(nn.Module):
         super().__init__()
         self.conv1 = nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False)
         self.bn1 = _bn(width, relu=True)
-        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        self.maxpool = MaxPool2d(3, stride=2, padding=1, fused=_FUSED_POOL)
         cin = width
         stages = []
         for i, n in enumerate(layers):

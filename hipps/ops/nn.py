@@ -27,16 +27,39 @@ _OWN_WGRAD = _os.environ.get("HIPPS_CONV_WGRAD", "0") != "0"
 MASK_NONE, MASK_X, MASK_Y, MASK_BITS = 0, 1, 2, 3
 
 
+class ResidualTap:
+    """Hands a fused BN's residual gradient to the stride-1 1x1 conv that reads the same block
+    input (ResNet identity blocks: x feeds conv1 and is bn3's residual).  bn3's backward stores
+    its (dy, ReLU bits) here instead of writing a dres tensor; conv1's backward -- which autograd
+    always runs later, since it needs the gradient that flows down from bn3 through conv3, bn2,
+    conv2 and bn1 -- adds dy * bits in its dgrad GEMM epilogue.  That removes one full-size write
+    (dres) and the autograd add kernel (read 2, write 1) per identity block."""
+
+    __slots__ = ("armed", "dy", "mask")
+
+    def __init__(self):
+        self.armed = False  # set when conv1 took the MFMA path (its backward will consume the tap)
+        self.dy = None
+        self.mask = None
+
+    def take(self):
+        dy, mask = self.dy, self.mask
+        self.dy = self.mask = None
+        return dy, mask
+
+
 class _Conv1x1(torch.autograd.Function):
     """1x1 convolution on channels-last bf16 as an MFMA GEMM (hipps/csrc/gemm.hip) that also
     emits the per-channel batch statistics of its output for the BatchNorm that follows.
     Backward: the input gradient of a stride-1 conv is the same NT GEMM against the transposed
     weight (dX[M,Cin] = dY[M,Cout] . W[Cout,Cin]); the weight gradient is the split-M MFMA
     reduction with transposing LDS reads (conv1x1_wgrad), written straight into an fp32 grad
-    for an fp32 master weight (no bf16 round trip); strided dgrad goes to MIOpen."""
+    for an fp32 master weight (no bf16 round trip); strided dgrad goes to MIOpen.
+    Other gradient paths into x are summed in the dgrad epilogue: a ResidualTap's (dy * bits),
+    and with ``alias`` the gradient of the returned alias of x (e.g. a downsample branch)."""
 
     @staticmethod
-    def forward(ctx, x, w_master, stride):
+    def forward(ctx, x, w_master, stride, tap=None, alias=False):
         w = w_master if w_master.dtype == torch.bfloat16 else w_master.to(torch.bfloat16)
         ctx.wdtype = w_master.dtype
         N, Cin, H, W = x.shape
@@ -47,20 +70,33 @@ class _Conv1x1(torch.autograd.Function):
         part = torch.empty((2, Cout, mt), dtype=torch.float32, device=x.device)
         native().conv1x1_forward(x, w.reshape(Cout, Cin), y, part, H, W, stride)
         ctx.stride = stride
+        ctx.tap = tap
         ctx.save_for_backward(x, w)
         ctx.mark_non_differentiable(part)
+        if alias:
+            return y, part, x  # an input returned as-is becomes a view whose grad comes back here
         return y, part
 
     @staticmethod
-    def backward(ctx, dy, _dpart):
+    def backward(ctx, dy, _dpart, d_alias=None):
         x, w = ctx.saved_tensors
         s = ctx.stride
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = None
+        add, add_mask = ctx.tap.take() if ctx.tap is not None else (None, None)
+        if d_alias is not None:
+            d_alias = d_alias.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            if add is None:
+                add = d_alias
+            else:  # both paths present (not produced by the ResNet blocks): fold eagerly
+                add = _masked(add, add_mask, x.shape[1]) + d_alias
+                add_mask = None
         own_dx = ctx.needs_input_grad[0] and s == 1
         if ctx.needs_input_grad[0] and not own_dx:
             dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
                                                      [True, False, False])[0]
+            if add is not None:
+                dx = dx + _masked(add, add_mask, x.shape[1])
         if ctx.needs_input_grad[1] and not _OWN_WGRAD:
             dw = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
                                                      [False, True, False])[1].to(ctx.wdtype)
@@ -73,8 +109,17 @@ class _Conv1x1(torch.autograd.Function):
             cout, cin = w.shape[0], w.shape[1]
             wt = w.reshape(cout, cin).t().contiguous()  # [Cin, Cout]: K-contiguous B operand
             dx = torch.empty_like(x, memory_format=torch.channels_last)
-            native().conv1x1_forward(dy, wt, dx, None, x.shape[2], x.shape[3], 1)
-        return dx, dw, None
+            native().conv1x1_forward(dy, wt, dx, None, x.shape[2], x.shape[3], 1, add, add_mask)
+        return dx, dw, None, None, None
+
+
+def _masked(t, mask, C):
+    """t * ReLU bits (uint8, bit j of byte i = element 8i+j of the channels-last storage)."""
+    if mask is None:
+        return t
+    bits = (mask.view(-1, 1) >> torch.arange(8, device=mask.device, dtype=torch.uint8)) & 1
+    flat = t.permute(0, 2, 3, 1).reshape(-1) * bits.view(-1).to(t.dtype)
+    return flat.view(t.shape[0], t.shape[2], t.shape[3], C).permute(0, 3, 1, 2)
 
 
 def conv1x1_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
@@ -89,14 +134,15 @@ def conv1x1_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     return conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0
 
 
-def conv1x1_stats(x, weight, stride=1):
-    """(y, part): bf16 1x1 conv output and its [2, Cout, m_tiles] BN partial statistics."""
-    return _Conv1x1.apply(x, weight, int(stride))
+def conv1x1_stats(x, weight, stride=1, tap=None, alias=False):
+    """(y, part[, x_alias]): bf16 1x1 conv output and its [2, Cout, m_tiles] BN partial
+    statistics (see _Conv1x1 for ``tap`` / ``alias``)."""
+    return _Conv1x1.apply(x, weight, int(stride), tap, bool(alias))
 
 
 class _FusedBNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, weight, bias, running_mean, running_var, eps, momentum, relu, part=None):
+    def forward(ctx, x, res, weight, bias, running_mean, running_var, eps, momentum, relu, part=None, tap=None):
         C = x.shape[1]
         y = torch.empty_like(x, memory_format=torch.channels_last)
         f32 = dict(dtype=torch.float32, device=x.device)
@@ -113,6 +159,8 @@ class _FusedBNAct(torch.autograd.Function):
             native().bn_forward_train(x, res, y, weight, bias, running_mean, running_var, mean, invstd, scale, shift,
                                       C, float(eps), float(momentum), bool(relu), mask)
         ctx.mode, ctx.C, ctx.has_res = mode, C, res is not None
+        # the residual gradient is dy * bits (or dy): hand it to the consumer through the tap
+        ctx.tap = tap if (res is not None and mode in (MASK_NONE, MASK_BITS)) else None
         ctx.save_for_backward(x, mask, weight, mean, invstd, scale, shift)
         return y
 
@@ -121,18 +169,24 @@ class _FusedBNAct(torch.autograd.Function):
         x, mask, weight, mean, invstd, scale, shift = ctx.saved_tensors
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = torch.empty_like(x, memory_format=torch.channels_last)
-        dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
+        tap = ctx.tap
+        dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res and tap is None else None
         dw = torch.empty_like(weight)
         db = torch.empty_like(weight)
         native().bn_backward(dy, x, None, ctx.mode, weight, mean, invstd, scale, shift, dx, dres, dw, db, ctx.C, mask)
-        return dx, dres, dw, db, None, None, None, None, None, None
+        if tap is not None:
+            tap.dy, tap.mask = dy, (mask if ctx.mode == MASK_BITS else None)
+        return dx, dres, dw, db, None, None, None, None, None, None, None
 
 
 def fused_bn_act(x, weight, bias, running_mean, running_var, eps=1e-5, momentum=0.1, relu=True, residual=None,
-                 part=None):
+                 part=None, res_tap=None):
     """Training-mode BN (+residual) (+ReLU) on a channels-last bf16 HIP tensor.  ``part``: the
-    [2, C, nrb] partial statistics when the producer (conv1x1_stats) already reduced them."""
-    return _FusedBNAct.apply(x, residual, weight, bias, running_mean, running_var, eps, momentum, relu, part)
+    [2, C, nrb] partial statistics when the producer (conv1x1_stats) already reduced them.
+    ``res_tap``: an armed ResidualTap -- the residual's gradient goes to its consumer instead
+    of autograd (the residual input then receives no gradient from this op)."""
+    return _FusedBNAct.apply(x, residual, weight, bias, running_mean, running_var, eps, momentum, relu, part,
+                             res_tap)
 
 
 class FusedBatchNorm2d(nn.BatchNorm2d):
@@ -171,12 +225,13 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
             return False
         return True
 
-    def forward(self, x, residual=None, stats=None):
+    def forward(self, x, residual=None, stats=None, res_tap=None):
         if self._fast_ok(x, residual):
             if self.training:
                 self._nbt_pending += 1
+                tap = res_tap if (res_tap is not None and res_tap.armed and residual is not None) else None
                 return fused_bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, self.eps,
-                                    self.momentum, self.relu, residual, stats)
+                                    self.momentum, self.relu, residual, stats, tap)
             if not torch.is_grad_enabled() or not (x.requires_grad or (residual is not None and
                                                                        residual.requires_grad)):
                 scale = self.weight / torch.sqrt(self.running_var + self.eps)
@@ -193,12 +248,77 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
         return y
 
 
-def conv_bn(conv: nn.Conv2d, bn: FusedBatchNorm2d, x, residual=None, fuse: bool = True):
+def conv_bn(conv: nn.Conv2d, bn: FusedBatchNorm2d, x, residual=None, fuse: bool = True, tap=None, res_tap=None,
+            alias: bool = False):
     """bn(conv(x), residual): a 1x1 conv that feeds a training-mode fused BN runs as the MFMA GEMM
-    with the BN statistics in its epilogue (one fewer pass over the conv output)."""
+    with the BN statistics in its epilogue (one fewer pass over the conv output).
+
+    Gradient fusion for residual blocks (see ResidualTap / _Conv1x1):
+      tap      this conv's dgrad epilogue adds the tap's residual gradient (armed here when the
+               MFMA path with its own dgrad is taken)
+      res_tap  this BN routes its residual gradient into that tap (only if armed)
+      alias    also return an alias of x whose gradient is summed in this conv's dgrad epilogue
+               -> returns (out, x_alias)"""
     if fuse and bn.training and conv1x1_ok(conv, x):
-        y, part = conv1x1_stats(x, conv.weight, conv.stride[0])
-        if bn._fast_ok(y, residual):
-            return bn(y, residual, stats=part)
-        return bn(y, residual)
-    return bn(conv(x), residual)
+        s = conv.stride[0]
+        own_tap = tap if s == 1 else None
+        outs = conv1x1_stats(x, conv.weight, s, own_tap, alias and s == 1)
+        y, part = outs[0], outs[1]
+        xa = outs[2] if len(outs) > 2 else x
+        if own_tap is not None:
+            own_tap.armed = True
+        out = bn(y, residual, stats=part, res_tap=res_tap) if bn._fast_ok(y, residual) else bn(y, residual)
+    else:
+        xa = x
+        out = bn(conv(x), residual)
+    return (out, xa) if alias else out
+
+
+def _pool_ok(m: nn.MaxPool2d, x: torch.Tensor) -> bool:
+    def two(v):
+        return tuple(v) if isinstance(v, (tuple, list)) else (v, v)
+
+    if m.return_indices or m.ceil_mode or two(m.kernel_size) != (3, 3) or two(m.stride) != (2, 2):
+        return False
+    if two(m.padding) != (1, 1) or two(m.dilation) != (1, 1):
+        return False
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0 and
+            x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0)
+
+
+class _MaxPool3s2(torch.autograd.Function):
+    """3x3/s2/p1 max pool on channels-last bf16 (hipps/csrc/pool.hip): 4-bit argmax codes,
+    gather-form backward (no atomics, no int64 index tensor)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        N, C, H, W = x.shape
+        Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        y = torch.empty((N, C, Ho, Wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+        code = torch.empty(N * Ho * Wo * (C // 8), dtype=torch.int32, device=x.device)
+        native().maxpool3s2_forward(x, y, code)
+        ctx.save_for_backward(code)
+        ctx.xshape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (code,) = ctx.saved_tensors
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dx = torch.empty(ctx.xshape, dtype=torch.bfloat16, device=dy.device, memory_format=torch.channels_last)
+        native().maxpool3s2_backward(dy, code, dx)
+        return dx
+
+
+class MaxPool2d(nn.MaxPool2d):
+    """nn.MaxPool2d; the ResNet stem case (3x3, stride 2, pad 1) on channels-last bf16 HIP
+    tensors runs the hipps kernels, everything else the PyTorch op."""
+
+    def __init__(self, *a, fused: bool = True, **kw):
+        super().__init__(*a, **kw)
+        self.fused = fused
+
+    def forward(self, x):
+        if self.fused and _pool_ok(self, x):
+            return _MaxPool3s2.apply(x)
+        return super().forward(x)

@@ -96,20 +96,96 @@ def test_conv_bn_autograd_matches_unfused(residual, stride):
         torch.testing.assert_close(a, b, rtol=3e-2, atol=3e-2)
 
 
+@pytest.mark.parametrize("masked", [False, True])
+def test_conv1x1_epilogue_add(masked):
+    """dgrad epilogue: y = conv(x) + add (* ReLU bits) vs the eager sum of the rounded conv."""
+    torch.manual_seed(3)
+    n, cin, h, w, cout = 2, 128, 9, 9, 256
+    x = _cl(torch.randn(n, cin, h, w, device=DEV).to(torch.bfloat16))
+    wt = (torch.randn(cout, cin, device=DEV) / cin ** 0.5).to(torch.bfloat16)
+    add = _cl(torch.randn(n, cout, h, w, device=DEV).to(torch.bfloat16))
+    mask = torch.randint(0, 256, (add.numel() // 8,), dtype=torch.uint8, device=DEV) if masked else None
+    y0 = _cl(torch.empty(n, cout, h, w, device=DEV, dtype=torch.bfloat16))
+    y1 = torch.empty_like(y0)
+    native().conv1x1_forward(x, wt, y0, None, h, w, 1)
+    native().conv1x1_forward(x, wt, y1, None, h, w, 1, add, mask)
+    want = (y0.float() + hnn._masked(add, mask, cout).float()).to(torch.bfloat16)
+    assert torch.equal(y1, want)
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (2, 16, 7, 9), (3, 8, 1, 2), (2, 32, 6, 6)])
+def test_maxpool3s2_matches_torch(shape):
+    torch.manual_seed(4)
+    x0 = _cl(torch.randint(-3, 4, shape, device=DEV).to(torch.bfloat16))  # many ties: tie rule must match
+    x = x0.clone().requires_grad_(True)
+    xr = x0.float().clone().requires_grad_(True)
+    pool = hnn.MaxPool2d(3, stride=2, padding=1)
+    y = pool(x)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(y.float(), yr)
+    g = _cl(torch.randn(yr.shape, device=DEV).to(torch.bfloat16))
+    y.backward(g)
+    yr.backward(g.float())
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
+
+
+def _resnet_run(R, m, x, conv, grad, pool):
+    R._FUSED_CONV, R._FUSED_GRAD = conv, grad
+    m.maxpool.fused = pool
+    try:
+        m.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = m(x)
+        y.float().sum().backward()
+    finally:
+        R._FUSED_CONV = R._FUSED_GRAD = True
+        m.maxpool.fused = True
+    return (y.float(), m.conv1.weight.grad.clone(), m.bn1.weight.grad.clone(), m.layer1[0].conv1.weight.grad.clone(),
+            m.layer1[1].conv1.weight.grad.clone(), m.layer2[0].downsample[0].weight.grad.clone(),
+            m.layer3[2].conv2.weight.grad.clone())
+
+
 def test_resnet50_fused_conv_matches_unfused():
+    """All ResNet fusions (1x1 MFMA conv + BN stats, residual-gradient epilogue sums, stem max
+    pool) against the plain path (MIOpen convs, autograd adds, PyTorch pool)."""
     import hipps.models.resnet as R
 
     torch.manual_seed(0)
     m = R.resnet50(num_classes=10).to(DEV).to(memory_format=torch.channels_last)
     x = _cl(torch.randn(4, 3, 64, 64, device=DEV))
-    out = {}
+    a = _resnet_run(R, m, x, True, True, True)
+    b = _resnet_run(R, m, x, False, False, False)
+    for u, v in zip(a, b):
+        torch.testing.assert_close(u, v, rtol=5e-2, atol=5e-2)
+
+
+@pytest.mark.parametrize("cin,width,stride,ds", [(256, 64, 1, False), (64, 64, 1, True), (256, 128, 2, True)])
+def test_bottleneck_gradient_fusions(cin, width, stride, ds):
+    """Residual-gradient epilogue sums (ResidualTap for identity blocks, x alias for downsample
+    blocks) only re-associate bf16 gradient sums: with a live residual branch (bn3 weight != 0)
+    x.grad and every weight gradient match the autograd-add path."""
+    import hipps.models.resnet as R
+
+    torch.manual_seed(5)
+    blk = R.Bottleneck(cin, width, stride=stride, downsample=ds).to(DEV).to(memory_format=torch.channels_last)
+    torch.nn.init.uniform_(blk.bn3.weight, 0.5, 1.5)
+    x0 = _cl(torch.randn(8, cin, 14, 14, device=DEV).to(torch.bfloat16))
+    g = None
+    res = {}
     for flag in (True, False):
-        R._FUSED_CONV = flag
-        m.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            y = m(x)
-        y.float().sum().backward()
-        out[flag] = (y.float(), m.conv1.weight.grad.clone(), m.layer1[0].conv1.weight.grad.clone())
-    R._FUSED_CONV = True
-    for a, b in zip(out[True], out[False]):
-        torch.testing.assert_close(a, b, rtol=5e-2, atol=5e-2)
+        R._FUSED_GRAD = flag
+        try:
+            blk.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = blk(x)
+            if g is None:
+                g = _cl(torch.randn(y.shape, device=DEV).to(torch.bfloat16))
+            y.backward(g)
+        finally:
+            R._FUSED_GRAD = True
+        res[flag] = [y.float(), x.grad.float()] + [p.grad.float().clone() for p in blk.parameters()]
+    for u, v in zip(res[True], res[False]):
+        scale = v.abs().max().item() + 1e-6
+        torch.testing.assert_close(u / scale, v / scale, rtol=0, atol=2e-2)
