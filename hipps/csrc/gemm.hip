@@ -49,7 +49,7 @@ __device__ __forceinline__ uint32_t add_bf16x2(uint32_t a, uint32_t b) {
                      __uint_as_float(a & 0xffff0000u) + __uint_as_float(b & 0xffff0000u));
 }
 
-template <int BN, bool STATS>
+template <int BN, bool STATS, bool ADD>
 __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W,
                                                     uint16_t* __restrict__ Y, float* __restrict__ pa,
                                                     float* __restrict__ pb, const uint16_t* __restrict__ R,
@@ -130,12 +130,29 @@ __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int KT = K / kGBK;
+  constexpr int RCH = BN / 8;                // 16-byte chunks per output row
+  constexpr int NOUT = kGBM * RCH / 256;     // output chunks per thread
+  u32x4 rr[NOUT];                            // epilogue addend, prefetched during the last k-tile
+  uint32_t rmb[NOUT];
   HIPPS_GLOAD(0);
   HIPPS_SSTORE(0);
   __syncthreads();
   for (int kt = 0; kt < KT; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < KT) HIPPS_GLOAD(kt + 1);
+    if (kt + 1 < KT) {
+      HIPPS_GLOAD(kt + 1);
+    } else if (ADD) {  // no next tile to fetch: load the addend now, hidden by the MFMAs
+#pragma unroll
+      for (int i = 0; i < NOUT; ++i) {
+        const int id = t + 256 * i;
+        const int row = id / RCH, c = id - row * RCH;
+        const bool ok = m0 + row < M;
+        const int64_t o = (int64_t)(ok ? m0 + row : m0) * N + n0 + c * 8;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(R + o);
+        rr[i] = ok ? v : u32x4{0u, 0u, 0u, 0u};
+        rmb[i] = RM != nullptr ? (uint32_t)RM[o >> 3] : 0xffu;
+      }
+    }
     const uint16_t* As = lds + cur * STAGE;
     const uint16_t* Bs = As + kGBM * kGBK;
 #pragma unroll
@@ -196,23 +213,20 @@ __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__
     }
   }
   __syncthreads();
-  constexpr int RCH = BN / 8;  // 16-byte chunks per output row
 #pragma unroll
-  for (int i = 0; i < kGBM * RCH / 256; ++i) {
+  for (int i = 0; i < NOUT; ++i) {
     const int id = t + 256 * i;
     const int row = id / RCH, c = id - row * RCH;
     if (m0 + row < M) {
       const int64_t o = (int64_t)(m0 + row) * N + n0 + c * 8;
       uint4 v = *reinterpret_cast<const uint4*>(lds + row * EP + c * 8);
-      if (R != nullptr) {  // fused "+ R" (R * ReLU-mask bits): a second gradient path into Y
-        uint4 r = *reinterpret_cast<const uint4*>(R + o);
-        if (RM != nullptr) {  // one mask byte per 8 channels = this 16-byte chunk
-          const uint32_t mb = RM[o >> 3];
-          r.x &= (mb & 1u ? 0xffffu : 0u) | (mb & 2u ? 0xffff0000u : 0u);
-          r.y &= (mb & 4u ? 0xffffu : 0u) | (mb & 8u ? 0xffff0000u : 0u);
-          r.z &= (mb & 16u ? 0xffffu : 0u) | (mb & 32u ? 0xffff0000u : 0u);
-          r.w &= (mb & 64u ? 0xffffu : 0u) | (mb & 128u ? 0xffff0000u : 0u);
-        }
+      if (ADD) {  // fused "+ R" (R * ReLU-mask bits): a second gradient path into Y
+        u32x4 r = rr[i];
+        const uint32_t mb = rmb[i];  // one mask byte per 8 channels = this 16-byte chunk
+        r.x &= (mb & 1u ? 0xffffu : 0u) | (mb & 2u ? 0xffff0000u : 0u);
+        r.y &= (mb & 4u ? 0xffffu : 0u) | (mb & 8u ? 0xffff0000u : 0u);
+        r.z &= (mb & 16u ? 0xffffu : 0u) | (mb & 32u ? 0xffff0000u : 0u);
+        r.w &= (mb & 64u ? 0xffffu : 0u) | (mb & 128u ? 0xffff0000u : 0u);
         v.x = add_bf16x2(v.x, r.x);
         v.y = add_bf16x2(v.y, r.y);
         v.z = add_bf16x2(v.z, r.z);
@@ -405,6 +419,129 @@ __global__ __launch_bounds__(kBlock) void k_wgrad_reduce2(const float* __restric
   reinterpret_cast<float4*>(dw)[i] = a;
 }
 
+// ------------------------------------------------------------------------------------------
+// Weight gradient v2 (channel counts multiples of 64, every ResNet 1x1 conv): the output tile
+// is TN x TK with TN, TK in {64, 128} picked per shape, so Cin = 64 / Cout = 64 layers do no
+// MFMA work on zero padding (v1 always used 128 x 128: 4x the work on the largest-M layer).
+// The M split S targets ~2 blocks per CU while keeping the fp32 partial slabs (S * N * K * 4 B,
+// written once, read once) small next to the operand bytes; v1's fixed ~2048 blocks wrote more
+// partial bytes than it read operands on the deep layers (1024x512: 134 MB of slabs).
+template <int TW>
+__device__ __forceinline__ int wt_off(int row, int ch) {  // byte offset in a [rows][TW x bf16] tile
+  if (TW == 128) return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+  return 128 * row + 16 * (ch ^ (((row & 3) << 1) | ((row >> 2) & 1)));
+}
+
+template <int TW>
+__device__ __forceinline__ bf16x8 tr_frag_w(const uint8_t* tile, int row0, int col0, int lane) {
+  const int il = lane & 15, q = il >> 2, p = il & 3;
+  const int r = row0 + 8 * (lane >> 4) + q;
+  const int ch = (col0 >> 3) + (p >> 1);
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + wt_off<TW>(r, ch) + 8 * (p & 1)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + wt_off<TW>(r + 4, ch) + 8 * (p & 1)));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <int TN, int TK>
+__global__ __launch_bounds__(256) void k_conv1x1_wgrad2(const uint16_t* __restrict__ dY, const uint16_t* __restrict__ X,
+                                                        float* __restrict__ part, int M, int N, int K, int Ho, int Wo,
+                                                        int Hi, int Wi, int stride, int chunk, int tn, int tk) {
+  constexpr int YCH = TN / 8, XCH = TK / 8;        // 16-byte chunks per staged row
+  constexpr int YP = 64 * YCH / 256, XP = 64 * XCH / 256;  // chunks per thread per stage
+  constexpr int YT = kWMS * TN * 2, XT = kWMS * TK * 2;  // bytes per staged tile
+  constexpr int FN = TN / 32, FK = TK / 32;        // 16-wide fragments per wave (2x2 waves)
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * (YT + XT)];
+  int bid = blockIdx.x;
+  const int nblk = gridDim.x;
+  if ((nblk & 7) == 0) bid = (bid & 7) * (nblk >> 3) + (bid >> 3);  // a split's tiles share an XCD
+  const int tiles = tn * tk;
+  const int sidx = bid / tiles, tile = bid - sidx * tiles;
+  const int n0 = (tile / tk) * TN, k0 = (tile % tk) * TK;
+  const int mbeg = sidx * chunk, mend = min(M, mbeg + chunk);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wn = w >> 1, wk = w & 1;
+  const int ych = t % YCH, xch = t % XCH;  // this thread's fixed 16-byte column chunk
+
+  u32x4 ry[YP], rx[XP];
+  auto src_row = [=](int m) -> int64_t {
+    if (stride == 1) return m;
+    const int hw = Ho * Wo, img = m / hw, rem = m - img * hw;
+    const int ho = rem / Wo, wo = rem - ho * Wo;
+    return ((int64_t)img * Hi + (int64_t)ho * stride) * Wi + (int64_t)wo * stride;
+  };
+#define HIPPS_W2LOAD(mb_)                                                                          \
+  {                                                                                                \
+    _Pragma("unroll") for (int i = 0; i < YP; ++i) {                                               \
+      const int m_ = (mb_) + t / YCH + (256 / YCH) * i;                                            \
+      const u32x4 v_ = *reinterpret_cast<const u32x4*>(dY + (int64_t)(m_ < mend ? m_ : mbeg) * N + \
+                                                       n0 + ych * 8);                              \
+      ry[i] = m_ < mend ? v_ : u32x4{0u, 0u, 0u, 0u};                                              \
+    }                                                                                              \
+    _Pragma("unroll") for (int i = 0; i < XP; ++i) {                                               \
+      const int m_ = (mb_) + t / XCH + (256 / XCH) * i;                                            \
+      const u32x4 v_ = *reinterpret_cast<const u32x4*>(X + src_row(m_ < mend ? m_ : mbeg) * K +    \
+                                                       k0 + xch * 8);                              \
+      rx[i] = m_ < mend ? v_ : u32x4{0u, 0u, 0u, 0u};                                              \
+    }                                                                                              \
+  }
+#define HIPPS_W2STORE(s_)                                                                          \
+  {                                                                                                \
+    uint8_t* ty_ = lds + (s_) * (YT + XT);                                                         \
+    uint8_t* tx_ = ty_ + YT;                                                                       \
+    _Pragma("unroll") for (int i = 0; i < YP; ++i)                                                 \
+        *reinterpret_cast<u32x4*>(ty_ + wt_off<TN>(t / YCH + (256 / YCH) * i, ych)) = ry[i];       \
+    _Pragma("unroll") for (int i = 0; i < XP; ++i)                                                 \
+        *reinterpret_cast<u32x4*>(tx_ + wt_off<TK>(t / XCH + (256 / XCH) * i, xch)) = rx[i];       \
+  }
+
+  f32x4 acc[FN][FK];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FK; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nst = (mend - mbeg + kWMS - 1) / kWMS;
+  HIPPS_W2LOAD(mbeg);
+  HIPPS_W2STORE(0);
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int cur = st & 1;
+    if (st + 1 < nst) HIPPS_W2LOAD(mbeg + (st + 1) * kWMS);
+    const uint8_t* ty = lds + cur * (YT + XT);
+    const uint8_t* tx = ty + YT;
+#pragma unroll
+    for (int ks = 0; ks < kWMS / 32; ++ks) {
+      bf16x8 a[FN], b[FK];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) a[i] = tr_frag_w<TN>(ty, ks * 32, wn * (TN / 2) + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < FK; ++j) b[j] = tr_frag_w<TK>(tx, ks * 32, wk * (TK / 2) + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FK; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (st + 1 < nst) HIPPS_W2STORE(cur ^ 1);
+    __syncthreads();
+  }
+#undef HIPPS_W2LOAD
+#undef HIPPS_W2STORE
+  // D map: column (k) = lane & 15, row (n) = (lane >> 4) * 4 + r
+  float* out = part + (int64_t)sidx * N * K;
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FK; ++j) {
+      const int k = k0 + wk * (TK / 2) + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * (TN / 2) + i * 16 + (lane >> 4) * 4 + r;
+        out[(int64_t)n * K + k] = acc[i][j][r];
+      }
+    }
+}
+
 // ==========================================================================================
 int64_t conv1x1_mtiles(int64_t M) { return (M + kGBM - 1) / kGBM; }
 
@@ -461,13 +598,14 @@ void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
   const uint16_t* xp = (const uint16_t*)x.data_ptr();
   const uint16_t* wp = (const uint16_t*)w.data_ptr();
   uint16_t* yp = (uint16_t*)y.data_ptr();
-#define HIPPS_C1(BNv, ST)                                                                                  \
-  hipLaunchKernelGGL((k_conv1x1_nt<BNv, ST>), (int)nblk, 256, 0, stream, xp, wp, yp, pa, pb, rp, mp, (int)M, (int)N, \
+#define HIPPS_C1(BNv, ST, AD)                                                                              \
+  hipLaunchKernelGGL((k_conv1x1_nt<BNv, ST, AD>), (int)nblk, 256, 0, stream, xp, wp, yp, pa, pb, rp, mp, (int)M, (int)N, \
                      (int)K, (int)Ho, (int)Wo, (int)Hi, (int)Wi, (int)stride, (int)mtiles, (int)ntiles)
+  TORCH_CHECK(!(pa && rp), "conv1x1: the statistics epilogue and the add epilogue are exclusive");
   if (bn128) {
-    if (pa) HIPPS_C1(128, true); else HIPPS_C1(128, false);
+    if (pa) HIPPS_C1(128, true, false); else if (rp) HIPPS_C1(128, false, true); else HIPPS_C1(128, false, false);
   } else {
-    if (pa) HIPPS_C1(64, true); else HIPPS_C1(64, false);
+    if (pa) HIPPS_C1(64, true, false); else if (rp) HIPPS_C1(64, false, true); else HIPPS_C1(64, false, false);
   }
 #undef HIPPS_C1
 }
@@ -492,6 +630,49 @@ void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64
   for (const at::Tensor* t : {&x, &dy, &dw})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "conv1x1_wgrad: 16-byte aligned tensors");
   TORCH_CHECK(M < (int64_t(1) << 31), "conv1x1_wgrad: size");
+  auto stream0 = c10::hip::getCurrentHIPStream();
+  if (N % 64 == 0 && K % 64 == 0) {  // v2: shape-fitted tiles, bounded split
+    const int TN = N % 128 == 0 ? 128 : 64, TK = K % 128 == 0 ? 128 : 64;
+    const int64_t tn = N / TN, tk = K / TK, tiles = tn * tk;
+    // one wave of resident blocks: 256 CUs x (2 | 3 | 5) blocks per CU at (186 | 124 | 92) VGPRs
+    const int64_t resident = 256 * (TN * TK == 128 * 128 ? 2 : TN * TK == 128 * 64 ? 3 : 5);
+    int64_t S = std::max<int64_t>(1, resident / tiles);
+    S = std::min<int64_t>(S, std::max<int64_t>(1, M / (8 * kWMS)));           // >= 8 stages per block
+    S = std::min<int64_t>(S, std::max<int64_t>(1, M * (N + K) / (4 * N * K)));  // slabs <= operand bytes
+    const int64_t chunk = ((M + S - 1) / S + kWMS - 1) / kWMS * kWMS;
+    S = (M + chunk - 1) / chunk;
+    TORCH_CHECK(S * tiles < (int64_t(1) << 31), "conv1x1_wgrad: grid");
+    at::Tensor part = S == 1 ? dw : at::empty({S, N, K}, dw.options());
+    const uint16_t* dyp = (const uint16_t*)dy.data_ptr();
+    const uint16_t* xp = (const uint16_t*)x.data_ptr();
+#define HIPPS_W2(TNv, TKv)                                                                                      \
+  hipLaunchKernelGGL((k_conv1x1_wgrad2<TNv, TKv>), (int)(S * tiles), 256, 0, stream0, dyp, xp,                 \
+                     part.data_ptr<float>(), (int)M, (int)N, (int)K, (int)Ho, (int)Wo, (int)Hi, (int)Wi, (int)stride, \
+                     (int)chunk, (int)tn, (int)tk)
+    if (TN == 128 && TK == 128) HIPPS_W2(128, 128);
+    else if (TN == 128) HIPPS_W2(128, 64);
+    else if (TK == 128) HIPPS_W2(64, 128);
+    else HIPPS_W2(64, 64);
+#undef HIPPS_W2
+    if (S > 1) {
+      // fixed-order slab sum; split over G groups when N*K alone is too few threads to keep the
+      // loads in flight (64x64 outputs: 1024 float4 lanes x S serial loads was ~60 us)
+      const int64_t NK4 = N * K / 4;
+      const int G = (int)std::min<int64_t>(S, std::max<int64_t>(1, (65536 + NK4 - 1) / NK4));
+      const unsigned gx = (unsigned)((NK4 + kBlock - 1) / kBlock);
+      if (G == 1) {
+        hipLaunchKernelGGL(k_wgrad_reduce1, dim3(gx, 1), kBlock, 0, stream0, part.data_ptr<float>(), (int)S, 1, NK4,
+                           dw.data_ptr<float>());
+      } else {
+        auto tmp = at::empty({(int64_t)G, N, K}, dw.options());
+        hipLaunchKernelGGL(k_wgrad_reduce1, dim3(gx, G), kBlock, 0, stream0, part.data_ptr<float>(), (int)S, G, NK4,
+                           tmp.data_ptr<float>());
+        hipLaunchKernelGGL(k_wgrad_reduce2, gx, kBlock, 0, stream0, tmp.data_ptr<float>(), G, NK4,
+                           dw.data_ptr<float>());
+      }
+    }
+    return;
+  }
   const int64_t tn = (N + kWT - 1) / kWT, tk = (K + kWT - 1) / kWT, tiles = tn * tk;
   int64_t S = std::max<int64_t>(1, std::min<int64_t>(2048 / tiles, (M + kWMS - 1) / kWMS));
   int64_t chunk = ((M + S - 1) / S + kWMS - 1) / kWMS * kWMS;

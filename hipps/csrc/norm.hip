@@ -138,28 +138,31 @@ __global__ __launch_bounds__(kBlock) void k_bn_reduce(const uint16_t* __restrict
   }
 }
 
-// Combine partial[c][rb] over rb: one wave per channel (4 channels per workgroup), lanes read
-// consecutive partials (coalesced), fp64 sums, 6-step shuffle tree.  (The first version looped
-// serially per channel: 180-270 us per call, profiles/bn_micro_r1.txt.)
-constexpr int kFinCh = 4;
+// Combine partial[c][rb] over rb: one workgroup per channel, the 256 lanes read consecutive
+// partials (coalesced), fp64 sums, shuffle tree per wave + fixed-order combine of the 4 waves.
+// (v1 looped serially per channel: 180-270 us per call, profiles/bn_micro_r1.txt; v2 used one
+// wave per channel: 12 us per call on the 1x1-GEMM partials, nrb = M/128 = 6272 on layer1,
+// profiles/bench_n1_steady_r1c.txt.)
+constexpr int kFinCh = 1;
 __device__ __forceinline__ bool combine_partials(const float* __restrict__ pa, const float* __restrict__ pb, int nrb,
                                                  int C, double& s, double& q) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * kFinCh + (threadIdx.x >> 6);
+  __shared__ double red[2][kBlock / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x;
   double a = 0.0, b = 0.0;
-  if (c < C) {
-    const float* ra = pa + (int64_t)c * nrb;
-    const float* rb = pb + (int64_t)c * nrb;
-    for (int i = lane; i < nrb; i += 64) { a += ra[i]; b += rb[i]; }
-  }
+  const float* ra = pa + (int64_t)c * nrb;
+  const float* rb = pb + (int64_t)c * nrb;
+  for (int i = threadIdx.x; i < nrb; i += kBlock) { a += ra[i]; b += rb[i]; }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     a += __shfl_xor(a, o, 64);
     b += __shfl_xor(b, o, 64);
   }
-  s = a;
-  q = b;
-  return lane == 0 && c < C;
+  if (lane == 0) { red[0][wv] = a; red[1][wv] = b; }
+  __syncthreads();
+  s = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+  q = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  return threadIdx.x == 0 && c < C;
 }
 
 // forward finalize: stats + running stats + per-channel scale/shift
@@ -172,7 +175,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_finalize_fwd(const float* __restr
                                                             float* __restrict__ shift) {
   double s, q;
   if (!combine_partials(pa, pb, nrb, C, s, q)) return;
-  const int c = blockIdx.x * kFinCh + (threadIdx.x >> 6);
+  const int c = blockIdx.x;
   const double m = s / (double)M;
   double var = q / (double)M - m * m;
   if (var < 0.0) var = 0.0;
@@ -198,7 +201,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_finalize_bwd(const float* __restr
                                                             float* __restrict__ ck1, float* __restrict__ ck0) {
   double s, q;
   if (!combine_partials(pa, pb, nrb, C, s, q)) return;
-  const int c = blockIdx.x * kFinCh + (threadIdx.x >> 6);
+  const int c = blockIdx.x;
   if (dw) dw[c] = (float)q;
   if (db) db[c] = (float)s;
   const double is = invstd[c];

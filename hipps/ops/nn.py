@@ -20,9 +20,9 @@ from ._native import native
 
 import os as _os
 
-# weight gradient of the MFMA 1x1 path: own split-M kernel (1) or MIOpen (0, default: measured
-# faster in the full step, profiles/conv1x1_wgrad_r1.json)
-_OWN_WGRAD = _os.environ.get("HIPPS_CONV_WGRAD", "0") != "0"
+# weight gradient of the MFMA 1x1 path: own split-M kernel (1, default; v2 beats MIOpen on the
+# ResNet-50 shapes, profiles/conv1x1_wgrad_v2.json) or MIOpen (0), for A/B runs
+_OWN_WGRAD = _os.environ.get("HIPPS_CONV_WGRAD", "1") != "0"
 
 MASK_NONE, MASK_X, MASK_Y, MASK_BITS = 0, 1, 2, 3
 
