@@ -52,6 +52,7 @@ void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
 void maxpool3s2_forward(at::Tensor x, at::Tensor y, at::Tensor code);
 void maxpool3s2_backward(at::Tensor dy, at::Tensor code, at::Tensor dx);
 void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64_t Wi, int64_t stride);
+void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t KW, int64_t stride, int64_t pad);
 namespace rt {
 void bind_control(pybind11::module& m);
 void bind_ipc(pybind11::module& m);
@@ -85,6 +86,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("part"), pybind11::arg("Hi"),
         pybind11::arg("Wi"), pybind11::arg("stride"), pybind11::arg("add") = pybind11::none(),
         pybind11::arg("add_mask") = pybind11::none());
+  m.def("conv_wgrad", &hipps::conv_wgrad, "MFMA KxK conv weight gradient (implicit GEMM, split-M, fp32 dW)");
   m.def("maxpool3s2_forward", &hipps::maxpool3s2_forward, "3x3/s2/p1 max pool, channels-last bf16, 4-bit tap codes");
   m.def("maxpool3s2_backward", &hipps::maxpool3s2_backward, "3x3/s2/p1 max pool backward (gather form, no atomics)");
   m.def("conv1x1_wgrad", &hipps::conv1x1_wgrad, "MFMA 1x1 conv weight gradient (tr_b16 LDS reads, split-M)");

@@ -49,12 +49,26 @@ __device__ __forceinline__ uint32_t add_bf16x2(uint32_t a, uint32_t b) {
                      __uint_as_float(a & 0xffff0000u) + __uint_as_float(b & 0xffff0000u));
 }
 
-template <int BN, bool STATS, bool ADD>
+// Backward BatchNorm statistics in the dgrad epilogue.  When the GEMM output Y is the COMPLETE
+// gradient dy of a training BatchNorm's output (the conv is that BN output's only consumer, every
+// other gradient path having been summed in through R), the BN backward's reduction pass
+//   a[c] = sum_m dz,  b[c] = sum_m dz * (x - mean) * invstd,  dz = dy * relu'
+// is done here on the tile still in registers (+ one read of the BN input x), instead of by a
+// separate kernel that re-reads dy and x.  relu' = the BN's stored ReLU bits, or recomputed from
+// x*scale + shift > 0 (bits == nullptr).  Per-M-tile partials go to pa/pb[c][mtile].
+struct BnBwdTap {
+  const uint16_t* x;
+  const uint8_t* bits;
+  const float *mean, *invstd, *scale, *shift;
+};
+
+template <int BN, bool STATS, bool ADD, bool BST = false>
 __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W,
                                                     uint16_t* __restrict__ Y, float* __restrict__ pa,
                                                     float* __restrict__ pb, const uint16_t* __restrict__ R,
                                                     const uint8_t* __restrict__ RM, int M, int N, int K, int Ho,
-                                                    int Wo, int Hi, int Wi, int stride, int mtiles, int ntiles) {
+                                                    int Wo, int Hi, int Wi, int stride, int mtiles, int ntiles,
+                                                    BnBwdTap bt) {
   constexpr int WM = GemmCfg<BN>::WM, WN = GemmCfg<BN>::WN;
   constexpr int TM = kGBM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
@@ -426,6 +440,22 @@ __global__ __launch_bounds__(kBlock) void k_wgrad_reduce2(const float* __restric
 // The M split S targets ~2 blocks per CU while keeping the fp32 partial slabs (S * N * K * 4 B,
 // written once, read once) small next to the operand bytes; v1's fixed ~2048 blocks wrote more
 // partial bytes than it read operands on the deep layers (1024x512: 134 MB of slabs).
+// n / d for 0 <= n < 2^31 with a host-precomputed multiplier (round-up method): the per-row
+// pixel decomposition of the implicit-GEMM loaders was two runtime integer divisions per 16-byte
+// load -- enough VALU work to make the 3x3 weight gradient slower than MIOpen's.
+struct FastDiv {
+  uint32_t d, mul, shift;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint64_t mul = ((((1ull << l) - d) << 32) / d) + 1;
+  return FastDiv{d, (uint32_t)mul, l};
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.mul) + n) >> f.shift;
+}
+
 template <int TW>
 __device__ __forceinline__ int wt_off(int row, int ch) {  // byte offset in a [rows][TW x bf16] tile
   if (TW == 128) return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
@@ -443,10 +473,15 @@ __device__ __forceinline__ bf16x8 tr_frag_w(const uint8_t* tile, int row0, int c
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+// KxK convolutions (implicit GEMM over K = KH*KW*Cin, k = (r*KW + s)*Cin + c: the physical
+// order of a channels-last [Cout, Cin, KH, KW] weight): a K tile never straddles two taps
+// (Cin % TK == 0), so each block has ONE tap (r, s) and its X loader reads the input pixel
+// (ho*stride - pad + r, wo*stride - pad + s) of each output row m, zeros outside the image.
 template <int TN, int TK>
 __global__ __launch_bounds__(256) void k_conv1x1_wgrad2(const uint16_t* __restrict__ dY, const uint16_t* __restrict__ X,
                                                         float* __restrict__ part, int M, int N, int K, int Ho, int Wo,
-                                                        int Hi, int Wi, int stride, int chunk, int tn, int tk) {
+                                                        int Hi, int Wi, int stride, int chunk, int tn, int tk, int Cin,
+                                                        int KW, int pad, FastDiv fd_hw, FastDiv fd_w) {
   constexpr int YCH = TN / 8, XCH = TK / 8;        // 16-byte chunks per staged row
   constexpr int YP = 64 * YCH / 256, XP = 64 * XCH / 256;  // chunks per thread per stage
   constexpr int YT = kWMS * TN * 2, XT = kWMS * TK * 2;  // bytes per staged tile
@@ -463,12 +498,18 @@ __global__ __launch_bounds__(256) void k_conv1x1_wgrad2(const uint16_t* __restri
   const int wn = w >> 1, wk = w & 1;
   const int ych = t % YCH, xch = t % XCH;  // this thread's fixed 16-byte column chunk
 
+  const int tap = k0 / Cin, c0 = k0 - tap * Cin;
+  const int kr = tap / KW, kc = tap - (tap / KW) * KW;
+  const bool direct = KW == 1 && pad == 0 && stride == 1 && Cin == K;  // plain 1x1: row m is pixel m
   u32x4 ry[YP], rx[XP];
-  auto src_row = [=](int m) -> int64_t {
-    if (stride == 1) return m;
-    const int hw = Ho * Wo, img = m / hw, rem = m - img * hw;
-    const int ho = rem / Wo, wo = rem - ho * Wo;
-    return ((int64_t)img * Hi + (int64_t)ho * stride) * Wi + (int64_t)wo * stride;
+  // element offset of (input pixel of output row m under this block's tap, channel c0); -1 = padding
+  auto src_off = [=](int m) -> int64_t {
+    if (direct) return (int64_t)m * Cin + c0;
+    const int img = (int)fdiv((uint32_t)m, fd_hw), rem = m - img * (int)fd_hw.d;
+    const int ho = (int)fdiv((uint32_t)rem, fd_w), wo = rem - ho * Wo;
+    const int hi = ho * stride - pad + kr, wi = wo * stride - pad + kc;
+    if (hi < 0 || hi >= Hi || wi < 0 || wi >= Wi) return -1;
+    return (((int64_t)img * Hi + hi) * Wi + wi) * Cin + c0;
   };
 #define HIPPS_W2LOAD(mb_)                                                                          \
   {                                                                                                \
@@ -480,9 +521,9 @@ __global__ __launch_bounds__(256) void k_conv1x1_wgrad2(const uint16_t* __restri
     }                                                                                              \
     _Pragma("unroll") for (int i = 0; i < XP; ++i) {                                               \
       const int m_ = (mb_) + t / XCH + (256 / XCH) * i;                                            \
-      const u32x4 v_ = *reinterpret_cast<const u32x4*>(X + src_row(m_ < mend ? m_ : mbeg) * K +    \
-                                                       k0 + xch * 8);                              \
-      rx[i] = m_ < mend ? v_ : u32x4{0u, 0u, 0u, 0u};                                              \
+      const int64_t so_ = m_ < mend ? src_off(m_) : -1;                                            \
+      const u32x4 v_ = *reinterpret_cast<const u32x4*>(X + (so_ < 0 ? 0 : so_) + xch * 8);         \
+      rx[i] = so_ >= 0 ? v_ : u32x4{0u, 0u, 0u, 0u};                                               \
     }                                                                                              \
   }
 #define HIPPS_W2STORE(s_)                                                                          \
@@ -611,6 +652,52 @@ void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
 }
 
 
+// v2 weight gradient launcher: dW[N][K] (K = KH*KW*Cin) as S split-M partial slabs + fixed-order sum.
+static void launch_wgrad2(const at::Tensor& dy, const at::Tensor& x, at::Tensor& dw, int64_t M, int64_t N, int64_t K,
+                          int64_t Cin, int64_t Ho, int64_t Wo, int64_t Hi, int64_t Wi, int64_t stride, int64_t KW,
+                          int64_t pad, hipStream_t stream0) {
+  const int TN = N % 128 == 0 ? 128 : 64, TK = Cin % 128 == 0 ? 128 : 64;  // a K tile stays in one tap
+  const int64_t tn = N / TN, tk = K / TK, tiles = tn * tk;
+  // one wave of resident blocks: 256 CUs x (2 | 3 | 5) blocks per CU at (186 | 124 | 92) VGPRs
+  const int64_t resident = 256 * (TN * TK == 128 * 128 ? 2 : TN * TK == 128 * 64 ? 3 : 5);
+  int64_t S = std::max<int64_t>(1, resident / tiles);
+  S = std::min<int64_t>(S, std::max<int64_t>(1, M / (8 * kWMS)));           // >= 8 stages per block
+  S = std::min<int64_t>(S, std::max<int64_t>(1, M * (N + K) / (4 * N * K)));  // slabs <= operand bytes
+  const int64_t chunk = ((M + S - 1) / S + kWMS - 1) / kWMS * kWMS;
+  S = (M + chunk - 1) / chunk;
+  TORCH_CHECK(S * tiles < (int64_t(1) << 31), "conv wgrad: grid");
+  at::Tensor part = S == 1 ? dw : at::empty({S, N, K}, dw.options());
+  const FastDiv fd_hw = make_fastdiv((uint32_t)(Ho * Wo)), fd_w = make_fastdiv((uint32_t)Wo);
+  const uint16_t* dyp = (const uint16_t*)dy.data_ptr();
+  const uint16_t* xp = (const uint16_t*)x.data_ptr();
+#define HIPPS_W2(TNv, TKv)                                                                                    \
+  hipLaunchKernelGGL((k_conv1x1_wgrad2<TNv, TKv>), (int)(S * tiles), 256, 0, stream0, dyp, xp,               \
+                     part.data_ptr<float>(), (int)M, (int)N, (int)K, (int)Ho, (int)Wo, (int)Hi, (int)Wi,      \
+                     (int)stride, (int)chunk, (int)tn, (int)tk, (int)Cin, (int)KW, (int)pad, fd_hw, fd_w)
+  if (TN == 128 && TK == 128) HIPPS_W2(128, 128);
+  else if (TN == 128) HIPPS_W2(128, 64);
+  else if (TK == 128) HIPPS_W2(64, 128);
+  else HIPPS_W2(64, 64);
+#undef HIPPS_W2
+  if (S > 1) {
+    // fixed-order slab sum; split over G groups when N*K alone is too few threads to keep the
+    // loads in flight (64x64 outputs: 1024 float4 lanes x S serial loads was ~60 us)
+    const int64_t NK4 = N * K / 4;
+    const int G = (int)std::min<int64_t>(S, std::max<int64_t>(1, (65536 + NK4 - 1) / NK4));
+    const unsigned gx = (unsigned)((NK4 + kBlock - 1) / kBlock);
+    if (G == 1) {
+      hipLaunchKernelGGL(k_wgrad_reduce1, dim3(gx, 1), kBlock, 0, stream0, part.data_ptr<float>(), (int)S, 1, NK4,
+                         dw.data_ptr<float>());
+    } else {
+      auto tmp = at::empty({(int64_t)G, N, K}, dw.options());
+      hipLaunchKernelGGL(k_wgrad_reduce1, dim3(gx, G), kBlock, 0, stream0, part.data_ptr<float>(), (int)S, G, NK4,
+                         tmp.data_ptr<float>());
+      hipLaunchKernelGGL(k_wgrad_reduce2, gx, kBlock, 0, stream0, tmp.data_ptr<float>(), G, NK4,
+                         dw.data_ptr<float>());
+    }
+  }
+}
+
 // dy: [img, Cout, Ho, Wo] channels-last bf16; x: [img, Cin, Hi, Wi] channels-last bf16;
 // dw: f32 [Cout, Cin] (written, not accumulated).
 void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64_t Wi, int64_t stride) {
@@ -632,45 +719,7 @@ void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64
   TORCH_CHECK(M < (int64_t(1) << 31), "conv1x1_wgrad: size");
   auto stream0 = c10::hip::getCurrentHIPStream();
   if (N % 64 == 0 && K % 64 == 0) {  // v2: shape-fitted tiles, bounded split
-    const int TN = N % 128 == 0 ? 128 : 64, TK = K % 128 == 0 ? 128 : 64;
-    const int64_t tn = N / TN, tk = K / TK, tiles = tn * tk;
-    // one wave of resident blocks: 256 CUs x (2 | 3 | 5) blocks per CU at (186 | 124 | 92) VGPRs
-    const int64_t resident = 256 * (TN * TK == 128 * 128 ? 2 : TN * TK == 128 * 64 ? 3 : 5);
-    int64_t S = std::max<int64_t>(1, resident / tiles);
-    S = std::min<int64_t>(S, std::max<int64_t>(1, M / (8 * kWMS)));           // >= 8 stages per block
-    S = std::min<int64_t>(S, std::max<int64_t>(1, M * (N + K) / (4 * N * K)));  // slabs <= operand bytes
-    const int64_t chunk = ((M + S - 1) / S + kWMS - 1) / kWMS * kWMS;
-    S = (M + chunk - 1) / chunk;
-    TORCH_CHECK(S * tiles < (int64_t(1) << 31), "conv1x1_wgrad: grid");
-    at::Tensor part = S == 1 ? dw : at::empty({S, N, K}, dw.options());
-    const uint16_t* dyp = (const uint16_t*)dy.data_ptr();
-    const uint16_t* xp = (const uint16_t*)x.data_ptr();
-#define HIPPS_W2(TNv, TKv)                                                                                      \
-  hipLaunchKernelGGL((k_conv1x1_wgrad2<TNv, TKv>), (int)(S * tiles), 256, 0, stream0, dyp, xp,                 \
-                     part.data_ptr<float>(), (int)M, (int)N, (int)K, (int)Ho, (int)Wo, (int)Hi, (int)Wi, (int)stride, \
-                     (int)chunk, (int)tn, (int)tk)
-    if (TN == 128 && TK == 128) HIPPS_W2(128, 128);
-    else if (TN == 128) HIPPS_W2(128, 64);
-    else if (TK == 128) HIPPS_W2(64, 128);
-    else HIPPS_W2(64, 64);
-#undef HIPPS_W2
-    if (S > 1) {
-      // fixed-order slab sum; split over G groups when N*K alone is too few threads to keep the
-      // loads in flight (64x64 outputs: 1024 float4 lanes x S serial loads was ~60 us)
-      const int64_t NK4 = N * K / 4;
-      const int G = (int)std::min<int64_t>(S, std::max<int64_t>(1, (65536 + NK4 - 1) / NK4));
-      const unsigned gx = (unsigned)((NK4 + kBlock - 1) / kBlock);
-      if (G == 1) {
-        hipLaunchKernelGGL(k_wgrad_reduce1, dim3(gx, 1), kBlock, 0, stream0, part.data_ptr<float>(), (int)S, 1, NK4,
-                           dw.data_ptr<float>());
-      } else {
-        auto tmp = at::empty({(int64_t)G, N, K}, dw.options());
-        hipLaunchKernelGGL(k_wgrad_reduce1, dim3(gx, G), kBlock, 0, stream0, part.data_ptr<float>(), (int)S, G, NK4,
-                           tmp.data_ptr<float>());
-        hipLaunchKernelGGL(k_wgrad_reduce2, gx, kBlock, 0, stream0, tmp.data_ptr<float>(), G, NK4,
-                           dw.data_ptr<float>());
-      }
-    }
+    launch_wgrad2(dy, x, dw, M, N, K, K, Ho, Wo, Hi, Wi, stride, 1, 0, stream0);
     return;
   }
   const int64_t tn = (N + kWT - 1) / kWT, tk = (K + kWT - 1) / kWT, tiles = tn * tk;
@@ -694,6 +743,30 @@ void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64
                        tmp.data_ptr<float>());
     hipLaunchKernelGGL(k_wgrad_reduce2, gx, kBlock, 0, stream, tmp.data_ptr<float>(), G, NK4, dw.data_ptr<float>());
   }
+}
+
+// KxK convolution weight gradient (stride, symmetric zero padding), channels-last bf16 dy/x;
+// dw: f32 with the weight's channels-last layout, i.e. [Cout][KH][KW][Cin] in memory.
+void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t KW, int64_t stride, int64_t pad) {
+  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dw.is_cuda(), "conv_wgrad: device tensors");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 && dw.scalar_type() == at::kFloat,
+              "conv_wgrad: bf16 dy/x, f32 dw");
+  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && dw.dim() == 4, "conv_wgrad: 4-d tensors");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  dw.is_contiguous(at::MemoryFormat::ChannelsLast), "conv_wgrad: channels-last dy, x, dw");
+  const int64_t imgs = x.size(0), Cin = x.size(1), Hi = x.size(2), Wi = x.size(3);
+  const int64_t N = dw.size(0);
+  TORCH_CHECK(dw.size(1) == Cin && dw.size(2) == KH && dw.size(3) == KW, "conv_wgrad: dw shape [Cout, Cin, KH, KW]");
+  TORCH_CHECK(stride >= 1 && pad >= 0 && KH >= 1 && KW >= 1, "conv_wgrad: geometry");
+  const int64_t Ho = (Hi + 2 * pad - KH) / stride + 1, Wo = (Wi + 2 * pad - KW) / stride + 1;
+  TORCH_CHECK(dy.size(0) == imgs && dy.size(1) == N && dy.size(2) == Ho && dy.size(3) == Wo, "conv_wgrad: dy shape");
+  TORCH_CHECK(N % 64 == 0 && Cin % 64 == 0, "conv_wgrad: needs Cout % 64 == 0 and Cin % 64 == 0");
+  for (const at::Tensor* t : {&x, &dy, &dw})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "conv_wgrad: 16-byte aligned tensors");
+  const int64_t M = imgs * Ho * Wo;
+  TORCH_CHECK(M < (int64_t(1) << 31) && x.numel() < (int64_t(1) << 40), "conv_wgrad: size");
+  launch_wgrad2(dy, x, dw, M, N, KH * KW * Cin, Cin, Ho, Wo, Hi, Wi, stride, KW, pad,
+                c10::hip::getCurrentHIPStream());
 }
 
 }  // namespace hipps

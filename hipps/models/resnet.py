@@ -14,7 +14,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from hipps.ops.nn import FusedBatchNorm2d, MaxPool2d, ResidualTap, conv_bn
+from hipps.ops.nn import FusedBatchNorm2d, MaxPool2d, ResidualTap, conv2d, conv_bn
 
 # One switch for the whole zoo: fused BN(+residual)(+ReLU) HIP kernels on channels-last bf16,
 # standard PyTorch elsewhere.  HIPPS_FUSED_BN=0 restores the eager MIOpen path for A/B runs.
@@ -27,6 +27,8 @@ _FUSED_CONV = _FUSED and _os.environ.get("HIPPS_FUSED_CONV", "1") != "0"
 _FUSED_GRAD = _FUSED_CONV and _os.environ.get("HIPPS_FUSED_GRAD", "1") != "0"
 # stem max pool on the hipps kernels
 _FUSED_POOL = _FUSED and _os.environ.get("HIPPS_FUSED_POOL", "1") != "0"
+# 3x3 convolutions: weight gradient on the hipps implicit-GEMM kernel (fwd / dgrad stay on MIOpen)
+_FUSED_WGRAD = _os.environ.get("HIPPS_FUSED_WGRAD", "1") != "0"
 
 
 def _bn(c, relu=False):
@@ -70,7 +72,7 @@ class Bottleneck(nn.Module):
                 y, xa = conv_bn(self.conv1, self.bn1, x, fuse=_FUSED_CONV), x
             tap = None
             idt = conv_bn(ds[0], ds[1], xa, fuse=_FUSED_CONV)
-        y = self.bn2(self.conv2(y))
+        y = self.bn2(conv2d(self.conv2, y, fuse=_FUSED_WGRAD))
         return conv_bn(self.conv3, self.bn3, y, residual=idt, fuse=_FUSED_CONV, res_tap=tap)
 
 
@@ -89,8 +91,8 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        y = self.bn1(self.conv1(x))
-        return self.bn2(self.conv2(y), residual=idt)
+        y = self.bn1(conv2d(self.conv1, x, fuse=_FUSED_WGRAD))
+        return self.bn2(conv2d(self.conv2, y, fuse=_FUSED_WGRAD), residual=idt)
 
 
 class ResNet(nn.Module):

@@ -113,6 +113,62 @@ class _Conv1x1(torch.autograd.Function):
         return dx, dw, None, None, None
 
 
+class _ConvKxK(torch.autograd.Function):
+    """KxK convolution on channels-last bf16: forward and input gradient on MIOpen, weight
+    gradient on the hipps implicit-GEMM MFMA kernel (conv_wgrad), written straight into an fp32
+    gradient for the fp32 master weight.  MIOpen's 3x3 weight-gradient kernels accumulate in an
+    fp32 workspace and need 3 extra zero-fill / cast kernels per call (profiles/bench_n1_steady_r1d.txt)."""
+
+    @staticmethod
+    def forward(ctx, x, w_master, stride, pad):
+        w = w_master if w_master.dtype == torch.bfloat16 else w_master.to(torch.bfloat16)
+        ctx.wdtype = w_master.dtype
+        y = torch.ops.aten.convolution(x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1)
+        ctx.geom = (stride, pad)
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        s, p = ctx.geom
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
+                                                     [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty(w.shape, dtype=torch.float32, device=w.device, memory_format=torch.channels_last)
+            native().conv_wgrad(dy, x, dw, w.shape[2], w.shape[3], s, p)
+            if ctx.wdtype != torch.float32:
+                dw = dw.to(ctx.wdtype)
+        return dx, dw, None, None
+
+
+def convkxk_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    """Can the hipps weight-gradient path run this (square, zero-padded, dense) convolution?"""
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and torch.is_grad_enabled() and
+            x.is_contiguous(memory_format=torch.channels_last)):
+        return False
+    k, s, p = conv.kernel_size, conv.stride, conv.padding
+    if k[0] != k[1] or s[0] != s[1] or not isinstance(p, tuple) or p[0] != p[1] or conv.dilation != (1, 1):
+        return False
+    if conv.groups != 1 or conv.bias is not None or conv.padding_mode != "zeros":
+        return False
+    w = conv.weight
+    # 64-channel KxK layers: a 64x64 output tile re-reads both operands once per tap and MIOpen
+    # is faster there (0.23 vs 0.29 ms at 64x56x56, profiles/conv3x3_wgrad.json)
+    return (conv.in_channels % 128 == 0 and conv.out_channels % 64 == 0 and
+            w.is_contiguous(memory_format=torch.channels_last))
+
+
+def conv2d(conv: nn.Conv2d, x: torch.Tensor, fuse: bool = True) -> torch.Tensor:
+    """conv(x) with the hipps weight gradient when eligible (see _ConvKxK); otherwise conv(x)."""
+    if fuse and conv.training and convkxk_ok(conv, x):
+        return _ConvKxK.apply(x, conv.weight, conv.stride[0], conv.padding[0])
+    return conv(x)
+
+
 def _masked(t, mask, C):
     """t * ReLU bits (uint8, bit j of byte i = element 8i+j of the channels-last storage)."""
     if mask is None:

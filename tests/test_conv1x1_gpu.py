@@ -56,6 +56,47 @@ def test_conv1x1_wgrad_matches_fp32(shape):
     torch.testing.assert_close(dw, ref, rtol=2e-3, atol=2e-3 * (n * ho * ho) ** 0.5)
 
 
+KXK = [  # (images, Cin, H, W, Cout, k, stride, pad)
+    (2, 64, 14, 14, 64, 3, 1, 1),
+    (2, 128, 15, 13, 256, 3, 2, 1),   # odd sizes, stride 2: padding on one side only
+    (4, 256, 7, 7, 128, 3, 1, 1),
+    (1, 64, 9, 9, 128, 5, 1, 2),
+    (2, 128, 6, 6, 64, 1, 1, 0),      # 1x1 through the general entry point
+]
+
+
+@pytest.mark.parametrize("shape", KXK)
+def test_conv_wgrad_matches_fp32(shape):
+    n, cin, h, w, cout, k, s, p = shape
+    torch.manual_seed(11 + cin + k)
+    x = _cl(torch.randn(n, cin, h, w, device=DEV).to(torch.bfloat16))
+    ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    dy = _cl(torch.randn(n, cout, ho, wo, device=DEV).to(torch.bfloat16))
+    wt = torch.zeros(cout, cin, k, k, device=DEV)
+    ref = torch.ops.aten.convolution_backward(dy.float(), x.float(), wt, None, [s, s], [p, p], [1, 1], False, [0, 0],
+                                              1, [False, True, False])[1]
+    dw = torch.empty(cout, cin, k, k, device=DEV, memory_format=torch.channels_last)
+    native().conv_wgrad(dy, x, dw, k, k, s, p)
+    torch.testing.assert_close(dw, ref, rtol=2e-3, atol=2e-3 * (n * ho * wo) ** 0.5)
+
+
+def test_conv3x3_autograd_matches_conv():
+    torch.manual_seed(12)
+    conv = torch.nn.Conv2d(128, 128, 3, stride=2, padding=1, bias=False).to(DEV).to(memory_format=torch.channels_last)
+    x0 = _cl(torch.randn(4, 128, 14, 14, device=DEV).to(torch.bfloat16))
+    outs = []
+    for fuse in (True, False):
+        conv.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = hnn.conv2d(conv, x, fuse=fuse)
+        y.float().square().sum().backward()
+        outs.append((y.float(), x.grad.float(), conv.weight.grad.float()))
+    for a, b in zip(*outs):
+        scale = b.abs().max().item() + 1e-6
+        torch.testing.assert_close(a / scale, b / scale, rtol=0, atol=1e-2)
+
+
 def test_conv1x1_exact_on_integers():
     """Small integers are exact in bf16 and fp32: any row/column/k mix-up shows up exactly."""
     n, cin, h, w, cout = 2, 128, 8, 8, 192
