@@ -44,10 +44,17 @@ void bn_forward_partials(at::Tensor part, int64_t nrb, at::Tensor x, c10::option
                          c10::optional<at::Tensor> running_var, at::Tensor mean, at::Tensor invstd, at::Tensor scale,
                          at::Tensor shift, int64_t C, double eps, double momentum, bool relu,
                          c10::optional<at::Tensor> mask_out);
+void bn_backward_partials(at::Tensor part, int64_t nrb, at::Tensor dy, at::Tensor x, int64_t mask_mode,
+                          at::Tensor weight, at::Tensor mean, at::Tensor invstd, at::Tensor scale, at::Tensor shift,
+                          at::Tensor dx, c10::optional<at::Tensor> dres, at::Tensor dweight, at::Tensor dbias, int64_t C,
+                          c10::optional<at::Tensor> mask_in);
 // gemm.hip
 int64_t conv1x1_mtiles(int64_t M);
 void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part, int64_t Hi,
-                     int64_t Wi, int64_t stride, c10::optional<at::Tensor> add, c10::optional<at::Tensor> add_mask);
+                     int64_t Wi, int64_t stride, c10::optional<at::Tensor> add, c10::optional<at::Tensor> add_mask,
+                     c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_bits,
+                     c10::optional<at::Tensor> bn_mean, c10::optional<at::Tensor> bn_invstd,
+                     c10::optional<at::Tensor> bn_scale, c10::optional<at::Tensor> bn_shift);
 // pool.hip
 void maxpool3s2_forward(at::Tensor x, at::Tensor y, at::Tensor code);
 void maxpool3s2_backward(at::Tensor dy, at::Tensor code, at::Tensor dx);
@@ -80,12 +87,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_apply", &hipps::bn_apply, "y = act(x*scale + shift (+res))");
   m.def("bn_backward", &hipps::bn_backward, "fused BN bwd with relu-mask recompute (+dres)");
   m.def("bn_forward_partials", &hipps::bn_forward_partials, "BN fwd finalize+apply from producer-reduced partials");
+  m.def("bn_backward_partials", &hipps::bn_backward_partials, "BN bwd finalize+apply from consumer-reduced partials");
   m.def("conv1x1_mtiles", &hipps::conv1x1_mtiles);
   m.def("conv1x1_forward", &hipps::conv1x1_forward,
         "MFMA 1x1 conv (NHWC GEMM) with fused BN-stats epilogue and optional (+ add * mask) epilogue",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("part"), pybind11::arg("Hi"),
         pybind11::arg("Wi"), pybind11::arg("stride"), pybind11::arg("add") = pybind11::none(),
-        pybind11::arg("add_mask") = pybind11::none());
+        pybind11::arg("add_mask") = pybind11::none(), pybind11::arg("bn_x") = pybind11::none(),
+        pybind11::arg("bn_bits") = pybind11::none(), pybind11::arg("bn_mean") = pybind11::none(),
+        pybind11::arg("bn_invstd") = pybind11::none(), pybind11::arg("bn_scale") = pybind11::none(),
+        pybind11::arg("bn_shift") = pybind11::none());
   m.def("conv_wgrad", &hipps::conv_wgrad, "MFMA KxK conv weight gradient (implicit GEMM, split-M, fp32 dW)");
   m.def("maxpool3s2_forward", &hipps::maxpool3s2_forward, "3x3/s2/p1 max pool, channels-last bf16, 4-bit tap codes");
   m.def("maxpool3s2_backward", &hipps::maxpool3s2_backward, "3x3/s2/p1 max pool backward (gather form, no atomics)");

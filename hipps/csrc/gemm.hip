@@ -62,7 +62,10 @@ struct BnBwdTap {
   const float *mean, *invstd, *scale, *shift;
 };
 
-template <int BN, bool STATS, bool ADD, bool BST = false>
+__device__ const uint8_t kOnes[16] = {0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+                                      0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff};
+
+template <int BN, bool STATS, bool ADD, int BST = 0>  // BST: 0 off, 1 relu' from x, 2 relu' from bits
 __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W,
                                                     uint16_t* __restrict__ Y, float* __restrict__ pa,
                                                     float* __restrict__ pb, const uint16_t* __restrict__ R,
@@ -148,6 +151,13 @@ __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__
   constexpr int NOUT = kGBM * RCH / 256;     // output chunks per thread
   u32x4 rr[NOUT];                            // epilogue addend, prefetched during the last k-tile
   uint32_t rmb[NOUT];
+  u32x4 bx[NOUT];                            // BST: the BN input x under the output tile
+  uint32_t bmb[NOUT];
+  // optional mask streams are read unconditionally (a missing one reads byte 0 of kOnes): a
+  // select between "load" and "constant" makes hipcc branch around each load and drain vmcnt
+  const uint8_t* rmp = RM != nullptr ? RM : kOnes;
+  const int64_t rmk = RM != nullptr ? ~int64_t(0) : 0;
+  const uint8_t* bmp = bt.bits;
   HIPPS_GLOAD(0);
   HIPPS_SSTORE(0);
   __syncthreads();
@@ -155,16 +165,22 @@ __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__
     const int cur = kt & 1;
     if (kt + 1 < KT) {
       HIPPS_GLOAD(kt + 1);
-    } else if (ADD) {  // no next tile to fetch: load the addend now, hidden by the MFMAs
+    } else if ((ADD || BST) && !(ADD && BST)) {  // last tile: load the epilogue operand now, under the MFMAs
 #pragma unroll
       for (int i = 0; i < NOUT; ++i) {
         const int id = t + 256 * i;
         const int row = id / RCH, c = id - row * RCH;
         const bool ok = m0 + row < M;
         const int64_t o = (int64_t)(ok ? m0 + row : m0) * N + n0 + c * 8;
-        const u32x4 v = *reinterpret_cast<const u32x4*>(R + o);
-        rr[i] = ok ? v : u32x4{0u, 0u, 0u, 0u};
-        rmb[i] = RM != nullptr ? (uint32_t)RM[o >> 3] : 0xffu;
+        if (ADD) {
+          const u32x4 v = *reinterpret_cast<const u32x4*>(R + o);
+          rr[i] = ok ? v : u32x4{0u, 0u, 0u, 0u};
+          rmb[i] = rmp[(o >> 3) & rmk];
+        }
+        if (BST && !ADD) {  // with ADD too, these wait for the epilogue (register budget: 2 waves/SIMD)
+          bx[i] = *reinterpret_cast<const u32x4*>(bt.x + o);
+          if (BST == 2) bmb[i] = bmp[o >> 3];
+        }
       }
     }
     const uint16_t* As = lds + cur * STAGE;
@@ -227,6 +243,34 @@ __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__
     }
   }
   __syncthreads();
+  if (BST && ADD) {  // both operands loaded only now, with the accumulators retired to LDS: held
+#pragma unroll       // through the last k-tile they cost 2 -> 1 waves/SIMD (276 registers)
+    for (int i = 0; i < NOUT; ++i) {
+      const int id = t + 256 * i;
+      const int row = id / RCH, c = id - row * RCH;
+      const bool ok = m0 + row < M;
+      const int64_t o = (int64_t)(ok ? m0 + row : m0) * N + n0 + c * 8;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(R + o);
+      rr[i] = ok ? v : u32x4{0u, 0u, 0u, 0u};
+      rmb[i] = rmp[(o >> 3) & rmk];
+      bx[i] = *reinterpret_cast<const u32x4*>(bt.x + o);
+      if (BST == 2) bmb[i] = bmp[o >> 3];
+    }
+  }
+  // BST: this thread's 8 channels are fixed (256 % RCH == 0): per-channel BN constants in registers
+  const int cc = (t % RCH) * 8;
+  float bmu[8], bis[8], bsc[8], bsh[8], bsa[8], bsb[8];
+  if (BST) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bmu[j] = bt.mean[n0 + cc + j];
+      bis[j] = bt.invstd[n0 + cc + j];
+      bsc[j] = BST == 1 ? bt.scale[n0 + cc + j] : 0.f;
+      bsh[j] = BST == 1 ? bt.shift[n0 + cc + j] : 0.f;
+      bsa[j] = 0.f;
+      bsb[j] = 0.f;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < NOUT; ++i) {
     const int id = t + 256 * i;
@@ -247,6 +291,40 @@ __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__
         v.w = add_bf16x2(v.w, r.w);
       }
       *reinterpret_cast<uint4*>(Y + o) = v;
+      if (BST) {  // dz = dy * relu'(.) on the stored bf16 dy; x-hat from the BN input
+        const uint32_t dv[4] = {v.x, v.y, v.z, v.w};
+        const u32x4 xu = bx[i];
+        const uint32_t xw[4] = {xu.x, xu.y, xu.z, xu.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = __uint_as_float(j & 1 ? dv[j >> 1] & 0xffff0000u : dv[j >> 1] << 16);
+          const float xv = __uint_as_float(j & 1 ? xw[j >> 1] & 0xffff0000u : xw[j >> 1] << 16);
+          const bool on = BST == 2 ? ((bmb[i] >> j) & 1u) != 0u : fmaf(xv, bsc[j], bsh[j]) > 0.f;
+          const float dz = on ? d : 0.f;
+          bsa[j] += dz;
+          bsb[j] = fmaf(dz, (xv - bmu[j]) * bis[j], bsb[j]);
+        }
+      }
+    }
+  }
+  if (BST) {  // combine the 256/RCH row lanes of each channel chunk through LDS, fixed order
+    constexpr int RL = 256 / RCH;
+    float* red = reinterpret_cast<float*>(lds);  // [2][RL][BN] floats = 16 KB; the staging area is free
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[(t / RCH) * BN + cc + j] = bsa[j];
+      red[RL * BN + (t / RCH) * BN + cc + j] = bsb[j];
+    }
+    __syncthreads();
+    if (t < BN) {
+      float s = 0.f, q = 0.f;
+      for (int r = 0; r < RL; ++r) {
+        s += red[r * BN + t];
+        q += red[RL * BN + r * BN + t];
+      }
+      pa[(int64_t)(n0 + t) * mtiles + mt] = s;
+      pb[(int64_t)(n0 + t) * mtiles + mt] = q;
     }
   }
   if (STATS && t < BN) {
@@ -590,8 +668,14 @@ int64_t conv1x1_mtiles(int64_t M) { return (M + kGBM - 1) / kGBM; }
 // y: [img, Cout, Ho, Wo] channels-last bf16.  part (optional): f32 [2, Cout, mtiles].
 // add (optional): bf16 shaped like y, added in the epilogue (y = conv(x) + add); add_mask
 // (optional, with add): uint8 [numel/8] ReLU bits, y = conv(x) + add * bit.
+// bn_x (optional, dgrad only): y is the complete gradient of a BatchNorm output whose input was
+// bn_x -- the epilogue then writes that BN backward's reduction partials into part (see BnBwdTap;
+// bn_bits = its ReLU bits, or none to recompute the mask from bn_x with bn_scale / bn_shift).
 void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part, int64_t Hi,
-                     int64_t Wi, int64_t stride, c10::optional<at::Tensor> add, c10::optional<at::Tensor> add_mask) {
+                     int64_t Wi, int64_t stride, c10::optional<at::Tensor> add, c10::optional<at::Tensor> add_mask,
+                     c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_bits,
+                     c10::optional<at::Tensor> bn_mean, c10::optional<at::Tensor> bn_invstd,
+                     c10::optional<at::Tensor> bn_scale, c10::optional<at::Tensor> bn_shift) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "conv1x1: device tensors");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
                   y.scalar_type() == at::kBFloat16, "conv1x1: bf16 tensors");
@@ -635,19 +719,53 @@ void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
                     add_mask->numel() == M * N / 8, "conv1x1: add_mask must be uint8[numel(y)/8]");
     mp = (const uint8_t*)add_mask->data_ptr();
   }
+  BnBwdTap bt{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  const bool bst = bn_x.has_value() && bn_x->defined();
+  if (bst) {
+    TORCH_CHECK(pa != nullptr, "conv1x1: BN-backward statistics need part");
+    TORCH_CHECK(bn_x->is_cuda() && bn_x->scalar_type() == at::kBFloat16 && bn_x->numel() == M * N &&
+                    (bn_x->is_contiguous(at::MemoryFormat::ChannelsLast) || bn_x->dim() != 4) &&
+                    reinterpret_cast<uintptr_t>(bn_x->data_ptr()) % 16 == 0,
+                "conv1x1: bn_x must be a 16-byte aligned channels-last bf16 tensor shaped like y");
+    for (const c10::optional<at::Tensor>* v : {&bn_mean, &bn_invstd, &bn_scale, &bn_shift})
+      TORCH_CHECK(v->has_value() && (*v)->defined() && (*v)->is_cuda() && (*v)->scalar_type() == at::kFloat &&
+                      (*v)->is_contiguous() && (*v)->numel() == N, "conv1x1: BN vectors must be f32 [C]");
+    bt.x = (const uint16_t*)bn_x->data_ptr();
+    bt.mean = bn_mean->data_ptr<float>();
+    bt.invstd = bn_invstd->data_ptr<float>();
+    bt.scale = bn_scale->data_ptr<float>();
+    bt.shift = bn_shift->data_ptr<float>();
+    if (bn_bits.has_value() && bn_bits->defined()) {
+      TORCH_CHECK(bn_bits->is_cuda() && bn_bits->scalar_type() == at::kByte && bn_bits->is_contiguous() &&
+                      bn_bits->numel() == M * N / 8, "conv1x1: bn_bits must be uint8[numel(y)/8]");
+      bt.bits = (const uint8_t*)bn_bits->data_ptr();
+    }
+  }
   auto stream = c10::hip::getCurrentHIPStream();
   const uint16_t* xp = (const uint16_t*)x.data_ptr();
   const uint16_t* wp = (const uint16_t*)w.data_ptr();
   uint16_t* yp = (uint16_t*)y.data_ptr();
-#define HIPPS_C1(BNv, ST, AD)                                                                              \
-  hipLaunchKernelGGL((k_conv1x1_nt<BNv, ST, AD>), (int)nblk, 256, 0, stream, xp, wp, yp, pa, pb, rp, mp, (int)M, (int)N, \
-                     (int)K, (int)Ho, (int)Wo, (int)Hi, (int)Wi, (int)stride, (int)mtiles, (int)ntiles)
-  TORCH_CHECK(!(pa && rp), "conv1x1: the statistics epilogue and the add epilogue are exclusive");
-  if (bn128) {
-    if (pa) HIPPS_C1(128, true, false); else if (rp) HIPPS_C1(128, false, true); else HIPPS_C1(128, false, false);
-  } else {
-    if (pa) HIPPS_C1(64, true, false); else if (rp) HIPPS_C1(64, false, true); else HIPPS_C1(64, false, false);
-  }
+#define HIPPS_C1(BNv, ST, AD, BS)                                                                           \
+  hipLaunchKernelGGL((k_conv1x1_nt<BNv, ST, AD, BS>), (int)nblk, 256, 0, stream, xp, wp, yp, pa, pb, rp, mp,     \
+                     (int)M, (int)N, (int)K, (int)Ho, (int)Wo, (int)Hi, (int)Wi, (int)stride, (int)mtiles,        \
+                     (int)ntiles, bt)
+#define HIPPS_C1_BN(BNv)                                                                                      \
+  do {                                                                                                        \
+    if (bst && bt.bits) {                                                                                     \
+      if (rp) HIPPS_C1(BNv, false, true, 2); else HIPPS_C1(BNv, false, false, 2);                             \
+    } else if (bst) {                                                                                         \
+      if (rp) HIPPS_C1(BNv, false, true, 1); else HIPPS_C1(BNv, false, false, 1);                             \
+    } else if (pa) {                                                                                          \
+      HIPPS_C1(BNv, true, false, 0);                                                                          \
+    } else if (rp) {                                                                                          \
+      HIPPS_C1(BNv, false, true, 0);                                                                          \
+    } else {                                                                                                  \
+      HIPPS_C1(BNv, false, false, 0);                                                                         \
+    }                                                                                                         \
+  } while (0)
+  TORCH_CHECK(bst || !(pa && rp), "conv1x1: the forward statistics epilogue and the add epilogue are exclusive");
+  if (bn128) HIPPS_C1_BN(128); else HIPPS_C1_BN(64);
+#undef HIPPS_C1_BN
 #undef HIPPS_C1
 }
 

@@ -523,3 +523,52 @@ void bn_forward_partials(at::Tensor part, int64_t nrb, at::Tensor x, c10::option
                      momentum, relu, c10::hip::getCurrentHIPStream());
 }
 }  // namespace hipps
+
+namespace hipps {
+// Backward BN whose reduction (sum dz, sum dz*x-hat per channel) was already done by the
+// producer of dy -- the 1x1 dgrad GEMM epilogue (gemm.hip, BnBwdTap): finalize + apply only,
+// i.e. one pass over dy and x instead of two.  part = f32 [2, C, nrb] channel-major partials.
+void bn_backward_partials(at::Tensor part, int64_t nrb, at::Tensor dy, at::Tensor x, int64_t mask_mode,
+                          at::Tensor weight, at::Tensor mean, at::Tensor invstd, at::Tensor scale, at::Tensor shift,
+                          at::Tensor dx, c10::optional<at::Tensor> dres, at::Tensor dweight, at::Tensor dbias, int64_t C,
+                          c10::optional<at::Tensor> mask_in) {
+  TORCH_CHECK(C % 8 == 0 && C <= kMaxC, "fused BN needs C % 8 == 0 and C <= 2048");
+  TORCH_CHECK(mask_mode == MASK_NONE || mask_mode == MASK_X || mask_mode == MASK_BITS, "bad mask mode");
+  const int64_t M = x.numel() / C;
+  check_act(dy, "dy", M * C);
+  check_act(x, "x", M * C);
+  check_act(dx, "dx", M * C);
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.numel() == 2 * C * nrb,
+              "part must be f32 [2, C, nrb]");
+  const uint8_t* mbp = nullptr;
+  if (mask_mode == MASK_BITS) {
+    TORCH_CHECK(mask_in.has_value() && mask_in->defined() && mask_in->scalar_type() == at::kByte &&
+                    mask_in->numel() == M * C / 8, "MASK_BITS needs a uint8[M*C/8] mask");
+    mbp = (const uint8_t*)mask_in->data_ptr();
+  }
+  uint16_t* drp = nullptr;
+  if (dres.has_value() && dres->defined()) {
+    check_act(*dres, "dres", M * C);
+    drp = (uint16_t*)dres->data_ptr();
+  }
+  for (auto* t : {&weight, &mean, &invstd, &scale, &shift, &dweight, &dbias}) check_vec(*t, "per-channel vector", (int)C);
+  auto coef = at::empty({3, C}, weight.options());
+  auto stream = c10::hip::getCurrentHIPStream();
+  const float* pa = part.data_ptr<float>();
+  hipLaunchKernelGGL(k_bn_finalize_bwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, pa, pa + C * nrb,
+                     (int)nrb, (int)C, M, weight.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                     dweight.data_ptr<float>(), dbias.data_ptr<float>(), coef[0].data_ptr<float>(),
+                     coef[1].data_ptr<float>(), coef[2].data_ptr<float>());
+  auto app = [&](auto kern) {
+    hipLaunchKernelGGL(kern, apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)dy.data_ptr(),
+                       (const uint16_t*)x.data_ptr(), nullptr, mbp, scale.data_ptr<float>(), shift.data_ptr<float>(),
+                       coef[0].data_ptr<float>(), coef[1].data_ptr<float>(), coef[2].data_ptr<float>(),
+                       (uint16_t*)dx.data_ptr(), drp, M, (int)C);
+  };
+  switch (mask_mode) {
+    case MASK_NONE: app(k_bn_apply_bwd<MASK_NONE>); break;
+    case MASK_X: app(k_bn_apply_bwd<MASK_X>); break;
+    default: app(k_bn_apply_bwd<MASK_BITS>); break;
+  }
+}
+}  // namespace hipps

@@ -27,6 +27,8 @@ _FUSED_CONV = _FUSED and _os.environ.get("HIPPS_FUSED_CONV", "1") != "0"
 _FUSED_GRAD = _FUSED_CONV and _os.environ.get("HIPPS_FUSED_GRAD", "1") != "0"
 # stem max pool on the hipps kernels
 _FUSED_POOL = _FUSED and _os.environ.get("HIPPS_FUSED_POOL", "1") != "0"
+# BN backward reductions done in the consuming 1x1 conv's dgrad epilogue (BNGradTap)
+_FUSED_BNGRAD = _os.environ.get("HIPPS_FUSED_BNGRAD", "1") != "0"
 # 3x3 convolutions: weight gradient on the hipps implicit-GEMM kernel (fwd / dgrad stay on MIOpen)
 _FUSED_WGRAD = _os.environ.get("HIPPS_FUSED_WGRAD", "1") != "0"
 
@@ -60,20 +62,23 @@ class Bottleneck(nn.Module):
         # (read 2, write 1 full-size tensors per block) conv1's dgrad epilogue sums them: the
         # identity residual's gradient (bn3's dy * ReLU bits) arrives through a ResidualTap, a
         # downsample branch's input gradient through an alias of x.
+        # With every gradient path into x summed there, conv1's dgrad epilogue also reduces the
+        # previous block's bn3 backward statistics, and conv3's those of bn2 (BNGradTap).
         ds = self.downsample
+        bng = _FUSED_GRAD and _FUSED_BNGRAD
         if ds is None:
             tap = ResidualTap() if _FUSED_GRAD else None
-            y = conv_bn(self.conv1, self.bn1, x, fuse=_FUSED_CONV, tap=tap)
+            y = conv_bn(self.conv1, self.bn1, x, fuse=_FUSED_CONV, tap=tap, bn_grad=bng)
             idt = x
         else:
             if _FUSED_GRAD:
-                y, xa = conv_bn(self.conv1, self.bn1, x, fuse=_FUSED_CONV, alias=True)
+                y, xa = conv_bn(self.conv1, self.bn1, x, fuse=_FUSED_CONV, alias=True, bn_grad=bng)
             else:
                 y, xa = conv_bn(self.conv1, self.bn1, x, fuse=_FUSED_CONV), x
             tap = None
             idt = conv_bn(ds[0], ds[1], xa, fuse=_FUSED_CONV)
         y = self.bn2(conv2d(self.conv2, y, fuse=_FUSED_WGRAD))
-        return conv_bn(self.conv3, self.bn3, y, residual=idt, fuse=_FUSED_CONV, res_tap=tap)
+        return conv_bn(self.conv3, self.bn3, y, residual=idt, fuse=_FUSED_CONV, res_tap=tap, bn_grad=bng)
 
 
 class BasicBlock(nn.Module):

@@ -48,6 +48,21 @@ class ResidualTap:
         return dy, mask
 
 
+class BNGradTap:
+    """Lets the 1x1 conv that consumes a fused BN's output compute that BN's backward reduction
+    (sum dz, sum dz * x-hat per channel) in its dgrad epilogue, on the gradient tile it has just
+    produced (gemm.hip BnBwdTap) -- the BN backward then skips its reduction pass over dy and x.
+    Valid only when the conv's input gradient IS the complete gradient of the BN output: the
+    model opts in (conv_bn(..., bn_grad=True)) where the BN output has no other consumer, or its
+    other gradient paths are summed into the same epilogue (ResidualTap / alias)."""
+
+    __slots__ = ("x", "mask", "mean", "invstd", "scale", "shift", "part")
+
+    def __init__(self, x, mask, mean, invstd, scale, shift):
+        self.x, self.mask, self.mean, self.invstd, self.scale, self.shift = x, mask, mean, invstd, scale, shift
+        self.part = None
+
+
 class _Conv1x1(torch.autograd.Function):
     """1x1 convolution on channels-last bf16 as an MFMA GEMM (hipps/csrc/gemm.hip) that also
     emits the per-channel batch statistics of its output for the BatchNorm that follows.
@@ -59,9 +74,10 @@ class _Conv1x1(torch.autograd.Function):
     and with ``alias`` the gradient of the returned alias of x (e.g. a downsample branch)."""
 
     @staticmethod
-    def forward(ctx, x, w_master, stride, tap=None, alias=False):
+    def forward(ctx, x, w_master, stride, tap=None, alias=False, bngrad=None):
         w = w_master if w_master.dtype == torch.bfloat16 else w_master.to(torch.bfloat16)
         ctx.wdtype = w_master.dtype
+        ctx.bngrad = bngrad if stride == 1 else None
         N, Cin, H, W = x.shape
         Cout = w.shape[0]
         Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
@@ -109,8 +125,20 @@ class _Conv1x1(torch.autograd.Function):
             cout, cin = w.shape[0], w.shape[1]
             wt = w.reshape(cout, cin).t().contiguous()  # [Cin, Cout]: K-contiguous B operand
             dx = torch.empty_like(x, memory_format=torch.channels_last)
-            native().conv1x1_forward(dy, wt, dx, None, x.shape[2], x.shape[3], 1, add, add_mask)
-        return dx, dw, None, None, None
+            bg = ctx.bngrad
+            # x's gradient is complete here only if the residual path it also feeds was summed in
+            # (an identity block's tap delivered, or no tap was involved)
+            if bg is not None and (ctx.tap is None or add is not None):
+                n_img, _, h, wd = x.shape
+                part = torch.empty((2, cin, native().conv1x1_mtiles(n_img * h * wd)), dtype=torch.float32,
+                                   device=x.device)
+                native().conv1x1_forward(dy, wt, dx, part, h, wd, 1, add, add_mask, bg.x, bg.mask, bg.mean,
+                                         bg.invstd, bg.scale, bg.shift)
+                bg.part = part
+            else:
+                native().conv1x1_forward(dy, wt, dx, None, x.shape[2], x.shape[3], 1, add, add_mask)
+        ctx.bngrad = None
+        return dx, dw, None, None, None, None
 
 
 class _ConvKxK(torch.autograd.Function):
@@ -190,10 +218,10 @@ def conv1x1_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     return conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0
 
 
-def conv1x1_stats(x, weight, stride=1, tap=None, alias=False):
+def conv1x1_stats(x, weight, stride=1, tap=None, alias=False, bngrad=None):
     """(y, part[, x_alias]): bf16 1x1 conv output and its [2, Cout, m_tiles] BN partial
-    statistics (see _Conv1x1 for ``tap`` / ``alias``)."""
-    return _Conv1x1.apply(x, weight, int(stride), tap, bool(alias))
+    statistics (see _Conv1x1 for ``tap`` / ``alias``, BNGradTap for ``bngrad``)."""
+    return _Conv1x1.apply(x, weight, int(stride), tap, bool(alias), bngrad)
 
 
 class _FusedBNAct(torch.autograd.Function):
@@ -218,6 +246,11 @@ class _FusedBNAct(torch.autograd.Function):
         # the residual gradient is dy * bits (or dy): hand it to the consumer through the tap
         ctx.tap = tap if (res is not None and mode in (MASK_NONE, MASK_BITS)) else None
         ctx.save_for_backward(x, mask, weight, mean, invstd, scale, shift)
+        # a consuming 1x1 conv may reduce this BN's backward statistics for it (BNGradTap)
+        ctx.bngrad = None
+        if mode in (MASK_X, MASK_BITS):
+            ctx.bngrad = BNGradTap(x, mask, mean, invstd, scale, shift)
+            y._hipps_bngrad = ctx.bngrad
         return y
 
     @staticmethod
@@ -229,7 +262,14 @@ class _FusedBNAct(torch.autograd.Function):
         dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res and tap is None else None
         dw = torch.empty_like(weight)
         db = torch.empty_like(weight)
-        native().bn_backward(dy, x, None, ctx.mode, weight, mean, invstd, scale, shift, dx, dres, dw, db, ctx.C, mask)
+        bg, ctx.bngrad = ctx.bngrad, None
+        if bg is not None and bg.part is not None:  # reduction already done in the consumer's epilogue
+            native().bn_backward_partials(bg.part, bg.part.shape[2], dy, x, ctx.mode, weight, mean, invstd, scale,
+                                          shift, dx, dres, dw, db, ctx.C, mask)
+            bg.part = None
+        else:
+            native().bn_backward(dy, x, None, ctx.mode, weight, mean, invstd, scale, shift, dx, dres, dw, db, ctx.C,
+                                 mask)
         if tap is not None:
             tap.dy, tap.mask = dy, (mask if ctx.mode == MASK_BITS else None)
         return dx, dres, dw, db, None, None, None, None, None, None, None
@@ -305,7 +345,7 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
 
 
 def conv_bn(conv: nn.Conv2d, bn: FusedBatchNorm2d, x, residual=None, fuse: bool = True, tap=None, res_tap=None,
-            alias: bool = False):
+            alias: bool = False, bn_grad: bool = False):
     """bn(conv(x), residual): a 1x1 conv that feeds a training-mode fused BN runs as the MFMA GEMM
     with the BN statistics in its epilogue (one fewer pass over the conv output).
 
@@ -314,11 +354,15 @@ def conv_bn(conv: nn.Conv2d, bn: FusedBatchNorm2d, x, residual=None, fuse: bool 
                MFMA path with its own dgrad is taken)
       res_tap  this BN routes its residual gradient into that tap (only if armed)
       alias    also return an alias of x whose gradient is summed in this conv's dgrad epilogue
-               -> returns (out, x_alias)"""
+               -> returns (out, x_alias)
+      bn_grad  x is the output of a fused BN whose only gradient is this conv's input gradient
+               (after the tap / alias sums): reduce that BN's backward statistics in the dgrad
+               epilogue (BNGradTap)"""
     if fuse and bn.training and conv1x1_ok(conv, x):
         s = conv.stride[0]
         own_tap = tap if s == 1 else None
-        outs = conv1x1_stats(x, conv.weight, s, own_tap, alias and s == 1)
+        bg = getattr(x, "_hipps_bngrad", None) if bn_grad else None
+        outs = conv1x1_stats(x, conv.weight, s, own_tap, alias and s == 1, bg)
         y, part = outs[0], outs[1]
         xa = outs[2] if len(outs) > 2 else x
         if own_tap is not None:

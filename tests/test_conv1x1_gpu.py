@@ -201,6 +201,68 @@ def test_resnet50_fused_conv_matches_unfused():
         torch.testing.assert_close(u, v, rtol=5e-2, atol=5e-2)
 
 
+@pytest.mark.parametrize("bngrad", [False, True])
+def test_bottleneck_chain_bn_backward_in_epilogue(bngrad):
+    """Two chained blocks (downsample, then identity): the second block's conv1 dgrad epilogue
+    reduces the first block's bn3 backward statistics, each conv3 those of its bn2 (BNGradTap);
+    every gradient must match the plain autograd path (all gradient fusions off)."""
+    import hipps.models.resnet as R
+
+    torch.manual_seed(6)
+    net = torch.nn.Sequential(R.Bottleneck(64, 64, stride=1, downsample=True), R.Bottleneck(256, 64),
+                              R.Bottleneck(256, 128, stride=2, downsample=True))
+    net = net.to(DEV).to(memory_format=torch.channels_last)
+    for blk in net:
+        torch.nn.init.uniform_(blk.bn3.weight, 0.5, 1.5)
+    x0 = _cl(torch.randn(8, 64, 14, 14, device=DEV).to(torch.bfloat16))
+    g = None
+    res = {}
+    for fused in (True, False):
+        R._FUSED_GRAD = fused
+        R._FUSED_BNGRAD = bngrad
+        try:
+            net.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = net(x)
+            if g is None:
+                g = _cl(torch.randn(y.shape, device=DEV).to(torch.bfloat16))
+            y.backward(g)
+        finally:
+            R._FUSED_GRAD = R._FUSED_BNGRAD = True
+        res[fused] = [y.float(), x.grad.float()] + [p.grad.float().clone() for p in net.parameters()]
+    for u, v in zip(res[True], res[False]):
+        scale = v.abs().max().item() + 1e-6
+        torch.testing.assert_close(u / scale, v / scale, rtol=0, atol=2e-2)
+
+
+def test_conv1x1_bn_backward_partials_match_reduce():
+    """The dgrad epilogue's BN-backward partials equal the BN reduction over the stored dy."""
+    torch.manual_seed(8)
+    n, c, h, w, cout = 4, 128, 10, 10, 256
+    dy_out = _cl(torch.randn(n, cout, h, w, device=DEV).to(torch.bfloat16))
+    wt = (torch.randn(c, cout, device=DEV) / cout ** 0.5).to(torch.bfloat16)  # [Cin, Cout] dgrad B operand
+    xbn = _cl(torch.randn(n, c, h, w, device=DEV).to(torch.bfloat16))
+    mean, invstd = torch.randn(c, device=DEV) * 0.1, torch.rand(c, device=DEV) + 0.5
+    scale, shift = torch.randn(c, device=DEV), torch.randn(c, device=DEV)
+    bits = torch.randint(0, 256, (xbn.numel() // 8,), dtype=torch.uint8, device=DEV)
+    mt = native().conv1x1_mtiles(n * h * w)
+    for use_bits in (True, False):
+        dx = torch.empty_like(xbn)
+        part = torch.empty(2, c, mt, device=DEV)
+        native().conv1x1_forward(dy_out, wt, dx, part, h, w, 1, None, None, xbn, bits if use_bits else None, mean,
+                                 invstd, scale, shift)
+        d = dx.float().permute(0, 2, 3, 1).reshape(-1, c)
+        xf = xbn.float().permute(0, 2, 3, 1).reshape(-1, c)
+        if use_bits:
+            m = ((bits.view(-1, 1) >> torch.arange(8, device=DEV, dtype=torch.uint8)) & 1).view(-1, c).bool()
+        else:
+            m = xf * scale + shift > 0
+        dz = torch.where(m, d, torch.zeros_like(d))
+        torch.testing.assert_close(part[0].sum(1), dz.sum(0), rtol=1e-4, atol=1e-3)
+        torch.testing.assert_close(part[1].sum(1), (dz * (xf - mean) * invstd).sum(0), rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("cin,width,stride,ds", [(256, 64, 1, False), (64, 64, 1, True), (256, 128, 2, True)])
 def test_bottleneck_gradient_fusions(cin, width, stride, ds):
     """Residual-gradient epilogue sums (ResidualTap for identity blocks, x alias for downsample
