@@ -49,6 +49,12 @@ class PSConfig:
     grad_gather: bool = True
     # published-parameter wire dtype for PS modes: 'fp32' | 'bf16'
     param_wire: str = "fp32"
+    # bf16 weight shadow: one flat bf16 copy of the fp32 params, refreshed by one cast kernel after
+    # every step()/irequest_params(), read by the hipps conv kernels instead of one autocast cast
+    # per layer per forward.  'auto' = on for ps_async on a GPU (the engine owns the params there:
+    # any out-of-band edit is overwritten by the next adoption anyway); 'on' | 'off' otherwise.
+    # With 'on', call opt.refresh_bf16_weights() after editing params outside step().
+    bf16_weights: str = "auto"
     # host pickle slow path compression level (mpi_comms.py:18; 0 = framing only)
     compress_level: int = 0
     # Adam eps placement: 'reference' (ps.py:255) or 'torch'
@@ -94,6 +100,8 @@ class PSConfig:
             raise ValueError("pull must be 'prefetch' or 'direct'")
         if self.param_wire not in ("fp32", "bf16"):
             raise ValueError("param_wire must be 'fp32' or 'bf16'")
+        if self.bf16_weights not in ("auto", "on", "off"):
+            raise ValueError("bf16_weights must be 'auto', 'on' or 'off'")
         if self.adam_variant not in ("reference", "torch"):
             raise ValueError("adam_variant must be 'reference' or 'torch'")
 

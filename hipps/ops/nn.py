@@ -63,6 +63,31 @@ class BNGradTap:
         self.part = None
 
 
+_SHADOWS: list = []  # [fp32 flat param buffer, bf16 shadow] pairs (FlatStore.enable_bf16_shadow)
+
+
+def register_weight_shadow(flat: torch.Tensor, shadow: torch.Tensor):
+    _SHADOWS.append((flat, shadow))
+
+
+def unregister_weight_shadow(shadow: torch.Tensor):
+    _SHADOWS[:] = [(f, s) for f, s in _SHADOWS if s is not shadow]
+
+
+def bf16_weight(w: torch.Tensor) -> torch.Tensor:
+    """The bf16 view of fp32 master weight ``w`` in a registered shadow (same shape and strides),
+    else a fresh cast.  The shadow is refreshed by the optimizer with one cast kernel per step, so
+    a ResNet-50 forward reads its 53 conv weights without 53 autocast cast launches."""
+    if w.dtype == torch.bfloat16:
+        return w
+    p = w.data_ptr()
+    for flat, sh in _SHADOWS:
+        base = flat.data_ptr()
+        if base <= p < base + flat.numel() * 4 and w.device == flat.device:
+            return sh.as_strided(w.shape, w.stride(), (p - base) // 4)
+    return w.to(torch.bfloat16)
+
+
 class _Conv1x1(torch.autograd.Function):
     """1x1 convolution on channels-last bf16 as an MFMA GEMM (hipps/csrc/gemm.hip) that also
     emits the per-channel batch statistics of its output for the BatchNorm that follows.
@@ -75,8 +100,10 @@ class _Conv1x1(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w_master, stride, tap=None, alias=False, bngrad=None):
-        w = w_master if w_master.dtype == torch.bfloat16 else w_master.to(torch.bfloat16)
+        w = bf16_weight(w_master)
         ctx.wdtype = w_master.dtype
+        # no zero-filled grad for the non-differentiable BN partials (a 12.8 MB fill per layer)
+        ctx.set_materialize_grads(False)
         ctx.bngrad = bngrad if stride == 1 else None
         N, Cin, H, W = x.shape
         Cout = w.shape[0]
@@ -97,6 +124,9 @@ class _Conv1x1(torch.autograd.Function):
     def backward(ctx, dy, _dpart, d_alias=None):
         x, w = ctx.saved_tensors
         s = ctx.stride
+        if dy is None:  # y unused (grads are not materialized): only the alias path carries a grad
+            ctx.bngrad = None
+            return d_alias, None, None, None, None, None
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = None
         add, add_mask = ctx.tap.take() if ctx.tap is not None else (None, None)
@@ -149,7 +179,7 @@ class _ConvKxK(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w_master, stride, pad):
-        w = w_master if w_master.dtype == torch.bfloat16 else w_master.to(torch.bfloat16)
+        w = bf16_weight(w_master)
         ctx.wdtype = w_master.dtype
         y = torch.ops.aten.convolution(x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1)
         ctx.geom = (stride, pad)

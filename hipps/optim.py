@@ -80,6 +80,9 @@ class MPI_PS(torch.optim.Optimizer):
         self._init_state()
         self.steps = 0
         self.engine = self._make_engine()
+        bw = self.cfg.bf16_weights
+        if bw == "on" or (bw == "auto" and self.mode == "ps_async" and self.store.device.type == "cuda"):
+            self.store.enable_bf16_shadow()
         self._metrics = None
         if self.cfg.metrics_path:
             from .utils.metrics import MetricsWriter
@@ -147,6 +150,7 @@ class MPI_PS(torch.optim.Optimizer):
         self.steps += 1
         t0 = time.perf_counter()
         data = self.engine.step()
+        self.store.refresh_shadow()
         data["step_time"] = time.perf_counter() - t0
         if self._metrics is not None:
             self._metrics.write(self.steps, data)
@@ -161,7 +165,13 @@ class MPI_PS(torch.optim.Optimizer):
     def irequest_params(self, **kw):
         """AsySG-InCon parameter refresh (README.md:63): adopt the newest published params that
         have arrived, without waiting for the rest (inconsistent read).  No-op in sync modes."""
-        return self.engine.irequest_params(**kw)
+        r = self.engine.irequest_params(**kw)
+        self.store.refresh_shadow()
+        return r
+
+    def refresh_bf16_weights(self):
+        """Re-cast the bf16 weight shadow after editing parameters outside ``step()``."""
+        self.store.refresh_shadow()
 
     def close(self):
         if getattr(self, "engine", None) is not None:
@@ -169,6 +179,8 @@ class MPI_PS(torch.optim.Optimizer):
             if hasattr(self.engine, "ps_stats"):
                 self._last_engine_stats = self.engine.ps_stats()  # drained totals after close
             self.engine = None
+        if getattr(self, "store", None) is not None:
+            self.store.disable_bf16_shadow()
         if self._metrics is not None:
             self._metrics.close()
 
@@ -201,6 +213,7 @@ class MPI_PS(torch.optim.Optimizer):
         self.steps = extra.get("steps", self.steps)
         if "group_steps" in extra:
             self._group_steps = list(extra["group_steps"])
+        self.store.refresh_shadow()
 
     def _ensure_state_nocopy(self, key):
         if key not in self.flat_state:

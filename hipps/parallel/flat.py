@@ -134,6 +134,26 @@ class FlatStore:
         self.grad.zero_()
         self.attach_grads()
 
+    def enable_bf16_shadow(self):
+        """Keep a flat bf16 copy of ``data`` that the hipps conv kernels read (ops.nn.bf16_weight)."""
+        from ..ops import nn as hnn
+
+        if getattr(self, "shadow", None) is None:
+            self.shadow = torch.empty(self.numel, dtype=torch.bfloat16, device=self.device)
+            hnn.register_weight_shadow(self.data, self.shadow)
+        self.refresh_shadow()
+
+    def disable_bf16_shadow(self):
+        from ..ops import nn as hnn
+
+        if getattr(self, "shadow", None) is not None:
+            hnn.unregister_weight_shadow(self.shadow)
+            self.shadow = None
+
+    def refresh_shadow(self):
+        if getattr(self, "shadow", None) is not None:
+            self.shadow.copy_(self.data)  # one vectorized cast kernel on the current stream
+
     def group_slice(self, buf: torch.Tensor, gi: int) -> torch.Tensor:
         a, b = self.group_ranges[gi]
         return buf[a:b]

@@ -79,5 +79,6 @@ def load(opt, path: str, model: Optional[torch.nn.Module] = None) -> dict:
         opt.store.data.copy_(ps["params"].to(opt.store.data.device))
         broadcast(opt.store.data, opt.world, 0)
         opt.engine.load_engine_state(es)
+    opt.store.refresh_shadow()
     barrier(opt.world)
     return ps.get("extra", {})

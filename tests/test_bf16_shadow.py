@@ -1,0 +1,79 @@
+"""bf16 weight shadow (FlatStore.enable_bf16_shadow / ops.nn.bf16_weight): the conv kernels read a
+flat bf16 copy of the fp32 params refreshed once per step instead of casting every layer's weight
+in every forward.  The cast is the same round-to-nearest, so training must be bit-identical."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import hipps
+from hipps.ops import nn as hnn
+
+
+def _conv_model():
+    torch.manual_seed(0)
+    return torch.nn.Sequential(torch.nn.Conv2d(8, 16, 3, bias=False), torch.nn.Conv2d(16, 4, 1, bias=False))
+
+
+def test_shadow_views_follow_steps_cpu():
+    m = _conv_model().to(memory_format=torch.channels_last)
+    opt = hipps.SGD(m.named_parameters(), lr=0.1, momentum=0.9, mode="local", bf16_weights="on")
+    try:
+        for p in m.parameters():
+            v = hnn.bf16_weight(p)
+            assert v.dtype == torch.bfloat16 and v.shape == p.shape and v.stride() == p.stride()
+            assert torch.equal(v, p.detach().to(torch.bfloat16))
+        x = torch.randn(2, 8, 6, 6).contiguous(memory_format=torch.channels_last)
+        m(x).square().mean().backward()
+        opt.step()
+        for p in m.parameters():  # refreshed by step()
+            assert torch.equal(hnn.bf16_weight(p), p.detach().to(torch.bfloat16))
+        with torch.no_grad():
+            for p in m.parameters():
+                p.mul_(0.5)
+        opt.refresh_bf16_weights()
+        for p in m.parameters():
+            assert torch.equal(hnn.bf16_weight(p), p.detach().to(torch.bfloat16))
+        foreign = torch.randn(3, 3)
+        assert torch.equal(hnn.bf16_weight(foreign), foreign.to(torch.bfloat16))
+    finally:
+        opt.close()
+    assert not hnn._SHADOWS  # close() unregisters
+
+
+def test_shadow_auto_off_for_sync_modes_cpu():
+    m = _conv_model()
+    opt = hipps.SGD(m.named_parameters(), lr=0.1, mode="local")
+    try:
+        assert getattr(opt.store, "shadow", None) is None
+    finally:
+        opt.close()
+
+
+@pytest.mark.gpu
+def test_shadow_resnet_bit_identical_gpu():
+    from hipps.models import resnet_tiny
+
+    def run(flag):
+        torch.manual_seed(0)
+        m = resnet_tiny().cuda().to(memory_format=torch.channels_last)
+        opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="local", bf16_weights=flag)
+        g = torch.Generator(device="cuda").manual_seed(1)
+        losses = []
+        try:
+            for _ in range(3):
+                x = torch.randn(8, 3, 32, 32, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+                y = torch.randint(0, 10, (8,), device="cuda", generator=g)
+                opt.zero_grad()
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    loss = F.cross_entropy(m(x), y)
+                loss.backward()
+                opt.step()
+                losses.append(loss.item())
+            return losses, opt.store.data.clone()
+        finally:
+            opt.close()
+
+    l_on, p_on = run("on")
+    l_off, p_off = run("off")
+    assert l_on == l_off
+    assert torch.equal(p_on, p_off)
