@@ -6,6 +6,7 @@ namespace hipps {
 void aggregate(const std::vector<at::Tensor>& slots, at::Tensor acc, double gscale, bool accumulate);
 void convert(at::Tensor src, at::Tensor dst, double scale);
 void gather_flat(const std::vector<at::Tensor>& srcs, at::Tensor table, at::Tensor dst, double scale);
+void transpose_cast(at::Tensor src, at::Tensor dst, at::Tensor tiles);
 void sgd_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p, c10::optional<at::Tensor> buf,
               c10::optional<at::Tensor> pub, bool zero_src, double lr, double wd, double momentum, double dampening,
               bool nesterov, bool first);
@@ -72,6 +73,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("aggregate", &hipps::aggregate, "acc (+)= gscale * sum_w slots[w] (rank order)");
   m.def("convert", &hipps::convert, "dst = scale * src with f32/bf16 conversion");
   m.def("gather_flat", &hipps::gather_flat, "multi-tensor gather (+cast) of grads into a flat buffer");
+  m.def("transpose_cast", &hipps::transpose_cast, "multi-matrix dst[c,r] = bf16(src[r,c]) (1x1 dgrad weights)");
   m.def("sgd_step", &hipps::sgd_step, "fused decode+sum+SGD (reference ps.py:197-214 math)");
   m.def("adam_step", &hipps::adam_step, "fused decode+sum+Adam (reference ps.py:217-261 math)");
   m.def("q8_encode", &hipps::q8_encode, "per-256-block absmax int8 quantization (+EF, +stochastic)");

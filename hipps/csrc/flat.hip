@@ -231,6 +231,35 @@ __global__ __launch_bounds__(kBlock) void k_gather(GatherPtrs src, const int64_t
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// k_transpose_cast: dst[c, r] = bf16(src[r, c]) for a list of row-major fp32 matrices, one
+// launch per weight refresh.  Used for the 1x1-conv weights [Cout, Cin] whose input gradient
+// GEMM wants the K-contiguous [Cin, Cout] B operand (otherwise one transpose+cast launch per
+// layer per backward).  64x64 tiles through LDS (row stride 65: conflict-free column reads);
+// the tile table (src off, dst off, R, C, r0, c0) is static and device-resident.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_transpose_cast(const float* __restrict__ src, uint16_t* __restrict__ dst,
+                                                           const int64_t* __restrict__ tiles, int64_t ntiles) {
+  __shared__ float t[64][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int64_t b = blockIdx.x; b < ntiles; b += gridDim.x) {
+    const int64_t* row = tiles + b * 6;
+    const float* s = src + row[0];
+    uint16_t* d = dst + row[1];
+    const int64_t R = row[2], C = row[3], r0 = row[4], c0 = row[5];
+    for (int i = ty; i < 64; i += kBlock / 64) {
+      const int64_t r = r0 + i, c = c0 + tx;
+      t[i][tx] = (r < R && c < C) ? s[r * C + c] : 0.f;
+    }
+    __syncthreads();
+    for (int i = ty; i < 64; i += kBlock / 64) {
+      const int64_t c = c0 + i, r = r0 + tx;
+      if (c < C && r < R) d[c * R + r] = f32_to_bf16(t[tx][i]);
+    }
+    __syncthreads();
+  }
+}
+
 // ==========================================================================================
 // host launchers
 // ==========================================================================================
@@ -332,6 +361,21 @@ void gather_flat(const std::vector<at::Tensor>& srcs, at::Tensor table, at::Tens
   else
     hipLaunchKernelGGL(k_gather<uint16_t>, grid, kBlock, 0, stream, p, table.data_ptr<int64_t>(), nchunks,
                        (uint16_t*)dst.data_ptr(), (float)scale);
+}
+
+void transpose_cast(at::Tensor src, at::Tensor dst, at::Tensor tiles) {
+  check_dev(src, "src");
+  check_dev(dst, "dst");
+  TORCH_CHECK(src.scalar_type() == at::kFloat && src.is_contiguous(), "src must be a contiguous f32 flat buffer");
+  TORCH_CHECK(dst.scalar_type() == at::kBFloat16 && dst.is_contiguous(), "dst must be a contiguous bf16 flat buffer");
+  TORCH_CHECK(tiles.is_cuda() && tiles.scalar_type() == at::kLong && tiles.dim() == 2 && tiles.size(1) == 6,
+              "tiles must be a device int64 [ntiles, 6]");
+  const int64_t ntiles = tiles.size(0);
+  if (ntiles == 0) return;
+  auto stream = c10::hip::getCurrentHIPStream();
+  const int grid = (int)std::min<int64_t>(ntiles, kMaxGrid);
+  hipLaunchKernelGGL(k_transpose_cast, grid, kBlock, 0, stream, src.data_ptr<float>(), (uint16_t*)dst.data_ptr(),
+                     tiles.data_ptr<int64_t>(), ntiles);
 }
 
 void sgd_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p, c10::optional<at::Tensor> buf,

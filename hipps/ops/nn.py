@@ -74,6 +74,17 @@ def unregister_weight_shadow(shadow: torch.Tensor):
     _SHADOWS[:] = [(f, s) for f, s in _SHADOWS if s is not shadow]
 
 
+_TSHADOWS: dict = {}  # fp32 1x1-conv weight data_ptr -> [Cin, Cout] bf16 view (FlatStore tshadow)
+
+
+def register_transposed_weight(p: torch.Tensor, view: torch.Tensor):
+    _TSHADOWS[p.data_ptr()] = view
+
+
+def unregister_transposed_weight(p: torch.Tensor):
+    _TSHADOWS.pop(p.data_ptr(), None)
+
+
 def bf16_weight(w: torch.Tensor) -> torch.Tensor:
     """The bf16 view of fp32 master weight ``w`` in a registered shadow (same shape and strides),
     else a fresh cast.  The shadow is refreshed by the optimizer with one cast kernel per step, so
@@ -104,6 +115,7 @@ class _Conv1x1(torch.autograd.Function):
         ctx.wdtype = w_master.dtype
         # no zero-filled grad for the non-differentiable BN partials (a 12.8 MB fill per layer)
         ctx.set_materialize_grads(False)
+        ctx.wt = _TSHADOWS.get(w_master.data_ptr()) if w_master.dtype == torch.float32 else None
         ctx.bngrad = bngrad if stride == 1 else None
         N, Cin, H, W = x.shape
         Cout = w.shape[0]
@@ -153,7 +165,9 @@ class _Conv1x1(torch.autograd.Function):
                 dw = dw.to(ctx.wdtype)
         if own_dx:
             cout, cin = w.shape[0], w.shape[1]
-            wt = w.reshape(cout, cin).t().contiguous()  # [Cin, Cout]: K-contiguous B operand
+            wt = ctx.wt  # [Cin, Cout]: K-contiguous B operand (refreshed with the weight shadow)
+            if wt is None:
+                wt = w.reshape(cout, cin).t().contiguous()
             dx = torch.empty_like(x, memory_format=torch.channels_last)
             bg = ctx.bngrad
             # x's gradient is complete here only if the residual path it also feeds was summed in

@@ -141,18 +141,51 @@ class FlatStore:
         if getattr(self, "shadow", None) is None:
             self.shadow = torch.empty(self.numel, dtype=torch.bfloat16, device=self.device)
             hnn.register_weight_shadow(self.data, self.shadow)
+            self._build_transposed_shadow()
         self.refresh_shadow()
+
+    def _build_transposed_shadow(self):
+        """[Cin, Cout] bf16 copies of every 1x1-conv weight (the input-gradient GEMM's B operand),
+        refreshed with the shadow by one multi-matrix transpose kernel (flat.hip k_transpose_cast)."""
+        from ..ops import _native
+        from ..ops import nn as hnn
+
+        self.tshadow = self._tiles = None
+        if self.device.type != "cuda" or not _native.available():
+            return
+        mats, off = [], 0
+        for s in self.slots:
+            p = s.param
+            if p.dim() == 4 and p.shape[2] == 1 and p.shape[3] == 1 and _is_dense(p.data):
+                mats.append((s, off))
+                off += s.numel
+        if not mats:
+            return
+        self.tshadow = torch.empty(off, dtype=torch.bfloat16, device=self.device)
+        rows = []
+        for s, toff in mats:
+            R, C = s.param.shape[0], s.param.shape[1]
+            rows += [(s.offset, toff, R, C, r0, c0) for r0 in range(0, R, 64) for c0 in range(0, C, 64)]
+            hnn.register_transposed_weight(s.param, self.tshadow[toff:toff + s.numel].view(C, R))
+        self._tiles = torch.tensor(rows, dtype=torch.int64).to(self.device)
 
     def disable_bf16_shadow(self):
         from ..ops import nn as hnn
 
         if getattr(self, "shadow", None) is not None:
             hnn.unregister_weight_shadow(self.shadow)
-            self.shadow = None
+            if getattr(self, "tshadow", None) is not None:
+                for s in self.slots:
+                    hnn.unregister_transposed_weight(s.param)
+            self.shadow = self.tshadow = self._tiles = None
 
     def refresh_shadow(self):
         if getattr(self, "shadow", None) is not None:
             self.shadow.copy_(self.data)  # one vectorized cast kernel on the current stream
+            if getattr(self, "tshadow", None) is not None:
+                from ..ops._native import native
+
+                native().transpose_cast(self.data, self.tshadow, self._tiles)
 
     def group_slice(self, buf: torch.Tensor, gi: int) -> torch.Tensor:
         a, b = self.group_ranges[gi]

@@ -77,3 +77,33 @@ def test_shadow_resnet_bit_identical_gpu():
     l_off, p_off = run("off")
     assert l_on == l_off
     assert torch.equal(p_on, p_off)
+
+
+@pytest.mark.gpu
+def test_transposed_shadow_matches_torch_gpu():
+    torch.manual_seed(0)
+    convs = torch.nn.ModuleList([torch.nn.Conv2d(130, 70, 1, bias=False), torch.nn.Conv2d(64, 256, 1, bias=False),
+                                 torch.nn.Conv2d(8, 8, 3, bias=False), torch.nn.Conv2d(2048, 512, 1, bias=False)])
+    convs = convs.cuda().to(memory_format=torch.channels_last)
+    opt = hipps.SGD(convs.named_parameters(), lr=0.1, mode="local", bf16_weights="on")
+    try:
+        for c in convs:
+            w = c.weight
+            t = hnn._TSHADOWS.get(w.data_ptr())
+            if w.shape[2] != 1:
+                assert t is None
+                continue
+            ref = w.detach().reshape(w.shape[0], w.shape[1]).t().to(torch.bfloat16)
+            assert t.shape == ref.shape and torch.equal(t, ref)
+        with torch.no_grad():
+            for c in convs:
+                c.weight.mul_(-3.0)
+        opt.refresh_bf16_weights()
+        for c in convs:
+            w = c.weight
+            if w.shape[2] == 1:
+                ref = w.detach().reshape(w.shape[0], w.shape[1]).t().to(torch.bfloat16)
+                assert torch.equal(hnn._TSHADOWS[w.data_ptr()], ref)
+    finally:
+        opt.close()
+    assert not hnn._TSHADOWS
