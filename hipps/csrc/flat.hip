@@ -232,29 +232,32 @@ __global__ __launch_bounds__(kBlock) void k_gather(GatherPtrs src, const int64_t
 }
 
 // ------------------------------------------------------------------------------------------
-// k_transpose_cast: dst[c, r] = bf16(src[r, c]) for a list of row-major fp32 matrices, one
-// launch per weight refresh.  Used for the 1x1-conv weights [Cout, Cin] whose input gradient
-// GEMM wants the K-contiguous [Cin, Cout] B operand (otherwise one transpose+cast launch per
-// layer per backward).  64x64 tiles through LDS (row stride 65: conflict-free column reads);
-// the tile table (src off, dst off, R, C, r0, c0) is static and device-resident.
+// k_transpose_cast: dst[c * dst_ld + r] = bf16(src[r * src_ld + c]) over a list of fp32 matrix
+// slices, one launch per weight refresh.  Feeds two backward operands: the 1x1-conv weights
+// [Cout, Cin] -> [Cin, Cout] (the input-gradient GEMM's K-contiguous B operand), and every tap of
+// a KxK weight (channels-last [Cout][KH][KW][Cin]) -> tap (KH-1-kh, KW-1-kw) of [Cin][KH][KW][Cout],
+// i.e. rot180(W)^T for the stride-1 input gradient run as a forward convolution.  Without it,
+// each layer pays one transpose (+flip) launch per backward.  64x64 tiles through LDS (row stride
+// 65: conflict-free column reads); the tile table (src off, dst off, R, C, r0, c0, src_ld,
+// dst_ld) is static and device-resident.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_transpose_cast(const float* __restrict__ src, uint16_t* __restrict__ dst,
                                                            const int64_t* __restrict__ tiles, int64_t ntiles) {
   __shared__ float t[64][65];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int64_t b = blockIdx.x; b < ntiles; b += gridDim.x) {
-    const int64_t* row = tiles + b * 6;
+    const int64_t* row = tiles + b * 8;
     const float* s = src + row[0];
     uint16_t* d = dst + row[1];
-    const int64_t R = row[2], C = row[3], r0 = row[4], c0 = row[5];
+    const int64_t R = row[2], C = row[3], r0 = row[4], c0 = row[5], sld = row[6], dld = row[7];
     for (int i = ty; i < 64; i += kBlock / 64) {
       const int64_t r = r0 + i, c = c0 + tx;
-      t[i][tx] = (r < R && c < C) ? s[r * C + c] : 0.f;
+      t[i][tx] = (r < R && c < C) ? s[r * sld + c] : 0.f;
     }
     __syncthreads();
     for (int i = ty; i < 64; i += kBlock / 64) {
       const int64_t c = c0 + i, r = r0 + tx;
-      if (c < C && r < R) d[c * R + r] = f32_to_bf16(t[tx][i]);
+      if (c < C && r < R) d[c * dld + r] = f32_to_bf16(t[tx][i]);
     }
     __syncthreads();
   }
@@ -368,8 +371,8 @@ void transpose_cast(at::Tensor src, at::Tensor dst, at::Tensor tiles) {
   check_dev(dst, "dst");
   TORCH_CHECK(src.scalar_type() == at::kFloat && src.is_contiguous(), "src must be a contiguous f32 flat buffer");
   TORCH_CHECK(dst.scalar_type() == at::kBFloat16 && dst.is_contiguous(), "dst must be a contiguous bf16 flat buffer");
-  TORCH_CHECK(tiles.is_cuda() && tiles.scalar_type() == at::kLong && tiles.dim() == 2 && tiles.size(1) == 6,
-              "tiles must be a device int64 [ntiles, 6]");
+  TORCH_CHECK(tiles.is_cuda() && tiles.scalar_type() == at::kLong && tiles.dim() == 2 && tiles.size(1) == 8,
+              "tiles must be a device int64 [ntiles, 8]");
   const int64_t ntiles = tiles.size(0);
   if (ntiles == 0) return;
   auto stream = c10::hip::getCurrentHIPStream();

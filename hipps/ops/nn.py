@@ -23,6 +23,10 @@ import os as _os
 # weight gradient of the MFMA 1x1 path: own split-M kernel (1, default; v2 beats MIOpen on the
 # ResNet-50 shapes, profiles/conv1x1_wgrad_v2.json) or MIOpen (0), for A/B runs
 _OWN_WGRAD = _os.environ.get("HIPPS_CONV_WGRAD", "1") != "0"
+# stride-1 "same" KxK input gradient as a forward convolution of dy with the flipped, transposed
+# weight: MIOpen's backward-data solvers zero-fill dx first (SubTensorOpWithScalar1d, ~0.47 ms per
+# ResNet-50 step) and run slower than its forward kernels on the same shapes
+_DGRAD_AS_FWD = _os.environ.get("HIPPS_DGRAD_FWD", "1") != "0"
 
 MASK_NONE, MASK_X, MASK_Y, MASK_BITS = 0, 1, 2, 3
 
@@ -74,7 +78,9 @@ def unregister_weight_shadow(shadow: torch.Tensor):
     _SHADOWS[:] = [(f, s) for f, s in _SHADOWS if s is not shadow]
 
 
-_TSHADOWS: dict = {}  # fp32 1x1-conv weight data_ptr -> [Cin, Cout] bf16 view (FlatStore tshadow)
+# fp32 conv weight data_ptr -> bf16 backward operand (FlatStore tshadow): [Cin, Cout] for 1x1,
+# rot180(W)^T as a channels-last [Cin, Cout, KH, KW] for KxK
+_TSHADOWS: dict = {}
 
 
 def register_transposed_weight(p: torch.Tensor, view: torch.Tensor):
@@ -192,9 +198,11 @@ class _ConvKxK(torch.autograd.Function):
     fp32 workspace and need 3 extra zero-fill / cast kernels per call (profiles/bench_n1_steady_r1d.txt)."""
 
     @staticmethod
-    def forward(ctx, x, w_master, stride, pad):
+    def forward(ctx, x, w_master, stride, pad, own_wgrad=True):
         w = bf16_weight(w_master)
         ctx.wdtype = w_master.dtype
+        ctx.own_wgrad = own_wgrad
+        ctx.wf = _TSHADOWS.get(w_master.data_ptr()) if w_master.dtype == torch.float32 else None
         y = torch.ops.aten.convolution(x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1)
         ctx.geom = (stride, pad)
         ctx.save_for_backward(x, w)
@@ -206,19 +214,30 @@ class _ConvKxK(torch.autograd.Function):
         s, p = ctx.geom
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = None
-        if ctx.needs_input_grad[0]:
+        k = w.shape[2]
+        if ctx.needs_input_grad[0] and _DGRAD_AS_FWD and s == 1 and k == w.shape[3] and 2 * p == k - 1:
+            # dx[n, ci] = sum_co conv(dy[n, co], rot180(W[co, ci])) with the same padding
+            wf = ctx.wf if ctx.wf is not None and ctx.wf.dim() == 4 else None
+            if wf is None:
+                wf = torch.flip(w, (2, 3)).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+            dx = torch.ops.aten.convolution(dy, wf, None, [1, 1], [p, p], [1, 1], False, [0, 0], 1)
+        elif ctx.needs_input_grad[0]:
             dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
                                                      [True, False, False])[0]
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and not ctx.own_wgrad:
+            dw = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
+                                                     [False, True, False])[1].to(ctx.wdtype)
+        elif ctx.needs_input_grad[1]:
             dw = torch.empty(w.shape, dtype=torch.float32, device=w.device, memory_format=torch.channels_last)
             native().conv_wgrad(dy, x, dw, w.shape[2], w.shape[3], s, p)
             if ctx.wdtype != torch.float32:
                 dw = dw.to(ctx.wdtype)
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
-def convkxk_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
-    """Can the hipps weight-gradient path run this (square, zero-padded, dense) convolution?"""
+def convkxk_ok(conv: nn.Conv2d, x: torch.Tensor, own_wgrad: bool = True) -> bool:
+    """Can _ConvKxK run this (square, zero-padded, dense) convolution (with the hipps weight
+    gradient when ``own_wgrad``)?"""
     if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and torch.is_grad_enabled() and
             x.is_contiguous(memory_format=torch.channels_last)):
         return False
@@ -228,6 +247,8 @@ def convkxk_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     if conv.groups != 1 or conv.bias is not None or conv.padding_mode != "zeros":
         return False
     w = conv.weight
+    if not own_wgrad:
+        return w.is_contiguous(memory_format=torch.channels_last)
     # 64-channel KxK layers: a 64x64 output tile re-reads both operands once per tap and MIOpen
     # is faster there (0.23 vs 0.29 ms at 64x56x56, profiles/conv3x3_wgrad.json)
     return (conv.in_channels % 128 == 0 and conv.out_channels % 64 == 0 and
@@ -238,6 +259,8 @@ def conv2d(conv: nn.Conv2d, x: torch.Tensor, fuse: bool = True) -> torch.Tensor:
     """conv(x) with the hipps weight gradient when eligible (see _ConvKxK); otherwise conv(x)."""
     if fuse and conv.training and convkxk_ok(conv, x):
         return _ConvKxK.apply(x, conv.weight, conv.stride[0], conv.padding[0])
+    if _DGRAD_AS_FWD and conv.training and convkxk_ok(conv, x, own_wgrad=False) and conv.stride[0] == 1:
+        return _ConvKxK.apply(x, conv.weight, 1, conv.padding[0], False)  # MIOpen weight gradient
     return conv(x)
 
 

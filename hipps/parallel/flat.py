@@ -145,8 +145,10 @@ class FlatStore:
         self.refresh_shadow()
 
     def _build_transposed_shadow(self):
-        """[Cin, Cout] bf16 copies of every 1x1-conv weight (the input-gradient GEMM's B operand),
-        refreshed with the shadow by one multi-matrix transpose kernel (flat.hip k_transpose_cast)."""
+        """Backward-operand bf16 copies refreshed with the shadow by one multi-matrix transpose
+        kernel (flat.hip k_transpose_cast): [Cin, Cout] for every 1x1-conv weight (the input-
+        gradient GEMM's B operand) and rot180(W)^T as a channels-last [Cin, Cout, KH, KW] weight for
+        every square KxK conv (stride-1 input gradient as a forward convolution, ops.nn._ConvKxK)."""
         from ..ops import _native
         from ..ops import nn as hnn
 
@@ -156,7 +158,8 @@ class FlatStore:
         mats, off = [], 0
         for s in self.slots:
             p = s.param
-            if p.dim() == 4 and p.shape[2] == 1 and p.shape[3] == 1 and _is_dense(p.data):
+            if p.dim() == 4 and p.shape[2] == p.shape[3] and _is_dense(p.data) and \
+                    (p.shape[2] == 1 or p.is_contiguous(memory_format=torch.channels_last)):
                 mats.append((s, off))
                 off += s.numel
         if not mats:
@@ -164,9 +167,16 @@ class FlatStore:
         self.tshadow = torch.empty(off, dtype=torch.bfloat16, device=self.device)
         rows = []
         for s, toff in mats:
-            R, C = s.param.shape[0], s.param.shape[1]
-            rows += [(s.offset, toff, R, C, r0, c0) for r0 in range(0, R, 64) for c0 in range(0, C, 64)]
-            hnn.register_transposed_weight(s.param, self.tshadow[toff:toff + s.numel].view(C, R))
+            R, C, KH, KW = s.param.shape
+            T = KH * KW
+            for kh in range(KH):
+                for kw in range(KW):
+                    so = s.offset + (kh * KW + kw) * C
+                    do = toff + ((KH - 1 - kh) * KW + (KW - 1 - kw)) * R
+                    rows += [(so, do, R, C, r0, c0, T * C, T * R) for r0 in range(0, R, 64) for c0 in range(0, C, 64)]
+            seg = self.tshadow[toff:toff + s.numel]
+            view = seg.view(C, R) if T == 1 else seg.as_strided((C, R, KH, KW), (T * R, 1, KW * R, R))
+            hnn.register_transposed_weight(s.param, view)
         self._tiles = torch.tensor(rows, dtype=torch.int64).to(self.device)
 
     def disable_bf16_shadow(self):

@@ -292,3 +292,25 @@ def test_bottleneck_gradient_fusions(cin, width, stride, ds):
     for u, v in zip(res[True], res[False]):
         scale = v.abs().max().item() + 1e-6
         torch.testing.assert_close(u / scale, v / scale, rtol=0, atol=2e-2)
+
+
+@pytest.mark.parametrize("cin,cout,k", [(64, 64, 3), (128, 128, 3), (256, 128, 3), (64, 32, 5)])
+def test_kxk_dgrad_as_forward_matches_fp32(cin, cout, k):
+    """Stride-1 'same' KxK input gradient computed as conv(dy, rot180(W)^T) (_ConvKxK) vs the
+    fp32 autograd gradient of F.conv2d."""
+    torch.manual_seed(cin + cout + k)
+    conv = torch.nn.Conv2d(cin, cout, k, padding=k // 2, bias=False).to(DEV).to(memory_format=torch.channels_last)
+    x0 = _cl(torch.randn(4, cin, 14, 14, device=DEV).to(torch.bfloat16))
+    g = _cl(torch.randn(4, cout, 14, 14, device=DEV).to(torch.bfloat16))
+    x = x0.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = hnn.conv2d(conv, x)
+    assert y.grad_fn is not None and "ConvKxK" in type(y.grad_fn).__name__
+    y.backward(g)
+    xr = x0.float().requires_grad_(True)
+    wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    F.conv2d(xr, wr, padding=k // 2).backward(g.float())
+    scale = xr.grad.abs().max().item()
+    torch.testing.assert_close(x.grad.float() / scale, xr.grad / scale, rtol=0, atol=1e-2)
+    scale = wr.grad.abs().max().item()
+    torch.testing.assert_close(conv.weight.grad.float() / scale, wr.grad / scale, rtol=0, atol=1e-2)
