@@ -81,7 +81,10 @@ class MPI_PS(torch.optim.Optimizer):
         self.steps = 0
         self.engine = self._make_engine()
         bw = self.cfg.bf16_weights
-        if bw == "on" or (bw == "auto" and self.mode == "ps_async" and self.store.device.type == "cuda"):
+        # auto: only where a reader exists (the hipps conv kernels read 4-D weights); a transformer
+        # would pay a full bf16 copy of the model (16 GB for Llama-3-8B) for nothing
+        has_conv = any(s.param.dim() == 4 for s in self.store.slots)
+        if bw == "on" or (bw == "auto" and self.mode == "ps_async" and self.store.device.type == "cuda" and has_conv):
             self.store.enable_bf16_shadow()
         self._metrics = None
         if self.cfg.metrics_path:

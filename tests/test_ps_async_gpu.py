@@ -31,8 +31,9 @@ def _gpu_async(rank, world, steps, codec, accumulate, max_delay):
         losses.append(loss.item())
         opt.step()
     eng = opt.engine
+    has_shadow = getattr(opt.store, "shadow", None) is not None
     opt.close()
-    return {"init": init, "losses": losses, "stats": eng.ps_stats(),
+    return {"init": init, "losses": losses, "stats": eng.ps_stats(), "shadow": has_shadow,
             "params": [p.detach().clone() for p in m.parameters()]}
 
 
@@ -40,6 +41,7 @@ def test_gpu_async_single_rank_equals_local():
     import hipps
 
     out = run_world(_gpu_async, 1, 5, "fp32", 1, 0)
+    assert not out[0]["shadow"]  # bf16_weights='auto': no conv weights, no bf16 shadow
     torch.cuda.set_device(0)
     m = _mlp().cuda()
     opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="local")
