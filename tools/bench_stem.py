@@ -43,8 +43,8 @@ def main():
         fwd = lambda: torch.ops.aten.convolution(x, w, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1)
         wgr = lambda: torch.ops.aten.convolution_backward(dy, x, w, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
                                                           [False, True, False])[1]
-        pad = lambda: torch.zeros(n, c, 224, 224, device="cuda", dtype=torch.bfloat16,
-                                  memory_format=cl)[:, :3].copy_(x3)
+        pad = lambda: torch.empty(n, c, 224, 224, device="cuda", dtype=torch.bfloat16,
+                                  memory_format=cl).zero_()[:, :3].copy_(x3)
         y = fwd()
         dw = wgr()
         err = (y.float() - y_ref.float()).abs().max().item()
