@@ -33,17 +33,20 @@ __device__ __forceinline__ void st8(uint16_t* p, const float v[8]) {
 }
 }  // namespace
 
+template <typename I>
 __global__ __launch_bounds__(kBlock) void k_maxpool3s2_fwd(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                            uint32_t* __restrict__ code, int64_t total, int H, int W,
                                                            int Ho, int Wo, int G) {
   const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= total) return;
-  const int g = (int)(v % G);
-  int64_t p = v / G;
-  const int wo = (int)(p % Wo);
-  p /= Wo;
-  const int ho = (int)(p % Ho);
-  const int64_t n = p / Ho;
+  // 32-bit index decomposition when the grid fits (the int64 div/mod sequence dominated)
+  I p = (I)v;
+  const int g = (int)(p % (I)G);
+  p /= (I)G;
+  const int wo = (int)(p % (I)Wo);
+  p /= (I)Wo;
+  const int ho = (int)(p % (I)Ho);
+  const int64_t n = (int64_t)(p / (I)Ho);
   float m[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
@@ -72,18 +75,20 @@ __global__ __launch_bounds__(kBlock) void k_maxpool3s2_fwd(const uint16_t* __res
   code[v] = c;
 }
 
+template <typename I>
 __global__ __launch_bounds__(kBlock) void k_maxpool3s2_bwd(const uint16_t* __restrict__ dy,
                                                            const uint32_t* __restrict__ code,
                                                            uint16_t* __restrict__ dx, int64_t total, int H, int W,
                                                            int Ho, int Wo, int G) {
   const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= total) return;
-  const int g = (int)(v % G);
-  int64_t p = v / G;
-  const int w = (int)(p % W);
-  p /= W;
-  const int h = (int)(p % H);
-  const int64_t n = p / H;
+  I p = (I)v;
+  const int g = (int)(p % (I)G);
+  p /= (I)G;
+  const int w = (int)(p % (I)W);
+  p /= (I)W;
+  const int h = (int)(p % (I)H);
+  const int64_t n = (int64_t)(p / (I)H);
   float acc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
@@ -120,9 +125,16 @@ void maxpool3s2_forward(at::Tensor x, at::Tensor y, at::Tensor code) {
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "maxpool: 16-byte aligned tensors");
   TORCH_CHECK(x.numel() < (int64_t(1) << 40) && (total + kBlock - 1) / kBlock < (int64_t(1) << 31), "maxpool: size");
   if (total == 0) return;
-  hipLaunchKernelGGL(k_maxpool3s2_fwd, (int)((total + kBlock - 1) / kBlock), kBlock, 0,
-                     c10::hip::getCurrentHIPStream(), (const uint16_t*)x.data_ptr(), (uint16_t*)y.data_ptr(),
-                     (uint32_t*)code.data_ptr(), total, (int)H, (int)W, (int)Ho, (int)Wo, (int)(C / 8));
+  const int grid = (int)((total + kBlock - 1) / kBlock);
+  auto stream = c10::hip::getCurrentHIPStream();
+  if (total < (int64_t(1) << 31))
+    hipLaunchKernelGGL(k_maxpool3s2_fwd<uint32_t>, grid, kBlock, 0, stream, (const uint16_t*)x.data_ptr(),
+                       (uint16_t*)y.data_ptr(), (uint32_t*)code.data_ptr(), total, (int)H, (int)W, (int)Ho, (int)Wo,
+                       (int)(C / 8));
+  else
+    hipLaunchKernelGGL(k_maxpool3s2_fwd<int64_t>, grid, kBlock, 0, stream, (const uint16_t*)x.data_ptr(),
+                       (uint16_t*)y.data_ptr(), (uint32_t*)code.data_ptr(), total, (int)H, (int)W, (int)Ho, (int)Wo,
+                       (int)(C / 8));
 }
 
 // dy: [N, C, Ho, Wo] channels-last bf16; dx: [N, C, H, W] channels-last bf16 (fully written).
@@ -143,9 +155,16 @@ void maxpool3s2_backward(at::Tensor dy, at::Tensor code, at::Tensor dx) {
   TORCH_CHECK(dx.numel() < (int64_t(1) << 40) && (total + kBlock - 1) / kBlock < (int64_t(1) << 31),
               "maxpool bwd: size");
   if (total == 0) return;
-  hipLaunchKernelGGL(k_maxpool3s2_bwd, (int)((total + kBlock - 1) / kBlock), kBlock, 0,
-                     c10::hip::getCurrentHIPStream(), (const uint16_t*)dy.data_ptr(), (const uint32_t*)code.data_ptr(),
-                     (uint16_t*)dx.data_ptr(), total, (int)H, (int)W, (int)Ho, (int)Wo, (int)(C / 8));
+  const int grid = (int)((total + kBlock - 1) / kBlock);
+  auto stream = c10::hip::getCurrentHIPStream();
+  if (total < (int64_t(1) << 31))
+    hipLaunchKernelGGL(k_maxpool3s2_bwd<uint32_t>, grid, kBlock, 0, stream, (const uint16_t*)dy.data_ptr(),
+                       (const uint32_t*)code.data_ptr(), (uint16_t*)dx.data_ptr(), total, (int)H, (int)W, (int)Ho,
+                       (int)Wo, (int)(C / 8));
+  else
+    hipLaunchKernelGGL(k_maxpool3s2_bwd<int64_t>, grid, kBlock, 0, stream, (const uint16_t*)dy.data_ptr(),
+                       (const uint32_t*)code.data_ptr(), (uint16_t*)dx.data_ptr(), total, (int)H, (int)W, (int)Ho,
+                       (int)Wo, (int)(C / 8));
 }
 
 }  // namespace hipps
