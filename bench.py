@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
+    ap.add_argument("--allow-fallback", action="store_true",
+                    help="if the ps_async transport cannot initialise, run ps_sync instead of failing")
     return ap.parse_args()
 
 
@@ -94,7 +96,7 @@ def main():
                         code=a.codec, accumulate=a.accumulate or None, average=True, param_wire=a.param_wire,
                         bucket_mb=a.bucket_mb)
     except Exception as e:  # robust fallback so a scaling run still reports a number
-        if mode != "ps_async" or N == 1:
+        if mode != "ps_async" or N == 1 or not a.allow_fallback:
             raise
         note = f"ps_async init failed ({type(e).__name__}: {e}); fell back to ps_sync"
         print("[bench] " + note, file=sys.stderr)
@@ -110,8 +112,11 @@ def main():
         _, data = opt.step()
         return loss, data
 
+    first_loss = None
     for _ in range(a.warmup):
-        step()
+        loss, _ = step()
+        if first_loss is None:
+            first_loss = float(loss.float().item())
     tr = opt.engine.tracer  # HIPPS_TRACE=1: per-phase device ms (HIP events), excluded from warmup
     if tr.enabled:
         torch.cuda.synchronize()
@@ -175,6 +180,7 @@ def main():
                 "num_params": nparams,
                 "buckets": nbuckets,
             },
+            "first_loss": None if first_loss is None else round(first_loss, 4),
             "final_loss": round(final_loss, 4),
             "ps": {k: (int(v) if isinstance(v, (int, float)) else v) for k, v in stats.items()},
         }

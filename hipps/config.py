@@ -31,8 +31,13 @@ class PSConfig:
     max_delay: int = -1
     # async PS: pull the newest published params at the end of every step() (AsySG-InCon read)
     auto_pull: bool = True
-    # async PS, remote GPU workers: 'prefetch' (side-stream xGMI read, adopted next step) | 'direct'
-    pull: str = "prefetch"
+    # async PS parameter pull on a GPU: 'device' (the GPU picks the newest published version when
+    # it reaches the pull, right before the next forward, and copies it in stream order; needs
+    # GPU-rung doorbells) | 'prefetch' (host-chosen version, side-stream copy adopted at the next
+    # step) | 'direct' (host-chosen, copy on the compute stream)
+    pull: str = "device"
+    # async PS: scale a kept gradient by 1/max(1, staleness) (staleness-aware async SGD)
+    staleness_lr: bool = False
     # async PS failure detection: a worker silent for this long (no heartbeat, no STOP) is dead
     dead_after_s: float = 60.0
     # async PS mailbox: bucket messages in flight per worker (0 = auto: min(2*buckets, mailbox_mb))
@@ -56,6 +61,19 @@ class PSConfig:
     # any out-of-band edit is overwritten by the next adoption anyway); 'on' | 'off' otherwise.
     # With 'on', call opt.refresh_bf16_weights() after editing params outside step().
     bf16_weights: str = "auto"
+    # parameters that produced no gradient this step are left untouched -- no weight decay, no
+    # momentum step (ps.py:178-179 `if p.grad is None: continue`); the sync modes OR the
+    # per-rank presence so replicas stay identical, the async PS ORs the accumulated messages'
+    skip_missing_grads: bool = True
+    # raise ValueError when a parameter produced no gradient (the reference's ps.py:118-119 check)
+    require_all_grads: bool = False
+    # collective / transport timeout: the process-group timeout for the sync modes and the
+    # async PS's waits; a watchdog thread aborts the process (exit code 3) if one step's
+    # exchange exceeds it, instead of hanging on a dead peer
+    comm_timeout_s: float = 600.0
+    # ObjectCodec (reference encode/decode/.codes objects): max serialized bytes per rank per
+    # step in the async PS mailbox (0 = auto: 2x the fp32 model + 1 MiB)
+    object_slot_mb: float = 0.0
     # host pickle slow path compression level (mpi_comms.py:18; 0 = framing only)
     compress_level: int = 0
     # Adam eps placement: 'reference' (ps.py:255) or 'torch'
@@ -97,8 +115,8 @@ class PSConfig:
     def validate(self):
         if self.mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}, got {self.mode!r}")
-        if self.pull not in ("prefetch", "direct"):
-            raise ValueError("pull must be 'prefetch' or 'direct'")
+        if self.pull not in ("device", "prefetch", "direct"):
+            raise ValueError("pull must be 'device', 'prefetch' or 'direct'")
         if self.param_wire not in ("fp32", "bf16"):
             raise ValueError("param_wire must be 'fp32' or 'bf16'")
         if self.bf16_weights not in ("auto", "on", "off"):

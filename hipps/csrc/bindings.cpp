@@ -9,11 +9,11 @@ void gather_flat(const std::vector<at::Tensor>& srcs, at::Tensor table, at::Tens
 void transpose_cast(at::Tensor src, at::Tensor dst, at::Tensor tiles);
 void sgd_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p, c10::optional<at::Tensor> buf,
               c10::optional<at::Tensor> pub, bool zero_src, double lr, double wd, double momentum, double dampening,
-              bool nesterov, bool first);
+              bool nesterov, bool first, c10::optional<at::Tensor> mask);
 void adam_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p, at::Tensor exp_avg,
                at::Tensor exp_avg_sq, c10::optional<at::Tensor> max_exp_avg_sq, c10::optional<at::Tensor> pub,
                bool zero_src, double lr, double beta1, double beta2, double eps, double wd, int64_t step,
-               bool amsgrad, bool torch_mode);
+               bool amsgrad, bool torch_mode, c10::optional<at::Tensor> mask);
 // quant.hip
 void q8_encode(at::Tensor x, c10::optional<at::Tensor> resid, at::Tensor q, at::Tensor scales, bool stochastic,
                int64_t seed);
@@ -62,6 +62,8 @@ void maxpool3s2_backward(at::Tensor dy, at::Tensor code, at::Tensor dx);
 void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64_t Wi, int64_t stride);
 void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t KW, int64_t stride, int64_t pad);
 namespace rt {
+void pull_params(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, at::Tensor pub,
+                 int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t ring_slot, int64_t tries);
 void bind_control(pybind11::module& m);
 void bind_ipc(pybind11::module& m);
 void bind_trace(pybind11::module& m);
@@ -74,8 +76,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("convert", &hipps::convert, "dst = scale * src with f32/bf16 conversion");
   m.def("gather_flat", &hipps::gather_flat, "multi-tensor gather (+cast) of grads into a flat buffer");
   m.def("transpose_cast", &hipps::transpose_cast, "multi-matrix dst[c,r] = bf16(src[r,c]) (1x1 dgrad weights)");
-  m.def("sgd_step", &hipps::sgd_step, "fused decode+sum+SGD (reference ps.py:197-214 math)");
-  m.def("adam_step", &hipps::adam_step, "fused decode+sum+Adam (reference ps.py:217-261 math)");
+  m.def("sgd_step", &hipps::sgd_step, "fused decode+sum+SGD (reference ps.py:197-214 math)", pybind11::arg("grads"),
+        pybind11::arg("gscale"), pybind11::arg("p"), pybind11::arg("buf"), pybind11::arg("pub"),
+        pybind11::arg("zero_src"), pybind11::arg("lr"), pybind11::arg("wd"), pybind11::arg("momentum"),
+        pybind11::arg("dampening"), pybind11::arg("nesterov"), pybind11::arg("first"),
+        pybind11::arg("mask") = pybind11::none());
+  m.def("adam_step", &hipps::adam_step, "fused decode+sum+Adam (reference ps.py:217-261 math)",
+        pybind11::arg("grads"), pybind11::arg("gscale"), pybind11::arg("p"), pybind11::arg("exp_avg"),
+        pybind11::arg("exp_avg_sq"), pybind11::arg("max_exp_avg_sq"), pybind11::arg("pub"), pybind11::arg("zero_src"),
+        pybind11::arg("lr"), pybind11::arg("beta1"), pybind11::arg("beta2"), pybind11::arg("eps"), pybind11::arg("wd"),
+        pybind11::arg("step"), pybind11::arg("amsgrad"), pybind11::arg("torch_mode"),
+        pybind11::arg("mask") = pybind11::none());
   m.def("q8_encode", &hipps::q8_encode, "per-256-block absmax int8 quantization (+EF, +stochastic)");
   m.def("q8_aggregate", &hipps::q8_aggregate, "acc (+)= gscale * sum_w dequant(q_w, s_w)");
   m.def("topk_encode", &hipps::topk_encode, "exact top-k |g| (radix select) -> idx asc, val");
@@ -103,6 +114,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool3s2_forward", &hipps::maxpool3s2_forward, "3x3/s2/p1 max pool, channels-last bf16, 4-bit tap codes");
   m.def("maxpool3s2_backward", &hipps::maxpool3s2_backward, "3x3/s2/p1 max pool backward (gather form, no atomics)");
   m.def("conv1x1_wgrad", &hipps::conv1x1_wgrad, "MFMA 1x1 conv weight gradient (tr_b16 LDS reads, split-M)");
+  m.def("pull_params", &hipps::rt::pull_params,
+        "GPU-time AsySG-InCon pull: select newest published version, copy it, release the reader word");
   hipps::rt::bind_control(m);
   hipps::rt::bind_ipc(m);
   hipps::rt::bind_trace(m);

@@ -133,14 +133,18 @@ __global__ __launch_bounds__(kBlock) void k_convert(const Tin* __restrict__ src,
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_sgd(SlotPtrs g, int W, float gscale, float* __restrict__ p,
                                                 float* __restrict__ buf, void* __restrict__ pub, int pub_mode,
-                                                int zero_src, int64_t n, SgdHp h) {
+                                                int zero_src, int64_t n, SgdHp h, const uint8_t* __restrict__ cmask) {
   const bool has_buf = buf != nullptr;
   const int64_t nv = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
     const int64_t i = v << 2;
-    float4 d = sum_slots4<T>(g, W, i, gscale);
     if (zero_src) Vec4<float>::store((float*)g.p[0], i, make_float4(0.f, 0.f, 0.f, 0.f));
     float4 pv = Vec4<float>::load(p, i);
+    if (cmask && !cmask[i >> 4]) {  // parameter without a gradient this step: untouched (ps.py:178-179)
+      pub_store4(pub, pub_mode, i, pv);
+      continue;
+    }
+    float4 d = sum_slots4<T>(g, W, i, gscale);
     float4 b = has_buf && !h.first ? Vec4<float>::load(buf, i) : make_float4(0.f, 0.f, 0.f, 0.f);
     sgd1(pv.x, b.x, d.x, h, has_buf);
     sgd1(pv.y, b.y, d.y, h, has_buf);
@@ -155,6 +159,10 @@ __global__ __launch_bounds__(kBlock) void k_sgd(SlotPtrs g, int W, float gscale,
       float d = sum_slots1<T>(g, W, i, gscale);
       if (zero_src) ((float*)g.p[0])[i] = 0.f;
       float pv = p[i];
+      if (cmask && !cmask[i >> 4]) {
+        pub_store1(pub, pub_mode, i, pv);
+        continue;
+      }
       float b = has_buf && !h.first ? buf[i] : 0.f;
       sgd1(pv, b, d, h, has_buf);
       p[i] = pv;
@@ -168,13 +176,17 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void k_adam(SlotPtrs g, int W, float gscale, float* __restrict__ p,
                                                  float* __restrict__ m, float* __restrict__ vv,
                                                  float* __restrict__ vmax, void* __restrict__ pub, int pub_mode,
-                                                 int zero_src, int64_t n, AdamHp h) {
+                                                 int zero_src, int64_t n, AdamHp h, const uint8_t* __restrict__ cmask) {
   const int64_t nv = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
   float dummy = 0.f;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
     const int64_t i = v << 2;
-    float4 d = sum_slots4<T>(g, W, i, gscale);
     if (zero_src) Vec4<float>::store((float*)g.p[0], i, make_float4(0.f, 0.f, 0.f, 0.f));
+    if (cmask && !cmask[i >> 4]) {
+      pub_store4(pub, pub_mode, i, Vec4<float>::load(p, i));
+      continue;
+    }
+    float4 d = sum_slots4<T>(g, W, i, gscale);
     float4 pv = Vec4<float>::load(p, i), mv = Vec4<float>::load(m, i), sv = Vec4<float>::load(vv, i);
     float4 xv = h.amsgrad ? Vec4<float>::load(vmax, i) : make_float4(0.f, 0.f, 0.f, 0.f);
     adam1(pv.x, mv.x, sv.x, &xv.x, d.x, h);
@@ -191,6 +203,10 @@ __global__ __launch_bounds__(kBlock) void k_adam(SlotPtrs g, int W, float gscale
     for (int64_t i = (nv << 2) + threadIdx.x; i < n; i += blockDim.x) {
       float d = sum_slots1<T>(g, W, i, gscale);
       if (zero_src) ((float*)g.p[0])[i] = 0.f;
+      if (cmask && !cmask[i >> 4]) {
+        pub_store1(pub, pub_mode, i, p[i]);
+        continue;
+      }
       float pv = p[i], mv = m[i], sv = vv[i];
       float* xp = h.amsgrad ? &vmax[i] : &dummy;
       adam1(pv, mv, sv, xp, d, h);
@@ -295,6 +311,16 @@ SlotPtrs make_slots(const std::vector<at::Tensor>& slots, int64_t n, WireT& wt) 
   return s;
 }
 
+// chunk mask: one byte per 16 flat elements (every parameter slot starts on a 16-element
+// boundary, so a chunk never straddles two parameters); 0 = skip the chunk this step
+const uint8_t* cmask_of(const c10::optional<at::Tensor>& mask, int64_t n) {
+  if (!mask.has_value() || !mask->defined()) return nullptr;
+  TORCH_CHECK(mask->is_cuda() && mask->is_contiguous() && mask->scalar_type() == at::kByte,
+              "mask must be a contiguous uint8 device tensor");
+  TORCH_CHECK(mask->numel() >= (n + 15) / 16, "mask has ", mask->numel(), " chunks, need ", (n + 15) / 16);
+  return mask->data_ptr<uint8_t>();
+}
+
 int pub_mode_of(const c10::optional<at::Tensor>& pub, int64_t n) {
   if (!pub.has_value() || !pub->defined()) return 0;
   check_dev(*pub, "publish");
@@ -383,7 +409,7 @@ void transpose_cast(at::Tensor src, at::Tensor dst, at::Tensor tiles) {
 
 void sgd_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p, c10::optional<at::Tensor> buf,
               c10::optional<at::Tensor> pub, bool zero_src, double lr, double wd, double momentum, double dampening,
-              bool nesterov, bool first) {
+              bool nesterov, bool first, c10::optional<at::Tensor> mask) {
   check_dev(p, "param");
   TORCH_CHECK(p.scalar_type() == at::kFloat, "param master must be float32");
   const int64_t n = p.numel();
@@ -400,20 +426,21 @@ void sgd_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p,
   const int pm = pub_mode_of(pub, n);
   void* pp = pm ? pub->data_ptr() : nullptr;
   SgdHp h{(float)lr, (float)wd, (float)momentum, (float)dampening, (int)nesterov, (int)first};
+  const uint8_t* cm = cmask_of(mask, n);
   auto stream = c10::hip::getCurrentHIPStream();
   const int grid = grid_for(n >> 2);
   if (wt == WireT::F32)
     hipLaunchKernelGGL(k_sgd<float>, grid, kBlock, 0, stream, s, (int)grads.size(), (float)gscale,
-                       p.data_ptr<float>(), bp, pp, pm, (int)zero_src, n, h);
+                       p.data_ptr<float>(), bp, pp, pm, (int)zero_src, n, h, cm);
   else
     hipLaunchKernelGGL(k_sgd<uint16_t>, grid, kBlock, 0, stream, s, (int)grads.size(), (float)gscale,
-                       p.data_ptr<float>(), bp, pp, pm, (int)zero_src, n, h);
+                       p.data_ptr<float>(), bp, pp, pm, (int)zero_src, n, h, cm);
 }
 
 void adam_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p, at::Tensor exp_avg,
                at::Tensor exp_avg_sq, c10::optional<at::Tensor> max_exp_avg_sq, c10::optional<at::Tensor> pub,
                bool zero_src, double lr, double beta1, double beta2, double eps, double wd, int64_t step,
-               bool amsgrad, bool torch_mode) {
+               bool amsgrad, bool torch_mode, c10::optional<at::Tensor> mask) {
   check_dev(p, "param");
   check_dev(exp_avg, "exp_avg");
   check_dev(exp_avg_sq, "exp_avg_sq");
@@ -434,16 +461,17 @@ void adam_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p
   const double step_size = torch_mode ? lr / bc1 : lr * std::sqrt(bc2) / bc1;
   AdamHp h{(float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, (float)step_size, (float)std::sqrt(bc2),
            (int)amsgrad, (int)torch_mode};
+  const uint8_t* cm = cmask_of(mask, n);
   auto stream = c10::hip::getCurrentHIPStream();
   const int grid = grid_for(n >> 2);
   if (wt == WireT::F32)
     hipLaunchKernelGGL(k_adam<float>, grid, kBlock, 0, stream, s, (int)grads.size(), (float)gscale,
                        p.data_ptr<float>(), exp_avg.data_ptr<float>(), exp_avg_sq.data_ptr<float>(), xp, pp, pm,
-                       (int)zero_src, n, h);
+                       (int)zero_src, n, h, cm);
   else
     hipLaunchKernelGGL(k_adam<uint16_t>, grid, kBlock, 0, stream, s, (int)grads.size(), (float)gscale,
                        p.data_ptr<float>(), exp_avg.data_ptr<float>(), exp_avg_sq.data_ptr<float>(), xp, pp, pm,
-                       (int)zero_src, n, h);
+                       (int)zero_src, n, h, cm);
 }
 
 }  // namespace hipps

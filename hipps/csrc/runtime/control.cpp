@@ -6,13 +6,16 @@
 // stop), and the PS owns the published-parameter version words.  Data never goes through here
 // (it moves device-to-device into IPC mailboxes, see ipc.cpp); only 8-byte doorbells do.
 //
-//   worker: copy grad -> PS mailbox slot (comm stream) ; then hipLaunchHostFunc -> push_seq = s
-//   PS:     wait_any(push_seq > seen) ; accumulate slot ; hostfunc -> ack_seq = s
-//   PS:     after M grads: update + publish into pub buffer b ; hostfunc -> buf_ver[b], pub_ver
-//   worker: irequest_params(): pub_ver newer? copy pub[pub_ver % NPUB] (one-sided pull)
+//   worker: copy grad -> PS mailbox slot (comm stream) ; then doorbell -> push_seq = s
+//   PS:     wait_any(push_seq > seen) ; accumulate slot ; doorbell -> ack_seq = s
+//   PS:     after M grads: update + publish into a free pub buffer b ; doorbell -> buf_ver[b], pub_ver
+//   worker: irequest_params(): pub_ver newer? reading = v ; copy pub[b] (one-sided pull) ;
+//           doorbell -> reading = -1   (the PS never rewrites a buffer somebody is reading)
 //
-// Doorbells written from a stream callback are ordered after the stream's earlier work, so a
-// doorbell never runs ahead of the bytes it announces.
+// Doorbells are stream-ordered: a one-wavefront kernel (doorbell.hip) stores the words with a
+// system-scope release into this block, which every process registers with hipHostRegister.
+// Without a HIP device (CPU runs) or if registration fails they fall back to
+// hipLaunchHostFunc callbacks.  Either way a doorbell never runs ahead of the bytes it announces.
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -25,11 +28,14 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+
+#include "runtime/doorbell.h"
 
 namespace py = pybind11;
 
@@ -39,7 +45,7 @@ namespace rt {
 constexpr int64_t kMagic = 0x5350504948ll;  // "HIPPS"
 constexpr int kMaxRanks = 64;
 constexpr int kSlots = 64;  // max mailbox slots per worker (bucket messages in flight)
-constexpr int kPub = 3;    // published parameter buffers
+constexpr int kPub = 4;    // published parameter buffers (>= 2 + concurrent readers of old versions)
 
 struct alignas(64) RankRec {
   std::atomic<int64_t> push_seq;           // last message fully landed in the PS mailbox
@@ -49,6 +55,8 @@ struct alignas(64) RankRec {
   std::atomic<int64_t> stop;               // worker has finished (seq of its last push)
   std::atomic<int64_t> heartbeat_ns;
   std::atomic<int64_t> incl_seq;           // newest own message reflected in the published params
+  std::atomic<int64_t> push_flag[kSlots];  // 1: the slot's step left some parameters without a gradient
+  std::atomic<int64_t> reading;            // version whose publish buffer this rank is copying (-1 none)
 };
 
 struct alignas(64) Header {
@@ -65,7 +73,7 @@ struct alignas(64) Header {
 
 enum Field : int {
   PUSH_SEQ = 0, ACK_SEQ = 1, PUSH_VER = 2, APPLIED_VER = 3, STOP = 4, HEARTBEAT = 5, INCL_SEQ = 6,
-  PUB_VER = 10, PS_STOP = 11, ERROR = 12, DROPS = 13, UPDATES = 14, BUF_VER = 15
+  PUSH_FLAG = 7, READING = 8, PUB_VER = 10, PS_STOP = 11, ERROR = 12, DROPS = 13, UPDATES = 14, BUF_VER = 15
 };
 
 static int64_t now_ns() {
@@ -92,6 +100,7 @@ class ControlBlock {
       std::memset(p, 0, sizeof(Header));
       h_->world = world;
       for (int b = 0; b <= kPub; ++b) h_->buf_ver[b].store(-1);
+      for (int r = 0; r < kMaxRanks; ++r) h_->rank[r].reading.store(-1);
       h_->pub_ver.store(-1);
       std::atomic_thread_fence(std::memory_order_release);
       h_->magic = kMagic;
@@ -103,8 +112,28 @@ class ControlBlock {
     }
   }
   ~ControlBlock() {
+    if (dev_) hipHostUnregister(h_);
     if (h_) munmap(h_, sizeof(Header));
   }
+
+  // Register the mapping with HIP so doorbell kernels can store into it.  Returns false (and
+  // keeps the host-callback doorbells) if the runtime refuses.
+  bool enable_device_doorbells() {
+    if (dev_) return true;
+    if (hipHostRegister(h_, sizeof(Header), hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h_, 0) != hipSuccess || d == nullptr) {
+      (void)hipGetLastError();
+      hipHostUnregister(h_);
+      return false;
+    }
+    dev_ = reinterpret_cast<char*>(d);
+    return true;
+  }
+  std::string bell_mode() const { return dev_ ? "device" : "host"; }
 
   void unlink() { shm_unlink(name_.c_str()); }
 
@@ -117,6 +146,8 @@ class ControlBlock {
       case STOP: return &rec(idx).stop;
       case HEARTBEAT: return &rec(idx).heartbeat_ns;
       case INCL_SEQ: return &rec(idx).incl_seq;
+      case PUSH_FLAG: return &rec(idx / kSlots).push_flag[idx % kSlots];
+      case READING: return &rec(idx).reading;
       case PUB_VER: return &h_->pub_ver;
       case PS_STOP: return &h_->ps_stop;
       case ERROR: return &h_->error;
@@ -129,8 +160,31 @@ class ControlBlock {
     throw std::out_of_range("unknown control field");
   }
 
-  int64_t load(int field, int idx) { return word(field, idx)->load(std::memory_order_acquire); }
-  void store(int field, int idx, int64_t v) { word(field, idx)->store(v, std::memory_order_release); }
+  // seq_cst: the reader/writer handshake on publish buffers (reading vs buf_ver) is Dekker-style
+  int64_t load(int field, int idx) { return word(field, idx)->load(std::memory_order_seq_cst); }
+  void store(int field, int idx, int64_t v) { word(field, idx)->store(v, std::memory_order_seq_cst); }
+
+  // Block (GIL released) until no rank is reading the publish buffer that holds version v.
+  bool wait_no_reader(int64_t v, int64_t timeout_us) {
+    py::gil_scoped_release nogil;
+    const int64_t deadline = now_ns() + timeout_us * 1000;
+    int spins = 0;
+    for (;;) {
+      bool busy = false;
+      for (int r = 0; r < (int)h_->world; ++r)
+        if (h_->rank[r].reading.load(std::memory_order_seq_cst) == v) busy = true;
+      if (!busy) return true;
+      if (h_->error.load(std::memory_order_relaxed) || now_ns() >= deadline) return false;
+      if (++spins < 2000) {
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+      } else {
+        struct timespec ts{0, 20000};
+        nanosleep(&ts, nullptr);
+      }
+    }
+  }
   int64_t fetch_add(int field, int idx, int64_t v) { return word(field, idx)->fetch_add(v, std::memory_order_acq_rel); }
 
   // Block (GIL released) until any rank's push_seq exceeds seen[rank] or PS_STOP / timeout.
@@ -178,36 +232,61 @@ class ControlBlock {
   }
 
   struct StorePayload {
-    std::atomic<int64_t>* w;
-    int64_t v;
-    std::atomic<int64_t>* w2;  // optional second word, stored after the first
-    int64_t v2;
+    std::atomic<int64_t>* w[kMaxBell];
+    int64_t v[kMaxBell];
+    int n;
   };
   static void store_cb(void* arg) {
     auto* p = reinterpret_cast<StorePayload*>(arg);
-    p->w->store(p->v, std::memory_order_release);
-    if (p->w2) p->w2->store(p->v2, std::memory_order_release);
+    for (int i = 0; i < p->n; ++i) p->w[i]->store(p->v[i], std::memory_order_release);
     delete p;
   }
 
-  // Stream-ordered doorbell: runs after every earlier operation on `stream` has completed.
-  void enqueue_store(uint64_t stream, int field, int idx, int64_t value) {
-    auto* p = new StorePayload{word(field, idx), value, nullptr, 0};
-    hipError_t e = hipLaunchHostFunc(reinterpret_cast<hipStream_t>(stream), &ControlBlock::store_cb, p);
+  // Stream-ordered doorbell: stores (field, idx, value) triples, in order, after every earlier
+  // operation on `stream` has completed.
+  // `srcs` (device doorbells only): per word, a device address whose int64 value is stored
+  // instead of the immediate (0 = immediate), e.g. the parameter version the GPU adopted.
+  void enqueue(uint64_t stream, const std::vector<std::tuple<int, int, int64_t>>& words,
+               const std::vector<int64_t>& srcs = {}) {
+    if (words.empty()) return;
+    if ((int)words.size() > kMaxBell) throw std::runtime_error("too many words for one doorbell");
+    auto s = reinterpret_cast<hipStream_t>(stream);
+    if (!srcs.empty() && !dev_) throw std::runtime_error("indirect doorbell values need device doorbells");
+    if (dev_) {
+      DoorbellArgs a{};
+      a.n = (int)words.size();
+      for (int i = 0; i < a.n; ++i) {
+        a.w[i] = dev_word(std::get<0>(words[i]), std::get<1>(words[i]));
+        a.v[i] = std::get<2>(words[i]);
+        a.src[i] = i < (int)srcs.size() ? reinterpret_cast<const int64_t*>(srcs[i]) : nullptr;
+      }
+      hipError_t e = launch_doorbell(s, a);
+      if (e != hipSuccess) throw std::runtime_error(std::string("doorbell launch failed: ") + hipGetErrorString(e));
+      return;
+    }
+    auto* p = new StorePayload{};
+    p->n = (int)words.size();
+    for (int i = 0; i < p->n; ++i) {
+      p->w[i] = word(std::get<0>(words[i]), std::get<1>(words[i]));
+      p->v[i] = std::get<2>(words[i]);
+    }
+    hipError_t e = hipLaunchHostFunc(s, &ControlBlock::store_cb, p);
     if (e != hipSuccess) {
       delete p;
       throw std::runtime_error(std::string("hipLaunchHostFunc failed: ") + hipGetErrorString(e));
     }
   }
 
-  // Two ordered doorbells in one callback (e.g. slot version, then the sequence word).
+  int64_t* dev_word(int field, int idx) {
+    if (!dev_) return nullptr;
+    auto* hw = word(field, idx);
+    return reinterpret_cast<int64_t*>(dev_ + (reinterpret_cast<char*>(hw) - reinterpret_cast<char*>(h_)));
+  }
+  int64_t device_addr(int field, int idx) { return reinterpret_cast<int64_t>(dev_word(field, idx)); }
+
+  void enqueue_store(uint64_t stream, int field, int idx, int64_t value) { enqueue(stream, {{field, idx, value}}); }
   void enqueue_store2(uint64_t stream, int f1, int i1, int64_t v1, int f2, int i2, int64_t v2) {
-    auto* p = new StorePayload{word(f1, i1), v1, word(f2, i2), v2};
-    hipError_t e = hipLaunchHostFunc(reinterpret_cast<hipStream_t>(stream), &ControlBlock::store_cb, p);
-    if (e != hipSuccess) {
-      delete p;
-      throw std::runtime_error(std::string("hipLaunchHostFunc failed: ") + hipGetErrorString(e));
-    }
+    enqueue(stream, {{f1, i1, v1}, {f2, i2, v2}});
   }
 
   void heartbeat(int rank) { rec(rank).heartbeat_ns.store(now_ns(), std::memory_order_relaxed); }
@@ -223,6 +302,7 @@ class ControlBlock {
   std::string name_;
   bool create_;
   Header* h_ = nullptr;
+  char* dev_ = nullptr;  // device view of h_ (registered), or null for host-callback doorbells
 };
 
 void bind_control(py::module& m) {
@@ -234,8 +314,14 @@ void bind_control(py::module& m) {
       .def("fetch_add", &ControlBlock::fetch_add)
       .def("wait_any", &ControlBlock::wait_any)
       .def("wait_ge", &ControlBlock::wait_ge)
+      .def("enqueue", &ControlBlock::enqueue, py::arg("stream"), py::arg("words"),
+           py::arg("srcs") = std::vector<int64_t>{})
+      .def("device_addr", &ControlBlock::device_addr)
       .def("enqueue_store", &ControlBlock::enqueue_store)
       .def("enqueue_store2", &ControlBlock::enqueue_store2)
+      .def("enable_device_doorbells", &ControlBlock::enable_device_doorbells)
+      .def_property_readonly("bell_mode", &ControlBlock::bell_mode)
+      .def("wait_no_reader", &ControlBlock::wait_no_reader)
       .def("heartbeat", &ControlBlock::heartbeat)
       .def_property_readonly("world", &ControlBlock::world)
       .def_property_readonly_static("SLOTS", [](py::object) { return kSlots; })
@@ -247,6 +333,8 @@ void bind_control(py::module& m) {
   m.attr("F_STOP") = (int)STOP;
   m.attr("F_HEARTBEAT") = (int)HEARTBEAT;
   m.attr("F_INCL_SEQ") = (int)INCL_SEQ;
+  m.attr("F_PUSH_FLAG") = (int)PUSH_FLAG;
+  m.attr("F_READING") = (int)READING;
   m.attr("F_PUB_VER") = (int)PUB_VER;
   m.attr("F_PS_STOP") = (int)PS_STOP;
   m.attr("F_ERROR") = (int)ERROR;

@@ -1,0 +1,119 @@
+// hipps runtime — GPU-time parameter pull for the asynchronous PS (AsySG-InCon read).
+//
+// README.md:63 `irequest_params()`: a worker adopts whatever parameters the PS has published
+// when it asks.  Round 1 asked on the HOST: the version was chosen when Python reached
+// irequest_params(), which runs up to a step ahead of the GPU, so a worker trained on params
+// ~2 updates older than what was already published by the time its forward actually ran.
+// Here the choice is made by the GPU, in stream order, right before the next forward:
+//
+//   k_pull_select (1 wave)  v = pub_ver; reading[rank] = v; re-check buf_ver[v % NPUB] == v
+//                           (Dekker handshake with the PS, which sets buf_ver = -1 and then waits
+//                           for reading != old version before rewriting a buffer); sel[0] = v or
+//                           -1 when nothing newer than the adopted version sel[1] exists
+//   k_pull_copy  (grid)     params <- publish buffer of sel[0] (fp32 copy or bf16 -> fp32),
+//                           read through the IPC mapping (local HBM on the PS rank, xGMI on others)
+//   k_pull_done  (1 wave)   reading[rank] = -1; sel[1] = v; applied[rank] = v;
+//                           ring[slot] = adopted version -- the version the NEXT step's gradient is
+//                           computed on, which its push doorbell reads indirectly
+//
+// Control words live in the registered shared-memory control block (system-scope atomics);
+// sel / ring are a small device tensor owned by the worker.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include "common.h"
+
+namespace hipps {
+namespace rt {
+
+struct PullWords {
+  int64_t* pub_ver;
+  int64_t* buf_ver;  // [npub]
+  int64_t* reading;
+  int64_t* applied;
+};
+
+__device__ __forceinline__ int64_t ld_sys(const int64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(int64_t* p, int64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void k_pull_select(PullWords w, int64_t* __restrict__ sel, int npub, int tries) {
+  if (threadIdx.x != 0) return;
+  const int64_t cur = sel[1];
+  int64_t out = -1;
+  for (int t = 0; t < tries; ++t) {  // bounded: a publish race only costs this step's adoption
+    const int64_t v = ld_sys(w.pub_ver);
+    if (v <= cur) break;
+    st_sys(w.reading, v);
+    if (ld_sys(w.buf_ver + (v % npub)) == v) {
+      out = v;
+      break;
+    }
+    st_sys(w.reading, -1);
+  }
+  sel[0] = out;
+}
+
+template <typename Tin>
+__global__ __launch_bounds__(kBlock) void k_pull_copy(const int64_t* __restrict__ sel, const uint8_t* __restrict__ pub,
+                                                      int64_t stride, int npub, float* __restrict__ dst, int64_t n) {
+  const int64_t v = sel[0];
+  if (v < 0) return;
+  // system-scope acquire: drop any stale copy of the (remote) publish buffer before reading it
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const Tin* src = reinterpret_cast<const Tin*>(pub + (v % npub) * stride);
+  const int64_t nv = n >> 2, step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += step)
+    Vec4<float>::store(dst, i << 2, Vec4<Tin>::load(src, i << 2));
+  if (blockIdx.x == 0)
+    for (int64_t i = (nv << 2) + threadIdx.x; i < n; i += blockDim.x) dst[i] = Vec4<Tin>::load1(src, i);
+}
+
+__global__ __launch_bounds__(64) void k_pull_done(PullWords w, int64_t* __restrict__ sel, int ring_slot) {
+  if (threadIdx.x != 0) return;
+  const int64_t v = sel[0];
+  if (v >= 0) {
+    st_sys(w.reading, -1);
+    sel[1] = v;
+    st_sys(w.applied, v);
+  }
+  sel[2 + ring_slot] = sel[1];
+}
+
+static PullWords words_of(int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied) {
+  TORCH_CHECK(pub_ver && buf_ver && reading && applied, "pull needs device-registered control words");
+  return PullWords{reinterpret_cast<int64_t*>(pub_ver), reinterpret_cast<int64_t*>(buf_ver),
+                   reinterpret_cast<int64_t*>(reading), reinterpret_cast<int64_t*>(applied)};
+}
+
+// One adoption: select + copy + done on the current stream.  sel: int64 device tensor
+// [2 + ring]; pub: the uint8 view of publish buffer 0 .. npub-1 (stride bytes apart).
+void pull_params(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, at::Tensor pub,
+                 int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t ring_slot, int64_t tries) {
+  TORCH_CHECK(sel.is_cuda() && sel.scalar_type() == at::kLong && sel.is_contiguous(), "sel must be int64 device");
+  TORCH_CHECK(ring_slot >= 0 && ring_slot + 2 < sel.numel(), "ring slot out of range");
+  TORCH_CHECK(pub.is_cuda() && pub.scalar_type() == at::kByte, "pub must be a uint8 device view");
+  TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kFloat && dst.is_contiguous(), "dst must be f32 device");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(pub.data_ptr()) % 16 == 0 && stride % 16 == 0, "pub must be 16B aligned");
+  const int64_t n = dst.numel();
+  TORCH_CHECK(npub >= 1 && pub.numel() >= (npub - 1) * stride + n * (bf16 ? 2 : 4), "publish view too small");
+  PullWords w = words_of(pub_ver, buf_ver, reading, applied);
+  auto stream = c10::hip::getCurrentHIPStream();
+  int64_t* s = sel.data_ptr<int64_t>();
+  hipLaunchKernelGGL(k_pull_select, dim3(1), dim3(64), 0, stream, w, s, (int)npub, (int)tries);
+  const int grid = grid_for(n >> 2);
+  if (bf16)
+    hipLaunchKernelGGL(k_pull_copy<uint16_t>, grid, kBlock, 0, stream, s, pub.data_ptr<uint8_t>(), stride, (int)npub,
+                       dst.data_ptr<float>(), n);
+  else
+    hipLaunchKernelGGL(k_pull_copy<float>, grid, kBlock, 0, stream, s, pub.data_ptr<uint8_t>(), stride, (int)npub,
+                       dst.data_ptr<float>(), n);
+  hipLaunchKernelGGL(k_pull_done, dim3(1), dim3(64), 0, stream, w, s, (int)ring_slot);
+}
+
+}  // namespace rt
+}  // namespace hipps

@@ -39,26 +39,30 @@ def convert(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0):
 def sgd_step(grads: Sequence[torch.Tensor], p: torch.Tensor, buf: Optional[torch.Tensor] = None,
              pub: Optional[torch.Tensor] = None, zero_src: bool = False, gscale: float = 1.0, lr: float = 0.0,
              weight_decay: float = 0.0, momentum: float = 0.0, dampening: float = 0.0, nesterov: bool = False,
-             first: bool = False):
-    """Fused decode + sum_W + SGD (reference ps.py:197-214) + optional publish copy."""
+             first: bool = False, mask: Optional[torch.Tensor] = None):
+    """Fused decode + sum_W + SGD (reference ps.py:197-214) + optional publish copy.  ``mask``
+    (uint8, one byte per 16 elements) leaves chunks with a 0 byte untouched (params without a
+    gradient, ps.py:178-179)."""
     if _dev(p):
         return native().sgd_step(list(grads), float(gscale), p, buf, pub, bool(zero_src), float(lr),
-                                 float(weight_decay), float(momentum), float(dampening), bool(nesterov), bool(first))
+                                 float(weight_decay), float(momentum), float(dampening), bool(nesterov), bool(first),
+                                 mask)
     return ref.sgd_step(list(grads), p, buf, pub, zero_src, gscale, lr, weight_decay, momentum, dampening,
-                        nesterov, first)
+                        nesterov, first, mask)
 
 
 def adam_step(grads: Sequence[torch.Tensor], p: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor,
               max_exp_avg_sq: Optional[torch.Tensor] = None, pub: Optional[torch.Tensor] = None,
               zero_src: bool = False, gscale: float = 1.0, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-              weight_decay: float = 0.0, step: int = 1, amsgrad: bool = False, torch_mode: bool = False):
+              weight_decay: float = 0.0, step: int = 1, amsgrad: bool = False, torch_mode: bool = False,
+              mask: Optional[torch.Tensor] = None):
     """Fused decode + sum_W + Adam (reference ps.py:217-261 eps placement unless torch_mode)."""
     if _dev(p):
         return native().adam_step(list(grads), float(gscale), p, exp_avg, exp_avg_sq, max_exp_avg_sq, pub,
                                   bool(zero_src), float(lr), float(betas[0]), float(betas[1]), float(eps),
-                                  float(weight_decay), int(step), bool(amsgrad), bool(torch_mode))
+                                  float(weight_decay), int(step), bool(amsgrad), bool(torch_mode), mask)
     return ref.adam_step(list(grads), p, exp_avg, exp_avg_sq, max_exp_avg_sq, pub, zero_src, gscale, lr, betas, eps,
-                         weight_decay, step, amsgrad, torch_mode)
+                         weight_decay, step, amsgrad, torch_mode, mask)
 
 
 def q8_encode(x, resid, q, scales, stochastic: bool = False, seed: int = 0):

@@ -42,9 +42,32 @@ def convert(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0):
     dst.copy_(x.to(dst.dtype))
 
 
+def _elem_mask(mask, n):
+    """Chunk mask (one byte per 16 elements) -> per-element bool."""
+    return mask.bool().repeat_interleave(16)[:n]
+
+
+def _masked(mask, n, fn, *bufs):
+    """Run ``fn`` and restore the elements of ``bufs`` whose chunk mask byte is 0."""
+    if mask is None:
+        return fn()
+    keep = ~_elem_mask(mask, n)
+    saved = [b[keep].clone() if b is not None else None for b in bufs]
+    fn()
+    for b, s in zip(bufs, saved):
+        if b is not None:
+            b[keep] = s
+
+
 def sgd_step(grads, p, buf=None, pub=None, zero_src=False, gscale=1.0, lr=0.0, weight_decay=0.0, momentum=0.0,
-             dampening=0.0, nesterov=False, first=False):
-    """Reference SGD (ps.py:197-214) on flat fp32 buffers."""
+             dampening=0.0, nesterov=False, first=False, mask=None):
+    """Reference SGD (ps.py:197-214) on flat fp32 buffers; masked chunks are left untouched."""
+    if mask is not None:
+        _masked(mask, p.numel(), lambda: sgd_step(grads, p, buf, None, zero_src, gscale, lr, weight_decay, momentum,
+                                                  dampening, nesterov, first), p, buf)
+        if pub is not None:
+            pub.copy_(p.to(pub.dtype))
+        return
     d = _f32(grads[0]).clone()
     for g in grads[1:]:
         d += _f32(g)
@@ -66,8 +89,15 @@ def sgd_step(grads, p, buf=None, pub=None, zero_src=False, gscale=1.0, lr=0.0, w
 
 
 def adam_step(grads, p, exp_avg, exp_avg_sq, max_exp_avg_sq=None, pub=None, zero_src=False, gscale=1.0, lr=1e-3,
-              betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, step=1, amsgrad=False, torch_mode=False):
+              betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, step=1, amsgrad=False, torch_mode=False, mask=None):
     """Reference Adam (ps.py:217-261): denom = sqrt(v) + eps; step = lr*sqrt(bc2)/bc1."""
+    if mask is not None:
+        _masked(mask, p.numel(), lambda: adam_step(grads, p, exp_avg, exp_avg_sq, max_exp_avg_sq, None, zero_src,
+                                                   gscale, lr, betas, eps, weight_decay, step, amsgrad, torch_mode),
+                p, exp_avg, exp_avg_sq, max_exp_avg_sq)
+        if pub is not None:
+            pub.copy_(p.to(pub.dtype))
+        return
     g = _f32(grads[0]).clone()
     for x in grads[1:]:
         g += _f32(x)

@@ -69,12 +69,22 @@ class MPI_PS(torch.optim.Optimizer):
             self.code = self.codec
         # names: named_params order (the reference sets param.name, ps.py:63-64)
         self.param_names: Dict[int, str] = {id(p): n for n, p in named_params}
-        groups = [g["params"] for g in self.param_groups]
-        seen = {id(p) for g in groups for p in g}
+        seen = {id(p) for g in self.param_groups for p in g["params"]}
         missing = [n for n, p in named_params if id(p) not in seen]
         if missing:
             raise ValueError(f"named parameters not in the optimizer's param groups: {missing[:5]}")
-        dev = groups[0][0].device
+        names = [self.param_names.get(id(p)) for g in self.param_groups for p in g["params"]]
+        names = [n for n in names if n is not None]
+        if len(names) != len(set(names)):  # ps.py:150-153
+            repeated = sorted({x for x in names if names.count(x) > 1})
+            raise ValueError(f"names not unique. Repeated names = {repeated}")
+        # frozen parameters (requires_grad=False) are neither hooked, exchanged nor updated; they
+        # keep their own storage (torch.optim skips them the same way: their .grad stays None)
+        groups = [[p for p in g["params"] if p.requires_grad] for g in self.param_groups]
+        self.frozen = [p for g in self.param_groups for p in g["params"] if not p.requires_grad]
+        if not any(groups):
+            raise ValueError("no trainable parameters (every parameter has requires_grad=False)")
+        dev = next(p for g in groups for p in g).device
         self.world = hdist.current()
         self.store = FlatStore(groups, self.param_names, device=dev)
         self._init_state()
@@ -129,17 +139,19 @@ class MPI_PS(torch.optim.Optimizer):
         return self.flat_state[key]
 
     def _update_flat(self, sources: List[torch.Tensor], target: torch.Tensor, gscale: float, zero_src: bool = False,
-                     pub: Optional[torch.Tensor] = None):
-        """Apply the optimizer to flat ``target`` from flat gradient ``sources`` (summed)."""
+                     pub: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None):
+        """Apply the optimizer to flat ``target`` from flat gradient ``sources`` (summed).
+        ``mask`` (uint8 per 16-element chunk, FlatStore.chunk_mask) skips the parameters that
+        produced no gradient this step, like ``if p.grad is None: continue`` (ps.py:178-179)."""
         for gi, group in enumerate(self.param_groups):
             a, b = self.store.group_ranges[gi]
             if b == a:
                 continue
             self._group_steps[gi] += 1
             self._update_group(gi, group, [s[a:b] for s in sources], target[a:b], gscale, zero_src,
-                               None if pub is None else pub[a:b])
+                               None if pub is None else pub[a:b], None if mask is None else mask[a // 16:b // 16])
 
-    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub):
+    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub, mask=None):
         raise NotImplementedError
 
     # ------------------------------------------------------------------ public API
@@ -159,11 +171,31 @@ class MPI_PS(torch.optim.Optimizer):
             self._metrics.write(self.steps, data)
         return loss, data
 
-    def zero_grad(self, set_to_none: bool = False):
-        """Zero the flat gradient buffer (grads stay views; set_to_none is ignored on purpose)."""
-        if hasattr(self, "engine"):
-            self.engine.before_zero_grad() if hasattr(self.engine, "before_zero_grad") else None
-        self.store.zero_grad()
+    def zero_grad(self, set_to_none: bool = True):
+        """torch semantics: ``p.grad = None`` by default; a parameter whose gradient is still None
+        at step() is skipped (ps.py:178-179).  ``set_to_none=False`` zero-fills the flat gradient
+        views instead (every parameter then counts as having a gradient)."""
+        if getattr(self, "engine", None) is not None and hasattr(self.engine, "before_zero_grad"):
+            self.engine.before_zero_grad()
+        self.store.zero_grad(set_to_none)
+
+    def no_sync(self):
+        """Gradient accumulation over several backward() calls (like DDP's ``no_sync``): inside
+        the context the hooks only record which parameters got a gradient; the encode and the
+        exchange run for the summed gradients at the next backward() outside it / at step()."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def ctx():
+            eng = self.engine
+            prev = eng.accumulating
+            eng.accumulating = True
+            try:
+                yield
+            finally:
+                eng.accumulating = prev
+
+        return ctx()
 
     def irequest_params(self, **kw):
         """AsySG-InCon parameter refresh (README.md:63): adopt the newest published params that
@@ -230,15 +262,19 @@ class SGD(MPI_PS, torch.optim.SGD):
 
     optim = "sgd"
 
-    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub):
+    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub, mask=None):
         mom = group.get("momentum", 0) or 0
         a, b = self.store.group_ranges[gi]
         buf = self._ensure_state("momentum_buffer")[a:b] if mom else None
-        first = mom and not self._momentum_started(gi)
+        # buf = d_p on the first step (ps.py:203-205); with a mask, later-starting params get
+        # buf = (1-dampening)*d_p from the zero-initialised buffer (identical for dampening=0)
+        first = mom and mask is None and not self._momentum_started(gi)
+        if mom and mask is not None:
+            self._momentum_started(gi)
         ops.sgd_step(srcs, target, buf, pub, zero_src, gscale, lr=group["lr"],
                      weight_decay=group.get("weight_decay", 0) or 0, momentum=mom,
                      dampening=group.get("dampening", 0) or 0, nesterov=bool(group.get("nesterov", False)),
-                     first=bool(first))
+                     first=bool(first), mask=mask)
 
     def _momentum_started(self, gi):
         started = getattr(self, "_mom_started", None)
@@ -261,7 +297,7 @@ class Adam(MPI_PS, torch.optim.Adam):
 
     optim = "adam"
 
-    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub):
+    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub, mask=None):
         a, b = self.store.group_ranges[gi]
         m = self._ensure_state("exp_avg")[a:b]
         v = self._ensure_state("exp_avg_sq")[a:b]
@@ -273,4 +309,4 @@ class Adam(MPI_PS, torch.optim.Adam):
                 self.state[s.param]["step"] = step
         ops.adam_step(srcs, target, m, v, vm, pub, zero_src, gscale, lr=group["lr"], betas=group["betas"],
                       eps=group["eps"], weight_decay=group.get("weight_decay", 0) or 0, step=step, amsgrad=ams,
-                      torch_mode=self.cfg.adam_variant == "torch")
+                      torch_mode=self.cfg.adam_variant == "torch", mask=mask)

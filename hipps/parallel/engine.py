@@ -39,13 +39,23 @@ class Engine:
         self.plan = BucketPlan(store, codec, int(cfg.bucket_mb * (1 << 20)), guard=cfg.debug_canary)
         self.cuda = store.device.type == "cuda"
         self.tracer = StepTracer(cfg.trace, self.cuda)
-        # zero-initialised: the 16-element alignment gaps between parameters are never written
-        self.wire = torch.zeros(self.plan.wire_nbytes, dtype=torch.uint8, device=store.device)
+        # zero-initialised: the 16-element alignment gaps between parameters are never written.
+        # The tail after the bucket messages carries this rank's per-parameter gradient-presence
+        # bytes in the sync modes (one byte per slot).
+        self.pres_off = self.plan.wire_nbytes
+        self.pres_bytes = (len(store.slots) + 15) // 16 * 16
+        self.wire_total = self.pres_off + self.pres_bytes
+        self.wire = torch.zeros(self.wire_total, dtype=torch.uint8, device=store.device)
         self.plan.fill_guards(self.wire)
         self.codec_state = [codec.init_state(b.numel, store.device) for b in self.plan.buckets]
         self.comm_stream = torch.cuda.Stream(device=store.device) if self.cuda else None
         self._encoded = [False] * len(self.plan.buckets)
         self._bucket_count = [0] * len(self.plan.buckets)
+        self._fired = bytearray(len(store.slots))  # slot's hook fired since the last step
+        self._late = set()  # buckets that received a gradient after they were encoded
+        self.accumulating = False  # MPI_PS.no_sync(): hooks only record presence
+        self.step_all_present = True
+        self.step_present = bytes(len(store.slots))
         self._hooks = []
         self.steps = 0
         self._order_log: List[str] = []
@@ -56,8 +66,7 @@ class Engine:
         if self.grad_mode == "gather":
             self._build_gather_plan()
             store.set_grad_mode("gather")
-        if cfg.overlap:
-            self._register_hooks()
+        self._register_hooks()
 
     supports_gather = True
     GATHER_CHUNK = 8192
@@ -85,12 +94,29 @@ class Engine:
 
     # ------------------------------------------------------------------ hooks / encode
     def _register_hooks(self):
+        """One post-accumulate-grad hook per parameter: records that the parameter got a gradient
+        this step and, with ``cfg.overlap``, encodes a bucket on the side stream as soon as all of
+        its parameters have one (the reference submits one encode task per tensor, ps.py:98-101).
+        A gradient that lands in an already-encoded bucket (a second backward() before step())
+        marks the bucket for re-encoding at step()."""
+        overlap = self.cfg.overlap
         for i, s in enumerate(self.store.slots):
             bi = self.plan.slot_bucket[i]
+            target = len(self.plan.buckets[bi].slot_ids)
 
-            def hook(p, bi=bi):
-                self._bucket_count[bi] += 1
-                if self._bucket_count[bi] == len(self.plan.buckets[bi].slot_ids) and not self._encoded[bi]:
+            def hook(p, i=i, bi=bi, target=target):
+                first = not self._fired[i]
+                self._fired[i] = 1
+                if self.grad_mode == "flat":
+                    self.store.attach_slot(i)  # the bucket encode reads the flat view
+                if self.accumulating:
+                    return
+                if self._encoded[bi]:
+                    self._late.add(bi)
+                    return
+                if first:
+                    self._bucket_count[bi] += 1
+                if overlap and self._bucket_count[bi] == target:
                     self.encode_bucket(bi)
 
             self._hooks.append(s.param.register_post_accumulate_grad_hook(hook))
@@ -100,12 +126,12 @@ class Engine:
             h.remove()
         self._hooks = []
 
-    def _gather_bucket(self, bi: int, views):
+    def _gather_bucket(self, bi: int, views, to_flat: bool = False):
         """Multi-tensor gather of this bucket's autograd gradients (on the comm stream)."""
         from hipps.ops._native import native
 
         b = self.plan.buckets[bi]
-        dense = self.codec.fusable  # per-bucket image: guards sit after the layout, not inside
+        dense = self.codec.fusable and not to_flat  # guards sit after the layout, not inside
         dst = views["x"] if dense else self.store.grad[b.lo:b.hi]
         C = native()
         for gids, table in self._gplan[bi]:
@@ -156,17 +182,58 @@ class Engine:
                 ids = bad.nonzero().view(-1).tolist()
                 raise RuntimeError(f"wire canary overwritten ({what}, message {r}) in buckets {ids}")
 
+    def _stateful_codec(self) -> bool:
+        return any("resid" in st for st in self.codec_state)
+
     def encode_all(self):
-        """Encode every bucket not yet handled by a hook; returns host seconds spent."""
+        """Encode every bucket not yet handled by a hook (and re-encode buckets that received
+        more gradient after their hook-time encode); returns host seconds spent.  Also latches
+        this step's gradient-presence vector (``step_present`` / ``step_all_present``)."""
         t = time.perf_counter()
         if self.grad_mode == "flat":
             self.store.attach_grads()
+        pres = bytes(self.store.presence())
+        self.step_present = pres
+        self.step_all_present = all(pres)
+        if not self.step_all_present and self.cfg.require_all_grads:
+            names = [s.name for s, f in zip(self.store.slots, pres) if not f]
+            # the reference requires a gradient for every parameter (ps.py:118-119)
+            raise ValueError(f"len(set(names)) != len(params): no gradient for {names[:8]}"
+                             f"{' ...' if len(names) > 8 else ''}")
+        if self._late and self._stateful_codec():
+            raise RuntimeError("a gradient arrived after its bucket was encoded (backward() called twice before "
+                               "step()) with an error-feedback codec: wrap the earlier micro-batches in "
+                               "opt.no_sync()")
         for bi in self.plan.ready_order:
-            if not self._encoded[bi]:
+            if not self._encoded[bi] or bi in self._late:
                 self.encode_bucket(bi)
         self._encoded = [False] * len(self._encoded)
         self._bucket_count = [0] * len(self._bucket_count)
+        self._late.clear()
+        self._fired = bytearray(len(self._fired))
         return time.perf_counter() - t
+
+    def presence_tensor(self) -> torch.Tensor:
+        """This step's per-slot presence as a uint8 tensor on the engine device (async H2D)."""
+        t = torch.frombuffer(bytearray(self.step_present), dtype=torch.uint8)
+        if self.cuda:
+            t = t.pin_memory().to(self.store.device, non_blocking=True)
+        return t
+
+    def local_mask(self) -> Optional[torch.Tensor]:
+        """Chunk mask from this rank's presence (None when every parameter has a gradient)."""
+        if self.step_all_present or not self.cfg.skip_missing_grads:
+            return None
+        return self.store.chunk_mask(self.presence_tensor())
+
+    def step_metrics(self) -> Dict[str, float]:
+        """The reference's per-step byte accounting (ps.py:135-136): mean encoded message bytes and
+        mean packaged (framed) bytes over this step's messages; ``iallgather_prepare_time`` is the
+        size-round time (ps.py:139-141) -- 0 here because device messages have static sizes."""
+        bs = self.plan.buckets
+        return {"msg_bytes": sum(b.layout.nbytes for b in bs) / len(bs),
+                "packaged_bytes": sum(b.msg_nbytes for b in bs) / len(bs),
+                "iallgather_prepare_time": 0.0}
 
     def _check_order(self):
         """Race detector: every rank must post the same exchange sequence."""
@@ -187,17 +254,37 @@ class Engine:
         return images
 
     def apply(self, wire_msgs: List[torch.Tensor], target: torch.Tensor, pub: Optional[torch.Tensor], gscale: float,
-              scratch: Optional[torch.Tensor] = None):
+              scratch: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None):
         """Decode W wire messages, sum in rank order, apply the optimizer to ``target`` (flat)."""
         if self.plan.dense_ok:
             imgs = [self.plan.dense_image(w) for w in wire_msgs]
-            self.opt._update_flat(imgs, target, gscale, zero_src=False, pub=pub)
+            self.opt._update_flat(imgs, target, gscale, zero_src=False, pub=pub, mask=mask)
         else:
             acc = scratch if scratch is not None else torch.empty_like(self.store.grad)
             for bi, b in enumerate(self.plan.buckets):
                 msgs = [self.plan.views(w, bi) for w in wire_msgs]
                 self.codec.accumulate(msgs, acc[b.lo:b.hi], 1.0, False)
-            self.opt._update_flat([acc], target, gscale, zero_src=False, pub=pub)
+            self.opt._update_flat([acc], target, gscale, zero_src=False, pub=pub, mask=mask)
+
+    def write_presence(self):
+        """Sync modes: put this step's presence bytes in the wire tail (comm stream)."""
+        if not self.cfg.skip_missing_grads:
+            return
+        ns = len(self.store.slots)
+        if self.cuda:
+            with torch.cuda.stream(self.comm_stream):
+                self.wire[self.pres_off:self.pres_off + ns].copy_(self.presence_tensor(), non_blocking=True)
+        else:
+            self.wire[self.pres_off:self.pres_off + ns].copy_(self.presence_tensor())
+
+    def gathered_mask(self, msgs: List[torch.Tensor]) -> Optional[torch.Tensor]:
+        """OR of every rank's presence bytes -> chunk mask (identical on every rank).  All-present
+        steps still pay these two tiny kernels: no host round trip is spent to find out."""
+        if not self.cfg.skip_missing_grads:
+            return None
+        ns = len(self.store.slots)
+        pres = torch.stack([m[self.pres_off:self.pres_off + ns] for m in msgs]).amax(0)
+        return self.store.chunk_mask(pres)
 
     def gscale(self, n: int) -> float:
         return 1.0 / n if self.cfg.average else 1.0
@@ -232,7 +319,6 @@ class LocalEngine(Engine):
     """World size 1: encode (codec round trip, e.g. to study compression) + fused update."""
 
     name = "local"
-    supports_gather = False  # the fused update reads the flat gradient directly
 
     def __init__(self, *a, **k):
         super().__init__(*a, **k)
@@ -240,6 +326,21 @@ class LocalEngine(Engine):
         self._bypass = self.plan.dense_ok and self.codec.lossless
 
     def encode_bucket(self, bi):
+        """Gather mode: one multi-tensor kernel gathers the bucket's gradients into the flat
+        gradient (comm stream), then the codec (if any) encodes from there."""
+        if self.grad_mode == "gather":
+            b = self.plan.buckets[bi]
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.store.device))
+            with torch.cuda.stream(self.comm_stream):
+                self.comm_stream.wait_event(ev)
+                with self.tracer.phase("encode", self.comm_stream):
+                    self._gather_bucket(bi, None, to_flat=True)
+                    if not self._bypass:
+                        self.codec.encode_into(self.store.grad[b.lo:b.hi], self.plan.views(self.wire, bi),
+                                               self.codec_state[bi])
+            self._encoded[bi] = True
+            return
         if self._bypass:  # fp32 identity: the flat grad IS the message
             self._encoded[bi] = True
             return
@@ -249,18 +350,21 @@ class LocalEngine(Engine):
         data = {}
         data["code_wait"] = self.encode_all()
         t = time.perf_counter()
-        if self.cuda and not self._bypass:
+        if self.cuda and (not self._bypass or self.grad_mode == "gather"):
             torch.cuda.current_stream(self.store.device).wait_stream(self.comm_stream)
         if not self._bypass:
             self.verify_guards([self.wire], "encode")
+        mask = self.local_mask()
         with self.tracer.phase("update"):
             if self._bypass:
-                self.opt._update_flat([self.store.grad], self.store.data, 1.0, zero_src=False, pub=None)
+                self.opt._update_flat([self.store.grad], self.store.data, 1.0, zero_src=False, pub=None, mask=mask)
             else:
-                self.apply([self.wire], self.store.data, None, 1.0, self._scratch)
+                self.apply([self.wire], self.store.data, None, 1.0, self._scratch, mask=mask)
         data["optim_step_time"] = time.perf_counter() - t
         data["decode_time"] = 0.0
         data["comm_wait"] = 0.0
+        data["isend_time"] = 0.0
+        data.update(self.step_metrics())
         data.update(self.bytes_per_step())
         data.update(self.tracer.collect())
         self.steps += 1
@@ -276,13 +380,14 @@ class AllGatherEngine(Engine):
     def __init__(self, *a, **k):
         super().__init__(*a, **k)
         W = self.world.size
-        self.gathered = torch.empty(W * self.plan.wire_nbytes, dtype=torch.uint8, device=self.store.device)
+        self.gathered = torch.empty(W * self.wire_total, dtype=torch.uint8, device=self.store.device)
         self._scratch = None if self.plan.dense_ok else torch.empty_like(self.store.grad)
 
     def step(self):
         data = {}
         data["code_wait"] = self.encode_all()
         self._check_order()
+        self.write_presence()
         t = time.perf_counter()
         if self.cuda:
             with torch.cuda.stream(self.comm_stream), self.tracer.phase("comm", self.comm_stream):
@@ -293,13 +398,15 @@ class AllGatherEngine(Engine):
                 all_gather_into(self.gathered, self.wire, self.world)
         data["isend_time"] = data["comm_wait"] = time.perf_counter() - t
         t = time.perf_counter()
-        n = self.plan.wire_nbytes
+        n = self.wire_total
         msgs = [self.gathered[w * n:(w + 1) * n] for w in range(self.world.size)]
         self.verify_guards(msgs, "allgather")
         with self.tracer.phase("update"):
-            self.apply(msgs, self.store.data, None, self.gscale(self.world.size), self._scratch)
+            self.apply(msgs, self.store.data, None, self.gscale(self.world.size), self._scratch,
+                       mask=self.gathered_mask(msgs))
         data["optim_step_time"] = time.perf_counter() - t
         data["decode_time"] = 0.0
+        data.update(self.step_metrics())
         data.update(self.bytes_per_step())
         data["grad_bytes_recv"] = n * self.world.size
         data.update(self.tracer.collect())
@@ -316,8 +423,8 @@ class PSSyncEngine(Engine):
         super().__init__(*a, **k)
         W = self.world.size
         dev = self.store.device
-        self.gathered = (torch.empty(W * self.plan.wire_nbytes, dtype=torch.uint8, device=dev)
-                         if self.world.is_ps else torch.empty(self.plan.wire_nbytes, dtype=torch.uint8, device=dev))
+        self.gathered = (torch.empty(W * self.wire_total, dtype=torch.uint8, device=dev)
+                         if self.world.is_ps else torch.empty(self.wire_total, dtype=torch.uint8, device=dev))
         self._scratch = None if self.plan.dense_ok else torch.empty_like(self.store.grad)
         self.pub = None
         if self.cfg.param_wire == "bf16":
@@ -326,6 +433,7 @@ class PSSyncEngine(Engine):
     def step(self):
         data = {}
         data["code_wait"] = self.encode_all()
+        self.write_presence()
         t = time.perf_counter()
         cs = self.comm_stream
         ctx = torch.cuda.stream(cs) if self.cuda else _null()
@@ -334,14 +442,15 @@ class PSSyncEngine(Engine):
             gather_into(self.gathered if self.world.is_ps else None, self.wire, self.world)
         if self.cuda:
             torch.cuda.current_stream(self.store.device).wait_stream(cs)
-        data["comm_wait"] = time.perf_counter() - t
+        data["comm_wait"] = data["isend_time"] = time.perf_counter() - t
         t = time.perf_counter()
         if self.world.is_ps:
-            n = self.plan.wire_nbytes
+            n = self.wire_total
             msgs = [self.gathered[w * n:(w + 1) * n] for w in range(self.world.size)]
             self.verify_guards(msgs, "gather")
             with self.tracer.phase("update"):
-                self.apply(msgs, self.store.data, self.pub, self.gscale(self.world.size), self._scratch)
+                self.apply(msgs, self.store.data, self.pub, self.gscale(self.world.size), self._scratch,
+                           mask=self.gathered_mask(msgs))
         data["optim_step_time"] = time.perf_counter() - t
         t = time.perf_counter()
         # ibroadcast of the parameters (mpi_comms.py:127-133 / README.md:76)
@@ -355,6 +464,8 @@ class PSSyncEngine(Engine):
             else:
                 broadcast(self.store.data, self.world, 0)
         data["bcast_time"] = time.perf_counter() - t
+        data["decode_time"] = 0.0
+        data.update(self.step_metrics())
         data.update(self.bytes_per_step())
         data.update(self.tracer.collect())
         self.steps += 1

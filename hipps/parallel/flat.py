@@ -76,6 +76,8 @@ class FlatStore:
         self.data = torch.zeros(self.numel, dtype=dtype, device=self.device)
         self.grad = torch.zeros(self.numel, dtype=dtype, device=self.device)
         self.grad_mode = "flat"
+        self._force_present = False
+        self._stale = [False] * len(self.slots)  # flat grad view holds data from an earlier step
         for s in self.slots:
             p = s.param
             if p.dtype != dtype:
@@ -87,7 +89,12 @@ class FlatStore:
             v = self._view(self.data, s, src)
             v.copy_(src)
             p.data = v
-        self.attach_grads()
+            if p.grad is not None:  # keep a gradient the caller already computed
+                g = p.grad
+                p.grad = None
+                gv = self._view(self.grad, s, p.data)
+                gv.copy_(g)
+                p.grad = gv
 
     @staticmethod
     def _view(buf: torch.Tensor, s: Slot, like: torch.Tensor) -> torch.Tensor:
@@ -103,36 +110,61 @@ class FlatStore:
     def set_grad_mode(self, mode: str):
         """'flat': p.grad are views of self.grad; 'gather': autograd owns p.grad (engines gather)."""
         self.grad_mode = mode
-        if mode == "gather":
-            for s in self.slots:
-                s.param.grad = None
-        else:
-            self.attach_grads()
+        for s in self.slots:
+            s.param.grad = None
+
+    def attach_slot(self, i: int):
+        """Flat mode: make ``param.grad`` the flat view, copying a stolen/assigned gradient in."""
+        s = self.slots[i]
+        p = s.param
+        g = p.grad
+        if g is None:
+            return
+        v = self._view(self.grad, s, p.data)
+        if g.data_ptr() != v.data_ptr():
+            v.copy_(g)
+            p.grad = v
 
     def attach_grads(self):
-        """(Re)point every ``param.grad`` at its flat slice, salvaging foreign grads."""
+        """Flat mode, at step time: every present gradient lives in its flat view; the view of a
+        parameter without a gradient (``p.grad is None``) is zeroed so codecs read zeros there."""
         if self.grad_mode == "gather":
             return
-        for s in self.slots:
-            p = s.param
-            v = self._view(self.grad, s, p.data)
-            g = p.grad
-            if g is None or g.data_ptr() != v.data_ptr():
-                if g is not None:
-                    v.copy_(g)
-                p.grad = v
+        for i, s in enumerate(self.slots):
+            if s.param.grad is None:
+                if self._stale[i]:
+                    self.grad[s.offset:s.offset + s.numel].zero_()
+                    self._stale[i] = False
+            else:
+                self.attach_slot(i)
+                self._stale[i] = True
+
+    def presence(self) -> List[bool]:
+        """Per slot: did the parameter get a gradient since the last zero_grad()?  torch
+        semantics -- ``p.grad is not None`` (zero_grad(set_to_none=False) keeps zero grads, which
+        count as present)."""
+        if self._force_present:
+            return [True] * len(self.slots)
+        return [s.param.grad is not None for s in self.slots]
 
     def grads_attached(self) -> bool:
         return all(s.param.grad is not None and s.param.grad.data_ptr() ==
                    self.grad[s.offset:].data_ptr() for s in self.slots)
 
-    def zero_grad(self):
-        if self.grad_mode == "gather":
-            for s in self.slots:  # let autograd steal fresh gradients (no memset, no += kernels)
+    def zero_grad(self, set_to_none: bool = True):
+        """torch semantics: ``set_to_none=True`` (default) -> ``p.grad = None`` (autograd then
+        hands its gradient tensor over without an accumulate kernel, and parameters that get no
+        gradient are skipped by the update); ``False`` -> zero-filled gradients that count as
+        present."""
+        self._force_present = not set_to_none
+        if set_to_none or self.grad_mode == "gather":
+            for s in self.slots:
                 s.param.grad = None
             return
         self.grad.zero_()
-        self.attach_grads()
+        for i, s in enumerate(self.slots):
+            s.param.grad = self._view(self.grad, s, s.param.data)
+            self._stale[i] = False
 
     def enable_bf16_shadow(self):
         """Keep a flat bf16 copy of ``data`` that the hipps conv kernels read (ops.nn.bf16_weight)."""
@@ -196,6 +228,28 @@ class FlatStore:
                 from ..ops._native import native
 
                 native().transpose_cast(self.data, self.tshadow, self._tiles)
+
+    # ---- per-step "parameter has a gradient" masks (ps.py:178-179 skip semantics) -----------
+    @property
+    def nchunks(self) -> int:
+        return self.numel // ALIGN_ELEMS  # numel is a multiple of 16
+
+    def chunk_slots(self) -> torch.Tensor:
+        """Device int32 [nchunks]: the slot owning each 16-element chunk (static, cached)."""
+        cs = getattr(self, "_chunk_slots", None)
+        if cs is None:
+            counts = torch.tensor([(_align(s.offset + s.numel) - s.offset) // ALIGN_ELEMS for s in self.slots],
+                                  dtype=torch.int64)
+            cs = torch.repeat_interleave(torch.arange(len(self.slots), dtype=torch.int32), counts)
+            if cs.numel() < self.nchunks:  # trailing group padding (never updated)
+                cs = torch.cat([cs, cs.new_zeros(self.nchunks - cs.numel())])
+            cs = cs.to(self.device)
+            self._chunk_slots = cs
+        return cs
+
+    def chunk_mask(self, slot_present: torch.Tensor) -> torch.Tensor:
+        """uint8 [nslots] (device) -> uint8 [nchunks] chunk mask for the fused update kernels."""
+        return slot_present.to(self.device, torch.uint8).index_select(0, self.chunk_slots())
 
     def group_slice(self, buf: torch.Tensor, gi: int) -> torch.Tensor:
         a, b = self.group_ranges[gi]

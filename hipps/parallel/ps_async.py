@@ -8,25 +8,34 @@ arrived (inconsistent reads).
 hipps design (one node, one process per GPU, rank 0 = PS *and* worker 0):
 
   data plane   one-sided device copies over xGMI into/out of PS-owned HIP-IPC mailboxes
-               (hipps/csrc/runtime/ipc.cpp): worker -> PS gradient slots (2 per worker), PS ->
-               workers published parameter buffers (3, rotating).  Nothing on the PS posts a
-               receive, so no RCCL kernel ever spins waiting for a straggler.
-  control      POSIX-shm doorbells (hipps/csrc/runtime/control.cpp) = the ANY_SOURCE: the PS
-               thread waits on all workers' push sequence words at once.
+               (hipps/csrc/runtime/ipc.cpp): worker -> PS gradient slots, PS -> workers published
+               parameter buffers (NPUB, rotating).  Nothing on the PS posts a receive, so no RCCL
+               kernel ever spins waiting for a straggler.
+  control      POSIX-shm control block (hipps/csrc/runtime/control.cpp) = the ANY_SOURCE: the PS
+               thread waits on all workers' push sequence words at once.  Doorbells are rung by
+               the GPU (doorbell.hip: one-wavefront kernels storing into the hipHostRegister'ed
+               block with system-scope release), in stream order, no host callbacks.
   PS loop      a thread on rank 0 with its own HIP stream: decode+accumulate each arriving
                message (fused codec kernel), after M messages run the fused optimizer kernel on
                the fp32 master, write the new version into the next publish buffer, then ring
                the version doorbell -- all stream-ordered, the thread never synchronises.
   worker       encode (side stream, overlapped with backward) -> copy into its mailbox slot ->
-               doorbell; ``irequest_params()`` adopts the newest published version if one has
-               landed (a D2D copy on the compute stream) and never waits unless ``max_delay`` asks.
+               doorbell; ``irequest_params()`` enqueues a GPU-time pull (pull.hip): the GPU picks
+               the newest published version when the pull actually runs, right before the next
+               forward, and copies it -- so the staleness is what the hardware timeline implies,
+               not how far the host ran ahead.
+  torn reads   a reader announces the version it copies (READING word, seq_cst handshake with the
+               PS's BUF_VER = -1) and the PS never rewrites a publish buffer while it is read.
   staleness    ConditionalAccumulator semantics (README.md:33-35): a gradient computed on params
-               older than ``version - staleness`` is dropped (staleness=-1 keeps all).
+               older than ``version - staleness`` is dropped (staleness=-1 keeps all);
+               ``staleness_lr`` scales a kept gradient by 1/max(1, staleness) (Zhang et al. 2016,
+               staleness-aware async SGD).
 
 CPU runs use the same protocol with POSIX-shm mailboxes and the torch reference ops.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import secrets
 import threading
@@ -43,6 +52,7 @@ from .dist import barrier
 from .engine import Engine
 
 TIMEOUT_US = int(float(os.environ.get("HIPPS_TIMEOUT_S", "600")) * 1e6)
+RING = 4  # per-step "version this gradient was computed on" ring (device pull mode)
 
 
 def _parse_fault(spec, rank):
@@ -88,13 +98,17 @@ class PSAsyncEngine(Engine):
         self.M = cfg.accumulate if cfg.accumulate > 0 else W
         self.MAXSLOTS = C.ControlBlock.SLOTS  # stride of the per-slot version words
         self.NPUB = C.ControlBlock.NPUB
+        self.timeout_us = int(min(TIMEOUT_US, cfg.comm_timeout_s * 1e6))
         self.pub_dtype = torch.bfloat16 if cfg.param_wire == "bf16" else torch.float32
         esz = torch.empty((), dtype=self.pub_dtype).element_size()
         # messages are BUCKETS, streamed in ready order; a worker's mailbox holds K of them, so the
-        # PS memory is W*K*max_bucket instead of W*2*model (Llama-3-8B: 8x4x512 MB vs 8x2x16 GB)
+        # PS memory is W*K*max_bucket instead of W*2*model (Llama-3-8B: 8x4x512 MB vs 8x2x16 GB).
+        # Each slot ends with the step's per-parameter presence bytes (used when a step left some
+        # parameters without a gradient; PUSH_FLAG says so).
         self.nb = len(self.plan.buckets)
         self.order = list(self.plan.ready_order)
-        self.slot_bytes = _align(max(b.msg_nbytes for b in self.plan.buckets))
+        self.slot_bytes = _align(max(b.msg_nbytes for b in self.plan.buckets)) + _align(self.pres_bytes)
+        self.slot_pres = self.slot_bytes - _align(self.pres_bytes)
         K = cfg.mailbox_slots if cfg.mailbox_slots > 0 else min(
             2 * self.nb, max(2, int(cfg.mailbox_mb * (1 << 20)) // self.slot_bytes))
         self.SLOTS = max(1, min(K, self.MAXSLOTS))
@@ -131,20 +145,39 @@ class PSAsyncEngine(Engine):
             if not self.cuda:
                 self.mailbox.unlink()
         self.mem = self.mailbox.tensor()
+        # GPU-rung doorbells need the control block registered with HIP in this process
+        self.device_bells = bool(self.cuda and self.ctl.enable_device_doorbells())
+        self.pull_mode = cfg.pull
+        if self.pull_mode == "device" and not self.device_bells:
+            self.pull_mode = "prefetch" if self.rank != 0 else "direct"
+        if not self.cuda:
+            self.pull_mode = "direct"
 
         # ---- PS state on rank 0 ------------------------------------------------------------
         self.seq = 0
         self.step_no = 0
         self.local_ver = -1
-        self._stats = {"drops": 0, "staleness_sum": 0, "accumulated": 0}
+        self._stats = {"drops": 0, "staleness_sum": 0, "accumulated": 0, "reader_waits": 0}
         self._err: Optional[str] = None
         self._thread = None
+        self._pause_req = threading.Event()
+        self._paused = threading.Event()
         self.enc_event = torch.cuda.Event() if self.cuda else None
+        if self.cuda:
+            # sel[0] selected, sel[1] adopted, sel[2:2+RING] version each step's gradient uses
+            self._sel = torch.full((2 + RING,), -1, dtype=torch.int64, device=store.device)
+            self._stage = [None, None]
+            self._stage_ev = [None, None]
+            self._stage_k = 0
         if self.rank == 0:
             self.master = store.data.detach().clone()
             self.acc = torch.zeros_like(store.data)
             self.ps_stream = torch.cuda.Stream(device=store.device) if self.cuda else None
             self.ver = 0
+            self._count = 0
+            self._pending_incl: List[tuple] = []
+            self._pres_full = False
+            self._pres_part = None
             self._publish_initial()
             self._thread = threading.Thread(target=self._serve_guard, name="hipps-ps", daemon=True)
             self._thread.start()
@@ -159,8 +192,7 @@ class PSAsyncEngine(Engine):
         """Prove both directions of the one-sided transport before training starts: every rank
         writes a tag into its mailbox slot through the same stream-ordered copy path, the PS checks
         them, and every rank compares its pulled version-0 params with the PS's checksum.  A broken
-        IPC/xGMI mapping raises here on ALL ranks (so callers can fall back) instead of corrupting
-        training later."""
+        IPC/xGMI mapping raises here on ALL ranks instead of corrupting training later."""
         W, dev = self.W, self.store.device
         tag = torch.full((16,), (self.rank * 7 + 3) % 251, dtype=torch.uint8, device=dev)
         dst = self.slot_buf(self.rank, self.SLOTS - 1)[:16]
@@ -216,11 +248,13 @@ class PSAsyncEngine(Engine):
         return self.mem[o:o + self.store.numel * esz].view(self.pub_dtype)
 
     # ------------------------------------------------------------------ PS side
-    def _ring(self, stream, field, idx, value):
+    def _ring(self, stream, words, srcs=None):
+        """Doorbell: [(field, idx, value)] stored in order after ``stream``'s earlier work."""
         if stream is not None:
-            self.ctl.enqueue_store(stream.cuda_stream, field, idx, value)
+            self.ctl.enqueue(stream.cuda_stream, words, srcs or [])
         else:
-            self.ctl.store(field, idx, value)
+            for f, i, v in words:
+                self.ctl.store(f, i, v)
 
     def _publish_initial(self):
         C = self.C
@@ -246,15 +280,14 @@ class PSAsyncEngine(Engine):
 
     def _serve(self):
         """PS loop.  Message s of worker i is bucket order[(s-1) % nb] of that worker's step
-        (s-1)//nb + 1; a step's first bucket carries the parameter version it was computed on.
-        Counting is in whole worker-steps (M per update, README.md:65-73); every bucket gradient
-        that has arrived is applied exactly once."""
+        (s-1)//nb + 1; a step's first bucket carries the parameter version it was computed on,
+        its last bucket whether the step left parameters without a gradient.  Counting is in
+        whole worker-steps (M per update, README.md:65-73); every bucket gradient that has
+        arrived is applied exactly once."""
         C, W, nb = self.C, self.W, self.nb
         seen = [0] * W
         dropping = [False] * W
-        pending_incl: List[tuple] = []  # (rank, last seq of a completed step) since the last update
-        count = 0
-        gscale = 1.0 / self.M if self.cfg.average else 1.0
+        scale = [1.0] * W
         st = self.ps_stream
         with torch.no_grad():
             while True:
@@ -265,10 +298,12 @@ class PSAsyncEngine(Engine):
                         slot = s % self.SLOTS
                         pos = (s - 1) % nb
                         bi = self.order[pos]
+                        vidx = i * self.MAXSLOTS + slot
                         if pos == 0:
-                            pv = self.ctl.load(C.F_PUSH_VER, i * self.MAXSLOTS + slot)
+                            pv = self.ctl.load(C.F_PUSH_VER, vidx)
                             stale = self.ver - pv
                             dropping[i] = 0 <= self.cfg.staleness < stale
+                            scale[i] = 1.0 / max(1, stale) if self.cfg.staleness_lr else 1.0
                             if not dropping[i]:
                                 self._stats["staleness_sum"] += max(0, stale)
                         if not dropping[i]:
@@ -277,41 +312,75 @@ class PSAsyncEngine(Engine):
                                 self._verify_slot(i, slot, bi, s)
                             with self.tracer.phase("ps_accumulate", st):
                                 self.codec.accumulate([self._bucket_msg(bi, self.slot_buf(i, slot))],
-                                                      self.acc[b.lo:b.hi], 1.0, True)
-                        self._ring(st, C.F_ACK_SEQ, i, s)  # stream-ordered: acks stay monotonic
+                                                      self.acc[b.lo:b.hi], scale[i], True)
+                            if pos == nb - 1:
+                                self._note_presence(i, slot, vidx)
+                        self._ring(st, [(C.F_ACK_SEQ, i, s)])  # stream-ordered: acks stay monotonic
                         if pos == nb - 1:
-                            pending_incl.append((i, s))  # a dropped step still counts for max_delay
+                            self._pending_incl.append((i, s))  # a dropped step still counts for max_delay
                             if dropping[i]:
                                 self._stats["drops"] += 1
                                 self.ctl.fetch_add(C.F_DROPS, 0, 1)
                             else:
                                 self._stats["accumulated"] += 1
-                                count += 1
-                                if count >= self.M:
-                                    self._update(pending_incl, gscale)
-                                    pending_incl = []
-                                    count = 0
+                                self._count += 1
+                                if self._count >= self.M:
+                                    self._update(self._pending_incl, self.gscale(self.M))
+                                    self._pending_incl = []
+                                    self._count = 0
                     seen[i] = s_now
+                if self._pause_req.is_set():
+                    self._hold()
                 if self._should_stop(seen):
                     break
+
+    def _note_presence(self, i: int, slot: int, vidx: int):
+        """OR the step's presence into this update's mask (skip_missing_grads)."""
+        if not self.cfg.skip_missing_grads or self._pres_full:
+            return
+        if not self.ctl.load(self.C.F_PUSH_FLAG, vidx):
+            self._pres_full = True  # some accumulated step had every gradient: no mask
+            self._pres_part = None
+            return
+        ns = len(self.store.slots)
+        p = self.slot_buf(i, slot)[self.slot_pres:self.slot_pres + ns]
+        self._pres_part = p.clone() if self._pres_part is None else torch.maximum(self._pres_part, p)
+
+    def _hold(self):
+        """Checkpoint quiesce: finish the stream, report paused, wait for release."""
+        if self.cuda:
+            self.ps_stream.synchronize()
+        self._paused.set()
+        while self._pause_req.is_set() and not self.ctl.load(self.C.F_PS_STOP, 0):
+            time.sleep(0.001)
+        self._paused.clear()
 
     def _update(self, included, gscale):
         C = self.C
         self.ver += 1
         b = self.ver % self.NPUB
-        self.ctl.store(C.F_BUF_VER, b, -1)  # readers skip a buffer being rewritten
+        old = self.ctl.load(C.F_BUF_VER, b)
+        self.ctl.store(C.F_BUF_VER, b, -1)  # readers skip a buffer being rewritten ...
+        if old >= 0 and not self.ctl.wait_no_reader(old, 0):  # ... and it waits for current readers
+            self._stats["reader_waits"] += 1
+            if not self.ctl.wait_no_reader(old, int(self.cfg.dead_after_s * 1e6)):
+                self._stats["reader_timeouts"] = self._stats.get("reader_timeouts", 0) + 1
+        mask = None
+        if self.cfg.skip_missing_grads and not self._pres_full and self._pres_part is not None:
+            mask = self.store.chunk_mask(self._pres_part)
+        self._pres_full, self._pres_part = False, None
         with self.tracer.phase("ps_update", self.ps_stream):
-            self.opt._update_flat([self.acc], self.master, gscale, zero_src=True, pub=self.pub_buf(b))
+            self.opt._update_flat([self.acc], self.master, gscale, zero_src=True, pub=self.pub_buf(b), mask=mask)
         st = self.ps_stream
         # order matters: buffer stamp -> version word -> per-worker "included" words, so a worker
         # that sees its message included also sees a version containing it
-        self._ring(st, C.F_BUF_VER, b, self.ver)
-        self._ring(st, C.F_PUB_VER, 0, self.ver)
         last = {}
         for i, s in included:
             last[i] = max(last.get(i, 0), s)
-        for i, s in last.items():
-            self._ring(st, C.F_INCL_SEQ, i, s)
+        words = [(C.F_BUF_VER, b, self.ver), (C.F_PUB_VER, 0, self.ver)] + [(C.F_INCL_SEQ, i, s)
+                                                                           for i, s in last.items()]
+        for k in range(0, len(words), 6):
+            self._ring(st, words[k:k + 6])
         self.ctl.fetch_add(C.F_UPDATES, 0, 1)
 
     def _should_stop(self, seen):
@@ -364,30 +433,43 @@ class PSAsyncEngine(Engine):
         t = time.perf_counter()
         if self.cuda:
             self.enc_event.record(self.comm_stream)
+        step = self.step_no + 1
+        partial = 0 if (self.step_all_present or not self.cfg.skip_missing_grads) else 1
+        ver_src = []
+        if self.pull_mode == "device":  # the version the GPU adopted before this step's forward
+            ver_src = [self._sel[2 + step % RING:].data_ptr(), 0, 0]
         for pos, bi in enumerate(self.order):
             self.seq += 1
             s = self.seq
             slot = s % self.SLOTS
             if s > self.SLOTS:  # slot reuse: message s - SLOTS must have been consumed
                 tw = time.perf_counter()
-                if not self.ctl.wait_ge(C.F_ACK_SEQ, self.rank, s - self.SLOTS, TIMEOUT_US):
+                if not self.ctl.wait_ge(C.F_ACK_SEQ, self.rank, s - self.SLOTS, self.timeout_us):
                     self._check_error()
                     raise TimeoutError(f"rank {self.rank}: PS did not consume message {s - self.SLOTS}")
                 t_wait += time.perf_counter() - tw
             b = self.plan.buckets[bi]
             src = self.plan.message(self.wire, bi)  # layout (+ canary guard in debug_canary)
-            dst = self.slot_buf(self.rank, slot)[: b.msg_nbytes]
+            sbuf = self.slot_buf(self.rank, slot)
+            dst = sbuf[: b.msg_nbytes]
             vidx = self.rank * self.MAXSLOTS + slot
+            last = pos == self.nb - 1
+            words = [(C.F_PUSH_VER, vidx, self.local_ver), (C.F_PUSH_FLAG, vidx, partial if last else 0),
+                     (C.F_PUSH_SEQ, self.rank, s)]
             if self.cuda:
                 cs = self.comm_stream
                 with torch.cuda.stream(cs), self.tracer.phase("push", cs):
                     dst.copy_(src, non_blocking=True)
-                self.ctl.enqueue_store2(cs.cuda_stream, C.F_PUSH_VER, vidx, self.local_ver, C.F_PUSH_SEQ,
-                                        self.rank, s)
+                    if last and partial:
+                        ns = len(self.store.slots)
+                        sbuf[self.slot_pres:self.slot_pres + ns].copy_(self.presence_tensor(), non_blocking=True)
+                self._ring(cs, words, ver_src)
             else:
                 dst.copy_(src)
-                self.ctl.store(C.F_PUSH_VER, vidx, self.local_ver)
-                self.ctl.store(C.F_PUSH_SEQ, self.rank, s)
+                if last and partial:
+                    ns = len(self.store.slots)
+                    sbuf[self.slot_pres:self.slot_pres + ns].copy_(self.presence_tensor())
+                self._ring(None, words)
         self.step_no += 1
         data["slot_wait"] = t_wait
         data["isend_time"] = time.perf_counter() - t
@@ -395,9 +477,10 @@ class PSAsyncEngine(Engine):
         if self.cfg.auto_pull:
             data["pulled"] = float(self.irequest_params())
         data["comm_wait"] = time.perf_counter() - t
-        data["version"] = float(self.local_ver)
+        data["version"] = float(self.adopted_version())
         data["optim_step_time"] = 0.0
         data["decode_time"] = 0.0
+        data.update(self.step_metrics())
         data.update(self.bytes_per_step())
         data["grad_bytes_recv"] = 0
         data["param_bytes_pulled"] = self.store.numel * torch.empty((), dtype=self.pub_dtype).element_size() \
@@ -406,33 +489,72 @@ class PSAsyncEngine(Engine):
         self.steps += 1
         return data
 
-    def irequest_params(self, block_for: Optional[int] = None) -> bool:
-        """Adopt the newest published parameter version that has landed (README.md:63).
+    def adopted_version(self) -> int:
+        """The version this worker trains on (device pull: as last reported by the GPU)."""
+        if self.pull_mode == "device":
+            return int(self.ctl.load(self.C.F_APPLIED_VER, self.rank))
+        return self.local_ver
 
-        Remote workers on a GPU prefetch: the xGMI read of the published buffer runs on a side
-        stream and is adopted (one local copy on the compute stream) at the next call, so the
-        pull overlaps compute instead of stalling the forward pass -- one extra version of
-        staleness, which AsySG-InCon tolerates by design.  ``block_for=v`` waits until version
-        >= v is published and adopts synchronously; ``cfg.max_delay >= 0`` waits until the
-        published params include all but this worker's newest ``max_delay`` gradients."""
+    def irequest_params(self, block_for: Optional[int] = None) -> bool:
+        """Adopt the newest published parameter version (README.md:63).
+
+        ``pull='device'`` (GPU default): enqueue a GPU-time pull on the compute stream -- the
+        version is chosen when the GPU reaches it (after this step's backward), and the copy
+        reads the publish buffer in place (local HBM on the PS rank, xGMI on the others).
+        Returns True (the outcome is known only to the GPU; ``adopted_version()`` reports it).
+        ``pull='prefetch'`` (host-chosen): a side-stream copy adopted at the next call, one extra
+        version of staleness.  ``block_for=v`` waits until version >= v is published and
+        adopts synchronously; ``cfg.max_delay >= 0`` waits until the published params include
+        all but this worker's newest ``max_delay`` gradients."""
         C = self.C
         sync = block_for is not None
         if block_for is not None:
-            if not self.ctl.wait_ge(C.F_PUB_VER, 0, block_for, TIMEOUT_US):
+            if not self.ctl.wait_ge(C.F_PUB_VER, 0, block_for, self.timeout_us):
                 self._check_error()
                 raise TimeoutError("no published parameters")
         if self.cfg.max_delay >= 0 and self.step_no - self.cfg.max_delay > 0:
             need = (self.step_no - self.cfg.max_delay) * self.nb  # last message of that step
-            sync = True
-            if not self.ctl.wait_ge(C.F_INCL_SEQ, self.rank, need, TIMEOUT_US):
+            if not self.ctl.wait_ge(C.F_INCL_SEQ, self.rank, need, self.timeout_us):
                 self._check_error()
                 raise TimeoutError(f"rank {self.rank}: params never caught up to message {need}")
-        if self._use_prefetch() and not sync:
-            return self._prefetch_pull()
-        return self._direct_pull()
+            if self.pull_mode != "device":
+                sync = True
+        if sync or self.pull_mode == "direct":
+            return self._direct_pull()
+        if self.pull_mode == "device":
+            return self._device_pull()
+        return self._prefetch_pull()
 
-    def _use_prefetch(self) -> bool:
-        return self.cuda and self.rank != 0 and self.cfg.pull == "prefetch"
+    def _device_pull(self) -> bool:
+        C = self.C
+        esz = torch.empty((), dtype=self.pub_dtype).element_size()
+        base = self.mem[self.pub_off:self.pub_off + (self.NPUB - 1) * self.pub_bytes + self.store.numel * esz]
+        self.C.pull_params(self._sel, self.ctl.device_addr(C.F_PUB_VER, 0), self.ctl.device_addr(C.F_BUF_VER, 0),
+                           self.ctl.device_addr(C.F_READING, self.rank), self.ctl.device_addr(C.F_APPLIED_VER, self.rank),
+                           base, self.pub_bytes, self.NPUB, self.pub_dtype == torch.bfloat16, self.store.data,
+                           (self.step_no + 1) % RING, 64)
+        return True
+
+    def _claim(self):
+        """Host-side reader handshake: (version, buffer) announced in READING, or None."""
+        C = self.C
+        for _ in range(16):
+            v = self.ctl.load(C.F_PUB_VER, 0)
+            if v <= self.local_ver:
+                return None
+            b = v % self.NPUB
+            self.ctl.store(C.F_READING, self.rank, v)
+            if self.ctl.load(C.F_BUF_VER, b) == v:
+                return v, b
+            self.ctl.store(C.F_READING, self.rank, -1)
+        return None
+
+    def _release(self, stream):
+        """Clear READING once the copy that read the publish buffer has completed."""
+        if stream is not None:
+            self._ring(stream, [(self.C.F_READING, self.rank, -1)])
+        else:
+            self.ctl.store(self.C.F_READING, self.rank, -1)
 
     def _adopt(self, src, v):
         if src.dtype == self.store.data.dtype:
@@ -440,54 +562,55 @@ class PSAsyncEngine(Engine):
         else:
             ops.convert(src, self.store.data)
         self.local_ver = v
+        if self.cuda:  # keep the GPU-side version record in step with a host adoption
+            self._sel[1:].fill_(v)
         self.ctl.store(self.C.F_APPLIED_VER, self.rank, v)
 
     def _direct_pull(self) -> bool:
-        C = self.C
         self._staged = None  # a synchronous adoption supersedes any prefetch in flight
-        for _ in range(8):
-            v = self.ctl.load(C.F_PUB_VER, 0)
-            if v <= self.local_ver:
-                return False
-            b = v % self.NPUB
-            if self.ctl.load(C.F_BUF_VER, b) != v:
-                continue  # rewritten under us: re-read the version word
-            src = self.pub_buf(b)
-            if self.cuda:
-                self._adopt(src, v)
-                return True
-            tmp = src.clone()
-            if self.ctl.load(C.F_BUF_VER, b) != v:
-                continue  # torn on the host path: retry (seqlock)
-            self._adopt(tmp, v)
-            return True
-        return False
+        got = self._claim()
+        if got is None:
+            return False
+        v, b = got
+        if self.cuda:
+            self._adopt(self.pub_buf(b), v)
+            self._release(torch.cuda.current_stream(self.store.device))
+        else:
+            self._adopt(self.pub_buf(b).clone(), v)
+            self._release(None)
+        return True
 
     def _prefetch_pull(self) -> bool:
-        C = self.C
         adopted = False
         st = getattr(self, "_staged", None)
-        if st is not None and st[1].query():
-            v, _ = st
-            torch.cuda.current_stream(self.store.device).wait_event(st[1])
-            self._adopt(self._stage_buf, v)
+        if st is not None and st[2].query():
+            v, k, ev = st
+            torch.cuda.current_stream(self.store.device).wait_event(ev)
+            self._adopt(self._stage[k], v)
+            done = torch.cuda.Event()
+            done.record(torch.cuda.current_stream(self.store.device))
+            self._stage_ev[k] = done  # the next prefetch into stage k waits for this adoption only
             self._staged = None
             adopted = True
         if getattr(self, "_staged", None) is None:
-            v = self.ctl.load(C.F_PUB_VER, 0)
-            b = v % self.NPUB
-            if v > self.local_ver and self.ctl.load(C.F_BUF_VER, b) == v:
-                if getattr(self, "_stage_buf", None) is None:
-                    self._stage_buf = torch.empty(self.store.numel, dtype=self.pub_dtype, device=self.store.device)
-                    self._pull_stream = torch.cuda.Stream(device=self.store.device)
+            got = self._claim()
+            if got is not None:
+                v, b = got
+                k = self._stage_k
+                self._stage_k ^= 1
+                if self._stage[k] is None:
+                    self._stage[k] = torch.empty(self.store.numel, dtype=self.pub_dtype, device=self.store.device)
+                    if getattr(self, "_pull_stream", None) is None:
+                        self._pull_stream = torch.cuda.Stream(device=self.store.device)
                 ps = self._pull_stream
-                # the compute stream may still read the staging buffer from the last adoption
-                ps.wait_stream(torch.cuda.current_stream(self.store.device))
+                if self._stage_ev[k] is not None:
+                    ps.wait_event(self._stage_ev[k])
                 with torch.cuda.stream(ps):
-                    self._stage_buf.copy_(self.pub_buf(b), non_blocking=True)
+                    self._stage[k].copy_(self.pub_buf(b), non_blocking=True)
+                self._release(ps)
                 ev = torch.cuda.Event()
                 ev.record(ps)
-                self._staged = (v, ev)
+                self._staged = (v, k, ev)
         return adopted
 
     def _inject(self, data) -> bool:
@@ -519,6 +642,10 @@ class PSAsyncEngine(Engine):
         d["version"] = self.ctl.load(C.F_PUB_VER, 0)
         return d
 
+    def transport_info(self) -> dict:
+        return {"doorbells": self.ctl.bell_mode, "pull": self.pull_mode, "npub": self.NPUB,
+                "mailbox_slots": self.SLOTS, "slot_bytes": self.slot_bytes}
+
     def close(self):
         if getattr(self, "_closed", False):
             return
@@ -532,7 +659,8 @@ class PSAsyncEngine(Engine):
             if not getattr(self, "_dead", False):
                 self.ctl.store(C.F_STOP, self.rank, self.seq + 1)
             if self.rank == 0 and self._thread is not None:
-                deadline = time.time() + TIMEOUT_US / 1e6
+                self._pause_req.clear()
+                deadline = time.time() + self.timeout_us / 1e6
                 while self._thread.is_alive() and time.time() < deadline:
                     self._thread.join(timeout=0.5)
                 if self._thread.is_alive():
@@ -547,15 +675,39 @@ class PSAsyncEngine(Engine):
             raise RuntimeError(self._err)
 
     # ------------------------------------------------------------------ checkpoint support
+    @contextlib.contextmanager
+    def quiesced(self):
+        """Hold the PS thread between messages (rank 0) so the master, optimizer state, pending
+        accumulator and version form one consistent snapshot; other ranks just sync."""
+        if self.cuda:
+            torch.cuda.synchronize(self.store.device)
+        held = False
+        if self.rank == 0 and self._thread is not None and self._thread.is_alive():
+            self._pause_req.set()
+            deadline = time.time() + self.timeout_us / 1e6
+            while not self._paused.is_set() and self._thread.is_alive():
+                if time.time() > deadline:
+                    self._pause_req.clear()
+                    raise TimeoutError("PS thread did not pause for the checkpoint")
+                time.sleep(0.001)
+            held = True
+        try:
+            yield
+        finally:
+            if held:
+                self._pause_req.clear()
+
     def engine_state(self) -> dict:
-        """PS state (rank 0) + this worker's codec state.  Call between steps."""
+        """PS state (rank 0) + this worker's codec state.  Call between steps; on rank 0 inside
+        :meth:`quiesced` (hipps.utils.checkpoint.save does) for a consistent PS snapshot."""
         if self.cuda:
             torch.cuda.synchronize(self.store.device)
         d = {"codec_state": [{k: v.detach().cpu() for k, v in st.items() if k != "ws"} for st in self.codec_state],
-             "seq": self.seq, "step_no": self.step_no, "local_ver": self.local_ver}
+             "seq": self.seq, "step_no": self.step_no, "local_ver": self.adopted_version()}
         if self.rank == 0:
             self.ps_stream.synchronize() if self.cuda else None
-            d.update({"master": self.master.detach().cpu(), "version": self.ver})
+            d.update({"master": self.master.detach().cpu(), "version": self.ver, "acc": self.acc.detach().cpu(),
+                      "acc_count": self._count})
         return d
 
     def load_engine_state(self, d: dict):
@@ -568,14 +720,18 @@ class PSAsyncEngine(Engine):
             C = self.C
             if self.steps or self._stats["accumulated"]:
                 raise RuntimeError("load the PS state before training starts")
-            self.master.copy_(d["master"].to(self.master.device))
-            self.ver = int(d["version"])
-            b = self.ver % self.NPUB
-            ops.convert(self.master, self.pub_buf(b))
-            if self.cuda:
-                torch.cuda.current_stream(self.store.device).synchronize()
-            self.ctl.store(C.F_BUF_VER, b, self.ver)
-            self.ctl.store(C.F_PUB_VER, 0, self.ver)
+            with self.quiesced():
+                self.master.copy_(d["master"].to(self.master.device))
+                if "acc" in d:
+                    self.acc.copy_(d["acc"].to(self.acc.device))
+                    self._count = int(d.get("acc_count", 0))
+                self.ver = int(d["version"])
+                b = self.ver % self.NPUB
+                ops.convert(self.master, self.pub_buf(b))
+                if self.cuda:
+                    torch.cuda.current_stream(self.store.device).synchronize()
+                self.ctl.store(C.F_BUF_VER, b, self.ver)
+                self.ctl.store(C.F_PUB_VER, 0, self.ver)
         barrier(self.world)
         ver = self.ctl.load(self.C.F_PUB_VER, 0)
         self.local_ver = -1

@@ -28,27 +28,50 @@ def _cpu(d):
     return {k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in d.items()}
 
 
+def _buffers(model: torch.nn.Module) -> dict:
+    for m in model.modules():  # fold host-side counters (FusedBatchNorm2d) into their buffers
+        if hasattr(m, "sync_num_batches_tracked"):
+            m.sync_num_batches_tracked()
+    return {k: v.detach().cpu() for k, v in model.named_buffers()}
+
+
 def save(opt, path: str, model: Optional[torch.nn.Module] = None, extra: Optional[dict] = None) -> None:
     os.makedirs(path, exist_ok=True)
     eng = opt.engine
     rank = opt.world.rank
-    es = eng.engine_state()
-    master = es.pop("master", None)
-    version = es.pop("version", None)
-    mine = {"engine": es}
-    if model is not None:
-        mine["buffers"] = {k: v.detach().cpu() for k, v in model.named_buffers()}
-    torch.save(mine, os.path.join(path, f"rank{rank}.pt"))
-    if rank == 0:
-        params = master if master is not None else opt.store.data.detach().cpu()
-        ps = {"params": params, "flat_state": _cpu(opt.flat_state), "group_steps": list(opt._group_steps),
-              "steps": opt.steps, "mode": opt.mode, "codec": opt.codec.name, "numel": opt.store.numel,
-              "version": -1 if version is None else int(version),
-              "mom_started": sorted(getattr(opt, "_mom_started", set()))}
-        if extra:
-            ps["extra"] = extra
-        torch.save(ps, os.path.join(path, "ps.pt"))
+    # async PS: the PS thread is held between messages for the whole snapshot, so the master,
+    # the optimizer state, the pending accumulator and the version belong to one PS state
+    quiesce = getattr(eng, "quiesced", None)
+    with (quiesce() if quiesce is not None else _nullctx()):
+        es = eng.engine_state()
+        master = es.pop("master", None)
+        version = es.pop("version", None)
+        acc = es.pop("acc", None)
+        acc_count = es.pop("acc_count", 0)
+        mine = {"engine": es}
+        if model is not None:
+            mine["buffers"] = _buffers(model)
+        torch.save(mine, os.path.join(path, f"rank{rank}.pt"))
+        if rank == 0:
+            params = master if master is not None else opt.store.data.detach().cpu()
+            ps = {"params": params, "flat_state": _cpu(opt.flat_state), "group_steps": list(opt._group_steps),
+                  "steps": opt.steps, "mode": opt.mode, "codec": opt.codec.name, "numel": opt.store.numel,
+                  "version": -1 if version is None else int(version),
+                  "mom_started": sorted(getattr(opt, "_mom_started", set()))}
+            if acc is not None:
+                ps["acc"], ps["acc_count"] = acc, int(acc_count)
+            if extra:
+                ps["extra"] = extra
+            torch.save(ps, os.path.join(path, "ps.pt"))
     barrier(opt.world)
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 def load(opt, path: str, model: Optional[torch.nn.Module] = None) -> dict:
@@ -74,6 +97,8 @@ def load(opt, path: str, model: Optional[torch.nn.Module] = None) -> dict:
         if rank == 0:
             es["master"] = ps["params"]
             es["version"] = max(0, ps["version"])
+            if "acc" in ps:
+                es["acc"], es["acc_count"] = ps["acc"], ps["acc_count"]
         opt.engine.load_engine_state(es)
     else:
         opt.store.data.copy_(ps["params"].to(opt.store.data.device))

@@ -57,7 +57,7 @@ def _simulate(world, steps, opt_name):
             gsum = g if gsum is None else [a + b for a, b in zip(gsum, g)]
         opt.zero_grad()
         for p, g in zip(m.parameters(), gsum):
-            p.grad.copy_(g)
+            p.grad = g.clone()
         opt.step()
     return [p.detach().clone() for p in m.parameters()]
 

@@ -95,6 +95,37 @@ def test_adam_fused(n, amsgrad, torch_mode, wd):
     torch.testing.assert_close(vd.cpu(), v, rtol=1e-5, atol=1e-7)
 
 
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+@pytest.mark.parametrize("n", [16 * 37 + 5, 1 << 18])
+def test_masked_update_skips_chunks(opt, n):
+    """Chunks (16 elements) whose mask byte is 0 keep p / state bit-exactly; publish gets p."""
+    torch.manual_seed(3)
+    nch = (n + 15) // 16
+    mask = (torch.rand(nch) > 0.3).to(torch.uint8)
+    p = torch.randn(n)
+    p0 = p.clone()
+    st = [torch.randn(n) * 0.1, torch.rand(n) * 0.1, torch.rand(n) * 0.1]
+    g = torch.randn(n)
+    pd, sd = p.to(DEV), [s.to(DEV) for s in st]
+    s0 = [s.clone() for s in sd]
+    pub = torch.empty(n, dtype=torch.float32, device=DEV)
+    if opt == "sgd":
+        kw = dict(lr=0.1, weight_decay=0.1, momentum=0.9)
+        ref.sgd_step([g], p, st[0], None, False, 1.0, mask=mask, **kw)
+        ops.sgd_step([g.to(DEV)], pd, sd[0], pub, False, 1.0, mask=mask.to(DEV), **kw)
+    else:
+        kw = dict(lr=1e-2, weight_decay=0.1, step=3, amsgrad=True)
+        ref.adam_step([g], p, st[0], st[1], st[2], None, False, 1.0, mask=mask, **kw)
+        ops.adam_step([g.to(DEV)], pd, sd[0], sd[1], sd[2], pub, False, 1.0, mask=mask.to(DEV), **kw)
+    keep = ~mask.bool().repeat_interleave(16)[:n]
+    assert torch.equal(pd.cpu()[keep], p0[keep])
+    assert not torch.equal(pd.cpu()[~keep], p0[~keep])
+    for a_, b_ in zip(sd, s0):
+        assert torch.equal(a_.cpu()[keep], b_.cpu()[keep])
+    torch.testing.assert_close(pd.cpu(), p, rtol=1e-5, atol=1e-6)
+    assert torch.equal(pub.cpu(), pd.cpu())
+
+
 @pytest.mark.parametrize("n", [1, 255, 256, 1000, 1 << 20])
 @pytest.mark.parametrize("ef,sr", [(False, False), (True, False), (False, True)])
 def test_q8_encode_matches_reference(n, ef, sr):

@@ -23,12 +23,15 @@ def test_flat_store_views_channels_last_and_grads():
         assert (p.data_ptr() - st.data.data_ptr()) % 64 == 0  # 16-element aligned slots
     assert m[0].weight.is_contiguous(memory_format=torch.channels_last)
     x = torch.randn(2, 3, 8, 8).contiguous(memory_format=torch.channels_last)
-    m(x).sum().backward()
+    m(x).sum().backward()  # autograd hands over fresh gradient tensors (p.grad was None) ...
+    assert not st.grads_attached() and all(st.presence())
+    st.attach_grads()  # ... which step() copies into the flat views
     assert st.grads_attached()
     assert st.grad.abs().sum() > 0
-    m.zero_grad(set_to_none=True)  # user drops the views ...
-    st.attach_grads()  # ... and they come back
-    assert st.grads_attached()
+    st.zero_grad(set_to_none=False)  # zero-filled views, still counted as gradients
+    assert st.grads_attached() and all(st.presence()) and st.grad.abs().sum() == 0
+    st.zero_grad()  # torch default: None -> no gradient
+    assert not any(st.presence())
 
 
 def test_bucket_plan_tiles_flat_buffer_and_dense_image():
