@@ -290,13 +290,148 @@ class Threshold(Codec):
         return int(views["count"][0])
 
 
+class ObjectCodec(Codec):
+    """Adapter for the reference's codec plug-in contract (ps.py:57, 65-66, 94, 165-166): any
+    object with ``encode(grad) -> code`` and ``decode(code, cuda=bool) -> tensor/ndarray``, whose
+    ``codes`` attribute the engine sets to every contributing rank's code before decoding
+    (ps.py:165).  Codes may be arbitrary picklable Python objects of unknown size (an SVD
+    factorisation, QSGD levels + norms, ...) -- the "generic object / unknown size" path of
+    README.md:24-31.
+
+    One message per rank per step: ``{slot index: code}`` for every parameter that has a
+    gradient, serialised with the zero-copy tensor frames of hipps.utils.serialization (+ the
+    optional zlib level, mpi_comms.py:18-30).  Transport:
+      allgather  size all-gather, then a payload all-gather of the max size (mpi_comms.py:144-174)
+      ps_sync    size all-gather, then a gather to the PS (mpi_comms.py:60-117)
+      ps_async   a length-prefixed blob in the worker's mailbox slot (capacity: object_slot_mb)
+    Decode: per parameter, ``code.codes = [codes in rank order]``, decode each, check the shapes
+    match (ps.py:172-175), sum in rank order (ps.py:176) into the fp32 flat gradient, then the
+    fused optimizer kernel.  Encodes run in a thread pool like the reference's (ps.py:85)."""
+
+    name = "object"
+    is_object = True
+    fusable = False
+    HDR = 16  # int64 payload length + int64 reserved, then the payload
+
+    def __init__(self, code, max_bytes: int = 0, level: int = 0, workers: int = 8):
+        super().__init__()
+        if not (callable(getattr(code, "encode", None)) and callable(getattr(code, "decode", None))):
+            raise TypeError("an object codec needs encode(grad) and decode(code, cuda=...)")
+        self.code = code
+        self.max_bytes = int(max_bytes)
+        self.level = int(level)
+        self.workers = workers
+        self.engine = None
+        self._pool = None
+        self.last_msg_bytes = 0
+        self.last_packaged_bytes = 0
+
+    def bind(self, engine):
+        self.engine = engine
+
+    def capacity(self, n: int) -> int:
+        return self.max_bytes if self.max_bytes > 0 else 8 * n + (1 << 20)
+
+    def layout(self, n):
+        return WireLayout([("hdr", torch.int64, 2), ("blob", torch.uint8, self.capacity(n))])
+
+    # ---- encode -----------------------------------------------------------------------------
+    def encode_bytes(self, x: torch.Tensor) -> bytes:
+        """Encode every present parameter of the bound store from flat gradient ``x`` (whole store)."""
+        from concurrent.futures import ThreadPoolExecutor
+
+        from hipps.utils.serialization import compress, dumps
+
+        st = self.engine.store
+        pres = st.presence()
+        todo = [i for i, f in enumerate(pres) if f]
+        if self._pool is None:
+            self._pool = ThreadPoolExecutor(max_workers=self.workers, thread_name_prefix="hipps-encode")
+
+        def enc(i):
+            s = st.slots[i]
+            return i, self.code.encode(x[s.offset:s.offset + s.numel].view(s.param.shape))
+
+        codes = dict(self._pool.map(enc, todo))
+        raw = dumps(codes)
+        packed = bytes(compress(raw, self.level)) if self.level else raw
+        self.last_msg_bytes, self.last_packaged_bytes = len(raw), len(packed)
+        return packed
+
+    def encode_into(self, x, views, state):
+        b = self.encode_bytes(x)
+        state["bytes"] = b
+        if getattr(self.engine, "object_wire", True):
+            cap = views["blob"].numel()
+            if len(b) > cap:
+                raise ValueError(f"encoded message is {len(b)} bytes, the object codec slot holds {cap}; "
+                                 "raise object_slot_mb")
+            hdr = torch.tensor([len(b), 0], dtype=torch.int64)
+            blob = torch.frombuffer(bytearray(b), dtype=torch.uint8) if b else torch.empty(0, dtype=torch.uint8)
+            views["hdr"].copy_(hdr)
+            views["blob"][: len(b)].copy_(blob)
+
+    # ---- decode -----------------------------------------------------------------------------
+    def decode_messages(self, blobs: Sequence[bytes]) -> List[dict]:
+        from hipps.utils.serialization import decompress, loads
+
+        out = []
+        for b in blobs:
+            raw = decompress(b) if self.level else b
+            out.append(loads(raw))
+        return out
+
+    def accumulate_codes(self, per_rank: Sequence[dict], acc: torch.Tensor, gscale: float = 1.0,
+                         accumulate: bool = False) -> List[bool]:
+        """acc (+)= gscale * sum over ranks of decode(code) per parameter; returns presence."""
+        from hipps.utils.serialization import to_torch
+
+        st = self.engine.store
+        if not accumulate:
+            acc.zero_()
+        present = [False] * len(st.slots)
+        cuda = acc.is_cuda
+        for i, s in enumerate(st.slots):
+            codes = [m[i] for m in per_rank if i in m]
+            if not codes:
+                continue
+            present[i] = True
+            self.code.codes = codes  # ps.py:165
+            grads = []
+            for c in codes:
+                g = to_torch(self.code.decode(c, cuda=cuda))
+                if not torch.is_tensor(g):
+                    g = torch.as_tensor(g)
+                grads.append(g.to(acc.device, torch.float32))
+            if not all(g.numel() == s.numel for g in grads) or not all(g.shape == grads[0].shape for g in grads):
+                raise ValueError(f"shapes not the same for {s.name}: {[tuple(g.shape) for g in grads]}")
+            d = grads[0].reshape(-1).clone()
+            for g in grads[1:]:  # rank order, like sum(grads) (ps.py:176)
+                d += g.reshape(-1)
+            if gscale != 1.0:
+                d *= gscale
+            acc[s.offset:s.offset + s.numel] += d
+        return present
+
+    def read_message(self, views) -> bytes:
+        n = int(views["hdr"][0].item())
+        return views["blob"][:n].cpu().numpy().tobytes()
+
+    def accumulate(self, msgs, acc, gscale=1.0, accumulate=False):
+        self.last_present = self.accumulate_codes(self.decode_messages([self.read_message(v) for v in msgs]), acc,
+                                                  gscale, accumulate)
+
+
 def get_codec(spec) -> Codec:
     """'fp32' | 'bf16' | 'int8' | 'int8_sr' | 'topk[:ratio]' | 'topk_bf16[:ratio]' | 'topk_int8[:ratio]' |
-    'threshold[:tau[:max_ratio]]' | Codec instance."""
+    'threshold[:tau[:max_ratio]]' | Codec instance | any object with encode()/decode() (the
+    reference's ``codings`` contract, wrapped in :class:`ObjectCodec`)."""
     if spec is None:
         return Identity(torch.float32)
     if isinstance(spec, Codec):
         return spec
+    if not isinstance(spec, str) and hasattr(spec, "encode") and hasattr(spec, "decode"):
+        return ObjectCodec(spec)
     name, _, arg = str(spec).partition(":")
     name = name.lower()
     if name in ("fp32", "identity", "none"):
@@ -320,4 +455,4 @@ def get_codec(spec) -> Codec:
     raise ValueError(f"unknown codec {spec!r}")
 
 
-__all__ = ["Codec", "Identity", "Int8", "TopK", "TopKInt8", "Threshold", "WireLayout", "get_codec"]
+__all__ = ["Codec", "Identity", "Int8", "TopK", "TopKInt8", "Threshold", "ObjectCodec", "WireLayout", "get_codec"]

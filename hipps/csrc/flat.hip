@@ -138,13 +138,14 @@ __global__ __launch_bounds__(kBlock) void k_sgd(SlotPtrs g, int W, float gscale,
   const int64_t nv = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
     const int64_t i = v << 2;
-    if (zero_src) Vec4<float>::store((float*)g.p[0], i, make_float4(0.f, 0.f, 0.f, 0.f));
     float4 pv = Vec4<float>::load(p, i);
     if (cmask && !cmask[i >> 4]) {  // parameter without a gradient this step: untouched (ps.py:178-179)
+      if (zero_src) Vec4<float>::store((float*)g.p[0], i, make_float4(0.f, 0.f, 0.f, 0.f));
       pub_store4(pub, pub_mode, i, pv);
       continue;
     }
     float4 d = sum_slots4<T>(g, W, i, gscale);
+    if (zero_src) Vec4<float>::store((float*)g.p[0], i, make_float4(0.f, 0.f, 0.f, 0.f));
     float4 b = has_buf && !h.first ? Vec4<float>::load(buf, i) : make_float4(0.f, 0.f, 0.f, 0.f);
     sgd1(pv.x, b.x, d.x, h, has_buf);
     sgd1(pv.y, b.y, d.y, h, has_buf);
@@ -181,12 +182,13 @@ __global__ __launch_bounds__(kBlock) void k_adam(SlotPtrs g, int W, float gscale
   float dummy = 0.f;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
     const int64_t i = v << 2;
-    if (zero_src) Vec4<float>::store((float*)g.p[0], i, make_float4(0.f, 0.f, 0.f, 0.f));
     if (cmask && !cmask[i >> 4]) {
+      if (zero_src) Vec4<float>::store((float*)g.p[0], i, make_float4(0.f, 0.f, 0.f, 0.f));
       pub_store4(pub, pub_mode, i, Vec4<float>::load(p, i));
       continue;
     }
     float4 d = sum_slots4<T>(g, W, i, gscale);
+    if (zero_src) Vec4<float>::store((float*)g.p[0], i, make_float4(0.f, 0.f, 0.f, 0.f));
     float4 pv = Vec4<float>::load(p, i), mv = Vec4<float>::load(m, i), sv = Vec4<float>::load(vv, i);
     float4 xv = h.amsgrad ? Vec4<float>::load(vmax, i) : make_float4(0.f, 0.f, 0.f, 0.f);
     adam1(pv.x, mv.x, sv.x, &xv.x, d.x, h);

@@ -36,7 +36,19 @@ class Engine:
         self.store = store
         self.codec = codec
         self.world = world
-        self.plan = BucketPlan(store, codec, int(cfg.bucket_mb * (1 << 20)), guard=cfg.debug_canary)
+        # reference-style codec objects (ObjectCodec): one host-serialised message per rank per
+        # step covering every parameter, so one bucket; only the async mailbox carries it as a
+        # device wire image (object_wire), the sync modes move the bytes with a size round
+        self.is_object = bool(getattr(codec, "is_object", False))
+        self.object_wire = False
+        bucket_bytes = int(cfg.bucket_mb * (1 << 20))
+        if self.is_object:
+            codec.bind(self)
+            if cfg.object_slot_mb > 0:
+                codec.max_bytes = int(cfg.object_slot_mb * (1 << 20))
+            codec.level = cfg.compress_level
+            bucket_bytes = 1 << 62
+        self.plan = BucketPlan(store, codec, bucket_bytes, guard=cfg.debug_canary)
         self.cuda = store.device.type == "cuda"
         self.tracer = StepTracer(cfg.trace, self.cuda)
         # zero-initialised: the 16-element alignment gaps between parameters are never written.
@@ -62,7 +74,8 @@ class Engine:
         # 'gather': autograd keeps ownership of p.grad (stolen, no per-parameter accumulate kernel,
         # no memset) and each bucket is gathered by ONE multi-tensor kernel; 'flat': p.grad are
         # views of the flat gradient buffer.
-        self.grad_mode = "gather" if (self.cuda and cfg.grad_gather and self.supports_gather) else "flat"
+        self.grad_mode = "gather" if (self.cuda and cfg.grad_gather and self.supports_gather and
+                                      not self.is_object) else "flat"
         if self.grad_mode == "gather":
             self._build_gather_plan()
             store.set_grad_mode("gather")
@@ -151,6 +164,13 @@ class Engine:
         b = self.plan.buckets[bi]
         g = self.store.grad[b.lo:b.hi]
         views = self.plan.views(self.wire, bi)
+        if self.is_object:  # host codec objects: run on finished gradients (ps.py:94 in a pool)
+            if self.cuda:
+                torch.cuda.current_stream(self.store.device).synchronize()
+            with self.tracer.phase("encode"):
+                self.codec.encode_into(g, views, self.codec_state[bi])
+            self._encoded[bi] = True
+            return
         if self.cuda:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.store.device))
@@ -230,6 +250,9 @@ class Engine:
         """The reference's per-step byte accounting (ps.py:135-136): mean encoded message bytes and
         mean packaged (framed) bytes over this step's messages; ``iallgather_prepare_time`` is the
         size-round time (ps.py:139-141) -- 0 here because device messages have static sizes."""
+        if self.is_object:
+            return {"msg_bytes": float(self.codec.last_msg_bytes), "packaged_bytes": float(self.codec.last_packaged_bytes),
+                    "iallgather_prepare_time": getattr(self, "_prep_time", 0.0)}
         bs = self.plan.buckets
         return {"msg_bytes": sum(b.layout.nbytes for b in bs) / len(bs),
                 "packaged_bytes": sum(b.msg_nbytes for b in bs) / len(bs),
@@ -312,7 +335,69 @@ class Engine:
                     st[k].copy_(v)
 
     def bytes_per_step(self) -> Dict[str, int]:
+        if self.is_object:
+            return {"grad_bytes_sent": int(self.codec.last_packaged_bytes)}
         return {"grad_bytes_sent": self.plan.wire_nbytes}
+
+    # ------------------------------------------------------------------ object-codec slow path
+    def _object_bytes(self) -> bytes:
+        return self.codec_state[0]["bytes"]
+
+    def _exchange_sizes(self, n: int) -> List[int]:
+        import torch.distributed as dist
+
+        W = self.world.size
+        if W == 1:
+            return [n]
+        dev = self.store.device if self.world.backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([n], dtype=torch.int64, device=dev)
+        out = torch.zeros(W, dtype=torch.int64, device=dev)
+        if self.world.backend == "nccl":
+            dist.all_gather_into_tensor(out, t)
+        else:
+            dist.all_gather(list(out.view(W, 1)), t)
+        return [int(v) for v in out.tolist()]
+
+    def object_exchange(self, root: Optional[int]) -> Optional[List[bytes]]:
+        """Variable-size exchange of this step's object messages: size round, then one payload
+        collective at the max size (all-gather, or gather to ``root``).  Returns every rank's
+        bytes (None on non-root ranks of a gather)."""
+        import torch.distributed as dist
+
+        blob = self._object_bytes()
+        W = self.world.size
+        t = time.perf_counter()
+        sizes = self._exchange_sizes(len(blob))
+        self._prep_time = time.perf_counter() - t
+        if W == 1:
+            return [blob]
+        slot = max(1, max(sizes))
+        dev = self.store.device if self.world.backend == "nccl" else torch.device("cpu")
+        send = torch.zeros(slot, dtype=torch.uint8)
+        if blob:
+            send[: len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
+        send = send.to(dev)
+        if root is None:
+            recv = torch.empty(W * slot, dtype=torch.uint8, device=dev)
+            all_gather_into(recv, send, self.world)
+        else:
+            recv = torch.empty(W * slot, dtype=torch.uint8, device=dev) if self.world.rank == root else None
+            gather_into(recv, send, self.world, dst=root)
+            if self.world.rank != root:
+                return None
+        host = recv.cpu().numpy()
+        return [host[w * slot: w * slot + sizes[w]].tobytes() for w in range(W)]
+
+    def object_apply(self, blobs: List[bytes], target: torch.Tensor, pub: Optional[torch.Tensor], gscale: float):
+        acc = self._obj_acc if getattr(self, "_obj_acc", None) is not None else torch.zeros_like(self.store.grad)
+        self._obj_acc = acc
+        t = time.perf_counter()
+        present = self.codec.accumulate_codes(self.codec.decode_messages(blobs), acc, 1.0, False)
+        self._decode_time = time.perf_counter() - t
+        mask = None
+        if not all(present) and self.cfg.skip_missing_grads:
+            mask = self.store.chunk_mask(torch.tensor(present, dtype=torch.uint8))
+        self.opt._update_flat([acc], target, gscale, zero_src=False, pub=pub, mask=mask)
 
 
 class LocalEngine(Engine):
@@ -350,6 +435,14 @@ class LocalEngine(Engine):
         data = {}
         data["code_wait"] = self.encode_all()
         t = time.perf_counter()
+        if self.is_object:
+            self.object_apply([self._object_bytes()], self.store.data, None, 1.0)
+            data.update(optim_step_time=time.perf_counter() - t, decode_time=self._decode_time, comm_wait=0.0,
+                        isend_time=0.0)
+            data.update(self.step_metrics())
+            data.update(self.bytes_per_step())
+            self.steps += 1
+            return data
         if self.cuda and (not self._bypass or self.grad_mode == "gather"):
             torch.cuda.current_stream(self.store.device).wait_stream(self.comm_stream)
         if not self._bypass:
@@ -387,6 +480,19 @@ class AllGatherEngine(Engine):
         data = {}
         data["code_wait"] = self.encode_all()
         self._check_order()
+        if self.is_object:  # ps.py:140-190: size round, payload all-gather, decode W codes, sum, step
+            t = time.perf_counter()
+            blobs = self.object_exchange(None)
+            data["isend_time"] = data["comm_wait"] = time.perf_counter() - t
+            t = time.perf_counter()
+            self.object_apply(blobs, self.store.data, None, self.gscale(self.world.size))
+            data["optim_step_time"] = time.perf_counter() - t
+            data["decode_time"] = self._decode_time
+            data.update(self.step_metrics())
+            data.update(self.bytes_per_step())
+            data["grad_bytes_recv"] = sum(len(b) for b in blobs)
+            self.steps += 1
+            return data
         self.write_presence()
         t = time.perf_counter()
         if self.cuda:
@@ -433,6 +539,21 @@ class PSSyncEngine(Engine):
     def step(self):
         data = {}
         data["code_wait"] = self.encode_all()
+        if self.is_object:
+            t = time.perf_counter()
+            blobs = self.object_exchange(0)  # igather to the PS (mpi_comms.py:60-117)
+            data["comm_wait"] = data["isend_time"] = time.perf_counter() - t
+            t = time.perf_counter()
+            data["decode_time"] = 0.0
+            if self.world.is_ps:
+                self.object_apply(blobs, self.store.data, self.pub, self.gscale(self.world.size))
+                data["decode_time"] = self._decode_time
+            data["optim_step_time"] = time.perf_counter() - t
+            self._bcast_params(data)
+            data.update(self.step_metrics())
+            data.update(self.bytes_per_step())
+            self.steps += 1
+            return data
         self.write_presence()
         t = time.perf_counter()
         cs = self.comm_stream
@@ -452,24 +573,31 @@ class PSSyncEngine(Engine):
                 self.apply(msgs, self.store.data, self.pub, self.gscale(self.world.size), self._scratch,
                            mask=self.gathered_mask(msgs))
         data["optim_step_time"] = time.perf_counter() - t
-        t = time.perf_counter()
-        # ibroadcast of the parameters (mpi_comms.py:127-133 / README.md:76)
-        with self.tracer.phase("bcast"):
-            if self.pub is not None:
-                broadcast(self.pub, self.world, 0)
-                if not self.world.is_ps:
-                    from hipps import ops
-
-                    ops.convert(self.pub, self.store.data)
-            else:
-                broadcast(self.store.data, self.world, 0)
-        data["bcast_time"] = time.perf_counter() - t
+        self._bcast_params(data)
         data["decode_time"] = 0.0
         data.update(self.step_metrics())
         data.update(self.bytes_per_step())
         data.update(self.tracer.collect())
         self.steps += 1
         return data
+
+
+def _bcast_params_impl(self, data):
+    """ibroadcast of the parameters (mpi_comms.py:127-133 / README.md:76)."""
+    t = time.perf_counter()
+    with self.tracer.phase("bcast"):
+        if self.pub is not None:
+            broadcast(self.pub, self.world, 0)
+            if not self.world.is_ps:
+                from hipps import ops
+
+                ops.convert(self.pub, self.store.data)
+        else:
+            broadcast(self.store.data, self.world, 0)
+    data["bcast_time"] = time.perf_counter() - t
+
+
+PSSyncEngine._bcast_params = _bcast_params_impl
 
 
 class _null:

@@ -90,6 +90,7 @@ class PSAsyncEngine(Engine):
 
     def _setup(self, opt, cfg, store, codec, world):
         C = native()
+        self.object_wire = True  # object codecs travel as [length | blob] mailbox messages
         self._fault = _parse_fault(os.environ.get("HIPPS_FAULT"), world.rank)
         self.C = C
         W = world.size

@@ -160,7 +160,8 @@ def dumps(obj, level: int = 0) -> bytes:
     metas, blobs, off = [], [], 0
     for t in tensors:
         c = t.detach().contiguous().cpu()
-        raw = c.view(torch.uint8).numpy().tobytes() if c.numel() else b""
+        # reshape(-1): a "contiguous" tensor with a size-1 last dim may still carry a stride != 1
+        raw = c.reshape(-1).view(torch.uint8).numpy().tobytes() if c.numel() else b""
         if level:
             raw = zlib.compress(raw, level)
         off = (off + 15) // 16 * 16

@@ -69,14 +69,20 @@ def test_sgd_fused(n, mom, damp, nesterov, wd, W, dt):
         torch.testing.assert_close(bd.cpu(), buf, rtol=1e-5, atol=1e-6)
 
 
-def test_sgd_zero_src():
+@pytest.mark.parametrize("masked", [False, True])
+def test_sgd_zero_src(masked):
+    """The async PS clears its accumulator in the update pass: the update must still use it."""
     n = 4099
     g = torch.randn(n, device=DEV)
     p = torch.randn(n, device=DEV)
-    p0 = p.clone()
-    ops.sgd_step([g], p, None, None, True, 1.0, lr=0.1)
+    want, gc = p.cpu().clone(), g.cpu().clone()
+    mask = torch.ones((n + 15) // 16, dtype=torch.uint8) if masked else None
+    if masked:
+        mask[::3] = 0
+    ref.sgd_step([gc], want, None, None, True, 1.0, lr=0.1, weight_decay=0.01, mask=mask)
+    ops.sgd_step([g], p, None, None, True, 1.0, lr=0.1, weight_decay=0.01, mask=None if mask is None else mask.to(DEV))
     assert g.abs().sum().item() == 0
-    assert not torch.equal(p, p0)
+    torch.testing.assert_close(p.cpu(), want, rtol=1e-6, atol=1e-6)
 
 
 @pytest.mark.parametrize("n", [3, 4096, 65537])
