@@ -33,8 +33,12 @@ class World:
         return self.rank == 0
 
 
-def init_from_env(backend: Optional[str] = None, timeout_s: float = 600.0) -> World:
-    """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* if present; bind rank->GPU."""
+def init_from_env(backend: Optional[str] = None, timeout_s: Optional[float] = None) -> World:
+    """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* if present; bind rank->GPU.
+    ``timeout_s`` (default ``HIPPS_COMM_TIMEOUT_S`` or 600) bounds every collective of the
+    default group; the engines add their own group with ``PSConfig.comm_timeout_s``."""
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("HIPPS_COMM_TIMEOUT_S", "600"))
     backend = backend or os.environ.get("HIPPS_BACKEND") or None  # e.g. gloo to rehearse N ranks on 1 GPU
     rank = int(os.environ.get("RANK", "0"))
     size = int(os.environ.get("WORLD_SIZE", "1"))

@@ -25,6 +25,7 @@ from hipps.utils.tracing import StepTracer
 
 from .dist import World, all_gather_into, barrier, broadcast, gather_into
 from .flat import BucketPlan, FlatStore, _is_dense
+from .watchdog import CommWatchdog, armed
 
 
 class Engine:
@@ -70,6 +71,9 @@ class Engine:
         self.step_present = bytes(len(store.slots))
         self._hooks = []
         self.steps = 0
+        self.group = None  # sync engines: collectives run on a group with cfg.comm_timeout_s
+        self.watchdog: Optional[CommWatchdog] = None
+        self._sync_fault = None
         self._order_log: List[str] = []
         # 'gather': autograd keeps ownership of p.grad (stolen, no per-parameter accumulate kernel,
         # no memset) and each bucket is gathered by ONE multi-tensor kernel; 'flat': p.grad are
@@ -315,11 +319,46 @@ class Engine:
     def step(self) -> Dict[str, float]:
         raise NotImplementedError
 
+    def _init_failure_handling(self):
+        """Sync engines: a process group whose collectives time out after cfg.comm_timeout_s
+        (RCCL communicator abort / gloo error) plus a host watchdog (hipps.parallel.watchdog)."""
+        import datetime
+        import os
+
+        import torch.distributed as dist
+
+        from .ps_async import _parse_fault
+
+        self._sync_fault = _parse_fault(os.environ.get("HIPPS_FAULT"), self.world.rank)
+        if self.world.size > 1 and dist.is_initialized():
+            self.group = dist.new_group(timeout=datetime.timedelta(seconds=self.cfg.comm_timeout_s))
+            self.watchdog = CommWatchdog(self.cfg.comm_timeout_s, self.world.rank)
+
+    def _fault_point(self):
+        """HIPPS_FAULT='rank:step:kind[:arg]' for the sync engines: hang (stop participating, stay
+        alive), die (exit 1), slow:<ms>."""
+        if self._sync_fault is None:
+            return
+        import os
+
+        kind, arg, at = self._sync_fault
+        if self.steps + 1 < at:
+            return
+        if kind == "hang":
+            while True:
+                time.sleep(3600)
+        if kind == "die":
+            os._exit(1)
+        if kind == "slow":
+            time.sleep(arg / 1000.0)
+
     def irequest_params(self, **kw):
         return None
 
     def close(self):
         self.remove_hooks()
+        if self.watchdog is not None:
+            self.watchdog.close()
 
     def engine_state(self) -> dict:
         """Codec state (e.g. error-feedback residuals) of this rank, for checkpoints."""
@@ -353,9 +392,9 @@ class Engine:
         t = torch.tensor([n], dtype=torch.int64, device=dev)
         out = torch.zeros(W, dtype=torch.int64, device=dev)
         if self.world.backend == "nccl":
-            dist.all_gather_into_tensor(out, t)
+            dist.all_gather_into_tensor(out, t, group=self.group)
         else:
-            dist.all_gather(list(out.view(W, 1)), t)
+            dist.all_gather(list(out.view(W, 1)), t, group=self.group)
         return [int(v) for v in out.tolist()]
 
     def object_exchange(self, root: Optional[int]) -> Optional[List[bytes]]:
@@ -379,10 +418,10 @@ class Engine:
         send = send.to(dev)
         if root is None:
             recv = torch.empty(W * slot, dtype=torch.uint8, device=dev)
-            all_gather_into(recv, send, self.world)
+            all_gather_into(recv, send, self.world, group=self.group)
         else:
             recv = torch.empty(W * slot, dtype=torch.uint8, device=dev) if self.world.rank == root else None
-            gather_into(recv, send, self.world, dst=root)
+            gather_into(recv, send, self.world, dst=root, group=self.group)
             if self.world.rank != root:
                 return None
         host = recv.cpu().numpy()
@@ -475,10 +514,16 @@ class AllGatherEngine(Engine):
         W = self.world.size
         self.gathered = torch.empty(W * self.wire_total, dtype=torch.uint8, device=self.store.device)
         self._scratch = None if self.plan.dense_ok else torch.empty_like(self.store.grad)
+        self._init_failure_handling()
 
     def step(self):
+        with armed(self.watchdog, f"allgather step {self.steps + 1}"):
+            return self._step()
+
+    def _step(self):
         data = {}
         data["code_wait"] = self.encode_all()
+        self._fault_point()
         self._check_order()
         if self.is_object:  # ps.py:140-190: size round, payload all-gather, decode W codes, sum, step
             t = time.perf_counter()
@@ -497,11 +542,11 @@ class AllGatherEngine(Engine):
         t = time.perf_counter()
         if self.cuda:
             with torch.cuda.stream(self.comm_stream), self.tracer.phase("comm", self.comm_stream):
-                all_gather_into(self.gathered, self.wire, self.world)
+                all_gather_into(self.gathered, self.wire, self.world, group=self.group)
             torch.cuda.current_stream(self.store.device).wait_stream(self.comm_stream)
         else:
             with self.tracer.phase("comm"):
-                all_gather_into(self.gathered, self.wire, self.world)
+                all_gather_into(self.gathered, self.wire, self.world, group=self.group)
         data["isend_time"] = data["comm_wait"] = time.perf_counter() - t
         t = time.perf_counter()
         n = self.wire_total
@@ -535,10 +580,16 @@ class PSSyncEngine(Engine):
         self.pub = None
         if self.cfg.param_wire == "bf16":
             self.pub = torch.empty(self.store.numel, dtype=torch.bfloat16, device=dev)
+        self._init_failure_handling()
 
     def step(self):
+        with armed(self.watchdog, f"ps_sync step {self.steps + 1}"):
+            return self._step()
+
+    def _step(self):
         data = {}
         data["code_wait"] = self.encode_all()
+        self._fault_point()
         if self.is_object:
             t = time.perf_counter()
             blobs = self.object_exchange(0)  # igather to the PS (mpi_comms.py:60-117)
@@ -560,7 +611,7 @@ class PSSyncEngine(Engine):
         ctx = torch.cuda.stream(cs) if self.cuda else _null()
         self.verify_guards([self.wire], "encode")
         with ctx, self.tracer.phase("comm", cs):
-            gather_into(self.gathered if self.world.is_ps else None, self.wire, self.world)
+            gather_into(self.gathered if self.world.is_ps else None, self.wire, self.world, group=self.group)
         if self.cuda:
             torch.cuda.current_stream(self.store.device).wait_stream(cs)
         data["comm_wait"] = data["isend_time"] = time.perf_counter() - t
@@ -587,13 +638,13 @@ def _bcast_params_impl(self, data):
     t = time.perf_counter()
     with self.tracer.phase("bcast"):
         if self.pub is not None:
-            broadcast(self.pub, self.world, 0)
+            broadcast(self.pub, self.world, 0, group=self.group)
             if not self.world.is_ps:
                 from hipps import ops
 
                 ops.convert(self.pub, self.store.data)
         else:
-            broadcast(self.store.data, self.world, 0)
+            broadcast(self.store.data, self.world, 0, group=self.group)
     data["bcast_time"] = time.perf_counter() - t
 
 

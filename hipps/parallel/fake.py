@@ -1,0 +1,141 @@
+"""In-process fake transport for the async PS protocol (SURVEY.md §4 tier 3).
+
+Runs the real protocol core (hipps.parallel.ps_core.PSCore) against a dict-backed control block
+and a Python mailbox, with the test deciding the exact order in which worker messages reach the
+PS.  Any-source arrival orders, staleness drops, M-accumulation with fast workers, dead workers
+and mailbox flow control become deterministic unit tests instead of multi-process timing.
+
+    fake = FakeAsyncPS(W=3, nb=2, M=3, staleness=1)
+    fake.push_step(1, grads=[0.5, 0.25])        # worker 1, computed on its adopted version
+    fake.deliver(1)                             # PS consumes whatever worker 1 pushed
+    fake.pull(1)                                # worker adopts the newest published version
+"""
+from __future__ import annotations
+
+from types import SimpleNamespace
+from typing import Dict, List, Optional, Sequence
+
+from .ps_core import PSCore
+
+# same field ids as hipps/csrc/runtime/control.cpp
+FIELDS = SimpleNamespace(F_PUSH_SEQ=0, F_ACK_SEQ=1, F_PUSH_VER=2, F_APPLIED_VER=3, F_STOP=4, F_HEARTBEAT=5,
+                         F_INCL_SEQ=6, F_PUSH_FLAG=7, F_READING=8, F_PUB_VER=10, F_PS_STOP=11, F_ERROR=12,
+                         F_DROPS=13, F_UPDATES=14, F_BUF_VER=15)
+
+
+class FakeControl:
+    """The ControlBlock word API on a dict (no shared memory, no atomics needed: one thread)."""
+
+    def __init__(self):
+        self.words: Dict[tuple, int] = {}
+
+    def load(self, field: int, idx: int) -> int:
+        return self.words.get((field, idx), 0)
+
+    def store(self, field: int, idx: int, v: int):
+        self.words[(field, idx)] = int(v)
+
+    def fetch_add(self, field: int, idx: int, v: int) -> int:
+        old = self.load(field, idx)
+        self.store(field, idx, old + v)
+        return old
+
+
+class WouldBlock(Exception):
+    """A worker tried to reuse a mailbox slot the PS has not consumed (it would wait here)."""
+
+
+class FakeAsyncPS:
+    MAXSLOTS = 64
+
+    def __init__(self, W: int, nb: int = 1, M: Optional[int] = None, staleness: int = -1,
+                 staleness_lr: bool = False, slots: int = 4, lr: float = 1.0, average: bool = False):
+        self.W, self.nb, self.SLOTS = W, nb, slots
+        self.M = M if M else W
+        self.lr = lr
+        self.ctl = FakeControl()
+        F = FIELDS
+        self.core = PSCore(self.ctl, F, W, nb, list(range(nb))[::-1], slots, self.MAXSLOTS, self.M, staleness,
+                           staleness_lr, 1.0 / self.M if average else 1.0)
+        self.core.backend = self
+        self.mail: Dict[tuple, float] = {}  # (worker, slot) -> gradient value of that bucket
+        self.acc = [0.0] * nb
+        self.params = [0.0] * nb  # published parameters, one scalar per bucket
+        self.history: List[dict] = []  # one record per PS update
+        self.accumulated: List[tuple] = []  # (worker, step, bucket, scale) in PS order
+        self._cur: List[tuple] = []
+        self.seq = [0] * W
+        self.local_ver = [0] * W
+        self.steps = [0] * W
+        self.ctl.store(F.F_PUB_VER, 0, 0)
+
+    # ---- worker side ------------------------------------------------------------------------
+    def push_step(self, i: int, grads: Sequence[float], version: Optional[int] = None, partial: bool = False):
+        """Worker i pushes one step (nb bucket messages in ready order) computed on ``version``
+        (default: the version it adopted last)."""
+        F = FIELDS
+        assert len(grads) == self.nb
+        ver = self.local_ver[i] if version is None else version
+        for pos in range(self.nb):
+            s = self.seq[i] + 1
+            if s > self.SLOTS and self.ctl.load(F.F_ACK_SEQ, i) < s - self.SLOTS:
+                raise WouldBlock(f"worker {i} message {s}: slot {s % self.SLOTS} not yet consumed")
+            slot = s % self.SLOTS
+            bi = self.core.order[pos]
+            self.mail[(i, slot)] = float(grads[bi])
+            vidx = i * self.MAXSLOTS + slot
+            self.ctl.store(F.F_PUSH_VER, vidx, ver)
+            self.ctl.store(F.F_PUSH_FLAG, vidx, 1 if (partial and pos == self.nb - 1) else 0)
+            self.ctl.store(F.F_PUSH_SEQ, i, s)
+            self.seq[i] = s
+        self.steps[i] += 1
+
+    def pull(self, i: int) -> int:
+        """AsySG-InCon read: adopt the newest published version."""
+        self.local_ver[i] = self.ctl.load(FIELDS.F_PUB_VER, 0)
+        return self.local_ver[i]
+
+    def stop(self, i: int):
+        self.ctl.store(FIELDS.F_STOP, i, self.seq[i] + 1)
+
+    def included(self, i: int) -> int:
+        return self.ctl.load(FIELDS.F_INCL_SEQ, i)
+
+    # ---- PS side ----------------------------------------------------------------------------
+    def deliver(self, i: int) -> int:
+        return self.core.pump(i)
+
+    def deliver_order(self, order: Sequence[int]):
+        for i in order:
+            self.deliver(i)
+
+    def accumulate(self, i, slot, bi, seq, scale):
+        self.acc[bi] += scale * self.mail[(i, slot)]
+        step = (seq - 1) // self.nb + 1
+        self.accumulated.append((i, step, bi, scale))
+        self._cur.append((i, step))
+
+    def note_presence(self, i, slot, vidx):
+        pass
+
+    def ack(self, i, seq):
+        self.ctl.store(FIELDS.F_ACK_SEQ, i, seq)
+
+    def update(self, included, gscale):
+        F = FIELDS
+        for b in range(self.nb):
+            self.params[b] -= self.lr * gscale * self.acc[b]
+            self.acc[b] = 0.0
+        v = self.core.ver
+        self.ctl.store(F.F_PUB_VER, 0, v)
+        for i, s in self.core.last_included(included).items():
+            self.ctl.store(F.F_INCL_SEQ, i, s)
+        self.ctl.fetch_add(F.F_UPDATES, 0, 1)
+        contrib = sorted({(i, st) for i, st in self._cur})
+        self._cur = []
+        self.history.append({"version": v, "params": list(self.params), "contributors": contrib,
+                             "included": dict(self.core.last_included(included))})
+
+    @property
+    def stats(self):
+        return dict(self.core.stats, updates=self.ctl.load(FIELDS.F_UPDATES, 0), version=self.core.ver)

@@ -50,6 +50,7 @@ from hipps import ops
 from hipps.ops._native import native
 from .dist import barrier
 from .engine import Engine
+from .ps_core import PSCore
 
 TIMEOUT_US = int(float(os.environ.get("HIPPS_TIMEOUT_S", "600")) * 1e6)
 RING = 4  # per-step "version this gradient was computed on" ring (device pull mode)
@@ -174,9 +175,9 @@ class PSAsyncEngine(Engine):
             self.master = store.data.detach().clone()
             self.acc = torch.zeros_like(store.data)
             self.ps_stream = torch.cuda.Stream(device=store.device) if self.cuda else None
-            self.ver = 0
-            self._count = 0
-            self._pending_incl: List[tuple] = []
+            self.core = PSCore(self.ctl, C, W, self.nb, self.order, self.SLOTS, self.MAXSLOTS, self.M,
+                               cfg.staleness, cfg.staleness_lr, self.gscale(self.M), self._stats)
+            self.core.backend = self
             self._pres_full = False
             self._pres_part = None
             self._publish_initial()
@@ -280,60 +281,44 @@ class PSAsyncEngine(Engine):
             self.ctl.store(self.C.F_ERROR, 0, 1)
 
     def _serve(self):
-        """PS loop.  Message s of worker i is bucket order[(s-1) % nb] of that worker's step
-        (s-1)//nb + 1; a step's first bucket carries the parameter version it was computed on,
-        its last bucket whether the step left parameters without a gradient.  Counting is in
-        whole worker-steps (M per update, README.md:65-73); every bucket gradient that has
-        arrived is applied exactly once."""
-        C, W, nb = self.C, self.W, self.nb
-        seen = [0] * W
-        dropping = [False] * W
-        scale = [1.0] * W
-        st = self.ps_stream
+        """PS loop: wait on every worker's push word at once (the ANY_SOURCE), hand what arrived
+        to the protocol core (hipps.parallel.ps_core), which calls back into accumulate /
+        note_presence / ack / update below -- all enqueued on the PS stream."""
+        core = self.core
         with torch.no_grad():
             while True:
-                ready = self.ctl.wait_any(seen, 20000)
+                ready = self.ctl.wait_any(core.seen, 20000)
                 for i in ready:
-                    s_now = self.ctl.load(C.F_PUSH_SEQ, i)
-                    for s in range(seen[i] + 1, s_now + 1):
-                        slot = s % self.SLOTS
-                        pos = (s - 1) % nb
-                        bi = self.order[pos]
-                        vidx = i * self.MAXSLOTS + slot
-                        if pos == 0:
-                            pv = self.ctl.load(C.F_PUSH_VER, vidx)
-                            stale = self.ver - pv
-                            dropping[i] = 0 <= self.cfg.staleness < stale
-                            scale[i] = 1.0 / max(1, stale) if self.cfg.staleness_lr else 1.0
-                            if not dropping[i]:
-                                self._stats["staleness_sum"] += max(0, stale)
-                        if not dropping[i]:
-                            b = self.plan.buckets[bi]
-                            if self.plan.guarded:
-                                self._verify_slot(i, slot, bi, s)
-                            with self.tracer.phase("ps_accumulate", st):
-                                self.codec.accumulate([self._bucket_msg(bi, self.slot_buf(i, slot))],
-                                                      self.acc[b.lo:b.hi], scale[i], True)
-                            if pos == nb - 1:
-                                self._note_presence(i, slot, vidx)
-                        self._ring(st, [(C.F_ACK_SEQ, i, s)])  # stream-ordered: acks stay monotonic
-                        if pos == nb - 1:
-                            self._pending_incl.append((i, s))  # a dropped step still counts for max_delay
-                            if dropping[i]:
-                                self._stats["drops"] += 1
-                                self.ctl.fetch_add(C.F_DROPS, 0, 1)
-                            else:
-                                self._stats["accumulated"] += 1
-                                self._count += 1
-                                if self._count >= self.M:
-                                    self._update(self._pending_incl, self.gscale(self.M))
-                                    self._pending_incl = []
-                                    self._count = 0
-                    seen[i] = s_now
+                    core.pump(i)
                 if self._pause_req.is_set():
                     self._hold()
-                if self._should_stop(seen):
+                if core.should_stop(self.dead_workers()):
                     break
+
+    # ---- PSCore backend (data plane on the PS stream) ----------------------------------------
+    def accumulate(self, i: int, slot: int, bi: int, seq: int, scale: float):
+        b = self.plan.buckets[bi]
+        if self.plan.guarded:
+            self._verify_slot(i, slot, bi, seq)
+        with self.tracer.phase("ps_accumulate", self.ps_stream):
+            self.codec.accumulate([self._bucket_msg(bi, self.slot_buf(i, slot))], self.acc[b.lo:b.hi], scale, True)
+
+    def ack(self, i: int, seq: int):
+        self._ring(self.ps_stream, [(self.C.F_ACK_SEQ, i, seq)])  # stream-ordered: acks stay monotonic
+
+    def note_presence(self, i: int, slot: int, vidx: int):
+        self._note_presence(i, slot, vidx)
+
+    def update(self, included, gscale):
+        self._update(included, gscale)
+
+    @property
+    def ver(self) -> int:
+        return self.core.ver
+
+    @ver.setter
+    def ver(self, v: int):
+        self.core.ver = v
 
     def _note_presence(self, i: int, slot: int, vidx: int):
         """OR the step's presence into this update's mask (skip_missing_grads)."""
@@ -358,8 +343,7 @@ class PSAsyncEngine(Engine):
 
     def _update(self, included, gscale):
         C = self.C
-        self.ver += 1
-        b = self.ver % self.NPUB
+        b = self.ver % self.NPUB  # PSCore advanced the version
         old = self.ctl.load(C.F_BUF_VER, b)
         self.ctl.store(C.F_BUF_VER, b, -1)  # readers skip a buffer being rewritten ...
         if old >= 0 and not self.ctl.wait_no_reader(old, 0):  # ... and it waits for current readers
@@ -375,27 +359,12 @@ class PSAsyncEngine(Engine):
         st = self.ps_stream
         # order matters: buffer stamp -> version word -> per-worker "included" words, so a worker
         # that sees its message included also sees a version containing it
-        last = {}
-        for i, s in included:
-            last[i] = max(last.get(i, 0), s)
+        last = self.core.last_included(included)
         words = [(C.F_BUF_VER, b, self.ver), (C.F_PUB_VER, 0, self.ver)] + [(C.F_INCL_SEQ, i, s)
                                                                            for i, s in last.items()]
         for k in range(0, len(words), 6):
             self._ring(st, words[k:k + 6])
         self.ctl.fetch_add(C.F_UPDATES, 0, 1)
-
-    def _should_stop(self, seen):
-        C = self.C
-        if self.ctl.load(C.F_PS_STOP, 0):
-            return True
-        dead = set(self.dead_workers())
-        for i in range(self.W):
-            if i in dead:
-                continue  # failure detection: a silent worker does not hold the PS open
-            stop = self.ctl.load(C.F_STOP, i)
-            if stop == 0 or seen[i] < stop - 1:
-                return False
-        return True
 
     def dead_workers(self) -> List[int]:
         """Ranks whose heartbeat is older than cfg.dead_after_s and that never said STOP."""
@@ -708,7 +677,7 @@ class PSAsyncEngine(Engine):
         if self.rank == 0:
             self.ps_stream.synchronize() if self.cuda else None
             d.update({"master": self.master.detach().cpu(), "version": self.ver, "acc": self.acc.detach().cpu(),
-                      "acc_count": self._count})
+                      "acc_count": self.core.count})
         return d
 
     def load_engine_state(self, d: dict):
@@ -725,7 +694,7 @@ class PSAsyncEngine(Engine):
                 self.master.copy_(d["master"].to(self.master.device))
                 if "acc" in d:
                     self.acc.copy_(d["acc"].to(self.acc.device))
-                    self._count = int(d.get("acc_count", 0))
+                    self.core.count = int(d.get("acc_count", 0))
                 self.ver = int(d["version"])
                 b = self.ver % self.NPUB
                 ops.convert(self.master, self.pub_buf(b))

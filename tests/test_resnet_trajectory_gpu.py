@@ -4,7 +4,8 @@
   wgrad/dgrad, HIP max pool, fused SGD kernel) vs plain PyTorch (every fusion off, MIOpen
   convs, eager BN, torch.optim.SGD): per-step losses agree within 2 % while the loss is
   above 0.1 (after that both are ~1e-3 and relative error is noise), and both fall;
-* ps_async at N=1 with max_delay=0 (rank 0 = PS + worker) is bit-identical to mode='local';
+* ps_async at N=1 with max_delay=0 (rank 0 = PS + worker) is bit-identical to mode='local'
+  (8 steps with MIOpen's deterministic algorithms: its default ones use atomics);
 * free-running ps_async (GPU-time pull) still trains the batch down.
 
 The fusion switches are read at import, so each side runs in a fresh child process.
@@ -30,8 +31,9 @@ def _run(args, out, timeout=420):
 
 
 def test_resnet50_fused_trains_like_plain_pytorch(tmp_path):
-    fused = _run(["--runs", "local,async_md0,async"], str(tmp_path / "fused.json"))
+    fused = _run(["--runs", "local,async"], str(tmp_path / "fused.json"))
     plain = _run(["--plain"], str(tmp_path / "plain.json"))["plain"]
+    det = _run(["--runs", "local,async_md0", "--steps", "8", "--deterministic"], str(tmp_path / "det.json"))
     a, b = fused["local"]["losses"], plain["losses"]
     assert len(a) == len(b) == 40
     checked = 0
@@ -43,8 +45,8 @@ def test_resnet50_fused_trains_like_plain_pytorch(tmp_path):
     assert checked >= 20
     assert a[-1] < 0.5 * a[0] and b[-1] < 0.5 * b[0]
     # N=1 async PS with max_delay=0 applies exactly the local update sequence
-    assert fused["async_md0"]["param_sha"] == fused["local"]["param_sha"]
-    assert fused["async_md0"]["losses"] == fused["local"]["losses"]
+    assert det["async_md0"]["param_sha"] == det["local"]["param_sha"]
+    assert det["async_md0"]["losses"] == det["local"]["losses"]
     # free-running AsySG-InCon: staleness bounded by the pipeline, and the loss still falls
     fr = fused["async"]
     assert fr["ps"]["doorbells"] == "device" and fr["ps"]["pull"] == "device"

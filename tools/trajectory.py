@@ -44,6 +44,7 @@ def parse(argv=None):
     ap.add_argument("--bf16-weights", default="off", choices=["on", "off", "auto"])
     ap.add_argument("--plain", action="store_true", help="all fusions off + torch.optim.SGD")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--deterministic", action="store_true", help="MIOpen deterministic algorithms (slow)")
     ap.add_argument("--out", default=None)
     return ap.parse_args(argv)
 
@@ -71,7 +72,7 @@ def main(argv=None):
     import torch.nn.functional as F
 
     torch.backends.cudnn.benchmark = False
-    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.deterministic = a.deterministic
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     from hipps.models import build_model
