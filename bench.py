@@ -49,7 +49,9 @@ def parse():
     ap.add_argument("--accumulate", type=int, default=0, help="PS update every M grads (0 = world size)")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--seq", type=int, default=512, help="sequence length (transformer configs)")
-    ap.add_argument("--param-wire", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--param-wire", default="auto", choices=["auto", "fp32", "bf16"],
+                    help="published-parameter dtype: auto = fp32 at N=1 (local pull), bf16 at N>1 (halves the "
+                         "xGMI pull; the PS keeps the fp32 master, workers compute in bf16 anyway)")
     ap.add_argument("--momentum", type=float, default=0.9)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--no-channels-last", action="store_true")
@@ -90,6 +92,8 @@ def main():
         y = torch.randint(0, 1000, (a.batch,), device=dev)
 
     mode = a.mode if N > 1 or a.mode in ("ps_async", "local") else "local"
+    if a.param_wire == "auto":
+        a.param_wire = "bf16" if N > 1 else "fp32"
     note = None
     try:
         opt = hipps.SGD(model.named_parameters(), lr=a.lr, momentum=a.momentum, weight_decay=5e-5, mode=mode,

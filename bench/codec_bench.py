@@ -27,22 +27,65 @@ from hipps import codecs  # noqa: E402
 SPECS = ["fp32", "bf16", "int8", "int8_sr", "topk:0.01", "topk_bf16:0.01", "topk_int8:0.01", "threshold:0.02:0.05"]
 
 
-def timed(fn, dev, iters):
+_FLUSH = None
+
+
+def _flush(dev):
+    """Evict the 256 MB MALL (and L2s) between timed iterations: write a 512 MB buffer."""
+    global _FLUSH
+    if _FLUSH is None:
+        _FLUSH = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+    _FLUSH.fill_(1)
+
+
+def timed(fn, dev, iters, cold=True):
     for _ in range(3):
         fn()
     if dev.type == "cuda":
         torch.cuda.synchronize()
-        s, e = torch.cuda.Event(True), torch.cuda.Event(True)
-        s.record()
+        if not cold:
+            s, e = torch.cuda.Event(True), torch.cuda.Event(True)
+            s.record()
+            for _ in range(iters):
+                fn()
+            e.record()
+            torch.cuda.synchronize()
+            return s.elapsed_time(e) * 1e3 / iters  # us
+        tot = 0.0
+        evs = []
         for _ in range(iters):
+            _flush(dev)
+            s, e = torch.cuda.Event(True), torch.cuda.Event(True)
+            s.record()
             fn()
-        e.record()
+            e.record()
+            evs.append((s, e))
         torch.cuda.synchronize()
-        return s.elapsed_time(e) * 1e3 / iters  # us
+        for s, e in evs:
+            tot += s.elapsed_time(e)
+        return tot * 1e3 / iters
     t = time.perf_counter()
     for _ in range(iters):
         fn()
     return (time.perf_counter() - t) * 1e6 / iters
+
+
+def _enc_bytes(spec, n, wire, ef):
+    """Minimum HBM traffic of one encode as the kernels are built (reads + writes), for the
+    effective-bandwidth column: dense casts read x and write the wire; int8 with error feedback
+    also reads and rewrites the residual; top-k makes three full passes (P1 fold: x, r read + r
+    written; P2 filter: r read; P5 compaction: r read) plus the small candidate passes."""
+    f = 4 * n
+    name = spec.split(":")[0]
+    if name in ("fp32", "bf16"):
+        return f + wire
+    if name.startswith("int8"):
+        return f + wire + (2 * f if ef else 0)
+    if name.startswith("topk"):
+        return (3 * f if ef else f) + 2 * f + wire
+    if name.startswith("thresh"):
+        return (3 * f if ef else 0) + f + wire
+    return f + wire
 
 
 def main():
@@ -50,13 +93,15 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--sizes", default="10,100,1000,10000,1000000,25557032")
+    ap.add_argument("--warm", action="store_true", help="do not flush the MALL between iterations")
+    ap.add_argument("--specs", default=",".join(SPECS))
     a = ap.parse_args()
     dev = torch.device("cpu" if a.cpu or not torch.cuda.is_available() else "cuda")
     sizes = [int(s) for s in a.sizes.split(",")]
     rows = []
     for n in sizes:
         x = torch.randn(n, device=dev) * 1e-2
-        for spec in SPECS:
+        for spec in a.specs.split(","):
             c = codecs.get_codec(spec)
             lay = c.layout(n)
             buf = torch.empty(lay.nbytes, dtype=torch.uint8, device=dev)
@@ -66,11 +111,15 @@ def main():
             iters = 200 if n <= 1_000_000 else 30
             if dev.type == "cpu" and n > 1_000_000:
                 iters = 3
-            enc = timed(lambda: c.encode_into(x, views, st), dev, iters)
-            dec = timed(lambda: c.accumulate([views], acc, 1.0, True), dev, iters)
-            row = {"n": n, "codec": spec, "device": dev.type, "encode_us": round(enc, 2), "decode_acc_us": round(dec, 2),
+            cold = not a.warm and dev.type == "cuda"
+            enc = timed(lambda: c.encode_into(x, views, st), dev, iters, cold)
+            dec = timed(lambda: c.accumulate([views], acc, 1.0, True), dev, iters, cold)
+            moved = _enc_bytes(spec, n, lay.nbytes, "resid" in st)
+            row = {"n": n, "codec": spec, "device": dev.type, "cache": "cold" if cold else "warm",
+                   "encode_us": round(enc, 2), "decode_acc_us": round(dec, 2),
                    "wire_bytes": lay.nbytes, "bytes_per_elem": round(lay.nbytes / n, 4),
-                   "encode_GBps_in": round(n * 4 / enc / 1e3, 1)}
+                   "encode_GBps_in": round(n * 4 / enc / 1e3, 1),
+                   "encode_bytes_moved_model": moved, "encode_TBps_model": round(moved / enc / 1e6, 2)}
             rows.append(row)
             print(json.dumps(row), flush=True)
     # reference method for the same payload sizes (host pickle of a float32 numpy array)

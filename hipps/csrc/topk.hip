@@ -1,16 +1,24 @@
-// hipps — exact top-k magnitude sparsification (radix select + deterministic compaction).
+// hipps — exact top-k magnitude sparsification (radix select + look-back compaction).
 //
 // Device replacement for the external codec's encode (ps.py:94) when the codec is top-k.
 // Output is a fixed-size message (k = ceil(ratio*n) known at plan time), so no size round-trip
 // is needed: the reference's per-tensor Iallgather of lengths (mpi_comms.py:150-158, M1) goes
 // away.  Wire: int32 idx[k] + val[k] (f32 or bf16), idx in ascending order.
 //
-// Pipeline (all stream-ordered, no host sync):
-//   hist(bits 30..20) -> pick -> hist(19..9) -> pick -> hist(8..0) -> pick   (exact k-th |x|)
-//   count per 1024-element chunk (> T, == T) -> exclusive scan -> write  (index order; ties
-//   admitted lowest-index-first, so the message is bitwise deterministic)
-// Optional error feedback: pass 0 folds the residual in (r <- g + r) and the write pass clears
-// the residual at transmitted positions (r[i] <- x - wire(x)).
+// Three full passes over the bucket (round 1 made five), everything else on ~1% of it:
+//   P1  hist of |x| bits 30..20 over the whole bucket (fused with the error-feedback fold
+//       r <- g + r, so later passes read one array)                               [full read]
+//   pick   single workgroup: the bin holding the k-th largest key
+//   P2  filter: keys in that bin -> candidate list (wave-aggregated append)         [full read]
+//   P3/P4  histograms of bits 19..9 and 8..0 over the candidates only, + picks -> exact k-th
+//       key T and how many == T to admit (lowest index first)
+//   P5  single-pass compaction with decoupled look-back: each 4096-element chunk takes a
+//       ticket, counts (> T, == T), publishes its aggregate, sums its predecessors' and writes
+//       its selected (index, value) pairs in index order                          [full read]
+// If the threshold bin holds more candidates than the list can take (e.g. mostly-zero
+// gradients) the candidate passes fall back to filtering the whole bucket (flag in device
+// state, no host sync).  Ties are admitted lowest-index-first, so the message is bitwise
+// deterministic and equal to the CPU reference.
 #include "common.h"
 
 #include <ATen/ATen.h>
@@ -23,30 +31,47 @@
 namespace hipps {
 
 constexpr int kHistBins = 2048;
-constexpr int kChunk = 1024;  // elements per compaction chunk = 256 lanes x float4
+constexpr int kCompactPer = 16;                     // elements per lane in P5 (4 x float4)
+constexpr int kChunk = kBlock * kCompactPer;        // 4096 elements per look-back chunk
 
 struct SelState {        // lives in a small device workspace
   uint32_t prefix;       // selected high bits of the k-th largest key
   uint32_t mask;         // which bits of prefix are decided
   uint32_t remaining;    // how many elements still to take inside the undecided bucket
+  uint32_t ncand;        // candidates appended by P2
+  uint32_t overflow;     // candidate list too small: later passes scan the whole bucket
+  uint32_t ticket;       // P5 chunk tickets
+  uint32_t cap_cand;
   uint32_t pad;
   uint32_t hist[kHistBins];
 };
 
 __device__ __forceinline__ uint32_t absbits(float x) { return __float_as_uint(x) & 0x7fffffffu; }
 
-__global__ __launch_bounds__(kBlock) void k_topk_init(SelState* __restrict__ st, uint32_t k) {
-  if (threadIdx.x == 0) { st->prefix = 0; st->mask = 0; st->remaining = k; st->pad = 0; }
-  for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) st->hist[b] = 0;
+__global__ __launch_bounds__(kBlock) void k_topk_init(SelState* __restrict__ st, uint32_t prefix, uint32_t mask,
+                                                      uint32_t k, uint32_t cap_cand,
+                                                      unsigned long long* __restrict__ flags, int64_t nchunks) {
+  if (blockIdx.x == 0) {
+    if (threadIdx.x == 0) {
+      st->prefix = prefix; st->mask = mask; st->remaining = k; st->ncand = 0; st->overflow = 0; st->ticket = 0;
+      st->cap_cand = cap_cand; st->pad = 0;
+    }
+    for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) st->hist[b] = 0;
+  }
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks; c += (int64_t)gridDim.x * blockDim.x)
+    flags[c] = 0ull;
 }
 
-// pass p histogram over elements whose decided bits match prefix
+// P1 (and the overflow fallback of P3/P4): histogram over elements whose decided bits match
+// prefix.  Four per-wave LDS sub-histograms cut same-address atomic serialisation 4x.
 __global__ __launch_bounds__(kBlock) void k_topk_hist(const float* __restrict__ g, float* __restrict__ resid,
                                                       int fold_resid, int64_t n, int lo, int nbits,
-                                                      SelState* __restrict__ st) {
-  __shared__ uint32_t h[kHistBins];
+                                                      SelState* __restrict__ st, int only_overflow) {
+  __shared__ uint32_t h[4][kHistBins];
+  if (only_overflow && !st->overflow) return;
   const int nb = 1 << nbits;
-  for (int b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
+  const int w = threadIdx.x >> 6;
+  for (int b = threadIdx.x; b < 4 * kHistBins; b += blockDim.x) (&h[0][0])[b] = 0;
   __syncthreads();
   const uint32_t prefix = st->prefix, mask = st->mask;
   const float* src = (resid && !fold_resid) ? resid : g;
@@ -60,22 +85,24 @@ __global__ __launch_bounds__(kBlock) void k_topk_hist(const float* __restrict__ 
       *reinterpret_cast<float4*>(resid + i) = x;
     }
     const uint32_t k0 = absbits(x.x), k1 = absbits(x.y), k2 = absbits(x.z), k3 = absbits(x.w);
-    if ((k0 & mask) == prefix) atomicAdd(&h[(k0 >> lo) & (nb - 1)], 1u);
-    if ((k1 & mask) == prefix) atomicAdd(&h[(k1 >> lo) & (nb - 1)], 1u);
-    if ((k2 & mask) == prefix) atomicAdd(&h[(k2 >> lo) & (nb - 1)], 1u);
-    if ((k3 & mask) == prefix) atomicAdd(&h[(k3 >> lo) & (nb - 1)], 1u);
+    if ((k0 & mask) == prefix) atomicAdd(&h[w][(k0 >> lo) & (nb - 1)], 1u);
+    if ((k1 & mask) == prefix) atomicAdd(&h[w][(k1 >> lo) & (nb - 1)], 1u);
+    if ((k2 & mask) == prefix) atomicAdd(&h[w][(k2 >> lo) & (nb - 1)], 1u);
+    if ((k3 & mask) == prefix) atomicAdd(&h[w][(k3 >> lo) & (nb - 1)], 1u);
   }
   if (blockIdx.x == 0) {
     for (int64_t i = (nv << 2) + threadIdx.x; i < n; i += blockDim.x) {
       float x = src[i];
       if (fold_resid) { x += resid[i]; resid[i] = x; }
       const uint32_t k = absbits(x);
-      if ((k & mask) == prefix) atomicAdd(&h[(k >> lo) & (nb - 1)], 1u);
+      if ((k & mask) == prefix) atomicAdd(&h[w][(k >> lo) & (nb - 1)], 1u);
     }
   }
   __syncthreads();
-  for (int b = threadIdx.x; b < nb; b += blockDim.x)
-    if (h[b]) atomicAdd(&st->hist[b], h[b]);
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    const uint32_t c = h[0][b] + h[1][b] + h[2][b] + h[3][b];
+    if (c) atomicAdd(&st->hist[b], c);
+  }
 }
 
 // single workgroup: locate the bucket holding the remaining-th largest key, descend one digit
@@ -117,117 +144,238 @@ __global__ __launch_bounds__(kBlock) void k_topk_pick(int lo, int nbits, SelStat
   }
 }
 
-__device__ __forceinline__ void wg_counts(uint32_t gt, uint32_t eq, uint32_t* red, uint32_t& tg, uint32_t& te) {
-  // 256 threads, 4 waves: reduce two counters
-  float a = (float)gt, b = (float)eq;  // counts <= 4 per thread -> exact in f32 sums up to 2^24
-  a = wave_sum(a);
-  b = wave_sum(b);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { red[w] = (uint32_t)a; red[4 + w] = (uint32_t)b; }
-  __syncthreads();
-  tg = red[0] + red[1] + red[2] + red[3];
-  te = red[4] + red[5] + red[6] + red[7];
-  __syncthreads();
-}
-
-__global__ __launch_bounds__(kBlock) void k_topk_count(const float* __restrict__ src, int64_t n,
-                                                       const SelState* __restrict__ st, uint32_t* __restrict__ cgt,
-                                                       uint32_t* __restrict__ ceq, int64_t nchunks) {
-  __shared__ uint32_t red[8];
-  const uint32_t T = st->prefix;
-  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-    const int64_t i = c * kChunk + threadIdx.x * 4;
-    uint32_t gt = 0, eq = 0;
+// P2: append every element of the selected top-11-bit bin to the candidate list.  One atomic
+// per wave per vector step (wave prefix sum of the lane counts).
+__global__ __launch_bounds__(kBlock) void k_topk_filter(const float* __restrict__ src, int64_t n,
+                                                        SelState* __restrict__ st, uint32_t* __restrict__ ckey,
+                                                        uint32_t* __restrict__ cidx) {
+  const uint32_t prefix = st->prefix, mask = st->mask, cap = st->cap_cand;
+  const int lane = threadIdx.x & 63;
+  const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t nv = (n + 3) >> 2;
+  const int64_t nvw = (nv + 63) & ~(int64_t)63;  // whole waves stay in the loop (ballots)
+  for (int64_t v = gtid; v < nvw; v += stride) {
+    const int64_t i = v << 2;
+    uint32_t k[4] = {0u, 0u, 0u, 0u};
+    bool m[4] = {false, false, false, false};
     if (i + 4 <= n) {
       float4 x = *reinterpret_cast<const float4*>(src + i);
-      const uint32_t k[4] = {absbits(x.x), absbits(x.y), absbits(x.z), absbits(x.w)};
+      k[0] = absbits(x.x); k[1] = absbits(x.y); k[2] = absbits(x.z); k[3] = absbits(x.w);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { gt += k[j] > T; eq += k[j] == T; }
+      for (int j = 0; j < 4; ++j) m[j] = (k[j] & mask) == prefix;
     } else {
+#pragma unroll
       for (int j = 0; j < 4; ++j)
-        if (i + j < n) { const uint32_t k = absbits(src[i + j]); gt += k > T; eq += k == T; }
+        if (i + j < n) { k[j] = absbits(src[i + j]); m[j] = (k[j] & mask) == prefix; }
     }
-    uint32_t tg, te;
-    wg_counts(gt, eq, red, tg, te);
-    if (threadIdx.x == 0) { cgt[c] = tg; ceq[c] = te; }
+    const uint32_t mine = (uint32_t)m[0] + m[1] + m[2] + m[3];
+    // wave-exclusive scan of `mine`, one atomicAdd by the last lane
+    uint32_t incl = mine;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t a = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += a;
+    }
+    const uint32_t total = __shfl(incl, 63, 64);
+    if (total == 0) continue;
+    uint32_t base = 0;
+    if (lane == 63) base = atomicAdd(&st->ncand, total);
+    base = __shfl(base, 63, 64);
+    uint32_t pos = base + incl - mine;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (m[j]) {
+        if (pos < cap) { ckey[pos] = k[j]; cidx[pos] = (uint32_t)(i + j); }
+        ++pos;
+      }
   }
 }
 
-// exclusive scan of both count arrays in place (one workgroup; nchunks ~ n/1024)
-__global__ __launch_bounds__(1024) void k_topk_scan(uint32_t* __restrict__ cgt, uint32_t* __restrict__ ceq,
-                                                    int64_t nchunks, int32_t* __restrict__ count_out,
-                                                    uint32_t cap) {
-  __shared__ uint32_t sg[1024], se[1024];
-  __shared__ uint32_t carry_g, carry_e;
-  if (threadIdx.x == 0) { carry_g = 0; carry_e = 0; }
+// P3/P4: histogram of the candidates; if P2 overflowed the list, of the whole bucket instead
+__global__ __launch_bounds__(kBlock) void k_topk_hist_cand(const uint32_t* __restrict__ ckey,
+                                                           const float* __restrict__ src, int64_t n, int lo, int nbits,
+                                                           SelState* __restrict__ st) {
+  __shared__ uint32_t h[kHistBins];
+  const uint32_t ncand = st->ncand;
+  const bool full = ncand > st->cap_cand;
+  const int nb = 1 << nbits;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
   __syncthreads();
-  for (int64_t base = 0; base < nchunks; base += 1024) {
-    const int64_t c = base + threadIdx.x;
-    const uint32_t vg = c < nchunks ? cgt[c] : 0, ve = c < nchunks ? ceq[c] : 0;
-    sg[threadIdx.x] = vg; se[threadIdx.x] = ve;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
-      uint32_t ag = threadIdx.x >= off ? sg[threadIdx.x - off] : 0;
-      uint32_t ae = threadIdx.x >= off ? se[threadIdx.x - off] : 0;
-      __syncthreads();
-      sg[threadIdx.x] += ag; se[threadIdx.x] += ae;
-      __syncthreads();
+  const uint32_t prefix = st->prefix, mask = st->mask;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if (!full) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < ncand; j += stride) {
+      const uint32_t k = ckey[j];
+      if ((k & mask) == prefix) atomicAdd(&h[(k >> lo) & (nb - 1)], 1u);
     }
-    if (c < nchunks) { cgt[c] = carry_g + sg[threadIdx.x] - vg; ceq[c] = carry_e + se[threadIdx.x] - ve; }
-    __syncthreads();
-    if (threadIdx.x == 1023) { carry_g += sg[1023]; carry_e += se[1023]; }
-    __syncthreads();
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+      const uint32_t k = absbits(src[i]);
+      if ((k & mask) == prefix) atomicAdd(&h[(k >> lo) & (nb - 1)], 1u);
+    }
   }
-  if (count_out && threadIdx.x == 0) count_out[0] = (int32_t)(carry_g < cap ? carry_g : cap);
+  __syncthreads();
+  for (int b = threadIdx.x; b < nb; b += blockDim.x)
+    if (h[b]) atomicAdd(&st->hist[b], h[b]);
+}
+
+// ---- P5: decoupled look-back compaction ---------------------------------------------------
+// Look-back word per chunk: bits 63..62 status (1 aggregate, 2 inclusive prefix), 61..31 the
+// == T count, 30..0 the > T count (n < 2^31).
+constexpr unsigned long long kStAgg = 1ull << 62, kStPre = 2ull << 62;
+__device__ __forceinline__ unsigned long long lb_pack(uint32_t gt, uint32_t eq, unsigned long long st) {
+  return st | ((unsigned long long)eq << 31) | (unsigned long long)gt;
 }
 
 template <typename VT>
-__global__ __launch_bounds__(kBlock) void k_topk_write(const float* __restrict__ src, float* __restrict__ resid,
-                                                       int64_t n, const SelState* __restrict__ st,
-                                                       const uint32_t* __restrict__ pgt,
-                                                       const uint32_t* __restrict__ peq, int64_t nchunks,
-                                                       int32_t* __restrict__ idx, VT* __restrict__ val, uint32_t cap) {
-  __shared__ uint32_t wg[4], we[4];
-  const uint32_t T = st->prefix, need_eq = st->remaining;
+__global__ __launch_bounds__(kBlock) void k_topk_compact(const float* __restrict__ src, float* __restrict__ resid,
+                                                         int64_t n, SelState* __restrict__ st,
+                                                         unsigned long long* __restrict__ flags, int64_t nchunks,
+                                                         int32_t* __restrict__ idx, VT* __restrict__ val, uint32_t cap,
+                                                         int32_t* __restrict__ count_out) {
+  __shared__ uint32_t s_chunk;
+  __shared__ uint32_t wsum[kCompactPer / 4][4];  // per segment, per wave: packed (eq << 16 | gt) totals
+  __shared__ uint32_t s_excl_gt, s_excl_eq;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-    const int64_t i = c * kChunk + threadIdx.x * 4;
-    float x[4];
-    uint32_t k[4];
-    if (i + 4 <= n) {
-      float4 t = *reinterpret_cast<const float4*>(src + i);
-      x[0] = t.x; x[1] = t.y; x[2] = t.z; x[3] = t.w;
-    } else {
-      for (int j = 0; j < 4; ++j) x[j] = (i + j < n) ? src[i + j] : 0.f;
-    }
-    for (int j = 0; j < 4; ++j) k[j] = (i + j < n) ? absbits(x[j]) : 0u;
-    uint32_t gt = 0, eq = 0;
-    for (int j = 0; j < 4; ++j) { gt += (i + j < n) && k[j] > T; eq += (i + j < n) && k[j] == T; }
-    // exclusive scan of (gt, eq) across the workgroup in index order
-    uint32_t sg = gt, se = eq;
-    for (int o = 1; o < 64; o <<= 1) {
-      uint32_t ag = __shfl_up(sg, o, 64), ae = __shfl_up(se, o, 64);
-      if (lane >= o) { sg += ag; se += ae; }
-    }
-    if (lane == 63) { wg[w] = sg; we[w] = se; }
+  const uint32_t T = st->prefix, need_eq = st->remaining;
+  for (;;) {
+    if (threadIdx.x == 0) s_chunk = atomicAdd(&st->ticket, 1u);
     __syncthreads();
-    uint32_t bg = pgt[c], be = peq[c];
-    for (int q = 0; q < w; ++q) { bg += wg[q]; be += we[q]; }
-    bg += sg - gt;
-    be += se - eq;
-    for (int j = 0; j < 4; ++j) {
-      if (i + j >= n) break;
-      const bool isgt = k[j] > T, iseq = k[j] == T;
-      const uint32_t pos = bg + (be < need_eq ? be : need_eq);
-      if ((isgt || (iseq && be < need_eq)) && pos < cap) {
-        idx[pos] = (int32_t)(i + j);
-        Vec4<VT>::store1(val, pos, x[j]);
-        if (resid) resid[i + j] = x[j] - Vec4<VT>::load1(val, pos);
+    const int64_t c = s_chunk;
+    if (c >= nchunks) return;
+    // load 16 elements: segment j covers [c*4096 + j*1024, +1024), lane-contiguous float4s
+    float x[kCompactPer];
+    uint32_t cnt[kCompactPer / 4];  // per segment: (eq << 16) | gt of this thread's 4 elements
+#pragma unroll
+    for (int j = 0; j < kCompactPer / 4; ++j) {
+      const int64_t i = c * kChunk + (int64_t)j * (kBlock * 4) + threadIdx.x * 4;
+      if (i + 4 <= n) {
+        float4 t = *reinterpret_cast<const float4*>(src + i);
+        x[4 * j] = t.x; x[4 * j + 1] = t.y; x[4 * j + 2] = t.z; x[4 * j + 3] = t.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[4 * j + e] = (i + e < n) ? src[i + e] : 0.f;
       }
-      bg += isgt;
-      be += iseq;
+      uint32_t gt = 0, eq = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool in = i + e < n;
+        const uint32_t k = absbits(x[4 * j + e]);
+        gt += in && k > T;
+        eq += in && k == T;
+      }
+      cnt[j] = (eq << 16) | gt;
+    }
+    // per-segment wave inclusive scans (index order: segment, then wave, then lane)
+    uint32_t incl[kCompactPer / 4];
+#pragma unroll
+    for (int j = 0; j < kCompactPer / 4; ++j) {
+      uint32_t v = cnt[j];
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t a = __shfl_up(v, o, 64);
+        if (lane >= o) v += a;
+      }
+      incl[j] = v;
+      if (lane == 63) wsum[j][w] = v;
     }
     __syncthreads();
+    // chunk aggregate and this thread's exclusive offset inside the chunk
+    uint32_t agg = 0;
+#pragma unroll
+    for (int j = 0; j < kCompactPer / 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) agg += wsum[j][q];
+    // elements of earlier segments + earlier waves of this segment precede this thread
+    uint32_t off[kCompactPer / 4];
+    {
+      uint32_t run = 0;
+#pragma unroll
+      for (int j = 0; j < kCompactPer / 4; ++j) {
+        uint32_t wb = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) wb += (q < w) ? wsum[j][q] : 0u;
+        off[j] = run + wb + incl[j] - cnt[j];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) run += wsum[j][q];
+      }
+    }
+    const uint32_t agg_gt = agg & 0xffffu, agg_eq = agg >> 16;  // <= 4096 each: no field overflow
+    // publish the aggregate, look back for the exclusive prefix, publish the inclusive prefix.
+    // Wave 0 inspects 64 predecessors per step (one flag per lane): the nearest inclusive prefix
+    // ends the walk, aggregates before it are summed; a not-yet-published predecessor in front of
+    // it (it holds an earlier ticket, so it is running) is re-read.  Bounded: never hangs.
+    if (w == 0) {
+      unsigned long long* fl = flags;
+      uint32_t eg = 0, ee = 0;
+      if (c == 0) {
+        if (lane == 0)
+          __hip_atomic_store(fl, lb_pack(agg_gt, agg_eq, kStPre), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        if (lane == 0)
+          __hip_atomic_store(fl + c, lb_pack(agg_gt, agg_eq, kStAgg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        int64_t base = c - 1;
+        uint32_t spins = 0;
+        for (;;) {
+          const int64_t p = base - lane;
+          const unsigned long long f =
+              p >= 0 ? __hip_atomic_load(fl + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : kStPre;
+          const unsigned long long stt = f & (3ull << 62);
+          const unsigned long long pre = __ballot(stt == kStPre), zero = __ballot(stt == 0);
+          const int first = pre ? __ffsll((long long)pre) - 1 : 64;
+          const unsigned long long before = first == 64 ? ~0ull : ((1ull << first) - 1ull);
+          if (zero & before) {
+            if (++spins > (1u << 24)) break;  // never reached in a healthy run
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+          }
+          uint32_t vg = 0, ve = 0;
+          if (lane <= first) {
+            vg = (uint32_t)(f & 0x7fffffffull);
+            ve = (uint32_t)((f >> 31) & 0x7fffffffull);
+          }
+          for (int o = 32; o > 0; o >>= 1) {
+            vg += __shfl_xor(vg, o, 64);
+            ve += __shfl_xor(ve, o, 64);
+          }
+          eg += vg;
+          ee += ve;
+          if (first < 64) break;
+          base -= 64;
+        }
+        if (lane == 0)
+          __hip_atomic_store(fl + c, lb_pack(eg + agg_gt, ee + agg_eq, kStPre), __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (lane == 0) {
+        s_excl_gt = eg;
+        s_excl_eq = ee;
+        if (count_out && c == nchunks - 1) {
+          const uint32_t tot = eg + agg_gt;
+          count_out[0] = (int32_t)(tot < cap ? tot : cap);
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t xg = s_excl_gt, xe = s_excl_eq;
+#pragma unroll
+    for (int j = 0; j < kCompactPer / 4; ++j) {
+      const int64_t i = c * kChunk + (int64_t)j * (kBlock * 4) + threadIdx.x * 4;
+      uint32_t bg = xg + (off[j] & 0xffffu), be = xe + (off[j] >> 16);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (i + e >= n) break;
+        const uint32_t k = absbits(x[4 * j + e]);
+        const bool isgt = k > T, iseq = k == T;
+        const uint32_t pos = bg + (be < need_eq ? be : need_eq);
+        if ((isgt || (iseq && be < need_eq)) && pos < cap) {
+          idx[pos] = (int32_t)(i + e);
+          Vec4<VT>::store1(val, pos, x[4 * j + e]);
+          if (resid) resid[i + e] = x[4 * j + e] - Vec4<VT>::load1(val, pos);
+        }
+        bg += isgt;
+        be += iseq;
+      }
+    }
+    __syncthreads();  // s_chunk / wsum reuse
   }
 }
 
@@ -261,6 +409,53 @@ __global__ __launch_bounds__(kBlock) void k_topk_q8_resid(const int32_t* __restr
 }
 
 // ------------------------------------------------------------------------------------------
+namespace {
+
+struct TopkWs {
+  SelState* st;
+  unsigned long long* flags;
+  uint32_t* ckey;
+  uint32_t* cidx;
+  int64_t nchunks;
+  int64_t cap;
+};
+
+int64_t cand_cap(int64_t n) { return std::max<int64_t>(4096, n / 16); }
+
+int64_t ws_bytes_for(int64_t n) {
+  const int64_t nchunks = (n + kChunk - 1) / kChunk;
+  return (int64_t)sizeof(SelState) + 8 * nchunks + 8 * cand_cap(n) + 64;
+}
+
+TopkWs carve(at::Tensor& workspace, int64_t n) {
+  const int64_t need = ws_bytes_for(n);
+  TORCH_CHECK(workspace.is_cuda() && workspace.numel() * workspace.element_size() >= need,
+              "workspace too small: need ", need, " bytes (topk_workspace_bytes)");
+  static_assert(sizeof(SelState) % 16 == 0, "SelState keeps the look-back words aligned");
+  char* ws = (char*)workspace.data_ptr();
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(ws) % 16 == 0, "workspace must be 16-byte aligned");
+  TopkWs w;
+  w.st = reinterpret_cast<SelState*>(ws);
+  w.nchunks = (n + kChunk - 1) / kChunk;
+  w.cap = cand_cap(n);
+  w.flags = reinterpret_cast<unsigned long long*>(ws + sizeof(SelState));
+  w.ckey = reinterpret_cast<uint32_t*>(w.flags + w.nchunks);
+  w.cidx = w.ckey + w.cap;
+  return w;
+}
+
+int init_grid(int64_t nchunks) { return (int)std::max<int64_t>(1, std::min<int64_t>(kMaxGrid, (nchunks + kBlock - 1) / kBlock)); }
+
+template <typename VT>
+void launch_compact(hipStream_t stream, const float* src, float* rp, int64_t n, const TopkWs& w, int32_t* idx, VT* val,
+                    uint32_t cap, int32_t* count_out) {
+  const int grid = (int)std::min<int64_t>(w.nchunks, kMaxGrid);
+  hipLaunchKernelGGL(k_topk_compact<VT>, grid, kBlock, 0, stream, src, rp, n, w.st, w.flags, w.nchunks, idx, val, cap,
+                     count_out);
+}
+
+}  // namespace
+
 void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::Tensor idx, at::Tensor val,
                  at::Tensor workspace) {
   TORCH_CHECK(g.is_cuda() && g.is_contiguous() && g.scalar_type() == at::kFloat, "g: contiguous f32 device tensor");
@@ -271,10 +466,7 @@ void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::T
   TORCH_CHECK(val.numel() == k && (val.scalar_type() == at::kFloat || val.scalar_type() == at::kBFloat16),
               "val must be f32/bf16[k]");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0, "g must be 16-byte aligned");
-  const int64_t nchunks = (n + kChunk - 1) / kChunk;
-  const int64_t ws_bytes = (int64_t)sizeof(SelState) + 8 * nchunks + 16;
-  TORCH_CHECK(workspace.is_cuda() && workspace.numel() * workspace.element_size() >= ws_bytes,
-              "workspace too small: need ", ws_bytes, " bytes (topk_workspace_bytes)");
+  TopkWs w = carve(workspace, n);
   float* rp = nullptr;
   if (resid.has_value() && resid->defined()) {
     TORCH_CHECK(resid->numel() == n && resid->scalar_type() == at::kFloat && resid->is_contiguous(), "residual");
@@ -282,28 +474,28 @@ void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::T
     rp = resid->data_ptr<float>();
   }
   auto stream = c10::hip::getCurrentHIPStream();
-  char* ws = (char*)workspace.data_ptr();
-  SelState* st = reinterpret_cast<SelState*>(ws);
-  uint32_t* cgt = reinterpret_cast<uint32_t*>(ws + sizeof(SelState));
-  uint32_t* ceq = cgt + nchunks;
-  hipLaunchKernelGGL(k_topk_init, 1, kBlock, 0, stream, st, (uint32_t)k);
+  hipLaunchKernelGGL(k_topk_init, init_grid(w.nchunks), kBlock, 0, stream, w.st, 0u, 0u, (uint32_t)k,
+                     (uint32_t)w.cap, w.flags, w.nchunks);
   const int grid = grid_for(n >> 2);
-  const int los[3] = {20, 9, 0}, bits[3] = {11, 11, 9};
-  for (int p = 0; p < 3; ++p) {
-    hipLaunchKernelGGL(k_topk_hist, grid, kBlock, 0, stream, g.data_ptr<float>(), rp, (int)(p == 0 && rp), n, los[p],
-                       bits[p], st);
-    hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, los[p], bits[p], st);
-  }
+  // P1: fold + top-11-bit histogram over the whole bucket
+  hipLaunchKernelGGL(k_topk_hist, grid, kBlock, 0, stream, g.data_ptr<float>(), rp, (int)(rp != nullptr), n, 20, 11,
+                     w.st, 0);
+  hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 20, 11, w.st);
   const float* src = rp ? rp : g.data_ptr<float>();
-  const int cgrid = (int)std::min<int64_t>(nchunks, kMaxGrid);
-  hipLaunchKernelGGL(k_topk_count, cgrid, kBlock, 0, stream, src, n, st, cgt, ceq, nchunks);
-  hipLaunchKernelGGL(k_topk_scan, 1, 1024, 0, stream, cgt, ceq, nchunks, nullptr, 0u);
+  // P2: candidates of the selected bin
+  hipLaunchKernelGGL(k_topk_filter, grid, kBlock, 0, stream, src, n, w.st, w.ckey, w.cidx);
+  // P3/P4 on the candidates
+  const int cgrid = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxGrid, w.cap / 1024));
+  hipLaunchKernelGGL(k_topk_hist_cand, cgrid, kBlock, 0, stream, w.ckey, src, n, 9, 11, w.st);
+  hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 9, 11, w.st);
+  hipLaunchKernelGGL(k_topk_hist_cand, cgrid, kBlock, 0, stream, w.ckey, src, n, 0, 9, w.st);
+  hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 0, 9, w.st);
+  // P5: look-back compaction in index order
   if (val.scalar_type() == at::kFloat)
-    hipLaunchKernelGGL(k_topk_write<float>, cgrid, kBlock, 0, stream, src, rp, n, st, cgt, ceq, nchunks,
-                       idx.data_ptr<int32_t>(), val.data_ptr<float>(), (uint32_t)k);
+    launch_compact<float>(stream, src, rp, n, w, idx.data_ptr<int32_t>(), val.data_ptr<float>(), (uint32_t)k, nullptr);
   else
-    hipLaunchKernelGGL(k_topk_write<uint16_t>, cgrid, kBlock, 0, stream, src, rp, n, st, cgt, ceq, nchunks,
-                       idx.data_ptr<int32_t>(), (uint16_t*)val.data_ptr(), (uint32_t)k);
+    launch_compact<uint16_t>(stream, src, rp, n, w, idx.data_ptr<int32_t>(), (uint16_t*)val.data_ptr(), (uint32_t)k,
+                             nullptr);
 }
 
 // ---- threshold sparsification (variable-size message, count in a device header) -----------
@@ -315,10 +507,6 @@ __global__ __launch_bounds__(kBlock) void k_fold(const float* __restrict__ g, fl
   }
   if (blockIdx.x == 0)
     for (int64_t i = (nv << 2) + threadIdx.x; i < n; i += blockDim.x) r[i] += g[i];
-}
-
-__global__ void k_thresh_init(SelState* __restrict__ st, uint32_t tbits) {
-  if (threadIdx.x == 0) { st->prefix = tbits; st->mask = 0xffffffffu; st->remaining = 0; st->pad = 0; }
 }
 
 template <typename VT>
@@ -340,9 +528,8 @@ void thresh_encode(at::Tensor g, c10::optional<at::Tensor> resid, double tau, at
   const int64_t n = g.numel(), cap = idx.numel();
   TORCH_CHECK(val.numel() == cap && count.scalar_type() == at::kInt && count.numel() >= 1, "count/idx/val");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0, "g must be 16-byte aligned");
-  const int64_t nchunks = (n + kChunk - 1) / kChunk;
-  TORCH_CHECK(workspace.numel() * workspace.element_size() >= (int64_t)sizeof(SelState) + 8 * nchunks + 16,
-              "workspace too small");
+  TORCH_CHECK(n < (int64_t)1 << 31, "bucket must have < 2^31 elements");
+  TopkWs w = carve(workspace, n);
   auto stream = c10::hip::getCurrentHIPStream();
   float* rp = nullptr;
   if (resid.has_value() && resid->defined()) {
@@ -350,24 +537,19 @@ void thresh_encode(at::Tensor g, c10::optional<at::Tensor> resid, double tau, at
     rp = resid->data_ptr<float>();
     hipLaunchKernelGGL(k_fold, grid_for(n >> 2), kBlock, 0, stream, g.data_ptr<float>(), rp, n);
   }
-  char* ws = (char*)workspace.data_ptr();
-  SelState* st = reinterpret_cast<SelState*>(ws);
-  uint32_t* cgt = reinterpret_cast<uint32_t*>(ws + sizeof(SelState));
-  uint32_t* ceq = cgt + nchunks;
   float t = (float)std::fabs(tau);
   uint32_t tbits;
   std::memcpy(&tbits, &t, 4);
-  hipLaunchKernelGGL(k_thresh_init, 1, 64, 0, stream, st, tbits);
+  // T = tau exactly, no ties admitted: every |x| > tau, in index order (one look-back pass)
+  hipLaunchKernelGGL(k_topk_init, init_grid(w.nchunks), kBlock, 0, stream, w.st, tbits, 0xffffffffu, 0u,
+                     (uint32_t)w.cap, w.flags, w.nchunks);
   const float* src = rp ? rp : g.data_ptr<float>();
-  const int cgrid = (int)std::min<int64_t>(nchunks, kMaxGrid);
-  hipLaunchKernelGGL(k_topk_count, cgrid, kBlock, 0, stream, src, n, st, cgt, ceq, nchunks);
-  hipLaunchKernelGGL(k_topk_scan, 1, 1024, 0, stream, cgt, ceq, nchunks, count.data_ptr<int32_t>(), (uint32_t)cap);
   if (val.scalar_type() == at::kFloat)
-    hipLaunchKernelGGL(k_topk_write<float>, cgrid, kBlock, 0, stream, src, rp, n, st, cgt, ceq, nchunks,
-                       idx.data_ptr<int32_t>(), val.data_ptr<float>(), (uint32_t)cap);
+    launch_compact<float>(stream, src, rp, n, w, idx.data_ptr<int32_t>(), val.data_ptr<float>(), (uint32_t)cap,
+                          count.data_ptr<int32_t>());
   else
-    hipLaunchKernelGGL(k_topk_write<uint16_t>, cgrid, kBlock, 0, stream, src, rp, n, st, cgt, ceq, nchunks,
-                       idx.data_ptr<int32_t>(), (uint16_t*)val.data_ptr(), (uint32_t)cap);
+    launch_compact<uint16_t>(stream, src, rp, n, w, idx.data_ptr<int32_t>(), (uint16_t*)val.data_ptr(), (uint32_t)cap,
+                             count.data_ptr<int32_t>());
 }
 
 void thresh_accumulate(at::Tensor count, at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale) {
@@ -384,9 +566,7 @@ void thresh_accumulate(at::Tensor count, at::Tensor idx, at::Tensor val, at::Ten
                        (float)gscale);
 }
 
-int64_t topk_workspace_bytes(int64_t n) {
-  return (int64_t)sizeof(SelState) + 8 * ((n + kChunk - 1) / kChunk) + 16;
-}
+int64_t topk_workspace_bytes(int64_t n) { return ws_bytes_for(n); }
 
 void topk_accumulate(at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale) {
   TORCH_CHECK(acc.is_cuda() && acc.scalar_type() == at::kFloat, "acc: f32 device tensor");

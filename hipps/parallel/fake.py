@@ -118,6 +118,9 @@ class FakeAsyncPS:
     def note_presence(self, i, slot, vidx):
         pass
 
+    def flush(self):
+        pass
+
     def ack(self, i, seq):
         self.ctl.store(FIELDS.F_ACK_SEQ, i, seq)
 

@@ -178,6 +178,7 @@ class PSAsyncEngine(Engine):
             self.core = PSCore(self.ctl, C, W, self.nb, self.order, self.SLOTS, self.MAXSLOTS, self.M,
                                cfg.staleness, cfg.staleness_lr, self.gscale(self.M), self._stats)
             self.core.backend = self
+            self._pend, self._pend_acks = [], []
             self._pres_full = False
             self._pres_part = None
             self._publish_initial()
@@ -290,21 +291,44 @@ class PSAsyncEngine(Engine):
                 ready = self.ctl.wait_any(core.seen, 20000)
                 for i in ready:
                     core.pump(i)
+                self.flush()
                 if self._pause_req.is_set():
                     self._hold()
                 if core.should_stop(self.dead_workers()):
                     break
 
     # ---- PSCore backend (data plane on the PS stream) ----------------------------------------
+    # Accumulates and acks are deferred to flush(): the messages that arrived together for one
+    # bucket are summed by ONE multi-source kernel (acc += m1 + m2 + ...: one read-modify-write of
+    # the fp32 accumulator instead of one per message), then the acks go out in order, several
+    # words per doorbell.
+    BATCH = 16  # max sources per aggregate launch (kMaxSlots)
+
     def accumulate(self, i: int, slot: int, bi: int, seq: int, scale: float):
-        b = self.plan.buckets[bi]
         if self.plan.guarded:
             self._verify_slot(i, slot, bi, seq)
-        with self.tracer.phase("ps_accumulate", self.ps_stream):
-            self.codec.accumulate([self._bucket_msg(bi, self.slot_buf(i, slot))], self.acc[b.lo:b.hi], scale, True)
+        self._pend.append((bi, scale, self._bucket_msg(bi, self.slot_buf(i, slot))))
 
     def ack(self, i: int, seq: int):
-        self._ring(self.ps_stream, [(self.C.F_ACK_SEQ, i, seq)])  # stream-ordered: acks stay monotonic
+        self._pend_acks.append((self.C.F_ACK_SEQ, i, seq))
+
+    def flush(self):
+        if self._pend:
+            groups = {}
+            for bi, scale, msg in self._pend:
+                groups.setdefault((bi, scale), []).append(msg)
+            with self.tracer.phase("ps_accumulate", self.ps_stream):
+                for (bi, scale), msgs in groups.items():
+                    b = self.plan.buckets[bi]
+                    for k in range(0, len(msgs), self.BATCH):
+                        self.codec.accumulate(msgs[k:k + self.BATCH], self.acc[b.lo:b.hi], scale, True)
+            self._stats["acc_launches"] = self._stats.get("acc_launches", 0) + sum(
+                (len(m) + self.BATCH - 1) // self.BATCH for m in groups.values())
+            self._pend = []
+        acks = self._pend_acks
+        for k in range(0, len(acks), 6):  # stream-ordered after the reads: acks stay monotonic
+            self._ring(self.ps_stream, acks[k:k + 6])
+        self._pend_acks = []
 
     def note_presence(self, i: int, slot: int, vidx: int):
         self._note_presence(i, slot, vidx)

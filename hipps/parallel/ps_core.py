@@ -11,6 +11,7 @@ control block) and calls a backend for the data plane:
     backend.note_presence(i, slot, vidx)          last bucket of a kept step (missing-grad masks)
     backend.ack(i, seq)                           the slot may be reused (stream-ordered doorbell)
     backend.update(included, gscale)              optimizer step + publish version ``core.ver``
+    backend.flush()                               (optional) issue deferred accumulates / acks
 
 PSAsyncEngine drives it with the shared-memory control block and HIP streams; the in-process
 fake transport (hipps.parallel.fake) drives it with scripted arrival orders, so protocol edge
@@ -79,6 +80,8 @@ class PSCore:
                 self.count += 1
                 if self.count >= self.M:
                     self.ver += 1
+                    if hasattr(be, "flush"):
+                        be.flush()
                     be.update(self.pending, self.gscale)
                     self.pending = []
                     self.count = 0

@@ -173,6 +173,27 @@ def test_topk_exact(n, k, vdt):
     torch.testing.assert_close(acc.cpu(), want)
 
 
+@pytest.mark.parametrize("case", ["mostly_zero", "all_equal", "two_levels"])
+def test_topk_candidate_overflow_and_ties(case):
+    """Threshold bins holding more elements than the candidate list (n/16): the candidate passes
+    fall back to the whole bucket and ties are still admitted lowest-index-first."""
+    n, k = 1 << 20, 20000
+    torch.manual_seed(7)
+    if case == "mostly_zero":
+        x = torch.zeros(n)
+        x[torch.randperm(n)[:5000]] = torch.randn(5000)
+    elif case == "all_equal":
+        x = torch.full((n,), -0.25)
+    else:
+        x = torch.where(torch.rand(n) < 0.5, torch.tensor(1.5), torch.tensor(-0.75))
+    idx, val = torch.empty(k, dtype=torch.int32), torch.empty(k)
+    ref.topk_encode(x, None, k, idx, val)
+    idd, vd = torch.empty(k, dtype=torch.int32, device=DEV), torch.empty(k, device=DEV)
+    ops.topk_encode(x.to(DEV), None, k, idd, vd)
+    assert torch.equal(idd.cpu(), idx)
+    assert torch.equal(vd.cpu(), val)
+
+
 def test_topk_error_feedback_conserves_mass():
     n, k = 100_000, 1000
     g = torch.randn(n, device=DEV)
