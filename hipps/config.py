@@ -67,6 +67,10 @@ class PSConfig:
     skip_missing_grads: bool = True
     # raise ValueError when a parameter produced no gradient (the reference's ps.py:118-119 check)
     require_all_grads: bool = False
+    # sync-mode collectives: 'torch' (torch.distributed: RCCL process group / gloo) | 'rccl'
+    # (hipps' native RCCL communicator, hipps/csrc/runtime/rccl.cpp: ncclGather for the PS
+    # gather, ncclCommGetAsyncError polling every step, ncclCommAbort from the watchdog)
+    transport: str = "torch"
     # collective / transport timeout: the process-group timeout for the sync modes and the
     # async PS's waits; a watchdog thread aborts the process (exit code 3) if one step's
     # exchange exceeds it, instead of hanging on a dead peer
@@ -121,6 +125,8 @@ class PSConfig:
             raise ValueError("param_wire must be 'fp32' or 'bf16'")
         if self.bf16_weights not in ("auto", "on", "off"):
             raise ValueError("bf16_weights must be 'auto', 'on' or 'off'")
+        if self.transport not in ("torch", "rccl"):
+            raise ValueError("transport must be 'torch' or 'rccl'")
         if self.adam_variant not in ("reference", "torch"):
             raise ValueError("adam_variant must be 'reference' or 'torch'")
 

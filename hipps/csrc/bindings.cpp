@@ -65,6 +65,7 @@ namespace rt {
 void pull_params(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, at::Tensor pub,
                  int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t ring_slot, int64_t tries);
 void bind_control(pybind11::module& m);
+void bind_rccl(pybind11::module& m);
 void bind_ipc(pybind11::module& m);
 void bind_trace(pybind11::module& m);
 }  // namespace rt
@@ -117,6 +118,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pull_params", &hipps::rt::pull_params,
         "GPU-time AsySG-InCon pull: select newest published version, copy it, release the reader word");
   hipps::rt::bind_control(m);
+  hipps::rt::bind_rccl(m);
   hipps::rt::bind_ipc(m);
   hipps::rt::bind_trace(m);
 }

@@ -72,6 +72,7 @@ class Engine:
         self._hooks = []
         self.steps = 0
         self.group = None  # sync engines: collectives run on a group with cfg.comm_timeout_s
+        self.rccl = None  # cfg.transport == 'rccl': hipps.parallel.rccl.RcclGroup
         self.watchdog: Optional[CommWatchdog] = None
         self._sync_fault = None
         self._order_log: List[str] = []
@@ -330,9 +331,17 @@ class Engine:
         from .ps_async import _parse_fault
 
         self._sync_fault = _parse_fault(os.environ.get("HIPPS_FAULT"), self.world.rank)
+        if self.cfg.transport == "rccl":
+            if not self.cuda or (self.world.size > 1 and self.world.backend != "nccl"):
+                raise ValueError("transport='rccl' needs HIP tensors and the nccl (RCCL) process group")
+            from .rccl import RcclGroup
+
+            self.rccl = RcclGroup(self.world, self.store.device)
         if self.world.size > 1 and dist.is_initialized():
             self.group = dist.new_group(timeout=datetime.timedelta(seconds=self.cfg.comm_timeout_s))
-            self.watchdog = CommWatchdog(self.cfg.comm_timeout_s, self.world.rank)
+        if self.world.size > 1 or self.rccl is not None:
+            self.watchdog = CommWatchdog(self.cfg.comm_timeout_s, self.world.rank,
+                                         on_abort=self.rccl.abort if self.rccl is not None else None)
 
     def _fault_point(self):
         """HIPPS_FAULT='rank:step:kind[:arg]' for the sync engines: hang (stop participating, stay
@@ -359,6 +368,11 @@ class Engine:
         self.remove_hooks()
         if self.watchdog is not None:
             self.watchdog.close()
+        if self.rccl is not None:
+            if self.cuda:
+                torch.cuda.synchronize(self.store.device)
+            self.rccl.close()
+            self.rccl = None
 
     def engine_state(self) -> dict:
         """Codec state (e.g. error-feedback residuals) of this rank, for checkpoints."""
@@ -542,8 +556,13 @@ class AllGatherEngine(Engine):
         t = time.perf_counter()
         if self.cuda:
             with torch.cuda.stream(self.comm_stream), self.tracer.phase("comm", self.comm_stream):
-                all_gather_into(self.gathered, self.wire, self.world, group=self.group)
+                if self.rccl is not None:
+                    self.rccl.all_gather_into(self.gathered, self.wire, self.comm_stream)
+                else:
+                    all_gather_into(self.gathered, self.wire, self.world, group=self.group)
             torch.cuda.current_stream(self.store.device).wait_stream(self.comm_stream)
+            if self.rccl is not None:
+                self.rccl.poll()
         else:
             with self.tracer.phase("comm"):
                 all_gather_into(self.gathered, self.wire, self.world, group=self.group)
@@ -611,9 +630,14 @@ class PSSyncEngine(Engine):
         ctx = torch.cuda.stream(cs) if self.cuda else _null()
         self.verify_guards([self.wire], "encode")
         with ctx, self.tracer.phase("comm", cs):
-            gather_into(self.gathered if self.world.is_ps else None, self.wire, self.world, group=self.group)
+            if self.rccl is not None:  # one ncclGather (rccl.h:745)
+                self.rccl.gather_into(self.gathered if self.world.is_ps else None, self.wire, 0, cs)
+            else:
+                gather_into(self.gathered if self.world.is_ps else None, self.wire, self.world, group=self.group)
         if self.cuda:
             torch.cuda.current_stream(self.store.device).wait_stream(cs)
+            if self.rccl is not None:
+                self.rccl.poll()
         data["comm_wait"] = data["isend_time"] = time.perf_counter() - t
         t = time.perf_counter()
         if self.world.is_ps:
@@ -637,7 +661,14 @@ def _bcast_params_impl(self, data):
     """ibroadcast of the parameters (mpi_comms.py:127-133 / README.md:76)."""
     t = time.perf_counter()
     with self.tracer.phase("bcast"):
-        if self.pub is not None:
+        if self.rccl is not None:
+            self.rccl.broadcast(self.pub if self.pub is not None else self.store.data, 0)
+            if self.pub is not None and not self.world.is_ps:
+                from hipps import ops
+
+                ops.convert(self.pub, self.store.data)
+            self.rccl.poll()
+        elif self.pub is not None:
             broadcast(self.pub, self.world, 0, group=self.group)
             if not self.world.is_ps:
                 from hipps import ops

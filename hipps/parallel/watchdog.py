@@ -24,9 +24,10 @@ from typing import Optional
 class CommWatchdog:
     EXIT_CODE = 3
 
-    def __init__(self, timeout_s: float, rank: int = 0):
+    def __init__(self, timeout_s: float, rank: int = 0, on_abort=None):
         self.limit = 1.5 * float(timeout_s) + 5.0
         self.rank = rank
+        self.on_abort = on_abort  # e.g. ncclCommAbort of hipps' own communicator
         self._armed: Optional[tuple] = None  # (what, t0)
         self._lock = threading.Lock()
         self._stop = threading.Event()
@@ -53,6 +54,11 @@ class CommWatchdog:
                                  f"(comm_timeout_s); a peer is dead or hung -- aborting with status "
                                  f"{self.EXIT_CODE}\n")
                 sys.stderr.flush()
+                if self.on_abort is not None:
+                    try:
+                        self.on_abort()
+                    except Exception:
+                        pass
                 os._exit(self.EXIT_CODE)
 
 
