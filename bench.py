@@ -57,7 +57,8 @@ def parse():
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--allow-fallback", action="store_true",
-                    help="if the ps_async transport cannot initialise, run ps_sync instead of failing")
+                    help="if the ps_async IPC transport cannot initialise, use its p2p transport instead of failing")
+    ap.add_argument("--async-transport", default="ipc", choices=["ipc", "p2p"])
     return ap.parse_args()
 
 
@@ -95,18 +96,19 @@ def main():
     if a.param_wire == "auto":
         a.param_wire = "bf16" if N > 1 else "fp32"
     note = None
+    kw = dict(lr=a.lr, momentum=a.momentum, weight_decay=5e-5, mode=mode, code=a.codec,
+              accumulate=a.accumulate or None, average=True, param_wire=a.param_wire, bucket_mb=a.bucket_mb,
+              async_transport=a.async_transport)
     try:
-        opt = hipps.SGD(model.named_parameters(), lr=a.lr, momentum=a.momentum, weight_decay=5e-5, mode=mode,
-                        code=a.codec, accumulate=a.accumulate or None, average=True, param_wire=a.param_wire,
-                        bucket_mb=a.bucket_mb)
-    except Exception as e:  # robust fallback so a scaling run still reports a number
-        if mode != "ps_async" or N == 1 or not a.allow_fallback:
+        opt = hipps.SGD(model.named_parameters(), **kw)
+    except Exception as e:
+        # opt-in: the same async PS over the two-sided (RCCL pair send/recv) transport
+        if mode != "ps_async" or N == 1 or not a.allow_fallback or a.async_transport == "p2p":
             raise
-        note = f"ps_async init failed ({type(e).__name__}: {e}); fell back to ps_sync"
+        note = f"ps_async ipc transport failed ({type(e).__name__}: {e}); fell back to the p2p transport"
         print("[bench] " + note, file=sys.stderr)
-        mode = "ps_sync"
-        opt = hipps.SGD(model.named_parameters(), lr=a.lr, momentum=a.momentum, weight_decay=5e-5, mode=mode,
-                        code=a.codec, average=True, param_wire=a.param_wire, bucket_mb=a.bucket_mb)
+        kw["async_transport"] = "p2p"
+        opt = hipps.SGD(model.named_parameters(), **kw)
 
     def step():
         opt.zero_grad()

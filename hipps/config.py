@@ -36,6 +36,10 @@ class PSConfig:
     # GPU-rung doorbells) | 'prefetch' (host-chosen version, side-stream copy adopted at the next
     # step) | 'direct' (host-chosen, copy on the compute stream)
     pull: str = "device"
+    # async PS data path: 'ipc' (workers map the PS's mailbox and copy one-sidedly over xGMI, GPU
+    # doorbells) | 'p2p' (two-sided send/recv: RCCL pair communicators through torch.distributed on
+    # GPU, gloo on CPU -- the fallback when IPC memory cannot be mapped)
+    async_transport: str = "ipc"
     # async PS: scale a kept gradient by 1/max(1, staleness) (staleness-aware async SGD)
     staleness_lr: bool = False
     # async PS failure detection: a worker silent for this long (no heartbeat, no STOP) is dead
@@ -125,6 +129,8 @@ class PSConfig:
             raise ValueError("param_wire must be 'fp32' or 'bf16'")
         if self.bf16_weights not in ("auto", "on", "off"):
             raise ValueError("bf16_weights must be 'auto', 'on' or 'off'")
+        if self.async_transport not in ("ipc", "p2p"):
+            raise ValueError("async_transport must be 'ipc' or 'p2p'")
         if self.transport not in ("torch", "rccl"):
             raise ValueError("transport must be 'torch' or 'rccl'")
         if self.adam_variant not in ("reference", "torch"):

@@ -57,6 +57,8 @@ struct alignas(64) RankRec {
   std::atomic<int64_t> incl_seq;           // newest own message reflected in the published params
   std::atomic<int64_t> push_flag[kSlots];  // 1: the slot's step left some parameters without a gradient
   std::atomic<int64_t> reading;            // version whose publish buffer this rank is copying (-1 none)
+  std::atomic<int64_t> pull_req;           // p2p transport: parameter requests posted by this worker
+  std::atomic<int64_t> sent_ver;           // p2p transport: version the PS sent for the last request
 };
 
 struct alignas(64) Header {
@@ -73,7 +75,7 @@ struct alignas(64) Header {
 
 enum Field : int {
   PUSH_SEQ = 0, ACK_SEQ = 1, PUSH_VER = 2, APPLIED_VER = 3, STOP = 4, HEARTBEAT = 5, INCL_SEQ = 6,
-  PUSH_FLAG = 7, READING = 8, PUB_VER = 10, PS_STOP = 11, ERROR = 12, DROPS = 13, UPDATES = 14, BUF_VER = 15
+  PUSH_FLAG = 7, READING = 8, PULL_REQ = 9, PUB_VER = 10, PS_STOP = 11, ERROR = 12, DROPS = 13, UPDATES = 14, BUF_VER = 15, SENT_VER = 16
 };
 
 static int64_t now_ns() {
@@ -148,6 +150,8 @@ class ControlBlock {
       case INCL_SEQ: return &rec(idx).incl_seq;
       case PUSH_FLAG: return &rec(idx / kSlots).push_flag[idx % kSlots];
       case READING: return &rec(idx).reading;
+      case PULL_REQ: return &rec(idx).pull_req;
+      case SENT_VER: return &rec(idx).sent_ver;
       case PUB_VER: return &h_->pub_ver;
       case PS_STOP: return &h_->ps_stop;
       case ERROR: return &h_->error;
@@ -335,6 +339,8 @@ void bind_control(py::module& m) {
   m.attr("F_INCL_SEQ") = (int)INCL_SEQ;
   m.attr("F_PUSH_FLAG") = (int)PUSH_FLAG;
   m.attr("F_READING") = (int)READING;
+  m.attr("F_PULL_REQ") = (int)PULL_REQ;
+  m.attr("F_SENT_VER") = (int)SENT_VER;
   m.attr("F_PUB_VER") = (int)PUB_VER;
   m.attr("F_PS_STOP") = (int)PS_STOP;
   m.attr("F_ERROR") = (int)ERROR;

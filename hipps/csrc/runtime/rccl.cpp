@@ -20,6 +20,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 #include <rccl/rccl.h>
+#include <torch/extension.h>
 
 namespace py = pybind11;
 

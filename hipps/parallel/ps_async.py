@@ -72,6 +72,38 @@ def _align(x: int, a: int = 256) -> int:
     return (x + a - 1) // a * a
 
 
+class _Pending:
+    """Completion of posted torch.distributed p2p works.  RCCL works report completion by event
+    query (``is_completed``); gloo's receive works only learn it inside ``wait()``, so on gloo a
+    helper thread waits and flags it."""
+
+    def __init__(self, works, poll: bool):
+        self.works = works
+        self._ev = None
+        if not poll:
+            self._ev = threading.Event()
+            threading.Thread(target=self._wait, daemon=True).start()
+
+    def _wait(self):
+        try:
+            for w in self.works:
+                w.wait()
+        finally:
+            self._ev.set()
+
+    def done(self) -> bool:
+        if self._ev is not None:
+            return self._ev.is_set()
+        return all(w.is_completed() for w in self.works)
+
+    def wait(self):
+        if self._ev is not None:  # gloo: wait() may be called once per work (the helper did)
+            self._ev.wait()
+            return
+        for w in self.works:
+            w.wait()
+
+
 class PSAsyncEngine(Engine):
     name = "ps_async"
 
@@ -120,13 +152,20 @@ class PSAsyncEngine(Engine):
         total = self.pub_off + self.NPUB * self.pub_bytes
 
         # ---- rendezvous: rank 0 creates control block + mailboxes, others map them ----------
+        # transport 'ipc': workers map the PS's mailbox (HIP IPC / POSIX shm) and copy one-sidedly;
+        # 'p2p': the mailbox stays private to the PS and data moves by two-sided send/recv
+        # (torch.distributed isend/irecv: RCCL pair communicators on GPU, gloo on CPU)
+        self.p2p = cfg.async_transport == "p2p" and W > 1
         token = secrets.token_hex(6) if self.rank == 0 else None
         handle = None
+        self.mailbox = None
         if self.rank == 0:
             self.ctl_name = f"/hipps_ctl_{os.getpid()}_{token}"
             self.mb_name = f"/hipps_mb_{os.getpid()}_{token}"
             self.ctl = C.ControlBlock(self.ctl_name, W, True)
-            if self.cuda:
+            if self.p2p:
+                self.mem = torch.zeros(total, dtype=torch.uint8, device=store.device)
+            elif self.cuda:
                 self.mailbox = C.DeviceMailbox(total)
                 handle = self.mailbox.handle()
             else:
@@ -137,16 +176,19 @@ class PSAsyncEngine(Engine):
         if self.rank != 0:
             self.ctl_name, self.mb_name, handle = meta
             self.ctl = C.ControlBlock(self.ctl_name, W, False)
-            if self.cuda:
+            if self.p2p:
+                self.mem = None
+            elif self.cuda:
                 self.mailbox = C.DeviceMailbox(handle, total)
             else:
                 self.mailbox = C.HostMailbox(self.mb_name, total, False)
         barrier(world)
         if self.rank == 0:  # everyone has mapped: remove the names (no /dev/shm leftovers)
             self.ctl.unlink()
-            if not self.cuda:
+            if not self.cuda and self.mailbox is not None:
                 self.mailbox.unlink()
-        self.mem = self.mailbox.tensor()
+        if self.mailbox is not None:
+            self.mem = self.mailbox.tensor()
         # GPU-rung doorbells need the control block registered with HIP in this process
         self.device_bells = bool(self.cuda and self.ctl.enable_device_doorbells())
         self.pull_mode = cfg.pull
@@ -154,6 +196,11 @@ class PSAsyncEngine(Engine):
             self.pull_mode = "prefetch" if self.rank != 0 else "direct"
         if not self.cuda:
             self.pull_mode = "direct"
+        if self.p2p and self.rank != 0:
+            self.pull_mode = "p2p"
+        self._p2p_req = None  # worker: (request seq, stage index, [works]) of the posted param recv
+        self._p2p_reqs = 0
+        self._pub_sends: dict = {}  # PS: publish buffer -> in-flight parameter sends reading it
 
         # ---- PS state on rank 0 ------------------------------------------------------------
         self.seq = 0
@@ -165,12 +212,12 @@ class PSAsyncEngine(Engine):
         self._pause_req = threading.Event()
         self._paused = threading.Event()
         self.enc_event = torch.cuda.Event() if self.cuda else None
+        self._stage = [None, None]  # double-buffered staging for prefetch / p2p pulls
+        self._stage_ev = [None, None]
+        self._stage_k = 0
         if self.cuda:
             # sel[0] selected, sel[1] adopted, sel[2:2+RING] version each step's gradient uses
             self._sel = torch.full((2 + RING,), -1, dtype=torch.int64, device=store.device)
-            self._stage = [None, None]
-            self._stage_ev = [None, None]
-            self._stage_k = 0
         if self.rank == 0:
             self.master = store.data.detach().clone()
             self.acc = torch.zeros_like(store.data)
@@ -182,14 +229,26 @@ class PSAsyncEngine(Engine):
             self._pres_full = False
             self._pres_part = None
             self._publish_initial()
+        if self.p2p:
+            # the PS thread is the only user of the pair channels once it runs, so version 0 and
+            # the transport self-test go first, on the main threads
+            pub0 = self.pub_buf(0) if self.rank == 0 else torch.empty(store.numel, dtype=self.pub_dtype,
+                                                                       device=store.device)
+            dist.broadcast(pub0, src=0)
+            self._adopt(pub0, 0)
+            if self.cuda:
+                torch.cuda.current_stream(store.device).synchronize()
+            self._self_test()
+        if self.rank == 0:
             self._thread = threading.Thread(target=self._serve_guard, name="hipps-ps", daemon=True)
             self._thread.start()
         barrier(world)
-        # every replica starts from the PS's version 0 (ranks may have initialised differently)
-        self.irequest_params(block_for=0)
-        if self.cuda:
-            torch.cuda.current_stream(store.device).synchronize()
-        self._self_test()
+        if not self.p2p:
+            # every replica starts from the PS's version 0 (ranks may have initialised differently)
+            self.irequest_params(block_for=0)
+            if self.cuda:
+                torch.cuda.current_stream(store.device).synchronize()
+            self._self_test()
 
     def _self_test(self):
         """Prove both directions of the one-sided transport before training starts: every rank
@@ -198,6 +257,8 @@ class PSAsyncEngine(Engine):
         IPC/xGMI mapping raises here on ALL ranks instead of corrupting training later."""
         W, dev = self.W, self.store.device
         tag = torch.full((16,), (self.rank * 7 + 3) % 251, dtype=torch.uint8, device=dev)
+        if self.p2p:
+            return self._self_test_p2p(tag)
         dst = self.slot_buf(self.rank, self.SLOTS - 1)[:16]
         if self.cuda:
             with torch.cuda.stream(self.comm_stream):
@@ -229,6 +290,30 @@ class PSAsyncEngine(Engine):
         if not all(flags):
             raise RuntimeError(f"ps_async transport self-test failed (per-rank ok={flags}); "
                                "IPC mailbox path unusable on this machine")
+
+    def _self_test_p2p(self, tag):
+        """p2p transport: every worker sends a tag to the PS (the PS thread is not serving yet:
+        the main thread of rank 0 receives them), and the version-0 params every worker received
+        through a parameter request must match the PS's checksum."""
+        W = self.W
+        ok = True
+        if self.rank == 0:
+            for r in range(1, W):
+                got = self.slot_buf(r, self.SLOTS - 1)[:16]
+                dist.recv(got, src=r)
+                ok &= bool((got.cpu() == (r * 7 + 3) % 251).all())
+        else:
+            dist.send(tag, dst=0)
+        ck = float(self.pub_buf(0).double().sum()) if self.rank == 0 else None
+        box = [ok, ck]
+        dist.broadcast_object_list(box, src=0)
+        ok, ck = box
+        mine = float(self.store.data.double().sum())
+        good = ok and abs(mine - ck) <= 1e-6 * max(1.0, abs(ck))
+        flags = [None] * W
+        dist.all_gather_object(flags, good)
+        if not all(flags):
+            raise RuntimeError(f"ps_async p2p transport self-test failed (per-rank ok={flags})")
 
     # ------------------------------------------------------------------ memory views
     def slot_buf(self, rank: int, slot: int) -> torch.Tensor:
@@ -281,10 +366,76 @@ class PSAsyncEngine(Engine):
             self._err = traceback.format_exc()
             self.ctl.store(self.C.F_ERROR, 0, 1)
 
+    def _serve_p2p(self):
+        """PS loop of the p2p transport: for every worker, post receives for the messages it has
+        announced (into its mailbox slots, at most SLOTS ahead of what was consumed; a receive is
+        ordered after the PS-stream work that read the slot's previous message), hand completed
+        ones to the protocol core in order, and answer parameter requests with a send of the
+        newest publish buffer.  Rank 0's own messages arrive through its local mailbox and
+        doorbell as in the IPC transport.  Receives complete in any order across workers: the
+        ANY_SOURCE of README.md:65-70 is this polling loop."""
+        from collections import deque
+
+        C, core, W = self.C, self.core, self.W
+        ns = len(self.store.slots)
+        posted = [0] * W
+        inflight = [deque() for _ in range(W)]
+        self._served = [0] * W
+        idle = 0
+        with torch.no_grad():
+            while True:
+                progressed = False
+                if self.ctl.load(C.F_PUSH_SEQ, 0) > core.seen[0]:
+                    progressed |= core.pump(0) > 0
+                for i in range(1, W):
+                    ann = self.ctl.load(C.F_PUSH_SEQ, i)
+                    while posted[i] < ann and posted[i] - core.seen[i] < self.SLOTS:
+                        s = posted[i] + 1
+                        slot = s % self.SLOTS
+                        pos = (s - 1) % self.nb
+                        b = self.plan.buckets[self.order[pos]]
+                        sbuf = self.slot_buf(i, slot)
+                        works = [dist.irecv(sbuf[: b.msg_nbytes], src=i)]
+                        if pos == self.nb - 1 and self.ctl.load(C.F_PUSH_FLAG, i * self.MAXSLOTS + slot):
+                            works.append(dist.irecv(sbuf[self.slot_pres:self.slot_pres + ns], src=i))
+                        inflight[i].append((s, _Pending(works, self.cuda)))
+                        posted[i] = s
+                    while inflight[i] and inflight[i][0][1].done():
+                        s, pend = inflight[i].popleft()
+                        pend.wait()  # the PS stream is ordered after the receive
+                        core.pump(i, upto=s)
+                        progressed = True
+                self.flush()
+                for i in range(1, W):
+                    req = self.ctl.load(C.F_PULL_REQ, i)
+                    if req > self._served[i]:
+                        self._send_params(i)
+                        self._served[i] = req
+                        progressed = True
+                if self._pause_req.is_set():
+                    self._hold()
+                dead = self.dead_workers()
+                if core.should_stop(dead) and all(self._served[i] >= self.ctl.load(C.F_PULL_REQ, i)
+                                                  for i in range(1, W) if i not in dead):
+                    break
+                idle = 0 if progressed else idle + 1
+                if idle > 50:
+                    time.sleep(20e-6)
+
+    def _send_params(self, i: int):
+        """Answer worker i's parameter request with the newest published version."""
+        v = self.ver
+        b = v % self.NPUB
+        self.ctl.store(self.C.F_SENT_VER, i, v)
+        w = dist.isend(self.pub_buf(b), dst=i)  # ordered after the update that wrote buffer b
+        self._pub_sends.setdefault(b, []).append(w)
+
     def _serve(self):
         """PS loop: wait on every worker's push word at once (the ANY_SOURCE), hand what arrived
         to the protocol core (hipps.parallel.ps_core), which calls back into accumulate /
         note_presence / ack / update below -- all enqueued on the PS stream."""
+        if self.p2p:
+            return self._serve_p2p()
         core = self.core
         with torch.no_grad():
             while True:
@@ -368,6 +519,8 @@ class PSAsyncEngine(Engine):
     def _update(self, included, gscale):
         C = self.C
         b = self.ver % self.NPUB  # PSCore advanced the version
+        for w in self._pub_sends.pop(b, []):  # p2p: sends still reading this buffer finish first
+            w.wait()
         old = self.ctl.load(C.F_BUF_VER, b)
         self.ctl.store(C.F_BUF_VER, b, -1)  # readers skip a buffer being rewritten ...
         if old >= 0 and not self.ctl.wait_no_reader(old, 0):  # ... and it waits for current readers
@@ -444,10 +597,13 @@ class PSAsyncEngine(Engine):
                 t_wait += time.perf_counter() - tw
             b = self.plan.buckets[bi]
             src = self.plan.message(self.wire, bi)  # layout (+ canary guard in debug_canary)
-            sbuf = self.slot_buf(self.rank, slot)
-            dst = sbuf[: b.msg_nbytes]
             vidx = self.rank * self.MAXSLOTS + slot
             last = pos == self.nb - 1
+            if self.p2p and self.rank != 0:
+                self._push_p2p(src, s, vidx, last and partial)
+                continue
+            sbuf = self.slot_buf(self.rank, slot)
+            dst = sbuf[: b.msg_nbytes]
             words = [(C.F_PUSH_VER, vidx, self.local_ver), (C.F_PUSH_FLAG, vidx, partial if last else 0),
                      (C.F_PUSH_SEQ, self.rank, s)]
             if self.cuda:
@@ -483,6 +639,68 @@ class PSAsyncEngine(Engine):
         self.steps += 1
         return data
 
+    # ------------------------------------------------------------------ p2p transport (worker)
+    def _push_p2p(self, msg: torch.Tensor, s: int, vidx: int, partial: bool):
+        """Announce message s (version + presence flag, then the sequence word the PS waits on)
+        and send it; the PS posts the matching receive when it sees the announcement.  The send
+        is ordered after the encode on the comm stream, and the comm stream waits for it before
+        the next encode overwrites the wire buffer."""
+        C = self.C
+        self.ctl.store(C.F_PUSH_VER, vidx, self.local_ver)
+        self.ctl.store(C.F_PUSH_FLAG, vidx, 1 if partial else 0)
+        self.ctl.store(C.F_PUSH_SEQ, self.rank, s)
+        ctx = torch.cuda.stream(self.comm_stream) if self.cuda else contextlib.nullcontext()
+        with ctx, self.tracer.phase("push", self.comm_stream):
+            works = [dist.isend(msg, dst=0)]
+            if partial:
+                self._pres_send = self.presence_tensor()
+                works.append(dist.isend(self._pres_send, dst=0))
+            for w in works:
+                w.wait()  # GPU: the comm stream waits; CPU: returns once the PS has the bytes
+
+    def _p2p_pull(self, sync: bool = False, need: int = -1) -> bool:
+        """irequest_params over send/recv (README.md:63 "post/consume non-blocking param receive"):
+        a posted receive into a staging buffer plus a request word; the PS answers with its newest
+        version.  A completed receive is adopted at the next call (one step of extra staleness,
+        no stall); ``sync`` waits for it, and re-requests until the version is >= ``need``."""
+        C = self.C
+        adopted = False
+        while True:
+            rq = self._p2p_req
+            if rq is not None and (sync or rq[2].done()):
+                r, k, pend = rq
+                pend.wait()
+                if self.cuda and sync:
+                    torch.cuda.current_stream(self.store.device).synchronize()
+                v = self.ctl.load(C.F_SENT_VER, self.rank)
+                self._adopt(self._stage[k], v)
+                if self.cuda:
+                    ev = torch.cuda.Event()
+                    ev.record(torch.cuda.current_stream(self.store.device))
+                    self._stage_ev[k] = ev
+                self._p2p_req = None
+                adopted = True
+            if self._p2p_req is None:
+                k = self._stage_k
+                self._stage_k ^= 1
+                if self._stage[k] is None:
+                    self._stage[k] = torch.empty(self.store.numel, dtype=self.pub_dtype, device=self.store.device)
+                if self.cuda:
+                    if getattr(self, "_pull_stream", None) is None:
+                        self._pull_stream = torch.cuda.Stream(device=self.store.device)
+                    ps = self._pull_stream
+                    if self._stage_ev[k] is not None:
+                        ps.wait_event(self._stage_ev[k])  # the last adoption from this stage is done
+                    with torch.cuda.stream(ps):
+                        works = [dist.irecv(self._stage[k], src=0)]
+                else:
+                    works = [dist.irecv(self._stage[k], src=0)]
+                self._p2p_reqs += 1
+                self._p2p_req = (self._p2p_reqs, k, _Pending(works, self.cuda))
+                self.ctl.store(C.F_PULL_REQ, self.rank, self._p2p_reqs)
+            if not sync or self.local_ver >= need:
+                return adopted
+
     def adopted_version(self) -> int:
         """The version this worker trains on (device pull: as last reported by the GPU)."""
         if self.pull_mode == "device":
@@ -513,6 +731,10 @@ class PSAsyncEngine(Engine):
                 raise TimeoutError(f"rank {self.rank}: params never caught up to message {need}")
             if self.pull_mode != "device":
                 sync = True
+        if self.pull_mode == "p2p":
+            need = max(block_for if block_for is not None else -1,
+                       self.ctl.load(C.F_PUB_VER, 0) if sync else -1)
+            return self._p2p_pull(sync=sync, need=need)
         if sync or self.pull_mode == "direct":
             return self._direct_pull()
         if self.pull_mode == "device":
@@ -637,7 +859,8 @@ class PSAsyncEngine(Engine):
         return d
 
     def transport_info(self) -> dict:
-        return {"doorbells": self.ctl.bell_mode, "pull": self.pull_mode, "npub": self.NPUB,
+        return {"transport": "p2p" if self.p2p else "ipc", "doorbells": self.ctl.bell_mode, "pull": self.pull_mode,
+                "npub": self.NPUB,
                 "mailbox_slots": self.SLOTS, "slot_bytes": self.slot_bytes}
 
     def close(self):
@@ -650,6 +873,11 @@ class PSAsyncEngine(Engine):
             if self.cuda:
                 torch.cuda.synchronize(self.store.device)
             self._staged = None
+            if self._p2p_req is not None:  # a posted parameter receive must be matched before exit
+                self._p2p_req[2].wait()
+                self._p2p_req = None
+                if self.cuda:
+                    torch.cuda.synchronize(self.store.device)
             if not getattr(self, "_dead", False):
                 self.ctl.store(C.F_STOP, self.rank, self.seq + 1)
             if self.rank == 0 and self._thread is not None:
@@ -663,7 +891,7 @@ class PSAsyncEngine(Engine):
                 if self.cuda:
                     self.ps_stream.synchronize()
         finally:
-            if self.rank != 0 and self.cuda:
+            if self.rank != 0 and self.cuda and self.mailbox is not None:
                 self.mailbox.close()
         if self._err:
             raise RuntimeError(self._err)

@@ -41,10 +41,11 @@ class PSCore:
         self.scale = [1.0] * W
         self.backend = None
 
-    def pump(self, i: int) -> int:
-        """Process every message worker ``i`` has pushed since the last call; returns how many."""
+    def pump(self, i: int, upto: Optional[int] = None) -> int:
+        """Process every message worker ``i`` has pushed since the last call (or up to message
+        ``upto``, for transports that learn about arrival from elsewhere); returns how many."""
         F = self.F
-        s_now = self.ctl.load(F.F_PUSH_SEQ, i)
+        s_now = self.ctl.load(F.F_PUSH_SEQ, i) if upto is None else upto
         n = 0
         for s in range(self.seen[i] + 1, s_now + 1):
             self._one(i, s)

@@ -36,13 +36,13 @@ def _unpack(o):
     return o
 
 
-def _entry(rank, world_size, port, fn, args, q):
+def _entry(rank, world_size, port, fn, args, q, backend="gloo"):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world_size), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     try:
         from hipps.parallel import dist as hdist
 
-        hdist.init_from_env(backend="gloo")
+        hdist.init_from_env(backend=backend)
         out = fn(rank, world_size, *args)
         q.put((rank, "ok", _pack(out)))
     except BaseException:
@@ -57,11 +57,11 @@ def _entry(rank, world_size, port, fn, args, q):
                 pass
 
 
-def run_world(fn, world_size=2, *args, timeout=240):
+def run_world(fn, world_size=2, *args, timeout=240, backend="gloo"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_entry, args=(r, world_size, port, fn, args, q)) for r in range(world_size)]
+    procs = [ctx.Process(target=_entry, args=(r, world_size, port, fn, args, q, backend)) for r in range(world_size)]
     for p in procs:
         p.start()
     results = {}

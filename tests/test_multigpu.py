@@ -18,7 +18,7 @@ NDEV = torch.cuda.device_count() if torch.cuda.is_available() else 0
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(NDEV < 2, reason="needs >= 2 HIP devices")]
 
 
-def _tiny(rank, world, pull, steps, codec):
+def _tiny(rank, world, pull, steps, codec, transport="ipc"):
     import torch.nn.functional as F
 
     import hipps
@@ -29,10 +29,10 @@ def _tiny(rank, world, pull, steps, codec):
     torch.manual_seed(rank)
     m = resnet_tiny().to(dev).to(memory_format=torch.channels_last)
     opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", code=codec, pull=pull,
-                    average=True)
+                    average=True, async_transport=transport)
     eng = opt.engine
     info = dict(eng.transport_info())
-    info["mem_device"] = eng.mem.device.index
+    info["mem_device"] = eng.mem.device.index if eng.mem is not None else rank
     x = torch.randn(8, 3, 32, 32, device=dev).contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 10, (8,), device=dev)
     vers = []
@@ -49,11 +49,12 @@ def _tiny(rank, world, pull, steps, codec):
     return info
 
 
-@pytest.mark.parametrize("pull,codec", [("device", "bf16"), ("prefetch", "bf16"), ("device", "topk_int8:0.05")])
-def test_async_ps_across_devices(pull, codec):
+@pytest.mark.parametrize("pull,codec,transport", [("device", "bf16", "ipc"), ("prefetch", "bf16", "ipc"),
+                                                  ("device", "topk_int8:0.05", "ipc"), ("device", "bf16", "p2p")])
+def test_async_ps_across_devices(pull, codec, transport):
     W = min(NDEV, 4)
     steps = 10
-    out = run_world(_tiny, W, pull, steps, codec, timeout=600)
+    out = run_world(_tiny, W, pull, steps, codec, transport, timeout=600, backend="nccl")
     st = out[0]["stats"]
     assert st["accumulated"] == W * steps, st
     assert st["updates"] == steps  # accumulate = W
@@ -62,5 +63,6 @@ def test_async_ps_across_devices(pull, codec):
         assert o["doorbells"] == "device"
         assert o["finite"]
         assert o["versions"][-1] > 0
-        if pull == "device":
+        if pull == "device" and transport == "ipc":
             assert o["pull"] == "device"
+        assert o["transport"] == transport

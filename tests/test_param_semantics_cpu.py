@@ -34,13 +34,13 @@ def _data(rank, step):
     return torch.randn(8, 16, generator=g), torch.randint(0, 4, (8,), generator=g)
 
 
-def _train(rank, world, mode, steps=3):
+def _train(rank, world, mode, steps=3, transport="ipc"):
     import hipps
 
     m = Net()
     keep = {n: p.detach().clone() for n, p in m.named_parameters() if n.startswith(("unused", "frozen"))}
     opt = hipps.SGD(m.named_parameters(), lr=0.1, momentum=0.9, weight_decay=0.1, mode=mode, max_delay=0,
-                    accumulate=world)
+                    accumulate=world, async_transport=transport)
     for s in range(steps):
         x, y = _data(rank, s)
         opt.zero_grad()
@@ -52,9 +52,10 @@ def _train(rank, world, mode, steps=3):
     return {"keep": keep, "after": after, "moved": moved}
 
 
-@pytest.mark.parametrize("mode,world", [("local", 1), ("allgather", 2), ("ps_sync", 2), ("ps_async", 2)])
-def test_frozen_and_unused_params_untouched(mode, world):
-    out = run_world(_train, world, mode)
+@pytest.mark.parametrize("mode,world,transport", [("local", 1, "ipc"), ("allgather", 2, "ipc"), ("ps_sync", 2, "ipc"),
+                                                   ("ps_async", 2, "ipc"), ("ps_async", 2, "p2p")])
+def test_frozen_and_unused_params_untouched(mode, world, transport):
+    out = run_world(_train, world, mode, 3, transport)
     for r in range(world):
         o = out[r]
         assert o["moved"], "trained parameters must move"

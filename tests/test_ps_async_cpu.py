@@ -7,7 +7,7 @@ from test_dist_cpu import _data, _mlp
 
 
 def _train_async(rank, world, steps, codec, accumulate, max_delay, staleness, opt_name="sgd", bucket_mb=64.0,
-                 slots=0):
+                 slots=0, transport="ipc"):
     import hipps
 
     m = _mlp()
@@ -18,7 +18,7 @@ def _train_async(rank, world, steps, codec, accumulate, max_delay, staleness, op
     cls = hipps.SGD if opt_name == "sgd" else hipps.Adam
     kw = dict(lr=0.05, momentum=0.9) if opt_name == "sgd" else dict(lr=1e-3)
     opt = cls(m.named_parameters(), mode="ps_async", code=codec, accumulate=accumulate, max_delay=max_delay,
-              staleness=staleness, bucket_mb=bucket_mb, mailbox_slots=slots, **kw)
+              staleness=staleness, bucket_mb=bucket_mb, mailbox_slots=slots, async_transport=transport, **kw)
     nb = len(opt.engine.plan.buckets)
     init = [p.detach().clone() for p in m.parameters()]
     losses = []
@@ -91,3 +91,28 @@ def test_async_staleness_drop_and_adam():
     st = out[0]["stats"]
     assert st["accumulated"] + st["drops"] == 18
     assert st["updates"] == st["accumulated"]
+
+
+@pytest.mark.parametrize("codec,bucket_mb,slots", [("fp32", 64.0, 0), ("bf16", 0.0005, 2), ("topk_int8:0.1", 0.0005, 0)])
+def test_async_p2p_transport_converges_and_accounts(codec, bucket_mb, slots):
+    """Two-sided send/recv transport (pair channels; RCCL on GPU, gloo here): same protocol,
+    same accounting as the one-sided mailbox."""
+    steps = 10
+    out = run_world(_train_async, 3, steps, codec, 0, -1, -1, "sgd", bucket_mb, slots, "p2p")
+    st = out[0]["stats"]
+    assert st["accumulated"] == 3 * steps and st["updates"] == steps
+    for r in (1, 2):
+        for a, b in zip(out[0]["init"], out[r]["init"]):
+            assert torch.equal(a, b)
+    for r in range(3):
+        L = out[r]["losses"]
+        assert sum(L[-3:]) / 3 < sum(L[:3]) / 3
+
+
+def test_async_p2p_max_delay_zero_matches_ipc():
+    """SSP bound 0 with M = W: both transports apply the same synchronous update sequence."""
+    a = run_world(_train_async, 2, 5, "fp32", 2, 0, -1, "sgd", 64.0, 0, "p2p")
+    b = run_world(_train_async, 2, 5, "fp32", 2, 0, -1, "sgd", 64.0, 0, "ipc")
+    for r in range(2):
+        for x, y in zip(a[r]["params"], b[r]["params"]):
+            torch.testing.assert_close(x, y, rtol=0, atol=0)
