@@ -143,15 +143,33 @@ class MPI_PS(torch.optim.Optimizer):
         """Apply the optimizer to flat ``target`` from flat gradient ``sources`` (summed).
         ``mask`` (uint8 per 16-element chunk, FlatStore.chunk_mask) skips the parameters that
         produced no gradient this step, like ``if p.grad is None: continue`` (ps.py:178-179)."""
+        self._begin_update()
+        self._update_range(sources, target, 0, self.store.numel, gscale, zero_src, pub, mask)
+
+    def _begin_update(self):
+        """Start one optimizer step: advance every non-empty group's step counter once (the
+        update itself may then run as several flat ranges, e.g. one per bucket as its gradient
+        exchange lands)."""
+        for gi in range(len(self.param_groups)):
+            a, b = self.store.group_ranges[gi]
+            if b > a:
+                self._group_steps[gi] += 1
+
+    def _update_range(self, sources: List[torch.Tensor], target: torch.Tensor, lo: int, hi: int, gscale: float,
+                      zero_src: bool = False, pub: Optional[torch.Tensor] = None,
+                      mask: Optional[torch.Tensor] = None, src_lo: int = 0):
+        """Update flat elements [lo, hi) (16-aligned).  ``target``/``pub``/``mask`` index the whole
+        flat space; ``sources`` start at flat element ``src_lo`` (e.g. one bucket's images)."""
         for gi, group in enumerate(self.param_groups):
             a, b = self.store.group_ranges[gi]
-            if b == a:
+            a, b = max(a, lo), min(b, hi)
+            if b <= a:
                 continue
-            self._group_steps[gi] += 1
-            self._update_group(gi, group, [s[a:b] for s in sources], target[a:b], gscale, zero_src,
-                               None if pub is None else pub[a:b], None if mask is None else mask[a // 16:b // 16])
+            self._update_group(gi, group, [s[a - src_lo:b - src_lo] for s in sources], target[a:b], gscale,
+                               zero_src, None if pub is None else pub[a:b],
+                               None if mask is None else mask[a // 16:b // 16], a, b)
 
-    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub, mask=None):
+    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub, mask=None, lo=None, hi=None):
         raise NotImplementedError
 
     # ------------------------------------------------------------------ public API
@@ -262,15 +280,19 @@ class SGD(MPI_PS, torch.optim.SGD):
 
     optim = "sgd"
 
-    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub, mask=None):
+    def _begin_update(self):
+        super()._begin_update()
+        # buf = d_p on the first step (ps.py:203-205), decided once per step for every range
+        self._first_now = {gi for gi, g in enumerate(self.param_groups)
+                           if (g.get("momentum", 0) or 0) and not self._momentum_started(gi)}
+
+    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub, mask=None, lo=None, hi=None):
         mom = group.get("momentum", 0) or 0
-        a, b = self.store.group_ranges[gi]
+        a, b = (lo, hi) if lo is not None else self.store.group_ranges[gi]
         buf = self._ensure_state("momentum_buffer")[a:b] if mom else None
-        # buf = d_p on the first step (ps.py:203-205); with a mask, later-starting params get
-        # buf = (1-dampening)*d_p from the zero-initialised buffer (identical for dampening=0)
-        first = mom and mask is None and not self._momentum_started(gi)
-        if mom and mask is not None:
-            self._momentum_started(gi)
+        # with a mask, later-starting params get buf = (1-dampening)*d_p from the zero-initialised
+        # buffer (identical for dampening=0)
+        first = mom and mask is None and gi in getattr(self, "_first_now", ())
         ops.sgd_step(srcs, target, buf, pub, zero_src, gscale, lr=group["lr"],
                      weight_decay=group.get("weight_decay", 0) or 0, momentum=mom,
                      dampening=group.get("dampening", 0) or 0, nesterov=bool(group.get("nesterov", False)),
@@ -297,16 +319,18 @@ class Adam(MPI_PS, torch.optim.Adam):
 
     optim = "adam"
 
-    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub, mask=None):
-        a, b = self.store.group_ranges[gi]
+    def _begin_update(self):
+        super()._begin_update()
+        for s in self.store.slots:  # torch-compatible per-parameter step (state_dict readers)
+            self.state[s.param]["step"] = self._group_steps[s.group]
+
+    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub, mask=None, lo=None, hi=None):
+        a, b = (lo, hi) if lo is not None else self.store.group_ranges[gi]
         m = self._ensure_state("exp_avg")[a:b]
         v = self._ensure_state("exp_avg_sq")[a:b]
         ams = bool(group.get("amsgrad", False))
         vm = self._ensure_state("max_exp_avg_sq")[a:b] if ams else None
         step = self._group_steps[gi]
-        for s in self.store.slots:
-            if s.group == gi:
-                self.state[s.param]["step"] = step
         ops.adam_step(srcs, target, m, v, vm, pub, zero_src, gscale, lr=group["lr"], betas=group["betas"],
                       eps=group["eps"], weight_decay=group.get("weight_decay", 0) or 0, step=step, amsgrad=ams,
                       torch_mode=self.cfg.adam_variant == "torch", mask=mask)
