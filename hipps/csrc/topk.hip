@@ -5,16 +5,18 @@
 // is needed: the reference's per-tensor Iallgather of lengths (mpi_comms.py:150-158, M1) goes
 // away.  Wire: int32 idx[k] + val[k] (f32 or bf16), idx in ascending order.
 //
-// Three full passes over the bucket (round 1 made five), everything else on ~1% of it:
+// Four full passes over the bucket (round 1 made five plus three single-workgroup histogram
+// walks over all of it), everything else on ~1% of it:
 //   P1  hist of |x| bits 30..20 over the whole bucket (fused with the error-feedback fold
 //       r <- g + r, so later passes read one array)                               [full read]
 //   pick   single workgroup: the bin holding the k-th largest key
 //   P2  filter: keys in that bin -> candidate list (wave-aggregated append)         [full read]
 //   P3/P4  histograms of bits 19..9 and 8..0 over the candidates only, + picks -> exact k-th
 //       key T and how many == T to admit (lowest index first)
-//   P5  single-pass compaction with decoupled look-back: each 4096-element chunk takes a
-//       ticket, counts (> T, == T), publishes its aggregate, sums its predecessors' and writes
-//       its selected (index, value) pairs in index order                          [full read]
+//   P5  compaction in index order: per-4096-element-chunk counts (> T, == T) [full read], one
+//       workgroup scans the ~n/4096 counts, each chunk writes its selected (index, value) pairs
+//       at its prefix [full read].  (A decoupled look-back would save the count pass, but its
+//       chunk tickets are one atomic address and serialised to ~2 ms on a 25 M bucket.)
 // If the threshold bin holds more candidates than the list can take (e.g. mostly-zero
 // gradients) the candidate passes fall back to filtering the whole bucket (flag in device
 // state, no host sync).  Ties are admitted lowest-index-first, so the message is bitwise
@@ -49,17 +51,12 @@ struct SelState {        // lives in a small device workspace
 __device__ __forceinline__ uint32_t absbits(float x) { return __float_as_uint(x) & 0x7fffffffu; }
 
 __global__ __launch_bounds__(kBlock) void k_topk_init(SelState* __restrict__ st, uint32_t prefix, uint32_t mask,
-                                                      uint32_t k, uint32_t cap_cand,
-                                                      unsigned long long* __restrict__ flags, int64_t nchunks) {
-  if (blockIdx.x == 0) {
-    if (threadIdx.x == 0) {
-      st->prefix = prefix; st->mask = mask; st->remaining = k; st->ncand = 0; st->overflow = 0; st->ticket = 0;
-      st->cap_cand = cap_cand; st->pad = 0;
-    }
-    for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) st->hist[b] = 0;
+                                                      uint32_t k, uint32_t cap_cand) {
+  if (threadIdx.x == 0) {
+    st->prefix = prefix; st->mask = mask; st->remaining = k; st->ncand = 0; st->overflow = 0; st->ticket = 0;
+    st->cap_cand = cap_cand; st->pad = 0;
   }
-  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks; c += (int64_t)gridDim.x * blockDim.x)
-    flags[c] = 0ull;
+  for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) st->hist[b] = 0;
 }
 
 // P1 (and the overflow fallback of P3/P4): histogram over elements whose decided bits match
@@ -144,17 +141,23 @@ __global__ __launch_bounds__(kBlock) void k_topk_pick(int lo, int nbits, SelStat
   }
 }
 
-// P2: append every element of the selected top-11-bit bin to the candidate list.  One atomic
-// per wave per vector step (wave prefix sum of the lane counts).
+// P2: append every element of the selected top-11-bit bin to the candidate list.  Each
+// workgroup scans one contiguous range, collects its candidates in LDS and reserves global space
+// with ONE atomic at the end (a per-wave atomic on one address serialises ~10^5 times on a
+// 25 M-element bucket); an LDS overflow spills straight to global with per-element atomics.
+constexpr int kCandLds = 2048;
 __global__ __launch_bounds__(kBlock) void k_topk_filter(const float* __restrict__ src, int64_t n,
                                                         SelState* __restrict__ st, uint32_t* __restrict__ ckey,
                                                         uint32_t* __restrict__ cidx) {
+  __shared__ uint32_t lkey[kCandLds], lidx[kCandLds];
+  __shared__ uint32_t lcount, lbase;
   const uint32_t prefix = st->prefix, mask = st->mask, cap = st->cap_cand;
-  const int lane = threadIdx.x & 63;
-  const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
+  if (threadIdx.x == 0) lcount = 0;
+  __syncthreads();
   const int64_t nv = (n + 3) >> 2;
-  const int64_t nvw = (nv + 63) & ~(int64_t)63;  // whole waves stay in the loop (ballots)
-  for (int64_t v = gtid; v < nvw; v += stride) {
+  const int64_t per = (nv + gridDim.x - 1) / gridDim.x;
+  const int64_t v0 = (int64_t)blockIdx.x * per, v1 = v0 + per < nv ? v0 + per : nv;
+  for (int64_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
     const int64_t i = v << 2;
     uint32_t k[4] = {0u, 0u, 0u, 0u};
     bool m[4] = {false, false, false, false};
@@ -168,25 +171,26 @@ __global__ __launch_bounds__(kBlock) void k_topk_filter(const float* __restrict_
       for (int j = 0; j < 4; ++j)
         if (i + j < n) { k[j] = absbits(src[i + j]); m[j] = (k[j] & mask) == prefix; }
     }
-    const uint32_t mine = (uint32_t)m[0] + m[1] + m[2] + m[3];
-    // wave-exclusive scan of `mine`, one atomicAdd by the last lane
-    uint32_t incl = mine;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t a = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += a;
-    }
-    const uint32_t total = __shfl(incl, 63, 64);
-    if (total == 0) continue;
-    uint32_t base = 0;
-    if (lane == 63) base = atomicAdd(&st->ncand, total);
-    base = __shfl(base, 63, 64);
-    uint32_t pos = base + incl - mine;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       if (m[j]) {
-        if (pos < cap) { ckey[pos] = k[j]; cidx[pos] = (uint32_t)(i + j); }
-        ++pos;
+        const uint32_t p = atomicAdd(&lcount, 1u);
+        if (p < kCandLds) {
+          lkey[p] = k[j];
+          lidx[p] = (uint32_t)(i + j);
+        } else {  // spill (rare): straight to the global list
+          const uint32_t g = atomicAdd(&st->ncand, 1u);
+          if (g < cap) { ckey[g] = k[j]; cidx[g] = (uint32_t)(i + j); }
+        }
       }
+  }
+  __syncthreads();
+  const uint32_t cnt = lcount < kCandLds ? lcount : kCandLds;
+  if (threadIdx.x == 0) lbase = cnt ? atomicAdd(&st->ncand, cnt) : 0u;
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
+    const uint32_t g = lbase + j;
+    if (g < cap) { ckey[g] = lkey[j]; cidx[g] = lidx[j]; }
   }
 }
 
@@ -218,57 +222,110 @@ __global__ __launch_bounds__(kBlock) void k_topk_hist_cand(const uint32_t* __res
     if (h[b]) atomicAdd(&st->hist[b], h[b]);
 }
 
-// ---- P5: decoupled look-back compaction ---------------------------------------------------
-// Look-back word per chunk: bits 63..62 status (1 aggregate, 2 inclusive prefix), 61..31 the
-// == T count, 30..0 the > T count (n < 2^31).
-constexpr unsigned long long kStAgg = 1ull << 62, kStPre = 2ull << 62;
-__device__ __forceinline__ unsigned long long lb_pack(uint32_t gt, uint32_t eq, unsigned long long st) {
-  return st | ((unsigned long long)eq << 31) | (unsigned long long)gt;
+// ---- P5: compaction in index order: count -> scan -> write ------------------------------
+// A 4096-element chunk per workgroup (16 elements per lane as 4 coalesced float4 segments).
+// count: per-chunk (> T, == T) totals; scan: one workgroup turns them into exclusive prefixes
+// (6 k chunks for a 25 M bucket); write: each chunk re-reads its elements and places the
+// selected ones at prefix + local rank.  No spin-waits, no single-address atomics.
+__device__ __forceinline__ void chunk_load(const float* __restrict__ src, int64_t n, int64_t c, float (&x)[kCompactPer]) {
+#pragma unroll
+  for (int j = 0; j < kCompactPer / 4; ++j) {
+    const int64_t i = c * kChunk + (int64_t)j * (kBlock * 4) + threadIdx.x * 4;
+    if (i + 4 <= n) {
+      float4 t = *reinterpret_cast<const float4*>(src + i);
+      x[4 * j] = t.x; x[4 * j + 1] = t.y; x[4 * j + 2] = t.z; x[4 * j + 3] = t.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[4 * j + e] = (i + e < n) ? src[i + e] : 0.f;
+    }
+  }
+}
+
+// per segment j: (eq << 16) | gt of this lane's 4 elements (each <= 4)
+__device__ __forceinline__ void chunk_counts(int64_t n, int64_t c, uint32_t T, const float (&x)[kCompactPer],
+                                             uint32_t (&cnt)[kCompactPer / 4]) {
+#pragma unroll
+  for (int j = 0; j < kCompactPer / 4; ++j) {
+    const int64_t i = c * kChunk + (int64_t)j * (kBlock * 4) + threadIdx.x * 4;
+    uint32_t gt = 0, eq = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bool in = i + e < n;
+      const uint32_t k = absbits(x[4 * j + e]);
+      gt += in && k > T;
+      eq += in && k == T;
+    }
+    cnt[j] = (eq << 16) | gt;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_topk_count(const float* __restrict__ src, int64_t n,
+                                                       const SelState* __restrict__ st, uint32_t* __restrict__ cgt,
+                                                       uint32_t* __restrict__ ceq, int64_t nchunks) {
+  __shared__ uint32_t red[4];
+  const uint32_t T = st->prefix;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    float x[kCompactPer];
+    uint32_t cnt[kCompactPer / 4];
+    chunk_load(src, n, c, x);
+    chunk_counts(n, c, T, x, cnt);
+    uint32_t v = cnt[0] + cnt[1] + cnt[2] + cnt[3];  // <= 16 per field: packed sum stays exact
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t t = red[0] + red[1] + red[2] + red[3];  // <= 4096 per field
+      cgt[c] = t & 0xffffu;
+      ceq[c] = t >> 16;
+    }
+    __syncthreads();
+  }
+}
+
+// exclusive scan of both count arrays in place (one workgroup; nchunks ~ n / 4096)
+__global__ __launch_bounds__(1024) void k_topk_scan(uint32_t* __restrict__ cgt, uint32_t* __restrict__ ceq,
+                                                    int64_t nchunks, int32_t* __restrict__ count_out, uint32_t cap) {
+  __shared__ uint32_t sg[1024], se[1024];
+  __shared__ uint32_t carry_g, carry_e;
+  if (threadIdx.x == 0) { carry_g = 0; carry_e = 0; }
+  __syncthreads();
+  for (int64_t base = 0; base < nchunks; base += 1024) {
+    const int64_t c = base + threadIdx.x;
+    const uint32_t vg = c < nchunks ? cgt[c] : 0, ve = c < nchunks ? ceq[c] : 0;
+    sg[threadIdx.x] = vg; se[threadIdx.x] = ve;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+      const uint32_t ag = threadIdx.x >= off ? sg[threadIdx.x - off] : 0;
+      const uint32_t ae = threadIdx.x >= off ? se[threadIdx.x - off] : 0;
+      __syncthreads();
+      sg[threadIdx.x] += ag; se[threadIdx.x] += ae;
+      __syncthreads();
+    }
+    if (c < nchunks) { cgt[c] = carry_g + sg[threadIdx.x] - vg; ceq[c] = carry_e + se[threadIdx.x] - ve; }
+    __syncthreads();
+    if (threadIdx.x == 1023) { carry_g += sg[1023]; carry_e += se[1023]; }
+    __syncthreads();
+  }
+  if (count_out && threadIdx.x == 0) count_out[0] = (int32_t)(carry_g < cap ? carry_g : cap);
 }
 
 template <typename VT>
-__global__ __launch_bounds__(kBlock) void k_topk_compact(const float* __restrict__ src, float* __restrict__ resid,
-                                                         int64_t n, SelState* __restrict__ st,
-                                                         unsigned long long* __restrict__ flags, int64_t nchunks,
-                                                         int32_t* __restrict__ idx, VT* __restrict__ val, uint32_t cap,
-                                                         int32_t* __restrict__ count_out) {
-  __shared__ uint32_t s_chunk;
-  __shared__ uint32_t wsum[kCompactPer / 4][4];  // per segment, per wave: packed (eq << 16 | gt) totals
-  __shared__ uint32_t s_excl_gt, s_excl_eq;
+__global__ __launch_bounds__(kBlock) void k_topk_write(const float* __restrict__ src, float* __restrict__ resid,
+                                                       int64_t n, const SelState* __restrict__ st,
+                                                       const uint32_t* __restrict__ pgt, const uint32_t* __restrict__ peq,
+                                                       int64_t nchunks, int32_t* __restrict__ idx, VT* __restrict__ val,
+                                                       uint32_t cap) {
+  __shared__ uint32_t wsum[kCompactPer / 4][4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint32_t T = st->prefix, need_eq = st->remaining;
-  for (;;) {
-    if (threadIdx.x == 0) s_chunk = atomicAdd(&st->ticket, 1u);
-    __syncthreads();
-    const int64_t c = s_chunk;
-    if (c >= nchunks) return;
-    // load 16 elements: segment j covers [c*4096 + j*1024, +1024), lane-contiguous float4s
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
     float x[kCompactPer];
-    uint32_t cnt[kCompactPer / 4];  // per segment: (eq << 16) | gt of this thread's 4 elements
+    uint32_t cnt[kCompactPer / 4], incl[kCompactPer / 4];
+    chunk_load(src, n, c, x);
+    chunk_counts(n, c, T, x, cnt);
+    if (pgt[c] >= cap && need_eq == 0) continue;  // nothing of this chunk fits (threshold overflow)
 #pragma unroll
-    for (int j = 0; j < kCompactPer / 4; ++j) {
-      const int64_t i = c * kChunk + (int64_t)j * (kBlock * 4) + threadIdx.x * 4;
-      if (i + 4 <= n) {
-        float4 t = *reinterpret_cast<const float4*>(src + i);
-        x[4 * j] = t.x; x[4 * j + 1] = t.y; x[4 * j + 2] = t.z; x[4 * j + 3] = t.w;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) x[4 * j + e] = (i + e < n) ? src[i + e] : 0.f;
-      }
-      uint32_t gt = 0, eq = 0;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bool in = i + e < n;
-        const uint32_t k = absbits(x[4 * j + e]);
-        gt += in && k > T;
-        eq += in && k == T;
-      }
-      cnt[j] = (eq << 16) | gt;
-    }
-    // per-segment wave inclusive scans (index order: segment, then wave, then lane)
-    uint32_t incl[kCompactPer / 4];
-#pragma unroll
-    for (int j = 0; j < kCompactPer / 4; ++j) {
+    for (int j = 0; j < kCompactPer / 4; ++j) {  // index order: segment, wave, lane
       uint32_t v = cnt[j];
       for (int o = 1; o < 64; o <<= 1) {
         const uint32_t a = __shfl_up(v, o, 64);
@@ -278,88 +335,17 @@ __global__ __launch_bounds__(kBlock) void k_topk_compact(const float* __restrict
       if (lane == 63) wsum[j][w] = v;
     }
     __syncthreads();
-    // chunk aggregate and this thread's exclusive offset inside the chunk
-    uint32_t agg = 0;
-#pragma unroll
-    for (int j = 0; j < kCompactPer / 4; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) agg += wsum[j][q];
-    // elements of earlier segments + earlier waves of this segment precede this thread
-    uint32_t off[kCompactPer / 4];
-    {
-      uint32_t run = 0;
-#pragma unroll
-      for (int j = 0; j < kCompactPer / 4; ++j) {
-        uint32_t wb = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) wb += (q < w) ? wsum[j][q] : 0u;
-        off[j] = run + wb + incl[j] - cnt[j];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) run += wsum[j][q];
-      }
-    }
-    const uint32_t agg_gt = agg & 0xffffu, agg_eq = agg >> 16;  // <= 4096 each: no field overflow
-    // publish the aggregate, look back for the exclusive prefix, publish the inclusive prefix.
-    // Wave 0 inspects 64 predecessors per step (one flag per lane): the nearest inclusive prefix
-    // ends the walk, aggregates before it are summed; a not-yet-published predecessor in front of
-    // it (it holds an earlier ticket, so it is running) is re-read.  Bounded: never hangs.
-    if (w == 0) {
-      unsigned long long* fl = flags;
-      uint32_t eg = 0, ee = 0;
-      if (c == 0) {
-        if (lane == 0)
-          __hip_atomic_store(fl, lb_pack(agg_gt, agg_eq, kStPre), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        if (lane == 0)
-          __hip_atomic_store(fl + c, lb_pack(agg_gt, agg_eq, kStAgg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        int64_t base = c - 1;
-        uint32_t spins = 0;
-        for (;;) {
-          const int64_t p = base - lane;
-          const unsigned long long f =
-              p >= 0 ? __hip_atomic_load(fl + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : kStPre;
-          const unsigned long long stt = f & (3ull << 62);
-          const unsigned long long pre = __ballot(stt == kStPre), zero = __ballot(stt == 0);
-          const int first = pre ? __ffsll((long long)pre) - 1 : 64;
-          const unsigned long long before = first == 64 ? ~0ull : ((1ull << first) - 1ull);
-          if (zero & before) {
-            if (++spins > (1u << 24)) break;  // never reached in a healthy run
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-          }
-          uint32_t vg = 0, ve = 0;
-          if (lane <= first) {
-            vg = (uint32_t)(f & 0x7fffffffull);
-            ve = (uint32_t)((f >> 31) & 0x7fffffffull);
-          }
-          for (int o = 32; o > 0; o >>= 1) {
-            vg += __shfl_xor(vg, o, 64);
-            ve += __shfl_xor(ve, o, 64);
-          }
-          eg += vg;
-          ee += ve;
-          if (first < 64) break;
-          base -= 64;
-        }
-        if (lane == 0)
-          __hip_atomic_store(fl + c, lb_pack(eg + agg_gt, ee + agg_eq, kStPre), __ATOMIC_RELEASE,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (lane == 0) {
-        s_excl_gt = eg;
-        s_excl_eq = ee;
-        if (count_out && c == nchunks - 1) {
-          const uint32_t tot = eg + agg_gt;
-          count_out[0] = (int32_t)(tot < cap ? tot : cap);
-        }
-      }
-    }
-    __syncthreads();
-    const uint32_t xg = s_excl_gt, xe = s_excl_eq;
+    uint32_t run = 0;
 #pragma unroll
     for (int j = 0; j < kCompactPer / 4; ++j) {
+      uint32_t wb = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wb += (q < w) ? wsum[j][q] : 0u;
+      const uint32_t off = run + wb + incl[j] - cnt[j];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) run += wsum[j][q];
       const int64_t i = c * kChunk + (int64_t)j * (kBlock * 4) + threadIdx.x * 4;
-      uint32_t bg = xg + (off[j] & 0xffffu), be = xe + (off[j] >> 16);
+      uint32_t bg = pgt[c] + (off & 0xffffu), be = peq[c] + (off >> 16);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         if (i + e >= n) break;
@@ -375,7 +361,7 @@ __global__ __launch_bounds__(kBlock) void k_topk_compact(const float* __restrict
         be += iseq;
       }
     }
-    __syncthreads();  // s_chunk / wsum reuse
+    __syncthreads();  // wsum reuse
   }
 }
 
@@ -413,7 +399,8 @@ namespace {
 
 struct TopkWs {
   SelState* st;
-  unsigned long long* flags;
+  uint32_t* cgt;  // per-chunk counts, then exclusive prefixes
+  uint32_t* ceq;
   uint32_t* ckey;
   uint32_t* cidx;
   int64_t nchunks;
@@ -431,27 +418,28 @@ TopkWs carve(at::Tensor& workspace, int64_t n) {
   const int64_t need = ws_bytes_for(n);
   TORCH_CHECK(workspace.is_cuda() && workspace.numel() * workspace.element_size() >= need,
               "workspace too small: need ", need, " bytes (topk_workspace_bytes)");
-  static_assert(sizeof(SelState) % 16 == 0, "SelState keeps the look-back words aligned");
+  static_assert(sizeof(SelState) % 16 == 0, "SelState keeps the count arrays aligned");
   char* ws = (char*)workspace.data_ptr();
   TORCH_CHECK(reinterpret_cast<uintptr_t>(ws) % 16 == 0, "workspace must be 16-byte aligned");
   TopkWs w;
   w.st = reinterpret_cast<SelState*>(ws);
   w.nchunks = (n + kChunk - 1) / kChunk;
   w.cap = cand_cap(n);
-  w.flags = reinterpret_cast<unsigned long long*>(ws + sizeof(SelState));
-  w.ckey = reinterpret_cast<uint32_t*>(w.flags + w.nchunks);
+  w.cgt = reinterpret_cast<uint32_t*>(ws + sizeof(SelState));
+  w.ceq = w.cgt + w.nchunks;
+  w.ckey = w.ceq + w.nchunks;
   w.cidx = w.ckey + w.cap;
   return w;
 }
-
-int init_grid(int64_t nchunks) { return (int)std::max<int64_t>(1, std::min<int64_t>(kMaxGrid, (nchunks + kBlock - 1) / kBlock)); }
 
 template <typename VT>
 void launch_compact(hipStream_t stream, const float* src, float* rp, int64_t n, const TopkWs& w, int32_t* idx, VT* val,
                     uint32_t cap, int32_t* count_out) {
   const int grid = (int)std::min<int64_t>(w.nchunks, kMaxGrid);
-  hipLaunchKernelGGL(k_topk_compact<VT>, grid, kBlock, 0, stream, src, rp, n, w.st, w.flags, w.nchunks, idx, val, cap,
-                     count_out);
+  hipLaunchKernelGGL(k_topk_count, grid, kBlock, 0, stream, src, n, w.st, w.cgt, w.ceq, w.nchunks);
+  hipLaunchKernelGGL(k_topk_scan, 1, 1024, 0, stream, w.cgt, w.ceq, w.nchunks, count_out, cap);
+  hipLaunchKernelGGL(k_topk_write<VT>, grid, kBlock, 0, stream, src, rp, n, w.st, w.cgt, w.ceq, w.nchunks, idx, val,
+                     cap);
 }
 
 }  // namespace
@@ -474,18 +462,19 @@ void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::T
     rp = resid->data_ptr<float>();
   }
   auto stream = c10::hip::getCurrentHIPStream();
-  hipLaunchKernelGGL(k_topk_init, init_grid(w.nchunks), kBlock, 0, stream, w.st, 0u, 0u, (uint32_t)k,
-                     (uint32_t)w.cap, w.flags, w.nchunks);
+  hipLaunchKernelGGL(k_topk_init, 1, kBlock, 0, stream, w.st, 0u, 0u, (uint32_t)k, (uint32_t)w.cap);
   const int grid = grid_for(n >> 2);
+  // histogram grids stay <= 1024 workgroups: every workgroup merges its bins with global atomics
+  const int hgrid = std::min(grid, 1024);
   // P1: fold + top-11-bit histogram over the whole bucket
-  hipLaunchKernelGGL(k_topk_hist, grid, kBlock, 0, stream, g.data_ptr<float>(), rp, (int)(rp != nullptr), n, 20, 11,
+  hipLaunchKernelGGL(k_topk_hist, hgrid, kBlock, 0, stream, g.data_ptr<float>(), rp, (int)(rp != nullptr), n, 20, 11,
                      w.st, 0);
   hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 20, 11, w.st);
   const float* src = rp ? rp : g.data_ptr<float>();
-  // P2: candidates of the selected bin
+  // P2: candidates of the selected bin (one contiguous range per workgroup)
   hipLaunchKernelGGL(k_topk_filter, grid, kBlock, 0, stream, src, n, w.st, w.ckey, w.cidx);
   // P3/P4 on the candidates
-  const int cgrid = (int)std::max<int64_t>(1, std::min<int64_t>(kMaxGrid, w.cap / 1024));
+  const int cgrid = (int)std::max<int64_t>(1, std::min<int64_t>(1024, w.cap / 1024));
   hipLaunchKernelGGL(k_topk_hist_cand, cgrid, kBlock, 0, stream, w.ckey, src, n, 9, 11, w.st);
   hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 9, 11, w.st);
   hipLaunchKernelGGL(k_topk_hist_cand, cgrid, kBlock, 0, stream, w.ckey, src, n, 0, 9, w.st);
@@ -541,8 +530,7 @@ void thresh_encode(at::Tensor g, c10::optional<at::Tensor> resid, double tau, at
   uint32_t tbits;
   std::memcpy(&tbits, &t, 4);
   // T = tau exactly, no ties admitted: every |x| > tau, in index order (one look-back pass)
-  hipLaunchKernelGGL(k_topk_init, init_grid(w.nchunks), kBlock, 0, stream, w.st, tbits, 0xffffffffu, 0u,
-                     (uint32_t)w.cap, w.flags, w.nchunks);
+  hipLaunchKernelGGL(k_topk_init, 1, kBlock, 0, stream, w.st, tbits, 0xffffffffu, 0u, (uint32_t)w.cap);
   const float* src = rp ? rp : g.data_ptr<float>();
   if (val.scalar_type() == at::kFloat)
     launch_compact<float>(stream, src, rp, n, w, idx.data_ptr<int32_t>(), val.data_ptr<float>(), (uint32_t)cap,

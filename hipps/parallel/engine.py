@@ -517,18 +517,149 @@ class LocalEngine(Engine):
         return data
 
 
-class AllGatherEngine(Engine):
-    """Reference semantics (ps.py:140-190) with static-size device messages: ONE all-gather of
-    the whole wire buffer per step (no per-tensor size round, M1 removed)."""
+class _BucketExchange(Engine):
+    """Per-bucket collectives posted as soon as a bucket is encoded (from the post-accumulate-grad
+    hook, on the comm stream), so the exchange of the last layers' gradients overlaps the rest of
+    backward -- the reference cannot start communicating before every tensor is encoded
+    (ps.py:128-132).  Buckets are posted strictly in ready order (the same on every rank, whatever
+    the hook timing), re-posted if more gradient arrives after their encode (backward() twice),
+    and land bucket-major: bucket b's W messages are contiguous at W * b.wire_offset, so each is
+    one collective and one fused update range."""
+
+    root: Optional[int] = None  # None: all-gather; else gather to this rank
+
+    def _init_exchange(self):
+        W = self.world.size
+        self._receives = self.root is None or self.world.rank == self.root
+        dev = self.store.device
+        self.gathered = torch.empty(W * self.plan.wire_nbytes, dtype=torch.uint8, device=dev) if self._receives else None
+        self.gathered_pres = torch.empty(W * self.pres_bytes, dtype=torch.uint8, device=dev) if self._receives else None
+        self._scratch = None if self.plan.dense_ok else torch.empty_like(self.store.grad)
+        # the race detector compares the posting sequence BEFORE anything is posted, so it turns
+        # the hook-time posting off (a mismatched collective would otherwise deadlock first)
+        self._overlap = bool(self.cfg.overlap) and not self.is_object and not self.cfg.debug_check_order
+        self._posted = [False] * len(self.plan.buckets)
+        self._events = [None] * len(self.plan.buckets)
+        self._next = 0
+        self._init_failure_handling()
+
+    def _collective(self, out, inp):
+        if self.rccl is not None:
+            if self.root is None:
+                self.rccl.all_gather_into(out, inp, self.comm_stream)
+            else:
+                self.rccl.gather_into(out, inp, self.root, self.comm_stream)
+        elif self.root is None:
+            all_gather_into(out, inp, self.world, group=self.group)
+        else:
+            gather_into(out, inp, self.world, dst=self.root, group=self.group)
+
+    def _post(self, bi: int):
+        b = self.plan.buckets[bi]
+        W = self.world.size
+        src = self.plan.message(self.wire, bi)
+        off = W * b.wire_offset
+        out = self.gathered[off:off + W * b.msg_nbytes] if self._receives else None
+        if self.cuda:
+            with torch.cuda.stream(self.comm_stream), self.tracer.phase("comm", self.comm_stream):
+                self._collective(out, src)
+                ev = torch.cuda.Event()
+                ev.record(self.comm_stream)
+                self._events[bi] = ev
+        else:
+            self._collective(out, src)
+        self._posted[bi] = True
+
+    def encode_bucket(self, bi: int):
+        super().encode_bucket(bi)
+        if not self._overlap:
+            return
+        if self._posted[bi]:  # more gradient after the first post: send the bucket again
+            self._post(bi)
+            return
+        ro = self.plan.ready_order
+        while self._next < len(ro) and self._encoded[ro[self._next]]:
+            self._post(ro[self._next])
+            self._next += 1
+
+    def _exchange(self):
+        """Post what the hooks did not, then the presence bytes; returns host seconds."""
+        t = time.perf_counter()
+        for bi in self.plan.ready_order:
+            if not self._posted[bi]:
+                self._post(bi)
+        if self.cfg.skip_missing_grads:
+            self.write_presence()
+            pres = self.wire[self.pres_off:self.pres_off + self.pres_bytes]
+            if self.cuda:
+                with torch.cuda.stream(self.comm_stream):
+                    self._collective(self.gathered_pres, pres)
+            else:
+                self._collective(self.gathered_pres, pres)
+        self._posted = [False] * len(self._posted)
+        self._next = 0
+        return time.perf_counter() - t
+
+    def _msgs(self, bi: int) -> List[torch.Tensor]:
+        b = self.plan.buckets[bi]
+        W, off, n = self.world.size, self.world.size * b.wire_offset, b.msg_nbytes
+        del W
+        return [self.gathered[off + r * n:off + (r + 1) * n] for r in range(self.world.size)]
+
+    def _apply_buckets(self, target: torch.Tensor, pub: Optional[torch.Tensor], gscale: float):
+        """Decode + sum in rank order + fused update, bucket by bucket as each one has landed."""
+        ns = len(self.store.slots)
+        mask = None
+        if self.cfg.skip_missing_grads:
+            if self.cuda:
+                torch.cuda.current_stream(self.store.device).wait_stream(self.comm_stream)
+            pres = self.gathered_pres.view(self.world.size, self.pres_bytes)[:, :ns].amax(0)
+            mask = self.store.chunk_mask(pres)
+        if self.plan.guarded:
+            if self.cuda:
+                torch.cuda.current_stream(self.store.device).wait_stream(self.comm_stream)
+            for bi, b in enumerate(self.plan.buckets):
+                for r, m in enumerate(self._msgs(bi)):
+                    if bool(self.plan.bad_guard(m, b.layout.nbytes)):
+                        raise RuntimeError(f"wire canary overwritten (exchange, rank {r} bucket {bi})")
+        cur = torch.cuda.current_stream(self.store.device) if self.cuda else None
+        if self.plan.dense_ok:
+            self.opt._begin_update()
+            for bi in self.plan.ready_order:
+                b = self.plan.buckets[bi]
+                if cur is not None and self._events[bi] is not None:
+                    cur.wait_event(self._events[bi])
+                dt = b.layout.fields[0].dtype
+                imgs = [m[:b.layout.nbytes].view(dt) for m in self._msgs(bi)]
+                self.opt._update_range(imgs, target, b.lo, b.hi, gscale, False, pub, mask, src_lo=b.lo)
+            return
+        acc = self._scratch
+        for bi in self.plan.ready_order:
+            b = self.plan.buckets[bi]
+            if cur is not None and self._events[bi] is not None:
+                cur.wait_event(self._events[bi])
+            msgs = [b.layout.views(m[:b.layout.nbytes]) for m in self._msgs(bi)]
+            self.codec.accumulate(msgs, acc[b.lo:b.hi], 1.0, False)
+        self.opt._update_flat([acc], target, gscale, zero_src=False, pub=pub, mask=mask)
+
+    def _finish_comm(self):
+        if self.cuda:
+            torch.cuda.current_stream(self.store.device).wait_stream(self.comm_stream)
+            if self.rccl is not None:
+                self.rccl.poll()
+
+
+class AllGatherEngine(_BucketExchange):
+    """Reference semantics (ps.py:140-190) with static-size device messages: every rank gets every
+    rank's code for each bucket (one all-gather per bucket, posted during backward), decodes and
+    sums them in rank order and steps locally -> bitwise-identical replicas.  No per-tensor size
+    round (M1 removed)."""
 
     name = "allgather"
 
     def __init__(self, *a, **k):
         super().__init__(*a, **k)
-        W = self.world.size
-        self.gathered = torch.empty(W * self.wire_total, dtype=torch.uint8, device=self.store.device)
-        self._scratch = None if self.plan.dense_ok else torch.empty_like(self.store.grad)
-        self._init_failure_handling()
+        self._init_exchange()
 
     def step(self):
         with armed(self.watchdog, f"allgather step {self.steps + 1}"):
@@ -552,54 +683,36 @@ class AllGatherEngine(Engine):
             data["grad_bytes_recv"] = sum(len(b) for b in blobs)
             self.steps += 1
             return data
-        self.write_presence()
+        data["isend_time"] = self._exchange()
         t = time.perf_counter()
-        if self.cuda:
-            with torch.cuda.stream(self.comm_stream), self.tracer.phase("comm", self.comm_stream):
-                if self.rccl is not None:
-                    self.rccl.all_gather_into(self.gathered, self.wire, self.comm_stream)
-                else:
-                    all_gather_into(self.gathered, self.wire, self.world, group=self.group)
-            torch.cuda.current_stream(self.store.device).wait_stream(self.comm_stream)
-            if self.rccl is not None:
-                self.rccl.poll()
-        else:
-            with self.tracer.phase("comm"):
-                all_gather_into(self.gathered, self.wire, self.world, group=self.group)
-        data["isend_time"] = data["comm_wait"] = time.perf_counter() - t
-        t = time.perf_counter()
-        n = self.wire_total
-        msgs = [self.gathered[w * n:(w + 1) * n] for w in range(self.world.size)]
-        self.verify_guards(msgs, "allgather")
         with self.tracer.phase("update"):
-            self.apply(msgs, self.store.data, None, self.gscale(self.world.size), self._scratch,
-                       mask=self.gathered_mask(msgs))
+            self._apply_buckets(self.store.data, None, self.gscale(self.world.size))
+        self._finish_comm()
+        data["comm_wait"] = 0.0
         data["optim_step_time"] = time.perf_counter() - t
         data["decode_time"] = 0.0
         data.update(self.step_metrics())
         data.update(self.bytes_per_step())
-        data["grad_bytes_recv"] = n * self.world.size
+        data["grad_bytes_recv"] = self.plan.wire_nbytes * self.world.size
         data.update(self.tracer.collect())
         self.steps += 1
         return data
 
 
-class PSSyncEngine(Engine):
-    """Centralized synchronous PS: gather -> rank-0 aggregate+update -> broadcast params."""
+class PSSyncEngine(_BucketExchange):
+    """Centralized synchronous PS: per-bucket gather to rank 0 (posted during backward) -> rank 0
+    decodes, sums in rank order and updates -> broadcast of the parameters."""
 
     name = "ps_sync"
+    root = 0
 
     def __init__(self, *a, **k):
         super().__init__(*a, **k)
-        W = self.world.size
         dev = self.store.device
-        self.gathered = (torch.empty(W * self.wire_total, dtype=torch.uint8, device=dev)
-                         if self.world.is_ps else torch.empty(self.wire_total, dtype=torch.uint8, device=dev))
-        self._scratch = None if self.plan.dense_ok else torch.empty_like(self.store.grad)
         self.pub = None
         if self.cfg.param_wire == "bf16":
             self.pub = torch.empty(self.store.numel, dtype=torch.bfloat16, device=dev)
-        self._init_failure_handling()
+        self._init_exchange()
 
     def step(self):
         with armed(self.watchdog, f"ps_sync step {self.steps + 1}"):
@@ -624,29 +737,14 @@ class PSSyncEngine(Engine):
             data.update(self.bytes_per_step())
             self.steps += 1
             return data
-        self.write_presence()
-        t = time.perf_counter()
-        cs = self.comm_stream
-        ctx = torch.cuda.stream(cs) if self.cuda else _null()
         self.verify_guards([self.wire], "encode")
-        with ctx, self.tracer.phase("comm", cs):
-            if self.rccl is not None:  # one ncclGather (rccl.h:745)
-                self.rccl.gather_into(self.gathered if self.world.is_ps else None, self.wire, 0, cs)
-            else:
-                gather_into(self.gathered if self.world.is_ps else None, self.wire, self.world, group=self.group)
-        if self.cuda:
-            torch.cuda.current_stream(self.store.device).wait_stream(cs)
-            if self.rccl is not None:
-                self.rccl.poll()
-        data["comm_wait"] = data["isend_time"] = time.perf_counter() - t
+        data["isend_time"] = self._exchange()
         t = time.perf_counter()
         if self.world.is_ps:
-            n = self.wire_total
-            msgs = [self.gathered[w * n:(w + 1) * n] for w in range(self.world.size)]
-            self.verify_guards(msgs, "gather")
             with self.tracer.phase("update"):
-                self.apply(msgs, self.store.data, self.pub, self.gscale(self.world.size), self._scratch,
-                           mask=self.gathered_mask(msgs))
+                self._apply_buckets(self.store.data, self.pub, self.gscale(self.world.size))
+        self._finish_comm()
+        data["comm_wait"] = 0.0
         data["optim_step_time"] = time.perf_counter() - t
         self._bcast_params(data)
         data["decode_time"] = 0.0
