@@ -143,6 +143,9 @@ def main():
     elapsed = float(el.item())
     final_loss = float(loss.float().item())
     grad_bytes = int(last.get("grad_bytes_sent", 0)) if last else 0
+    # bytes that carry information in the last step's messages (reads the device count header of
+    # variable-size codecs; outside the timed region)
+    grad_used = opt.engine.wire_bytes_used() if not opt.engine.is_object else grad_bytes
     trace = None
     if tr.enabled:
         tr.flush()
@@ -182,6 +185,7 @@ def main():
                 "codec": a.codec,
                 "accumulate": a.accumulate or N,
                 "grad_bytes_per_step_per_worker": grad_bytes,
+                "grad_bytes_per_step_used": int(grad_used),
                 "param_wire": a.param_wire,
                 "num_params": nparams,
                 "buckets": nbuckets,

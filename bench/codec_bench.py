@@ -129,7 +129,8 @@ def main():
     for n in sizes[:4]:
         arr = np.random.randn(n).astype(np.float32)
         dumps, loads, comp = [], [], []
-        for _ in range(100):
+        reps = int(max(3, min(100, 4e7 // n)))  # zlib of a 100 MB pickle takes seconds
+        for _ in range(reps):
             t = time.perf_counter()
             b = pickle.dumps(arr)
             dumps.append(time.perf_counter() - t)
@@ -150,7 +151,7 @@ def main():
             continue
         payload = arr.tobytes()
         md, ml = [], []
-        for _ in range(100):
+        for _ in range(reps):
             t = time.perf_counter()
             mb = msgpack.packb({"shape": [n], "dtype": "float32", "data": payload})
             md.append(time.perf_counter() - t)

@@ -95,6 +95,15 @@ class Codec:
     def dense_source(self, views: Dict[str, torch.Tensor]) -> torch.Tensor:
         raise NotImplementedError
 
+    def push_copy(self, layout: "WireLayout", src: torch.Tensor, dst: torch.Tensor) -> bool:
+        """Copy one message for the async PS push; codecs with a device-side count move only the
+        used part.  Returns False to let the caller do a plain copy."""
+        return False
+
+    def used_bytes(self, layout: "WireLayout", msg: torch.Tensor) -> int:
+        """Bytes of ``msg`` that carry information (host read for variable-size codecs)."""
+        return layout.nbytes
+
     def nbytes(self, n: int) -> int:
         return self.layout(n).nbytes
 
@@ -288,6 +297,19 @@ class Threshold(Codec):
     def count(views) -> int:
         """Host read of a message's element count (diagnostics only; forces a sync)."""
         return int(views["count"][0])
+
+    def push_copy(self, layout, src, dst) -> bool:
+        if not src.is_cuda:
+            return False
+        f = {fl.name: fl for fl in layout.fields}
+        ops.native().copy_counted(src, dst, f["idx"].offset, f["val"].offset,
+                                  torch.empty((), dtype=self.value_dtype).element_size(), f["idx"].numel)
+        return True
+
+    def used_bytes(self, layout, msg) -> int:
+        f = {fl.name: fl for fl in layout.fields}
+        k = min(int(msg[:4].view(torch.int32)[0]), f["idx"].numel)
+        return 16 + k * (4 + torch.empty((), dtype=self.value_dtype).element_size())
 
 
 class ObjectCodec(Codec):

@@ -29,6 +29,7 @@ void topk_q8_residual(at::Tensor idx, at::Tensor v, at::Tensor q, at::Tensor sca
 void thresh_encode(at::Tensor g, c10::optional<at::Tensor> resid, double tau, at::Tensor count, at::Tensor idx,
                    at::Tensor val, at::Tensor workspace);
 void thresh_accumulate(at::Tensor count, at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale);
+void copy_counted(at::Tensor src, at::Tensor dst, int64_t idx_off, int64_t val_off, int64_t val_esz, int64_t cap);
 // norm.hip
 void bn_forward_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, at::Tensor weight, at::Tensor bias,
                       c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var, at::Tensor mean,
@@ -97,6 +98,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("topk_q8_residual", &hipps::topk_q8_residual, "EF: r[idx] += v - deq(q)");
   m.def("thresh_encode", &hipps::thresh_encode, "variable-size |x|>tau sparsification, device count header");
   m.def("thresh_accumulate", &hipps::thresh_accumulate, "acc[idx[:count]] += gscale * val[:count]");
+  m.def("copy_counted", &hipps::copy_counted, "copy a [count | idx | val] message moving only count entries");
   m.def("bn_forward_train", &hipps::bn_forward_train, "fused channels-last BN train fwd (+res) (+relu)");
   m.def("bn_apply", &hipps::bn_apply, "y = act(x*scale + shift (+res))");
   m.def("bn_backward", &hipps::bn_backward, "fused BN bwd with relu-mask recompute (+dres)");

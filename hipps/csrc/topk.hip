@@ -540,6 +540,40 @@ void thresh_encode(at::Tensor g, c10::optional<at::Tensor> resid, double tau, at
                              count.data_ptr<int32_t>());
 }
 
+// Copy a threshold message [count header | idx[cap] | val[cap]] moving only what the count says:
+// the async PS push of a variable-size code costs 16 + count * (4 + value bytes) over xGMI instead
+// of the static capacity (README.md:28-31 "unknown size" without a size round trip).
+__global__ __launch_bounds__(kBlock) void k_copy_counted(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                         int64_t idx_off, int64_t val_off, int val_esz, int64_t cap) {
+  const int64_t k = min((int64_t)reinterpret_cast<const int32_t*>(src)[0], cap);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t0 < 4) reinterpret_cast<int32_t*>(dst)[t0] = reinterpret_cast<const int32_t*>(src)[t0];
+  const int32_t* si = reinterpret_cast<const int32_t*>(src + idx_off);
+  int32_t* di = reinterpret_cast<int32_t*>(dst + idx_off);
+  for (int64_t j = t0; j < k; j += stride) di[j] = si[j];
+  if (val_esz == 4) {
+    const float* sv = reinterpret_cast<const float*>(src + val_off);
+    float* dv = reinterpret_cast<float*>(dst + val_off);
+    for (int64_t j = t0; j < k; j += stride) dv[j] = sv[j];
+  } else {
+    const uint16_t* sv = reinterpret_cast<const uint16_t*>(src + val_off);
+    uint16_t* dv = reinterpret_cast<uint16_t*>(dst + val_off);
+    for (int64_t j = t0; j < k; j += stride) dv[j] = sv[j];
+  }
+}
+
+void copy_counted(at::Tensor src, at::Tensor dst, int64_t idx_off, int64_t val_off, int64_t val_esz, int64_t cap) {
+  TORCH_CHECK(src.is_cuda() && dst.is_cuda() && src.scalar_type() == at::kByte && dst.scalar_type() == at::kByte,
+              "copy_counted: uint8 device buffers");
+  TORCH_CHECK(val_esz == 2 || val_esz == 4, "value size 2 or 4");
+  TORCH_CHECK(src.numel() >= val_off + cap * val_esz && dst.numel() >= val_off + cap * val_esz, "message too small");
+  TORCH_CHECK(idx_off % 4 == 0 && val_off % 4 == 0 && reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16 == 0, "alignment");
+  hipLaunchKernelGGL(k_copy_counted, grid_for(std::max<int64_t>(cap, 4)), kBlock, 0, c10::hip::getCurrentHIPStream(),
+                     src.data_ptr<uint8_t>(), dst.data_ptr<uint8_t>(), idx_off, val_off, (int)val_esz, cap);
+}
+
 void thresh_accumulate(at::Tensor count, at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale) {
   TORCH_CHECK(acc.is_cuda() && acc.scalar_type() == at::kFloat, "acc: f32 device tensor");
   const int64_t cap = idx.numel();

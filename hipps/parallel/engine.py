@@ -387,6 +387,13 @@ class Engine:
                 if k in st:
                     st[k].copy_(v)
 
+    def wire_bytes_used(self) -> int:
+        """Bytes of this rank's last step messages that carry information (host read: for the
+        variable-size codecs it reads every bucket's device count header -- diagnostics only)."""
+        if self.cuda:
+            torch.cuda.current_stream(self.store.device).wait_stream(self.comm_stream)
+        return sum(self.codec.used_bytes(b.layout, self.plan.message(self.wire, b.index)) for b in self.plan.buckets)
+
     def bytes_per_step(self) -> Dict[str, int]:
         if self.is_object:
             return {"grad_bytes_sent": int(self.codec.last_packaged_bytes)}

@@ -609,7 +609,9 @@ class PSAsyncEngine(Engine):
             if self.cuda:
                 cs = self.comm_stream
                 with torch.cuda.stream(cs), self.tracer.phase("push", cs):
-                    dst.copy_(src, non_blocking=True)
+                    # variable-size codes (threshold) move 16 + count * entry bytes, not capacity
+                    if self.plan.guarded or not self.codec.push_copy(b.layout, src, dst):
+                        dst.copy_(src, non_blocking=True)
                     if last and partial:
                         ns = len(self.store.slots)
                         sbuf[self.slot_pres:self.slot_pres + ns].copy_(self.presence_tensor(), non_blocking=True)
