@@ -211,7 +211,7 @@ class TopK(Codec):
         if self.error_feedback:
             st["resid"] = torch.zeros(n, dtype=torch.float32, device=device)
         if device is not None and torch.device(device).type == "cuda":
-            st["ws"] = torch.empty(ops.topk_workspace_bytes(n), dtype=torch.uint8, device=device)
+            st["ws"] = torch.zeros(ops.topk_workspace_bytes(n, self.k_of(n)), dtype=torch.uint8, device=device)
         return st
 
     def encode_into(self, x, views, state):
@@ -281,7 +281,7 @@ class Threshold(Codec):
         if self.error_feedback:
             st["resid"] = torch.zeros(n, dtype=torch.float32, device=device)
         if device is not None and torch.device(device).type == "cuda":
-            st["ws"] = torch.empty(ops.topk_workspace_bytes(n), dtype=torch.uint8, device=device)
+            st["ws"] = torch.zeros(ops.topk_workspace_bytes(n, self.cap_of(n)), dtype=torch.uint8, device=device)
         return st
 
     def encode_into(self, x, views, state):

@@ -22,7 +22,7 @@ void q8_aggregate(const std::vector<at::Tensor>& qs, const std::vector<at::Tenso
 // topk.hip
 void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::Tensor idx, at::Tensor val,
                  at::Tensor workspace);
-int64_t topk_workspace_bytes(int64_t n);
+int64_t topk_workspace_bytes(int64_t n, int64_t k);
 void topk_accumulate(at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale);
 void topk_q8_accumulate(at::Tensor idx, at::Tensor q, at::Tensor scales, at::Tensor acc, double gscale);
 void topk_q8_residual(at::Tensor idx, at::Tensor v, at::Tensor q, at::Tensor scales, at::Tensor resid);
@@ -92,7 +92,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("q8_encode", &hipps::q8_encode, "per-256-block absmax int8 quantization (+EF, +stochastic)");
   m.def("q8_aggregate", &hipps::q8_aggregate, "acc (+)= gscale * sum_w dequant(q_w, s_w)");
   m.def("topk_encode", &hipps::topk_encode, "exact top-k |g| (radix select) -> idx asc, val");
-  m.def("topk_workspace_bytes", &hipps::topk_workspace_bytes);
+  m.def("topk_workspace_bytes", &hipps::topk_workspace_bytes, py::arg("n"), py::arg("k") = 0);
   m.def("topk_accumulate", &hipps::topk_accumulate, "acc[idx] += gscale * val");
   m.def("topk_q8_accumulate", &hipps::topk_q8_accumulate, "acc[idx] += gscale * deq(q)");
   m.def("topk_q8_residual", &hipps::topk_q8_residual, "EF: r[idx] += v - deq(q)");

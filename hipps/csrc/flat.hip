@@ -112,12 +112,21 @@ __global__ __launch_bounds__(kBlock) void k_aggregate(SlotPtrs g, int W, float g
 template <typename Tin, typename Tout>
 __global__ __launch_bounds__(kBlock) void k_convert(const Tin* __restrict__ src, Tout* __restrict__ dst, int64_t n,
                                                     float scale) {
+  // four 4-element groups per lane per iteration, all loads issued before the first store
+  constexpr int U = 4;
   const int64_t nv = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
-    const int64_t i = v << 2;
-    float4 d = Vec4<Tin>::load(src, i);
-    if (scale != 1.f) { d.x *= scale; d.y *= scale; d.z *= scale; d.w *= scale; }
-    Vec4<Tout>::store(dst, i, d);
+  for (int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v0 < nv; v0 += U * stride) {
+    float4 d[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (v0 + u * stride < nv) d[u] = Vec4<Tin>::load(src, (v0 + u * stride) << 2);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (v0 + u * stride >= nv) break;
+      float4 e = d[u];
+      if (scale != 1.f) { e.x *= scale; e.y *= scale; e.z *= scale; e.w *= scale; }
+      Vec4<Tout>::store(dst, (v0 + u * stride) << 2, e);
+    }
   }
   if (blockIdx.x == 0) {
     for (int64_t i = (nv << 2) + threadIdx.x; i < n; i += blockDim.x)

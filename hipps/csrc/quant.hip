@@ -27,47 +27,68 @@ __device__ __forceinline__ int8_t q8_round(float x, float inv, bool stochastic, 
   return (int8_t)(int)y;
 }
 
+// One wave per 256-element block; each wave takes kQUnroll consecutive blocks per iteration so
+// every lane has 2 x kQUnroll 16-byte loads in flight (x and residual) before the first use.
+constexpr int kQUnroll = 4;
 __global__ __launch_bounds__(kBlock) void k_q8_encode(const float* __restrict__ x, float* __restrict__ resid,
                                                       int8_t* __restrict__ q, float* __restrict__ scales, int64_t n,
                                                       int stochastic, uint64_t seed) {
   const int lane = threadIdx.x & 63;
   const int64_t nblocks = (n + kQBlock - 1) / kQBlock;
-  const int64_t wstride = (int64_t)gridDim.x * (blockDim.x >> 6);
-  for (int64_t b = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); b < nblocks; b += wstride) {
-    const int64_t i = b * kQBlock + lane * 4;
-    float v[4];
-    if (i + 4 <= n) {
-      float4 t = *reinterpret_cast<const float4*>(x + i);
-      v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-      if (resid) {
-        float4 r = *reinterpret_cast<const float4*>(resid + i);
-        v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+  const int64_t wstride = (int64_t)gridDim.x * (blockDim.x >> 6) * kQUnroll;
+  for (int64_t b0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * kQUnroll; b0 < nblocks;
+       b0 += wstride) {
+    float v[kQUnroll][4];
+#pragma unroll
+    for (int u = 0; u < kQUnroll; ++u) {
+      const int64_t i = (b0 + u) * kQBlock + lane * 4;
+      if (i + 4 <= n) {
+        float4 t = *reinterpret_cast<const float4*>(x + i);
+        v[u][0] = t.x; v[u][1] = t.y; v[u][2] = t.z; v[u][3] = t.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[u][j] = (i + j < n) ? x[i + j] : 0.f;
       }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = (i + j < n) ? x[i + j] + (resid ? resid[i + j] : 0.f) : 0.f;
     }
-    float amax = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
-    amax = wave_max(amax);
-    const float scale = amax / 127.f;
-    const float inv = amax > 0.f ? 127.f / amax : 0.f;
-    int8_t o[4];
+    if (resid) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = q8_round(v[j], inv, stochastic, seed, i + j);
-    if (lane == 0) scales[b] = scale;
-    if (i + 4 <= n) {
-      char4 c = make_char4(o[0], o[1], o[2], o[3]);
-      *reinterpret_cast<char4*>(q + i) = c;
-      if (resid)
-        *reinterpret_cast<float4*>(resid + i) =
-            make_float4(v[0] - o[0] * scale, v[1] - o[1] * scale, v[2] - o[2] * scale, v[3] - o[3] * scale);
-    } else {
+      for (int u = 0; u < kQUnroll; ++u) {
+        const int64_t i = (b0 + u) * kQBlock + lane * 4;
+        if (i + 4 <= n) {
+          float4 r = *reinterpret_cast<const float4*>(resid + i);
+          v[u][0] += r.x; v[u][1] += r.y; v[u][2] += r.z; v[u][3] += r.w;
+        } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (i + j < n) {
-          q[i + j] = o[j];
-          if (resid) resid[i + j] = v[j] - o[j] * scale;
+          for (int j = 0; j < 4; ++j) v[u][j] += (i + j < n) ? resid[i + j] : 0.f;
         }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kQUnroll; ++u) {
+      const int64_t b = b0 + u;
+      if (b >= nblocks) break;
+      const int64_t i = b * kQBlock + lane * 4;
+      float amax = fmaxf(fmaxf(fabsf(v[u][0]), fabsf(v[u][1])), fmaxf(fabsf(v[u][2]), fabsf(v[u][3])));
+      amax = wave_max(amax);
+      const float scale = amax / 127.f;
+      const float inv = amax > 0.f ? 127.f / amax : 0.f;
+      int8_t o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = q8_round(v[u][j], inv, stochastic, seed, i + j);
+      if (lane == 0) scales[b] = scale;
+      if (i + 4 <= n) {
+        *reinterpret_cast<char4*>(q + i) = make_char4(o[0], o[1], o[2], o[3]);
+        if (resid)
+          *reinterpret_cast<float4*>(resid + i) = make_float4(v[u][0] - o[0] * scale, v[u][1] - o[1] * scale,
+                                                              v[u][2] - o[2] * scale, v[u][3] - o[3] * scale);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (i + j < n) {
+            q[i + j] = o[j];
+            if (resid) resid[i + j] = v[u][j] - o[j] * scale;
+          }
+      }
     }
   }
 }
@@ -123,7 +144,7 @@ void q8_encode(at::Tensor x, c10::optional<at::Tensor> resid, at::Tensor q, at::
     rp = resid->data_ptr<float>();
   }
   const int64_t nblocks = (n + kQBlock - 1) / kQBlock;
-  const int grid = grid_for(nblocks * 64);
+  const int grid = grid_for((nblocks + kQUnroll - 1) / kQUnroll * 64);
   hipLaunchKernelGGL(k_q8_encode, grid, kBlock, 0, c10::hip::getCurrentHIPStream(), x.data_ptr<float>(), rp,
                      (int8_t*)q.data_ptr(), scales.data_ptr<float>(), n, (int)stochastic, (uint64_t)seed);
 }

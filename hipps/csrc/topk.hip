@@ -1,236 +1,112 @@
-// hipps — exact top-k magnitude sparsification (radix select + look-back compaction).
+// hipps — exact top-k magnitude sparsification and threshold sparsification.
 //
 // Device replacement for the external codec's encode (ps.py:94) when the codec is top-k.
 // Output is a fixed-size message (k = ceil(ratio*n) known at plan time), so no size round-trip
 // is needed: the reference's per-tensor Iallgather of lengths (mpi_comms.py:150-158, M1) goes
 // away.  Wire: int32 idx[k] + val[k] (f32 or bf16), idx in ascending order.
 //
-// Four full passes over the bucket (round 1 made five plus three single-workgroup histogram
-// walks over all of it), everything else on ~1% of it:
-//   P1  hist of |x| bits 30..20 over the whole bucket (fused with the error-feedback fold
-//       r <- g + r, so later passes read one array)                               [full read]
-//   pick   single workgroup: the bin holding the k-th largest key
-//   P2  filter: keys in that bin -> candidate list (wave-aggregated append)         [full read]
-//   P3/P4  histograms of bits 19..9 and 8..0 over the candidates only, + picks -> exact k-th
-//       key T and how many == T to admit (lowest index first)
-//   P5  compaction in index order: per-4096-element-chunk counts (> T, == T) [full read], one
-//       workgroup scans the ~n/4096 counts, each chunk writes its selected (index, value) pairs
-//       at its prefix [full read].  (A decoupled look-back would save the count pass, but its
-//       chunk tickets are one atomic address and serialised to ~2 ms on a 25 M bucket.)
-// If the threshold bin holds more candidates than the list can take (e.g. mostly-zero
-// gradients) the candidate passes fall back to filtering the whole bucket (flag in device
-// state, no host sync).  Ties are admitted lowest-index-first, so the message is bitwise
-// deterministic and equal to the CPU reference.
+// ONE full pass over the bucket in the steady state (round 1 made five, plus three
+// single-workgroup histogram walks over all of it); everything else works on a short list:
+//   P1  per workgroup a contiguous range of 4096-element chunks ("region"): error-feedback fold
+//       r <- g + r, histogram of key bits 30..20 (key = |x| as bits), and an index-ordered list
+//       of every element with key >= spec_lo, where spec_lo is one radix bin below the
+//       threshold the previous call on this workspace found (the threshold of an error-feedback
+//       gradient moves little from step to step)                      [read g, r; write r]
+//       A chunk whose entries do not fit the region's slot spills them to a shared pool
+//       (one atomic per spilled chunk, on one of 8 pool shards).
+//   pick   one workgroup: the bin B holding the k-th largest key
+//   P2  repair, only when bin B lies below spec_lo (first call, or the gradient shrank): every
+//       region re-reads its range and lists keys >= B's lower edge
+//   P3/P4  histograms of bits 19..9 and 8..0 over the listed keys of bin B + picks -> the exact
+//       k-th key T and how many keys == T to admit (lowest index first)
+//   P5  per region: count the listed keys > T and == T, one workgroup scans the region counts,
+//       each region writes its selected (index, value) pairs at its prefix (list order = index
+//       order), clearing their residuals.
+// If a pool shard runs out (e.g. a mostly-constant bucket), P3-P5 fall back to full passes
+// over the bucket (flag in device state, no host sync).  Ties are admitted lowest-index-first,
+// so a message is bitwise deterministic and equal to the CPU reference.
+//
+// The threshold codec (variable size) is P1 with the fixed bound key > tau (no histogram), then
+// the scan and the write: one full pass.
+//
+// No spin-waits and no single-address atomic hot spots: a decoupled look-back compaction was
+// measured slower (its chunk tickets are one atomic address, serialised to ~2 ms on 25 M).
 #include "common.h"
 
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
 namespace hipps {
 
 constexpr int kHistBins = 2048;
-constexpr int kCompactPer = 16;                     // elements per lane in P5 (4 x float4)
-constexpr int kChunk = kBlock * kCompactPer;        // 4096 elements per look-back chunk
+constexpr int kCompactPer = 16;                 // elements per lane per chunk (4 x float4)
+constexpr int kChunk = kBlock * kCompactPer;    // 4096 elements
+constexpr int kMaxRegions = 1024;               // workgroups of the region passes
+constexpr uint32_t kBinMask = 0x7ff00000u;      // key bits 30..20: the first radix digit
+constexpr uint32_t kSpecBins = 1;               // P1 lists keys down to this many bins below last T
 
-struct SelState {        // lives in a small device workspace
-  uint32_t prefix;       // selected high bits of the k-th largest key
+constexpr uint32_t kNoList = 0x80000000u;       // a bound no key reaches
+constexpr int kHistCopies = 8;
+constexpr int kPoolShards = 8;                  // spill counters, one 128-byte line each
+constexpr int kMaxCpw = 512;                    // chunks per region (n < 2^31)
+
+struct SelState {        // lives at the head of the workspace
+  uint32_t prefix;       // selected high bits of the k-th largest key (threshold codec: T)
   uint32_t mask;         // which bits of prefix are decided
   uint32_t remaining;    // how many elements still to take inside the undecided bucket
-  uint32_t ncand;        // candidates appended by P2
-  uint32_t overflow;     // candidate list too small: later passes scan the whole bucket
-  uint32_t ticket;       // P5 chunk tickets
-  uint32_t cap_cand;
-  uint32_t pad;
-  uint32_t hist[kHistBins];
+  uint32_t capw;         // list slot entries per region
+  uint32_t pool_cap;     // entries per pool shard
+  uint32_t full;         // a pool shard ran out: P3-P5 take full passes over the bucket
+  uint32_t spec_lo;      // P1's list bound
+  uint32_t prev_T;       // final key of the previous call (persists in the workspace)
+  uint32_t pad[24];
+  uint32_t pool_used[kPoolShards * 32];
+  // kHistCopies histograms: workgroup b merges into copy b % kHistCopies, so a bin's global
+  // atomics come from 1/8 of the workgroups (depth ~110 instead of ~900 on a 25 M bucket); the
+  // pick sums the copies
+  uint32_t hist[kHistCopies][kHistBins];
 };
 
 __device__ __forceinline__ uint32_t absbits(float x) { return __float_as_uint(x) & 0x7fffffffu; }
 
-__global__ __launch_bounds__(kBlock) void k_topk_init(SelState* __restrict__ st, uint32_t prefix, uint32_t mask,
-                                                      uint32_t k, uint32_t cap_cand) {
+// topk: did P1's bound cover bin B?  (prefix's top digit is final after the first pick)
+__device__ __forceinline__ bool spec_covers(const SelState* st) { return (st->prefix & kBinMask) >= st->spec_lo; }
+
+// mode: 0 = top-k, 1 = threshold (prefix = T, no ties)
+__global__ __launch_bounds__(kBlock) void k_sel_init(SelState* __restrict__ st, uint32_t prefix, uint32_t mask,
+                                                     uint32_t k, uint32_t capw, uint32_t pool_cap, int topk) {
   if (threadIdx.x == 0) {
-    st->prefix = prefix; st->mask = mask; st->remaining = k; st->ncand = 0; st->overflow = 0; st->ticket = 0;
-    st->cap_cand = cap_cand; st->pad = 0;
-  }
-  for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) st->hist[b] = 0;
-}
-
-// P1 (and the overflow fallback of P3/P4): histogram over elements whose decided bits match
-// prefix.  Four per-wave LDS sub-histograms cut same-address atomic serialisation 4x.
-__global__ __launch_bounds__(kBlock) void k_topk_hist(const float* __restrict__ g, float* __restrict__ resid,
-                                                      int fold_resid, int64_t n, int lo, int nbits,
-                                                      SelState* __restrict__ st, int only_overflow) {
-  __shared__ uint32_t h[4][kHistBins];
-  if (only_overflow && !st->overflow) return;
-  const int nb = 1 << nbits;
-  const int w = threadIdx.x >> 6;
-  for (int b = threadIdx.x; b < 4 * kHistBins; b += blockDim.x) (&h[0][0])[b] = 0;
-  __syncthreads();
-  const uint32_t prefix = st->prefix, mask = st->mask;
-  const float* src = (resid && !fold_resid) ? resid : g;
-  const int64_t nv = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
-    const int64_t i = v << 2;
-    float4 x = *reinterpret_cast<const float4*>(src + i);
-    if (fold_resid) {
-      float4 r = *reinterpret_cast<const float4*>(resid + i);
-      x.x += r.x; x.y += r.y; x.z += r.z; x.w += r.w;
-      *reinterpret_cast<float4*>(resid + i) = x;
-    }
-    const uint32_t k0 = absbits(x.x), k1 = absbits(x.y), k2 = absbits(x.z), k3 = absbits(x.w);
-    if ((k0 & mask) == prefix) atomicAdd(&h[w][(k0 >> lo) & (nb - 1)], 1u);
-    if ((k1 & mask) == prefix) atomicAdd(&h[w][(k1 >> lo) & (nb - 1)], 1u);
-    if ((k2 & mask) == prefix) atomicAdd(&h[w][(k2 >> lo) & (nb - 1)], 1u);
-    if ((k3 & mask) == prefix) atomicAdd(&h[w][(k3 >> lo) & (nb - 1)], 1u);
-  }
-  if (blockIdx.x == 0) {
-    for (int64_t i = (nv << 2) + threadIdx.x; i < n; i += blockDim.x) {
-      float x = src[i];
-      if (fold_resid) { x += resid[i]; resid[i] = x; }
-      const uint32_t k = absbits(x);
-      if ((k & mask) == prefix) atomicAdd(&h[w][(k >> lo) & (nb - 1)], 1u);
-    }
-  }
-  __syncthreads();
-  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
-    const uint32_t c = h[0][b] + h[1][b] + h[2][b] + h[3][b];
-    if (c) atomicAdd(&st->hist[b], c);
-  }
-}
-
-// single workgroup: locate the bucket holding the remaining-th largest key, descend one digit
-__global__ __launch_bounds__(kBlock) void k_topk_pick(int lo, int nbits, SelState* __restrict__ st) {
-  __shared__ uint32_t part[kBlock];
-  __shared__ uint32_t sel_bin, sel_above;
-  const int nb = 1 << nbits;
-  const int per = nb / kBlock;  // 8 or 2 bins per thread
-  const int t = threadIdx.x;
-  // thread t owns bins [nb - (t+1)*per, nb - t*per): t = 0 holds the largest keys
-  uint32_t s = 0;
-  for (int j = 0; j < per; ++j) s += st->hist[nb - (t + 1) * per + j];
-  part[t] = s;
-  __syncthreads();
-  if (t == 0) {
-    const uint32_t need = st->remaining;
-    uint32_t cum = 0;
-    int c = 0;
-    for (; c < kBlock - 1; ++c) {
-      if (cum + part[c] >= need) break;
-      cum += part[c];
-    }
-    int bin = nb - c * per - 1;
-    const int lowest = nb - (c + 1) * per;
-    for (; bin > lowest; --bin) {
-      const uint32_t hb = st->hist[bin];
-      if (cum + hb >= need) break;
-      cum += hb;
-    }
-    sel_bin = (uint32_t)bin;
-    sel_above = cum;
-  }
-  __syncthreads();
-  for (int b = t; b < nb; b += kBlock) st->hist[b] = 0;  // re-arm for the next digit
-  if (t == 0) {
-    st->prefix |= sel_bin << lo;
-    st->mask |= (uint32_t)(nb - 1) << lo;
-    st->remaining -= sel_above;
-  }
-}
-
-// P2: append every element of the selected top-11-bit bin to the candidate list.  Each
-// workgroup scans one contiguous range, collects its candidates in LDS and reserves global space
-// with ONE atomic at the end (a per-wave atomic on one address serialises ~10^5 times on a
-// 25 M-element bucket); an LDS overflow spills straight to global with per-element atomics.
-constexpr int kCandLds = 2048;
-__global__ __launch_bounds__(kBlock) void k_topk_filter(const float* __restrict__ src, int64_t n,
-                                                        SelState* __restrict__ st, uint32_t* __restrict__ ckey,
-                                                        uint32_t* __restrict__ cidx) {
-  __shared__ uint32_t lkey[kCandLds], lidx[kCandLds];
-  __shared__ uint32_t lcount, lbase;
-  const uint32_t prefix = st->prefix, mask = st->mask, cap = st->cap_cand;
-  if (threadIdx.x == 0) lcount = 0;
-  __syncthreads();
-  const int64_t nv = (n + 3) >> 2;
-  const int64_t per = (nv + gridDim.x - 1) / gridDim.x;
-  const int64_t v0 = (int64_t)blockIdx.x * per, v1 = v0 + per < nv ? v0 + per : nv;
-  for (int64_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
-    const int64_t i = v << 2;
-    uint32_t k[4] = {0u, 0u, 0u, 0u};
-    bool m[4] = {false, false, false, false};
-    if (i + 4 <= n) {
-      float4 x = *reinterpret_cast<const float4*>(src + i);
-      k[0] = absbits(x.x); k[1] = absbits(x.y); k[2] = absbits(x.z); k[3] = absbits(x.w);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) m[j] = (k[j] & mask) == prefix;
+    st->prefix = prefix; st->mask = mask; st->remaining = k; st->capw = capw;
+    st->pool_cap = pool_cap; st->full = 0;
+    if (topk) {
+      const uint32_t b = (st->prev_T & 0x7fffffffu) >> 20;
+      // no usable previous threshold: P1 lists nothing, P2 lists from bin B's edge
+      st->spec_lo = b > kSpecBins ? (b - kSpecBins) << 20 : kNoList;
     } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (i + j < n) { k[j] = absbits(src[i + j]); m[j] = (k[j] & mask) == prefix; }
+      st->spec_lo = 0;
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (m[j]) {
-        const uint32_t p = atomicAdd(&lcount, 1u);
-        if (p < kCandLds) {
-          lkey[p] = k[j];
-          lidx[p] = (uint32_t)(i + j);
-        } else {  // spill (rare): straight to the global list
-          const uint32_t g = atomicAdd(&st->ncand, 1u);
-          if (g < cap) { ckey[g] = k[j]; cidx[g] = (uint32_t)(i + j); }
-        }
-      }
   }
-  __syncthreads();
-  const uint32_t cnt = lcount < kCandLds ? lcount : kCandLds;
-  if (threadIdx.x == 0) lbase = cnt ? atomicAdd(&st->ncand, cnt) : 0u;
-  __syncthreads();
-  for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
-    const uint32_t g = lbase + j;
-    if (g < cap) { ckey[g] = lkey[j]; cidx[g] = lidx[j]; }
-  }
+  if (threadIdx.x < kPoolShards) st->pool_used[threadIdx.x * 32] = 0;
+  if (topk)
+    for (int b = threadIdx.x; b < kHistCopies * kHistBins; b += blockDim.x) (&st->hist[0][0])[b] = 0;
 }
 
-// P3/P4: histogram of the candidates; if P2 overflowed the list, of the whole bucket instead
-__global__ __launch_bounds__(kBlock) void k_topk_hist_cand(const uint32_t* __restrict__ ckey,
-                                                           const float* __restrict__ src, int64_t n, int lo, int nbits,
-                                                           SelState* __restrict__ st) {
-  __shared__ uint32_t h[kHistBins];
-  const uint32_t ncand = st->ncand;
-  const bool full = ncand > st->cap_cand;
-  const int nb = 1 << nbits;
-  for (int b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
-  __syncthreads();
-  const uint32_t prefix = st->prefix, mask = st->mask;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  if (!full) {
-    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < ncand; j += stride) {
-      const uint32_t k = ckey[j];
-      if ((k & mask) == prefix) atomicAdd(&h[(k >> lo) & (nb - 1)], 1u);
-    }
-  } else {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-      const uint32_t k = absbits(src[i]);
-      if ((k & mask) == prefix) atomicAdd(&h[(k >> lo) & (nb - 1)], 1u);
-    }
-  }
-  __syncthreads();
-  for (int b = threadIdx.x; b < nb; b += blockDim.x)
-    if (h[b]) atomicAdd(&st->hist[b], h[b]);
+// ---- chunked streaming ------------------------------------------------------------------
+// Lane t holds elements c*4096 + j*1024 + 4t + e (segment j < 4, e < 4): four coalesced 16-byte
+// loads per array in flight per lane.  Index order within a chunk = (segment, wave, lane, e).
+__device__ __forceinline__ int64_t seg_index(int64_t c, int j) {
+  return c * kChunk + (int64_t)j * (kBlock * 4) + threadIdx.x * 4;
 }
 
-// ---- P5: compaction in index order: count -> scan -> write ------------------------------
-// A 4096-element chunk per workgroup (16 elements per lane as 4 coalesced float4 segments).
-// count: per-chunk (> T, == T) totals; scan: one workgroup turns them into exclusive prefixes
-// (6 k chunks for a 25 M bucket); write: each chunk re-reads its elements and places the
-// selected ones at prefix + local rank.  No spin-waits, no single-address atomics.
 __device__ __forceinline__ void chunk_load(const float* __restrict__ src, int64_t n, int64_t c, float (&x)[kCompactPer]) {
 #pragma unroll
   for (int j = 0; j < kCompactPer / 4; ++j) {
-    const int64_t i = c * kChunk + (int64_t)j * (kBlock * 4) + threadIdx.x * 4;
+    const int64_t i = seg_index(c, j);
     if (i + 4 <= n) {
       float4 t = *reinterpret_cast<const float4*>(src + i);
       x[4 * j] = t.x; x[4 * j + 1] = t.y; x[4 * j + 2] = t.z; x[4 * j + 3] = t.w;
@@ -241,91 +117,527 @@ __device__ __forceinline__ void chunk_load(const float* __restrict__ src, int64_
   }
 }
 
-// per segment j: (eq << 16) | gt of this lane's 4 elements (each <= 4)
-__device__ __forceinline__ void chunk_counts(int64_t n, int64_t c, uint32_t T, const float (&x)[kCompactPer],
-                                             uint32_t (&cnt)[kCompactPer / 4]) {
+__device__ __forceinline__ void chunk_store(float* __restrict__ dst, int64_t n, int64_t c, const float (&x)[kCompactPer]) {
 #pragma unroll
   for (int j = 0; j < kCompactPer / 4; ++j) {
-    const int64_t i = c * kChunk + (int64_t)j * (kBlock * 4) + threadIdx.x * 4;
-    uint32_t gt = 0, eq = 0;
+    const int64_t i = seg_index(c, j);
+    if (i + 4 <= n) {
+      *reinterpret_cast<float4*>(dst + i) = make_float4(x[4 * j], x[4 * j + 1], x[4 * j + 2], x[4 * j + 3]);
+    } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const bool in = i + e < n;
-      const uint32_t k = absbits(x[4 * j + e]);
-      gt += in && k > T;
-      eq += in && k == T;
+      for (int e = 0; e < 4; ++e)
+        if (i + e < n) dst[i + e] = x[4 * j + e];
     }
-    cnt[j] = (eq << 16) | gt;
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_topk_count(const float* __restrict__ src, int64_t n,
-                                                       const SelState* __restrict__ st, uint32_t* __restrict__ cgt,
-                                                       uint32_t* __restrict__ ceq, int64_t nchunks) {
-  __shared__ uint32_t red[4];
-  const uint32_t T = st->prefix;
-  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-    float x[kCompactPer];
-    uint32_t cnt[kCompactPer / 4];
-    chunk_load(src, n, c, x);
-    chunk_counts(n, c, T, x, cnt);
-    uint32_t v = cnt[0] + cnt[1] + cnt[2] + cnt[3];  // <= 16 per field: packed sum stays exact
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const uint32_t t = red[0] + red[1] + red[2] + red[3];  // <= 4096 per field
-      cgt[c] = t & 0xffffu;
-      ceq[c] = t >> 16;
-    }
-    __syncthreads();
+// x = src (+ r, and r <- x when fold_r is given): both arrays' loads issued together
+__device__ __forceinline__ void chunk_fold(const float* __restrict__ src, float* __restrict__ fold_r, int64_t n,
+                                           int64_t c, float (&x)[kCompactPer]) {
+  chunk_load(src, n, c, x);
+  if (fold_r) {
+    float y[kCompactPer];
+    chunk_load(fold_r, n, c, y);
+#pragma unroll
+    for (int e = 0; e < kCompactPer; ++e) x[e] += y[e];
+    chunk_store(fold_r, n, c, x);
   }
 }
 
-// exclusive scan of both count arrays in place (one workgroup; nchunks ~ n / 4096)
-__global__ __launch_bounds__(1024) void k_topk_scan(uint32_t* __restrict__ cgt, uint32_t* __restrict__ ceq,
-                                                    int64_t nchunks, int32_t* __restrict__ count_out, uint32_t cap) {
-  __shared__ uint32_t sg[1024], se[1024];
-  __shared__ uint32_t carry_g, carry_e;
-  if (threadIdx.x == 0) { carry_g = 0; carry_e = 0; }
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* red4) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = v;
   __syncthreads();
-  for (int64_t base = 0; base < nchunks; base += 1024) {
-    const int64_t c = base + threadIdx.x;
-    const uint32_t vg = c < nchunks ? cgt[c] : 0, ve = c < nchunks ? ceq[c] : 0;
-    sg[threadIdx.x] = vg; se[threadIdx.x] = ve;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
-      const uint32_t ag = threadIdx.x >= off ? sg[threadIdx.x - off] : 0;
-      const uint32_t ae = threadIdx.x >= off ? se[threadIdx.x - off] : 0;
-      __syncthreads();
-      sg[threadIdx.x] += ag; se[threadIdx.x] += ae;
-      __syncthreads();
-    }
-    if (c < nchunks) { cgt[c] = carry_g + sg[threadIdx.x] - vg; ceq[c] = carry_e + se[threadIdx.x] - ve; }
-    __syncthreads();
-    if (threadIdx.x == 1023) { carry_g += sg[1023]; carry_e += se[1023]; }
-    __syncthreads();
-  }
-  if (count_out && threadIdx.x == 0) count_out[0] = (int32_t)(carry_g < cap ? carry_g : cap);
+  const uint32_t t = red4[0] + red4[1] + red4[2] + red4[3];
+  __syncthreads();
+  return t;
 }
 
-template <typename VT>
-__global__ __launch_bounds__(kBlock) void k_topk_write(const float* __restrict__ src, float* __restrict__ resid,
-                                                       int64_t n, const SelState* __restrict__ st,
-                                                       const uint32_t* __restrict__ pgt, const uint32_t* __restrict__ peq,
-                                                       int64_t nchunks, int32_t* __restrict__ idx, VT* __restrict__ val,
-                                                       uint32_t cap) {
-  __shared__ uint32_t wsum[kCompactPer / 4][4];
+// exclusive workgroup scan; *total gets the workgroup sum
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* red4, uint32_t* total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint32_t T = st->prefix, need_eq = st->remaining;
-  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-    float x[kCompactPer];
-    uint32_t cnt[kCompactPer / 4], incl[kCompactPer / 4];
-    chunk_load(src, n, c, x);
-    chunk_counts(n, c, T, x, cnt);
-    if (pgt[c] >= cap && need_eq == 0) continue;  // nothing of this chunk fits (threshold overflow)
+  uint32_t incl = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t a = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += a;
+  }
+  if (lane == 63) red4[w] = incl;
+  __syncthreads();
+  uint32_t wb = 0, t = 0;
 #pragma unroll
-    for (int j = 0; j < kCompactPer / 4; ++j) {  // index order: segment, wave, lane
+  for (int q = 0; q < 4; ++q) {
+    wb += (q < w) ? red4[q] : 0u;
+    t += red4[q];
+  }
+  __syncthreads();
+  *total = t;
+  return wb + incl - v;
+}
+
+struct Regions {       // region r = chunks [r*cpw, min((r+1)*cpw, nchunks))
+  uint32_t* lval;      // list entries: raw f32 bits
+  uint32_t* lidx;      //               element index
+  uint32_t* coff;      // per chunk: first list entry (slot or pool)
+  uint32_t* ccnt;      //            entries
+  uint32_t* sfill;     // per region: entries in its slot
+  uint32_t* cgt;       //             selected count (> T), then exclusive prefix
+  uint32_t* ceq;       //             == T count, then exclusive prefix
+  int64_t nchunks;
+  int64_t cpw;         // chunks per region
+  int64_t pool_off;    // first pool entry (after nreg * capw slot entries)
+};
+
+constexpr uint32_t kNoBase = 0xffffffffu;
+
+// Index-ordered list of the chunk's elements with key >= bound (entry = raw f32 bits + index).
+// The entries go to the region's slot if they fit, else to a pool shard (one atomic); the chunk's
+// record (first entry, count) goes to coff / ccnt.  Returns the count (workgroup-uniform).
+__device__ __forceinline__ uint32_t collect_chunk(const float (&x)[kCompactPer], int64_t n, int64_t c, uint32_t bound,
+                                                  uint32_t& slot_pos, uint32_t slot_end, SelState* __restrict__ st,
+                                                  const Regions& R, uint32_t (*wsum)[4], uint32_t* sbase) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t m[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t i = seg_index(c, j);
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cnt += (i + e < n) && absbits(x[4 * j + e]) >= bound;
+    m[j] = cnt;
+  }
+  // two segments per 32-bit word: a wave's segment total is <= 256, so 16-bit fields never carry
+  uint32_t ia = m[0] | (m[1] << 16), ib = m[2] | (m[3] << 16);
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t ta = __shfl_up(ia, o, 64), tb = __shfl_up(ib, o, 64);
+    if (lane >= o) { ia += ta; ib += tb; }
+  }
+  if (lane == 63) { wsum[0][w] = ia & 0xffffu; wsum[1][w] = ia >> 16; wsum[2][w] = ib & 0xffffu; wsum[3][w] = ib >> 16; }
+  __syncthreads();
+  const uint32_t incl[4] = {ia & 0xffffu, ia >> 16, ib & 0xffffu, ib >> 16};
+  uint32_t off[4], run = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint32_t wb = 0, tot = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      wb += (q < w) ? wsum[j][q] : 0u;
+      tot += wsum[j][q];
+    }
+    off[j] = run + wb + incl[j] - m[j];
+    run += tot;
+  }
+  uint32_t base;
+  if (slot_pos + run <= slot_end) {  // uniform: every thread computed the same run
+    base = slot_pos;
+    slot_pos += run;
+  } else {
+    if (threadIdx.x == 0) {
+      const int shard = blockIdx.x & (kPoolShards - 1);
+      const uint32_t p = atomicAdd(&st->pool_used[shard * 32], run);
+      uint32_t b = kNoBase;
+      if ((uint64_t)p + run <= st->pool_cap) b = (uint32_t)R.pool_off + shard * st->pool_cap + p;
+      else atomicOr(&st->full, 1u);
+      *sbase = b;
+    }
+    __syncthreads();
+    base = *sbase;
+  }
+  if (base != kNoBase) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!m[j]) continue;
+      uint32_t p = base + off[j];
+      const int64_t i = seg_index(c, j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if ((i + e < n) && absbits(x[4 * j + e]) >= bound) {
+          R.lval[p] = __float_as_uint(x[4 * j + e]);
+          R.lidx[p] = (uint32_t)(i + e);
+          ++p;
+        }
+    }
+  }
+  if (threadIdx.x == 0) { R.coff[c] = base; R.ccnt[c] = run; }
+  __syncthreads();  // wsum / sbase reuse
+  return run;
+}
+
+// P1 / P2: [fold] + [histogram of bits 30..20] + the region's ordered list of keys >= bound.
+// mode 0: top-k P1 (bound = spec_lo); 1: threshold (bound = T + 1, counts -> cgt / ceq);
+// 2: top-k repair (bound = bin B's lower edge; nothing to do when P1's bound covered bin B).
+template <bool HIST>
+__global__ __launch_bounds__(kBlock) void k_collect(const float* __restrict__ src, float* __restrict__ fold_r,
+                                                    int64_t n, SelState* __restrict__ st, Regions R, int mode) {
+  __shared__ uint32_t h[HIST ? 4 : 1][HIST ? kHistBins : 1];
+  __shared__ uint32_t wsum[4][4], sbase;
+  if (mode == 2 && spec_covers(st)) return;  // grid-uniform
+  const int w = threadIdx.x >> 6;
+  if (HIST) {
+    for (int b = threadIdx.x; b < 4 * kHistBins; b += blockDim.x) (&h[0][0])[b] = 0;
+    __syncthreads();
+  }
+  const uint32_t bound = mode == 0 ? st->spec_lo : mode == 1 ? st->prefix + 1u : (st->prefix & kBinMask);
+  const uint32_t capw = st->capw;
+  uint32_t slot_pos = blockIdx.x * capw;
+  const uint32_t slot_end = slot_pos + capw;
+  uint32_t total = 0;
+  const int64_t c0 = blockIdx.x * R.cpw, c1 = std::min<int64_t>(c0 + R.cpw, R.nchunks);
+  for (int64_t c = c0; c < c1; ++c) {
+    float x[kCompactPer];
+    chunk_fold(src, fold_r, n, c, x);
+    if (HIST) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t i = seg_index(c, j);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (i + e < n) atomicAdd(&h[w][absbits(x[4 * j + e]) >> 20], 1u);
+      }
+    }
+    total += collect_chunk(x, n, c, bound, slot_pos, slot_end, st, R, wsum, &sbase);
+  }
+  if (threadIdx.x == 0) {
+    R.sfill[blockIdx.x] = slot_pos - blockIdx.x * capw;
+    if (mode == 1) { R.cgt[blockIdx.x] = total; R.ceq[blockIdx.x] = 0; }
+  }
+  if (HIST) {
+    __syncthreads();
+    for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) {
+      const uint32_t c = h[0][b] + h[1][b] + h[2][b] + h[3][b];
+      if (c) atomicAdd(&st->hist[blockIdx.x % kHistCopies][b], c);
+    }
+  }
+}
+
+// A region's list, chunk by chunk: records in LDS with exclusive prefixes, so list entry j of the
+// region (index order) is found by a binary search over <= cpw chunks.
+struct RegionView {
+  uint32_t* off;  // [kMaxCpw] chunk's first entry
+  uint32_t* pre;  // [kMaxCpw] entries of the region before the chunk
+  int nc;
+  uint32_t total;
+  __device__ __forceinline__ uint32_t entry(uint32_t j) const {
+    int lo = 0, hi = nc - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pre[mid] <= j) lo = mid; else hi = mid - 1;
+    }
+    return off[lo] + (j - pre[lo]);
+  }
+  // entries j, j+1, ..., j+U-1 (those < total): one search, then walk forward
+  template <int U>
+  __device__ __forceinline__ void entries(uint32_t j, uint32_t (&e)[U]) const {
+    int lo = 0, hi = nc - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pre[mid] <= j) lo = mid; else hi = mid - 1;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      while (lo + 1 < nc && pre[lo + 1] <= j + u) ++lo;
+      e[u] = off[lo] + (j + u - pre[lo]);
+    }
+  }
+};
+
+constexpr int kListU = 8;  // list entries per lane per step: 8 independent loads in flight
+
+__device__ __forceinline__ RegionView load_region(const Regions& R, uint32_t* s_off, uint32_t* s_pre, uint32_t* red4) {
+  RegionView v;
+  const int64_t c0 = blockIdx.x * R.cpw;
+  v.nc = (int)(std::min<int64_t>(c0 + R.cpw, R.nchunks) - c0);
+  // two chunks per thread (cpw <= 512)
+  const int t = threadIdx.x;
+  uint32_t a = 0, b = 0;
+  if (2 * t < v.nc) { a = R.ccnt[c0 + 2 * t]; s_off[2 * t] = R.coff[c0 + 2 * t]; }
+  if (2 * t + 1 < v.nc) { b = R.ccnt[c0 + 2 * t + 1]; s_off[2 * t + 1] = R.coff[c0 + 2 * t + 1]; }
+  uint32_t tot;
+  const uint32_t ex = block_excl_scan(a + b, red4, &tot);
+  if (2 * t < v.nc) s_pre[2 * t] = ex;
+  if (2 * t + 1 < v.nc) s_pre[2 * t + 1] = ex + a;
+  __syncthreads();
+  v.off = s_off;
+  v.pre = s_pre;
+  v.total = tot;
+  return v;
+}
+
+// The list storage walked flat, for passes that need no index order: every region's slot
+// (filled part), then every pool shard's used part.  v = virtual position; the walk is coalesced.
+struct FlatList {
+  uint32_t slot_total, capw, pool_cap, size;
+  uint32_t pre[kPoolShards + 1];  // virtual start of each pool shard
+  int64_t pool_off;
+  __device__ __forceinline__ void init(const SelState* st, const Regions& R, int nreg) {
+    capw = st->capw;
+    pool_cap = st->pool_cap;
+    slot_total = (uint32_t)nreg * capw;
+    pool_off = R.pool_off;
+    uint32_t v = slot_total;
+#pragma unroll
+    for (int s = 0; s < kPoolShards; ++s) {
+      pre[s] = v;
+      const uint32_t u = st->pool_used[s * 32];
+      v += u < pool_cap ? u : pool_cap;
+    }
+    pre[kPoolShards] = v;
+    size = v;
+  }
+  // storage position of virtual position v, or kNoBase for an unfilled slot position
+  __device__ __forceinline__ uint32_t at(uint32_t v, const Regions& R) const {
+    if (v < slot_total) {
+      const uint32_t b = v / capw;
+      return v - b * capw < R.sfill[b] ? v : kNoBase;
+    }
+    int s = 0;
+#pragma unroll
+    for (int q = 1; q < kPoolShards; ++q) s += v >= pre[q];
+    return (uint32_t)pool_off + s * pool_cap + (v - pre[s]);
+  }
+};
+
+// One workgroup: find the bin holding the remaining-th largest key and descend one digit.
+// Thread t owns bins [nb - (t+1)*per, nb - t*per) (t = 0 the largest keys); a wave-shuffle scan
+// of the per-thread sums finds the owning thread in log steps.  The final digit records T for the
+// next call's speculative bound.
+__global__ __launch_bounds__(kBlock) void k_topk_pick(int lo, int nbits, SelState* __restrict__ st, int final_digit) {
+  __shared__ uint32_t wtot[4];
+  const int nb = 1 << nbits;
+  const int per = nb / kBlock;  // 8 or 2
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t hv[kHistBins / kBlock];
+  uint32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < kHistBins / kBlock; ++j) {
+    uint32_t c = 0;
+    if (j < per) {
+#pragma unroll
+      for (int q = 0; q < kHistCopies; ++q) c += st->hist[q][nb - t * per - 1 - j];  // descending
+    }
+    hv[j] = c;
+    s += c;
+  }
+  const uint32_t need = st->remaining;
+  uint32_t incl = s;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t a = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += a;
+  }
+  if (lane == 63) wtot[w] = incl;
+  __syncthreads();  // every hist read and the remaining read happened before this barrier
+#pragma unroll
+  for (int q = 0; q < 4; ++q) incl += (q < w) ? wtot[q] : 0u;
+  const uint32_t excl = incl - s;
+  for (int b = t; b < nb; b += kBlock)  // re-arm for the next digit
+#pragma unroll
+    for (int q = 0; q < kHistCopies; ++q) st->hist[q][b] = 0;
+  if ((excl < need && need <= incl) || (t == kBlock - 1 && incl < need)) {
+    uint32_t cum = excl;
+    int bin = nb - t * per - 1;
+#pragma unroll
+    for (int j = 0; j < kHistBins / kBlock; ++j) {
+      if (j >= per - 1) break;
+      if (cum + hv[j] >= need) break;
+      cum += hv[j];
+      --bin;
+    }
+    const uint32_t prefix = st->prefix | ((uint32_t)bin << lo);
+    st->prefix = prefix;
+    st->mask |= (uint32_t)(nb - 1) << lo;
+    st->remaining = need - cum;
+    if (final_digit) st->prev_T = prefix;
+    if (lo == 20 && (prefix & kBinMask) < st->spec_lo) {  // P2 will re-list everything: fresh pool
+      st->full = 0;
+      for (int s = 0; s < kPoolShards; ++s) st->pool_used[s * 32] = 0;
+    }
+  }
+}
+
+// P3/P4: histogram of the listed keys of the selected bin; full pass over the bucket if the pool ran out
+__global__ __launch_bounds__(kBlock) void k_hist_list(const float* __restrict__ src, int64_t n, int lo, int nbits,
+                                                      SelState* __restrict__ st, Regions R, int nreg) {
+  __shared__ uint32_t h[kHistBins];
+  const int nb = 1 << nbits;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  const uint32_t prefix = st->prefix, mask = st->mask;
+  if (!st->full) {
+    FlatList L;
+    L.init(st, R, nreg);
+    const uint32_t step = gridDim.x * blockDim.x * kListU;
+    for (uint32_t v0 = blockIdx.x * blockDim.x * kListU + threadIdx.x; v0 < L.size; v0 += step) {
+      uint32_t k[kListU];
+#pragma unroll
+      for (int u = 0; u < kListU; ++u) {
+        const uint32_t v = v0 + u * blockDim.x;
+        const uint32_t p = v < L.size ? L.at(v, R) : kNoBase;
+        k[u] = p != kNoBase ? (R.lval[p] & 0x7fffffffu) : 0xffffffffu;
+      }
+#pragma unroll
+      for (int u = 0; u < kListU; ++u)
+        if (k[u] != 0xffffffffu && (k[u] & mask) == prefix) atomicAdd(&h[(k[u] >> lo) & (nb - 1)], 1u);
+    }
+  } else {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+      const uint32_t k = absbits(src[i]);
+      if ((k & mask) == prefix) atomicAdd(&h[(k >> lo) & (nb - 1)], 1u);
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < nb; b += blockDim.x)
+    if (h[b]) atomicAdd(&st->hist[blockIdx.x % kHistCopies][b], h[b]);
+}
+
+// P5a (top-k): per region, the counts of keys > T and == T, from its list (the full-mode twin
+// below re-reads the region's chunks instead)
+__global__ __launch_bounds__(kBlock) void k_count_list(const SelState* __restrict__ st, Regions R) {
+  __shared__ uint32_t red[4], s_off[kMaxCpw], s_pre[kMaxCpw];
+  if (st->full) return;
+  const uint32_t T = st->prefix;
+  uint32_t gt = 0, eq = 0;
+  const RegionView v = load_region(R, s_off, s_pre, red);
+  for (uint32_t j0 = threadIdx.x * kListU; j0 < v.total; j0 += blockDim.x * kListU) {
+    uint32_t e[kListU], k[kListU];
+    v.entries<kListU>(j0, e);
+#pragma unroll
+    for (int u = 0; u < kListU; ++u) k[u] = j0 + u < v.total ? (R.lval[e[u]] & 0x7fffffffu) : 0u;
+#pragma unroll
+    for (int u = 0; u < kListU; ++u) {
+      gt += k[u] > T;
+      eq += j0 + u < v.total && k[u] == T;
+    }
+  }
+  gt = block_sum(gt, red);
+  eq = block_sum(eq, red);
+  if (threadIdx.x == 0) { R.cgt[blockIdx.x] = gt; R.ceq[blockIdx.x] = eq; }
+}
+
+__global__ __launch_bounds__(kBlock) void k_count_full(const float* __restrict__ src, int64_t n,
+                                                       const SelState* __restrict__ st, Regions R) {
+  __shared__ uint32_t red[4];
+  if (!st->full) return;
+  const uint32_t T = st->prefix;
+  uint32_t gt = 0, eq = 0;
+  const int64_t c0 = blockIdx.x * R.cpw, c1 = std::min<int64_t>(c0 + R.cpw, R.nchunks);
+  for (int64_t c = c0; c < c1; ++c) {
+    float x[kCompactPer];
+    chunk_load(src, n, c, x);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t i = seg_index(c, j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t k = absbits(x[4 * j + e]);
+        gt += (i + e < n) && k > T;
+        eq += (i + e < n) && k == T;
+      }
+    }
+  }
+  gt = block_sum(gt, red);
+  eq = block_sum(eq, red);
+  if (threadIdx.x == 0) { R.cgt[blockIdx.x] = gt; R.ceq[blockIdx.x] = eq; }
+}
+
+// P5b: exclusive scan of the (<= 1024) region counts, one 1024-thread workgroup
+__global__ __launch_bounds__(1024) void k_scan_regions(uint32_t* __restrict__ cgt, uint32_t* __restrict__ ceq, int nreg,
+                                                       int32_t* __restrict__ count_out, uint32_t cap) {
+  __shared__ uint32_t wg[16], we[16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t sg = t < nreg ? cgt[t] : 0u, se = t < nreg ? ceq[t] : 0u;
+  uint32_t ig = sg, ie = se;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t a = __shfl_up(ig, o, 64), b = __shfl_up(ie, o, 64);
+    if (lane >= o) { ig += a; ie += b; }
+  }
+  if (lane == 63) { wg[w] = ig; we[w] = ie; }
+  __syncthreads();
+  uint32_t og = 0, oe = 0, tg = 0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    og += (q < w) ? wg[q] : 0u;
+    oe += (q < w) ? we[q] : 0u;
+    tg += wg[q];
+  }
+  if (t < nreg) { cgt[t] = og + ig - sg; ceq[t] = oe + ie - se; }
+  if (count_out && t == 0) count_out[0] = (int32_t)(tg < cap ? tg : cap);
+}
+
+// place one element: rank-th > T / eq-th == T of the bucket in index order
+template <typename VT>
+__device__ __forceinline__ void place(uint32_t bits, uint32_t i, bool isgt, bool iseq, uint32_t g, uint32_t e,
+                                      uint32_t need_eq, uint32_t cap, int32_t* __restrict__ idx, VT* __restrict__ val,
+                                      float* __restrict__ resid) {
+  if (!(isgt || (iseq && e < need_eq))) return;
+  const uint32_t pos = g + (e < need_eq ? e : need_eq);
+  if (pos >= cap) return;
+  const float x = __uint_as_float(bits);
+  idx[pos] = (int32_t)i;
+  Vec4<VT>::store1(val, pos, x);
+  if (resid) resid[i] = x - Vec4<VT>::load1(val, pos);  // error feedback keeps the rounding residue
+}
+
+// P5c: each region writes its selected pairs at its prefix, in index order
+template <typename VT>
+__global__ __launch_bounds__(kBlock) void k_write_regions(const float* __restrict__ src, float* __restrict__ resid,
+                                                          int64_t n, const SelState* __restrict__ st, Regions R,
+                                                          int32_t* __restrict__ idx, VT* __restrict__ val,
+                                                          uint32_t cap) {
+  __shared__ uint32_t red[4], wsum[4][4], s_off[kMaxCpw], s_pre[kMaxCpw];
+  const uint32_t T = st->prefix, need_eq = st->remaining;
+  uint32_t bg = R.cgt[blockIdx.x], be = R.ceq[blockIdx.x];
+  if (bg >= cap) return;  // every position of this region is past the message
+  if (!st->full) {
+    const RegionView v = load_region(R, s_off, s_pre, red);
+    const uint32_t m = v.total;
+    // each lane takes kListU consecutive entries (index order), one workgroup scan per step
+    for (uint32_t j0 = 0; j0 < m; j0 += blockDim.x * kListU) {
+      const uint32_t j = j0 + threadIdx.x * kListU;
+      uint32_t e[kListU], bits[kListU];
+      v.entries<kListU>(j, e);
+#pragma unroll
+      for (int u = 0; u < kListU; ++u) bits[u] = j + u < m ? R.lval[e[u]] : 0u;
+      uint32_t cnt = 0;  // (eq << 16) | gt of this lane's entries
+#pragma unroll
+      for (int u = 0; u < kListU; ++u) {
+        const uint32_t k = bits[u] & 0x7fffffffu;
+        cnt += (j + u < m) ? ((uint32_t)(k > T) | ((uint32_t)(k == T) << 16)) : 0u;
+      }
+      uint32_t tot;
+      const uint32_t ex = block_excl_scan(cnt, red, &tot);  // <= 2048 per field per step
+      uint32_t g = bg + (ex & 0xffffu), q = be + (ex >> 16);
+#pragma unroll
+      for (int u = 0; u < kListU; ++u) {
+        if (j + u >= m) break;
+        const uint32_t k = bits[u] & 0x7fffffffu;
+        const bool isgt = k > T, iseq = k == T;
+        if (isgt || iseq) place<VT>(bits[u], R.lidx[e[u]], isgt, iseq, g, q, need_eq, cap, idx, val, resid);
+        g += isgt;
+        q += iseq;
+      }
+      bg += tot & 0xffffu;
+      be += tot >> 16;
+    }
+    return;
+  }
+  // full mode: the region's chunks in order, ordered positions within each chunk
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t c0 = blockIdx.x * R.cpw, c1 = std::min<int64_t>(c0 + R.cpw, R.nchunks);
+  for (int64_t c = c0; c < c1; ++c) {
+    float x[kCompactPer];
+    chunk_load(src, n, c, x);
+    uint32_t cnt[4], incl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t i = seg_index(c, j);
+      uint32_t gt = 0, eq = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t k = absbits(x[4 * j + e]);
+        gt += (i + e < n) && k > T;
+        eq += (i + e < n) && k == T;
+      }
+      cnt[j] = (eq << 16) | gt;
       uint32_t v = cnt[j];
       for (int o = 1; o < 64; o <<= 1) {
         const uint32_t a = __shfl_up(v, o, 64);
@@ -337,30 +649,29 @@ __global__ __launch_bounds__(kBlock) void k_topk_write(const float* __restrict__
     __syncthreads();
     uint32_t run = 0;
 #pragma unroll
-    for (int j = 0; j < kCompactPer / 4; ++j) {
-      uint32_t wb = 0;
+    for (int j = 0; j < 4; ++j) {
+      uint32_t wb = 0, tot = 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) wb += (q < w) ? wsum[j][q] : 0u;
+      for (int q = 0; q < 4; ++q) {
+        wb += (q < w) ? wsum[j][q] : 0u;
+        tot += wsum[j][q];
+      }
       const uint32_t off = run + wb + incl[j] - cnt[j];
+      run += tot;
+      const int64_t i = seg_index(c, j);
+      uint32_t g = bg + (off & 0xffffu), e = be + (off >> 16);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) run += wsum[j][q];
-      const int64_t i = c * kChunk + (int64_t)j * (kBlock * 4) + threadIdx.x * 4;
-      uint32_t bg = pgt[c] + (off & 0xffffu), be = peq[c] + (off >> 16);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (i + e >= n) break;
-        const uint32_t k = absbits(x[4 * j + e]);
+      for (int q = 0; q < 4; ++q) {
+        if (i + q >= n) break;
+        const uint32_t k = absbits(x[4 * j + q]);
         const bool isgt = k > T, iseq = k == T;
-        const uint32_t pos = bg + (be < need_eq ? be : need_eq);
-        if ((isgt || (iseq && be < need_eq)) && pos < cap) {
-          idx[pos] = (int32_t)(i + e);
-          Vec4<VT>::store1(val, pos, x[4 * j + e]);
-          if (resid) resid[i + e] = x[4 * j + e] - Vec4<VT>::load1(val, pos);
-        }
-        bg += isgt;
-        be += iseq;
+        place<VT>(__float_as_uint(x[4 * j + q]), (uint32_t)(i + q), isgt, iseq, g, e, need_eq, cap, idx, val, resid);
+        g += isgt;
+        e += iseq;
       }
     }
+    bg += run & 0xffffu;
+    be += run >> 16;
     __syncthreads();  // wsum reuse
   }
 }
@@ -397,49 +708,68 @@ __global__ __launch_bounds__(kBlock) void k_topk_q8_resid(const int32_t* __restr
 // ------------------------------------------------------------------------------------------
 namespace {
 
-struct TopkWs {
-  SelState* st;
-  uint32_t* cgt;  // per-chunk counts, then exclusive prefixes
-  uint32_t* ceq;
-  uint32_t* ckey;
-  uint32_t* cidx;
-  int64_t nchunks;
-  int64_t cap;
+struct Geo {
+  int64_t nchunks, cpw, nreg, capw, pool;
 };
 
-int64_t cand_cap(int64_t n) { return std::max<int64_t>(4096, n / 16); }
-
-int64_t ws_bytes_for(int64_t n) {
-  const int64_t nchunks = (n + kChunk - 1) / kChunk;
-  return (int64_t)sizeof(SelState) + 8 * nchunks + 8 * cand_cap(n) + 64;
+// regions of cpw chunks, <= kMaxRegions of them; a region's list slot holds 1/16 of its elements
+// (or 2k / nreg if larger); the pool (8 shards) takes 1/8 of the bucket (or 3k)
+Geo geo_for(int64_t n, int64_t k) {
+  Geo g;
+  g.nchunks = std::max<int64_t>(1, (n + kChunk - 1) / kChunk);
+  g.cpw = (g.nchunks + kMaxRegions - 1) / kMaxRegions;
+  g.nreg = (g.nchunks + g.cpw - 1) / g.cpw;
+  const int64_t per = g.cpw * kChunk;
+  int64_t capw = std::max<int64_t>(per / 16, (2 * k + g.nreg - 1) / g.nreg);
+  capw = std::min<int64_t>(per, (capw + 63) / 64 * 64);
+  g.capw = capw;
+  g.pool = (std::max<int64_t>(n / 8, 3 * k) / kPoolShards + 64) / 64 * 64 * kPoolShards;
+  return g;
 }
 
-TopkWs carve(at::Tensor& workspace, int64_t n) {
-  const int64_t need = ws_bytes_for(n);
+int64_t ws_bytes_for(int64_t n, int64_t k) {
+  const Geo g = geo_for(n, k);
+  const int64_t entries = g.nreg * g.capw + g.pool;
+  return (int64_t)sizeof(SelState) + 4 * (2 * g.nchunks + 3 * g.nreg) + 8 * entries + 64;
+}
+
+struct Ws {
+  SelState* st;
+  Regions R;
+  Geo g;
+};
+
+Ws carve(at::Tensor& workspace, int64_t n, int64_t k) {
+  const int64_t need = ws_bytes_for(n, k);
   TORCH_CHECK(workspace.is_cuda() && workspace.numel() * workspace.element_size() >= need,
-              "workspace too small: need ", need, " bytes (topk_workspace_bytes)");
-  static_assert(sizeof(SelState) % 16 == 0, "SelState keeps the count arrays aligned");
+              "workspace too small: need ", need, " bytes (topk_workspace_bytes(n, k))");
+  static_assert(sizeof(SelState) % 16 == 0, "SelState keeps the arrays aligned");
   char* ws = (char*)workspace.data_ptr();
   TORCH_CHECK(reinterpret_cast<uintptr_t>(ws) % 16 == 0, "workspace must be 16-byte aligned");
-  TopkWs w;
+  Ws w;
+  w.g = geo_for(n, k);
   w.st = reinterpret_cast<SelState*>(ws);
-  w.nchunks = (n + kChunk - 1) / kChunk;
-  w.cap = cand_cap(n);
-  w.cgt = reinterpret_cast<uint32_t*>(ws + sizeof(SelState));
-  w.ceq = w.cgt + w.nchunks;
-  w.ckey = w.ceq + w.nchunks;
-  w.cidx = w.ckey + w.cap;
+  uint32_t* a = reinterpret_cast<uint32_t*>(ws + sizeof(SelState));
+  const int64_t entries = w.g.nreg * w.g.capw + w.g.pool;
+  TORCH_CHECK(entries < ((int64_t)1 << 32), "top-k list too large");
+  w.R.coff = a;
+  w.R.ccnt = a + w.g.nchunks;
+  w.R.sfill = a + 2 * w.g.nchunks;
+  w.R.cgt = w.R.sfill + w.g.nreg;
+  w.R.ceq = w.R.cgt + w.g.nreg;
+  w.R.lval = w.R.ceq + w.g.nreg;
+  w.R.lidx = w.R.lval + entries;
+  w.R.nchunks = w.g.nchunks;
+  w.R.cpw = w.g.cpw;
+  w.R.pool_off = w.g.nreg * w.g.capw;
   return w;
 }
 
 template <typename VT>
-void launch_compact(hipStream_t stream, const float* src, float* rp, int64_t n, const TopkWs& w, int32_t* idx, VT* val,
-                    uint32_t cap, int32_t* count_out) {
-  const int grid = (int)std::min<int64_t>(w.nchunks, kMaxGrid);
-  hipLaunchKernelGGL(k_topk_count, grid, kBlock, 0, stream, src, n, w.st, w.cgt, w.ceq, w.nchunks);
-  hipLaunchKernelGGL(k_topk_scan, 1, 1024, 0, stream, w.cgt, w.ceq, w.nchunks, count_out, cap);
-  hipLaunchKernelGGL(k_topk_write<VT>, grid, kBlock, 0, stream, src, rp, n, w.st, w.cgt, w.ceq, w.nchunks, idx, val,
-                     cap);
+void launch_scan_write(hipStream_t stream, const float* src, float* rp, int64_t n, const Ws& w, int32_t* idx, VT* val,
+                       uint32_t cap, int32_t* count_out) {
+  hipLaunchKernelGGL(k_scan_regions, 1, 1024, 0, stream, w.R.cgt, w.R.ceq, (int)w.g.nreg, count_out, cap);
+  hipLaunchKernelGGL(k_write_regions<VT>, (int)w.g.nreg, kBlock, 0, stream, src, rp, n, w.st, w.R, idx, val, cap);
 }
 
 }  // namespace
@@ -454,7 +784,7 @@ void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::T
   TORCH_CHECK(val.numel() == k && (val.scalar_type() == at::kFloat || val.scalar_type() == at::kBFloat16),
               "val must be f32/bf16[k]");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0, "g must be 16-byte aligned");
-  TopkWs w = carve(workspace, n);
+  Ws w = carve(workspace, n, k);
   float* rp = nullptr;
   if (resid.has_value() && resid->defined()) {
     TORCH_CHECK(resid->numel() == n && resid->scalar_type() == at::kFloat && resid->is_contiguous(), "residual");
@@ -462,42 +792,33 @@ void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::T
     rp = resid->data_ptr<float>();
   }
   auto stream = c10::hip::getCurrentHIPStream();
-  hipLaunchKernelGGL(k_topk_init, 1, kBlock, 0, stream, w.st, 0u, 0u, (uint32_t)k, (uint32_t)w.cap);
-  const int grid = grid_for(n >> 2);
-  // histogram grids stay <= 1024 workgroups: every workgroup merges its bins with global atomics
-  const int hgrid = std::min(grid, 1024);
-  // P1: fold + top-11-bit histogram over the whole bucket
-  hipLaunchKernelGGL(k_topk_hist, hgrid, kBlock, 0, stream, g.data_ptr<float>(), rp, (int)(rp != nullptr), n, 20, 11,
-                     w.st, 0);
-  hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 20, 11, w.st);
+  const int nreg = (int)w.g.nreg;
+  TORCH_CHECK(w.g.cpw <= kMaxCpw, "bucket too large for the region geometry");
+  hipLaunchKernelGGL(k_sel_init, 1, kBlock, 0, stream, w.st, 0u, 0u, (uint32_t)k, (uint32_t)w.g.capw,
+                     (uint32_t)(w.g.pool / kPoolShards), 1);
+  // P1: fold + top-digit histogram + speculative ordered list (the only full pass)
+  hipLaunchKernelGGL(k_collect<true>, nreg, kBlock, 0, stream, g.data_ptr<float>(), rp, n, w.st, w.R, 0);
+  hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 20, 11, w.st, 0);
   const float* src = rp ? rp : g.data_ptr<float>();
-  // P2: candidates of the selected bin (one contiguous range per workgroup)
-  hipLaunchKernelGGL(k_topk_filter, grid, kBlock, 0, stream, src, n, w.st, w.ckey, w.cidx);
-  // P3/P4 on the candidates
-  const int cgrid = (int)std::max<int64_t>(1, std::min<int64_t>(1024, w.cap / 1024));
-  hipLaunchKernelGGL(k_topk_hist_cand, cgrid, kBlock, 0, stream, w.ckey, src, n, 9, 11, w.st);
-  hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 9, 11, w.st);
-  hipLaunchKernelGGL(k_topk_hist_cand, cgrid, kBlock, 0, stream, w.ckey, src, n, 0, 9, w.st);
-  hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 0, 9, w.st);
-  // P5: look-back compaction in index order
+  // P2: only if P1's bound missed bin B, every region re-lists its range (returns at once otherwise)
+  hipLaunchKernelGGL(k_collect<false>, nreg, kBlock, 0, stream, src, (float*)nullptr, n, w.st, w.R, 2);
+  // P3/P4 on the listed keys of bin B
+  hipLaunchKernelGGL(k_hist_list, nreg, kBlock, 0, stream, src, n, 9, 11, w.st, w.R, nreg);
+  hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 9, 11, w.st, 0);
+  hipLaunchKernelGGL(k_hist_list, nreg, kBlock, 0, stream, src, n, 0, 9, w.st, w.R, nreg);
+  hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 0, 9, w.st, 1);
+  // P5: region counts, scan, ordered write
+  hipLaunchKernelGGL(k_count_list, nreg, kBlock, 0, stream, w.st, w.R);
+  hipLaunchKernelGGL(k_count_full, nreg, kBlock, 0, stream, src, n, w.st, w.R);
   if (val.scalar_type() == at::kFloat)
-    launch_compact<float>(stream, src, rp, n, w, idx.data_ptr<int32_t>(), val.data_ptr<float>(), (uint32_t)k, nullptr);
-  else
-    launch_compact<uint16_t>(stream, src, rp, n, w, idx.data_ptr<int32_t>(), (uint16_t*)val.data_ptr(), (uint32_t)k,
+    launch_scan_write<float>(stream, src, rp, n, w, idx.data_ptr<int32_t>(), val.data_ptr<float>(), (uint32_t)k,
                              nullptr);
+  else
+    launch_scan_write<uint16_t>(stream, src, rp, n, w, idx.data_ptr<int32_t>(), (uint16_t*)val.data_ptr(),
+                                (uint32_t)k, nullptr);
 }
 
 // ---- threshold sparsification (variable-size message, count in a device header) -----------
-__global__ __launch_bounds__(kBlock) void k_fold(const float* __restrict__ g, float* __restrict__ r, int64_t n) {
-  const int64_t nv = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
-    float4 a = *reinterpret_cast<const float4*>(g + 4 * v), b = *reinterpret_cast<const float4*>(r + 4 * v);
-    *reinterpret_cast<float4*>(r + 4 * v) = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
-  }
-  if (blockIdx.x == 0)
-    for (int64_t i = (nv << 2) + threadIdx.x; i < n; i += blockDim.x) r[i] += g[i];
-}
-
 template <typename VT>
 __global__ __launch_bounds__(kBlock) void k_scatter_acc_count(const int32_t* __restrict__ idx,
                                                               const VT* __restrict__ val,
@@ -515,29 +836,34 @@ void thresh_encode(at::Tensor g, c10::optional<at::Tensor> resid, double tau, at
                    at::Tensor val, at::Tensor workspace) {
   TORCH_CHECK(g.is_cuda() && g.is_contiguous() && g.scalar_type() == at::kFloat, "g: contiguous f32 device tensor");
   const int64_t n = g.numel(), cap = idx.numel();
+  TORCH_CHECK(n >= 1, "empty bucket");
   TORCH_CHECK(val.numel() == cap && count.scalar_type() == at::kInt && count.numel() >= 1, "count/idx/val");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0, "g must be 16-byte aligned");
   TORCH_CHECK(n < (int64_t)1 << 31, "bucket must have < 2^31 elements");
-  TopkWs w = carve(workspace, n);
+  Ws w = carve(workspace, n, cap);
   auto stream = c10::hip::getCurrentHIPStream();
-  float* rp = nullptr;
-  if (resid.has_value() && resid->defined()) {
-    TORCH_CHECK(resid->numel() == n && resid->scalar_type() == at::kFloat, "residual");
-    rp = resid->data_ptr<float>();
-    hipLaunchKernelGGL(k_fold, grid_for(n >> 2), kBlock, 0, stream, g.data_ptr<float>(), rp, n);
-  }
   float t = (float)std::fabs(tau);
   uint32_t tbits;
   std::memcpy(&tbits, &t, 4);
-  // T = tau exactly, no ties admitted: every |x| > tau, in index order (one look-back pass)
-  hipLaunchKernelGGL(k_topk_init, 1, kBlock, 0, stream, w.st, tbits, 0xffffffffu, 0u, (uint32_t)w.cap);
+  float* rp = nullptr;
+  if (resid.has_value() && resid->defined()) {
+    TORCH_CHECK(resid->numel() == n && resid->scalar_type() == at::kFloat && resid->is_contiguous(), "residual");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(resid->data_ptr()) % 16 == 0, "residual must be 16-byte aligned");
+    rp = resid->data_ptr<float>();
+  }
+  const int nreg = (int)w.g.nreg;
+  // T = tau exactly, no ties admitted: every |x| > tau, in index order
+  TORCH_CHECK(w.g.cpw <= kMaxCpw, "bucket too large for the region geometry");
+  hipLaunchKernelGGL(k_sel_init, 1, kBlock, 0, stream, w.st, tbits, 0xffffffffu, 0u, (uint32_t)w.g.capw,
+                     (uint32_t)(w.g.pool / kPoolShards), 0);
+  hipLaunchKernelGGL(k_collect<false>, nreg, kBlock, 0, stream, g.data_ptr<float>(), rp, n, w.st, w.R, 1);
   const float* src = rp ? rp : g.data_ptr<float>();
   if (val.scalar_type() == at::kFloat)
-    launch_compact<float>(stream, src, rp, n, w, idx.data_ptr<int32_t>(), val.data_ptr<float>(), (uint32_t)cap,
-                          count.data_ptr<int32_t>());
-  else
-    launch_compact<uint16_t>(stream, src, rp, n, w, idx.data_ptr<int32_t>(), (uint16_t*)val.data_ptr(), (uint32_t)cap,
+    launch_scan_write<float>(stream, src, rp, n, w, idx.data_ptr<int32_t>(), val.data_ptr<float>(), (uint32_t)cap,
                              count.data_ptr<int32_t>());
+  else
+    launch_scan_write<uint16_t>(stream, src, rp, n, w, idx.data_ptr<int32_t>(), (uint16_t*)val.data_ptr(),
+                                (uint32_t)cap, count.data_ptr<int32_t>());
 }
 
 // Copy a threshold message [count header | idx[cap] | val[cap]] moving only what the count says:
@@ -588,7 +914,7 @@ void thresh_accumulate(at::Tensor count, at::Tensor idx, at::Tensor val, at::Ten
                        (float)gscale);
 }
 
-int64_t topk_workspace_bytes(int64_t n) { return ws_bytes_for(n); }
+int64_t topk_workspace_bytes(int64_t n, int64_t k) { return ws_bytes_for(n, k); }
 
 void topk_accumulate(at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale) {
   TORCH_CHECK(acc.is_cuda() && acc.scalar_type() == at::kFloat, "acc: f32 device tensor");

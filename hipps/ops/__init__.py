@@ -77,14 +77,17 @@ def q8_aggregate(qs, ss, acc, gscale: float = 1.0, accumulate: bool = False):
     return ref.q8_aggregate(qs, ss, acc, gscale, accumulate)
 
 
-def topk_workspace_bytes(n: int) -> int:
-    return native().topk_workspace_bytes(int(n)) if native_available() else ref.topk_workspace_bytes(n)
+def topk_workspace_bytes(n: int, k: int = 0) -> int:
+    """Bytes of the device workspace of a top-k (k) / threshold (k = capacity) encoder over n
+    elements.  Allocate it zeroed and keep it per bucket: it carries the previous call's threshold,
+    which bounds the next call's candidate list."""
+    return native().topk_workspace_bytes(int(n), int(k)) if native_available() else ref.topk_workspace_bytes(n, k)
 
 
 def topk_encode(g, resid, k: int, idx, val, workspace=None):
     if _dev(g):
         if workspace is None:
-            workspace = torch.empty(native().topk_workspace_bytes(g.numel()), dtype=torch.uint8, device=g.device)
+            workspace = torch.zeros(native().topk_workspace_bytes(g.numel(), int(k)), dtype=torch.uint8, device=g.device)
         return native().topk_encode(g, resid, int(k), idx, val, workspace)
     return ref.topk_encode(g, resid, k, idx, val)
 
@@ -111,7 +114,8 @@ def thresh_encode(g, resid, tau: float, count, idx, val, workspace=None):
     """Variable-size sparsification: |x| > tau, capacity idx.numel(), true count in count[0]."""
     if _dev(g):
         if workspace is None:
-            workspace = torch.empty(native().topk_workspace_bytes(g.numel()), dtype=torch.uint8, device=g.device)
+            workspace = torch.zeros(native().topk_workspace_bytes(g.numel(), idx.numel()), dtype=torch.uint8,
+                                    device=g.device)
         return native().thresh_encode(g, resid, float(tau), count, idx, val, workspace)
     return ref.thresh_encode(g, resid, tau, count, idx, val)
 

@@ -219,7 +219,7 @@ def topk_q8_residual(idx, v, q, scales, resid):
     resid.index_add_(0, idx.long(), v.float() - q8_dequant(q, scales))
 
 
-def topk_workspace_bytes(n: int) -> int:
+def topk_workspace_bytes(n: int, k: int = 0) -> int:
     return 16
 
 

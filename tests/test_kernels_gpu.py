@@ -194,6 +194,38 @@ def test_topk_candidate_overflow_and_ties(case):
     assert torch.equal(vd.cpu(), val)
 
 
+@pytest.mark.parametrize("vdt", [torch.float32, torch.bfloat16])
+def test_topk_repeated_calls_speculative_list(vdt):
+    """One workspace across calls, as a codec keeps it per bucket: call 1 has no previous threshold
+    (P1 lists nothing, the repair pass lists bin B and up); later calls list from one radix bin
+    below the previous threshold (the single-pass path); a 10x smaller gradient drops the threshold below that bound (every region
+    repairs); a skewed bucket overflows a few regions' slots (shared pool); an all-equal bucket
+    exhausts the pool (full-pass mode).  Every call must equal the CPU reference bit for bit,
+    error-feedback residual included."""
+    n, k = 3_000_001, 30001
+    torch.manual_seed(3)
+    ws = torch.zeros(ops.topk_workspace_bytes(n, k), dtype=torch.uint8, device=DEV)
+    r_cpu, r_dev = torch.zeros(n), torch.zeros(n, device=DEV)
+    gens = [lambda: torch.randn(n), lambda: torch.randn(n), lambda: torch.randn(n) * 1.3,
+            lambda: torch.randn(n) * 0.1, lambda: torch.randn(n) * 0.1]
+
+    def skew():
+        x = torch.randn(n) * 0.01
+        x[1_000_000:1_200_000] = torch.randn(200_000) * 10  # one layer with large gradients
+        return x
+
+    gens += [skew, skew, lambda: torch.full((n,), 0.5), lambda: torch.randn(n)]
+    for step, gen in enumerate(gens):
+        g = gen()
+        idx, val = torch.empty(k, dtype=torch.int32), torch.empty(k, dtype=vdt)
+        ref.topk_encode(g, r_cpu, k, idx, val)
+        idd, vd = torch.empty(k, dtype=torch.int32, device=DEV), torch.empty(k, dtype=vdt, device=DEV)
+        ops.topk_encode(g.to(DEV), r_dev, k, idd, vd, ws)
+        assert torch.equal(idd.cpu(), idx), step
+        assert torch.equal(vd.cpu(), val), step
+        assert torch.equal(r_dev.cpu(), r_cpu), step
+
+
 def test_topk_error_feedback_conserves_mass():
     n, k = 100_000, 1000
     g = torch.randn(n, device=DEV)
