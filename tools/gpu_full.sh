@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
 ROOT=$GRAFT_REPO_ROOT
-[ -n "$NOTESTS" ] || timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 gpurun_out/gpu_tests.log; exit 1; }
+[ -n "$NOTESTS" ] || timeout -k 10 800 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 gpurun_out/gpu_tests.log; exit 1; }
 [ -n "$NOTESTS" ] || tail -1 gpurun_out/gpu_tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -40 gpurun_out/smoke.log; exit 1; }
 tail -1 gpurun_out/smoke.log
