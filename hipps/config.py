@@ -56,8 +56,9 @@ class PSConfig:
     # GPU distributed modes: gather autograd-owned grads per bucket with one multi-tensor kernel
     # instead of accumulating into preset flat-buffer views (161 fewer kernels for ResNet-50)
     grad_gather: bool = True
-    # published-parameter wire dtype for PS modes: 'fp32' | 'bf16'
-    param_wire: str = "fp32"
+    # published-parameter wire dtype for PS modes: 'fp32' | 'bf16' | 'auto' (bf16 for ps_sync and
+    # ps_async with more than one GPU rank, fp32 otherwise)
+    param_wire: str = "auto"
     # bf16 weight shadow: one flat bf16 copy of the fp32 params, refreshed by one cast kernel after
     # every step()/irequest_params(), read by the hipps conv kernels instead of one autocast cast
     # per layer per forward.  'auto' = on for ps_async on a GPU for models with conv weights (the
@@ -125,8 +126,8 @@ class PSConfig:
             raise ValueError(f"mode must be one of {MODES}, got {self.mode!r}")
         if self.pull not in ("device", "prefetch", "direct"):
             raise ValueError("pull must be 'device', 'prefetch' or 'direct'")
-        if self.param_wire not in ("fp32", "bf16"):
-            raise ValueError("param_wire must be 'fp32' or 'bf16'")
+        if self.param_wire not in ("fp32", "bf16", "auto"):
+            raise ValueError("param_wire must be 'fp32', 'bf16' or 'auto'")
         if self.bf16_weights not in ("auto", "on", "off"):
             raise ValueError("bf16_weights must be 'auto', 'on' or 'off'")
         if self.async_transport not in ("ipc", "p2p"):

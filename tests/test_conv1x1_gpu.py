@@ -171,34 +171,56 @@ def test_maxpool3s2_matches_torch(shape):
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
 
 
-def _resnet_run(R, m, x, conv, grad, pool):
-    R._FUSED_CONV, R._FUSED_GRAD = conv, grad
-    m.maxpool.fused = pool
+def _resnet_run(R, m, x, fused):
+    """One forward/backward with every runtime fusion switch on or off: 1x1 MFMA conv + BN stats,
+    residual-gradient and BN-backward epilogues, 3x3 weight gradient, own 1x1 weight gradient,
+    3x3 input gradient as a forward conv, fused BN, stem max pool."""
+    import hipps.ops.nn as N
+
+    saved = (R._FUSED_CONV, R._FUSED_GRAD, R._FUSED_BNGRAD, R._FUSED_WGRAD, N._OWN_WGRAD, N._DGRAD_AS_FWD)
+    bns = [mod for mod in m.modules() if isinstance(mod, N.FusedBatchNorm2d)]
+    R._FUSED_CONV = R._FUSED_GRAD = R._FUSED_BNGRAD = R._FUSED_WGRAD = fused
+    N._OWN_WGRAD = N._DGRAD_AS_FWD = fused
+    m.maxpool.fused = fused
+    for bn in bns:
+        bn.fused = fused
     try:
         m.zero_grad(set_to_none=True)
         with torch.autocast("cuda", dtype=torch.bfloat16):
             y = m(x)
         y.float().sum().backward()
     finally:
-        R._FUSED_CONV = R._FUSED_GRAD = True
+        R._FUSED_CONV, R._FUSED_GRAD, R._FUSED_BNGRAD, R._FUSED_WGRAD, N._OWN_WGRAD, N._DGRAD_AS_FWD = saved
         m.maxpool.fused = True
+        for bn in bns:
+            bn.fused = True
     return (y.float(), m.conv1.weight.grad.clone(), m.bn1.weight.grad.clone(), m.layer1[0].conv1.weight.grad.clone(),
-            m.layer1[1].conv1.weight.grad.clone(), m.layer2[0].downsample[0].weight.grad.clone(),
-            m.layer3[2].conv2.weight.grad.clone())
+            m.layer1[1].conv1.weight.grad.clone(), m.layer1[1].conv2.weight.grad.clone(),
+            m.layer2[0].downsample[0].weight.grad.clone(), m.layer3[2].conv2.weight.grad.clone(),
+            m.layer4[2].bn3.weight.grad.clone())
+
+
+def _rel(u, v):
+    return float((u.float() - v.float()).norm() / v.float().norm().clamp_min(1e-12))
 
 
 def test_resnet50_fused_conv_matches_unfused():
-    """All ResNet fusions (1x1 MFMA conv + BN stats, residual-gradient epilogue sums, stem max
-    pool) against the plain path (MIOpen convs, autograd adds, PyTorch pool)."""
+    """All ResNet fusions against the plain path (MIOpen convs, eager BN, autograd adds, PyTorch
+    pool).  bn3 weights are drawn uniformly in [0.5, 1.5] (zero-init would make every residual
+    branch gradient exactly zero in both runs); gradients compared by relative norm error."""
     import hipps.models.resnet as R
 
     torch.manual_seed(0)
     m = R.resnet50(num_classes=10).to(DEV).to(memory_format=torch.channels_last)
+    for blk in [b for layer in (m.layer1, m.layer2, m.layer3, m.layer4) for b in layer]:
+        torch.nn.init.uniform_(blk.bn3.weight, 0.5, 1.5)
     x = _cl(torch.randn(4, 3, 64, 64, device=DEV))
-    a = _resnet_run(R, m, x, True, True, True)
-    b = _resnet_run(R, m, x, False, False, False)
-    for u, v in zip(a, b):
-        torch.testing.assert_close(u, v, rtol=5e-2, atol=5e-2)
+    a = _resnet_run(R, m, x, True)
+    b = _resnet_run(R, m, x, False)
+    names = ["out", "stem", "bn1.w", "l1.0.conv1", "l1.1.conv1", "l1.1.conv2", "l2.0.down", "l3.2.conv2", "l4.2.bn3.w"]
+    for name, u, v in zip(names, a, b):
+        assert float(v.float().abs().max()) > 0, name  # every compared gradient is live
+        assert _rel(u, v) < 3e-2, (name, _rel(u, v))
 
 
 @pytest.mark.parametrize("bngrad", [False, True])
