@@ -171,7 +171,7 @@ def test_maxpool3s2_matches_torch(shape):
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
 
 
-def _resnet_run(R, m, x, fused):
+def _resnet_run(R, m, x, fused, bf16=True):
     """One forward/backward with every runtime fusion switch on or off: 1x1 MFMA conv + BN stats,
     residual-gradient and BN-backward epilogues, 3x3 weight gradient, own 1x1 weight gradient,
     3x3 input gradient as a forward conv, fused BN, stem max pool."""
@@ -186,7 +186,7 @@ def _resnet_run(R, m, x, fused):
         bn.fused = fused
     try:
         m.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16):
             y = m(x)
         y.float().sum().backward()
     finally:
@@ -206,21 +206,25 @@ def _rel(u, v):
 
 def test_resnet50_fused_conv_matches_unfused():
     """All ResNet fusions against the plain path (MIOpen convs, eager BN, autograd adds, PyTorch
-    pool).  bn3 weights are drawn uniformly in [0.5, 1.5] (zero-init would make every residual
-    branch gradient exactly zero in both runs); gradients compared by relative norm error."""
+    pool), both under bf16 autocast, judged against a plain fp32 run: the fused path may not add
+    error beyond what bf16 itself costs (50 layers of bf16 with training-mode BN drift far from
+    fp32, so a fixed tolerance between the two bf16 runs says little).  bn3 weights are drawn in
+    [0.5, 1.5]: zero-init would make every residual branch gradient exactly zero in all runs."""
     import hipps.models.resnet as R
 
     torch.manual_seed(0)
     m = R.resnet50(num_classes=10).to(DEV).to(memory_format=torch.channels_last)
     for blk in [b for layer in (m.layer1, m.layer2, m.layer3, m.layer4) for b in layer]:
         torch.nn.init.uniform_(blk.bn3.weight, 0.5, 1.5)
-    x = _cl(torch.randn(4, 3, 64, 64, device=DEV))
-    a = _resnet_run(R, m, x, True)
-    b = _resnet_run(R, m, x, False)
+    x = _cl(torch.randn(8, 3, 96, 96, device=DEV))
+    fused = _resnet_run(R, m, x, True)
+    plain = _resnet_run(R, m, x, False)
+    ref = _resnet_run(R, m, x, False, bf16=False)
     names = ["out", "stem", "bn1.w", "l1.0.conv1", "l1.1.conv1", "l1.1.conv2", "l2.0.down", "l3.2.conv2", "l4.2.bn3.w"]
-    for name, u, v in zip(names, a, b):
-        assert float(v.float().abs().max()) > 0, name  # every compared gradient is live
-        assert _rel(u, v) < 3e-2, (name, _rel(u, v))
+    for name, f, p, r in zip(names, fused, plain, ref):
+        assert float(r.float().abs().max()) > 0, name  # every compared gradient is live
+        ef, ep = _rel(f, r), _rel(p, r)
+        assert ef <= 1.5 * ep + 0.02, (name, ef, ep)
 
 
 @pytest.mark.parametrize("bngrad", [False, True])
