@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--allow-fallback", action="store_true",
                     help="if the ps_async IPC transport cannot initialise, use its p2p transport instead of failing")
     ap.add_argument("--async-transport", default="ipc", choices=["ipc", "p2p"])
+    ap.add_argument("--no-pull-overlap", action="store_true",
+                    help="ps_async: one GPU-time pull of all params before the forward (A/B)")
     return ap.parse_args()
 
 
@@ -109,6 +111,11 @@ def main():
         print("[bench] " + note, file=sys.stderr)
         kw["async_transport"] = "p2p"
         opt = hipps.SGD(model.named_parameters(), **kw)
+    # N > 1: pull the last stage's parameters (ResNet layer4 + fc: 2/3 of the model) over xGMI on a
+    # side stream, overlapped with the forward of layers 1-3.  At N = 1 the pull is a local
+    # 0.1 ms copy and the split costs more than it hides (A/B: 10099 vs 10170 img/s)
+    pull_overlap = bool(N > 1 and not a.no_pull_overlap and hasattr(model, "layer4")
+                        and opt.overlap_pull(model.layer4))
 
     def step():
         opt.zero_grad()
@@ -186,7 +193,7 @@ def main():
                 "accumulate": a.accumulate or N,
                 "grad_bytes_per_step_per_worker": grad_bytes,
                 "grad_bytes_per_step_used": int(grad_used),
-                "param_wire": a.param_wire,
+                "param_wire": a.param_wire, "pull_overlap": pull_overlap,
                 "num_params": nparams,
                 "buckets": nbuckets,
             },

@@ -65,6 +65,11 @@ void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t 
 namespace rt {
 void pull_params(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, at::Tensor pub,
                  int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t ring_slot, int64_t tries);
+void pull_select(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, int64_t npub,
+                 int64_t tries);
+void pull_copy(at::Tensor sel, at::Tensor pub, int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t lo,
+               int64_t hi);
+void pull_done(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, int64_t ring_slot);
 void bind_control(pybind11::module& m);
 void bind_rccl(pybind11::module& m);
 void bind_ipc(pybind11::module& m);
@@ -119,6 +124,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_wgrad", &hipps::conv1x1_wgrad, "MFMA 1x1 conv weight gradient (tr_b16 LDS reads, split-M)");
   m.def("pull_params", &hipps::rt::pull_params,
         "GPU-time AsySG-InCon pull: select newest published version, copy it, release the reader word");
+  m.def("pull_select", &hipps::rt::pull_select, "GPU-time pull, stage 1: choose the version, announce the reader");
+  m.def("pull_copy", &hipps::rt::pull_copy, "GPU-time pull, stage 2: copy params[lo, hi) of the chosen version");
+  m.def("pull_done", &hipps::rt::pull_done, "GPU-time pull, stage 3: release the reader word, record the version");
   hipps::rt::bind_control(m);
   hipps::rt::bind_rccl(m);
   hipps::rt::bind_ipc(m);

@@ -58,17 +58,27 @@ __global__ __launch_bounds__(64) void k_pull_select(PullWords w, int64_t* __rest
   sel[0] = out;
 }
 
+// params[lo, hi) <- publish buffer of sel[0]; four 4-element groups per lane in flight (the
+// remote reads cross xGMI, where latency, not the lane count, bounds a one-load-per-lane loop)
 template <typename Tin>
 __global__ __launch_bounds__(kBlock) void k_pull_copy(const int64_t* __restrict__ sel, const uint8_t* __restrict__ pub,
                                                       int64_t stride, int npub, float* __restrict__ dst, int64_t n) {
+  constexpr int U = 4;
   const int64_t v = sel[0];
   if (v < 0) return;
   // system-scope acquire: drop any stale copy of the (remote) publish buffer before reading it
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   const Tin* src = reinterpret_cast<const Tin*>(pub + (v % npub) * stride);
   const int64_t nv = n >> 2, step = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += step)
-    Vec4<float>::store(dst, i << 2, Vec4<Tin>::load(src, i << 2));
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < nv; i0 += U * step) {
+    float4 t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + u * step < nv) t[u] = Vec4<Tin>::load(src, (i0 + u * step) << 2);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + u * step < nv) Vec4<float>::store(dst, (i0 + u * step) << 2, t[u]);
+  }
   if (blockIdx.x == 0)
     for (int64_t i = (nv << 2) + threadIdx.x; i < n; i += blockDim.x) dst[i] = Vec4<Tin>::load1(src, i);
 }
@@ -90,29 +100,54 @@ static PullWords words_of(int64_t pub_ver, int64_t buf_ver, int64_t reading, int
                    reinterpret_cast<int64_t*>(reading), reinterpret_cast<int64_t*>(applied)};
 }
 
-// One adoption: select + copy + done on the current stream.  sel: int64 device tensor
-// [2 + ring]; pub: the uint8 view of publish buffer 0 .. npub-1 (stride bytes apart).
-void pull_params(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, at::Tensor pub,
-                 int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t ring_slot, int64_t tries) {
+// The three stages as separate launches on the current stream, so a caller can split the copy
+// over streams (ps_async pull_overlap: the late layers' range lands on a side stream while the
+// forward of the early layers runs).  sel: int64 device tensor [2 + ring]; pub: the uint8 view
+// of publish buffers 0 .. npub-1 (stride bytes apart); dst: the flat f32 parameters.
+void pull_select(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, int64_t npub,
+                 int64_t tries) {
+  TORCH_CHECK(sel.is_cuda() && sel.scalar_type() == at::kLong && sel.is_contiguous() && sel.numel() >= 3,
+              "sel must be int64 device [2 + ring]");
+  TORCH_CHECK(npub >= 1, "npub");
+  hipLaunchKernelGGL(k_pull_select, dim3(1), dim3(64), 0, c10::hip::getCurrentHIPStream(),
+                     words_of(pub_ver, buf_ver, reading, applied), sel.data_ptr<int64_t>(), (int)npub, (int)tries);
+}
+
+void pull_copy(at::Tensor sel, at::Tensor pub, int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t lo,
+               int64_t hi) {
   TORCH_CHECK(sel.is_cuda() && sel.scalar_type() == at::kLong && sel.is_contiguous(), "sel must be int64 device");
-  TORCH_CHECK(ring_slot >= 0 && ring_slot + 2 < sel.numel(), "ring slot out of range");
   TORCH_CHECK(pub.is_cuda() && pub.scalar_type() == at::kByte, "pub must be a uint8 device view");
   TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kFloat && dst.is_contiguous(), "dst must be f32 device");
+  const int64_t esz = bf16 ? 2 : 4;
+  TORCH_CHECK(0 <= lo && lo <= hi && hi <= dst.numel() && lo % 4 == 0, "range [lo, hi) of dst, lo % 4 == 0");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(pub.data_ptr()) % 16 == 0 && stride % 16 == 0, "pub must be 16B aligned");
-  const int64_t n = dst.numel();
-  TORCH_CHECK(npub >= 1 && pub.numel() >= (npub - 1) * stride + n * (bf16 ? 2 : 4), "publish view too small");
-  PullWords w = words_of(pub_ver, buf_ver, reading, applied);
+  TORCH_CHECK(npub >= 1 && pub.numel() >= (npub - 1) * stride + dst.numel() * esz, "publish view too small");
+  if (hi == lo) return;
+  const int64_t n = hi - lo;
   auto stream = c10::hip::getCurrentHIPStream();
-  int64_t* s = sel.data_ptr<int64_t>();
-  hipLaunchKernelGGL(k_pull_select, dim3(1), dim3(64), 0, stream, w, s, (int)npub, (int)tries);
-  const int grid = grid_for(n >> 2);
+  const int grid = grid_for((n >> 2) / 4 + 1);
+  const uint8_t* src = pub.data_ptr<uint8_t>() + lo * esz;
   if (bf16)
-    hipLaunchKernelGGL(k_pull_copy<uint16_t>, grid, kBlock, 0, stream, s, pub.data_ptr<uint8_t>(), stride, (int)npub,
-                       dst.data_ptr<float>(), n);
+    hipLaunchKernelGGL(k_pull_copy<uint16_t>, grid, kBlock, 0, stream, sel.data_ptr<int64_t>(), src, stride, (int)npub,
+                       dst.data_ptr<float>() + lo, n);
   else
-    hipLaunchKernelGGL(k_pull_copy<float>, grid, kBlock, 0, stream, s, pub.data_ptr<uint8_t>(), stride, (int)npub,
-                       dst.data_ptr<float>(), n);
-  hipLaunchKernelGGL(k_pull_done, dim3(1), dim3(64), 0, stream, w, s, (int)ring_slot);
+    hipLaunchKernelGGL(k_pull_copy<float>, grid, kBlock, 0, stream, sel.data_ptr<int64_t>(), src, stride, (int)npub,
+                       dst.data_ptr<float>() + lo, n);
+}
+
+void pull_done(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, int64_t ring_slot) {
+  TORCH_CHECK(sel.is_cuda() && sel.scalar_type() == at::kLong && sel.is_contiguous(), "sel must be int64 device");
+  TORCH_CHECK(ring_slot >= 0 && ring_slot + 2 < sel.numel(), "ring slot out of range");
+  hipLaunchKernelGGL(k_pull_done, dim3(1), dim3(64), 0, c10::hip::getCurrentHIPStream(),
+                     words_of(pub_ver, buf_ver, reading, applied), sel.data_ptr<int64_t>(), (int)ring_slot);
+}
+
+// One adoption: select + copy + done on the current stream.
+void pull_params(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, at::Tensor pub,
+                 int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t ring_slot, int64_t tries) {
+  pull_select(sel, pub_ver, buf_ver, reading, applied, npub, tries);
+  pull_copy(sel, pub, stride, npub, bf16, dst, 0, dst.numel());
+  pull_done(sel, pub_ver, buf_ver, reading, applied, ring_slot);
 }
 
 }  // namespace rt

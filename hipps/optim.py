@@ -188,7 +188,7 @@ class MPI_PS(torch.optim.Optimizer):
         self.steps += 1
         t0 = time.perf_counter()
         data = self.engine.step()
-        self.store.refresh_shadow()
+        self._refresh_shadow()
         data["step_time"] = time.perf_counter() - t0
         if self._metrics is not None:
             self._metrics.write(self.steps, data)
@@ -224,11 +224,35 @@ class MPI_PS(torch.optim.Optimizer):
         """AsySG-InCon parameter refresh (README.md:63): adopt the newest published params that
         have arrived, without waiting for the rest (inconsistent read).  No-op in sync modes."""
         r = self.engine.irequest_params(**kw)
-        self.store.refresh_shadow()
+        self._refresh_shadow()
         return r
+
+    def _refresh_shadow(self):
+        eng = self.engine
+        if hasattr(eng, "take_shadow_done"):
+            if eng.take_shadow_done():  # a split pull refreshed each half on its own stream
+                return
+            eng.join_pull()
+        self.store.refresh_shadow()
+
+    def overlap_pull(self, module: torch.nn.Module) -> bool:
+        """ps_async with the GPU-time pull: copy the parameters of ``module`` and of everything
+        after it in parameter order on a side stream, overlapped with the forward of the earlier
+        layers; ``module``'s forward waits for them.  Use it only when no parameter from ``module``
+        on is read before ``module`` runs (ResNet: ``model.layer4``).  Returns False (no-op) in
+        other modes or when the module has no managed parameters."""
+        eng = self.engine
+        if not hasattr(eng, "set_pull_overlap"):
+            return False
+        offs = [s.offset for s in self.store.slots if any(s.param is p for p in module.parameters())]
+        if not offs:
+            return False
+        return eng.set_pull_overlap(min(offs), module)
 
     def refresh_bf16_weights(self):
         """Re-cast the bf16 weight shadow after editing parameters outside ``step()``."""
+        if hasattr(self.engine, "join_pull"):
+            self.engine.join_pull()
         self.store.refresh_shadow()
 
     def close(self):

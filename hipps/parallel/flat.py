@@ -185,6 +185,7 @@ class FlatStore:
         from ..ops import nn as hnn
 
         self.tshadow = self._tiles = None
+        self._tile_ranges = {}
         if self.device.type != "cuda" or not _native.available():
             return
         mats, off = [], 0
@@ -220,14 +221,32 @@ class FlatStore:
                 for s in self.slots:
                     hnn.unregister_transposed_weight(s.param)
             self.shadow = self.tshadow = self._tiles = None
+            self._tile_ranges = {}
 
-    def refresh_shadow(self):
-        if getattr(self, "shadow", None) is not None:
-            self.shadow.copy_(self.data)  # one vectorized cast kernel on the current stream
-            if getattr(self, "tshadow", None) is not None:
-                from ..ops._native import native
+    def refresh_shadow(self, lo: int = 0, hi: Optional[int] = None):
+        """Re-cast the bf16 shadows of ``data[lo:hi]`` (default: all) on the current stream; a
+        range must start and end at slot boundaries (ps_async pull_overlap refreshes the two
+        halves of a split pull on their own streams)."""
+        if getattr(self, "shadow", None) is None:
+            return
+        full = lo == 0 and (hi is None or hi >= self.numel)
+        hi = self.numel if hi is None else hi
+        self.shadow[lo:hi].copy_(self.data[lo:hi])  # one vectorized cast kernel
+        if getattr(self, "tshadow", None) is not None:
+            from ..ops._native import native
 
-                native().transpose_cast(self.data, self.tshadow, self._tiles)
+            tiles = self._tiles if full else self._tiles_in(lo, hi)
+            if tiles is not None and tiles.numel():
+                native().transpose_cast(self.data, self.tshadow, tiles)
+
+    def _tiles_in(self, lo: int, hi: int):
+        """The transpose tiles whose source matrix lies in data[lo:hi] (cached per range)."""
+        cache = self.__dict__.setdefault("_tile_ranges", {})
+        if (lo, hi) not in cache:
+            t = self._tiles
+            sel = (t[:, 0] >= lo) & (t[:, 0] < hi)
+            cache[(lo, hi)] = t[sel].contiguous()
+        return cache[(lo, hi)]
 
     # ---- per-step "parameter has a gradient" masks (ps.py:178-179 skip semantics) -----------
     @property

@@ -215,6 +215,10 @@ class PSAsyncEngine(Engine):
         self._stage = [None, None]  # double-buffered staging for prefetch / p2p pulls
         self._stage_ev = [None, None]
         self._stage_k = 0
+        # pull_overlap state (set_pull_overlap): split offset, side stream, pending late event
+        self._split = None
+        self._late_stream = self._late_ev = self._late_hook = None
+        self._shadow_done = False
         if self.cuda:
             # sel[0] selected, sel[1] adopted, sel[2:2+RING] version each step's gradient uses
             self._sel = torch.full((2 + RING,), -1, dtype=torch.int64, device=store.device)
@@ -721,6 +725,8 @@ class PSAsyncEngine(Engine):
         adopts synchronously; ``cfg.max_delay >= 0`` waits until the published params include
         all but this worker's newest ``max_delay`` gradients."""
         C = self.C
+        if self.cuda:
+            self.join_pull()  # a split pull whose late half no forward has waited for yet
         sync = block_for is not None
         if block_for is not None:
             if not self.ctl.wait_ge(C.F_PUB_VER, 0, block_for, self.timeout_us):
@@ -747,11 +753,70 @@ class PSAsyncEngine(Engine):
         C = self.C
         esz = torch.empty((), dtype=self.pub_dtype).element_size()
         base = self.mem[self.pub_off:self.pub_off + (self.NPUB - 1) * self.pub_bytes + self.store.numel * esz]
-        self.C.pull_params(self._sel, self.ctl.device_addr(C.F_PUB_VER, 0), self.ctl.device_addr(C.F_BUF_VER, 0),
-                           self.ctl.device_addr(C.F_READING, self.rank), self.ctl.device_addr(C.F_APPLIED_VER, self.rank),
-                           base, self.pub_bytes, self.NPUB, self.pub_dtype == torch.bfloat16, self.store.data,
-                           (self.step_no + 1) % RING, 64)
+        words = (self.ctl.device_addr(C.F_PUB_VER, 0), self.ctl.device_addr(C.F_BUF_VER, 0),
+                 self.ctl.device_addr(C.F_READING, self.rank), self.ctl.device_addr(C.F_APPLIED_VER, self.rank))
+        bf16 = self.pub_dtype == torch.bfloat16
+        ring = (self.step_no + 1) % RING
+        if self._split is None:
+            self.C.pull_params(self._sel, *words, base, self.pub_bytes, self.NPUB, bf16, self.store.data, ring, 64)
+            return True
+        # pull_overlap: the early layers' range [0, split) on the compute stream, the late range on
+        # a side stream that the late module's forward pre-hook waits for (set_pull_overlap)
+        dev, n, s = self.store.device, self.store.numel, self._split
+        cs = torch.cuda.current_stream(dev)
+        self.C.pull_select(self._sel, *words, self.NPUB, 64)
+        ev_sel = torch.cuda.Event()
+        ev_sel.record(cs)
+        self.C.pull_copy(self._sel, base, self.pub_bytes, self.NPUB, bf16, self.store.data, 0, s)
+        self.store.refresh_shadow(0, s)
+        ev_early = torch.cuda.Event()
+        ev_early.record(cs)
+        side = self._late_stream
+        with torch.cuda.stream(side):
+            side.wait_event(ev_sel)
+            self.C.pull_copy(self._sel, base, self.pub_bytes, self.NPUB, bf16, self.store.data, s, n)
+            self.store.refresh_shadow(s, n)
+            side.wait_event(ev_early)  # the reader word is released after BOTH halves were read
+            self.C.pull_done(self._sel, *words, ring)
+        late = torch.cuda.Event()
+        late.record(side)
+        self._late_ev = late
+        self._shadow_done = True
         return True
+
+    def set_pull_overlap(self, split: int, module) -> bool:
+        """Split the GPU-time pull at flat offset ``split``: params [split, numel) -- those of
+        ``module`` and every parameter after it in the flat layout -- are copied (and their bf16
+        shadows refreshed) on a side stream while the forward of the earlier layers runs;
+        ``module``'s forward pre-hook makes the compute stream wait for them.  Contract: no
+        parameter at or after ``split`` is read before ``module``'s forward starts (true for a
+        network whose late layers are one submodule called in order, e.g. ResNet ``layer4``, whose
+        successors are only the head)."""
+        if not (self.cuda and self.pull_mode == "device") or not 0 < split < self.store.numel:
+            return False
+        self._split = int(split)
+        if self._late_stream is None:
+            self._late_stream = torch.cuda.Stream(device=self.store.device)
+
+        def wait_late(_mod, _args):
+            self.join_pull()
+
+        if self._late_hook is not None:
+            self._late_hook.remove()
+        self._late_hook = module.register_forward_pre_hook(wait_late)
+        return True
+
+    def join_pull(self):
+        """Order the compute stream after the late half of a split pull (no-op otherwise)."""
+        ev = self._late_ev
+        if ev is not None:
+            torch.cuda.current_stream(self.store.device).wait_event(ev)
+            self._late_ev = None
+
+    def take_shadow_done(self) -> bool:
+        """True once after a split pull refreshed the bf16 shadows itself."""
+        v, self._shadow_done = self._shadow_done, False
+        return v
 
     def _claim(self):
         """Host-side reader handshake: (version, buffer) announced in READING, or None."""

@@ -102,7 +102,9 @@ def _gpu_sync(rank, world, mode, codec):
 
     torch.cuda.set_device(0)
     m = _mlp().cuda()
-    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode=mode, code=codec)
+    # fp32 parameter wire: with 'auto' (bf16 at W > 1 on GPUs) the PS rank keeps its fp32 master
+    # while the others train on the bf16 broadcast, so replicas differ by design
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode=mode, code=codec, param_wire="fp32")
     for s in range(4):
         x, y = _data(rank, s)
         opt.zero_grad()
@@ -122,3 +124,50 @@ def test_gpu_sync_engines_replicas_identical(mode, codec):
     assert out[0][1] == "gather"
     for a, b in zip(out[0][0], out[1][0]):
         assert torch.equal(a, b)
+
+
+def _tiny_overlap(rank, world, overlap, steps):
+    import hashlib
+
+    import torch.nn.functional as F
+
+    import hipps
+    from hipps.models import resnet_tiny
+
+    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.benchmark = False
+    torch.cuda.set_device(0)
+    torch.manual_seed(0)
+    m = resnet_tiny().cuda().to(memory_format=torch.channels_last)
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", code="fp32", max_delay=0,
+                    bf16_weights="on")
+    ok = opt.overlap_pull(m.layer2) if overlap else False
+    g = torch.Generator().manual_seed(1)
+    losses = []
+    for _ in range(steps):
+        x = torch.randn(8, 3, 32, 32, generator=g).cuda().contiguous(memory_format=torch.channels_last)
+        y = torch.randint(0, 10, (8,), generator=g).cuda()
+        opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = F.cross_entropy(m(x), y)
+        loss.backward()
+        losses.append(loss.item())
+        opt.step()
+    torch.cuda.synchronize()
+    out = {"ok": ok, "losses": losses, "ver": opt.engine.adopted_version(),
+           "sha": hashlib.sha1(opt.store.data.cpu().numpy().tobytes()).hexdigest(),
+           "shadow": hashlib.sha1(opt.store.shadow.view(torch.int16).cpu().numpy().tobytes()).hexdigest()}
+    opt.close()
+    return out
+
+
+def test_gpu_async_pull_overlap_bitwise():
+    """pull_overlap (late layers' params pulled + shadow-cast on a side stream, the late module's
+    forward waits) must train bit for bit like the one-stream pull (max_delay=0: the pulled
+    version is deterministic)."""
+    a = run_world(_tiny_overlap, 1, True, 8)[0]
+    b = run_world(_tiny_overlap, 1, False, 8)[0]
+    assert a["ok"] and not b["ok"]
+    assert a["losses"] == b["losses"]
+    assert a["sha"] == b["sha"] and a["shadow"] == b["shadow"]
+    assert a["ver"] == b["ver"] >= 7
