@@ -37,6 +37,17 @@ class MPI_PS(torch.optim.Optimizer):
 
     optim = "base"
 
+    def __new__(cls, *args, optim=None, **kwargs):
+        # MPI_PS(..., optim='sgd' | 'adam') builds the matching subclass (the reference's MPI_PS
+        # selects its update rule from ``optim``, ps.py:56, 182-190)
+        if cls is MPI_PS:
+            key = (optim or "sgd").lower()
+            sub = {c.optim: c for c in MPI_PS.__subclasses__()}.get(key)
+            if sub is None:
+                raise ValueError(f"optim must be one of {sorted(c.optim for c in MPI_PS.__subclasses__())}")
+            cls = sub
+        return super().__new__(cls)
+
     def __init__(self, named_params, *args, names=(), optim=None, code=None, use_mpi=True, cuda=None,
                  config: Optional[PSConfig] = None, **kwargs):
         """``named_params, *args, names, optim, code, use_mpi, cuda`` as in ps.py:54-59; any

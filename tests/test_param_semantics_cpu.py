@@ -175,3 +175,26 @@ def test_step_metrics_keep_reference_keys(mode, world):
               "iallgather_prepare_time", "isend_time", "grad_bytes_sent"):
         assert k in data, (mode, k)
     assert data["msg_bytes"] > 0 and data["packaged_bytes"] >= data["msg_bytes"]
+
+
+def test_mpi_ps_factory_and_reference_constructor():
+    """``MPI_PS(named_params, *params, names=, optim=, code=, use_mpi=, cuda=, **torch_kwargs)``
+    (ps.py:54-59) builds the subclass its ``optim`` names and keeps the reference attributes."""
+    import hipps
+
+    m = torch.nn.Linear(4, 2)
+    o = hipps.MPI_PS(m.named_parameters(), m.parameters(), names=["w", "b"], optim="sgd", code=None, use_mpi=True,
+                     cuda=False, lr=0.1, momentum=0.9)
+    assert isinstance(o, hipps.SGD) and o.optim == "sgd" and o.use_mpi and o.cuda is False and o.names == ["w", "b"]
+    o.zero_grad()
+    m(torch.randn(3, 4)).sum().backward()
+    loss, data = o.step()
+    assert loss is None and {"msg_bytes", "packaged_bytes", "iallgather_prepare_time"} <= set(data)
+    o.close()
+    a = hipps.MPI_PS(m.named_parameters(), optim="adam", lr=1e-3)
+    assert isinstance(a, hipps.Adam)
+    a.close()
+    with pytest.raises(ValueError):
+        hipps.MPI_PS(m.named_parameters(), optim="rmsprop", lr=0.1)
+    with pytest.raises(ValueError):
+        hipps.SGD(m.named_parameters(), optim="adam", lr=0.1)
