@@ -19,6 +19,8 @@
 // Control words live in the registered shared-memory control block (system-scope atomics);
 // sel / ring are a small device tensor owned by the worker.
 #include <ATen/ATen.h>
+#include <cstdlib>
+#include <algorithm>
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
@@ -62,12 +64,16 @@ __global__ __launch_bounds__(64) void k_pull_select(PullWords w, int64_t* __rest
 // remote reads cross xGMI, where latency, not the lane count, bounds a one-load-per-lane loop)
 template <typename Tin>
 __global__ __launch_bounds__(kBlock) void k_pull_copy(const int64_t* __restrict__ sel, const uint8_t* __restrict__ pub,
-                                                      int64_t stride, int npub, float* __restrict__ dst, int64_t n) {
+                                                      int64_t stride, int npub, float* __restrict__ dst, int64_t n,
+                                                      int fence_mode) {
   constexpr int U = 4;
   const int64_t v = sel[0];
   if (v < 0) return;
-  // system-scope acquire: drop any stale copy of the (remote) publish buffer before reading it
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  // system-scope acquire: drop any stale copy of the (remote) publish buffer before reading it.
+  // The invalidation acts on the CU's L1 and its XCD's L2, so one wave per workgroup issues it
+  // and the others wait at the barrier (every wave fencing cost 4x the invalidations)
+  if (fence_mode == 0 || threadIdx.x < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  if (fence_mode == 1) __syncthreads();
   const Tin* src = reinterpret_cast<const Tin*>(pub + (v % npub) * stride);
   const int64_t nv = n >> 2, step = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < nv; i0 += U * step) {
@@ -125,14 +131,22 @@ void pull_copy(at::Tensor sel, at::Tensor pub, int64_t stride, int64_t npub, boo
   if (hi == lo) return;
   const int64_t n = hi - lo;
   auto stream = c10::hip::getCurrentHIPStream();
-  const int grid = grid_for((n >> 2) / 4 + 1);
+  static const int fence_mode = [] {  // A/B knob: 0 every wave fences, 1 one wave per workgroup
+    const char* e = std::getenv("HIPPS_PULL_FENCE");
+    return e ? std::atoi(e) : 1;
+  }();
+  static const int grid_div = [] {  // lanes per 16 elements: fewer workgroups, fewer fences
+    const char* e = std::getenv("HIPPS_PULL_GRID_DIV");
+    return e ? std::max(1, std::atoi(e)) : 16;
+  }();
+  const int grid = grid_for((n >> 2) / grid_div + 1);
   const uint8_t* src = pub.data_ptr<uint8_t>() + lo * esz;
   if (bf16)
     hipLaunchKernelGGL(k_pull_copy<uint16_t>, grid, kBlock, 0, stream, sel.data_ptr<int64_t>(), src, stride, (int)npub,
-                       dst.data_ptr<float>() + lo, n);
+                       dst.data_ptr<float>() + lo, n, fence_mode);
   else
     hipLaunchKernelGGL(k_pull_copy<float>, grid, kBlock, 0, stream, sel.data_ptr<int64_t>(), src, stride, (int)npub,
-                       dst.data_ptr<float>() + lo, n);
+                       dst.data_ptr<float>() + lo, n, fence_mode);
 }
 
 void pull_done(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, int64_t ring_slot) {
