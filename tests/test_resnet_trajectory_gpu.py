@@ -4,8 +4,9 @@
   wgrad/dgrad, HIP max pool, fused SGD kernel) vs plain PyTorch (every fusion off, MIOpen
   convs, eager BN, torch.optim.SGD): per-step losses agree within 3 % -- or within three times
   the run-to-run spread of plain PyTorch itself at that step (MIOpen's default kernels use
-  atomics; two identical plain runs already differ by ~1 % once the loss is below ~0.6) -- for
-  every step while the loss is above 0.1, at least 15 steps within 2 %, and both fall;
+  atomics; two identical plain runs already differ by ~1 % once the loss is below ~0.6; floor
+  0.01 nats) -- for every step while the loss is above 0.1, at least 15 steps within 2 %, and
+  both fall;
 * ps_async at N=1 with max_delay=0 (rank 0 = PS + worker) is bit-identical to mode='local'
   (8 steps with MIOpen's deterministic algorithms: its default ones use atomics);
 * free-running ps_async (GPU-time pull, one update of staleness per step) still trains the batch
@@ -45,8 +46,10 @@ def test_resnet50_fused_trains_like_plain_pytorch(tmp_path):
     for i, (u, v, v2) in enumerate(zip(a, b, b2)):
         if v < 0.1:
             break
-        # one fused and one plain sample against one plain-vs-plain spread: 3 % or 3x that spread
-        assert abs(u - v) <= max(0.03 * v, 3 * abs(v2 - v)), f"step {i}: fused {u:.4f} vs plain {v:.4f} / {v2:.4f}"
+        # one fused and one plain sample against one plain-vs-plain spread: 3 % or 3x that spread,
+        # and never less than 0.01 nats (near the 0.1 cut-off 3 % is 0.003)
+        tol = max(0.03 * v, 3 * abs(v2 - v), 0.01)
+        assert abs(u - v) <= tol, f"step {i}: fused {u:.4f} vs plain {v:.4f} / {v2:.4f}"
         checked += 1
         strict += abs(u - v) <= 0.02 * v
     assert checked >= 20 and strict >= 15
