@@ -9,16 +9,17 @@
 // single-workgroup histogram walks over all of it); everything else works on a short list:
 //   P1  per workgroup a contiguous range of 4096-element chunks ("region"): error-feedback fold
 //       r <- g + r, histogram of key bits 30..20 (key = |x| as bits), and an index-ordered list
-//       of every element with key >= spec_lo, where spec_lo is one radix bin below the
-//       threshold the previous call on this workspace found (the threshold of an error-feedback
-//       gradient moves little from step to step)                      [read g, r; write r]
+//       of every element with key >= spec_lo = 0.95 x the threshold the previous call on this
+//       workspace found (the threshold of an error-feedback gradient moves little from step to
+//       step)                                                           [read g, r; write r]
 //       A chunk whose entries do not fit the region's slot spills them to a shared pool
 //       (one atomic per spilled chunk, on one of 8 pool shards).
 //   pick   one workgroup: the bin B holding the k-th largest key
-//   P2  repair, only when bin B lies below spec_lo (first call, or the gradient shrank): every
-//       region re-reads its range and lists keys >= B's lower edge
 //   P3/P4  histograms of bits 19..9 and 8..0 over the listed keys of bin B + picks -> the exact
-//       k-th key T and how many keys == T to admit (lowest index first)
+//       k-th key T and how many keys == T to admit (lowest index first).  P3's pick first checks
+//       that the list reaches the k-th key (listed keys of B >= the number still needed);
+//   P2  only when it does not (first call, or the gradient shrank by > 5 %): every region
+//       re-reads its range and lists keys >= B's lower edge, and P3 is redone
 //   P5  per region: count the listed keys > T and == T, one workgroup scans the region counts,
 //       each region writes its selected (index, value) pairs at its prefix (list order = index
 //       order), clearing their residuals.
@@ -48,7 +49,7 @@ constexpr int kCompactPer = 16;                 // elements per lane per chunk (
 constexpr int kChunk = kBlock * kCompactPer;    // 4096 elements
 constexpr int kMaxRegions = 1024;               // workgroups of the region passes
 constexpr uint32_t kBinMask = 0x7ff00000u;      // key bits 30..20: the first radix digit
-constexpr uint32_t kSpecBins = 1;               // P1 lists keys down to this many bins below last T
+constexpr float kSpecMargin = 0.95f;            // P1 lists keys >= 0.95 x the previous call's threshold
 
 constexpr uint32_t kNoList = 0x80000000u;       // a bound no key reaches
 constexpr int kHistCopies = 8;
@@ -64,7 +65,8 @@ struct SelState {        // lives at the head of the workspace
   uint32_t full;         // a pool shard ran out: P3-P5 take full passes over the bucket
   uint32_t spec_lo;      // P1's list bound
   uint32_t prev_T;       // final key of the previous call (persists in the workspace)
-  uint32_t pad[24];
+  uint32_t redo;         // the list missed part of the k-th key's range: repair + recount
+  uint32_t pad[23];
   uint32_t pool_used[kPoolShards * 32];
   // kHistCopies histograms: workgroup b merges into copy b % kHistCopies, so a bin's global
   // atomics come from 1/8 of the workgroups (depth ~110 instead of ~900 on a 25 M bucket); the
@@ -74,8 +76,6 @@ struct SelState {        // lives at the head of the workspace
 
 __device__ __forceinline__ uint32_t absbits(float x) { return __float_as_uint(x) & 0x7fffffffu; }
 
-// topk: did P1's bound cover bin B?  (prefix's top digit is final after the first pick)
-__device__ __forceinline__ bool spec_covers(const SelState* st) { return (st->prefix & kBinMask) >= st->spec_lo; }
 
 // mode: 0 = top-k, 1 = threshold (prefix = T, no ties)
 __global__ __launch_bounds__(kBlock) void k_sel_init(SelState* __restrict__ st, uint32_t prefix, uint32_t mask,
@@ -83,10 +83,12 @@ __global__ __launch_bounds__(kBlock) void k_sel_init(SelState* __restrict__ st, 
   if (threadIdx.x == 0) {
     st->prefix = prefix; st->mask = mask; st->remaining = k; st->capw = capw;
     st->pool_cap = pool_cap; st->full = 0;
+    st->redo = 0;
     if (topk) {
-      const uint32_t b = (st->prev_T & 0x7fffffffu) >> 20;
-      // no usable previous threshold: P1 lists nothing, P2 lists from bin B's edge
-      st->spec_lo = b > kSpecBins ? (b - kSpecBins) << 20 : kNoList;
+      // no usable previous threshold (first call, or a zero / non-finite one): P1 lists nothing
+      // and the repair pass lists from bin B's edge
+      const float pt = __uint_as_float(st->prev_T & 0x7fffffffu);
+      st->spec_lo = (pt > 0.f && pt < __builtin_inff()) ? absbits(pt * kSpecMargin) : kNoList;
     } else {
       st->spec_lo = 0;
     }
@@ -270,7 +272,7 @@ __global__ __launch_bounds__(kBlock) void k_collect(const float* __restrict__ sr
                                                     int64_t n, SelState* __restrict__ st, Regions R, int mode) {
   __shared__ uint32_t h[HIST ? 4 : 1][HIST ? kHistBins : 1];
   __shared__ uint32_t wsum[4][4], sbase;
-  if (mode == 2 && spec_covers(st)) return;  // grid-uniform
+  if (mode == 2 && !st->redo) return;  // grid-uniform
   const int w = threadIdx.x >> 6;
   if (HIST) {
     for (int b = threadIdx.x; b < 4 * kHistBins; b += blockDim.x) (&h[0][0])[b] = 0;
@@ -398,10 +400,15 @@ struct FlatList {
 
 // One workgroup: find the bin holding the remaining-th largest key and descend one digit.
 // Thread t owns bins [nb - (t+1)*per, nb - t*per) (t = 0 the largest keys); a wave-shuffle scan
-// of the per-thread sums finds the owning thread in log steps.  The final digit records T for the
-// next call's speculative bound.
-__global__ __launch_bounds__(kBlock) void k_topk_pick(int lo, int nbits, SelState* __restrict__ st, int final_digit) {
+// of the per-thread sums finds the owning thread in log steps.  flags: kPickFinal records T for
+// the next call's speculative bound; kPickCheck (first digit over the list) verifies that the
+// listed keys of bin B reach down to the remaining-th one -- the list holds every key >= spec_lo,
+// so that holds iff their count >= remaining -- and otherwise raises redo (repair pass, fresh
+// pool) without descending; kPickRetry runs only after such a redo.
+constexpr int kPickFinal = 1, kPickCheck = 2, kPickRetry = 4;
+__global__ __launch_bounds__(kBlock) void k_topk_pick(int lo, int nbits, SelState* __restrict__ st, int flags) {
   __shared__ uint32_t wtot[4];
+  if ((flags & kPickRetry) && !st->redo) return;
   const int nb = 1 << nbits;
   const int per = nb / kBlock;  // 8 or 2
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -431,6 +438,17 @@ __global__ __launch_bounds__(kBlock) void k_topk_pick(int lo, int nbits, SelStat
   for (int b = t; b < nb; b += kBlock)  // re-arm for the next digit
 #pragma unroll
     for (int q = 0; q < kHistCopies; ++q) st->hist[q][b] = 0;
+  if (flags & kPickCheck) {
+    const uint32_t total = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+    if (total < need && !st->full) {  // (full mode counted every key of bin B)
+      if (t == 0) {
+        st->redo = 1;
+        st->full = 0;
+        for (int q = 0; q < kPoolShards; ++q) st->pool_used[q * 32] = 0;
+      }
+      return;
+    }
+  }
   if ((excl < need && need <= incl) || (t == kBlock - 1 && incl < need)) {
     uint32_t cum = excl;
     int bin = nb - t * per - 1;
@@ -445,18 +463,16 @@ __global__ __launch_bounds__(kBlock) void k_topk_pick(int lo, int nbits, SelStat
     st->prefix = prefix;
     st->mask |= (uint32_t)(nb - 1) << lo;
     st->remaining = need - cum;
-    if (final_digit) st->prev_T = prefix;
-    if (lo == 20 && (prefix & kBinMask) < st->spec_lo) {  // P2 will re-list everything: fresh pool
-      st->full = 0;
-      for (int s = 0; s < kPoolShards; ++s) st->pool_used[s * 32] = 0;
-    }
+    if (flags & kPickFinal) st->prev_T = prefix;
+    if (flags & kPickRetry) st->redo = 0;
   }
 }
 
 // P3/P4: histogram of the listed keys of the selected bin; full pass over the bucket if the pool ran out
 __global__ __launch_bounds__(kBlock) void k_hist_list(const float* __restrict__ src, int64_t n, int lo, int nbits,
-                                                      SelState* __restrict__ st, Regions R, int nreg) {
+                                                      SelState* __restrict__ st, Regions R, int nreg, int retry) {
   __shared__ uint32_t h[kHistBins];
+  if (retry && !st->redo) return;
   const int nb = 1 << nbits;
   for (int b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
   __syncthreads();
@@ -800,13 +816,16 @@ void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::T
   hipLaunchKernelGGL(k_collect<true>, nreg, kBlock, 0, stream, g.data_ptr<float>(), rp, n, w.st, w.R, 0);
   hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 20, 11, w.st, 0);
   const float* src = rp ? rp : g.data_ptr<float>();
-  // P2: only if P1's bound missed bin B, every region re-lists its range (returns at once otherwise)
+  // P3 over the listed keys of bin B; its pick checks that the list reaches the remaining-th key
+  hipLaunchKernelGGL(k_hist_list, nreg, kBlock, 0, stream, src, n, 9, 11, w.st, w.R, nreg, 0);
+  hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 9, 11, w.st, kPickCheck);
+  // only after a miss (first call, shrinking gradients): re-list from bin B's edge, P3 again
   hipLaunchKernelGGL(k_collect<false>, nreg, kBlock, 0, stream, src, (float*)nullptr, n, w.st, w.R, 2);
-  // P3/P4 on the listed keys of bin B
-  hipLaunchKernelGGL(k_hist_list, nreg, kBlock, 0, stream, src, n, 9, 11, w.st, w.R, nreg);
-  hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 9, 11, w.st, 0);
-  hipLaunchKernelGGL(k_hist_list, nreg, kBlock, 0, stream, src, n, 0, 9, w.st, w.R, nreg);
-  hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 0, 9, w.st, 1);
+  hipLaunchKernelGGL(k_hist_list, nreg, kBlock, 0, stream, src, n, 9, 11, w.st, w.R, nreg, 1);
+  hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 9, 11, w.st, kPickRetry);
+  // P4
+  hipLaunchKernelGGL(k_hist_list, nreg, kBlock, 0, stream, src, n, 0, 9, w.st, w.R, nreg, 0);
+  hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 0, 9, w.st, kPickFinal);
   // P5: region counts, scan, ordered write
   hipLaunchKernelGGL(k_count_list, nreg, kBlock, 0, stream, w.st, w.R);
   hipLaunchKernelGGL(k_count_full, nreg, kBlock, 0, stream, src, n, w.st, w.R);

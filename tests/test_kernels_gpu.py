@@ -197,8 +197,8 @@ def test_topk_candidate_overflow_and_ties(case):
 @pytest.mark.parametrize("vdt", [torch.float32, torch.bfloat16])
 def test_topk_repeated_calls_speculative_list(vdt):
     """One workspace across calls, as a codec keeps it per bucket: call 1 has no previous threshold
-    (P1 lists nothing, the repair pass lists bin B and up); later calls list from one radix bin
-    below the previous threshold (the single-pass path); a 10x smaller gradient drops the threshold below that bound (every region
+    (P1 lists nothing, the repair pass lists bin B and up); later calls list from 0.95 x the
+    previous threshold (the single-pass path); a 10x smaller gradient drops the threshold below that bound (every region
     repairs); a skewed bucket overflows a few regions' slots (shared pool); an all-equal bucket
     exhausts the pool (full-pass mode).  Every call must equal the CPU reference bit for bit,
     error-feedback residual included."""

@@ -20,7 +20,7 @@ xs = [torch.randn(n, device=dev) * 1e-2 for _ in range(4)]
 nchunks = (n + 4095) // 4096
 cpw = (nchunks + 1023) // 1024
 nreg = (nchunks + cpw - 1) // cpw
-SEL = (8 + 24 + 256 + 8 * 2048) * 4
+SEL = (8 + 24 + 256 + 8 * 2048) * 4  # prefix..prev_T, redo + pad, pool_used, hist copies
 for step in range(12):
     c.encode_into(xs[step % 4], views, st)
     torch.cuda.synchronize()
