@@ -56,11 +56,16 @@ void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
                      int64_t Wi, int64_t stride, c10::optional<at::Tensor> add, c10::optional<at::Tensor> add_mask,
                      c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_bits,
                      c10::optional<at::Tensor> bn_mean, c10::optional<at::Tensor> bn_invstd,
-                     c10::optional<at::Tensor> bn_scale, c10::optional<at::Tensor> bn_shift);
+                     c10::optional<at::Tensor> bn_scale, c10::optional<at::Tensor> bn_shift,
+                     c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift);
 // pool.hip
 void maxpool3s2_forward(at::Tensor x, at::Tensor y, at::Tensor code);
 void maxpool3s2_backward(at::Tensor dy, at::Tensor code, at::Tensor dx);
-void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64_t Wi, int64_t stride);
+void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64_t Wi, int64_t stride,
+                   c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift);
+void bn_forward_stats(at::Tensor x, at::Tensor weight, at::Tensor bias, c10::optional<at::Tensor> running_mean,
+                      c10::optional<at::Tensor> running_var, at::Tensor mean, at::Tensor invstd, at::Tensor scale,
+                      at::Tensor shift, int64_t C, double eps, double momentum);
 void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t KW, int64_t stride, int64_t pad);
 namespace rt {
 void pull_params(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, at::Tensor pub,
@@ -117,11 +122,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("add_mask") = pybind11::none(), pybind11::arg("bn_x") = pybind11::none(),
         pybind11::arg("bn_bits") = pybind11::none(), pybind11::arg("bn_mean") = pybind11::none(),
         pybind11::arg("bn_invstd") = pybind11::none(), pybind11::arg("bn_scale") = pybind11::none(),
-        pybind11::arg("bn_shift") = pybind11::none());
+        pybind11::arg("bn_shift") = pybind11::none(), pybind11::arg("pro_scale") = pybind11::none(),
+        pybind11::arg("pro_shift") = pybind11::none());
   m.def("conv_wgrad", &hipps::conv_wgrad, "MFMA KxK conv weight gradient (implicit GEMM, split-M, fp32 dW)");
   m.def("maxpool3s2_forward", &hipps::maxpool3s2_forward, "3x3/s2/p1 max pool, channels-last bf16, 4-bit tap codes");
   m.def("maxpool3s2_backward", &hipps::maxpool3s2_backward, "3x3/s2/p1 max pool backward (gather form, no atomics)");
-  m.def("conv1x1_wgrad", &hipps::conv1x1_wgrad, "MFMA 1x1 conv weight gradient (tr_b16 LDS reads, split-M)");
+  m.def("conv1x1_wgrad", &hipps::conv1x1_wgrad, "MFMA 1x1 conv weight gradient (tr_b16 LDS reads, split-M)",
+        pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("dw"), pybind11::arg("Hi"), pybind11::arg("Wi"),
+        pybind11::arg("stride"), pybind11::arg("pro_scale") = pybind11::none(),
+        pybind11::arg("pro_shift") = pybind11::none());
+  m.def("bn_forward_stats", &hipps::bn_forward_stats,
+        "training BatchNorm statistics only (reduce + finalize: mean, invstd, scale, shift, running stats); the "
+        "apply is left to a consumer's prologue");
   m.def("pull_params", &hipps::rt::pull_params,
         "GPU-time AsySG-InCon pull: select newest published version, copy it, release the reader word");
   m.def("pull_select", &hipps::rt::pull_select, "GPU-time pull, stage 1: choose the version, announce the reader");

@@ -65,13 +65,29 @@ struct BnBwdTap {
 __device__ const uint8_t kOnes[16] = {0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
                                       0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff};
 
-template <int BN, bool STATS, bool ADD, int BST = 0>  // BST: 0 off, 1 relu' from x, 2 relu' from bits
+// A-operand prologue: X is the INPUT of a training BatchNorm + ReLU whose output this conv
+// consumes; each staged 16-byte chunk (8 channels) becomes bf16(max(x * scale[c] + shift[c], 0))
+// -- the same rounding as the BN apply kernel -- so the BN output is never written to HBM.
+__device__ __forceinline__ u32x4 bn_relu8(u32x4 v, const float (&sc)[8], const float (&sh)[8]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float lo = fmaxf(fmaf(__uint_as_float(w[j] << 16), sc[2 * j], sh[2 * j]), 0.f);
+    const float hi = fmaxf(fmaf(__uint_as_float(w[j] & 0xffff0000u), sc[2 * j + 1], sh[2 * j + 1]), 0.f);
+    o[j] = pack_bf16x2(lo, hi);
+  }
+  return u32x4{o[0], o[1], o[2], o[3]};
+}
+
+template <int BN, bool STATS, bool ADD, int BST = 0, bool PRO = false>  // BST: 0 off, 1 relu' from x, 2 from bits
 __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W,
                                                     uint16_t* __restrict__ Y, float* __restrict__ pa,
                                                     float* __restrict__ pb, const uint16_t* __restrict__ R,
                                                     const uint8_t* __restrict__ RM, int M, int N, int K, int Ho,
                                                     int Wo, int Hi, int Wi, int stride, int mtiles, int ntiles,
-                                                    BnBwdTap bt) {
+                                                    BnBwdTap bt, const float* __restrict__ psc,
+                                                    const float* __restrict__ psh) {
   constexpr int WM = GemmCfg<BN>::WM, WN = GemmCfg<BN>::WN;
   constexpr int TM = kGBM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
@@ -115,6 +131,7 @@ __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__
   for (int i = 0; i < B_CH; ++i) b_off[i] = (int64_t)(n0 + (t >> 3) + 32 * i) * K + cchunk * 8;
 
   u32x4 ra[A_CH], rb[B_CH];
+  float psr[PRO ? 8 : 1], phr[PRO ? 8 : 1];  // prologue scale / shift of this thread's 8 channels
   // (macros, not lambdas: a by-reference lambda capture of these arrays put them in scratch)
 #define HIPPS_GLOAD(kt_)                                                        \
   {                                                                             \
@@ -125,13 +142,26 @@ __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__
     }                                                                           \
     _Pragma("unroll") for (int i = 0; i < B_CH; ++i) rb[i] =                    \
         *reinterpret_cast<const u32x4*>(W + b_off[i] + k0_);                    \
+    if constexpr (PRO) {                                                        \
+      const int c_ = k0_ + cchunk * 8; /* 32-byte aligned: four 16-byte loads */ \
+      const float4 s0_ = *reinterpret_cast<const float4*>(psc + c_);            \
+      const float4 s1_ = *reinterpret_cast<const float4*>(psc + c_ + 4);        \
+      const float4 h0_ = *reinterpret_cast<const float4*>(psh + c_);            \
+      const float4 h1_ = *reinterpret_cast<const float4*>(psh + c_ + 4);        \
+      psr[0] = s0_.x; psr[1] = s0_.y; psr[2] = s0_.z; psr[3] = s0_.w;           \
+      psr[4] = s1_.x; psr[5] = s1_.y; psr[6] = s1_.z; psr[7] = s1_.w;           \
+      phr[0] = h0_.x; phr[1] = h0_.y; phr[2] = h0_.z; phr[3] = h0_.w;           \
+      phr[4] = h1_.x; phr[5] = h1_.y; phr[6] = h1_.z; phr[7] = h1_.w;           \
+    }                                                                           \
   }
 #define HIPPS_SSTORE(s_)                                                                           \
   {                                                                                                \
     uint16_t* base_ = lds + (s_) * STAGE;                                                          \
     _Pragma("unroll") for (int i = 0; i < A_CH; ++i) {                                             \
       const int row_ = (t >> 3) + 32 * i;                                                          \
-      *reinterpret_cast<u32x4*>(base_ + row_ * kGBK + ((cchunk ^ (row_ & 7)) << 3)) = ra[i];       \
+      u32x4 v_ = ra[i];                                                                            \
+      if constexpr (PRO) v_ = a_ok[i] ? bn_relu8(v_, psr, phr) : u32x4{0u, 0u, 0u, 0u};          \
+      *reinterpret_cast<u32x4*>(base_ + row_ * kGBK + ((cchunk ^ (row_ & 7)) << 3)) = v_;         \
     }                                                                                              \
     _Pragma("unroll") for (int i = 0; i < B_CH; ++i) {                                             \
       const int row_ = (t >> 3) + 32 * i;                                                          \
@@ -555,11 +585,12 @@ __device__ __forceinline__ bf16x8 tr_frag_w(const uint8_t* tile, int row0, int c
 // order of a channels-last [Cout, Cin, KH, KW] weight): a K tile never straddles two taps
 // (Cin % TK == 0), so each block has ONE tap (r, s) and its X loader reads the input pixel
 // (ho*stride - pad + r, wo*stride - pad + s) of each output row m, zeros outside the image.
-template <int TN, int TK>
+template <int TN, int TK, bool PRO = false>
 __global__ __launch_bounds__(256) void k_conv1x1_wgrad2(const uint16_t* __restrict__ dY, const uint16_t* __restrict__ X,
                                                         float* __restrict__ part, int M, int N, int K, int Ho, int Wo,
                                                         int Hi, int Wi, int stride, int chunk, int tn, int tk, int Cin,
-                                                        int KW, int pad, FastDiv fd_hw, FastDiv fd_w) {
+                                                        int KW, int pad, FastDiv fd_hw, FastDiv fd_w,
+                                                        const float* __restrict__ psc, const float* __restrict__ psh) {
   constexpr int YCH = TN / 8, XCH = TK / 8;        // 16-byte chunks per staged row
   constexpr int YP = 64 * YCH / 256, XP = 64 * XCH / 256;  // chunks per thread per stage
   constexpr int YT = kWMS * TN * 2, XT = kWMS * TK * 2;  // bytes per staged tile
@@ -578,6 +609,14 @@ __global__ __launch_bounds__(256) void k_conv1x1_wgrad2(const uint16_t* __restri
 
   const int tap = k0 / Cin, c0 = k0 - tap * Cin;
   const int kr = tap / KW, kc = tap - (tap / KW) * KW;
+  float psr[PRO ? 8 : 1], phr[PRO ? 8 : 1];  // prologue (X = a BN input): this thread's 8 channels
+  if (PRO) {
+#pragma unroll
+    for (int j = 0; j < (PRO ? 8 : 1); ++j) {
+      psr[j] = psc[c0 + xch * 8 + j];
+      phr[j] = psh[c0 + xch * 8 + j];
+    }
+  }
   const bool direct = KW == 1 && pad == 0 && stride == 1 && Cin == K;  // plain 1x1: row m is pixel m
   u32x4 ry[YP], rx[XP];
   // element offset of (input pixel of output row m under this block's tap, channel c0); -1 = padding
@@ -600,7 +639,8 @@ __global__ __launch_bounds__(256) void k_conv1x1_wgrad2(const uint16_t* __restri
     _Pragma("unroll") for (int i = 0; i < XP; ++i) {                                               \
       const int m_ = (mb_) + t / XCH + (256 / XCH) * i;                                            \
       const int64_t so_ = m_ < mend ? src_off(m_) : -1;                                            \
-      const u32x4 v_ = *reinterpret_cast<const u32x4*>(X + (so_ < 0 ? 0 : so_) + xch * 8);         \
+      u32x4 v_ = *reinterpret_cast<const u32x4*>(X + (so_ < 0 ? 0 : so_) + xch * 8);               \
+      if constexpr (PRO) v_ = bn_relu8(v_, psr, phr);                                              \
       rx[i] = so_ >= 0 ? v_ : u32x4{0u, 0u, 0u, 0u};                                               \
     }                                                                                              \
   }
@@ -671,11 +711,14 @@ int64_t conv1x1_mtiles(int64_t M) { return (M + kGBM - 1) / kGBM; }
 // bn_x (optional, dgrad only): y is the complete gradient of a BatchNorm output whose input was
 // bn_x -- the epilogue then writes that BN backward's reduction partials into part (see BnBwdTap;
 // bn_bits = its ReLU bits, or none to recompute the mask from bn_x with bn_scale / bn_shift).
+// pro_scale / pro_shift (optional, forward with statistics): x is a BatchNorm INPUT, the conv
+// reads relu(x * scale + shift) per input channel (bn_relu8) -- the BN apply pass is skipped.
 void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part, int64_t Hi,
                      int64_t Wi, int64_t stride, c10::optional<at::Tensor> add, c10::optional<at::Tensor> add_mask,
                      c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_bits,
                      c10::optional<at::Tensor> bn_mean, c10::optional<at::Tensor> bn_invstd,
-                     c10::optional<at::Tensor> bn_scale, c10::optional<at::Tensor> bn_shift) {
+                     c10::optional<at::Tensor> bn_scale, c10::optional<at::Tensor> bn_shift,
+                     c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "conv1x1: device tensors");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
                   y.scalar_type() == at::kBFloat16, "conv1x1: bf16 tensors");
@@ -748,7 +791,7 @@ void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
 #define HIPPS_C1(BNv, ST, AD, BS)                                                                           \
   hipLaunchKernelGGL((k_conv1x1_nt<BNv, ST, AD, BS>), (int)nblk, 256, 0, stream, xp, wp, yp, pa, pb, rp, mp,     \
                      (int)M, (int)N, (int)K, (int)Ho, (int)Wo, (int)Hi, (int)Wi, (int)stride, (int)mtiles,        \
-                     (int)ntiles, bt)
+                     (int)ntiles, bt, (const float*)nullptr, (const float*)nullptr)
 #define HIPPS_C1_BN(BNv)                                                                                      \
   do {                                                                                                        \
     if (bst && bt.bits) {                                                                                     \
@@ -764,6 +807,23 @@ void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
     }                                                                                                         \
   } while (0)
   TORCH_CHECK(bst || !(pa && rp), "conv1x1: the forward statistics epilogue and the add epilogue are exclusive");
+  const bool pro = pro_scale.has_value() && pro_scale->defined();
+  if (pro) {
+    TORCH_CHECK(pro_shift.has_value() && pro_shift->defined(), "conv1x1: prologue needs scale and shift");
+    for (const c10::optional<at::Tensor>* v : {&pro_scale, &pro_shift})
+      TORCH_CHECK((*v)->is_cuda() && (*v)->scalar_type() == at::kFloat && (*v)->is_contiguous() && (*v)->numel() == K,
+                  "conv1x1: prologue vectors must be f32 [Cin]");
+    TORCH_CHECK(pa && !rp && !bst, "conv1x1: the BN-apply prologue runs with the statistics epilogue only");
+    const float* ps = pro_scale->data_ptr<float>();
+    const float* ph = pro_shift->data_ptr<float>();
+#define HIPPS_C1P(BNv)                                                                                        \
+  hipLaunchKernelGGL((k_conv1x1_nt<BNv, true, false, 0, true>), (int)nblk, 256, 0, stream, xp, wp, yp, pa, pb,  \
+                     rp, mp, (int)M, (int)N, (int)K, (int)Ho, (int)Wo, (int)Hi, (int)Wi, (int)stride,             \
+                     (int)mtiles, (int)ntiles, bt, ps, ph)
+    if (bn128) HIPPS_C1P(128); else HIPPS_C1P(64);
+#undef HIPPS_C1P
+    return;
+  }
   if (bn128) HIPPS_C1_BN(128); else HIPPS_C1_BN(64);
 #undef HIPPS_C1_BN
 #undef HIPPS_C1
@@ -773,7 +833,7 @@ void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
 // v2 weight gradient launcher: dW[N][K] (K = KH*KW*Cin) as S split-M partial slabs + fixed-order sum.
 static void launch_wgrad2(const at::Tensor& dy, const at::Tensor& x, at::Tensor& dw, int64_t M, int64_t N, int64_t K,
                           int64_t Cin, int64_t Ho, int64_t Wo, int64_t Hi, int64_t Wi, int64_t stride, int64_t KW,
-                          int64_t pad, hipStream_t stream0) {
+                          int64_t pad, hipStream_t stream0, const float* psc = nullptr, const float* psh = nullptr) {
   const int TN = N % 128 == 0 ? 128 : 64, TK = Cin % 128 == 0 ? 128 : 64;  // a K tile stays in one tap
   const int64_t tn = N / TN, tk = K / TK, tiles = tn * tk;
   // one wave of resident blocks: 256 CUs x (2 | 3 | 5) blocks per CU at (186 | 124 | 92) VGPRs
@@ -789,9 +849,18 @@ static void launch_wgrad2(const at::Tensor& dy, const at::Tensor& x, at::Tensor&
   const uint16_t* dyp = (const uint16_t*)dy.data_ptr();
   const uint16_t* xp = (const uint16_t*)x.data_ptr();
 #define HIPPS_W2(TNv, TKv)                                                                                    \
-  hipLaunchKernelGGL((k_conv1x1_wgrad2<TNv, TKv>), (int)(S * tiles), 256, 0, stream0, dyp, xp,               \
-                     part.data_ptr<float>(), (int)M, (int)N, (int)K, (int)Ho, (int)Wo, (int)Hi, (int)Wi,      \
-                     (int)stride, (int)chunk, (int)tn, (int)tk, (int)Cin, (int)KW, (int)pad, fd_hw, fd_w)
+  do {                                                                                                        \
+    if (psc)                                                                                                  \
+      hipLaunchKernelGGL((k_conv1x1_wgrad2<TNv, TKv, true>), (int)(S * tiles), 256, 0, stream0, dyp, xp,     \
+                         part.data_ptr<float>(), (int)M, (int)N, (int)K, (int)Ho, (int)Wo, (int)Hi, (int)Wi,  \
+                         (int)stride, (int)chunk, (int)tn, (int)tk, (int)Cin, (int)KW, (int)pad, fd_hw, fd_w, \
+                         psc, psh);                                                                           \
+    else                                                                                                      \
+      hipLaunchKernelGGL((k_conv1x1_wgrad2<TNv, TKv>), (int)(S * tiles), 256, 0, stream0, dyp, xp,           \
+                         part.data_ptr<float>(), (int)M, (int)N, (int)K, (int)Ho, (int)Wo, (int)Hi, (int)Wi,  \
+                         (int)stride, (int)chunk, (int)tn, (int)tk, (int)Cin, (int)KW, (int)pad, fd_hw, fd_w, \
+                         (const float*)nullptr, (const float*)nullptr);                                       \
+  } while (0)
   if (TN == 128 && TK == 128) HIPPS_W2(128, 128);
   else if (TN == 128) HIPPS_W2(128, 64);
   else if (TK == 128) HIPPS_W2(64, 128);
@@ -818,7 +887,9 @@ static void launch_wgrad2(const at::Tensor& dy, const at::Tensor& x, at::Tensor&
 
 // dy: [img, Cout, Ho, Wo] channels-last bf16; x: [img, Cin, Hi, Wi] channels-last bf16;
 // dw: f32 [Cout, Cin] (written, not accumulated).
-void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64_t Wi, int64_t stride) {
+// pro_scale / pro_shift (optional): x is a BatchNorm input; the GEMM reads relu(x * scale + shift).
+void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64_t Wi, int64_t stride,
+                   c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dw.is_cuda(), "conv1x1_wgrad: device tensors");
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 && dw.scalar_type() == at::kFloat,
               "conv1x1_wgrad: bf16 dy/x, f32 dw");
@@ -836,8 +907,18 @@ void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "conv1x1_wgrad: 16-byte aligned tensors");
   TORCH_CHECK(M < (int64_t(1) << 31), "conv1x1_wgrad: size");
   auto stream0 = c10::hip::getCurrentHIPStream();
+  const float *psc = nullptr, *psh = nullptr;
+  if (pro_scale.has_value() && pro_scale->defined()) {
+    TORCH_CHECK(pro_shift.has_value() && pro_shift->defined(), "conv1x1_wgrad: prologue needs scale and shift");
+    for (const c10::optional<at::Tensor>* v : {&pro_scale, &pro_shift})
+      TORCH_CHECK((*v)->is_cuda() && (*v)->scalar_type() == at::kFloat && (*v)->is_contiguous() && (*v)->numel() == K,
+                  "conv1x1_wgrad: prologue vectors must be f32 [Cin]");
+    TORCH_CHECK(N % 64 == 0 && K % 64 == 0, "conv1x1_wgrad: the prologue needs Cin, Cout % 64 == 0");
+    psc = pro_scale->data_ptr<float>();
+    psh = pro_shift->data_ptr<float>();
+  }
   if (N % 64 == 0 && K % 64 == 0) {  // v2: shape-fitted tiles, bounded split
-    launch_wgrad2(dy, x, dw, M, N, K, K, Ho, Wo, Hi, Wi, stride, 1, 0, stream0);
+    launch_wgrad2(dy, x, dw, M, N, K, K, Ho, Wo, Hi, Wi, stride, 1, 0, stream0, psc, psh);
     return;
   }
   const int64_t tn = (N + kWT - 1) / kWT, tk = (K + kWT - 1) / kWT, tiles = tn * tk;

@@ -400,6 +400,36 @@ void bn_forward_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y,
                      relu, stream);
 }
 
+// Statistics only (reduce + finalize): mean, invstd, scale, shift and the running stats, no apply
+// pass -- the consuming 1x1 conv applies scale/shift + ReLU in its operand prologue (gemm.hip).
+void bn_forward_stats(at::Tensor x, at::Tensor weight, at::Tensor bias, c10::optional<at::Tensor> running_mean,
+                      c10::optional<at::Tensor> running_var, at::Tensor mean, at::Tensor invstd, at::Tensor scale,
+                      at::Tensor shift, int64_t C, double eps, double momentum) {
+  TORCH_CHECK(C % 8 == 0 && C <= kMaxC && C >= 8, "fused BN needs C % 8 == 0 and 8 <= C <= 2048");
+  const int64_t M = x.numel() / C;
+  check_act(x, "x", M * C);
+  for (auto* t : {&weight, &bias, &mean, &invstd, &scale, &shift}) check_vec(*t, "per-channel vector", (int)C);
+  float* rm = nullptr;
+  float* rv = nullptr;
+  if (running_mean.has_value() && running_mean->defined()) {
+    check_vec(*running_mean, "running_mean", (int)C);
+    check_vec(*running_var, "running_var", (int)C);
+    rm = running_mean->data_ptr<float>();
+    rv = running_var->data_ptr<float>();
+  }
+  int nrb;
+  const int64_t rows = pick_rows(M, (int)C, nrb);
+  auto part = at::empty({2, C, (int64_t)nrb}, weight.options());
+  auto stream = c10::hip::getCurrentHIPStream();
+  hipLaunchKernelGGL((k_bn_reduce<false, MASK_NONE, 8>), nrb, kBlock, 0, stream, (const uint16_t*)x.data_ptr(),
+                     nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, (int)C, rows, nrb,
+                     part[0].data_ptr<float>(), part[1].data_ptr<float>());
+  hipLaunchKernelGGL(k_bn_finalize_fwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, part[0].data_ptr<float>(),
+                     part[1].data_ptr<float>(), nrb, (int)C, M, weight.data_ptr<float>(), bias.data_ptr<float>(),
+                     (float)eps, (float)momentum, rm, rv, mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                     scale.data_ptr<float>(), shift.data_ptr<float>());
+}
+
 // eval / affine-only apply with given scale/shift
 void bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, at::Tensor scale, at::Tensor shift, int64_t C,
               bool relu) {

@@ -14,7 +14,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from hipps.ops.nn import FusedBatchNorm2d, MaxPool2d, ResidualTap, conv2d, conv_bn
+from hipps.ops.nn import (FusedBatchNorm2d, MaxPool2d, ResidualTap, bn_relu_conv1x1_ok, bn_relu_conv_bn, conv2d,
+                          conv_bn)
 
 # One switch for the whole zoo: fused BN(+residual)(+ReLU) HIP kernels on channels-last bf16,
 # standard PyTorch elsewhere.  HIPPS_FUSED_BN=0 restores the eager MIOpen path for A/B runs.
@@ -31,6 +32,10 @@ _FUSED_POOL = _FUSED and _os.environ.get("HIPPS_FUSED_POOL", "1") != "0"
 _FUSED_BNGRAD = _os.environ.get("HIPPS_FUSED_BNGRAD", "1") != "0"
 # 3x3 convolutions: weight gradient on the hipps implicit-GEMM kernel (fwd / dgrad stay on MIOpen)
 _FUSED_WGRAD = _os.environ.get("HIPPS_FUSED_WGRAD", "1") != "0"
+# bn2 -> conv3: BN apply + ReLU in the 1x1 GEMM's operand prologue (the BN output is never written).
+# Opt-in: measured on ResNet-50 bs256 it removes 16 apply passes (-0.23 ms/step) but the prologue
+# GEMMs lose about as much (+0.10..0.17 ms/step), profiles/ab_r2/prologue_*.txt
+_FUSED_PRO = _FUSED_CONV and _os.environ.get("HIPPS_FUSED_PRO", "0") != "0"
 
 
 def _bn(c, relu=False):
@@ -77,7 +82,11 @@ class Bottleneck(nn.Module):
                 y, xa = conv_bn(self.conv1, self.bn1, x, fuse=_FUSED_CONV), x
             tap = None
             idt = conv_bn(ds[0], ds[1], xa, fuse=_FUSED_CONV)
-        y = self.bn2(conv2d(self.conv2, y, fuse=_FUSED_WGRAD))
+        y = conv2d(self.conv2, y, fuse=_FUSED_WGRAD)
+        if _FUSED_PRO and bn_relu_conv1x1_ok(self.bn2, self.conv3, y):
+            # bn2's apply happens in conv3's operand prologue: its output is never written
+            return bn_relu_conv_bn(self.bn2, self.conv3, self.bn3, y, residual=idt, res_tap=tap)
+        y = self.bn2(y)
         return conv_bn(self.conv3, self.bn3, y, residual=idt, fuse=_FUSED_CONV, res_tap=tap, bn_grad=bng)
 
 

@@ -191,6 +191,77 @@ class _Conv1x1(torch.autograd.Function):
         return dx, dw, None, None, None, None
 
 
+class _BNReluConv1x1(torch.autograd.Function):
+    """conv1x1(relu(bn(x))) for a training-mode BatchNorm whose output only feeds this stride-1
+    1x1 conv (ResNet bn2 -> conv3): the BN's statistics (reduce + finalize, no apply pass), then
+    the MFMA GEMM reading relu(x * scale + shift) in its operand prologue (gemm.hip bn_relu8; the
+    same bf16 rounding as the apply kernel), with the next BN's statistics in its epilogue.  The
+    BN output is never written or re-read.  Backward: the input-gradient GEMM with this BN's
+    backward reduction in its epilogue (relu' recomputed from x), the BN backward apply, and the
+    weight gradient with the same prologue on its X operand."""
+
+    @staticmethod
+    def forward(ctx, x, bn_w, bn_b, running_mean, running_var, eps, momentum, w_master):
+        w = bf16_weight(w_master)
+        ctx.wdtype = w_master.dtype
+        ctx.set_materialize_grads(False)
+        ctx.wt = _TSHADOWS.get(w_master.data_ptr()) if w_master.dtype == torch.float32 else None
+        n, c, h, wd = x.shape
+        cout = w.shape[0]
+        f32 = dict(dtype=torch.float32, device=x.device)
+        mean, invstd, scale, shift = (torch.empty(c, **f32) for _ in range(4))
+        native().bn_forward_stats(x, bn_w, bn_b, running_mean, running_var, mean, invstd, scale, shift, c, float(eps),
+                                  float(momentum))
+        y = torch.empty((n, cout, h, wd), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        part = torch.empty((2, cout, native().conv1x1_mtiles(n * h * wd)), **f32)
+        native().conv1x1_forward(x, w.reshape(cout, c), y, part, h, wd, 1, pro_scale=scale, pro_shift=shift)
+        ctx.save_for_backward(x, w, bn_w, mean, invstd, scale, shift)
+        ctx.mark_non_differentiable(part)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, dy, _dpart):
+        x, w, bn_w, mean, invstd, scale, shift = ctx.saved_tensors
+        if dy is None:
+            return (None,) * 8
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        n, c, h, wd = x.shape
+        cout = w.shape[0]
+        wt = ctx.wt if ctx.wt is not None else w.reshape(cout, c).t().contiguous()
+        # gradient of the (never materialised) BN output + that BN's backward reduction
+        dbn = torch.empty_like(x, memory_format=torch.channels_last)
+        part = torch.empty((2, c, native().conv1x1_mtiles(n * h * wd)), dtype=torch.float32, device=x.device)
+        native().conv1x1_forward(dy, wt, dbn, part, h, wd, 1, None, None, x, None, mean, invstd, scale, shift)
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dgw, dgb = torch.empty_like(bn_w), torch.empty_like(bn_w)
+        native().bn_backward_partials(part, part.shape[2], dbn, x, MASK_X, bn_w, mean, invstd, scale, shift, dx, None,
+                                      dgw, dgb, c, None)
+        dw = None
+        if ctx.needs_input_grad[7]:
+            dw = torch.empty(w.shape, dtype=torch.float32, device=w.device)
+            native().conv1x1_wgrad(dy, x, dw.view(cout, c), h, wd, 1, scale, shift)
+            if ctx.wdtype != torch.float32:
+                dw = dw.to(ctx.wdtype)
+        return dx, dgw, dgb, None, None, None, None, dw
+
+
+def bn_relu_conv1x1_ok(bn, conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    """Can _BNReluConv1x1 run conv(relu(bn(x)))?"""
+    return (bn.training and getattr(bn, "relu", False) and bn._fast_ok(x, None) and conv.stride == (1, 1)
+            and conv1x1_ok(conv, x) and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0)
+
+
+def bn_relu_conv_bn(bn, conv: nn.Conv2d, bn_next, x, residual=None, res_tap=None):
+    """bn_next(conv(relu(bn(x))), residual) with bn's apply folded into the conv's operand prologue
+    (_BNReluConv1x1); callers check bn_relu_conv1x1_ok first."""
+    bn._nbt_pending += 1
+    y, part = _BNReluConv1x1.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, bn.momentum,
+                                   conv.weight)
+    if bn_next._fast_ok(y, residual):
+        return bn_next(y, residual, stats=part, res_tap=res_tap)
+    return bn_next(y, residual)
+
+
 class _ConvKxK(torch.autograd.Function):
     """KxK convolution on channels-last bf16: forward and input gradient on MIOpen, weight
     gradient on the hipps implicit-GEMM MFMA kernel (conv_wgrad), written straight into an fp32

@@ -340,3 +340,70 @@ def test_kxk_dgrad_as_forward_matches_fp32(cin, cout, k):
     torch.testing.assert_close(x.grad.float() / scale, xr.grad / scale, rtol=0, atol=1e-2)
     scale = wr.grad.abs().max().item()
     torch.testing.assert_close(conv.weight.grad.float() / scale, wr.grad / scale, rtol=0, atol=1e-2)
+
+
+@pytest.mark.parametrize("cin,cout,hw", [(64, 256, 14), (128, 512, 7), (256, 1024, 7)])
+def test_bn_relu_prologue_matches_materialized(cin, cout, hw):
+    """conv1x1 forward / weight gradient reading relu(x * scale + shift) in the operand prologue
+    == the same GEMMs on the materialised bf16 BN output (the apply kernel rounds identically)."""
+    from hipps.ops._native import native
+
+    C = native()
+    torch.manual_seed(cin)
+    x = _cl(torch.randn(4, cin, hw, hw, device=DEV).to(torch.bfloat16))
+    scale = torch.rand(cin, device=DEV) + 0.5
+    shift = torch.randn(cin, device=DEV) * 0.5
+    w = torch.randn(cout, cin, device=DEV).to(torch.bfloat16) * 0.05
+    yref = torch.empty_like(x)
+    C.bn_apply(x, None, yref, scale, shift, cin, True)
+    M = 4 * hw * hw
+    mt = C.conv1x1_mtiles(M)
+    out_a = _cl(torch.empty(4, cout, hw, hw, device=DEV, dtype=torch.bfloat16))
+    out_b = torch.empty_like(out_a)
+    pa = torch.empty(2, cout, mt, device=DEV)
+    pb = torch.empty_like(pa)
+    C.conv1x1_forward(x, w, out_a, pa, hw, hw, 1, pro_scale=scale, pro_shift=shift)
+    C.conv1x1_forward(yref, w, out_b, pb, hw, hw, 1)
+    assert torch.equal(out_a, out_b) and torch.equal(pa, pb)
+    dy = _cl(torch.randn(4, cout, hw, hw, device=DEV).to(torch.bfloat16))
+    dwa = torch.empty(cout, cin, device=DEV)
+    dwb = torch.empty_like(dwa)
+    C.conv1x1_wgrad(dy, x, dwa, hw, hw, 1, scale, shift)
+    C.conv1x1_wgrad(dy, yref, dwb, hw, hw, 1)
+    assert torch.equal(dwa, dwb)
+
+
+def test_bottleneck_bn2_prologue_matches_apply_path():
+    """ResNet bottlenecks with bn2's apply in conv3's operand prologue vs the apply-kernel path:
+    forward output and every gradient agree (the prologue recomputes the same bf16 values)."""
+    import hipps.models.resnet as R
+
+    torch.manual_seed(5)
+    net = torch.nn.Sequential(R.Bottleneck(64, 64, stride=1, downsample=True), R.Bottleneck(256, 64),
+                              R.Bottleneck(256, 128, stride=2, downsample=True))
+    net = net.to(DEV).to(memory_format=torch.channels_last)
+    for blk in net:
+        torch.nn.init.uniform_(blk.bn3.weight, 0.5, 1.5)
+    x0 = _cl(torch.randn(8, 64, 14, 14, device=DEV).to(torch.bfloat16))
+    g = None
+    res = {}
+    for pro in (True, False):
+        R._FUSED_PRO = pro
+        try:
+            net.zero_grad(set_to_none=True)
+            for b in net.modules():
+                if isinstance(b, torch.nn.BatchNorm2d):
+                    b.reset_running_stats()
+            x = x0.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = net(x)
+            if g is None:
+                g = _cl(torch.randn(y.shape, device=DEV).to(torch.bfloat16))
+            y.backward(g)
+            res[pro] = [y.detach().float(), x.grad.float()] + [p.grad.float() for p in net.parameters()]
+            res[pro] += [b.running_mean.clone() for b in net.modules() if isinstance(b, torch.nn.BatchNorm2d)]
+        finally:
+            R._FUSED_PRO = False
+    for u, v in zip(res[True], res[False]):  # MIOpen's 3x3 kernels reduce with atomics: run-to-run noise
+        scale = v.abs().max().item() + 1e-6
+        torch.testing.assert_close(u / scale, v / scale, rtol=0, atol=2e-2)
