@@ -15,7 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from hipps.ops.nn import (FusedBatchNorm2d, MaxPool2d, ResidualTap, bn_relu_conv1x1_ok, bn_relu_conv_bn, conv2d,
-                          conv_bn)
+                          conv_bn, global_avg_pool)
 
 # One switch for the whole zoo: fused BN(+residual)(+ReLU) HIP kernels on channels-last bf16,
 # standard PyTorch elsewhere.  HIPPS_FUSED_BN=0 restores the eager MIOpen path for A/B runs.
@@ -147,7 +147,7 @@ class ResNet(nn.Module):
         x = self.maxpool(self.bn1(self.conv1(x)))
         for i in range(self.num_stages):
             x = getattr(self, f"layer{i + 1}")(x)
-        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        x = global_avg_pool(x)
         return self.fc(x)
 
 

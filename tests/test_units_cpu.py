@@ -100,3 +100,19 @@ def test_launcher_propagates_failure(tmp_path):
     r = subprocess.run([sys.executable, "-m", "hipps.launch", "-n", "2", str(bad)], capture_output=True, text=True,
                        timeout=60)
     assert r.returncode == 3
+
+
+def test_global_avg_pool_channels_last_backward():
+    """hipps' global average pool equals adaptive_avg_pool2d + flatten, and its input gradient
+    comes back NHWC-contiguous (the fused BatchNorm backward then needs no layout copy)."""
+    import torch
+
+    from hipps.ops.nn import global_avg_pool
+
+    x = torch.randn(3, 16, 5, 4).contiguous(memory_format=torch.channels_last).requires_grad_()
+    x2 = x.detach().clone().requires_grad_()
+    g = torch.randn(3, 16)
+    global_avg_pool(x).backward(g)
+    torch.flatten(torch.nn.functional.adaptive_avg_pool2d(x2, 1), 1).backward(g)
+    torch.testing.assert_close(x.grad, x2.grad)
+    assert x.grad.is_contiguous(memory_format=torch.channels_last)
