@@ -250,8 +250,10 @@ class MPI_PS(torch.optim.Optimizer):
         """ps_async with the GPU-time pull: copy the parameters of ``module`` and of everything
         after it in parameter order on a side stream, overlapped with the forward of the earlier
         layers; ``module``'s forward waits for them.  Use it only when no parameter from ``module``
-        on is read before ``module`` runs (ResNet: ``model.layer4``).  Returns False (no-op) in
-        other modes or when the module has no managed parameters."""
+        on is read before ``module`` runs (ResNet: ``model.layer4``).  Code that reads parameters
+        outside the model's forward (evaluation copies, logging) calls ``join_pull()`` first;
+        checkpoints and the next pull do.  Returns False (no-op) in other modes or when the module
+        has no managed parameters."""
         eng = self.engine
         if not hasattr(eng, "set_pull_overlap"):
             return False
@@ -259,6 +261,11 @@ class MPI_PS(torch.optim.Optimizer):
         if not offs:
             return False
         return eng.set_pull_overlap(min(offs), module)
+
+    def join_pull(self):
+        """Order the current stream after any parameter copy still in flight (split pull)."""
+        if hasattr(self.engine, "join_pull"):
+            self.engine.join_pull()
 
     def refresh_bf16_weights(self):
         """Re-cast the bf16 weight shadow after editing parameters outside ``step()``."""

@@ -39,6 +39,8 @@ def save(opt, path: str, model: Optional[torch.nn.Module] = None, extra: Optiona
     os.makedirs(path, exist_ok=True)
     eng = opt.engine
     rank = opt.world.rank
+    if hasattr(eng, "join_pull"):  # a split pull's late half may still be landing on a side stream
+        eng.join_pull()
     # async PS: the PS thread is held between messages for the whole snapshot, so the master,
     # the optimizer state, the pending accumulator and the version belong to one PS state
     quiesce = getattr(eng, "quiesced", None)
