@@ -67,6 +67,8 @@ void bn_forward_stats(at::Tensor x, at::Tensor weight, at::Tensor bias, c10::opt
                       c10::optional<at::Tensor> running_var, at::Tensor mean, at::Tensor invstd, at::Tensor scale,
                       at::Tensor shift, int64_t C, double eps, double momentum);
 void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t KW, int64_t stride, int64_t pad);
+void convkxk_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part, int64_t stride,
+                     int64_t pad);
 namespace rt {
 void pull_params(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, at::Tensor pub,
                  int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t ring_slot, int64_t tries);
@@ -124,6 +126,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("bn_invstd") = pybind11::none(), pybind11::arg("bn_scale") = pybind11::none(),
         pybind11::arg("bn_shift") = pybind11::none(), pybind11::arg("pro_scale") = pybind11::none(),
         pybind11::arg("pro_shift") = pybind11::none());
+  m.def("convkxk_forward", &hipps::convkxk_forward,
+        "MFMA KxK conv forward (implicit GEMM, channels-last bf16) with optional BN-statistics epilogue",
+        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("part") = pybind11::none(),
+        pybind11::arg("stride") = 1, pybind11::arg("pad") = 1);
   m.def("conv_wgrad", &hipps::conv_wgrad, "MFMA KxK conv weight gradient (implicit GEMM, split-M, fp32 dW)");
   m.def("maxpool3s2_forward", &hipps::maxpool3s2_forward, "3x3/s2/p1 max pool, channels-last bf16, 4-bit tap codes");
   m.def("maxpool3s2_backward", &hipps::maxpool3s2_backward, "3x3/s2/p1 max pool backward (gather form, no atomics)");

@@ -80,14 +80,22 @@ __device__ __forceinline__ u32x4 bn_relu8(u32x4 v, const float (&sc)[8], const f
   return u32x4{o[0], o[1], o[2], o[3]};
 }
 
-template <int BN, bool STATS, bool ADD, int BST = 0, bool PRO = false>  // BST: 0 off, 1 relu' from x, 2 from bits
+// KxK convolutions as implicit GEMM over K = KH*KW*Cin (k = (r*KW + s)*Cin + c, the physical order
+// of a channels-last [Cout, Cin, KH, KW] weight); a 64-deep K tile stays inside one tap (Cin % 64
+// == 0), so the A loader reads input pixel (ho*stride - pad + r, wo*stride - pad + s), zeros
+// outside the image.  KH = KW = 1, pad = 0 is the plain 1x1 path.
+struct ConvGeom {
+  int KW, pad, Cin;
+};
+
+template <int BN, bool STATS, bool ADD, int BST = 0, bool PRO = false, bool TAPS = false>
 __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W,
                                                     uint16_t* __restrict__ Y, float* __restrict__ pa,
                                                     float* __restrict__ pb, const uint16_t* __restrict__ R,
                                                     const uint8_t* __restrict__ RM, int M, int N, int K, int Ho,
                                                     int Wo, int Hi, int Wi, int stride, int mtiles, int ntiles,
                                                     BnBwdTap bt, const float* __restrict__ psc,
-                                                    const float* __restrict__ psh) {
+                                                    const float* __restrict__ psh, ConvGeom cg) {
   constexpr int WM = GemmCfg<BN>::WM, WN = GemmCfg<BN>::WN;
   constexpr int TM = kGBM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
@@ -111,6 +119,7 @@ __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__
   // per-thread A source rows (fixed over the K loop); rows past M load zeros
   int64_t a_off[A_CH];
   bool a_ok[A_CH];
+  int a_h[TAPS ? A_CH : 1], a_w[TAPS ? A_CH : 1];  // TAPS: top-left input pixel of the row's window
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) {
     const int row = (t >> 3) + 32 * i;
@@ -118,13 +127,19 @@ __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__
     a_ok[i] = m < M;
     m = a_ok[i] ? m : M - 1;
     int64_t src = m;
-    if (stride != 1) {
+    if (TAPS || stride != 1) {
       const int hw = Ho * Wo;
       const int img = m / hw, rem = m - img * hw;
       const int ho = rem / Wo, wo = rem - ho * Wo;
-      src = ((int64_t)img * Hi + (int64_t)ho * stride) * Wi + (int64_t)wo * stride;
+      if constexpr (TAPS) {
+        a_h[i] = ho * stride - cg.pad;
+        a_w[i] = wo * stride - cg.pad;
+        src = (int64_t)img * Hi * Wi;  // pixel index of the image's first pixel
+      } else {
+        src = ((int64_t)img * Hi + (int64_t)ho * stride) * Wi + (int64_t)wo * stride;
+      }
     }
-    a_off[i] = src * K + cchunk * 8;
+    a_off[i] = TAPS ? src : src * K + cchunk * 8;
   }
   int64_t b_off[B_CH];
 #pragma unroll
@@ -136,9 +151,21 @@ __global__ __launch_bounds__(256) void k_conv1x1_nt(const uint16_t* __restrict__
 #define HIPPS_GLOAD(kt_)                                                        \
   {                                                                             \
     const int k0_ = (kt_) * kGBK;                                               \
-    _Pragma("unroll") for (int i = 0; i < A_CH; ++i) {                          \
-      u32x4 v_ = *reinterpret_cast<const u32x4*>(X + a_off[i] + k0_);           \
-      ra[i] = a_ok[i] ? v_ : u32x4{0u, 0u, 0u, 0u};                             \
+    if constexpr (TAPS) {                                                       \
+      const int tap_ = k0_ / cg.Cin, c0_ = k0_ - tap_ * cg.Cin;                 \
+      const int r_ = tap_ / cg.KW, s_ = tap_ - r_ * cg.KW;                      \
+      _Pragma("unroll") for (int i = 0; i < A_CH; ++i) {                        \
+        const int hi_ = a_h[i] + r_, wi_ = a_w[i] + s_;                         \
+        const bool ok_ = a_ok[i] && hi_ >= 0 && hi_ < Hi && wi_ >= 0 && wi_ < Wi; \
+        const int64_t o_ = ok_ ? (a_off[i] + (int64_t)hi_ * Wi + wi_) * cg.Cin + c0_ + cchunk * 8 : 0; \
+        u32x4 v_ = *reinterpret_cast<const u32x4*>(X + o_);                     \
+        ra[i] = ok_ ? v_ : u32x4{0u, 0u, 0u, 0u};                               \
+      }                                                                         \
+    } else {                                                                    \
+      _Pragma("unroll") for (int i = 0; i < A_CH; ++i) {                        \
+        u32x4 v_ = *reinterpret_cast<const u32x4*>(X + a_off[i] + k0_);         \
+        ra[i] = a_ok[i] ? v_ : u32x4{0u, 0u, 0u, 0u};                           \
+      }                                                                         \
     }                                                                           \
     _Pragma("unroll") for (int i = 0; i < B_CH; ++i) rb[i] =                    \
         *reinterpret_cast<const u32x4*>(W + b_off[i] + k0_);                    \
@@ -791,7 +818,7 @@ void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
 #define HIPPS_C1(BNv, ST, AD, BS)                                                                           \
   hipLaunchKernelGGL((k_conv1x1_nt<BNv, ST, AD, BS>), (int)nblk, 256, 0, stream, xp, wp, yp, pa, pb, rp, mp,     \
                      (int)M, (int)N, (int)K, (int)Ho, (int)Wo, (int)Hi, (int)Wi, (int)stride, (int)mtiles,        \
-                     (int)ntiles, bt, (const float*)nullptr, (const float*)nullptr)
+                     (int)ntiles, bt, (const float*)nullptr, (const float*)nullptr, ConvGeom{1, 0, (int)K})
 #define HIPPS_C1_BN(BNv)                                                                                      \
   do {                                                                                                        \
     if (bst && bt.bits) {                                                                                     \
@@ -819,7 +846,7 @@ void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
 #define HIPPS_C1P(BNv)                                                                                        \
   hipLaunchKernelGGL((k_conv1x1_nt<BNv, true, false, 0, true>), (int)nblk, 256, 0, stream, xp, wp, yp, pa, pb,  \
                      rp, mp, (int)M, (int)N, (int)K, (int)Ho, (int)Wo, (int)Hi, (int)Wi, (int)stride,             \
-                     (int)mtiles, (int)ntiles, bt, ps, ph)
+                     (int)mtiles, (int)ntiles, bt, ps, ph, ConvGeom{1, 0, (int)K})
     if (bn128) HIPPS_C1P(128); else HIPPS_C1P(64);
 #undef HIPPS_C1P
     return;
@@ -829,6 +856,59 @@ void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
 #undef HIPPS_C1
 }
 
+
+// KxK convolution forward (stride, symmetric zero padding) as the implicit-GEMM variant of the
+// 1x1 MFMA kernel: x [img, Cin, Hi, Wi], w [Cout, Cin, KH, KW], y [img, Cout, Ho, Wo], all
+// channels-last bf16; Cin % 64 == 0, Cout % 64 == 0.  part (optional): the following BatchNorm's
+// per-channel partial statistics f32 [2, Cout, mtiles] from the epilogue.
+void convkxk_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part, int64_t stride,
+                     int64_t pad) {
+  TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "convkxk: device tensors");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
+                  y.scalar_type() == at::kBFloat16, "convkxk: bf16 tensors");
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && y.dim() == 4, "convkxk: 4-d tensors");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  y.is_contiguous(at::MemoryFormat::ChannelsLast), "convkxk: channels-last x, w, y");
+  const int64_t imgs = x.size(0), Cin = x.size(1), Hi = x.size(2), Wi = x.size(3);
+  const int64_t N = w.size(0), KH = w.size(2), KW = w.size(3);
+  TORCH_CHECK(w.size(1) == Cin, "convkxk: weight Cin");
+  TORCH_CHECK(Cin % kGBK == 0 && N % 64 == 0, "convkxk: needs Cin % 64 == 0 and Cout % 64 == 0");
+  TORCH_CHECK(stride >= 1 && pad >= 0, "convkxk: geometry");
+  const int64_t Ho = (Hi + 2 * pad - KH) / stride + 1, Wo = (Wi + 2 * pad - KW) / stride + 1;
+  TORCH_CHECK(y.size(0) == imgs && y.size(1) == N && y.size(2) == Ho && y.size(3) == Wo, "convkxk: y shape");
+  for (const at::Tensor* t : {&x, &w, &y})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "convkxk: 16-byte aligned tensors");
+  const int64_t M = imgs * Ho * Wo, K = KH * KW * Cin;
+  TORCH_CHECK(M < (int64_t(1) << 31) && x.numel() < (int64_t(1) << 40), "convkxk: size");
+  const int64_t mtiles = conv1x1_mtiles(M);
+  const bool bn128 = N % 128 == 0;
+  const int64_t ntiles = N / (bn128 ? 128 : 64);
+  const int64_t nblk = mtiles * ntiles;
+  float *pa = nullptr, *pb = nullptr;
+  if (part.has_value() && part->defined()) {
+    TORCH_CHECK(part->is_cuda() && part->scalar_type() == at::kFloat && part->is_contiguous() &&
+                    part->numel() == 2 * N * mtiles, "convkxk: part must be f32 [2, Cout, mtiles]");
+    pa = part->data_ptr<float>();
+    pb = pa + N * mtiles;
+  }
+  auto stream = c10::hip::getCurrentHIPStream();
+  const uint16_t* xp = (const uint16_t*)x.data_ptr();
+  const uint16_t* wp = (const uint16_t*)w.data_ptr();
+  uint16_t* yp = (uint16_t*)y.data_ptr();
+  const ConvGeom cg{(int)KW, (int)pad, (int)Cin};
+  BnBwdTap bt{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+#define HIPPS_CK(BNv, ST)                                                                                        \
+  hipLaunchKernelGGL((k_conv1x1_nt<BNv, ST, false, 0, false, true>), (int)nblk, 256, 0, stream, xp, wp, yp, pa, pb, \
+                     (const uint16_t*)nullptr, (const uint8_t*)nullptr, (int)M, (int)N, (int)K, (int)Ho, (int)Wo,     \
+                     (int)Hi, (int)Wi, (int)stride, (int)mtiles, (int)ntiles, bt, (const float*)nullptr,            \
+                     (const float*)nullptr, cg)
+  if (bn128) {
+    if (pa) HIPPS_CK(128, true); else HIPPS_CK(128, false);
+  } else {
+    if (pa) HIPPS_CK(64, true); else HIPPS_CK(64, false);
+  }
+#undef HIPPS_CK
+}
 
 // v2 weight gradient launcher: dW[N][K] (K = KH*KW*Cin) as S split-M partial slabs + fixed-order sum.
 static void launch_wgrad2(const at::Tensor& dy, const at::Tensor& x, at::Tensor& dw, int64_t M, int64_t N, int64_t K,

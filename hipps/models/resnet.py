@@ -15,7 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from hipps.ops.nn import (FusedBatchNorm2d, MaxPool2d, ResidualTap, bn_relu_conv1x1_ok, bn_relu_conv_bn, conv2d,
-                          conv_bn, global_avg_pool)
+                          conv2d_bn, conv_bn, global_avg_pool)
 
 # One switch for the whole zoo: fused BN(+residual)(+ReLU) HIP kernels on channels-last bf16,
 # standard PyTorch elsewhere.  HIPPS_FUSED_BN=0 restores the eager MIOpen path for A/B runs.
@@ -82,11 +82,14 @@ class Bottleneck(nn.Module):
                 y, xa = conv_bn(self.conv1, self.bn1, x, fuse=_FUSED_CONV), x
             tap = None
             idt = conv_bn(ds[0], ds[1], xa, fuse=_FUSED_CONV)
-        y = conv2d(self.conv2, y, fuse=_FUSED_WGRAD)
-        if _FUSED_PRO and bn_relu_conv1x1_ok(self.bn2, self.conv3, y):
-            # bn2's apply happens in conv3's operand prologue: its output is never written
-            return bn_relu_conv_bn(self.bn2, self.conv3, self.bn3, y, residual=idt, res_tap=tap)
-        y = self.bn2(y)
+        if _FUSED_PRO:
+            y = conv2d(self.conv2, y, fuse=_FUSED_WGRAD)
+            if bn_relu_conv1x1_ok(self.bn2, self.conv3, y):
+                # bn2's apply happens in conv3's operand prologue: its output is never written
+                return bn_relu_conv_bn(self.bn2, self.conv3, self.bn3, y, residual=idt, res_tap=tap)
+            y = self.bn2(y)
+        else:
+            y = conv2d_bn(self.conv2, self.bn2, y, fuse=_FUSED_WGRAD)
         return conv_bn(self.conv3, self.bn3, y, residual=idt, fuse=_FUSED_CONV, res_tap=tap, bn_grad=bng)
 
 
@@ -105,8 +108,8 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        y = self.bn1(conv2d(self.conv1, x, fuse=_FUSED_WGRAD))
-        return self.bn2(conv2d(self.conv2, y, fuse=_FUSED_WGRAD), residual=idt)
+        y = conv2d_bn(self.conv1, self.bn1, x, fuse=_FUSED_WGRAD)
+        return conv2d_bn(self.conv2, self.bn2, y, residual=idt, fuse=_FUSED_WGRAD)
 
 
 class ResNet(nn.Module):

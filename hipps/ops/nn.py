@@ -27,6 +27,12 @@ _OWN_WGRAD = _os.environ.get("HIPPS_CONV_WGRAD", "1") != "0"
 # weight: MIOpen's backward-data solvers zero-fill dx first (SubTensorOpWithScalar1d, ~0.47 ms per
 # ResNet-50 step) and run slower than its forward kernels on the same shapes
 _DGRAD_AS_FWD = _os.environ.get("HIPPS_DGRAD_FWD", "1") != "0"
+# KxK forward (and the stride-1 input gradient run as a forward conv) on hipps' implicit-GEMM MFMA
+# kernel, with the following BN's statistics in its epilogue, instead of MIOpen/CK.  Opt-in: it
+# beats MIOpen's immediate-mode choice on every ResNet-50 3x3 shape, but not the kernels MIOpen's
+# Find picks under cudnn.benchmark (bench A/B: 25.26 vs 24.90 ms of kernels per step,
+# profiles/ab_r2/own_kxk_*)
+_OWN_KXK_FWD = _os.environ.get("HIPPS_OWN_KXK", "0") != "0"
 
 MASK_NONE, MASK_X, MASK_Y, MASK_BITS = 0, 1, 2, 3
 
@@ -269,20 +275,38 @@ class _ConvKxK(torch.autograd.Function):
     fp32 workspace and need 3 extra zero-fill / cast kernels per call (profiles/bench_n1_steady_r1d.txt)."""
 
     @staticmethod
-    def forward(ctx, x, w_master, stride, pad, own_wgrad=True):
+    def forward(ctx, x, w_master, stride, pad, own_wgrad=True, stats=False):
         w = bf16_weight(w_master)
         ctx.wdtype = w_master.dtype
         ctx.own_wgrad = own_wgrad
+        ctx.set_materialize_grads(False)
         ctx.wf = _TSHADOWS.get(w_master.data_ptr()) if w_master.dtype == torch.float32 else None
-        y = torch.ops.aten.convolution(x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1)
+        part = None
+        if _own_kxk(x.shape[1], w.shape[0]):
+            n, _, h, wd = x.shape
+            k = w.shape[2]
+            ho, wo = (h + 2 * pad - k) // stride + 1, (wd + 2 * pad - k) // stride + 1
+            y = torch.empty((n, w.shape[0], ho, wo), dtype=torch.bfloat16, device=x.device,
+                            memory_format=torch.channels_last)
+            if stats:  # the following BatchNorm's statistics from the GEMM epilogue
+                part = torch.empty((2, w.shape[0], native().conv1x1_mtiles(n * ho * wo)), dtype=torch.float32,
+                                   device=x.device)
+            native().convkxk_forward(x, w, y, part, stride, pad)
+        else:
+            y = torch.ops.aten.convolution(x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1)
         ctx.geom = (stride, pad)
         ctx.save_for_backward(x, w)
-        return y
+        if part is None:
+            part = torch.empty(0, device=x.device)
+        ctx.mark_non_differentiable(part)
+        return y, part
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, _dpart=None):
         x, w = ctx.saved_tensors
         s, p = ctx.geom
+        if dy is None:
+            return None, None, None, None, None, None
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = None
         k = w.shape[2]
@@ -291,7 +315,11 @@ class _ConvKxK(torch.autograd.Function):
             wf = ctx.wf if ctx.wf is not None and ctx.wf.dim() == 4 else None
             if wf is None:
                 wf = torch.flip(w, (2, 3)).transpose(0, 1).contiguous(memory_format=torch.channels_last)
-            dx = torch.ops.aten.convolution(dy, wf, None, [1, 1], [p, p], [1, 1], False, [0, 0], 1)
+            if _own_kxk(dy.shape[1], wf.shape[0]):
+                dx = torch.empty_like(x, memory_format=torch.channels_last)
+                native().convkxk_forward(dy, wf, dx, None, 1, p)
+            else:
+                dx = torch.ops.aten.convolution(dy, wf, None, [1, 1], [p, p], [1, 1], False, [0, 0], 1)
         elif ctx.needs_input_grad[0]:
             dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
                                                      [True, False, False])[0]
@@ -303,7 +331,12 @@ class _ConvKxK(torch.autograd.Function):
             native().conv_wgrad(dy, x, dw, w.shape[2], w.shape[3], s, p)
             if ctx.wdtype != torch.float32:
                 dw = dw.to(ctx.wdtype)
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
+
+
+def _own_kxk(cin: int, cout: int) -> bool:
+    """Route this KxK forward to hipps' implicit-GEMM kernel (gemm.hip convkxk_forward)?"""
+    return _OWN_KXK_FWD and cin % 64 == 0 and cout % 64 == 0
 
 
 def convkxk_ok(conv: nn.Conv2d, x: torch.Tensor, own_wgrad: bool = True) -> bool:
@@ -326,13 +359,31 @@ def convkxk_ok(conv: nn.Conv2d, x: torch.Tensor, own_wgrad: bool = True) -> bool
             w.is_contiguous(memory_format=torch.channels_last))
 
 
-def conv2d(conv: nn.Conv2d, x: torch.Tensor, fuse: bool = True) -> torch.Tensor:
-    """conv(x) with the hipps weight gradient when eligible (see _ConvKxK); otherwise conv(x)."""
+def conv2d_stats(conv: nn.Conv2d, x: torch.Tensor, fuse: bool = True):
+    """(conv(x), part): with the hipps implicit-GEMM forward, ``part`` holds the following
+    BatchNorm's partial statistics [2, Cout, m_tiles] from its epilogue (None otherwise); the
+    hipps weight gradient when eligible (see _ConvKxK)."""
     if fuse and conv.training and convkxk_ok(conv, x):
-        return _ConvKxK.apply(x, conv.weight, conv.stride[0], conv.padding[0])
-    if _DGRAD_AS_FWD and conv.training and convkxk_ok(conv, x, own_wgrad=False) and conv.stride[0] == 1:
-        return _ConvKxK.apply(x, conv.weight, 1, conv.padding[0], False)  # MIOpen weight gradient
-    return conv(x)
+        y, part = _ConvKxK.apply(x, conv.weight, conv.stride[0], conv.padding[0], True, True)
+        return y, (part if part.numel() else None)
+    if conv.training and convkxk_ok(conv, x, own_wgrad=False) and (
+            (_DGRAD_AS_FWD and conv.stride[0] == 1) or _own_kxk(conv.in_channels, conv.out_channels)):
+        y, part = _ConvKxK.apply(x, conv.weight, conv.stride[0], conv.padding[0], False, True)  # MIOpen wgrad
+        return y, (part if part.numel() else None)
+    return conv(x), None
+
+
+def conv2d(conv: nn.Conv2d, x: torch.Tensor, fuse: bool = True) -> torch.Tensor:
+    """conv(x) with the hipps kernels when eligible (see _ConvKxK); otherwise conv(x)."""
+    return conv2d_stats(conv, x, fuse)[0]
+
+
+def conv2d_bn(conv: nn.Conv2d, bn, x: torch.Tensor, residual=None, fuse: bool = True):
+    """bn(conv(x), residual) with the BN statistics from the conv's GEMM epilogue when available."""
+    y, part = conv2d_stats(conv, x, fuse)
+    if part is not None and bn.training and bn._fast_ok(y, residual):
+        return bn(y, residual, stats=part)
+    return bn(y, residual)
 
 
 def _masked(t, mask, C):

@@ -177,10 +177,11 @@ def _resnet_run(R, m, x, fused, bf16=True):
     3x3 input gradient as a forward conv, fused BN, stem max pool."""
     import hipps.ops.nn as N
 
-    saved = (R._FUSED_CONV, R._FUSED_GRAD, R._FUSED_BNGRAD, R._FUSED_WGRAD, N._OWN_WGRAD, N._DGRAD_AS_FWD)
+    saved = (R._FUSED_CONV, R._FUSED_GRAD, R._FUSED_BNGRAD, R._FUSED_WGRAD, N._OWN_WGRAD, N._DGRAD_AS_FWD,
+             N._OWN_KXK_FWD)
     bns = [mod for mod in m.modules() if isinstance(mod, N.FusedBatchNorm2d)]
     R._FUSED_CONV = R._FUSED_GRAD = R._FUSED_BNGRAD = R._FUSED_WGRAD = fused
-    N._OWN_WGRAD = N._DGRAD_AS_FWD = fused
+    N._OWN_WGRAD = N._DGRAD_AS_FWD = N._OWN_KXK_FWD = fused
     m.maxpool.fused = fused
     for bn in bns:
         bn.fused = fused
@@ -190,7 +191,8 @@ def _resnet_run(R, m, x, fused, bf16=True):
             y = m(x)
         y.float().sum().backward()
     finally:
-        R._FUSED_CONV, R._FUSED_GRAD, R._FUSED_BNGRAD, R._FUSED_WGRAD, N._OWN_WGRAD, N._DGRAD_AS_FWD = saved
+        (R._FUSED_CONV, R._FUSED_GRAD, R._FUSED_BNGRAD, R._FUSED_WGRAD, N._OWN_WGRAD, N._DGRAD_AS_FWD,
+         N._OWN_KXK_FWD) = saved
         m.maxpool.fused = True
         for bn in bns:
             bn.fused = True
@@ -407,3 +409,24 @@ def test_bottleneck_bn2_prologue_matches_apply_path():
     for u, v in zip(res[True], res[False]):  # MIOpen's 3x3 kernels reduce with atomics: run-to-run noise
         scale = v.abs().max().item() + 1e-6
         torch.testing.assert_close(u / scale, v / scale, rtol=0, atol=2e-2)
+
+
+@pytest.mark.parametrize("c,h,stride,k", [(64, 20, 1, 3), (128, 15, 2, 3), (256, 9, 1, 3), (64, 11, 1, 5),
+                                          (128, 8, 2, 1)])
+def test_convkxk_forward_matches_fp32(c, h, stride, k):
+    """hipps implicit-GEMM KxK forward (taps, zero padding, stride) + BN-statistics epilogue vs an
+    fp32 convolution of the same bf16 operands."""
+    from hipps.ops._native import native
+
+    torch.manual_seed(c + h)
+    n, cout, pad = 3, 2 * c, k // 2
+    x = _cl(torch.randn(n, c, h, h, device=DEV).to(torch.bfloat16))
+    w = _cl((torch.randn(cout, c, k, k, device=DEV) / (k * c ** 0.5)).to(torch.bfloat16))
+    ref = torch.nn.functional.conv2d(x.float(), w.float(), stride=stride, padding=pad)
+    y = _cl(torch.empty(ref.shape, device=DEV, dtype=torch.bfloat16))
+    part = torch.empty(2, cout, native().conv1x1_mtiles(n * ref.shape[2] * ref.shape[3]), device=DEV)
+    native().convkxk_forward(x, w, y, part, stride, pad)
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+    yf = y.float()
+    torch.testing.assert_close(part[0].sum(1), yf.sum((0, 2, 3)), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(part[1].sum(1), (yf * yf).sum((0, 2, 3)), rtol=1e-4, atol=1e-3)

@@ -26,7 +26,8 @@ import sys
 import time
 
 PLAIN_ENV = {"HIPPS_FUSED_BN": "0", "HIPPS_FUSED_CONV": "0", "HIPPS_FUSED_GRAD": "0", "HIPPS_FUSED_POOL": "0",
-             "HIPPS_FUSED_BNGRAD": "0", "HIPPS_FUSED_WGRAD": "0", "HIPPS_CONV_WGRAD": "0", "HIPPS_DGRAD_FWD": "0"}
+             "HIPPS_FUSED_BNGRAD": "0", "HIPPS_FUSED_WGRAD": "0", "HIPPS_CONV_WGRAD": "0", "HIPPS_DGRAD_FWD": "0",
+             "HIPPS_OWN_KXK": "0", "HIPPS_FUSED_PRO": "0"}
 
 
 def parse(argv=None):
