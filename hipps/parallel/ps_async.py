@@ -936,6 +936,10 @@ class PSAsyncEngine(Engine):
         self._closed = True
         super().close()
         C = self.C
+        if self._late_hook is not None:  # the model outlives the engine: drop the pull-overlap hook
+            self._late_hook.remove()
+            self._late_hook = None
+        self._late_ev = None
         try:
             if self.cuda:
                 torch.cuda.synchronize(self.store.device)

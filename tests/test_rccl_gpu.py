@@ -91,3 +91,20 @@ def test_sync_engine_on_native_rccl_matches_local(mode):
         res.append([p.detach().clone() for p in m.parameters()])
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_comm_bench_single_rank(tmp_path):
+    """bench/comm_bench.py at N = 1 (one-rank RCCL group, IPC mailbox, pull kernel) runs and
+    reports every row."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "comm.json"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench", "comm_bench.py"), "--sizes-mb", "1,4", "--iters",
+                        "3", "--out", str(out)], cwd=root, capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0, r.stderr[-3000:]
+    ops = {row["op"] for row in json.load(open(out))}
+    assert {"torch.all_gather", "torch.broadcast", "ipc.push", "ipc.pull_kernel", "local.copy"} <= ops
