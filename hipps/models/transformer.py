@@ -21,6 +21,17 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 
+def _ln(mod: nn.LayerNorm, x: torch.Tensor) -> torch.Tensor:
+    """LayerNorm on the autocast dtype: PyTorch's kernel reads bf16, computes in fp32 and writes
+    bf16, where autocast's fp32 policy for layer_norm would cast the activation up, write fp32 and
+    cast it back down for the next GEMM (two extra passes per norm, fp32 residual adds)."""
+    if x.is_cuda and torch.is_autocast_enabled():
+        dt = torch.get_autocast_dtype("cuda")
+        with torch.autocast("cuda", enabled=False):
+            return F.layer_norm(x.to(dt), mod.normalized_shape, mod.weight.to(dt), mod.bias.to(dt), mod.eps)
+    return mod(x)
+
+
 # ------------------------------------------------------------------------------------- BERT
 @dataclass
 class BertConfig:
@@ -56,8 +67,8 @@ class BertLayer(nn.Module):
 
         a = F.scaled_dot_product_attention(split(self.q(x)), split(self.k(x)), split(self.v(x)), attn_mask=mask)
         a = a.transpose(1, 2).reshape(B, S, D)
-        x = self.attn_ln(x + self.attn_out(a))
-        return self.out_ln(x + self.out(F.gelu(self.inter(x))))
+        x = _ln(self.attn_ln, x + self.attn_out(a))
+        return _ln(self.out_ln, x + self.out(F.gelu(self.inter(x))))
 
 
 class Bert(nn.Module):
@@ -88,13 +99,13 @@ class Bert(nn.Module):
         B, S = ids.shape
         pos = torch.arange(S, device=ids.device)
         x = self.word(ids) + self.pos(pos)[None] + self.tok_type(torch.zeros_like(ids))
-        x = self.emb_ln(x)
+        x = _ln(self.emb_ln, x)
         for layer in self.layers:
             x = layer(x)
         pooled = torch.tanh(self.pooler(x[:, 0]))
         if not self.mlm:
             return x, pooled
-        h = self.mlm_ln(F.gelu(self.mlm_dense(x)))
+        h = _ln(self.mlm_ln, F.gelu(self.mlm_dense(x)))
         logits = F.linear(h, self.word.weight, self.mlm_bias)  # tied decoder
         if labels is None:
             return logits
