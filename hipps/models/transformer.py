@@ -133,6 +133,12 @@ class RMSNorm(nn.Module):
         self.eps = eps
 
     def forward(self, x):
+        if x.is_cuda:
+            # one fused kernel (aten._fused_rms_norm, fp32 math) on the activation dtype instead of
+            # six eager ops over an fp32 copy
+            dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled() else x.dtype
+            with torch.autocast("cuda", enabled=False):
+                return F.rms_norm(x.to(dt), (x.shape[-1],), self.weight.to(dt), self.eps)
         xf = x.float()
         return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.eps)).to(x.dtype) * self.weight.to(x.dtype)
 
