@@ -2,8 +2,8 @@
 # Secondary BASELINE configs + codec microbenchmark on one MI355X.
 set -o pipefail
 mkdir -p gpurun_out/cfg
-timeout -k 10 300 python bench/codec_bench.py --out gpurun_out/cfg/codec_bench.json > gpurun_out/cfg/codec_bench.log 2>&1 || { echo "codec bench failed"; tail -20 gpurun_out/cfg/codec_bench.log; exit 1; }
-echo "codec bench ok"
+[ -n "$WITH_CODEC" ] && { timeout -k 10 300 python bench/codec_bench.py --out gpurun_out/cfg/codec_bench.json > gpurun_out/cfg/codec_bench.log 2>&1 || exit 1; }
+
 run() { name=$1; shift; timeout -k 10 420 python bench.py "$@" --out gpurun_out/cfg/$name.json > gpurun_out/cfg/$name.log 2>&1; rc=$?; echo "$name rc=$rc"; [ -f gpurun_out/cfg/$name.json ] && cat gpurun_out/cfg/$name.json; return $rc; }
 run r50_topk_int8 --codec topk_int8:0.01 --steps 15 --warmup 5 || exit 1
 run r50_int8 --codec int8 --steps 15 --warmup 5 || exit 1
