@@ -69,6 +69,10 @@ void bn_forward_stats(at::Tensor x, at::Tensor weight, at::Tensor bias, c10::opt
 void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t KW, int64_t stride, int64_t pad);
 void convkxk_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part, int64_t stride,
                      int64_t pad);
+// stem.hip
+int64_t stem_mtiles(int64_t imgs, int64_t Ho);
+void stem_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part);
+void stem_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw);
 namespace rt {
 void pull_params(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, at::Tensor pub,
                  int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t ring_slot, int64_t tries);
@@ -130,6 +134,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "MFMA KxK conv forward (implicit GEMM, channels-last bf16) with optional BN-statistics epilogue",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("part") = pybind11::none(),
         pybind11::arg("stride") = 1, pybind11::arg("pad") = 1);
+  m.def("stem_mtiles", &hipps::stem_mtiles, "number of BN partial-statistic columns of stem_forward");
+  m.def("stem_forward", &hipps::stem_forward,
+        "ResNet stem 7x7/s2/p3 3->64 conv forward on MFMA (channels-last bf16), optional BN-statistics epilogue",
+        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("part") = pybind11::none());
+  m.def("stem_wgrad", &hipps::stem_wgrad, "ResNet stem 7x7/s2/p3 weight gradient on MFMA (fp32 dW, deterministic)");
   m.def("conv_wgrad", &hipps::conv_wgrad, "MFMA KxK conv weight gradient (implicit GEMM, split-M, fp32 dW)");
   m.def("maxpool3s2_forward", &hipps::maxpool3s2_forward, "3x3/s2/p1 max pool, channels-last bf16, 4-bit tap codes");
   m.def("maxpool3s2_backward", &hipps::maxpool3s2_backward, "3x3/s2/p1 max pool backward (gather form, no atomics)");

@@ -35,6 +35,9 @@ _FUSED_WGRAD = _os.environ.get("HIPPS_FUSED_WGRAD", "1") != "0"
 # bn2 -> conv3: BN apply + ReLU in the 1x1 GEMM's operand prologue (the BN output is never written).
 # Opt-in: measured on ResNet-50 bs256 it removes 16 apply passes (-0.23 ms/step) but the prologue
 # GEMMs lose about as much (+0.10..0.17 ms/step), profiles/ab_r2/prologue_*.txt
+# stem conv on the hipps MFMA stem kernels (BN statistics in the forward epilogue); HIPPS_OWN_STEM=0
+# keeps it on MIOpen
+_FUSED_STEM = _FUSED
 _FUSED_PRO = _FUSED_CONV and _os.environ.get("HIPPS_FUSED_PRO", "0") != "0"
 
 
@@ -147,7 +150,7 @@ class ResNet(nn.Module):
                     nn.init.zeros_(m.bn2.weight)
 
     def forward(self, x):
-        x = self.maxpool(self.bn1(self.conv1(x)))
+        x = self.maxpool(conv2d_bn(self.conv1, self.bn1, x, fuse=_FUSED_STEM))
         for i in range(self.num_stages):
             x = getattr(self, f"layer{i + 1}")(x)
         x = global_avg_pool(x)

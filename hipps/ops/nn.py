@@ -33,6 +33,9 @@ _DGRAD_AS_FWD = _os.environ.get("HIPPS_DGRAD_FWD", "1") != "0"
 # Find picks under cudnn.benchmark (bench A/B: 25.26 vs 24.90 ms of kernels per step,
 # profiles/ab_r2/own_kxk_*)
 _OWN_KXK_FWD = _os.environ.get("HIPPS_OWN_KXK", "0") != "0"
+# ResNet stem (7x7/s2/p3, 3 -> 64 channels): forward + BN statistics and weight gradient on the
+# hipps MFMA stem kernels (stem.hip) instead of MIOpen
+_OWN_STEM = _os.environ.get("HIPPS_OWN_STEM", "1") != "0"
 
 MASK_NONE, MASK_X, MASK_Y, MASK_BITS = 0, 1, 2, 3
 
@@ -359,10 +362,69 @@ def convkxk_ok(conv: nn.Conv2d, x: torch.Tensor, own_wgrad: bool = True) -> bool
             w.is_contiguous(memory_format=torch.channels_last))
 
 
+class _StemConv(torch.autograd.Function):
+    """ResNet stem convolution (7x7, stride 2, pad 3, 3 -> 64 channels) on the hipps MFMA kernels
+    (csrc/stem.hip): forward with the following BatchNorm's partial statistics in the epilogue,
+    fp32 weight gradient straight into the master's dtype; an input gradient (never needed for an
+    image batch) falls back to MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x, w_master, stats=True):
+        w = bf16_weight(w_master).contiguous(memory_format=torch.channels_last)
+        n, _, h, wd = x.shape
+        ho, wo = (h - 1) // 2 + 1, (wd - 1) // 2 + 1
+        y = torch.empty((n, 64, ho, wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        part = (torch.empty((2, 64, native().stem_mtiles(n, ho)), dtype=torch.float32, device=x.device) if stats
+                else torch.empty(0, device=x.device))
+        native().stem_forward(x, w, y, part if stats else None)
+        ctx.wdtype = w_master.dtype
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(x, w)
+        ctx.mark_non_differentiable(part)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, dy, _dpart=None):
+        x, w = ctx.saved_tensors
+        if dy is None:
+            return None, None, None
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(dy, x, w, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
+                                                     [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty((64, 3, 7, 7), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+            native().stem_wgrad(dy, x, dw)
+            if ctx.wdtype != torch.float32:
+                dw = dw.to(ctx.wdtype)
+        return dx, dw, None
+
+
+def stem_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    """Can _StemConv run this convolution on this input (after the autocast cast)?"""
+    if not (_OWN_STEM and x.is_cuda and x.dim() == 4 and x.shape[1] == 3):
+        return False
+    if x.dtype != torch.bfloat16 and not (x.dtype == torch.float32 and torch.is_autocast_enabled("cuda") and
+                                          torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return False
+    if (conv.in_channels, conv.out_channels, conv.kernel_size, conv.stride, conv.padding, conv.dilation,
+            conv.groups) != (3, 64, (7, 7), (2, 2), (3, 3), (1, 1), 1):
+        return False
+    if conv.bias is not None or conv.padding_mode != "zeros":
+        return False
+    h, w = x.shape[2], x.shape[3]
+    return w % 8 == 0 and h >= 7 and w >= 7 and (w - 1) // 2 + 1 <= 128
+
+
 def conv2d_stats(conv: nn.Conv2d, x: torch.Tensor, fuse: bool = True):
     """(conv(x), part): with the hipps implicit-GEMM forward, ``part`` holds the following
     BatchNorm's partial statistics [2, Cout, m_tiles] from its epilogue (None otherwise); the
     hipps weight gradient when eligible (see _ConvKxK)."""
+    if fuse and stem_ok(conv, x):
+        xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        y, part = _StemConv.apply(xb, conv.weight, conv.training)
+        return y, (part if part.numel() else None)
     if fuse and conv.training and convkxk_ok(conv, x):
         y, part = _ConvKxK.apply(x, conv.weight, conv.stride[0], conv.padding[0], True, True)
         return y, (part if part.numel() else None)

@@ -1,0 +1,105 @@
+"""GPU: ResNet stem kernels (hipps/csrc/stem.hip, 7x7/s2/p3, 3 -> 64 channels) vs an fp32 PyTorch
+convolution: forward, the BatchNorm partial statistics of its epilogue, the weight gradient, and the
+ResNet-50 stem routed through them (with the MIOpen path as the A/B reference)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from hipps.ops import nn as hnn
+from hipps.ops._native import native
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+SHAPES = [  # (images, H, W)
+    (2, 224, 224),  # ResNet-50: 112x112 outputs, 14 row groups of 8
+    (3, 56, 40),    # 28x20 outputs: partial 16-pixel fragments, row groups past Ho
+    (1, 37, 16),    # odd height, 19x8 outputs
+    (2, 64, 256),   # 128-wide outputs (the widest staged dy row)
+]
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def _inputs(n, h, w, seed):
+    torch.manual_seed(seed)
+    x = _cl(torch.randn(n, 3, h, w, device=DEV).to(torch.bfloat16))
+    wt = _cl((torch.randn(64, 3, 7, 7, device=DEV) / 147 ** 0.5).to(torch.bfloat16))
+    return x, wt
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_stem_forward_matches_fp32_conv_and_stats(shape):
+    n, h, w = shape
+    x, wt = _inputs(n, h, w, h + w)
+    ref = F.conv2d(x.float(), wt.float(), stride=2, padding=3)
+    y = _cl(torch.empty(ref.shape, device=DEV, dtype=torch.bfloat16))
+    mt = native().stem_mtiles(n, ref.shape[2])
+    part = torch.empty(2, 64, mt, device=DEV)
+    native().stem_forward(x, wt, y, part)
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, 64)  # statistics of the stored bf16 values
+    torch.testing.assert_close(part[0].sum(1), yf.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(part[1].sum(1), (yf * yf).sum(0), rtol=1e-4, atol=1e-2)
+    y2 = _cl(torch.empty_like(y))
+    native().stem_forward(x, wt, y2)  # no statistics: same outputs
+    assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_stem_wgrad_matches_fp32(shape):
+    n, h, w = shape
+    x, wt = _inputs(n, h, w, 3 * h + w)
+    xf = x.float().requires_grad_(False)
+    wf = wt.float().requires_grad_(True)
+    ref_y = F.conv2d(xf, wf, stride=2, padding=3)
+    dy = _cl(torch.randn(ref_y.shape, device=DEV).to(torch.bfloat16))
+    (ref_y * dy.float()).sum().backward()
+    dw = _cl(torch.empty(64, 3, 7, 7, device=DEV))
+    native().stem_wgrad(dy, x, dw)
+    m = n * ref_y.shape[2] * ref_y.shape[3]
+    torch.testing.assert_close(dw, wf.grad, rtol=2e-3, atol=2e-3 * m ** 0.5)
+    dw2 = _cl(torch.empty_like(dw))
+    native().stem_wgrad(dy, x, dw2)
+    assert torch.equal(dw, dw2)  # fixed-order slab sum: bitwise repeatable
+
+
+def test_stem_nonfinite_input_stays_local():
+    """A NaN input pixel may only reach the outputs whose window covers it (zero-weighted padding
+    lanes of the k steps must not carry it into neighbouring pixels)."""
+    x, wt = _inputs(1, 32, 32, 5)
+    x[0, 1, 10, 10] = float("nan")
+    y = _cl(torch.empty(1, 64, 16, 16, device=DEV, dtype=torch.bfloat16))
+    native().stem_forward(x, wt, y)
+    bad = torch.isnan(y.float()).any(1)[0]
+    # input (10, 10) is in the windows of outputs ho, wo with |2*ho - 10| <= 3: ho, wo in {4, 5, 6}
+    expect = torch.zeros(16, 16, dtype=torch.bool, device=DEV)
+    expect[4:7, 4:7] = True
+    assert torch.equal(bad, expect)
+
+
+def test_resnet_stem_routes_through_hipps_and_matches_miopen():
+    from hipps.models import resnet50
+
+    torch.manual_seed(0)
+    m = resnet50().to(DEV).to(memory_format=torch.channels_last)
+    x = _cl(torch.randn(4, 3, 224, 224, device=DEV))
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        assert hnn.stem_ok(m.conv1, x)
+        y, part = hnn.conv2d_stats(m.conv1, x)
+    assert part is not None and part.shape[1] == 64  # only the hipps stem returns statistics
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        ref = m.conv1(x)
+    torch.testing.assert_close(y.float(), ref.float(), rtol=2e-2, atol=2e-2)
+    # weight gradient through autograd into the fp32 master
+    dy = torch.randn_like(ref.float())
+    (y.float() * dy).sum().backward()
+    g_own = m.conv1.weight.grad.clone()
+    m.conv1.weight.grad = None
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        ref = m.conv1(x)
+    (ref.float() * dy).sum().backward()
+    assert g_own.dtype == torch.float32
+    torch.testing.assert_close(g_own, m.conv1.weight.grad, rtol=2e-2, atol=2e-2 * g_own.abs().max().item())

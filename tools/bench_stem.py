@@ -1,4 +1,5 @@
-"""Stem 7x7/s2 convolution on MIOpen with the 3 input channels zero-padded to 4 or 8.
+"""Stem 7x7/s2 convolution: hipps' MFMA stem kernels (csrc/stem.hip) vs MIOpen, and MIOpen with
+the 3 input channels zero-padded to 4 or 8.
 
 Cin = 3 gives a 147-long reduction that MIOpen's implicit-GEMM solvers tile poorly. The padded
 channels are zero, so the outputs are unchanged and the weight gradient of the real channels is the same.
@@ -6,8 +7,12 @@ channels are zero, so the outputs are unchanged and the weight gradient of the r
 """
 import argparse
 import json
+import os
+import sys
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def timeit(fn, iters=10, warm=3):
@@ -51,6 +56,21 @@ def main():
         out[f"c{c}"] = {"fwd_us": timeit(fwd), "wgrad_us": timeit(wgr), "pad_us": timeit(pad) if c > 3 else 0.0,
                         "max_abs_diff_vs_c3": err, "dw_shape": list(dw.shape)}
         print(f"C={c}", json.dumps(out[f"c{c}"]), flush=True)
+    from hipps.ops._native import native
+
+    w3c = w3.contiguous(memory_format=cl)
+    y = torch.empty_like(y_ref)
+    part = torch.empty(2, 64, native().stem_mtiles(n, y_ref.shape[2]), device="cuda")
+    dw = torch.empty(64, 3, 7, 7, device="cuda").contiguous(memory_format=cl)
+    native().stem_forward(x3, w3c, y, part)
+    native().stem_wgrad(dy, x3, dw)
+    ref_dw = torch.ops.aten.convolution_backward(dy, x3, w3, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
+                                                 [False, True, False])[1].float()
+    out["hipps"] = {"fwd_us": timeit(lambda: native().stem_forward(x3, w3c, y, part)),
+                    "wgrad_us": timeit(lambda: native().stem_wgrad(dy, x3, dw)),
+                    "max_abs_diff_fwd_vs_miopen": (y.float() - y_ref.float()).abs().max().item(),
+                    "max_rel_diff_wgrad_vs_miopen": ((dw - ref_dw).abs().max() / ref_dw.abs().max()).item()}
+    print("hipps", json.dumps(out["hipps"]), flush=True)
     print(json.dumps(out))
 
 
