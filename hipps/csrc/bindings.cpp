@@ -59,7 +59,12 @@ void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
                      c10::optional<at::Tensor> bn_scale, c10::optional<at::Tensor> bn_shift,
                      c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift);
 // pool.hip
-void maxpool3s2_forward(at::Tensor x, at::Tensor y, at::Tensor code);
+void maxpool3s2_forward(at::Tensor x, at::Tensor y, at::Tensor code, c10::optional<at::Tensor> scale,
+                        c10::optional<at::Tensor> shift);
+void bn_finalize_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tensor weight, at::Tensor bias,
+                          c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
+                          at::Tensor mean, at::Tensor invstd, at::Tensor scale, at::Tensor shift, int64_t C, double eps,
+                          double momentum);
 void maxpool3s2_backward(at::Tensor dy, at::Tensor code, at::Tensor dx);
 void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64_t Wi, int64_t stride,
                    c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift);
@@ -140,7 +145,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("part") = pybind11::none());
   m.def("stem_wgrad", &hipps::stem_wgrad, "ResNet stem 7x7/s2/p3 weight gradient on MFMA (fp32 dW, deterministic)");
   m.def("conv_wgrad", &hipps::conv_wgrad, "MFMA KxK conv weight gradient (implicit GEMM, split-M, fp32 dW)");
-  m.def("maxpool3s2_forward", &hipps::maxpool3s2_forward, "3x3/s2/p1 max pool, channels-last bf16, 4-bit tap codes");
+  m.def("maxpool3s2_forward", &hipps::maxpool3s2_forward,
+        "3x3/s2/p1 max pool, channels-last bf16, 4-bit tap codes; optional BN-apply + ReLU prologue",
+        pybind11::arg("x"), pybind11::arg("y"), pybind11::arg("code"), pybind11::arg("scale") = pybind11::none(),
+        pybind11::arg("shift") = pybind11::none());
+  m.def("bn_finalize_partials", &hipps::bn_finalize_partials,
+        "BN train-mode finalize from producer partial sums (mean/invstd/scale/shift + running stats)");
   m.def("maxpool3s2_backward", &hipps::maxpool3s2_backward, "3x3/s2/p1 max pool backward (gather form, no atomics)");
   m.def("conv1x1_wgrad", &hipps::conv1x1_wgrad, "MFMA 1x1 conv weight gradient (tr_b16 LDS reads, split-M)",
         pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("dw"), pybind11::arg("Hi"), pybind11::arg("Wi"),

@@ -400,6 +400,32 @@ void bn_forward_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y,
                      relu, stream);
 }
 
+// Finalize only, from a producer's partial sums part [2, C, nrb] over M rows: mean, invstd, scale,
+// shift and the running stats; no pass over the activations (the stem's max pool applies them).
+void bn_finalize_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tensor weight, at::Tensor bias,
+                          c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
+                          at::Tensor mean, at::Tensor invstd, at::Tensor scale, at::Tensor shift, int64_t C, double eps,
+                          double momentum) {
+  TORCH_CHECK(C % 8 == 0 && C <= kMaxC && C >= 8, "fused BN needs C % 8 == 0 and 8 <= C <= 2048");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.numel() == 2 * C * nrb,
+              "bn_finalize_partials: part must be f32 [2, C, nrb]");
+  TORCH_CHECK(M > 0 && nrb > 0 && nrb < (int64_t(1) << 31), "bn_finalize_partials: sizes");
+  for (auto* t : {&weight, &bias, &mean, &invstd, &scale, &shift}) check_vec(*t, "per-channel vector", (int)C);
+  float* rm = nullptr;
+  float* rv = nullptr;
+  if (running_mean.has_value() && running_mean->defined()) {
+    check_vec(*running_mean, "running_mean", (int)C);
+    check_vec(*running_var, "running_var", (int)C);
+    rm = running_mean->data_ptr<float>();
+    rv = running_var->data_ptr<float>();
+  }
+  hipLaunchKernelGGL(k_bn_finalize_fwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, c10::hip::getCurrentHIPStream(),
+                     part[0].data_ptr<float>(), part[1].data_ptr<float>(), (int)nrb, (int)C, M,
+                     weight.data_ptr<float>(), bias.data_ptr<float>(), (float)eps, (float)momentum, rm, rv,
+                     mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
+                     shift.data_ptr<float>());
+}
+
 // Statistics only (reduce + finalize): mean, invstd, scale, shift and the running stats, no apply
 // pass -- the consuming 1x1 conv applies scale/shift + ReLU in its operand prologue (gemm.hip).
 void bn_forward_stats(at::Tensor x, at::Tensor weight, at::Tensor bias, c10::optional<at::Tensor> running_mean,

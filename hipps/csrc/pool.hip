@@ -8,6 +8,10 @@
 //           a 4-bit tap code (kh*3 + kw) per channel, 8 codes in one uint32 per lane: 1/4 of the
 //           output bytes instead of 4x (int64 indices).  Ties and NaNs follow PyTorch's rule
 //           (first maximum in scan order; a NaN always wins), so values and gradients match it.
+// BN variant (the ResNet stem): the input is a training BatchNorm's INPUT and each tap is read as
+//           bf16(max(x * scale[c] + shift[c], 0)) -- the BN apply kernel's exact rounding -- so the
+//           BN + ReLU output (411 MB at batch 256) is never written or re-read; pooled values and
+//           tap codes are bit-identical to apply-then-pool.
 // backward: gather form, no atomics: one lane = one input pixel x 8 channels.  With k=3, s=2,
 //           p=1 an input row h lies in the windows oh in [h>>1, (h+1)>>1] (1 or 2 of them), so a
 //           lane checks at most 4 windows' codes and sums the matching dy in fp32.
@@ -33,10 +37,11 @@ __device__ __forceinline__ void st8(uint16_t* p, const float v[8]) {
 }
 }  // namespace
 
-template <typename I>
+template <typename I, bool BN = false>
 __global__ __launch_bounds__(kBlock) void k_maxpool3s2_fwd(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                            uint32_t* __restrict__ code, int64_t total, int H, int W,
-                                                           int Ho, int Wo, int G) {
+                                                           int Ho, int Wo, int G, const float* __restrict__ scale,
+                                                           const float* __restrict__ shift) {
   const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= total) return;
   // 32-bit index decomposition when the grid fits (the int64 div/mod sequence dominated)
@@ -47,9 +52,13 @@ __global__ __launch_bounds__(kBlock) void k_maxpool3s2_fwd(const uint16_t* __res
   p /= (I)Wo;
   const int ho = (int)(p % (I)Ho);
   const int64_t n = (int64_t)(p / (I)Ho);
-  float m[8];
+  float m[8], sc[8], sh[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+  for (int j = 0; j < 8; ++j) {
+    m[j] = -INFINITY;
+    sc[j] = BN ? scale[g * 8 + j] : 1.f;
+    sh[j] = BN ? shift[g * 8 + j] : 0.f;
+  }
   uint32_t c = 0;
 #pragma unroll
   for (int kh = 0; kh < 3; ++kh) {
@@ -61,6 +70,10 @@ __global__ __launch_bounds__(kBlock) void k_maxpool3s2_fwd(const uint16_t* __res
       if (w < 0 || w >= W) continue;
       float xv[8];
       ld8(x + (((n * H + h) * W + w) * G + g) * 8, xv);
+      if (BN) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[j] = bf16_to_f32(f32_to_bf16(fmaxf(fmaf(xv[j], sc[j], sh[j]), 0.f)));
+      }
       const uint32_t t = (uint32_t)(kh * 3 + kw);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -108,8 +121,10 @@ __global__ __launch_bounds__(kBlock) void k_maxpool3s2_bwd(const uint16_t* __res
 }
 
 // x: [N, C, H, W] channels-last bf16 (C % 8 == 0); y: [N, C, Ho, Wo] channels-last bf16;
-// code: int32 [N*Ho*Wo*C/8] (4-bit tap codes).
-void maxpool3s2_forward(at::Tensor x, at::Tensor y, at::Tensor code) {
+// code: int32 [N*Ho*Wo*C/8] (4-bit tap codes).  scale / shift (optional, f32 [C]): pool
+// relu(x * scale + shift) instead of x (x is a BatchNorm input, see the BN variant above).
+void maxpool3s2_forward(at::Tensor x, at::Tensor y, at::Tensor code, c10::optional<at::Tensor> scale,
+                        c10::optional<at::Tensor> shift) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast), "maxpool: x must be channels-last bf16 NCHW");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
@@ -124,17 +139,29 @@ void maxpool3s2_forward(at::Tensor x, at::Tensor y, at::Tensor code) {
   for (const at::Tensor* t : {&x, &y, &code})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "maxpool: 16-byte aligned tensors");
   TORCH_CHECK(x.numel() < (int64_t(1) << 40) && (total + kBlock - 1) / kBlock < (int64_t(1) << 31), "maxpool: size");
+  const bool bn = scale.has_value() && scale->defined();
+  const float *sc = nullptr, *sh = nullptr;
+  if (bn) {
+    TORCH_CHECK(shift.has_value() && shift->defined(), "maxpool: scale needs shift");
+    for (const c10::optional<at::Tensor>* v : {&scale, &shift})
+      TORCH_CHECK((*v)->is_cuda() && (*v)->scalar_type() == at::kFloat && (*v)->is_contiguous() && (*v)->numel() == C,
+                  "maxpool: scale / shift must be f32 [C]");
+    sc = scale->data_ptr<float>();
+    sh = shift->data_ptr<float>();
+  }
   if (total == 0) return;
   const int grid = (int)((total + kBlock - 1) / kBlock);
   auto stream = c10::hip::getCurrentHIPStream();
-  if (total < (int64_t(1) << 31))
-    hipLaunchKernelGGL(k_maxpool3s2_fwd<uint32_t>, grid, kBlock, 0, stream, (const uint16_t*)x.data_ptr(),
-                       (uint16_t*)y.data_ptr(), (uint32_t*)code.data_ptr(), total, (int)H, (int)W, (int)Ho, (int)Wo,
-                       (int)(C / 8));
-  else
-    hipLaunchKernelGGL(k_maxpool3s2_fwd<int64_t>, grid, kBlock, 0, stream, (const uint16_t*)x.data_ptr(),
-                       (uint16_t*)y.data_ptr(), (uint32_t*)code.data_ptr(), total, (int)H, (int)W, (int)Ho, (int)Wo,
-                       (int)(C / 8));
+#define HIPPS_MP(I, B)                                                                                        \
+  hipLaunchKernelGGL((k_maxpool3s2_fwd<I, B>), grid, kBlock, 0, stream, (const uint16_t*)x.data_ptr(),          \
+                     (uint16_t*)y.data_ptr(), (uint32_t*)code.data_ptr(), total, (int)H, (int)W, (int)Ho, (int)Wo, \
+                     (int)(C / 8), sc, sh)
+  if (total < (int64_t(1) << 31)) {
+    if (bn) HIPPS_MP(uint32_t, true); else HIPPS_MP(uint32_t, false);
+  } else {
+    if (bn) HIPPS_MP(int64_t, true); else HIPPS_MP(int64_t, false);
+  }
+#undef HIPPS_MP
 }
 
 // dy: [N, C, Ho, Wo] channels-last bf16; dx: [N, C, H, W] channels-last bf16 (fully written).

@@ -14,8 +14,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from hipps.ops.nn import (FusedBatchNorm2d, MaxPool2d, ResidualTap, bn_relu_conv1x1_ok, bn_relu_conv_bn, conv2d,
-                          conv2d_bn, conv_bn, global_avg_pool)
+from hipps.ops.nn import (FusedBatchNorm2d, MaxPool2d, ResidualTap, bn_relu_conv1x1_ok, bn_relu_conv_bn,
+                          bn_relu_maxpool, conv2d, conv2d_bn, conv2d_stats, conv_bn, global_avg_pool)
 
 # One switch for the whole zoo: fused BN(+residual)(+ReLU) HIP kernels on channels-last bf16,
 # standard PyTorch elsewhere.  HIPPS_FUSED_BN=0 restores the eager MIOpen path for A/B runs.
@@ -38,6 +38,8 @@ _FUSED_WGRAD = _os.environ.get("HIPPS_FUSED_WGRAD", "1") != "0"
 # stem conv on the hipps MFMA stem kernels (BN statistics in the forward epilogue); HIPPS_OWN_STEM=0
 # keeps it on MIOpen
 _FUSED_STEM = _FUSED
+# stem BN apply + ReLU folded into the max pool's load (the BN output is never materialised)
+_FUSED_STEM_POOL = _FUSED_STEM and _os.environ.get("HIPPS_FUSED_STEMPOOL", "1") != "0"
 _FUSED_PRO = _FUSED_CONV and _os.environ.get("HIPPS_FUSED_PRO", "0") != "0"
 
 
@@ -150,7 +152,8 @@ class ResNet(nn.Module):
                     nn.init.zeros_(m.bn2.weight)
 
     def forward(self, x):
-        x = self.maxpool(conv2d_bn(self.conv1, self.bn1, x, fuse=_FUSED_STEM))
+        y, part = conv2d_stats(self.conv1, x, fuse=_FUSED_STEM)
+        x = bn_relu_maxpool(self.bn1, self.maxpool, y, part if _FUSED_STEM_POOL else None)
         for i in range(self.num_stages):
             x = getattr(self, f"layer{i + 1}")(x)
         x = global_avg_pool(x)

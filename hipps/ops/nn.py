@@ -685,6 +685,54 @@ class _MaxPool3s2(torch.autograd.Function):
         return dx
 
 
+class _BNReluPool(torch.autograd.Function):
+    """maxpool3s2(relu(bn(y))) for a training BatchNorm whose statistics arrive as producer partials
+    (the stem conv's epilogue): finalize, then ONE pool pass that reads y and applies the BN + ReLU
+    in its load (pool.hip, BN variant) -- the 411 MB BN output of a batch-256 stem is never written
+    or re-read.  Backward: the pool's gather into dz, then the BN backward with the ReLU mask
+    recomputed from y.  Values, tap codes and gradients are bit-identical to bn -> pool."""
+
+    @staticmethod
+    def forward(ctx, y, part, weight, bias, running_mean, running_var, eps, momentum):
+        N, C, H, W = y.shape
+        f32 = dict(dtype=torch.float32, device=y.device)
+        mean, invstd = torch.empty(C, **f32), torch.empty(C, **f32)
+        scale, shift = torch.empty(C, **f32), torch.empty(C, **f32)
+        native().bn_finalize_partials(part, part.shape[2], N * H * W, weight, bias, running_mean, running_var, mean,
+                                      invstd, scale, shift, C, float(eps), float(momentum))
+        Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        out = torch.empty((N, C, Ho, Wo), dtype=torch.bfloat16, device=y.device, memory_format=torch.channels_last)
+        code = torch.empty(N * Ho * Wo * (C // 8), dtype=torch.int32, device=y.device)
+        native().maxpool3s2_forward(y, out, code, scale, shift)
+        ctx.save_for_backward(y, code, weight, mean, invstd, scale, shift)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        y, code, weight, mean, invstd, scale, shift = ctx.saved_tensors
+        dout = dout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dz = torch.empty_like(y, memory_format=torch.channels_last)
+        native().maxpool3s2_backward(dout, code, dz)
+        dy = torch.empty_like(y, memory_format=torch.channels_last)
+        dw, db = torch.empty_like(weight), torch.empty_like(weight)
+        native().bn_backward(dz, y, None, MASK_X, weight, mean, invstd, scale, shift, dy, None, dw, db, y.shape[1],
+                             None)
+        return dy, None, dw, db, None, None, None, None
+
+
+def bn_relu_maxpool(bn, pool, y, part=None):
+    """pool(bn(y)) for a ReLU BatchNorm followed by the 3x3/s2 max pool (the ResNet stem); with the
+    producer's partial statistics ``part`` and every piece on the fused kernels this is one pool
+    pass (_BNReluPool), otherwise the two modules."""
+    if (part is not None and bn.training and bn.relu and bn._fast_ok(y, None) and isinstance(pool, MaxPool2d)
+            and pool.fused and _pool_ok(pool, y)):
+        bn._nbt_pending += 1
+        return _BNReluPool.apply(y, part, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, bn.momentum)
+    if part is not None and bn.training and bn._fast_ok(y, None):
+        return pool(bn(y, stats=part))
+    return pool(bn(y))
+
+
 class MaxPool2d(nn.MaxPool2d):
     """nn.MaxPool2d; the ResNet stem case (3x3, stride 2, pad 1) on channels-last bf16 HIP
     tensors runs the hipps kernels, everything else the PyTorch op."""

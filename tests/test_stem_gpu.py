@@ -103,3 +103,45 @@ def test_resnet_stem_routes_through_hipps_and_matches_miopen():
     (ref.float() * dy).sum().backward()
     assert g_own.dtype == torch.float32
     torch.testing.assert_close(g_own, m.conv1.weight.grad, rtol=2e-2, atol=2e-2 * g_own.abs().max().item())
+
+
+@pytest.mark.parametrize("shape", [(4, 112, 112), (3, 27, 20)])
+def test_bn_relu_pool_bit_identical_to_bn_then_pool(shape):
+    """_BNReluPool (BN apply + ReLU in the pool's load) vs the fused BN module then the pool module:
+    pooled values, running statistics and every gradient bitwise equal."""
+    n, h, w = shape
+    torch.manual_seed(h)
+    y = _cl(torch.randn(n, 64, h, w, device=DEV).mul_(3).add_(0.5).to(torch.bfloat16))
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, 64)
+    part = torch.stack([yf.sum(0), (yf * yf).sum(0)]).unsqueeze(-1).contiguous()  # one partial column
+    outs = []
+    for fused in (True, False):
+        bn = hnn.FusedBatchNorm2d(64, relu=True).to(DEV)
+        with torch.no_grad():
+            bn.weight.copy_(torch.linspace(-1.5, 2.0, 64))  # negative scales too
+            bn.bias.copy_(torch.linspace(-0.5, 0.5, 64))
+        pool = hnn.MaxPool2d(3, stride=2, padding=1)
+        yi = y.detach().clone().requires_grad_(True)
+        out = hnn.bn_relu_maxpool(bn, pool, yi, part) if fused else pool(bn(yi, stats=part))
+        g = _cl(torch.randn(out.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(1)).to(torch.bfloat16))
+        out.backward(g)
+        outs.append((out.detach(), yi.grad, bn.weight.grad, bn.bias.grad, bn.running_mean, bn.running_var))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+def test_resnet_forward_uses_bn_relu_pool():
+    from hipps.models import resnet50
+
+    m = resnet50().to(DEV).to(memory_format=torch.channels_last)
+    x = _cl(torch.randn(2, 3, 64, 64, device=DEV))
+    calls = []
+    orig = hnn._BNReluPool.apply
+    hnn._BNReluPool.apply = lambda *a: calls.append(1) or orig(*a)
+    try:
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            m(x).float().sum().backward()
+    finally:
+        hnn._BNReluPool.apply = orig
+    assert calls == [1]
+    assert m.bn1.weight.grad is not None and torch.isfinite(m.conv1.weight.grad).all()
