@@ -78,6 +78,9 @@ void convkxk_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
 int64_t stem_mtiles(int64_t imgs, int64_t Ho);
 void stem_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part);
 void stem_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw);
+void stem_bnpool_backward(at::Tensor dp, at::Tensor code, at::Tensor y, at::Tensor x, at::Tensor bn_weight,
+                          at::Tensor mean, at::Tensor invstd, at::Tensor scale, at::Tensor shift, at::Tensor dbn_w,
+                          at::Tensor dbn_b, at::Tensor dw);
 namespace rt {
 void pull_params(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, at::Tensor pub,
                  int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t ring_slot, int64_t tries);
@@ -143,6 +146,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_forward", &hipps::stem_forward,
         "ResNet stem 7x7/s2/p3 3->64 conv forward on MFMA (channels-last bf16), optional BN-statistics epilogue",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("part") = pybind11::none());
+  m.def("stem_bnpool_backward", &hipps::stem_bnpool_backward,
+        "backward of maxpool(relu(bn(stem(x)))): BN parameter grads + stem weight grad, no pool/BN input grads "
+        "materialised");
   m.def("stem_wgrad", &hipps::stem_wgrad, "ResNet stem 7x7/s2/p3 weight gradient on MFMA (fp32 dW, deterministic)");
   m.def("conv_wgrad", &hipps::conv_wgrad, "MFMA KxK conv weight gradient (implicit GEMM, split-M, fp32 dW)");
   m.def("maxpool3s2_forward", &hipps::maxpool3s2_forward,

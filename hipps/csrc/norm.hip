@@ -426,6 +426,25 @@ void bn_finalize_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tensor we
                      shift.data_ptr<float>());
 }
 
+// Backward finalize only, from a producer's partials part [2, C, nrb] (a = sum dz', b = sum dz' x-hat
+// over M rows): dweight, dbias and coef [3, C] = (a, k1, k0) of dx = a*dz' + k1*x + k0.  The stem's
+// fused pool backward (stem.hip) reduces and applies on its own.
+void bn_finalize_bwd_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tensor weight, at::Tensor mean,
+                              at::Tensor invstd, at::Tensor dweight, at::Tensor dbias, at::Tensor coef) {
+  const int64_t C = weight.numel();
+  TORCH_CHECK(C % 8 == 0 && C <= kMaxC && C >= 8, "fused BN needs C % 8 == 0 and 8 <= C <= 2048");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.numel() == 2 * C * nrb,
+              "bn_finalize_bwd_partials: part must be f32 [2, C, nrb]");
+  TORCH_CHECK(coef.is_cuda() && coef.scalar_type() == at::kFloat && coef.is_contiguous() && coef.numel() == 3 * C,
+              "bn_finalize_bwd_partials: coef must be f32 [3, C]");
+  for (auto* t : {&weight, &mean, &invstd, &dweight, &dbias}) check_vec(*t, "per-channel vector", (int)C);
+  hipLaunchKernelGGL(k_bn_finalize_bwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, c10::hip::getCurrentHIPStream(),
+                     part[0].data_ptr<float>(), part[1].data_ptr<float>(), (int)nrb, (int)C, M,
+                     weight.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                     dweight.data_ptr<float>(), dbias.data_ptr<float>(), coef[0].data_ptr<float>(),
+                     coef[1].data_ptr<float>(), coef[2].data_ptr<float>());
+}
+
 // Statistics only (reduce + finalize): mean, invstd, scale, shift and the running stats, no apply
 // pass -- the consuming 1x1 conv applies scale/shift + ReLU in its operand prologue (gemm.hip).
 void bn_forward_stats(at::Tensor x, at::Tensor weight, at::Tensor bias, c10::optional<at::Tensor> running_mean,

@@ -292,9 +292,138 @@ __device__ __forceinline__ bf16x8 dy_frag(const uint8_t* tile, int row0, int col
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+// Fused stem backward: the gradient reaching the stem conv output y (= the BatchNorm input) is
+//   dy = a * dz * [y*scale + shift > 0] + k1 * y + k0,   dz = max-pool gather of dp (4-bit tap codes)
+// (BN backward with the ReLU mask recomputed from y; a, k1, k0 from k_bn_finalize_bwd).  Neither dz
+// nor dy is materialised: k_stem_pool_bwd_reduce computes dz on the fly for the BN reductions and
+// the weight gradient's dy staging recomputes it (bf16-rounded exactly where the unfused pool
+// backward / BN backward store it, so the staged dy equals the unfused kernels' output).
+struct StemBnPoolBwd {
+  const uint16_t* dp;     // pooled gradient [imgs, 64, Hp, Wp] channels-last bf16
+  const uint32_t* code;   // tap codes, one uint32 per (pooled pixel, 8 channels)
+  const uint16_t* y;      // stem conv output = BN input [imgs, 64, Ho, Wo]
+  const float *scale, *shift, *ca, *ck1, *ck0;
+  int Hp, Wp;
+};
+
+__device__ __forceinline__ void ld8f(const uint16_t* p, float v[8]) {
+  const u32x4 u = *reinterpret_cast<const u32x4*>(p);
+  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+  v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
+  v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+
+// dz (bf16-rounded, before the ReLU mask) of pixel (img, h, w), channels 8g .. 8g+7: the pool
+// backward's gather, same window order as k_maxpool3s2_bwd
+__device__ __forceinline__ void pool_dz8(const StemBnPoolBwd& f, int img, int h, int w, int g, float dz[8]) {
+  // candidate windows (h>>1 | (h>>1)+1) x (w>>1 | (w>>1)+1); the +1 ones exist for odd h / w inside
+  // the pooled map.  Static 2x2 with predicates: the 4 code / dp loads are independent and issue
+  // together (a data-dependent loop serialised them)
+  const int oh0 = h >> 1, ow0 = w >> 1;
+  const bool h1 = (h & 1) && oh0 + 1 < f.Hp, w1 = (w & 1) && ow0 + 1 < f.Wp;
+  uint32_t c[4];
+  u32x4 d[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int oh = oh0 + (k >> 1), ow = ow0 + (k & 1);
+    const bool ok = (!(k >> 1) || h1) && (!(k & 1) || w1);
+    const int64_t o = ok ? ((int64_t)(img * f.Hp + oh) * f.Wp + ow) * (kCout / 8) + g : 0;
+    const uint32_t cv = f.code[o];
+    const u32x4 dv = *reinterpret_cast<const u32x4*>(f.dp + o * 8);
+    c[k] = ok ? cv : 0xffffffffu;  // tap 15 never matches
+    d[k] = dv;
+  }
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // same (oh, ow) order as k_maxpool3s2_bwd
+    const uint32_t tap = (uint32_t)((h - 2 * (oh0 + (k >> 1)) + 1) * 3 + (w - 2 * (ow0 + (k & 1)) + 1));
+    const uint32_t dw[4] = {d[k].x, d[k].y, d[k].z, d[k].w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = __uint_as_float(j & 1 ? dw[j >> 1] & 0xffff0000u : dw[j >> 1] << 16);
+      acc[j] += ((c[k] >> (4 * j)) & 15u) == tap ? v : 0.f;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dz[j] = bf16_to_f32(f32_to_bf16(acc[j]));
+}
+
+// BN backward reductions over dz * relu'(y): a[c] = sum dz', b[c] = sum dz' * (y - mean) * invstd,
+// per block partials pa/pb[c][block] (the format k_bn_finalize_bwd combines).  Lane = 8 channels of
+// one pixel; the grid stride is a multiple of the 8 channel groups, so each lane keeps its group.
+__global__ __launch_bounds__(256) void k_stem_pool_bwd_reduce(StemBnPoolBwd f, const float* __restrict__ mean,
+                                                              const float* __restrict__ invstd, int Ho, int Wo,
+                                                              int64_t total, float* __restrict__ pa,
+                                                              float* __restrict__ pb) {
+  __shared__ float red[2][256][9];  // +1 pad
+  constexpr int G = kCout / 8;
+  const int t = threadIdx.x, g = t % G;
+  float sc[8], sh[8], mu[8], is[8], sa[8], sb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = f.scale[8 * g + j];
+    sh[j] = f.shift[8 * g + j];
+    mu[j] = mean[8 * g + j];
+    is[j] = invstd[8 * g + j];
+    sa[j] = sb[j] = 0.f;
+  }
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + t; v < total; v += stride) {
+    // 32-bit index decomposition (the host checks total < 2^32); int64 div/mod dominated
+    const uint32_t px = (uint32_t)v / G;
+    const uint32_t r = px / (uint32_t)Wo;
+    const int w = (int)(px - r * (uint32_t)Wo);
+    const int img = (int)(r / (uint32_t)Ho), h = (int)(r - (uint32_t)img * (uint32_t)Ho);
+    float dz[8], yv[8];
+    pool_dz8(f, img, h, w, g, dz);
+    ld8f(f.y + v * 8, yv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = fmaf(yv[j], sc[j], sh[j]) > 0.f ? dz[j] : 0.f;
+      sa[j] += d;
+      sb[j] = fmaf(d, (yv[j] - mu[j]) * is[j], sb[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][t][j] = sa[j];
+    red[1][t][j] = sb[j];
+  }
+  __syncthreads();
+  if (t < kCout) {  // channel t: group t / 8, element t % 8, summed over the 256 / G lanes in order
+    const int gg = t >> 3, j = t & 7;
+    float a = 0.f, c = 0.f;
+    for (int l = gg; l < 256; l += G) {
+      a += red[0][l][j];
+      c += red[1][l][j];
+    }
+    pa[(int64_t)t * gridDim.x + blockIdx.x] = a;
+    pb[(int64_t)t * gridDim.x + blockIdx.x] = c;
+  }
+}
+
+// staged dy chunk (bf16 x 8) of pixel (img, h, w), channel group g: the BN backward apply on the
+// recomputed dz, bit-for-bit the expression of k_bn_apply_bwd<MASK_X>
+__device__ __forceinline__ u32x4 bnpool_dy8(const StemBnPoolBwd& f, int img, int h, int w, int g, int Ho, int Wo) {
+  float dz[8], yv[8], o[8];
+  pool_dz8(f, img, h, w, g, dz);
+  ld8f(f.y + (((int64_t)img * Ho + h) * Wo + w) * kCout + 8 * g, yv);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = 8 * g + j;
+    const float d = fmaf(yv[j], f.scale[c], f.shift[c]) > 0.f ? dz[j] : 0.f;
+    o[j] = fmaf(f.ca[c], d, fmaf(f.ck1[c], yv[j], f.ck0[c]));
+  }
+  return u32x4{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]), pack_bf16x2(o[6], o[7])};
+}
+
+template <bool PRO>
 __global__ __launch_bounds__(256) void k_stem_wgrad(const uint16_t* __restrict__ dY, const uint16_t* __restrict__ X,
                                                     float* __restrict__ part, int Hi, int Wi, int Ho, int Wo,
-                                                    int pitch, int rows_per_blk, int splits) {
+                                                    int pitch, int rows_per_blk, int splits, StemBnPoolBwd fb) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   // [2 stages][dy tile kWPx x 64 | 7 input rows x pitch]
   const int stage_elems = kWPx * kCout + kTaps * pitch;
@@ -337,8 +466,13 @@ __global__ __launch_bounds__(256) void k_stem_wgrad(const uint16_t* __restrict__
     _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                                \
       const int i_ = t + 256 * u;                                                                  \
       const int j_ = i_ < dch ? i_ : 0;                                                            \
-      const u32x4 v_ = *reinterpret_cast<const u32x4*>(src_ + (int64_t)(j_ >> 3) * kCout + (j_ & 7) * 8); \
-      rdy[u] = i_ < dch ? v_ : u32x4{0u, 0u, 0u, 0u};                                              \
+      if constexpr (PRO) {                                                                         \
+        rdy[u] = u32x4{0u, 0u, 0u, 0u};                                                            \
+        if (i_ < dch) rdy[u] = bnpool_dy8(fb, img, (ho_), j_ >> 3, j_ & 7, Ho, Wo);                \
+      } else {                                                                                     \
+        const u32x4 v_ = *reinterpret_cast<const u32x4*>(src_ + (int64_t)(j_ >> 3) * kCout + (j_ & 7) * 8); \
+        rdy[u] = i_ < dch ? v_ : u32x4{0u, 0u, 0u, 0u};                                            \
+      }                                                                                            \
     }                                                                                              \
     _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                                \
       const int i_ = t + 256 * u;                                                                  \
@@ -510,16 +644,13 @@ void stem_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Te
                      (int)Hi, (int)Wi, (int)Ho, (int)Wo, (int)pitch, (int)rgs, (int)groups);
 }
 
-// dy [imgs, 64, Ho, Wo], x [imgs, 3, H, W] channels-last bf16; dw f32 [64, 3, 7, 7] channels-last
-// (written, not accumulated).
-void stem_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw) {
+void bn_finalize_bwd_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tensor weight, at::Tensor mean,
+                              at::Tensor invstd, at::Tensor dweight, at::Tensor dbias, at::Tensor coef);  // norm.hip
+
+static void launch_stem_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor& dw, const StemBnPoolBwd* fb) {
   int64_t Hi, Wi, Ho, Wo;
   check_geom(x, Hi, Wi, Ho, Wo);
   const int64_t imgs = x.size(0);
-  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 && dy.size(0) == imgs &&
-                  dy.size(1) == kCout && dy.size(2) == Ho && dy.size(3) == Wo &&
-                  dy.is_contiguous(at::MemoryFormat::ChannelsLast) && reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0,
-              "stem_wgrad: dy must be a 16-byte aligned channels-last bf16 [imgs, 64, Ho, Wo] tensor");
   TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == at::kFloat && dw.numel() == kCout * kK &&
                   dw.is_contiguous(at::MemoryFormat::ChannelsLast), "stem_wgrad: dw must be f32 [64, 3, 7, 7] channels-last");
   const int64_t pitch = stem_pitch(Wi, Wo);
@@ -532,9 +663,15 @@ void stem_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw) {
   TORCH_CHECK(S < (int64_t(1) << 31), "stem_wgrad: grid");
   auto stream = c10::hip::getCurrentHIPStream();
   auto part = at::empty({S, kCout * kK}, dw.options().memory_format(at::MemoryFormat::Contiguous));
-  hipLaunchKernelGGL(k_stem_wgrad, (int)S, 256, lds, stream, (const uint16_t*)dy.data_ptr(),
-                     (const uint16_t*)x.data_ptr(), part.data_ptr<float>(), (int)Hi, (int)Wi, (int)Ho, (int)Wo,
-                     (int)pitch, (int)rows, (int)splits);
+  const uint16_t* dyp = fb ? nullptr : (const uint16_t*)dy.data_ptr();
+  if (fb)
+    hipLaunchKernelGGL(k_stem_wgrad<true>, (int)S, 256, lds, stream, dyp, (const uint16_t*)x.data_ptr(),
+                       part.data_ptr<float>(), (int)Hi, (int)Wi, (int)Ho, (int)Wo, (int)pitch, (int)rows, (int)splits,
+                       *fb);
+  else
+    hipLaunchKernelGGL(k_stem_wgrad<false>, (int)S, 256, lds, stream, dyp, (const uint16_t*)x.data_ptr(),
+                       part.data_ptr<float>(), (int)Hi, (int)Wi, (int)Ho, (int)Wo, (int)pitch, (int)rows, (int)splits,
+                       StemBnPoolBwd{});
   const int n = kCout * kK;
   const int G = (int)std::min<int64_t>(S, 32);
   const unsigned gx = (unsigned)((n + kBlock - 1) / kBlock);
@@ -542,6 +679,59 @@ void stem_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw) {
   hipLaunchKernelGGL(k_stem_reduce1, dim3(gx, G), kBlock, 0, stream, part.data_ptr<float>(), (int)S, G, n,
                      tmp.data_ptr<float>());
   hipLaunchKernelGGL(k_stem_reduce2, gx, kBlock, 0, stream, tmp.data_ptr<float>(), G, n, dw.data_ptr<float>());
+}
+
+// dy [imgs, 64, Ho, Wo], x [imgs, 3, H, W] channels-last bf16; dw f32 [64, 3, 7, 7] channels-last
+// (written, not accumulated).
+void stem_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw) {
+  int64_t Hi, Wi, Ho, Wo;
+  check_geom(x, Hi, Wi, Ho, Wo);
+  const int64_t imgs = x.size(0);
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 && dy.size(0) == imgs &&
+                  dy.size(1) == kCout && dy.size(2) == Ho && dy.size(3) == Wo &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast) && reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0,
+              "stem_wgrad: dy must be a 16-byte aligned channels-last bf16 [imgs, 64, Ho, Wo] tensor");
+  launch_stem_wgrad(dy, x, dw, nullptr);
+}
+
+// Backward of pool(relu(bn(stem(x)))) without materialising the pool or BN input gradients:
+// dp [imgs, 64, Hp, Wp] bf16 + code (max pool tap codes) + y (stem output, BN input); BN vectors
+// f32 [64] (weight, mean, invstd, scale, shift).  Writes dbn_w, dbn_b (BN parameter gradients) and
+// dw (stem weight gradient, f32 channels-last [64, 3, 7, 7]).
+void stem_bnpool_backward(at::Tensor dp, at::Tensor code, at::Tensor y, at::Tensor x, at::Tensor bn_weight,
+                          at::Tensor mean, at::Tensor invstd, at::Tensor scale, at::Tensor shift, at::Tensor dbn_w,
+                          at::Tensor dbn_b, at::Tensor dw) {
+  int64_t Hi, Wi, Ho, Wo;
+  check_geom(x, Hi, Wi, Ho, Wo);
+  const int64_t imgs = x.size(0), Hp = (Ho - 1) / 2 + 1, Wp = (Wo - 1) / 2 + 1;
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kBFloat16 && y.dim() == 4 && y.size(0) == imgs &&
+                  y.size(1) == kCout && y.size(2) == Ho && y.size(3) == Wo &&
+                  y.is_contiguous(at::MemoryFormat::ChannelsLast) && reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
+              "stem_bnpool_backward: y must be the channels-last bf16 stem output");
+  TORCH_CHECK(dp.is_cuda() && dp.scalar_type() == at::kBFloat16 && dp.dim() == 4 && dp.size(0) == imgs &&
+                  dp.size(1) == kCout && dp.size(2) == Hp && dp.size(3) == Wp &&
+                  dp.is_contiguous(at::MemoryFormat::ChannelsLast) && reinterpret_cast<uintptr_t>(dp.data_ptr()) % 16 == 0,
+              "stem_bnpool_backward: dp must be the channels-last bf16 pooled gradient");
+  TORCH_CHECK(code.is_cuda() && code.scalar_type() == at::kInt && code.is_contiguous() &&
+                  code.numel() == imgs * Hp * Wp * (kCout / 8), "stem_bnpool_backward: code size");
+  for (const at::Tensor* v : {&bn_weight, &mean, &invstd, &scale, &shift, &dbn_w, &dbn_b})
+    TORCH_CHECK(v->is_cuda() && v->scalar_type() == at::kFloat && v->is_contiguous() && v->numel() == kCout,
+                "stem_bnpool_backward: BN vectors must be f32 [64]");
+  auto stream = c10::hip::getCurrentHIPStream();
+  StemBnPoolBwd fb{(const uint16_t*)dp.data_ptr(), (const uint32_t*)code.data_ptr(), (const uint16_t*)y.data_ptr(),
+                   scale.data_ptr<float>(), shift.data_ptr<float>(), nullptr, nullptr, nullptr, (int)Hp, (int)Wp};
+  const int64_t total = imgs * Ho * Wo * (kCout / 8);
+  TORCH_CHECK(total < (int64_t(1) << 32), "stem_bnpool_backward: size");
+  const int nrb = (int)std::max<int64_t>(1, std::min<int64_t>(256 * 4, (total + 255) / 256));
+  auto part = at::empty({2, kCout, (int64_t)nrb}, scale.options());
+  hipLaunchKernelGGL(k_stem_pool_bwd_reduce, nrb, 256, 0, stream, fb, mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                     (int)Ho, (int)Wo, total, part[0].data_ptr<float>(), part[1].data_ptr<float>());
+  auto coef = at::empty({3, kCout}, scale.options());
+  bn_finalize_bwd_partials(part, nrb, imgs * Ho * Wo, bn_weight, mean, invstd, dbn_w, dbn_b, coef);
+  fb.ca = coef[0].data_ptr<float>();
+  fb.ck1 = coef[1].data_ptr<float>();
+  fb.ck0 = coef[2].data_ptr<float>();
+  launch_stem_wgrad(y, x, dw, &fb);
 }
 
 }  // namespace hipps

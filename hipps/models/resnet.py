@@ -15,7 +15,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from hipps.ops.nn import (FusedBatchNorm2d, MaxPool2d, ResidualTap, bn_relu_conv1x1_ok, bn_relu_conv_bn,
-                          bn_relu_maxpool, conv2d, conv2d_bn, conv2d_stats, conv_bn, global_avg_pool)
+                          bn_relu_maxpool, conv2d, conv2d_bn, conv2d_stats, conv_bn, global_avg_pool,
+                          stem_block, stem_block_ok)
 
 # One switch for the whole zoo: fused BN(+residual)(+ReLU) HIP kernels on channels-last bf16,
 # standard PyTorch elsewhere.  HIPPS_FUSED_BN=0 restores the eager MIOpen path for A/B runs.
@@ -40,6 +41,10 @@ _FUSED_WGRAD = _os.environ.get("HIPPS_FUSED_WGRAD", "1") != "0"
 _FUSED_STEM = _FUSED
 # stem BN apply + ReLU folded into the max pool's load (the BN output is never materialised)
 _FUSED_STEM_POOL = _FUSED_STEM and _os.environ.get("HIPPS_FUSED_STEMPOOL", "1") != "0"
+# ... and the stem's backward as one pass pair (no pool / BN input gradients materialised).
+# Opt-in: it moves 1.9 GB/step less, but the recomputed pool gather in the weight gradient's dy
+# staging is latency-bound (A/B on one box: 10308 on / 10342 off img/s, profiles/ab_r2/stembwd_*)
+_FUSED_STEM_BWD = _FUSED_STEM_POOL and _os.environ.get("HIPPS_FUSED_STEMBWD", "0") != "0"
 _FUSED_PRO = _FUSED_CONV and _os.environ.get("HIPPS_FUSED_PRO", "0") != "0"
 
 
@@ -152,8 +157,11 @@ class ResNet(nn.Module):
                     nn.init.zeros_(m.bn2.weight)
 
     def forward(self, x):
-        y, part = conv2d_stats(self.conv1, x, fuse=_FUSED_STEM)
-        x = bn_relu_maxpool(self.bn1, self.maxpool, y, part if _FUSED_STEM_POOL else None)
+        if _FUSED_STEM_BWD and stem_block_ok(self.conv1, self.bn1, self.maxpool, x):
+            x = stem_block(self.conv1, self.bn1, self.maxpool, x)
+        else:
+            y, part = conv2d_stats(self.conv1, x, fuse=_FUSED_STEM)
+            x = bn_relu_maxpool(self.bn1, self.maxpool, y, part if _FUSED_STEM_POOL else None)
         for i in range(self.num_stages):
             x = getattr(self, f"layer{i + 1}")(x)
         x = global_avg_pool(x)

@@ -720,6 +720,71 @@ class _BNReluPool(torch.autograd.Function):
         return dy, None, dw, db, None, None, None, None
 
 
+class _StemBlock(torch.autograd.Function):
+    """pool(relu(bn(stem(x)))) for the ResNet stem in training mode, as one autograd node so the
+    backward never materialises the pool's or the BatchNorm's input gradient (2 x 411 MB at batch
+    256): csrc/stem.hip stem_bnpool_backward reduces the BN backward statistics on a recomputed
+    pool gradient, then the stem weight gradient stages dy = BN-backward(pool-backward(dp)) straight
+    into LDS.  Forward = _StemConv + _BNReluPool.  The image needs no gradient (checked by the
+    caller)."""
+
+    @staticmethod
+    def forward(ctx, x, w_master, bn_w, bn_b, running_mean, running_var, eps, momentum):
+        w = bf16_weight(w_master).contiguous(memory_format=torch.channels_last)
+        n, _, h, wd = x.shape
+        ho, wo = (h - 1) // 2 + 1, (wd - 1) // 2 + 1
+        y = torch.empty((n, 64, ho, wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        part = torch.empty((2, 64, native().stem_mtiles(n, ho)), dtype=torch.float32, device=x.device)
+        native().stem_forward(x, w, y, part)
+        f32 = dict(dtype=torch.float32, device=x.device)
+        mean, invstd = torch.empty(64, **f32), torch.empty(64, **f32)
+        scale, shift = torch.empty(64, **f32), torch.empty(64, **f32)
+        native().bn_finalize_partials(part, part.shape[2], n * ho * wo, bn_w, bn_b, running_mean, running_var, mean,
+                                      invstd, scale, shift, 64, float(eps), float(momentum))
+        hp, wp = (ho - 1) // 2 + 1, (wo - 1) // 2 + 1
+        out = torch.empty((n, 64, hp, wp), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        code = torch.empty(n * hp * wp * 8, dtype=torch.int32, device=x.device)
+        native().maxpool3s2_forward(y, out, code, scale, shift)
+        ctx.wdtype = w_master.dtype
+        ctx.save_for_backward(x, y, code, bn_w, mean, invstd, scale, shift)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, y, code, bn_w, mean, invstd, scale, shift = ctx.saved_tensors
+        dout = dout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dbw, dbb = torch.empty_like(bn_w), torch.empty_like(bn_w)
+        dw = torch.empty((64, 3, 7, 7), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+        native().stem_bnpool_backward(dout, code, y, x, bn_w, mean, invstd, scale, shift, dbw, dbb, dw)
+        if ctx.wdtype != torch.float32:
+            dw = dw.to(ctx.wdtype)
+        return None, dw, dbw, dbb, None, None, None, None
+
+
+def _pool_geom_ok(m) -> bool:
+    def two(v):
+        return tuple(v) if isinstance(v, (tuple, list)) else (v, v)
+
+    return (not m.return_indices and not m.ceil_mode and two(m.kernel_size) == (3, 3) and two(m.stride) == (2, 2)
+            and two(m.padding) == (1, 1) and two(m.dilation) == (1, 1))
+
+
+def stem_block_ok(conv: nn.Conv2d, bn, pool, x: torch.Tensor) -> bool:
+    """Can _StemBlock run conv -> bn (+ReLU) -> pool on this input?"""
+    return (stem_ok(conv, x) and not x.requires_grad and torch.is_grad_enabled() and conv.training and
+            isinstance(bn, FusedBatchNorm2d) and bn.training and bn.relu and bn.fused and bn.affine and
+            bn.track_running_stats and bn.momentum is not None and bn.num_features == 64 and
+            bn.weight.dtype == torch.float32 and isinstance(pool, MaxPool2d) and pool.fused and _pool_geom_ok(pool))
+
+
+def stem_block(conv: nn.Conv2d, bn, pool, x: torch.Tensor) -> torch.Tensor:
+    """pool(bn(conv(x))) on _StemBlock (callers check stem_block_ok first)."""
+    bn._nbt_pending += 1
+    xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    return _StemBlock.apply(xb, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps,
+                            bn.momentum)
+
+
 def bn_relu_maxpool(bn, pool, y, part=None):
     """pool(bn(y)) for a ReLU BatchNorm followed by the 3x3/s2 max pool (the ResNet stem); with the
     producer's partial statistics ``part`` and every piece on the fused kernels this is one pool

@@ -130,18 +130,52 @@ def test_bn_relu_pool_bit_identical_to_bn_then_pool(shape):
         assert torch.equal(a, b)
 
 
-def test_resnet_forward_uses_bn_relu_pool():
+@pytest.mark.parametrize("fused_bwd", [True, False])
+def test_resnet_stem_route(fused_bwd, monkeypatch):
+    """The ResNet stem runs _StemBlock (HIPPS_FUSED_STEMBWD=1) or _StemConv + _BNReluPool (default)."""
+    from hipps.models import resnet as R
     from hipps.models import resnet50
 
+    monkeypatch.setattr(R, "_FUSED_STEM_BWD", fused_bwd)
     m = resnet50().to(DEV).to(memory_format=torch.channels_last)
     x = _cl(torch.randn(2, 3, 64, 64, device=DEV))
     calls = []
-    orig = hnn._BNReluPool.apply
-    hnn._BNReluPool.apply = lambda *a: calls.append(1) or orig(*a)
-    try:
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            m(x).float().sum().backward()
-    finally:
-        hnn._BNReluPool.apply = orig
-    assert calls == [1]
+    for cls in (hnn._StemBlock, hnn._BNReluPool):
+        orig = cls.apply
+        monkeypatch.setattr(cls, "apply", (lambda o, c: lambda *a: calls.append(c.__name__) or o(*a))(orig, cls))
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        m(x).float().sum().backward()
+    assert calls == (["_StemBlock"] if fused_bwd else ["_BNReluPool"])
     assert m.bn1.weight.grad is not None and torch.isfinite(m.conv1.weight.grad).all()
+
+
+@pytest.mark.parametrize("n", [4, 2])
+def test_stem_block_matches_unfused_ops(n):
+    """_StemBlock (fused stem backward: BN reductions on a recomputed pool gradient, dy staged into
+    the weight gradient) vs _StemConv -> FusedBatchNorm2d -> MaxPool2d on the hipps kernels:
+    identical forward and running statistics; gradients equal up to the BN reduction order."""
+    torch.manual_seed(n)
+    x = _cl(torch.randn(n, 3, 224 if n == 4 else 96, 224 if n == 4 else 64, device=DEV).to(torch.bfloat16))
+    res = []
+    for fused in (True, False):
+        torch.manual_seed(1)
+        conv = torch.nn.Conv2d(3, 64, 7, 2, 3, bias=False).to(DEV).to(memory_format=torch.channels_last)
+        bn = hnn.FusedBatchNorm2d(64, relu=True).to(DEV)
+        with torch.no_grad():
+            bn.weight.copy_(torch.linspace(-1.5, 2.0, 64))
+            bn.bias.copy_(torch.linspace(-0.5, 0.5, 64))
+        pool = hnn.MaxPool2d(3, stride=2, padding=1)
+        if fused:
+            assert hnn.stem_block_ok(conv, bn, pool, x)
+            out = hnn.stem_block(conv, bn, pool, x)
+        else:
+            y, part = hnn._StemConv.apply(x, conv.weight, True)
+            out = pool(bn(y, stats=part))
+        g = _cl(torch.randn(out.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(2)).to(torch.bfloat16))
+        out.backward(g)
+        res.append((out.detach(), bn.running_mean, bn.running_var, bn.weight.grad, bn.bias.grad, conv.weight.grad))
+    (o1, rm1, rv1, bw1, bb1, cw1), (o2, rm2, rv2, bw2, bb2, cw2) = res
+    assert torch.equal(o1, o2) and torch.equal(rm1, rm2) and torch.equal(rv1, rv2)
+    torch.testing.assert_close(bw1, bw2, rtol=1e-4, atol=1e-4 * bw2.abs().max().item())
+    torch.testing.assert_close(bb1, bb2, rtol=1e-4, atol=1e-4 * bb2.abs().max().item())
+    torch.testing.assert_close(cw1, cw2, rtol=2e-3, atol=2e-3 * cw2.abs().max().item())
