@@ -2,7 +2,8 @@
 
 Reference (mpi4py, host bytearrays): ``igather``/``irecv`` (mpi_comms.py:60-117),
 ``ibroadcast``/``irecv1`` (:120-133), ``Iallgather`` (:144-174), ``to_mpi``/``to_mpi_v``
-(:135-141).  These are the "generic Python object" slow path the README asks for
+(:135-141), and ``ialltoallv`` (the variable-size all-to-all the reference's test module posts at
+import, test_mpi.py:14-21).  These are the "generic Python object" slow path the README asks for
 (README.md:23-27): tensors inside objects become numpy, the object is pickled + framed
 (hipps.utils.serialization), and bytes travel as uint8 tensors -- on the HIP device over RCCL
 when the process group is ``nccl``, on the host over gloo otherwise.  Gradients never take this
@@ -200,3 +201,41 @@ class Iallgather:
         (req, counts), = self.prepare([len(packaged)])
         req.Wait()
         return self.recv(*self.send(packaged, counts), cuda=cuda)
+
+
+def ialltoallv(objs: List[Any], level: int = 0):
+    """Personalised all-to-all of Python objects: ``objs[d]`` goes to rank ``d``; returns
+    ``(recv, req, sizes)`` for ``irecv_alltoallv`` (the reference posts ``comm.Ialltoallv`` on
+    pickled bytes, test_mpi.py:14-21).  One all-to-all of int64 sizes, then one variable-split
+    all-to-all of the payload (``all_to_all_single`` = ``ncclAllToAllv`` on RCCL, gloo on the host)."""
+    rank, W, _ = _world()
+    if len(objs) != W:
+        raise ValueError(f"ialltoallv: {len(objs)} objects for a world of {W} ranks")
+    dev = _dev()
+    parts = [bytes(format_for_send(o, level)[0]) for o in objs]
+    send_sizes = torch.tensor([len(b) for b in parts], dtype=torch.int64, device=dev)
+    recv_sizes = torch.empty(W, dtype=torch.int64, device=dev)
+    if W == 1:
+        recv_sizes.copy_(send_sizes)
+    else:
+        dist.all_to_all_single(recv_sizes, send_sizes)
+    rs = [int(v) for v in recv_sizes.tolist()]
+    send = _to_tensor(b"".join(parts), sum(len(b) for b in parts), dev)
+    recv = torch.empty(sum(rs), dtype=torch.uint8, device=dev)
+    if W == 1:
+        recv.copy_(send)
+        return recv, Request(), rs
+    work = dist.all_to_all_single(recv, send, output_split_sizes=rs, input_split_sizes=[len(b) for b in parts],
+                                  async_op=True)
+    return recv, Request([work], on_done=lambda: send), rs
+
+
+def irecv_alltoallv(recv: torch.Tensor, req: Request, sizes: List[int], cuda: bool = False) -> List[Any]:
+    """Complete an ialltoallv: the W objects addressed to this rank, in source-rank order."""
+    req.Wait()
+    host = recv.cpu().numpy().tobytes()
+    out, o = [], 0
+    for n in sizes:
+        out.append(unformat(host[o:o + n], cuda=cuda))
+        o += n
+    return out

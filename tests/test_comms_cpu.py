@@ -39,7 +39,12 @@ def _gather_bcast(rank, W):
         req.Wait()
         resp.append(ag.send(msg, count))
     ok_p = all([o["i"] for o in ag.recv(*r)] == [i] * W for i, r in enumerate(resp))
-    return ok_g, ok_b, ok_a, ok_p
+    # test_mpi.py:14-21 Ialltoallv: rank r sends a different-size object to each destination d
+    out = [{"src": rank, "dst": d, "pad": "y" * (100 * d + 7 * rank)} for d in range(W)]
+    got = comms.irecv_alltoallv(*comms.ialltoallv(out))
+    ok_t = [g["src"] for g in got] == list(range(W)) and all(
+        g["dst"] == rank and len(g["pad"]) == 100 * rank + 7 * g["src"] for g in got)
+    return ok_g, ok_b, ok_a, ok_p, ok_t
 
 
 @pytest.mark.parametrize("W", [2, 3])
