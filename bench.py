@@ -56,8 +56,10 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
-    ap.add_argument("--allow-fallback", action="store_true",
-                    help="if the ps_async IPC transport cannot initialise, use its p2p transport instead of failing")
+    ap.add_argument("--no-fallback", action="store_true",
+                    help="fail if the ps_async IPC transport cannot initialise (default: run the SAME async PS over "
+                         "its p2p transport -- RCCL pair send/recv -- and record that in the JSON line)")
+    ap.add_argument("--allow-fallback", action="store_true", help=argparse.SUPPRESS)  # round-1 flag, now the default
     ap.add_argument("--async-transport", default="ipc", choices=["ipc", "p2p"])
     ap.add_argument("--no-pull-overlap", action="store_true",
                     help="ps_async: one GPU-time pull of all params before the forward (A/B)")
@@ -104,8 +106,9 @@ def main():
     try:
         opt = hipps.SGD(model.named_parameters(), **kw)
     except Exception as e:
-        # opt-in: the same async PS over the two-sided (RCCL pair send/recv) transport
-        if mode != "ps_async" or N == 1 or not a.allow_fallback or a.async_transport == "p2p":
+        # the same async PS algorithm over its two-sided (RCCL pair send/recv) transport; never a
+        # different mode under the async-PS metric
+        if mode != "ps_async" or N == 1 or a.no_fallback or a.async_transport == "p2p":
             raise
         note = f"ps_async ipc transport failed ({type(e).__name__}: {e}); fell back to the p2p transport"
         print("[bench] " + note, file=sys.stderr)
@@ -194,6 +197,7 @@ def main():
                 "grad_bytes_per_step_per_worker": grad_bytes,
                 "grad_bytes_per_step_used": int(grad_used),
                 "param_wire": a.param_wire, "pull_overlap": pull_overlap,
+                "async_transport": kw.get("async_transport") if mode == "ps_async" else None,
                 "num_params": nparams,
                 "buckets": nbuckets,
             },

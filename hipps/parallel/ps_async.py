@@ -173,15 +173,32 @@ class PSAsyncEngine(Engine):
         meta = [getattr(self, "ctl_name", None), getattr(self, "mb_name", None), handle]
         if W > 1:
             dist.broadcast_object_list(meta, src=0)
+        map_err = None
         if self.rank != 0:
             self.ctl_name, self.mb_name, handle = meta
-            self.ctl = C.ControlBlock(self.ctl_name, W, False)
-            if self.p2p:
-                self.mem = None
-            elif self.cuda:
-                self.mailbox = C.DeviceMailbox(handle, total)
-            else:
-                self.mailbox = C.HostMailbox(self.mb_name, total, False)
+            try:
+                self.ctl = C.ControlBlock(self.ctl_name, W, False)
+                if self.p2p:
+                    self.mem = None
+                elif self.cuda:
+                    self.mailbox = C.DeviceMailbox(handle, total)
+                else:
+                    self.mailbox = C.HostMailbox(self.mb_name, total, False)
+            except Exception as e:  # e.g. hipIpcOpenMemHandle refused across devices
+                map_err = f"rank {self.rank}: {type(e).__name__}: {e}"
+        if W > 1:
+            # agree before the barrier: a rank that cannot map must not leave the others waiting,
+            # and every rank raises together (bench.py then rebuilds the engine on 'p2p')
+            errs = [None] * W
+            dist.all_gather_object(errs, map_err)
+            errs = [e for e in errs if e]
+            if errs:
+                self.remove_hooks()
+                if self.rank == 0:
+                    self.ctl.unlink()
+                    if not self.cuda and self.mailbox is not None:
+                        self.mailbox.unlink()
+                raise RuntimeError("ps_async ipc transport: mapping the PS mailbox failed (" + "; ".join(errs) + ")")
         barrier(world)
         if self.rank == 0:  # everyone has mapped: remove the names (no /dev/shm leftovers)
             self.ctl.unlink()
@@ -252,7 +269,16 @@ class PSAsyncEngine(Engine):
             self.irequest_params(block_for=0)
             if self.cuda:
                 torch.cuda.current_stream(store.device).synchronize()
-            self._self_test()
+            try:
+                self._self_test()
+            except RuntimeError:
+                # collective failure (every rank raises): stop the PS thread and drop the hooks so
+                # a replacement engine can be built on the same model
+                try:
+                    self.close()
+                except Exception:
+                    pass
+                raise
 
     def _self_test(self):
         """Prove both directions of the one-sided transport before training starts: every rank

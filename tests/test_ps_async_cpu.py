@@ -116,3 +116,48 @@ def test_async_p2p_max_delay_zero_matches_ipc():
     for r in range(2):
         for x, y in zip(a[r]["params"], b[r]["params"]):
             torch.testing.assert_close(x, y, rtol=0, atol=0)
+
+
+def _ipc_fails_then_p2p(rank, world):
+    """Rank 1 cannot map the PS mailbox: every rank must raise together (nobody left in a barrier),
+    the failed engine must leave no hooks behind, and the same async PS then trains over 'p2p' --
+    the recovery bench.py performs at N > 1."""
+    import hipps
+    from hipps.ops import _native
+
+    C = _native.native()
+    m = _mlp()
+    if rank == 1:
+        real = C.HostMailbox
+
+        class Refuse:
+            def __init__(self, name, total, create):
+                if not create:
+                    raise OSError("simulated: mailbox mapping refused")
+                self._m = real(name, total, create)
+
+        C.HostMailbox = Refuse
+    err = None
+    try:
+        hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", code="fp32")
+    except RuntimeError as e:
+        err = str(e)
+    finally:
+        if rank == 1:
+            C.HostMailbox = real
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", code="fp32",
+                    async_transport="p2p")
+    for s in range(3):
+        x, y = _data(rank, s)
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x), y).backward()
+        opt.step()
+    eng = opt.engine
+    opt.close()
+    return {"err": err, "stats": eng.ps_stats() if rank == 0 else None}
+
+
+def test_ipc_mapping_failure_is_collective_and_p2p_recovers():
+    out = run_world(_ipc_fails_then_p2p, 2)
+    assert all(o["err"] and "mapping the PS mailbox failed" in o["err"] and "rank 1" in o["err"] for o in out), out
+    assert out[0]["stats"]["accumulated"] == 2 * 3
