@@ -116,3 +116,26 @@ def test_global_avg_pool_channels_last_backward():
     torch.flatten(torch.nn.functional.adaptive_avg_pool2d(x2, 1), 1).backward(g)
     torch.testing.assert_close(x.grad, x2.grad)
     assert x.grad.is_contiguous(memory_format=torch.channels_last)
+
+
+def test_stem_routing_predicates():
+    """The hipps stem path is taken only for the ResNet stem geometry on a GPU tensor (CPU tensors,
+    other convolutions, odd widths and eval-mode BNs stay on the library / module path), and the
+    CPU model still trains through the module fallbacks."""
+    import torch.nn as nn
+
+    from hipps.models import resnet50
+    from hipps.ops import nn as hnn
+
+    stem = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+    x = torch.randn(2, 3, 224, 224)
+    assert not hnn.stem_ok(stem, x)  # CPU tensor
+    assert not hnn.stem_ok(nn.Conv2d(3, 64, 3, stride=2, padding=1, bias=False), x)
+    assert not hnn.stem_ok(nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=True), x)
+    bn, pool = hnn.FusedBatchNorm2d(64, relu=True), hnn.MaxPool2d(3, stride=2, padding=1)
+    assert not hnn.stem_block_ok(stem, bn, pool, x)
+    assert hnn._pool_geom_ok(pool) and not hnn._pool_geom_ok(nn.MaxPool2d(2, 2))
+    m = resnet50(num_classes=10)
+    out = m(torch.randn(2, 3, 64, 64))
+    out.sum().backward()
+    assert m.conv1.weight.grad is not None and m.bn1.weight.grad is not None
