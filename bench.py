@@ -129,8 +129,10 @@ def main():
         return loss, data
 
     first_loss = None
+    losses = []  # device scalars; read after the timed region (no host sync inside it)
     for _ in range(a.warmup):
         loss, _ = step()
+        losses.append(loss.detach())
         if first_loss is None:
             first_loss = float(loss.float().item())
     tr = opt.engine.tracer  # HIPPS_TRACE=1: per-phase device ms (HIP events), excluded from warmup
@@ -144,6 +146,7 @@ def main():
     last = None
     for _ in range(a.steps):
         loss, last = step()
+        losses.append(loss.detach())
     torch.cuda.synchronize()
     hdist.barrier(world)
     t1 = time.perf_counter()
@@ -203,6 +206,9 @@ def main():
             },
             "first_loss": None if first_loss is None else round(first_loss, 4),
             "final_loss": round(final_loss, 4),
+            # every 5th step's loss (warmup included), read back after timing
+            "loss_every5": [round(float(v.float()), 4) for v in losses[::5]],
+            "staleness_last": last.get("staleness") if last else None,
             "ps": {k: (int(v) if isinstance(v, (int, float)) else v) for k, v in stats.items()},
         }
         if trace:

@@ -42,6 +42,13 @@ class PSConfig:
     async_transport: str = "ipc"
     # async PS: scale a kept gradient by 1/max(1, staleness) (staleness-aware async SGD)
     staleness_lr: bool = False
+    # async PS look-ahead publish (delay-compensated momentum): workers read the parameters
+    # extrapolated by the momentum of the next tau updates, the tau updates their gradient will
+    # arrive late by; the PS master is unchanged.  -1 = auto (tau = mean measured staleness of the
+    # recent accumulated steps; off when max_delay == 0), 0 = off, > 0 = fixed tau
+    stale_lookahead: float = -1.0
+    # samples per worker step (e.g. the batch size): adds samples_per_sec to step() data
+    samples_per_step: int = 0
     # async PS failure detection: a worker silent for this long (no heartbeat, no STOP) is dead
     dead_after_s: float = 60.0
     # async PS mailbox: bucket messages in flight per worker (0 = auto: min(2*buckets, mailbox_mb))

@@ -9,11 +9,12 @@ void gather_flat(const std::vector<at::Tensor>& srcs, at::Tensor table, at::Tens
 void transpose_cast(at::Tensor src, at::Tensor dst, at::Tensor tiles);
 void sgd_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p, c10::optional<at::Tensor> buf,
               c10::optional<at::Tensor> pub, bool zero_src, double lr, double wd, double momentum, double dampening,
-              bool nesterov, bool first, c10::optional<at::Tensor> mask);
+              bool nesterov, bool first, c10::optional<at::Tensor> mask, c10::optional<at::Tensor> csteps,
+              double lookahead);
 void adam_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p, at::Tensor exp_avg,
                at::Tensor exp_avg_sq, c10::optional<at::Tensor> max_exp_avg_sq, c10::optional<at::Tensor> pub,
                bool zero_src, double lr, double beta1, double beta2, double eps, double wd, int64_t step,
-               bool amsgrad, bool torch_mode, c10::optional<at::Tensor> mask);
+               bool amsgrad, bool torch_mode, c10::optional<at::Tensor> mask, c10::optional<at::Tensor> csteps);
 // quant.hip
 void q8_encode(at::Tensor x, c10::optional<at::Tensor> resid, at::Tensor q, at::Tensor scales, bool stochastic,
                int64_t seed);
@@ -106,13 +107,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("gscale"), pybind11::arg("p"), pybind11::arg("buf"), pybind11::arg("pub"),
         pybind11::arg("zero_src"), pybind11::arg("lr"), pybind11::arg("wd"), pybind11::arg("momentum"),
         pybind11::arg("dampening"), pybind11::arg("nesterov"), pybind11::arg("first"),
-        pybind11::arg("mask") = pybind11::none());
+        pybind11::arg("mask") = pybind11::none(), pybind11::arg("csteps") = pybind11::none(),
+        pybind11::arg("lookahead") = 0.0);
   m.def("adam_step", &hipps::adam_step, "fused decode+sum+Adam (reference ps.py:217-261 math)",
         pybind11::arg("grads"), pybind11::arg("gscale"), pybind11::arg("p"), pybind11::arg("exp_avg"),
         pybind11::arg("exp_avg_sq"), pybind11::arg("max_exp_avg_sq"), pybind11::arg("pub"), pybind11::arg("zero_src"),
         pybind11::arg("lr"), pybind11::arg("beta1"), pybind11::arg("beta2"), pybind11::arg("eps"), pybind11::arg("wd"),
         pybind11::arg("step"), pybind11::arg("amsgrad"), pybind11::arg("torch_mode"),
-        pybind11::arg("mask") = pybind11::none());
+        pybind11::arg("mask") = pybind11::none(), pybind11::arg("csteps") = pybind11::none());
   m.def("q8_encode", &hipps::q8_encode, "per-256-block absmax int8 quantization (+EF, +stochastic)");
   m.def("q8_aggregate", &hipps::q8_aggregate, "acc (+)= gscale * sum_w dequant(q_w, s_w)");
   m.def("topk_encode", &hipps::topk_encode, "exact top-k |g| (radix select) -> idx asc, val");

@@ -23,6 +23,7 @@ namespace hipps {
 struct SgdHp {
   float lr, wd, mom, damp;
   int nesterov, first;
+  float la;  // look-ahead publish: pub = p - la * buf (delay-compensated async read, 0 = off)
 };
 
 __device__ __forceinline__ float sgd1(float& p, float& b, float d, const SgdHp& h, bool has_buf) {
@@ -37,8 +38,16 @@ __device__ __forceinline__ float sgd1(float& p, float& b, float d, const SgdHp& 
 
 struct AdamHp {
   float lr, b1, b2, eps, wd, step_size, bc2_sqrt;
-  int amsgrad, torch_mode;
+  int amsgrad, torch_mode, step;
 };
+
+// bias-correction scalars for step t, in double like the host launcher (a chunk whose own step
+// count equals the group's uses the host's values unchanged, so both paths agree bit for bit)
+__device__ __forceinline__ void adam_bias(AdamHp& h, int t) {
+  const double bc1 = 1.0 - pow((double)h.b1, (double)t), bc2 = 1.0 - pow((double)h.b2, (double)t);
+  h.step_size = (float)(h.torch_mode ? (double)h.lr / bc1 : (double)h.lr * sqrt(bc2) / bc1);
+  h.bc2_sqrt = (float)sqrt(bc2);
+}
 
 __device__ __forceinline__ float adam1(float& p, float& m, float& v, float* vmax, float g, const AdamHp& h) {
   if (h.wd != 0.f) g = fmaf(h.wd, p, g);
@@ -54,6 +63,14 @@ __device__ __forceinline__ float adam1(float& p, float& m, float& v, float* vmax
   float denom = h.torch_mode ? (sqrtf(vv) / h.bc2_sqrt + h.eps) : (sqrtf(vv) + h.eps);
   p = fmaf(-h.step_size, m / denom, p);
   return p;
+}
+
+// Look-ahead publish for asynchronous readers (delay-compensated momentum, cf. DANA, Hakimi et
+// al. 2019): a worker's gradient lands tau updates after the version it read, and those updates
+// carry at least the momentum part lr * (mu + ... + mu^tau) * buf, so the PS publishes the
+// parameters extrapolated by it; the fp32 master itself is unchanged.
+__device__ __forceinline__ float4 lookahead4(float4 p, float4 b, float la) {
+  return make_float4(fmaf(-la, b.x, p.x), fmaf(-la, b.y, p.y), fmaf(-la, b.z, p.z), fmaf(-la, b.w, p.w));
 }
 
 template <typename T>
@@ -142,7 +159,8 @@ __global__ __launch_bounds__(kBlock) void k_convert(const Tin* __restrict__ src,
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_sgd(SlotPtrs g, int W, float gscale, float* __restrict__ p,
                                                 float* __restrict__ buf, void* __restrict__ pub, int pub_mode,
-                                                int zero_src, int64_t n, SgdHp h, const uint8_t* __restrict__ cmask) {
+                                                int zero_src, int64_t n, SgdHp h, const uint8_t* __restrict__ cmask,
+                                                int* __restrict__ cstep) {
   const bool has_buf = buf != nullptr;
   const int64_t nv = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
@@ -150,19 +168,26 @@ __global__ __launch_bounds__(kBlock) void k_sgd(SlotPtrs g, int W, float gscale,
     float4 pv = Vec4<float>::load(p, i);
     if (cmask && !cmask[i >> 4]) {  // parameter without a gradient this step: untouched (ps.py:178-179)
       if (zero_src) Vec4<float>::store((float*)g.p[0], i, make_float4(0.f, 0.f, 0.f, 0.f));
+      if (h.la != 0.f && has_buf) pv = lookahead4(pv, Vec4<float>::load(buf, i), h.la);
       pub_store4(pub, pub_mode, i, pv);
       continue;
     }
     float4 d = sum_slots4<T>(g, W, i, gscale);
     if (zero_src) Vec4<float>::store((float*)g.p[0], i, make_float4(0.f, 0.f, 0.f, 0.f));
-    float4 b = has_buf && !h.first ? Vec4<float>::load(buf, i) : make_float4(0.f, 0.f, 0.f, 0.f);
-    sgd1(pv.x, b.x, d.x, h, has_buf);
-    sgd1(pv.y, b.y, d.y, h, has_buf);
-    sgd1(pv.z, b.z, d.z, h, has_buf);
-    sgd1(pv.w, b.w, d.w, h, has_buf);
+    SgdHp hc = h;
+    if (cstep) {  // per-parameter first step (ps.py:203-205): this chunk's own update count
+      const int cs = cstep[i >> 4];
+      hc.first = cs == 0;
+      if ((i & 15) == 0) cstep[i >> 4] = cs + 1;  // one lane per chunk; n % 16 == 0 (host check)
+    }
+    float4 b = has_buf && !hc.first ? Vec4<float>::load(buf, i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    sgd1(pv.x, b.x, d.x, hc, has_buf);
+    sgd1(pv.y, b.y, d.y, hc, has_buf);
+    sgd1(pv.z, b.z, d.z, hc, has_buf);
+    sgd1(pv.w, b.w, d.w, hc, has_buf);
     Vec4<float>::store(p, i, pv);
     if (has_buf && h.mom != 0.f) Vec4<float>::store(buf, i, b);
-    pub_store4(pub, pub_mode, i, pv);
+    pub_store4(pub, pub_mode, i, h.la != 0.f && has_buf ? lookahead4(pv, b, h.la) : pv);
   }
   if (blockIdx.x == 0) {
     for (int64_t i = (nv << 2) + threadIdx.x; i < n; i += blockDim.x) {
@@ -170,14 +195,14 @@ __global__ __launch_bounds__(kBlock) void k_sgd(SlotPtrs g, int W, float gscale,
       if (zero_src) ((float*)g.p[0])[i] = 0.f;
       float pv = p[i];
       if (cmask && !cmask[i >> 4]) {
-        pub_store1(pub, pub_mode, i, pv);
+        pub_store1(pub, pub_mode, i, h.la != 0.f && has_buf ? fmaf(-h.la, buf[i], pv) : pv);
         continue;
       }
       float b = has_buf && !h.first ? buf[i] : 0.f;
       sgd1(pv, b, d, h, has_buf);
       p[i] = pv;
       if (has_buf && h.mom != 0.f) buf[i] = b;
-      pub_store1(pub, pub_mode, i, pv);
+      pub_store1(pub, pub_mode, i, h.la != 0.f && has_buf ? fmaf(-h.la, b, pv) : pv);
     }
   }
 }
@@ -186,7 +211,8 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void k_adam(SlotPtrs g, int W, float gscale, float* __restrict__ p,
                                                  float* __restrict__ m, float* __restrict__ vv,
                                                  float* __restrict__ vmax, void* __restrict__ pub, int pub_mode,
-                                                 int zero_src, int64_t n, AdamHp h, const uint8_t* __restrict__ cmask) {
+                                                 int zero_src, int64_t n, AdamHp h, const uint8_t* __restrict__ cmask,
+                                                 int* __restrict__ cstep) {
   const int64_t nv = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
   float dummy = 0.f;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
@@ -200,10 +226,16 @@ __global__ __launch_bounds__(kBlock) void k_adam(SlotPtrs g, int W, float gscale
     if (zero_src) Vec4<float>::store((float*)g.p[0], i, make_float4(0.f, 0.f, 0.f, 0.f));
     float4 pv = Vec4<float>::load(p, i), mv = Vec4<float>::load(m, i), sv = Vec4<float>::load(vv, i);
     float4 xv = h.amsgrad ? Vec4<float>::load(vmax, i) : make_float4(0.f, 0.f, 0.f, 0.f);
-    adam1(pv.x, mv.x, sv.x, &xv.x, d.x, h);
-    adam1(pv.y, mv.y, sv.y, &xv.y, d.y, h);
-    adam1(pv.z, mv.z, sv.z, &xv.z, d.z, h);
-    adam1(pv.w, mv.w, sv.w, &xv.w, d.w, h);
+    AdamHp hc = h;
+    if (cstep) {  // per-parameter step (ps.py:241): a late-starting parameter is corrected for its own t
+      const int t = cstep[i >> 4] + 1;
+      if (t != h.step) adam_bias(hc, t);
+      if ((i & 15) == 0) cstep[i >> 4] = t;
+    }
+    adam1(pv.x, mv.x, sv.x, &xv.x, d.x, hc);
+    adam1(pv.y, mv.y, sv.y, &xv.y, d.y, hc);
+    adam1(pv.z, mv.z, sv.z, &xv.z, d.z, hc);
+    adam1(pv.w, mv.w, sv.w, &xv.w, d.w, hc);
     Vec4<float>::store(p, i, pv);
     Vec4<float>::store(m, i, mv);
     Vec4<float>::store(vv, i, sv);
@@ -332,6 +364,17 @@ const uint8_t* cmask_of(const c10::optional<at::Tensor>& mask, int64_t n) {
   return mask->data_ptr<uint8_t>();
 }
 
+// per-chunk update counts (int32, one per 16 elements): the per-parameter optimizer step of
+// ps.py:203-205 (momentum first step) and ps.py:241 (Adam state['step'])
+int* csteps_of(const c10::optional<at::Tensor>& cs, int64_t n) {
+  if (!cs.has_value() || !cs->defined()) return nullptr;
+  TORCH_CHECK(cs->is_cuda() && cs->is_contiguous() && cs->scalar_type() == at::kInt,
+              "csteps must be a contiguous int32 device tensor");
+  TORCH_CHECK(n % 16 == 0 && cs->numel() == n / 16, "csteps must hold one count per 16-element chunk of a "
+              "16-aligned range (", cs->numel(), " vs n=", n, ")");
+  return cs->data_ptr<int>();
+}
+
 int pub_mode_of(const c10::optional<at::Tensor>& pub, int64_t n) {
   if (!pub.has_value() || !pub->defined()) return 0;
   check_dev(*pub, "publish");
@@ -420,7 +463,8 @@ void transpose_cast(at::Tensor src, at::Tensor dst, at::Tensor tiles) {
 
 void sgd_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p, c10::optional<at::Tensor> buf,
               c10::optional<at::Tensor> pub, bool zero_src, double lr, double wd, double momentum, double dampening,
-              bool nesterov, bool first, c10::optional<at::Tensor> mask) {
+              bool nesterov, bool first, c10::optional<at::Tensor> mask, c10::optional<at::Tensor> csteps,
+              double lookahead) {
   check_dev(p, "param");
   TORCH_CHECK(p.scalar_type() == at::kFloat, "param master must be float32");
   const int64_t n = p.numel();
@@ -436,22 +480,24 @@ void sgd_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p,
   TORCH_CHECK(!zero_src || (grads.size() == 1 && wt == WireT::F32), "zero_src needs a single fp32 source");
   const int pm = pub_mode_of(pub, n);
   void* pp = pm ? pub->data_ptr() : nullptr;
-  SgdHp h{(float)lr, (float)wd, (float)momentum, (float)dampening, (int)nesterov, (int)first};
+  SgdHp h{(float)lr, (float)wd, (float)momentum, (float)dampening, (int)nesterov, (int)first, (float)lookahead};
+  TORCH_CHECK(lookahead == 0.0 || bp != nullptr, "a look-ahead publish needs the momentum buffer");
   const uint8_t* cm = cmask_of(mask, n);
+  int* cs = csteps_of(csteps, n);
   auto stream = c10::hip::getCurrentHIPStream();
   const int grid = grid_for(n >> 2);
   if (wt == WireT::F32)
     hipLaunchKernelGGL(k_sgd<float>, grid, kBlock, 0, stream, s, (int)grads.size(), (float)gscale,
-                       p.data_ptr<float>(), bp, pp, pm, (int)zero_src, n, h, cm);
+                       p.data_ptr<float>(), bp, pp, pm, (int)zero_src, n, h, cm, cs);
   else
     hipLaunchKernelGGL(k_sgd<uint16_t>, grid, kBlock, 0, stream, s, (int)grads.size(), (float)gscale,
-                       p.data_ptr<float>(), bp, pp, pm, (int)zero_src, n, h, cm);
+                       p.data_ptr<float>(), bp, pp, pm, (int)zero_src, n, h, cm, cs);
 }
 
 void adam_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p, at::Tensor exp_avg,
                at::Tensor exp_avg_sq, c10::optional<at::Tensor> max_exp_avg_sq, c10::optional<at::Tensor> pub,
                bool zero_src, double lr, double beta1, double beta2, double eps, double wd, int64_t step,
-               bool amsgrad, bool torch_mode, c10::optional<at::Tensor> mask) {
+               bool amsgrad, bool torch_mode, c10::optional<at::Tensor> mask, c10::optional<at::Tensor> csteps) {
   check_dev(p, "param");
   check_dev(exp_avg, "exp_avg");
   check_dev(exp_avg_sq, "exp_avg_sq");
@@ -471,18 +517,19 @@ void adam_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p
   const double bc1 = 1.0 - std::pow(beta1, (double)step), bc2 = 1.0 - std::pow(beta2, (double)step);
   const double step_size = torch_mode ? lr / bc1 : lr * std::sqrt(bc2) / bc1;
   AdamHp h{(float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, (float)step_size, (float)std::sqrt(bc2),
-           (int)amsgrad, (int)torch_mode};
+           (int)amsgrad, (int)torch_mode, (int)step};
   const uint8_t* cm = cmask_of(mask, n);
+  int* cs = csteps_of(csteps, n);
   auto stream = c10::hip::getCurrentHIPStream();
   const int grid = grid_for(n >> 2);
   if (wt == WireT::F32)
     hipLaunchKernelGGL(k_adam<float>, grid, kBlock, 0, stream, s, (int)grads.size(), (float)gscale,
                        p.data_ptr<float>(), exp_avg.data_ptr<float>(), exp_avg_sq.data_ptr<float>(), xp, pp, pm,
-                       (int)zero_src, n, h, cm);
+                       (int)zero_src, n, h, cm, cs);
   else
     hipLaunchKernelGGL(k_adam<uint16_t>, grid, kBlock, 0, stream, s, (int)grads.size(), (float)gscale,
                        p.data_ptr<float>(), exp_avg.data_ptr<float>(), exp_avg_sq.data_ptr<float>(), xp, pp, pm,
-                       (int)zero_src, n, h, cm);
+                       (int)zero_src, n, h, cm, cs);
 }
 
 }  // namespace hipps

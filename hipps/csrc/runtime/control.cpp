@@ -59,6 +59,8 @@ struct alignas(64) RankRec {
   std::atomic<int64_t> reading;            // version whose publish buffer this rank is copying (-1 none)
   std::atomic<int64_t> pull_req;           // p2p transport: parameter requests posted by this worker
   std::atomic<int64_t> sent_ver;           // p2p transport: version the PS sent for the last request
+  std::atomic<int64_t> last_stale;         // staleness (updates) of this worker's newest consumed step
+  std::atomic<int64_t> last_stale_seq;     // ... and that step's last message seq
 };
 
 struct alignas(64) Header {
@@ -75,7 +77,8 @@ struct alignas(64) Header {
 
 enum Field : int {
   PUSH_SEQ = 0, ACK_SEQ = 1, PUSH_VER = 2, APPLIED_VER = 3, STOP = 4, HEARTBEAT = 5, INCL_SEQ = 6,
-  PUSH_FLAG = 7, READING = 8, PULL_REQ = 9, PUB_VER = 10, PS_STOP = 11, ERROR = 12, DROPS = 13, UPDATES = 14, BUF_VER = 15, SENT_VER = 16
+  PUSH_FLAG = 7, READING = 8, PULL_REQ = 9, PUB_VER = 10, PS_STOP = 11, ERROR = 12, DROPS = 13, UPDATES = 14, BUF_VER = 15, SENT_VER = 16,
+  LAST_STALE = 17, LAST_STALE_SEQ = 18
 };
 
 static int64_t now_ns() {
@@ -152,6 +155,8 @@ class ControlBlock {
       case READING: return &rec(idx).reading;
       case PULL_REQ: return &rec(idx).pull_req;
       case SENT_VER: return &rec(idx).sent_ver;
+      case LAST_STALE: return &rec(idx).last_stale;
+      case LAST_STALE_SEQ: return &rec(idx).last_stale_seq;
       case PUB_VER: return &h_->pub_ver;
       case PS_STOP: return &h_->ps_stop;
       case ERROR: return &h_->error;
@@ -347,6 +352,8 @@ void bind_control(py::module& m) {
   m.attr("F_DROPS") = (int)DROPS;
   m.attr("F_UPDATES") = (int)UPDATES;
   m.attr("F_BUF_VER") = (int)BUF_VER;
+  m.attr("F_LAST_STALE") = (int)LAST_STALE;
+  m.attr("F_LAST_STALE_SEQ") = (int)LAST_STALE_SEQ;
 }
 
 }  // namespace rt

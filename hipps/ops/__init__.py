@@ -39,30 +39,36 @@ def convert(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0):
 def sgd_step(grads: Sequence[torch.Tensor], p: torch.Tensor, buf: Optional[torch.Tensor] = None,
              pub: Optional[torch.Tensor] = None, zero_src: bool = False, gscale: float = 1.0, lr: float = 0.0,
              weight_decay: float = 0.0, momentum: float = 0.0, dampening: float = 0.0, nesterov: bool = False,
-             first: bool = False, mask: Optional[torch.Tensor] = None):
+             first: bool = False, mask: Optional[torch.Tensor] = None, csteps: Optional[torch.Tensor] = None,
+             lookahead: float = 0.0):
     """Fused decode + sum_W + SGD (reference ps.py:197-214) + optional publish copy.  ``mask``
     (uint8, one byte per 16 elements) leaves chunks with a 0 byte untouched (params without a
-    gradient, ps.py:178-179)."""
+    gradient, ps.py:178-179).  ``csteps`` (int32 per 16-element chunk) makes the first-step rule
+    per parameter (buf = d_p where the chunk's count is 0) and counts the chunks it updates.
+    ``lookahead`` c != 0 writes ``pub = p - c * buf`` (look-ahead publish for async readers)."""
     if _dev(p):
         return native().sgd_step(list(grads), float(gscale), p, buf, pub, bool(zero_src), float(lr),
                                  float(weight_decay), float(momentum), float(dampening), bool(nesterov), bool(first),
-                                 mask)
+                                 mask, csteps, float(lookahead))
     return ref.sgd_step(list(grads), p, buf, pub, zero_src, gscale, lr, weight_decay, momentum, dampening,
-                        nesterov, first, mask)
+                        nesterov, first, mask, csteps, lookahead)
 
 
 def adam_step(grads: Sequence[torch.Tensor], p: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor,
               max_exp_avg_sq: Optional[torch.Tensor] = None, pub: Optional[torch.Tensor] = None,
               zero_src: bool = False, gscale: float = 1.0, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
               weight_decay: float = 0.0, step: int = 1, amsgrad: bool = False, torch_mode: bool = False,
-              mask: Optional[torch.Tensor] = None):
-    """Fused decode + sum_W + Adam (reference ps.py:217-261 eps placement unless torch_mode)."""
+              mask: Optional[torch.Tensor] = None, csteps: Optional[torch.Tensor] = None):
+    """Fused decode + sum_W + Adam (reference ps.py:217-261 eps placement unless torch_mode).
+    ``csteps`` (int32 per 16-element chunk): per-parameter step t = count + 1 for the bias
+    correction (ps.py:241), advanced for the chunks it updates; ``step`` is then only the hint
+    for the common t (chunks at that t use the host-computed scalars)."""
     if _dev(p):
         return native().adam_step(list(grads), float(gscale), p, exp_avg, exp_avg_sq, max_exp_avg_sq, pub,
                                   bool(zero_src), float(lr), float(betas[0]), float(betas[1]), float(eps),
-                                  float(weight_decay), int(step), bool(amsgrad), bool(torch_mode), mask)
+                                  float(weight_decay), int(step), bool(amsgrad), bool(torch_mode), mask, csteps)
     return ref.adam_step(list(grads), p, exp_avg, exp_avg_sq, max_exp_avg_sq, pub, zero_src, gscale, lr, betas, eps,
-                         weight_decay, step, amsgrad, torch_mode, mask)
+                         weight_decay, step, amsgrad, torch_mode, mask, csteps)
 
 
 def q8_encode(x, resid, q, scales, stochastic: bool = False, seed: int = 0):

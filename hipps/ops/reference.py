@@ -59,9 +59,39 @@ def _masked(mask, n, fn, *bufs):
             b[keep] = s
 
 
+def _chunk_groups(mask, csteps, key):
+    """Split the chunks this step updates (mask byte != 0, or all) by ``key(count)`` -> list of
+    (key value, chunk mask) so each group runs the scalar-hyper-parameter formula."""
+    live = torch.ones_like(csteps, dtype=torch.bool) if mask is None else mask[: csteps.numel()].to(torch.bool)
+    keys = key(csteps)
+    out = []
+    for kv in sorted(set(keys[live].tolist())):
+        out.append((kv, (live & (keys == kv)).to(torch.uint8)))
+    return live, out
+
+
 def sgd_step(grads, p, buf=None, pub=None, zero_src=False, gscale=1.0, lr=0.0, weight_decay=0.0, momentum=0.0,
-             dampening=0.0, nesterov=False, first=False, mask=None):
-    """Reference SGD (ps.py:197-214) on flat fp32 buffers; masked chunks are left untouched."""
+             dampening=0.0, nesterov=False, first=False, mask=None, csteps=None, lookahead=0.0):
+    """Reference SGD (ps.py:197-214) on flat fp32 buffers; masked chunks are left untouched.
+    ``csteps``: per-chunk update counts -- first step (buf = d_p) where the count is 0.
+    ``lookahead`` c: the published copy is ``p - c * buf``."""
+    if lookahead:
+        sgd_step(grads, p, buf, None, zero_src, gscale, lr, weight_decay, momentum, dampening, nesterov, first, mask,
+                 csteps)
+        if pub is not None:
+            pub.copy_(p.add(buf, alpha=-lookahead).to(pub.dtype))
+        return
+    if csteps is not None:
+        live, groups = _chunk_groups(mask, csteps, lambda c: (c == 0).to(torch.int32))
+        for is_first, m in groups:
+            sgd_step(grads, p, buf, None, False, gscale, lr, weight_decay, momentum, dampening, nesterov,
+                     bool(is_first), m)
+        csteps[live] += 1
+        if zero_src:
+            grads[0].zero_()
+        if pub is not None:
+            pub.copy_(p.to(pub.dtype))
+        return
     if mask is not None:
         _masked(mask, p.numel(), lambda: sgd_step(grads, p, buf, None, zero_src, gscale, lr, weight_decay, momentum,
                                                   dampening, nesterov, first), p, buf)
@@ -89,8 +119,21 @@ def sgd_step(grads, p, buf=None, pub=None, zero_src=False, gscale=1.0, lr=0.0, w
 
 
 def adam_step(grads, p, exp_avg, exp_avg_sq, max_exp_avg_sq=None, pub=None, zero_src=False, gscale=1.0, lr=1e-3,
-              betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, step=1, amsgrad=False, torch_mode=False, mask=None):
-    """Reference Adam (ps.py:217-261): denom = sqrt(v) + eps; step = lr*sqrt(bc2)/bc1."""
+              betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, step=1, amsgrad=False, torch_mode=False, mask=None,
+              csteps=None):
+    """Reference Adam (ps.py:217-261): denom = sqrt(v) + eps; step = lr*sqrt(bc2)/bc1.
+    ``csteps``: per-chunk update counts -- each chunk is corrected for its own t = count + 1."""
+    if csteps is not None:
+        live, groups = _chunk_groups(mask, csteps, lambda c: c + 1)
+        for t, m in groups:
+            adam_step(grads, p, exp_avg, exp_avg_sq, max_exp_avg_sq, None, False, gscale, lr, betas, eps,
+                      weight_decay, int(t), amsgrad, torch_mode, m)
+        csteps[live] += 1
+        if zero_src:
+            grads[0].zero_()
+        if pub is not None:
+            pub.copy_(p.to(pub.dtype))
+        return
     if mask is not None:
         _masked(mask, p.numel(), lambda: adam_step(grads, p, exp_avg, exp_avg_sq, max_exp_avg_sq, None, zero_src,
                                                    gscale, lr, betas, eps, weight_decay, step, amsgrad, torch_mode),

@@ -145,6 +145,20 @@ class MPI_PS(torch.optim.Optimizer):
         """Flat optimizer state; per-param torch-compatible views in self.state."""
         self.flat_state: Dict[str, torch.Tensor] = {}
         self._group_steps = [0] * len(self.param_groups)
+        # per-16-element-chunk update counts (int32; a chunk never straddles two parameters): the
+        # reference's per-parameter optimizer state -- momentum buffer created on a parameter's
+        # first gradient (ps.py:202-205), Adam state['step'] advanced only when the parameter has
+        # a gradient (ps.py:178-179, 241).  The fused kernels read and advance them under the
+        # chunk mask, so a parameter that starts late gets its own first step.
+        self.chunk_steps: Optional[torch.Tensor] = None
+
+    def _csteps(self) -> Optional[torch.Tensor]:
+        if self.chunk_steps is None and self._needs_csteps():
+            self.chunk_steps = torch.zeros(self.store.nchunks, dtype=torch.int32, device=self.store.device)
+        return self.chunk_steps
+
+    def _needs_csteps(self) -> bool:
+        return True
 
     def _ensure_state(self, key: str) -> torch.Tensor:
         if key not in self.flat_state:
@@ -155,12 +169,14 @@ class MPI_PS(torch.optim.Optimizer):
         return self.flat_state[key]
 
     def _update_flat(self, sources: List[torch.Tensor], target: torch.Tensor, gscale: float, zero_src: bool = False,
-                     pub: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None):
+                     pub: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None, lookahead: float = 0.0):
         """Apply the optimizer to flat ``target`` from flat gradient ``sources`` (summed).
         ``mask`` (uint8 per 16-element chunk, FlatStore.chunk_mask) skips the parameters that
-        produced no gradient this step, like ``if p.grad is None: continue`` (ps.py:178-179)."""
+        produced no gradient this step, like ``if p.grad is None: continue`` (ps.py:178-179).
+        ``lookahead`` tau > 0 (async PS): ``pub`` receives the parameters extrapolated by the
+        momentum of the next tau updates (optimizers without momentum ignore it)."""
         self._begin_update()
-        self._update_range(sources, target, 0, self.store.numel, gscale, zero_src, pub, mask)
+        self._update_range(sources, target, 0, self.store.numel, gscale, zero_src, pub, mask, lookahead=lookahead)
 
     def _begin_update(self):
         """Start one optimizer step: advance every non-empty group's step counter once (the
@@ -173,7 +189,7 @@ class MPI_PS(torch.optim.Optimizer):
 
     def _update_range(self, sources: List[torch.Tensor], target: torch.Tensor, lo: int, hi: int, gscale: float,
                       zero_src: bool = False, pub: Optional[torch.Tensor] = None,
-                      mask: Optional[torch.Tensor] = None, src_lo: int = 0):
+                      mask: Optional[torch.Tensor] = None, src_lo: int = 0, lookahead: float = 0.0):
         """Update flat elements [lo, hi) (16-aligned).  ``target``/``pub``/``mask`` index the whole
         flat space; ``sources`` start at flat element ``src_lo`` (e.g. one bucket's images)."""
         for gi, group in enumerate(self.param_groups):
@@ -181,12 +197,22 @@ class MPI_PS(torch.optim.Optimizer):
             a, b = max(a, lo), min(b, hi)
             if b <= a:
                 continue
+            cs = self._csteps()
             self._update_group(gi, group, [s[a - src_lo:b - src_lo] for s in sources], target[a:b], gscale,
                                zero_src, None if pub is None else pub[a:b],
-                               None if mask is None else mask[a // 16:b // 16], a, b)
+                               None if mask is None else mask[a // 16:b // 16], a, b,
+                               None if cs is None else cs[a // 16:b // 16], lookahead)
 
-    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub, mask=None, lo=None, hi=None):
+    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub, mask=None, lo=None, hi=None,
+                      csteps=None, lookahead=0.0):
         raise NotImplementedError
+
+    def param_steps(self) -> Dict[int, int]:
+        """slot index -> number of updates that parameter has received (host read)."""
+        if self.chunk_steps is None:
+            return {i: self._group_steps[s.group] for i, s in enumerate(self.store.slots)}
+        cs = self.chunk_steps.cpu()
+        return {i: int(cs[s.offset // 16]) for i, s in enumerate(self.store.slots)}
 
     # ------------------------------------------------------------------ public API
     @torch.no_grad()
@@ -200,7 +226,13 @@ class MPI_PS(torch.optim.Optimizer):
         t0 = time.perf_counter()
         data = self.engine.step()
         self._refresh_shadow()
-        data["step_time"] = time.perf_counter() - t0
+        now = time.perf_counter()
+        data["step_time"] = now - t0
+        if self.cfg.samples_per_step > 0:  # host wall time between consecutive step() calls
+            last = getattr(self, "_last_step_t", None)
+            if last is not None and now > last:
+                data["samples_per_sec"] = self.cfg.samples_per_step / (now - last)
+            self._last_step_t = now
         if self._metrics is not None:
             self._metrics.write(self.steps, data)
         return loss, data
@@ -291,10 +323,16 @@ class MPI_PS(torch.optim.Optimizer):
             pass
 
     def state_dict(self):
+        self._sync_param_state()
         sd = super().state_dict()
         sd["hipps"] = {"steps": self.steps, "group_steps": list(self._group_steps), "mode": self.mode,
                        "codec": self.codec.name}
+        if self.chunk_steps is not None:
+            sd["hipps"]["chunk_steps"] = self.chunk_steps.detach().cpu()
         return sd
+
+    def _sync_param_state(self):
+        """Refresh host-side per-parameter state entries derived from device state."""
 
     def load_state_dict(self, state_dict):
         extra = state_dict.get("hipps", {})
@@ -313,7 +351,22 @@ class MPI_PS(torch.optim.Optimizer):
         self.steps = extra.get("steps", self.steps)
         if "group_steps" in extra:
             self._group_steps = list(extra["group_steps"])
+        cs = self._csteps()
+        if cs is not None:
+            if "chunk_steps" in extra:
+                cs.copy_(extra["chunk_steps"].to(cs.device))
+            else:  # a plain torch state dict: per-parameter counts from its own entries
+                self._csteps_from_state(cs)
         self.store.refresh_shadow()
+
+    def _csteps_from_state(self, cs: torch.Tensor):
+        for s in self.store.slots:
+            n = self._state_count(self.state.get(s.param, {}), s.group)
+            a = s.offset // 16
+            cs[a:a + (s.numel + 15) // 16].fill_(n)
+
+    def _state_count(self, st: dict, gi: int) -> int:
+        return self._group_steps[gi]
 
     def _ensure_state_nocopy(self, key):
         if key not in self.flat_state:
@@ -327,37 +380,34 @@ class SGD(MPI_PS, torch.optim.SGD):
 
     optim = "sgd"
 
-    def _begin_update(self):
-        super()._begin_update()
-        # buf = d_p on the first step (ps.py:203-205), decided once per step for every range
-        self._first_now = {gi for gi, g in enumerate(self.param_groups)
-                           if (g.get("momentum", 0) or 0) and not self._momentum_started(gi)}
+    def _needs_csteps(self) -> bool:
+        return any(g.get("momentum", 0) for g in self.param_groups)
 
-    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub, mask=None, lo=None, hi=None):
+    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub, mask=None, lo=None, hi=None,
+                      csteps=None, lookahead=0.0):
         mom = group.get("momentum", 0) or 0
         a, b = (lo, hi) if lo is not None else self.store.group_ranges[gi]
         buf = self._ensure_state("momentum_buffer")[a:b] if mom else None
-        # with a mask, later-starting params get buf = (1-dampening)*d_p from the zero-initialised
-        # buffer (identical for dampening=0)
-        first = mom and mask is None and gi in getattr(self, "_first_now", ())
+        # buf = d_p on each parameter's own first step (ps.py:203-205): the kernel reads the
+        # chunk's update count, so masked steps and late-starting parameters follow the reference
         ops.sgd_step(srcs, target, buf, pub, zero_src, gscale, lr=group["lr"],
                      weight_decay=group.get("weight_decay", 0) or 0, momentum=mom,
                      dampening=group.get("dampening", 0) or 0, nesterov=bool(group.get("nesterov", False)),
-                     first=bool(first), mask=mask)
+                     first=False, mask=mask, csteps=csteps if mom else None,
+                     lookahead=self.lookahead_coef(group, lookahead) if pub is not None else 0.0)
 
-    def _momentum_started(self, gi):
-        started = getattr(self, "_mom_started", None)
-        if started is None:
-            started = self._mom_started = set()
-        if gi in started:
-            return True
-        started.add(gi)
-        return False
+    @staticmethod
+    def lookahead_coef(group, tau: float) -> float:
+        """lr * (mu + mu^2 + ... + mu^tau): the momentum displacement of the next tau updates
+        (fractional tau interpolates the geometric sum)."""
+        mom = group.get("momentum", 0) or 0
+        if tau <= 0 or not mom or group.get("nesterov", False):
+            return 0.0
+        geo = mom * (1 - mom ** tau) / (1 - mom) if mom < 1 else tau
+        return float(group["lr"]) * geo
 
-    def load_state_dict(self, state_dict):
-        super().load_state_dict(state_dict)
-        if "momentum_buffer" in self.flat_state:
-            self._mom_started = set(range(len(self.param_groups)))
+    def _state_count(self, st: dict, gi: int) -> int:
+        return max(1, self._group_steps[gi]) if "momentum_buffer" in st else 0
 
 
 class Adam(MPI_PS, torch.optim.Adam):
@@ -366,12 +416,15 @@ class Adam(MPI_PS, torch.optim.Adam):
 
     optim = "adam"
 
-    def _begin_update(self):
-        super()._begin_update()
-        for s in self.store.slots:  # torch-compatible per-parameter step (state_dict readers)
-            self.state[s.param]["step"] = self._group_steps[s.group]
+    def _sync_param_state(self):
+        for i, n in self.param_steps().items():  # torch-compatible per-parameter step (ps.py:241)
+            self.state[self.store.slots[i].param]["step"] = n
 
-    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub, mask=None, lo=None, hi=None):
+    def _state_count(self, st: dict, gi: int) -> int:
+        return int(st.get("step", 0))
+
+    def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub, mask=None, lo=None, hi=None,
+                      csteps=None, lookahead=0.0):
         a, b = (lo, hi) if lo is not None else self.store.group_ranges[gi]
         m = self._ensure_state("exp_avg")[a:b]
         v = self._ensure_state("exp_avg_sq")[a:b]
@@ -380,4 +433,4 @@ class Adam(MPI_PS, torch.optim.Adam):
         step = self._group_steps[gi]
         ops.adam_step(srcs, target, m, v, vm, pub, zero_src, gscale, lr=group["lr"], betas=group["betas"],
                       eps=group["eps"], weight_decay=group.get("weight_decay", 0) or 0, step=step, amsgrad=ams,
-                      torch_mode=self.cfg.adam_variant == "torch", mask=mask)
+                      torch_mode=self.cfg.adam_variant == "torch", mask=mask, csteps=csteps)

@@ -20,7 +20,8 @@ from .ps_core import PSCore
 # same field ids as hipps/csrc/runtime/control.cpp
 FIELDS = SimpleNamespace(F_PUSH_SEQ=0, F_ACK_SEQ=1, F_PUSH_VER=2, F_APPLIED_VER=3, F_STOP=4, F_HEARTBEAT=5,
                          F_INCL_SEQ=6, F_PUSH_FLAG=7, F_READING=8, F_PULL_REQ=9, F_PUB_VER=10, F_PS_STOP=11,
-                         F_ERROR=12, F_DROPS=13, F_UPDATES=14, F_BUF_VER=15, F_SENT_VER=16)
+                         F_ERROR=12, F_DROPS=13, F_UPDATES=14, F_BUF_VER=15, F_SENT_VER=16,
+                         F_LAST_STALE=17, F_LAST_STALE_SEQ=18)
 
 
 class FakeControl:

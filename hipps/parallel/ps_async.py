@@ -561,8 +561,11 @@ class PSAsyncEngine(Engine):
         if self.cfg.skip_missing_grads and not self._pres_full and self._pres_part is not None:
             mask = self.store.chunk_mask(self._pres_part)
         self._pres_full, self._pres_part = False, None
+        tau = self.lookahead_tau()
+        self._stats["lookahead_tau_x1000"] = int(round(tau * 1000))
         with self.tracer.phase("ps_update", self.ps_stream):
-            self.opt._update_flat([self.acc], self.master, gscale, zero_src=True, pub=self.pub_buf(b), mask=mask)
+            self.opt._update_flat([self.acc], self.master, gscale, zero_src=True, pub=self.pub_buf(b), mask=mask,
+                                  lookahead=tau)
         st = self.ps_stream
         # order matters: buffer stamp -> version word -> per-worker "included" words, so a worker
         # that sees its message included also sees a version containing it
@@ -572,6 +575,16 @@ class PSAsyncEngine(Engine):
         for k in range(0, len(words), 6):
             self._ring(st, words[k:k + 6])
         self.ctl.fetch_add(C.F_UPDATES, 0, 1)
+
+    def lookahead_tau(self) -> float:
+        """Updates to extrapolate the published parameters by (cfg.stale_lookahead): readers'
+        gradients arrive that many updates late, so they are computed where the momentum will
+        have carried the master by then.  Auto: the mean measured staleness of the recent steps;
+        never with max_delay == 0 (exactly the synchronous update sequence)."""
+        tau = float(self.cfg.stale_lookahead)
+        if tau < 0:
+            tau = 0.0 if self.cfg.max_delay == 0 else self.core.mean_staleness()
+        return tau
 
     def dead_workers(self) -> List[int]:
         """Ranks whose heartbeat is older than cfg.dead_after_s and that never said STOP."""
@@ -660,6 +673,8 @@ class PSAsyncEngine(Engine):
             data["pulled"] = float(self.irequest_params())
         data["comm_wait"] = time.perf_counter() - t
         data["version"] = float(self.adopted_version())
+        # staleness (PS updates) of this worker's newest step the PS has consumed
+        data["staleness"] = float(self.ctl.load(C.F_LAST_STALE, self.rank))
         data["optim_step_time"] = 0.0
         data["decode_time"] = 0.0
         data.update(self.step_metrics())

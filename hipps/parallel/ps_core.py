@@ -40,6 +40,8 @@ class PSCore:
         self.dropping = [False] * W
         self.scale = [1.0] * W
         self.backend = None
+        self.recent: List[int] = []  # staleness of the newest accumulated steps (look-ahead tau)
+        self.RECENT = max(8, 2 * W)
 
     def pump(self, i: int, upto: Optional[int] = None) -> int:
         """Process every message worker ``i`` has pushed since the last call (or up to message
@@ -66,6 +68,12 @@ class PSCore:
             self.scale[i] = 1.0 / max(1, stale) if self.staleness_lr else 1.0
             if not self.dropping[i]:
                 self.stats["staleness_sum"] += max(0, stale)
+                self.recent.append(max(0, stale))
+                if len(self.recent) > self.RECENT:
+                    del self.recent[0]
+            # per-step staleness record the worker reads back into its step() data
+            self.ctl.store(F.F_LAST_STALE, i, stale)
+            self.ctl.store(F.F_LAST_STALE_SEQ, i, s + nb - 1)
         if not self.dropping[i]:
             be.accumulate(i, slot, bi, s, self.scale[i])
             if pos == nb - 1:
@@ -86,6 +94,10 @@ class PSCore:
                     be.update(self.pending, self.gscale)
                     self.pending = []
                     self.count = 0
+
+    def mean_staleness(self) -> float:
+        """Mean staleness (in updates) of the newest accumulated steps."""
+        return sum(self.recent) / len(self.recent) if self.recent else 0.0
 
     @staticmethod
     def last_included(included) -> Dict[int, int]:

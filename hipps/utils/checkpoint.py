@@ -59,7 +59,7 @@ def save(opt, path: str, model: Optional[torch.nn.Module] = None, extra: Optiona
             ps = {"params": params, "flat_state": _cpu(opt.flat_state), "group_steps": list(opt._group_steps),
                   "steps": opt.steps, "mode": opt.mode, "codec": opt.codec.name, "numel": opt.store.numel,
                   "version": -1 if version is None else int(version),
-                  "mom_started": sorted(getattr(opt, "_mom_started", set()))}
+                  "chunk_steps": None if opt.chunk_steps is None else opt.chunk_steps.detach().cpu()}
             if acc is not None:
                 ps["acc"], ps["acc_count"] = acc, int(acc_count)
             if extra:
@@ -84,8 +84,9 @@ def load(opt, path: str, model: Optional[torch.nn.Module] = None) -> dict:
         opt._ensure_state(k).copy_(v)
     opt._group_steps = list(ps["group_steps"])
     opt.steps = ps["steps"]
-    if ps.get("mom_started"):
-        opt._mom_started = set(ps["mom_started"])
+    cs = opt._csteps()
+    if cs is not None and ps.get("chunk_steps") is not None:
+        cs.copy_(ps["chunk_steps"].to(cs.device))
     rank = opt.world.rank
     rp = os.path.join(path, f"rank{rank}.pt")
     mine = torch.load(rp, map_location="cpu", weights_only=True) if os.path.exists(rp) else {"engine": {}}

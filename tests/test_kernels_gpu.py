@@ -282,3 +282,47 @@ def test_threshold_codec_gpu_matches_reference(n, tau, ratio, ef):
     torch.testing.assert_close(outs[1][2], outs[0][2])
     if ef:
         torch.testing.assert_close(outs[1][3], outs[0][3])
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_chunk_steps_per_parameter_state(opt):
+    """Per-chunk update counts (csteps): a chunk's first momentum step is buf = d_p and Adam's bias
+    correction uses the chunk's own t, whatever the group step; counts advance under the mask."""
+    torch.manual_seed(5)
+    n = 16 * 4001
+    nch = n // 16
+    cs = torch.randint(0, 4, (nch,), dtype=torch.int32)
+    p, st = torch.randn(n), [torch.randn(n) * 0.1, torch.rand(n) * 0.1]
+    pd, sd, csd = p.to(DEV), [s.to(DEV) for s in st], cs.to(DEV)
+    for t in range(3):
+        mask = (torch.rand(nch) > 0.25).to(torch.uint8)
+        g = torch.randn(n)
+        if opt == "sgd":
+            kw = dict(lr=0.1, weight_decay=0.01, momentum=0.9, dampening=0.3)
+            ref.sgd_step([g], p, st[0], None, False, 1.0, mask=mask, csteps=cs, **kw)
+            ops.sgd_step([g.to(DEV)], pd, sd[0], None, False, 1.0, mask=mask.to(DEV), csteps=csd, **kw)
+        else:
+            kw = dict(lr=1e-2, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, step=t + 2)
+            ref.adam_step([g], p, st[0], st[1], None, None, False, 1.0, mask=mask, csteps=cs, **kw)
+            ops.adam_step([g.to(DEV)], pd, sd[0], sd[1], None, None, False, 1.0, mask=mask.to(DEV), csteps=csd, **kw)
+    assert torch.equal(csd.cpu(), cs)
+    torch.testing.assert_close(pd.cpu(), p, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(sd[0].cpu(), st[0], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("masked", [False, True])
+def test_sgd_lookahead_publish(masked):
+    """Look-ahead publish: pub = p_new - c * buf_new (masked chunks: p - c * buf); master unchanged."""
+    torch.manual_seed(6)
+    n = 16 * 999
+    p, buf = torch.randn(n), torch.randn(n) * 0.1
+    g = torch.randn(n)
+    mask = (torch.rand(n // 16) > 0.5).to(torch.uint8) if masked else None
+    pd, bd = p.to(DEV), buf.to(DEV)
+    pub = torch.empty(n, device=DEV)
+    kw = dict(lr=0.1, weight_decay=1e-4, momentum=0.9)
+    ref.sgd_step([g], p, buf, None, False, 1.0, mask=mask, **kw)
+    ops.sgd_step([g.to(DEV)], pd, bd, pub, False, 1.0, mask=None if mask is None else mask.to(DEV), lookahead=0.09,
+                 **kw)
+    torch.testing.assert_close(pd.cpu(), p, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(pub.cpu(), p - 0.09 * buf, rtol=1e-5, atol=1e-6)

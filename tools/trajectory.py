@@ -12,9 +12,16 @@ variant runs in its own process (tests/test_resnet_trajectory_gpu.py spawns both
   async          mode='ps_async', max_delay=-1 (free-running AsySG-InCon)
   async_slr      as async, with staleness-aware gradient scaling
   async_prefetch as async, with the host-chosen prefetch/direct pull instead of the GPU pull
+  async_mc       as async, with delay-compensated momentum (``stale_momentum='comp'``)
+A run name may carry ``+key=value`` overrides of the hipps.SGD keywords, e.g.
+``local+code=fp32+bf16_weights=off`` (bisects the bf16 wire and the bf16 weight shadow).
+
+``--headline`` is the exact bench.py configuration (BASELINE.json headline): batch 256, bf16 wire,
+auto bf16 weight shadow, wd 5e-5, average=True, lr 0.1, momentum 0.9, 60 steps.
 
     python tools/trajectory.py --runs local,async_md0,async --out a.json
     python tools/trajectory.py --plain --out b.json
+    python tools/trajectory.py --headline --runs local,async_md0,async --out h.json
 """
 from __future__ import annotations
 
@@ -46,11 +53,34 @@ def parse(argv=None):
     ap.add_argument("--plain", action="store_true", help="all fusions off + torch.optim.SGD")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--deterministic", action="store_true", help="MIOpen deterministic algorithms (slow)")
+    ap.add_argument("--headline", action="store_true",
+                    help="bench.py's config: batch 256, bf16 wire, auto shadow, 60 steps")
     ap.add_argument("--out", default=None)
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    if a.headline:
+        a.batch, a.codec, a.bf16_weights, a.steps = 256, "bf16", "auto", max(a.steps, 60)
+    return a
 
 
-def _cfg(run):
+def _val(v):
+    for t in (int, float):
+        try:
+            return t(v)
+        except ValueError:
+            pass
+    return {"true": True, "false": False}.get(v.lower(), v)
+
+
+def _cfg(spec):
+    run, *mods = spec.split("+")
+    d = _base_cfg(run)
+    for m in mods:
+        k, v = m.split("=", 1)
+        d[k] = _val(v)
+    return d
+
+
+def _base_cfg(run):
     if run == "local":
         return {"mode": "local"}
     if run.startswith("async_md"):
@@ -61,6 +91,8 @@ def _cfg(run):
         return {"mode": "ps_async", "max_delay": -1, "staleness_lr": True}
     if run == "async_prefetch":
         return {"mode": "ps_async", "max_delay": -1, "pull": "prefetch"}
+    if run == "async_mc":
+        return {"mode": "ps_async", "max_delay": -1, "stale_momentum": "comp"}
     raise ValueError(run)
 
 
@@ -92,17 +124,22 @@ def main(argv=None):
         else:
             import hipps
 
-            opt = hipps.SGD(model.named_parameters(), lr=a.lr, momentum=a.momentum, weight_decay=a.wd,
-                            code=a.codec, average=True, bf16_weights=a.bf16_weights, **_cfg(run))
-        losses = []
+            kw = dict(lr=a.lr, momentum=a.momentum, weight_decay=a.wd, code=a.codec, average=True,
+                      bf16_weights=a.bf16_weights)
+            kw.update(_cfg(run))
+            opt = hipps.SGD(model.named_parameters(), **kw)
+        losses, stale = [], []
         t0 = time.time()
         for s in range(a.steps):
             opt.zero_grad()
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 loss = F.cross_entropy(model(x), y)
             loss.backward()
-            opt.step()
+            r = opt.step()
+            data = r[1] if isinstance(r, tuple) else {}
             losses.append(float(loss.float().item()))
+            if data and "staleness" in data:
+                stale.append(float(data["staleness"]))
             if s % 10 == 0:
                 print(f"[trajectory] {run} step {s} loss {losses[-1]:.4f}", file=sys.stderr, flush=True)
         torch.cuda.synchronize()
@@ -115,7 +152,8 @@ def main(argv=None):
         flat = torch.cat([p.detach().float().reshape(-1).cpu() for p in model.parameters()])
         recs.append({"variant": run, "model": a.model, "batch": a.batch, "image": a.image, "steps": a.steps,
                      "lr": a.lr, "losses": losses, "param_sha": hashlib.sha1(flat.numpy().tobytes()).hexdigest()[:16],
-                     "param_norm": float(flat.norm()), "seconds": round(time.time() - t0, 2), "ps": stats})
+                     "param_norm": float(flat.norm()), "seconds": round(time.time() - t0, 2), "ps": stats,
+                     "staleness": stale, "codec": a.codec, "bf16_weights": a.bf16_weights})
         print(json.dumps(recs[-1]), flush=True)
         del opt, model
     if a.out:
