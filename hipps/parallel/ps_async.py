@@ -156,6 +156,15 @@ class PSAsyncEngine(Engine):
         # 'p2p': the mailbox stays private to the PS and data moves by two-sided send/recv
         # (torch.distributed isend/irecv: RCCL pair communicators on GPU, gloo on CPU)
         self.p2p = cfg.async_transport == "p2p" and W > 1
+        # p2p: gradients and parameters travel on two process groups of their own.  Each group has
+        # its own RCCL communicators and streams, so (a) a posted gradient receive can never sit
+        # in front of a parameter send on the same pair channel (ops of one channel complete in
+        # post order), and (b) the PS thread's traffic never interleaves with collectives that
+        # rank 0's main thread issues on the default group (barrier, all_reduce).
+        self._gpg = self._ppg = None
+        if self.p2p:
+            self._gpg = dist.new_group(list(range(W)))
+            self._ppg = dist.new_group(list(range(W)))
         token = secrets.token_hex(6) if self.rank == 0 else None
         handle = None
         self.mailbox = None
@@ -255,7 +264,7 @@ class PSAsyncEngine(Engine):
             # the transport self-test go first, on the main threads
             pub0 = self.pub_buf(0) if self.rank == 0 else torch.empty(store.numel, dtype=self.pub_dtype,
                                                                        device=store.device)
-            dist.broadcast(pub0, src=0)
+            dist.broadcast(pub0, src=0, group=self._ppg)
             self._adopt(pub0, 0)
             if self.cuda:
                 torch.cuda.current_stream(store.device).synchronize()
@@ -330,10 +339,10 @@ class PSAsyncEngine(Engine):
         if self.rank == 0:
             for r in range(1, W):
                 got = self.slot_buf(r, self.SLOTS - 1)[:16]
-                dist.recv(got, src=r)
+                dist.recv(got, src=r, group=self._gpg)
                 ok &= bool((got.cpu() == (r * 7 + 3) % 251).all())
         else:
-            dist.send(tag, dst=0)
+            dist.send(tag, dst=0, group=self._gpg)
         ck = float(self.pub_buf(0).double().sum()) if self.rank == 0 else None
         box = [ok, ck]
         dist.broadcast_object_list(box, src=0)
@@ -412,9 +421,20 @@ class PSAsyncEngine(Engine):
         inflight = [deque() for _ in range(W)]
         self._served = [0] * W
         idle = 0
+        delay = float(os.environ.get("HIPPS_PS_LOOP_DELAY_US", "0")) * 1e-6  # tests: a slow PS thread
         with torch.no_grad():
             while True:
+                if delay:
+                    time.sleep(delay)
                 progressed = False
+                # parameter requests first: the worker posted its receive before announcing newer
+                # gradients, so answering it never waits behind a gradient receive
+                for i in range(1, W):
+                    req = self.ctl.load(C.F_PULL_REQ, i)
+                    if req > self._served[i]:
+                        self._send_params(i)
+                        self._served[i] = req
+                        progressed = True
                 if self.ctl.load(C.F_PUSH_SEQ, 0) > core.seen[0]:
                     progressed |= core.pump(0) > 0
                 for i in range(1, W):
@@ -425,9 +445,9 @@ class PSAsyncEngine(Engine):
                         pos = (s - 1) % self.nb
                         b = self.plan.buckets[self.order[pos]]
                         sbuf = self.slot_buf(i, slot)
-                        works = [dist.irecv(sbuf[: b.msg_nbytes], src=i)]
+                        works = [dist.irecv(sbuf[: b.msg_nbytes], src=i, group=self._gpg)]
                         if pos == self.nb - 1 and self.ctl.load(C.F_PUSH_FLAG, i * self.MAXSLOTS + slot):
-                            works.append(dist.irecv(sbuf[self.slot_pres:self.slot_pres + ns], src=i))
+                            works.append(dist.irecv(sbuf[self.slot_pres:self.slot_pres + ns], src=i, group=self._gpg))
                         inflight[i].append((s, _Pending(works, self.cuda)))
                         posted[i] = s
                     while inflight[i] and inflight[i][0][1].done():
@@ -436,12 +456,6 @@ class PSAsyncEngine(Engine):
                         core.pump(i, upto=s)
                         progressed = True
                 self.flush()
-                for i in range(1, W):
-                    req = self.ctl.load(C.F_PULL_REQ, i)
-                    if req > self._served[i]:
-                        self._send_params(i)
-                        self._served[i] = req
-                        progressed = True
                 if self._pause_req.is_set():
                     self._hold()
                 dead = self.dead_workers()
@@ -457,7 +471,7 @@ class PSAsyncEngine(Engine):
         v = self.ver
         b = v % self.NPUB
         self.ctl.store(self.C.F_SENT_VER, i, v)
-        w = dist.isend(self.pub_buf(b), dst=i)  # ordered after the update that wrote buffer b
+        w = dist.isend(self.pub_buf(b), dst=i, group=self._ppg)  # ordered after the update that wrote buffer b
         self._pub_sends.setdefault(b, []).append(w)
 
     def _serve(self):
@@ -698,10 +712,10 @@ class PSAsyncEngine(Engine):
         self.ctl.store(C.F_PUSH_SEQ, self.rank, s)
         ctx = torch.cuda.stream(self.comm_stream) if self.cuda else contextlib.nullcontext()
         with ctx, self.tracer.phase("push", self.comm_stream):
-            works = [dist.isend(msg, dst=0)]
+            works = [dist.isend(msg, dst=0, group=self._gpg)]
             if partial:
                 self._pres_send = self.presence_tensor()
-                works.append(dist.isend(self._pres_send, dst=0))
+                works.append(dist.isend(self._pres_send, dst=0, group=self._gpg))
             for w in works:
                 w.wait()  # GPU: the comm stream waits; CPU: returns once the PS has the bytes
 
@@ -739,9 +753,9 @@ class PSAsyncEngine(Engine):
                     if self._stage_ev[k] is not None:
                         ps.wait_event(self._stage_ev[k])  # the last adoption from this stage is done
                     with torch.cuda.stream(ps):
-                        works = [dist.irecv(self._stage[k], src=0)]
+                        works = [dist.irecv(self._stage[k], src=0, group=self._ppg)]
                 else:
-                    works = [dist.irecv(self._stage[k], src=0)]
+                    works = [dist.irecv(self._stage[k], src=0, group=self._ppg)]
                 self._p2p_reqs += 1
                 self._p2p_req = (self._p2p_reqs, k, _Pending(works, self.cuda))
                 self.ctl.store(C.F_PULL_REQ, self.rank, self._p2p_reqs)

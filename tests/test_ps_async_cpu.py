@@ -7,7 +7,7 @@ from test_dist_cpu import _data, _mlp
 
 
 def _train_async(rank, world, steps, codec, accumulate, max_delay, staleness, opt_name="sgd", bucket_mb=64.0,
-                 slots=0, transport="ipc"):
+                 slots=0, transport="ipc", main_collectives=False):
     import hipps
 
     m = _mlp()
@@ -29,6 +29,13 @@ def _train_async(rank, world, steps, codec, accumulate, max_delay, staleness, op
         loss.backward()
         losses.append(loss.item())
         opt.step()
+        if main_collectives:  # rank 0's main thread uses the default group while its PS thread serves
+            import torch.distributed as dist
+
+            t = torch.ones(1)
+            dist.all_reduce(t)
+            assert t.item() == world
+            dist.barrier()
     eng = opt.engine
     opt.close()  # drains: the PS thread exits only after consuming every pushed message
     stats = eng.ps_stats()
@@ -161,3 +168,15 @@ def test_ipc_mapping_failure_is_collective_and_p2p_recovers():
     out = run_world(_ipc_fails_then_p2p, 2)
     assert all(o["err"] and "mapping the PS mailbox failed" in o["err"] and "rank 1" in o["err"] for o in out), out
     assert out[0]["stats"]["accumulated"] == 2 * 3
+
+
+def test_async_p2p_slow_ps_with_main_thread_collectives(monkeypatch):
+    """with a slowed PS loop the PS sees a worker's parameter request and its next
+    step's announcement in one iteration; parameters travel on their own process group and the
+    request is answered first, so the pair channel cannot deadlock.  Rank 0's main thread runs
+    all_reduce + barrier on the default group every step meanwhile."""
+    monkeypatch.setenv("HIPPS_PS_LOOP_DELAY_US", "3000")
+    steps = 8
+    out = run_world(_train_async, 3, steps, "fp32", 0, -1, -1, "sgd", 0.0005, 2, "p2p", True)
+    st = out[0]["stats"]
+    assert st["accumulated"] == 3 * steps and st["updates"] == steps

@@ -9,9 +9,11 @@
   both fall;
 * ps_async at N=1 with max_delay=0 (rank 0 = PS + worker) is bit-identical to mode='local'
   (8 steps with MIOpen's deterministic algorithms: its default ones use atomics);
-* free-running ps_async (GPU-time pull, one update of staleness per step) still trains the batch
-  down, more slowly than local SGD (delayed gradients with momentum 0.9: 6.95 -> ~3.8 in 40
-  steps where local SGD reaches ~0.1).
+* the headline bench configuration (batch 256, bf16 wire, bf16 weight shadow, lr 0.1, momentum
+  0.9, 60 steps): free-running ps_async (GPU-time pull, one update of staleness per step) with the
+  look-ahead publish falls below half its first loss and never climbs more than 10 % above its
+  running minimum after step 20 (without the look-ahead the delayed gradient under momentum 0.9
+  oscillates around 4.3-5.3: profiles/convergence/), and max_delay=0 stays bit-identical to local.
 
 The fusion switches are read at import, so each side runs in a fresh child process.
 """
@@ -36,7 +38,7 @@ def _run(args, out, timeout=420):
 
 
 def test_resnet50_fused_trains_like_plain_pytorch(tmp_path):
-    fused = _run(["--runs", "local,async"], str(tmp_path / "fused.json"))
+    fused = _run(["--runs", "local"], str(tmp_path / "fused.json"))
     plain = _run(["--plain"], str(tmp_path / "plain.json"))["plain"]
     plain2 = _run(["--plain"], str(tmp_path / "plain2.json"))["plain"]
     det = _run(["--runs", "local,async_md0", "--steps", "8", "--deterministic"], str(tmp_path / "det.json"))
@@ -57,9 +59,22 @@ def test_resnet50_fused_trains_like_plain_pytorch(tmp_path):
     # N=1 async PS with max_delay=0 applies exactly the local update sequence
     assert det["async_md0"]["param_sha"] == det["local"]["param_sha"]
     assert det["async_md0"]["losses"] == det["local"]["losses"]
-    # free-running AsySG-InCon: staleness bounded by the pipeline, and the loss still falls
-    fr = fused["async"]
+
+
+def test_headline_config_async_converges(tmp_path):
+    h = _run(["--headline", "--runs", "local,async"], str(tmp_path / "headline.json"))
+    det = _run(["--headline", "--runs", "local,async_md0", "--steps", "6", "--deterministic"],
+               str(tmp_path / "hdet.json"))
+    assert det["async_md0"]["param_sha"] == det["local"]["param_sha"]
+    assert det["async_md0"]["losses"] == det["local"]["losses"]
+    fr = h["async"]
+    assert fr["batch"] == 256 and fr["codec"] == "bf16" and fr["bf16_weights"] == "auto"
     assert fr["ps"]["doorbells"] == "device" and fr["ps"]["pull"] == "device"
+    assert fr["ps"]["lookahead_tau_x1000"] > 0
     lf = fr["losses"]
-    assert min(lf[-5:]) < 0.6 * lf[0]
-    assert sum(lf[-5:]) < sum(lf[15:20])  # still falling at the end
+    assert len(lf) == 60 and lf[-1] < 0.5 * lf[0], lf
+    for i in range(20, len(lf)):
+        assert lf[i] <= 1.1 * min(lf[: i + 1]), f"step {i}: {lf[i]:.3f} rebounds above {min(lf[: i + 1]):.3f}"
+    # per-step staleness in the step data: one update at N=1
+    assert fr["staleness"] and max(fr["staleness"][5:]) <= 2
+    assert h["local"]["losses"][-1] < 0.2 * h["local"]["losses"][0]
