@@ -63,6 +63,16 @@ def parse():
     ap.add_argument("--async-transport", default="ipc", choices=["ipc", "p2p"])
     ap.add_argument("--no-pull-overlap", action="store_true",
                     help="ps_async: one GPU-time pull of all params before the forward (A/B)")
+    ap.add_argument("--ps-dedicated", action="store_true",
+                    help="reference topology (README.md:64-75): rank 0 only serves, ranks 1..N-1 train; the value "
+                         "counts the N-1 workers' samples")
+    ap.add_argument("--emulate-workers", type=int, default=0,
+                    help="rehearse the N=8 PS load on ONE GPU: launch 1+E ranks (HIPPS_BACKEND=gloo); rank 0 trains "
+                         "as worker 0 + PS, ranks 1..E push real bucket messages and pull parameters in lockstep "
+                         "with worker 0 without computing (the PS-side load of E remote workers)")
+    ap.add_argument("--emulate-remote", type=int, default=0,
+                    help="N=1 rehearsal of the co-located PS at N=1+E: the PS also accumulates E emulated remote "
+                         "messages per step and sweeps their push / pull bytes (PSConfig.emulate_remote)")
     return ap.parse_args()
 
 
@@ -96,13 +106,21 @@ def main():
             x = x.contiguous(memory_format=torch.channels_last)
         y = torch.randint(0, 1000, (a.batch,), device=dev)
 
+    emulated = a.emulate_workers > 0 and world.rank > 0
+    if a.emulate_workers and N != a.emulate_workers + 1:
+        raise SystemExit(f"--emulate-workers {a.emulate_workers} needs WORLD_SIZE={a.emulate_workers + 1}")
+    if emulated:  # tiny batch: only the gradients' shapes matter, the messages are real bucket images
+        x, y = x[:2, :, :64, :64].contiguous(memory_format=torch.channels_last), y[:2]
     mode = a.mode if N > 1 or a.mode in ("ps_async", "local") else "local"
     if a.param_wire == "auto":
         a.param_wire = "bf16" if N > 1 else "fp32"
     note = None
+    dedicated = bool(a.ps_dedicated and mode == "ps_async" and N > 1)
     kw = dict(lr=a.lr, momentum=a.momentum, weight_decay=5e-5, mode=mode, code=a.codec,
               accumulate=a.accumulate or None, average=True, param_wire=a.param_wire, bucket_mb=a.bucket_mb,
-              async_transport=a.async_transport)
+              async_transport=a.async_transport, ps_dedicated=dedicated)
+    if a.emulate_remote and N == 1:
+        kw["emulate_remote"] = a.emulate_remote
     try:
         opt = hipps.SGD(model.named_parameters(), **kw)
     except Exception as e:
@@ -128,13 +146,34 @@ def main():
         _, data = opt.step()
         return loss, data
 
+    ps_only = bool(getattr(opt, "ps_only", False))
+    if emulated:
+        # gradients once; every step re-encodes and pushes them (real bucket images through the
+        # real mailbox / doorbells) and pulls the newest parameters -- paced so that message k is
+        # pushed after worker 0 pushed its step k, as identical GPUs would
+        with torch.autocast("cuda", dtype=torch.bfloat16):  # zero gradients: load without perturbing training
+            (0.0 * F.cross_entropy(model(x), y)).backward()
+        eng = opt.engine
+        nb = len(eng.plan.buckets)
+        k = [0]
+
+        def step():  # noqa: F811
+            k[0] += 1
+            eng.ctl.wait_ge(eng.C.F_PUSH_SEQ, 0, (k[0] - 1) * nb + 1, 600 * 1000000)
+            _, data = opt.step()
+            return None, data
+    elif ps_only:
+        def step():  # noqa: F811  -- the PS thread serves; rank 0's main thread only times
+            return None, {}
+
     first_loss = None
     losses = []  # device scalars; read after the timed region (no host sync inside it)
     for _ in range(a.warmup):
         loss, _ = step()
-        losses.append(loss.detach())
-        if first_loss is None:
-            first_loss = float(loss.float().item())
+        if loss is not None:
+            losses.append(loss.detach())
+            if first_loss is None:
+                first_loss = float(loss.float().item())
     tr = opt.engine.tracer  # HIPPS_TRACE=1: per-phase device ms (HIP events), excluded from warmup
     if tr.enabled:
         torch.cuda.synchronize()
@@ -146,7 +185,8 @@ def main():
     last = None
     for _ in range(a.steps):
         loss, last = step()
-        losses.append(loss.detach())
+        if loss is not None:
+            losses.append(loss.detach())
     torch.cuda.synchronize()
     hdist.barrier(world)
     t1 = time.perf_counter()
@@ -154,7 +194,15 @@ def main():
     if N > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
-    final_loss = float(loss.float().item())
+    if dedicated and N > 1:  # the losses live on the workers: rank 1 reports them
+        box = [(first_loss, [float(v.float()) for v in losses], last)]
+        allb = [None] * N
+        dist.all_gather_object(allb, box[0])
+        if world.rank == 0:
+            first_loss, lvals, last = allb[1]
+            losses = [torch.tensor(v) for v in lvals]
+            loss = losses[-1]
+    final_loss = float(loss.float().item()) if loss is not None else float("nan")
     grad_bytes = int(last.get("grad_bytes_sent", 0)) if last else 0
     # bytes that carry information in the last step's messages (reads the device count header of
     # variable-size codecs; outside the timed region)
@@ -170,10 +218,17 @@ def main():
     if hasattr(opt, "_last_engine_stats"):
         stats = opt._last_engine_stats
     per_sample = a.seq if is_tf else 1
-    value = N * a.batch * per_sample * a.steps / elapsed
+    trainers = N - 1 if dedicated else (1 if a.emulate_workers else N)
+    value = trainers * a.batch * per_sample * a.steps / elapsed
     if world.rank == 0:
         metric = METRIC if a.model == "resnet50" else (
             f"{'tokens' if is_tf else 'samples'}/sec (node) {a.model} {mode} (secondary BASELINE config)")
+        if a.emulate_remote and N == 1:
+            metric = (f"worker-0 samples/sec with the co-located PS carrying {a.emulate_remote} emulated remote "
+                      "workers (one GPU; rehearsal, not the headline)")
+        if a.emulate_workers:
+            metric = (f"worker-0 samples/sec under an emulated {a.emulate_workers}-worker async PS load on one GPU "
+                      "(rehearsal, not the headline)")
         rec = {
             "metric": metric,
             "value": round(value, 2),
@@ -190,11 +245,13 @@ def main():
                      "synthetic (random 224x224 images / labels, random-init weights)"),
             "config": {
                 "model": a.model,
-                "global_batch": a.batch * N,
                 "per_gpu_batch": a.batch,
                 "seq_len": a.seq if is_tf else None,
                 "image": None if is_tf else a.image,
-                "parallelism": f"dp{N} {mode} (rank0 = PS + worker)",
+                "parallelism": (f"dp{N - 1} {mode} (rank0 = dedicated PS, ranks 1..{N - 1} = workers)" if dedicated
+                                else f"dp{N} {mode} (rank0 = PS + worker)" if not a.emulate_workers
+                                else f"1 worker + PS, {a.emulate_workers} emulated workers on the same GPU"),
+                "global_batch": a.batch * trainers,
                 "codec": a.codec,
                 "accumulate": a.accumulate or N,
                 "grad_bytes_per_step_per_worker": grad_bytes,
@@ -210,6 +267,8 @@ def main():
             "loss_every5": [round(float(v.float()), 4) for v in losses[::5]],
             "staleness_last": last.get("staleness") if last else None,
             "ps": {k: (int(v) if isinstance(v, (int, float)) else v) for k, v in stats.items()},
+            "ps_staleness_mean": (round(stats["staleness_sum"] / stats["accumulated"], 3)
+                                  if stats.get("accumulated") else None),
         }
         if trace:
             rec["trace_device_ms_per_step"] = trace

@@ -40,6 +40,10 @@ class PSConfig:
     # doorbells) | 'p2p' (two-sided send/recv: RCCL pair communicators through torch.distributed on
     # GPU, gloo on CPU -- the fallback when IPC memory cannot be mapped)
     async_transport: str = "ipc"
+    # async PS topology: False = rank 0 is the PS *and* worker 0 (default: N GPUs train); True =
+    # the reference's topology (README.md:64-75): rank 0 only receives, sums, steps and publishes,
+    # ranks 1..N-1 are the workers (rank 0 calls opt.serve() instead of training)
+    ps_dedicated: bool = False
     # async PS: scale a kept gradient by 1/max(1, staleness) (staleness-aware async SGD)
     staleness_lr: bool = False
     # async PS look-ahead publish (delay-compensated momentum): workers read the parameters
@@ -47,6 +51,13 @@ class PSConfig:
     # arrive late by; the PS master is unchanged.  -1 = auto (tau = mean measured staleness of the
     # recent accumulated steps; off when max_delay == 0), 0 = off, > 0 = fixed tau
     stale_lookahead: float = -1.0
+    # rehearsal knob (one process, one GPU): the co-located PS also carries the load of this many
+    # emulated remote workers -- every message of worker 0 is accumulated 1 + E times (one launch
+    # each; the update scales by 1/(1+E), so the math is unchanged) and every update is followed by
+    # E write sweeps of the step's wire bytes (their pushes landing in HBM) and E read sweeps of the
+    # published parameters (their pulls) on a low-priority stream.  Pessimistic: on a real node
+    # that traffic moves over xGMI without running on this GPU's CUs
+    emulate_remote: int = 0
     # samples per worker step (e.g. the batch size): adds samples_per_sec to step() data
     samples_per_step: int = 0
     # async PS failure detection: a worker silent for this long (no heartbeat, no STOP) is dead

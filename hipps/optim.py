@@ -263,6 +263,19 @@ class MPI_PS(torch.optim.Optimizer):
 
         return ctx()
 
+    @property
+    def ps_only(self) -> bool:
+        """True on rank 0 of a dedicated async parameter server (``ps_dedicated=True``)."""
+        return bool(getattr(self.engine, "ps_only", False))
+
+    def serve(self, timeout_s: Optional[float] = None) -> dict:
+        """Dedicated PS rank: receive, sum, step and publish until the workers stop; returns the
+        PS statistics (the reference's ``if rank == 0`` loop, README.md:64-73)."""
+        stats = self.engine.serve(timeout_s)
+        self._last_engine_stats = stats
+        self.close()
+        return stats
+
     def irequest_params(self, **kw):
         """AsySG-InCon parameter refresh (README.md:63): adopt the newest published params that
         have arrived, without waiting for the rest (inconsistent read).  No-op in sync modes."""

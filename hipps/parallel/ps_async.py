@@ -129,7 +129,11 @@ class PSAsyncEngine(Engine):
         W = world.size
         self.W = W
         self.rank = world.rank
-        self.M = cfg.accumulate if cfg.accumulate > 0 else W
+        # dedicated PS (cfg.ps_dedicated): rank 0 never trains, so an update waits for the
+        # W - 1 workers' gradients by default
+        self.dedicated = bool(cfg.ps_dedicated) and W > 1
+        self.M = cfg.accumulate if cfg.accumulate > 0 else (W - 1 if self.dedicated else W)
+        self.emu = int(cfg.emulate_remote) if W == 1 else 0  # emulated remote-worker PS load
         self.MAXSLOTS = C.ControlBlock.SLOTS  # stride of the per-slot version words
         self.NPUB = C.ControlBlock.NPUB
         self.timeout_us = int(min(TIMEOUT_US, cfg.comm_timeout_s * 1e6))
@@ -251,9 +255,16 @@ class PSAsyncEngine(Engine):
         if self.rank == 0:
             self.master = store.data.detach().clone()
             self.acc = torch.zeros_like(store.data)
-            self.ps_stream = torch.cuda.Stream(device=store.device) if self.cuda else None
+            # high priority: on a co-located PS (rank 0 also trains) the accumulate / update /
+            # publish kernels must not queue behind worker 0's forward and backward launches
+            self.ps_stream = torch.cuda.Stream(device=store.device, priority=-1) if self.cuda else None
+            gs = self.gscale(self.M) / (1 + self.emu)  # emulated copies leave the average unchanged
             self.core = PSCore(self.ctl, C, W, self.nb, self.order, self.SLOTS, self.MAXSLOTS, self.M,
-                               cfg.staleness, cfg.staleness_lr, self.gscale(self.M), self._stats)
+                               cfg.staleness, cfg.staleness_lr, gs, self._stats)
+            if self.emu:
+                self._emu_stream = torch.cuda.Stream(device=store.device, priority=0) if self.cuda else None
+                self._emu_in = torch.empty(self.plan.wire_nbytes, dtype=torch.uint8, device=store.device)
+                self._emu_sink = torch.empty(self.emu, dtype=self.pub_dtype, device=store.device)
             self.core.backend = self
             self._pend, self._pend_acks = [], []
             self._pres_full = False
@@ -270,6 +281,8 @@ class PSAsyncEngine(Engine):
                 torch.cuda.current_stream(store.device).synchronize()
             self._self_test()
         if self.rank == 0:
+            if self.dedicated:
+                self.remove_hooks()  # rank 0 computes no gradients
             self._thread = threading.Thread(target=self._serve_guard, name="hipps-ps", daemon=True)
             self._thread.start()
         barrier(world)
@@ -503,6 +516,8 @@ class PSAsyncEngine(Engine):
         if self.plan.guarded:
             self._verify_slot(i, slot, bi, seq)
         self._pend.append((bi, scale, self._bucket_msg(bi, self.slot_buf(i, slot))))
+        for _ in range(self.emu):  # emulated remote workers: the same bytes, one launch each
+            self._pend.append((bi, scale, None))
 
     def ack(self, i: int, seq: int):
         self._pend_acks.append((self.C.F_ACK_SEQ, i, seq))
@@ -510,14 +525,21 @@ class PSAsyncEngine(Engine):
     def flush(self):
         if self._pend:
             groups = {}
+            emu = []
             for bi, scale, msg in self._pend:
+                if msg is None:  # emulated remote copy of the preceding real message
+                    emu.append((bi, scale, groups[(bi, scale)][-1]))
+                    continue
                 groups.setdefault((bi, scale), []).append(msg)
             with self.tracer.phase("ps_accumulate", self.ps_stream):
                 for (bi, scale), msgs in groups.items():
                     b = self.plan.buckets[bi]
                     for k in range(0, len(msgs), self.BATCH):
                         self.codec.accumulate(msgs[k:k + self.BATCH], self.acc[b.lo:b.hi], scale, True)
-            self._stats["acc_launches"] = self._stats.get("acc_launches", 0) + sum(
+                for bi, scale, msg in emu:
+                    b = self.plan.buckets[bi]
+                    self.codec.accumulate([msg], self.acc[b.lo:b.hi], scale, True)
+            self._stats["acc_launches"] = self._stats.get("acc_launches", 0) + len(emu) + sum(
                 (len(m) + self.BATCH - 1) // self.BATCH for m in groups.values())
             self._pend = []
         acks = self._pend_acks
@@ -588,7 +610,22 @@ class PSAsyncEngine(Engine):
                                                                            for i, s in last.items()]
         for k in range(0, len(words), 6):
             self._ring(st, words[k:k + 6])
+        if self.emu:
+            self._emulate_remote_traffic(b)
         self.ctl.fetch_add(C.F_UPDATES, 0, 1)
+
+    def _emulate_remote_traffic(self, b: int):
+        """cfg.emulate_remote: E remote workers' pushes (write sweeps of one step's wire bytes)
+        and pulls (read sweeps of the new publish buffer) after this update."""
+        st = self._emu_stream
+        ctx = torch.cuda.stream(st) if st is not None else contextlib.nullcontext()
+        if st is not None:
+            st.wait_stream(self.ps_stream)
+        with ctx:
+            pub = self.pub_buf(b)
+            for e in range(self.emu):
+                self._emu_in.fill_(e)
+                torch.amax(pub, dim=0, out=self._emu_sink[e])
 
     def lookahead_tau(self) -> float:
         """Updates to extrapolate the published parameters by (cfg.stale_lookahead): readers'
@@ -624,7 +661,27 @@ class PSAsyncEngine(Engine):
         if self.cuda and self.enc_event is not None and self.grad_mode == "flat":
             torch.cuda.current_stream(self.store.device).wait_event(self.enc_event)
 
+    @property
+    def ps_only(self) -> bool:
+        return self.dedicated and self.rank == 0
+
+    def serve(self, timeout_s: Optional[float] = None) -> dict:
+        """Dedicated PS (rank 0): serve until every live worker has stopped and every pushed
+        message is consumed (README.md:64-73: rank 0 only receives, sums and steps), then shut the
+        engine down; returns the PS statistics."""
+        if not self.ps_only:
+            raise RuntimeError("serve() is for rank 0 of a dedicated parameter server (ps_dedicated=True)")
+        self.ctl.store(self.C.F_STOP, 0, 1)  # rank 0 pushes nothing
+        deadline = None if timeout_s is None else time.time() + timeout_s
+        while self._thread.is_alive() and (deadline is None or time.time() < deadline):
+            self._thread.join(timeout=0.5)
+        self.close()
+        return self.ps_stats()
+
     def step(self):
+        if self.ps_only:
+            raise RuntimeError("rank 0 is a dedicated parameter server (ps_dedicated=True): it does not train; "
+                               "call opt.serve() there")
         C = self.C
         data = {}
         data["code_wait"] = self.encode_all()
@@ -982,6 +1039,7 @@ class PSAsyncEngine(Engine):
 
     def transport_info(self) -> dict:
         return {"transport": "p2p" if self.p2p else "ipc", "doorbells": self.ctl.bell_mode, "pull": self.pull_mode,
+                "ps_dedicated": self.dedicated, "accumulate": self.M,
                 "npub": self.NPUB,
                 "mailbox_slots": self.SLOTS, "slot_bytes": self.slot_bytes}
 

@@ -180,3 +180,44 @@ def test_async_p2p_slow_ps_with_main_thread_collectives(monkeypatch):
     out = run_world(_train_async, 3, steps, "fp32", 0, -1, -1, "sgd", 0.0005, 2, "p2p", True)
     st = out[0]["stats"]
     assert st["accumulated"] == 3 * steps and st["updates"] == steps
+
+
+def _dedicated(rank, world, steps, transport):
+    """The reference's topology (README.md:64-75): rank 0 only serves, ranks 1..W-1 train."""
+    import hipps
+
+    m = _mlp()
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", ps_dedicated=True,
+                    async_transport=transport)
+    if rank == 0:
+        assert opt.ps_only
+        with pytest.raises(RuntimeError, match="dedicated"):
+            opt.step()
+        st = opt.serve(timeout_s=120)
+        return {"stats": st, "losses": []}
+    assert not opt.ps_only
+    losses, stale = [], []
+    for s in range(steps):
+        x, y = _data(rank, s % 4)
+        opt.zero_grad()
+        loss = torch.nn.functional.cross_entropy(m(x), y)
+        loss.backward()
+        losses.append(loss.item())
+        _, data = opt.step()
+        stale.append(data["staleness"])
+    info = opt.engine.transport_info()
+    opt.close()
+    return {"losses": losses, "info": info, "stale": stale}
+
+
+@pytest.mark.parametrize("transport", ["ipc", "p2p"])
+def test_async_dedicated_ps_topology(transport):
+    steps = 8
+    out = run_world(_dedicated, 3, steps, transport)
+    st = out[0]["stats"]
+    # M defaults to the number of workers (2): one update per round of worker steps
+    assert st["accumulated"] == 2 * steps and st["updates"] == steps, st
+    for r in (1, 2):
+        assert out[r]["info"]["ps_dedicated"] and out[r]["info"]["accumulate"] == 2
+        assert sum(out[r]["losses"][-3:]) < sum(out[r]["losses"][:3])
+        assert all(s >= 0 for s in out[r]["stale"])
