@@ -74,8 +74,9 @@ class PSConfig:
     # GPU distributed modes: gather autograd-owned grads per bucket with one multi-tensor kernel
     # instead of accumulating into preset flat-buffer views (161 fewer kernels for ResNet-50)
     grad_gather: bool = True
-    # published-parameter wire dtype for PS modes: 'fp32' | 'bf16' | 'auto' (bf16 for ps_sync and
-    # ps_async with more than one GPU rank, fp32 otherwise)
+    # published-parameter wire dtype for PS modes: 'fp32' | 'bf16' | 'auto' (bf16 for ps_async with
+    # more than one GPU rank, fp32 otherwise -- ps_sync 'bf16' halves the broadcast but leaves the
+    # non-PS replicas on bf16-rounded copies of the PS's fp32 parameters)
     param_wire: str = "auto"
     # bf16 weight shadow: one flat bf16 copy of the fp32 params, refreshed by one cast kernel after
     # every step()/irequest_params(), read by the hipps conv kernels instead of one autocast cast

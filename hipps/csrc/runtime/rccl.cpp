@@ -6,7 +6,8 @@
 //   * ncclGather (rccl.h:745) -- the PS gather of the sync PS mode in ONE collective;
 //   * all-gather-v as grouped ncclSend/ncclRecv at static per-rank offsets (RCCL has no
 //     allgatherv; the reference needs one, mpi_comms.py:160-163);
-//   * ncclCommSplit (rccl.h:290) for (PS, worker) pair communicators;
+//   * gather-v (grouped ncclRecv at the root) for variable-size object messages;
+//   * ncclCommSplit (rccl.h:290) for sub-communicators;
 //   * ncclCommGetAsyncError / ncclCommAbort (rccl.h:271, 362): the engines poll for a dead peer
 //     and abort the communicator instead of hanging (failure detection).
 // Every call enqueues on the given HIP stream (the engines' comm stream) and returns at once.
@@ -117,6 +118,35 @@ class RcclComm {
                             st(stream)));
   }
 
+  // variable-size gather to root: rank r's send lands at root's recv[displs[r] : + counts[r]]
+  // (the reference's Igatherv with exact counts, mpi_comms.py:88, without its padded slots)
+  void gather_v(at::Tensor send, c10::optional<at::Tensor> recv, const std::vector<int64_t>& counts,
+                const std::vector<int64_t>& displs, int root, uint64_t stream) {
+    dev_contig(send, "send");
+    if ((int)counts.size() != nranks_ || (int)displs.size() != nranks_) throw std::runtime_error("counts/displs size");
+    if (counts[rank_] != send.numel()) throw std::runtime_error("gather_v: send size != counts[rank]");
+    const size_t es = send.element_size();
+    auto dt = dtype_of(send);
+    if (rank_ != root) {
+      if (counts[rank_]) nccl_check(ncclSend(send.data_ptr(), counts[rank_], dt, root, live(), st(stream)), "ncclSend");
+      return;
+    }
+    if (!recv.has_value() || !recv->defined()) throw std::runtime_error("gather_v: root needs recv");
+    dev_contig(*recv, "recv");
+    if (recv->element_size() != (int64_t)es) throw std::runtime_error("gather_v: dtype mismatch");
+    char* rb = static_cast<char*>(recv->data_ptr());
+    for (int r = 0; r < nranks_; ++r)
+      if (displs[r] + counts[r] > recv->numel()) throw std::runtime_error("gather_v: recv too small");
+    nccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (int r = 0; r < nranks_; ++r)
+      if (r != rank_ && counts[r])
+        nccl_check(ncclRecv(rb + displs[r] * es, counts[r], dt, r, live(), st(stream)), "ncclRecv");
+    nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+    if (counts[rank_])
+      hip_ok(hipMemcpyAsync(rb + displs[rank_] * es, send.data_ptr(), counts[rank_] * es, hipMemcpyDeviceToDevice,
+                            st(stream)));
+  }
+
   void gather(at::Tensor send, c10::optional<at::Tensor> recv, int root, uint64_t stream) {
     dev_contig(send, "send");
     void* rp = nullptr;
@@ -210,6 +240,8 @@ void bind_rccl(py::module& m) {
       .def("all_gather", &RcclComm::all_gather)
       .def("all_gather_v", &RcclComm::all_gather_v)
       .def("gather", &RcclComm::gather, py::arg("send"), py::arg("recv"), py::arg("root"), py::arg("stream"))
+      .def("gather_v", &RcclComm::gather_v, py::arg("send"), py::arg("recv"), py::arg("counts"), py::arg("displs"),
+           py::arg("root"), py::arg("stream"))
       .def("broadcast", &RcclComm::broadcast)
       .def("all_reduce_sum", &RcclComm::all_reduce_sum)
       .def("send", &RcclComm::send)

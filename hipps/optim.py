@@ -122,10 +122,13 @@ class MPI_PS(torch.optim.Optimizer):
             mode = "allgather" if self.world.size > 1 else "local"
         self.mode = mode
         if self.cfg.param_wire == "auto":
-            # the PS modes move whole-model parameter versions every step: at W > 1 on GPUs they go
-            # as bf16 (workers compute under bf16 autocast anyway; the fp32 master stays on the PS)
+            # (self.cfg is this optimizer's own copy: PSConfig.replace in __init__)
+            # the async PS moves whole-model parameter versions every step: at W > 1 on GPUs they go
+            # as bf16 (workers compute under bf16 autocast anyway; the fp32 master stays on the PS).
+            # ps_sync keeps the reference's full-precision broadcast (README.md:76), so its replicas
+            # stay bitwise identical to the PS's parameters
             multi = self.world.size > 1 and self.store.device.type == "cuda"
-            self.cfg.param_wire = "bf16" if multi and mode in ("ps_sync", "ps_async") else "fp32"
+            self.cfg.param_wire = "bf16" if multi and mode == "ps_async" else "fp32"
         if mode == "local":
             if self.world.size > 1:
                 raise ValueError("mode='local' with world size > 1")

@@ -103,3 +103,45 @@ def gather_into(out: Optional[torch.Tensor], inp: torch.Tensor, world: World, ds
 def broadcast(t: torch.Tensor, world: World, src: int = 0, group=None):
     if world.size > 1:
         dist.broadcast(t, src=src, group=group)
+
+
+def all_gather_v(out: torch.Tensor, inp: torch.Tensor, counts, world: World, group=None):
+    """Variable-size all-gather (reference Iallgatherv, mpi_comms.py:160-163): rank r's ``counts[r]``
+    elements land at ``out[sum(counts[:r]):]``; exactly the counted bytes move (pairwise
+    isend/irecv: RCCL pair channels on GPU, gloo on CPU)."""
+    displs = [0]
+    for c in counts[:-1]:
+        displs.append(displs[-1] + c)
+    me = world.rank
+    out[displs[me]:displs[me] + counts[me]].copy_(inp)
+    if world.size == 1:
+        return
+    ops = []
+    for r in range(world.size):
+        if r == me:
+            continue
+        if counts[me]:
+            ops.append(dist.P2POp(dist.isend, inp, r, group=group))
+        if counts[r]:
+            ops.append(dist.P2POp(dist.irecv, out[displs[r]:displs[r] + counts[r]], r, group=group))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+
+
+def gather_v(out: Optional[torch.Tensor], inp: torch.Tensor, counts, world: World, dst: int = 0, group=None):
+    """Variable-size gather to ``dst`` (reference Igatherv, mpi_comms.py:88, with exact counts
+    instead of padded slots)."""
+    me = world.rank
+    if me != dst:
+        if counts[me]:
+            dist.send(inp, dst, group=group)
+        return
+    displs = [0]
+    for c in counts[:-1]:
+        displs.append(displs[-1] + c)
+    out[displs[me]:displs[me] + counts[me]].copy_(inp)
+    works = [dist.irecv(out[displs[r]:displs[r] + counts[r]], r, group=group)
+             for r in range(world.size) if r != me and counts[r]]
+    for w in works:
+        w.wait()

@@ -23,7 +23,7 @@ import torch
 
 from hipps.utils.tracing import StepTracer
 
-from .dist import World, all_gather_into, barrier, broadcast, gather_into
+from .dist import World, all_gather_into, all_gather_v, barrier, broadcast, gather_into, gather_v
 from .flat import BucketPlan, FlatStore, _is_dense
 from .watchdog import CommWatchdog, armed
 
@@ -419,11 +419,12 @@ class Engine:
         return [int(v) for v in out.tolist()]
 
     def object_exchange(self, root: Optional[int]) -> Optional[List[bytes]]:
-        """Variable-size exchange of this step's object messages: size round, then one payload
-        collective at the max size (all-gather, or gather to ``root``).  Returns every rank's
-        bytes (None on non-root ranks of a gather)."""
-        import torch.distributed as dist
-
+        """Variable-size exchange of this step's object messages, the reference's two rounds
+        (ps.py:140-147, mpi_comms.py:150-163): one all-gather of the byte counts, then a
+        variable-size all-gather (or gather to ``root``) that moves exactly ``counts[r]`` bytes per
+        rank -- RCCL grouped send/recv (``transport='rccl'``: hipps' native communicator; else the
+        torch process group's pair channels), gloo on CPU.  Returns every rank's bytes (None on
+        non-root ranks of a gather)."""
         blob = self._object_bytes()
         W = self.world.size
         t = time.perf_counter()
@@ -431,22 +432,30 @@ class Engine:
         self._prep_time = time.perf_counter() - t
         if W == 1:
             return [blob]
-        slot = max(1, max(sizes))
-        dev = self.store.device if self.world.backend == "nccl" else torch.device("cpu")
-        send = torch.zeros(slot, dtype=torch.uint8)
-        if blob:
-            send[: len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
+        dev = self.store.device if (self.world.backend == "nccl" or self.rccl is not None) else torch.device("cpu")
+        send = torch.frombuffer(bytearray(blob), dtype=torch.uint8) if blob else torch.empty(0, dtype=torch.uint8)
         send = send.to(dev)
-        if root is None:
-            recv = torch.empty(W * slot, dtype=torch.uint8, device=dev)
-            all_gather_into(recv, send, self.world, group=self.group)
+        receives = root is None or self.world.rank == root
+        recv = torch.empty(max(1, sum(sizes)), dtype=torch.uint8, device=dev) if receives else None
+        displs = [sum(sizes[:r]) for r in range(W)]
+        if self.rccl is not None:
+            st = self.comm_stream
+            st.wait_stream(torch.cuda.current_stream(self.store.device))
+            if root is None:
+                self.rccl.all_gather_v(recv, send, sizes, displs, st)
+            else:
+                self.rccl.gather_v(recv, send, sizes, displs, root, st)
+            send.record_stream(st)
+            torch.cuda.current_stream(self.store.device).wait_stream(st)
+            self.rccl.poll()
+        elif root is None:
+            all_gather_v(recv, send, sizes, self.world, group=self.group)
         else:
-            recv = torch.empty(W * slot, dtype=torch.uint8, device=dev) if self.world.rank == root else None
-            gather_into(recv, send, self.world, dst=root, group=self.group)
-            if self.world.rank != root:
-                return None
+            gather_v(recv, send, sizes, self.world, dst=root, group=self.group)
+        if not receives:
+            return None
         host = recv.cpu().numpy()
-        return [host[w * slot: w * slot + sizes[w]].tobytes() for w in range(W)]
+        return [host[displs[w]: displs[w] + sizes[w]].tobytes() for w in range(W)]
 
     def object_apply(self, blobs: List[bytes], target: torch.Tensor, pub: Optional[torch.Tensor], gscale: float):
         acc = self._obj_acc if getattr(self, "_obj_acc", None) is not None else torch.zeros_like(self.store.grad)
@@ -654,6 +663,14 @@ class _BucketExchange(Engine):
             torch.cuda.current_stream(self.store.device).wait_stream(self.comm_stream)
             if self.rccl is not None:
                 self.rccl.poll()
+                self._watch_device(self.comm_stream, f"{self.name} step {self.steps + 1} collectives")
+
+    def _watch_device(self, stream, what: str):
+        """transport='rccl' enqueues and returns: the watchdog follows the device completion."""
+        if self.watchdog is not None and self.rccl is not None:
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            self.watchdog.watch(ev, what, self.rccl.poll)
 
 
 class AllGatherEngine(_BucketExchange):
@@ -773,6 +790,7 @@ def _bcast_params_impl(self, data):
 
                 ops.convert(self.pub, self.store.data)
             self.rccl.poll()
+            self._watch_device(torch.cuda.current_stream(self.store.device), f"ps_sync step {self.steps + 1} bcast")
         elif self.pub is not None:
             broadcast(self.pub, self.world, 0, group=self.group)
             if not self.world.is_ps:

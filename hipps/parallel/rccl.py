@@ -9,11 +9,15 @@ group it adds what the PS engines need natively:
   * ``all_gather_v`` = grouped send/recv into static per-rank offsets (no allgatherv in RCCL);
   * ``poll()`` = ``ncclCommGetAsyncError``: a lost peer raises instead of hanging;
   * ``abort()`` = ``ncclCommAbort``: the watchdog tears the communicator down before exiting;
-  * ``pair(i)`` = (PS, worker i) communicators from ``ncclCommSplit`` (rccl.h:290).
+  * ``gather_v`` = grouped receives at the root (exact per-rank counts, no padded slots).
+
+``Engine.object_exchange`` moves the reference-style codec objects (ps.py:140-147 /
+mpi_comms.py:150-163: a size round, then a variable-size all-gather) through ``all_gather_v`` /
+``gather_v`` when ``transport='rccl'``.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Optional
+from typing import List, Optional
 
 import torch
 import torch.distributed as dist
@@ -35,7 +39,6 @@ class RcclGroup:
             dist.broadcast_object_list(uid, src=0)
         with torch.cuda.device(device):
             self.comm = C.RcclComm(uid[0], world.size, world.rank)
-        self._pairs: Dict[int, object] = {}
 
     @staticmethod
     def _stream(stream=None) -> int:
@@ -50,16 +53,12 @@ class RcclGroup:
     def gather_into(self, out: Optional[torch.Tensor], inp: torch.Tensor, dst: int = 0, stream=None):
         self.comm.gather(inp, out, dst, self._stream(stream))
 
+    def gather_v(self, out: Optional[torch.Tensor], inp: torch.Tensor, counts: List[int], displs: List[int],
+                 dst: int = 0, stream=None):
+        self.comm.gather_v(inp, out, counts, displs, dst, self._stream(stream))
+
     def broadcast(self, t: torch.Tensor, src: int = 0, stream=None):
         self.comm.broadcast(t, src, self._stream(stream))
-
-    def pair(self, i: int):
-        """(PS = rank 0, worker i) communicator; collective: every rank calls pair(i) in order."""
-        if i not in self._pairs:
-            r = self.world.rank
-            color = 0 if r in (0, i) else -1
-            self._pairs[i] = self.comm.split(color, 0 if r == 0 else 1)
-        return self._pairs[i]
 
     def poll(self):
         """Raise if RCCL reported an asynchronous error (ncclCommGetAsyncError)."""
@@ -68,14 +67,7 @@ class RcclGroup:
             raise RcclError(f"RCCL communicator failed: {self.comm.error_string(code)} (code {code})")
 
     def abort(self):
-        for p in self._pairs.values():
-            if p is not None:
-                p.abort()
         self.comm.abort()
 
     def close(self):
-        for p in self._pairs.values():
-            if p is not None:
-                p.destroy()
-        self._pairs = {}
         self.comm.destroy()

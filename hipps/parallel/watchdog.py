@@ -10,7 +10,11 @@ hipps bounds every exchange twice:
   * a host-side watchdog thread covers what the process group cannot see (a host wait on a
     device result, a peer that hangs mid-protocol): if one exchange stays armed longer than
     ``1.5 * comm_timeout_s + 5`` s it prints which exchange and step stalled and exits the
-    process with status 3 (``os._exit`` -- never a re-exec), so the launcher tears the job down.
+    process with status 3 (``os._exit`` -- never a re-exec), so the launcher tears the job down;
+  * enqueue-only exchanges (hipps' own RCCL communicator returns as soon as the collectives are
+    queued, so ``step()`` never blocks on them) hand the watchdog a HIP event recorded after their
+    last collective: the thread polls ``ncclCommGetAsyncError`` and the event until the event
+    completes, and aborts the communicator and exits if it has not after the same limit.
 """
 from __future__ import annotations
 
@@ -29,6 +33,7 @@ class CommWatchdog:
         self.rank = rank
         self.on_abort = on_abort  # e.g. ncclCommAbort of hipps' own communicator
         self._armed: Optional[tuple] = None  # (what, t0)
+        self._events: list = []  # [(event, what, t0, poll)] device completions still pending
         self._lock = threading.Lock()
         self._stop = threading.Event()
         self._thread = threading.Thread(target=self._run, name="hipps-watchdog", daemon=True)
@@ -42,24 +47,57 @@ class CommWatchdog:
         with self._lock:
             self._armed = None
 
+    def watch(self, event, what: str, poll=None):
+        """Track an enqueued exchange until ``event`` (recorded after its last collective) has
+        completed; ``poll()`` raises on an asynchronous communicator error."""
+        with self._lock:
+            self._events.append((event, what, time.monotonic(), poll))
+
+    def pending(self) -> int:
+        with self._lock:
+            return len(self._events)
+
     def close(self):
         self._stop.set()
+
+    def _fail(self, what: str, why: str):
+        sys.stderr.write(f"[hipps] rank {self.rank}: exchange '{what}' {why}; a peer is dead or hung -- aborting "
+                         f"with status {self.EXIT_CODE}\n")
+        sys.stderr.flush()
+        if self.on_abort is not None:
+            try:
+                self.on_abort()
+            except Exception:
+                pass
+        os._exit(self.EXIT_CODE)
+
+    def _check_events(self):
+        with self._lock:
+            evs = list(self._events)
+        done = []
+        now = time.monotonic()
+        for item in evs:
+            ev, what, t0, poll = item
+            if poll is not None:
+                try:
+                    poll()
+                except Exception as e:  # ncclCommGetAsyncError reported a failure
+                    self._fail(what, f"failed asynchronously ({e})")
+            if ev.query():
+                done.append(item)
+            elif now - t0 > self.limit:
+                self._fail(what, f"did not complete on the device within {self.limit:.0f}s (comm_timeout_s)")
+        if done:
+            with self._lock:
+                self._events = [e for e in self._events if e not in done]
 
     def _run(self):
         while not self._stop.wait(min(1.0, self.limit / 10)):
             with self._lock:
                 a = self._armed
             if a is not None and time.monotonic() - a[1] > self.limit:
-                sys.stderr.write(f"[hipps] rank {self.rank}: exchange '{a[0]}' stalled for {self.limit:.0f}s "
-                                 f"(comm_timeout_s); a peer is dead or hung -- aborting with status "
-                                 f"{self.EXIT_CODE}\n")
-                sys.stderr.flush()
-                if self.on_abort is not None:
-                    try:
-                        self.on_abort()
-                    except Exception:
-                        pass
-                os._exit(self.EXIT_CODE)
+                self._fail(a[0], f"stalled for {self.limit:.0f}s (comm_timeout_s)")
+            self._check_events()
 
 
 class armed:

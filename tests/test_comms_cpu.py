@@ -73,3 +73,31 @@ def test_serialization_roundtrip_and_compat():
     assert S.bytes_of({"a": torch.ones(2, 3), "b": [torch.ones(4, dtype=torch.int8)]}) == 28
     back = S.to_torch(S.to_np({"a": torch.ones(2, dtype=torch.float64)}))
     assert back["a"].dtype == torch.float64
+
+
+def _agv(rank, world):
+    import torch
+
+    from hipps.parallel import dist as hdist
+
+    w = hdist.current()
+    counts = [5, 0, 11][:world]
+    inp = torch.arange(counts[rank], dtype=torch.uint8) + 10 * rank
+    out = torch.full((sum(counts),), 255, dtype=torch.uint8)
+    hdist.all_gather_v(out, inp, counts, w)
+    g = torch.full((sum(counts),), 255, dtype=torch.uint8) if rank == 1 else None
+    hdist.gather_v(g, inp, counts, w, dst=1)
+    return out, g
+
+
+def test_all_gather_v_and_gather_v_exact_counts():
+    """Iallgatherv / Igatherv with exact per-rank counts (mpi_comms.py:88, 160-163), a zero count
+    included: nothing padded, nothing lost."""
+    import torch
+
+    out = run_world(_agv, 3)
+    want = torch.cat([torch.arange(5, dtype=torch.uint8), torch.arange(11, dtype=torch.uint8) + 20])
+    for r in range(3):
+        assert torch.equal(out[r][0], want)
+    assert torch.equal(out[1][1], want)
+    assert out[0][1] is None and out[2][1] is None

@@ -58,3 +58,48 @@ def test_dead_peer_fails_fast(monkeypatch, mode, kind):
             if p.is_alive():
                 p.kill()
                 p.join()
+
+
+_WD_SCRIPT = r"""
+import sys, time
+sys.path.insert(0, {root!r})
+from hipps.parallel.watchdog import CommWatchdog
+
+class Ev:
+    def __init__(self, done): self.done = done
+    def query(self): return self.done
+
+aborted = []
+wd = CommWatchdog(0.01, rank=0, on_abort=lambda: print("ABORT", flush=True))
+kind = sys.argv[1]
+wd.watch(Ev(True), "finished collective")
+if kind == "hang":
+    wd.watch(Ev(False), "allgather step 3 collectives")
+elif kind == "error":
+    def poll():
+        raise RuntimeError("RCCL communicator failed: remote process exited")
+    wd.watch(Ev(False), "ps_sync step 2 bcast", poll)
+time.sleep(9)
+print("pending", wd.pending(), flush=True)
+"""
+
+
+@pytest.mark.parametrize("kind", ["ok", "hang", "error"])
+def test_watchdog_follows_enqueued_device_exchanges(kind, tmp_path):
+    """transport='rccl' exchanges return once enqueued; the watchdog keeps following
+    their completion event -- a collective that never completes, or an asynchronous RCCL error,
+    aborts the communicator and exits with status 3 instead of surfacing later in user code."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    f = tmp_path / "wd.py"
+    f.write_text(_WD_SCRIPT.format(root=root))
+    r = subprocess.run([sys.executable, str(f), kind], capture_output=True, text=True, timeout=60)
+    if kind == "ok":
+        assert r.returncode == 0 and "pending 0" in r.stdout, r.stderr
+    else:
+        assert r.returncode == 3, (r.returncode, r.stdout, r.stderr)
+        assert "ABORT" in r.stdout
+        assert ("did not complete" in r.stderr) if kind == "hang" else ("failed asynchronously" in r.stderr)

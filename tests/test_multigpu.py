@@ -66,3 +66,135 @@ def test_async_ps_across_devices(pull, codec, transport):
         if pull == "device" and transport == "ipc":
             assert o["pull"] == "device"
         assert o["transport"] == transport
+
+
+def _sync(rank, world, mode, transport, codec):
+    """allgather / ps_sync across devices: replicas must be bitwise identical."""
+    import torch.nn.functional as F
+
+    import hipps
+    from hipps.models import resnet_tiny
+
+    dev = torch.device("cuda", rank)
+    torch.manual_seed(0)
+    m = resnet_tiny().to(dev).to(memory_format=torch.channels_last)
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, dampening=0.1, mode=mode, code=codec,
+                    transport=transport, param_wire="fp32", average=True)
+    g = torch.Generator(device="cpu").manual_seed(rank)
+    x = torch.randn(8, 3, 32, 32, generator=g).to(dev).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), generator=g).to(dev)
+    for _ in range(4):
+        opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = F.cross_entropy(m(x), y)
+        loss.backward()
+        opt.step()
+    torch.cuda.synchronize()
+    opt.close()
+    return [p.detach().float().cpu() for p in m.parameters()]
+
+
+@pytest.mark.parametrize("mode", ["allgather", "ps_sync"])
+@pytest.mark.parametrize("transport", ["torch", "rccl"])
+@pytest.mark.parametrize("codec", ["bf16", "topk_int8:0.05"])
+def test_sync_modes_across_devices_bitwise_replicas(mode, transport, codec):
+    W = min(NDEV, 4)
+    out = run_world(_sync, W, mode, transport, codec, timeout=600, backend="nccl")
+    for r in range(1, W):
+        for a, b in zip(out[0], out[r]):
+            assert torch.equal(a, b), f"rank {r} diverged ({mode}, {transport}, {codec})"
+
+
+def _rccl_v(rank, world):
+    from hipps.parallel import dist as hdist
+    from hipps.parallel.rccl import RcclGroup
+
+    dev = torch.device("cuda", rank)
+    g = RcclGroup(hdist.current(), dev)
+    counts = [(7 * r + 3) % 11 for r in range(world)]  # includes a zero count at rank 1
+    displs = [sum(counts[:r]) for r in range(world)]
+    inp = (torch.arange(counts[rank], device=dev, dtype=torch.int32) + 100 * rank)
+    out = torch.full((sum(counts),), -1, dtype=torch.int32, device=dev)
+    g.all_gather_v(out, inp, counts, displs)
+    gat = torch.full((sum(counts),), -1, dtype=torch.int32, device=dev) if rank == 0 else None
+    g.gather_v(gat, inp, counts, displs, 0)
+    torch.cuda.synchronize()
+    g.poll()
+    g.close()
+    return out.cpu(), None if gat is None else gat.cpu(), counts
+
+
+def test_rccl_all_gather_v_and_gather_v_across_devices():
+    W = min(NDEV, 4)
+    out = run_world(_rccl_v, W, timeout=300, backend="nccl")
+    counts = out[0][2]
+    want = torch.cat([torch.arange(c, dtype=torch.int32) + 100 * r for r, c in enumerate(counts)])
+    for r in range(W):
+        assert torch.equal(out[r][0], want)
+    assert torch.equal(out[0][1], want)
+
+
+def _p2p_collectives(rank, world):
+    """p2p async transport: the PS thread serves pair send/recv while rank 0's main thread runs
+    all_reduce + barrier on the default RCCL group every step."""
+    import torch.distributed as dist
+    import torch.nn.functional as F
+
+    import hipps
+    from hipps.models import resnet_tiny
+
+    dev = torch.device("cuda", rank)
+    m = resnet_tiny().to(dev).to(memory_format=torch.channels_last)
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", code="bf16",
+                    async_transport="p2p", average=True)
+    x = torch.randn(8, 3, 32, 32, device=dev).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device=dev)
+    for _ in range(12):
+        opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            F.cross_entropy(m(x), y).backward()
+        opt.step()
+        t = torch.ones(1, device=dev)
+        dist.all_reduce(t)
+        assert t.item() == world
+        dist.barrier(device_ids=[rank])
+    torch.cuda.synchronize()
+    eng = opt.engine
+    opt.close()
+    return eng.ps_stats()
+
+
+def test_p2p_transport_with_main_thread_collectives_across_devices():
+    W = min(NDEV, 4)
+    out = run_world(_p2p_collectives, W, timeout=600, backend="nccl")
+    assert out[0]["accumulated"] == 12 * W
+
+
+def _dedicated(rank, world):
+    import torch.nn.functional as F
+
+    import hipps
+    from hipps.models import resnet_tiny
+
+    dev = torch.device("cuda", rank)
+    m = resnet_tiny().to(dev).to(memory_format=torch.channels_last)
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", code="bf16", ps_dedicated=True,
+                    average=True)
+    if opt.ps_only:
+        return opt.serve(timeout_s=300)
+    x = torch.randn(8, 3, 32, 32, device=dev).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device=dev)
+    for _ in range(10):
+        opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            F.cross_entropy(m(x), y).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    opt.close()
+    return None
+
+
+def test_dedicated_ps_across_devices():
+    W = min(NDEV, 4)
+    out = run_world(_dedicated, W, timeout=600, backend="nccl")
+    assert out[0]["accumulated"] == 10 * (W - 1) and out[0]["updates"] == 10
