@@ -1,0 +1,368 @@
+// hipps — second-generation MFMA GEMM core for channels-last convolutions (gfx950).
+//
+//   Y[M, N] = X[M, K] · W[N, K]^T       1x1 conv: M = images*Ho*Wo, K = Cin, N = Cout
+//                                       KxK conv: implicit GEMM, K = KH*KW*Cin (k = tap*Cin + c)
+//
+// What changes against the first core (gemm.hip k_conv1x1_nt, register-staged 128x128 tiles of
+// 64x64-per-wave, 4 waves):
+//   * staging by LDS DMA: every 16-byte chunk goes global -> LDS with global_load_lds_dwordx4,
+//     no VGPR round trip and no ds_write pass (cdna_hip_programming.md §5 'Async global->LDS
+//     copy'); the XOR swizzle (LDS slot = chunk ^ (row & 7)) is applied on the per-lane GLOBAL
+//     address, so each wave-instruction's 1 KB LDS image stays lane-linear;
+//   * rows outside M and zero-padding taps fetch a 16-byte zero page instead of branching;
+//   * larger per-wave tiles (128x64 of 16x16x32 accumulators: 12 fragment reads per 32 MFMAs
+//     instead of 8 per 16) -- the 64x64 core was LDS-read bound at the MFMA rate
+//     (profiles/ab_r2/gemm_pf2_probe.json);
+//   * block tiles 256x256 (8 waves), 256x128 / 128x128 (4 waves), picked per shape by the host
+//     so the grid covers the 256 CUs; a bijective XCD-aware block order keeps the N tiles of one
+//     M tile on one XCD (A rows re-read from that XCD's L2);
+//   * one raw s_barrier per K-tile: the DMA of tile k+1 is issued right after it and lands
+//     during the MFMAs of tile k; s_setprio(1) around the MFMA cluster.
+// The epilogue (bf16 tile staged through LDS for 16-byte row stores, optional per-channel BN
+// statistics, optional "+ R * mask" residual-gradient add) matches the first core's semantics.
+#include "common.h"
+
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+namespace hipps {
+namespace g2 {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
+constexpr int BK = 64;  // k per stage = 8 chunks of 16 bytes per row
+
+// 16-byte zero source for out-of-range rows and zero-padding taps (global memory, read-only)
+__device__ __attribute__((aligned(64))) const uint16_t kZero16[32] = {0};
+
+enum Epi : int { kPlain = 0, kStats = 1, kAdd = 2 };
+
+template <int BM, int BN> struct Cfg;
+template <> struct Cfg<256, 256> { static constexpr int TM = 128, TN = 64; };
+template <> struct Cfg<256, 128> { static constexpr int TM = 128, TN = 64; };
+template <> struct Cfg<128, 128> { static constexpr int TM = 64, TN = 64; };
+template <> struct Cfg<256, 64> { static constexpr int TM = 64, TN = 64; };
+
+template <int BM, int BN> constexpr int nthreads() { return 64 * (BM / Cfg<BM, BN>::TM) * (BN / Cfg<BM, BN>::TN); }
+
+template <int BM, int BN> constexpr int lds_bytes() {
+  constexpr int stage = 2 * (BM + BN) * BK * 2;
+  constexpr int epi = BM * (BN + 8) * 2;
+  constexpr int wm = BM / Cfg<BM, BN>::TM;
+  return (stage > epi ? stage : epi) + 2 * 2 * wm * BN * 4;
+}
+
+struct Args {
+  const uint16_t* X;
+  const uint16_t* W;
+  uint16_t* Y;
+  float* pa;
+  float* pb;
+  const uint16_t* R;
+  const uint8_t* RM;
+  int M, N, K, Ho, Wo, Hi, Wi, stride, mtiles, ntiles;
+  int KW, pad, Cin;  // implicit-GEMM geometry (TAPS)
+};
+
+__device__ __forceinline__ uint32_t add_bf16x2(uint32_t a, uint32_t b) {
+  return pack_bf16x2(__uint_as_float(a << 16) + __uint_as_float(b << 16),
+                     __uint_as_float(a & 0xffff0000u) + __uint_as_float(b & 0xffff0000u));
+}
+
+__device__ __forceinline__ void glds16(const void* src, void* dst) {
+  __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)dst, 16, 0, 0);
+}
+
+template <int BM, int BN, int EPI, bool TAPS>
+__global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
+  constexpr int TM = Cfg<BM, BN>::TM, TN = Cfg<BM, BN>::TN;
+  constexpr int WM = BM / TM, WN = BN / TN, NW = WM * WN, NT = 64 * NW;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int STAGE = (BM + BN) * BK;   // elements per stage
+  constexpr int AI = BM / 8 / NW;         // A wave-instructions (8 rows x 128 B each) per stage per wave
+  constexpr int BI = BN / 8 / NW;
+  constexpr int EP = BN + 8;              // epilogue row pitch (elements)
+  constexpr int SCR = (2 * STAGE * 2 > BM * EP * 2 ? 2 * STAGE * 2 : BM * EP * 2);  // bytes before the stats scratch
+  static_assert(AI >= 1 && BI >= 1, "tile too small for the wave count");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[lds_bytes<BM, BN>() / 2];
+
+  // bijective XCD-aware block order (cdna_hip_programming.md §5 'XCD swizzle must be bijective'):
+  // the hardware deals blocks round-robin to 8 XCDs; give each XCD a contiguous run of tiles
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int mt = bid / g.ntiles, nt = bid - mt * g.ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w / WN, wn = w - (w / WN) * WN;
+  const int lr = lane >> 3, lc = (lane & 7) ^ lr;  // row in the 8-row group, logical chunk fetched
+
+  // ---- per-lane sources (fixed over the K loop) ----
+  const uint16_t* a_src[AI];  // 1x1: row base + chunk; TAPS: image base
+  int a_h[TAPS ? AI : 1], a_w[TAPS ? AI : 1];
+  bool a_ok[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int row = 8 * (i * NW + w) + lr;
+    int m = m0 + row;
+    a_ok[i] = m < g.M;
+    m = a_ok[i] ? m : g.M - 1;
+    if constexpr (TAPS) {
+      const int hw = g.Ho * g.Wo;
+      const int img = m / hw, rem = m - img * hw;
+      const int ho = rem / g.Wo, wo = rem - ho * g.Wo;
+      a_h[i] = ho * g.stride - g.pad;
+      a_w[i] = wo * g.stride - g.pad;
+      a_src[i] = g.X + (int64_t)img * g.Hi * g.Wi * g.Cin + lc * 8;
+    } else {
+      int64_t src = m;
+      if (g.stride != 1) {
+        const int hw = g.Ho * g.Wo;
+        const int img = m / hw, rem = m - img * hw;
+        const int ho = rem / g.Wo, wo = rem - ho * g.Wo;
+        src = ((int64_t)img * g.Hi + (int64_t)ho * g.stride) * g.Wi + (int64_t)wo * g.stride;
+      }
+      a_src[i] = g.X + src * g.K + lc * 8;
+    }
+  }
+  const uint16_t* b_src[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) b_src[i] = g.W + (int64_t)(n0 + 8 * (i * NW + w) + lr) * g.K + lc * 8;
+
+  auto issue = [&](int kt, int s) {
+    const int k0 = kt * BK;
+    uint16_t* base = lds + s * STAGE;
+    if constexpr (TAPS) {
+      const int tap = k0 / g.Cin, c0 = k0 - tap * g.Cin;
+      const int kr = tap / g.KW, kc = tap - kr * g.KW;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const int hi = a_h[i] + kr, wi = a_w[i] + kc;
+        const bool ok = a_ok[i] && hi >= 0 && hi < g.Hi && wi >= 0 && wi < g.Wi;
+        const uint16_t* p = ok ? a_src[i] + ((int64_t)hi * g.Wi + wi) * g.Cin + c0 : kZero16;
+        glds16(p, base + 8 * (i * NW + w) * BK);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < AI; ++i) glds16(a_ok[i] ? a_src[i] + k0 : kZero16, base + 8 * (i * NW + w) * BK);
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) glds16(b_src[i] + k0, base + BM * BK + 8 * (i * NW + w) * BK);
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int KT = g.K / BK;
+  issue(0, 0);
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    // this wave's DMA of tile kt has landed and its reads of tile kt-1 are retired; after the
+    // barrier every wave's have, so tile kt is readable and the other buffer is free to refill
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 1 < KT) issue(kt + 1, cur ^ 1);
+    const uint16_t* As = lds + cur * STAGE;
+    const uint16_t* Bs = As + BM * BK;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      const int c = ks * 4 + (lane >> 4);
+      bf16x8 a[FM], b[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = wn * TN + j * 16 + (lane & 15);
+        b[j] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + ((c ^ (row & 7)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int row = wm * TM + i * 16 + (lane & 15);
+        a[i] = *reinterpret_cast<const bf16x8*>(As + row * BK + ((c ^ (row & 7)) << 3));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue: bf16 tile -> LDS (padded rows), per-channel stats, 16-byte row stores ----
+  // C/D map (16x16x32): column = lane & 15, row = (lane >> 4) * 4 + r.
+  float* st = reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(lds) + SCR);
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col = wn * TN + j * 16 + (lane & 15);
+    float s = 0.f, qq = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+        const uint16_t hb = f32_to_bf16(acc[i][j][r]);
+        lds[row * EP + col] = hb;
+        if (EPI == kStats && m0 + row < g.M) {
+          const float v = bf16_to_f32(hb);
+          s += v;
+          qq = fmaf(v, v, qq);
+        }
+      }
+    }
+    if (EPI == kStats) {
+      s += __shfl_xor(s, 16, 64);
+      qq += __shfl_xor(qq, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      qq += __shfl_xor(qq, 32, 64);
+      if (lane < 16) {
+        st[(wm * BN + col) * 2] = s;
+        st[(wm * BN + col) * 2 + 1] = qq;
+      }
+    }
+  }
+  __syncthreads();
+  constexpr int RCH = BN / 8;             // 16-byte chunks per output row
+  constexpr int NOUT = BM * RCH / NT;     // output chunks per thread
+  static_assert(BM * RCH % NT == 0, "epilogue split");
+#pragma unroll
+  for (int i = 0; i < NOUT; ++i) {
+    const int id = t + NT * i;
+    const int row = id / RCH, c = id - row * RCH;
+    if (m0 + row < g.M) {
+      const int64_t o = (int64_t)(m0 + row) * g.N + n0 + c * 8;
+      uint4 v = *reinterpret_cast<const uint4*>(lds + row * EP + c * 8);
+      if (EPI == kAdd) {  // + R (* ReLU-mask bits): a second gradient path into Y
+        u32x4 r = *reinterpret_cast<const u32x4*>(g.R + o);
+        if (g.RM != nullptr) {
+          const uint32_t mb = g.RM[o >> 3];
+          r.x &= (mb & 1u ? 0xffffu : 0u) | (mb & 2u ? 0xffff0000u : 0u);
+          r.y &= (mb & 4u ? 0xffffu : 0u) | (mb & 8u ? 0xffff0000u : 0u);
+          r.z &= (mb & 16u ? 0xffffu : 0u) | (mb & 32u ? 0xffff0000u : 0u);
+          r.w &= (mb & 64u ? 0xffffu : 0u) | (mb & 128u ? 0xffff0000u : 0u);
+        }
+        v.x = add_bf16x2(v.x, r.x);
+        v.y = add_bf16x2(v.y, r.y);
+        v.z = add_bf16x2(v.z, r.z);
+        v.w = add_bf16x2(v.w, r.w);
+      }
+      *reinterpret_cast<uint4*>(g.Y + o) = v;
+    }
+  }
+  if (EPI == kStats && t < BN) {
+    float s = 0.f, qq = 0.f;
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+      s += st[(i * BN + t) * 2];
+      qq += st[(i * BN + t) * 2 + 1];
+    }
+    g.pa[(int64_t)(n0 + t) * g.mtiles + mt] = s;
+    g.pb[(int64_t)(n0 + t) * g.mtiles + mt] = qq;
+  }
+}
+
+// block tile for a problem: the largest tile whose grid still gives every CU work
+inline void pick_tile(int64_t M, int64_t N, int& bm, int& bn) {
+  auto blocks = [&](int a, int b) { return ((M + a - 1) / a) * (N / b); };
+  if (N % 256 == 0 && blocks(256, 256) >= 256) { bm = 256; bn = 256; return; }
+  if (N % 128 == 0 && blocks(256, 128) >= 256) { bm = 256; bn = 128; return; }
+  if (N % 128 == 0) { bm = 128; bn = 128; return; }
+  bm = 256; bn = 64;
+}
+
+}  // namespace g2
+
+int64_t gemm2_mtiles(int64_t M, int64_t N, int64_t bm_req) {
+  int bm = (int)bm_req, bn = 0;
+  if (bm <= 0) g2::pick_tile(M, N, bm, bn);
+  return (M + bm - 1) / bm;
+}
+
+// x: [img, Cin, Hi, Wi] channels-last bf16; w: [Cout, Cin, KH, KW] channels-last bf16 (1x1: [Cout, Cin]);
+// y: [img, Cout, Ho, Wo] channels-last bf16.  part (optional): f32 [2, Cout, mtiles] BN statistics
+// partials (mtiles = gemm2_mtiles(M, N, bm)).  add (+ add_mask): y = conv(x) + add (* mask bits).
+// bm / bn: block tile (0 = pick per shape).
+void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part,
+                c10::optional<at::Tensor> add, c10::optional<at::Tensor> add_mask, int64_t Hi, int64_t Wi,
+                int64_t stride, int64_t KH, int64_t KW, int64_t pad, int64_t bm, int64_t bn) {
+  TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "gemm2: device tensors");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
+                  y.scalar_type() == at::kBFloat16, "gemm2: bf16 tensors");
+  const int64_t N = w.size(0), K = w.numel() / N, Cin = K / (KH * KW);
+  TORCH_CHECK(Cin * KH * KW == K && Cin % g2::BK == 0 && N % 64 == 0, "gemm2: needs Cin % 64 == 0, Cout % 64 == 0");
+  const int64_t imgs = x.numel() / (Cin * Hi * Wi);
+  TORCH_CHECK(imgs * Cin * Hi * Wi == x.numel(), "gemm2: x size");
+  const int64_t Ho = (Hi + 2 * pad - KH) / stride + 1, Wo = (Wi + 2 * pad - KW) / stride + 1;
+  const int64_t M = imgs * Ho * Wo;
+  TORCH_CHECK(y.numel() == M * N, "gemm2: y size");
+  for (const at::Tensor* t : {&x, &w, &y})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm2: 16-byte aligned tensors");
+  TORCH_CHECK(x.dim() != 4 || x.is_contiguous(at::MemoryFormat::ChannelsLast), "gemm2: channels-last x");
+  TORCH_CHECK(y.dim() != 4 || y.is_contiguous(at::MemoryFormat::ChannelsLast), "gemm2: channels-last y");
+  TORCH_CHECK(w.dim() != 4 || KH * KW == 1 || w.is_contiguous(at::MemoryFormat::ChannelsLast), "gemm2: channels-last w");
+  TORCH_CHECK(M < (int64_t(1) << 31) && x.numel() < (int64_t(1) << 40), "gemm2: size");
+  int BMv = (int)bm, BNv = (int)bn;
+  if (BMv <= 0 || BNv <= 0) g2::pick_tile(M, N, BMv, BNv);
+  TORCH_CHECK(N % BNv == 0, "gemm2: Cout must be a multiple of the block tile");
+  const int64_t mtiles = (M + BMv - 1) / BMv, ntiles = N / BNv;
+  g2::Args a{};
+  a.X = (const uint16_t*)x.data_ptr();
+  a.W = (const uint16_t*)w.data_ptr();
+  a.Y = (uint16_t*)y.data_ptr();
+  a.M = (int)M; a.N = (int)N; a.K = (int)K; a.Ho = (int)Ho; a.Wo = (int)Wo; a.Hi = (int)Hi; a.Wi = (int)Wi;
+  a.stride = (int)stride; a.mtiles = (int)mtiles; a.ntiles = (int)ntiles;
+  a.KW = (int)KW; a.pad = (int)pad; a.Cin = (int)Cin;
+  int epi = g2::kPlain;
+  if (part.has_value() && part->defined()) {
+    TORCH_CHECK(part->is_cuda() && part->scalar_type() == at::kFloat && part->is_contiguous() &&
+                    part->numel() == 2 * N * mtiles, "gemm2: part must be f32 [2, Cout, mtiles]");
+    a.pa = part->data_ptr<float>();
+    a.pb = a.pa + N * mtiles;
+    epi = g2::kStats;
+  }
+  if (add.has_value() && add->defined()) {
+    TORCH_CHECK(epi == g2::kPlain, "gemm2: statistics and add epilogues are exclusive");
+    TORCH_CHECK(add->is_cuda() && add->scalar_type() == at::kBFloat16 && add->numel() == M * N &&
+                    reinterpret_cast<uintptr_t>(add->data_ptr()) % 16 == 0, "gemm2: add shaped like y");
+    a.R = (const uint16_t*)add->data_ptr();
+    if (add_mask.has_value() && add_mask->defined()) {
+      TORCH_CHECK(add_mask->is_cuda() && add_mask->scalar_type() == at::kByte && add_mask->numel() == M * N / 8,
+                  "gemm2: add_mask must be uint8[numel(y)/8]");
+      a.RM = (const uint8_t*)add_mask->data_ptr();
+    }
+    epi = g2::kAdd;
+  }
+  const bool taps = !(KH == 1 && KW == 1 && pad == 0);
+  auto stream = c10::hip::getCurrentHIPStream();
+  const int grid = (int)(mtiles * ntiles);
+#define HIPPS_G2(BMc, BNc, EPc, TPc) \
+  hipLaunchKernelGGL((g2::k_gemm<BMc, BNc, EPc, TPc>), grid, (g2::nthreads<BMc, BNc>()), 0, stream, a)
+#define HIPPS_G2_E(BMc, BNc)                                                    \
+  do {                                                                          \
+    if (taps) {                                                                 \
+      if (epi == g2::kStats) HIPPS_G2(BMc, BNc, g2::kStats, true);              \
+      else HIPPS_G2(BMc, BNc, g2::kPlain, true);                                \
+    } else if (epi == g2::kStats) HIPPS_G2(BMc, BNc, g2::kStats, false);        \
+    else if (epi == g2::kAdd) HIPPS_G2(BMc, BNc, g2::kAdd, false);              \
+    else HIPPS_G2(BMc, BNc, g2::kPlain, false);                                 \
+  } while (0)
+  TORCH_CHECK(!(taps && epi == g2::kAdd), "gemm2: the add epilogue is for 1x1 convolutions");
+  if (BMv == 256 && BNv == 256) HIPPS_G2_E(256, 256);
+  else if (BMv == 256 && BNv == 128) HIPPS_G2_E(256, 128);
+  else if (BMv == 128 && BNv == 128) HIPPS_G2_E(128, 128);
+  else if (BMv == 256 && BNv == 64) HIPPS_G2_E(256, 64);
+  else TORCH_CHECK(false, "gemm2: unsupported block tile ", BMv, "x", BNv);
+#undef HIPPS_G2_E
+#undef HIPPS_G2
+}
+
+}  // namespace hipps

@@ -494,8 +494,11 @@ class PSAsyncEngine(Engine):
         if self.p2p:
             return self._serve_p2p()
         core = self.core
+        delay = float(os.environ.get("HIPPS_PS_LOOP_DELAY_US", "0")) * 1e-6  # tests: a slow PS thread
         with torch.no_grad():
             while True:
+                if delay:
+                    time.sleep(delay)
                 ready = self.ctl.wait_any(core.seen, 20000)
                 for i in ready:
                     core.pump(i)
@@ -1113,7 +1116,8 @@ class PSAsyncEngine(Engine):
         if self.rank == 0:
             self.ps_stream.synchronize() if self.cuda else None
             d.update({"master": self.master.detach().cpu(), "version": self.ver, "acc": self.acc.detach().cpu(),
-                      "acc_count": self.core.count})
+                      "acc_count": self.core.count, "ps_accumulated": self._stats["accumulated"],
+                      "ps_seen": list(self.core.seen)})
         return d
 
     def load_engine_state(self, d: dict):

@@ -50,6 +50,7 @@ def save(opt, path: str, model: Optional[torch.nn.Module] = None, extra: Optiona
         version = es.pop("version", None)
         acc = es.pop("acc", None)
         acc_count = es.pop("acc_count", 0)
+        ps_acc, ps_seen = es.pop("ps_accumulated", None), es.pop("ps_seen", None)
         mine = {"engine": es}
         if model is not None:
             mine["buffers"] = _buffers(model)
@@ -62,6 +63,8 @@ def save(opt, path: str, model: Optional[torch.nn.Module] = None, extra: Optiona
                   "chunk_steps": None if opt.chunk_steps is None else opt.chunk_steps.detach().cpu()}
             if acc is not None:
                 ps["acc"], ps["acc_count"] = acc, int(acc_count)
+                # PS consumption at the snapshot: messages accumulated so far, per-worker seen seq
+                ps["ps_accumulated"], ps["ps_seen"] = int(ps_acc), [int(v) for v in ps_seen]
             if extra:
                 ps["extra"] = extra
             torch.save(ps, os.path.join(path, "ps.pt"))
