@@ -44,6 +44,12 @@ class PSConfig:
     # the reference's topology (README.md:64-75): rank 0 only receives, sums, steps and publishes,
     # ranks 1..N-1 are the workers (rank 0 calls opt.serve() instead of training)
     ps_dedicated: bool = False
+    # async PS update/publication granularity: 'model' (one version for the whole model: the PS
+    # steps once M complete worker steps arrived) | 'bucket' (README.md:64-76, the reference PS
+    # steps and broadcasts each parameter on its own: every bucket is updated and published as soon
+    # as M messages for it arrived, workers adopt the newest version of each bucket -- reads may
+    # mix versions across buckets; ipc transport only)
+    ps_granularity: str = "model"
     # async PS: scale a kept gradient by 1/max(1, staleness) (staleness-aware async SGD)
     staleness_lr: bool = False
     # async PS look-ahead publish (delay-compensated momentum): workers read the parameters
@@ -153,6 +159,8 @@ class PSConfig:
             raise ValueError("async_transport must be 'ipc' or 'p2p'")
         if self.transport not in ("torch", "rccl"):
             raise ValueError("transport must be 'torch' or 'rccl'")
+        if self.ps_granularity not in ("model", "bucket"):
+            raise ValueError("ps_granularity must be 'model' or 'bucket'")
         if self.adam_variant not in ("reference", "torch"):
             raise ValueError("adam_variant must be 'reference' or 'torch'")
 

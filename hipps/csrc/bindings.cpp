@@ -95,6 +95,12 @@ void pull_select(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t readi
 void pull_copy(at::Tensor sel, at::Tensor pub, int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t lo,
                int64_t hi);
 void pull_done(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, int64_t ring_slot);
+void pull_select_b(at::Tensor selb, int64_t bpub, int64_t bbuf, int64_t reading_b, int64_t applied, int64_t npub,
+                   int64_t tries);
+void pull_copy_b(at::Tensor selb, at::Tensor boff, at::Tensor pub, int64_t stride, int64_t npub, bool bf16,
+                 at::Tensor dst, int64_t lo, int64_t hi);
+void pull_done_b(at::Tensor selb, int64_t bpub, int64_t bbuf, int64_t reading_b, int64_t applied, at::Tensor sel,
+                 int64_t ring_slot);
 void bind_control(pybind11::module& m);
 void bind_rccl(pybind11::module& m);
 void bind_ipc(pybind11::module& m);
@@ -182,6 +188,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pull_select", &hipps::rt::pull_select, "GPU-time pull, stage 1: choose the version, announce the reader");
   m.def("pull_copy", &hipps::rt::pull_copy, "GPU-time pull, stage 2: copy params[lo, hi) of the chosen version");
   m.def("pull_done", &hipps::rt::pull_done, "GPU-time pull, stage 3: release the reader word, record the version");
+  m.def("pull_select_b", &hipps::rt::pull_select_b, "bucket-granular pull, stage 1: newest version per bucket");
+  m.def("pull_copy_b", &hipps::rt::pull_copy_b, "bucket-granular pull, stage 2: copy each bucket's selected slot");
+  m.def("pull_done_b", &hipps::rt::pull_done_b, "bucket-granular pull, stage 3: release, record min version");
   hipps::rt::bind_control(m);
   hipps::rt::bind_rccl(m);
   hipps::rt::bind_ipc(m);

@@ -46,6 +46,7 @@ constexpr int64_t kMagic = 0x5350504948ll;  // "HIPPS"
 constexpr int kMaxRanks = 64;
 constexpr int kSlots = 64;  // max mailbox slots per worker (bucket messages in flight)
 constexpr int kPub = 4;    // published parameter buffers (>= 2 + concurrent readers of old versions)
+constexpr int kMaxBuckets = 256;  // bucket-granular publication (ps_granularity='bucket')
 
 struct alignas(64) RankRec {
   std::atomic<int64_t> push_seq;           // last message fully landed in the PS mailbox
@@ -61,6 +62,7 @@ struct alignas(64) RankRec {
   std::atomic<int64_t> sent_ver;           // p2p transport: version the PS sent for the last request
   std::atomic<int64_t> last_stale;         // staleness (updates) of this worker's newest consumed step
   std::atomic<int64_t> last_stale_seq;     // ... and that step's last message seq
+  std::atomic<int64_t> reading_b[kMaxBuckets];  // bucket mode: version of bucket b being copied (-1)
 };
 
 struct alignas(64) Header {
@@ -72,13 +74,15 @@ struct alignas(64) Header {
   std::atomic<int64_t> drops;
   std::atomic<int64_t> updates;
   std::atomic<int64_t> buf_ver[kPub + 1];
+  std::atomic<int64_t> bpub_ver[kMaxBuckets];        // bucket mode: newest published version of bucket b
+  std::atomic<int64_t> bbuf_ver[kMaxBuckets][kPub];  // bucket mode: version in publish slot k of bucket b
   RankRec rank[kMaxRanks];
 };
 
 enum Field : int {
   PUSH_SEQ = 0, ACK_SEQ = 1, PUSH_VER = 2, APPLIED_VER = 3, STOP = 4, HEARTBEAT = 5, INCL_SEQ = 6,
   PUSH_FLAG = 7, READING = 8, PULL_REQ = 9, PUB_VER = 10, PS_STOP = 11, ERROR = 12, DROPS = 13, UPDATES = 14, BUF_VER = 15, SENT_VER = 16,
-  LAST_STALE = 17, LAST_STALE_SEQ = 18
+  LAST_STALE = 17, LAST_STALE_SEQ = 18, BPUB_VER = 19, BBUF_VER = 20, READING_B = 21
 };
 
 static int64_t now_ns() {
@@ -105,7 +109,14 @@ class ControlBlock {
       std::memset(p, 0, sizeof(Header));
       h_->world = world;
       for (int b = 0; b <= kPub; ++b) h_->buf_ver[b].store(-1);
-      for (int r = 0; r < kMaxRanks; ++r) h_->rank[r].reading.store(-1);
+      for (int r = 0; r < kMaxRanks; ++r) {
+        h_->rank[r].reading.store(-1);
+        for (int b = 0; b < kMaxBuckets; ++b) h_->rank[r].reading_b[b].store(-1);
+      }
+      for (int b = 0; b < kMaxBuckets; ++b) {
+        h_->bpub_ver[b].store(-1);
+        for (int k = 0; k < kPub; ++k) h_->bbuf_ver[b][k].store(-1);
+      }
       h_->pub_ver.store(-1);
       std::atomic_thread_fence(std::memory_order_release);
       h_->magic = kMagic;
@@ -165,6 +176,14 @@ class ControlBlock {
       case BUF_VER:
         if (idx < 0 || idx > kPub) throw std::out_of_range("buf_ver index");
         return &h_->buf_ver[idx];
+      case BPUB_VER:
+        if (idx < 0 || idx >= kMaxBuckets) throw std::out_of_range("bucket index");
+        return &h_->bpub_ver[idx];
+      case BBUF_VER:  // idx = bucket * kPub + slot
+        if (idx < 0 || idx >= kMaxBuckets * kPub) throw std::out_of_range("bucket slot index");
+        return &h_->bbuf_ver[idx / kPub][idx % kPub];
+      case READING_B:  // idx = rank * kMaxBuckets + bucket
+        return &rec(idx / kMaxBuckets).reading_b[idx % kMaxBuckets];
     }
     throw std::out_of_range("unknown control field");
   }
@@ -182,6 +201,28 @@ class ControlBlock {
       bool busy = false;
       for (int r = 0; r < (int)h_->world; ++r)
         if (h_->rank[r].reading.load(std::memory_order_seq_cst) == v) busy = true;
+      if (!busy) return true;
+      if (h_->error.load(std::memory_order_relaxed) || now_ns() >= deadline) return false;
+      if (++spins < 2000) {
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+      } else {
+        struct timespec ts{0, 20000};
+        nanosleep(&ts, nullptr);
+      }
+    }
+  }
+  // Bucket mode: block until no rank is reading bucket b at version v.
+  bool wait_no_reader_b(int b, int64_t v, int64_t timeout_us) {
+    if (b < 0 || b >= kMaxBuckets) throw std::out_of_range("bucket index");
+    py::gil_scoped_release nogil;
+    const int64_t deadline = now_ns() + timeout_us * 1000;
+    int spins = 0;
+    for (;;) {
+      bool busy = false;
+      for (int r = 0; r < (int)h_->world; ++r)
+        if (h_->rank[r].reading_b[b].load(std::memory_order_seq_cst) == v) busy = true;
       if (!busy) return true;
       if (h_->error.load(std::memory_order_relaxed) || now_ns() >= deadline) return false;
       if (++spins < 2000) {
@@ -331,10 +372,12 @@ void bind_control(py::module& m) {
       .def("enable_device_doorbells", &ControlBlock::enable_device_doorbells)
       .def_property_readonly("bell_mode", &ControlBlock::bell_mode)
       .def("wait_no_reader", &ControlBlock::wait_no_reader)
+      .def("wait_no_reader_b", &ControlBlock::wait_no_reader_b)
       .def("heartbeat", &ControlBlock::heartbeat)
       .def_property_readonly("world", &ControlBlock::world)
       .def_property_readonly_static("SLOTS", [](py::object) { return kSlots; })
-      .def_property_readonly_static("NPUB", [](py::object) { return kPub; });
+      .def_property_readonly_static("NPUB", [](py::object) { return kPub; })
+      .def_property_readonly_static("MAX_BUCKETS", [](py::object) { return kMaxBuckets; });
   m.attr("F_PUSH_SEQ") = (int)PUSH_SEQ;
   m.attr("F_ACK_SEQ") = (int)ACK_SEQ;
   m.attr("F_PUSH_VER") = (int)PUSH_VER;
@@ -354,6 +397,9 @@ void bind_control(py::module& m) {
   m.attr("F_BUF_VER") = (int)BUF_VER;
   m.attr("F_LAST_STALE") = (int)LAST_STALE;
   m.attr("F_LAST_STALE_SEQ") = (int)LAST_STALE_SEQ;
+  m.attr("F_BPUB_VER") = (int)BPUB_VER;
+  m.attr("F_BBUF_VER") = (int)BBUF_VER;
+  m.attr("F_READING_B") = (int)READING_B;
 }
 
 }  // namespace rt

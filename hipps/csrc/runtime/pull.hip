@@ -100,6 +100,88 @@ __global__ __launch_bounds__(64) void k_pull_done(PullWords w, int64_t* __restri
   sel[2 + ring_slot] = sel[1];
 }
 
+// ---- bucket granularity (ps_granularity='bucket'): every bucket has its own version ---------
+// The same Dekker handshake per bucket (reading_b[b] vs bbuf_ver[b][slot]), one lane per bucket,
+// so a worker adopts the newest published version of EACH bucket -- versions may differ across
+// buckets (the inconsistent read of README.md:79-81).  selb: int64 [2 * nb] (selected, adopted).
+struct PullWordsB {
+  int64_t* bpub_ver;   // [kMaxBuckets]
+  int64_t* bbuf_ver;   // [kMaxBuckets][npub]
+  int64_t* reading_b;  // this rank's [kMaxBuckets]
+  int64_t* applied;
+};
+
+__global__ __launch_bounds__(64) void k_pull_select_b(PullWordsB w, int64_t* __restrict__ selb, int nb, int npub,
+                                                      int tries) {
+  for (int b = threadIdx.x; b < nb; b += 64) {
+    const int64_t cur = selb[nb + b];
+    int64_t out = -1;
+    for (int t = 0; t < tries; ++t) {
+      const int64_t v = ld_sys(w.bpub_ver + b);
+      if (v <= cur) break;
+      st_sys(w.reading_b + b, v);
+      if (ld_sys(w.bbuf_ver + (int64_t)b * npub + (v % npub)) == v) {
+        out = v;
+        break;
+      }
+      st_sys(w.reading_b + b, -1);
+    }
+    selb[b] = out;
+  }
+}
+
+// params[lo, hi) <- per bucket (blockIdx.y), the publish slot of that bucket's selected version
+template <typename Tin>
+__global__ __launch_bounds__(kBlock) void k_pull_copy_b(const int64_t* __restrict__ selb,
+                                                        const int64_t* __restrict__ boff, const uint8_t* __restrict__ pub,
+                                                        int64_t stride, int npub, float* __restrict__ dst, int64_t lo,
+                                                        int64_t hi, int fence_mode) {
+  constexpr int U = 4;
+  const int b = blockIdx.y;
+  const int64_t v = selb[b];
+  if (v < 0) return;
+  const int64_t a = max(boff[b], lo), e = min(boff[b + 1], hi);
+  if (a >= e) return;
+  if (fence_mode == 0 || threadIdx.x < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  if (fence_mode == 1) __syncthreads();
+  const Tin* src = reinterpret_cast<const Tin*>(pub + (v % npub) * stride);
+  const int64_t a4 = (a + 3) >> 2, e4 = e >> 2, step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = a4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < e4; i0 += U * step) {
+    float4 t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + u * step < e4) t[u] = Vec4<Tin>::load(src, (i0 + u * step) << 2);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + u * step < e4) Vec4<float>::store(dst, (i0 + u * step) << 2, t[u]);
+  }
+  if (blockIdx.x == 0) {  // unaligned head / tail of the range
+    for (int64_t i = a + threadIdx.x; i < min(e, a4 << 2); i += blockDim.x) dst[i] = Vec4<Tin>::load1(src, i);
+    for (int64_t i = max(a, e4 << 2) + threadIdx.x; i < e; i += blockDim.x) dst[i] = Vec4<Tin>::load1(src, i);
+  }
+}
+
+__global__ __launch_bounds__(64) void k_pull_done_b(PullWordsB w, int64_t* __restrict__ selb, int nb,
+                                                    int64_t* __restrict__ sel, int ring_slot) {
+  int64_t mn = INT64_MAX;
+  for (int b = threadIdx.x; b < nb; b += 64) {
+    const int64_t v = selb[b];
+    if (v >= 0) {
+      st_sys(w.reading_b + b, -1);
+      selb[nb + b] = v;
+    }
+    mn = min(mn, selb[nb + b]);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) mn = min(mn, (int64_t)__shfl_xor((long long)mn, o, 64));
+  if (threadIdx.x == 0) {
+    // the global (min over buckets) version: what the next step's gradient is computed on
+    sel[1] = mn;
+    st_sys(w.applied, mn);
+    sel[2 + ring_slot] = mn;
+  }
+}
+
 static PullWords words_of(int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied) {
   TORCH_CHECK(pub_ver && buf_ver && reading && applied, "pull needs device-registered control words");
   return PullWords{reinterpret_cast<int64_t*>(pub_ver), reinterpret_cast<int64_t*>(buf_ver),
@@ -162,6 +244,55 @@ void pull_params(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t readi
   pull_select(sel, pub_ver, buf_ver, reading, applied, npub, tries);
   pull_copy(sel, pub, stride, npub, bf16, dst, 0, dst.numel());
   pull_done(sel, pub_ver, buf_ver, reading, applied, ring_slot);
+}
+
+static PullWordsB words_b(int64_t bpub, int64_t bbuf, int64_t reading_b, int64_t applied) {
+  TORCH_CHECK(bpub && bbuf && reading_b && applied, "bucket pull needs device-registered control words");
+  return PullWordsB{reinterpret_cast<int64_t*>(bpub), reinterpret_cast<int64_t*>(bbuf),
+                    reinterpret_cast<int64_t*>(reading_b), reinterpret_cast<int64_t*>(applied)};
+}
+
+void pull_select_b(at::Tensor selb, int64_t bpub, int64_t bbuf, int64_t reading_b, int64_t applied, int64_t npub,
+                   int64_t tries) {
+  TORCH_CHECK(selb.is_cuda() && selb.scalar_type() == at::kLong && selb.is_contiguous() && selb.numel() % 2 == 0,
+              "selb must be int64 device [2 * nb]");
+  hipLaunchKernelGGL(k_pull_select_b, dim3(1), dim3(64), 0, c10::hip::getCurrentHIPStream(),
+                     words_b(bpub, bbuf, reading_b, applied), selb.data_ptr<int64_t>(), (int)(selb.numel() / 2),
+                     (int)npub, (int)tries);
+}
+
+void pull_copy_b(at::Tensor selb, at::Tensor boff, at::Tensor pub, int64_t stride, int64_t npub, bool bf16,
+                 at::Tensor dst, int64_t lo, int64_t hi) {
+  TORCH_CHECK(selb.is_cuda() && selb.scalar_type() == at::kLong && selb.is_contiguous(), "selb must be int64 device");
+  const int64_t nb = selb.numel() / 2;
+  TORCH_CHECK(boff.is_cuda() && boff.scalar_type() == at::kLong && boff.numel() == nb + 1, "boff: int64 [nb + 1]");
+  TORCH_CHECK(pub.is_cuda() && pub.scalar_type() == at::kByte, "pub must be a uint8 device view");
+  TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kFloat && dst.is_contiguous(), "dst must be f32 device");
+  const int64_t esz = bf16 ? 2 : 4;
+  TORCH_CHECK(0 <= lo && lo <= hi && hi <= dst.numel(), "range [lo, hi) of dst");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(pub.data_ptr()) % 16 == 0 && stride % 16 == 0, "pub must be 16B aligned");
+  TORCH_CHECK(npub >= 1 && pub.numel() >= (npub - 1) * stride + dst.numel() * esz, "publish view too small");
+  if (hi == lo || nb == 0) return;
+  const int gx = std::max(1, std::min(grid_for(((hi - lo) >> 2) / 16 + 1), (int)(4096 / nb) + 1));
+  auto stream = c10::hip::getCurrentHIPStream();
+  if (bf16)
+    hipLaunchKernelGGL(k_pull_copy_b<uint16_t>, dim3(gx, nb), kBlock, 0, stream, selb.data_ptr<int64_t>(),
+                       boff.data_ptr<int64_t>(), pub.data_ptr<uint8_t>(), stride, (int)npub, dst.data_ptr<float>(), lo,
+                       hi, 1);
+  else
+    hipLaunchKernelGGL(k_pull_copy_b<float>, dim3(gx, nb), kBlock, 0, stream, selb.data_ptr<int64_t>(),
+                       boff.data_ptr<int64_t>(), pub.data_ptr<uint8_t>(), stride, (int)npub, dst.data_ptr<float>(), lo,
+                       hi, 1);
+}
+
+void pull_done_b(at::Tensor selb, int64_t bpub, int64_t bbuf, int64_t reading_b, int64_t applied, at::Tensor sel,
+                 int64_t ring_slot) {
+  TORCH_CHECK(selb.is_cuda() && selb.scalar_type() == at::kLong && selb.is_contiguous(), "selb must be int64 device");
+  TORCH_CHECK(sel.is_cuda() && sel.scalar_type() == at::kLong && sel.is_contiguous(), "sel must be int64 device");
+  TORCH_CHECK(ring_slot >= 0 && ring_slot + 2 < sel.numel(), "ring slot out of range");
+  hipLaunchKernelGGL(k_pull_done_b, dim3(1), dim3(64), 0, c10::hip::getCurrentHIPStream(),
+                     words_b(bpub, bbuf, reading_b, applied), selb.data_ptr<int64_t>(), (int)(selb.numel() / 2),
+                     sel.data_ptr<int64_t>(), (int)ring_slot);
 }
 
 }  // namespace rt

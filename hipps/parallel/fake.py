@@ -21,7 +21,7 @@ from .ps_core import PSCore
 FIELDS = SimpleNamespace(F_PUSH_SEQ=0, F_ACK_SEQ=1, F_PUSH_VER=2, F_APPLIED_VER=3, F_STOP=4, F_HEARTBEAT=5,
                          F_INCL_SEQ=6, F_PUSH_FLAG=7, F_READING=8, F_PULL_REQ=9, F_PUB_VER=10, F_PS_STOP=11,
                          F_ERROR=12, F_DROPS=13, F_UPDATES=14, F_BUF_VER=15, F_SENT_VER=16,
-                         F_LAST_STALE=17, F_LAST_STALE_SEQ=18)
+                         F_LAST_STALE=17, F_LAST_STALE_SEQ=18, F_BPUB_VER=19, F_BBUF_VER=20, F_READING_B=21)
 
 
 class FakeControl:
@@ -50,14 +50,16 @@ class FakeAsyncPS:
     MAXSLOTS = 64
 
     def __init__(self, W: int, nb: int = 1, M: Optional[int] = None, staleness: int = -1,
-                 staleness_lr: bool = False, slots: int = 4, lr: float = 1.0, average: bool = False):
+                 staleness_lr: bool = False, slots: int = 4, lr: float = 1.0, average: bool = False,
+                 bucketwise: bool = False):
         self.W, self.nb, self.SLOTS = W, nb, slots
         self.M = M if M else W
         self.lr = lr
         self.ctl = FakeControl()
         F = FIELDS
+        self.bucketwise = bucketwise
         self.core = PSCore(self.ctl, F, W, nb, list(range(nb))[::-1], slots, self.MAXSLOTS, self.M, staleness,
-                           staleness_lr, 1.0 / self.M if average else 1.0)
+                           staleness_lr, 1.0 / self.M if average else 1.0, bucketwise=bucketwise)
         self.core.backend = self
         self.mail: Dict[tuple, float] = {}  # (worker, slot) -> gradient value of that bucket
         self.acc = [0.0] * nb
@@ -65,10 +67,13 @@ class FakeAsyncPS:
         self.history: List[dict] = []  # one record per PS update
         self.accumulated: List[tuple] = []  # (worker, step, bucket, scale) in PS order
         self._cur: List[tuple] = []
+        self._cur_b: Dict[int, List[tuple]] = {}
         self.seq = [0] * W
         self.local_ver = [0] * W
         self.steps = [0] * W
         self.ctl.store(F.F_PUB_VER, 0, 0)
+        self.local_ver_b = [[0] * nb for _ in range(W)]  # bucketwise: per-bucket adopted versions
+        self.pub_b = [[0.0] for _ in range(nb)]  # bucketwise: published value of bucket b per version
 
     # ---- worker side ------------------------------------------------------------------------
     def push_step(self, i: int, grads: Sequence[float], version: Optional[int] = None, partial: bool = False):
@@ -92,9 +97,22 @@ class FakeAsyncPS:
         self.steps[i] += 1
 
     def pull(self, i: int) -> int:
-        """AsySG-InCon read: adopt the newest published version."""
+        """AsySG-InCon read: adopt the newest published version (bucketwise: the newest version of
+        EACH bucket, which may differ across buckets)."""
         self.local_ver[i] = self.ctl.load(FIELDS.F_PUB_VER, 0)
+        if self.bucketwise:
+            self.local_ver_b[i] = [self.ctl.load(FIELDS.F_BPUB_VER, b) for b in range(self.nb)]
         return self.local_ver[i]
+
+    def read_params(self, i: int) -> List[float]:
+        """The parameters worker i adopted at its last pull (bucketwise: per-bucket versions)."""
+        if not self.bucketwise:
+            return list(self.history[self.local_ver[i] - 1]["params"]) if self.local_ver[i] else [0.0] * self.nb
+        return [self.pub_b[b][v] for b, v in enumerate(self.local_ver_b[i])]
+
+    def deliver_upto(self, i: int, s: int) -> int:
+        """PS consumes worker i's messages up to sequence number s (partial arrival)."""
+        return self.core.pump(i, upto=s)
 
     def stop(self, i: int):
         self.ctl.store(FIELDS.F_STOP, i, self.seq[i] + 1)
@@ -114,10 +132,32 @@ class FakeAsyncPS:
         self.acc[bi] += scale * self.mail[(i, slot)]
         step = (seq - 1) // self.nb + 1
         self.accumulated.append((i, step, bi, scale))
-        self._cur.append((i, step))
+        if self.bucketwise:
+            self._cur_b.setdefault(bi, []).append((i, step))
+        else:
+            self._cur.append((i, step))
 
     def note_presence(self, i, slot, vidx):
         pass
+
+    def note_presence_b(self, i, slot, vidx, bi):
+        pass
+
+    def update_bucket(self, bi, v, gver, incl, gscale):
+        F = FIELDS
+        self.params[bi] -= self.lr * gscale * self.acc[bi]
+        self.acc[bi] = 0.0
+        self.pub_b[bi].append(self.params[bi])
+        assert len(self.pub_b[bi]) == v + 1
+        self.ctl.store(F.F_BPUB_VER, bi, v)
+        if gver is not None:
+            self.ctl.store(F.F_PUB_VER, 0, gver)
+            self.ctl.fetch_add(F.F_UPDATES, 0, 1)
+        for i, s in incl.items():
+            self.ctl.store(F.F_INCL_SEQ, i, s)
+        contrib = sorted(set(self._cur_b.pop(bi, [])))
+        self.history.append({"bucket": bi, "version": v, "global": gver, "params": list(self.params),
+                             "contributors": contrib, "included": dict(incl)})
 
     def flush(self):
         pass

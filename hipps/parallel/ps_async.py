@@ -134,6 +134,7 @@ class PSAsyncEngine(Engine):
         self.dedicated = bool(cfg.ps_dedicated) and W > 1
         self.M = cfg.accumulate if cfg.accumulate > 0 else (W - 1 if self.dedicated else W)
         self.emu = int(cfg.emulate_remote) if W == 1 else 0  # emulated remote-worker PS load
+        self.bucketwise = cfg.ps_granularity == "bucket"
         self.MAXSLOTS = C.ControlBlock.SLOTS  # stride of the per-slot version words
         self.NPUB = C.ControlBlock.NPUB
         self.timeout_us = int(min(TIMEOUT_US, cfg.comm_timeout_s * 1e6))
@@ -160,6 +161,9 @@ class PSAsyncEngine(Engine):
         # 'p2p': the mailbox stays private to the PS and data moves by two-sided send/recv
         # (torch.distributed isend/irecv: RCCL pair communicators on GPU, gloo on CPU)
         self.p2p = cfg.async_transport == "p2p" and W > 1
+        if self.bucketwise and (self.p2p or self.nb > C.ControlBlock.MAX_BUCKETS or self.emu):
+            raise ValueError("ps_granularity='bucket' needs the ipc transport, at most "
+                             f"{C.ControlBlock.MAX_BUCKETS} buckets and no emulate_remote")
         # p2p: gradients and parameters travel on two process groups of their own.  Each group has
         # its own RCCL communicators and streams, so (a) a posted gradient receive can never sit
         # in front of a parameter send on the same pair channel (ops of one channel complete in
@@ -228,6 +232,15 @@ class PSAsyncEngine(Engine):
             self.pull_mode = "direct"
         if self.p2p and self.rank != 0:
             self.pull_mode = "p2p"
+        if self.bucketwise and self.pull_mode == "prefetch":
+            self.pull_mode = "direct"
+        # bucket granularity: per-bucket adopted versions (host) and bucket bounds / GPU selection
+        self._lver_b = [-1] * self.nb
+        self._boff = self._selb = None
+        if self.bucketwise and self.cuda:
+            self._boff = torch.tensor([b.lo for b in self.plan.buckets] + [store.numel], dtype=torch.int64,
+                                      device=store.device)
+            self._selb = torch.full((2 * self.nb,), -1, dtype=torch.int64, device=store.device)
         self._p2p_req = None  # worker: (request seq, stage index, [works]) of the posted param recv
         self._p2p_reqs = 0
         self._pub_sends: dict = {}  # PS: publish buffer -> in-flight parameter sends reading it
@@ -260,7 +273,10 @@ class PSAsyncEngine(Engine):
             self.ps_stream = torch.cuda.Stream(device=store.device, priority=-1) if self.cuda else None
             gs = self.gscale(self.M) / (1 + self.emu)  # emulated copies leave the average unchanged
             self.core = PSCore(self.ctl, C, W, self.nb, self.order, self.SLOTS, self.MAXSLOTS, self.M,
-                               cfg.staleness, cfg.staleness_lr, gs, self._stats)
+                               cfg.staleness, cfg.staleness_lr, gs, self._stats, bucketwise=self.bucketwise)
+            self._pres_full_b = [False] * self.nb
+            self._pres_part_b = [None] * self.nb
+            self._gsteps = 0
             if self.emu:
                 self._emu_stream = torch.cuda.Stream(device=store.device, priority=0) if self.cuda else None
                 self._emu_in = torch.empty(self.plan.wire_nbytes, dtype=torch.uint8, device=store.device)
@@ -404,6 +420,10 @@ class PSAsyncEngine(Engine):
             torch.cuda.current_stream(self.store.device).synchronize()
         self.ctl.store(C.F_BUF_VER, 0, 0)
         self.ctl.store(C.F_PUB_VER, 0, 0)
+        if self.bucketwise:
+            for bi in range(self.nb):
+                self.ctl.store(C.F_BBUF_VER, bi * self.NPUB, 0)
+                self.ctl.store(C.F_BPUB_VER, bi, 0)
 
     def _serve_guard(self):
         try:
@@ -555,6 +575,55 @@ class PSAsyncEngine(Engine):
 
     def update(self, included, gscale):
         self._update(included, gscale)
+
+    def note_presence_b(self, i: int, slot: int, vidx: int, bi: int):
+        """Bucket granularity: OR a kept message's step presence into bucket bi's mask."""
+        if not self.cfg.skip_missing_grads or self._pres_full_b[bi]:
+            return
+        if not self.ctl.load(self.C.F_PUSH_FLAG, vidx):
+            self._pres_full_b[bi] = True
+            self._pres_part_b[bi] = None
+            return
+        ns = len(self.store.slots)
+        p = self.slot_buf(i, slot)[self.slot_pres:self.slot_pres + ns]
+        cur = self._pres_part_b[bi]
+        self._pres_part_b[bi] = p.clone() if cur is None else torch.maximum(cur, p)
+
+    def update_bucket(self, bi: int, v: int, gver, incl, gscale):
+        """Bucket granularity: optimizer step of bucket bi's range of the fp32 master from its
+        accumulator, published into that bucket's slot v % NPUB; then (stream-ordered) the slot
+        stamp, the bucket version, the global version if it advanced, the included words."""
+        C, b = self.C, self.plan.buckets[bi]
+        k = v % self.NPUB
+        idx = bi * self.NPUB + k
+        old = self.ctl.load(C.F_BBUF_VER, idx)
+        self.ctl.store(C.F_BBUF_VER, idx, -1)  # readers skip a slot being rewritten ...
+        if old >= 0 and not self.ctl.wait_no_reader_b(bi, old, 0):  # ... and it waits for current readers
+            self._stats["reader_waits"] += 1
+            if not self.ctl.wait_no_reader_b(bi, old, int(self.cfg.dead_after_s * 1e6)):
+                self._stats["reader_timeouts"] = self._stats.get("reader_timeouts", 0) + 1
+        mask = None
+        if self.cfg.skip_missing_grads and not self._pres_full_b[bi] and self._pres_part_b[bi] is not None:
+            mask = self.store.chunk_mask(self._pres_part_b[bi])
+        self._pres_full_b[bi], self._pres_part_b[bi] = False, None
+        top = max(self.core.ver_b)
+        if top > self._gsteps:  # group step hint (per-chunk step counts decide the optimizer math)
+            self.opt._begin_update()
+            self._gsteps = top
+        tau = self.lookahead_tau()
+        self._stats["lookahead_tau_x1000"] = int(round(tau * 1000))
+        with self.tracer.phase("ps_update", self.ps_stream):
+            self.opt._update_range([self.acc], self.master, b.lo, b.hi, gscale, True, self.pub_buf(k), mask, 0,
+                                   lookahead=tau)
+        words = [(C.F_BBUF_VER, idx, v), (C.F_BPUB_VER, bi, v)]
+        if gver is not None:
+            words.append((C.F_PUB_VER, 0, gver))
+        words += [(C.F_INCL_SEQ, i, s) for i, s in incl.items()]
+        for j in range(0, len(words), 6):
+            self._ring(self.ps_stream, words[j:j + 6])
+        if gver is not None:
+            self.ctl.fetch_add(C.F_UPDATES, 0, 1)
+        self._stats["bucket_updates"] = self._stats.get("bucket_updates", 0) + 1
 
     @property
     def ver(self) -> int:
@@ -715,7 +784,7 @@ class PSAsyncEngine(Engine):
             b = self.plan.buckets[bi]
             src = self.plan.message(self.wire, bi)  # layout (+ canary guard in debug_canary)
             vidx = self.rank * self.MAXSLOTS + slot
-            last = pos == self.nb - 1
+            last = pos == self.nb - 1 or self.bucketwise  # bucket mode: every message carries presence
             if self.p2p and self.rank != 0:
                 self._push_p2p(src, s, vidx, last and partial)
                 continue
@@ -858,11 +927,94 @@ class PSAsyncEngine(Engine):
             need = max(block_for if block_for is not None else -1,
                        self.ctl.load(C.F_PUB_VER, 0) if sync else -1)
             return self._p2p_pull(sync=sync, need=need)
+        if self.bucketwise:
+            if sync or self.pull_mode == "direct":
+                return self._direct_pull_b()
+            return self._device_pull_b()
         if sync or self.pull_mode == "direct":
             return self._direct_pull()
         if self.pull_mode == "device":
             return self._device_pull()
         return self._prefetch_pull()
+
+    # ---- bucket granularity pulls ----------------------------------------------------------------
+    def _bucket_words(self):
+        C, ctl = self.C, self.ctl
+        return (ctl.device_addr(C.F_BPUB_VER, 0), ctl.device_addr(C.F_BBUF_VER, 0),
+                ctl.device_addr(C.F_READING_B, self.rank * C.ControlBlock.MAX_BUCKETS),
+                ctl.device_addr(C.F_APPLIED_VER, self.rank))
+
+    def _device_pull_b(self) -> bool:
+        """GPU-time pull, bucket by bucket: each bucket's newest published version is chosen and
+        copied when the GPU reaches the pull (pull.hip k_pull_*_b)."""
+        C = self.C
+        esz = torch.empty((), dtype=self.pub_dtype).element_size()
+        base = self.mem[self.pub_off:self.pub_off + (self.NPUB - 1) * self.pub_bytes + self.store.numel * esz]
+        words = self._bucket_words()
+        bf16 = self.pub_dtype == torch.bfloat16
+        ring = (self.step_no + 1) % RING
+        n = self.store.numel
+        C.pull_select_b(self._selb, *words, self.NPUB, 64)
+        if self._split is None:
+            C.pull_copy_b(self._selb, self._boff, base, self.pub_bytes, self.NPUB, bf16, self.store.data, 0, n)
+            C.pull_done_b(self._selb, *words, self._sel, ring)
+            return True
+        dev, s = self.store.device, self._split
+        cs = torch.cuda.current_stream(dev)
+        ev_sel = torch.cuda.Event()
+        ev_sel.record(cs)
+        C.pull_copy_b(self._selb, self._boff, base, self.pub_bytes, self.NPUB, bf16, self.store.data, 0, s)
+        self.store.refresh_shadow(0, s)
+        ev_early = torch.cuda.Event()
+        ev_early.record(cs)
+        side = self._late_stream
+        with torch.cuda.stream(side):
+            side.wait_event(ev_sel)
+            C.pull_copy_b(self._selb, self._boff, base, self.pub_bytes, self.NPUB, bf16, self.store.data, s, n)
+            self.store.refresh_shadow(s, n)
+            side.wait_event(ev_early)
+            C.pull_done_b(self._selb, *words, self._sel, ring)
+        late = torch.cuda.Event()
+        late.record(side)
+        self._late_ev = late
+        self._shadow_done = True
+        return True
+
+    def _direct_pull_b(self) -> bool:
+        """Host-chosen pull, bucket by bucket (reader handshake per bucket)."""
+        C, MB = self.C, self.C.ControlBlock.MAX_BUCKETS
+        got = False
+        stream = torch.cuda.current_stream(self.store.device) if self.cuda else None
+        if self.cuda and self._selb is not None:  # a device pull's adoptions are the host's starting point
+            self._lver_b = [max(a, int(v)) for a, v in zip(self._lver_b, self._selb[self.nb:].tolist())]
+        for bi, b in enumerate(self.plan.buckets):
+            for _ in range(16):
+                v = self.ctl.load(C.F_BPUB_VER, bi)
+                if v <= self._lver_b[bi]:
+                    break
+                k = v % self.NPUB
+                ridx = self.rank * MB + bi
+                self.ctl.store(C.F_READING_B, ridx, v)
+                if self.ctl.load(C.F_BBUF_VER, bi * self.NPUB + k) == v:
+                    src = self.pub_buf(k)[b.lo:b.hi]
+                    dst = self.store.data[b.lo:b.hi]
+                    if src.dtype == dst.dtype:
+                        dst.copy_(src, non_blocking=self.cuda)
+                    else:
+                        ops.convert(src if self.cuda else src.clone(), dst)
+                    self._ring(stream, [(C.F_READING_B, ridx, -1)])
+                    self._lver_b[bi] = v
+                    got = True
+                    break
+                self.ctl.store(C.F_READING_B, ridx, -1)
+        v = min(self._lver_b)
+        self.local_ver = v
+        if self.cuda:
+            self._sel[1:].fill_(v)
+            if self._selb is not None:
+                self._selb[self.nb:].copy_(torch.tensor(self._lver_b, dtype=torch.int64))
+        self.ctl.store(C.F_APPLIED_VER, self.rank, v)
+        return got
 
     def _device_pull(self) -> bool:
         C = self.C
@@ -1118,6 +1270,9 @@ class PSAsyncEngine(Engine):
             d.update({"master": self.master.detach().cpu(), "version": self.ver, "acc": self.acc.detach().cpu(),
                       "acc_count": self.core.count, "ps_accumulated": self._stats["accumulated"],
                       "ps_seen": list(self.core.seen)})
+            if self.bucketwise:  # per-bucket pending counts and versions
+                d["acc_count_b"] = list(self.core.count_b)
+                d["ver_b"] = list(self.core.ver_b)
         return d
 
     def load_engine_state(self, d: dict):
@@ -1142,9 +1297,21 @@ class PSAsyncEngine(Engine):
                     torch.cuda.current_stream(self.store.device).synchronize()
                 self.ctl.store(C.F_BUF_VER, b, self.ver)
                 self.ctl.store(C.F_PUB_VER, 0, self.ver)
+                if self.bucketwise:
+                    # every bucket restarts at the global version (a mid-round bucket that was ahead
+                    # republishes its own newer master range under that version number)
+                    self.core.ver_b = [self.ver] * self.nb
+                    self.core.count_b = list(d.get("acc_count_b", [0] * self.nb))
+                    self._gsteps = self.ver
+                    for bi in range(self.nb):
+                        self.ctl.store(C.F_BBUF_VER, bi * self.NPUB + b, self.ver)
+                        self.ctl.store(C.F_BPUB_VER, bi, self.ver)
         barrier(self.world)
         ver = self.ctl.load(self.C.F_PUB_VER, 0)
         self.local_ver = -1
+        self._lver_b = [-1] * self.nb
+        if self._selb is not None:
+            self._selb.fill_(-1)
         self.irequest_params(block_for=ver)
         if self.cuda:
             torch.cuda.current_stream(self.store.device).synchronize()

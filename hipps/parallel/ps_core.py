@@ -13,6 +13,18 @@ control block) and calls a backend for the data plane:
     backend.update(included, gscale)              optimizer step + publish version ``core.ver``
     backend.flush()                               (optional) issue deferred accumulates / acks
 
+Bucket granularity (``bucketwise=True``, README.md:64-76: the reference's PS steps and
+broadcasts each parameter on its own): every bucket keeps its own accumulation count and version.
+Bucket b is updated and published as soon as M messages for b have arrived (the PS update is
+pipelined with message arrival), so a worker's next read may mix versions across buckets --
+the inconsistent read of README.md:79-81.  The global version ``ver`` is min over buckets.
+
+    backend.note_presence_b(i, slot, vidx, bi)   a kept message (missing-grad mask of bucket bi)
+    backend.update_bucket(bi, v, gver, incl, gscale)
+                                                 update + publish bucket bi at version v; gver is
+                                                 the new global version if it advanced (else
+                                                 None); incl = {worker: newest fully included seq}
+
 PSAsyncEngine drives it with the shared-memory control block and HIP streams; the in-process
 fake transport (hipps.parallel.fake) drives it with scripted arrival orders, so protocol edge
 cases are tested deterministically instead of through multi-process timing.
@@ -25,7 +37,7 @@ from typing import Dict, List, Optional, Sequence
 class PSCore:
     def __init__(self, ctl, F, W: int, nb: int, order: Sequence[int], slots: int, maxslots: int, M: int,
                  staleness: int = -1, staleness_lr: bool = False, gscale: float = 1.0,
-                 stats: Optional[Dict[str, int]] = None):
+                 stats: Optional[Dict[str, int]] = None, bucketwise: bool = False):
         self.ctl, self.F = ctl, F
         self.W, self.nb, self.order = W, nb, list(order)
         self.SLOTS, self.MAXSLOTS, self.M = slots, maxslots, M
@@ -42,6 +54,12 @@ class PSCore:
         self.backend = None
         self.recent: List[int] = []  # staleness of the newest accumulated steps (look-ahead tau)
         self.RECENT = max(8, 2 * W)
+        self.bucketwise = bucketwise
+        if bucketwise:
+            self.count_b = [0] * nb
+            self.ver_b = [0] * nb
+            self.pending_b: List[List[tuple]] = [[] for _ in range(nb)]  # (worker, step) since b's update
+            self.incl_b = [[0] * nb for _ in range(W)]  # [worker][bucket] newest step reflected in b
 
     def pump(self, i: int, upto: Optional[int] = None) -> int:
         """Process every message worker ``i`` has pushed since the last call (or up to message
@@ -74,6 +92,9 @@ class PSCore:
             # per-step staleness record the worker reads back into its step() data
             self.ctl.store(F.F_LAST_STALE, i, stale)
             self.ctl.store(F.F_LAST_STALE_SEQ, i, s + nb - 1)
+        if self.bucketwise:
+            self._one_bucket(i, s, slot, pos, bi, vidx)
+            return
         if not self.dropping[i]:
             be.accumulate(i, slot, bi, s, self.scale[i])
             if pos == nb - 1:
@@ -94,6 +115,44 @@ class PSCore:
                     be.update(self.pending, self.gscale)
                     self.pending = []
                     self.count = 0
+
+    def _one_bucket(self, i: int, s: int, slot: int, pos: int, bi: int, vidx: int):
+        F, be, nb = self.F, self.backend, self.nb
+        step = (s - 1) // nb + 1
+        kept = not self.dropping[i]
+        if kept:
+            be.accumulate(i, slot, bi, s, self.scale[i])
+            be.note_presence_b(i, slot, vidx, bi)
+        be.ack(i, s)
+        # a dropped step still counts as included for max_delay once each bucket moves on
+        self.pending_b[bi].append((i, step))
+        if pos == nb - 1:
+            if kept:
+                self.stats["accumulated"] += 1
+            else:
+                self.stats["drops"] += 1
+                self.ctl.fetch_add(F.F_DROPS, 0, 1)
+        if not kept:
+            return
+        self.count_b[bi] += 1
+        if self.count_b[bi] < self.M:
+            return
+        self.ver_b[bi] += 1
+        self.count_b[bi] = 0
+        touched = set()
+        for w, st in self.pending_b[bi]:
+            if st > self.incl_b[w][bi]:
+                self.incl_b[w][bi] = st
+            touched.add(w)
+        self.pending_b[bi] = []
+        incl = {w: min(self.incl_b[w]) * nb for w in touched}
+        gver = min(self.ver_b)
+        adv = gver > self.ver
+        if adv:
+            self.ver = gver
+        if hasattr(be, "flush"):
+            be.flush()
+        be.update_bucket(bi, self.ver_b[bi], gver if adv else None, incl, self.gscale)
 
     def mean_staleness(self) -> float:
         """Mean staleness (in updates) of the newest accumulated steps."""

@@ -139,3 +139,66 @@ def test_random_interleavings_apply_every_gradient_exactly_once(seed):
     rounds = pushed // 2
     assert f.stats["updates"] == rounds
     assert f.params == [-1.0 * 2 * rounds, -2.0 * 2 * rounds]
+
+
+# ---- bucket granularity (per-bucket PS updates and publication) ----------------------------------
+
+def test_bucketwise_updates_publish_each_bucket_when_complete():
+    """README.md:64-76: the PS steps and broadcasts each bucket as soon as M messages for it have
+    arrived, so a worker reading in between adopts bucket versions that differ."""
+    from hipps.parallel.fake import FakeAsyncPS
+
+    f = FakeAsyncPS(W=2, nb=3, M=2, bucketwise=True)
+    order = f.core.order  # messages of a step go in this bucket order
+    f.push_step(0, grads=[1.0, 2.0, 4.0])
+    f.push_step(1, grads=[1.0, 2.0, 4.0])
+    # worker 0's whole step arrives, worker 1's first message only: one bucket has M = 2
+    f.deliver(0)
+    f.deliver_upto(1, 1)
+    first = order[0]
+    assert [h["bucket"] for h in f.history] == [first]
+    assert f.core.ver_b[first] == 1 and f.core.ver == 0  # global version = min over buckets
+    assert f.stats["updates"] == 0
+    f.pull(0)
+    assert f.local_ver_b[0][first] == 1 and sum(f.local_ver_b[0]) == 1  # a mixed-version read
+    p = f.read_params(0)
+    g = [1.0, 2.0, 4.0]
+    assert p[first] == -2.0 * g[first] and all(p[b] == 0.0 for b in range(3) if b != first)
+    f.deliver(1)
+    assert f.core.ver_b == [1, 1, 1] and f.core.ver == 1 and f.stats["updates"] == 1
+    assert [h["global"] for h in f.history] == [None, None, 1]
+    f.pull(0)
+    assert f.read_params(0) == [-2.0, -4.0, -8.0]
+
+
+def test_bucketwise_max_delay_accounting_needs_every_bucket():
+    """INCL_SEQ (what max_delay waits on) covers a step only once EVERY bucket holding one of its
+    messages has been published."""
+    from hipps.parallel.fake import FIELDS, FakeAsyncPS
+
+    f = FakeAsyncPS(W=2, nb=2, M=2, bucketwise=True)
+    f.push_step(0, grads=[1.0, 1.0])
+    f.push_step(1, grads=[1.0, 1.0])
+    f.deliver(0)
+    f.deliver_upto(1, 1)  # bucket order[0] complete for step 1, order[1] not yet
+    assert f.ctl.load(FIELDS.F_INCL_SEQ, 0) == 0 and f.ctl.load(FIELDS.F_INCL_SEQ, 1) == 0
+    f.deliver(1)
+    assert f.ctl.load(FIELDS.F_INCL_SEQ, 0) == 2 and f.ctl.load(FIELDS.F_INCL_SEQ, 1) == 2
+    # a fast worker runs ahead: its second step is included bucket by bucket
+    f.push_step(0, grads=[1.0, 1.0])
+    f.push_step(0, grads=[1.0, 1.0])
+    f.deliver(0)  # bucket counts reach M = 2 from worker 0 alone (ConditionalAccumulator)
+    assert f.ctl.load(FIELDS.F_INCL_SEQ, 0) == 6
+    assert f.stats["accumulated"] == 4
+
+
+def test_bucketwise_staleness_drop_counts_whole_steps():
+    from hipps.parallel.fake import FakeAsyncPS
+
+    f = FakeAsyncPS(W=2, nb=2, M=1, staleness=0, bucketwise=True)
+    f.push_step(0, grads=[1.0, 1.0])
+    f.push_step(1, grads=[1.0, 1.0], version=0)
+    f.deliver(0)  # M = 1: both buckets update, global version 1
+    f.deliver(1)  # computed on version 0, now stale by 1 > 0: the whole step is dropped
+    st = f.stats
+    assert st["drops"] == 1 and st["accumulated"] == 1 and st["version"] == 1

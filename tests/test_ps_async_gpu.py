@@ -171,3 +171,52 @@ def test_gpu_async_pull_overlap_bitwise():
     assert a["losses"] == b["losses"]
     assert a["sha"] == b["sha"] and a["shadow"] == b["shadow"]
     assert a["ver"] == b["ver"] >= 7
+
+
+def _gpu_bucketwise(rank, world, steps, max_delay, pull):
+    import hipps
+
+    torch.cuda.set_device(0)
+    m = _mlp().cuda()
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", ps_granularity="bucket",
+                    bucket_mb=0.0005, max_delay=max_delay, accumulate=world, pull=pull)
+    info = dict(opt.engine.transport_info())
+    nb = len(opt.engine.plan.buckets)
+    losses = []
+    for s in range(steps):
+        x, y = _data(rank, s % 4)
+        opt.zero_grad()
+        loss = torch.nn.functional.cross_entropy(m(x.cuda()), y.cuda())
+        loss.backward()
+        losses.append(loss.item())
+        opt.step()
+    torch.cuda.synchronize()
+    eng = opt.engine
+    selb = eng._selb.cpu().tolist()
+    opt.close()
+    return {"stats": eng.ps_stats(), "nb": nb, "losses": losses, "info": info, "selb": selb,
+            "params": [p.detach().cpu() for p in m.parameters()]}
+
+
+def test_gpu_bucket_granularity_md0_equals_model_granularity():
+    """Per-bucket device pulls (pull.hip k_pull_*_b) with max_delay=0 reproduce the whole-model
+    update sequence bit for bit (single rank, so both equal local SGD)."""
+    a = run_world(_gpu_bucketwise, 1, 5, 0, "device")
+    b = run_world(_gpu_async, 1, 5, "fp32", 1, 0)
+    assert a[0]["nb"] >= 3
+    for x, y in zip(a[0]["params"], b[0]["params"]):
+        torch.testing.assert_close(x, y, rtol=0, atol=0)
+
+
+def test_gpu_bucket_granularity_three_ranks_device_pull():
+    steps = 10
+    out = run_world(_gpu_bucketwise, 3, steps, -1, "device", timeout=300)
+    st = out[0]["stats"]
+    nb = out[0]["nb"]
+    assert out[0]["info"]["pull"] == "device"
+    assert st["accumulated"] == 3 * steps and st["version"] == steps
+    assert st["bucket_updates"] == nb * steps
+    for r in range(3):
+        adopted = out[r]["selb"][nb:]
+        assert min(adopted) >= 1 and max(adopted) <= steps  # every bucket adopted a real version
+        assert sum(out[r]["losses"][-3:]) < sum(out[r]["losses"][:3])
