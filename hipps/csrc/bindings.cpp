@@ -60,10 +60,13 @@ void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
                      c10::optional<at::Tensor> bn_scale, c10::optional<at::Tensor> bn_shift,
                      c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift);
 // gemm2.hip
-int64_t gemm2_mtiles(int64_t M, int64_t N, int64_t bm);
+int64_t gemm2_mtiles(int64_t M, int64_t N, int64_t K, int64_t bm);
 void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part,
                 c10::optional<at::Tensor> add, c10::optional<at::Tensor> add_mask, int64_t Hi, int64_t Wi,
-                int64_t stride, int64_t KH, int64_t KW, int64_t pad, int64_t bm, int64_t bn);
+                int64_t stride, int64_t KH, int64_t KW, int64_t pad, int64_t bm, int64_t bn,
+                c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_bits, c10::optional<at::Tensor> bn_mean,
+                c10::optional<at::Tensor> bn_invstd, c10::optional<at::Tensor> bn_scale,
+                c10::optional<at::Tensor> bn_shift);
 // pool.hip
 void maxpool3s2_forward(at::Tensor x, at::Tensor y, at::Tensor code, c10::optional<at::Tensor> scale,
                         c10::optional<at::Tensor> shift);
@@ -142,11 +145,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_forward_partials", &hipps::bn_forward_partials, "BN fwd finalize+apply from producer-reduced partials");
   m.def("bn_backward_partials", &hipps::bn_backward_partials, "BN bwd finalize+apply from consumer-reduced partials");
   m.def("conv1x1_mtiles", &hipps::conv1x1_mtiles);
-  m.def("gemm2_mtiles", &hipps::gemm2_mtiles, py::arg("M"), py::arg("N"), py::arg("bm") = 0);
+  m.def("gemm2_mtiles", &hipps::gemm2_mtiles, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("bm") = 0);
   m.def("gemm2_conv", &hipps::gemm2_conv, "second-generation MFMA conv GEMM (LDS-DMA staged, 256-row tiles)",
         py::arg("x"), py::arg("w"), py::arg("y"), py::arg("part") = py::none(), py::arg("add") = py::none(),
         py::arg("add_mask") = py::none(), py::arg("Hi"), py::arg("Wi"), py::arg("stride") = 1, py::arg("KH") = 1,
-        py::arg("KW") = 1, py::arg("pad") = 0, py::arg("bm") = 0, py::arg("bn") = 0);
+        py::arg("KW") = 1, py::arg("pad") = 0, py::arg("bm") = 0, py::arg("bn") = 0, py::arg("bn_x") = py::none(),
+        py::arg("bn_bits") = py::none(), py::arg("bn_mean") = py::none(), py::arg("bn_invstd") = py::none(),
+        py::arg("bn_scale") = py::none(), py::arg("bn_shift") = py::none());
   m.def("conv1x1_forward", &hipps::conv1x1_forward,
         "MFMA 1x1 conv (NHWC GEMM) with fused BN-stats epilogue and optional (+ add * mask) epilogue",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("part"), pybind11::arg("Hi"),

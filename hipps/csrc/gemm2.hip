@@ -40,13 +40,17 @@ constexpr int BK = 64;  // k per stage = 8 chunks of 16 bytes per row
 // 16-byte zero source for out-of-range rows and zero-padding taps (global memory, read-only)
 __device__ __attribute__((aligned(64))) const uint16_t kZero16[32] = {0};
 
-enum Epi : int { kPlain = 0, kStats = 1, kAdd = 2 };
+// epilogue flags: kStats = forward BN statistics of Y; kAdd = Y += R (* mask bits); kBst =
+// backward BN statistics of the BN whose output gradient Y is (relu' recomputed from x * scale +
+// shift), kBstBits = the same with the BN's stored ReLU bits (gemm.hip BnBwdTap)
+enum Epi : int { kPlain = 0, kStats = 1, kAdd = 2, kBst = 4, kBstBits = 8 };
 
 template <int BM, int BN> struct Cfg;
 template <> struct Cfg<256, 256> { static constexpr int TM = 128, TN = 64; };
 template <> struct Cfg<256, 128> { static constexpr int TM = 128, TN = 64; };
 template <> struct Cfg<128, 128> { static constexpr int TM = 64, TN = 64; };
 template <> struct Cfg<256, 64> { static constexpr int TM = 64, TN = 64; };
+template <> struct Cfg<128, 64> { static constexpr int TM = 64, TN = 32; };
 
 template <int BM, int BN> constexpr int nthreads() { return 64 * (BM / Cfg<BM, BN>::TM) * (BN / Cfg<BM, BN>::TN); }
 
@@ -65,6 +69,9 @@ struct Args {
   float* pb;
   const uint16_t* R;
   const uint8_t* RM;
+  const uint16_t* bx;  // kBst*: the BN input x under the output tile
+  const uint8_t* bbits;
+  const float *bmean, *binvstd, *bscale, *bshift;
   int M, N, K, Ho, Wo, Hi, Wi, stride, mtiles, ntiles;
   int KW, pad, Cin;  // implicit-GEMM geometry (TAPS)
 };
@@ -161,6 +168,16 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // epilogue operands (residual-gradient addend, BN-backward x and bits) are loaded during the
+  // MFMAs of the last K tile, when no DMA is in flight, if they fit the register budget
+  constexpr bool ADDE = (EPI & kAdd) != 0;
+  constexpr int BSTE = (EPI & kBstBits) ? 2 : (EPI & kBst) ? 1 : 0;
+  constexpr int RCH = BN / 8;             // 16-byte chunks per output row
+  constexpr int NOUT = BM * RCH / NT;     // output chunks per thread
+  constexpr bool PF = (ADDE != (BSTE != 0)) && NOUT * 5 <= 40;  // one operand stream, <= 40 registers
+  u32x4 pr[PF && ADDE ? NOUT : 1], px[PF && BSTE ? NOUT : 1];
+  uint32_t prm[PF && ADDE ? NOUT : 1], pxm[PF && BSTE ? NOUT : 1];
+
   const int KT = g.K / BK;
   issue(0, 0);
   for (int kt = 0; kt < KT; ++kt) {
@@ -170,7 +187,24 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + 1 < KT) issue(kt + 1, cur ^ 1);
+    if (kt + 1 < KT) {
+      issue(kt + 1, cur ^ 1);
+    } else if constexpr (PF) {
+#pragma unroll
+      for (int i = 0; i < NOUT; ++i) {
+        const int id = t + NT * i;
+        const int row = id / RCH, c = id - row * RCH;
+        const int64_t o = (int64_t)(m0 + row < g.M ? m0 + row : m0) * g.N + n0 + c * 8;
+        if constexpr (ADDE) {
+          pr[i] = *reinterpret_cast<const u32x4*>(g.R + o);
+          prm[i] = g.RM != nullptr ? g.RM[o >> 3] : 0xffu;
+        }
+        if constexpr (BSTE) {
+          px[i] = *reinterpret_cast<const u32x4*>(g.bx + o);
+          pxm[i] = BSTE == 2 ? g.bbits[o >> 3] : 0u;
+        }
+      }
+    }
     const uint16_t* As = lds + cur * STAGE;
     const uint16_t* Bs = As + BM * BK;
 #pragma unroll
@@ -201,6 +235,8 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   // ---- epilogue: bf16 tile -> LDS (padded rows), per-channel stats, 16-byte row stores ----
   // C/D map (16x16x32): column = lane & 15, row = (lane >> 4) * 4 + r.
   float* st = reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(lds) + SCR);
+  constexpr bool STATS = (EPI & kStats) != 0, ADD = (EPI & kAdd) != 0;
+  constexpr int BST = (EPI & kBstBits) ? 2 : (EPI & kBst) ? 1 : 0;
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int col = wn * TN + j * 16 + (lane & 15);
@@ -212,14 +248,14 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
         const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
         const uint16_t hb = f32_to_bf16(acc[i][j][r]);
         lds[row * EP + col] = hb;
-        if (EPI == kStats && m0 + row < g.M) {
+        if (STATS) {  // rows past M hold zeros (zero-page operands)
           const float v = bf16_to_f32(hb);
           s += v;
           qq = fmaf(v, v, qq);
         }
       }
     }
-    if (EPI == kStats) {
+    if (STATS) {
       s += __shfl_xor(s, 16, 64);
       qq += __shfl_xor(qq, 16, 64);
       s += __shfl_xor(s, 32, 64);
@@ -231,9 +267,21 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
     }
   }
   __syncthreads();
-  constexpr int RCH = BN / 8;             // 16-byte chunks per output row
-  constexpr int NOUT = BM * RCH / NT;     // output chunks per thread
-  static_assert(BM * RCH % NT == 0, "epilogue split");
+  static_assert(BM * RCH % NT == 0 && NT % RCH == 0, "epilogue split");
+  // BST: this thread's 8 channels are fixed (NT % RCH == 0): per-channel BN constants in registers
+  const int cc = (t % RCH) * 8;
+  float bmu[8], bis[8], bsc[8], bsh[8], bsa[8], bsb[8];
+  if (BST) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bmu[j] = g.bmean[n0 + cc + j];
+      bis[j] = g.binvstd[n0 + cc + j];
+      bsc[j] = BST == 1 ? g.bscale[n0 + cc + j] : 0.f;
+      bsh[j] = BST == 1 ? g.bshift[n0 + cc + j] : 0.f;
+      bsa[j] = 0.f;
+      bsb[j] = 0.f;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < NOUT; ++i) {
     const int id = t + NT * i;
@@ -241,10 +289,17 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
     if (m0 + row < g.M) {
       const int64_t o = (int64_t)(m0 + row) * g.N + n0 + c * 8;
       uint4 v = *reinterpret_cast<const uint4*>(lds + row * EP + c * 8);
-      if (EPI == kAdd) {  // + R (* ReLU-mask bits): a second gradient path into Y
-        u32x4 r = *reinterpret_cast<const u32x4*>(g.R + o);
-        if (g.RM != nullptr) {
-          const uint32_t mb = g.RM[o >> 3];
+      if (ADD) {  // + R (* ReLU-mask bits): a second gradient path into Y
+        u32x4 r;
+        uint32_t mb;
+        if constexpr (PF) {
+          r = pr[i];
+          mb = prm[i];
+        } else {
+          r = *reinterpret_cast<const u32x4*>(g.R + o);
+          mb = g.RM != nullptr ? g.RM[o >> 3] : 0xffu;
+        }
+        {
           r.x &= (mb & 1u ? 0xffffu : 0u) | (mb & 2u ? 0xffff0000u : 0u);
           r.y &= (mb & 4u ? 0xffffu : 0u) | (mb & 8u ? 0xffff0000u : 0u);
           r.z &= (mb & 16u ? 0xffffu : 0u) | (mb & 32u ? 0xffff0000u : 0u);
@@ -256,44 +311,96 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
         v.w = add_bf16x2(v.w, r.w);
       }
       *reinterpret_cast<uint4*>(g.Y + o) = v;
+      if (BST) {  // dz = dy * relu'(.) on the stored bf16 dy; x-hat from the BN input
+        u32x4 xu;
+        uint32_t mbits;
+        if constexpr (PF) {
+          xu = px[i];
+          mbits = pxm[i];
+        } else {
+          xu = *reinterpret_cast<const u32x4*>(g.bx + o);
+          mbits = BST == 2 ? g.bbits[o >> 3] : 0u;
+        }
+        const uint32_t dv[4] = {v.x, v.y, v.z, v.w};
+        const uint32_t xw[4] = {xu.x, xu.y, xu.z, xu.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = __uint_as_float(j & 1 ? dv[j >> 1] & 0xffff0000u : dv[j >> 1] << 16);
+          const float xv = __uint_as_float(j & 1 ? xw[j >> 1] & 0xffff0000u : xw[j >> 1] << 16);
+          const bool on = BST == 2 ? ((mbits >> j) & 1u) != 0u : fmaf(xv, bsc[j], bsh[j]) > 0.f;
+          const float dz = on ? d : 0.f;
+          bsa[j] += dz;
+          bsb[j] = fmaf(dz, (xv - bmu[j]) * bis[j], bsb[j]);
+        }
+      }
     }
   }
-  if (EPI == kStats && t < BN) {
-    float s = 0.f, qq = 0.f;
+  if (BST) {  // combine the NT/RCH row lanes of each channel chunk through LDS, fixed order
+    constexpr int RL = NT / RCH;
+    static_assert(2 * RL * BN * 4 <= lds_bytes<BM, BN>(), "BST scratch");
+    float* red = reinterpret_cast<float*>(lds);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[(t / RCH) * BN + cc + j] = bsa[j];
+      red[RL * BN + (t / RCH) * BN + cc + j] = bsb[j];
+    }
+    __syncthreads();
+    if (t < BN) {
+      float sa = 0.f, sb = 0.f;
+      for (int r = 0; r < RL; ++r) {
+        sa += red[r * BN + t];
+        sb += red[RL * BN + r * BN + t];
+      }
+      g.pa[(int64_t)(n0 + t) * g.mtiles + mt] = sa;
+      g.pb[(int64_t)(n0 + t) * g.mtiles + mt] = sb;
+    }
+  }
+  if (STATS && t < BN) {
+    float sa = 0.f, qa = 0.f;
 #pragma unroll
     for (int i = 0; i < WM; ++i) {
-      s += st[(i * BN + t) * 2];
-      qq += st[(i * BN + t) * 2 + 1];
+      sa += st[(i * BN + t) * 2];
+      qa += st[(i * BN + t) * 2 + 1];
     }
-    g.pa[(int64_t)(n0 + t) * g.mtiles + mt] = s;
-    g.pb[(int64_t)(n0 + t) * g.mtiles + mt] = qq;
+    g.pa[(int64_t)(n0 + t) * g.mtiles + mt] = sa;
+    g.pb[(int64_t)(n0 + t) * g.mtiles + mt] = qa;
   }
 }
 
-// block tile for a problem: the largest tile whose grid still gives every CU work
-inline void pick_tile(int64_t M, int64_t N, int& bm, int& bn) {
+// default block tile for a problem (the Python side autotunes per shape and passes bm / bn)
+inline void pick_tile(int64_t M, int64_t N, int64_t K, int& bm, int& bn) {
   auto blocks = [&](int a, int b) { return ((M + a - 1) / a) * (N / b); };
-  if (N % 256 == 0 && blocks(256, 256) >= 256) { bm = 256; bn = 256; return; }
-  if (N % 128 == 0 && blocks(256, 128) >= 256) { bm = 256; bn = 128; return; }
+  if (N % 256 == 0 && ((K >= 1024 && blocks(256, 256) >= 192 && blocks(128, 128) < 1536) ||
+                       (K >= 2048 && blocks(256, 256) >= 512))) {
+    bm = 256; bn = 256; return;
+  }
   if (N % 128 == 0) { bm = 128; bn = 128; return; }
-  bm = 256; bn = 64;
+  bm = 128; bn = 64;
 }
 
 }  // namespace g2
 
-int64_t gemm2_mtiles(int64_t M, int64_t N, int64_t bm_req) {
-  int bm = (int)bm_req, bn = 0;
-  if (bm <= 0) g2::pick_tile(M, N, bm, bn);
-  return (M + bm - 1) / bm;
+int64_t gemm2_mtiles(int64_t M, int64_t N, int64_t K, int64_t bm) {
+  int b = (int)bm, n = 0;
+  if (b <= 0) g2::pick_tile(M, N, K, b, n);
+  return (M + b - 1) / b;
 }
 
 // x: [img, Cin, Hi, Wi] channels-last bf16; w: [Cout, Cin, KH, KW] channels-last bf16 (1x1: [Cout, Cin]);
-// y: [img, Cout, Ho, Wo] channels-last bf16.  part (optional): f32 [2, Cout, mtiles] BN statistics
-// partials (mtiles = gemm2_mtiles(M, N, bm)).  add (+ add_mask): y = conv(x) + add (* mask bits).
-// bm / bn: block tile (0 = pick per shape).
+// y: [img, Cout, Ho, Wo] channels-last bf16.
+//   part (optional): f32 [2, Cout, mtiles] (mtiles = gemm2_mtiles(M, N, K, bm)): the forward BN
+//     statistics of y, or -- with bn_x -- the backward BN reduction of the BN whose output
+//     gradient y is (bn_x its input, bn_bits its ReLU bits or none to recompute relu' from
+//     bn_x * bn_scale + bn_shift)
+//   add (+ add_mask, 1x1 only): y = conv(x) + add (* mask bits)
+//   bm / bn: block tile (0 = default per shape)
 void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part,
                 c10::optional<at::Tensor> add, c10::optional<at::Tensor> add_mask, int64_t Hi, int64_t Wi,
-                int64_t stride, int64_t KH, int64_t KW, int64_t pad, int64_t bm, int64_t bn) {
+                int64_t stride, int64_t KH, int64_t KW, int64_t pad, int64_t bm, int64_t bn,
+                c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_bits, c10::optional<at::Tensor> bn_mean,
+                c10::optional<at::Tensor> bn_invstd, c10::optional<at::Tensor> bn_scale,
+                c10::optional<at::Tensor> bn_shift) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "gemm2: device tensors");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
                   y.scalar_type() == at::kBFloat16, "gemm2: bf16 tensors");
@@ -304,6 +411,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
   const int64_t Ho = (Hi + 2 * pad - KH) / stride + 1, Wo = (Wi + 2 * pad - KW) / stride + 1;
   const int64_t M = imgs * Ho * Wo;
   TORCH_CHECK(y.numel() == M * N, "gemm2: y size");
+  TORCH_CHECK(w.is_contiguous() || w.is_contiguous(at::MemoryFormat::ChannelsLast), "gemm2: dense w");
   for (const at::Tensor* t : {&x, &w, &y})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm2: 16-byte aligned tensors");
   TORCH_CHECK(x.dim() != 4 || x.is_contiguous(at::MemoryFormat::ChannelsLast), "gemm2: channels-last x");
@@ -311,9 +419,10 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
   TORCH_CHECK(w.dim() != 4 || KH * KW == 1 || w.is_contiguous(at::MemoryFormat::ChannelsLast), "gemm2: channels-last w");
   TORCH_CHECK(M < (int64_t(1) << 31) && x.numel() < (int64_t(1) << 40), "gemm2: size");
   int BMv = (int)bm, BNv = (int)bn;
-  if (BMv <= 0 || BNv <= 0) g2::pick_tile(M, N, BMv, BNv);
+  if (BMv <= 0 || BNv <= 0) g2::pick_tile(M, N, K, BMv, BNv);
   TORCH_CHECK(N % BNv == 0, "gemm2: Cout must be a multiple of the block tile");
   const int64_t mtiles = (M + BMv - 1) / BMv, ntiles = N / BNv;
+  TORCH_CHECK(mtiles * ntiles < (int64_t(1) << 31), "gemm2: grid");
   g2::Args a{};
   a.X = (const uint16_t*)x.data_ptr();
   a.W = (const uint16_t*)w.data_ptr();
@@ -327,39 +436,72 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
                     part->numel() == 2 * N * mtiles, "gemm2: part must be f32 [2, Cout, mtiles]");
     a.pa = part->data_ptr<float>();
     a.pb = a.pa + N * mtiles;
-    epi = g2::kStats;
   }
+  const bool taps = !(KH == 1 && KW == 1 && pad == 0);
   if (add.has_value() && add->defined()) {
-    TORCH_CHECK(epi == g2::kPlain, "gemm2: statistics and add epilogues are exclusive");
+    TORCH_CHECK(!taps, "gemm2: the add epilogue is for 1x1 convolutions");
     TORCH_CHECK(add->is_cuda() && add->scalar_type() == at::kBFloat16 && add->numel() == M * N &&
+                    (add->dim() != 4 || add->is_contiguous(at::MemoryFormat::ChannelsLast)) &&
                     reinterpret_cast<uintptr_t>(add->data_ptr()) % 16 == 0, "gemm2: add shaped like y");
     a.R = (const uint16_t*)add->data_ptr();
     if (add_mask.has_value() && add_mask->defined()) {
-      TORCH_CHECK(add_mask->is_cuda() && add_mask->scalar_type() == at::kByte && add_mask->numel() == M * N / 8,
-                  "gemm2: add_mask must be uint8[numel(y)/8]");
+      TORCH_CHECK(add_mask->is_cuda() && add_mask->scalar_type() == at::kByte && add_mask->is_contiguous() &&
+                      add_mask->numel() == M * N / 8, "gemm2: add_mask must be uint8[numel(y)/8]");
       a.RM = (const uint8_t*)add_mask->data_ptr();
     }
-    epi = g2::kAdd;
+    epi |= g2::kAdd;
   }
-  const bool taps = !(KH == 1 && KW == 1 && pad == 0);
+  if (bn_x.has_value() && bn_x->defined()) {
+    TORCH_CHECK(!taps && a.pa != nullptr, "gemm2: BN-backward statistics need a 1x1 conv and part");
+    TORCH_CHECK(bn_x->is_cuda() && bn_x->scalar_type() == at::kBFloat16 && bn_x->numel() == M * N &&
+                    (bn_x->dim() != 4 || bn_x->is_contiguous(at::MemoryFormat::ChannelsLast)) &&
+                    reinterpret_cast<uintptr_t>(bn_x->data_ptr()) % 16 == 0, "gemm2: bn_x shaped like y");
+    for (const c10::optional<at::Tensor>* v : {&bn_mean, &bn_invstd, &bn_scale, &bn_shift})
+      TORCH_CHECK(v->has_value() && (*v)->defined() && (*v)->is_cuda() && (*v)->scalar_type() == at::kFloat &&
+                      (*v)->is_contiguous() && (*v)->numel() == N, "gemm2: BN vectors must be f32 [C]");
+    a.bx = (const uint16_t*)bn_x->data_ptr();
+    a.bmean = bn_mean->data_ptr<float>();
+    a.binvstd = bn_invstd->data_ptr<float>();
+    a.bscale = bn_scale->data_ptr<float>();
+    a.bshift = bn_shift->data_ptr<float>();
+    if (bn_bits.has_value() && bn_bits->defined()) {
+      TORCH_CHECK(bn_bits->is_cuda() && bn_bits->scalar_type() == at::kByte && bn_bits->is_contiguous() &&
+                      bn_bits->numel() == M * N / 8, "gemm2: bn_bits must be uint8[numel(y)/8]");
+      a.bbits = (const uint8_t*)bn_bits->data_ptr();
+      epi |= g2::kBstBits;
+    } else {
+      epi |= g2::kBst;
+    }
+  } else if (a.pa != nullptr) {
+    TORCH_CHECK(!(epi & g2::kAdd), "gemm2: forward statistics and the add epilogue are exclusive");
+    epi |= g2::kStats;
+  }
   auto stream = c10::hip::getCurrentHIPStream();
   const int grid = (int)(mtiles * ntiles);
 #define HIPPS_G2(BMc, BNc, EPc, TPc) \
   hipLaunchKernelGGL((g2::k_gemm<BMc, BNc, EPc, TPc>), grid, (g2::nthreads<BMc, BNc>()), 0, stream, a)
-#define HIPPS_G2_E(BMc, BNc)                                                    \
-  do {                                                                          \
-    if (taps) {                                                                 \
-      if (epi == g2::kStats) HIPPS_G2(BMc, BNc, g2::kStats, true);              \
-      else HIPPS_G2(BMc, BNc, g2::kPlain, true);                                \
-    } else if (epi == g2::kStats) HIPPS_G2(BMc, BNc, g2::kStats, false);        \
-    else if (epi == g2::kAdd) HIPPS_G2(BMc, BNc, g2::kAdd, false);              \
-    else HIPPS_G2(BMc, BNc, g2::kPlain, false);                                 \
+#define HIPPS_G2_E(BMc, BNc)                                                                        \
+  do {                                                                                              \
+    if (taps) {                                                                                     \
+      if (epi == g2::kStats) HIPPS_G2(BMc, BNc, g2::kStats, true);                                  \
+      else HIPPS_G2(BMc, BNc, g2::kPlain, true);                                                    \
+    } else {                                                                                        \
+      switch (epi) {                                                                                \
+        case g2::kStats: HIPPS_G2(BMc, BNc, g2::kStats, false); break;                              \
+        case g2::kAdd: HIPPS_G2(BMc, BNc, g2::kAdd, false); break;                                  \
+        case g2::kBst: HIPPS_G2(BMc, BNc, g2::kBst, false); break;                                  \
+        case g2::kBst | g2::kAdd: HIPPS_G2(BMc, BNc, (g2::kBst | g2::kAdd), false); break;          \
+        case g2::kBstBits: HIPPS_G2(BMc, BNc, g2::kBstBits, false); break;                          \
+        case g2::kBstBits | g2::kAdd: HIPPS_G2(BMc, BNc, (g2::kBstBits | g2::kAdd), false); break;  \
+        default: HIPPS_G2(BMc, BNc, g2::kPlain, false); break;                                      \
+      }                                                                                             \
+    }                                                                                               \
   } while (0)
-  TORCH_CHECK(!(taps && epi == g2::kAdd), "gemm2: the add epilogue is for 1x1 convolutions");
   if (BMv == 256 && BNv == 256) HIPPS_G2_E(256, 256);
   else if (BMv == 256 && BNv == 128) HIPPS_G2_E(256, 128);
   else if (BMv == 128 && BNv == 128) HIPPS_G2_E(128, 128);
   else if (BMv == 256 && BNv == 64) HIPPS_G2_E(256, 64);
+  else if (BMv == 128 && BNv == 64) HIPPS_G2_E(128, 64);
   else TORCH_CHECK(false, "gemm2: unsupported block tile ", BMv, "x", BNv);
 #undef HIPPS_G2_E
 #undef HIPPS_G2

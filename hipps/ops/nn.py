@@ -37,7 +37,123 @@ _OWN_KXK_FWD = _os.environ.get("HIPPS_OWN_KXK", "0") != "0"
 # hipps MFMA stem kernels (stem.hip) instead of MIOpen
 _OWN_STEM = _os.environ.get("HIPPS_OWN_STEM", "1") != "0"
 
+# second-generation GEMM core (gemm2.hip: LDS-DMA staging, 128x64 .. 256x256 tiles) for the 1x1
+# convolutions and the KxK forward / stride-1 input gradient; per shape the fastest of {gemm2
+# tiles, first core / MIOpen} is picked on first use (timed on the real operands) and cached
+_GEMM2 = _os.environ.get("HIPPS_GEMM2", "1") != "0"
+
 MASK_NONE, MASK_X, MASK_Y, MASK_BITS = 0, 1, 2, 3
+
+
+class _Tuner:
+    """Per-shape kernel choice by measurement (like cudnn.benchmark): on the first call for a
+    key, every candidate runs once to warm up and then 3 times between HIP events on the current
+    stream; the fastest name is cached.  Candidates must be side-effect free apart from writing
+    their output (every candidate writes the same values)."""
+
+    def __init__(self):
+        self.cache: dict = {}
+        self.times: dict = {}
+
+    def pick(self, key, cands: dict) -> str:
+        got = self.cache.get(key)
+        if got is not None:
+            return got
+        if len(cands) == 1:
+            got = next(iter(cands))
+        else:
+            for fn in cands.values():
+                fn()
+            t = {}
+            for name, fn in cands.items():
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(3):
+                    fn()
+                e.record()
+                e.synchronize()
+                t[name] = s.elapsed_time(e) / 3
+            got = min(t, key=t.get)
+            self.times[key] = t
+        self.cache[key] = got
+        return got
+
+
+TUNER = _Tuner()
+_G2_TILES = ((128, 128), (256, 256), (128, 64), (256, 64))
+
+
+def _g2_names(N: int):
+    return [f"g2_{bm}x{bn}" for bm, bn in _G2_TILES if N % bn == 0]
+
+
+def _conv1x1_gemm(x2, w2d, y, Hi, Wi, stride, part_needed, add=None, add_mask=None, bg=None):
+    """y = x . w2d^T as a 1x1 conv (x channels-last [n, K, Hi, Wi] or [M, K]; w2d [N, K]) on the
+    fastest core for this shape AND epilogue (candidates are timed with the real epilogue: the
+    memory-bound residual / BN-backward epilogues change the ranking); returns the statistics
+    partials [2, N, mtiles] if requested (the forward BN statistics, or with ``bg`` the backward
+    reduction of that BN)."""
+    C = native()
+    N, K = w2d.shape
+    M = y.numel() // N
+
+    def run(name):
+        part = None
+        if name == "g1":
+            if part_needed:
+                part = torch.empty((2, N, C.conv1x1_mtiles(M)), dtype=torch.float32, device=y.device)
+            if bg is not None:
+                C.conv1x1_forward(x2, w2d, y, part, Hi, Wi, stride, add, add_mask, bg.x, bg.mask, bg.mean, bg.invstd,
+                                  bg.scale, bg.shift)
+            else:
+                C.conv1x1_forward(x2, w2d, y, part, Hi, Wi, stride, add, add_mask)
+            return part
+        bm, bn = (int(v) for v in name[3:].split("x"))
+        if part_needed:
+            part = torch.empty((2, N, C.gemm2_mtiles(M, N, K, bm)), dtype=torch.float32, device=y.device)
+        if bg is not None:
+            C.gemm2_conv(x2, w2d, y, part, add, add_mask, Hi, Wi, stride, 1, 1, 0, bm, bn, bg.x, bg.mask, bg.mean,
+                         bg.invstd, bg.scale, bg.shift)
+        else:
+            C.gemm2_conv(x2, w2d, y, part, add, add_mask, Hi, Wi, stride, 1, 1, 0, bm, bn)
+        return part
+
+    name = "g1"
+    if _GEMM2 and K % 64 == 0 and N % 64 == 0:
+        epi = (part_needed, add is not None, add_mask is not None, bg is not None and bg.mask is not None,
+               bg is not None)
+        name = TUNER.pick(("1x1", M, K, N, stride, Hi, Wi, epi),
+                          {n: (lambda n=n: run(n)) for n in ["g1"] + _g2_names(N)})
+    return run(name)
+
+
+def _convkxk_gemm(x, w, stride, pad, stats: bool):
+    """KxK conv forward (channels-last bf16) on the fastest of {gemm2 implicit GEMM tiles, MIOpen}
+    for this shape; returns (y, part or None) -- part: the following BN's statistics partials
+    when the GEMM ran (MIOpen gives none)."""
+    C = native()
+    n, cin, h, wd = x.shape
+    cout, k = w.shape[0], w.shape[2]
+    ho, wo = (h + 2 * pad - k) // stride + 1, (wd + 2 * pad - k) // stride + 1
+    y = torch.empty((n, cout, ho, wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    mio = lambda: torch.ops.aten.convolution(x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1)  # noqa: E731
+
+    def run(name):
+        if name == "miopen":
+            return mio(), None
+        bm, bn = (int(v) for v in name[3:].split("x"))
+        part = None
+        if stats:
+            part = torch.empty((2, cout, C.gemm2_mtiles(n * ho * wo, cout, k * k * cin, bm)), dtype=torch.float32,
+                               device=x.device)
+        C.gemm2_conv(x, w, y, part, None, None, h, wd, stride, k, k, pad, bm, bn)
+        return y, part
+
+    name = "miopen"
+    if _GEMM2 and cin % 64 == 0 and cout % 64 == 0:
+        name = TUNER.pick(("kxk", n, cin, h, wd, cout, k, stride, pad, stats),
+                          {nm: (lambda nm=nm: run(nm)) for nm in ["miopen"] + _g2_names(cout)})
+    return run(name)
 
 
 class ResidualTap:
@@ -136,9 +252,7 @@ class _Conv1x1(torch.autograd.Function):
         Cout = w.shape[0]
         Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
         y = torch.empty((N, Cout, Ho, Wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
-        mt = native().conv1x1_mtiles(N * Ho * Wo)
-        part = torch.empty((2, Cout, mt), dtype=torch.float32, device=x.device)
-        native().conv1x1_forward(x, w.reshape(Cout, Cin), y, part, H, W, stride)
+        part = _conv1x1_gemm(x, w.reshape(Cout, Cin), y, H, W, stride, True)
         ctx.stride = stride
         ctx.tap = tap
         ctx.save_for_backward(x, w)
@@ -188,14 +302,9 @@ class _Conv1x1(torch.autograd.Function):
             # x's gradient is complete here only if the residual path it also feeds was summed in
             # (an identity block's tap delivered, or no tap was involved)
             if bg is not None and (ctx.tap is None or add is not None):
-                n_img, _, h, wd = x.shape
-                part = torch.empty((2, cin, native().conv1x1_mtiles(n_img * h * wd)), dtype=torch.float32,
-                                   device=x.device)
-                native().conv1x1_forward(dy, wt, dx, part, h, wd, 1, add, add_mask, bg.x, bg.mask, bg.mean,
-                                         bg.invstd, bg.scale, bg.shift)
-                bg.part = part
+                bg.part = _conv1x1_gemm(dy, wt, dx, x.shape[2], x.shape[3], 1, True, add, add_mask, bg)
             else:
-                native().conv1x1_forward(dy, wt, dx, None, x.shape[2], x.shape[3], 1, add, add_mask)
+                _conv1x1_gemm(dy, wt, dx, x.shape[2], x.shape[3], 1, False, add, add_mask)
         ctx.bngrad = None
         return dx, dw, None, None, None, None
 
@@ -285,7 +394,9 @@ class _ConvKxK(torch.autograd.Function):
         ctx.set_materialize_grads(False)
         ctx.wf = _TSHADOWS.get(w_master.data_ptr()) if w_master.dtype == torch.float32 else None
         part = None
-        if _own_kxk(x.shape[1], w.shape[0]):
+        if _GEMM2 and w.is_contiguous(memory_format=torch.channels_last):
+            y, part = _convkxk_gemm(x, w, stride, pad, stats)  # the next BN's statistics from the epilogue
+        elif _own_kxk(x.shape[1], w.shape[0]):
             n, _, h, wd = x.shape
             k = w.shape[2]
             ho, wo = (h + 2 * pad - k) // stride + 1, (wd + 2 * pad - k) // stride + 1
@@ -318,7 +429,9 @@ class _ConvKxK(torch.autograd.Function):
             wf = ctx.wf if ctx.wf is not None and ctx.wf.dim() == 4 else None
             if wf is None:
                 wf = torch.flip(w, (2, 3)).transpose(0, 1).contiguous(memory_format=torch.channels_last)
-            if _own_kxk(dy.shape[1], wf.shape[0]):
+            if _GEMM2 and wf.is_contiguous(memory_format=torch.channels_last):
+                dx = _convkxk_gemm(dy, wf, 1, p, False)[0]
+            elif _own_kxk(dy.shape[1], wf.shape[0]):
                 dx = torch.empty_like(x, memory_format=torch.channels_last)
                 native().convkxk_forward(dy, wf, dx, None, 1, p)
             else:
@@ -429,7 +542,7 @@ def conv2d_stats(conv: nn.Conv2d, x: torch.Tensor, fuse: bool = True):
         y, part = _ConvKxK.apply(x, conv.weight, conv.stride[0], conv.padding[0], True, True)
         return y, (part if part.numel() else None)
     if conv.training and convkxk_ok(conv, x, own_wgrad=False) and (
-            (_DGRAD_AS_FWD and conv.stride[0] == 1) or _own_kxk(conv.in_channels, conv.out_channels)):
+            (_DGRAD_AS_FWD and conv.stride[0] == 1) or _own_kxk(conv.in_channels, conv.out_channels) or _GEMM2):
         y, part = _ConvKxK.apply(x, conv.weight, conv.stride[0], conv.padding[0], False, True)  # MIOpen wgrad
         return y, (part if part.numel() else None)
     return conv(x), None

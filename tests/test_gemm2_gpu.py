@@ -1,0 +1,123 @@
+"""Second-generation conv GEMM core (hipps/csrc/gemm2.hip) against the first core (gemm.hip,
+itself checked against fp32 torch in test_conv1x1_gpu.py) and against fp32 torch directly.
+
+Both cores accumulate each output over K in the same order (64-deep K tiles, two 16x16x32 MFMA
+k-steps each), so the bf16 outputs must be bit-identical for every block tile; the statistics
+partials are grouped by M tile (128 vs the gemm2 tile), so their sums agree to rounding.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+CL = torch.channels_last
+TILES = [(128, 128), (256, 256), (256, 128), (128, 64), (256, 64)]
+
+
+def C():
+    from hipps.ops._native import native
+
+    return native()
+
+
+def _x(n, c, h, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return torch.randn(n, c, h, h, generator=g).to(DEV).to(torch.bfloat16).contiguous(memory_format=CL)
+
+
+@pytest.mark.parametrize("bm,bn", TILES)
+@pytest.mark.parametrize("cin,cout,stride", [(64, 256, 1), (256, 128, 1), (512, 256, 2)])
+def test_gemm2_1x1_forward_stats_bitwise_first_core(bm, bn, cin, cout, stride):
+    if cout % bn:
+        pytest.skip("tile wider than Cout")
+    n, h = 3, 13  # M tails: 3 * 13 * 13 = 507 rows (stride 2: 3 * 7 * 7)
+    x = _x(n, cin, h)
+    w = (torch.randn(cout, cin, device=DEV) / cin ** 0.5).to(torch.bfloat16)
+    ho = (h - 1) // stride + 1
+    M = n * ho * ho
+    y1 = torch.empty(n, cout, ho, ho, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
+    y2 = torch.full_like(y1, 7.0)
+    p1 = torch.empty(2, cout, C().conv1x1_mtiles(M), device=DEV)
+    p2 = torch.empty(2, cout, C().gemm2_mtiles(M, cout, cin, bm), device=DEV)
+    C().conv1x1_forward(x, w, y1, p1, h, h, stride)
+    C().gemm2_conv(x, w, y2, p2, None, None, h, h, stride, 1, 1, 0, bm, bn)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    torch.testing.assert_close(p2.sum(2), p1.sum(2), rtol=1e-5, atol=1e-3)
+    ref = F.conv2d(x.float(), w.float().view(cout, cin, 1, 1), stride=stride)
+    torch.testing.assert_close(y2.float(), ref, rtol=2e-2, atol=2e-2)
+    # the statistics are those of the stored bf16 output
+    yf = y2.float()
+    torch.testing.assert_close(p2[0].sum(1), yf.sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(p2[1].sum(1), (yf * yf).sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("bm,bn", [(128, 128), (256, 256), (128, 64)])
+@pytest.mark.parametrize("mode", ["add", "add_mask", "bst", "bst_bits", "bst_add"])
+def test_gemm2_dgrad_epilogues_match_first_core(bm, bn, mode):
+    n, h, cin, cout = 2, 15, 256, 256  # the dgrad GEMM: dy [M, cout] . wt [cin, cout]^T -> dx [M, cin]
+    if cin % bn:
+        pytest.skip("tile")
+    dy = _x(n, cout, h, 1)
+    wt = (torch.randn(cin, cout, device=DEV) / cout ** 0.5).to(torch.bfloat16)
+    M = n * h * h
+    add = _x(n, cin, h, 2) if "add" in mode else None
+    amask = torch.randint(0, 256, (M * cin // 8,), dtype=torch.uint8, device=DEV) if mode == "add_mask" else None
+    bx = bits = mean = inv = sc = sh = None
+    if "bst" in mode:
+        bx = _x(n, cin, h, 3)
+        mean = torch.randn(cin, device=DEV) * 0.1
+        inv = torch.rand(cin, device=DEV) + 0.5
+        sc = torch.randn(cin, device=DEV)
+        sh = torch.randn(cin, device=DEV) * 0.1
+        if mode == "bst_bits":
+            bits = torch.randint(0, 256, (M * cin // 8,), dtype=torch.uint8, device=DEV)
+    y1 = torch.empty(n, cin, h, h, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
+    y2 = torch.empty_like(y1)
+    p1 = p2 = None
+    if bx is not None:
+        p1 = torch.empty(2, cin, C().conv1x1_mtiles(M), device=DEV)
+        p2 = torch.empty(2, cin, C().gemm2_mtiles(M, cin, cout, bm), device=DEV)
+    C().conv1x1_forward(dy, wt, y1, p1, h, h, 1, add, amask, bx, bits, mean, inv, sc, sh)
+    C().gemm2_conv(dy, wt, y2, p2, add, amask, h, h, 1, 1, 1, 0, bm, bn, bx, bits, mean, inv, sc, sh)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    if p1 is not None:
+        torch.testing.assert_close(p2.sum(2), p1.sum(2), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("bm,bn", TILES)
+@pytest.mark.parametrize("cin,cout,h,stride", [(64, 128, 14, 1), (128, 128, 15, 2), (256, 256, 7, 1)])
+def test_gemm2_3x3_implicit_gemm(bm, bn, cin, cout, h, stride):
+    if cout % bn:
+        pytest.skip("tile")
+    n = 2
+    x = _x(n, cin, h, 4)
+    w = (torch.randn(cout, cin, 3, 3, device=DEV) / (9 * cin) ** 0.5).to(torch.bfloat16).contiguous(memory_format=CL)
+    ho = (h + 2 - 3) // stride + 1
+    M = n * ho * ho
+    y1 = torch.empty(n, cout, ho, ho, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
+    y2 = torch.full_like(y1, 3.0)
+    p2 = torch.empty(2, cout, C().gemm2_mtiles(M, cout, 9 * cin, bm), device=DEV)
+    C().convkxk_forward(x, w, y1, None, stride, 1)
+    C().gemm2_conv(x, w, y2, p2, None, None, h, h, stride, 3, 3, 1, bm, bn)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)  # zero-page padding == the first core's masked loads
+    ref = F.conv2d(x.float(), w.float(), stride=stride, padding=1)
+    torch.testing.assert_close(y2.float(), ref, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(p2[0].sum(1), y2.float().sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+
+
+def test_tuner_picks_and_caches():
+    from hipps.ops import nn as hnn
+
+    x = _x(4, 256, 14)
+    w = (torch.randn(512, 256, device=DEV) / 16).to(torch.bfloat16)
+    y = torch.empty(4, 512, 14, 14, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
+    part = hnn._conv1x1_gemm(x, w, y, 14, 14, 1, True)
+    key = ("1x1", 4 * 14 * 14, 256, 512, 1, 14, 14)
+    assert key in hnn.TUNER.cache and part.shape[:2] == (2, 512)
+    ref = F.conv2d(x.float(), w.float().view(512, 256, 1, 1))
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)

@@ -26,7 +26,7 @@ GEMMS = [  # (M, K, N): ResNet-50 bs256 1x1 convolutions + large steady-state pr
 CONVS = [  # (Cin, H, Cout, stride): ResNet-50 bs256 3x3 convolutions (pad 1)
     (64, 56, 64, 1), (128, 56, 128, 2), (128, 28, 128, 1), (256, 28, 256, 2), (256, 14, 256, 1),
     (512, 14, 512, 2), (512, 7, 512, 1)]
-TILES = [(256, 256), (256, 128), (128, 128), (256, 64)]
+TILES = [(256, 256), (256, 128), (128, 128), (256, 64), (128, 64)]
 
 
 def timeit(fn, it):
@@ -64,7 +64,7 @@ def gemm_row(M, K, N, it):
         ms = timeit(lambda: C.gemm2_conv(x, w, y, None, None, None, M, 1, bm=bm, bn=bn), it)
         row[f"g2_{bm}x{bn}_ms"] = round(ms, 4)
         row[f"g2_{bm}x{bn}_TF"] = round(flop / ms / 1e9, 1)
-    mt = C.gemm2_mtiles(M, N, 0)
+    mt = C.gemm2_mtiles(M, N, K, 0)
     part = torch.empty(2, N, mt, device="cuda")
     ms = timeit(lambda: C.gemm2_conv(x, w, y, part, None, None, M, 1), it)
     row["g2_auto_stats_ms"] = round(ms, 4)

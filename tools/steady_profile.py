@@ -34,7 +34,7 @@ def main():
     for k, (d, c) in agg.items():
         if "hipps" in k:
             key = ("hipps-norm" if "k_bn_" in k else
-                   "hipps-gemm" if ("conv1x1" in k or "wgrad" in k or "stem" in k) else "hipps-ps")
+                   "hipps-gemm" if ("conv1x1" in k or "wgrad" in k or "stem" in k or "k_gemm" in k) else "hipps-ps")
         elif "BatchNorm" in k:
             key = "miopen-batchnorm"
         elif any(s in k for s in ("conv", "igemm", "gemm", "Cijk", "xdl")):
