@@ -117,7 +117,7 @@ def test_tuner_picks_and_caches():
     w = (torch.randn(512, 256, device=DEV) / 16).to(torch.bfloat16)
     y = torch.empty(4, 512, 14, 14, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
     part = hnn._conv1x1_gemm(x, w, y, 14, 14, 1, True)
-    key = ("1x1", 4 * 14 * 14, 256, 512, 1, 14, 14)
-    assert key in hnn.TUNER.cache and part.shape[:2] == (2, 512)
+    keys = [k for k in hnn.TUNER.cache if k[:7] == ("1x1", 4 * 14 * 14, 256, 512, 1, 14, 14)]
+    assert len(keys) == 1 and part.shape[:2] == (2, 512)
     ref = F.conv2d(x.float(), w.float().view(512, 256, 1, 1))
     torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
