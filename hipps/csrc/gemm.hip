@@ -910,6 +910,9 @@ void convkxk_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
 #undef HIPPS_CK
 }
 
+void wgrad_reduce_slabs(const at::Tensor& part, int64_t S, int64_t N, int64_t K, at::Tensor& dw,
+                        hipStream_t stream0);
+
 // v2 weight gradient launcher: dW[N][K] (K = KH*KW*Cin) as S split-M partial slabs + fixed-order sum.
 static void launch_wgrad2(const at::Tensor& dy, const at::Tensor& x, at::Tensor& dw, int64_t M, int64_t N, int64_t K,
                           int64_t Cin, int64_t Ho, int64_t Wo, int64_t Hi, int64_t Wi, int64_t stride, int64_t KW,
@@ -946,22 +949,25 @@ static void launch_wgrad2(const at::Tensor& dy, const at::Tensor& x, at::Tensor&
   else if (TK == 128) HIPPS_W2(64, 128);
   else HIPPS_W2(64, 64);
 #undef HIPPS_W2
-  if (S > 1) {
-    // fixed-order slab sum; split over G groups when N*K alone is too few threads to keep the
-    // loads in flight (64x64 outputs: 1024 float4 lanes x S serial loads was ~60 us)
-    const int64_t NK4 = N * K / 4;
-    const int G = (int)std::min<int64_t>(S, std::max<int64_t>(1, (65536 + NK4 - 1) / NK4));
-    const unsigned gx = (unsigned)((NK4 + kBlock - 1) / kBlock);
-    if (G == 1) {
-      hipLaunchKernelGGL(k_wgrad_reduce1, dim3(gx, 1), kBlock, 0, stream0, part.data_ptr<float>(), (int)S, 1, NK4,
-                         dw.data_ptr<float>());
-    } else {
-      auto tmp = at::empty({(int64_t)G, N, K}, dw.options());
-      hipLaunchKernelGGL(k_wgrad_reduce1, dim3(gx, G), kBlock, 0, stream0, part.data_ptr<float>(), (int)S, G, NK4,
-                         tmp.data_ptr<float>());
-      hipLaunchKernelGGL(k_wgrad_reduce2, gx, kBlock, 0, stream0, tmp.data_ptr<float>(), G, NK4,
-                         dw.data_ptr<float>());
-    }
+  if (S > 1) wgrad_reduce_slabs(part, S, N, K, dw, stream0);
+}
+
+// dw[N][K] = sum_s part[s][N][K] in a fixed order (deterministic); shared with gemm2.hip's
+// weight-gradient core.  Split over G groups when N*K alone is too few threads to keep the
+// loads in flight (64x64 outputs: 1024 float4 lanes x S serial loads was ~60 us).
+void wgrad_reduce_slabs(const at::Tensor& part, int64_t S, int64_t N, int64_t K, at::Tensor& dw,
+                        hipStream_t stream0) {
+  const int64_t NK4 = N * K / 4;
+  const int G = (int)std::min<int64_t>(S, std::max<int64_t>(1, (65536 + NK4 - 1) / NK4));
+  const unsigned gx = (unsigned)((NK4 + kBlock - 1) / kBlock);
+  if (G == 1) {
+    hipLaunchKernelGGL(k_wgrad_reduce1, dim3(gx, 1), kBlock, 0, stream0, part.data_ptr<float>(), (int)S, 1, NK4,
+                       dw.data_ptr<float>());
+  } else {
+    auto tmp = at::empty({(int64_t)G, N, K}, dw.options());
+    hipLaunchKernelGGL(k_wgrad_reduce1, dim3(gx, G), kBlock, 0, stream0, part.data_ptr<float>(), (int)S, G, NK4,
+                       tmp.data_ptr<float>());
+    hipLaunchKernelGGL(k_wgrad_reduce2, gx, kBlock, 0, stream0, tmp.data_ptr<float>(), G, NK4, dw.data_ptr<float>());
   }
 }
 

@@ -368,6 +368,159 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   }
 }
 
+// ==========================================================================================
+// Weight gradient:  dW[N][Kt] = sum_m dY[m][n] * X[src(m, tap)][c]     (Kt = KH*KW*Cin, k = tap*Cin + c)
+//
+// The first core's split-M kernel (gemm.hip k_conv1x1_wgrad2) with the operand path of this file:
+// each 64-row M stage of dY [64][TN] and X [64][TK] goes global -> LDS by DMA (16-byte chunks, the
+// XOR swizzle ch ^ f(row) applied on the per-lane global address), two stages, one barrier per
+// stage; fragments are read with the transposing ds_read_b64_tr_b16 (8 consecutive m per lane).
+// Rows past the block's M chunk and padding taps read the zero page.  Each block writes an fp32
+// partial slab; gemm.hip wgrad_reduce_slabs sums the S slabs in a fixed order.
+struct FastDiv2 {
+  uint32_t d, mul, shift;
+};
+inline FastDiv2 make_fastdiv2(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint64_t mul = ((((1ull << l) - d) << 32) / d) + 1;
+  return FastDiv2{d, (uint32_t)mul, l};
+}
+__device__ __forceinline__ uint32_t fdiv2(uint32_t n, const FastDiv2& f) { return (__umulhi(n, f.mul) + n) >> f.shift; }
+
+struct WArgs {
+  const uint16_t* dY;
+  const uint16_t* X;
+  float* part;
+  int M, N, K, Cin, Ho, Wo, Hi, Wi, stride, KW, pad, chunk, tn, tk;
+  FastDiv2 fd_hw, fd_w;
+};
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+template <int TW>
+__device__ __forceinline__ int wswz(int row) {  // chunk XOR of a [rows][TW x bf16] tile row
+  return TW == 128 ? (((row & 3) << 2) | ((row >> 2) & 3)) : (((row & 3) << 1) | ((row >> 2) & 1));
+}
+
+template <int TW>
+__device__ __forceinline__ bf16x8 tr_frag2(const uint8_t* tile, int row0, int col0, int lane) {
+  // rows row0 + 8*(lane>>4) + {0..3, 4..7}, columns col0 .. col0+15 (col0 % 16 == 0)
+  const int il = lane & 15, q = il >> 2, p = il & 3;
+  const int r = row0 + 8 * (lane >> 4) + q;
+  const int ch = (col0 >> 3) + (p >> 1);
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4*)(tile + 2 * TW * r + 16 * (ch ^ wswz<TW>(r)) + 8 * (p & 1)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4*)(tile + 2 * TW * (r + 4) + 16 * (ch ^ wswz<TW>(r + 4)) + 8 * (p & 1)));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+constexpr int kWM = 64;  // m rows per stage
+
+template <int TN, int TK>
+__global__ __launch_bounds__(256) void k_wgrad(WArgs g) {
+  constexpr int YT = kWM * TN * 2, XT = kWM * TK * 2;  // bytes per staged tile
+  constexpr int CY = TN / 8, CX = TK / 8;             // 16-byte chunks per staged row
+  constexpr int RY = 64 / CY, RX = 64 / CX;           // rows per wave-instruction (1 KB)
+  constexpr int IY = kWM / RY / 4, IX = kWM / RX / 4; // wave-instructions per stage per wave
+  constexpr int FN = TN / 32, FK = TK / 32;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * (YT + XT)];
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tiles = g.tn * g.tk;
+  const int sidx = bid / tiles, tile = bid - sidx * tiles;
+  const int n0 = (tile / g.tk) * TN, k0 = (tile % g.tk) * TK;
+  const int mbeg = sidx * g.chunk, mend = min(g.M, mbeg + g.chunk);
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wn = w >> 1, wk = w & 1;
+  const int tap = k0 / g.Cin, c0 = k0 - tap * g.Cin;
+  const int kr = tap / g.KW, kc = tap - kr * g.KW;
+  const bool direct = g.KW == 1 && g.pad == 0 && g.stride == 1 && g.Cin == g.K;
+  // lane -> (row within the wave-instruction, logical chunk); the LDS slot is lane % C
+  const int ry = lane / CY, sy = lane % CY, rx = lane / CX, sx = lane % CX;
+
+  auto issue = [&](int st, int s) {
+    uint8_t* ty = lds + s * (YT + XT);
+    uint8_t* tx = ty + YT;
+    const int mb = mbeg + st * kWM;
+#pragma unroll
+    for (int i = 0; i < IY; ++i) {
+      const int row = (i * 4 + w) * RY + ry;
+      const int m = mb + row;
+      const int ch = sy ^ wswz<TN>(row);
+      const uint16_t* p = m < mend ? g.dY + (int64_t)m * g.N + n0 + ch * 8 : kZero16;
+      glds16(p, ty + (i * 4 + w) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < IX; ++i) {
+      const int row = (i * 4 + w) * RX + rx;
+      const int m = mb + row;
+      const int ch = sx ^ wswz<TK>(row);
+      const uint16_t* p = kZero16;
+      if (m < mend) {
+        if (direct) {
+          p = g.X + (int64_t)m * g.Cin + c0 + ch * 8;
+        } else {
+          const int img = (int)fdiv2((uint32_t)m, g.fd_hw), rem = m - img * (int)g.fd_hw.d;
+          const int ho = (int)fdiv2((uint32_t)rem, g.fd_w), wo = rem - ho * g.Wo;
+          const int hi = ho * g.stride - g.pad + kr, wi = wo * g.stride - g.pad + kc;
+          if (hi >= 0 && hi < g.Hi && wi >= 0 && wi < g.Wi)
+            p = g.X + (((int64_t)img * g.Hi + hi) * g.Wi + wi) * g.Cin + c0 + ch * 8;
+        }
+      }
+      glds16(p, tx + (i * 4 + w) * 1024);
+    }
+  };
+
+  f32x4 acc[FN][FK];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FK; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nst = (mend - mbeg + kWM - 1) / kWM;
+  issue(0, 0);
+  for (int st = 0; st < nst; ++st) {
+    const int cur = st & 1;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (st + 1 < nst) issue(st + 1, cur ^ 1);
+    const uint8_t* ty = lds + cur * (YT + XT);
+    const uint8_t* tx = ty + YT;
+#pragma unroll
+    for (int ks = 0; ks < kWM / 32; ++ks) {
+      bf16x8 a[FN], b[FK];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) a[i] = tr_frag2<TN>(ty, ks * 32, wn * (TN / 2) + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < FK; ++j) b[j] = tr_frag2<TK>(tx, ks * 32, wk * (TK / 2) + j * 16, lane);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FK; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  // D map: column (k) = lane & 15, row (n) = (lane >> 4) * 4 + r
+  float* out = g.part + (int64_t)sidx * g.N * g.K;
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FK; ++j) {
+      const int k = k0 + wk * (TK / 2) + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * (TN / 2) + i * 16 + (lane >> 4) * 4 + r;
+        out[(int64_t)n * g.K + k] = acc[i][j][r];
+      }
+    }
+}
+
 // default block tile for a problem (the Python side autotunes per shape and passes bm / bn)
 inline void pick_tile(int64_t M, int64_t N, int64_t K, int& bm, int& bn) {
   auto blocks = [&](int a, int b) { return ((M + a - 1) / a) * (N / b); };
@@ -505,6 +658,61 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
   else TORCH_CHECK(false, "gemm2: unsupported block tile ", BMv, "x", BNv);
 #undef HIPPS_G2_E
 #undef HIPPS_G2
+}
+
+void wgrad_reduce_slabs(const at::Tensor& part, int64_t S, int64_t N, int64_t K, at::Tensor& dw,
+                        hipStream_t stream0);
+
+// Weight gradient on the LDS-DMA core: dy [img, Cout, Ho, Wo] and x [img, Cin, Hi, Wi] channels-last
+// bf16; dw f32 [Cout, KH, KW, Cin] in memory (the channels-last weight layout; 1x1: [Cout, Cin]).
+// Cout % 64 == 0, Cin % 64 == 0.  S split-M partial slabs (~2 resident blocks per CU) + fixed-order sum.
+void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
+                 int64_t Hi, int64_t Wi) {
+  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dw.is_cuda(), "gemm2_wgrad: device tensors");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 && dw.scalar_type() == at::kFloat,
+              "gemm2_wgrad: bf16 dy/x, f32 dw");
+  TORCH_CHECK(dw.is_contiguous() || dw.is_contiguous(at::MemoryFormat::ChannelsLast), "gemm2_wgrad: dense dw");
+  const int64_t N = dw.size(0), K = dw.numel() / N, Cin = K / (KH * KW);
+  TORCH_CHECK(Cin * KH * KW == K && N % 64 == 0 && Cin % 64 == 0, "gemm2_wgrad: Cout % 64 == 0, Cin % 64 == 0");
+  const int64_t imgs = x.numel() / (Cin * Hi * Wi);
+  TORCH_CHECK(imgs * Cin * Hi * Wi == x.numel(), "gemm2_wgrad: x size");
+  const int64_t Ho = (Hi + 2 * pad - KH) / stride + 1, Wo = (Wi + 2 * pad - KW) / stride + 1;
+  const int64_t M = imgs * Ho * Wo;
+  TORCH_CHECK(dy.numel() == M * N, "gemm2_wgrad: dy size");
+  TORCH_CHECK(x.dim() != 4 || x.is_contiguous(at::MemoryFormat::ChannelsLast), "gemm2_wgrad: channels-last x");
+  TORCH_CHECK(dy.dim() != 4 || dy.is_contiguous(at::MemoryFormat::ChannelsLast), "gemm2_wgrad: channels-last dy");
+  for (const at::Tensor* t : {&x, &dy, &dw})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm2_wgrad: 16-byte aligned tensors");
+  TORCH_CHECK(M < (int64_t(1) << 31) && x.numel() < (int64_t(1) << 40), "gemm2_wgrad: size");
+  const int TN = N % 128 == 0 ? 128 : 64, TK = Cin % 128 == 0 ? 128 : 64;
+  const int64_t tn = N / TN, tk = K / TK, tiles = tn * tk;
+  const int64_t resident = 256 * (TN * TK == 128 * 128 ? 2 : TN * TK == 128 * 64 ? 3 : 5);
+  int64_t S = std::max<int64_t>(1, resident / tiles);
+  S = std::min<int64_t>(S, std::max<int64_t>(1, M / (8 * g2::kWM)));           // >= 8 stages per block
+  S = std::min<int64_t>(S, std::max<int64_t>(1, M * (N + K) / (4 * N * K)));  // slabs <= operand bytes
+  const int64_t chunk = ((M + S - 1) / S + g2::kWM - 1) / g2::kWM * g2::kWM;
+  S = (M + chunk - 1) / chunk;
+  TORCH_CHECK(S * tiles < (int64_t(1) << 31), "gemm2_wgrad: grid");
+  auto stream = c10::hip::getCurrentHIPStream();
+  at::Tensor part = S == 1 ? dw : at::empty({S, N, K}, dw.options());
+  g2::WArgs a{};
+  a.dY = (const uint16_t*)dy.data_ptr();
+  a.X = (const uint16_t*)x.data_ptr();
+  a.part = part.data_ptr<float>();
+  a.M = (int)M; a.N = (int)N; a.K = (int)K; a.Cin = (int)Cin; a.Ho = (int)Ho; a.Wo = (int)Wo; a.Hi = (int)Hi;
+  a.Wi = (int)Wi; a.stride = (int)stride; a.KW = (int)KW; a.pad = (int)pad; a.chunk = (int)chunk;
+  a.tn = (int)tn; a.tk = (int)tk;
+  a.fd_hw = g2::make_fastdiv2((uint32_t)(Ho * Wo));
+  a.fd_w = g2::make_fastdiv2((uint32_t)Wo);
+  const int grid = (int)(S * tiles);
+  if (TN == 128 && TK == 128) hipLaunchKernelGGL((g2::k_wgrad<128, 128>), grid, 256, 0, stream, a);
+  else if (TN == 128) hipLaunchKernelGGL((g2::k_wgrad<128, 64>), grid, 256, 0, stream, a);
+  else if (TK == 128) hipLaunchKernelGGL((g2::k_wgrad<64, 128>), grid, 256, 0, stream, a);
+  else hipLaunchKernelGGL((g2::k_wgrad<64, 64>), grid, 256, 0, stream, a);
+  if (S > 1) {
+    at::Tensor dwv = dw;
+    wgrad_reduce_slabs(part, S, N, K, dwv, stream);
+  }
 }
 
 }  // namespace hipps

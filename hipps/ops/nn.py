@@ -127,6 +127,26 @@ def _conv1x1_gemm(x2, w2d, y, Hi, Wi, stride, part_needed, add=None, add_mask=No
     return run(name)
 
 
+def _conv_wgrad(dy, x, dw, kh, kw, stride, pad):
+    """fp32 weight gradient dw ([Cout, Cin] for 1x1, channels-last [Cout, Cin, KH, KW] for KxK) on
+    the faster of the first core's split-M kernel and the LDS-DMA core (measured per shape)."""
+    C = native()
+    hi, wi = x.shape[2], x.shape[3]
+    cout, cin = dy.shape[1], x.shape[1]
+    if kh == kw == 1 and pad == 0:
+        first = lambda: C.conv1x1_wgrad(dy, x, dw.view(cout, cin), hi, wi, stride)  # noqa: E731
+    else:
+        first = lambda: C.conv_wgrad(dy, x, dw, kh, kw, stride, pad)  # noqa: E731
+    name = "w2"
+    if _GEMM2 and cout % 64 == 0 and cin % 64 == 0:
+        cands = {"w2": first, "w3": lambda: C.gemm2_wgrad(dy, x, dw, kh, kw, stride, pad, hi, wi)}
+        name = TUNER.pick(("wgrad", tuple(x.shape), cout, kh, kw, stride, pad), cands)
+    if name == "w3":
+        C.gemm2_wgrad(dy, x, dw, kh, kw, stride, pad, hi, wi)
+    else:
+        first()
+
+
 def _convkxk_gemm(x, w, stride, pad, stats: bool):
     """KxK conv forward (channels-last bf16) on the fastest of {gemm2 implicit GEMM tiles, MIOpen}
     for this shape; returns (y, part or None) -- part: the following BN's statistics partials
@@ -289,7 +309,7 @@ class _Conv1x1(torch.autograd.Function):
                                                      [False, True, False])[1].to(ctx.wdtype)
         elif ctx.needs_input_grad[1]:
             dw = torch.empty(w.shape, dtype=torch.float32, device=w.device)
-            native().conv1x1_wgrad(dy, x, dw.view(w.shape[0], w.shape[1]), x.shape[2], x.shape[3], s)
+            _conv_wgrad(dy, x, dw, 1, 1, s, 0)
             if ctx.wdtype != torch.float32:
                 dw = dw.to(ctx.wdtype)
         if own_dx:
@@ -444,7 +464,7 @@ class _ConvKxK(torch.autograd.Function):
                                                      [False, True, False])[1].to(ctx.wdtype)
         elif ctx.needs_input_grad[1]:
             dw = torch.empty(w.shape, dtype=torch.float32, device=w.device, memory_format=torch.channels_last)
-            native().conv_wgrad(dy, x, dw, w.shape[2], w.shape[3], s, p)
+            _conv_wgrad(dy, x, dw, w.shape[2], w.shape[3], s, p)
             if ctx.wdtype != torch.float32:
                 dw = dw.to(ctx.wdtype)
         return dx, dw, None, None, None, None

@@ -121,3 +121,29 @@ def test_tuner_picks_and_caches():
     assert len(keys) == 1 and part.shape[:2] == (2, 512)
     ref = F.conv2d(x.float(), w.float().view(512, 256, 1, 1))
     torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("cin,cout,k,h,stride", [(64, 256, 1, 14, 1), (256, 64, 1, 13, 1), (512, 256, 1, 15, 2),
+                                                 (128, 128, 3, 14, 1), (256, 256, 3, 15, 2), (64, 64, 3, 9, 1)])
+def test_gemm2_wgrad_bitwise_first_core(cin, cout, k, h, stride):
+    """Same split-M slabs and per-slab accumulation order as gemm.hip's kernel: bit-identical."""
+    n = 3
+    pad = k // 2
+    x = _x(n, cin, h, 5)
+    ho = (h + 2 * pad - k) // stride + 1
+    dy = _x(n, cout, ho, 6)
+    if k == 1:
+        d1 = torch.empty(cout, cin, device=DEV)
+        d2 = torch.full_like(d1, 9.0)
+        C().conv1x1_wgrad(dy, x, d1, h, h, stride)
+    else:
+        d1 = torch.empty(cout, cin, k, k, device=DEV).contiguous(memory_format=CL)
+        d2 = torch.full_like(d1, 9.0)
+        C().conv_wgrad(dy, x, d1, k, k, stride, pad)
+    C().gemm2_wgrad(dy, x, d2, k, k, stride, pad, h, h)
+    torch.cuda.synchronize()
+    assert torch.equal(d1, d2)
+    ref = torch.ops.aten.convolution_backward(dy.float(), x.float(), d1.view(cout, cin, k, k).float(), None,
+                                              [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
+                                              [False, True, False])[1]
+    torch.testing.assert_close(d2.view(cout, cin, k, k), ref, rtol=1e-3, atol=1e-2)
