@@ -400,7 +400,8 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 template <int TW>
 __device__ __forceinline__ int wswz(int row) {  // chunk XOR of a [rows][TW x bf16] tile row
-  return TW == 128 ? (((row & 3) << 2) | ((row >> 2) & 3)) : (((row & 3) << 1) | ((row >> 2) & 1));
+  // (a 256-wide row spans two 256-byte bank rows: the XOR acts on the chunk within a bank row)
+  return TW >= 128 ? (((row & 3) << 2) | ((row >> 2) & 3)) : (((row & 3) << 1) | ((row >> 2) & 1));
 }
 
 template <int TW>
@@ -419,13 +420,18 @@ __device__ __forceinline__ bf16x8 tr_frag2(const uint8_t* tile, int row0, int co
 
 constexpr int kWM = 64;  // m rows per stage
 
-template <int TN, int TK>
-__global__ __launch_bounds__(256) void k_wgrad(WArgs g) {
+// TN x TK output tile on WN x WK waves (each (TN/WN) x (TK/WK) of 16x16 accumulators)
+template <int TN, int TK, int WN, int WK>
+__global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
+  constexpr int NW = WN * WK;
   constexpr int YT = kWM * TN * 2, XT = kWM * TK * 2;  // bytes per staged tile
   constexpr int CY = TN / 8, CX = TK / 8;             // 16-byte chunks per staged row
-  constexpr int RY = 64 / CY, RX = 64 / CX;           // rows per wave-instruction (1 KB)
-  constexpr int IY = kWM / RY / 4, IX = kWM / RX / 4; // wave-instructions per stage per wave
-  constexpr int FN = TN / 32, FK = TK / 32;
+  constexpr int RY = 64 / CY > 0 ? 64 / CY : 1;       // rows per wave-instruction (1 KB)
+  constexpr int RX = 64 / CX > 0 ? 64 / CX : 1;
+  constexpr int IY = kWM / RY / NW, IX = kWM / RX / NW;  // wave-instructions per stage per wave
+  constexpr int WTN = TN / WN, WTK = TK / WK;
+  constexpr int FN = WTN / 16, FK = WTK / 16;
+  static_assert(CY <= 64 && CX <= 64 && IY >= 1 && IX >= 1, "wgrad tile");
   __shared__ __attribute__((aligned(16))) uint8_t lds[2 * (YT + XT)];
   const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
@@ -435,7 +441,7 @@ __global__ __launch_bounds__(256) void k_wgrad(WArgs g) {
   const int mbeg = sidx * g.chunk, mend = min(g.M, mbeg + g.chunk);
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wn = w >> 1, wk = w & 1;
+  const int wn = w / WK, wk = w - (w / WK) * WK;
   const int tap = k0 / g.Cin, c0 = k0 - tap * g.Cin;
   const int kr = tap / g.KW, kc = tap - kr * g.KW;
   const bool direct = g.KW == 1 && g.pad == 0 && g.stride == 1 && g.Cin == g.K;
@@ -448,15 +454,15 @@ __global__ __launch_bounds__(256) void k_wgrad(WArgs g) {
     const int mb = mbeg + st * kWM;
 #pragma unroll
     for (int i = 0; i < IY; ++i) {
-      const int row = (i * 4 + w) * RY + ry;
+      const int row = (i * NW + w) * RY + ry;
       const int m = mb + row;
       const int ch = sy ^ wswz<TN>(row);
       const uint16_t* p = m < mend ? g.dY + (int64_t)m * g.N + n0 + ch * 8 : kZero16;
-      glds16(p, ty + (i * 4 + w) * 1024);
+      glds16(p, ty + (i * NW + w) * 1024);
     }
 #pragma unroll
     for (int i = 0; i < IX; ++i) {
-      const int row = (i * 4 + w) * RX + rx;
+      const int row = (i * NW + w) * RX + rx;
       const int m = mb + row;
       const int ch = sx ^ wswz<TK>(row);
       const uint16_t* p = kZero16;
@@ -471,7 +477,7 @@ __global__ __launch_bounds__(256) void k_wgrad(WArgs g) {
             p = g.X + (((int64_t)img * g.Hi + hi) * g.Wi + wi) * g.Cin + c0 + ch * 8;
         }
       }
-      glds16(p, tx + (i * 4 + w) * 1024);
+      glds16(p, tx + (i * NW + w) * 1024);
     }
   };
 
@@ -495,9 +501,9 @@ __global__ __launch_bounds__(256) void k_wgrad(WArgs g) {
     for (int ks = 0; ks < kWM / 32; ++ks) {
       bf16x8 a[FN], b[FK];
 #pragma unroll
-      for (int i = 0; i < FN; ++i) a[i] = tr_frag2<TN>(ty, ks * 32, wn * (TN / 2) + i * 16, lane);
+      for (int i = 0; i < FN; ++i) a[i] = tr_frag2<TN>(ty, ks * 32, wn * WTN + i * 16, lane);
 #pragma unroll
-      for (int j = 0; j < FK; ++j) b[j] = tr_frag2<TK>(tx, ks * 32, wk * (TK / 2) + j * 16, lane);
+      for (int j = 0; j < FK; ++j) b[j] = tr_frag2<TK>(tx, ks * 32, wk * WTK + j * 16, lane);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FN; ++i)
@@ -512,10 +518,10 @@ __global__ __launch_bounds__(256) void k_wgrad(WArgs g) {
   for (int i = 0; i < FN; ++i)
 #pragma unroll
     for (int j = 0; j < FK; ++j) {
-      const int k = k0 + wk * (TK / 2) + j * 16 + (lane & 15);
+      const int k = k0 + wk * WTK + j * 16 + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int n = n0 + wn * (TN / 2) + i * 16 + (lane >> 4) * 4 + r;
+        const int n = n0 + wn * WTN + i * 16 + (lane >> 4) * 4 + r;
         out[(int64_t)n * g.K + k] = acc[i][j][r];
       }
     }
@@ -667,7 +673,7 @@ void wgrad_reduce_slabs(const at::Tensor& part, int64_t S, int64_t N, int64_t K,
 // bf16; dw f32 [Cout, KH, KW, Cin] in memory (the channels-last weight layout; 1x1: [Cout, Cin]).
 // Cout % 64 == 0, Cin % 64 == 0.  S split-M partial slabs (~2 resident blocks per CU) + fixed-order sum.
 void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
-                 int64_t Hi, int64_t Wi) {
+                 int64_t Hi, int64_t Wi, int64_t cfg) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dw.is_cuda(), "gemm2_wgrad: device tensors");
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 && dw.scalar_type() == at::kFloat,
               "gemm2_wgrad: bf16 dy/x, f32 dw");
@@ -684,9 +690,19 @@ void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t
   for (const at::Tensor* t : {&x, &dy, &dw})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm2_wgrad: 16-byte aligned tensors");
   TORCH_CHECK(M < (int64_t(1) << 31) && x.numel() < (int64_t(1) << 40), "gemm2_wgrad: size");
-  const int TN = N % 128 == 0 ? 128 : 64, TK = Cin % 128 == 0 ? 128 : 64;
+  // cfg 0: 128|64 x 128|64 tile on 4 waves (64x64 each: the first core's tiling and slab split);
+  // 1: 256 x 128 on 4 waves of 128x64; 2: 256 x 256 on 8 waves of 128x64 (a third of the LDS
+  // bytes per MFMA of cfg 0: the transposing-read wgrad is LDS-bandwidth bound)
+  int TN = N % 128 == 0 ? 128 : 64, TK = Cin % 128 == 0 ? 128 : 64;
+  if (cfg == 1) {
+    TORCH_CHECK(N % 256 == 0 && Cin % 128 == 0, "gemm2_wgrad cfg 1 needs Cout % 256, Cin % 128");
+    TN = 256; TK = 128;
+  } else if (cfg == 2) {
+    TORCH_CHECK(N % 256 == 0 && Cin % 256 == 0, "gemm2_wgrad cfg 2 needs Cout % 256, Cin % 256");
+    TN = 256; TK = 256;
+  }
   const int64_t tn = N / TN, tk = K / TK, tiles = tn * tk;
-  const int64_t resident = 256 * (TN * TK == 128 * 128 ? 2 : TN * TK == 128 * 64 ? 3 : 5);
+  const int64_t resident = 256 * (cfg ? 1 : TN * TK == 128 * 128 ? 2 : TN * TK == 128 * 64 ? 3 : 5);
   int64_t S = std::max<int64_t>(1, resident / tiles);
   S = std::min<int64_t>(S, std::max<int64_t>(1, M / (8 * g2::kWM)));           // >= 8 stages per block
   S = std::min<int64_t>(S, std::max<int64_t>(1, M * (N + K) / (4 * N * K)));  // slabs <= operand bytes
@@ -705,10 +721,12 @@ void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t
   a.fd_hw = g2::make_fastdiv2((uint32_t)(Ho * Wo));
   a.fd_w = g2::make_fastdiv2((uint32_t)Wo);
   const int grid = (int)(S * tiles);
-  if (TN == 128 && TK == 128) hipLaunchKernelGGL((g2::k_wgrad<128, 128>), grid, 256, 0, stream, a);
-  else if (TN == 128) hipLaunchKernelGGL((g2::k_wgrad<128, 64>), grid, 256, 0, stream, a);
-  else if (TK == 128) hipLaunchKernelGGL((g2::k_wgrad<64, 128>), grid, 256, 0, stream, a);
-  else hipLaunchKernelGGL((g2::k_wgrad<64, 64>), grid, 256, 0, stream, a);
+  if (cfg == 2) hipLaunchKernelGGL((g2::k_wgrad<256, 256, 2, 4>), grid, 512, 0, stream, a);
+  else if (cfg == 1) hipLaunchKernelGGL((g2::k_wgrad<256, 128, 2, 2>), grid, 256, 0, stream, a);
+  else if (TN == 128 && TK == 128) hipLaunchKernelGGL((g2::k_wgrad<128, 128, 2, 2>), grid, 256, 0, stream, a);
+  else if (TN == 128) hipLaunchKernelGGL((g2::k_wgrad<128, 64, 2, 2>), grid, 256, 0, stream, a);
+  else if (TK == 128) hipLaunchKernelGGL((g2::k_wgrad<64, 128, 2, 2>), grid, 256, 0, stream, a);
+  else hipLaunchKernelGGL((g2::k_wgrad<64, 64, 2, 2>), grid, 256, 0, stream, a);
   if (S > 1) {
     at::Tensor dwv = dw;
     wgrad_reduce_slabs(part, S, N, K, dwv, stream);

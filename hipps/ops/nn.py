@@ -139,10 +139,13 @@ def _conv_wgrad(dy, x, dw, kh, kw, stride, pad):
         first = lambda: C.conv_wgrad(dy, x, dw, kh, kw, stride, pad)  # noqa: E731
     name = "w2"
     if _GEMM2 and cout % 64 == 0 and cin % 64 == 0:
-        cands = {"w2": first, "w3": lambda: C.gemm2_wgrad(dy, x, dw, kh, kw, stride, pad, hi, wi)}
+        cands = {"w2": first}
+        for cfg in (0, 1, 2):  # gemm2.hip k_wgrad tilings: 128x128 / 256x128 / 256x256 outputs
+            if cfg == 0 or (cout % 256 == 0 and cin % (128 * cfg) == 0):
+                cands[f"w3_{cfg}"] = (lambda cfg=cfg: C.gemm2_wgrad(dy, x, dw, kh, kw, stride, pad, hi, wi, cfg))
         name = TUNER.pick(("wgrad", tuple(x.shape), cout, kh, kw, stride, pad), cands)
-    if name == "w3":
-        C.gemm2_wgrad(dy, x, dw, kh, kw, stride, pad, hi, wi)
+    if name.startswith("w3"):
+        C.gemm2_wgrad(dy, x, dw, kh, kw, stride, pad, hi, wi, int(name[3:]))
     else:
         first()
 

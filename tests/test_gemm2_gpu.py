@@ -147,3 +147,22 @@ def test_gemm2_wgrad_bitwise_first_core(cin, cout, k, h, stride):
                                               [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
                                               [False, True, False])[1]
     torch.testing.assert_close(d2.view(cout, cin, k, k), ref, rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("cfg", [1, 2])
+@pytest.mark.parametrize("cin,cout,k,h,stride", [(256, 256, 1, 14, 1), (512, 512, 3, 7, 1), (256, 512, 3, 15, 2)])
+def test_gemm2_wgrad_wide_tiles(cfg, cin, cout, k, h, stride):
+    """256 x 128 / 256 x 256 output tiles (other slab split: fp32-close, not bitwise)."""
+    if cfg == 2 and cin % 256:
+        pytest.skip("tile")
+    n = 2
+    pad = k // 2
+    x = _x(n, cin, h, 7)
+    ho = (h + 2 * pad - k) // stride + 1
+    dy = _x(n, cout, ho, 8)
+    d0 = torch.empty(cout, cin, k, k, device=DEV).contiguous(memory_format=CL)
+    d1 = torch.full_like(d0, 9.0)
+    C().gemm2_wgrad(dy, x, d0, k, k, stride, pad, h, h, 0)
+    C().gemm2_wgrad(dy, x, d1, k, k, stride, pad, h, h, cfg)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(d1, d0, rtol=1e-5, atol=1e-4)
