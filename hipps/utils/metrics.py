@@ -1,8 +1,11 @@
 """Per-step metrics (reference: the ``data`` dict returned by ps.py:step, ps.py:116-191).
 
 Reference keys kept: comm_wait, optim_step_time, decode_time, msg_bytes, packaged_bytes,
-code_wait, iallgather_prepare_time, isend_time.  Added: grad_bytes_sent/recv, staleness,
-version, step_time.  ``MetricsWriter`` appends one JSON line per step per rank.
+code_wait, iallgather_prepare_time, isend_time.  Added: grad_bytes_sent/recv, version, step_time,
+``staleness`` (async workers: PS updates between the version a worker's newest consumed gradient
+was computed on and the update that applied it, read from the control block's LAST_STALE word,
+``PSAsyncEngine.step`` in ps_async.py) and ``samples_per_sec`` (every mode, when ``samples_per_step`` is
+configured; optim.py ``step``).  ``MetricsWriter`` appends one JSON line per step per rank.
 """
 from __future__ import annotations
 
