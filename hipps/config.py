@@ -50,6 +50,12 @@ class PSConfig:
     # as M messages for it arrived, workers adopt the newest version of each bucket -- reads may
     # mix versions across buckets; ipc transport only)
     ps_granularity: str = "model"
+    # async PS: push each bucket's message from its backward hook as soon as it is encoded
+    # ('auto' = on for the ipc transport), instead of all messages at step(): the PS accumulates
+    # (and with ps_granularity='bucket' updates and publishes) the last layers' buckets while the
+    # worker still runs backward.  A gradient arriving later for a pushed bucket (backward()
+    # twice before step() without opt.no_sync()) is an error.  'auto' | 'on' | 'off'
+    push_early: str = "auto"
     # async PS: scale a kept gradient by 1/max(1, staleness) (staleness-aware async SGD)
     staleness_lr: bool = False
     # async PS look-ahead publish (delay-compensated momentum): workers read the parameters
@@ -159,6 +165,8 @@ class PSConfig:
             raise ValueError("async_transport must be 'ipc' or 'p2p'")
         if self.transport not in ("torch", "rccl"):
             raise ValueError("transport must be 'torch' or 'rccl'")
+        if self.push_early not in ("auto", "on", "off"):
+            raise ValueError("push_early must be 'auto', 'on' or 'off'")
         if self.ps_granularity not in ("model", "bucket"):
             raise ValueError("ps_granularity must be 'model' or 'bucket'")
         if self.adam_variant not in ("reference", "torch"):

@@ -788,6 +788,127 @@ void launch_scan_write(hipStream_t stream, const float* src, float* rp, int64_t 
   hipLaunchKernelGGL(k_write_regions<VT>, (int)w.g.nreg, kBlock, 0, stream, src, rp, n, w.st, w.R, idx, val, cap);
 }
 
+// ------------------------------------------------------------------------------------------
+// Small buckets (n <= kSmallMax, e.g. the reference notebook's n = 10 .. 10^4): ONE launch of one
+// 1024-thread workgroup.  The folded values live in LDS (128 KB at n = 32768); the radix select
+// runs its three digit passes (bits 30..20, 19..9, 8..0 of |x|) as LDS-atomic histograms (two
+// copies, even / odd waves, for the clustered exponent digit) and picks each digit with a block
+// suffix scan (every thread owns two bins).  Then each thread owns a contiguous index range of
+// ODD length (so the 64 lanes of a wave start in 64 different LDS banks), counts keys > T and
+// == T, two block scans give its tie admission (lowest index first) and its output offset, it
+// writes its selected (index, value) pairs in index order and leaves each element's residual in
+// LDS, and a last coalesced loop stores the residuals.  The multi-pass path above costs ~12
+// launches, which dominates at these sizes.
+constexpr int kSmallMax = 32768;
+constexpr int kSmallThreads = 1024;
+
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  if (wv == 0) {
+    uint32_t s = lane < kSmallThreads / 64 ? wsum[lane] : 0u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(s, o, 64);
+      if (lane >= o) s += y;
+    }
+    if (lane < kSmallThreads / 64) wsum[lane] = s;  // inclusive wave totals
+  }
+  __syncthreads();
+  total = wsum[kSmallThreads / 64 - 1];
+  const uint32_t before = wv ? wsum[wv - 1] : 0u;
+  __syncthreads();  // wsum is reused by the next scan
+  return before + x - v;
+}
+
+template <typename VT>
+__global__ __launch_bounds__(kSmallThreads) void k_topk_small(const float* __restrict__ g, float* __restrict__ resid,
+                                                             int n, int k, int32_t* __restrict__ idx,
+                                                             VT* __restrict__ val) {
+  __shared__ float sv[kSmallMax];
+  __shared__ uint32_t hist[2][kHistBins];
+  __shared__ uint32_t wsum[64];
+  __shared__ uint32_t sel[2];  // chosen bin, keys above it
+  const int t = threadIdx.x, wv = t >> 6;
+  for (int i = t; i < n; i += kSmallThreads) sv[i] = g[i] + (resid ? resid[i] : 0.f);
+  uint32_t prefix = 0, pmask = 0, rem = (uint32_t)k;
+#pragma unroll
+  for (int pass = 0; pass < 3; ++pass) {
+    const int sh = pass == 0 ? 20 : pass == 1 ? 9 : 0, nb = pass == 2 ? 512 : 2048;
+    for (int b = t; b < 2 * kHistBins; b += kSmallThreads) (&hist[0][0])[b] = 0u;
+    __syncthreads();
+    uint32_t* h = hist[pass == 0 ? (wv & 1) : 0];
+    for (int i = t; i < n; i += kSmallThreads) {
+      const uint32_t key = __float_as_uint(sv[i]) & 0x7fffffffu;
+      if ((key & pmask) == prefix) atomicAdd(&h[(key >> sh) & (nb - 1)], 1u);
+    }
+    __syncthreads();
+    // thread t owns bins hi = nb-1-2t and lo = nb-2-2t (t < nb/2); exclusive scan from the top
+    const int bh = nb - 1 - 2 * t, bl = bh - 1;
+    uint32_t ch = 0, cl = 0;
+    if (bl >= 0) {
+      ch = hist[0][bh] + hist[1][bh];
+      cl = hist[0][bl] + hist[1][bl];
+    }
+    uint32_t tot;
+    const uint32_t above = block_excl_scan(ch + cl, wsum, tot);
+    if (above < rem && above + ch + cl >= rem) {  // exactly one thread holds the rem-th key
+      if (above + ch >= rem) {
+        sel[0] = (uint32_t)bh;
+        sel[1] = above;
+      } else {
+        sel[0] = (uint32_t)bl;
+        sel[1] = above + ch;
+      }
+    }
+    __syncthreads();
+    prefix |= sel[0] << sh;
+    pmask |= (uint32_t)(nb - 1) << sh;
+    rem -= sel[1];
+  }
+  // prefix = T (the k-th largest key); admit rem keys == T, lowest index first
+  const uint32_t T = prefix;
+  const int per = ((n + kSmallThreads - 1) / kSmallThreads) | 1;  // odd: bank-conflict-free LDS walks
+  const int lo = min(n, t * per), hi = min(n, lo + per);
+  uint32_t gt = 0, eq = 0;
+  for (int i = lo; i < hi; ++i) {
+    const uint32_t key = __float_as_uint(sv[i]) & 0x7fffffffu;
+    gt += key > T;
+    eq += key == T;
+  }
+  uint32_t tot;
+  const uint32_t eq_before = block_excl_scan(eq, wsum, tot);
+  const uint32_t adm = eq_before >= rem ? 0u : min(eq, rem - eq_before);
+  const uint32_t off = block_excl_scan(gt + adm, wsum, tot);
+  uint32_t o = off, taken = 0;
+  for (int i = lo; i < hi; ++i) {
+    const float v = sv[i];
+    const uint32_t key = __float_as_uint(v) & 0x7fffffffu;
+    bool take = key > T;
+    if (key == T && taken < adm) {
+      take = true;
+      ++taken;
+    }
+    if (take) {
+      idx[o] = i;
+      Vec4<VT>::store1(val, o, v);
+      sv[i] = v - Vec4<VT>::load1(val, o);  // what the wire dropped (bf16 rounding), fed back
+      ++o;
+    }
+  }
+  if (resid) {
+    __syncthreads();
+    for (int i = t; i < n; i += kSmallThreads) resid[i] = sv[i];
+  }
+}
+
 }  // namespace
 
 void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::Tensor idx, at::Tensor val,
@@ -808,6 +929,15 @@ void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::T
     rp = resid->data_ptr<float>();
   }
   auto stream = c10::hip::getCurrentHIPStream();
+  if (n <= kSmallMax) {  // one workgroup, one launch
+    if (val.scalar_type() == at::kFloat)
+      hipLaunchKernelGGL(k_topk_small<float>, 1, kSmallThreads, 0, stream, g.data_ptr<float>(), rp, (int)n, (int)k,
+                         idx.data_ptr<int32_t>(), val.data_ptr<float>());
+    else
+      hipLaunchKernelGGL(k_topk_small<uint16_t>, 1, kSmallThreads, 0, stream, g.data_ptr<float>(), rp, (int)n,
+                         (int)k, idx.data_ptr<int32_t>(), (uint16_t*)val.data_ptr());
+    return;
+  }
   const int nreg = (int)w.g.nreg;
   TORCH_CHECK(w.g.cpw <= kMaxCpw, "bucket too large for the region geometry");
   hipLaunchKernelGGL(k_sel_init, 1, kBlock, 0, stream, w.st, 0u, 0u, (uint32_t)k, (uint32_t)w.g.capw,

@@ -172,10 +172,22 @@ def _convkxk_gemm(x, w, stride, pad, stats: bool):
         C.gemm2_conv(x, w, y, part, None, None, h, wd, stride, k, k, pad, bm, bn)
         return y, part
 
+    def timed(name):
+        # what the choice costs the step: with ``stats`` MIOpen leaves the following BN a
+        # statistics pass over y (reduce + finalize), the GEMM leaves it a finalize of its partials
+        yy, part = run(name)
+        if stats:
+            v = [torch.empty(cout, dtype=torch.float32, device=x.device) for _ in range(6)]
+            if part is None:
+                C.bn_forward_stats(yy, v[0], v[1], None, None, v[2], v[3], v[4], v[5], cout, 1e-5, 0.1)
+            else:
+                C.bn_finalize_partials(part, part.shape[2], n * ho * wo, v[0], v[1], None, None, v[2], v[3], v[4],
+                                       v[5], cout, 1e-5, 0.1)
+
     name = "miopen"
     if _GEMM2 and cin % 64 == 0 and cout % 64 == 0:
         name = TUNER.pick(("kxk", n, cin, h, wd, cout, k, stride, pad, stats),
-                          {nm: (lambda nm=nm: run(nm)) for nm in ["miopen"] + _g2_names(cout)})
+                          {nm: (lambda nm=nm: timed(nm)) for nm in ["miopen"] + _g2_names(cout)})
     return run(name)
 
 

@@ -41,7 +41,7 @@ import secrets
 import threading
 import time
 import traceback
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -104,6 +104,53 @@ class _Pending:
             w.wait()
 
 
+class _LatencyProbe:
+    """``HIPPS_PS_LATENCY=1`` with the PS co-located on rank 0: GPU time from the local worker's
+    push doorbell of a bucket message (event on the comm stream) to the event on the PS stream
+    after the publish that first includes it (whole-model update, or that bucket's update under
+    ``ps_granularity='bucket'``).  Reported by ps_stats() as push_to_publish_us_{mean,p50,max}."""
+
+    def __init__(self, cap: int = 1024):
+        self.lock = threading.Lock()
+        self.push: Dict[int, torch.cuda.Event] = {}
+        self.noted: Dict[int, List[int]] = {}
+        self.pairs: list = []
+        self.cap = cap
+
+    def pushed(self, seq: int, stream):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(stream)
+        with self.lock:
+            self.push[seq] = ev
+            if len(self.push) > self.cap:  # a message whose publish was never seen (dropped)
+                del self.push[min(self.push)]
+
+    def note(self, bi: int, seq: int):
+        with self.lock:
+            self.noted.setdefault(bi, []).append(seq)
+
+    def published(self, bi: Optional[int], stream):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(stream)
+        with self.lock:
+            for b in (list(self.noted) if bi is None else [bi]):
+                for q in self.noted.pop(b, []):
+                    pe = self.push.pop(q, None)
+                    if pe is not None:
+                        self.pairs.append((pe, ev))
+            del self.pairs[:-self.cap]
+
+    def summary(self) -> dict:
+        with self.lock:
+            pairs = list(self.pairs)
+        if not pairs:
+            return {}
+        pairs[-1][1].synchronize()
+        us = sorted(p.elapsed_time(e) * 1e3 for p, e in pairs)
+        return {"push_to_publish_us_mean": sum(us) / len(us), "push_to_publish_us_p50": us[len(us) // 2],
+                "push_to_publish_us_max": us[-1], "push_to_publish_n": len(us)}
+
+
 class PSAsyncEngine(Engine):
     name = "ps_async"
 
@@ -161,9 +208,9 @@ class PSAsyncEngine(Engine):
         # 'p2p': the mailbox stays private to the PS and data moves by two-sided send/recv
         # (torch.distributed isend/irecv: RCCL pair communicators on GPU, gloo on CPU)
         self.p2p = cfg.async_transport == "p2p" and W > 1
-        if self.bucketwise and (self.p2p or self.nb > C.ControlBlock.MAX_BUCKETS or self.emu):
-            raise ValueError("ps_granularity='bucket' needs the ipc transport, at most "
-                             f"{C.ControlBlock.MAX_BUCKETS} buckets and no emulate_remote")
+        if self.bucketwise and (self.p2p or self.nb > C.ControlBlock.MAX_BUCKETS):
+            raise ValueError("ps_granularity='bucket' needs the ipc transport and at most "
+                             f"{C.ControlBlock.MAX_BUCKETS} buckets")
         # p2p: gradients and parameters travel on two process groups of their own.  Each group has
         # its own RCCL communicators and streams, so (a) a posted gradient receive can never sit
         # in front of a parameter send on the same pair channel (ops of one channel complete in
@@ -250,6 +297,13 @@ class PSAsyncEngine(Engine):
         self.step_no = 0
         self.local_ver = -1
         self._stats = {"drops": 0, "staleness_sum": 0, "accumulated": 0, "reader_waits": 0}
+        # push_early: push each bucket's message from its backward hook (see encode_bucket)
+        pe = cfg.push_early
+        self._early = pe != "off" and not self.p2p and cfg.overlap and not self.is_object \
+            and self._fault is None and not self.plan.guarded and not self.ps_only
+        self._npushed, self._push_wait, self._in_encode_all = 0, 0.0, False
+        self._lat = (_LatencyProbe() if self.cuda and self.rank == 0 and not self.dedicated
+                     and os.environ.get("HIPPS_PS_LATENCY", "0") == "1" else None)
         self._err: Optional[str] = None
         self._thread = None
         self._pause_req = threading.Event()
@@ -539,6 +593,8 @@ class PSAsyncEngine(Engine):
         if self.plan.guarded:
             self._verify_slot(i, slot, bi, seq)
         self._pend.append((bi, scale, self._bucket_msg(bi, self.slot_buf(i, slot))))
+        if self._lat is not None and i == 0:
+            self._lat.note(bi, seq)
         for _ in range(self.emu):  # emulated remote workers: the same bytes, one launch each
             self._pend.append((bi, scale, None))
 
@@ -621,6 +677,10 @@ class PSAsyncEngine(Engine):
         words += [(C.F_INCL_SEQ, i, s) for i, s in incl.items()]
         for j in range(0, len(words), 6):
             self._ring(self.ps_stream, words[j:j + 6])
+        if self._lat is not None:
+            self._lat.published(bi, self.ps_stream)
+        if self.emu:
+            self._emulate_remote_traffic(k, bi)
         if gver is not None:
             self.ctl.fetch_add(C.F_UPDATES, 0, 1)
         self._stats["bucket_updates"] = self._stats.get("bucket_updates", 0) + 1
@@ -682,21 +742,27 @@ class PSAsyncEngine(Engine):
                                                                            for i, s in last.items()]
         for k in range(0, len(words), 6):
             self._ring(st, words[k:k + 6])
+        if self._lat is not None:
+            self._lat.published(None, st)
         if self.emu:
             self._emulate_remote_traffic(b)
         self.ctl.fetch_add(C.F_UPDATES, 0, 1)
 
-    def _emulate_remote_traffic(self, b: int):
+    def _emulate_remote_traffic(self, b: int, bi: Optional[int] = None):
         """cfg.emulate_remote: E remote workers' pushes (write sweeps of one step's wire bytes)
-        and pulls (read sweeps of the new publish buffer) after this update."""
+        and pulls (read sweeps of the new publish buffer) after this update (bucket granularity:
+        of bucket ``bi``'s message and publish range)."""
         st = self._emu_stream
         ctx = torch.cuda.stream(st) if st is not None else contextlib.nullcontext()
         if st is not None:
             st.wait_stream(self.ps_stream)
         with ctx:
-            pub = self.pub_buf(b)
+            pub, win = self.pub_buf(b), self._emu_in
+            if bi is not None:
+                bk = self.plan.buckets[bi]
+                pub, win = pub[bk.lo:bk.hi], self.plan.message(self._emu_in, bi)
             for e in range(self.emu):
-                self._emu_in.fill_(e)
+                win.fill_(e)
                 torch.amax(pub, dim=0, out=self._emu_sink[e])
 
     def lookahead_tau(self) -> float:
@@ -750,64 +816,106 @@ class PSAsyncEngine(Engine):
         self.close()
         return self.ps_stats()
 
+    def _push_one(self, pos: int, bi: int, partial: int) -> float:
+        """Push message ``pos`` of this step (bucket ``bi``) into the next mailbox slot: copy on the
+        comm stream (after the bucket's encode), then the GPU doorbell with its version / presence /
+        sequence words.  Returns the host seconds spent waiting for a free slot."""
+        C = self.C
+        t_wait = 0.0
+        step = self.step_no + 1
+        ver_src = []
+        if self.pull_mode == "device":  # the version the GPU adopted before this step's forward
+            ver_src = [self._sel[2 + step % RING:].data_ptr(), 0, 0]
+        self.seq += 1
+        s = self.seq
+        slot = s % self.SLOTS
+        if s > self.SLOTS:  # slot reuse: message s - SLOTS must have been consumed
+            tw = time.perf_counter()
+            if not self.ctl.wait_ge(C.F_ACK_SEQ, self.rank, s - self.SLOTS, self.timeout_us):
+                self._check_error()
+                raise TimeoutError(f"rank {self.rank}: PS did not consume message {s - self.SLOTS}")
+            t_wait += time.perf_counter() - tw
+        b = self.plan.buckets[bi]
+        src = self.plan.message(self.wire, bi)  # layout (+ canary guard in debug_canary)
+        vidx = self.rank * self.MAXSLOTS + slot
+        last = pos == self.nb - 1 or self.bucketwise  # bucket mode: every message carries presence
+        if self.p2p and self.rank != 0:
+            self._push_p2p(src, s, vidx, last and partial)
+            return t_wait
+        sbuf = self.slot_buf(self.rank, slot)
+        dst = sbuf[: b.msg_nbytes]
+        words = [(C.F_PUSH_VER, vidx, self.local_ver), (C.F_PUSH_FLAG, vidx, partial if last else 0),
+                 (C.F_PUSH_SEQ, self.rank, s)]
+        if self.cuda:
+            cs = self.comm_stream
+            with torch.cuda.stream(cs), self.tracer.phase("push", cs):
+                # variable-size codes (threshold) move 16 + count * entry bytes, not capacity
+                if self.plan.guarded or not self.codec.push_copy(b.layout, src, dst):
+                    dst.copy_(src, non_blocking=True)
+                if last and partial:
+                    ns = len(self.store.slots)
+                    sbuf[self.slot_pres:self.slot_pres + ns].copy_(self.presence_tensor(), non_blocking=True)
+            self._ring(cs, words, ver_src)
+            if self._lat is not None:
+                self._lat.pushed(s, cs)
+        else:
+            dst.copy_(src)
+            if last and partial:
+                ns = len(self.store.slots)
+                sbuf[self.slot_pres:self.slot_pres + ns].copy_(self.presence_tensor())
+            self._ring(None, words)
+        return t_wait
+
+    def encode_bucket(self, bi: int):
+        """Hook-time encode; with push_early the encoded prefix of this step's messages (in
+        message order) is pushed right away, during backward: the PS accumulates -- and under
+        ps_granularity='bucket' updates and publishes -- the last layers' buckets while the
+        worker is still computing the first layers' gradients."""
+        super().encode_bucket(bi)
+        if not self._early or self._in_encode_all:
+            return
+        while self._npushed < self.nb:
+            b = self.order[self._npushed]
+            if not self._encoded[b] or self._bucket_count[b] != len(self.plan.buckets[b].slot_ids):
+                return
+            # every parameter of an early-pushed bucket has its gradient: no presence mask
+            self._push_wait += self._push_one(self._npushed, b, 0)
+            self._npushed += 1
+
+    def encode_all(self):
+        self._in_encode_all = True
+        try:
+            return super().encode_all()
+        finally:
+            self._in_encode_all = False
+
     def step(self):
         if self.ps_only:
             raise RuntimeError("rank 0 is a dedicated parameter server (ps_dedicated=True): it does not train; "
                                "call opt.serve() there")
         C = self.C
         data = {}
+        early = self._npushed
+        if early and any(self.order[p] in self._late for p in range(early)):
+            self._npushed = 0
+            raise RuntimeError("a gradient arrived for a bucket that was already pushed to the PS during backward "
+                               "(backward() called twice before step()): wrap the earlier micro-batches in "
+                               "opt.no_sync(), or set push_early='off'")
         data["code_wait"] = self.encode_all()
         self.verify_guards([self.wire], "encode")
         self._check_error()
         if self._fault is not None and self._inject(data):
             return data
         self.ctl.heartbeat(self.rank)
-        t_wait = 0.0
         t = time.perf_counter()
         if self.cuda:
             self.enc_event.record(self.comm_stream)
-        step = self.step_no + 1
         partial = 0 if (self.step_all_present or not self.cfg.skip_missing_grads) else 1
-        ver_src = []
-        if self.pull_mode == "device":  # the version the GPU adopted before this step's forward
-            ver_src = [self._sel[2 + step % RING:].data_ptr(), 0, 0]
-        for pos, bi in enumerate(self.order):
-            self.seq += 1
-            s = self.seq
-            slot = s % self.SLOTS
-            if s > self.SLOTS:  # slot reuse: message s - SLOTS must have been consumed
-                tw = time.perf_counter()
-                if not self.ctl.wait_ge(C.F_ACK_SEQ, self.rank, s - self.SLOTS, self.timeout_us):
-                    self._check_error()
-                    raise TimeoutError(f"rank {self.rank}: PS did not consume message {s - self.SLOTS}")
-                t_wait += time.perf_counter() - tw
-            b = self.plan.buckets[bi]
-            src = self.plan.message(self.wire, bi)  # layout (+ canary guard in debug_canary)
-            vidx = self.rank * self.MAXSLOTS + slot
-            last = pos == self.nb - 1 or self.bucketwise  # bucket mode: every message carries presence
-            if self.p2p and self.rank != 0:
-                self._push_p2p(src, s, vidx, last and partial)
-                continue
-            sbuf = self.slot_buf(self.rank, slot)
-            dst = sbuf[: b.msg_nbytes]
-            words = [(C.F_PUSH_VER, vidx, self.local_ver), (C.F_PUSH_FLAG, vidx, partial if last else 0),
-                     (C.F_PUSH_SEQ, self.rank, s)]
-            if self.cuda:
-                cs = self.comm_stream
-                with torch.cuda.stream(cs), self.tracer.phase("push", cs):
-                    # variable-size codes (threshold) move 16 + count * entry bytes, not capacity
-                    if self.plan.guarded or not self.codec.push_copy(b.layout, src, dst):
-                        dst.copy_(src, non_blocking=True)
-                    if last and partial:
-                        ns = len(self.store.slots)
-                        sbuf[self.slot_pres:self.slot_pres + ns].copy_(self.presence_tensor(), non_blocking=True)
-                self._ring(cs, words, ver_src)
-            else:
-                dst.copy_(src)
-                if last and partial:
-                    ns = len(self.store.slots)
-                    sbuf[self.slot_pres:self.slot_pres + ns].copy_(self.presence_tensor())
-                self._ring(None, words)
+        t_wait = self._push_wait
+        for pos in range(early, self.nb):
+            t_wait += self._push_one(pos, self.order[pos], partial)
+        self._npushed, self._push_wait = 0, 0.0
+        data["pushed_early"] = float(early)
         self.step_no += 1
         data["slot_wait"] = t_wait
         data["isend_time"] = time.perf_counter() - t
@@ -1190,6 +1298,8 @@ class PSAsyncEngine(Engine):
         d = dict(self._stats)
         d["updates"] = self.ctl.load(C.F_UPDATES, 0)
         d["version"] = self.ctl.load(C.F_PUB_VER, 0)
+        if self._lat is not None:
+            d.update(self._lat.summary())
         return d
 
     def transport_info(self) -> dict:

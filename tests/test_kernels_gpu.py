@@ -326,3 +326,26 @@ def test_sgd_lookahead_publish(masked):
                  **kw)
     torch.testing.assert_close(pd.cpu(), p, rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(pub.cpu(), p - 0.09 * buf, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("n,k", [(1, 1), (10, 10), (17, 5), (10_000, 100), (32768, 3277), (32769, 3277)])
+@pytest.mark.parametrize("vdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", ["randn", "ties", "zeros"])
+def test_topk_small_single_workgroup(n, k, vdt, case):
+    """n <= 32768 runs the one-launch LDS radix select (topk.hip k_topk_small): indices, values
+    and the error-feedback residual equal the CPU reference bit for bit (32769 = the multi-pass
+    path, same contract)."""
+    torch.manual_seed(n + k)
+    g = torch.randn(n) if case != "zeros" else torch.zeros(n)
+    if case == "ties":
+        g[::3] = 0.5
+        g[1::7] = -0.5
+    r0 = torch.randn(n) * 0.01 if case != "zeros" else torch.zeros(n)
+    r_cpu, r_dev = r0.clone(), r0.to(DEV)
+    idx, val = torch.empty(k, dtype=torch.int32), torch.empty(k, dtype=vdt)
+    ref.topk_encode(g, r_cpu, k, idx, val)
+    idd, vd = torch.empty(k, dtype=torch.int32, device=DEV), torch.empty(k, dtype=vdt, device=DEV)
+    ops.topk_encode(g.to(DEV), r_dev, k, idd, vd)
+    assert torch.equal(idd.cpu(), idx)
+    assert torch.equal(vd.cpu(), val)
+    assert torch.equal(r_dev.cpu(), r_cpu)

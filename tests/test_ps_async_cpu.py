@@ -268,3 +268,49 @@ def test_async_bucket_granularity_max_delay_zero_matches_model():
     for r in range(2):
         for x, y in zip(a[r]["params"], b[r]["params"]):
             torch.testing.assert_close(x, y, rtol=0, atol=0)
+
+
+def _early(rank, world, steps, push_early, granularity="model", twice=False):
+    import hipps
+
+    m = _mlp()
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", bucket_mb=0.0005,
+                    max_delay=0, accumulate=world, push_early=push_early, ps_granularity=granularity)
+    nb = len(opt.engine.plan.buckets)
+    early = []
+    err = None
+    for s in range(steps):
+        x, y = _data(rank, s % 4)
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x), y).backward()
+        if twice:
+            torch.nn.functional.cross_entropy(m(x), y).backward()
+        try:
+            _, data = opt.step()
+        except RuntimeError as e:
+            err = str(e)
+            break
+        early.append(data["pushed_early"])
+    opt.close()
+    return {"nb": nb, "early": early, "err": err, "params": [p.detach().clone() for p in m.parameters()]}
+
+
+@pytest.mark.parametrize("granularity", ["model", "bucket"])
+def test_async_push_early_during_backward_matches_push_at_step(granularity):
+    """push_early: every bucket's message leaves from its backward hook (all nb of them: every
+    parameter gets a gradient), and with max_delay=0 the parameters are bit-identical to pushing
+    everything at step()."""
+    a = run_world(_early, 2, 5, "on", granularity)
+    b = run_world(_early, 2, 5, "off", granularity)
+    for r in range(2):
+        assert a[r]["nb"] >= 3 and all(e == a[r]["nb"] for e in a[r]["early"]), a[r]["early"]
+        assert all(e == 0 for e in b[r]["early"])
+        for x, y in zip(a[r]["params"], b[r]["params"]):
+            torch.testing.assert_close(x, y, rtol=0, atol=0)
+
+
+def test_async_push_early_rejects_a_late_gradient():
+    """A second backward() before step() adds gradient to buckets already pushed: an error, not a
+    silently dropped gradient (opt.no_sync() or push_early='off' are the ways out)."""
+    out = run_world(_early, 1, 2, "on", "model", True)
+    assert out[0]["err"] is not None and "no_sync" in out[0]["err"]

@@ -31,8 +31,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _run(args, out, timeout=420):
     cmd = [sys.executable, "-u", os.path.join(ROOT, "tools", "trajectory.py"), "--out", out] + args
-    r = subprocess.run(cmd, cwd=ROOT, timeout=timeout, capture_output=True, text=True)
-    assert r.returncode == 0, r.stderr[-4000:]
+    # the child's per-step progress goes to our stderr (visible with pytest -s: these runs take
+    # minutes), and to a log whose tail is the failure message
+    log = out + ".log"
+    with open(log, "w") as f:
+        p = subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+        try:
+            for line in p.stderr:
+                f.write(line)
+                sys.stderr.write(line)
+            p.wait(timeout=timeout)
+        finally:
+            if p.poll() is None:
+                p.kill()
+    with open(log) as f:
+        assert p.returncode == 0, f.read()[-4000:]
     with open(out) as f:
         return {rec["variant"]: rec for rec in json.load(f)}
 
