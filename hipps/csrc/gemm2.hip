@@ -43,7 +43,9 @@ __device__ __attribute__((aligned(64))) const uint16_t kZero16[32] = {0};
 // epilogue flags: kStats = forward BN statistics of Y; kAdd = Y += R (* mask bits); kBst =
 // backward BN statistics of the BN whose output gradient Y is (relu' recomputed from x * scale +
 // shift), kBstBits = the same with the BN's stored ReLU bits (gemm.hip BnBwdTap)
-enum Epi : int { kPlain = 0, kStats = 1, kAdd = 2, kBst = 4, kBstBits = 8 };
+// kAddS2 (with kAdd, 1x1 only): R is the compact input gradient of a stride-2 1x1 conv reading the
+// same tensor ([img, ceil(Ho/2), ceil(Wo/2), N]); it lands on the even (h, w) rows of Y only
+enum Epi : int { kPlain = 0, kStats = 1, kAdd = 2, kBst = 4, kBstBits = 8, kAddS2 = 16 };
 
 template <int BM, int BN> struct Cfg;
 template <> struct Cfg<256, 256> { static constexpr int TM = 128, TN = 64; };
@@ -54,8 +56,8 @@ template <> struct Cfg<128, 64> { static constexpr int TM = 64, TN = 32; };
 
 template <int BM, int BN> constexpr int nthreads() { return 64 * (BM / Cfg<BM, BN>::TM) * (BN / Cfg<BM, BN>::TN); }
 
-template <int BM, int BN> constexpr int lds_bytes() {
-  constexpr int stage = 2 * (BM + BN) * BK * 2;
+template <int BM, int BN, int NS = 2> constexpr int lds_bytes() {
+  constexpr int stage = NS * (BM + BN) * BK * 2;
   constexpr int epi = BM * (BN + 8) * 2;
   constexpr int wm = BM / Cfg<BM, BN>::TM;
   return (stage > epi ? stage : epi) + 2 * 2 * wm * BN * 4;
@@ -85,7 +87,17 @@ __device__ __forceinline__ void glds16(const void* src, void* dst) {
   __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)dst, 16, 0, 0);
 }
 
-template <int BM, int BN, int EPI, bool TAPS>
+// vmcnt-only s_waitcnt immediate (gfx9 encoding: vmcnt[3:0] + vmcnt[5:4] at bits 15:14; expcnt and
+// lgkmcnt at their maxima, i.e. not waited for)
+constexpr int waitcnt_vm(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
+// lgkmcnt-only s_waitcnt immediate (vmcnt / expcnt at their maxima)
+constexpr int waitcnt_lgkm(int n) { return 15 | (3 << 14) | (7 << 4) | ((n & 15) << 8); }
+
+// NS: LDS stages.  2: the DMA of tile k+1 is issued after the barrier of tile k and drained
+// (vmcnt(0)) before the next barrier.  3: tile k+2 is issued after the barrier of tile k and the
+// wait before each barrier is counted (vmcnt(glds per tile)), so one tile's DMA stays in flight
+// across every barrier (cdna_hip_programming.md §5 'Pipelining across barriers').
+template <int BM, int BN, int EPI, bool TAPS, int NS>
 __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   constexpr int TM = Cfg<BM, BN>::TM, TN = Cfg<BM, BN>::TN;
   constexpr int WM = BM / TM, WN = BN / TN, NW = WM * WN, NT = 64 * NW;
@@ -94,9 +106,11 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   constexpr int AI = BM / 8 / NW;         // A wave-instructions (8 rows x 128 B each) per stage per wave
   constexpr int BI = BN / 8 / NW;
   constexpr int EP = BN + 8;              // epilogue row pitch (elements)
-  constexpr int SCR = (2 * STAGE * 2 > BM * EP * 2 ? 2 * STAGE * 2 : BM * EP * 2);  // bytes before the stats scratch
+  constexpr int SCR = (NS * STAGE * 2 > BM * EP * 2 ? NS * STAGE * 2 : BM * EP * 2);  // bytes before the stats scratch
   static_assert(AI >= 1 && BI >= 1, "tile too small for the wave count");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[lds_bytes<BM, BN>() / 2];
+  static_assert(NS == 2 || NS == 3, "stages");
+  constexpr int NG = AI + BI;  // glds per tile per wave
+  __shared__ __attribute__((aligned(16))) uint16_t lds[lds_bytes<BM, BN, NS>() / 2];
 
   // bijective XCD-aware block order (cdna_hip_programming.md §5 'XCD swizzle must be bijective'):
   // the hardware deals blocks round-robin to 8 XCDs; give each XCD a contiguous run of tiles
@@ -171,7 +185,21 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   // epilogue operands (residual-gradient addend, BN-backward x and bits) are loaded during the
   // MFMAs of the last K tile, when no DMA is in flight, if they fit the register budget
   constexpr bool ADDE = (EPI & kAdd) != 0;
+  constexpr bool S2 = (EPI & kAddS2) != 0;
   constexpr int BSTE = (EPI & kBstBits) ? 2 : (EPI & kBst) ? 1 : 0;
+  // element offset in R of output row m's chunk (col), or -1 for a row that gets no addend (S2)
+  auto r_off = [&](int m, int col) -> int64_t {
+    if constexpr (S2) {
+      const int hw = g.Ho * g.Wo;
+      const int img = m / hw, rem = m - img * hw;
+      const int h = rem / g.Wo, wv = rem - h * g.Wo;
+      if ((h | wv) & 1) return -1;
+      const int hs = (g.Ho + 1) >> 1, ws = (g.Wo + 1) >> 1;
+      return (((int64_t)img * hs + (h >> 1)) * ws + (wv >> 1)) * g.N + col;
+    } else {
+      return (int64_t)m * g.N + col;
+    }
+  };
   constexpr int RCH = BN / 8;             // 16-byte chunks per output row
   constexpr int NOUT = BM * RCH / NT;     // output chunks per thread
   constexpr bool PF = (ADDE != (BSTE != 0)) && NOUT * 5 <= 40;  // one operand stream, <= 40 registers
@@ -180,15 +208,25 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
 
   const int KT = g.K / BK;
   issue(0, 0);
+  if (NS == 3 && KT > 1) issue(1, 1);
+  int cur = 0;
   for (int kt = 0; kt < KT; ++kt) {
-    const int cur = kt & 1;
     // this wave's DMA of tile kt has landed and its reads of tile kt-1 are retired; after the
-    // barrier every wave's have, so tile kt is readable and the other buffer is free to refill
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    // barrier every wave's have, so tile kt is readable and tile kt-1's buffer is free to refill
+    if (NS == 3 && kt + 1 < KT) {
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(NG));  // tile kt+1 stays in flight
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + 1 < KT) {
-      issue(kt + 1, cur ^ 1);
+    if (kt + NS - 1 < KT) {
+      int nxt = cur + NS - 1;
+      nxt = nxt >= NS ? nxt - NS : nxt;
+      issue(kt + NS - 1, nxt);
+    } else if (kt + 1 < KT) {
+      // NS == 3, second-to-last tile: nothing left to issue
     } else if constexpr (PF) {
 #pragma unroll
       for (int i = 0; i < NOUT; ++i) {
@@ -196,7 +234,8 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
         const int row = id / RCH, c = id - row * RCH;
         const int64_t o = (int64_t)(m0 + row < g.M ? m0 + row : m0) * g.N + n0 + c * 8;
         if constexpr (ADDE) {
-          pr[i] = *reinterpret_cast<const u32x4*>(g.R + o);
+          const int64_t ro = r_off(m0 + row < g.M ? m0 + row : m0, n0 + c * 8);
+          pr[i] = ro >= 0 ? *reinterpret_cast<const u32x4*>(g.R + ro) : u32x4{0u, 0u, 0u, 0u};
           prm[i] = g.RM != nullptr ? g.RM[o >> 3] : 0xffu;
         }
         if constexpr (BSTE) {
@@ -206,26 +245,47 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
       }
     }
     const uint16_t* As = lds + cur * STAGE;
+    cur = cur + 1 == NS ? 0 : cur + 1;
     const uint16_t* Bs = As + BM * BK;
-#pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
+    // FPF (one wave per SIMD): both k-steps' fragments are read up front, so the second step's
+    // reads are in flight while the first step's MFMAs run (counted lgkmcnt) instead of a
+    // read-wait-MFMA round per step; at two waves per SIMD (256x256) the other wave covers the
+    // read latency and the registers are not there for two fragment sets
+    constexpr bool FPF = NW <= 4;
+    constexpr int KS = BK / 32, FS = FPF ? KS : 1;
+    bf16x8 a[FS][FM], b[FS][FN];
+    auto frag = [&](int ks, int slot) {
       const int c = ks * 4 + (lane >> 4);
-      bf16x8 a[FM], b[FN];
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int row = wn * TN + j * 16 + (lane & 15);
-        b[j] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + ((c ^ (row & 7)) << 3));
+        b[slot][j] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + ((c ^ (row & 7)) << 3));
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int row = wm * TM + i * 16 + (lane & 15);
-        a[i] = *reinterpret_cast<const bf16x8*>(As + row * BK + ((c ^ (row & 7)) << 3));
+        a[slot][i] = *reinterpret_cast<const bf16x8*>(As + row * BK + ((c ^ (row & 7)) << 3));
+      }
+    };
+    if constexpr (FPF) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) frag(ks, ks);
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int slot = FPF ? ks : 0;
+      if constexpr (FPF) {
+        // step 0 needs its own FM + FN reads; the other step's stay in flight
+        if (ks == 0 && FM + FN <= 15) __builtin_amdgcn_s_waitcnt(waitcnt_lgkm(FM + FN));
+      } else {
+        frag(ks, 0);
       }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[slot][i], b[slot][j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
   }
@@ -295,6 +355,10 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
         if constexpr (PF) {
           r = pr[i];
           mb = prm[i];
+        } else if constexpr (S2) {
+          const int64_t ro = r_off(m0 + row, n0 + c * 8);
+          r = ro >= 0 ? *reinterpret_cast<const u32x4*>(g.R + ro) : u32x4{0u, 0u, 0u, 0u};
+          mb = g.RM != nullptr ? g.RM[o >> 3] : 0xffu;
         } else {
           r = *reinterpret_cast<const u32x4*>(g.R + o);
           mb = g.RM != nullptr ? g.RM[o >> 3] : 0xffu;
@@ -337,7 +401,7 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   }
   if (BST) {  // combine the NT/RCH row lanes of each channel chunk through LDS, fixed order
     constexpr int RL = NT / RCH;
-    static_assert(2 * RL * BN * 4 <= lds_bytes<BM, BN>(), "BST scratch");
+    static_assert(2 * RL * BN * 4 <= lds_bytes<BM, BN, NS>(), "BST scratch");
     float* red = reinterpret_cast<float*>(lds);
     __syncthreads();
 #pragma unroll
@@ -421,7 +485,8 @@ __device__ __forceinline__ bf16x8 tr_frag2(const uint8_t* tile, int row0, int co
 constexpr int kWM = 64;  // m rows per stage
 
 // TN x TK output tile on WN x WK waves (each (TN/WN) x (TK/WK) of 16x16 accumulators)
-template <int TN, int TK, int WN, int WK>
+// NS LDS stages as in k_gemm (3: one stage's DMA in flight across every barrier)
+template <int TN, int TK, int WN, int WK, int NS>
 __global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
   constexpr int NW = WN * WK;
   constexpr int YT = kWM * TN * 2, XT = kWM * TK * 2;  // bytes per staged tile
@@ -432,7 +497,9 @@ __global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
   constexpr int WTN = TN / WN, WTK = TK / WK;
   constexpr int FN = WTN / 16, FK = WTK / 16;
   static_assert(CY <= 64 && CX <= 64 && IY >= 1 && IX >= 1, "wgrad tile");
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * (YT + XT)];
+  static_assert(NS == 2 || NS == 3, "stages");
+  constexpr int NG = IY + IX;  // glds per stage per wave
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NS * (YT + XT)];
   const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
   const int tiles = g.tn * g.tk;
@@ -489,26 +556,55 @@ __global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
 
   const int nst = (mend - mbeg + kWM - 1) / kWM;
   issue(0, 0);
+  if (NS == 3 && nst > 1) issue(1, 1);
+  int cur = 0;
   for (int st = 0; st < nst; ++st) {
-    const int cur = st & 1;
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if (NS == 3 && st + 1 < nst) {
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(NG));  // stage st+1 stays in flight
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (st + 1 < nst) issue(st + 1, cur ^ 1);
+    if (st + NS - 1 < nst) {
+      int nxt = cur + NS - 1;
+      nxt = nxt >= NS ? nxt - NS : nxt;
+      issue(st + NS - 1, nxt);
+    }
     const uint8_t* ty = lds + cur * (YT + XT);
+    cur = cur + 1 == NS ? 0 : cur + 1;
     const uint8_t* tx = ty + YT;
+    // one wave per SIMD (NW <= 4): both 32-row steps' fragments are read up front and the
+    // second step's transposing reads overlap the first step's MFMAs (counted lgkmcnt)
+    constexpr bool FPF = NW <= 4;
+    constexpr int KS = kWM / 32, FS = FPF ? KS : 1;
+    bf16x8 a[FS][FN], b[FS][FK];
+    auto frag = [&](int ks, int slot) {
 #pragma unroll
-    for (int ks = 0; ks < kWM / 32; ++ks) {
-      bf16x8 a[FN], b[FK];
+      for (int i = 0; i < FN; ++i) a[slot][i] = tr_frag2<TN>(ty, ks * 32, wn * WTN + i * 16, lane);
 #pragma unroll
-      for (int i = 0; i < FN; ++i) a[i] = tr_frag2<TN>(ty, ks * 32, wn * WTN + i * 16, lane);
+      for (int j = 0; j < FK; ++j) b[slot][j] = tr_frag2<TK>(tx, ks * 32, wk * WTK + j * 16, lane);
+    };
+    if constexpr (FPF) {
 #pragma unroll
-      for (int j = 0; j < FK; ++j) b[j] = tr_frag2<TK>(tx, ks * 32, wk * WTK + j * 16, lane);
+      for (int ks = 0; ks < KS; ++ks) frag(ks, ks);
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int slot = FPF ? ks : 0;
+      if constexpr (FPF) {
+        constexpr int later = 2 * (FN + FK);  // ds_read_b64_tr per step
+        if (ks == 0) __builtin_amdgcn_s_waitcnt(waitcnt_lgkm(later < 15 ? later : 15));
+      } else {
+        frag(ks, 0);
+      }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll
-        for (int j = 0; j < FK; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FK; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[slot][i], b[slot][j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
   }
@@ -552,15 +648,18 @@ int64_t gemm2_mtiles(int64_t M, int64_t N, int64_t K, int64_t bm) {
 //     statistics of y, or -- with bn_x -- the backward BN reduction of the BN whose output
 //     gradient y is (bn_x its input, bn_bits its ReLU bits or none to recompute relu' from
 //     bn_x * bn_scale + bn_shift)
-//   add (+ add_mask, 1x1 only): y = conv(x) + add (* mask bits)
-//   bm / bn: block tile (0 = default per shape)
+//   add (+ add_mask, 1x1 only): y = conv(x) + add (* mask bits); with add_s2 add is the compact
+//     [img, ceil(Ho/2), ceil(Wo/2), Cout] input gradient of a stride-2 1x1 conv over the same
+//     tensor, added on the even (h, w) rows only (ResNet downsample branch)
+//   bm / bn: block tile (0 = default per shape); stages: LDS stages (2, or 3 below 256x256)
 void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part,
                 c10::optional<at::Tensor> add, c10::optional<at::Tensor> add_mask, int64_t Hi, int64_t Wi,
                 int64_t stride, int64_t KH, int64_t KW, int64_t pad, int64_t bm, int64_t bn,
                 c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_bits, c10::optional<at::Tensor> bn_mean,
                 c10::optional<at::Tensor> bn_invstd, c10::optional<at::Tensor> bn_scale,
-                c10::optional<at::Tensor> bn_shift) {
+                c10::optional<at::Tensor> bn_shift, int64_t stages, bool add_s2) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "gemm2: device tensors");
+  TORCH_CHECK(stages == 2 || stages == 3, "gemm2: stages must be 2 or 3");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
                   y.scalar_type() == at::kBFloat16, "gemm2: bf16 tensors");
   const int64_t N = w.size(0), K = w.numel() / N, Cin = K / (KH * KW);
@@ -599,9 +698,16 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
   const bool taps = !(KH == 1 && KW == 1 && pad == 0);
   if (add.has_value() && add->defined()) {
     TORCH_CHECK(!taps, "gemm2: the add epilogue is for 1x1 convolutions");
-    TORCH_CHECK(add->is_cuda() && add->scalar_type() == at::kBFloat16 && add->numel() == M * N &&
+    // add shaped like y, or (a stride-1 conv over [img, Ho, Wo]) the compact [img, ceil(Ho/2),
+    // ceil(Wo/2), N] input gradient of a stride-2 1x1 conv over the same tensor (add_s2)
+    const int64_t Ms2 = imgs * ((Ho + 1) / 2) * ((Wo + 1) / 2);
+    const bool s2 = add_s2;
+    TORCH_CHECK(!s2 || (stride == 1 && !(add_mask.has_value() && add_mask->defined())),
+                "gemm2: add_s2 needs a stride-1 conv and no add mask");
+    TORCH_CHECK(add->is_cuda() && add->scalar_type() == at::kBFloat16 && add->numel() == (s2 ? Ms2 : M) * N &&
                     (add->dim() != 4 || add->is_contiguous(at::MemoryFormat::ChannelsLast)) &&
-                    reinterpret_cast<uintptr_t>(add->data_ptr()) % 16 == 0, "gemm2: add shaped like y");
+                    reinterpret_cast<uintptr_t>(add->data_ptr()) % 16 == 0, "gemm2: add shaped like y (or compact)");
+    if (s2) epi |= g2::kAddS2;
     a.R = (const uint16_t*)add->data_ptr();
     if (add_mask.has_value() && add_mask->defined()) {
       TORCH_CHECK(add_mask->is_cuda() && add_mask->scalar_type() == at::kByte && add_mask->is_contiguous() &&
@@ -611,7 +717,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
     epi |= g2::kAdd;
   }
   if (bn_x.has_value() && bn_x->defined()) {
-    TORCH_CHECK(!taps && a.pa != nullptr, "gemm2: BN-backward statistics need a 1x1 conv and part");
+    TORCH_CHECK(a.pa != nullptr, "gemm2: BN-backward statistics need part");
     TORCH_CHECK(bn_x->is_cuda() && bn_x->scalar_type() == at::kBFloat16 && bn_x->numel() == M * N &&
                     (bn_x->dim() != 4 || bn_x->is_contiguous(at::MemoryFormat::ChannelsLast)) &&
                     reinterpret_cast<uintptr_t>(bn_x->data_ptr()) % 16 == 0, "gemm2: bn_x shaped like y");
@@ -637,13 +743,22 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
   }
   auto stream = c10::hip::getCurrentHIPStream();
   const int grid = (int)(mtiles * ntiles);
+#define HIPPS_G2S(BMc, BNc, EPc, TPc, NSc) \
+  hipLaunchKernelGGL((g2::k_gemm<BMc, BNc, EPc, TPc, NSc>), grid, (g2::nthreads<BMc, BNc>()), 0, stream, a)
 #define HIPPS_G2(BMc, BNc, EPc, TPc) \
-  hipLaunchKernelGGL((g2::k_gemm<BMc, BNc, EPc, TPc>), grid, (g2::nthreads<BMc, BNc>()), 0, stream, a)
+  do {                                                      \
+    if (NS3) HIPPS_G2S(BMc, BNc, EPc, TPc, NS3_OF(BMc, BNc)); \
+    else HIPPS_G2S(BMc, BNc, EPc, TPc, 2);                   \
+  } while (0)
 #define HIPPS_G2_E(BMc, BNc)                                                                        \
   do {                                                                                              \
     if (taps) {                                                                                     \
-      if (epi == g2::kStats) HIPPS_G2(BMc, BNc, g2::kStats, true);                                  \
-      else HIPPS_G2(BMc, BNc, g2::kPlain, true);                                                    \
+      switch (epi) {                                                                                \
+        case g2::kStats: HIPPS_G2(BMc, BNc, g2::kStats, true); break;                               \
+        case g2::kBst: HIPPS_G2(BMc, BNc, g2::kBst, true); break;                                   \
+        case g2::kBstBits: HIPPS_G2(BMc, BNc, g2::kBstBits, true); break;                           \
+        default: HIPPS_G2(BMc, BNc, g2::kPlain, true); break;                                       \
+      }                                                                                             \
     } else {                                                                                        \
       switch (epi) {                                                                                \
         case g2::kStats: HIPPS_G2(BMc, BNc, g2::kStats, false); break;                              \
@@ -652,10 +767,19 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
         case g2::kBst | g2::kAdd: HIPPS_G2(BMc, BNc, (g2::kBst | g2::kAdd), false); break;          \
         case g2::kBstBits: HIPPS_G2(BMc, BNc, g2::kBstBits, false); break;                          \
         case g2::kBstBits | g2::kAdd: HIPPS_G2(BMc, BNc, (g2::kBstBits | g2::kAdd), false); break;  \
+        case g2::kAdd | g2::kAddS2: HIPPS_G2(BMc, BNc, (g2::kAdd | g2::kAddS2), false); break;      \
+        case g2::kBst | g2::kAdd | g2::kAddS2:                                                        \
+          HIPPS_G2(BMc, BNc, (g2::kBst | g2::kAdd | g2::kAddS2), false); break;                      \
+        case g2::kBstBits | g2::kAdd | g2::kAddS2:                                                    \
+          HIPPS_G2(BMc, BNc, (g2::kBstBits | g2::kAdd | g2::kAddS2), false); break;                  \
         default: HIPPS_G2(BMc, BNc, g2::kPlain, false); break;                                      \
       }                                                                                             \
     }                                                                                               \
   } while (0)
+  // 3 stages where they fit the LDS (not 256x256: 3 x 64 KB)
+  const bool NS3 = stages == 3;
+  TORCH_CHECK(!NS3 || !(BMv == 256 && BNv == 256), "gemm2: 3 stages do not fit a 256x256 tile");
+#define NS3_OF(BMc, BNc) ((BMc) == 256 && (BNc) == 256 ? 2 : 3)
   if (BMv == 256 && BNv == 256) HIPPS_G2_E(256, 256);
   else if (BMv == 256 && BNv == 128) HIPPS_G2_E(256, 128);
   else if (BMv == 128 && BNv == 128) HIPPS_G2_E(128, 128);
@@ -664,6 +788,8 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
   else TORCH_CHECK(false, "gemm2: unsupported block tile ", BMv, "x", BNv);
 #undef HIPPS_G2_E
 #undef HIPPS_G2
+#undef HIPPS_G2S
+#undef NS3_OF
 }
 
 void wgrad_reduce_slabs(const at::Tensor& part, int64_t S, int64_t N, int64_t K, at::Tensor& dw,
@@ -673,8 +799,9 @@ void wgrad_reduce_slabs(const at::Tensor& part, int64_t S, int64_t N, int64_t K,
 // bf16; dw f32 [Cout, KH, KW, Cin] in memory (the channels-last weight layout; 1x1: [Cout, Cin]).
 // Cout % 64 == 0, Cin % 64 == 0.  S split-M partial slabs (~2 resident blocks per CU) + fixed-order sum.
 void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
-                 int64_t Hi, int64_t Wi, int64_t cfg) {
+                 int64_t Hi, int64_t Wi, int64_t cfg, int64_t stages) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dw.is_cuda(), "gemm2_wgrad: device tensors");
+  TORCH_CHECK(stages == 2 || (stages == 3 && cfg != 2), "gemm2_wgrad: stages 2, or 3 below the 256x256 tile");
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 && dw.scalar_type() == at::kFloat,
               "gemm2_wgrad: bf16 dy/x, f32 dw");
   TORCH_CHECK(dw.is_contiguous() || dw.is_contiguous(at::MemoryFormat::ChannelsLast), "gemm2_wgrad: dense dw");
@@ -702,7 +829,8 @@ void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t
     TN = 256; TK = 256;
   }
   const int64_t tn = N / TN, tk = K / TK, tiles = tn * tk;
-  const int64_t resident = 256 * (cfg ? 1 : TN * TK == 128 * 128 ? 2 : TN * TK == 128 * 64 ? 3 : 5);
+  int64_t resident = 256 * (cfg ? 1 : TN * TK == 128 * 128 ? 2 : TN * TK == 128 * 64 ? 3 : 5);
+  if (stages == 3) resident = 256 * std::max<int64_t>(1, 160 * 1024 / (3 * g2::kWM * (TN + TK) * 2));
   int64_t S = std::max<int64_t>(1, resident / tiles);
   S = std::min<int64_t>(S, std::max<int64_t>(1, M / (8 * g2::kWM)));           // >= 8 stages per block
   S = std::min<int64_t>(S, std::max<int64_t>(1, M * (N + K) / (4 * N * K)));  // slabs <= operand bytes
@@ -721,12 +849,18 @@ void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t
   a.fd_hw = g2::make_fastdiv2((uint32_t)(Ho * Wo));
   a.fd_w = g2::make_fastdiv2((uint32_t)Wo);
   const int grid = (int)(S * tiles);
-  if (cfg == 2) hipLaunchKernelGGL((g2::k_wgrad<256, 256, 2, 4>), grid, 512, 0, stream, a);
-  else if (cfg == 1) hipLaunchKernelGGL((g2::k_wgrad<256, 128, 2, 2>), grid, 256, 0, stream, a);
-  else if (TN == 128 && TK == 128) hipLaunchKernelGGL((g2::k_wgrad<128, 128, 2, 2>), grid, 256, 0, stream, a);
-  else if (TN == 128) hipLaunchKernelGGL((g2::k_wgrad<128, 64, 2, 2>), grid, 256, 0, stream, a);
-  else if (TK == 128) hipLaunchKernelGGL((g2::k_wgrad<64, 128, 2, 2>), grid, 256, 0, stream, a);
-  else hipLaunchKernelGGL((g2::k_wgrad<64, 64, 2, 2>), grid, 256, 0, stream, a);
+#define HIPPS_W2(TNc, TKc, WNc, WKc)                                                                      \
+  do {                                                                                                  \
+    if (stages == 3) hipLaunchKernelGGL((g2::k_wgrad<TNc, TKc, WNc, WKc, 3>), grid, 64 * WNc * WKc, 0, stream, a); \
+    else hipLaunchKernelGGL((g2::k_wgrad<TNc, TKc, WNc, WKc, 2>), grid, 64 * WNc * WKc, 0, stream, a);            \
+  } while (0)
+  if (cfg == 2) hipLaunchKernelGGL((g2::k_wgrad<256, 256, 2, 4, 2>), grid, 512, 0, stream, a);
+  else if (cfg == 1) HIPPS_W2(256, 128, 2, 2);
+  else if (TN == 128 && TK == 128) HIPPS_W2(128, 128, 2, 2);
+  else if (TN == 128) HIPPS_W2(128, 64, 2, 2);
+  else if (TK == 128) HIPPS_W2(64, 128, 2, 2);
+  else HIPPS_W2(64, 64, 2, 2);
+#undef HIPPS_W2
   if (S > 1) {
     at::Tensor dwv = dw;
     wgrad_reduce_slabs(part, S, N, K, dwv, stream);

@@ -99,7 +99,8 @@ class Bottleneck(nn.Module):
                 return bn_relu_conv_bn(self.bn2, self.conv3, self.bn3, y, residual=idt, res_tap=tap)
             y = self.bn2(y)
         else:
-            y = conv2d_bn(self.conv2, self.bn2, y, fuse=_FUSED_WGRAD)
+            # bn1's output only feeds conv2: its backward reduction rides conv2's input-gradient GEMM
+            y = conv2d_bn(self.conv2, self.bn2, y, fuse=_FUSED_WGRAD, bn_grad=bng)
         return conv_bn(self.conv3, self.bn3, y, residual=idt, fuse=_FUSED_CONV, res_tap=tap, bn_grad=bng)
 
 

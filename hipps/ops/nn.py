@@ -80,14 +80,27 @@ class _Tuner:
 
 
 TUNER = _Tuner()
-_G2_TILES = ((128, 128), (256, 256), (128, 64), (256, 64))
+# (block rows, block cols, LDS stages): 3 stages keep one tile's DMA in flight across every
+# K-loop barrier (gemm2.hip k_gemm NS).  Only 128x64 keeps two blocks per CU with 3 stages; the
+# others drop to one wave per SIMD and lose (profiles/gemm2_probe_r3_stages.json)
+_G2_TILES = ((128, 128, 2), (256, 256, 2), (128, 64, 2), (256, 64, 2), (128, 64, 3))
 
 
 def _g2_names(N: int):
-    return [f"g2_{bm}x{bn}" for bm, bn in _G2_TILES if N % bn == 0]
+    return [f"g2_{bm}x{bn}" + ("" if ns == 2 else f"s{ns}") for bm, bn, ns in _G2_TILES if N % bn == 0]
 
 
-def _conv1x1_gemm(x2, w2d, y, Hi, Wi, stride, part_needed, add=None, add_mask=None, bg=None):
+def _g2_parse(name: str):
+    """'g2_256x128s3' -> (256, 128, 3); 'g2_128x64' -> (128, 64, 2)"""
+    t = name[3:]
+    ns = 2
+    if "s" in t:
+        t, ns = t.split("s")
+    bm, bn = (int(v) for v in t.split("x"))
+    return bm, bn, int(ns)
+
+
+def _conv1x1_gemm(x2, w2d, y, Hi, Wi, stride, part_needed, add=None, add_mask=None, bg=None, add_s2=False):
     """y = x . w2d^T as a 1x1 conv (x channels-last [n, K, Hi, Wi] or [M, K]; w2d [N, K]) on the
     fastest core for this shape AND epilogue (candidates are timed with the real epilogue: the
     memory-bound residual / BN-backward epilogues change the ranking); returns the statistics
@@ -108,22 +121,24 @@ def _conv1x1_gemm(x2, w2d, y, Hi, Wi, stride, part_needed, add=None, add_mask=No
             else:
                 C.conv1x1_forward(x2, w2d, y, part, Hi, Wi, stride, add, add_mask)
             return part
-        bm, bn = (int(v) for v in name[3:].split("x"))
+        bm, bn, ns = _g2_parse(name)
         if part_needed:
             part = torch.empty((2, N, C.gemm2_mtiles(M, N, K, bm)), dtype=torch.float32, device=y.device)
         if bg is not None:
             C.gemm2_conv(x2, w2d, y, part, add, add_mask, Hi, Wi, stride, 1, 1, 0, bm, bn, bg.x, bg.mask, bg.mean,
-                         bg.invstd, bg.scale, bg.shift)
+                         bg.invstd, bg.scale, bg.shift, stages=ns, add_s2=add_s2)
         else:
-            C.gemm2_conv(x2, w2d, y, part, add, add_mask, Hi, Wi, stride, 1, 1, 0, bm, bn)
+            C.gemm2_conv(x2, w2d, y, part, add, add_mask, Hi, Wi, stride, 1, 1, 0, bm, bn, stages=ns, add_s2=add_s2)
         return part
 
     name = "g1"
     if _GEMM2 and K % 64 == 0 and N % 64 == 0:
         epi = (part_needed, add is not None, add_mask is not None, bg is not None and bg.mask is not None,
-               bg is not None)
+               bg is not None, add_s2)
         name = TUNER.pick(("1x1", M, K, N, stride, Hi, Wi, epi),
-                          {n: (lambda n=n: run(n)) for n in ["g1"] + _g2_names(N)})
+                          {n: (lambda n=n: run(n)) for n in ([] if add_s2 else ["g1"]) + _g2_names(N)})
+    elif add_s2:
+        raise RuntimeError("the compact stride-2 addend needs the gemm2 core")
     return run(name)
 
 
@@ -137,23 +152,37 @@ def _conv_wgrad(dy, x, dw, kh, kw, stride, pad):
         first = lambda: C.conv1x1_wgrad(dy, x, dw.view(cout, cin), hi, wi, stride)  # noqa: E731
     else:
         first = lambda: C.conv_wgrad(dy, x, dw, kh, kw, stride, pad)  # noqa: E731
+    def mio():  # MIOpen's bf16 weight gradient (the 64-channel KxK layers' previous route)
+        w = torch.empty((cout, cin, kh, kw), dtype=torch.bfloat16, device=dy.device)
+        g = torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
+                                                [False, True, False])[1]
+        dw.copy_(g)
+
     name = "w2"
     if _GEMM2 and cout % 64 == 0 and cin % 64 == 0:
         cands = {"w2": first}
         for cfg in (0, 1, 2):  # gemm2.hip k_wgrad tilings: 128x128 / 256x128 / 256x256 outputs
             if cfg == 0 or (cout % 256 == 0 and cin % (128 * cfg) == 0):
-                cands[f"w3_{cfg}"] = (lambda cfg=cfg: C.gemm2_wgrad(dy, x, dw, kh, kw, stride, pad, hi, wi, cfg))
+                for ns in ((2, 3) if cfg < 2 else (2,)):  # LDS stages (3 do not fit 256x256)
+                    cands[f"w3_{cfg}" + ("s3" if ns == 3 else "")] = (
+                        lambda cfg=cfg, ns=ns: C.gemm2_wgrad(dy, x, dw, kh, kw, stride, pad, hi, wi, cfg, ns))
+        if kh > 1 and cin < 128:
+            cands["miopen"] = mio
         name = TUNER.pick(("wgrad", tuple(x.shape), cout, kh, kw, stride, pad), cands)
     if name.startswith("w3"):
-        C.gemm2_wgrad(dy, x, dw, kh, kw, stride, pad, hi, wi, int(name[3:]))
+        C.gemm2_wgrad(dy, x, dw, kh, kw, stride, pad, hi, wi, int(name[3]), 3 if name.endswith("s3") else 2)
+    elif name == "miopen":
+        mio()
     else:
         first()
 
 
-def _convkxk_gemm(x, w, stride, pad, stats: bool):
+def _convkxk_gemm(x, w, stride, pad, stats: bool, bg=None):
     """KxK conv forward (channels-last bf16) on the fastest of {gemm2 implicit GEMM tiles, MIOpen}
     for this shape; returns (y, part or None) -- part: the following BN's statistics partials
-    when the GEMM ran (MIOpen gives none)."""
+    when the GEMM ran (MIOpen gives none), or with ``bg`` (a BNGradTap; y is then the gradient of
+    that BN's output, e.g. a stride-1 input gradient run as a forward conv) the BN's backward
+    reduction from the epilogue."""
     C = native()
     n, cin, h, wd = x.shape
     cout, k = w.shape[0], w.shape[2]
@@ -164,17 +193,22 @@ def _convkxk_gemm(x, w, stride, pad, stats: bool):
     def run(name):
         if name == "miopen":
             return mio(), None
-        bm, bn = (int(v) for v in name[3:].split("x"))
+        bm, bn, ns = _g2_parse(name)
         part = None
-        if stats:
+        if stats or bg is not None:
             part = torch.empty((2, cout, C.gemm2_mtiles(n * ho * wo, cout, k * k * cin, bm)), dtype=torch.float32,
                                device=x.device)
-        C.gemm2_conv(x, w, y, part, None, None, h, wd, stride, k, k, pad, bm, bn)
+        if bg is not None:
+            C.gemm2_conv(x, w, y, part, None, None, h, wd, stride, k, k, pad, bm, bn, bg.x, bg.mask, bg.mean,
+                         bg.invstd, bg.scale, bg.shift, stages=ns)
+        else:
+            C.gemm2_conv(x, w, y, part, None, None, h, wd, stride, k, k, pad, bm, bn, stages=ns)
         return y, part
 
     def timed(name):
         # what the choice costs the step: with ``stats`` MIOpen leaves the following BN a
-        # statistics pass over y (reduce + finalize), the GEMM leaves it a finalize of its partials
+        # statistics pass over y (reduce + finalize), the GEMM leaves it a finalize of its partials;
+        # with ``bg`` MIOpen leaves that BN's backward its reduction pass over (y, bn x)
         yy, part = run(name)
         if stats:
             v = [torch.empty(cout, dtype=torch.float32, device=x.device) for _ in range(6)]
@@ -183,10 +217,20 @@ def _convkxk_gemm(x, w, stride, pad, stats: bool):
             else:
                 C.bn_finalize_partials(part, part.shape[2], n * ho * wo, v[0], v[1], None, None, v[2], v[3], v[4],
                                        v[5], cout, 1e-5, 0.1)
+        if bg is not None:
+            mode = MASK_BITS if bg.mask is not None else MASK_X
+            dx, dgw, dgb = torch.empty_like(yy), torch.empty_like(bg.scale), torch.empty_like(bg.scale)
+            if part is None:
+                C.bn_backward(yy, bg.x, None, mode, bg.scale, bg.mean, bg.invstd, bg.scale, bg.shift, dx, None,
+                              dgw, dgb, cout, bg.mask)
+            else:
+                C.bn_backward_partials(part, part.shape[2], yy, bg.x, mode, bg.scale, bg.mean, bg.invstd, bg.scale,
+                                       bg.shift, dx, None, dgw, dgb, cout, bg.mask)
 
     name = "miopen"
     if _GEMM2 and cin % 64 == 0 and cout % 64 == 0:
-        name = TUNER.pick(("kxk", n, cin, h, wd, cout, k, stride, pad, stats),
+        epi = (stats, None if bg is None else bg.mask is not None)
+        name = TUNER.pick(("kxk", n, cin, h, wd, cout, k, stride, pad, epi),
                           {nm: (lambda nm=nm: timed(nm)) for nm in ["miopen"] + _g2_names(cout)})
     return run(name)
 
@@ -225,6 +269,21 @@ class BNGradTap:
     def __init__(self, x, mask, mean, invstd, scale, shift):
         self.x, self.mask, self.mean, self.invstd, self.scale, self.shift = x, mask, mean, invstd, scale, shift
         self.part = None
+
+
+class S2Tap:
+    """Hands the input gradient of a stride-2 1x1 conv (a ResNet downsample) to the stride-1 1x1
+    conv that reads the same tensor (the block's conv1, through the alias it returned).  The
+    downsample's backward computes only the compact gradient [img, C, ceil(H/2), ceil(W/2)] (a
+    plain GEMM over its output rows) and returns no gradient for the alias; conv1's backward --
+    which autograd runs after it, the alias being one of conv1's outputs -- adds it on the even
+    (h, w) rows in its dgrad epilogue (gemm2 kAddS2).  No zero-filled full-size gradient is
+    written or re-read (MIOpen's strided backward-data writes one: zero fill + scatter)."""
+
+    __slots__ = ("dx",)
+
+    def __init__(self):
+        self.dx = None
 
 
 _SHADOWS: list = []  # [fp32 flat param buffer, bf16 shadow] pairs (FlatStore.enable_bf16_shadow)
@@ -276,7 +335,7 @@ class _Conv1x1(torch.autograd.Function):
     and with ``alias`` the gradient of the returned alias of x (e.g. a downsample branch)."""
 
     @staticmethod
-    def forward(ctx, x, w_master, stride, tap=None, alias=False, bngrad=None):
+    def forward(ctx, x, w_master, stride, tap=None, alias=False, bngrad=None, s2tap=None):
         w = bf16_weight(w_master)
         ctx.wdtype = w_master.dtype
         # no zero-filled grad for the non-differentiable BN partials (a 12.8 MB fill per layer)
@@ -290,6 +349,9 @@ class _Conv1x1(torch.autograd.Function):
         part = _conv1x1_gemm(x, w.reshape(Cout, Cin), y, H, W, stride, True)
         ctx.stride = stride
         ctx.tap = tap
+        # alias (conv1): the downsample's compact gradient arrives here; stride 2 (downsample): put
+        # it here
+        ctx.s2tap = s2tap if (_GEMM2 and ((alias and stride == 1) or stride == 2)) else None
         ctx.save_for_backward(x, w)
         ctx.mark_non_differentiable(part)
         if alias:
@@ -300,12 +362,21 @@ class _Conv1x1(torch.autograd.Function):
     def backward(ctx, dy, _dpart, d_alias=None):
         x, w = ctx.saved_tensors
         s = ctx.stride
+        s2tap, ctx.s2tap = ctx.s2tap, None
         if dy is None:  # y unused (grads are not materialized): only the alias path carries a grad
             ctx.bngrad = None
-            return d_alias, None, None, None, None, None
+            if s2tap is not None and s2tap.dx is not None:
+                raise RuntimeError("compact stride-2 gradient without a consuming dgrad")
+            return d_alias, None, None, None, None, None, None
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = None
         add, add_mask = ctx.tap.take() if ctx.tap is not None else (None, None)
+        add_s2 = False
+        if s2tap is not None and s == 1 and s2tap.dx is not None:  # conv1: the downsample's gradient
+            if d_alias is not None or add is not None:
+                raise RuntimeError("compact stride-2 gradient next to another alias / tap gradient")
+            add, add_s2 = s2tap.dx, True
+            s2tap.dx = None
         if d_alias is not None:
             d_alias = d_alias.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
             if add is None:
@@ -314,7 +385,9 @@ class _Conv1x1(torch.autograd.Function):
                 add = _masked(add, add_mask, x.shape[1]) + d_alias
                 add_mask = None
         own_dx = ctx.needs_input_grad[0] and s == 1
-        if ctx.needs_input_grad[0] and not own_dx:
+        s2_dx = (ctx.needs_input_grad[0] and s == 2 and s2tap is not None and x.shape[1] % 64 == 0 and
+                 dy.shape[1] % 64 == 0)
+        if ctx.needs_input_grad[0] and not own_dx and not s2_dx:
             dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
                                                      [True, False, False])[0]
             if add is not None:
@@ -327,6 +400,15 @@ class _Conv1x1(torch.autograd.Function):
             _conv_wgrad(dy, x, dw, 1, 1, s, 0)
             if ctx.wdtype != torch.float32:
                 dw = dw.to(ctx.wdtype)
+        if s2_dx:  # compact gradient at the output positions, summed in conv1's dgrad epilogue
+            cout, cin = w.shape[0], w.shape[1]
+            wt = ctx.wt if ctx.wt is not None else w.reshape(cout, cin).t().contiguous()
+            n, _, ho, wo = dy.shape
+            dxc = torch.empty((n, cin, ho, wo), dtype=torch.bfloat16, device=dy.device,
+                              memory_format=torch.channels_last)
+            _conv1x1_gemm(dy, wt, dxc, ho, wo, 1, False)
+            s2tap.dx = dxc
+            dx = None
         if own_dx:
             cout, cin = w.shape[0], w.shape[1]
             wt = ctx.wt  # [Cin, Cout]: K-contiguous B operand (refreshed with the weight shadow)
@@ -337,11 +419,11 @@ class _Conv1x1(torch.autograd.Function):
             # x's gradient is complete here only if the residual path it also feeds was summed in
             # (an identity block's tap delivered, or no tap was involved)
             if bg is not None and (ctx.tap is None or add is not None):
-                bg.part = _conv1x1_gemm(dy, wt, dx, x.shape[2], x.shape[3], 1, True, add, add_mask, bg)
+                bg.part = _conv1x1_gemm(dy, wt, dx, x.shape[2], x.shape[3], 1, True, add, add_mask, bg, add_s2)
             else:
-                _conv1x1_gemm(dy, wt, dx, x.shape[2], x.shape[3], 1, False, add, add_mask)
+                _conv1x1_gemm(dy, wt, dx, x.shape[2], x.shape[3], 1, False, add, add_mask, None, add_s2)
         ctx.bngrad = None
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
 class _BNReluConv1x1(torch.autograd.Function):
@@ -422,10 +504,13 @@ class _ConvKxK(torch.autograd.Function):
     fp32 workspace and need 3 extra zero-fill / cast kernels per call (profiles/bench_n1_steady_r1d.txt)."""
 
     @staticmethod
-    def forward(ctx, x, w_master, stride, pad, own_wgrad=True, stats=False):
+    def forward(ctx, x, w_master, stride, pad, own_wgrad=True, stats=False, bngrad=None):
         w = bf16_weight(w_master)
         ctx.wdtype = w_master.dtype
         ctx.own_wgrad = own_wgrad
+        # x is the output of a fused BN whose only gradient is this conv's input gradient: the
+        # stride-1 input gradient (a forward conv on gemm2) reduces that BN's backward statistics
+        ctx.bngrad = bngrad if stride == 1 else None
         ctx.set_materialize_grads(False)
         ctx.wf = _TSHADOWS.get(w_master.data_ptr()) if w_master.dtype == torch.float32 else None
         part = None
@@ -454,8 +539,9 @@ class _ConvKxK(torch.autograd.Function):
     def backward(ctx, dy, _dpart=None):
         x, w = ctx.saved_tensors
         s, p = ctx.geom
+        bg, ctx.bngrad = ctx.bngrad, None
         if dy is None:
-            return None, None, None, None, None, None
+            return None, None, None, None, None, None, None
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = None
         k = w.shape[2]
@@ -465,7 +551,9 @@ class _ConvKxK(torch.autograd.Function):
             if wf is None:
                 wf = torch.flip(w, (2, 3)).transpose(0, 1).contiguous(memory_format=torch.channels_last)
             if _GEMM2 and wf.is_contiguous(memory_format=torch.channels_last):
-                dx = _convkxk_gemm(dy, wf, 1, p, False)[0]
+                dx, part = _convkxk_gemm(dy, wf, 1, p, False, bg)
+                if bg is not None:
+                    bg.part = part  # None when MIOpen ran: the BN backward then reduces itself
             elif _own_kxk(dy.shape[1], wf.shape[0]):
                 dx = torch.empty_like(x, memory_format=torch.channels_last)
                 native().convkxk_forward(dy, wf, dx, None, 1, p)
@@ -482,7 +570,7 @@ class _ConvKxK(torch.autograd.Function):
             _conv_wgrad(dy, x, dw, w.shape[2], w.shape[3], s, p)
             if ctx.wdtype != torch.float32:
                 dw = dw.to(ctx.wdtype)
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
 def _own_kxk(cin: int, cout: int) -> bool:
@@ -504,9 +592,11 @@ def convkxk_ok(conv: nn.Conv2d, x: torch.Tensor, own_wgrad: bool = True) -> bool
     w = conv.weight
     if not own_wgrad:
         return w.is_contiguous(memory_format=torch.channels_last)
-    # 64-channel KxK layers: a 64x64 output tile re-reads both operands once per tap and MIOpen
-    # is faster there (0.23 vs 0.29 ms at 64x56x56, profiles/conv3x3_wgrad.json)
-    return (conv.in_channels % 128 == 0 and conv.out_channels % 64 == 0 and
+    # 64-channel KxK layers: the first core's 64x64 output tile re-reads both operands once per tap
+    # and MIOpen is faster there (0.23 vs 0.29 ms at 64x56x56, profiles/conv3x3_wgrad.json); with
+    # gemm2 the tuner measures its 128x128-tile kernel against MIOpen for them
+    cmin = 64 if _GEMM2 else 128
+    return (conv.in_channels % cmin == 0 and conv.out_channels % 64 == 0 and
             w.is_contiguous(memory_format=torch.channels_last))
 
 
@@ -565,20 +655,22 @@ def stem_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     return w % 8 == 0 and h >= 7 and w >= 7 and (w - 1) // 2 + 1 <= 128
 
 
-def conv2d_stats(conv: nn.Conv2d, x: torch.Tensor, fuse: bool = True):
+def conv2d_stats(conv: nn.Conv2d, x: torch.Tensor, fuse: bool = True, bn_grad: bool = False):
     """(conv(x), part): with the hipps implicit-GEMM forward, ``part`` holds the following
     BatchNorm's partial statistics [2, Cout, m_tiles] from its epilogue (None otherwise); the
-    hipps weight gradient when eligible (see _ConvKxK)."""
+    hipps weight gradient when eligible (see _ConvKxK).  ``bn_grad``: x is the output of a fused
+    BN whose only consumer is this conv (see BNGradTap)."""
     if fuse and stem_ok(conv, x):
         xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         y, part = _StemConv.apply(xb, conv.weight, conv.training)
         return y, (part if part.numel() else None)
+    bg = getattr(x, "_hipps_bngrad", None) if bn_grad else None
     if fuse and conv.training and convkxk_ok(conv, x):
-        y, part = _ConvKxK.apply(x, conv.weight, conv.stride[0], conv.padding[0], True, True)
+        y, part = _ConvKxK.apply(x, conv.weight, conv.stride[0], conv.padding[0], True, True, bg)
         return y, (part if part.numel() else None)
     if conv.training and convkxk_ok(conv, x, own_wgrad=False) and (
             (_DGRAD_AS_FWD and conv.stride[0] == 1) or _own_kxk(conv.in_channels, conv.out_channels) or _GEMM2):
-        y, part = _ConvKxK.apply(x, conv.weight, conv.stride[0], conv.padding[0], False, True)  # MIOpen wgrad
+        y, part = _ConvKxK.apply(x, conv.weight, conv.stride[0], conv.padding[0], False, True, bg)  # MIOpen wgrad
         return y, (part if part.numel() else None)
     return conv(x), None
 
@@ -588,9 +680,10 @@ def conv2d(conv: nn.Conv2d, x: torch.Tensor, fuse: bool = True) -> torch.Tensor:
     return conv2d_stats(conv, x, fuse)[0]
 
 
-def conv2d_bn(conv: nn.Conv2d, bn, x: torch.Tensor, residual=None, fuse: bool = True):
-    """bn(conv(x), residual) with the BN statistics from the conv's GEMM epilogue when available."""
-    y, part = conv2d_stats(conv, x, fuse)
+def conv2d_bn(conv: nn.Conv2d, bn, x: torch.Tensor, residual=None, fuse: bool = True, bn_grad: bool = False):
+    """bn(conv(x), residual) with the BN statistics from the conv's GEMM epilogue when available
+    (``bn_grad``: see conv2d_stats)."""
+    y, part = conv2d_stats(conv, x, fuse, bn_grad)
     if part is not None and bn.training and bn._fast_ok(y, residual):
         return bn(y, residual, stats=part)
     return bn(y, residual)
@@ -617,10 +710,11 @@ def conv1x1_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     return conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0
 
 
-def conv1x1_stats(x, weight, stride=1, tap=None, alias=False, bngrad=None):
+def conv1x1_stats(x, weight, stride=1, tap=None, alias=False, bngrad=None, s2tap=None):
     """(y, part[, x_alias]): bf16 1x1 conv output and its [2, Cout, m_tiles] BN partial
-    statistics (see _Conv1x1 for ``tap`` / ``alias``, BNGradTap for ``bngrad``)."""
-    return _Conv1x1.apply(x, weight, int(stride), tap, bool(alias), bngrad)
+    statistics (see _Conv1x1 for ``tap`` / ``alias``, BNGradTap for ``bngrad``, S2Tap for
+    ``s2tap``)."""
+    return _Conv1x1.apply(x, weight, int(stride), tap, bool(alias), bngrad, s2tap)
 
 
 class _FusedBNAct(torch.autograd.Function):
@@ -761,9 +855,14 @@ def conv_bn(conv: nn.Conv2d, bn: FusedBatchNorm2d, x, residual=None, fuse: bool 
         s = conv.stride[0]
         own_tap = tap if s == 1 else None
         bg = getattr(x, "_hipps_bngrad", None) if bn_grad else None
-        outs = conv1x1_stats(x, conv.weight, s, own_tap, alias and s == 1, bg)
+        # alias (conv1 of a downsample block): its dgrad takes the downsample's compact gradient;
+        # stride 2 reading such an alias (the downsample): hand that gradient over (S2Tap)
+        s2tap = S2Tap() if (alias and s == 1) else (getattr(x, "_hipps_s2tap", None) if s == 2 else None)
+        outs = conv1x1_stats(x, conv.weight, s, own_tap, alias and s == 1, bg, s2tap)
         y, part = outs[0], outs[1]
         xa = outs[2] if len(outs) > 2 else x
+        if alias and s == 1 and s2tap is not None:
+            xa._hipps_s2tap = s2tap
         if own_tap is not None:
             own_tap.armed = True
         out = bn(y, residual, stats=part, res_tap=res_tap) if bn._fast_ok(y, residual) else bn(y, residual)

@@ -36,8 +36,12 @@ def test_conv1x1_matches_fp32_conv_and_stats(shape):
     assert y.is_contiguous(memory_format=torch.channels_last) and y.shape == ref.shape
     torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=2e-2)
     yf = y.float().permute(0, 2, 3, 1).reshape(-1, cout)  # stats are of the stored bf16 values
-    mt = native().conv1x1_mtiles(yf.shape[0])
-    assert part.shape == (2, cout, mt)
+    # one partial column per M tile of whichever core the tuner picked (first core: 128 rows,
+    # gemm2: 128 or 256)
+    M = yf.shape[0]
+    assert part.shape[:2] == (2, cout)
+    assert part.shape[2] in (native().conv1x1_mtiles(M), native().gemm2_mtiles(M, cout, cin, 128),
+                             native().gemm2_mtiles(M, cout, cin, 256))
     torch.testing.assert_close(part[0].sum(1), yf.sum(0), rtol=1e-4, atol=1e-2)
     torch.testing.assert_close(part[1].sum(1), (yf * yf).sum(0), rtol=1e-4, atol=1e-2)
 

@@ -80,15 +80,18 @@ def test_gpu_fused_eval_apply():
 
 
 @pytest.mark.gpu
-def test_gpu_resnet_fused_vs_unfused_step():
+@pytest.mark.parametrize("width", [16, 64])
+def test_gpu_resnet_fused_vs_unfused_step(width):
     """One autocast step of a small ResNet: the fused-BN model's grads are no further from an fp32
-    reference than the eager bf16 (MIOpen BN) model's grads are."""
+    reference than the eager bf16 (MIOpen BN) model's grads are.  width 64 puts every conv on the
+    MFMA paths (BNGradTap through the 3x3 input gradient, the downsample's compact stride-2
+    gradient summed in conv1's dgrad epilogue)."""
     import copy
 
     from hipps.models.resnet import ResNet, Bottleneck
 
     torch.manual_seed(3)
-    base = ResNet(Bottleneck, [1, 1], num_classes=10, width=16, zero_init_residual=False).cuda()
+    base = ResNet(Bottleneck, [1, 1], num_classes=10, width=width, zero_init_residual=False).cuda()
     base = base.to(memory_format=torch.channels_last)
     models = {k: copy.deepcopy(base) for k in ("fused", "eager", "fp32")}
     for k in ("eager", "fp32"):

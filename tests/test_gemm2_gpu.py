@@ -166,3 +166,139 @@ def test_gemm2_wgrad_wide_tiles(cfg, cin, cout, k, h, stride):
     C().gemm2_wgrad(dy, x, d1, k, k, stride, pad, h, h, cfg)
     torch.cuda.synchronize()
     torch.testing.assert_close(d1, d0, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("bm,bn", [(128, 128), (256, 256), (128, 64)])
+@pytest.mark.parametrize("bits", [False, True])
+def test_gemm2_3x3_bn_backward_epilogue(bm, bn, bits):
+    """Stride-1 3x3 input gradient run as a forward conv (rot180(W)^T) with the backward reduction
+    of the BN whose output gradient it is in the epilogue (ResNet bn1 -> conv2): output equals the
+    plain implicit GEMM bit for bit, partials equal fp32 torch sums of dz = dy * relu' and
+    dz * x-hat on the stored bf16 dy."""
+    n, h, cin, cout = 2, 13, 128, 256  # dgrad-as-forward: dy [n, cin, h, h] (*) wf [cout, cin, 3, 3]
+    if cout % bn:
+        pytest.skip("tile")
+    dy = _x(n, cin, h, 11)
+    wf = (torch.randn(cout, cin, 3, 3, device=DEV) / (9 * cin) ** 0.5).to(torch.bfloat16).contiguous(memory_format=CL)
+    M = n * h * h
+    bx = _x(n, cout, h, 12)
+    mean = torch.randn(cout, device=DEV) * 0.1
+    inv = torch.rand(cout, device=DEV) + 0.5
+    sc = torch.randn(cout, device=DEV)
+    sh = torch.randn(cout, device=DEV) * 0.1
+    mbits = torch.randint(0, 256, (M * cout // 8,), dtype=torch.uint8, device=DEV) if bits else None
+    y0 = torch.empty(n, cout, h, h, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
+    y1 = torch.full_like(y0, 5.0)
+    C().gemm2_conv(dy, wf, y0, None, None, None, h, h, 1, 3, 3, 1, bm, bn)
+    p = torch.empty(2, cout, C().gemm2_mtiles(M, cout, 9 * cin, bm), device=DEV)
+    C().gemm2_conv(dy, wf, y1, p, None, None, h, h, 1, 3, 3, 1, bm, bn, bx, mbits, mean, inv, sc, sh)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    d = y1.permute(0, 2, 3, 1).reshape(M, cout).float()
+    xv = bx.permute(0, 2, 3, 1).reshape(M, cout).float()
+    if bits:
+        on = ((mbits.view(-1, 1) >> torch.arange(8, device=DEV, dtype=torch.uint8)) & 1).view(M, cout).bool()
+    else:
+        on = xv * sc + sh > 0
+    dz = torch.where(on, d, torch.zeros_like(d))
+    torch.testing.assert_close(p[0].sum(1), dz.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(p[1].sum(1), (dz * (xv - mean) * inv).sum(0), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("bm,bn", [(256, 128), (128, 128), (128, 64), (256, 64)])
+@pytest.mark.parametrize("kind", ["1x1", "1x1_k64", "3x3", "3x3_s2", "dgrad_bst_add"])
+def test_gemm2_three_stage_pipeline_bitwise(bm, bn, kind):
+    """3 LDS stages (one tile's DMA in flight across every barrier, counted vmcnt) accumulate in
+    the same order as the 2-stage loop: outputs and partials bit-identical, every K-tile count
+    (1, 2, 3+ tiles: prologue / drain edges)."""
+    n, h = 2, 11
+    cin, cout, k, st = {"1x1": (320, 256, 1, 1), "1x1_k64": (64, 256, 1, 1), "3x3": (128, 256, 3, 1),
+                        "3x3_s2": (64, 128, 3, 2), "dgrad_bst_add": (256, 256, 1, 1)}[kind]
+    if cout % bn:
+        pytest.skip("tile")
+    x = _x(n, cin, h, 21)
+    if k == 1:
+        w = (torch.randn(cout, cin, device=DEV) / cin ** 0.5).to(torch.bfloat16)
+    else:
+        w = (torch.randn(cout, cin, k, k, device=DEV) / (k * k * cin) ** 0.5).to(torch.bfloat16).contiguous(
+            memory_format=CL)
+    pad = k // 2
+    ho = (h + 2 * pad - k) // st + 1
+    M = n * ho * ho
+    extra = {}
+    if kind == "dgrad_bst_add":
+        extra = dict(add=_x(n, cout, ho, 22), bn_x=_x(n, cout, ho, 23), bn_mean=torch.randn(cout, device=DEV) * 0.1,
+                     bn_invstd=torch.rand(cout, device=DEV) + 0.5, bn_scale=torch.randn(cout, device=DEV),
+                     bn_shift=torch.randn(cout, device=DEV) * 0.1)
+    outs = []
+    for ns in (2, 3):
+        y = torch.full((n, cout, ho, ho), 3.0, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
+        p = torch.empty(2, cout, C().gemm2_mtiles(M, cout, k * k * cin, bm), device=DEV)
+        C().gemm2_conv(x, w, y, p, extra.get("add"), None, h, h, st, k, k, pad, bm, bn, extra.get("bn_x"), None,
+                       extra.get("bn_mean"), extra.get("bn_invstd"), extra.get("bn_scale"), extra.get("bn_shift"),
+                       stages=ns)
+        outs.append((y, p))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    if kind != "dgrad_bst_add":
+        ref = F.conv2d(x.float(), w.float().view(cout, cin, k, k), stride=st, padding=pad)
+        torch.testing.assert_close(outs[1][0].float(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("cfg", [0, 1])
+@pytest.mark.parametrize("cin,cout,k,h,stride", [(256, 256, 1, 14, 1), (128, 256, 3, 15, 2), (64, 64, 3, 9, 1)])
+def test_gemm2_wgrad_three_stages_bitwise(cfg, cin, cout, k, h, stride):
+    """3-stage weight gradient: same slabs and per-slab order as 2 stages -> bit-identical when the
+    slab split matches (it can differ: 3 stages use more LDS, fewer resident blocks) else fp32-close."""
+    if cfg == 1 and (cout % 256 or cin % 128):
+        pytest.skip("tile")
+    n = 2
+    pad = k // 2
+    x = _x(n, cin, h, 31)
+    ho = (h + 2 * pad - k) // stride + 1
+    dy = _x(n, cout, ho, 32)
+    d2 = torch.empty(cout, cin, k, k, device=DEV).contiguous(memory_format=CL)
+    d3 = torch.full_like(d2, 9.0)
+    C().gemm2_wgrad(dy, x, d2, k, k, stride, pad, h, h, cfg, 2)
+    C().gemm2_wgrad(dy, x, d3, k, k, stride, pad, h, h, cfg, 3)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(d3, d2, rtol=1e-5, atol=1e-4)
+    ref = torch.ops.aten.convolution_backward(dy.float(), x.float(), d2.float(), None, [stride, stride], [pad, pad],
+                                              [1, 1], False, [0, 0], 1, [False, True, False])[1]
+    torch.testing.assert_close(d3, ref, rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("bm,bn", [(128, 128), (256, 256), (128, 64)])
+@pytest.mark.parametrize("h,bst", [(14, False), (13, True)])
+def test_gemm2_add_s2_compact_stride2_gradient(bm, bn, h, bst):
+    """conv1 dgrad + the downsample's compact stride-2 input gradient added on the even (h, w)
+    rows (kAddS2), odd sizes included: equals the same GEMM with the zero-filled full-size addend."""
+    n, cin, cout = 2, 256, 128  # dgrad: dy [M, cout] . wt [cin, cout]^T -> dx [M, cin]
+    if cin % bn:
+        pytest.skip("tile")
+    dy = _x(n, cout, h, 41)
+    wt = (torch.randn(cin, cout, device=DEV) / cout ** 0.5).to(torch.bfloat16)
+    hs = (h + 1) // 2
+    comp = _x(n, cin, hs, 42)
+    full = torch.zeros(n, cin, h, h, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
+    full[:, :, ::2, ::2] = comp
+    M = n * h * h
+    extra = ()
+    p1 = p2 = None
+    if bst:
+        bx = _x(n, cin, h, 43)
+        bits = torch.randint(0, 256, (M * cin // 8,), dtype=torch.uint8, device=DEV)
+        mean = torch.randn(cin, device=DEV) * 0.1
+        inv = torch.rand(cin, device=DEV) + 0.5
+        extra = (bx, bits, mean, inv, torch.ones_like(mean), torch.zeros_like(mean))
+        p1 = torch.empty(2, cin, C().gemm2_mtiles(M, cin, cout, bm), device=DEV)
+        p2 = torch.empty_like(p1)
+    y1 = torch.empty(n, cin, h, h, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
+    y2 = torch.full_like(y1, 7.0)
+    C().gemm2_conv(dy, wt, y1, p1, full, None, h, h, 1, 1, 1, 0, bm, bn, *extra)
+    C().gemm2_conv(dy, wt, y2, p2, comp, None, h, h, 1, 1, 1, 0, bm, bn, *extra, add_s2=True)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    if bst:
+        assert torch.equal(p1, p2)

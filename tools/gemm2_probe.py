@@ -26,7 +26,8 @@ GEMMS = [  # (M, K, N): ResNet-50 bs256 1x1 convolutions + large steady-state pr
 CONVS = [  # (Cin, H, Cout, stride): ResNet-50 bs256 3x3 convolutions (pad 1)
     (64, 56, 64, 1), (128, 56, 128, 2), (128, 28, 128, 1), (256, 28, 256, 2), (256, 14, 256, 1),
     (512, 14, 512, 2), (512, 7, 512, 1)]
-TILES = [(256, 256), (256, 128), (128, 128), (256, 64), (128, 64)]
+TILES = [(256, 256, 2), (256, 128, 2), (256, 128, 3), (128, 128, 2), (128, 128, 3), (256, 64, 2), (128, 64, 2),
+         (128, 64, 3)]  # (bm, bn, LDS stages)
 
 
 def timeit(fn, it):
@@ -53,17 +54,17 @@ def gemm_row(M, K, N, it):
     row = {"M": M, "K": K, "N": N}
     flop = 2.0 * M * N * K
     y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    for bm, bn in TILES:
+    for bm, bn, ns in TILES:
         if N % bn:
             continue
         y.zero_()
-        C.gemm2_conv(x, w, y, None, None, None, M, 1, bm=bm, bn=bn)
+        C.gemm2_conv(x, w, y, None, None, None, M, 1, bm=bm, bn=bn, stages=ns)
         torch.cuda.synchronize()
         err = rel_err(y[:4096], ref)
         assert err < 2e-2, (M, K, N, bm, bn, err)
-        ms = timeit(lambda: C.gemm2_conv(x, w, y, None, None, None, M, 1, bm=bm, bn=bn), it)
-        row[f"g2_{bm}x{bn}_ms"] = round(ms, 4)
-        row[f"g2_{bm}x{bn}_TF"] = round(flop / ms / 1e9, 1)
+        ms = timeit(lambda: C.gemm2_conv(x, w, y, None, None, None, M, 1, bm=bm, bn=bn, stages=ns), it)
+        row[f"g2_{bm}x{bn}s{ns}_ms"] = round(ms, 4)
+        row[f"g2_{bm}x{bn}s{ns}_TF"] = round(flop / ms / 1e9, 1)
     mt = C.gemm2_mtiles(M, N, K, 0)
     part = torch.empty(2, N, mt, device="cuda")
     ms = timeit(lambda: C.gemm2_conv(x, w, y, part, None, None, M, 1), it)
@@ -93,17 +94,17 @@ def conv_row(cin, h, cout, st, it):
     ref = F.conv2d(x[:4].float(), w.float(), stride=st, padding=1)
     row = {"Cin": cin, "H": h, "Cout": cout, "stride": st, "M": M}
     y = torch.empty(256, cout, ho, ho, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=cl)
-    for bm, bn in TILES:
+    for bm, bn, ns in TILES:
         if cout % bn:
             continue
         y.zero_()
-        C.gemm2_conv(x, w, y, None, None, None, h, h, st, 3, 3, 1, bm, bn)
+        C.gemm2_conv(x, w, y, None, None, None, h, h, st, 3, 3, 1, bm, bn, stages=ns)
         torch.cuda.synchronize()
         err = rel_err(y[:4], ref)
         assert err < 2e-2, (cin, h, cout, st, bm, bn, err)
-        ms = timeit(lambda: C.gemm2_conv(x, w, y, None, None, None, h, h, st, 3, 3, 1, bm, bn), it)
-        row[f"g2_{bm}x{bn}_ms"] = round(ms, 4)
-        row[f"g2_{bm}x{bn}_TF"] = round(flop / ms / 1e9, 1)
+        ms = timeit(lambda: C.gemm2_conv(x, w, y, None, None, None, h, h, st, 3, 3, 1, bm, bn, stages=ns), it)
+        row[f"g2_{bm}x{bn}s{ns}_ms"] = round(ms, 4)
+        row[f"g2_{bm}x{bn}s{ns}_TF"] = round(flop / ms / 1e9, 1)
     y1 = torch.empty_like(y)
     ms1 = timeit(lambda: C.convkxk_forward(x, w, y1, None, st, 1), it)
     row["g1_ms"] = round(ms1, 4)
