@@ -59,6 +59,17 @@ void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at:
                      c10::optional<at::Tensor> bn_mean, c10::optional<at::Tensor> bn_invstd,
                      c10::optional<at::Tensor> bn_scale, c10::optional<at::Tensor> bn_shift,
                      c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift);
+// norm.hip dual BN (downsample block tail)
+void bn_dual_forward(at::Tensor part3, int64_t nrb3, at::Tensor partd, int64_t nrbd, at::Tensor x3, at::Tensor xd,
+                     at::Tensor z, at::Tensor mask, at::Tensor w3, at::Tensor b3, at::Tensor rm3, at::Tensor rv3,
+                     at::Tensor mean3, at::Tensor invstd3, at::Tensor scale3, at::Tensor shift3, at::Tensor wd,
+                     at::Tensor bd, at::Tensor rmd, at::Tensor rvd, at::Tensor meand, at::Tensor invstdd,
+                     at::Tensor scaled, at::Tensor shiftd, int64_t C, double eps3, double mom3, double epsd,
+                     double momd);
+void bn_dual_backward(c10::optional<at::Tensor> part3, int64_t nrb3, at::Tensor dz, at::Tensor x3, at::Tensor xd,
+                      at::Tensor mask, at::Tensor w3, at::Tensor mean3, at::Tensor invstd3, at::Tensor wd,
+                      at::Tensor meand, at::Tensor invstdd, at::Tensor dx3, at::Tensor dxd, at::Tensor dw3,
+                      at::Tensor db3, at::Tensor dwd, at::Tensor dbd, int64_t C);
 // gemm2.hip
 int64_t gemm2_mtiles(int64_t M, int64_t N, int64_t K, int64_t bm);
 void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part,
@@ -147,6 +158,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_forward_partials", &hipps::bn_forward_partials, "BN fwd finalize+apply from producer-reduced partials");
   m.def("bn_backward_partials", &hipps::bn_backward_partials, "BN bwd finalize+apply from consumer-reduced partials");
   m.def("conv1x1_mtiles", &hipps::conv1x1_mtiles);
+  m.def("bn_dual_forward", &hipps::bn_dual_forward,
+        "z = relu(bn3(x3) + bnd(xd)) from producer partials: two finalizes + one apply (downsample block)");
+  m.def("bn_dual_backward", &hipps::bn_dual_backward,
+        "backward of bn_dual_forward: dx3 + the downsample BN's reduction in one pass, then dxd");
   m.def("gemm2_mtiles", &hipps::gemm2_mtiles, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("bm") = 0);
   m.def("gemm2_conv", &hipps::gemm2_conv, "second-generation MFMA conv GEMM (LDS-DMA staged, 256-row tiles)",
         py::arg("x"), py::arg("w"), py::arg("y"), py::arg("part") = py::none(), py::arg("add") = py::none(),

@@ -57,7 +57,7 @@ template <> struct Cfg<128, 64> { static constexpr int TM = 64, TN = 32; };
 template <int BM, int BN> constexpr int nthreads() { return 64 * (BM / Cfg<BM, BN>::TM) * (BN / Cfg<BM, BN>::TN); }
 
 template <int BM, int BN, int NS = 2> constexpr int lds_bytes() {
-  constexpr int stage = NS * (BM + BN) * BK * 2;
+  constexpr int stage = (NS == 4 ? 2 : NS) * (BM + BN) * BK * 2;
   constexpr int epi = BM * (BN + 8) * 2;
   constexpr int wm = BM / Cfg<BM, BN>::TM;
   return (stage > epi ? stage : epi) + 2 * 2 * wm * BN * 4;
@@ -97,19 +97,31 @@ constexpr int waitcnt_lgkm(int n) { return 15 | (3 << 14) | (7 << 4) | ((n & 15)
 // (vmcnt(0)) before the next barrier.  3: tile k+2 is issued after the barrier of tile k and the
 // wait before each barrier is counted (vmcnt(glds per tile)), so one tile's DMA stays in flight
 // across every barrier (cdna_hip_programming.md §5 'Pipelining across barriers').
+// 4 (k-halves): the two stages' LDS split into four 32-deep units (rows of 64 bytes); one barrier
+// per unit, unit u+3 is issued right after the barrier of unit u into the slot unit u-1 just
+// freed, and each wait leaves the two younger units in flight (3 half-tiles of lead instead of 2,
+// with no drain before any barrier) -- same LDS bytes as 2 stages.
+__host__ __device__ constexpr int khalf_swz(int row) {  // conflict-free ds_read_b128 on 64-byte rows
+  return ((0x1320 >> (4 * ((row >> 2) & 3))) & 3);     // [0, 2, 3, 1][(row >> 2) & 3]
+}
+
 template <int BM, int BN, int EPI, bool TAPS, int NS>
 __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   constexpr int TM = Cfg<BM, BN>::TM, TN = Cfg<BM, BN>::TN;
   constexpr int WM = BM / TM, WN = BN / TN, NW = WM * WN, NT = 64 * NW;
   constexpr int FM = TM / 16, FN = TN / 16;
-  constexpr int STAGE = (BM + BN) * BK;   // elements per stage
-  constexpr int AI = BM / 8 / NW;         // A wave-instructions (8 rows x 128 B each) per stage per wave
-  constexpr int BI = BN / 8 / NW;
+  constexpr bool KH = NS == 4;
+  constexpr int STAGE = (BM + BN) * BK;   // elements per stage (KH: two 32-deep units)
+  constexpr int UNIT = (BM + BN) * 32;    // KH: elements per unit
+  constexpr int RPI = KH ? 16 : 8;        // rows per wave-instruction (1 KB)
+  constexpr int AI = BM / RPI / NW;       // A wave-instructions per stage (KH: per unit) per wave
+  constexpr int BI = BN / RPI / NW;
   constexpr int EP = BN + 8;              // epilogue row pitch (elements)
-  constexpr int SCR = (NS * STAGE * 2 > BM * EP * 2 ? NS * STAGE * 2 : BM * EP * 2);  // bytes before the stats scratch
+  constexpr int NSB = KH ? 2 : NS;        // stage-sized LDS buffers
+  constexpr int SCR = (NSB * STAGE * 2 > BM * EP * 2 ? NSB * STAGE * 2 : BM * EP * 2);  // bytes before the stats scratch
   static_assert(AI >= 1 && BI >= 1, "tile too small for the wave count");
-  static_assert(NS == 2 || NS == 3, "stages");
-  constexpr int NG = AI + BI;  // glds per tile per wave
+  static_assert(NS == 2 || NS == 3 || NS == 4, "stages");
+  constexpr int NG = AI + BI;  // glds per tile (KH: per unit) per wave
   __shared__ __attribute__((aligned(16))) uint16_t lds[lds_bytes<BM, BN, NS>() / 2];
 
   // bijective XCD-aware block order (cdna_hip_programming.md §5 'XCD swizzle must be bijective'):
@@ -121,7 +133,10 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = w / WN, wn = w - (w / WN) * WN;
-  const int lr = lane >> 3, lc = (lane & 7) ^ lr;  // row in the 8-row group, logical chunk fetched
+  // row in the wave-instruction's row group, logical chunk this lane fetches (the LDS slot is
+  // lane-linear; the swizzle is applied on the source)
+  const int lr = KH ? lane >> 2 : lane >> 3;
+  const int lc = KH ? (lane & 3) ^ khalf_swz(lr) : (lane & 7) ^ lr;
 
   // ---- per-lane sources (fixed over the K loop) ----
   const uint16_t* a_src[AI];  // 1x1: row base + chunk; TAPS: image base
@@ -129,7 +144,7 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   bool a_ok[AI];
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
-    const int row = 8 * (i * NW + w) + lr;
+    const int row = RPI * (i * NW + w) + lr;
     int m = m0 + row;
     a_ok[i] = m < g.M;
     m = a_ok[i] ? m : g.M - 1;
@@ -153,11 +168,10 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   }
   const uint16_t* b_src[BI];
 #pragma unroll
-  for (int i = 0; i < BI; ++i) b_src[i] = g.W + (int64_t)(n0 + 8 * (i * NW + w) + lr) * g.K + lc * 8;
+  for (int i = 0; i < BI; ++i) b_src[i] = g.W + (int64_t)(n0 + RPI * (i * NW + w) + lr) * g.K + lc * 8;
 
-  auto issue = [&](int kt, int s) {
-    const int k0 = kt * BK;
-    uint16_t* base = lds + s * STAGE;
+  // stage kt (KH: unit 2*kt + h, k0 = 64*kt + 32*h, rows of 32 elements) into LDS at ``base``
+  auto issue_at = [&](int k0, uint16_t* base, int rowlen) {
     if constexpr (TAPS) {
       const int tap = k0 / g.Cin, c0 = k0 - tap * g.Cin;
       const int kr = tap / g.KW, kc = tap - kr * g.KW;
@@ -166,15 +180,17 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
         const int hi = a_h[i] + kr, wi = a_w[i] + kc;
         const bool ok = a_ok[i] && hi >= 0 && hi < g.Hi && wi >= 0 && wi < g.Wi;
         const uint16_t* p = ok ? a_src[i] + ((int64_t)hi * g.Wi + wi) * g.Cin + c0 : kZero16;
-        glds16(p, base + 8 * (i * NW + w) * BK);
+        glds16(p, base + RPI * (i * NW + w) * rowlen);
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < AI; ++i) glds16(a_ok[i] ? a_src[i] + k0 : kZero16, base + 8 * (i * NW + w) * BK);
+      for (int i = 0; i < AI; ++i) glds16(a_ok[i] ? a_src[i] + k0 : kZero16, base + RPI * (i * NW + w) * rowlen);
     }
 #pragma unroll
-    for (int i = 0; i < BI; ++i) glds16(b_src[i] + k0, base + BM * BK + 8 * (i * NW + w) * BK);
+    for (int i = 0; i < BI; ++i) glds16(b_src[i] + k0, base + BM * rowlen + RPI * (i * NW + w) * rowlen);
   };
+  auto issue = [&](int kt, int s) { issue_at(kt * BK, lds + s * STAGE, BK); };
+  auto issue_unit = [&](int u) { issue_at(u * 32, lds + (u & 3) * UNIT, 32); };
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -206,87 +222,134 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   u32x4 pr[PF && ADDE ? NOUT : 1], px[PF && BSTE ? NOUT : 1];
   uint32_t prm[PF && ADDE ? NOUT : 1], pxm[PF && BSTE ? NOUT : 1];
 
-  const int KT = g.K / BK;
-  issue(0, 0);
-  if (NS == 3 && KT > 1) issue(1, 1);
-  int cur = 0;
-  for (int kt = 0; kt < KT; ++kt) {
-    // this wave's DMA of tile kt has landed and its reads of tile kt-1 are retired; after the
-    // barrier every wave's have, so tile kt is readable and tile kt-1's buffer is free to refill
-    if (NS == 3 && kt + 1 < KT) {
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm(NG));  // tile kt+1 stays in flight
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (kt + NS - 1 < KT) {
-      int nxt = cur + NS - 1;
-      nxt = nxt >= NS ? nxt - NS : nxt;
-      issue(kt + NS - 1, nxt);
-    } else if (kt + 1 < KT) {
-      // NS == 3, second-to-last tile: nothing left to issue
-    } else if constexpr (PF) {
+  // epilogue operands loaded during the MFMAs of the last K step (no DMA in flight then)
+  auto prefetch_epi = [&]() {
+    if constexpr (PF) {
 #pragma unroll
-      for (int i = 0; i < NOUT; ++i) {
-        const int id = t + NT * i;
-        const int row = id / RCH, c = id - row * RCH;
-        const int64_t o = (int64_t)(m0 + row < g.M ? m0 + row : m0) * g.N + n0 + c * 8;
-        if constexpr (ADDE) {
-          const int64_t ro = r_off(m0 + row < g.M ? m0 + row : m0, n0 + c * 8);
-          pr[i] = ro >= 0 ? *reinterpret_cast<const u32x4*>(g.R + ro) : u32x4{0u, 0u, 0u, 0u};
-          prm[i] = g.RM != nullptr ? g.RM[o >> 3] : 0xffu;
+        for (int i = 0; i < NOUT; ++i) {
+          const int id = t + NT * i;
+          const int row = id / RCH, c = id - row * RCH;
+          const int64_t o = (int64_t)(m0 + row < g.M ? m0 + row : m0) * g.N + n0 + c * 8;
+          if constexpr (ADDE) {
+            const int64_t ro = r_off(m0 + row < g.M ? m0 + row : m0, n0 + c * 8);
+            pr[i] = ro >= 0 ? *reinterpret_cast<const u32x4*>(g.R + ro) : u32x4{0u, 0u, 0u, 0u};
+            prm[i] = g.RM != nullptr ? g.RM[o >> 3] : 0xffu;
+          }
+          if constexpr (BSTE) {
+            px[i] = *reinterpret_cast<const u32x4*>(g.bx + o);
+            pxm[i] = BSTE == 2 ? g.bbits[o >> 3] : 0u;
+          }
         }
-        if constexpr (BSTE) {
-          px[i] = *reinterpret_cast<const u32x4*>(g.bx + o);
-          pxm[i] = BSTE == 2 ? g.bbits[o >> 3] : 0u;
-        }
-      }
     }
-    const uint16_t* As = lds + cur * STAGE;
-    cur = cur + 1 == NS ? 0 : cur + 1;
-    const uint16_t* Bs = As + BM * BK;
-    // FPF (one wave per SIMD): both k-steps' fragments are read up front, so the second step's
-    // reads are in flight while the first step's MFMAs run (counted lgkmcnt) instead of a
-    // read-wait-MFMA round per step; at two waves per SIMD (256x256) the other wave covers the
-    // read latency and the registers are not there for two fragment sets
-    constexpr bool FPF = NW <= 4;
-    constexpr int KS = BK / 32, FS = FPF ? KS : 1;
-    bf16x8 a[FS][FM], b[FS][FN];
-    auto frag = [&](int ks, int slot) {
-      const int c = ks * 4 + (lane >> 4);
+  };
+  if constexpr (KH) {
+    // k-half units: unit u = K rows [32u, 32u + 32) in LDS slot u & 3
+    const int NU = g.K / 32;
+    issue_unit(0);
+    if (NU > 1) issue_unit(1);
+    if (NU > 2) issue_unit(2);
+    for (int u = 0; u < NU; ++u) {
+      // unit u landed (this wave's DMAs; up to two younger units stay in flight), this wave's
+      // reads of unit u-1 retired; after the barrier the same holds for every wave
+      const int younger = (NU - 1 - u) < 2 ? (NU - 1 - u) : 2;
+      if (younger == 2) __builtin_amdgcn_s_waitcnt(waitcnt_vm(2 * NG));
+      else if (younger == 1) __builtin_amdgcn_s_waitcnt(waitcnt_vm(NG));
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (u + 3 < NU) issue_unit(u + 3);  // into slot (u + 3) & 3 == (u - 1) & 3, just freed
+      else if (u + 1 == NU) prefetch_epi();
+      const uint16_t* As = lds + (u & 3) * UNIT;
+      const uint16_t* Bs = As + BM * 32;
+      bf16x8 a[FM], b[FN];
+      const int c = lane >> 4;
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int row = wn * TN + j * 16 + (lane & 15);
-        b[slot][j] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + ((c ^ (row & 7)) << 3));
+        b[j] = *reinterpret_cast<const bf16x8*>(Bs + row * 32 + ((c ^ khalf_swz(row)) << 3));
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int row = wm * TM + i * 16 + (lane & 15);
-        a[slot][i] = *reinterpret_cast<const bf16x8*>(As + row * BK + ((c ^ (row & 7)) << 3));
-      }
-    };
-    if constexpr (FPF) {
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) frag(ks, ks);
-    }
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int slot = FPF ? ks : 0;
-      if constexpr (FPF) {
-        // step 0 needs its own FM + FN reads; the other step's stay in flight
-        if (ks == 0 && FM + FN <= 15) __builtin_amdgcn_s_waitcnt(waitcnt_lgkm(FM + FN));
-      } else {
-        frag(ks, 0);
+        a[i] = *reinterpret_cast<const bf16x8*>(As + row * 32 + ((c ^ khalf_swz(row)) << 3));
       }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[slot][i], b[slot][j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
+    }
+  } else {
+    const int KT = g.K / BK;
+    issue(0, 0);
+    if (NS == 3 && KT > 1) issue(1, 1);
+    int cur = 0;
+    for (int kt = 0; kt < KT; ++kt) {
+      // this wave's DMA of tile kt has landed and its reads of tile kt-1 are retired; after the
+      // barrier every wave's have, so tile kt is readable and tile kt-1's buffer is free to refill
+      if (NS == 3 && kt + 1 < KT) {
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(NG));  // tile kt+1 stays in flight
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt + NS - 1 < KT) {
+        int nxt = cur + NS - 1;
+        nxt = nxt >= NS ? nxt - NS : nxt;
+        issue(kt + NS - 1, nxt);
+      } else if (kt + 1 < KT) {
+        // NS == 3, second-to-last tile: nothing left to issue
+      } else {
+        prefetch_epi();
+      }
+      const uint16_t* As = lds + cur * STAGE;
+      cur = cur + 1 == NS ? 0 : cur + 1;
+      const uint16_t* Bs = As + BM * BK;
+      // FPF (one wave per SIMD): both k-steps' fragments are read up front, so the second step's
+      // reads are in flight while the first step's MFMAs run (counted lgkmcnt) instead of a
+      // read-wait-MFMA round per step; at two waves per SIMD (256x256) the other wave covers the
+      // read latency and the registers are not there for two fragment sets
+      constexpr bool FPF = NW <= 4;
+      constexpr int KS = BK / 32, FS = FPF ? KS : 1;
+      bf16x8 a[FS][FM], b[FS][FN];
+      auto frag = [&](int ks, int slot) {
+        const int c = ks * 4 + (lane >> 4);
+  #pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int row = wn * TN + j * 16 + (lane & 15);
+          b[slot][j] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + ((c ^ (row & 7)) << 3));
+        }
+  #pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int row = wm * TM + i * 16 + (lane & 15);
+          a[slot][i] = *reinterpret_cast<const bf16x8*>(As + row * BK + ((c ^ (row & 7)) << 3));
+        }
+      };
+      if constexpr (FPF) {
+  #pragma unroll
+        for (int ks = 0; ks < KS; ++ks) frag(ks, ks);
+      }
+  #pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int slot = FPF ? ks : 0;
+        if constexpr (FPF) {
+          // step 0 needs its own FM + FN reads; the other step's stay in flight
+          if (ks == 0 && FM + FN <= 15) __builtin_amdgcn_s_waitcnt(waitcnt_lgkm(FM + FN));
+        } else {
+          frag(ks, 0);
+        }
+        __builtin_amdgcn_s_setprio(1);
+  #pragma unroll
+        for (int i = 0; i < FM; ++i)
+  #pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[slot][i], b[slot][j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
     }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -486,20 +549,27 @@ constexpr int kWM = 64;  // m rows per stage
 
 // TN x TK output tile on WN x WK waves (each (TN/WN) x (TK/WK) of 16x16 accumulators)
 // NS LDS stages as in k_gemm (3: one stage's DMA in flight across every barrier)
-template <int TN, int TK, int WN, int WK, int NS>
+// MT (multi-tap): TK > Cin, each 16-byte X chunk takes its own tap (k = tap*Cin + c); K may be
+// padded up to a multiple of TK (columns past K read the zero page and are not stored) -- the
+// 64-channel 3x3 layers, whose 64-wide tiles are LDS-read bound
+template <int TN, int TK, int WN, int WK, int NS, bool MT = false>
 __global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
   constexpr int NW = WN * WK;
-  constexpr int YT = kWM * TN * 2, XT = kWM * TK * 2;  // bytes per staged tile
+  // NS == 4 (k-half units, as k_gemm): 32-row units in 4 slots, two in flight at each barrier
+  constexpr bool KH = NS == 4;
+  constexpr int UR = KH ? 32 : kWM;                    // M rows per staged unit
+  constexpr int NSLOT = KH ? 4 : NS;
+  constexpr int YT = UR * TN * 2, XT = UR * TK * 2;    // bytes per staged unit
   constexpr int CY = TN / 8, CX = TK / 8;             // 16-byte chunks per staged row
   constexpr int RY = 64 / CY > 0 ? 64 / CY : 1;       // rows per wave-instruction (1 KB)
   constexpr int RX = 64 / CX > 0 ? 64 / CX : 1;
-  constexpr int IY = kWM / RY / NW, IX = kWM / RX / NW;  // wave-instructions per stage per wave
+  constexpr int IY = UR / RY / NW, IX = UR / RX / NW;  // wave-instructions per unit per wave
   constexpr int WTN = TN / WN, WTK = TK / WK;
   constexpr int FN = WTN / 16, FK = WTK / 16;
   static_assert(CY <= 64 && CX <= 64 && IY >= 1 && IX >= 1, "wgrad tile");
-  static_assert(NS == 2 || NS == 3, "stages");
-  constexpr int NG = IY + IX;  // glds per stage per wave
-  __shared__ __attribute__((aligned(16))) uint8_t lds[NS * (YT + XT)];
+  static_assert(NS >= 2 && NS <= 4, "stages");
+  constexpr int NG = IY + IX;  // glds per unit per wave
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NSLOT * (YT + XT)];
   const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
   const int tiles = g.tn * g.tk;
@@ -511,14 +581,29 @@ __global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
   const int wn = w / WK, wk = w - (w / WK) * WK;
   const int tap = k0 / g.Cin, c0 = k0 - tap * g.Cin;
   const int kr = tap / g.KW, kc = tap - kr * g.KW;
-  const bool direct = g.KW == 1 && g.pad == 0 && g.stride == 1 && g.Cin == g.K;
+  const bool direct = !MT && g.KW == 1 && g.pad == 0 && g.stride == 1 && g.Cin == g.K;
   // lane -> (row within the wave-instruction, logical chunk); the LDS slot is lane % C
   const int ry = lane / CY, sy = lane % CY, rx = lane / CX, sx = lane % CX;
+  // MT: per X wave-instruction, this lane's chunk column -> (tap row, tap col, channel, in K)
+  int xkr[MT ? IX : 1], xkc[MT ? IX : 1], xch[MT ? IX : 1];
+  bool xin[MT ? IX : 1];
+  if constexpr (MT) {
+#pragma unroll
+    for (int i = 0; i < IX; ++i) {
+      const int row = (i * NW + w) * RX + rx;
+      const int kk = k0 + (sx ^ wswz<TK>(row)) * 8;
+      const int tp = kk / g.Cin;
+      xin[i] = kk < g.K;
+      xkr[i] = tp / g.KW;
+      xkc[i] = tp - xkr[i] * g.KW;
+      xch[i] = kk - tp * g.Cin;
+    }
+  }
 
   auto issue = [&](int st, int s) {
     uint8_t* ty = lds + s * (YT + XT);
     uint8_t* tx = ty + YT;
-    const int mb = mbeg + st * kWM;
+    const int mb = mbeg + st * UR;
 #pragma unroll
     for (int i = 0; i < IY; ++i) {
       const int row = (i * NW + w) * RY + ry;
@@ -539,9 +624,11 @@ __global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
         } else {
           const int img = (int)fdiv2((uint32_t)m, g.fd_hw), rem = m - img * (int)g.fd_hw.d;
           const int ho = (int)fdiv2((uint32_t)rem, g.fd_w), wo = rem - ho * g.Wo;
-          const int hi = ho * g.stride - g.pad + kr, wi = wo * g.stride - g.pad + kc;
-          if (hi >= 0 && hi < g.Hi && wi >= 0 && wi < g.Wi)
-            p = g.X + (((int64_t)img * g.Hi + hi) * g.Wi + wi) * g.Cin + c0 + ch * 8;
+          const int hi = ho * g.stride - g.pad + (MT ? xkr[MT ? i : 0] : kr);
+          const int wi = wo * g.stride - g.pad + (MT ? xkc[MT ? i : 0] : kc);
+          const bool inx = MT ? xin[MT ? i : 0] : true;
+          if (inx && hi >= 0 && hi < g.Hi && wi >= 0 && wi < g.Wi)
+            p = g.X + (((int64_t)img * g.Hi + hi) * g.Wi + wi) * g.Cin + (MT ? xch[MT ? i : 0] : c0 + ch * 8);
         }
       }
       glds16(p, tx + (i * NW + w) * 1024);
@@ -554,6 +641,35 @@ __global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
 #pragma unroll
     for (int j = 0; j < FK; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  if constexpr (KH) {
+    const int nu = (mend - mbeg + UR - 1) / UR;
+    issue(0, 0);
+    if (nu > 1) issue(1, 1);
+    if (nu > 2) issue(2, 2);
+    for (int u = 0; u < nu; ++u) {
+      const int younger = (nu - 1 - u) < 2 ? (nu - 1 - u) : 2;
+      if (younger == 2) __builtin_amdgcn_s_waitcnt(waitcnt_vm(2 * NG));
+      else if (younger == 1) __builtin_amdgcn_s_waitcnt(waitcnt_vm(NG));
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (u + 3 < nu) issue(u + 3, (u + 3) & 3);  // the slot unit u-1 just freed
+      const uint8_t* ty = lds + (u & 3) * (YT + XT);
+      const uint8_t* tx = ty + YT;
+      bf16x8 a[FN], b[FK];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) a[i] = tr_frag2<TN>(ty, 0, wn * WTN + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < FK; ++j) b[j] = tr_frag2<TK>(tx, 0, wk * WTK + j * 16, lane);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FK; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  } else {
   const int nst = (mend - mbeg + kWM - 1) / kWM;
   issue(0, 0);
   if (NS == 3 && nst > 1) issue(1, 1);
@@ -608,6 +724,7 @@ __global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
       __builtin_amdgcn_s_setprio(0);
     }
   }
+  }
   // D map: column (k) = lane & 15, row (n) = (lane >> 4) * 4 + r
   float* out = g.part + (int64_t)sidx * g.N * g.K;
 #pragma unroll
@@ -615,6 +732,7 @@ __global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
 #pragma unroll
     for (int j = 0; j < FK; ++j) {
       const int k = k0 + wk * WTK + j * 16 + (lane & 15);
+      if (MT && k >= g.K) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = n0 + wn * WTN + i * 16 + (lane >> 4) * 4 + r;
@@ -659,7 +777,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
                 c10::optional<at::Tensor> bn_invstd, c10::optional<at::Tensor> bn_scale,
                 c10::optional<at::Tensor> bn_shift, int64_t stages, bool add_s2) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "gemm2: device tensors");
-  TORCH_CHECK(stages == 2 || stages == 3, "gemm2: stages must be 2 or 3");
+  TORCH_CHECK(stages >= 2 && stages <= 4, "gemm2: stages must be 2, 3 or 4 (k-half units)");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
                   y.scalar_type() == at::kBFloat16, "gemm2: bf16 tensors");
   const int64_t N = w.size(0), K = w.numel() / N, Cin = K / (KH * KW);
@@ -748,6 +866,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
 #define HIPPS_G2(BMc, BNc, EPc, TPc) \
   do {                                                      \
     if (NS3) HIPPS_G2S(BMc, BNc, EPc, TPc, NS3_OF(BMc, BNc)); \
+    else if (NS4) HIPPS_G2S(BMc, BNc, EPc, TPc, 4);          \
     else HIPPS_G2S(BMc, BNc, EPc, TPc, 2);                   \
   } while (0)
 #define HIPPS_G2_E(BMc, BNc)                                                                        \
@@ -777,7 +896,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
     }                                                                                               \
   } while (0)
   // 3 stages where they fit the LDS (not 256x256: 3 x 64 KB)
-  const bool NS3 = stages == 3;
+  const bool NS3 = stages == 3, NS4 = stages == 4;  // 4: k-half units (see k_gemm)
   TORCH_CHECK(!NS3 || !(BMv == 256 && BNv == 256), "gemm2: 3 stages do not fit a 256x256 tile");
 #define NS3_OF(BMc, BNc) ((BMc) == 256 && (BNc) == 256 ? 2 : 3)
   if (BMv == 256 && BNv == 256) HIPPS_G2_E(256, 256);
@@ -801,7 +920,8 @@ void wgrad_reduce_slabs(const at::Tensor& part, int64_t S, int64_t N, int64_t K,
 void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
                  int64_t Hi, int64_t Wi, int64_t cfg, int64_t stages) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dw.is_cuda(), "gemm2_wgrad: device tensors");
-  TORCH_CHECK(stages == 2 || (stages == 3 && cfg != 2), "gemm2_wgrad: stages 2, or 3 below the 256x256 tile");
+  TORCH_CHECK(stages == 2 || stages == 4 || (stages == 3 && cfg != 2),
+              "gemm2_wgrad: stages 2, 4 (k-half units), or 3 below the 256x256 tile");
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 && dw.scalar_type() == at::kFloat,
               "gemm2_wgrad: bf16 dy/x, f32 dw");
   TORCH_CHECK(dw.is_contiguous() || dw.is_contiguous(at::MemoryFormat::ChannelsLast), "gemm2_wgrad: dense dw");
@@ -820,6 +940,8 @@ void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t
   // cfg 0: 128|64 x 128|64 tile on 4 waves (64x64 each: the first core's tiling and slab split);
   // 1: 256 x 128 on 4 waves of 128x64; 2: 256 x 256 on 8 waves of 128x64 (a third of the LDS
   // bytes per MFMA of cfg 0: the transposing-read wgrad is LDS-bandwidth bound)
+  // 3: 128 x 256 and 4: 256 x 128 on 8 waves of 64x64 (more MFMA work per staged byte than cfg 0
+  // at two waves per SIMD; 3 stages fit)
   int TN = N % 128 == 0 ? 128 : 64, TK = Cin % 128 == 0 ? 128 : 64;
   if (cfg == 1) {
     TORCH_CHECK(N % 256 == 0 && Cin % 128 == 0, "gemm2_wgrad cfg 1 needs Cout % 256, Cin % 128");
@@ -827,10 +949,28 @@ void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t
   } else if (cfg == 2) {
     TORCH_CHECK(N % 256 == 0 && Cin % 256 == 0, "gemm2_wgrad cfg 2 needs Cout % 256, Cin % 256");
     TN = 256; TK = 256;
+  } else if (cfg == 3) {
+    TORCH_CHECK(N % 128 == 0 && Cin % 256 == 0, "gemm2_wgrad cfg 3 needs Cout % 128, Cin % 256");
+    TN = 128; TK = 256;
+  } else if (cfg == 4) {
+    TORCH_CHECK(N % 256 == 0 && Cin % 128 == 0, "gemm2_wgrad cfg 4 needs Cout % 256, Cin % 128");
+    TN = 256; TK = 128;
   }
-  const int64_t tn = N / TN, tk = K / TK, tiles = tn * tk;
+  // 5 / 6: multi-tap TN x 128 tiles for Cin == 64 KxK layers (2 taps per tile, K padded to a
+  // multiple of 128): 5 on 2 waves of TNx64, 6 on 4 waves of TNx32
+  const bool mt = cfg == 5 || cfg == 6;
+  if (mt) {
+    TORCH_CHECK(Cin == 64 && KH * KW > 1, "gemm2_wgrad cfg 5/6: 64-channel KxK layers");
+    TN = N % 128 == 0 && cfg == 6 ? 128 : 64;
+    TK = 128;
+  }
+  TORCH_CHECK(cfg >= 0 && cfg <= 6, "gemm2_wgrad: cfg 0..6");
+  const int64_t tn = N / TN, tk = (K + TK - 1) / TK, tiles = tn * tk;
+  TORCH_CHECK(mt || tk * TK == K, "gemm2_wgrad: K tile");
   int64_t resident = 256 * (cfg ? 1 : TN * TK == 128 * 128 ? 2 : TN * TK == 128 * 64 ? 3 : 5);
-  if (stages == 3) resident = 256 * std::max<int64_t>(1, 160 * 1024 / (3 * g2::kWM * (TN + TK) * 2));
+  if (cfg >= 3) resident = 256;
+  if (stages == 3 || mt)  // (stages 4 = the LDS bytes of 2)
+    resident = 256 * std::max<int64_t>(1, 160 * 1024 / ((stages == 4 ? 2 : stages) * g2::kWM * (TN + TK) * 2));
   int64_t S = std::max<int64_t>(1, resident / tiles);
   S = std::min<int64_t>(S, std::max<int64_t>(1, M / (8 * g2::kWM)));           // >= 8 stages per block
   S = std::min<int64_t>(S, std::max<int64_t>(1, M * (N + K) / (4 * N * K)));  // slabs <= operand bytes
@@ -849,18 +989,27 @@ void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t
   a.fd_hw = g2::make_fastdiv2((uint32_t)(Ho * Wo));
   a.fd_w = g2::make_fastdiv2((uint32_t)Wo);
   const int grid = (int)(S * tiles);
-#define HIPPS_W2(TNc, TKc, WNc, WKc)                                                                      \
-  do {                                                                                                  \
-    if (stages == 3) hipLaunchKernelGGL((g2::k_wgrad<TNc, TKc, WNc, WKc, 3>), grid, 64 * WNc * WKc, 0, stream, a); \
-    else hipLaunchKernelGGL((g2::k_wgrad<TNc, TKc, WNc, WKc, 2>), grid, 64 * WNc * WKc, 0, stream, a);            \
+#define HIPPS_W2M(TNc, TKc, WNc, WKc, MTc)                                                                         \
+  do {                                                                                                            \
+    if (stages == 3) hipLaunchKernelGGL((g2::k_wgrad<TNc, TKc, WNc, WKc, 3, MTc>), grid, 64 * WNc * WKc, 0, stream, a); \
+    else if (stages == 4) hipLaunchKernelGGL((g2::k_wgrad<TNc, TKc, WNc, WKc, 4, MTc>), grid, 64 * WNc * WKc, 0, stream, a); \
+    else hipLaunchKernelGGL((g2::k_wgrad<TNc, TKc, WNc, WKc, 2, MTc>), grid, 64 * WNc * WKc, 0, stream, a);            \
   } while (0)
-  if (cfg == 2) hipLaunchKernelGGL((g2::k_wgrad<256, 256, 2, 4, 2>), grid, 512, 0, stream, a);
+#define HIPPS_W2(TNc, TKc, WNc, WKc) HIPPS_W2M(TNc, TKc, WNc, WKc, false)
+  if (cfg == 2 && stages == 4) hipLaunchKernelGGL((g2::k_wgrad<256, 256, 2, 4, 4>), grid, 512, 0, stream, a);
+  else if (cfg == 2) hipLaunchKernelGGL((g2::k_wgrad<256, 256, 2, 4, 2>), grid, 512, 0, stream, a);
+  else if (cfg == 5) HIPPS_W2M(64, 128, 1, 2, true);
+  else if (cfg == 6 && TN == 128) HIPPS_W2M(128, 128, 2, 2, true);
+  else if (cfg == 6) HIPPS_W2M(64, 128, 1, 4, true);
+  else if (cfg == 3) HIPPS_W2(128, 256, 2, 4);
+  else if (cfg == 4) HIPPS_W2(256, 128, 4, 2);
   else if (cfg == 1) HIPPS_W2(256, 128, 2, 2);
   else if (TN == 128 && TK == 128) HIPPS_W2(128, 128, 2, 2);
   else if (TN == 128) HIPPS_W2(128, 64, 2, 2);
   else if (TK == 128) HIPPS_W2(64, 128, 2, 2);
   else HIPPS_W2(64, 64, 2, 2);
 #undef HIPPS_W2
+#undef HIPPS_W2M
   if (S > 1) {
     at::Tensor dwv = dw;
     wgrad_reduce_slabs(part, S, N, K, dwv, stream);

@@ -213,18 +213,25 @@ __global__ __launch_bounds__(kBlock) void k_bn_finalize_bwd(const float* __restr
   ck0[c] = (float)k0;
 }
 
-// y = act(x*scale + shift [+ res])
+// y = act(x*scale + shift [+ res]); with rsc/rsh the residual is itself a pre-BN tensor whose
+// BN is applied in the same pass: res*rsc + rsh (a ResNet downsample branch, never materialised)
 __global__ __launch_bounds__(kBlock) void k_bn_apply_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                          uint16_t* __restrict__ y, uint8_t* __restrict__ mbits,
                                                          const float* __restrict__ scale,
-                                                         const float* __restrict__ shift, int64_t M, int C, int relu) {
+                                                         const float* __restrict__ shift, int64_t M, int C, int relu,
+                                                         const float* __restrict__ rsc = nullptr,
+                                                         const float* __restrict__ rsh = nullptr) {
   const int G = C >> 3;
   const int64_t V = M * (int64_t)G, stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int c0 = (int)(v0 % G) * 8;  // fixed per lane: stride is a multiple of G
-  float sc[8], sh[8];
+  float sc[8], sh[8], rs[8], rh[8];
   load8f(scale + c0, sc);
   load8f(shift + c0, sh);
+  if (rsc) {
+    load8f(rsc + c0, rs);
+    load8f(rsh + c0, rh);
+  }
   for (int64_t v = v0; v < V; v += stride) {
     const int64_t off = v * 8;
     float xv[8];
@@ -234,6 +241,10 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_fwd(const uint16_t* __restr
     if (res) {
       float rv[8];
       load8(res + off, rv);
+      if (rsc) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rv[j] = fmaf(rv[j], rs[j], rh[j]);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) xv[j] += rv[j];
     }
@@ -311,6 +322,79 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_bwd(const uint16_t* __restr
     if (need_y) load8(y + o0, y0);
     const uint32_t m0 = need_b ? (uint32_t)mbits[v] : 0u;
     body(d0, x0, y0, m0, o0);
+  }
+}
+
+// Backward of z = relu(bn3(x3) + bnd(xd)) (ResNet downsample block), pass 1: with dz' = dz * bits,
+// dx3 = a3*dz' + k1*x3 + k0 (bn3's apply) and, in the same pass, the downsample BN's reduction
+// (sum dz', sum dz' * (xd - mean_d) * invstd_d) into per-WG partials -- the residual gradient dz'
+// is never written (pass 2 recomputes it from dz and the bits).
+template <int UNR>
+__global__ __launch_bounds__(kBlock) void k_bn_bwd_dual(const uint16_t* __restrict__ dz, const uint16_t* __restrict__ x3,
+                                                        const uint16_t* __restrict__ xd,
+                                                        const uint8_t* __restrict__ mbits,
+                                                        const float* __restrict__ ca, const float* __restrict__ ck1,
+                                                        const float* __restrict__ ck0, const float* __restrict__ meand,
+                                                        const float* __restrict__ invstdd, uint16_t* __restrict__ dx3,
+                                                        int64_t M, int C, int64_t rows_per_wg, int nrb,
+                                                        float* __restrict__ pa, float* __restrict__ pb) {
+  __shared__ float la[kBlock * 8], lb[kBlock * 8];
+  const int G = C >> 3, R = kBlock / G;
+  const int g = threadIdx.x % G, r = threadIdx.x / G;
+  const int c0 = g * 8;
+  float sa[8], sb[8], a[8], k1[8], k0[8], mu[8], is[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sa[j] = 0.f; sb[j] = 0.f; }
+  load8f(ca + c0, a);
+  load8f(ck1 + c0, k1);
+  load8f(ck0 + c0, k0);
+  load8f(meand + c0, mu);
+  load8f(invstdd + c0, is);
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_wg;
+  const int64_t r1 = min(M, r0 + rows_per_wg);
+  auto body = [&](const float* d, const float* xv, const float* xr, uint32_t mb, int64_t off) {
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float dzm = ((mb >> j) & 1u) ? d[j] : 0.f;
+      o[j] = fmaf(a[j], dzm, fmaf(k1[j], xv[j], k0[j]));
+      sa[j] += dzm;
+      sb[j] = fmaf(dzm, (xr[j] - mu[j]) * is[j], sb[j]);
+    }
+    store8(dx3 + off, o);
+  };
+  int64_t row = r0 + r;
+  for (; row + (UNR - 1) * (int64_t)R < r1; row += UNR * (int64_t)R) {
+    float d[UNR][8], xv[UNR][8], xr[UNR][8];
+    uint32_t mb[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int64_t rr = row + u * (int64_t)R;
+      const int64_t off = rr * C + c0;
+      load8(dz + off, d[u]);
+      load8(x3 + off, xv[u]);
+      load8(xd + off, xr[u]);
+      mb[u] = (uint32_t)mbits[rr * G + g];
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) body(d[u], xv[u], xr[u], mb[u], (row + u * (int64_t)R) * C + c0);
+  }
+  for (; row < r1; row += R) {
+    const int64_t off = row * C + c0;
+    float d[8], xv[8], xr[8];
+    load8(dz + off, d);
+    load8(x3 + off, xv);
+    load8(xd + off, xr);
+    body(d, xv, xr, (uint32_t)mbits[row * G + g], off);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { la[r * C + c0 + j] = sa[j]; lb[r * C + c0 + j] = sb[j]; }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += kBlock) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int q = 0; q < R; ++q) { s0 += la[q * C + c]; s1 += lb[q * C + c]; }
+    pa[(int64_t)c * nrb + blockIdx.x] = s0;
+    pb[(int64_t)c * nrb + blockIdx.x] = s1;
   }
 }
 
@@ -645,5 +729,100 @@ void bn_backward_partials(at::Tensor part, int64_t nrb, at::Tensor dy, at::Tenso
     case MASK_X: app(k_bn_apply_bwd<MASK_X>); break;
     default: app(k_bn_apply_bwd<MASK_BITS>); break;
   }
+}
+}  // namespace hipps
+
+namespace hipps {
+// z = relu(bn3(x3) + bnd(xd)) for a ResNet downsample block, both BNs' statistics from their
+// producers' epilogues (part3 [2, C, nrb3], partd [2, C, nrbd]): two finalizes and ONE apply pass
+// that reads x3 and the pre-BN downsample output xd -- the downsample BN's output is never
+// written or re-read.  mask: uint8 [M*C/8] ReLU bits of z.
+void bn_dual_forward(at::Tensor part3, int64_t nrb3, at::Tensor partd, int64_t nrbd, at::Tensor x3, at::Tensor xd,
+                     at::Tensor z, at::Tensor mask, at::Tensor w3, at::Tensor b3, at::Tensor rm3, at::Tensor rv3,
+                     at::Tensor mean3, at::Tensor invstd3, at::Tensor scale3, at::Tensor shift3, at::Tensor wd,
+                     at::Tensor bd, at::Tensor rmd, at::Tensor rvd, at::Tensor meand, at::Tensor invstdd,
+                     at::Tensor scaled, at::Tensor shiftd, int64_t C, double eps3, double mom3, double epsd,
+                     double momd) {
+  TORCH_CHECK(C % 8 == 0 && C <= kMaxC && C >= 8, "fused BN needs C % 8 == 0 and 8 <= C <= 2048");
+  const int64_t M = x3.numel() / C;
+  check_act(x3, "x3", M * C);
+  check_act(xd, "xd", M * C);
+  check_act(z, "z", M * C);
+  TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == at::kByte && mask.numel() == M * C / 8, "mask: uint8[M*C/8]");
+  for (const at::Tensor* p : {&part3, &partd})
+    TORCH_CHECK(p->is_cuda() && p->scalar_type() == at::kFloat && p->is_contiguous(), "partials: f32");
+  TORCH_CHECK(part3.numel() == 2 * C * nrb3 && partd.numel() == 2 * C * nrbd, "partials: [2, C, nrb]");
+  for (auto* t : {&w3, &b3, &rm3, &rv3, &mean3, &invstd3, &scale3, &shift3, &wd, &bd, &rmd, &rvd, &meand, &invstdd,
+                  &scaled, &shiftd})
+    check_vec(*t, "per-channel vector", (int)C);
+  auto stream = c10::hip::getCurrentHIPStream();
+  auto fin = [&](const at::Tensor& part, int64_t nrb, at::Tensor& w, at::Tensor& b, at::Tensor& rm, at::Tensor& rv,
+                 at::Tensor& mean, at::Tensor& invstd, at::Tensor& scale, at::Tensor& shift, double eps, double mom) {
+    const float* pa = part.data_ptr<float>();
+    hipLaunchKernelGGL(k_bn_finalize_fwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, pa, pa + C * nrb,
+                       (int)nrb, (int)C, M, w.data_ptr<float>(), b.data_ptr<float>(), (float)eps, (float)mom,
+                       rm.data_ptr<float>(), rv.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                       scale.data_ptr<float>(), shift.data_ptr<float>());
+  };
+  fin(part3, nrb3, w3, b3, rm3, rv3, mean3, invstd3, scale3, shift3, eps3, mom3);
+  fin(partd, nrbd, wd, bd, rmd, rvd, meand, invstdd, scaled, shiftd, epsd, momd);
+  hipLaunchKernelGGL(k_bn_apply_fwd, apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)x3.data_ptr(),
+                     (const uint16_t*)xd.data_ptr(), (uint16_t*)z.data_ptr(), (uint8_t*)mask.data_ptr(),
+                     scale3.data_ptr<float>(), shift3.data_ptr<float>(), M, (int)C, 1, scaled.data_ptr<float>(),
+                     shiftd.data_ptr<float>());
+}
+
+// Backward of bn_dual_forward: dx3 (bn3's input gradient), dxd (the downsample BN's), the four
+// affine gradients.  part3: bn3's backward reduction from the consumer's dgrad epilogue
+// (BNGradTap) or none (reduced here).  Passes: [reduce bn3] -> finalize -> dx3 + the downsample
+// BN's reduction in one pass (k_bn_bwd_dual) -> finalize -> dxd.
+void bn_dual_backward(c10::optional<at::Tensor> part3, int64_t nrb3, at::Tensor dz, at::Tensor x3, at::Tensor xd,
+                      at::Tensor mask, at::Tensor w3, at::Tensor mean3, at::Tensor invstd3, at::Tensor wd,
+                      at::Tensor meand, at::Tensor invstdd, at::Tensor dx3, at::Tensor dxd, at::Tensor dw3,
+                      at::Tensor db3, at::Tensor dwd, at::Tensor dbd, int64_t C) {
+  TORCH_CHECK(C % 8 == 0 && C <= kMaxC && C >= 8, "fused BN needs C % 8 == 0 and 8 <= C <= 2048");
+  const int64_t M = x3.numel() / C;
+  for (auto* t : {&dz, &x3, &xd, &dx3, &dxd}) check_act(*t, "activation", M * C);
+  TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == at::kByte && mask.numel() == M * C / 8, "mask: uint8[M*C/8]");
+  for (auto* t : {&w3, &mean3, &invstd3, &wd, &meand, &invstdd, &dw3, &db3, &dwd, &dbd})
+    check_vec(*t, "per-channel vector", (int)C);
+  auto stream = c10::hip::getCurrentHIPStream();
+  const auto* mbp = (const uint8_t*)mask.data_ptr();
+  int nrb;
+  const int64_t rows = pick_rows(M, (int)C, nrb);
+  at::Tensor p3;
+  int64_t n3 = nrb3;
+  if (part3.has_value() && part3->defined()) {
+    p3 = *part3;
+    TORCH_CHECK(p3.is_cuda() && p3.scalar_type() == at::kFloat && p3.is_contiguous() && p3.numel() == 2 * C * nrb3,
+                "part3: f32 [2, C, nrb3]");
+  } else {
+    p3 = at::empty({2, C, (int64_t)nrb}, w3.options());
+    n3 = nrb;
+    hipLaunchKernelGGL((k_bn_reduce<true, MASK_BITS, 4>), nrb, kBlock, 0, stream, (const uint16_t*)x3.data_ptr(),
+                       (const uint16_t*)dz.data_ptr(), nullptr, mbp, mean3.data_ptr<float>(), invstd3.data_ptr<float>(),
+                       nullptr, nullptr, M, (int)C, rows, nrb, p3[0].data_ptr<float>(), p3[1].data_ptr<float>());
+  }
+  auto coef3 = at::empty({3, C}, w3.options());
+  auto coefd = at::empty({3, C}, w3.options());
+  auto pd = at::empty({2, C, (int64_t)nrb}, w3.options());
+  auto finb = [&](const float* pa, int64_t n, at::Tensor& w, at::Tensor& mean, at::Tensor& invstd, at::Tensor& dw,
+                  at::Tensor& db, at::Tensor& coef) {
+    hipLaunchKernelGGL(k_bn_finalize_bwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, pa, pa + C * n, (int)n,
+                       (int)C, M, w.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                       dw.data_ptr<float>(), db.data_ptr<float>(), coef[0].data_ptr<float>(), coef[1].data_ptr<float>(),
+                       coef[2].data_ptr<float>());
+  };
+  finb(p3.data_ptr<float>(), n3, w3, mean3, invstd3, dw3, db3, coef3);
+  hipLaunchKernelGGL((k_bn_bwd_dual<4>), nrb, kBlock, 0, stream, (const uint16_t*)dz.data_ptr(),
+                     (const uint16_t*)x3.data_ptr(), (const uint16_t*)xd.data_ptr(), mbp, coef3[0].data_ptr<float>(),
+                     coef3[1].data_ptr<float>(), coef3[2].data_ptr<float>(), meand.data_ptr<float>(),
+                     invstdd.data_ptr<float>(), (uint16_t*)dx3.data_ptr(), M, (int)C, rows, nrb,
+                     pd[0].data_ptr<float>(), pd[1].data_ptr<float>());
+  finb(pd.data_ptr<float>(), nrb, wd, meand, invstdd, dwd, dbd, coefd);
+  hipLaunchKernelGGL(k_bn_apply_bwd<MASK_BITS>, apply_grid(M, (int)C), kBlock, 0, stream,
+                     (const uint16_t*)dz.data_ptr(), (const uint16_t*)xd.data_ptr(), nullptr, mbp, nullptr, nullptr,
+                     coefd[0].data_ptr<float>(), coefd[1].data_ptr<float>(), coefd[2].data_ptr<float>(),
+                     (uint16_t*)dxd.data_ptr(), nullptr, M, (int)C);
 }
 }  // namespace hipps

@@ -15,8 +15,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from hipps.ops.nn import (FusedBatchNorm2d, MaxPool2d, ResidualTap, bn_relu_conv1x1_ok, bn_relu_conv_bn,
-                          bn_relu_maxpool, conv2d, conv2d_bn, conv2d_stats, conv_bn, global_avg_pool,
-                          stem_block, stem_block_ok)
+                          bn_relu_maxpool, conv1x1_bn_input, conv1x1_ok, conv2d, conv2d_bn, conv2d_stats, conv_bn,
+                          dual_bn_relu, dual_bn_relu_ok, global_avg_pool, stem_block, stem_block_ok)
 
 # One switch for the whole zoo: fused BN(+residual)(+ReLU) HIP kernels on channels-last bf16,
 # standard PyTorch elsewhere.  HIPPS_FUSED_BN=0 restores the eager MIOpen path for A/B runs.
@@ -46,6 +46,9 @@ _FUSED_STEM_POOL = _FUSED_STEM and _os.environ.get("HIPPS_FUSED_STEMPOOL", "1") 
 # staging is latency-bound (A/B on one box: 10308 on / 10342 off img/s, profiles/ab_r2/stembwd_*)
 _FUSED_STEM_BWD = _FUSED_STEM_POOL and _os.environ.get("HIPPS_FUSED_STEMBWD", "0") != "0"
 _FUSED_PRO = _FUSED_CONV and _os.environ.get("HIPPS_FUSED_PRO", "0") != "0"
+# downsample blocks: the downsample BN applied inside bn3's apply pass (its output, the residual,
+# is never materialised) and both BNs' backward in two passes (ops.nn._DualBNRelu)
+_FUSED_DUAL = _FUSED_GRAD and _os.environ.get("HIPPS_FUSED_DUAL", "1") != "0"
 
 
 def _bn(c, relu=False):
@@ -85,6 +88,17 @@ class Bottleneck(nn.Module):
             tap = ResidualTap() if _FUSED_GRAD else None
             y = conv_bn(self.conv1, self.bn1, x, fuse=_FUSED_CONV, tap=tap, bn_grad=bng)
             idt = x
+        elif (_FUSED_DUAL and self.training and self.bn1.training and conv1x1_ok(self.conv1, x) and
+              conv1x1_ok(ds[0], x) and conv1x1_ok(self.conv3, x)):  # (conv3's input: bf16 channels-last too)
+            # downsample block with the downsample BN folded into bn3's apply (_DualBNRelu)
+            y1, p1, xa = conv1x1_bn_input(self.conv1, x, alias=True, bn_grad=bng)
+            y = self.bn1(y1, stats=p1) if self.bn1._fast_ok(y1, None) else self.bn1(y1)
+            xd, pd = conv1x1_bn_input(ds[0], xa)
+            y = conv2d_bn(self.conv2, self.bn2, y, fuse=_FUSED_WGRAD, bn_grad=bng)
+            x3, p3 = conv1x1_bn_input(self.conv3, y, bn_grad=bng)
+            if dual_bn_relu_ok(self.bn3, ds[1], x3, xd):
+                return dual_bn_relu(self.bn3, x3, p3, ds[1], xd, pd)
+            return self.bn3(x3, ds[1](xd, stats=pd), stats=p3)
         else:
             if _FUSED_GRAD:
                 y, xa = conv_bn(self.conv1, self.bn1, x, fuse=_FUSED_CONV, alias=True, bn_grad=bng)

@@ -161,16 +161,23 @@ def _conv_wgrad(dy, x, dw, kh, kw, stride, pad):
     name = "w2"
     if _GEMM2 and cout % 64 == 0 and cin % 64 == 0:
         cands = {"w2": first}
-        for cfg in (0, 1, 2):  # gemm2.hip k_wgrad tilings: 128x128 / 256x128 / 256x256 outputs
-            if cfg == 0 or (cout % 256 == 0 and cin % (128 * cfg) == 0):
-                for ns in ((2, 3) if cfg < 2 else (2,)):  # LDS stages (3 do not fit 256x256)
-                    cands[f"w3_{cfg}" + ("s3" if ns == 3 else "")] = (
+        # gemm2.hip k_wgrad tilings (Cout x Cin*taps outputs): 0 128x128 (4 waves), 1 256x128
+        # (4 waves), 2 256x256 (8 waves), 3 128x256 / 4 256x128 (8 waves of 64x64)
+        ok = {0: True, 1: cout % 256 == 0 and cin % 128 == 0, 2: cout % 256 == 0 and cin % 256 == 0,
+              3: cout % 128 == 0 and cin % 256 == 0, 4: cout % 256 == 0 and cin % 128 == 0}
+        # 5 / 6: 64-channel KxK layers, two taps per 128-wide tile (K padded): 2 / 4 waves
+        ok[5] = ok[6] = cin == 64 and kh * kw > 1
+        for cfg in (0, 1, 2, 3, 4, 5, 6):
+            if ok[cfg]:
+                # LDS stages (3 do not fit 256x256; 4 = 32-row k-half units, see gemm2.hip)
+                for ns in ((2, 3) if cfg != 2 else (2, 4)) + ((4,) if cfg == 0 else ()):
+                    cands[f"w3_{cfg}" + ("" if ns == 2 else f"s{ns}")] = (
                         lambda cfg=cfg, ns=ns: C.gemm2_wgrad(dy, x, dw, kh, kw, stride, pad, hi, wi, cfg, ns))
         if kh > 1 and cin < 128:
             cands["miopen"] = mio
         name = TUNER.pick(("wgrad", tuple(x.shape), cout, kh, kw, stride, pad), cands)
     if name.startswith("w3"):
-        C.gemm2_wgrad(dy, x, dw, kh, kw, stride, pad, hi, wi, int(name[3]), 3 if name.endswith("s3") else 2)
+        C.gemm2_wgrad(dy, x, dw, kh, kw, stride, pad, hi, wi, int(name[3]), int(name[5]) if len(name) > 4 else 2)
     elif name == "miopen":
         mio()
     else:
@@ -766,6 +773,80 @@ class _FusedBNAct(torch.autograd.Function):
         if tap is not None:
             tap.dy, tap.mask = dy, (mask if ctx.mode == MASK_BITS else None)
         return dx, dres, dw, db, None, None, None, None, None, None, None
+
+
+class _DualBNRelu(torch.autograd.Function):
+    """z = relu(bn3(x3) + bnd(xd)) for a ResNet downsample block, both training BNs' statistics
+    from their convs' epilogues: the downsample BN is applied inside bn3's apply pass
+    (norm.hip bn_dual_forward), so its output -- the residual -- is never written or re-read.
+    Backward (bn_dual_backward): bn3's input gradient and the downsample BN's reduction in one
+    pass (the residual gradient dz * bits is recomputed, never stored), then the downsample BN's
+    input gradient.  bn3's backward reduction may come from the consumer's dgrad epilogue
+    (BNGradTap on z, as for _FusedBNAct)."""
+
+    @staticmethod
+    def forward(ctx, x3, part3, w3, b3, rm3, rv3, eps3, mom3, xd, partd, wd, bd, rmd, rvd, epsd, momd):
+        C = x3.shape[1]
+        f32 = dict(dtype=torch.float32, device=x3.device)
+        v3 = [torch.empty(C, **f32) for _ in range(4)]
+        vd = [torch.empty(C, **f32) for _ in range(4)]
+        z = torch.empty_like(x3, memory_format=torch.channels_last)
+        mask = torch.empty(x3.numel() // 8, dtype=torch.uint8, device=x3.device)
+        native().bn_dual_forward(part3, part3.shape[2], partd, partd.shape[2], x3, xd, z, mask, w3, b3, rm3, rv3, *v3,
+                                 wd, bd, rmd, rvd, *vd, C, float(eps3), float(mom3), float(epsd), float(momd))
+        ctx.C = C
+        ctx.save_for_backward(x3, xd, mask, w3, v3[0], v3[1], wd, vd[0], vd[1])
+        ctx.bngrad = BNGradTap(x3, mask, v3[0], v3[1], v3[2], v3[3])
+        z._hipps_bngrad = ctx.bngrad
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        x3, xd, mask, w3, mean3, invstd3, wd, meand, invstdd = ctx.saved_tensors
+        dz = dz.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        bg, ctx.bngrad = ctx.bngrad, None
+        part3 = bg.part if bg is not None else None
+        if bg is not None:
+            bg.part = None
+        dx3 = torch.empty_like(x3, memory_format=torch.channels_last)
+        dxd = torch.empty_like(xd, memory_format=torch.channels_last)
+        dw3, db3, dwd, dbd = (torch.empty_like(w3) for _ in range(4))
+        native().bn_dual_backward(part3, 0 if part3 is None else part3.shape[2], dz, x3, xd, mask, w3, mean3, invstd3,
+                                  wd, meand, invstdd, dx3, dxd, dw3, db3, dwd, dbd, ctx.C)
+        return dx3, None, dw3, db3, None, None, None, None, dxd, None, dwd, dbd, None, None, None, None
+
+
+def dual_bn_relu_ok(bn3, bnd, x3, xd) -> bool:
+    """Can _DualBNRelu run relu(bn3(x3) + bnd(xd))?"""
+    return (bn3.training and bnd.training and bn3.relu and not bnd.relu and bn3._fast_ok(x3, None) and
+            bnd._fast_ok(xd, None) and x3.shape == xd.shape and bn3.weight.dtype == torch.float32 and
+            bnd.weight.dtype == torch.float32)
+
+
+def dual_bn_relu(bn3, x3, part3, bnd, xd, partd):
+    """relu(bn3(x3) + bnd(xd)) with both BNs' statistics partials from their producers
+    (callers check dual_bn_relu_ok first)."""
+    bn3._nbt_pending += 1
+    bnd._nbt_pending += 1
+    return _DualBNRelu.apply(x3, part3, bn3.weight, bn3.bias, bn3.running_mean, bn3.running_var, bn3.eps,
+                             bn3.momentum, xd, partd, bnd.weight, bnd.bias, bnd.running_mean, bnd.running_var,
+                             bnd.eps, bnd.momentum)
+
+
+def conv1x1_bn_input(conv: nn.Conv2d, x, tap=None, alias: bool = False, bn_grad: bool = False):
+    """The conv half of conv_bn for a 1x1 conv on the MFMA path: (y, part[, x_alias]) -- the conv
+    output and the following BN's statistics partials, with the same tap / alias / S2Tap /
+    BNGradTap wiring as conv_bn.  Callers check conv1x1_ok (and training) first."""
+    s = conv.stride[0]
+    own_tap = tap if s == 1 else None
+    bg = getattr(x, "_hipps_bngrad", None) if bn_grad else None
+    s2tap = S2Tap() if (alias and s == 1) else (getattr(x, "_hipps_s2tap", None) if s == 2 else None)
+    outs = conv1x1_stats(x, conv.weight, s, own_tap, alias and s == 1, bg, s2tap)
+    if own_tap is not None:
+        own_tap.armed = True
+    if alias and s == 1:
+        outs[2]._hipps_s2tap = s2tap
+    return outs
 
 
 def fused_bn_act(x, weight, bias, running_mean, running_var, eps=1e-5, momentum=0.1, relu=True, residual=None,

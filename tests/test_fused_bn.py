@@ -118,3 +118,57 @@ def test_gpu_resnet_fused_vs_unfused_step(width):
         if ef > 1.5 * ee + 1e-3 * g.norm().item() + 1e-6:
             worse.append((n, ef, ee))
     assert not worse, worse
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_part3", [False, True])
+def test_gpu_dual_bn_relu_matches_fp32(with_part3):
+    """relu(bn3(x3) + bnd(xd)) on _DualBNRelu (statistics from producer partials, the downsample BN
+    applied inside bn3's pass, backward in two passes) against fp32 torch BatchNorm autograd."""
+    from hipps.ops import nn as hnn
+    from hipps.ops._native import native
+
+    torch.manual_seed(5)
+    n, C, h = 4, 256, 9
+    cl = torch.channels_last
+    x3 = torch.randn(n, C, h, h, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    xd = (torch.randn(n, C, h, h, device="cuda") * 2 + 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
+    bn3, bnd = FusedBatchNorm2d(C, relu=True).cuda(), FusedBatchNorm2d(C).cuda()
+    with torch.no_grad():
+        for b in (bn3, bnd):
+            b.weight.uniform_(0.5, 1.5)
+            b.bias.uniform_(-0.2, 0.2)
+
+    def parts(x):  # producer-style partials [2, C, nrb] (sum, sum of squares per row block)
+        xf = x.permute(0, 2, 3, 1).reshape(-1, C).float()
+        blocks = xf.split(64)
+        return torch.stack([torch.stack([b.sum(0) for b in blocks], 1),
+                            torch.stack([(b * b).sum(0) for b in blocks], 1)]).contiguous()
+
+    a3 = x3.clone().requires_grad_(True)
+    ad = xd.clone().requires_grad_(True)
+    z = hnn.dual_bn_relu(bn3, a3, parts(x3), bnd, ad, parts(xd))
+    g = torch.randn_like(z)
+    if with_part3:  # bn3's backward reduction delivered by the consumer (as a dgrad epilogue would)
+        bg = z._hipps_bngrad
+        gf = g.float().permute(0, 2, 3, 1).reshape(-1, C)
+        bits = ((bg.mask.view(-1, 1) >> torch.arange(8, device="cuda", dtype=torch.uint8)) & 1).view(-1, C).bool()
+        dzm = torch.where(bits, gf, torch.zeros_like(gf))
+        xh = (x3.float().permute(0, 2, 3, 1).reshape(-1, C) - bg.mean) * bg.invstd
+        bg.part = torch.stack([dzm.sum(0), (dzm * xh).sum(0)]).view(2, C, 1).contiguous()
+    z.backward(g)
+    r3, rd = torch.nn.BatchNorm2d(C).cuda(), torch.nn.BatchNorm2d(C).cuda()
+    with torch.no_grad():
+        r3.weight.copy_(bn3.weight), r3.bias.copy_(bn3.bias), rd.weight.copy_(bnd.weight), rd.bias.copy_(bnd.bias)
+    f3 = x3.float().requires_grad_(True)
+    fd = xd.float().requires_grad_(True)
+    zr = torch.relu(r3(f3) + rd(fd))
+    zr.backward(g.float())
+    torch.testing.assert_close(z.float(), zr, rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(a3.grad.float(), f3.grad, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(ad.grad.float(), fd.grad, rtol=3e-2, atol=3e-2)
+    for mine, ref in ((bn3, r3), (bnd, rd)):
+        torch.testing.assert_close(mine.weight.grad, ref.weight.grad, rtol=2e-2, atol=5e-2)
+        torch.testing.assert_close(mine.bias.grad, ref.bias.grad, rtol=2e-2, atol=5e-2)
+        torch.testing.assert_close(mine.running_mean, ref.running_mean, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(mine.running_var, ref.running_var, rtol=1e-3, atol=1e-3)

@@ -205,12 +205,13 @@ def test_gemm2_3x3_bn_backward_epilogue(bm, bn, bits):
     torch.testing.assert_close(p[1].sum(1), (dz * (xv - mean) * inv).sum(0), rtol=1e-4, atol=1e-2)
 
 
-@pytest.mark.parametrize("bm,bn", [(256, 128), (128, 128), (128, 64), (256, 64)])
+@pytest.mark.parametrize("bm,bn", [(256, 256), (256, 128), (128, 128), (128, 64), (256, 64)])
 @pytest.mark.parametrize("kind", ["1x1", "1x1_k64", "3x3", "3x3_s2", "dgrad_bst_add"])
 def test_gemm2_three_stage_pipeline_bitwise(bm, bn, kind):
-    """3 LDS stages (one tile's DMA in flight across every barrier, counted vmcnt) accumulate in
-    the same order as the 2-stage loop: outputs and partials bit-identical, every K-tile count
-    (1, 2, 3+ tiles: prologue / drain edges)."""
+    """3 LDS stages (one tile's DMA in flight across every barrier, counted vmcnt) and the k-half
+    units (stages=4: 32-deep units, two in flight) accumulate in the same order as the 2-stage
+    loop: outputs and partials bit-identical, every K-tile count (1, 2, 3+ tiles: prologue /
+    drain edges)."""
     n, h = 2, 11
     cin, cout, k, st = {"1x1": (320, 256, 1, 1), "1x1_k64": (64, 256, 1, 1), "3x3": (128, 256, 3, 1),
                         "3x3_s2": (64, 128, 3, 2), "dgrad_bst_add": (256, 256, 1, 1)}[kind]
@@ -231,7 +232,7 @@ def test_gemm2_three_stage_pipeline_bitwise(bm, bn, kind):
                      bn_invstd=torch.rand(cout, device=DEV) + 0.5, bn_scale=torch.randn(cout, device=DEV),
                      bn_shift=torch.randn(cout, device=DEV) * 0.1)
     outs = []
-    for ns in (2, 3):
+    for ns in ((2, 4) if (bm, bn) == (256, 256) else (2, 3, 4)):
         y = torch.full((n, cout, ho, ho), 3.0, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
         p = torch.empty(2, cout, C().gemm2_mtiles(M, cout, k * k * cin, bm), device=DEV)
         C().gemm2_conv(x, w, y, p, extra.get("add"), None, h, h, st, k, k, pad, bm, bn, extra.get("bn_x"), None,
@@ -239,8 +240,9 @@ def test_gemm2_three_stage_pipeline_bitwise(bm, bn, kind):
                        stages=ns)
         outs.append((y, p))
     torch.cuda.synchronize()
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
+    for o in outs[1:]:
+        assert torch.equal(outs[0][0], o[0])
+        assert torch.equal(outs[0][1], o[1])
     if kind != "dgrad_bst_add":
         ref = F.conv2d(x.float(), w.float().view(cout, cin, k, k), stride=st, padding=pad)
         torch.testing.assert_close(outs[1][0].float(), ref, rtol=2e-2, atol=2e-2)
@@ -260,10 +262,13 @@ def test_gemm2_wgrad_three_stages_bitwise(cfg, cin, cout, k, h, stride):
     dy = _x(n, cout, ho, 32)
     d2 = torch.empty(cout, cin, k, k, device=DEV).contiguous(memory_format=CL)
     d3 = torch.full_like(d2, 9.0)
+    d4 = torch.full_like(d2, 9.0)
     C().gemm2_wgrad(dy, x, d2, k, k, stride, pad, h, h, cfg, 2)
     C().gemm2_wgrad(dy, x, d3, k, k, stride, pad, h, h, cfg, 3)
+    C().gemm2_wgrad(dy, x, d4, k, k, stride, pad, h, h, cfg, 4)  # k-half units: same slabs, same order
     torch.cuda.synchronize()
     torch.testing.assert_close(d3, d2, rtol=1e-5, atol=1e-4)
+    assert torch.equal(d4, d2)
     ref = torch.ops.aten.convolution_backward(dy.float(), x.float(), d2.float(), None, [stride, stride], [pad, pad],
                                               [1, 1], False, [0, 0], 1, [False, True, False])[1]
     torch.testing.assert_close(d3, ref, rtol=1e-3, atol=1e-2)
@@ -302,3 +307,27 @@ def test_gemm2_add_s2_compact_stride2_gradient(bm, bn, h, bst):
     assert torch.equal(y1, y2)
     if bst:
         assert torch.equal(p1, p2)
+
+
+@pytest.mark.parametrize("cfg", [3, 4, 5, 6])
+@pytest.mark.parametrize("ns", [2, 3, 4])
+@pytest.mark.parametrize("cin,cout,k,h,stride", [(256, 256, 1, 14, 1), (256, 256, 3, 9, 1), (128, 256, 3, 15, 2),
+                                                 (64, 64, 3, 13, 1), (64, 128, 3, 9, 2)])
+def test_gemm2_wgrad_eight_wave_and_multitap(cfg, ns, cin, cout, k, h, stride):
+    """8-wave 128x256 / 256x128 weight-gradient tiles (cfg 3 / 4) and the multi-tap tiles of the
+    64-channel KxK layers (cfg 5 / 6: two taps per 128-wide tile, K padded) against fp32 torch."""
+    ok = {3: cout % 128 == 0 and cin % 256 == 0, 4: cout % 256 == 0 and cin % 128 == 0,
+          5: cin == 64 and k > 1, 6: cin == 64 and k > 1}
+    if not ok[cfg]:
+        pytest.skip("tile")
+    n = 2
+    pad = k // 2
+    x = _x(n, cin, h, 51)
+    ho = (h + 2 * pad - k) // stride + 1
+    dy = _x(n, cout, ho, 52)
+    d = torch.full((cout, cin, k, k), 9.0, device=DEV).contiguous(memory_format=CL)
+    C().gemm2_wgrad(dy, x, d, k, k, stride, pad, h, h, cfg, ns)
+    torch.cuda.synchronize()
+    ref = torch.ops.aten.convolution_backward(dy.float(), x.float(), d.float(), None, [stride, stride], [pad, pad],
+                                              [1, 1], False, [0, 0], 1, [False, True, False])[1]
+    torch.testing.assert_close(d, ref, rtol=1e-3, atol=1e-2)
