@@ -71,6 +71,10 @@ void bn_dual_backward(c10::optional<at::Tensor> part3, int64_t nrb3, at::Tensor 
                       at::Tensor meand, at::Tensor invstdd, at::Tensor dx3, at::Tensor dxd, at::Tensor dw3,
                       at::Tensor db3, at::Tensor dwd, at::Tensor dbd, int64_t C);
 // gemm2.hip
+at::Tensor gemm2_dgrad_s2(at::Tensor dy, at::Tensor wf, at::Tensor dx, int64_t bm, int64_t bn,
+                          c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_bits,
+                          c10::optional<at::Tensor> bn_mean, c10::optional<at::Tensor> bn_invstd,
+                          c10::optional<at::Tensor> bn_scale, c10::optional<at::Tensor> bn_shift);
 int64_t gemm2_mtiles(int64_t M, int64_t N, int64_t K, int64_t bm);
 void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part,
                 c10::optional<at::Tensor> add, c10::optional<at::Tensor> add_mask, int64_t Hi, int64_t Wi,
@@ -170,6 +174,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bn_bits") = py::none(), py::arg("bn_mean") = py::none(), py::arg("bn_invstd") = py::none(),
         py::arg("bn_scale") = py::none(), py::arg("bn_shift") = py::none(), py::arg("stages") = 2,
         py::arg("add_s2") = false);
+  m.def("gemm2_dgrad_s2", &hipps::gemm2_dgrad_s2,
+        "stride-2 3x3 input gradient as four output-parity implicit GEMMs (+ BN-backward reduction)",
+        py::arg("dy"), py::arg("wf"), py::arg("dx"), py::arg("bm") = 128, py::arg("bn") = 128,
+        py::arg("bn_x") = py::none(), py::arg("bn_bits") = py::none(), py::arg("bn_mean") = py::none(),
+        py::arg("bn_invstd") = py::none(), py::arg("bn_scale") = py::none(), py::arg("bn_shift") = py::none());
   m.def("gemm2_wgrad", &hipps::gemm2_wgrad, "conv weight gradient on the LDS-DMA MFMA core (split-M slabs)",
         py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
         py::arg("Hi"), py::arg("Wi"), py::arg("cfg") = 0, py::arg("stages") = 2);

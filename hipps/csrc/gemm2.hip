@@ -45,7 +45,10 @@ __device__ __attribute__((aligned(64))) const uint16_t kZero16[32] = {0};
 // shift), kBstBits = the same with the BN's stored ReLU bits (gemm.hip BnBwdTap)
 // kAddS2 (with kAdd, 1x1 only): R is the compact input gradient of a stride-2 1x1 conv reading the
 // same tensor ([img, ceil(Ho/2), ceil(Wo/2), N]); it lands on the even (h, w) rows of Y only
-enum Epi : int { kPlain = 0, kStats = 1, kAdd = 2, kBst = 4, kBstBits = 8, kAddS2 = 16 };
+// kPar (with TAPS): one output-parity class (ph, pw) of a stride-2 KxK input gradient -- the rows
+// are the class's dx positions (2a+ph, 2b+pw), A is dy read at (a + tdr[t], b + tdc[t]) for the
+// class's taps t, whose weights sit at K offset tko[t] * Cin of B (rot180(W)^T, all taps)
+enum Epi : int { kPlain = 0, kStats = 1, kAdd = 2, kBst = 4, kBstBits = 8, kAddS2 = 16, kPar = 32 };
 
 template <int BM, int BN> struct Cfg;
 template <> struct Cfg<256, 256> { static constexpr int TM = 128, TN = 64; };
@@ -76,6 +79,10 @@ struct Args {
   const float *bmean, *binvstd, *bscale, *bshift;
   int M, N, K, Ho, Wo, Hi, Wi, stride, mtiles, ntiles;
   int KW, pad, Cin;  // implicit-GEMM geometry (TAPS)
+  int ldb;           // B row stride (elements; K unless kPar)
+  int pstride, pcol0;  // partials: row stride and first column (several launches share one array)
+  int ph, pw, Hx, Wx;  // kPar: output parity class and the dx grid
+  int tdr[4], tdc[4], tko[4];
 };
 
 __device__ __forceinline__ uint32_t add_bf16x2(uint32_t a, uint32_t b) {
@@ -111,6 +118,19 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   constexpr int WM = BM / TM, WN = BN / TN, NW = WM * WN, NT = 64 * NW;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr bool KH = NS == 4;
+  constexpr bool PAR = (EPI & kPar) != 0;
+  static_assert(!PAR || TAPS, "kPar needs the implicit-GEMM loader");
+  // output row of GEMM row m (kPar: the class's dx position)
+  auto orow = [&](int m) -> int64_t {
+    if constexpr (PAR) {
+      const int hw = g.Ho * g.Wo;
+      const int img = m / hw, rem = m - img * hw;
+      const int a = rem / g.Wo, b = rem - a * g.Wo;
+      return ((int64_t)img * g.Hx + 2 * a + g.ph) * g.Wx + 2 * b + g.pw;
+    } else {
+      return m;
+    }
+  };
   constexpr int STAGE = (BM + BN) * BK;   // elements per stage (KH: two 32-deep units)
   constexpr int UNIT = (BM + BN) * 32;    // KH: elements per unit
   constexpr int RPI = KH ? 16 : 8;        // rows per wave-instruction (1 KB)
@@ -152,8 +172,8 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
       const int hw = g.Ho * g.Wo;
       const int img = m / hw, rem = m - img * hw;
       const int ho = rem / g.Wo, wo = rem - ho * g.Wo;
-      a_h[i] = ho * g.stride - g.pad;
-      a_w[i] = wo * g.stride - g.pad;
+      a_h[i] = PAR ? ho : ho * g.stride - g.pad;
+      a_w[i] = PAR ? wo : wo * g.stride - g.pad;
       a_src[i] = g.X + (int64_t)img * g.Hi * g.Wi * g.Cin + lc * 8;
     } else {
       int64_t src = m;
@@ -168,13 +188,22 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   }
   const uint16_t* b_src[BI];
 #pragma unroll
-  for (int i = 0; i < BI; ++i) b_src[i] = g.W + (int64_t)(n0 + RPI * (i * NW + w) + lr) * g.K + lc * 8;
+  for (int i = 0; i < BI; ++i) b_src[i] = g.W + (int64_t)(n0 + RPI * (i * NW + w) + lr) * g.ldb + lc * 8;
 
   // stage kt (KH: unit 2*kt + h, k0 = 64*kt + 32*h, rows of 32 elements) into LDS at ``base``
   auto issue_at = [&](int k0, uint16_t* base, int rowlen) {
+    int bk = k0;  // B column of this K tile
     if constexpr (TAPS) {
       const int tap = k0 / g.Cin, c0 = k0 - tap * g.Cin;
-      const int kr = tap / g.KW, kc = tap - kr * g.KW;
+      int kr, kc;
+      if constexpr (PAR) {
+        kr = g.tdr[tap];
+        kc = g.tdc[tap];
+        bk = g.tko[tap] * g.Cin + c0;
+      } else {
+        kr = tap / g.KW;
+        kc = tap - kr * g.KW;
+      }
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
         const int hi = a_h[i] + kr, wi = a_w[i] + kc;
@@ -187,7 +216,7 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
       for (int i = 0; i < AI; ++i) glds16(a_ok[i] ? a_src[i] + k0 : kZero16, base + RPI * (i * NW + w) * rowlen);
     }
 #pragma unroll
-    for (int i = 0; i < BI; ++i) glds16(b_src[i] + k0, base + BM * rowlen + RPI * (i * NW + w) * rowlen);
+    for (int i = 0; i < BI; ++i) glds16(b_src[i] + bk, base + BM * rowlen + RPI * (i * NW + w) * rowlen);
   };
   auto issue = [&](int kt, int s) { issue_at(kt * BK, lds + s * STAGE, BK); };
   auto issue_unit = [&](int u) { issue_at(u * 32, lds + (u & 3) * UNIT, 32); };
@@ -229,7 +258,7 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
         for (int i = 0; i < NOUT; ++i) {
           const int id = t + NT * i;
           const int row = id / RCH, c = id - row * RCH;
-          const int64_t o = (int64_t)(m0 + row < g.M ? m0 + row : m0) * g.N + n0 + c * 8;
+          const int64_t o = orow(m0 + row < g.M ? m0 + row : m0) * g.N + n0 + c * 8;
           if constexpr (ADDE) {
             const int64_t ro = r_off(m0 + row < g.M ? m0 + row : m0, n0 + c * 8);
             pr[i] = ro >= 0 ? *reinterpret_cast<const u32x4*>(g.R + ro) : u32x4{0u, 0u, 0u, 0u};
@@ -410,7 +439,7 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
     const int id = t + NT * i;
     const int row = id / RCH, c = id - row * RCH;
     if (m0 + row < g.M) {
-      const int64_t o = (int64_t)(m0 + row) * g.N + n0 + c * 8;
+      const int64_t o = orow(m0 + row) * g.N + n0 + c * 8;
       uint4 v = *reinterpret_cast<const uint4*>(lds + row * EP + c * 8);
       if (ADD) {  // + R (* ReLU-mask bits): a second gradient path into Y
         u32x4 r;
@@ -479,8 +508,8 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
         sa += red[r * BN + t];
         sb += red[RL * BN + r * BN + t];
       }
-      g.pa[(int64_t)(n0 + t) * g.mtiles + mt] = sa;
-      g.pb[(int64_t)(n0 + t) * g.mtiles + mt] = sb;
+      g.pa[(int64_t)(n0 + t) * g.pstride + g.pcol0 + mt] = sa;
+      g.pb[(int64_t)(n0 + t) * g.pstride + g.pcol0 + mt] = sb;
     }
   }
   if (STATS && t < BN) {
@@ -490,8 +519,8 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
       sa += st[(i * BN + t) * 2];
       qa += st[(i * BN + t) * 2 + 1];
     }
-    g.pa[(int64_t)(n0 + t) * g.mtiles + mt] = sa;
-    g.pb[(int64_t)(n0 + t) * g.mtiles + mt] = qa;
+    g.pa[(int64_t)(n0 + t) * g.pstride + g.pcol0 + mt] = sa;
+    g.pb[(int64_t)(n0 + t) * g.pstride + g.pcol0 + mt] = qa;
   }
 }
 
@@ -806,6 +835,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.Ho = (int)Ho; a.Wo = (int)Wo; a.Hi = (int)Hi; a.Wi = (int)Wi;
   a.stride = (int)stride; a.mtiles = (int)mtiles; a.ntiles = (int)ntiles;
   a.KW = (int)KW; a.pad = (int)pad; a.Cin = (int)Cin;
+  a.ldb = (int)K; a.pstride = (int)mtiles; a.pcol0 = 0;
   int epi = g2::kPlain;
   if (part.has_value() && part->defined()) {
     TORCH_CHECK(part->is_cuda() && part->scalar_type() == at::kFloat && part->is_contiguous() &&
@@ -909,6 +939,124 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
 #undef HIPPS_G2
 #undef HIPPS_G2S
 #undef NS3_OF
+}
+
+// Input gradient of a stride-2 3x3 / pad-1 convolution as four output-parity classes (kPar): dx
+// positions (2a+ph, 2b+pw) take 1, 2, 2 and 4 taps of dy (the taps whose stride-2 footprint hits
+// them), each class one implicit GEMM writing its rows of dx -- every dx element written exactly
+// once, no zero fill, no scatter.  dy [img, Cout, Hd, Wd], wf = rot180(W)^T [Cin, Cout, 3, 3]
+// (channels-last, i.e. [Cin][3][3][Cout]), dx [img, Cin, Hx, Wx].  With bn_x: the backward
+// reduction of the BN whose output gradient dx is (epilogue kBst / kBstBits), all four classes'
+// partials in one [2, Cin, sum of m tiles] array, returned.
+at::Tensor gemm2_dgrad_s2(at::Tensor dy, at::Tensor wf, at::Tensor dx, int64_t bm, int64_t bn,
+                          c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_bits,
+                          c10::optional<at::Tensor> bn_mean, c10::optional<at::Tensor> bn_invstd,
+                          c10::optional<at::Tensor> bn_scale, c10::optional<at::Tensor> bn_shift) {
+  TORCH_CHECK(dy.is_cuda() && wf.is_cuda() && dx.is_cuda(), "gemm2_dgrad_s2: device tensors");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && wf.scalar_type() == at::kBFloat16 && dx.scalar_type() == at::kBFloat16,
+              "gemm2_dgrad_s2: bf16 tensors");
+  TORCH_CHECK(dy.dim() == 4 && dx.dim() == 4 && wf.dim() == 4 && wf.size(2) == 3 && wf.size(3) == 3,
+              "gemm2_dgrad_s2: 4-d tensors, 3x3 weight");
+  const int64_t imgs = dy.size(0), Cout = dy.size(1), Hd = dy.size(2), Wd = dy.size(3);
+  const int64_t Cin = dx.size(1), Hx = dx.size(2), Wx = dx.size(3);
+  TORCH_CHECK(dx.size(0) == imgs && wf.size(0) == Cin && wf.size(1) == Cout, "gemm2_dgrad_s2: shapes");
+  TORCH_CHECK((Hx - 1) / 2 + 1 == Hd && (Wx - 1) / 2 + 1 == Wd, "gemm2_dgrad_s2: dy must be the stride-2 / pad-1 output");
+  TORCH_CHECK(Cout % 64 == 0 && Cin % 64 == 0, "gemm2_dgrad_s2: Cin % 64 == 0, Cout % 64 == 0");
+  TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) && dx.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  wf.is_contiguous(at::MemoryFormat::ChannelsLast), "gemm2_dgrad_s2: channels-last tensors");
+  for (const at::Tensor* t : {&dy, &wf, &dx})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm2_dgrad_s2: 16-byte aligned tensors");
+  TORCH_CHECK(dx.numel() < (int64_t(1) << 31) && dy.numel() < (int64_t(1) << 31), "gemm2_dgrad_s2: size");
+  const int BMv = (int)bm, BNv = (int)bn;
+  TORCH_CHECK(Cin % BNv == 0, "gemm2_dgrad_s2: Cin must be a multiple of the block tile");
+  // classes: (ph, pw) -> rows Ma x Mb of dx positions, taps (dy offset, rot180 tap index)
+  int64_t Mc[4], mt[4], tot = 0;
+  for (int c = 0; c < 4; ++c) {
+    const int ph = c >> 1, pw = c & 1;
+    Mc[c] = imgs * ((Hx - ph + 1) / 2) * ((Wx - pw + 1) / 2);
+    mt[c] = (Mc[c] + BMv - 1) / BMv;
+    tot += mt[c];
+  }
+  const bool bst = bn_x.has_value() && bn_x->defined();
+  at::Tensor part;
+  int epi = g2::kPar;
+  g2::Args a{};
+  if (bst) {
+    TORCH_CHECK(bn_x->is_cuda() && bn_x->scalar_type() == at::kBFloat16 && bn_x->numel() == dx.numel() &&
+                    bn_x->is_contiguous(at::MemoryFormat::ChannelsLast), "gemm2_dgrad_s2: bn_x shaped like dx");
+    for (const c10::optional<at::Tensor>* v : {&bn_mean, &bn_invstd, &bn_scale, &bn_shift})
+      TORCH_CHECK(v->has_value() && (*v)->defined() && (*v)->is_cuda() && (*v)->scalar_type() == at::kFloat &&
+                      (*v)->is_contiguous() && (*v)->numel() == Cin, "gemm2_dgrad_s2: BN vectors must be f32 [Cin]");
+    part = at::empty({2, Cin, tot}, dy.options().dtype(at::kFloat));
+    a.pa = part.data_ptr<float>();
+    a.pb = a.pa + Cin * tot;
+    a.bx = (const uint16_t*)bn_x->data_ptr();
+    a.bmean = bn_mean->data_ptr<float>();
+    a.binvstd = bn_invstd->data_ptr<float>();
+    a.bscale = bn_scale->data_ptr<float>();
+    a.bshift = bn_shift->data_ptr<float>();
+    if (bn_bits.has_value() && bn_bits->defined()) {
+      TORCH_CHECK(bn_bits->is_cuda() && bn_bits->scalar_type() == at::kByte && bn_bits->numel() == dx.numel() / 8,
+                  "gemm2_dgrad_s2: bn_bits uint8[numel(dx)/8]");
+      a.bbits = (const uint8_t*)bn_bits->data_ptr();
+      epi |= g2::kBstBits;
+    } else {
+      epi |= g2::kBst;
+    }
+  }
+  a.X = (const uint16_t*)dy.data_ptr();
+  a.W = (const uint16_t*)wf.data_ptr();
+  a.Y = (uint16_t*)dx.data_ptr();
+  a.N = (int)Cin;
+  a.Hi = (int)Hd; a.Wi = (int)Wd; a.Cin = (int)Cout;
+  a.stride = 1; a.KW = 3; a.pad = 0;
+  a.ldb = (int)(9 * Cout);
+  a.Hx = (int)Hx; a.Wx = (int)Wx;
+  a.pstride = (int)tot;
+  a.ntiles = (int)(Cin / BNv);
+  auto stream = c10::hip::getCurrentHIPStream();
+  int64_t col = 0;
+  for (int c = 0; c < 4; ++c) {
+    const int ph = c >> 1, pw = c & 1;
+    // dx row 2a+ph takes dy row a + (ph + 1 - kr) / 2 for the kr of its parity
+    const int nkr = ph ? 2 : 1, nkc = pw ? 2 : 1;
+    int nt = 0;
+    for (int i = 0; i < nkr; ++i)
+      for (int j = 0; j < nkc; ++j) {
+        const int kr = ph ? 2 * i : 1, kc = pw ? 2 * j : 1;
+        a.tdr[nt] = (ph + 1 - kr) / 2;
+        a.tdc[nt] = (pw + 1 - kc) / 2;
+        a.tko[nt] = (2 - kr) * 3 + (2 - kc);  // rot180: wf tap (2-kr, 2-kc) holds W[.., kr, kc]
+        ++nt;
+      }
+    a.ph = ph; a.pw = pw;
+    a.Ho = (int)((Hx - ph + 1) / 2); a.Wo = (int)((Wx - pw + 1) / 2);
+    a.M = (int)Mc[c];
+    a.K = (int)(nt * Cout);
+    a.mtiles = (int)mt[c];
+    a.pcol0 = (int)col;
+    col += mt[c];
+    const int grid = (int)(mt[c] * a.ntiles);
+    if (grid == 0) continue;
+#define HIPPS_G2P(BMc, BNc)                                                                                          \
+  do {                                                                                                             \
+    if (epi == (g2::kPar | g2::kBst))                                                                              \
+      hipLaunchKernelGGL((g2::k_gemm<BMc, BNc, g2::kPar | g2::kBst, true, 2>), grid, (g2::nthreads<BMc, BNc>()), 0, \
+                         stream, a);                                                                               \
+    else if (epi == (g2::kPar | g2::kBstBits))                                                                     \
+      hipLaunchKernelGGL((g2::k_gemm<BMc, BNc, g2::kPar | g2::kBstBits, true, 2>), grid, (g2::nthreads<BMc, BNc>()), \
+                         0, stream, a);                                                                            \
+    else                                                                                                           \
+      hipLaunchKernelGGL((g2::k_gemm<BMc, BNc, g2::kPar, true, 2>), grid, (g2::nthreads<BMc, BNc>()), 0, stream, a); \
+  } while (0)
+    if (BMv == 256 && BNv == 256) HIPPS_G2P(256, 256);
+    else if (BMv == 128 && BNv == 128) HIPPS_G2P(128, 128);
+    else if (BMv == 128 && BNv == 64) HIPPS_G2P(128, 64);
+    else if (BMv == 256 && BNv == 64) HIPPS_G2P(256, 64);
+    else TORCH_CHECK(false, "gemm2_dgrad_s2: unsupported block tile ", BMv, "x", BNv);
+#undef HIPPS_G2P
+  }
+  return part;
 }
 
 void wgrad_reduce_slabs(const at::Tensor& part, int64_t S, int64_t N, int64_t K, at::Tensor& dw,

@@ -242,6 +242,48 @@ def _convkxk_gemm(x, w, stride, pad, stats: bool, bg=None):
     return run(name)
 
 
+def _dgrad_s2(dy, x, w, wf, bg=None):
+    """Input gradient of a stride-2 3x3 / pad-1 conv: the fastest of MIOpen's backward-data and the
+    gemm2 output-parity GEMMs (gemm2_dgrad_s2) per shape, the latter with the backward reduction of
+    the BN whose output x is (``bg``, BNGradTap) in its epilogue -- timed with what each leaves that
+    BN's backward.  Returns (dx, part or None)."""
+    C = native()
+    n, cin, h, wd = x.shape
+    cout = dy.shape[1]
+
+    def mio():
+        return torch.ops.aten.convolution_backward(dy, x, w, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1,
+                                                   [True, False, False])[0], None
+
+    def run(name):
+        if name == "miopen":
+            return mio()
+        bm, bn, _ = _g2_parse(name)
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        if bg is not None:
+            part = C.gemm2_dgrad_s2(dy, wf, dx, bm, bn, bg.x, bg.mask, bg.mean, bg.invstd, bg.scale, bg.shift)
+            return dx, part
+        C.gemm2_dgrad_s2(dy, wf, dx, bm, bn)
+        return dx, None
+
+    def timed(name):
+        dx, part = run(name)
+        if bg is not None:
+            mode = MASK_BITS if bg.mask is not None else MASK_X
+            d2, dgw, dgb = torch.empty_like(dx), torch.empty_like(bg.scale), torch.empty_like(bg.scale)
+            if part is None:
+                C.bn_backward(dx, bg.x, None, mode, bg.scale, bg.mean, bg.invstd, bg.scale, bg.shift, d2, None, dgw,
+                              dgb, cin, bg.mask)
+            else:
+                C.bn_backward_partials(part, part.shape[2], dx, bg.x, mode, bg.scale, bg.mean, bg.invstd, bg.scale,
+                                       bg.shift, d2, None, dgw, dgb, cin, bg.mask)
+
+    names = ["miopen"] + [nm for nm in ("g2_128x128", "g2_256x256", "g2_128x64", "g2_256x64") if cin % _g2_parse(nm)[1] == 0]
+    name = TUNER.pick(("dgrad_s2", n, cin, h, wd, cout, None if bg is None else bg.mask is not None),
+                      {nm: (lambda nm=nm: timed(nm)) for nm in names})
+    return run(name)
+
+
 class ResidualTap:
     """Hands a fused BN's residual gradient to the stride-1 1x1 conv that reads the same block
     input (ResNet identity blocks: x feeds conv1 and is bn3's residual).  bn3's backward stores
@@ -516,8 +558,10 @@ class _ConvKxK(torch.autograd.Function):
         ctx.wdtype = w_master.dtype
         ctx.own_wgrad = own_wgrad
         # x is the output of a fused BN whose only gradient is this conv's input gradient: the
-        # stride-1 input gradient (a forward conv on gemm2) reduces that BN's backward statistics
+        # input gradient (stride 1: a forward conv on gemm2; stride 2: the parity GEMMs) reduces
+        # that BN's backward statistics in its epilogue
         ctx.bngrad = bngrad if stride == 1 else None
+        ctx.bngrad_s2 = bngrad if stride == 2 else None
         ctx.set_materialize_grads(False)
         ctx.wf = _TSHADOWS.get(w_master.data_ptr()) if w_master.dtype == torch.float32 else None
         part = None
@@ -548,6 +592,7 @@ class _ConvKxK(torch.autograd.Function):
         s, p = ctx.geom
         bg, ctx.bngrad = ctx.bngrad, None
         if dy is None:
+            ctx.bngrad_s2 = None
             return None, None, None, None, None, None, None
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = None
@@ -566,6 +611,17 @@ class _ConvKxK(torch.autograd.Function):
                 native().convkxk_forward(dy, wf, dx, None, 1, p)
             else:
                 dx = torch.ops.aten.convolution(dy, wf, None, [1, 1], [p, p], [1, 1], False, [0, 0], 1)
+        elif (ctx.needs_input_grad[0] and _GEMM2 and s == 2 and p == 1 and k == 3 and w.shape[3] == 3 and
+              x.shape[1] % 64 == 0 and dy.shape[1] % 64 == 0):
+            # stride-2 3x3: four output-parity GEMMs (no zero fill), bn1's reduction in the epilogue
+            wf = ctx.wf if ctx.wf is not None and ctx.wf.dim() == 4 else None
+            if wf is None:
+                wf = torch.flip(w, (2, 3)).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+            bg2 = getattr(ctx, "bngrad_s2", None)
+            ctx.bngrad_s2 = None
+            dx, part = _dgrad_s2(dy, x, w, wf, bg2)
+            if bg2 is not None:
+                bg2.part = part
         elif ctx.needs_input_grad[0]:
             dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
                                                      [True, False, False])[0]

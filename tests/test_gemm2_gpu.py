@@ -331,3 +331,39 @@ def test_gemm2_wgrad_eight_wave_and_multitap(cfg, ns, cin, cout, k, h, stride):
     ref = torch.ops.aten.convolution_backward(dy.float(), x.float(), d.float(), None, [stride, stride], [pad, pad],
                                               [1, 1], False, [0, 0], 1, [False, True, False])[1]
     torch.testing.assert_close(d, ref, rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("bm,bn", [(128, 128), (256, 256), (128, 64), (256, 64)])
+@pytest.mark.parametrize("cin,cout,h,bst", [(128, 128, 14, False), (256, 128, 15, True), (64, 64, 9, False),
+                                            (128, 256, 8, True)])
+def test_gemm2_dgrad_stride2_parity_classes(bm, bn, cin, cout, h, bst):
+    """Stride-2 3x3 input gradient as four output-parity GEMMs (odd and even sizes) against fp32
+    torch, and its BN-backward epilogue partials against fp32 sums."""
+    if cin % bn:
+        pytest.skip("tile")
+    n = 2
+    ho = (h - 1) // 2 + 1
+    dy = _x(n, cout, ho, 61)
+    w = (torch.randn(cout, cin, 3, 3, device=DEV) / (9 * cout) ** 0.5).to(torch.bfloat16).contiguous(memory_format=CL)
+    wf = torch.flip(w, (2, 3)).transpose(0, 1).contiguous(memory_format=CL)
+    dx = torch.full((n, cin, h, h), 7.0, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
+    extra = ()
+    if bst:
+        bx = _x(n, cin, h, 62)
+        mean = torch.randn(cin, device=DEV) * 0.1
+        inv = torch.rand(cin, device=DEV) + 0.5
+        sc = torch.randn(cin, device=DEV)
+        sh = torch.randn(cin, device=DEV) * 0.1
+        extra = (bx, None, mean, inv, sc, sh)
+    part = C().gemm2_dgrad_s2(dy, wf, dx, bm, bn, *extra)
+    torch.cuda.synchronize()
+    ref = torch.ops.aten.convolution_backward(dy.float(), torch.zeros(n, cin, h, h, device=DEV), w.float(), None,
+                                              [2, 2], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False])[0]
+    torch.testing.assert_close(dx.float(), ref, rtol=2e-2, atol=2e-2)
+    if bst:
+        M = n * h * h
+        d = dx.permute(0, 2, 3, 1).reshape(M, cin).float()
+        xv = bx.permute(0, 2, 3, 1).reshape(M, cin).float()
+        dz = torch.where(xv * sc + sh > 0, d, torch.zeros_like(d))
+        torch.testing.assert_close(part[0].sum(1), dz.sum(0), rtol=1e-4, atol=1e-2)
+        torch.testing.assert_close(part[1].sum(1), (dz * (xv - mean) * inv).sum(0), rtol=1e-4, atol=1e-2)
