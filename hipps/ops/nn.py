@@ -41,6 +41,13 @@ _OWN_STEM = _os.environ.get("HIPPS_OWN_STEM", "1") != "0"
 # convolutions and the KxK forward / stride-1 input gradient; per shape the fastest of {gemm2
 # tiles, first core / MIOpen} is picked on first use (timed on the real operands) and cached
 _GEMM2 = _os.environ.get("HIPPS_GEMM2", "1") != "0"
+# downsample blocks: the stride-2 1x1 input gradient as a compact GEMM summed on conv1's even rows
+# (S2Tap) instead of MIOpen's zero-filled full-size gradient
+_S2TAP = _GEMM2 and _os.environ.get("HIPPS_S2TAP", "1") != "0"
+# stride-2 3x3 input gradient as four output-parity GEMMs (gemm2_dgrad_s2), measured against MIOpen.
+# Opt-in: the tuner picks it on two of the three layers by < 2 %, but the step is 0.07 ms slower
+# with it (same-box A/B 11099 on vs 11131 img/s off, profiles/r3b/ab/)
+_DGRAD_S2 = _GEMM2 and _os.environ.get("HIPPS_DGRAD_S2", "0") != "0"
 
 MASK_NONE, MASK_X, MASK_Y, MASK_BITS = 0, 1, 2, 3
 
@@ -400,7 +407,7 @@ class _Conv1x1(torch.autograd.Function):
         ctx.tap = tap
         # alias (conv1): the downsample's compact gradient arrives here; stride 2 (downsample): put
         # it here
-        ctx.s2tap = s2tap if (_GEMM2 and ((alias and stride == 1) or stride == 2)) else None
+        ctx.s2tap = s2tap if (_S2TAP and ((alias and stride == 1) or stride == 2)) else None
         ctx.save_for_backward(x, w)
         ctx.mark_non_differentiable(part)
         if alias:
@@ -611,7 +618,7 @@ class _ConvKxK(torch.autograd.Function):
                 native().convkxk_forward(dy, wf, dx, None, 1, p)
             else:
                 dx = torch.ops.aten.convolution(dy, wf, None, [1, 1], [p, p], [1, 1], False, [0, 0], 1)
-        elif (ctx.needs_input_grad[0] and _GEMM2 and s == 2 and p == 1 and k == 3 and w.shape[3] == 3 and
+        elif (ctx.needs_input_grad[0] and _DGRAD_S2 and s == 2 and p == 1 and k == 3 and w.shape[3] == 3 and
               x.shape[1] % 64 == 0 and dy.shape[1] % 64 == 0):
             # stride-2 3x3: four output-parity GEMMs (no zero fill), bn1's reduction in the epilogue
             wf = ctx.wf if ctx.wf is not None and ctx.wf.dim() == 4 else None
