@@ -247,7 +247,8 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   };
   constexpr int RCH = BN / 8;             // 16-byte chunks per output row
   constexpr int NOUT = BM * RCH / NT;     // output chunks per thread
-  constexpr bool PF = (ADDE != (BSTE != 0)) && NOUT * 5 <= 40;  // one operand stream, <= 40 registers
+  constexpr int NSTR = (ADDE ? 1 : 0) + (BSTE ? 1 : 0);       // epilogue operand streams
+  constexpr bool PF = NSTR > 0 && NOUT * 5 * NSTR <= 40;     // <= 40 registers
   u32x4 pr[PF && ADDE ? NOUT : 1], px[PF && BSTE ? NOUT : 1];
   uint32_t prm[PF && ADDE ? NOUT : 1], pxm[PF && BSTE ? NOUT : 1];
 
