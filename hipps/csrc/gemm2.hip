@@ -48,7 +48,11 @@ __device__ __attribute__((aligned(64))) const uint16_t kZero16[32] = {0};
 // kPar (with TAPS): one output-parity class (ph, pw) of a stride-2 KxK input gradient -- the rows
 // are the class's dx positions (2a+ph, 2b+pw), A is dy read at (a + tdr[t], b + tdc[t]) for the
 // class's taps t, whose weights sit at K offset tko[t] * Cin of B (rot180(W)^T, all taps)
-enum Epi : int { kPlain = 0, kStats = 1, kAdd = 2, kBst = 4, kBstBits = 8, kAddS2 = 16, kPar = 32 };
+// kPro (2 LDS stages): the A operand is a BatchNorm input x; the GEMM reads relu(x * psc + psh)
+// per K channel -- every thread transforms the 16-byte chunks it staged, in LDS, after its own
+// DMA landed and before the tile's barrier (rows / taps that read the zero page stay zero), so
+// the BN's output is never written (ResNet bn1 -> conv2, bn2 -> conv3)
+enum Epi : int { kPlain = 0, kStats = 1, kAdd = 2, kBst = 4, kBstBits = 8, kAddS2 = 16, kPar = 32, kPro = 64 };
 
 template <int BM, int BN> struct Cfg;
 template <> struct Cfg<256, 256> { static constexpr int TM = 128, TN = 64; };
@@ -83,6 +87,7 @@ struct Args {
   int pstride, pcol0;  // partials: row stride and first column (several launches share one array)
   int ph, pw, Hx, Wx;  // kPar: output parity class and the dx grid
   int tdr[4], tdc[4], tko[4];
+  const float *psc, *psh;  // kPro: per-channel scale / shift of the A operand's BN
 };
 
 __device__ __forceinline__ uint32_t add_bf16x2(uint32_t a, uint32_t b) {
@@ -119,7 +124,9 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr bool KH = NS == 4;
   constexpr bool PAR = (EPI & kPar) != 0;
+  constexpr bool PRO = (EPI & kPro) != 0;
   static_assert(!PAR || TAPS, "kPar needs the implicit-GEMM loader");
+  static_assert(!PRO || NS == 2, "kPro: 2 LDS stages");
   // output row of GEMM row m (kPar: the class's dx position)
   auto orow = [&](int m) -> int64_t {
     if constexpr (PAR) {
@@ -190,9 +197,25 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
 #pragma unroll
   for (int i = 0; i < BI; ++i) b_src[i] = g.W + (int64_t)(n0 + RPI * (i * NW + w) + lr) * g.ldb + lc * 8;
 
+  // kPro: which of this thread's A chunks of the staged tile hold data (not the zero page), and
+  // the BN scale / shift of its 8 channels -- loaded with the tile's DMA, used at the next barrier
+  uint32_t pro_ok = 0;
+  float pro_sc[PRO ? 8 : 1], pro_sh[PRO ? 8 : 1];
   // stage kt (KH: unit 2*kt + h, k0 = 64*kt + 32*h, rows of 32 elements) into LDS at ``base``
   auto issue_at = [&](int k0, uint16_t* base, int rowlen) {
     int bk = k0;  // B column of this K tile
+    if constexpr (PRO) {
+      const int ch = (TAPS ? k0 - (k0 / g.Cin) * g.Cin : k0) + lc * 8;
+      const float4 s0 = *reinterpret_cast<const float4*>(g.psc + ch);
+      const float4 s1 = *reinterpret_cast<const float4*>(g.psc + ch + 4);
+      const float4 h0 = *reinterpret_cast<const float4*>(g.psh + ch);
+      const float4 h1 = *reinterpret_cast<const float4*>(g.psh + ch + 4);
+      pro_sc[PRO ? 0 : 0] = s0.x; pro_sc[PRO ? 1 : 0] = s0.y; pro_sc[PRO ? 2 : 0] = s0.z; pro_sc[PRO ? 3 : 0] = s0.w;
+      pro_sc[PRO ? 4 : 0] = s1.x; pro_sc[PRO ? 5 : 0] = s1.y; pro_sc[PRO ? 6 : 0] = s1.z; pro_sc[PRO ? 7 : 0] = s1.w;
+      pro_sh[PRO ? 0 : 0] = h0.x; pro_sh[PRO ? 1 : 0] = h0.y; pro_sh[PRO ? 2 : 0] = h0.z; pro_sh[PRO ? 3 : 0] = h0.w;
+      pro_sh[PRO ? 4 : 0] = h1.x; pro_sh[PRO ? 5 : 0] = h1.y; pro_sh[PRO ? 6 : 0] = h1.z; pro_sh[PRO ? 7 : 0] = h1.w;
+      pro_ok = 0;
+    }
     if constexpr (TAPS) {
       const int tap = k0 / g.Cin, c0 = k0 - tap * g.Cin;
       int kr, kc;
@@ -210,10 +233,14 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
         const bool ok = a_ok[i] && hi >= 0 && hi < g.Hi && wi >= 0 && wi < g.Wi;
         const uint16_t* p = ok ? a_src[i] + ((int64_t)hi * g.Wi + wi) * g.Cin + c0 : kZero16;
         glds16(p, base + RPI * (i * NW + w) * rowlen);
+        if constexpr (PRO) pro_ok |= (ok ? 1u : 0u) << i;
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < AI; ++i) glds16(a_ok[i] ? a_src[i] + k0 : kZero16, base + RPI * (i * NW + w) * rowlen);
+      for (int i = 0; i < AI; ++i) {
+        glds16(a_ok[i] ? a_src[i] + k0 : kZero16, base + RPI * (i * NW + w) * rowlen);
+        if constexpr (PRO) pro_ok |= (a_ok[i] ? 1u : 0u) << i;
+      }
     }
 #pragma unroll
     for (int i = 0; i < BI; ++i) glds16(b_src[i] + bk, base + BM * rowlen + RPI * (i * NW + w) * rowlen);
@@ -324,6 +351,27 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      }
+      if constexpr (PRO) {  // relu(x * scale + shift) on this thread's landed chunks of tile kt
+        uint16_t* tb = lds + cur * STAGE;
+#pragma unroll
+        for (int i = 0; i < AI; ++i) {
+          if ((pro_ok >> i) & 1u) {
+            uint4* q = reinterpret_cast<uint4*>(tb + RPI * (i * NW + w) * BK + lane * 8);
+            const uint4 v = *q;
+            const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+            uint32_t o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float lo = fmaxf(fmaf(__uint_as_float(u[j] << 16), pro_sc[PRO ? 2 * j : 0], pro_sh[PRO ? 2 * j : 0]), 0.f);
+              const float hi = fmaxf(fmaf(__uint_as_float(u[j] & 0xffff0000u), pro_sc[PRO ? 2 * j + 1 : 0],
+                                          pro_sh[PRO ? 2 * j + 1 : 0]), 0.f);
+              o[j] = pack_bf16x2(lo, hi);
+            }
+            *q = make_uint4(o[0], o[1], o[2], o[3]);
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -551,6 +599,7 @@ struct WArgs {
   float* part;
   int M, N, K, Cin, Ho, Wo, Hi, Wi, stride, KW, pad, chunk, tn, tk;
   FastDiv2 fd_hw, fd_w;
+  const float *psc, *psh;  // PRO: the X operand is a BN input; the GEMM reads relu(x * psc + psh)
 };
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -582,7 +631,10 @@ constexpr int kWM = 64;  // m rows per stage
 // MT (multi-tap): TK > Cin, each 16-byte X chunk takes its own tap (k = tap*Cin + c); K may be
 // padded up to a multiple of TK (columns past K read the zero page and are not stored) -- the
 // 64-channel 3x3 layers, whose 64-wide tiles are LDS-read bound
-template <int TN, int TK, int WN, int WK, int NS, bool MT = false>
+// PRO (2 stages): BN + ReLU on the X operand, transformed in LDS by the thread that staged each
+// chunk after its own DMA landed (as k_gemm kPro); the per-channel scale / shift of the tile's
+// channels sit in a table at the end of the LDS array
+template <int TN, int TK, int WN, int WK, int NS, bool MT = false, bool PRO = false>
 __global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
   constexpr int NW = WN * WK;
   // NS == 4 (k-half units, as k_gemm): 32-row units in 4 slots, two in flight at each barrier
@@ -599,7 +651,10 @@ __global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
   static_assert(CY <= 64 && CX <= 64 && IY >= 1 && IX >= 1, "wgrad tile");
   static_assert(NS >= 2 && NS <= 4, "stages");
   constexpr int NG = IY + IX;  // glds per unit per wave
-  __shared__ __attribute__((aligned(16))) uint8_t lds[NSLOT * (YT + XT)];
+  static_assert(!PRO || NS == 2, "PRO: 2 stages");
+  constexpr int TT = PRO ? (MT ? 64 : TK) : 0;  // channels in the BN table
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NSLOT * (YT + XT) + 2 * TT * 4];
+  float* ptab = reinterpret_cast<float*>(lds + NSLOT * (YT + XT));  // [2][TT]: scale, shift
   const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
   const int tiles = g.tn * g.tk;
@@ -630,10 +685,20 @@ __global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
     }
   }
 
+  const int tc0 = MT ? 0 : c0;  // PRO: first channel of the table
+  if constexpr (PRO) {  // before any DMA is in flight (the barrier would drain it)
+    for (int c = t; c < TT; c += 64 * NW) {
+      ptab[c] = g.psc[tc0 + c];
+      ptab[TT + c] = g.psh[tc0 + c];
+    }
+    __syncthreads();
+  }
+  uint32_t xok = 0;  // PRO: this thread's X chunks of the staged stage that hold data
   auto issue = [&](int st, int s) {
     uint8_t* ty = lds + s * (YT + XT);
     uint8_t* tx = ty + YT;
     const int mb = mbeg + st * UR;
+    if constexpr (PRO) xok = 0;
 #pragma unroll
     for (int i = 0; i < IY; ++i) {
       const int row = (i * NW + w) * RY + ry;
@@ -662,6 +727,7 @@ __global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
         }
       }
       glds16(p, tx + (i * NW + w) * 1024);
+      if constexpr (PRO) xok |= (p != kZero16 ? 1u : 0u) << i;
     }
   };
 
@@ -710,6 +776,29 @@ __global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    if constexpr (PRO) {  // relu(x * scale + shift) on this thread's landed X chunks of stage st
+      uint8_t* txs = lds + cur * (YT + XT) + YT;
+#pragma unroll
+      for (int i = 0; i < IX; ++i) {
+        if ((xok >> i) & 1u) {
+          const int row = (i * NW + w) * RX + rx;
+          const int chan = (MT ? xch[MT ? i : 0] : c0 + (sx ^ wswz<TK>(row)) * 8) - tc0;
+          uint4* q = reinterpret_cast<uint4*>(txs + (i * NW + w) * 1024 + lane * 16);
+          const uint4 v = *q;
+          const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+          uint32_t o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float lo = fmaxf(fmaf(__uint_as_float(u[j] << 16), ptab[chan + 2 * j], ptab[TT + chan + 2 * j]), 0.f);
+            const float hi = fmaxf(fmaf(__uint_as_float(u[j] & 0xffff0000u), ptab[chan + 2 * j + 1],
+                                        ptab[TT + chan + 2 * j + 1]), 0.f);
+            o[j] = pack_bf16x2(lo, hi);
+          }
+          *q = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -805,7 +894,8 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
                 int64_t stride, int64_t KH, int64_t KW, int64_t pad, int64_t bm, int64_t bn,
                 c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_bits, c10::optional<at::Tensor> bn_mean,
                 c10::optional<at::Tensor> bn_invstd, c10::optional<at::Tensor> bn_scale,
-                c10::optional<at::Tensor> bn_shift, int64_t stages, bool add_s2) {
+                c10::optional<at::Tensor> bn_shift, int64_t stages, bool add_s2,
+                c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "gemm2: device tensors");
   TORCH_CHECK(stages >= 2 && stages <= 4, "gemm2: stages must be 2, 3 or 4 (k-half units)");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
@@ -890,6 +980,17 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
     TORCH_CHECK(!(epi & g2::kAdd), "gemm2: forward statistics and the add epilogue are exclusive");
     epi |= g2::kStats;
   }
+  if (pro_scale.has_value() && pro_scale->defined()) {
+    TORCH_CHECK(stages == 2 && epi == g2::kStats, "gemm2: the BN prologue runs with 2 stages and forward statistics");
+    for (const c10::optional<at::Tensor>* v : {&pro_scale, &pro_shift})
+      TORCH_CHECK(v->has_value() && (*v)->defined() && (*v)->is_cuda() && (*v)->scalar_type() == at::kFloat &&
+                      (*v)->is_contiguous() && (*v)->numel() == Cin &&
+                      reinterpret_cast<uintptr_t>((*v)->data_ptr()) % 16 == 0,
+                  "gemm2: prologue scale / shift must be 16-byte aligned f32 [Cin]");
+    a.psc = pro_scale->data_ptr<float>();
+    a.psh = pro_shift->data_ptr<float>();
+    epi |= g2::kPro;
+  }
   auto stream = c10::hip::getCurrentHIPStream();
   const int grid = (int)(mtiles * ntiles);
 #define HIPPS_G2S(BMc, BNc, EPc, TPc, NSc) \
@@ -904,6 +1005,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
   do {                                                                                              \
     if (taps) {                                                                                     \
       switch (epi) {                                                                                \
+        case g2::kStats | g2::kPro: HIPPS_G2S(BMc, BNc, (g2::kStats | g2::kPro), true, 2); break;    \
         case g2::kStats: HIPPS_G2(BMc, BNc, g2::kStats, true); break;                               \
         case g2::kBst: HIPPS_G2(BMc, BNc, g2::kBst, true); break;                                   \
         case g2::kBstBits: HIPPS_G2(BMc, BNc, g2::kBstBits, true); break;                           \
@@ -911,6 +1013,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
       }                                                                                             \
     } else {                                                                                        \
       switch (epi) {                                                                                \
+        case g2::kStats | g2::kPro: HIPPS_G2S(BMc, BNc, (g2::kStats | g2::kPro), false, 2); break;   \
         case g2::kStats: HIPPS_G2(BMc, BNc, g2::kStats, false); break;                              \
         case g2::kAdd: HIPPS_G2(BMc, BNc, g2::kAdd, false); break;                                  \
         case g2::kBst: HIPPS_G2(BMc, BNc, g2::kBst, false); break;                                  \
@@ -1067,8 +1170,11 @@ void wgrad_reduce_slabs(const at::Tensor& part, int64_t S, int64_t N, int64_t K,
 // bf16; dw f32 [Cout, KH, KW, Cin] in memory (the channels-last weight layout; 1x1: [Cout, Cin]).
 // Cout % 64 == 0, Cin % 64 == 0.  S split-M partial slabs (~2 resident blocks per CU) + fixed-order sum.
 void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
-                 int64_t Hi, int64_t Wi, int64_t cfg, int64_t stages) {
+                 int64_t Hi, int64_t Wi, int64_t cfg, int64_t stages, c10::optional<at::Tensor> pro_scale,
+                 c10::optional<at::Tensor> pro_shift) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dw.is_cuda(), "gemm2_wgrad: device tensors");
+  const bool pro = pro_scale.has_value() && pro_scale->defined();
+  TORCH_CHECK(!pro || stages == 2, "gemm2_wgrad: the BN prologue runs with 2 stages");
   TORCH_CHECK(stages == 2 || stages == 4 || (stages == 3 && cfg != 2),
               "gemm2_wgrad: stages 2, 4 (k-half units), or 3 below the 256x256 tile");
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 && dw.scalar_type() == at::kFloat,
@@ -1137,15 +1243,24 @@ void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t
   a.tn = (int)tn; a.tk = (int)tk;
   a.fd_hw = g2::make_fastdiv2((uint32_t)(Ho * Wo));
   a.fd_w = g2::make_fastdiv2((uint32_t)Wo);
+  if (pro) {
+    for (const c10::optional<at::Tensor>* v : {&pro_scale, &pro_shift})
+      TORCH_CHECK(v->has_value() && (*v)->defined() && (*v)->is_cuda() && (*v)->scalar_type() == at::kFloat &&
+                      (*v)->is_contiguous() && (*v)->numel() == Cin, "gemm2_wgrad: prologue scale / shift f32 [Cin]");
+    a.psc = pro_scale->data_ptr<float>();
+    a.psh = pro_shift->data_ptr<float>();
+  }
   const int grid = (int)(S * tiles);
 #define HIPPS_W2M(TNc, TKc, WNc, WKc, MTc)                                                                         \
   do {                                                                                                            \
-    if (stages == 3) hipLaunchKernelGGL((g2::k_wgrad<TNc, TKc, WNc, WKc, 3, MTc>), grid, 64 * WNc * WKc, 0, stream, a); \
+    if (pro) hipLaunchKernelGGL((g2::k_wgrad<TNc, TKc, WNc, WKc, 2, MTc, true>), grid, 64 * WNc * WKc, 0, stream, a); \
+    else if (stages == 3) hipLaunchKernelGGL((g2::k_wgrad<TNc, TKc, WNc, WKc, 3, MTc>), grid, 64 * WNc * WKc, 0, stream, a); \
     else if (stages == 4) hipLaunchKernelGGL((g2::k_wgrad<TNc, TKc, WNc, WKc, 4, MTc>), grid, 64 * WNc * WKc, 0, stream, a); \
     else hipLaunchKernelGGL((g2::k_wgrad<TNc, TKc, WNc, WKc, 2, MTc>), grid, 64 * WNc * WKc, 0, stream, a);            \
   } while (0)
 #define HIPPS_W2(TNc, TKc, WNc, WKc) HIPPS_W2M(TNc, TKc, WNc, WKc, false)
-  if (cfg == 2 && stages == 4) hipLaunchKernelGGL((g2::k_wgrad<256, 256, 2, 4, 4>), grid, 512, 0, stream, a);
+  if (cfg == 2 && pro) hipLaunchKernelGGL((g2::k_wgrad<256, 256, 2, 4, 2, false, true>), grid, 512, 0, stream, a);
+  else if (cfg == 2 && stages == 4) hipLaunchKernelGGL((g2::k_wgrad<256, 256, 2, 4, 4>), grid, 512, 0, stream, a);
   else if (cfg == 2) hipLaunchKernelGGL((g2::k_wgrad<256, 256, 2, 4, 2>), grid, 512, 0, stream, a);
   else if (cfg == 5) HIPPS_W2M(64, 128, 1, 2, true);
   else if (cfg == 6 && TN == 128) HIPPS_W2M(128, 128, 2, 2, true);

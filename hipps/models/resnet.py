@@ -14,9 +14,10 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from hipps.ops.nn import (FusedBatchNorm2d, MaxPool2d, ResidualTap, bn_relu_conv1x1_ok, bn_relu_conv_bn,
-                          bn_relu_maxpool, conv1x1_bn_input, conv1x1_ok, conv2d, conv2d_bn, conv2d_stats, conv_bn,
-                          dual_bn_relu, dual_bn_relu_ok, global_avg_pool, stem_block, stem_block_ok)
+from hipps.ops.nn import (FusedBatchNorm2d, MaxPool2d, ResidualTap, bn_relu_conv, bn_relu_conv1x1_ok,
+                          bn_relu_conv_bn, bn_relu_conv_ok, bn_relu_maxpool, conv1x1_bn_input, conv1x1_ok, conv2d,
+                          conv2d_bn, conv2d_stats, conv_bn, dual_bn_relu, dual_bn_relu_ok, global_avg_pool,
+                          stem_block, stem_block_ok)
 
 # One switch for the whole zoo: fused BN(+residual)(+ReLU) HIP kernels on channels-last bf16,
 # standard PyTorch elsewhere.  HIPPS_FUSED_BN=0 restores the eager MIOpen path for A/B runs.
@@ -49,6 +50,12 @@ _FUSED_PRO = _FUSED_CONV and _os.environ.get("HIPPS_FUSED_PRO", "0") != "0"
 # downsample blocks: the downsample BN applied inside bn3's apply pass (its output, the residual,
 # is never materialised) and both BNs' backward in two passes (ops.nn._DualBNRelu)
 _FUSED_DUAL = _FUSED_GRAD and _os.environ.get("HIPPS_FUSED_DUAL", "1") != "0"
+# bn1 -> conv2 and bn2 -> conv3 with the BN + ReLU applied to the conv's staged A tiles in LDS
+# (ops.nn._BNReluConv): the bn1 / bn2 outputs are never written.  Opt-in: bit-identical to the
+# apply pass + plain GEMM (tests), but the in-LDS transform sits between each tile's DMA and its
+# barrier and the compute-bound 3x3 GEMMs lose 15-47 % (forward and weight gradient) -- more
+# than the 32 apply passes cost (same box: 11070 off vs 10629 img/s on, profiles/r3b/bnpro/)
+_BN_PRO = _FUSED_DUAL and _os.environ.get("HIPPS_BN_PRO", "0") != "0"
 
 
 def _bn(c, relu=False):
@@ -75,6 +82,26 @@ class Bottleneck(nn.Module):
         if downsample:
             self.downsample = nn.Sequential(_conv(cin, cout, 1, stride=stride), _bn(cout))
 
+    def _forward_pro(self, x, bng):
+        """conv1 (statistics) -> [bn1 + ReLU inside conv2] -> [bn2 + ReLU inside conv3] -> bn3 (+
+        residual / downsample BN) -> ReLU; every gradient tap of forward() kept."""
+        ds = self.downsample
+        if ds is None:
+            tap = ResidualTap() if _FUSED_GRAD else None
+            y1, p1 = conv1x1_bn_input(self.conv1, x, tap=tap, bn_grad=bng)
+            xd = pd = None
+        else:
+            tap = None
+            y1, p1, xa = conv1x1_bn_input(self.conv1, x, alias=True, bn_grad=bng)
+            xd, pd = conv1x1_bn_input(ds[0], xa)
+        x2, p2 = bn_relu_conv(self.bn1, self.conv2, y1, p1)
+        x3, p3 = bn_relu_conv(self.bn2, self.conv3, x2, p2)
+        if ds is None:
+            return self.bn3(x3, x, stats=p3, res_tap=tap) if self.bn3._fast_ok(x3, x) else self.bn3(x3, x)
+        if dual_bn_relu_ok(self.bn3, ds[1], x3, xd):
+            return dual_bn_relu(self.bn3, x3, p3, ds[1], xd, pd)
+        return self.bn3(x3, ds[1](xd, stats=pd), stats=p3)
+
     def forward(self, x):
         # Gradient of x = conv1's dgrad + the residual path's gradient.  Instead of autograd's add
         # (read 2, write 1 full-size tensors per block) conv1's dgrad epilogue sums them: the
@@ -84,6 +111,10 @@ class Bottleneck(nn.Module):
         # previous block's bn3 backward statistics, and conv3's those of bn2 (BNGradTap).
         ds = self.downsample
         bng = _FUSED_GRAD and _FUSED_BNGRAD
+        if (_BN_PRO and bng and self.training and conv1x1_ok(self.conv1, x) and conv1x1_ok(self.conv3, x) and
+                (ds is None or conv1x1_ok(ds[0], x)) and bn_relu_conv_ok(self.bn1, self.conv2, x) and
+                bn_relu_conv_ok(self.bn2, self.conv3, x)):
+            return self._forward_pro(x, bng)
         if ds is None:
             tap = ResidualTap() if _FUSED_GRAD else None
             y = conv_bn(self.conv1, self.bn1, x, fuse=_FUSED_CONV, tap=tap, bn_grad=bng)

@@ -291,6 +291,137 @@ def _dgrad_s2(dy, x, w, wf, bg=None):
     return run(name)
 
 
+def _conv_pro_fwd(x, w, stride, pad, scale, shift):
+    """conv(relu(x * scale + shift)) (channels-last bf16 x = a BN's input; 1x1 or KxK) on gemm2 with
+    the BN + ReLU applied to the A tile in LDS (kPro) and the following BN's statistics in the
+    epilogue; the fastest 2-stage tile per shape.  Returns (y, part)."""
+    C = native()
+    n, cin, h, wd = x.shape
+    cout, k = w.shape[0], w.shape[2]
+    ho, wo = (h + 2 * pad - k) // stride + 1, (wd + 2 * pad - k) // stride + 1
+    y = torch.empty((n, cout, ho, wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    w2 = w.reshape(cout, cin) if k == 1 else w
+
+    def run(name):
+        bm, bn, _ = _g2_parse(name)
+        part = torch.empty((2, cout, C.gemm2_mtiles(n * ho * wo, cout, k * k * cin, bm)), dtype=torch.float32,
+                           device=x.device)
+        C.gemm2_conv(x, w2, y, part, None, None, h, wd, stride, k, k, pad, bm, bn, pro_scale=scale, pro_shift=shift)
+        return y, part
+
+    names = [nm for nm in _g2_names(cout) if _g2_parse(nm)[2] == 2]
+    name = TUNER.pick(("pro", n, cin, h, wd, cout, k, stride, pad), {nm: (lambda nm=nm: run(nm)) for nm in names})
+    return run(name)
+
+
+def _conv_wgrad_pro(dy, x, dw, kh, kw, stride, pad, scale, shift):
+    """fp32 weight gradient of conv(relu(x * scale + shift)) on the gemm2 weight-gradient kernels
+    with the BN + ReLU applied to the X tile in LDS (the BN output is never materialised)."""
+    C = native()
+    hi, wi = x.shape[2], x.shape[3]
+    cout, cin = dy.shape[1], x.shape[1]
+    ok = {0: True, 1: cout % 256 == 0 and cin % 128 == 0, 3: cout % 128 == 0 and cin % 256 == 0,
+          4: cout % 256 == 0 and cin % 128 == 0, 5: cin == 64 and kh * kw > 1, 6: cin == 64 and kh * kw > 1}
+    cands = {f"w3_{cfg}": (lambda cfg=cfg: C.gemm2_wgrad(dy, x, dw, kh, kw, stride, pad, hi, wi, cfg, 2, scale, shift))
+             for cfg, v in ok.items() if v}
+    name = TUNER.pick(("wgrad_pro", tuple(x.shape), cout, kh, kw, stride, pad), cands)
+    cands[name]()
+
+
+class _BNReluConv(torch.autograd.Function):
+    """conv(relu(bn(x))) for a training BatchNorm whose output only feeds this conv (ResNet bn1 ->
+    conv2, bn2 -> conv3), the BN's statistics from its producer's epilogue (``part``): finalize,
+    then the conv GEMM reading x with the BN + ReLU applied to each staged A tile in LDS (gemm2
+    kPro), the next BN's statistics in its epilogue.  The BN output is never written or re-read.
+    Backward: the input-gradient GEMM with this BN's backward reduction in its epilogue (relu'
+    recomputed from x), the BN backward apply, and the weight gradient with the same BN + ReLU on
+    its X tiles."""
+
+    @staticmethod
+    def forward(ctx, x, part, bn_w, bn_b, running_mean, running_var, eps, momentum, w_master, stride, pad):
+        w = bf16_weight(w_master)
+        if w.dim() == 4 and w.shape[2] > 1:
+            w = w.contiguous(memory_format=torch.channels_last)
+        ctx.wdtype = w_master.dtype
+        ctx.set_materialize_grads(False)
+        ctx.wt = _TSHADOWS.get(w_master.data_ptr()) if w_master.dtype == torch.float32 else None
+        n, c, h, wd = x.shape
+        f32 = dict(dtype=torch.float32, device=x.device)
+        mean, invstd, scale, shift = (torch.empty(c, **f32) for _ in range(4))
+        native().bn_finalize_partials(part, part.shape[2], n * h * wd, bn_w, bn_b, running_mean, running_var, mean,
+                                      invstd, scale, shift, c, float(eps), float(momentum))
+        y, part_out = _conv_pro_fwd(x, w, stride, pad, scale, shift)
+        ctx.geom = (stride, pad)
+        ctx.save_for_backward(x, w, bn_w, mean, invstd, scale, shift)
+        ctx.mark_non_differentiable(part_out)
+        return y, part_out
+
+    @staticmethod
+    def backward(ctx, dy, _dpart):
+        x, w, bn_w, mean, invstd, scale, shift = ctx.saved_tensors
+        if dy is None:
+            return (None,) * 11
+        s, p = ctx.geom
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        n, c, h, wd = x.shape
+        cout, k = w.shape[0], w.shape[2]
+        bg = BNGradTap(x, None, mean, invstd, scale, shift)
+        # gradient of the (never materialised) BN output, with that BN's backward reduction
+        if k == 1:
+            wt = ctx.wt if ctx.wt is not None else w.reshape(cout, c).t().contiguous()
+            dbn = torch.empty_like(x, memory_format=torch.channels_last)
+            part = _conv1x1_gemm(dy, wt, dbn, h, wd, 1, True, None, None, bg)
+        else:
+            wf = ctx.wt if ctx.wt is not None and ctx.wt.dim() == 4 else None  # rot180(W)^T shadow
+            if wf is None:
+                wf = torch.flip(w, (2, 3)).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+            if s == 1:
+                dbn, part = _convkxk_gemm(dy, wf, 1, p, False, bg)
+            else:
+                dbn, part = _dgrad_s2(dy, x, w, wf, bg)
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dgw, dgb = torch.empty_like(bn_w), torch.empty_like(bn_w)
+        if part is not None:
+            native().bn_backward_partials(part, part.shape[2], dbn, x, MASK_X, bn_w, mean, invstd, scale, shift, dx,
+                                          None, dgw, dgb, c, None)
+        else:
+            native().bn_backward(dbn, x, None, MASK_X, bn_w, mean, invstd, scale, shift, dx, None, dgw, dgb, c, None)
+        dw = None
+        if ctx.needs_input_grad[8]:
+            dw = torch.empty(w.shape, dtype=torch.float32, device=w.device,
+                             memory_format=torch.channels_last if k > 1 else torch.contiguous_format)
+            _conv_wgrad_pro(dy, x, dw, k, k, s, p, scale, shift)
+            if ctx.wdtype != torch.float32:
+                dw = dw.to(ctx.wdtype)
+        return dx, None, dgw, dgb, None, None, None, None, dw, None, None
+
+
+def bn_relu_conv_ok(bn, conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    """Can _BNReluConv run conv(relu(bn(x))) (x: the BN's bf16 channels-last input)?"""
+    if not (_GEMM2 and bn.training and getattr(bn, "relu", False) and bn._fast_ok(x, None) and conv.training):
+        return False
+    k, st, pd = conv.kernel_size, conv.stride, conv.padding
+    if k[0] != k[1] or st[0] != st[1] or pd[0] != pd[1] or conv.groups != 1 or conv.bias is not None:
+        return False
+    if conv.dilation != (1, 1) or conv.padding_mode != "zeros" or k[0] not in (1, 3):
+        return False
+    if k[0] == 1 and (pd[0] != 0 or st[0] != 1):
+        return False
+    if k[0] == 3 and (pd[0] != 1 or st[0] not in (1, 2)):
+        return False
+    w = conv.weight
+    return (conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0 and bn.weight.dtype == torch.float32 and
+            (k[0] == 1 or w.is_contiguous(memory_format=torch.channels_last)))
+
+
+def bn_relu_conv(bn, conv: nn.Conv2d, x, part):
+    """(conv(relu(bn(x))), the next BN's statistics partials) on _BNReluConv (callers check
+    bn_relu_conv_ok; ``part``: bn's statistics partials from x's producer)."""
+    bn._nbt_pending += 1
+    return _BNReluConv.apply(x, part, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, bn.momentum,
+                             conv.weight, conv.stride[0], conv.padding[0])
+
+
 class ResidualTap:
     """Hands a fused BN's residual gradient to the stride-1 1x1 conv that reads the same block
     input (ResNet identity blocks: x feeds conv1 and is bn3's residual).  bn3's backward stores

@@ -80,16 +80,18 @@ def test_gpu_fused_eval_apply():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("width", [16, 64])
-def test_gpu_resnet_fused_vs_unfused_step(width):
+@pytest.mark.parametrize("width,pro", [(16, False), (64, False), (64, True)])
+def test_gpu_resnet_fused_vs_unfused_step(width, pro, monkeypatch):
     """One autocast step of a small ResNet: the fused-BN model's grads are no further from an fp32
     reference than the eager bf16 (MIOpen BN) model's grads are.  width 64 puts every conv on the
     MFMA paths (BNGradTap through the 3x3 input gradient, the downsample's compact stride-2
     gradient summed in conv1's dgrad epilogue)."""
     import copy
 
+    import hipps.models.resnet as rn
     from hipps.models.resnet import ResNet, Bottleneck
 
+    monkeypatch.setattr(rn, "_BN_PRO", pro)  # bn1 / bn2 applied inside conv2 / conv3 (_BNReluConv)
     torch.manual_seed(3)
     base = ResNet(Bottleneck, [1, 1], num_classes=10, width=width, zero_init_residual=False).cuda()
     base = base.to(memory_format=torch.channels_last)

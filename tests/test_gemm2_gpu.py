@@ -367,3 +367,65 @@ def test_gemm2_dgrad_stride2_parity_classes(bm, bn, cin, cout, h, bst):
         dz = torch.where(xv * sc + sh > 0, d, torch.zeros_like(d))
         torch.testing.assert_close(part[0].sum(1), dz.sum(0), rtol=1e-4, atol=1e-2)
         torch.testing.assert_close(part[1].sum(1), (dz * (xv - mean) * inv).sum(0), rtol=1e-4, atol=1e-2)
+
+
+def _bn_apply_ref(x, sc, sh):
+    """bf16(relu(x * sc + sh)) exactly as the fused BN apply kernel rounds it (channels-last)."""
+    y = torch.empty_like(x)
+    C().bn_apply(x, None, y, sc, sh, x.shape[1], True)
+    return y
+
+
+@pytest.mark.parametrize("bm,bn", [(128, 128), (256, 256), (128, 64), (256, 64)])
+@pytest.mark.parametrize("cin,cout,k,h,stride", [(128, 256, 1, 13, 1), (64, 64, 3, 11, 1), (128, 128, 3, 15, 2),
+                                                 (256, 256, 3, 7, 1)])
+def test_gemm2_bn_prologue_bitwise(bm, bn, cin, cout, k, h, stride):
+    """kPro: relu(x * scale + shift) applied to the staged A tiles in LDS gives the same output and
+    statistics as the BN apply pass followed by the plain GEMM (padding taps stay zero)."""
+    if cout % bn:
+        pytest.skip("tile")
+    n = 2
+    x = _x(n, cin, h, 71)
+    sc = torch.randn(cin, device=DEV)
+    sh = torch.randn(cin, device=DEV) * 0.5
+    if k == 1:
+        w = (torch.randn(cout, cin, device=DEV) / cin ** 0.5).to(torch.bfloat16)
+    else:
+        w = (torch.randn(cout, cin, k, k, device=DEV) / (k * k * cin) ** 0.5).to(torch.bfloat16).contiguous(
+            memory_format=CL)
+    pad = k // 2
+    ho = (h + 2 * pad - k) // stride + 1
+    M = n * ho * ho
+    y1 = torch.empty(n, cout, ho, ho, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
+    y2 = torch.full_like(y1, 3.0)
+    p1 = torch.empty(2, cout, C().gemm2_mtiles(M, cout, k * k * cin, bm), device=DEV)
+    p2 = torch.empty_like(p1)
+    C().gemm2_conv(_bn_apply_ref(x, sc, sh), w, y1, p1, None, None, h, h, stride, k, k, pad, bm, bn)
+    C().gemm2_conv(x, w, y2, p2, None, None, h, h, stride, k, k, pad, bm, bn, pro_scale=sc, pro_shift=sh)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    assert torch.equal(p1, p2)
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 3, 4, 5, 6])
+@pytest.mark.parametrize("cin,cout,k,h,stride", [(128, 256, 1, 13, 1), (64, 64, 3, 11, 1), (128, 256, 3, 15, 2),
+                                                 (256, 256, 3, 7, 1)])
+def test_gemm2_wgrad_bn_prologue_bitwise(cfg, cin, cout, k, h, stride):
+    """Weight gradient with the BN + ReLU applied to the X tiles in LDS == apply pass + plain kernel."""
+    ok = {0: True, 1: cout % 256 == 0 and cin % 128 == 0, 3: cout % 128 == 0 and cin % 256 == 0,
+          4: cout % 256 == 0 and cin % 128 == 0, 5: cin == 64 and k > 1, 6: cin == 64 and k > 1}
+    if not ok[cfg]:
+        pytest.skip("tile")
+    n = 2
+    pad = k // 2
+    x = _x(n, cin, h, 72)
+    sc = torch.randn(cin, device=DEV)
+    sh = torch.randn(cin, device=DEV) * 0.5
+    ho = (h + 2 * pad - k) // stride + 1
+    dy = _x(n, cout, ho, 73)
+    d1 = torch.empty(cout, cin, k, k, device=DEV).contiguous(memory_format=CL)
+    d2 = torch.full_like(d1, 9.0)
+    C().gemm2_wgrad(dy, _bn_apply_ref(x, sc, sh), d1, k, k, stride, pad, h, h, cfg, 2)
+    C().gemm2_wgrad(dy, x, d2, k, k, stride, pad, h, h, cfg, 2, sc, sh)
+    torch.cuda.synchronize()
+    assert torch.equal(d1, d2)
