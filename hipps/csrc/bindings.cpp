@@ -85,7 +85,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
                 c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift);
 void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
                  int64_t Hi, int64_t Wi, int64_t cfg, int64_t stages,
-                 c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift);
+                 c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift, int64_t sdiv);
 // pool.hip
 void maxpool3s2_forward(at::Tensor x, at::Tensor y, at::Tensor code, c10::optional<at::Tensor> scale,
                         c10::optional<at::Tensor> shift);
@@ -184,7 +184,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm2_wgrad", &hipps::gemm2_wgrad, "conv weight gradient on the LDS-DMA MFMA core (split-M slabs)",
         py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
         py::arg("Hi"), py::arg("Wi"), py::arg("cfg") = 0, py::arg("stages") = 2, py::arg("pro_scale") = py::none(),
-        py::arg("pro_shift") = py::none());
+        py::arg("pro_shift") = py::none(), py::arg("sdiv") = 1);
   m.def("conv1x1_forward", &hipps::conv1x1_forward,
         "MFMA 1x1 conv (NHWC GEMM) with fused BN-stats epilogue and optional (+ add * mask) epilogue",
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"), pybind11::arg("part"), pybind11::arg("Hi"),

@@ -56,7 +56,7 @@ enum Epi : int { kPlain = 0, kStats = 1, kAdd = 2, kBst = 4, kBstBits = 8, kAddS
 
 template <int BM, int BN> struct Cfg;
 template <> struct Cfg<256, 256> { static constexpr int TM = 128, TN = 64; };
-template <> struct Cfg<256, 128> { static constexpr int TM = 128, TN = 64; };
+template <> struct Cfg<256, 128> { static constexpr int TM = 64, TN = 64; };  // 8 waves (3 stages fit: 144 KB)
 template <> struct Cfg<128, 128> { static constexpr int TM = 64, TN = 64; };
 template <> struct Cfg<256, 64> { static constexpr int TM = 64, TN = 64; };
 template <> struct Cfg<128, 64> { static constexpr int TM = 64, TN = 32; };
@@ -1171,7 +1171,7 @@ void wgrad_reduce_slabs(const at::Tensor& part, int64_t S, int64_t N, int64_t K,
 // Cout % 64 == 0, Cin % 64 == 0.  S split-M partial slabs (~2 resident blocks per CU) + fixed-order sum.
 void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
                  int64_t Hi, int64_t Wi, int64_t cfg, int64_t stages, c10::optional<at::Tensor> pro_scale,
-                 c10::optional<at::Tensor> pro_shift) {
+                 c10::optional<at::Tensor> pro_shift, int64_t sdiv) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dw.is_cuda(), "gemm2_wgrad: device tensors");
   const bool pro = pro_scale.has_value() && pro_scale->defined();
   TORCH_CHECK(!pro || stages == 2, "gemm2_wgrad: the BN prologue runs with 2 stages");
@@ -1226,7 +1226,9 @@ void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t
   if (cfg >= 3) resident = 256;
   if (stages == 3 || mt)  // (stages 4 = the LDS bytes of 2)
     resident = 256 * std::max<int64_t>(1, 160 * 1024 / ((stages == 4 ? 2 : stages) * g2::kWM * (TN + TK) * 2));
-  int64_t S = std::max<int64_t>(1, resident / tiles);
+  // sdiv > 1: fewer, longer M slabs (less fp32 slab traffic, fewer resident blocks)
+  TORCH_CHECK(sdiv >= 1, "gemm2_wgrad: sdiv >= 1");
+  int64_t S = std::max<int64_t>(1, resident / tiles / sdiv);
   S = std::min<int64_t>(S, std::max<int64_t>(1, M / (8 * g2::kWM)));           // >= 8 stages per block
   S = std::min<int64_t>(S, std::max<int64_t>(1, M * (N + K) / (4 * N * K)));  // slabs <= operand bytes
   const int64_t chunk = ((M + S - 1) / S + g2::kWM - 1) / g2::kWM * g2::kWM;

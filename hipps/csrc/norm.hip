@@ -152,7 +152,16 @@ __device__ __forceinline__ bool combine_partials(const float* __restrict__ pa, c
   double a = 0.0, b = 0.0;
   const float* ra = pa + (int64_t)c * nrb;
   const float* rb = pb + (int64_t)c * nrb;
-  for (int i = threadIdx.x; i < nrb; i += kBlock) { a += ra[i]; b += rb[i]; }
+  // 8 independent loads in flight per lane (a dependent chain of nrb/256 L2 round trips was the
+  // kernel's time on the 6272-column layer-1 partials); each lane's sum keeps its fixed order
+  int i = threadIdx.x;
+  for (; i + 3 * kBlock < nrb; i += 4 * kBlock) {
+    const float a0 = ra[i], a1 = ra[i + kBlock], a2 = ra[i + 2 * kBlock], a3 = ra[i + 3 * kBlock];
+    const float b0 = rb[i], b1 = rb[i + kBlock], b2 = rb[i + 2 * kBlock], b3 = rb[i + 3 * kBlock];
+    a += a0; a += a1; a += a2; a += a3;
+    b += b0; b += b1; b += b2; b += b3;
+  }
+  for (; i < nrb; i += kBlock) { a += ra[i]; b += rb[i]; }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     a += __shfl_xor(a, o, 64);

@@ -180,11 +180,15 @@ def _conv_wgrad(dy, x, dw, kh, kw, stride, pad):
                 for ns in ((2, 3) if cfg != 2 else (2, 4)) + ((4,) if cfg == 0 else ()):
                     cands[f"w3_{cfg}" + ("" if ns == 2 else f"s{ns}")] = (
                         lambda cfg=cfg, ns=ns: C.gemm2_wgrad(dy, x, dw, kh, kw, stride, pad, hi, wi, cfg, ns))
+        # (fewer, longer M slabs -- gemm2_wgrad sdiv=2, half the fp32 slab traffic -- measured: no
+        # shape faster by more than 1 %, profiles/r3b/tuner_sdiv.json; not a candidate)
         if kh > 1 and cin < 128:
             cands["miopen"] = mio
         name = TUNER.pick(("wgrad", tuple(x.shape), cout, kh, kw, stride, pad), cands)
     if name.startswith("w3"):
-        C.gemm2_wgrad(dy, x, dw, kh, kw, stride, pad, hi, wi, int(name[3]), int(name[5]) if len(name) > 4 else 2)
+        sdiv = int(name.split("d")[1]) if "d" in name else 1
+        C.gemm2_wgrad(dy, x, dw, kh, kw, stride, pad, hi, wi, int(name[3]), int(name[5]) if len(name) > 4 else 2,
+                      sdiv=sdiv)
     elif name == "miopen":
         mio()
     else:

@@ -429,3 +429,20 @@ def test_gemm2_wgrad_bn_prologue_bitwise(cfg, cin, cout, k, h, stride):
     C().gemm2_wgrad(dy, x, d2, k, k, stride, pad, h, h, cfg, 2, sc, sh)
     torch.cuda.synchronize()
     assert torch.equal(d1, d2)
+
+
+@pytest.mark.parametrize("cfg", [0, 2])
+@pytest.mark.parametrize("cin,cout,k,h,stride", [(256, 256, 1, 28, 1), (256, 256, 3, 14, 2)])
+def test_gemm2_wgrad_fewer_slabs(cfg, cin, cout, k, h, stride):
+    """sdiv=2 (half as many, twice as long M slabs) == the default split to fp32 rounding."""
+    n = 8
+    pad = k // 2
+    x = _x(n, cin, h, 81)
+    ho = (h + 2 * pad - k) // stride + 1
+    dy = _x(n, cout, ho, 82)
+    d1 = torch.empty(cout, cin, k, k, device=DEV).contiguous(memory_format=CL)
+    d2 = torch.full_like(d1, 9.0)
+    C().gemm2_wgrad(dy, x, d1, k, k, stride, pad, h, h, cfg, 2)
+    C().gemm2_wgrad(dy, x, d2, k, k, stride, pad, h, h, cfg, 2, sdiv=2)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(d2, d1, rtol=1e-5, atol=1e-4)
