@@ -694,6 +694,24 @@ __global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
     __syncthreads();
   }
   uint32_t xok = 0;  // PRO: this thread's X chunks of the staged stage that hold data
+  // implicit-GEMM X rows: (image, ho, wo) of this lane's row i in the next stage to issue, advanced
+  // by UR rows per stage with adds and compares instead of two divisions per chunk per stage
+  // (stages are issued strictly in order)
+  // (8-wave tiles keep the divisions: the 256x256 kernel is at the 256-register cap)
+  constexpr bool INC = NW <= 4;
+  int xs_img[INC ? IX : 1], xs_ho[INC ? IX : 1], xs_wo[INC ? IX : 1];
+  const int dq = UR / g.Wo, dr = UR - dq * g.Wo;
+  if (INC && !direct) {
+#pragma unroll
+    for (int i = 0; i < IX; ++i) {
+      const int m = mbeg + (i * NW + w) * RX + rx;
+      const int img = (int)fdiv2((uint32_t)m, g.fd_hw), rem = m - img * (int)g.fd_hw.d;
+      const int ho = (int)fdiv2((uint32_t)rem, g.fd_w);
+      xs_img[INC ? i : 0] = img;
+      xs_ho[INC ? i : 0] = ho;
+      xs_wo[INC ? i : 0] = rem - ho * g.Wo;
+    }
+  }
   auto issue = [&](int st, int s) {
     uint8_t* ty = lds + s * (YT + XT);
     uint8_t* tx = ty + YT;
@@ -717,8 +735,17 @@ __global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
         if (direct) {
           p = g.X + (int64_t)m * g.Cin + c0 + ch * 8;
         } else {
-          const int img = (int)fdiv2((uint32_t)m, g.fd_hw), rem = m - img * (int)g.fd_hw.d;
-          const int ho = (int)fdiv2((uint32_t)rem, g.fd_w), wo = rem - ho * g.Wo;
+          int img, ho, wo;
+          if constexpr (INC) {
+            img = xs_img[INC ? i : 0];
+            ho = xs_ho[INC ? i : 0];
+            wo = xs_wo[INC ? i : 0];
+          } else {
+            img = (int)fdiv2((uint32_t)m, g.fd_hw);
+            const int rem = m - img * (int)g.fd_hw.d;
+            ho = (int)fdiv2((uint32_t)rem, g.fd_w);
+            wo = rem - ho * g.Wo;
+          }
           const int hi = ho * g.stride - g.pad + (MT ? xkr[MT ? i : 0] : kr);
           const int wi = wo * g.stride - g.pad + (MT ? xkc[MT ? i : 0] : kc);
           const bool inx = MT ? xin[MT ? i : 0] : true;
@@ -728,6 +755,14 @@ __global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
       }
       glds16(p, tx + (i * NW + w) * 1024);
       if constexpr (PRO) xok |= (p != kZero16 ? 1u : 0u) << i;
+      if (INC && !direct) {  // this row in the next stage: m + UR
+        int wo = xs_wo[INC ? i : 0] + dr, ho = xs_ho[INC ? i : 0] + dq, img = xs_img[INC ? i : 0];
+        if (wo >= g.Wo) { wo -= g.Wo; ++ho; }
+        while (ho >= g.Ho) { ho -= g.Ho; ++img; }
+        xs_wo[INC ? i : 0] = wo;
+        xs_ho[INC ? i : 0] = ho;
+        xs_img[INC ? i : 0] = img;
+      }
     }
   };
 
