@@ -50,7 +50,7 @@ void bn_forward_partials(at::Tensor part, int64_t nrb, at::Tensor x, c10::option
 void bn_backward_partials(at::Tensor part, int64_t nrb, at::Tensor dy, at::Tensor x, int64_t mask_mode,
                           at::Tensor weight, at::Tensor mean, at::Tensor invstd, at::Tensor scale, at::Tensor shift,
                           at::Tensor dx, c10::optional<at::Tensor> dres, at::Tensor dweight, at::Tensor dbias, int64_t C,
-                          c10::optional<at::Tensor> mask_in);
+                          c10::optional<at::Tensor> mask_in, int64_t unr);
 // gemm.hip
 int64_t conv1x1_mtiles(int64_t M);
 void conv1x1_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part, int64_t Hi,
@@ -69,7 +69,7 @@ void bn_dual_forward(at::Tensor part3, int64_t nrb3, at::Tensor partd, int64_t n
 void bn_dual_backward(c10::optional<at::Tensor> part3, int64_t nrb3, at::Tensor dz, at::Tensor x3, at::Tensor xd,
                       at::Tensor mask, at::Tensor w3, at::Tensor mean3, at::Tensor invstd3, at::Tensor wd,
                       at::Tensor meand, at::Tensor invstdd, at::Tensor dx3, at::Tensor dxd, at::Tensor dw3,
-                      at::Tensor db3, at::Tensor dwd, at::Tensor dbd, int64_t C);
+                      at::Tensor db3, at::Tensor dwd, at::Tensor dbd, int64_t C, int64_t unr);
 // gemm2.hip
 at::Tensor gemm2_dgrad_s2(at::Tensor dy, at::Tensor wf, at::Tensor dx, int64_t bm, int64_t bn,
                           c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_bits,
@@ -162,12 +162,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_apply", &hipps::bn_apply, "y = act(x*scale + shift (+res))");
   m.def("bn_backward", &hipps::bn_backward, "fused BN bwd with relu-mask recompute (+dres)");
   m.def("bn_forward_partials", &hipps::bn_forward_partials, "BN fwd finalize+apply from producer-reduced partials");
-  m.def("bn_backward_partials", &hipps::bn_backward_partials, "BN bwd finalize+apply from consumer-reduced partials");
+  m.def("bn_backward_partials", &hipps::bn_backward_partials, "BN bwd finalize+apply from consumer-reduced partials",
+        py::arg("part"), py::arg("nrb"), py::arg("dy"), py::arg("x"), py::arg("mask_mode"), py::arg("weight"),
+        py::arg("mean"), py::arg("invstd"), py::arg("scale"), py::arg("shift"), py::arg("dx"), py::arg("dres"),
+        py::arg("dweight"), py::arg("dbias"), py::arg("C"), py::arg("mask_in"), py::arg("unr") = 0);
   m.def("conv1x1_mtiles", &hipps::conv1x1_mtiles);
   m.def("bn_dual_forward", &hipps::bn_dual_forward,
         "z = relu(bn3(x3) + bnd(xd)) from producer partials: two finalizes + one apply (downsample block)");
   m.def("bn_dual_backward", &hipps::bn_dual_backward,
-        "backward of bn_dual_forward: dx3 + the downsample BN's reduction in one pass, then dxd");
+        "backward of bn_dual_forward: dx3 + the downsample BN's reduction in one pass, then dxd",
+        py::arg("part3"), py::arg("nrb3"), py::arg("dz"), py::arg("x3"), py::arg("xd"), py::arg("mask"), py::arg("w3"),
+        py::arg("mean3"), py::arg("invstd3"), py::arg("wd"), py::arg("meand"), py::arg("invstdd"), py::arg("dx3"),
+        py::arg("dxd"), py::arg("dw3"), py::arg("db3"), py::arg("dwd"), py::arg("dbd"), py::arg("C"),
+        py::arg("unr") = 4);
   m.def("gemm2_mtiles", &hipps::gemm2_mtiles, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("bm") = 0);
   m.def("gemm2_conv", &hipps::gemm2_conv, "second-generation MFMA conv GEMM (LDS-DMA staged, 256-row tiles)",
         py::arg("x"), py::arg("w"), py::arg("y"), py::arg("part") = py::none(), py::arg("add") = py::none(),

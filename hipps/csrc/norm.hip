@@ -271,8 +271,9 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_fwd(const uint16_t* __restr
   }
 }
 
-// dx = a*dz + k1*x + k0, dz = dy * mask;  dres = dz (when a residual was fused)
-template <int MODE>
+// dx = a*dz + k1*x + k0, dz = dy * mask;  dres = dz (when a residual was fused).  UNR vectors
+// in flight per lane.
+template <int MODE, int UNR = 2>
 __global__ __launch_bounds__(kBlock) void k_bn_apply_bwd(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
                                                          const uint16_t* __restrict__ y,
                                                          const uint8_t* __restrict__ mbits,
@@ -311,17 +312,19 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_bwd(const uint16_t* __restr
   };
   constexpr bool need_y = mask_mode == MASK_Y, need_b = mask_mode == MASK_BITS;
   int64_t v = v0;
-  for (; v + stride < V; v += 2 * stride) {  // two vectors in flight per lane
-    float d0[8], x0[8], y0[8], d1[8], x1[8], y1[8];
-    const int64_t o0 = v * 8, o1 = (v + stride) * 8;
-    load8(dy + o0, d0);
-    load8(x + o0, x0);
-    load8(dy + o1, d1);
-    load8(x + o1, x1);
-    if (need_y) { load8(y + o0, y0); load8(y + o1, y1); }
-    const uint32_t m0 = need_b ? (uint32_t)mbits[v] : 0u, m1 = need_b ? (uint32_t)mbits[v + stride] : 0u;
-    body(d0, x0, y0, m0, o0);
-    body(d1, x1, y1, m1, o1);
+  for (; v + (UNR - 1) * stride < V; v += UNR * stride) {  // UNR vectors in flight per lane
+    float d[UNR][8], xv[UNR][8], yv[need_y ? UNR : 1][8];
+    uint32_t mb[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int64_t o = (v + u * stride) * 8;
+      load8(dy + o, d[u]);
+      load8(x + o, xv[u]);
+      if (need_y) load8(y + o, yv[need_y ? u : 0]);
+      mb[u] = need_b ? (uint32_t)mbits[v + u * stride] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) body(d[u], xv[u], yv[need_y ? u : 0], mb[u], (v + u * stride) * 8);
   }
   for (; v < V; v += stride) {
     float d0[8], x0[8], y0[8];
@@ -699,9 +702,13 @@ namespace hipps {
 void bn_backward_partials(at::Tensor part, int64_t nrb, at::Tensor dy, at::Tensor x, int64_t mask_mode,
                           at::Tensor weight, at::Tensor mean, at::Tensor invstd, at::Tensor scale, at::Tensor shift,
                           at::Tensor dx, c10::optional<at::Tensor> dres, at::Tensor dweight, at::Tensor dbias, int64_t C,
-                          c10::optional<at::Tensor> mask_in) {
+                          c10::optional<at::Tensor> mask_in, int64_t unr) {
   TORCH_CHECK(C % 8 == 0 && C <= kMaxC, "fused BN needs C % 8 == 0 and C <= 2048");
   TORCH_CHECK(mask_mode == MASK_NONE || mask_mode == MASK_X || mask_mode == MASK_BITS, "bad mask mode");
+  TORCH_CHECK(unr == 0 || unr == 2 || unr == 4, "bn_backward_partials: unr 0 (auto), 2 or 4");
+  // 0: 4 vectors in flight per lane on small tensors (latency-bound: layer-4 BN 15.9 -> 11.5 us),
+  // 2 on large ones (layer-2 BN 115 vs 126 us), tools/bench_bn_dual.py
+  if (unr == 0) unr = (int64_t)x.numel() <= (int64_t(1) << 24) ? 4 : 2;
   const int64_t M = x.numel() / C;
   check_act(dy, "dy", M * C);
   check_act(x, "x", M * C);
@@ -733,10 +740,18 @@ void bn_backward_partials(at::Tensor part, int64_t nrb, at::Tensor dy, at::Tenso
                        coef[0].data_ptr<float>(), coef[1].data_ptr<float>(), coef[2].data_ptr<float>(),
                        (uint16_t*)dx.data_ptr(), drp, M, (int)C);
   };
-  switch (mask_mode) {
-    case MASK_NONE: app(k_bn_apply_bwd<MASK_NONE>); break;
-    case MASK_X: app(k_bn_apply_bwd<MASK_X>); break;
-    default: app(k_bn_apply_bwd<MASK_BITS>); break;
+  if (unr == 4) {
+    switch (mask_mode) {
+      case MASK_NONE: app(k_bn_apply_bwd<MASK_NONE, 4>); break;
+      case MASK_X: app(k_bn_apply_bwd<MASK_X, 4>); break;
+      default: app(k_bn_apply_bwd<MASK_BITS, 4>); break;
+    }
+  } else {
+    switch (mask_mode) {
+      case MASK_NONE: app(k_bn_apply_bwd<MASK_NONE>); break;
+      case MASK_X: app(k_bn_apply_bwd<MASK_X>); break;
+      default: app(k_bn_apply_bwd<MASK_BITS>); break;
+    }
   }
 }
 }  // namespace hipps
@@ -788,7 +803,7 @@ void bn_dual_forward(at::Tensor part3, int64_t nrb3, at::Tensor partd, int64_t n
 void bn_dual_backward(c10::optional<at::Tensor> part3, int64_t nrb3, at::Tensor dz, at::Tensor x3, at::Tensor xd,
                       at::Tensor mask, at::Tensor w3, at::Tensor mean3, at::Tensor invstd3, at::Tensor wd,
                       at::Tensor meand, at::Tensor invstdd, at::Tensor dx3, at::Tensor dxd, at::Tensor dw3,
-                      at::Tensor db3, at::Tensor dwd, at::Tensor dbd, int64_t C) {
+                      at::Tensor db3, at::Tensor dwd, at::Tensor dbd, int64_t C, int64_t unr) {
   TORCH_CHECK(C % 8 == 0 && C <= kMaxC && C >= 8, "fused BN needs C % 8 == 0 and 8 <= C <= 2048");
   const int64_t M = x3.numel() / C;
   for (auto* t : {&dz, &x3, &xd, &dx3, &dxd}) check_act(*t, "activation", M * C);
@@ -823,11 +838,16 @@ void bn_dual_backward(c10::optional<at::Tensor> part3, int64_t nrb3, at::Tensor 
                        coef[2].data_ptr<float>());
   };
   finb(p3.data_ptr<float>(), n3, w3, mean3, invstd3, dw3, db3, coef3);
-  hipLaunchKernelGGL((k_bn_bwd_dual<4>), nrb, kBlock, 0, stream, (const uint16_t*)dz.data_ptr(),
-                     (const uint16_t*)x3.data_ptr(), (const uint16_t*)xd.data_ptr(), mbp, coef3[0].data_ptr<float>(),
-                     coef3[1].data_ptr<float>(), coef3[2].data_ptr<float>(), meand.data_ptr<float>(),
-                     invstdd.data_ptr<float>(), (uint16_t*)dx3.data_ptr(), M, (int)C, rows, nrb,
-                     pd[0].data_ptr<float>(), pd[1].data_ptr<float>());
+  auto dual = [&](auto kern) {
+    hipLaunchKernelGGL(kern, nrb, kBlock, 0, stream, (const uint16_t*)dz.data_ptr(), (const uint16_t*)x3.data_ptr(),
+                       (const uint16_t*)xd.data_ptr(), mbp, coef3[0].data_ptr<float>(), coef3[1].data_ptr<float>(),
+                       coef3[2].data_ptr<float>(), meand.data_ptr<float>(), invstdd.data_ptr<float>(),
+                       (uint16_t*)dx3.data_ptr(), M, (int)C, rows, nrb, pd[0].data_ptr<float>(), pd[1].data_ptr<float>());
+  };
+  TORCH_CHECK(unr == 2 || unr == 4 || unr == 8, "bn_dual_backward: unr 2, 4 or 8");
+  if (unr == 2) dual(k_bn_bwd_dual<2>);
+  else if (unr == 8) dual(k_bn_bwd_dual<8>);
+  else dual(k_bn_bwd_dual<4>);
   finb(pd.data_ptr<float>(), nrb, wd, meand, invstdd, dwd, dbd, coefd);
   hipLaunchKernelGGL(k_bn_apply_bwd<MASK_BITS>, apply_grid(M, (int)C), kBlock, 0, stream,
                      (const uint16_t*)dz.data_ptr(), (const uint16_t*)xd.data_ptr(), nullptr, mbp, nullptr, nullptr,
