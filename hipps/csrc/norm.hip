@@ -144,37 +144,50 @@ __global__ __launch_bounds__(kBlock) void k_bn_reduce(const uint16_t* __restrict
 // wave per channel: 12 us per call on the 1x1-GEMM partials, nrb = M/128 = 6272 on layer1,
 // profiles/bench_n1_steady_r1c.txt.)
 constexpr int kFinCh = 1;
+// WPC (nrb <= 512, the deep layers' partials): one wave per channel, 4 channels per block -- the
+// block-per-channel form spent most of its ~5 us on 2048 mostly idle workgroups there
+template <bool WPC>
 __device__ __forceinline__ bool combine_partials(const float* __restrict__ pa, const float* __restrict__ pb, int nrb,
-                                                 int C, double& s, double& q) {
+                                                 int C, double& s, double& q, int& c) {
   __shared__ double red[2][kBlock / 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int c = blockIdx.x;
+  c = WPC ? blockIdx.x * (kBlock / 64) + wv : blockIdx.x;
   double a = 0.0, b = 0.0;
-  const float* ra = pa + (int64_t)c * nrb;
-  const float* rb = pb + (int64_t)c * nrb;
-  // 8 independent loads in flight per lane (a dependent chain of nrb/256 L2 round trips was the
-  // kernel's time on the 6272-column layer-1 partials); each lane's sum keeps its fixed order
-  int i = threadIdx.x;
-  for (; i + 3 * kBlock < nrb; i += 4 * kBlock) {
-    const float a0 = ra[i], a1 = ra[i + kBlock], a2 = ra[i + 2 * kBlock], a3 = ra[i + 3 * kBlock];
-    const float b0 = rb[i], b1 = rb[i + kBlock], b2 = rb[i + 2 * kBlock], b3 = rb[i + 3 * kBlock];
-    a += a0; a += a1; a += a2; a += a3;
-    b += b0; b += b1; b += b2; b += b3;
+  if (c < C) {
+    const float* ra = pa + (int64_t)c * nrb;
+    const float* rb = pb + (int64_t)c * nrb;
+    // 8 independent loads in flight per lane (a dependent chain of nrb/256 L2 round trips was the
+    // kernel's time on the 6272-column layer-1 partials); each lane's sum keeps its fixed order
+    constexpr int L = WPC ? 64 : kBlock;
+    int i = WPC ? lane : (int)threadIdx.x;
+    for (; i + 3 * L < nrb; i += 4 * L) {
+      const float a0 = ra[i], a1 = ra[i + L], a2 = ra[i + 2 * L], a3 = ra[i + 3 * L];
+      const float b0 = rb[i], b1 = rb[i + L], b2 = rb[i + 2 * L], b3 = rb[i + 3 * L];
+      a += a0; a += a1; a += a2; a += a3;
+      b += b0; b += b1; b += b2; b += b3;
+    }
+    for (; i < nrb; i += L) { a += ra[i]; b += rb[i]; }
   }
-  for (; i < nrb; i += kBlock) { a += ra[i]; b += rb[i]; }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     a += __shfl_xor(a, o, 64);
     b += __shfl_xor(b, o, 64);
   }
-  if (lane == 0) { red[0][wv] = a; red[1][wv] = b; }
-  __syncthreads();
-  s = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-  q = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
-  return threadIdx.x == 0 && c < C;
+  if constexpr (WPC) {
+    s = a;
+    q = b;
+    return lane == 0 && c < C;
+  } else {
+    if (lane == 0) { red[0][wv] = a; red[1][wv] = b; }
+    __syncthreads();
+    s = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    q = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    return threadIdx.x == 0 && c < C;
+  }
 }
 
 // forward finalize: stats + running stats + per-channel scale/shift
+template <bool WPC>
 __global__ __launch_bounds__(kBlock) void k_bn_finalize_fwd(const float* __restrict__ pa, const float* __restrict__ pb,
                                                             int nrb, int C, int64_t M, const float* __restrict__ w,
                                                             const float* __restrict__ bias, float eps, float momentum,
@@ -183,8 +196,8 @@ __global__ __launch_bounds__(kBlock) void k_bn_finalize_fwd(const float* __restr
                                                             float* __restrict__ invstd, float* __restrict__ scale,
                                                             float* __restrict__ shift) {
   double s, q;
-  if (!combine_partials(pa, pb, nrb, C, s, q)) return;
-  const int c = blockIdx.x;
+  int c;
+  if (!combine_partials<WPC>(pa, pb, nrb, C, s, q, c)) return;
   const double m = s / (double)M;
   double var = q / (double)M - m * m;
   if (var < 0.0) var = 0.0;
@@ -202,6 +215,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_finalize_fwd(const float* __restr
 }
 
 // backward finalize: dgamma, dbeta and dx = a*dz + k1*x + k0 coefficients
+template <bool WPC>
 __global__ __launch_bounds__(kBlock) void k_bn_finalize_bwd(const float* __restrict__ pa, const float* __restrict__ pb,
                                                             int nrb, int C, int64_t M, const float* __restrict__ w,
                                                             const float* __restrict__ mean,
@@ -209,8 +223,8 @@ __global__ __launch_bounds__(kBlock) void k_bn_finalize_bwd(const float* __restr
                                                             float* __restrict__ db, float* __restrict__ ca,
                                                             float* __restrict__ ck1, float* __restrict__ ck0) {
   double s, q;
-  if (!combine_partials(pa, pb, nrb, C, s, q)) return;
-  const int c = blockIdx.x;
+  int c;
+  if (!combine_partials<WPC>(pa, pb, nrb, C, s, q, c)) return;
   if (dw) dw[c] = (float)q;
   if (db) db[c] = (float)s;
   const double is = invstd[c];
@@ -220,6 +234,26 @@ __global__ __launch_bounds__(kBlock) void k_bn_finalize_bwd(const float* __restr
   ca[c] = (float)a;
   ck1[c] = (float)k1;
   ck0[c] = (float)k0;
+}
+
+static void fin_fwd(hipStream_t st, const float* pa, const float* pb, int nrb, int C, int64_t M, const float* w,
+                    const float* bias, float eps, float mom, float* rm, float* rv, float* mean, float* invstd,
+                    float* scale, float* shift) {
+  if (nrb <= 512)
+    hipLaunchKernelGGL(k_bn_finalize_fwd<true>, (C + kBlock / 64 - 1) / (kBlock / 64), kBlock, 0, st, pa, pb, nrb, C, M,
+                       w, bias, eps, mom, rm, rv, mean, invstd, scale, shift);
+  else
+    hipLaunchKernelGGL(k_bn_finalize_fwd<false>, C, kBlock, 0, st, pa, pb, nrb, C, M, w, bias, eps, mom, rm, rv, mean,
+                       invstd, scale, shift);
+}
+static void fin_bwd(hipStream_t st, const float* pa, const float* pb, int nrb, int C, int64_t M, const float* w,
+                    const float* mean, const float* invstd, float* dw, float* db, float* ca, float* ck1, float* ck0) {
+  if (nrb <= 512)
+    hipLaunchKernelGGL(k_bn_finalize_bwd<true>, (C + kBlock / 64 - 1) / (kBlock / 64), kBlock, 0, st, pa, pb, nrb, C, M,
+                       w, mean, invstd, dw, db, ca, ck1, ck0);
+  else
+    hipLaunchKernelGGL(k_bn_finalize_bwd<false>, C, kBlock, 0, st, pa, pb, nrb, C, M, w, mean, invstd, dw, db, ca, ck1,
+                       ck0);
 }
 
 // y = act(x*scale + shift [+ res]); with rsc/rsh the residual is itself a pre-BN tensor whose
@@ -445,7 +479,7 @@ void finalize_apply_fwd(const at::Tensor& part, int nrb, const at::Tensor& x, co
                         double momentum, bool relu, hipStream_t stream) {
   const float* pa = part.data_ptr<float>();
   const float* pb = pa + C * (int64_t)nrb;
-  hipLaunchKernelGGL(k_bn_finalize_fwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, pa, pb, nrb, (int)C, M,
+  fin_fwd( stream, pa, pb, nrb, (int)C, M,
                      weight.data_ptr<float>(), bias.data_ptr<float>(), (float)eps, (float)momentum, rm, rv,
                      mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
                      shift.data_ptr<float>());
@@ -515,7 +549,7 @@ void bn_finalize_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tensor we
     rm = running_mean->data_ptr<float>();
     rv = running_var->data_ptr<float>();
   }
-  hipLaunchKernelGGL(k_bn_finalize_fwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, c10::hip::getCurrentHIPStream(),
+  fin_fwd( c10::hip::getCurrentHIPStream(),
                      part[0].data_ptr<float>(), part[1].data_ptr<float>(), (int)nrb, (int)C, M,
                      weight.data_ptr<float>(), bias.data_ptr<float>(), (float)eps, (float)momentum, rm, rv,
                      mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
@@ -534,7 +568,7 @@ void bn_finalize_bwd_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tenso
   TORCH_CHECK(coef.is_cuda() && coef.scalar_type() == at::kFloat && coef.is_contiguous() && coef.numel() == 3 * C,
               "bn_finalize_bwd_partials: coef must be f32 [3, C]");
   for (auto* t : {&weight, &mean, &invstd, &dweight, &dbias}) check_vec(*t, "per-channel vector", (int)C);
-  hipLaunchKernelGGL(k_bn_finalize_bwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, c10::hip::getCurrentHIPStream(),
+  fin_bwd( c10::hip::getCurrentHIPStream(),
                      part[0].data_ptr<float>(), part[1].data_ptr<float>(), (int)nrb, (int)C, M,
                      weight.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
                      dweight.data_ptr<float>(), dbias.data_ptr<float>(), coef[0].data_ptr<float>(),
@@ -565,7 +599,7 @@ void bn_forward_stats(at::Tensor x, at::Tensor weight, at::Tensor bias, c10::opt
   hipLaunchKernelGGL((k_bn_reduce<false, MASK_NONE, 8>), nrb, kBlock, 0, stream, (const uint16_t*)x.data_ptr(),
                      nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, M, (int)C, rows, nrb,
                      part[0].data_ptr<float>(), part[1].data_ptr<float>());
-  hipLaunchKernelGGL(k_bn_finalize_fwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, part[0].data_ptr<float>(),
+  fin_fwd( stream, part[0].data_ptr<float>(),
                      part[1].data_ptr<float>(), nrb, (int)C, M, weight.data_ptr<float>(), bias.data_ptr<float>(),
                      (float)eps, (float)momentum, rm, rv, mean.data_ptr<float>(), invstd.data_ptr<float>(),
                      scale.data_ptr<float>(), shift.data_ptr<float>());
@@ -636,7 +670,7 @@ void bn_backward(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> y, int64
     case MASK_Y: red(k_bn_reduce<true, MASK_Y, 4>); break;
     default: red(k_bn_reduce<true, MASK_BITS, 4>); break;
   }
-  hipLaunchKernelGGL(k_bn_finalize_bwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, part[0].data_ptr<float>(),
+  fin_bwd( stream, part[0].data_ptr<float>(),
                      part[1].data_ptr<float>(), nrb, (int)C, M, weight.data_ptr<float>(), mean.data_ptr<float>(),
                      invstd.data_ptr<float>(), dweight.data_ptr<float>(), dbias.data_ptr<float>(),
                      coef[0].data_ptr<float>(), coef[1].data_ptr<float>(), coef[2].data_ptr<float>());
@@ -730,7 +764,7 @@ void bn_backward_partials(at::Tensor part, int64_t nrb, at::Tensor dy, at::Tenso
   auto coef = at::empty({3, C}, weight.options());
   auto stream = c10::hip::getCurrentHIPStream();
   const float* pa = part.data_ptr<float>();
-  hipLaunchKernelGGL(k_bn_finalize_bwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, pa, pa + C * nrb,
+  fin_bwd( stream, pa, pa + C * nrb,
                      (int)nrb, (int)C, M, weight.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
                      dweight.data_ptr<float>(), dbias.data_ptr<float>(), coef[0].data_ptr<float>(),
                      coef[1].data_ptr<float>(), coef[2].data_ptr<float>());
@@ -783,7 +817,7 @@ void bn_dual_forward(at::Tensor part3, int64_t nrb3, at::Tensor partd, int64_t n
   auto fin = [&](const at::Tensor& part, int64_t nrb, at::Tensor& w, at::Tensor& b, at::Tensor& rm, at::Tensor& rv,
                  at::Tensor& mean, at::Tensor& invstd, at::Tensor& scale, at::Tensor& shift, double eps, double mom) {
     const float* pa = part.data_ptr<float>();
-    hipLaunchKernelGGL(k_bn_finalize_fwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, pa, pa + C * nrb,
+    fin_fwd( stream, pa, pa + C * nrb,
                        (int)nrb, (int)C, M, w.data_ptr<float>(), b.data_ptr<float>(), (float)eps, (float)mom,
                        rm.data_ptr<float>(), rv.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
                        scale.data_ptr<float>(), shift.data_ptr<float>());
@@ -832,7 +866,7 @@ void bn_dual_backward(c10::optional<at::Tensor> part3, int64_t nrb3, at::Tensor 
   auto pd = at::empty({2, C, (int64_t)nrb}, w3.options());
   auto finb = [&](const float* pa, int64_t n, at::Tensor& w, at::Tensor& mean, at::Tensor& invstd, at::Tensor& dw,
                   at::Tensor& db, at::Tensor& coef) {
-    hipLaunchKernelGGL(k_bn_finalize_bwd, (int)((C + kFinCh - 1) / kFinCh), kBlock, 0, stream, pa, pa + C * n, (int)n,
+    fin_bwd( stream, pa, pa + C * n, (int)n,
                        (int)C, M, w.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
                        dw.data_ptr<float>(), db.data_ptr<float>(), coef[0].data_ptr<float>(), coef[1].data_ptr<float>(),
                        coef[2].data_ptr<float>());
