@@ -236,10 +236,13 @@ __global__ __launch_bounds__(kBlock) void k_bn_finalize_bwd(const float* __restr
   ck0[c] = (float)k0;
 }
 
+// wave-per-channel finalize: measured no faster in the step (the ~5 us per call is launch
+// latency, not the combine), so it is off (kWpcMax = 0); kept for the micro-benchmarks
+constexpr int kWpcMax = 0;
 static void fin_fwd(hipStream_t st, const float* pa, const float* pb, int nrb, int C, int64_t M, const float* w,
                     const float* bias, float eps, float mom, float* rm, float* rv, float* mean, float* invstd,
                     float* scale, float* shift) {
-  if (nrb <= 512)
+  if (nrb <= kWpcMax)
     hipLaunchKernelGGL(k_bn_finalize_fwd<true>, (C + kBlock / 64 - 1) / (kBlock / 64), kBlock, 0, st, pa, pb, nrb, C, M,
                        w, bias, eps, mom, rm, rv, mean, invstd, scale, shift);
   else
@@ -248,7 +251,7 @@ static void fin_fwd(hipStream_t st, const float* pa, const float* pb, int nrb, i
 }
 static void fin_bwd(hipStream_t st, const float* pa, const float* pb, int nrb, int C, int64_t M, const float* w,
                     const float* mean, const float* invstd, float* dw, float* db, float* ca, float* ck1, float* ck0) {
-  if (nrb <= 512)
+  if (nrb <= kWpcMax)
     hipLaunchKernelGGL(k_bn_finalize_bwd<true>, (C + kBlock / 64 - 1) / (kBlock / 64), kBlock, 0, st, pa, pb, nrb, C, M,
                        w, mean, invstd, dw, db, ca, ck1, ck0);
   else
@@ -257,7 +260,10 @@ static void fin_bwd(hipStream_t st, const float* pa, const float* pb, int nrb, i
 }
 
 // y = act(x*scale + shift [+ res]); with rsc/rsh the residual is itself a pre-BN tensor whose
-// BN is applied in the same pass: res*rsc + rsh (a ResNet downsample branch, never materialised)
+// BN is applied in the same pass: res*rsc + rsh (a ResNet downsample branch, never materialised).
+// UNR vectors in flight per lane (UNR = 4 on the small layer-3/4 tensors measured no faster in the
+// step, so every call site uses 1).
+template <int UNR = 1>
 __global__ __launch_bounds__(kBlock) void k_bn_apply_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                          uint16_t* __restrict__ y, uint8_t* __restrict__ mbits,
                                                          const float* __restrict__ scale,
@@ -275,15 +281,10 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_fwd(const uint16_t* __restr
     load8f(rsc + c0, rs);
     load8f(rsh + c0, rh);
   }
-  for (int64_t v = v0; v < V; v += stride) {
-    const int64_t off = v * 8;
-    float xv[8];
-    load8(x + off, xv);
+  auto body = [&](float* xv, float* rv, int64_t v) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) xv[j] = fmaf(xv[j], sc[j], sh[j]);
     if (res) {
-      float rv[8];
-      load8(res + off, rv);
       if (rsc) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) rv[j] = fmaf(rv[j], rs[j], rh[j]);
@@ -295,13 +296,32 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_fwd(const uint16_t* __restr
 #pragma unroll
       for (int j = 0; j < 8; ++j) xv[j] = fmaxf(xv[j], 0.f);
     }
-    store8(y + off, xv);
+    store8(y + v * 8, xv);
     if (mbits) {
       uint32_t b = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) b |= (xv[j] > 0.f ? 1u : 0u) << j;
       mbits[v] = (uint8_t)b;
     }
+  };
+  int64_t v = v0;
+  if constexpr (UNR > 1) {
+    for (; v + (UNR - 1) * stride < V; v += UNR * stride) {
+      float xv[UNR][8], rv[UNR][8];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        load8(x + (v + u * stride) * 8, xv[u]);
+        if (res) load8(res + (v + u * stride) * 8, rv[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) body(xv[u], rv[u], v + u * stride);
+    }
+  }
+  for (; v < V; v += stride) {
+    float xv[8], rv[8];
+    load8(x + v * 8, xv);
+    if (res) load8(res + v * 8, rv);
+    body(xv, rv, v);
   }
 }
 
@@ -483,9 +503,9 @@ void finalize_apply_fwd(const at::Tensor& part, int nrb, const at::Tensor& x, co
                      weight.data_ptr<float>(), bias.data_ptr<float>(), (float)eps, (float)momentum, rm, rv,
                      mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
                      shift.data_ptr<float>());
-  hipLaunchKernelGGL(k_bn_apply_fwd, apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)x.data_ptr(), rp,
+  hipLaunchKernelGGL(k_bn_apply_fwd<1>, apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)x.data_ptr(), rp,
                      (uint16_t*)y.data_ptr(), mo, scale.data_ptr<float>(), shift.data_ptr<float>(), M, (int)C,
-                     (int)relu);
+                     (int)relu, nullptr, nullptr);
 }
 }  // namespace
 
@@ -619,9 +639,9 @@ void bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, at::Ten
   }
   check_vec(scale, "scale", (int)C);
   check_vec(shift, "shift", (int)C);
-  hipLaunchKernelGGL(k_bn_apply_fwd, apply_grid(M, (int)C), kBlock, 0, c10::hip::getCurrentHIPStream(),
+  hipLaunchKernelGGL(k_bn_apply_fwd<1>, apply_grid(M, (int)C), kBlock, 0, c10::hip::getCurrentHIPStream(),
                      (const uint16_t*)x.data_ptr(), rp, (uint16_t*)y.data_ptr(), nullptr, scale.data_ptr<float>(),
-                     shift.data_ptr<float>(), M, (int)C, (int)relu);
+                     shift.data_ptr<float>(), M, (int)C, (int)relu, nullptr, nullptr);
 }
 
 // returns nothing; writes dx (and dres), dweight, dbias
@@ -824,7 +844,7 @@ void bn_dual_forward(at::Tensor part3, int64_t nrb3, at::Tensor partd, int64_t n
   };
   fin(part3, nrb3, w3, b3, rm3, rv3, mean3, invstd3, scale3, shift3, eps3, mom3);
   fin(partd, nrbd, wd, bd, rmd, rvd, meand, invstdd, scaled, shiftd, epsd, momd);
-  hipLaunchKernelGGL(k_bn_apply_fwd, apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)x3.data_ptr(),
+  hipLaunchKernelGGL(k_bn_apply_fwd<1>, apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)x3.data_ptr(),
                      (const uint16_t*)xd.data_ptr(), (uint16_t*)z.data_ptr(), (uint8_t*)mask.data_ptr(),
                      scale3.data_ptr<float>(), shift3.data_ptr<float>(), M, (int)C, 1, scaled.data_ptr<float>(),
                      shiftd.data_ptr<float>());
