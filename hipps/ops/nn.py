@@ -51,6 +51,61 @@ _DGRAD_S2 = _GEMM2 and _os.environ.get("HIPPS_DGRAD_S2", "0") != "0"
 
 MASK_NONE, MASK_X, MASK_Y, MASK_BITS = 0, 1, 2, 3
 
+# weight gradients on a side stream: a conv's dw only feeds its gradient bucket, so it runs beside
+# the input-gradient / BatchNorm-backward chain (which the rest of the backward waits on) instead of
+# in series with it (ResNet-50 bs256: 23.0 -> 22.0 ms/step, profiles/r3b/ab_wgs).  The bucket encode
+# waits for the side stream (engine.encode_bucket), and the caller's stream joins it at the end of
+# every backward (an autograd final callback), so whatever reads .grad after backward() -- step(),
+# clipping -- sees finished gradients.  Only for a parameter whose .grad is None, without tensor
+# hooks, and whose dw has the parameter's layout: autograd then stores dw as is (no accumulate or
+# layout copy on the main stream that would read it early).
+_WGRAD_SIDE = _os.environ.get("HIPPS_WGRAD_STREAM", "1") != "0"
+_WG_STREAMS: dict = {}
+_WG_JOINED: dict = {}  # device -> autograd graph task whose end joins the side stream
+
+
+def wgrad_stream(device):
+    """The weight-gradient side stream of ``device`` if one was used, else None."""
+    idx = device.index if isinstance(device, torch.device) else device
+    return _WG_STREAMS.get(idx)
+
+
+def _same_layout(a, b):
+    return a.shape == b.shape and all(sa == sb for n, sa, sb in zip(a.shape, a.stride(), b.stride()) if n > 1)
+
+
+def _join_wgrad(idx):
+    torch.cuda.current_stream(idx).wait_stream(_WG_STREAMS[idx])
+
+
+def _on_wgrad_stream(param, tensors, fn):
+    """fn() (allocates and returns dw) on the weight-gradient side stream when enabled and
+    ``param`` takes dw as is; ``tensors`` (its inputs) are recorded on that stream."""
+    if not (_WGRAD_SIDE and param is not None and param.grad is None and tensors[0].is_cuda
+            and not param._backward_hooks):
+        return fn()
+    dev = tensors[0].device
+    idx = dev.index
+    side = _WG_STREAMS.get(idx)
+    if side is None:
+        side = _WG_STREAMS[idx] = torch.cuda.Stream(device=dev)
+    cur = torch.cuda.current_stream(dev)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        out = fn()
+    for t in tensors:
+        t.record_stream(side)
+    if out.dtype != param.dtype or not _same_layout(out, param):
+        cur.wait_stream(side)  # autograd would copy dw on this stream
+    else:
+        task = torch._C._current_graph_task_id()
+        if task < 0:  # not inside an autograd backward pass
+            cur.wait_stream(side)
+        elif _WG_JOINED.get(idx) != task:
+            torch.autograd.Variable._execution_engine.queue_callback(lambda: _join_wgrad(idx))
+            _WG_JOINED[idx] = task
+    return out
+
 
 class _Tuner:
     """Per-shape kernel choice by measurement (like cudnn.benchmark): on the first call for a
@@ -529,6 +584,7 @@ class _Conv1x1(torch.autograd.Function):
     def forward(ctx, x, w_master, stride, tap=None, alias=False, bngrad=None, s2tap=None):
         w = bf16_weight(w_master)
         ctx.wdtype = w_master.dtype
+        ctx.wparam = w_master
         # no zero-filled grad for the non-differentiable BN partials (a 12.8 MB fill per layer)
         ctx.set_materialize_grads(False)
         ctx.wt = _TSHADOWS.get(w_master.data_ptr()) if w_master.dtype == torch.float32 else None
@@ -587,10 +643,13 @@ class _Conv1x1(torch.autograd.Function):
             dw = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1,
                                                      [False, True, False])[1].to(ctx.wdtype)
         elif ctx.needs_input_grad[1]:
-            dw = torch.empty(w.shape, dtype=torch.float32, device=w.device)
-            _conv_wgrad(dy, x, dw, 1, 1, s, 0)
-            if ctx.wdtype != torch.float32:
-                dw = dw.to(ctx.wdtype)
+            def wg():
+                d = torch.empty(w.shape, dtype=torch.float32, device=w.device)
+                _conv_wgrad(dy, x, d, 1, 1, s, 0)
+                return d if ctx.wdtype == torch.float32 else d.to(ctx.wdtype)
+
+            dw = _on_wgrad_stream(ctx.wparam, (dy, x), wg)
+        ctx.wparam = None
         if s2_dx:  # compact gradient at the output positions, summed in conv1's dgrad epilogue
             cout, cin = w.shape[0], w.shape[1]
             wt = ctx.wt if ctx.wt is not None else w.reshape(cout, cin).t().contiguous()
@@ -698,6 +757,7 @@ class _ConvKxK(torch.autograd.Function):
     def forward(ctx, x, w_master, stride, pad, own_wgrad=True, stats=False, bngrad=None):
         w = bf16_weight(w_master)
         ctx.wdtype = w_master.dtype
+        ctx.wparam = w_master
         ctx.own_wgrad = own_wgrad
         # x is the output of a fused BN whose only gradient is this conv's input gradient: the
         # input gradient (stride 1: a forward conv on gemm2; stride 2: the parity GEMMs) reduces
@@ -771,10 +831,13 @@ class _ConvKxK(torch.autograd.Function):
             dw = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
                                                      [False, True, False])[1].to(ctx.wdtype)
         elif ctx.needs_input_grad[1]:
-            dw = torch.empty(w.shape, dtype=torch.float32, device=w.device, memory_format=torch.channels_last)
-            _conv_wgrad(dy, x, dw, w.shape[2], w.shape[3], s, p)
-            if ctx.wdtype != torch.float32:
-                dw = dw.to(ctx.wdtype)
+            def wg():
+                d = torch.empty(w.shape, dtype=torch.float32, device=w.device, memory_format=torch.channels_last)
+                _conv_wgrad(dy, x, d, w.shape[2], w.shape[3], s, p)
+                return d if ctx.wdtype == torch.float32 else d.to(ctx.wdtype)
+
+            dw = _on_wgrad_stream(ctx.wparam, (dy, x), wg)
+        ctx.wparam = None
         return dx, dw, None, None, None, None, None
 
 

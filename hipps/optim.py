@@ -227,6 +227,12 @@ class MPI_PS(torch.optim.Optimizer):
                 loss = closure()
         self.steps += 1
         t0 = time.perf_counter()
+        if self.store.device.type == "cuda":
+            from .ops.nn import wgrad_stream
+
+            wgs = wgrad_stream(self.store.device)
+            if wgs is not None:  # gradients computed on the weight-gradient side stream
+                torch.cuda.current_stream(self.store.device).wait_stream(wgs)
         data = self.engine.step()
         self._refresh_shadow()
         now = time.perf_counter()

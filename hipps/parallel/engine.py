@@ -179,8 +179,13 @@ class Engine:
         if self.cuda:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.store.device))
+            from hipps.ops.nn import wgrad_stream
+
+            wgs = wgrad_stream(self.store.device)
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
+                if wgs is not None:  # weight gradients computed beside the backward chain
+                    self.comm_stream.wait_stream(wgs)
                 with self.tracer.phase("encode", self.comm_stream):
                     if self.grad_mode == "gather" and self._gather_bucket(bi, views):
                         pass  # dense codec: the gather already wrote the wire image
@@ -486,8 +491,13 @@ class LocalEngine(Engine):
             b = self.plan.buckets[bi]
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.store.device))
+            from hipps.ops.nn import wgrad_stream
+
+            wgs = wgrad_stream(self.store.device)
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
+                if wgs is not None:
+                    self.comm_stream.wait_stream(wgs)
                 with self.tracer.phase("encode", self.comm_stream):
                     self._gather_bucket(bi, None, to_flat=True)
                     if not self._bypass:

@@ -174,3 +174,34 @@ def test_gpu_dual_bn_relu_matches_fp32(with_part3):
         torch.testing.assert_close(mine.bias.grad, ref.bias.grad, rtol=2e-2, atol=5e-2)
         torch.testing.assert_close(mine.running_mean, ref.running_mean, rtol=1e-4, atol=1e-4)
         torch.testing.assert_close(mine.running_var, ref.running_var, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_gpu_wgrad_side_stream_grads_ready_after_backward(monkeypatch):
+    """Weight gradients computed on the side stream are complete when backward() returns: read
+    straight after it on the caller's stream (as a clip_grad_norm_ would), they equal the in-line
+    ones.  A second backward (accumulation into an existing .grad) takes the in-line path."""
+    import copy
+
+    import hipps.ops.nn as hnn
+    from hipps.models.resnet import ResNet, Bottleneck
+
+    torch.manual_seed(4)
+    base = ResNet(Bottleneck, [1, 1], num_classes=10, width=64).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(32, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (32,), device="cuda")
+
+    def grads(side, twice=False):
+        monkeypatch.setattr(hnn, "_WGRAD_SIDE", side)
+        m = copy.deepcopy(base)
+        for _ in range(2 if twice else 1):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                F.cross_entropy(m(x), y).backward()
+        return torch.cat([p.grad.float().flatten() for p in m.parameters()])  # no synchronize first
+
+    grads(False)  # tuner warm-up
+    ref = grads(False)
+    got = grads(True)
+    assert hnn.wgrad_stream(0) is not None
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(grads(True, twice=True), grads(False, twice=True), rtol=1e-4, atol=1e-6)

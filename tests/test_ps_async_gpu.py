@@ -220,3 +220,51 @@ def test_gpu_bucket_granularity_three_ranks_device_pull():
         adopted = out[r]["selb"][nb:]
         assert min(adopted) >= 1 and max(adopted) <= steps  # every bucket adopted a real version
         assert sum(out[r]["losses"][-3:]) < sum(out[r]["losses"][:3])
+
+
+def _gpu_wgrad_side(rank, world):
+    import copy
+
+    import torch.nn.functional as F
+
+    import hipps
+    import hipps.ops.nn as hnn
+    from hipps.models.resnet import Bottleneck, ResNet
+
+    torch.cuda.set_device(0)
+    torch.manual_seed(5)
+    base = ResNet(Bottleneck, [1, 1], num_classes=10, width=64).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(16, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (16,), device="cuda")
+
+    def train(side, steps=3):
+        hnn._WGRAD_SIDE = side
+        m = copy.deepcopy(base)
+        opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", code="fp32", max_delay=0)
+        for _ in range(steps):
+            opt.zero_grad()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = F.cross_entropy(m(x), y)
+            loss.backward()
+            opt.step()
+        torch.cuda.synchronize()
+        opt.close()
+        return [p.detach().float().cpu() for p in m.parameters()]
+
+    train(False, 1)  # fills the per-shape kernel tuner: both runs below use the same kernels
+    ref = train(False)
+    ref2 = train(False)
+    print("in-line run-to-run max diff", max((a - b).abs().max().item() for a, b in zip(ref, ref2)))
+    side = train(True)
+    return {"ref": ref, "side": side, "used": hnn.wgrad_stream(0) is not None}
+
+
+def test_gpu_wgrad_side_stream_bitwise():
+    """Weight gradients on the side stream (HIPPS_WGRAD_STREAM) give the training trajectory of
+    in-line weight gradients: the bucket encode and step() wait for that stream (a missed wait reads
+    a half-written gradient).  Not bitwise: two in-line runs already differ in the last bit of a
+    few BN parameters (library kernels with atomics on the Cin=64 3x3 weight gradient)."""
+    out = run_world(_gpu_wgrad_side, 1, timeout=300)[0]
+    assert out["used"]
+    for a, b in zip(out["ref"], out["side"]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
