@@ -109,8 +109,8 @@ def _on_wgrad_stream(param, tensors, fn):
 
 class _Tuner:
     """Per-shape kernel choice by measurement (like cudnn.benchmark): on the first call for a
-    key, every candidate runs once to warm up and then 3 times between HIP events on the current
-    stream; the fastest name is cached.  Candidates must be side-effect free apart from writing
+    key, every candidate runs once to warm up and then, with the device drained, 3 times between
+    HIP events on the current stream; the fastest name is cached.  Candidates must be side-effect free apart from writing
     their output (every candidate writes the same values)."""
 
     def __init__(self):
@@ -126,6 +126,9 @@ class _Tuner:
         else:
             for fn in cands.values():
                 fn()
+            # drain every stream first: kernels still running on another stream (the weight-gradient
+            # side stream, the PS stream) would otherwise share the GPU with the timed candidates
+            torch.cuda.synchronize()
             t = {}
             for name, fn in cands.items():
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

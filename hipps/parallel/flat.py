@@ -122,6 +122,12 @@ class FlatStore:
             return
         v = self._view(self.grad, s, p.data)
         if g.data_ptr() != v.data_ptr():
+            if g.is_cuda:
+                from hipps.ops.nn import wgrad_stream
+
+                wgs = wgrad_stream(g.device)
+                if wgs is not None:  # g may still be written on the weight-gradient side stream
+                    torch.cuda.current_stream(g.device).wait_stream(wgs)
             v.copy_(g)
             p.grad = v
 
