@@ -138,12 +138,27 @@ def main():
     pull_overlap = bool(N > 1 and not a.no_pull_overlap and hasattr(model, "layer4")
                         and opt.overlap_pull(model.layer4))
 
+    host_t = [0.0] * 7 if os.environ.get("HIPPS_HOST_TIMING") else None  # diagnostics: host s per phase
+
     def step():
+        if host_t is not None:
+            t = [time.perf_counter()]
         opt.zero_grad()
         with torch.autocast("cuda", dtype=torch.bfloat16):
             loss = model(x, y) if is_tf else F.cross_entropy(model(x), y)
+        if host_t is not None:
+            t.append(time.perf_counter())
         loss.backward()
+        if host_t is not None:
+            t.append(time.perf_counter())
         _, data = opt.step()
+        if host_t is not None:
+            t.append(time.perf_counter())
+            for i in range(3):
+                host_t[i] += t[i + 1] - t[i]
+            host_t[3] += 1
+            for i, k in enumerate(("slot_wait", "code_wait", "comm_wait")):
+                host_t[4 + i] += float(data.get(k, 0.0))
         return loss, data
 
     ps_only = bool(getattr(opt, "ps_only", False))
@@ -181,6 +196,8 @@ def main():
         tr.totals.clear()
     hdist.barrier(world)
     torch.cuda.synchronize()
+    if host_t is not None:
+        host_t[:] = [0.0] * 7
     t0 = time.perf_counter()
     last = None
     for _ in range(a.steps):
@@ -194,6 +211,10 @@ def main():
     if N > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
+    if host_t is not None and host_t[3]:
+        print("[bench] host ms/step: forward %.2f backward %.2f step %.2f (wall %.2f); waits: slot %.2f "
+              "encode %.2f pull %.2f" % tuple([1e3 * v / host_t[3] for v in host_t[:3]] + [1e3 * elapsed / a.steps]
+                                              + [1e3 * v / host_t[3] for v in host_t[4:]]), file=sys.stderr)
     if dedicated and N > 1:  # the losses live on the workers: rank 1 reports them
         box = [(first_loss, [float(v.float()) for v in losses], last)]
         allb = [None] * N

@@ -48,11 +48,47 @@ def main():
                       f"launches/step={len(steady) / n:.0f}"]
     for k, v in sorted(cat.items(), key=lambda x: -x[1]):
         lines.append(f"  {k:18s} {v / n / 1e6:8.3f} ms/step {100 * v / tot:5.1f}%")
+    # GPU idle time: the wall time no kernel covers (side-stream kernels overlap, so the kernel
+    # sum can exceed the wall), and the longest idle gaps with the kernel that ended before them
+    busy, cur_s, cur_e, gaps = 0, None, None, collections.defaultdict(lambda: [0, 0])
+    prev = ""
+    for r in steady:
+        st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if cur_e is None or st > cur_e:
+            if cur_e is not None:
+                busy += cur_e - cur_s
+                g = gaps[prev[:60] + " -> " + r["Kernel_Name"][:60]]
+                g[0] += st - cur_e
+                g[1] += 1
+            cur_s, cur_e = st, en
+        else:
+            cur_e = max(cur_e, en)
+        if en >= cur_e:
+            prev = r["Kernel_Name"]
+    if cur_e is not None:
+        busy += min(cur_e, t1) - cur_s
+    lines.append(f"GPU busy/step={busy / n / 1e6:.2f} ms idle/step={((t1 - t0) - busy) / n / 1e6:.2f} ms")
+    for k, (d, c) in sorted(gaps.items(), key=lambda x: -x[1][0])[:12]:
+        lines.append(f"  idle {d / n / 1e3:7.1f} us/step gaps/step={c / n:5.1f}  {k}")
+    # one steady step's idle gaps >= 40 us in context (stream / queue ids when the trace has them)
+    sid = next((c for c in ("Stream_Id", "Queue_Id") if c in rows[0]), None)
+    m0, m1 = marks[a.skip + n // 2], marks[a.skip + n // 2 + 1]
+    one = [r for r in rows if m0 <= int(r["Start_Timestamp"]) < m1]
+    lines.append(f"step timeline gaps (step {a.skip + n // 2}, {len(one)} kernels, t=0 at its marker):")
+    end = None
+    for j, r in enumerate(one):
+        st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if end is not None and st - end >= 40000:
+            for q in one[max(0, j - 2):j + 2]:
+                lines.append(f"    t={(int(q['Start_Timestamp']) - m0) / 1e3:9.1f} us dur={(int(q['End_Timestamp']) - int(q['Start_Timestamp'])) / 1e3:7.1f}"
+                             f" {('s' + str(q[sid])) if sid else ''} {q['Kernel_Name'][:70]}")
+            lines.append(f"  ^ idle {(st - end) / 1e3:.1f} us")
+        end = en if end is None else max(end, en)
     lines.append("")
     for k, (d, c) in sorted(agg.items(), key=lambda x: -x[1][0])[:60]:
         lines.append(f"{d / n / 1e3:9.1f} us/step calls/step={c / n:6.1f}  {k[:140]}")
     open(a.out, "w").write("\n".join(lines) + "\n")
-    print("\n".join(lines[:12]))
+    print("\n".join(lines[:24]))
 
 
 if __name__ == "__main__":
