@@ -54,6 +54,8 @@ def parse():
                          "xGMI pull; the PS keeps the fp32 master, workers compute in bf16 anyway)")
     ap.add_argument("--momentum", type=float, default=0.9)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--mailbox-slots", type=int, default=0,
+                    help="ps_async: bucket messages in flight per worker (0 = the library's auto)")
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--no-fallback", action="store_true",
@@ -118,6 +120,7 @@ def main():
     dedicated = bool(a.ps_dedicated and mode == "ps_async" and N > 1)
     kw = dict(lr=a.lr, momentum=a.momentum, weight_decay=5e-5, mode=mode, code=a.codec,
               accumulate=a.accumulate or None, average=True, param_wire=a.param_wire, bucket_mb=a.bucket_mb,
+              mailbox_slots=a.mailbox_slots,
               async_transport=a.async_transport, ps_dedicated=dedicated)
     if a.emulate_remote and N == 1:
         kw["emulate_remote"] = a.emulate_remote
@@ -198,6 +201,7 @@ def main():
     torch.cuda.synchronize()
     if host_t is not None:
         host_t[:] = [0.0] * 7
+        ms0 = torch.cuda.memory_stats(dev)
     t0 = time.perf_counter()
     last = None
     for _ in range(a.steps):
@@ -215,6 +219,11 @@ def main():
         print("[bench] host ms/step: forward %.2f backward %.2f step %.2f (wall %.2f); waits: slot %.2f "
               "encode %.2f pull %.2f" % tuple([1e3 * v / host_t[3] for v in host_t[:3]] + [1e3 * elapsed / a.steps]
                                               + [1e3 * v / host_t[3] for v in host_t[4:]]), file=sys.stderr)
+        ms1 = torch.cuda.memory_stats(dev)
+        print("[bench] allocator during timed steps: " + " ".join(
+            f"{k}+{ms1.get(k, 0) - ms0.get(k, 0)}" for k in ("num_alloc_retries", "num_device_alloc", "num_device_free",
+                                                              "num_sync_all_streams", "segment.all.allocated"))
+              + f" reserved={ms1.get('reserved_bytes.all.current', 0) / 2**30:.1f} GiB", file=sys.stderr)
     if dedicated and N > 1:  # the losses live on the workers: rank 1 reports them
         box = [(first_loss, [float(v.float()) for v in losses], last)]
         allb = [None] * N

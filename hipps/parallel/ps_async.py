@@ -353,6 +353,11 @@ class PSAsyncEngine(Engine):
         if self.rank == 0:
             if self.dedicated:
                 self.remove_hooks()  # rank 0 computes no gradients
+            sw = float(os.environ.get("HIPPS_GIL_SWITCH_US", "0"))
+            if sw > 0:  # the PS thread shares the GIL with the trainer: hand it over sooner
+                import sys
+
+                sys.setswitchinterval(sw * 1e-6)
             self._thread = threading.Thread(target=self._serve_guard, name="hipps-ps", daemon=True)
             self._thread.start()
         barrier(world)

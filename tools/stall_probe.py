@@ -1,0 +1,46 @@
+"""For each long GPU idle gap in a rocprofv3 kernel trace, show when the host LAUNCHED the kernel
+that ended it (hip API trace, matched by correlation id) and the host API calls around the gap:
+a launch after the gap began means the host was late; a launch before it means the GPU waited
+on a dependency.
+    python tools/stall_probe.py kernel_trace.csv hip_api_trace.csv out.txt [--min-us 300]"""
+import argparse
+import csv
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("ktrace")
+    ap.add_argument("htrace")
+    ap.add_argument("out")
+    ap.add_argument("--min-us", type=float, default=300)
+    ap.add_argument("--skip", type=int, default=5)
+    a = ap.parse_args()
+    ks = sorted(csv.DictReader(open(a.ktrace)), key=lambda r: int(r["Start_Timestamp"]))
+    hs = sorted(csv.DictReader(open(a.htrace)), key=lambda r: int(r["Start_Timestamp"]))
+    by_corr = {r["Correlation_Id"]: r for r in hs}
+    marks = [int(r["Start_Timestamp"]) for r in ks if "k_sgd" in r["Kernel_Name"]]
+    t0 = marks[a.skip] if len(marks) > a.skip else int(ks[0]["Start_Timestamp"])
+    lines, end, n = [], None, 0
+    for r in ks:
+        st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if st < t0:
+            end = en if end is None else max(end, en)
+            continue
+        if end is not None and st - end >= a.min_us * 1e3 and n < 6:
+            n += 1
+            h = by_corr.get(r["Correlation_Id"])
+            lines.append(f"gap {(st - end) / 1e3:.1f} us before {r['Kernel_Name'][:80]}")
+            if h is not None:
+                lines.append(f"  its launch {h['Function']} (thread {h['Thread_Id']}) at {(int(h['Start_Timestamp']) - end) / 1e3:+.1f} us "
+                             f"from the gap start, returned {(int(h['End_Timestamp']) - end) / 1e3:+.1f} us")
+            for q in hs:
+                qs, qe = int(q["Start_Timestamp"]), int(q["End_Timestamp"])
+                if qe >= end - 100000 and qs <= st and qe - qs >= 20000:
+                    lines.append(f"    host {q['Function'][:40]:40s} thread {q['Thread_Id']} {(qs - end) / 1e3:+9.1f} .. {(qe - end) / 1e3:+9.1f} us")
+        end = en if end is None else max(end, en)
+    open(a.out, "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines[:80]))
+
+
+if __name__ == "__main__":
+    main()

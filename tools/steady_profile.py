@@ -84,6 +84,16 @@ def main():
                              f" {('s' + str(q[sid])) if sid else ''} {q['Kernel_Name'][:70]}")
             lines.append(f"  ^ idle {(st - end) / 1e3:.1f} us")
         end = en if end is None else max(end, en)
+    big, end = 0, None  # the long stalls (>= 200 us) anywhere in the steady steps, in context
+    for j, r in enumerate(steady):
+        st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if end is not None and st - end >= 200000 and big < 4:
+            big += 1
+            lines.append(f"stall {(st - end) / 1e3:.1f} us:")
+            for q in steady[max(0, j - 6):j + 3]:
+                lines.append(f"    t={(int(q['Start_Timestamp']) - t0) / 1e3:10.1f} us dur={(int(q['End_Timestamp']) - int(q['Start_Timestamp'])) / 1e3:7.1f}"
+                             f" {('s' + str(q[sid])) if sid else ''} {q['Kernel_Name'][:70]}")
+        end = en if end is None else max(end, en)
     lines.append("")
     for k, (d, c) in sorted(agg.items(), key=lambda x: -x[1][0])[:60]:
         lines.append(f"{d / n / 1e3:9.1f} us/step calls/step={c / n:6.1f}  {k[:140]}")
