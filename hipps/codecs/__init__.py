@@ -89,7 +89,10 @@ class Codec:
         raise NotImplementedError
 
     def accumulate(self, msgs: Sequence[Dict[str, torch.Tensor]], acc: torch.Tensor, gscale: float = 1.0,
-                   accumulate: bool = False) -> None:
+                   accumulate: bool = False, acquire: bool = False) -> None:
+        """acc (+)= gscale * sum of the decoded messages, in order.  ``acquire``: some message was
+        written into this device's memory by another GPU (a remote worker's async-PS mailbox
+        slot), so the decode kernels acquire at system scope before reading it."""
         raise NotImplementedError
 
     def dense_source(self, views: Dict[str, torch.Tensor]) -> torch.Tensor:
@@ -157,8 +160,8 @@ class Identity(Codec):
     def encode_into(self, x, views, state):
         ops.convert(x, views["x"])
 
-    def accumulate(self, msgs, acc, gscale=1.0, accumulate=False):
-        ops.aggregate([m["x"] for m in msgs], acc, gscale, accumulate)
+    def accumulate(self, msgs, acc, gscale=1.0, accumulate=False, acquire=False):
+        ops.aggregate([m["x"] for m in msgs], acc, gscale, accumulate, acquire)
 
     def dense_source(self, views):
         return views["x"]
@@ -183,8 +186,8 @@ class Int8(Codec):
     def encode_into(self, x, views, state):
         ops.q8_encode(x, state.get("resid"), views["q"], views["scales"], self.stochastic, self.next_seed())
 
-    def accumulate(self, msgs, acc, gscale=1.0, accumulate=False):
-        ops.q8_aggregate([m["q"] for m in msgs], [m["scales"] for m in msgs], acc, gscale, accumulate)
+    def accumulate(self, msgs, acc, gscale=1.0, accumulate=False, acquire=False):
+        ops.q8_aggregate([m["q"] for m in msgs], [m["scales"] for m in msgs], acc, gscale, accumulate, acquire)
 
 
 class TopK(Codec):
@@ -217,11 +220,11 @@ class TopK(Codec):
     def encode_into(self, x, views, state):
         ops.topk_encode(x, state.get("resid"), views["idx"].numel(), views["idx"], views["val"], state.get("ws"))
 
-    def accumulate(self, msgs, acc, gscale=1.0, accumulate=False):
+    def accumulate(self, msgs, acc, gscale=1.0, accumulate=False, acquire=False):
         if not accumulate:
             acc.zero_()
         for m in msgs:  # rank order; one message has unique indices
-            ops.topk_accumulate(m["idx"], m["val"], acc, gscale)
+            ops.topk_accumulate(m["idx"], m["val"], acc, gscale, acquire)
 
 
 class TopKInt8(TopK):
@@ -246,11 +249,11 @@ class TopKInt8(TopK):
         if resid is not None:
             ops.topk_q8_residual(views["idx"], state["vals"], views["q"], views["scales"], resid)
 
-    def accumulate(self, msgs, acc, gscale=1.0, accumulate=False):
+    def accumulate(self, msgs, acc, gscale=1.0, accumulate=False, acquire=False):
         if not accumulate:
             acc.zero_()
         for m in msgs:
-            ops.topk_q8_accumulate(m["idx"], m["q"], m["scales"], acc, gscale)
+            ops.topk_q8_accumulate(m["idx"], m["q"], m["scales"], acc, gscale, acquire)
 
 
 class Threshold(Codec):
@@ -287,11 +290,11 @@ class Threshold(Codec):
     def encode_into(self, x, views, state):
         ops.thresh_encode(x, state.get("resid"), self.tau, views["count"], views["idx"], views["val"], state.get("ws"))
 
-    def accumulate(self, msgs, acc, gscale=1.0, accumulate=False):
+    def accumulate(self, msgs, acc, gscale=1.0, accumulate=False, acquire=False):
         if not accumulate:
             acc.zero_()
         for m in msgs:
-            ops.thresh_accumulate(m["count"], m["idx"], m["val"], acc, gscale)
+            ops.thresh_accumulate(m["count"], m["idx"], m["val"], acc, gscale, acquire)
 
     @staticmethod
     def count(views) -> int:
@@ -435,13 +438,22 @@ class ObjectCodec(Codec):
             acc[s.offset:s.offset + s.numel] += d
         return present
 
-    def read_message(self, views) -> bytes:
-        n = int(views["hdr"][0].item())
-        return views["blob"][:n].cpu().numpy().tobytes()
+    def read_message(self, views, acquire: bool = False) -> bytes:
+        hdr, blob = views["hdr"], views["blob"]
+        if acquire and hdr.is_cuda:  # written by a peer GPU: stage through a system-scope acquire
+            h = torch.empty(16, dtype=torch.uint8, device=hdr.device)
+            ops.copy_acquire(hdr.view(torch.uint8), h)
+            n = int(h.view(torch.int64)[0].item())
+            m = min((n + 15) // 16 * 16, blob.numel())
+            b = torch.empty(m, dtype=torch.uint8, device=blob.device)
+            ops.copy_acquire(blob[:m], b)
+            return b[:n].cpu().numpy().tobytes()
+        n = int(hdr[0].item())
+        return blob[:n].cpu().numpy().tobytes()
 
-    def accumulate(self, msgs, acc, gscale=1.0, accumulate=False):
-        self.last_present = self.accumulate_codes(self.decode_messages([self.read_message(v) for v in msgs]), acc,
-                                                  gscale, accumulate)
+    def accumulate(self, msgs, acc, gscale=1.0, accumulate=False, acquire=False):
+        self.last_present = self.accumulate_codes(
+            self.decode_messages([self.read_message(v, acquire) for v in msgs]), acc, gscale, accumulate)
 
 
 def get_codec(spec) -> Codec:

@@ -3,7 +3,8 @@
 
 namespace hipps {
 // flat.hip
-void aggregate(const std::vector<at::Tensor>& slots, at::Tensor acc, double gscale, bool accumulate);
+void aggregate(const std::vector<at::Tensor>& slots, at::Tensor acc, double gscale, bool accumulate, bool acquire);
+void copy_acquire(at::Tensor src, at::Tensor dst);
 void convert(at::Tensor src, at::Tensor dst, double scale);
 void gather_flat(const std::vector<at::Tensor>& srcs, at::Tensor table, at::Tensor dst, double scale);
 void transpose_cast(at::Tensor src, at::Tensor dst, at::Tensor tiles);
@@ -19,17 +20,19 @@ void adam_step(const std::vector<at::Tensor>& grads, double gscale, at::Tensor p
 void q8_encode(at::Tensor x, c10::optional<at::Tensor> resid, at::Tensor q, at::Tensor scales, bool stochastic,
                int64_t seed);
 void q8_aggregate(const std::vector<at::Tensor>& qs, const std::vector<at::Tensor>& ss, at::Tensor acc, double gscale,
-                  bool accumulate);
+                  bool accumulate, bool acquire);
 // topk.hip
 void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::Tensor idx, at::Tensor val,
                  at::Tensor workspace);
 int64_t topk_workspace_bytes(int64_t n, int64_t k);
-void topk_accumulate(at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale);
-void topk_q8_accumulate(at::Tensor idx, at::Tensor q, at::Tensor scales, at::Tensor acc, double gscale);
+void topk_accumulate(at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale, bool acquire);
+void topk_q8_accumulate(at::Tensor idx, at::Tensor q, at::Tensor scales, at::Tensor acc, double gscale,
+                        bool acquire);
 void topk_q8_residual(at::Tensor idx, at::Tensor v, at::Tensor q, at::Tensor scales, at::Tensor resid);
 void thresh_encode(at::Tensor g, c10::optional<at::Tensor> resid, double tau, at::Tensor count, at::Tensor idx,
                    at::Tensor val, at::Tensor workspace);
-void thresh_accumulate(at::Tensor count, at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale);
+void thresh_accumulate(at::Tensor count, at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale,
+                       bool acquire);
 void copy_counted(at::Tensor src, at::Tensor dst, int64_t idx_off, int64_t val_off, int64_t val_esz, int64_t cap);
 // norm.hip
 void bn_forward_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, at::Tensor weight, at::Tensor bias,
@@ -132,7 +135,9 @@ void bind_trace(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hipps native kernels (gfx950) and parameter-server runtime";
-  m.def("aggregate", &hipps::aggregate, "acc (+)= gscale * sum_w slots[w] (rank order)");
+  m.def("aggregate", &hipps::aggregate, "acc (+)= gscale * sum_w slots[w] (rank order)", py::arg("slots"),
+        py::arg("acc"), py::arg("gscale"), py::arg("accumulate"), py::arg("acquire") = false);
+  m.def("copy_acquire", &hipps::copy_acquire, "dst = src after a system-scope acquire (bytes written by a peer GPU)");
   m.def("convert", &hipps::convert, "dst = scale * src with f32/bf16 conversion");
   m.def("gather_flat", &hipps::gather_flat, "multi-tensor gather (+cast) of grads into a flat buffer");
   m.def("transpose_cast", &hipps::transpose_cast, "multi-matrix dst[c,r] = bf16(src[r,c]) (1x1 dgrad weights)");
@@ -149,14 +154,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("step"), pybind11::arg("amsgrad"), pybind11::arg("torch_mode"),
         pybind11::arg("mask") = pybind11::none(), pybind11::arg("csteps") = pybind11::none());
   m.def("q8_encode", &hipps::q8_encode, "per-256-block absmax int8 quantization (+EF, +stochastic)");
-  m.def("q8_aggregate", &hipps::q8_aggregate, "acc (+)= gscale * sum_w dequant(q_w, s_w)");
+  m.def("q8_aggregate", &hipps::q8_aggregate, "acc (+)= gscale * sum_w dequant(q_w, s_w)", py::arg("qs"), py::arg("ss"),
+        py::arg("acc"), py::arg("gscale"), py::arg("accumulate"), py::arg("acquire") = false);
   m.def("topk_encode", &hipps::topk_encode, "exact top-k |g| (radix select) -> idx asc, val");
   m.def("topk_workspace_bytes", &hipps::topk_workspace_bytes, py::arg("n"), py::arg("k") = 0);
-  m.def("topk_accumulate", &hipps::topk_accumulate, "acc[idx] += gscale * val");
-  m.def("topk_q8_accumulate", &hipps::topk_q8_accumulate, "acc[idx] += gscale * deq(q)");
+  m.def("topk_accumulate", &hipps::topk_accumulate, "acc[idx] += gscale * val", py::arg("idx"), py::arg("val"),
+        py::arg("acc"), py::arg("gscale"), py::arg("acquire") = false);
+  m.def("topk_q8_accumulate", &hipps::topk_q8_accumulate, "acc[idx] += gscale * deq(q)", py::arg("idx"), py::arg("q"),
+        py::arg("scales"), py::arg("acc"), py::arg("gscale"), py::arg("acquire") = false);
   m.def("topk_q8_residual", &hipps::topk_q8_residual, "EF: r[idx] += v - deq(q)");
   m.def("thresh_encode", &hipps::thresh_encode, "variable-size |x|>tau sparsification, device count header");
-  m.def("thresh_accumulate", &hipps::thresh_accumulate, "acc[idx[:count]] += gscale * val[:count]");
+  m.def("thresh_accumulate", &hipps::thresh_accumulate, "acc[idx[:count]] += gscale * val[:count]", py::arg("count"),
+        py::arg("idx"), py::arg("val"), py::arg("acc"), py::arg("gscale"), py::arg("acquire") = false);
   m.def("copy_counted", &hipps::copy_counted, "copy a [count | idx | val] message moving only count entries");
   m.def("bn_forward_train", &hipps::bn_forward_train, "fused channels-last BN train fwd (+res) (+relu)");
   m.def("bn_apply", &hipps::bn_apply, "y = act(x*scale + shift (+res))");

@@ -59,6 +59,24 @@ struct SlotPtrs {
   const void* p[kMaxSlots];
 };
 
+// ---- reading bytes another GPU wrote into this GPU's memory ---------------------------------
+// The async PS's mailbox slots are plain (coarse-grained) hipMalloc memory that remote workers
+// fill over xGMI; the PS learns of a message from a host-polled doorbell, so no HIP-level
+// synchronisation tells this device's caches that the bytes changed.  A slot is rewritten every
+// SLOTS messages, so this XCD's L2 (and the CU's L1) may still hold the previous message's lines.
+// The consumer therefore acquires at SYSTEM scope before its first load of the slot
+// (MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility"; cdna_hip_programming.md
+// Guideline 16 consumer recipe): one wave issues the invalidate (buffer_inv sc0 sc1), waits for it
+// to complete with an explicit vmcnt(0) (the fence's own wait sits BEFORE the invalidate), and the
+// barrier holds the other waves until then.  Call it uniformly from every thread of the block.
+__device__ __forceinline__ void acquire_remote_block() {
+  if (threadIdx.x < 64) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
 // ---- launch geometry ----------------------------------------------------------------------
 inline int grid_for(int64_t work_items, int block = kBlock) {
   int64_t g = (work_items + block - 1) / block;

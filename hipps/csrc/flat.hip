@@ -104,7 +104,8 @@ __device__ __forceinline__ void pub_store1(void* pub, int pub_mode, int64_t i, f
 // ------------------------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_aggregate(SlotPtrs g, int W, float gscale, float* __restrict__ acc,
-                                                      int64_t n, int accumulate) {
+                                                      int64_t n, int accumulate, int acquire) {
+  if (acquire) acquire_remote_block();  // a source slot was written by another GPU (common.h)
   const int64_t nv = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
     const int64_t i = v << 2;
@@ -121,6 +122,21 @@ __global__ __launch_bounds__(kBlock) void k_aggregate(SlotPtrs g, int W, float g
       acc[i] = accumulate ? acc[i] + d : d;
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_copy_acquire: dst = src (bytes), after a system-scope acquire -- stages bytes another GPU
+// wrote into this device's memory (presence bytes, canaries, object-codec blobs of a remote
+// worker's mailbox slot) into a private buffer that ordinary torch kernels may then read.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_copy_acquire(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                         int64_t n) {
+  acquire_remote_block();
+  const int64_t nv = n >> 4, stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t v = t0; v < nv; v += stride)
+    reinterpret_cast<uint4*>(dst)[v] = reinterpret_cast<const uint4*>(src)[v];
+  for (int64_t i = (nv << 4) + t0; i < n; i += stride) dst[i] = src[i];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -384,7 +400,7 @@ int pub_mode_of(const c10::optional<at::Tensor>& pub, int64_t n) {
 
 }  // namespace
 
-void aggregate(const std::vector<at::Tensor>& slots, at::Tensor acc, double gscale, bool accumulate) {
+void aggregate(const std::vector<at::Tensor>& slots, at::Tensor acc, double gscale, bool accumulate, bool acquire) {
   check_dev(acc, "acc");
   TORCH_CHECK(acc.scalar_type() == at::kFloat, "acc must be float32");
   const int64_t n = acc.numel();
@@ -394,10 +410,22 @@ void aggregate(const std::vector<at::Tensor>& slots, at::Tensor acc, double gsca
   const int grid = grid_for(n >> 2);
   if (wt == WireT::F32)
     hipLaunchKernelGGL(k_aggregate<float>, grid, kBlock, 0, stream, s, (int)slots.size(), (float)gscale,
-                       acc.data_ptr<float>(), n, (int)accumulate);
+                       acc.data_ptr<float>(), n, (int)accumulate, (int)acquire);
   else
     hipLaunchKernelGGL(k_aggregate<uint16_t>, grid, kBlock, 0, stream, s, (int)slots.size(), (float)gscale,
-                       acc.data_ptr<float>(), n, (int)accumulate);
+                       acc.data_ptr<float>(), n, (int)accumulate, (int)acquire);
+}
+
+void copy_acquire(at::Tensor src, at::Tensor dst) {
+  TORCH_CHECK(src.is_cuda() && dst.is_cuda() && src.scalar_type() == at::kByte && dst.scalar_type() == at::kByte,
+              "copy_acquire: uint8 device tensors");
+  TORCH_CHECK(src.is_contiguous() && dst.is_contiguous() && src.numel() == dst.numel(), "copy_acquire: sizes");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16 == 0,
+              "copy_acquire: 16-byte aligned buffers");
+  const int64_t n = src.numel();
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_copy_acquire, grid_for((n + 15) >> 4), kBlock, 0, c10::hip::getCurrentHIPStream(),
+                     src.data_ptr<uint8_t>(), dst.data_ptr<uint8_t>(), n);
 }
 
 void convert(at::Tensor src, at::Tensor dst, double scale) {

@@ -95,7 +95,9 @@ __global__ __launch_bounds__(kBlock) void k_q8_encode(const float* __restrict__ 
 
 // acc (+)= gscale * sum_w deq(q_w, s_w)   — rank-ordered, 4 elements per lane
 __global__ __launch_bounds__(kBlock) void k_q8_aggregate(SlotPtrs qs, SlotPtrs ss, int W, float gscale,
-                                                         float* __restrict__ acc, int64_t n, int accumulate) {
+                                                         float* __restrict__ acc, int64_t n, int accumulate,
+                                                         int acquire) {
+  if (acquire) acquire_remote_block();  // a source slot was written by another GPU (common.h)
   const int64_t nv = (n + 3) >> 2, stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
     const int64_t i = v << 2;
@@ -150,7 +152,7 @@ void q8_encode(at::Tensor x, c10::optional<at::Tensor> resid, at::Tensor q, at::
 }
 
 void q8_aggregate(const std::vector<at::Tensor>& qs, const std::vector<at::Tensor>& ss, at::Tensor acc, double gscale,
-                  bool accumulate) {
+                  bool accumulate, bool acquire) {
   TORCH_CHECK(acc.is_cuda() && acc.scalar_type() == at::kFloat && acc.is_contiguous(), "acc: f32 device tensor");
   TORCH_CHECK(!qs.empty() && qs.size() == ss.size() && (int)qs.size() <= kMaxSlots, "1..16 (q, scale) pairs");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(acc.data_ptr()) % 16 == 0, "acc must be 16-byte aligned");
@@ -165,7 +167,7 @@ void q8_aggregate(const std::vector<at::Tensor>& qs, const std::vector<at::Tenso
   }
   const int grid = grid_for((n + 3) >> 2);
   hipLaunchKernelGGL(k_q8_aggregate, grid, kBlock, 0, c10::hip::getCurrentHIPStream(), qp, sp, (int)qs.size(),
-                     (float)gscale, acc.data_ptr<float>(), n, (int)accumulate);
+                     (float)gscale, acc.data_ptr<float>(), n, (int)accumulate, (int)acquire);
 }
 
 }  // namespace hipps

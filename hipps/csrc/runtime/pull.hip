@@ -70,9 +70,13 @@ __global__ __launch_bounds__(kBlock) void k_pull_copy(const int64_t* __restrict_
   const int64_t v = sel[0];
   if (v < 0) return;
   // system-scope acquire: drop any stale copy of the (remote) publish buffer before reading it.
-  // The invalidation acts on the CU's L1 and its XCD's L2, so one wave per workgroup issues it
-  // and the others wait at the barrier (every wave fencing cost 4x the invalidations)
-  if (fence_mode == 0 || threadIdx.x < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  // The invalidation acts on the CU's L1 and its XCD's L2, so one wave per workgroup issues it,
+  // waits for it (vmcnt(0) AFTER the buffer_inv: the fence's own wait precedes it), and the
+  // others wait at the barrier (every wave fencing cost 4x the invalidations)
+  if (fence_mode == 0 || threadIdx.x < 64) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before any load
+  }
   if (fence_mode == 1) __syncthreads();
   const Tin* src = reinterpret_cast<const Tin*>(pub + (v % npub) * stride);
   const int64_t nv = n >> 2, step = (int64_t)gridDim.x * blockDim.x;
@@ -142,7 +146,10 @@ __global__ __launch_bounds__(kBlock) void k_pull_copy_b(const int64_t* __restric
   if (v < 0) return;
   const int64_t a = max(boff[b], lo), e = min(boff[b + 1], hi);
   if (a >= e) return;
-  if (fence_mode == 0 || threadIdx.x < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  if (fence_mode == 0 || threadIdx.x < 64) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before any load
+  }
   if (fence_mode == 1) __syncthreads();
   const Tin* src = reinterpret_cast<const Tin*>(pub + (v % npub) * stride);
   const int64_t a4 = (a + 3) >> 2, e4 = e >> 2, step = (int64_t)gridDim.x * blockDim.x;

@@ -695,7 +695,8 @@ __global__ __launch_bounds__(kBlock) void k_write_regions(const float* __restric
 // acc[idx[j]] (+)= gscale * val[j]; one message has unique indices, so no atomics are needed.
 template <typename VT>
 __global__ __launch_bounds__(kBlock) void k_scatter_acc(const int32_t* __restrict__ idx, const VT* __restrict__ val,
-                                                        int64_t k, float* __restrict__ acc, float gscale) {
+                                                        int64_t k, float* __restrict__ acc, float gscale, int acquire) {
+  if (acquire) acquire_remote_block();  // the message was written by another GPU (common.h)
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < k; j += stride)
     acc[idx[j]] += gscale * Vec4<VT>::load1(val, j);
@@ -705,7 +706,8 @@ __global__ __launch_bounds__(kBlock) void k_scatter_acc(const int32_t* __restric
 __global__ __launch_bounds__(kBlock) void k_scatter_acc_q8(const int32_t* __restrict__ idx,
                                                            const int8_t* __restrict__ q,
                                                            const float* __restrict__ scales, int64_t k,
-                                                           float* __restrict__ acc, float gscale) {
+                                                           float* __restrict__ acc, float gscale, int acquire) {
+  if (acquire) acquire_remote_block();
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < k; j += stride)
     acc[idx[j]] += gscale * (float)q[j] * scales[j >> 8];
@@ -971,9 +973,12 @@ void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::T
 template <typename VT>
 __global__ __launch_bounds__(kBlock) void k_scatter_acc_count(const int32_t* __restrict__ idx,
                                                               const VT* __restrict__ val,
-                                                              const int32_t* __restrict__ count, int64_t cap,
-                                                              float* __restrict__ acc, float gscale) {
-  const int64_t k = min((int64_t)count[0], cap);
+                                                              const int32_t* count, int64_t cap,
+                                                              float* __restrict__ acc, float gscale, int acquire) {
+  if (acquire) acquire_remote_block();
+  // the count header through the VECTOR path (a uniform `const __restrict__` load may go through
+  // the scalar cache, which the acquire does not refresh)
+  const int64_t k = min((int64_t)__hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), cap);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < k; j += stride)
     acc[idx[j]] += gscale * Vec4<VT>::load1(val, j);
@@ -1049,23 +1054,25 @@ void copy_counted(at::Tensor src, at::Tensor dst, int64_t idx_off, int64_t val_o
                      src.data_ptr<uint8_t>(), dst.data_ptr<uint8_t>(), idx_off, val_off, (int)val_esz, cap);
 }
 
-void thresh_accumulate(at::Tensor count, at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale) {
+void thresh_accumulate(at::Tensor count, at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale,
+                       bool acquire) {
   TORCH_CHECK(acc.is_cuda() && acc.scalar_type() == at::kFloat, "acc: f32 device tensor");
   const int64_t cap = idx.numel();
   if (cap == 0) return;
   auto stream = c10::hip::getCurrentHIPStream();
   if (val.scalar_type() == at::kFloat)
     hipLaunchKernelGGL(k_scatter_acc_count<float>, grid_for(cap), kBlock, 0, stream, idx.data_ptr<int32_t>(),
-                       val.data_ptr<float>(), count.data_ptr<int32_t>(), cap, acc.data_ptr<float>(), (float)gscale);
+                       val.data_ptr<float>(), count.data_ptr<int32_t>(), cap, acc.data_ptr<float>(), (float)gscale,
+                       (int)acquire);
   else
     hipLaunchKernelGGL(k_scatter_acc_count<uint16_t>, grid_for(cap), kBlock, 0, stream, idx.data_ptr<int32_t>(),
                        (const uint16_t*)val.data_ptr(), count.data_ptr<int32_t>(), cap, acc.data_ptr<float>(),
-                       (float)gscale);
+                       (float)gscale, (int)acquire);
 }
 
 int64_t topk_workspace_bytes(int64_t n, int64_t k) { return ws_bytes_for(n, k); }
 
-void topk_accumulate(at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale) {
+void topk_accumulate(at::Tensor idx, at::Tensor val, at::Tensor acc, double gscale, bool acquire) {
   TORCH_CHECK(acc.is_cuda() && acc.scalar_type() == at::kFloat, "acc: f32 device tensor");
   TORCH_CHECK(idx.scalar_type() == at::kInt && idx.numel() == val.numel(), "idx/val mismatch");
   const int64_t k = idx.numel();
@@ -1074,15 +1081,16 @@ void topk_accumulate(at::Tensor idx, at::Tensor val, at::Tensor acc, double gsca
   const int grid = grid_for(k);
   if (val.scalar_type() == at::kFloat)
     hipLaunchKernelGGL(k_scatter_acc<float>, grid, kBlock, 0, stream, idx.data_ptr<int32_t>(), val.data_ptr<float>(),
-                       k, acc.data_ptr<float>(), (float)gscale);
+                       k, acc.data_ptr<float>(), (float)gscale, (int)acquire);
   else if (val.scalar_type() == at::kBFloat16)
     hipLaunchKernelGGL(k_scatter_acc<uint16_t>, grid, kBlock, 0, stream, idx.data_ptr<int32_t>(),
-                       (const uint16_t*)val.data_ptr(), k, acc.data_ptr<float>(), (float)gscale);
+                       (const uint16_t*)val.data_ptr(), k, acc.data_ptr<float>(), (float)gscale, (int)acquire);
   else
     TORCH_CHECK(false, "val must be f32 or bf16");
 }
 
-void topk_q8_accumulate(at::Tensor idx, at::Tensor q, at::Tensor scales, at::Tensor acc, double gscale) {
+void topk_q8_accumulate(at::Tensor idx, at::Tensor q, at::Tensor scales, at::Tensor acc, double gscale,
+                        bool acquire) {
   TORCH_CHECK(acc.is_cuda() && acc.scalar_type() == at::kFloat, "acc: f32 device tensor");
   TORCH_CHECK(idx.scalar_type() == at::kInt && q.scalar_type() == at::kChar && idx.numel() == q.numel(), "idx/q");
   const int64_t k = idx.numel();
@@ -1090,7 +1098,7 @@ void topk_q8_accumulate(at::Tensor idx, at::Tensor q, at::Tensor scales, at::Ten
   if (k == 0) return;
   hipLaunchKernelGGL(k_scatter_acc_q8, grid_for(k), kBlock, 0, c10::hip::getCurrentHIPStream(),
                      idx.data_ptr<int32_t>(), (const int8_t*)q.data_ptr(), scales.data_ptr<float>(), k,
-                     acc.data_ptr<float>(), (float)gscale);
+                     acc.data_ptr<float>(), (float)gscale, (int)acquire);
 }
 
 void topk_q8_residual(at::Tensor idx, at::Tensor v, at::Tensor q, at::Tensor scales, at::Tensor resid) {

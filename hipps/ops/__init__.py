@@ -22,11 +22,22 @@ def _dev(t: torch.Tensor) -> bool:
     return t.is_cuda
 
 
-def aggregate(slots: Sequence[torch.Tensor], acc: torch.Tensor, gscale: float = 1.0, accumulate: bool = False):
-    """acc (+)= gscale * sum_w slots[w], summed in rank order (reference ps.py:176)."""
+def aggregate(slots: Sequence[torch.Tensor], acc: torch.Tensor, gscale: float = 1.0, accumulate: bool = False,
+              acquire: bool = False):
+    """acc (+)= gscale * sum_w slots[w], summed in rank order (reference ps.py:176).
+    ``acquire``: a source was written by another GPU (async PS mailbox slot of a remote worker):
+    every workgroup does a system-scope acquire before its first load (csrc/common.h)."""
     if _dev(acc):
-        return native().aggregate(list(slots), acc, float(gscale), bool(accumulate))
+        return native().aggregate(list(slots), acc, float(gscale), bool(accumulate), bool(acquire))
     return ref.aggregate(slots, acc, gscale, accumulate)
+
+
+def copy_acquire(src: torch.Tensor, dst: torch.Tensor):
+    """dst = src (uint8) after a system-scope acquire: stages bytes a peer GPU wrote into this
+    device's memory before ordinary kernels read them."""
+    if _dev(src):
+        return native().copy_acquire(src, dst)
+    dst.copy_(src)
 
 
 def convert(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0):
@@ -77,9 +88,9 @@ def q8_encode(x, resid, q, scales, stochastic: bool = False, seed: int = 0):
     return ref.q8_encode(x, resid, q, scales, stochastic, int(seed) & ((1 << 63) - 1))
 
 
-def q8_aggregate(qs, ss, acc, gscale: float = 1.0, accumulate: bool = False):
+def q8_aggregate(qs, ss, acc, gscale: float = 1.0, accumulate: bool = False, acquire: bool = False):
     if _dev(acc):
-        return native().q8_aggregate(list(qs), list(ss), acc, float(gscale), bool(accumulate))
+        return native().q8_aggregate(list(qs), list(ss), acc, float(gscale), bool(accumulate), bool(acquire))
     return ref.q8_aggregate(qs, ss, acc, gscale, accumulate)
 
 
@@ -98,15 +109,15 @@ def topk_encode(g, resid, k: int, idx, val, workspace=None):
     return ref.topk_encode(g, resid, k, idx, val)
 
 
-def topk_accumulate(idx, val, acc, gscale: float = 1.0):
+def topk_accumulate(idx, val, acc, gscale: float = 1.0, acquire: bool = False):
     if _dev(acc):
-        return native().topk_accumulate(idx, val, acc, float(gscale))
+        return native().topk_accumulate(idx, val, acc, float(gscale), bool(acquire))
     return ref.topk_accumulate(idx, val, acc, gscale)
 
 
-def topk_q8_accumulate(idx, q, scales, acc, gscale: float = 1.0):
+def topk_q8_accumulate(idx, q, scales, acc, gscale: float = 1.0, acquire: bool = False):
     if _dev(acc):
-        return native().topk_q8_accumulate(idx, q, scales, acc, float(gscale))
+        return native().topk_q8_accumulate(idx, q, scales, acc, float(gscale), bool(acquire))
     return ref.topk_q8_accumulate(idx, q, scales, acc, gscale)
 
 
@@ -126,7 +137,7 @@ def thresh_encode(g, resid, tau: float, count, idx, val, workspace=None):
     return ref.thresh_encode(g, resid, tau, count, idx, val)
 
 
-def thresh_accumulate(count, idx, val, acc, gscale: float = 1.0):
+def thresh_accumulate(count, idx, val, acc, gscale: float = 1.0, acquire: bool = False):
     if _dev(acc):
-        return native().thresh_accumulate(count, idx, val, acc, float(gscale))
+        return native().thresh_accumulate(count, idx, val, acc, float(gscale), bool(acquire))
     return ref.thresh_accumulate(count, idx, val, acc, gscale)

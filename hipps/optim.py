@@ -163,6 +163,10 @@ class MPI_PS(torch.optim.Optimizer):
     def _needs_csteps(self) -> bool:
         return True
 
+    def state_floats(self) -> int:
+        """fp32 optimizer-state words per parameter (PS memory budget)."""
+        return 0
+
     def _ensure_state(self, key: str) -> torch.Tensor:
         if key not in self.flat_state:
             buf = self.store.new_buffer()
@@ -345,12 +349,24 @@ class MPI_PS(torch.optim.Optimizer):
             pass
 
     def state_dict(self):
-        self._sync_param_state()
-        sd = super().state_dict()
-        sd["hipps"] = {"steps": self.steps, "group_steps": list(self._group_steps), "mode": self.mode,
-                       "codec": self.codec.name}
-        if self.chunk_steps is not None:
-            sd["hipps"]["chunk_steps"] = self.chunk_steps.detach().cpu()
+        """torch-compatible state dict.  In ps_async mode the PS thread advances the optimizer
+        state on its own stream, so the snapshot is taken with that thread held between messages
+        (engine.quiesced(), as checkpoint.save does) and the tensors are copied out before it
+        resumes: per-parameter 'step' counts, moments and chunk counts belong to one PS state."""
+        import contextlib
+
+        eng = getattr(self, "engine", None)
+        q = getattr(eng, "quiesced", None) if eng is not None else None
+        with (q() if q is not None else contextlib.nullcontext()):
+            self._sync_param_state()
+            sd = super().state_dict()
+            if q is not None:  # detach from the live flat buffers the PS keeps updating
+                sd["state"] = {k: {n: (v.detach().clone() if torch.is_tensor(v) else v) for n, v in st.items()}
+                               for k, st in sd["state"].items()}
+            sd["hipps"] = {"steps": self.steps, "group_steps": list(self._group_steps), "mode": self.mode,
+                           "codec": self.codec.name}
+            if self.chunk_steps is not None:
+                sd["hipps"]["chunk_steps"] = self.chunk_steps.detach().cpu()
         return sd
 
     def _sync_param_state(self):
@@ -390,6 +406,17 @@ class MPI_PS(torch.optim.Optimizer):
     def _state_count(self, st: dict, gi: int) -> int:
         return self._group_steps[gi]
 
+    def csteps_from_groups(self, cs: torch.Tensor, started=None):
+        """Per-chunk counts for a checkpoint written before chunk_steps existed (it stored only
+        per-group step counts, and for SGD the groups whose momentum had started,
+        ``mom_started``): every parameter of a group took that group's steps."""
+        for s in self.store.slots:
+            a = s.offset // 16
+            cs[a:a + (s.numel + 15) // 16].fill_(self._group_count(s.group, started))
+
+    def _group_count(self, gi: int, started=None) -> int:
+        return self._group_steps[gi]
+
     def _ensure_state_nocopy(self, key):
         if key not in self.flat_state:
             self.flat_state[key] = self.store.new_buffer()
@@ -404,6 +431,9 @@ class SGD(MPI_PS, torch.optim.SGD):
 
     def _needs_csteps(self) -> bool:
         return any(g.get("momentum", 0) for g in self.param_groups)
+
+    def state_floats(self) -> int:
+        return 1 if any(g.get("momentum", 0) for g in self.param_groups) else 0
 
     def _update_group(self, gi, group, srcs, target, gscale, zero_src, pub, mask=None, lo=None, hi=None,
                       csteps=None, lookahead=0.0):
@@ -431,12 +461,22 @@ class SGD(MPI_PS, torch.optim.SGD):
     def _state_count(self, st: dict, gi: int) -> int:
         return max(1, self._group_steps[gi]) if "momentum_buffer" in st else 0
 
+    def _group_count(self, gi: int, started=None) -> int:
+        if started is not None:
+            has = gi in set(started)
+        else:
+            has = "momentum_buffer" in self.flat_state and self._group_steps[gi] > 0
+        return max(1, self._group_steps[gi]) if has else 0
+
 
 class Adam(MPI_PS, torch.optim.Adam):
     """Reference Adam (ps.py:217-261): eps added to the un-corrected sqrt(v) unless
     ``adam_variant='torch'``; amsgrad honoured (the reference never passes it, ps.py:185-186)."""
 
     optim = "adam"
+
+    def state_floats(self) -> int:
+        return 3 if any(g.get("amsgrad", False) for g in self.param_groups) else 2
 
     def _sync_param_state(self):
         for i, n in self.param_steps().items():  # torch-compatible per-parameter step (ps.py:241)

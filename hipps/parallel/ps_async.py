@@ -72,6 +72,86 @@ def _align(x: int, a: int = 256) -> int:
     return (x + a - 1) // a * a
 
 
+def ps_memory_budget(numel: int, W: int, slots: int, slot_bytes: int, npub: int, pub_esz: int, opt_floats: int,
+                     colocated: bool = True, worker_wire_bytes: int = 0, shadow: bool = False,
+                     codec_state_floats: int = 0) -> Dict[str, int]:
+    """Bytes the async PS adds on rank 0's GPU, term by term.
+
+    PS terms (allocated by the engine):
+      mailbox      W * slots * slot_bytes        every worker's in-flight bucket messages
+      publish      npub * numel * pub_esz        rotating published versions (readers never torn)
+      master       numel * 4                     the fp32 master parameters
+      accumulator  numel * 4                     the fp32 gradient accumulator
+      optimizer    opt_floats * numel * 4        momentum (SGD) / moments (Adam) on the master
+      chunk_steps  numel / 16 * 4                per-parameter step counters
+    Co-located worker 0 (rank 0 also trains, ``colocated``): its fp32 parameters and gradients,
+    the bf16 weight shadow, its wire image and codec state (error-feedback residuals).  Its
+    activations are the model's own and are not counted."""
+    b = {
+        "mailbox": W * slots * slot_bytes,
+        "publish": npub * numel * pub_esz,
+        "master": numel * 4,
+        "accumulator": numel * 4,
+        "optimizer": opt_floats * numel * 4,
+        "chunk_steps": (numel + 15) // 16 * 4,
+    }
+    b["ps_total"] = sum(b.values())
+    if colocated:
+        w = {"worker_params": numel * 4, "worker_grads": numel * 4, "worker_shadow": numel * 2 if shadow else 0,
+             "worker_wire": worker_wire_bytes, "worker_codec_state": codec_state_floats * numel * 4}
+        b.update(w)
+        b["worker_total"] = sum(w.values())
+    else:
+        b["worker_total"] = 0
+    b["total"] = b["ps_total"] + b["worker_total"]
+    return b
+
+
+def budget_for_shapes(shapes, W: int, codec="bf16", bucket_mb: float = 64.0, mailbox_mb: float = 4096.0,
+                      mailbox_slots: int = 0, param_wire: str = "bf16", opt_floats: int = 1,
+                      dedicated: bool = False, shadow: bool = True, npub: Optional[int] = None,
+                      max_slots: int = 64) -> Dict[str, int]:
+    """:func:`ps_memory_budget` of a model given only its parameter shapes (no allocation: usable
+    for an 8B model on a laptop).  Reproduces the engine's bucketing (flat.BucketPlan over
+    16-aligned slots) and mailbox sizing (``mailbox_slots`` or min(2 * buckets, mailbox_mb))."""
+    import math
+    from types import SimpleNamespace
+
+    from hipps.codecs import get_codec
+
+    from .flat import BucketPlan
+
+    slots, off = [], 0
+    for shp in shapes:
+        n = int(math.prod(shp))
+        slots.append(SimpleNamespace(numel=n, offset=off))
+        off = _align(off + n, 16)
+    store = SimpleNamespace(slots=slots, numel=off, data=torch.empty(0, dtype=torch.float32))
+    c = get_codec(codec)
+    plan = BucketPlan(store, c, int(bucket_mb * (1 << 20)))
+    nb = len(plan.buckets)
+    pres = (len(slots) + 15) // 16 * 16
+    slot_bytes = _align(max(b.msg_nbytes for b in plan.buckets)) + _align(pres)
+    K = mailbox_slots if mailbox_slots > 0 else min(2 * nb, max(2, int(mailbox_mb * (1 << 20)) // slot_bytes))
+    K = max(1, min(K, max_slots))
+    if npub is None:
+        from hipps.ops._native import available, native
+
+        npub = native().ControlBlock.NPUB if available() else 4
+    esz = 2 if param_wire == "bf16" else 4
+    ef = 1 if getattr(c, "error_feedback", False) else 0
+    b = ps_memory_budget(off, W, K, slot_bytes, npub, esz, opt_floats, colocated=not dedicated,
+                         worker_wire_bytes=plan.wire_nbytes + pres, shadow=shadow, codec_state_floats=ef)
+    b["buckets"], b["mailbox_slots"], b["slot_bytes"] = nb, K, slot_bytes
+    return b
+
+
+def format_budget(b: Dict[str, int]) -> str:
+    gib = float(1 << 30)
+    skip = ("buckets", "mailbox_slots", "slot_bytes")
+    return ", ".join(f"{k} {v / gib:.2f} GiB" for k, v in b.items() if v and k not in skip)
+
+
 class _Pending:
     """Completion of posted torch.distributed p2p works.  RCCL works report completion by event
     query (``is_completed``); gloo's receive works only learn it inside ``wait()``, so on gloo a
@@ -202,6 +282,8 @@ class PSAsyncEngine(Engine):
         self.mail_off = 0
         self.pub_off = W * self.SLOTS * self.slot_bytes
         total = self.pub_off + self.NPUB * self.pub_bytes
+        if world.rank == 0:
+            self._check_budget(opt, store, esz)
 
         # ---- rendezvous: rank 0 creates control block + mailboxes, others map them ----------
         # transport 'ipc': workers map the PS's mailbox (HIP IPC / POSIX shm) and copy one-sidedly;
@@ -305,6 +387,7 @@ class PSAsyncEngine(Engine):
         self._lat = (_LatencyProbe() if self.cuda and self.rank == 0 and not self.dedicated
                      and os.environ.get("HIPPS_PS_LATENCY", "0") == "1" else None)
         self._err: Optional[str] = None
+        self._broken: Optional[str] = None  # set when this worker's message sequence is unusable
         self._thread = None
         self._pause_req = threading.Event()
         self._paused = threading.Event()
@@ -377,6 +460,38 @@ class PSAsyncEngine(Engine):
                     pass
                 raise
 
+    def memory_budget(self) -> Dict[str, int]:
+        """The rank-0 PS byte budget of this engine (see :func:`ps_memory_budget`)."""
+        opt, store = self.opt, self.store
+        esz = torch.empty((), dtype=self.pub_dtype).element_size()
+        cs = sum(1 for st in self.codec_state if "resid" in st)
+        return ps_memory_budget(store.numel, self.W, self.SLOTS, self.slot_bytes, self.NPUB, esz,
+                                opt.state_floats(), colocated=not self.dedicated, worker_wire_bytes=self.wire_total,
+                                shadow=getattr(store, "shadow", None) is not None,
+                                codec_state_floats=1 if cs else 0)
+
+    def _check_budget(self, opt, store, esz):
+        """Before the PS allocates anything: the PS's own bytes must fit in what is free on this
+        GPU now (worker 0's model, gradients and wire are already resident), with 5 % + 1 GiB left
+        for activations and the allocator.  A clear error naming every term beats an allocation
+        failure deep in the first update."""
+        self.budget = self.memory_budget()
+        if not self.cuda:
+            return
+        free, total_hbm = torch.cuda.mem_get_info(store.device)
+        need = self.budget["ps_total"]
+        reserve = int(0.05 * total_hbm) + (1 << 30)
+        if need + reserve > free and os.environ.get("HIPPS_SKIP_BUDGET", "0") != "1":
+            gib = float(1 << 30)
+            raise MemoryError(
+                f"ps_async: the parameter server needs {need / gib:.1f} GiB on rank 0's GPU "
+                f"({format_budget({k: v for k, v in self.budget.items() if not k.startswith('worker')})}) "
+                f"but only {free / gib:.1f} GiB of {total_hbm / gib:.1f} are free (keeping {reserve / gib:.1f} GiB "
+                "for activations); co-located worker 0 already holds "
+                f"{self.budget['worker_total'] / gib:.1f} GiB.  Options: ps_dedicated=True (rank 0 only serves), "
+                "a smaller mailbox (mailbox_mb / mailbox_slots / bucket_mb), param_wire='bf16', or fewer workers "
+                "per PS.  HIPPS_SKIP_BUDGET=1 skips this check.")
+
     def _self_test(self):
         """Prove both directions of the one-sided transport before training starts: every rank
         writes a tag into its mailbox slot through the same stream-ordered copy path, the PS checks
@@ -397,7 +512,7 @@ class PSAsyncEngine(Engine):
         ok = True
         if self.rank == 0:
             for r in range(W):
-                got = self.slot_buf(r, self.SLOTS - 1)[:16].cpu()
+                got = self._slot_read(r, self.SLOTS - 1, 0, 16).cpu()
                 ok &= bool((got == (r * 7 + 3) % 251).all())
             ck = float(self.pub_buf(0).double().sum())  # what workers actually receive
         else:
@@ -454,7 +569,8 @@ class PSAsyncEngine(Engine):
     def _verify_slot(self, rank: int, slot: int, bi: int, seq: int):
         """debug_canary on the PS: the pushed message must end in its intact 0x29 guard."""
         b = self.plan.buckets[bi]
-        if bool(self.plan.bad_guard(self.slot_buf(rank, slot), b.layout.nbytes)):
+        buf = self._slot_read(rank, slot, 0, self.slot_bytes) if self._remote(rank) else self.slot_buf(rank, slot)
+        if bool(self.plan.bad_guard(buf, b.layout.nbytes)):
             raise RuntimeError(f"mailbox canary overwritten: worker {rank} message {seq} (bucket {bi})")
 
     def pub_buf(self, b: int) -> torch.Tensor:
@@ -594,14 +710,30 @@ class PSAsyncEngine(Engine):
     # words per doorbell.
     BATCH = 16  # max sources per aggregate launch (kMaxSlots)
 
+    def _remote(self, i: int) -> bool:
+        """Worker i's mailbox slots are written by another GPU over xGMI (ipc transport): the PS's
+        kernels must acquire at system scope before reading them (csrc/common.h).  The p2p
+        transport's receives are RCCL kernels on this device, ordered before the PS stream."""
+        return self.cuda and not self.p2p and i != self.rank
+
+    def _slot_read(self, i: int, slot: int, lo: int, hi: int) -> torch.Tensor:
+        """Bytes [lo, hi) of worker i's slot for ordinary torch kernels: a remote worker's bytes
+        are first staged through a system-scope acquire."""
+        v = self.slot_buf(i, slot)[lo:hi]
+        if not self._remote(i):
+            return v
+        out = torch.empty(hi - lo, dtype=torch.uint8, device=v.device)
+        ops.copy_acquire(v, out)
+        return out
+
     def accumulate(self, i: int, slot: int, bi: int, seq: int, scale: float):
         if self.plan.guarded:
             self._verify_slot(i, slot, bi, seq)
-        self._pend.append((bi, scale, self._bucket_msg(bi, self.slot_buf(i, slot))))
+        self._pend.append((bi, scale, self._bucket_msg(bi, self.slot_buf(i, slot)), self._remote(i)))
         if self._lat is not None and i == 0:
             self._lat.note(bi, seq)
         for _ in range(self.emu):  # emulated remote workers: the same bytes, one launch each
-            self._pend.append((bi, scale, None))
+            self._pend.append((bi, scale, None, False))
 
     def ack(self, i: int, seq: int):
         self._pend_acks.append((self.C.F_ACK_SEQ, i, seq))
@@ -609,17 +741,22 @@ class PSAsyncEngine(Engine):
     def flush(self):
         if self._pend:
             groups = {}
+            remote = {}
             emu = []
-            for bi, scale, msg in self._pend:
+            for bi, scale, msg, rem in self._pend:
                 if msg is None:  # emulated remote copy of the preceding real message
                     emu.append((bi, scale, groups[(bi, scale)][-1]))
                     continue
                 groups.setdefault((bi, scale), []).append(msg)
+                remote.setdefault((bi, scale), []).append(rem)
             with self.tracer.phase("ps_accumulate", self.ps_stream):
                 for (bi, scale), msgs in groups.items():
                     b = self.plan.buckets[bi]
+                    rem = remote[(bi, scale)]
                     for k in range(0, len(msgs), self.BATCH):
-                        self.codec.accumulate(msgs[k:k + self.BATCH], self.acc[b.lo:b.hi], scale, True)
+                        # a batch holding a peer-written slot acquires at system scope first
+                        kw = {"acquire": True} if any(rem[k:k + self.BATCH]) else {}
+                        self.codec.accumulate(msgs[k:k + self.BATCH], self.acc[b.lo:b.hi], scale, True, **kw)
                 for bi, scale, msg in emu:
                     b = self.plan.buckets[bi]
                     self.codec.accumulate([msg], self.acc[b.lo:b.hi], scale, True)
@@ -646,7 +783,7 @@ class PSAsyncEngine(Engine):
             self._pres_part_b[bi] = None
             return
         ns = len(self.store.slots)
-        p = self.slot_buf(i, slot)[self.slot_pres:self.slot_pres + ns]
+        p = self._slot_read(i, slot, self.slot_pres, self.slot_pres + ns)
         cur = self._pres_part_b[bi]
         self._pres_part_b[bi] = p.clone() if cur is None else torch.maximum(cur, p)
 
@@ -707,7 +844,7 @@ class PSAsyncEngine(Engine):
             self._pres_part = None
             return
         ns = len(self.store.slots)
-        p = self.slot_buf(i, slot)[self.slot_pres:self.slot_pres + ns]
+        p = self._slot_read(i, slot, self.slot_pres, self.slot_pres + ns)
         self._pres_part = p.clone() if self._pres_part is None else torch.maximum(self._pres_part, p)
 
     def _hold(self):
@@ -899,13 +1036,26 @@ class PSAsyncEngine(Engine):
             raise RuntimeError("rank 0 is a dedicated parameter server (ps_dedicated=True): it does not train; "
                                "call opt.serve() there")
         C = self.C
+        if self._broken:
+            raise RuntimeError(self._broken)
         data = {}
         early = self._npushed
         if early and any(self.order[p] in self._late for p in range(early)):
-            self._npushed = 0
-            raise RuntimeError("a gradient arrived for a bucket that was already pushed to the PS during backward "
-                               "(backward() called twice before step()): wrap the earlier micro-batches in "
-                               "opt.no_sync(), or set push_early='off'")
+            # The PS maps message s to bucket order[(s-1) % nb]: the `early` messages already sent
+            # moved this worker's sequence, and the step cannot be completed with the gradients
+            # the PS expects.  Continuing would shift every later message onto the wrong bucket,
+            # so the engine is unusable from here on (every later step() raises the same error).
+            self._broken = ("a gradient arrived for a bucket that was already pushed to the PS during backward "
+                            "(backward() called twice before step()): wrap the earlier micro-batches in "
+                            "opt.no_sync(), or set push_early='off'; this ps_async engine cannot continue "
+                            "(its message sequence is now out of step with the PS)")
+            self._npushed, self._push_wait = 0, 0.0
+            self._encoded = [False] * len(self._encoded)
+            self._bucket_count = [0] * len(self._bucket_count)
+            self._late.clear()
+            self._fired = bytearray(len(self._fired))
+            self.remove_hooks()
+            raise RuntimeError(self._broken)
         data["code_wait"] = self.encode_all()
         self.verify_guards([self.wire], "encode")
         self._check_error()

@@ -57,8 +57,16 @@ class CommWatchdog:
         with self._lock:
             return len(self._events)
 
-    def close(self):
+    def close(self, join_s: float = 5.0):
+        """Stop the thread and wait for it (bounded), then forget pending events: the caller may
+        destroy the communicator next, and a poll racing that destroy would read the destroyed
+        comm's error state as a failure and exit with the abort status."""
         self._stop.set()
+        if self._thread.is_alive() and self._thread is not threading.current_thread():
+            self._thread.join(timeout=join_s)
+        with self._lock:
+            self._events = []
+            self._armed = None
 
     def _fail(self, what: str, why: str):
         sys.stderr.write(f"[hipps] rank {self.rank}: exchange '{what}' {why}; a peer is dead or hung -- aborting "
@@ -77,15 +85,20 @@ class CommWatchdog:
         done = []
         now = time.monotonic()
         for item in evs:
+            if self._stop.is_set():  # close() in progress: the communicator may be going away
+                return
             ev, what, t0, poll = item
+            if ev.query():  # completed: nothing left to poll the communicator for
+                done.append(item)
+                continue
             if poll is not None:
                 try:
                     poll()
                 except Exception as e:  # ncclCommGetAsyncError reported a failure
+                    if self._stop.is_set():
+                        return
                     self._fail(what, f"failed asynchronously ({e})")
-            if ev.query():
-                done.append(item)
-            elif now - t0 > self.limit:
+            if now - t0 > self.limit:
                 self._fail(what, f"did not complete on the device within {self.limit:.0f}s (comm_timeout_s)")
         if done:
             with self._lock:

@@ -88,8 +88,11 @@ def load(opt, path: str, model: Optional[torch.nn.Module] = None) -> dict:
     opt._group_steps = list(ps["group_steps"])
     opt.steps = ps["steps"]
     cs = opt._csteps()
-    if cs is not None and ps.get("chunk_steps") is not None:
-        cs.copy_(ps["chunk_steps"].to(cs.device))
+    if cs is not None:
+        if ps.get("chunk_steps") is not None:
+            cs.copy_(ps["chunk_steps"].to(cs.device))
+        else:  # older checkpoint: per-group counts only (SGD: + the groups whose momentum started)
+            opt.csteps_from_groups(cs, ps["mom_started"] if "mom_started" in ps else None)
     rank = opt.world.rank
     rp = os.path.join(path, f"rank{rank}.pt")
     mine = torch.load(rp, map_location="cpu", weights_only=True) if os.path.exists(rp) else {"engine": {}}

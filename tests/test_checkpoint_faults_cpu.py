@@ -9,7 +9,7 @@ from dist_util import run_world
 from test_dist_cpu import _data, _mlp
 
 
-def _run(rank, world, mode, steps_a, steps_b, ckpt, codec, max_delay):
+def _run(rank, world, mode, steps_a, steps_b, ckpt, codec, max_delay, legacy=None, optim="SGD"):
     import hipps
     from hipps.utils import checkpoint
 
@@ -18,6 +18,8 @@ def _run(rank, world, mode, steps_a, steps_b, ckpt, codec, max_delay):
         kw = dict(mode=mode, code=codec)
         if mode == "ps_async":
             kw["max_delay"] = max_delay
+        if optim == "Adam":
+            return m, hipps.Adam(m.named_parameters(), lr=0.01, **kw)
         return m, hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, **kw)
 
     m, opt = make()
@@ -29,6 +31,13 @@ def _run(rank, world, mode, steps_a, steps_b, ckpt, codec, max_delay):
     if ckpt:
         checkpoint.save(opt, ckpt, m)
         opt.close()
+        if legacy is not None and rank == 0:  # rewrite ps.pt in the pre-chunk_steps layout
+            path = os.path.join(ckpt, "ps.pt")
+            ps = torch.load(path, weights_only=True)
+            del ps["chunk_steps"]
+            if legacy == "mom_started":
+                ps["mom_started"] = [0]
+            torch.save(ps, path)
         m, opt = make()  # fresh process state: different init is overwritten by the load
         checkpoint.load(opt, ckpt, m)
     for s in range(steps_a, steps_a + steps_b):
@@ -52,6 +61,17 @@ def test_resume_is_exact(tmp_path, mode, W, codec, max_delay):
     assert os.path.exists(tmp_path / "ck" / "ps.pt")
     sd = torch.load(tmp_path / "ck" / "ps.pt", weights_only=True)
     assert sd["mode"] == mode
+
+
+@pytest.mark.parametrize("optim,legacy", [("SGD", "mom_started"), ("SGD", "none"), ("Adam", "none")])
+def test_resume_from_checkpoint_without_chunk_steps(tmp_path, optim, legacy):
+    """a checkpoint written before per-chunk step counts existed stores only per-group
+    counts (SGD: 'mom_started').  Loading it must rebuild the counts, or the first step after the
+    resume would restart every momentum buffer (buf = d_p) and Adam's bias correction at t=1."""
+    straight = run_world(_run, 1, "local", 3, 3, None, "fp32", 0, None, optim)
+    resumed = run_world(_run, 1, "local", 3, 3, str(tmp_path / "ck"), "fp32", 0, legacy, optim)
+    for a, b in zip(straight[0], resumed[0]):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
 
 
 def _faulty(rank, world, steps):

@@ -349,3 +349,32 @@ def test_topk_small_single_workgroup(n, k, vdt, case):
     assert torch.equal(idd.cpu(), idx)
     assert torch.equal(vd.cpu(), val)
     assert torch.equal(r_dev.cpu(), r_cpu)
+
+
+@pytest.mark.parametrize("spec", ["fp32", "bf16", "int8", "topk:0.05", "topk_int8:0.05", "threshold:0.5:0.2"])
+def test_codec_accumulate_acquire_path_matches(spec):
+    """The PS's acquire path for peer-written mailbox slots (system-scope acquire in every
+    workgroup before the first load, csrc/common.h) computes exactly what the plain path does."""
+    n = 70001
+    torch.manual_seed(3)
+    c = codecs.get_codec(spec)
+    lay = c.layout(n)
+    msgs = []
+    for w in range(3):
+        buf = torch.zeros(lay.nbytes, dtype=torch.uint8, device=DEV)
+        v = lay.views(buf)
+        c.encode_into(torch.randn(n, device=DEV), v, c.init_state(n, torch.device(DEV)))
+        msgs.append(v)
+    base = torch.randn(n, device=DEV)
+    a, b = base.clone(), base.clone()
+    c.accumulate(msgs, a, 0.5, True)
+    c.accumulate(msgs, b, 0.5, True, acquire=True)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n", [1, 15, 16, 4097, 1 << 20])
+def test_copy_acquire(n):
+    src = torch.randint(0, 256, (n,), dtype=torch.uint8, device=DEV)
+    dst = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    ops.copy_acquire(src, dst)
+    assert torch.equal(src, dst)

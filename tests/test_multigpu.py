@@ -18,7 +18,7 @@ NDEV = torch.cuda.device_count() if torch.cuda.is_available() else 0
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(NDEV < 2, reason="needs >= 2 HIP devices")]
 
 
-def _tiny(rank, world, pull, steps, codec, transport="ipc"):
+def _tiny(rank, world, pull, steps, codec, transport="ipc", bucket_mb=64.0, slots=0):
     import torch.nn.functional as F
 
     import hipps
@@ -29,7 +29,7 @@ def _tiny(rank, world, pull, steps, codec, transport="ipc"):
     torch.manual_seed(rank)
     m = resnet_tiny().to(dev).to(memory_format=torch.channels_last)
     opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", code=codec, pull=pull,
-                    average=True, async_transport=transport)
+                    average=True, async_transport=transport, bucket_mb=bucket_mb, mailbox_slots=slots)
     eng = opt.engine
     info = dict(eng.transport_info())
     info["mem_device"] = eng.mem.device.index if eng.mem is not None else rank
@@ -66,6 +66,21 @@ def test_async_ps_across_devices(pull, codec, transport):
         if pull == "device" and transport == "ipc":
             assert o["pull"] == "device"
         assert o["transport"] == transport
+
+
+@pytest.mark.parametrize("codec", ["fp32", "int8", "topk:0.05"])
+def test_async_ps_across_devices_small_buckets_slot_reuse(codec):
+    """tiny buckets and a 2-slot mailbox, so a peer rewrites each slot every
+    second message over xGMI while the PS's L2 may still hold the previous message's lines; the PS
+    kernels' system-scope acquire (csrc/common.h) must make every message count exactly once."""
+    W = min(NDEV, 4)
+    steps = 10
+    out = run_world(_tiny, W, "device", steps, codec, "ipc", 0.02, 2, timeout=600, backend="nccl")
+    st = out[0]["stats"]
+    assert st["accumulated"] == W * steps, st
+    assert st["updates"] == steps
+    for o in out:
+        assert o["finite"] and o["versions"][-1] > 0
 
 
 def _sync(rank, world, mode, transport, codec):

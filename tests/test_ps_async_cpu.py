@@ -291,8 +291,17 @@ def _early(rank, world, steps, push_early, granularity="model", twice=False):
             err = str(e)
             break
         early.append(data["pushed_early"])
+    err2 = None
+    if err is not None:  # a caller that catches the error and keeps training
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x), y).backward()
+        try:
+            opt.step()
+        except RuntimeError as e:
+            err2 = str(e)
     opt.close()
-    return {"nb": nb, "early": early, "err": err, "params": [p.detach().clone() for p in m.parameters()]}
+    return {"nb": nb, "early": early, "err": err, "err2": err2,
+            "params": [p.detach().clone() for p in m.parameters()]}
 
 
 @pytest.mark.parametrize("granularity", ["model", "bucket"])
@@ -314,3 +323,6 @@ def test_async_push_early_rejects_a_late_gradient():
     silently dropped gradient (opt.no_sync() or push_early='off' are the ways out)."""
     out = run_world(_early, 1, 2, "on", "model", True)
     assert out[0]["err"] is not None and "no_sync" in out[0]["err"]
+    # ADVICE r3: the early messages already moved the worker's sequence, so the engine must not
+    # accept another step (later messages would land on the wrong buckets of the PS)
+    assert out[0]["err2"] is not None and "cannot continue" in out[0]["err2"]

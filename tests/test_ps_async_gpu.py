@@ -268,3 +268,49 @@ def test_gpu_wgrad_side_stream_bitwise():
     assert out["used"]
     for a, b in zip(out["ref"], out["side"]):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
+
+
+def _slot_reuse(rank, world, steps, bucket_mb, slots, mode="ps_async", codec="fp32", granularity="model"):
+    """Every rank trains on rank 0's data: identical gradients, so the PS's sum is independent of
+    the order messages arrive in and runs are comparable bit for bit."""
+    import hipps
+
+    torch.cuda.set_device(0)
+    m = _mlp().cuda()
+    kw = dict(mode=mode, code=codec, bucket_mb=bucket_mb)  # same buckets: same int8 blocks
+    if mode == "ps_async":
+        kw.update(max_delay=0, accumulate=world, mailbox_slots=slots, ps_granularity=granularity)
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, **kw)
+    nb = len(opt.engine.plan.buckets)
+    used_slots = getattr(opt.engine, "SLOTS", None)
+    for s in range(steps):
+        x, y = _data(0, s % 4)
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x.cuda()), y.cuda()).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    st = opt.engine.ps_stats() if mode == "ps_async" else {}
+    opt.close()
+    return {"nb": nb, "slots": used_slots, "stats": st, "params": [p.detach().cpu() for p in m.parameters()]}
+
+
+@pytest.mark.parametrize("codec", ["fp32", "int8"])
+def test_async_slot_reuse_stress_bitwise(codec):
+    """tiny buckets (bucket_mb=0.05) and a 2-slot mailbox, so every
+    slot is rewritten every second message.  W=1 must equal local SGD bit for bit; W=3 on one
+    device (ranks 1 and 2 take the PS's acquire path for peer-written slots) must equal the same
+    world with roomy default slots (2 per bucket: no reuse within a step)."""
+    steps = 8
+    a = run_world(_slot_reuse, 1, steps, 0.05, 2, "ps_async", codec)[0]
+    b = run_world(_slot_reuse, 1, steps, 0.05, 2, "local", codec)[0]
+    assert a["nb"] >= 4 and a["slots"] == 2
+    assert a["stats"]["accumulated"] == steps
+    for x, y in zip(a["params"], b["params"]):
+        torch.testing.assert_close(x, y, rtol=0, atol=0)
+    c = run_world(_slot_reuse, 3, steps, 0.05, 2, "ps_async", codec, timeout=300)
+    d = run_world(_slot_reuse, 3, steps, 0.05, 0, "ps_async", codec, timeout=300)
+    assert c[0]["slots"] == 2 and c[0]["nb"] >= 4 and d[0]["slots"] == 2 * d[0]["nb"]
+    assert c[0]["stats"]["accumulated"] == 3 * steps and c[0]["stats"]["updates"] == steps
+    for r in range(3):
+        for x, y in zip(c[r]["params"], d[r]["params"]):
+            torch.testing.assert_close(x, y, rtol=0, atol=0)

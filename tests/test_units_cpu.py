@@ -139,3 +139,61 @@ def test_stem_routing_predicates():
     out = m(torch.randn(2, 3, 64, 64))
     out.sum().backward()
     assert m.conv1.weight.grad is not None and m.bn1.weight.grad is not None
+
+
+def test_watchdog_close_joins_and_skips_completed_events():
+    """a completed event is never polled (the communicator may already be gone), and
+    close() joins the thread and drops pending events before the caller destroys the comm, so a
+    clean shutdown cannot end in the watchdog's abort exit."""
+    import threading
+
+    from hipps.parallel.watchdog import CommWatchdog
+
+    class Ev:
+        def __init__(self, done):
+            self.done = done
+
+        def query(self):
+            return self.done
+
+    polls = []
+    wd = CommWatchdog(timeout_s=100.0)
+    wd.watch(Ev(True), "done-exchange", lambda: polls.append(1))
+    wd._check_events()
+    assert polls == [] and wd.pending() == 0
+
+    def bad_poll():
+        raise RuntimeError("ncclInvalidUsage: communicator destroyed")
+
+    wd.watch(Ev(False), "pending-exchange", bad_poll)
+    wd.close()
+    assert not wd._thread.is_alive() and wd.pending() == 0
+    wd._check_events()  # after close: nothing left to poll, no exit
+    assert threading.current_thread().is_alive()
+
+
+def test_ps_memory_budget_terms_and_engine_agree():
+    """the rank-0 PS budget is computed before allocation; the shape-only
+    calculator (tools/ps_budget.py) and a live engine agree term by term."""
+    import hipps
+    from hipps.parallel.ps_async import budget_for_shapes, ps_memory_budget
+    from test_dist_cpu import _mlp
+
+    b = ps_memory_budget(1000, W=8, slots=4, slot_bytes=4096, npub=4, pub_esz=2, opt_floats=1)
+    assert b["mailbox"] == 8 * 4 * 4096 and b["publish"] == 4 * 1000 * 2
+    assert b["master"] == b["accumulator"] == b["optimizer"] == 4000
+    assert b["ps_total"] == sum(b[k] for k in ("mailbox", "publish", "master", "accumulator", "optimizer",
+                                                  "chunk_steps"))
+    assert b["total"] == b["ps_total"] + b["worker_total"]
+    d = ps_memory_budget(1000, 8, 4, 4096, 4, 2, 1, colocated=False)
+    assert d["worker_total"] == 0 and d["total"] == d["ps_total"] == b["ps_total"]
+
+    m = _mlp()
+    opt = hipps.SGD(m.named_parameters(), lr=0.1, momentum=0.9, mode="ps_async", bucket_mb=0.05, code="int8")
+    live = opt.engine.memory_budget()
+    shp = budget_for_shapes([tuple(p.shape) for p in m.parameters()], W=1, codec="int8", bucket_mb=0.05,
+                            param_wire="fp32", opt_floats=1, shadow=False)
+    opt.close()
+    for k in ("mailbox", "publish", "master", "accumulator", "optimizer", "chunk_steps", "worker_wire",
+              "worker_codec_state"):
+        assert live[k] == shp[k], (k, live[k], shp[k])
