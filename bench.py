@@ -53,7 +53,13 @@ def parse():
                     help="published-parameter dtype: auto = fp32 at N=1 (local pull), bf16 at N>1 (halves the "
                          "xGMI pull; the PS keeps the fp32 master, workers compute in bf16 anyway)")
     ap.add_argument("--momentum", type=float, default=0.9)
-    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--bucket-mb", type=float, default=None,
+                    help="bucket size (default: 16 with --granularity bucket, else 64)")
+    ap.add_argument("--granularity", default=None, choices=["model", "bucket"],
+                    help="ps_async update/publication granularity (default: the library's, PSConfig.ps_granularity)")
+    ap.add_argument("--lookahead", type=float, default=None,
+                    help="ps_async look-ahead publish tau (default: the library's, PSConfig.stale_lookahead = 0: "
+                         "plain AsySG-InCon, the reference's algorithm; -1 = auto delay compensation)")
     ap.add_argument("--mailbox-slots", type=int, default=0,
                     help="ps_async: bucket messages in flight per worker (0 = the library's auto)")
     ap.add_argument("--no-channels-last", action="store_true")
@@ -118,9 +124,18 @@ def main():
         a.param_wire = "bf16" if N > 1 else "fp32"
     note = None
     dedicated = bool(a.ps_dedicated and mode == "ps_async" and N > 1)
+    from hipps.config import PSConfig
+
+    dflt = PSConfig()
+    if a.granularity is None:
+        a.granularity = dflt.ps_granularity
+    if a.lookahead is None:
+        a.lookahead = dflt.stale_lookahead
+    if a.bucket_mb is None:
+        a.bucket_mb = dflt.bucket_mb
     kw = dict(lr=a.lr, momentum=a.momentum, weight_decay=5e-5, mode=mode, code=a.codec,
               accumulate=a.accumulate or None, average=True, param_wire=a.param_wire, bucket_mb=a.bucket_mb,
-              mailbox_slots=a.mailbox_slots,
+              mailbox_slots=a.mailbox_slots, ps_granularity=a.granularity, stale_lookahead=a.lookahead,
               async_transport=a.async_transport, ps_dedicated=dedicated)
     if a.emulate_remote and N == 1:
         kw["emulate_remote"] = a.emulate_remote
@@ -134,6 +149,7 @@ def main():
         note = f"ps_async ipc transport failed ({type(e).__name__}: {e}); fell back to the p2p transport"
         print("[bench] " + note, file=sys.stderr)
         kw["async_transport"] = "p2p"
+        kw["ps_granularity"] = "model"  # per-bucket publication needs the ipc transport
         opt = hipps.SGD(model.named_parameters(), **kw)
     # N > 1: pull the last stage's parameters (ResNet layer4 + fc: 2/3 of the model) over xGMI on a
     # side stream, overlapped with the forward of layers 1-3.  At N = 1 the pull is a local
@@ -288,6 +304,14 @@ def main():
                 "grad_bytes_per_step_used": int(grad_used),
                 "param_wire": a.param_wire, "pull_overlap": pull_overlap,
                 "async_transport": kw.get("async_transport") if mode == "ps_async" else None,
+                # which algorithm ran: AsySG-InCon (README.md:56-81) reads the PS's parameters as
+                # published (stale_lookahead 0); > 0 / -1 = delay-compensated (look-ahead) publish
+                "algorithm": ("AsySG-InCon" + ("" if kw.get("stale_lookahead", 0) == 0 else
+                                               " + look-ahead publish (delay compensation)"))
+                if mode == "ps_async" else mode,
+                "ps_granularity": kw.get("ps_granularity") if mode == "ps_async" else None,
+                "stale_lookahead": kw.get("stale_lookahead") if mode == "ps_async" else None,
+                "bucket_mb": a.bucket_mb,
                 "num_params": nparams,
                 "buckets": nbuckets,
             },

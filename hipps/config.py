@@ -58,11 +58,13 @@ class PSConfig:
     push_early: str = "auto"
     # async PS: scale a kept gradient by 1/max(1, staleness) (staleness-aware async SGD)
     staleness_lr: bool = False
-    # async PS look-ahead publish (delay-compensated momentum): workers read the parameters
-    # extrapolated by the momentum of the next tau updates, the tau updates their gradient will
-    # arrive late by; the PS master is unchanged.  -1 = auto (tau = mean measured staleness of the
-    # recent accumulated steps; off when max_delay == 0), 0 = off, > 0 = fixed tau
-    stale_lookahead: float = -1.0
+    # async PS look-ahead publish (delay-compensated momentum, DANA-style; NOT part of the
+    # reference's AsySG-InCon, README.md:56-81, which reads the PS's parameters as they are):
+    # workers read the parameters extrapolated by the momentum of the next tau updates, the tau
+    # updates their gradient will arrive late by; the PS master is unchanged.  0 = off (default:
+    # the reference's algorithm), -1 = auto (tau = mean measured staleness of the recent accumulated
+    # steps; off when max_delay == 0), > 0 = fixed tau
+    stale_lookahead: float = 0.0
     # rehearsal knob (one process, one GPU): the co-located PS also carries the load of this many
     # emulated remote workers -- every message of worker 0 is accumulated 1 + E times (one launch
     # each; the update scales by 1/(1+E), so the math is unchanged) and every update is followed by

@@ -955,10 +955,15 @@ static void launch_wgrad2(const at::Tensor& dy, const at::Tensor& x, at::Tensor&
 // dw[N][K] = sum_s part[s][N][K] in a fixed order (deterministic); shared with gemm2.hip's
 // weight-gradient core.  Split over G groups when N*K alone is too few threads to keep the
 // loads in flight (64x64 outputs: 1024 float4 lanes x S serial loads was ~60 us).
+int64_t wgrad_reduce_groups(int64_t S, int64_t N, int64_t K) {
+  const int64_t NK4 = N * K / 4;
+  return std::min<int64_t>(S, std::max<int64_t>(1, (65536 + NK4 - 1) / NK4));
+}
+
 void wgrad_reduce_slabs(const at::Tensor& part, int64_t S, int64_t N, int64_t K, at::Tensor& dw,
                         hipStream_t stream0) {
   const int64_t NK4 = N * K / 4;
-  const int G = (int)std::min<int64_t>(S, std::max<int64_t>(1, (65536 + NK4 - 1) / NK4));
+  const int G = (int)wgrad_reduce_groups(S, N, K);
   const unsigned gx = (unsigned)((NK4 + kBlock - 1) / kBlock);
   if (G == 1) {
     hipLaunchKernelGGL(k_wgrad_reduce1, dim3(gx, 1), kBlock, 0, stream0, part.data_ptr<float>(), (int)S, 1, NK4,

@@ -23,6 +23,8 @@
 #include "common.h"
 
 #include <ATen/ATen.h>
+#include <cstdlib>
+#include <mutex>
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
@@ -600,6 +602,12 @@ struct WArgs {
   int M, N, K, Cin, Ho, Wo, Hi, Wi, stride, KW, pad, chunk, tn, tk;
   FastDiv2 fd_hw, fd_w;
   const float *psc, *psh;  // PRO: the X operand is a BN input; the GEMM reads relu(x * psc + psh)
+  // in-launch split-M reduction (S > 1): per-tile arrival tickets (zero on entry, re-armed by the
+  // reducer), the number of slabs S, the reduce1 group count G (same order as gemm.hip
+  // wgrad_reduce_slabs, so the result is bit-identical to the separate reduce kernels) and dW
+  int* cnt;
+  int S, G;
+  float* dw;
 };
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -893,6 +901,69 @@ __global__ __launch_bounds__(64 * WN * WK) void k_wgrad(WArgs g) {
         out[(int64_t)n * g.K + k] = acc[i][j][r];
       }
     }
+  if (g.cnt == nullptr) return;  // S == 1 wrote dW directly, or the separate reduce kernels run
+  // In-launch split-M reduction: the block that completes a tile's S slabs sums them
+  // (cdna_hip_programming.md, "In-launch split-K reduction": plain slab stores, every wave drains,
+  // one agent-scope release before the ticket, one agent-scope acquire in the reducer; correct for
+  // any placement of a tile's slabs over XCDs).  Replaces one or two reduce launches per layer.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave's slab stores have completed; LDS is free (main loop done)
+  int* flag = reinterpret_cast<int*>(lds);  // the one LDS array (no second __shared__ object)
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(g.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == g.S - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(g.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+    }
+    flag[0] = last;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  // dW[n][k..k+3] = sum over slabs in wgrad_reduce_slabs' order: G groups of consecutive slabs,
+  // each summed with 4 interleaved accumulators, then the group sums in order
+  const int64_t NK = (int64_t)g.N * g.K;
+  constexpr int TK4 = TK / 4;
+  for (int e = t; e < TN * TK4; e += 64 * NW) {
+    const int n = n0 + e / TK4, k = k0 + (e - (e / TK4) * TK4) * 4;
+    if (MT && k >= g.K) continue;
+    const float* base = g.part + (int64_t)n * g.K + k;
+    float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int gi = 0; gi < g.G; ++gi) {
+      const int s0 = (int)((int64_t)gi * g.S / g.G), s1 = (int)((int64_t)(gi + 1) * g.S / g.G);
+      float4 a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      int s = s0;
+      for (; s + 3 < s1; s += 4) {
+        float4 b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) b[u] = *reinterpret_cast<const float4*>(base + (int64_t)(s + u) * NK);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          a[u].x += b[u].x; a[u].y += b[u].y; a[u].z += b[u].z; a[u].w += b[u].w;
+        }
+      }
+      for (; s < s1; ++s) {
+        const float4 b = *reinterpret_cast<const float4*>(base + (int64_t)s * NK);
+        a[0].x += b.x; a[0].y += b.y; a[0].z += b.z; a[0].w += b.w;
+      }
+      float4 r;
+      r.x = (a[0].x + a[1].x) + (a[2].x + a[3].x);
+      r.y = (a[0].y + a[1].y) + (a[2].y + a[3].y);
+      r.z = (a[0].z + a[1].z) + (a[2].z + a[3].z);
+      r.w = (a[0].w + a[1].w) + (a[2].w + a[3].w);
+      if (gi == 0) {
+        tot = r;
+      } else {
+        tot.x += r.x; tot.y += r.y; tot.z += r.z; tot.w += r.w;
+      }
+    }
+    *reinterpret_cast<float4*>(g.dw + (int64_t)n * g.K + k) = tot;
+  }
 }
 
 // default block tile for a problem (the Python side autotunes per shape and passes bm / bn)
@@ -1200,6 +1271,34 @@ at::Tensor gemm2_dgrad_s2(at::Tensor dy, at::Tensor wf, at::Tensor dx, int64_t b
 
 void wgrad_reduce_slabs(const at::Tensor& part, int64_t S, int64_t N, int64_t K, at::Tensor& dw,
                         hipStream_t stream0);
+int64_t wgrad_reduce_groups(int64_t S, int64_t N, int64_t K);
+
+// Arrival tickets of the in-launch weight-gradient reduction: a zeroed per-device ring, handed out
+// in consecutive ranges (one counter per output tile); the reducer of a tile re-arms its counter, so
+// the ring is never cleared again.  Launches in flight at once never share counters unless 64K
+// tiles' worth of launches are queued between them.
+static int* wgrad_tickets(const at::Tensor& like, int64_t n) {
+  constexpr int64_t kRing = 1 << 16;
+  static std::mutex mu;
+  static at::Tensor ring[64];
+  static int64_t cur[64];
+  const int dev = like.get_device();
+  TORCH_CHECK(dev >= 0 && dev < 64 && n <= kRing / 4, "wgrad tickets");
+  std::lock_guard<std::mutex> lock(mu);
+  if (!ring[dev].defined()) ring[dev] = at::zeros({kRing}, like.options().dtype(at::kInt));
+  if (cur[dev] + n > kRing) cur[dev] = 0;
+  int* p = ring[dev].data_ptr<int>() + cur[dev];
+  cur[dev] += n;
+  return p;
+}
+
+static bool wgrad_fused_reduce() {
+  static const bool on = [] {
+    const char* e = std::getenv("HIPPS_WGRAD_FUSED_REDUCE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 // Weight gradient on the LDS-DMA core: dy [img, Cout, Ho, Wo] and x [img, Cin, Hi, Wi] channels-last
 // bf16; dw f32 [Cout, KH, KW, Cin] in memory (the channels-last weight layout; 1x1: [Cout, Cin]).
@@ -1287,6 +1386,13 @@ void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t
     a.psc = pro_scale->data_ptr<float>();
     a.psh = pro_shift->data_ptr<float>();
   }
+  const bool fused = S > 1 && wgrad_fused_reduce();
+  if (fused) {  // the last block of each tile sums its S slabs in the launch (no reduce kernels)
+    a.cnt = wgrad_tickets(dw, tiles);
+    a.S = (int)S;
+    a.G = (int)wgrad_reduce_groups(S, N, K);
+    a.dw = dw.data_ptr<float>();
+  }
   const int grid = (int)(S * tiles);
 #define HIPPS_W2M(TNc, TKc, WNc, WKc, MTc)                                                                         \
   do {                                                                                                            \
@@ -1311,7 +1417,7 @@ void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t
   else HIPPS_W2(64, 64, 2, 2);
 #undef HIPPS_W2
 #undef HIPPS_W2M
-  if (S > 1) {
+  if (S > 1 && !fused) {
     at::Tensor dwv = dw;
     wgrad_reduce_slabs(part, S, N, K, dwv, stream);
   }

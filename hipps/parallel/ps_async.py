@@ -184,6 +184,92 @@ class _Pending:
             w.wait()
 
 
+class _TorchChannel:
+    """A p2p channel of the async PS on a torch.distributed process group of its own (RCCL pair
+    communicators on GPU, gloo on CPU): the group has its own communicators and streams, so two
+    channels never order each other's operations."""
+
+    def __init__(self, W: int):
+        self.pg = dist.new_group(list(range(W)))
+        self.native = False
+
+    def isend(self, t, peer):
+        return dist.isend(t, dst=peer, group=self.pg)
+
+    def irecv(self, t, peer):
+        return dist.irecv(t, src=peer, group=self.pg)
+
+    def send(self, t, peer):
+        dist.send(t, dst=peer, group=self.pg)
+
+    def recv(self, t, peer):
+        dist.recv(t, src=peer, group=self.pg)
+
+    def broadcast(self, t, src):
+        dist.broadcast(t, src=src, group=self.pg)
+
+    def close(self):
+        pass
+
+
+class _EventWork:
+    """Completion of an operation enqueued on a native RCCL channel's stream."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def is_completed(self) -> bool:
+        return self.ev.query()
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+
+
+class _RcclChannel:
+    """A p2p channel on a communicator split from hipps' native RCCL communicator
+    (``ncclCommSplit``, SURVEY.md §5.8 option (a); ``PSConfig.transport='rccl'``): one communicator
+    and one HIP stream per channel, so the gradient channel's posted receives never sit in front of
+    the parameter channel's sends.  Every operation is ordered after the caller's current stream
+    and reports completion through a HIP event, like a torch RCCL work."""
+
+    def __init__(self, base, rank: int, color: int, device):
+        self.comm = base.split(color, rank)
+        self.stream = torch.cuda.Stream(device=device)
+        self.native = True
+
+    def _post(self, fn, t, peer):
+        self.stream.wait_stream(torch.cuda.current_stream(t.device))
+        fn(t, peer, self.stream.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        return _EventWork(ev)
+
+    def isend(self, t, peer):
+        return self._post(self.comm.send, t, peer)
+
+    def irecv(self, t, peer):
+        return self._post(self.comm.recv, t, peer)
+
+    def send(self, t, peer):
+        self.isend(t, peer).ev.synchronize()
+
+    def recv(self, t, peer):
+        w = self.irecv(t, peer)
+        w.ev.synchronize()
+
+    def broadcast(self, t, src):
+        self.stream.wait_stream(torch.cuda.current_stream(t.device))
+        self.comm.broadcast(t, src, self.stream.cuda_stream)
+        torch.cuda.current_stream(t.device).wait_stream(self.stream)
+
+    def close(self):
+        try:
+            self.stream.synchronize()
+            self.comm.destroy()
+        except Exception:
+            pass
+
+
 class _LatencyProbe:
     """``HIPPS_PS_LATENCY=1`` with the PS co-located on rank 0: GPU time from the local worker's
     push doorbell of a bucket message (event on the comm stream) to the event on the PS stream
@@ -299,9 +385,18 @@ class PSAsyncEngine(Engine):
         # post order), and (b) the PS thread's traffic never interleaves with collectives that
         # rank 0's main thread issues on the default group (barrier, all_reduce).
         self._gpg = self._ppg = None
+        self._rccl_base = None
         if self.p2p:
-            self._gpg = dist.new_group(list(range(W)))
-            self._ppg = dist.new_group(list(range(W)))
+            if cfg.transport == "rccl" and self.cuda and world.backend == "nccl":
+                # native RCCL pair channels: two communicators split from hipps' own communicator
+                from .rccl import RcclGroup
+
+                self._rccl_base = RcclGroup(world, store.device)
+                self._gpg = _RcclChannel(self._rccl_base.comm, world.rank, 0, store.device)
+                self._ppg = _RcclChannel(self._rccl_base.comm, world.rank, 1, store.device)
+            else:
+                self._gpg = _TorchChannel(W)
+                self._ppg = _TorchChannel(W)
         token = secrets.token_hex(6) if self.rank == 0 else None
         handle = None
         self.mailbox = None
@@ -428,7 +523,7 @@ class PSAsyncEngine(Engine):
             # the transport self-test go first, on the main threads
             pub0 = self.pub_buf(0) if self.rank == 0 else torch.empty(store.numel, dtype=self.pub_dtype,
                                                                        device=store.device)
-            dist.broadcast(pub0, src=0, group=self._ppg)
+            self._ppg.broadcast(pub0, 0)
             self._adopt(pub0, 0)
             if self.cuda:
                 torch.cuda.current_stream(store.device).synchronize()
@@ -542,10 +637,10 @@ class PSAsyncEngine(Engine):
         if self.rank == 0:
             for r in range(1, W):
                 got = self.slot_buf(r, self.SLOTS - 1)[:16]
-                dist.recv(got, src=r, group=self._gpg)
+                self._gpg.recv(got, r)
                 ok &= bool((got.cpu() == (r * 7 + 3) % 251).all())
         else:
-            dist.send(tag, dst=0, group=self._gpg)
+            self._gpg.send(tag, 0)
         ck = float(self.pub_buf(0).double().sum()) if self.rank == 0 else None
         box = [ok, ck]
         dist.broadcast_object_list(box, src=0)
@@ -653,10 +748,10 @@ class PSAsyncEngine(Engine):
                         pos = (s - 1) % self.nb
                         b = self.plan.buckets[self.order[pos]]
                         sbuf = self.slot_buf(i, slot)
-                        works = [dist.irecv(sbuf[: b.msg_nbytes], src=i, group=self._gpg)]
+                        works = [self._gpg.irecv(sbuf[: b.msg_nbytes], i)]
                         if pos == self.nb - 1 and self.ctl.load(C.F_PUSH_FLAG, i * self.MAXSLOTS + slot):
-                            works.append(dist.irecv(sbuf[self.slot_pres:self.slot_pres + ns], src=i, group=self._gpg))
-                        inflight[i].append((s, _Pending(works, self.cuda)))
+                            works.append(self._gpg.irecv(sbuf[self.slot_pres:self.slot_pres + ns], i))
+                        inflight[i].append((s, _Pending(works, self.cuda or self._gpg.native)))
                         posted[i] = s
                     while inflight[i] and inflight[i][0][1].done():
                         s, pend = inflight[i].popleft()
@@ -679,7 +774,7 @@ class PSAsyncEngine(Engine):
         v = self.ver
         b = v % self.NPUB
         self.ctl.store(self.C.F_SENT_VER, i, v)
-        w = dist.isend(self.pub_buf(b), dst=i, group=self._ppg)  # ordered after the update that wrote buffer b
+        w = self._ppg.isend(self.pub_buf(b), i)  # ordered after the update that wrote buffer b
         self._pub_sends.setdefault(b, []).append(w)
 
     def _serve(self):
@@ -1104,10 +1199,10 @@ class PSAsyncEngine(Engine):
         self.ctl.store(C.F_PUSH_SEQ, self.rank, s)
         ctx = torch.cuda.stream(self.comm_stream) if self.cuda else contextlib.nullcontext()
         with ctx, self.tracer.phase("push", self.comm_stream):
-            works = [dist.isend(msg, dst=0, group=self._gpg)]
+            works = [self._gpg.isend(msg, 0)]
             if partial:
                 self._pres_send = self.presence_tensor()
-                works.append(dist.isend(self._pres_send, dst=0, group=self._gpg))
+                works.append(self._gpg.isend(self._pres_send, 0))
             for w in works:
                 w.wait()  # GPU: the comm stream waits; CPU: returns once the PS has the bytes
 
@@ -1145,11 +1240,11 @@ class PSAsyncEngine(Engine):
                     if self._stage_ev[k] is not None:
                         ps.wait_event(self._stage_ev[k])  # the last adoption from this stage is done
                     with torch.cuda.stream(ps):
-                        works = [dist.irecv(self._stage[k], src=0, group=self._ppg)]
+                        works = [self._ppg.irecv(self._stage[k], 0)]
                 else:
-                    works = [dist.irecv(self._stage[k], src=0, group=self._ppg)]
+                    works = [self._ppg.irecv(self._stage[k], 0)]
                 self._p2p_reqs += 1
-                self._p2p_req = (self._p2p_reqs, k, _Pending(works, self.cuda))
+                self._p2p_req = (self._p2p_reqs, k, _Pending(works, self.cuda or self._ppg.native))
                 self.ctl.store(C.F_PULL_REQ, self.rank, self._p2p_reqs)
             if not sync or self.local_ver >= need:
                 return adopted
@@ -1459,6 +1554,7 @@ class PSAsyncEngine(Engine):
 
     def transport_info(self) -> dict:
         return {"transport": "p2p" if self.p2p else "ipc", "doorbells": self.ctl.bell_mode, "pull": self.pull_mode,
+                "p2p_channels": (None if not self.p2p else "rccl-split" if self._gpg.native else "torch"),
                 "ps_dedicated": self.dedicated, "accumulate": self.M,
                 "npub": self.NPUB,
                 "mailbox_slots": self.SLOTS, "slot_bytes": self.slot_bytes}
@@ -1497,6 +1593,12 @@ class PSAsyncEngine(Engine):
         finally:
             if self.rank != 0 and self.cuda and self.mailbox is not None:
                 self.mailbox.close()
+            for ch in (self._gpg, self._ppg):
+                if ch is not None:
+                    ch.close()
+            if self._rccl_base is not None:
+                self._rccl_base.close()
+                self._rccl_base = None
         if self._err:
             raise RuntimeError(self._err)
 

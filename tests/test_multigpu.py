@@ -18,7 +18,7 @@ NDEV = torch.cuda.device_count() if torch.cuda.is_available() else 0
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(NDEV < 2, reason="needs >= 2 HIP devices")]
 
 
-def _tiny(rank, world, pull, steps, codec, transport="ipc", bucket_mb=64.0, slots=0):
+def _tiny(rank, world, pull, steps, codec, transport="ipc", bucket_mb=64.0, slots=0, comm="torch"):
     import torch.nn.functional as F
 
     import hipps
@@ -29,7 +29,8 @@ def _tiny(rank, world, pull, steps, codec, transport="ipc", bucket_mb=64.0, slot
     torch.manual_seed(rank)
     m = resnet_tiny().to(dev).to(memory_format=torch.channels_last)
     opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", code=codec, pull=pull,
-                    average=True, async_transport=transport, bucket_mb=bucket_mb, mailbox_slots=slots)
+                    average=True, async_transport=transport, bucket_mb=bucket_mb, mailbox_slots=slots,
+                    transport=comm)
     eng = opt.engine
     info = dict(eng.transport_info())
     info["mem_device"] = eng.mem.device.index if eng.mem is not None else rank
@@ -66,6 +67,19 @@ def test_async_ps_across_devices(pull, codec, transport):
         if pull == "device" and transport == "ipc":
             assert o["pull"] == "device"
         assert o["transport"] == transport
+
+
+@pytest.mark.parametrize("codec", ["fp32", "int8", "topk:0.05"])
+def test_async_p2p_on_native_rccl_split_channels():
+    """the p2p transport's gradient and parameter channels as two communicators
+    split from hipps' own RCCL communicator (ncclCommSplit) instead of torch process groups."""
+    W = min(NDEV, 4)
+    steps = 10
+    out = run_world(_tiny, W, "device", steps, "bf16", "p2p", 64.0, 0, "rccl", timeout=600, backend="nccl")
+    st = out[0]["stats"]
+    assert st["accumulated"] == W * steps and st["updates"] == steps
+    for o in out:
+        assert o["transport"] == "p2p" and o["p2p_channels"] == "rccl-split" and o["finite"]
 
 
 @pytest.mark.parametrize("codec", ["fp32", "int8", "topk:0.05"])

@@ -296,20 +296,20 @@ def _slot_reuse(rank, world, steps, bucket_mb, slots, mode="ps_async", codec="fp
 
 @pytest.mark.parametrize("codec", ["fp32", "int8"])
 def test_async_slot_reuse_stress_bitwise(codec):
-    """tiny buckets (bucket_mb=0.05) and a 2-slot mailbox, so every
-    slot is rewritten every second message.  W=1 must equal local SGD bit for bit; W=3 on one
+    """one bucket per parameter (bucket_mb=1e-5) and a 2-slot mailbox,
+    so every slot is rewritten every second message.  W=1 must equal local SGD bit for bit; W=3 on one
     device (ranks 1 and 2 take the PS's acquire path for peer-written slots) must equal the same
     world with roomy default slots (2 per bucket: no reuse within a step)."""
     steps = 8
-    a = run_world(_slot_reuse, 1, steps, 0.05, 2, "ps_async", codec)[0]
-    b = run_world(_slot_reuse, 1, steps, 0.05, 2, "local", codec)[0]
-    assert a["nb"] >= 4 and a["slots"] == 2
+    a = run_world(_slot_reuse, 1, steps, 1e-5, 2, "ps_async", codec)[0]
+    b = run_world(_slot_reuse, 1, steps, 1e-5, 2, "local", codec)[0]
+    assert a["nb"] == 4 and a["slots"] == 2
     assert a["stats"]["accumulated"] == steps
     for x, y in zip(a["params"], b["params"]):
         torch.testing.assert_close(x, y, rtol=0, atol=0)
-    c = run_world(_slot_reuse, 3, steps, 0.05, 2, "ps_async", codec, timeout=300)
-    d = run_world(_slot_reuse, 3, steps, 0.05, 0, "ps_async", codec, timeout=300)
-    assert c[0]["slots"] == 2 and c[0]["nb"] >= 4 and d[0]["slots"] == 2 * d[0]["nb"]
+    c = run_world(_slot_reuse, 3, steps, 1e-5, 2, "ps_async", codec, timeout=300)
+    d = run_world(_slot_reuse, 3, steps, 1e-5, 0, "ps_async", codec, timeout=300)
+    assert c[0]["slots"] == 2 and c[0]["nb"] == 4 and d[0]["slots"] == 2 * d[0]["nb"]
     assert c[0]["stats"]["accumulated"] == 3 * steps and c[0]["stats"]["updates"] == steps
     for r in range(3):
         for x, y in zip(c[r]["params"], d[r]["params"]):
