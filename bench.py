@@ -62,6 +62,11 @@ def parse():
                          "plain AsySG-InCon, the reference's algorithm; -1 = auto delay compensation)")
     ap.add_argument("--mailbox-slots", type=int, default=0,
                     help="ps_async: bucket messages in flight per worker (0 = the library's auto)")
+    ap.add_argument("--gc", default=os.environ.get("BENCH_GC", "freeze"), choices=["freeze", "default", "off"],
+                    help="Python garbage collector during the timed steps: 'freeze' (default) moves every object "
+                         "alive after warmup (model, optimizer, autograd machinery) out of the collector's "
+                         "generations, so periodic full collections no longer stall the host at step boundaries; "
+                         "'off' disables it for the timed steps; 'default' leaves it alone")
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--no-fallback", action="store_true",
@@ -127,6 +132,7 @@ def main():
     from hipps.config import PSConfig
 
     dflt = PSConfig()
+    dflt.apply_env()  # HIPPS_<FIELD> overrides count as the defaults (and are recorded below)
     if a.granularity is None:
         a.granularity = dflt.ps_granularity
     if a.lookahead is None:
@@ -213,6 +219,13 @@ def main():
         torch.cuda.synchronize()
         tr.flush()
         tr.totals.clear()
+    import gc
+
+    if a.gc != "default":
+        gc.collect()
+        gc.freeze()  # long-lived objects leave the collector's generations (Python >= 3.7)
+        if a.gc == "off":
+            gc.disable()
     hdist.barrier(world)
     torch.cuda.synchronize()
     if host_t is not None:
@@ -227,6 +240,8 @@ def main():
     torch.cuda.synchronize()
     hdist.barrier(world)
     t1 = time.perf_counter()
+    if a.gc == "off":
+        gc.enable()
     el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev if world.backend == "nccl" else "cpu")
     if N > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -312,6 +327,7 @@ def main():
                 "ps_granularity": kw.get("ps_granularity") if mode == "ps_async" else None,
                 "stale_lookahead": kw.get("stale_lookahead") if mode == "ps_async" else None,
                 "bucket_mb": a.bucket_mb,
+                "python_gc": a.gc,
                 "num_params": nparams,
                 "buckets": nbuckets,
             },

@@ -830,6 +830,25 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
   return before + x - v;
 }
 
+// h[bin] += 1 for every lane with ``want``.  Gradient magnitudes cluster in a few exponent bins,
+// so plain LDS atomics serialise up to 64-way inside a wave on the top-digit pass: the first
+// rounds let one leader lane add the popcount of all lanes that share its bin, the lanes left
+// after them (diverse bins, little contention) add one each.
+__device__ __forceinline__ void wave_hist_add(uint32_t* h, uint32_t bin, bool want) {
+  const int lane = threadIdx.x & 63;
+  uint64_t pending = __ballot(want);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (!pending) break;
+    const int leader = __ffsll((unsigned long long)pending) - 1;
+    const uint32_t lb = __shfl(bin, leader, 64);
+    const uint64_t same = __ballot(want && bin == lb) & pending;
+    if (lane == leader) atomicAdd(&h[lb], (uint32_t)__popcll(same));
+    pending &= ~same;
+  }
+  if ((pending >> lane) & 1ull) atomicAdd(&h[bin], 1u);
+}
+
 template <typename VT>
 __global__ __launch_bounds__(kSmallThreads) void k_topk_small(const float* __restrict__ g, float* __restrict__ resid,
                                                              int n, int k, int32_t* __restrict__ idx,
@@ -847,9 +866,10 @@ __global__ __launch_bounds__(kSmallThreads) void k_topk_small(const float* __res
     for (int b = t; b < 2 * kHistBins; b += kSmallThreads) (&hist[0][0])[b] = 0u;
     __syncthreads();
     uint32_t* h = hist[pass == 0 ? (wv & 1) : 0];
-    for (int i = t; i < n; i += kSmallThreads) {
-      const uint32_t key = __float_as_uint(sv[i]) & 0x7fffffffu;
-      if ((key & pmask) == prefix) atomicAdd(&h[(key >> sh) & (nb - 1)], 1u);
+    for (int i0 = 0; i0 < n; i0 += kSmallThreads) {  // whole waves iterate together (ballots)
+      const int i = i0 + t;
+      const uint32_t key = i < n ? __float_as_uint(sv[i]) & 0x7fffffffu : 0u;
+      wave_hist_add(h, (key >> sh) & (nb - 1), i < n && (key & pmask) == prefix);
     }
     __syncthreads();
     // thread t owns bins hi = nb-1-2t and lo = nb-2-2t (t < nb/2); exclusive scan from the top

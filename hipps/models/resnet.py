@@ -55,7 +55,10 @@ _FUSED_DUAL = _FUSED_GRAD and _os.environ.get("HIPPS_FUSED_DUAL", "1") != "0"
 # apply pass + plain GEMM (tests), but the in-LDS transform sits between each tile's DMA and its
 # barrier and the compute-bound 3x3 GEMMs lose 15-47 % (forward and weight gradient) -- more
 # than the 32 apply passes cost (same box: 11070 off vs 10629 img/s on, profiles/r3b/bnpro/)
-_BN_PRO = _FUSED_DUAL and _os.environ.get("HIPPS_BN_PRO", "0") != "0"
+_BN_PRO = _FUSED_DUAL and _os.environ.get("HIPPS_BN_PRO", "0") == "1"
+# HIPPS_BN_PRO=2: only bn2 -> conv3 (the 1x1, memory-bound side) takes the prologue; bn1 is applied
+# by its own pass and conv2 (the compute-bound 3x3 GEMM that the in-LDS transform slows) stays plain
+_BN_PRO2 = _FUSED_DUAL and _os.environ.get("HIPPS_BN_PRO", "0") == "2"
 
 
 def _bn(c, relu=False):
@@ -102,6 +105,33 @@ class Bottleneck(nn.Module):
             return dual_bn_relu(self.bn3, x3, p3, ds[1], xd, pd)
         return self.bn3(x3, ds[1](xd, stats=pd), stats=p3)
 
+    def _forward_pro2(self, x, bng):
+        """bn2 + ReLU inside conv3 only: conv1 -> bn1 (apply pass) -> conv2 (statistics) ->
+        [bn2 + ReLU inside conv3] -> bn3 (+ residual / downsample BN) -> ReLU."""
+        ds = self.downsample
+        if ds is None:
+            tap = ResidualTap() if _FUSED_GRAD else None
+            y = conv_bn(self.conv1, self.bn1, x, fuse=_FUSED_CONV, tap=tap, bn_grad=bng)
+            xd = pd = None
+        else:
+            tap = None
+            y1, p1, xa = conv1x1_bn_input(self.conv1, x, alias=True, bn_grad=bng)
+            y = self.bn1(y1, stats=p1) if self.bn1._fast_ok(y1, None) else self.bn1(y1)
+            xd, pd = conv1x1_bn_input(ds[0], xa)
+        x2, p2 = conv2d_stats(self.conv2, y, fuse=_FUSED_WGRAD, bn_grad=bng)
+        if p2 is None or not bn_relu_conv_ok(self.bn2, self.conv3, x2):  # (MIOpen forward: no statistics)
+            y = self.bn2(x2, stats=p2) if p2 is not None and self.bn2._fast_ok(x2, None) else self.bn2(x2)
+            if ds is None:
+                return conv_bn(self.conv3, self.bn3, y, residual=x, fuse=_FUSED_CONV, res_tap=tap, bn_grad=bng)
+            x3, p3 = conv1x1_bn_input(self.conv3, y, bn_grad=bng)
+        else:
+            x3, p3 = bn_relu_conv(self.bn2, self.conv3, x2, p2)
+        if ds is None:
+            return self.bn3(x3, x, stats=p3, res_tap=tap) if self.bn3._fast_ok(x3, x) else self.bn3(x3, x)
+        if dual_bn_relu_ok(self.bn3, ds[1], x3, xd):
+            return dual_bn_relu(self.bn3, x3, p3, ds[1], xd, pd)
+        return self.bn3(x3, ds[1](xd, stats=pd), stats=p3)
+
     def forward(self, x):
         # Gradient of x = conv1's dgrad + the residual path's gradient.  Instead of autograd's add
         # (read 2, write 1 full-size tensors per block) conv1's dgrad epilogue sums them: the
@@ -115,6 +145,9 @@ class Bottleneck(nn.Module):
                 (ds is None or conv1x1_ok(ds[0], x)) and bn_relu_conv_ok(self.bn1, self.conv2, x) and
                 bn_relu_conv_ok(self.bn2, self.conv3, x)):
             return self._forward_pro(x, bng)
+        if (_BN_PRO2 and bng and self.training and conv1x1_ok(self.conv1, x) and conv1x1_ok(self.conv3, x) and
+                (ds is None or conv1x1_ok(ds[0], x))):
+            return self._forward_pro2(x, bng)
         if ds is None:
             tap = ResidualTap() if _FUSED_GRAD else None
             y = conv_bn(self.conv1, self.bn1, x, fuse=_FUSED_CONV, tap=tap, bn_grad=bng)

@@ -80,7 +80,7 @@ def test_gpu_fused_eval_apply():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("width,pro", [(16, False), (64, False), (64, True)])
+@pytest.mark.parametrize("width,pro", [(16, False), (64, False), (64, True), (64, 2)])
 def test_gpu_resnet_fused_vs_unfused_step(width, pro, monkeypatch):
     """One autocast step of a small ResNet: the fused-BN model's grads are no further from an fp32
     reference than the eager bf16 (MIOpen BN) model's grads are.  width 64 puts every conv on the
@@ -91,7 +91,8 @@ def test_gpu_resnet_fused_vs_unfused_step(width, pro, monkeypatch):
     import hipps.models.resnet as rn
     from hipps.models.resnet import ResNet, Bottleneck
 
-    monkeypatch.setattr(rn, "_BN_PRO", pro)  # bn1 / bn2 applied inside conv2 / conv3 (_BNReluConv)
+    monkeypatch.setattr(rn, "_BN_PRO", pro is True)  # bn1 / bn2 applied inside conv2 / conv3 (_BNReluConv)
+    monkeypatch.setattr(rn, "_BN_PRO2", pro == 2)  # bn2 inside conv3 only
     torch.manual_seed(3)
     base = ResNet(Bottleneck, [1, 1], num_classes=10, width=width, zero_init_residual=False).cuda()
     base = base.to(memory_format=torch.channels_last)

@@ -26,7 +26,7 @@ def main():
         if st < t0:
             end = en if end is None else max(end, en)
             continue
-        if end is not None and st - end >= a.min_us * 1e3 and n < 6:
+        if end is not None and st - end >= a.min_us * 1e3 and n < 10:
             n += 1
             h = by_corr.get(r["Correlation_Id"])
             lines.append(f"gap {(st - end) / 1e3:.1f} us before {r['Kernel_Name'][:80]}")
@@ -37,6 +37,32 @@ def main():
                 qs, qe = int(q["Start_Timestamp"]), int(q["End_Timestamp"])
                 if qe >= end - 100000 and qs <= st and qe - qs >= 20000:
                     lines.append(f"    host {q['Function'][:40]:40s} thread {q['Thread_Id']} {(qs - end) / 1e3:+9.1f} .. {(qe - end) / 1e3:+9.1f} us")
+            # every HIP call of every thread inside the gap: per thread, the calls (count, time in
+            # them) and the longest stretches with NO call (the thread ran Python / held or waited
+            # for the GIL)
+            per = {}
+            for q in hs:
+                qs, qe = int(q["Start_Timestamp"]), int(q["End_Timestamp"])
+                if qe >= end and qs <= st:
+                    per.setdefault(q["Thread_Id"], []).append((qs, qe, q["Function"]))
+            for tid, calls in sorted(per.items()):
+                calls.sort()
+                busy = sum(min(qe, st) - max(qs, end) for qs, qe, _ in calls) / 1e3
+                holes, prev = [], end
+                for qs, qe, fn in calls:
+                    if qs > prev:
+                        holes.append(((qs - prev) / 1e3, (prev - end) / 1e3, fn))
+                    prev = max(prev, qe)
+                if st > prev:
+                    holes.append(((st - prev) / 1e3, (prev - end) / 1e3, "<gap end>"))
+                holes.sort(reverse=True)
+                names = {}
+                for _, _, fn in calls:
+                    names[fn] = names.get(fn, 0) + 1
+                top = ", ".join(f"{k} x{v}" for k, v in sorted(names.items(), key=lambda kv: -kv[1])[:6])
+                lines.append(f"    thread {tid}: {len(calls)} HIP calls, {busy:.1f} us inside them ({top})")
+                for dur, at, fn in holes[:3]:
+                    lines.append(f"      no HIP call for {dur:7.1f} us from {at:+8.1f} us (next: {fn[:40]})")
         end = en if end is None else max(end, en)
     open(a.out, "w").write("\n".join(lines) + "\n")
     print("\n".join(lines[:80]))
