@@ -54,8 +54,8 @@ def parse():
                          "xGMI pull; the PS keeps the fp32 master, workers compute in bf16 anyway)")
     ap.add_argument("--momentum", type=float, default=0.9)
     ap.add_argument("--bucket-mb", type=float, default=None,
-                    help="bucket size (default: 16 with --granularity bucket, else 64)")
-    ap.add_argument("--granularity", default=None, choices=["model", "bucket"],
+                    help="bucket size in MB (default: the library's, PSConfig.bucket_mb)")
+    ap.add_argument("--granularity", default=None, choices=["model", "bucket", "auto"],
                     help="ps_async update/publication granularity (default: the library's, PSConfig.ps_granularity)")
     ap.add_argument("--lookahead", type=float, default=None,
                     help="ps_async look-ahead publish tau (default: the library's, PSConfig.stale_lookahead = 0: "
@@ -273,6 +273,7 @@ def main():
         tr.flush()
         trace = {k: round(v / a.steps, 4) for k, v in tr.totals.items()}
     nbuckets = len(opt.engine.plan.buckets)
+    gran_eff = getattr(opt.engine, "granularity", None)
     nparams = sum(p.numel() for p in model.parameters())
     opt.close()
     stats = {}
@@ -324,7 +325,7 @@ def main():
                 "algorithm": ("AsySG-InCon" + ("" if kw.get("stale_lookahead", 0) == 0 else
                                                " + look-ahead publish (delay compensation)"))
                 if mode == "ps_async" else mode,
-                "ps_granularity": kw.get("ps_granularity") if mode == "ps_async" else None,
+                "ps_granularity": gran_eff if mode == "ps_async" else None,
                 "stale_lookahead": kw.get("stale_lookahead") if mode == "ps_async" else None,
                 "bucket_mb": a.bucket_mb,
                 "python_gc": a.gc,

@@ -48,7 +48,8 @@ class PSConfig:
     # steps once M complete worker steps arrived) | 'bucket' (README.md:64-76, the reference PS
     # steps and broadcasts each parameter on its own: every bucket is updated and published as soon
     # as M messages for it arrived, workers adopt the newest version of each bucket -- reads may
-    # mix versions across buckets; ipc transport only)
+    # mix versions across buckets; ipc transport only) | 'auto' (bucket where it applies -- ipc
+    # transport, device codecs -- model otherwise)
     ps_granularity: str = "model"
     # async PS: push each bucket's message from its backward hook as soon as it is encoded
     # ('auto' = on for the ipc transport), instead of all messages at step(): the PS accumulates
@@ -169,8 +170,8 @@ class PSConfig:
             raise ValueError("transport must be 'torch' or 'rccl'")
         if self.push_early not in ("auto", "on", "off"):
             raise ValueError("push_early must be 'auto', 'on' or 'off'")
-        if self.ps_granularity not in ("model", "bucket"):
-            raise ValueError("ps_granularity must be 'model' or 'bucket'")
+        if self.ps_granularity not in ("model", "bucket", "auto"):
+            raise ValueError("ps_granularity must be 'model', 'bucket' or 'auto'")
         if self.adam_variant not in ("reference", "torch"):
             raise ValueError("adam_variant must be 'reference' or 'torch'")
 

@@ -347,7 +347,15 @@ class PSAsyncEngine(Engine):
         self.dedicated = bool(cfg.ps_dedicated) and W > 1
         self.M = cfg.accumulate if cfg.accumulate > 0 else (W - 1 if self.dedicated else W)
         self.emu = int(cfg.emulate_remote) if W == 1 else 0  # emulated remote-worker PS load
-        self.bucketwise = cfg.ps_granularity == "bucket"
+        # 'auto': per-bucket versions wherever they apply (ipc transport, bucket count within the
+        # control block's table, device codecs), whole-model versions otherwise
+        self.p2p = cfg.async_transport == "p2p" and W > 1
+        gran = cfg.ps_granularity
+        if gran == "auto":
+            gran = "bucket" if (not self.p2p and not self.is_object
+                                and len(self.plan.buckets) <= C.ControlBlock.MAX_BUCKETS) else "model"
+        self.granularity = gran
+        self.bucketwise = gran == "bucket"
         self.MAXSLOTS = C.ControlBlock.SLOTS  # stride of the per-slot version words
         self.NPUB = C.ControlBlock.NPUB
         self.timeout_us = int(min(TIMEOUT_US, cfg.comm_timeout_s * 1e6))
@@ -375,7 +383,6 @@ class PSAsyncEngine(Engine):
         # transport 'ipc': workers map the PS's mailbox (HIP IPC / POSIX shm) and copy one-sidedly;
         # 'p2p': the mailbox stays private to the PS and data moves by two-sided send/recv
         # (torch.distributed isend/irecv: RCCL pair communicators on GPU, gloo on CPU)
-        self.p2p = cfg.async_transport == "p2p" and W > 1
         if self.bucketwise and (self.p2p or self.nb > C.ControlBlock.MAX_BUCKETS):
             raise ValueError("ps_granularity='bucket' needs the ipc transport and at most "
                              f"{C.ControlBlock.MAX_BUCKETS} buckets")
@@ -1555,6 +1562,7 @@ class PSAsyncEngine(Engine):
     def transport_info(self) -> dict:
         return {"transport": "p2p" if self.p2p else "ipc", "doorbells": self.ctl.bell_mode, "pull": self.pull_mode,
                 "p2p_channels": (None if not self.p2p else "rccl-split" if self._gpg.native else "torch"),
+                "granularity": self.granularity,
                 "ps_dedicated": self.dedicated, "accumulate": self.M,
                 "npub": self.NPUB,
                 "mailbox_slots": self.SLOTS, "slot_bytes": self.slot_bytes}

@@ -326,3 +326,24 @@ def test_async_push_early_rejects_a_late_gradient():
     # the early messages already moved the worker's sequence, so the engine must not
     # accept another step (later messages would land on the wrong buckets of the PS)
     assert out[0]["err2"] is not None and "cannot continue" in out[0]["err2"]
+
+
+def _gran(rank, world, transport):
+    import hipps
+
+    m = _mlp()
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", bucket_mb=0.0005,
+                    ps_granularity="auto", async_transport=transport, max_delay=0)
+    info = dict(opt.engine.transport_info())
+    x, y = _data(rank, 0)
+    opt.zero_grad()
+    torch.nn.functional.cross_entropy(m(x), y).backward()
+    opt.step()
+    opt.close()
+    return info
+
+
+def test_async_granularity_auto():
+    """ps_granularity='auto': per-bucket versions on the ipc transport, whole-model on p2p."""
+    assert run_world(_gran, 2, "ipc")[0]["granularity"] == "bucket"
+    assert run_world(_gran, 2, "p2p")[0]["granularity"] == "model"
