@@ -49,8 +49,10 @@ class PSConfig:
     # steps and broadcasts each parameter on its own: every bucket is updated and published as soon
     # as M messages for it arrived, workers adopt the newest version of each bucket -- reads may
     # mix versions across buckets; ipc transport only) | 'auto' (bucket where it applies -- ipc
-    # transport, device codecs -- model otherwise)
-    ps_granularity: str = "model"
+    # transport, device codecs -- model otherwise; the default: on the headline config plain
+    # AsySG-InCon converges like local SGD with it and oscillates with whole-model versions,
+    # profiles/r4/traj_headline.json)
+    ps_granularity: str = "auto"
     # async PS: push each bucket's message from its backward hook as soon as it is encoded
     # ('auto' = on for the ipc transport), instead of all messages at step(): the PS accumulates
     # (and with ps_granularity='bucket' updates and publishes) the last layers' buckets while the
@@ -80,8 +82,9 @@ class PSConfig:
     # async PS mailbox: bucket messages in flight per worker (0 = auto: min(2*buckets, mailbox_mb))
     mailbox_slots: int = 0
     mailbox_mb: float = 4096.0
-    # bucket size for hook-driven encode overlap (also the async PS message granularity)
-    bucket_mb: float = 64.0
+    # bucket size for hook-driven encode overlap (also the async PS message / version granularity:
+    # ResNet-50 is 7 buckets at 16 MB)
+    bucket_mb: float = 16.0
     # scale the rank-summed gradient by 1/accumulate (reference sums: ps.py:176)
     average: bool = False
     # encode buckets from post-accumulate-grad hooks on a side stream during backward

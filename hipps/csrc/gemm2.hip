@@ -1292,10 +1292,14 @@ static int* wgrad_tickets(const at::Tensor& like, int64_t n) {
   return p;
 }
 
+// Opt-in (HIPPS_WGRAD_FUSED_REDUCE=1): bit-identical, 76 fewer launches per ResNet-50 step, but
+// measured 1.5 % slower in the step (same-box A/B 11554 / 11544 on vs 11762 / 11705 img/s off,
+// profiles/r4/ab_r4b.txt): the serial slab reads of each tile's last block lengthen the weight-
+// gradient kernels on the side stream more than the separate, chip-wide reduce costs there.
 static bool wgrad_fused_reduce() {
   static const bool on = [] {
     const char* e = std::getenv("HIPPS_WGRAD_FUSED_REDUCE");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }

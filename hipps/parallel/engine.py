@@ -81,6 +81,10 @@ class Engine:
         # views of the flat gradient buffer.
         self.grad_mode = "gather" if (self.cuda and cfg.grad_gather and self.supports_gather and
                                       not self.is_object) else "flat"
+        from collections import deque
+
+        self._held: deque = deque()  # (comm-stream event, [gradients its gathers read])
+        self._held_cur: list = []
         if self.grad_mode == "gather":
             self._build_gather_plan()
             store.set_grad_mode("gather")
@@ -89,6 +93,30 @@ class Engine:
     supports_gather = True
     GATHER_CHUNK = 8192
     GATHER_MAX = 256
+    HOLD_MAX = 3  # steps of gathered gradients kept alive at most before the host waits
+
+    def _release_held(self, force: bool = False):
+        """Drop the references to gradients whose gather has completed on the comm stream (their
+        memory then returns to the allocator with no pending stream use, so no event is needed)."""
+        held = self._held
+        while held:
+            ev = held[0][0]
+            if not ev.query():
+                if not (force or len(held) > self.HOLD_MAX):
+                    break
+                ev.synchronize()  # the host ran HOLD_MAX steps ahead of the comm stream
+            held.popleft()
+
+    def _hold_step(self):
+        """End of a step's encodes: the gradients gathered this step stay referenced until an
+        event on the comm stream after their gathers has completed."""
+        if not self._held_cur:
+            return
+        ev = torch.cuda.Event()
+        ev.record(self.comm_stream)
+        self._held.append((ev, self._held_cur))
+        self._held_cur = []
+        self._release_held()
 
     def _build_gather_plan(self):
         """Static per-bucket chunk tables: (tensor index, src offset, dst offset, length)."""
@@ -159,8 +187,11 @@ class Engine:
                 g = p.grad
                 if g is None or g.dtype != torch.float32 or not _is_dense(g):
                     g = self._zeros if g is None else g.float().contiguous()
-                else:
-                    g.record_stream(self.comm_stream)  # keep it alive until the gather ran
+                # keep it alive until the gather has run (released in _release_held): one event
+                # per step instead of record_stream's event per tensor at every free -- 161
+                # hipEventRecord + allocator event queries on the host at each zero_grad, ~2 ms
+                # of main-thread time at the step boundary (profiles/r4/stalls_r4b_gcdefault.txt)
+                self._held_cur.append(g)
                 srcs.append(g)
             C.gather_flat(srcs, table, dst, 1.0)
         return dense
@@ -237,6 +268,8 @@ class Engine:
         for bi in self.plan.ready_order:
             if not self._encoded[bi] or bi in self._late:
                 self.encode_bucket(bi)
+        if self.cuda:
+            self._hold_step()
         self._encoded = [False] * len(self._encoded)
         self._bucket_count = [0] * len(self._bucket_count)
         self._late.clear()
@@ -371,6 +404,8 @@ class Engine:
 
     def close(self):
         self.remove_hooks()
+        if self.cuda:
+            self._release_held(force=True)
         if self.watchdog is not None:
             self.watchdog.close()
         if self.rccl is not None:

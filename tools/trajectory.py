@@ -9,12 +9,12 @@ variant runs in its own process (tests/test_resnet_trajectory_gpu.py spawns both
 ``--runs`` trains several hipps configurations in one process from the same init and batch:
   local          mode='local'
   async_md<k>    mode='ps_async', max_delay=k (N=1: rank 0 is PS and worker)
-  async          mode='ps_async', max_delay=-1 (free-running AsySG-InCon: the reference's algorithm,
-                 whole-model versions)
+  async          mode='ps_async', max_delay=-1 (free-running AsySG-InCon, the reference's algorithm,
+                 with the library defaults: per-bucket versions, 16 MB buckets)
+  async_model    as async, whole-model versions (ps_granularity='model')
   async_la       as async, with the look-ahead publish (stale_lookahead=-1, delay compensation)
-  async_bucket   as async, per-bucket updates and publication (ps_granularity='bucket',
-                 bucket_mb=16): the reference's per-parameter PS granularity (README.md:64-76)
-  async_bucket_la  async_bucket with the look-ahead publish
+  async_model_la async_model with the look-ahead publish
+  async_bucket   as async with per-bucket versions and 16 MB buckets spelled out
   async_slr      as async, with staleness-aware gradient scaling
   async_prefetch as async, with the host-chosen prefetch/direct pull instead of the GPU pull
   async_mc       as async, with delay-compensated momentum (``stale_momentum='comp'``)
@@ -94,11 +94,12 @@ def _base_cfg(run):
         return {"mode": "ps_async", "max_delay": -1}
     if run == "async_la":
         return {"mode": "ps_async", "max_delay": -1, "stale_lookahead": -1.0}
+    if run == "async_model":
+        return {"mode": "ps_async", "max_delay": -1, "ps_granularity": "model"}
+    if run == "async_model_la":
+        return {"mode": "ps_async", "max_delay": -1, "ps_granularity": "model", "stale_lookahead": -1.0}
     if run == "async_bucket":
         return {"mode": "ps_async", "max_delay": -1, "ps_granularity": "bucket", "bucket_mb": 16.0}
-    if run == "async_bucket_la":
-        return {"mode": "ps_async", "max_delay": -1, "ps_granularity": "bucket", "bucket_mb": 16.0,
-                "stale_lookahead": -1.0}
     if run == "async_slr":
         return {"mode": "ps_async", "max_delay": -1, "staleness_lr": True}
     if run == "async_prefetch":
