@@ -69,7 +69,6 @@ def test_async_ps_across_devices(pull, codec, transport):
         assert o["transport"] == transport
 
 
-@pytest.mark.parametrize("codec", ["fp32", "int8", "topk:0.05"])
 def test_async_p2p_on_native_rccl_split_channels():
     """the p2p transport's gradient and parameter channels as two communicators
     split from hipps' own RCCL communicator (ncclCommSplit) instead of torch process groups."""

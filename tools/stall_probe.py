@@ -37,6 +37,15 @@ def main():
                 qs, qe = int(q["Start_Timestamp"]), int(q["End_Timestamp"])
                 if qe >= end - 100000 and qs <= st and qe - qs >= 20000:
                     lines.append(f"    host {q['Function'][:40]:40s} thread {q['Thread_Id']} {(qs - end) / 1e3:+9.1f} .. {(qe - end) / 1e3:+9.1f} us")
+            # what every thread did last before the gap began (which thread launched the work the
+            # GPU just finished, and how long before)
+            lastb = {}
+            for q in hs:
+                qs = int(q["Start_Timestamp"])
+                if end - 20_000_000 <= qs <= end:
+                    lastb[q["Thread_Id"]] = q
+            for tid, q in sorted(lastb.items()):
+                lines.append(f"    before: thread {tid} last {q['Function'][:36]} at {(int(q['Start_Timestamp']) - end) / 1e3:+9.1f} us")
             # every HIP call of every thread inside the gap: per thread, the calls (count, time in
             # them) and the longest stretches with NO call (the thread ran Python / held or waited
             # for the GIL)
