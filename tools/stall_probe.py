@@ -18,7 +18,7 @@ def main():
     ks = sorted(csv.DictReader(open(a.ktrace)), key=lambda r: int(r["Start_Timestamp"]))
     hs = sorted(csv.DictReader(open(a.htrace)), key=lambda r: int(r["Start_Timestamp"]))
     by_corr = {r["Correlation_Id"]: r for r in hs}
-    marks = [int(r["Start_Timestamp"]) for r in ks if "k_sgd" in r["Kernel_Name"]]
+    marks = [int(r["Start_Timestamp"]) for r in ks if "k_pull_select" in r["Kernel_Name"]]
     t0 = marks[a.skip] if len(marks) > a.skip else int(ks[0]["Start_Timestamp"])
     lines, end, n = [], None, 0
     for r in ks:

@@ -1,7 +1,7 @@
 """Summarize a rocprofv3 kernel trace to steady-state per-step costs.
 
-Steps are delimited by a marker kernel that runs once per optimizer step (default: hipps
-k_sgd); the first `--skip` steps (warmup incl. MIOpen find) are dropped.
+Steps are delimited by a marker kernel that runs once per optimizer step (default: the async PS
+pull-select kernel, once per worker step; k_sgd runs once per bucket update); the first `--skip` steps (warmup incl. MIOpen find) are dropped.
     python tools/steady_profile.py trace.csv out.txt [--marker k_sgd] [--skip 5]
 """
 import argparse
@@ -13,7 +13,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("out")
-    ap.add_argument("--marker", default="k_sgd")
+    ap.add_argument("--marker", default="k_pull_select")
     ap.add_argument("--skip", type=int, default=5)
     ap.add_argument("--title", default="")
     a = ap.parse_args()
