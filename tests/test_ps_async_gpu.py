@@ -314,3 +314,29 @@ def test_async_slot_reuse_stress_bitwise(codec):
     for r in range(3):
         for x, y in zip(c[r]["params"], d[r]["params"]):
             torch.testing.assert_close(x, y, rtol=0, atol=0)
+
+
+def _budget_refused(rank, world):
+    import hipps
+
+    torch.cuda.set_device(0)
+    m = _mlp().cuda()
+    real = torch.cuda.mem_get_info
+    torch.cuda.mem_get_info = lambda dev=None: (1 << 20, real(dev)[1])  # pretend 1 MiB is free
+    try:
+        hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async")
+    except MemoryError as e:
+        return str(e)
+    finally:
+        torch.cuda.mem_get_info = real
+    return None
+
+
+def test_gpu_async_memory_budget_refuses_before_allocating():
+    """when the PS's state does not fit in the free HBM the engine raises a
+    MemoryError naming every term before it allocates anything (tools/ps_budget.py computes the
+    same budget offline: Llama-3-8B at W=8 does not fit co-located)."""
+    msg = run_world(_budget_refused, 1)[0]
+    assert msg is not None
+    for term in ("mailbox", "publish", "master", "accumulator", "optimizer", "ps_dedicated"):
+        assert term in msg, msg
