@@ -39,6 +39,7 @@
 #include <torch/extension.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 
@@ -66,7 +67,8 @@ struct SelState {        // lives at the head of the workspace
   uint32_t spec_lo;      // P1's list bound
   uint32_t prev_T;       // final key of the previous call (persists in the workspace)
   uint32_t redo;         // the list missed part of the k-th key's range: repair + recount
-  uint32_t pad[23];
+  uint32_t ticket[4];    // arrival counters of the in-launch picks (zero between launches)
+  uint32_t pad[19];
   uint32_t pool_used[kPoolShards * 32];
   // kHistCopies histograms: workgroup b merges into copy b % kHistCopies, so a bin's global
   // atomics come from 1/8 of the workgroups (depth ~110 instead of ~900 on a 25 M bucket); the
@@ -75,6 +77,10 @@ struct SelState {        // lives at the head of the workspace
 };
 
 __device__ __forceinline__ uint32_t absbits(float x) { return __float_as_uint(x) & 0x7fffffffu; }
+
+// in-launch digit pick (defined with k_topk_pick below)
+__device__ __forceinline__ void pick_body(int lo, int nbits, SelState* __restrict__ st, int flags, uint32_t* wtot);
+__device__ __forceinline__ bool last_arriver(uint32_t* ticket, uint32_t* flag);
 
 
 // mode: 0 = top-k, 1 = threshold (prefix = T, no ties)
@@ -269,7 +275,8 @@ __device__ __forceinline__ uint32_t collect_chunk(const float (&x)[kCompactPer],
 // 2: top-k repair (bound = bin B's lower edge; nothing to do when P1's bound covered bin B).
 template <bool HIST>
 __global__ __launch_bounds__(kBlock) void k_collect(const float* __restrict__ src, float* __restrict__ fold_r,
-                                                    int64_t n, SelState* __restrict__ st, Regions R, int mode) {
+                                                    int64_t n, SelState* __restrict__ st, Regions R, int mode,
+                                                    int fold_pick = 0) {
   __shared__ uint32_t h[HIST ? 4 : 1][HIST ? kHistBins : 1];
   __shared__ uint32_t wsum[4][4], sbase;
   if (mode == 2 && !st->redo) return;  // grid-uniform
@@ -308,6 +315,8 @@ __global__ __launch_bounds__(kBlock) void k_collect(const float* __restrict__ sr
       const uint32_t c = h[0][b] + h[1][b] + h[2][b] + h[3][b];
       if (c) atomicAdd(&st->hist[blockIdx.x % kHistCopies][b], c);
     }
+    if (fold_pick && last_arriver(&st->ticket[0], &h[0][0]))  // (h is free after the merge)
+      pick_body(20, 11, st, 0, &h[0][4]);
   }
 }
 
@@ -406,8 +415,7 @@ struct FlatList {
 // so that holds iff their count >= remaining -- and otherwise raises redo (repair pass, fresh
 // pool) without descending; kPickRetry runs only after such a redo.
 constexpr int kPickFinal = 1, kPickCheck = 2, kPickRetry = 4;
-__global__ __launch_bounds__(kBlock) void k_topk_pick(int lo, int nbits, SelState* __restrict__ st, int flags) {
-  __shared__ uint32_t wtot[4];
+__device__ __forceinline__ void pick_body(int lo, int nbits, SelState* __restrict__ st, int flags, uint32_t* wtot) {
   if ((flags & kPickRetry) && !st->redo) return;
   const int nb = 1 << nbits;
   const int per = nb / kBlock;  // 8 or 2
@@ -468,9 +476,39 @@ __global__ __launch_bounds__(kBlock) void k_topk_pick(int lo, int nbits, SelStat
   }
 }
 
+__global__ __launch_bounds__(kBlock) void k_topk_pick(int lo, int nbits, SelState* __restrict__ st, int flags) {
+  __shared__ uint32_t wtot[4];
+  pick_body(lo, nbits, st, flags, wtot);
+}
+
+// The pick of a digit inside the launch that built its histogram: every workgroup merges its
+// histogram with global atomics, drains, and one lane releases (agent scope) and takes an arrival
+// ticket; the workgroup that arrives last acquires and runs the pick (cdna_hip_programming.md
+// 'In-launch split-K reduction': correct for any placement over XCDs).  Saves one dependent
+// single-workgroup launch per digit.  ``flag`` is a word of the caller's LDS.
+__device__ __forceinline__ bool last_arriver(uint32_t* ticket, uint32_t* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t last = old == gridDim.x - 1 ? 1u : 0u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0u;
+}
+
 // P3/P4: histogram of the listed keys of the selected bin; full pass over the bucket if the pool ran out
 __global__ __launch_bounds__(kBlock) void k_hist_list(const float* __restrict__ src, int64_t n, int lo, int nbits,
-                                                      SelState* __restrict__ st, Regions R, int nreg, int retry) {
+                                                      SelState* __restrict__ st, Regions R, int nreg, int retry,
+                                                      int pick_flags = -1, int ticket = 1) {
   __shared__ uint32_t h[kHistBins];
   if (retry && !st->redo) return;
   const int nb = 1 << nbits;
@@ -503,6 +541,10 @@ __global__ __launch_bounds__(kBlock) void k_hist_list(const float* __restrict__ 
   __syncthreads();
   for (int b = threadIdx.x; b < nb; b += blockDim.x)
     if (h[b]) atomicAdd(&st->hist[blockIdx.x % kHistCopies][b], h[b]);
+  if (pick_flags >= 0) {
+    __syncthreads();  // h is reused for the arrival flag and the pick's wave totals
+    if (last_arriver(&st->ticket[ticket], &h[0])) pick_body(lo, nbits, st, pick_flags, &h[4]);
+  }
 }
 
 // P5a (top-k): per region, the counts of keys > T and == T, from its list (the full-mode twin
@@ -965,19 +1007,31 @@ void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::T
   hipLaunchKernelGGL(k_sel_init, 1, kBlock, 0, stream, w.st, 0u, 0u, (uint32_t)k, (uint32_t)w.g.capw,
                      (uint32_t)(w.g.pool / kPoolShards), 1);
   // P1: fold + top-digit histogram + speculative ordered list (the only full pass)
-  hipLaunchKernelGGL(k_collect<true>, nreg, kBlock, 0, stream, g.data_ptr<float>(), rp, n, w.st, w.R, 0);
-  hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 20, 11, w.st, 0);
+  static const bool fold = [] {  // picks inside the histogram launches (HIPPS_TOPK_FOLD=0: separate)
+    const char* e = std::getenv("HIPPS_TOPK_FOLD");
+    return !(e && e[0] == '0');
+  }();
   const float* src = rp ? rp : g.data_ptr<float>();
-  // P3 over the listed keys of bin B; its pick checks that the list reaches the remaining-th key
-  hipLaunchKernelGGL(k_hist_list, nreg, kBlock, 0, stream, src, n, 9, 11, w.st, w.R, nreg, 0);
-  hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 9, 11, w.st, kPickCheck);
-  // only after a miss (first call, shrinking gradients): re-list from bin B's edge, P3 again
-  hipLaunchKernelGGL(k_collect<false>, nreg, kBlock, 0, stream, src, (float*)nullptr, n, w.st, w.R, 2);
-  hipLaunchKernelGGL(k_hist_list, nreg, kBlock, 0, stream, src, n, 9, 11, w.st, w.R, nreg, 1);
-  hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 9, 11, w.st, kPickRetry);
-  // P4
-  hipLaunchKernelGGL(k_hist_list, nreg, kBlock, 0, stream, src, n, 0, 9, w.st, w.R, nreg, 0);
-  hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 0, 9, w.st, kPickFinal);
+  if (fold) {
+    hipLaunchKernelGGL(k_collect<true>, nreg, kBlock, 0, stream, g.data_ptr<float>(), rp, n, w.st, w.R, 0, 1);
+    // P3 over the listed keys of bin B; its pick checks that the list reaches the remaining-th key
+    hipLaunchKernelGGL(k_hist_list, nreg, kBlock, 0, stream, src, n, 9, 11, w.st, w.R, nreg, 0, kPickCheck, 1);
+    // only after a miss (first call, shrinking gradients): re-list from bin B's edge, P3 again
+    hipLaunchKernelGGL(k_collect<false>, nreg, kBlock, 0, stream, src, (float*)nullptr, n, w.st, w.R, 2, 0);
+    hipLaunchKernelGGL(k_hist_list, nreg, kBlock, 0, stream, src, n, 9, 11, w.st, w.R, nreg, 1, kPickRetry, 2);
+    // P4
+    hipLaunchKernelGGL(k_hist_list, nreg, kBlock, 0, stream, src, n, 0, 9, w.st, w.R, nreg, 0, kPickFinal, 3);
+  } else {
+    hipLaunchKernelGGL(k_collect<true>, nreg, kBlock, 0, stream, g.data_ptr<float>(), rp, n, w.st, w.R, 0, 0);
+    hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 20, 11, w.st, 0);
+    hipLaunchKernelGGL(k_hist_list, nreg, kBlock, 0, stream, src, n, 9, 11, w.st, w.R, nreg, 0, -1, 1);
+    hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 9, 11, w.st, kPickCheck);
+    hipLaunchKernelGGL(k_collect<false>, nreg, kBlock, 0, stream, src, (float*)nullptr, n, w.st, w.R, 2, 0);
+    hipLaunchKernelGGL(k_hist_list, nreg, kBlock, 0, stream, src, n, 9, 11, w.st, w.R, nreg, 1, -1, 2);
+    hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 9, 11, w.st, kPickRetry);
+    hipLaunchKernelGGL(k_hist_list, nreg, kBlock, 0, stream, src, n, 0, 9, w.st, w.R, nreg, 0, -1, 3);
+    hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 0, 9, w.st, kPickFinal);
+  }
   // P5: region counts, scan, ordered write
   hipLaunchKernelGGL(k_count_list, nreg, kBlock, 0, stream, w.st, w.R);
   hipLaunchKernelGGL(k_count_full, nreg, kBlock, 0, stream, src, n, w.st, w.R);
@@ -1030,7 +1084,7 @@ void thresh_encode(at::Tensor g, c10::optional<at::Tensor> resid, double tau, at
   TORCH_CHECK(w.g.cpw <= kMaxCpw, "bucket too large for the region geometry");
   hipLaunchKernelGGL(k_sel_init, 1, kBlock, 0, stream, w.st, tbits, 0xffffffffu, 0u, (uint32_t)w.g.capw,
                      (uint32_t)(w.g.pool / kPoolShards), 0);
-  hipLaunchKernelGGL(k_collect<false>, nreg, kBlock, 0, stream, g.data_ptr<float>(), rp, n, w.st, w.R, 1);
+  hipLaunchKernelGGL(k_collect<false>, nreg, kBlock, 0, stream, g.data_ptr<float>(), rp, n, w.st, w.R, 1, 0);
   const float* src = rp ? rp : g.data_ptr<float>();
   if (val.scalar_type() == at::kFloat)
     launch_scan_write<float>(stream, src, rp, n, w, idx.data_ptr<int32_t>(), val.data_ptr<float>(), (uint32_t)cap,
