@@ -24,4 +24,5 @@ for r in 1 2; do
   ab default_r$r || exit 1
   ab model64_r$r --granularity model --bucket-mb 64 || exit 1
   ab slots32_r$r --mailbox-slots 32 || exit 1
+  ab local_r$r --mode local || exit 1
 done
