@@ -33,6 +33,7 @@ import torch.nn.functional as F  # noqa: E402
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 METRIC = "samples/sec (node) ResNet-50 async PS at 1/2/4/8 MI355X; grad bytes/step"
+TIMED_HOOKS: list = []  # callables(bool): True right before the timed steps, False right after (tools/)
 TRANSFORMERS = ("bert-base", "bert-tiny", "llama3-8b", "llama3-1b", "llama-tiny")
 
 
@@ -231,12 +232,16 @@ def main():
     if host_t is not None:
         host_t[:] = [0.0] * 7
         ms0 = torch.cuda.memory_stats(dev)
+    for hook in TIMED_HOOKS:
+        hook(True)
     t0 = time.perf_counter()
     last = None
     for _ in range(a.steps):
         loss, last = step()
         if loss is not None:
             losses.append(loss.detach())
+    for hook in TIMED_HOOKS:
+        hook(False)
     torch.cuda.synchronize()
     hdist.barrier(world)
     t1 = time.perf_counter()

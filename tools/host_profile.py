@@ -60,32 +60,26 @@ def main():
         out = args[i + 1]
         del args[i:i + 2]
     import bench
-    from hipps.parallel import dist as hdist
 
     sys.argv = ["bench.py"] + args
     prof = cProfile.Profile()
     smp = Sampler()
     smp.start()
-    orig_barrier = hdist.barrier
-    calls = [0]
 
-    def barrier(world):  # bench: barrier -> timed steps -> barrier
-        r = orig_barrier(world)
-        calls[0] += 1
-        if calls[0] == 1:
-            smp.on = True
+    def timed(on: bool):  # bench.TIMED_HOOKS: around the timed steps
+        smp.on = on
+        if on:
             prof.enable()
-        elif calls[0] == 2:
+        else:
             prof.disable()
-            smp.on = False
-        return r
 
-    hdist.barrier = barrier
+    bench.TIMED_HOOKS.append(timed)
     try:
         bench.main()
     finally:
-        hdist.barrier = orig_barrier
+        smp.on = False
         smp.stop = True
+        smp.join(timeout=2)
     lines = []
     for tn, n in smp.n.most_common():
         lines.append(f"== thread {tn}: {n} samples")
@@ -99,7 +93,12 @@ def main():
     if out:
         open(out, "w").write(txt)
     print(txt[:6000])
+    sys.stdout.flush()
+    sys.stderr.flush()
 
 
 if __name__ == "__main__":
     main()
+    # skip interpreter teardown: a sampled run once ended in std::terminate there after all output
+    # was written (torch's atexit handlers racing the sampler's frame walks)
+    os._exit(0)
