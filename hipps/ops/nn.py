@@ -405,6 +405,7 @@ class _BNReluConv(torch.autograd.Function):
         if w.dim() == 4 and w.shape[2] > 1:
             w = w.contiguous(memory_format=torch.channels_last)
         ctx.wdtype = w_master.dtype
+        ctx.wparam = w_master
         ctx.set_materialize_grads(False)
         ctx.wt = _TSHADOWS.get(w_master.data_ptr()) if w_master.dtype == torch.float32 else None
         n, c, h, wd = x.shape
@@ -422,11 +423,24 @@ class _BNReluConv(torch.autograd.Function):
     def backward(ctx, dy, _dpart):
         x, w, bn_w, mean, invstd, scale, shift = ctx.saved_tensors
         if dy is None:
+            ctx.wparam = None
             return (None,) * 11
         s, p = ctx.geom
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         n, c, h, wd = x.shape
         cout, k = w.shape[0], w.shape[2]
+        dw = None
+        if ctx.needs_input_grad[8]:
+            # the weight gradient first, on the weight-gradient side stream (as _Conv1x1 /
+            # _ConvKxK), beside the input-gradient / BN-backward chain below
+            def wg():
+                d = torch.empty(w.shape, dtype=torch.float32, device=w.device,
+                                memory_format=torch.channels_last if k > 1 else torch.contiguous_format)
+                _conv_wgrad_pro(dy, x, d, k, k, s, p, scale, shift)
+                return d if ctx.wdtype == torch.float32 else d.to(ctx.wdtype)
+
+            dw = _on_wgrad_stream(ctx.wparam, (dy, x, scale, shift), wg)
+        ctx.wparam = None
         bg = BNGradTap(x, None, mean, invstd, scale, shift)
         # gradient of the (never materialised) BN output, with that BN's backward reduction
         if k == 1:
@@ -448,13 +462,6 @@ class _BNReluConv(torch.autograd.Function):
                                           None, dgw, dgb, c, None)
         else:
             native().bn_backward(dbn, x, None, MASK_X, bn_w, mean, invstd, scale, shift, dx, None, dgw, dgb, c, None)
-        dw = None
-        if ctx.needs_input_grad[8]:
-            dw = torch.empty(w.shape, dtype=torch.float32, device=w.device,
-                             memory_format=torch.channels_last if k > 1 else torch.contiguous_format)
-            _conv_wgrad_pro(dy, x, dw, k, k, s, p, scale, shift)
-            if ctx.wdtype != torch.float32:
-                dw = dw.to(ctx.wdtype)
         return dx, None, dgw, dgb, None, None, None, None, dw, None, None
 
 

@@ -26,3 +26,9 @@ for r in 1 2; do
   ab slots32_r$r --mailbox-slots 32 || exit 1
   ab local_r$r --mode local || exit 1
 done
+for r in 1 2; do
+  for pv in 2 1; do
+    timeout -k 10 300 env HIPPS_BN_PRO=$pv python bench.py --steps 30 --warmup 5 --out $O/ab_bnpro${pv}_r$r.json > $O/ab_bnpro${pv}_r$r.log 2>&1 || { tail -20 $O/ab_bnpro${pv}_r$r.log; exit 1; }
+    python -c "import json;d=json.load(open('$O/ab_bnpro${pv}_r$r.json'));print('bnpro$pv r$r', d['value'], d['ms_per_step'], d['final_loss'], d['ps_staleness_mean'])"
+  done
+done
