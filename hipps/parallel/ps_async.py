@@ -522,6 +522,12 @@ class PSAsyncEngine(Engine):
                 self._emu_sink = torch.empty(self.emu, dtype=self.pub_dtype, device=store.device)
             self.core.backend = self
             self._pend, self._pend_acks = [], []
+            # M = 1 with per-bucket versions and a dense codec (every N=1 run): each message is
+            # applied by its own update, read straight from the slot (HIPPS_PS_DIRECT=0: off)
+            self._direct: dict = {}
+            self._direct_ok = (self.cuda and self.bucketwise and self.M == 1 and not self.emu
+                               and bool(getattr(codec, "fusable", False)) and not self.is_object
+                               and os.environ.get("HIPPS_PS_DIRECT", "1") != "0")
             self._pres_full = False
             self._pres_part = None
             self._publish_initial()
@@ -831,6 +837,13 @@ class PSAsyncEngine(Engine):
     def accumulate(self, i: int, slot: int, bi: int, seq: int, scale: float):
         if self.plan.guarded:
             self._verify_slot(i, slot, bi, seq)
+        if self._direct_ok and not self._remote(i):
+            # M = 1, per-bucket versions, dense codec: the update reads the message itself (no
+            # fp32 accumulator round trip); its slot is acked after that update (see ack)
+            self._direct[bi] = (self._bucket_msg(bi, self.slot_buf(i, slot))["x"], scale, (i, seq))
+            if self._lat is not None and i == 0:
+                self._lat.note(bi, seq)
+            return
         self._pend.append((bi, scale, self._bucket_msg(bi, self.slot_buf(i, slot)), self._remote(i)))
         if self._lat is not None and i == 0:
             self._lat.note(bi, seq)
@@ -838,6 +851,9 @@ class PSAsyncEngine(Engine):
             self._pend.append((bi, scale, None, False))
 
     def ack(self, i: int, seq: int):
+        for d in self._direct.values():
+            if d[2] == (i, seq):  # rung by update_bucket, after the update kernel that reads the slot
+                return
         self._pend_acks.append((self.C.F_ACK_SEQ, i, seq))
 
     def flush(self):
@@ -912,10 +928,19 @@ class PSAsyncEngine(Engine):
             self._gsteps = top
         tau = self.lookahead_tau()
         self._stats["lookahead_tau_x1000"] = int(round(tau * 1000))
+        direct = self._direct.pop(bi, None)
         with self.tracer.phase("ps_update", self.ps_stream):
-            self.opt._update_range([self.acc], self.master, b.lo, b.hi, gscale, True, self.pub_buf(k), mask, 0,
-                                   lookahead=tau)
+            if direct is not None:  # straight from the mailbox slot (M = 1)
+                msg, scale, (wi, ws) = direct
+                self.opt._update_range([msg], self.master, b.lo, b.hi, gscale * scale, False, self.pub_buf(k), mask,
+                                       b.lo, lookahead=tau)
+                self._stats["direct_updates"] = self._stats.get("direct_updates", 0) + 1
+            else:
+                self.opt._update_range([self.acc], self.master, b.lo, b.hi, gscale, True, self.pub_buf(k), mask, 0,
+                                       lookahead=tau)
         words = [(C.F_BBUF_VER, idx, v), (C.F_BPUB_VER, bi, v)]
+        if direct is not None:
+            words.insert(0, (C.F_ACK_SEQ, wi, ws))  # the slot is free once the update has read it
         if gver is not None:
             words.append((C.F_PUB_VER, 0, gver))
         words += [(C.F_INCL_SEQ, i, s) for i, s in incl.items()]

@@ -13,13 +13,13 @@ from test_dist_cpu import _data, _mlp
 pytestmark = pytest.mark.gpu
 
 
-def _gpu_async(rank, world, steps, codec, accumulate, max_delay):
+def _gpu_async(rank, world, steps, codec, accumulate, max_delay, granularity="auto"):
     import hipps
 
     torch.cuda.set_device(0)
     m = _mlp().cuda()
     opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", code=codec,
-                    accumulate=accumulate, max_delay=max_delay)
+                    accumulate=accumulate, max_delay=max_delay, ps_granularity=granularity)
     init = [p.detach().clone() for p in m.parameters()]
     losses = []
     for s in range(steps):
@@ -202,8 +202,10 @@ def test_gpu_bucket_granularity_md0_equals_model_granularity():
     """Per-bucket device pulls (pull.hip k_pull_*_b) with max_delay=0 reproduce the whole-model
     update sequence bit for bit (single rank, so both equal local SGD)."""
     a = run_world(_gpu_bucketwise, 1, 5, 0, "device")
-    b = run_world(_gpu_async, 1, 5, "fp32", 1, 0)
+    b = run_world(_gpu_async, 1, 5, "fp32", 1, 0, "model")
     assert a[0]["nb"] >= 3
+    # M = 1: every bucket update read its message straight from the mailbox slot (no accumulator)
+    assert a[0]["stats"].get("direct_updates", 0) == 5 * a[0]["nb"]
     for x, y in zip(a[0]["params"], b[0]["params"]):
         torch.testing.assert_close(x, y, rtol=0, atol=0)
 
