@@ -12,3 +12,5 @@ for r in 1 2; do
     python -c "import json;d=json.load(open('$O/ab_direct${v}_r$r.json'));print('direct$v r$r', d['value'], d['ms_per_step'], d['final_loss'], d['ps'].get('direct_updates'))"
   done
 done
+STALL_OUT=$O/stall bash tools/gpu_stall.sh > /dev/null || exit 1
+grep -A1 "host lead" $O/stall/stalls.txt

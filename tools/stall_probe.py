@@ -73,6 +73,26 @@ def main():
                 for dur, at, fn in holes[:3]:
                     lines.append(f"      no HIP call for {dur:7.1f} us from {at:+8.1f} us (next: {fn[:40]})")
         end = en if end is None else max(end, en)
+    # host lead: for every kernel, GPU start minus the end of its launch call on the host -- how
+    # far ahead of the GPU the launching thread was.  Small values for most kernels mean the host
+    # (not the GPU) sets the pace; report percentiles per phase of the step
+    leads = []
+    for r in ks:
+        st = int(r["Start_Timestamp"])
+        if st < t0:
+            continue
+        h = by_corr.get(r["Correlation_Id"])
+        if h is None:
+            continue
+        leads.append(((st - int(h["End_Timestamp"])) / 1e3, r["Kernel_Name"][:60]))
+    if leads:
+        v = sorted(x for x, _ in leads)
+        pct = lambda q: v[min(len(v) - 1, int(q * len(v)))]  # noqa: E731
+        lines.append(f"host lead (GPU start - launch return, us) over {len(v)} kernels: p5 {pct(0.05):.0f} "
+                     f"p25 {pct(0.25):.0f} p50 {pct(0.5):.0f} p75 {pct(0.75):.0f} p95 {pct(0.95):.0f}")
+        firsts = [x for x, nm in leads if "bfloat16_copy" in nm]
+        if firsts:
+            lines.append("host lead at the input casts (step starts), us: " + " ".join(f"{x:.0f}" for x in firsts[:20]))
     open(a.out, "w").write("\n".join(lines) + "\n")
     print("\n".join(lines[:80]))
 
