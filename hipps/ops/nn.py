@@ -76,6 +76,17 @@ def _same_layout(a, b):
 
 def _join_wgrad(idx):
     torch.cuda.current_stream(idx).wait_stream(_WG_STREAMS[idx])
+    _WG_UNJOINED.discard(idx)
+
+
+_WG_UNJOINED: set = set()  # devices whose side stream took work after the last backward's join
+
+
+def wgrad_join_pending(device) -> bool:
+    """True if the weight-gradient side stream of ``device`` may hold work that no backward's final
+    callback has joined into the caller's stream yet."""
+    idx = device.index if isinstance(device, torch.device) else device
+    return idx in _WG_UNJOINED
 
 
 def _on_wgrad_stream(param, tensors, fn):
@@ -91,16 +102,19 @@ def _on_wgrad_stream(param, tensors, fn):
         side = _WG_STREAMS[idx] = torch.cuda.Stream(device=dev)
     cur = torch.cuda.current_stream(dev)
     side.wait_stream(cur)
+    _WG_UNJOINED.add(idx)
     with torch.cuda.stream(side):
         out = fn()
     for t in tensors:
         t.record_stream(side)
     if out.dtype != param.dtype or not _same_layout(out, param):
         cur.wait_stream(side)  # autograd would copy dw on this stream
+        _WG_UNJOINED.discard(idx)
     else:
         task = torch._C._current_graph_task_id()
         if task < 0:  # not inside an autograd backward pass
             cur.wait_stream(side)
+            _WG_UNJOINED.discard(idx)
         elif _WG_JOINED.get(idx) != task:
             torch.autograd.Variable._execution_engine.queue_callback(lambda: _join_wgrad(idx))
             _WG_JOINED[idx] = task

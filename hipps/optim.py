@@ -232,11 +232,14 @@ class MPI_PS(torch.optim.Optimizer):
         self.steps += 1
         t0 = time.perf_counter()
         if self.store.device.type == "cuda":
-            from .ops.nn import wgrad_stream
+            from .ops import nn as hnn
 
-            wgs = wgrad_stream(self.store.device)
-            if wgs is not None:  # gradients computed on the weight-gradient side stream
-                torch.cuda.current_stream(self.store.device).wait_stream(wgs)
+            # gradients computed on the weight-gradient side stream: every backward already ends by
+            # joining it into the caller's stream (an autograd final callback, ops.nn._join_wgrad),
+            # so only a side-stream use outside a backward pass needs the join here (one event
+            # record less on the host at every step boundary)
+            if hnn.wgrad_stream(self.store.device) is not None and hnn.wgrad_join_pending(self.store.device):
+                torch.cuda.current_stream(self.store.device).wait_stream(hnn.wgrad_stream(self.store.device))
         data = self.engine.step()
         self._refresh_shadow()
         now = time.perf_counter()

@@ -116,7 +116,10 @@ class Engine:
         ev.record(self.comm_stream)
         self._held.append((ev, self._held_cur))
         self._held_cur = []
-        self._release_held()
+        if len(self._held) > self.HOLD_MAX:
+            self._release_held()
+        # (otherwise the frees -- ~2 us per gradient tensor -- happen at the next step's first
+        # bucket gather, on the autograd thread that has slack there, not at the step boundary)
 
     def _build_gather_plan(self):
         """Static per-bucket chunk tables: (tensor index, src offset, dst offset, length)."""
@@ -180,6 +183,8 @@ class Engine:
         dense = self.codec.fusable and not to_flat  # guards sit after the layout, not inside
         dst = views["x"] if dense else self.store.grad[b.lo:b.hi]
         C = native()
+        if self._held and not self._held_cur:  # the step's first gather: drop finished holds
+            self._release_held()
         for gids, table in self._gplan[bi]:
             srcs = []
             for si in gids:

@@ -1191,7 +1191,8 @@ class PSAsyncEngine(Engine):
         self.ctl.heartbeat(self.rank)
         t = time.perf_counter()
         if self.cuda:
-            self.enc_event.record(self.comm_stream)
+            if self.grad_mode == "flat":  # (gather mode: the gradient hold list carries its own event)
+                self.enc_event.record(self.comm_stream)
         partial = 0 if (self.step_all_present or not self.cfg.skip_missing_grads) else 1
         t_wait = self._push_wait
         for pos in range(early, self.nb):
