@@ -97,6 +97,8 @@ void bn_finalize_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tensor we
                           at::Tensor mean, at::Tensor invstd, at::Tensor scale, at::Tensor shift, int64_t C, double eps,
                           double momentum);
 void maxpool3s2_backward(at::Tensor dy, at::Tensor code, at::Tensor dx);
+void bn_finalize_bwd_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tensor weight, at::Tensor mean,
+                              at::Tensor invstd, at::Tensor dweight, at::Tensor dbias, at::Tensor coef);
 void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64_t Wi, int64_t stride,
                    c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift);
 void bn_forward_stats(at::Tensor x, at::Tensor weight, at::Tensor bias, c10::optional<at::Tensor> running_mean,
@@ -229,6 +231,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("shift") = pybind11::none());
   m.def("bn_finalize_partials", &hipps::bn_finalize_partials,
         "BN train-mode finalize from producer partial sums (mean/invstd/scale/shift + running stats)");
+  m.def("bn_finalize_bwd_partials", &hipps::bn_finalize_bwd_partials,
+        "BN backward finalize from partial sums (dweight, dbias, dx coefficients [3, C])");
   m.def("maxpool3s2_backward", &hipps::maxpool3s2_backward, "3x3/s2/p1 max pool backward (gather form, no atomics)");
   m.def("conv1x1_wgrad", &hipps::conv1x1_wgrad, "MFMA 1x1 conv weight gradient (tr_b16 LDS reads, split-M)",
         pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("dw"), pybind11::arg("Hi"), pybind11::arg("Wi"),

@@ -485,8 +485,42 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
       bsb[j] = 0.f;
     }
   }
+  // Without the MFMA-time prefetch (PF), the epilogue operands of NB chunks are loaded together
+  // before any of them is used: loads and the Y stores interleaved chunk by chunk serialised every
+  // chunk on two HBM round trips (the compiler cannot hoist a load of R / bx over a store to Y).
+  constexpr int NB = PF ? 1 : (NOUT < 8 ? NOUT : 8);
+  static_assert(NOUT % NB == 0, "epilogue batches");
 #pragma unroll
-  for (int i = 0; i < NOUT; ++i) {
+  for (int i0 = 0; i0 < NOUT; i0 += NB) {
+    u32x4 lr[NB], lx[NB];
+    uint32_t lrm[NB], lxm[NB];
+    if constexpr (!PF && NSTR > 0) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const int id = t + NT * (i0 + b);
+        const int row = id / RCH, c = id - row * RCH;
+        const int mr = m0 + row < g.M ? m0 + row : m0;
+        const int64_t o = orow(mr) * g.N + n0 + c * 8;
+        if constexpr (ADDE) {
+          if constexpr (S2) {
+            const int64_t ro = r_off(mr, n0 + c * 8);
+            const int64_t rc = ro >= 0 ? ro : 0;
+            const u32x4 rv = *reinterpret_cast<const u32x4*>(g.R + rc);
+            lr[b] = ro >= 0 ? rv : u32x4{0u, 0u, 0u, 0u};
+          } else {
+            lr[b] = *reinterpret_cast<const u32x4*>(g.R + o);
+          }
+          lrm[b] = g.RM != nullptr ? g.RM[o >> 3] : 0xffu;
+        }
+        if constexpr (BSTE) {
+          lx[b] = *reinterpret_cast<const u32x4*>(g.bx + o);
+          lxm[b] = BSTE == 2 ? g.bbits[o >> 3] : 0u;
+        }
+      }
+    }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int i = i0 + b;
     const int id = t + NT * i;
     const int row = id / RCH, c = id - row * RCH;
     if (m0 + row < g.M) {
@@ -498,13 +532,9 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
         if constexpr (PF) {
           r = pr[i];
           mb = prm[i];
-        } else if constexpr (S2) {
-          const int64_t ro = r_off(m0 + row, n0 + c * 8);
-          r = ro >= 0 ? *reinterpret_cast<const u32x4*>(g.R + ro) : u32x4{0u, 0u, 0u, 0u};
-          mb = g.RM != nullptr ? g.RM[o >> 3] : 0xffu;
         } else {
-          r = *reinterpret_cast<const u32x4*>(g.R + o);
-          mb = g.RM != nullptr ? g.RM[o >> 3] : 0xffu;
+          r = lr[b];
+          mb = lrm[b];
         }
         {
           r.x &= (mb & 1u ? 0xffffu : 0u) | (mb & 2u ? 0xffff0000u : 0u);
@@ -525,8 +555,8 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
           xu = px[i];
           mbits = pxm[i];
         } else {
-          xu = *reinterpret_cast<const u32x4*>(g.bx + o);
-          mbits = BST == 2 ? g.bbits[o >> 3] : 0u;
+          xu = lx[b];
+          mbits = lxm[b];
         }
         const uint32_t dv[4] = {v.x, v.y, v.z, v.w};
         const uint32_t xw[4] = {xu.x, xu.y, xu.z, xu.w};
@@ -541,6 +571,7 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
         }
       }
     }
+  }
   }
   if (BST) {  // combine the NT/RCH row lanes of each channel chunk through LDS, fixed order
     constexpr int RL = NT / RCH;

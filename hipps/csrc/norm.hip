@@ -21,6 +21,8 @@
 // Partials are combined in a fixed order, so results are deterministic run to run.
 #include "common.h"
 
+#include <cstdlib>
+
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
@@ -146,7 +148,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_reduce(const uint16_t* __restrict
 constexpr int kFinCh = 1;
 // WPC (nrb <= 512, the deep layers' partials): one wave per channel, 4 channels per block -- the
 // block-per-channel form spent most of its ~5 us on 2048 mostly idle workgroups there
-template <bool WPC>
+template <bool WPC, int U>
 __device__ __forceinline__ bool combine_partials(const float* __restrict__ pa, const float* __restrict__ pb, int nrb,
                                                  int C, double& s, double& q, int& c) {
   __shared__ double red[2][kBlock / 64];
@@ -156,17 +158,27 @@ __device__ __forceinline__ bool combine_partials(const float* __restrict__ pa, c
   if (c < C) {
     const float* ra = pa + (int64_t)c * nrb;
     const float* rb = pb + (int64_t)c * nrb;
-    // 8 independent loads in flight per lane (a dependent chain of nrb/256 L2 round trips was the
-    // kernel's time on the 6272-column layer-1 partials); each lane's sum keeps its fixed order
+    // 2*U independent loads in flight per lane: the partials were just written by the producer
+    // and mostly sit in MALL / HBM (a layer-1 GEMM's are 12.8 MB), so the kernel's time is the
+    // number of dependent round trips (nrb / (U*256)); out-of-range lanes load a clamped index and
+    // add zero (a branch around each load would wait per element).  Each lane's sum keeps its
+    // fixed order.
     constexpr int L = WPC ? 64 : kBlock;
-    int i = WPC ? lane : (int)threadIdx.x;
-    for (; i + 3 * L < nrb; i += 4 * L) {
-      const float a0 = ra[i], a1 = ra[i + L], a2 = ra[i + 2 * L], a3 = ra[i + 3 * L];
-      const float b0 = rb[i], b1 = rb[i + L], b2 = rb[i + 2 * L], b3 = rb[i + 3 * L];
-      a += a0; a += a1; a += a2; a += a3;
-      b += b0; b += b1; b += b2; b += b3;
+    for (int i0 = WPC ? lane : (int)threadIdx.x; i0 < nrb; i0 += U * L) {
+      float va[U], vb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = min(i0 + u * L, nrb - 1);
+        va[u] = ra[i];
+        vb[u] = rb[i];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool in = i0 + u * L < nrb;
+        a += in ? (double)va[u] : 0.0;
+        b += in ? (double)vb[u] : 0.0;
+      }
     }
-    for (; i < nrb; i += L) { a += ra[i]; b += rb[i]; }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -187,7 +199,7 @@ __device__ __forceinline__ bool combine_partials(const float* __restrict__ pa, c
 }
 
 // forward finalize: stats + running stats + per-channel scale/shift
-template <bool WPC>
+template <bool WPC, int U = 12>
 __global__ __launch_bounds__(kBlock) void k_bn_finalize_fwd(const float* __restrict__ pa, const float* __restrict__ pb,
                                                             int nrb, int C, int64_t M, const float* __restrict__ w,
                                                             const float* __restrict__ bias, float eps, float momentum,
@@ -197,7 +209,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_finalize_fwd(const float* __restr
                                                             float* __restrict__ shift) {
   double s, q;
   int c;
-  if (!combine_partials<WPC>(pa, pb, nrb, C, s, q, c)) return;
+  if (!combine_partials<WPC, U>(pa, pb, nrb, C, s, q, c)) return;
   const double m = s / (double)M;
   double var = q / (double)M - m * m;
   if (var < 0.0) var = 0.0;
@@ -215,7 +227,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_finalize_fwd(const float* __restr
 }
 
 // backward finalize: dgamma, dbeta and dx = a*dz + k1*x + k0 coefficients
-template <bool WPC>
+template <bool WPC, int U = 12>
 __global__ __launch_bounds__(kBlock) void k_bn_finalize_bwd(const float* __restrict__ pa, const float* __restrict__ pb,
                                                             int nrb, int C, int64_t M, const float* __restrict__ w,
                                                             const float* __restrict__ mean,
@@ -224,7 +236,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_finalize_bwd(const float* __restr
                                                             float* __restrict__ ck1, float* __restrict__ ck0) {
   double s, q;
   int c;
-  if (!combine_partials<WPC>(pa, pb, nrb, C, s, q, c)) return;
+  if (!combine_partials<WPC, U>(pa, pb, nrb, C, s, q, c)) return;
   if (dw) dw[c] = (float)q;
   if (db) db[c] = (float)s;
   const double is = invstd[c];
@@ -239,12 +251,20 @@ __global__ __launch_bounds__(kBlock) void k_bn_finalize_bwd(const float* __restr
 // wave-per-channel finalize: measured no faster in the step (the ~5 us per call is launch
 // latency, not the combine), so it is off (kWpcMax = 0); kept for the micro-benchmarks
 constexpr int kWpcMax = 0;
+// loads in flight per lane in the combine: 2*12 (HIPPS_BN_FIN_U=4: the round-3 depth, for A/B)
+static bool fin_shallow() {
+  static const bool v = [] { const char* e = std::getenv("HIPPS_BN_FIN_U"); return e && std::atoi(e) == 4; }();
+  return v;
+}
 static void fin_fwd(hipStream_t st, const float* pa, const float* pb, int nrb, int C, int64_t M, const float* w,
                     const float* bias, float eps, float mom, float* rm, float* rv, float* mean, float* invstd,
                     float* scale, float* shift) {
   if (nrb <= kWpcMax)
     hipLaunchKernelGGL(k_bn_finalize_fwd<true>, (C + kBlock / 64 - 1) / (kBlock / 64), kBlock, 0, st, pa, pb, nrb, C, M,
                        w, bias, eps, mom, rm, rv, mean, invstd, scale, shift);
+  else if (fin_shallow())
+    hipLaunchKernelGGL((k_bn_finalize_fwd<false, 4>), C, kBlock, 0, st, pa, pb, nrb, C, M, w, bias, eps, mom, rm, rv,
+                       mean, invstd, scale, shift);
   else
     hipLaunchKernelGGL(k_bn_finalize_fwd<false>, C, kBlock, 0, st, pa, pb, nrb, C, M, w, bias, eps, mom, rm, rv, mean,
                        invstd, scale, shift);
@@ -254,6 +274,9 @@ static void fin_bwd(hipStream_t st, const float* pa, const float* pb, int nrb, i
   if (nrb <= kWpcMax)
     hipLaunchKernelGGL(k_bn_finalize_bwd<true>, (C + kBlock / 64 - 1) / (kBlock / 64), kBlock, 0, st, pa, pb, nrb, C, M,
                        w, mean, invstd, dw, db, ca, ck1, ck0);
+  else if (fin_shallow())
+    hipLaunchKernelGGL((k_bn_finalize_bwd<false, 4>), C, kBlock, 0, st, pa, pb, nrb, C, M, w, mean, invstd, dw, db, ca,
+                       ck1, ck0);
   else
     hipLaunchKernelGGL(k_bn_finalize_bwd<false>, C, kBlock, 0, st, pa, pb, nrb, C, M, w, mean, invstd, dw, db, ca, ck1,
                        ck0);

@@ -59,28 +59,35 @@ __global__ __launch_bounds__(kBlock) void k_maxpool3s2_fwd(const uint16_t* __res
     sc[j] = BN ? scale[g * 8 + j] : 1.f;
     sh[j] = BN ? shift[g * 8 + j] : 0.f;
   }
-  uint32_t c = 0;
+  // all 9 taps' loads issue together: out-of-range taps read a clamped (valid) address and are
+  // skipped in the compare (a branch around each load serialised them: 159 us per batch-256 stem
+  // pool, profiles/r4/r4e/steady.txt)
+  float xv[9][8];
+  bool ok[9];
 #pragma unroll
   for (int kh = 0; kh < 3; ++kh) {
     const int h = 2 * ho - 1 + kh;
-    if (h < 0 || h >= H) continue;
+    const int hc = min(max(h, 0), H - 1);
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
       const int w = 2 * wo - 1 + kw;
-      if (w < 0 || w >= W) continue;
-      float xv[8];
-      ld8(x + (((n * H + h) * W + w) * G + g) * 8, xv);
-      if (BN) {
+      const int wc = min(max(w, 0), W - 1);
+      ok[kh * 3 + kw] = h >= 0 && h < H && w >= 0 && w < W;
+      ld8(x + (((n * H + hc) * W + wc) * G + g) * 8, xv[kh * 3 + kw]);
+    }
+  }
+  uint32_t c = 0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) xv[j] = bf16_to_f32(f32_to_bf16(fmaxf(fmaf(xv[j], sc[j], sh[j]), 0.f)));
-      }
-      const uint32_t t = (uint32_t)(kh * 3 + kw);
+  for (int t = 0; t < 9; ++t) {
+    if (BN) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (xv[j] > m[j] || __builtin_isnan(xv[j])) {
-          m[j] = xv[j];
-          c = (c & ~(15u << (4 * j))) | (t << (4 * j));
-        }
+      for (int j = 0; j < 8; ++j) xv[t][j] = bf16_to_f32(f32_to_bf16(fmaxf(fmaf(xv[t][j], sc[j], sh[j]), 0.f)));
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (ok[t] && (xv[t][j] > m[j] || __builtin_isnan(xv[t][j]))) {
+        m[j] = xv[t][j];
+        c = (c & ~(15u << (4 * j))) | ((uint32_t)t << (4 * j));
       }
     }
   }
@@ -105,16 +112,30 @@ __global__ __launch_bounds__(kBlock) void k_maxpool3s2_bwd(const uint16_t* __res
   float acc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-  const int oh1 = min((h + 1) >> 1, Ho - 1), ow1 = min((w + 1) >> 1, Wo - 1);
-  for (int oh = h >> 1; oh <= oh1; ++oh) {
-    for (int ow = w >> 1; ow <= ow1; ++ow) {
-      const uint32_t t = (uint32_t)((h - 2 * oh + 1) * 3 + (w - 2 * ow + 1));
-      const int64_t o = ((n * Ho + oh) * Wo + ow) * G + g;
-      const uint32_t c = code[o];
-      float d[8];
-      ld8(dy + o * 8, d);
+  // candidate windows (h>>1 | (h>>1)+1) x (w>>1 | (w>>1)+1), the +1 ones only for odd h / w inside
+  // the pooled map: a static 2x2 with predicates, so the 4 code / dy loads issue together (the
+  // data-dependent loop serialised them: 280 us per batch-256 stem pool backward, profiles/r4/r4e/
+  // steady.txt).  Same (oh, ow) summation order as that loop; absent windows add +0.
+  const int oh0 = h >> 1, ow0 = w >> 1;
+  const bool h1 = (h & 1) && oh0 + 1 < Ho, w1 = (w & 1) && ow0 + 1 < Wo;
+  uint32_t c[4];
+  uint4 d[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += ((c >> (4 * j)) & 15u) == t ? d[j] : 0.f;
+  for (int k = 0; k < 4; ++k) {
+    const bool okk = (!(k >> 1) || h1) && (!(k & 1) || w1);
+    const int64_t o = okk ? ((n * Ho + oh0 + (k >> 1)) * Wo + ow0 + (k & 1)) * G + g : 0;
+    const uint32_t cv = code[o];
+    d[k] = *reinterpret_cast<const uint4*>(dy + o * 8);
+    c[k] = okk ? cv : 0xffffffffu;  // tap 15 never matches
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t t = (uint32_t)((h - 2 * (oh0 + (k >> 1)) + 1) * 3 + (w - 2 * (ow0 + (k & 1)) + 1));
+    const uint32_t dw[4] = {d[k].x, d[k].y, d[k].z, d[k].w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float dv = __uint_as_float(j & 1 ? dw[j >> 1] & 0xffff0000u : dw[j >> 1] << 16);
+      acc[j] += ((c[k] >> (4 * j)) & 15u) == t ? dv : 0.f;
     }
   }
   st8(dx + v * 8, acc);

@@ -12,6 +12,8 @@
 // counter-based hash so a message is reproducible from (seed, index).
 #include "common.h"
 
+#include <cstdlib>
+
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
@@ -93,6 +95,102 @@ __global__ __launch_bounds__(kBlock) void k_q8_encode(const float* __restrict__ 
   }
 }
 
+// Row form (the default): one 16-lane DPP row per 256-element block, 16 elements per lane as four
+// 16-byte loads 64 elements apart (each load instruction covers four 256-byte runs), four blocks per
+// wave per iteration.  The block absmax is 4 DPP steps inside the row instead of a 6-step
+// cross-lane shuffle through LDS per block (6 LDS round trips per block in k_q8_encode), and the
+// next iteration's x / residual loads are issued before this one's quantization (software
+// pipelined: one HBM round trip exposed per wave, not per iteration).  Same element -> (block,
+// scale, rounding index) mapping as k_q8_encode, so the message is bit-identical.
+__device__ __forceinline__ float row16_max(float v) {
+  // quad xor 1, quad xor 2, half-row mirror, row mirror: every lane of the 16-lane row ends with the
+  // row's maximum
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false)));
+  return v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_q8_encode_rows(const float* __restrict__ x, float* __restrict__ resid,
+                                                           int8_t* __restrict__ q, float* __restrict__ scales,
+                                                           int64_t n, int stochastic, uint64_t seed) {
+  const int lane = threadIdx.x & 63, row = lane >> 4, rl = lane & 15;
+  const int64_t nblocks = (n + kQBlock - 1) / kQBlock;
+  const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t wstride = (int64_t)gridDim.x * (blockDim.x >> 6) * 4;
+  // element e = 4*j + k of this lane in block b: b*256 + 64*j + 4*rl + k
+  auto load = [&](const float* src, int64_t b, float (&v)[16]) {
+    const int64_t base = b * kQBlock + 4 * rl;
+    if ((b + 1) * kQBlock <= n) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 t = *reinterpret_cast<const float4*>(src + base + 64 * j);
+        v[4 * j] = t.x; v[4 * j + 1] = t.y; v[4 * j + 2] = t.z; v[4 * j + 3] = t.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t i = base + 64 * j + k;
+          v[4 * j + k] = i < n ? src[i] : 0.f;
+        }
+    }
+  };
+  int64_t b0 = wave * 4;  // the wave's first block this iteration (wave-uniform)
+  int64_t b = b0 + row;   // this row's block
+  float xv[16], rv[16];
+  if (b < nblocks) {
+    load(x, b, xv);
+    if (resid) load(resid, b, rv);
+  }
+  while (b0 < nblocks) {
+    const int64_t b0n = b0 + wstride, bn = b0n + row;
+    float v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) v[e] = resid ? xv[e] + rv[e] : xv[e];
+    if (bn < nblocks) {  // the next iteration's operands in flight during this one's work
+      load(x, bn, xv);
+      if (resid) load(resid, bn, rv);
+    }
+    float amax = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) amax = fmaxf(amax, fabsf(v[e]));
+    amax = row16_max(amax);  // every lane of the wave is active here (wave-uniform loop)
+    if (b < nblocks) {
+      const float scale = amax / 127.f;
+      const float inv = amax > 0.f ? 127.f / amax : 0.f;
+      const int64_t base = b * kQBlock + 4 * rl;
+      if (rl == 0) scales[b] = scale;
+      const bool full = (b + 1) * kQBlock <= n;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t i = base + 64 * j;
+        int8_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = q8_round(v[4 * j + k], inv, stochastic, seed, i + k);
+        if (full) {
+          *reinterpret_cast<char4*>(q + i) = make_char4(o[0], o[1], o[2], o[3]);
+          if (resid)
+            *reinterpret_cast<float4*>(resid + i) =
+                make_float4(v[4 * j] - o[0] * scale, v[4 * j + 1] - o[1] * scale, v[4 * j + 2] - o[2] * scale,
+                            v[4 * j + 3] - o[3] * scale);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (i + k < n) {
+              q[i + k] = o[k];
+              if (resid) resid[i + k] = v[4 * j + k] - o[k] * scale;
+            }
+        }
+      }
+    }
+    b0 = b0n;
+    b = bn;
+  }
+}
+
 // acc (+)= gscale * sum_w deq(q_w, s_w)   — rank-ordered, 4 elements per lane
 __global__ __launch_bounds__(kBlock) void k_q8_aggregate(SlotPtrs qs, SlotPtrs ss, int W, float gscale,
                                                          float* __restrict__ acc, int64_t n, int accumulate,
@@ -146,9 +244,17 @@ void q8_encode(at::Tensor x, c10::optional<at::Tensor> resid, at::Tensor q, at::
     rp = resid->data_ptr<float>();
   }
   const int64_t nblocks = (n + kQBlock - 1) / kQBlock;
+  static const bool rows = [] {  // HIPPS_Q8_ENC=0: the one-wave-per-block kernel, for A/B
+    const char* e = std::getenv("HIPPS_Q8_ENC");
+    return !(e && e[0] == '0');
+  }();
   const int grid = grid_for((nblocks + kQUnroll - 1) / kQUnroll * 64);
-  hipLaunchKernelGGL(k_q8_encode, grid, kBlock, 0, c10::hip::getCurrentHIPStream(), x.data_ptr<float>(), rp,
-                     (int8_t*)q.data_ptr(), scales.data_ptr<float>(), n, (int)stochastic, (uint64_t)seed);
+  if (rows)
+    hipLaunchKernelGGL(k_q8_encode_rows, grid, kBlock, 0, c10::hip::getCurrentHIPStream(), x.data_ptr<float>(), rp,
+                       (int8_t*)q.data_ptr(), scales.data_ptr<float>(), n, (int)stochastic, (uint64_t)seed);
+  else
+    hipLaunchKernelGGL(k_q8_encode, grid, kBlock, 0, c10::hip::getCurrentHIPStream(), x.data_ptr<float>(), rp,
+                       (int8_t*)q.data_ptr(), scales.data_ptr<float>(), n, (int)stochastic, (uint64_t)seed);
 }
 
 void q8_aggregate(const std::vector<at::Tensor>& qs, const std::vector<at::Tensor>& ss, at::Tensor acc, double gscale,

@@ -273,7 +273,10 @@ __device__ __forceinline__ uint32_t collect_chunk(const float (&x)[kCompactPer],
 // P1 / P2: [fold] + [histogram of bits 30..20] + the region's ordered list of keys >= bound.
 // mode 0: top-k P1 (bound = spec_lo); 1: threshold (bound = T + 1, counts -> cgt / ceq);
 // 2: top-k repair (bound = bin B's lower edge; nothing to do when P1's bound covered bin B).
-template <bool HIST>
+// PF: the next chunk's loads (g, and r when folding) are issued before the current chunk is
+// processed, so a region's chunks stream with one HBM round trip exposed per region instead of
+// one per chunk (HIPPS_TOPK_PF=0: the unpipelined loop, for A/B)
+template <bool HIST, bool PF = true>
 __global__ __launch_bounds__(kBlock) void k_collect(const float* __restrict__ src, float* __restrict__ fold_r,
                                                     int64_t n, SelState* __restrict__ st, Regions R, int mode,
                                                     int fold_pick = 0) {
@@ -291,9 +294,26 @@ __global__ __launch_bounds__(kBlock) void k_collect(const float* __restrict__ sr
   const uint32_t slot_end = slot_pos + capw;
   uint32_t total = 0;
   const int64_t c0 = blockIdx.x * R.cpw, c1 = std::min<int64_t>(c0 + R.cpw, R.nchunks);
+  float gx[PF ? kCompactPer : 1], rx[PF ? kCompactPer : 1];
+  if constexpr (PF) {
+    if (c0 < c1) {
+      chunk_load(src, n, c0, gx);
+      if (fold_r) chunk_load(fold_r, n, c0, rx);
+    }
+  }
   for (int64_t c = c0; c < c1; ++c) {
     float x[kCompactPer];
-    chunk_fold(src, fold_r, n, c, x);
+    if constexpr (PF) {
+#pragma unroll
+      for (int e = 0; e < kCompactPer; ++e) x[e] = fold_r ? gx[e] + rx[e] : gx[e];
+      if (c + 1 < c1) {  // next chunk in flight during this one's histogram, list and stores
+        chunk_load(src, n, c + 1, gx);
+        if (fold_r) chunk_load(fold_r, n, c + 1, rx);
+      }
+      if (fold_r) chunk_store(fold_r, n, c, x);
+    } else {
+      chunk_fold(src, fold_r, n, c, x);
+    }
     if (HIST) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -1007,13 +1027,21 @@ void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::T
   hipLaunchKernelGGL(k_sel_init, 1, kBlock, 0, stream, w.st, 0u, 0u, (uint32_t)k, (uint32_t)w.g.capw,
                      (uint32_t)(w.g.pool / kPoolShards), 1);
   // P1: fold + top-digit histogram + speculative ordered list (the only full pass)
+  static const bool pf = [] {
+    const char* e = std::getenv("HIPPS_TOPK_PF");
+    return !(e && e[0] == '0');
+  }();
   static const bool fold = [] {  // picks inside the histogram launches (HIPPS_TOPK_FOLD=0: separate)
     const char* e = std::getenv("HIPPS_TOPK_FOLD");
     return !(e && e[0] == '0');
   }();
   const float* src = rp ? rp : g.data_ptr<float>();
   if (fold) {
-    hipLaunchKernelGGL(k_collect<true>, nreg, kBlock, 0, stream, g.data_ptr<float>(), rp, n, w.st, w.R, 0, 1);
+    if (pf)
+      hipLaunchKernelGGL((k_collect<true, true>), nreg, kBlock, 0, stream, g.data_ptr<float>(), rp, n, w.st, w.R, 0, 1);
+    else
+      hipLaunchKernelGGL((k_collect<true, false>), nreg, kBlock, 0, stream, g.data_ptr<float>(), rp, n, w.st, w.R, 0,
+                         1);
     // P3 over the listed keys of bin B; its pick checks that the list reaches the remaining-th key
     hipLaunchKernelGGL(k_hist_list, nreg, kBlock, 0, stream, src, n, 9, 11, w.st, w.R, nreg, 0, kPickCheck, 1);
     // only after a miss (first call, shrinking gradients): re-list from bin B's edge, P3 again

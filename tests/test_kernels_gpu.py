@@ -132,7 +132,7 @@ def test_masked_update_skips_chunks(opt, n):
     assert torch.equal(pub.cpu(), pd.cpu())
 
 
-@pytest.mark.parametrize("n", [1, 255, 256, 1000, 1 << 20])
+@pytest.mark.parametrize("n", [1, 255, 256, 1000, 1 << 20, 9_000_001])
 @pytest.mark.parametrize("ef,sr", [(False, False), (True, False), (False, True)])
 def test_q8_encode_matches_reference(n, ef, sr):
     torch.manual_seed(n)

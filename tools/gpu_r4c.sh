@@ -7,9 +7,11 @@ set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r4c
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "topk or codec or threshold" > $O/ktests.log 2>&1 || { tail -30 $O/ktests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "topk or codec or threshold or q8" > $O/ktests.log 2>&1 || { tail -30 $O/ktests.log; exit 1; }
 tail -1 $O/ktests.log
 HIPPS_TOPK_FOLD=0 timeout -k 10 240 python -u bench/codec_bench.py --sizes 1000000,25557032 --specs topk:0.01 --no-host --out $O/codec_bench_nofold.json > $O/codec_nofold.log 2>&1 || { tail -20 $O/codec_nofold.log; exit 1; }
+HIPPS_Q8_ENC=0 timeout -k 10 240 python -u bench/codec_bench.py --sizes 1000000,25557032 --specs int8 --no-host --out $O/codec_bench_q8old.json > $O/codec_q8old.log 2>&1 || { tail -20 $O/codec_q8old.log; exit 1; }
+HIPPS_TOPK_PF=0 timeout -k 10 240 python -u bench/codec_bench.py --sizes 1000000,25557032 --specs topk:0.01 --no-host --out $O/codec_bench_nopf.json > $O/codec_nopf.log 2>&1 || { tail -20 $O/codec_nopf.log; exit 1; }
 timeout -k 10 240 python -u bench/codec_bench.py --sizes 10,100,1000,10000,32768,1000000,25557032 --specs bf16,int8,topk:0.01,topk_int8:0.01,threshold:0.02:0.05 --no-host --out $O/codec_bench.json > $O/codec.log 2>&1 || { tail -20 $O/codec.log; exit 1; }
 tail -3 $O/codec.log
 ARGS="bench/codec_bench.py --sizes 25557032 --specs bf16,int8,topk:0.01,threshold:0.002:0.05 --no-host --warm"
