@@ -915,12 +915,34 @@ template <typename VT>
 __global__ __launch_bounds__(kSmallThreads) void k_topk_small(const float* __restrict__ g, float* __restrict__ resid,
                                                              int n, int k, int32_t* __restrict__ idx,
                                                              VT* __restrict__ val) {
-  __shared__ float sv[kSmallMax];
+  __shared__ __attribute__((aligned(16))) float sv[kSmallMax];
   __shared__ uint32_t hist[2][kHistBins];
   __shared__ uint32_t wsum[64];
   __shared__ uint32_t sel[2];  // chosen bin, keys above it
   const int t = threadIdx.x, wv = t >> 6;
-  for (int i = t; i < n; i += kSmallThreads) sv[i] = g[i] + (resid ? resid[i] : 0.f);
+  // The fold: one CU pulls up to 256 KB, so it is a latency problem -- a strided loop of dependent
+  // single loads left one HBM round trip per 1024 elements exposed (~40 us cold at n = 32768).
+  // Every lane issues all its 16-byte loads of g and r first (8 + 8 in flight), then writes LDS.
+  {
+    const bool vec = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(resid)) & 15) == 0;
+    const int n4 = vec ? n >> 2 : 0;
+    constexpr int U = kSmallMax / 4 / kSmallThreads;  // 8 float4 per lane at n = kSmallMax
+    float4 a[U], r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int v = t + u * kSmallThreads;
+      const int vc = v < n4 ? v : 0;  // clamped index, result discarded: no branch around a load
+      a[u] = n4 ? reinterpret_cast<const float4*>(g)[vc] : make_float4(0.f, 0.f, 0.f, 0.f);
+      r[u] = (n4 && resid) ? reinterpret_cast<const float4*>(resid)[vc] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int v = t + u * kSmallThreads;
+      if (v < n4)
+        reinterpret_cast<float4*>(sv)[v] = make_float4(a[u].x + r[u].x, a[u].y + r[u].y, a[u].z + r[u].z, a[u].w + r[u].w);
+    }
+    for (int i = 4 * n4 + t; i < n; i += kSmallThreads) sv[i] = g[i] + (resid ? resid[i] : 0.f);
+  }
   uint32_t prefix = 0, pmask = 0, rem = (uint32_t)k;
 #pragma unroll
   for (int pass = 0; pass < 3; ++pass) {
