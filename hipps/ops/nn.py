@@ -580,10 +580,30 @@ def unregister_transposed_weight(p: torch.Tensor):
     _TSHADOWS.pop(p.data_ptr(), None)
 
 
+# Host work that may run whenever the forward is ahead of the GPU (e.g. the engine dropping the
+# previous steps' gathered gradients, ~2 us per tensor): bf16_weight runs each task once per conv
+# of the forward, where the host leads the GPU by milliseconds, instead of at the step boundary or
+# the start of backward, where a late host idles the GPU.
+_HOST_IDLE_TASKS: list = []
+
+
+def add_host_idle_task(fn) -> None:
+    _HOST_IDLE_TASKS.append(fn)
+
+
+def remove_host_idle_task(fn) -> None:
+    try:
+        _HOST_IDLE_TASKS.remove(fn)
+    except ValueError:
+        pass
+
+
 def bf16_weight(w: torch.Tensor) -> torch.Tensor:
     """The bf16 view of fp32 master weight ``w`` in a registered shadow (same shape and strides),
     else a fresh cast.  The shadow is refreshed by the optimizer with one cast kernel per step, so
     a ResNet-50 forward reads its 53 conv weights without 53 autocast cast launches."""
+    for fn in _HOST_IDLE_TASKS:
+        fn()
     if w.dtype == torch.bfloat16:
         return w
     p = w.data_ptr()

@@ -16,6 +16,7 @@ communicating before every tensor is encoded (ps.py:128-132).
 from __future__ import annotations
 
 import hashlib
+import os
 import time
 from typing import Dict, List, Optional
 
@@ -85,6 +86,14 @@ class Engine:
 
         self._held: deque = deque()  # (comm-stream event, [gradients its gathers read])
         self._held_cur: list = []
+        self._drain: list = []  # gradients whose gathers completed, freed a few at a time
+        self._idle_task = None
+        self._idle_ran = False  # the host-idle task ran since the last step (it drains _drain)
+        if self.cuda and os.environ.get("HIPPS_HOLD_DRAIN", "1") != "0":
+            from ..ops import nn as hnn
+
+            self._idle_task = self._drain_some
+            hnn.add_host_idle_task(self._idle_task)
         if self.grad_mode == "gather":
             self._build_gather_plan()
             store.set_grad_mode("gather")
@@ -95,9 +104,13 @@ class Engine:
     GATHER_MAX = 256
     HOLD_MAX = 3  # steps of gathered gradients kept alive at most before the host waits
 
+    DRAIN_PER_CALL = 4  # gradients freed per host-idle call (53 per ResNet-50 forward)
+
     def _release_held(self, force: bool = False):
         """Drop the references to gradients whose gather has completed on the comm stream (their
-        memory then returns to the allocator with no pending stream use, so no event is needed)."""
+        memory then returns to the allocator with no pending stream use, so no event is needed).
+        With a host-idle task registered the completed lists only move to the drain list (no
+        frees here); the forward frees them a few per conv (``_drain_some``)."""
         held = self._held
         while held:
             ev = held[0][0]
@@ -105,7 +118,24 @@ class Engine:
                 if not (force or len(held) > self.HOLD_MAX):
                     break
                 ev.synchronize()  # the host ran HOLD_MAX steps ahead of the comm stream
-            held.popleft()
+            _, lst = held.popleft()
+            if self._idle_ran and not force:  # a forward drains them (else they are freed here)
+                self._drain.extend(lst)
+        if force:
+            self._drain.clear()
+
+    def _drain_some(self):
+        """Host-idle task (called from the forward, hipps.ops.nn.bf16_weight): free a few
+        gradients whose gathers have completed; when none are pending, move the oldest completed
+        step's list over (one event query)."""
+        self._idle_ran = True
+        d = self._drain
+        if not d:
+            if not self._held or not self._held[0][0].query():
+                return
+            d.extend(self._held.popleft()[1])
+        for _ in range(min(self.DRAIN_PER_CALL, len(d))):
+            d.pop()
 
     def _hold_step(self):
         """End of a step's encodes: the gradients gathered this step stay referenced until an
@@ -116,6 +146,9 @@ class Engine:
         ev.record(self.comm_stream)
         self._held.append((ev, self._held_cur))
         self._held_cur = []
+        if not self._idle_ran and self._drain:  # no forward drained them this step
+            self._drain.clear()
+        self._idle_ran = False
         if len(self._held) > self.HOLD_MAX:
             self._release_held()
         # (otherwise the frees -- ~2 us per gradient tensor -- happen at the next step's first
@@ -410,6 +443,11 @@ class Engine:
     def close(self):
         self.remove_hooks()
         if self.cuda:
+            if self._idle_task is not None:
+                from ..ops import nn as hnn
+
+                hnn.remove_host_idle_task(self._idle_task)
+                self._idle_task = None
             self._release_held(force=True)
         if self.watchdog is not None:
             self.watchdog.close()
