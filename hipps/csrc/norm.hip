@@ -512,6 +512,18 @@ int apply_grid(int64_t M, int C) {
   const int64_t V = M * (C / 8);
   return grid_for(V);
 }
+// forward apply: UNR vectors in flight per lane on the large (>= 4 M-vector, layer-1/2) tensors
+// when HIPPS_BN_APPLY_UNR=2 (A/B; 1 measured no slower on the layer-3/4 sizes)
+typedef void (*ApplyFwdFn)(const uint16_t*, const uint16_t*, uint16_t*, uint8_t*, const float*, const float*, int64_t,
+                           int, int, const float*, const float*);
+ApplyFwdFn apply_fwd_kernel(int64_t M, int C) {
+  static const int unr = [] {
+    const char* e = std::getenv("HIPPS_BN_APPLY_UNR");
+    return e ? std::atoi(e) : 1;
+  }();
+  if (unr == 2 && M * (C / 8) >= (int64_t(4) << 20)) return k_bn_apply_fwd<2>;
+  return k_bn_apply_fwd<1>;
+}
 }  // namespace
 
 namespace {
@@ -526,7 +538,7 @@ void finalize_apply_fwd(const at::Tensor& part, int nrb, const at::Tensor& x, co
                      weight.data_ptr<float>(), bias.data_ptr<float>(), (float)eps, (float)momentum, rm, rv,
                      mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
                      shift.data_ptr<float>());
-  hipLaunchKernelGGL(k_bn_apply_fwd<1>, apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)x.data_ptr(), rp,
+  hipLaunchKernelGGL(apply_fwd_kernel(M, (int)C), apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)x.data_ptr(), rp,
                      (uint16_t*)y.data_ptr(), mo, scale.data_ptr<float>(), shift.data_ptr<float>(), M, (int)C,
                      (int)relu, nullptr, nullptr);
 }
@@ -662,7 +674,7 @@ void bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, at::Ten
   }
   check_vec(scale, "scale", (int)C);
   check_vec(shift, "shift", (int)C);
-  hipLaunchKernelGGL(k_bn_apply_fwd<1>, apply_grid(M, (int)C), kBlock, 0, c10::hip::getCurrentHIPStream(),
+  hipLaunchKernelGGL(apply_fwd_kernel(M, (int)C), apply_grid(M, (int)C), kBlock, 0, c10::hip::getCurrentHIPStream(),
                      (const uint16_t*)x.data_ptr(), rp, (uint16_t*)y.data_ptr(), nullptr, scale.data_ptr<float>(),
                      shift.data_ptr<float>(), M, (int)C, (int)relu, nullptr, nullptr);
 }
@@ -867,7 +879,7 @@ void bn_dual_forward(at::Tensor part3, int64_t nrb3, at::Tensor partd, int64_t n
   };
   fin(part3, nrb3, w3, b3, rm3, rv3, mean3, invstd3, scale3, shift3, eps3, mom3);
   fin(partd, nrbd, wd, bd, rmd, rvd, meand, invstdd, scaled, shiftd, epsd, momd);
-  hipLaunchKernelGGL(k_bn_apply_fwd<1>, apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)x3.data_ptr(),
+  hipLaunchKernelGGL(apply_fwd_kernel(M, (int)C), apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)x3.data_ptr(),
                      (const uint16_t*)xd.data_ptr(), (uint16_t*)z.data_ptr(), (uint8_t*)mask.data_ptr(),
                      scale3.data_ptr<float>(), shift3.data_ptr<float>(), M, (int)C, 1, scaled.data_ptr<float>(),
                      shiftd.data_ptr<float>());

@@ -197,3 +197,53 @@ def test_ps_memory_budget_terms_and_engine_agree():
     for k in ("mailbox", "publish", "master", "accumulator", "optimizer", "chunk_steps", "worker_wire",
               "worker_codec_state"):
         assert live[k] == shp[k], (k, live[k], shp[k])
+
+
+def test_gradient_hold_drain_frees_only_completed_steps():
+    """Engine gradient holds (gather mode): a step's gathered gradients stay referenced until the
+    comm-stream event after their gathers has completed; with a host-idle task (the forward) they
+    are freed a few per call, without one they are freed at the next release (bounded memory)."""
+    import types
+    import weakref
+
+    from hipps.parallel.engine import Engine
+
+    class Ev:
+        def __init__(self, done):
+            self.done = done
+
+        def query(self):
+            return self.done
+
+        def synchronize(self):
+            self.done = True
+
+    e = types.SimpleNamespace(_held=__import__("collections").deque(), _drain=[], _idle_ran=False,
+                              _idle_task=object(), HOLD_MAX=Engine.HOLD_MAX, DRAIN_PER_CALL=Engine.DRAIN_PER_CALL)
+    release = Engine._release_held.__get__(e)
+    drain = Engine._drain_some.__get__(e)
+    grads = [torch.zeros(2) for _ in range(6)]
+    refs = [weakref.ref(g) for g in grads]
+    ev0, ev1 = Ev(False), Ev(False)
+    e._held.append((ev0, grads[:3]))
+    e._held.append((ev1, grads[3:]))
+    del grads
+    drain()  # oldest event not complete: nothing moves, nothing freed
+    assert e._idle_ran and not e._drain and all(r() is not None for r in refs)
+    ev0.done = True
+    drain()  # moves step 0's list over and frees DRAIN_PER_CALL of it
+    assert len(e._held) == 1 and sum(r() is None for r in refs[:3]) == min(3, Engine.DRAIN_PER_CALL)
+    drain()
+    assert all(r() is None for r in refs[:3]) and all(r() is not None for r in refs[3:])
+    # no forward ran: the release frees a completed step at once
+    e._idle_ran = False
+    ev1.done = True
+    release()
+    assert not e._held and not e._drain and all(r() is None for r in refs)
+    # more than HOLD_MAX pending steps: the oldest is waited for (synchronize) and released
+    for _ in range(Engine.HOLD_MAX + 1):
+        e._held.append((Ev(False), [torch.zeros(1)]))
+    release()
+    assert len(e._held) == Engine.HOLD_MAX
+    release(force=True)
+    assert not e._held and not e._drain
