@@ -914,7 +914,9 @@ __device__ __forceinline__ void wave_hist_add(uint32_t* h, uint32_t bin, bool wa
 template <typename VT>
 __global__ __launch_bounds__(kSmallThreads) void k_topk_small(const float* __restrict__ g, float* __restrict__ resid,
                                                              int n, int k, int32_t* __restrict__ idx,
-                                                             VT* __restrict__ val) {
+                                                             VT* __restrict__ val, int flags) {
+  // flags bit 0: wave-aggregated histogram adds (else one LDS atomic per lane); bit 1: all fold
+  // loads issued before the LDS writes (else a strided loop) -- HIPPS_TOPK_SMALL=<flags> for A/B
   __shared__ __attribute__((aligned(16))) float sv[kSmallMax];
   __shared__ uint32_t hist[2][kHistBins];
   __shared__ uint32_t wsum[64];
@@ -924,7 +926,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_topk_small(const float* __res
   // single loads left one HBM round trip per 1024 elements exposed (~40 us cold at n = 32768).
   // Every lane issues all its 16-byte loads of g and r first (8 + 8 in flight), then writes LDS.
   {
-    const bool vec = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(resid)) & 15) == 0;
+    const bool vec = (flags & 2) && ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(resid)) & 15) == 0;
     const int n4 = vec ? n >> 2 : 0;
     constexpr int U = kSmallMax / 4 / kSmallThreads;  // 8 float4 per lane at n = kSmallMax
     float4 a[U], r[U];
@@ -953,7 +955,9 @@ __global__ __launch_bounds__(kSmallThreads) void k_topk_small(const float* __res
     for (int i0 = 0; i0 < n; i0 += kSmallThreads) {  // whole waves iterate together (ballots)
       const int i = i0 + t;
       const uint32_t key = i < n ? __float_as_uint(sv[i]) & 0x7fffffffu : 0u;
-      wave_hist_add(h, (key >> sh) & (nb - 1), i < n && (key & pmask) == prefix);
+      const bool want = i < n && (key & pmask) == prefix;
+      if (flags & 1) wave_hist_add(h, (key >> sh) & (nb - 1), want);
+      else if (want) atomicAdd(&h[(key >> sh) & (nb - 1)], 1u);
     }
     __syncthreads();
     // thread t owns bins hi = nb-1-2t and lo = nb-2-2t (t < nb/2); exclusive scan from the top
@@ -1036,12 +1040,16 @@ void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::T
   }
   auto stream = c10::hip::getCurrentHIPStream();
   if (n <= kSmallMax) {  // one workgroup, one launch
+    static const int sflags = [] {
+      const char* e = std::getenv("HIPPS_TOPK_SMALL");
+      return e ? std::atoi(e) : 2;  // measured: the wave-aggregated adds were slower (see k_topk_small)
+    }();
     if (val.scalar_type() == at::kFloat)
       hipLaunchKernelGGL(k_topk_small<float>, 1, kSmallThreads, 0, stream, g.data_ptr<float>(), rp, (int)n, (int)k,
-                         idx.data_ptr<int32_t>(), val.data_ptr<float>());
+                         idx.data_ptr<int32_t>(), val.data_ptr<float>(), sflags);
     else
       hipLaunchKernelGGL(k_topk_small<uint16_t>, 1, kSmallThreads, 0, stream, g.data_ptr<float>(), rp, (int)n,
-                         (int)k, idx.data_ptr<int32_t>(), (uint16_t*)val.data_ptr());
+                         (int)k, idx.data_ptr<int32_t>(), (uint16_t*)val.data_ptr(), sflags);
     return;
   }
   const int nreg = (int)w.g.nreg;
@@ -1053,9 +1061,13 @@ void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::T
     const char* e = std::getenv("HIPPS_TOPK_PF");
     return !(e && e[0] == '0');
   }();
-  static const bool fold = [] {  // picks inside the histogram launches (HIPPS_TOPK_FOLD=0: separate)
+  // picks inside the histogram launches (last-arriving block) instead of their own launches:
+  // opt-in, HIPPS_TOPK_FOLD=1 -- measured slower on 25.6 M elements (236 vs 183 us cold,
+  // profiles/codec/r4/): every region block's agent-scope release before its ticket writes back
+  // its dirty L2 lines (the folded residual), where the separate launch boundary costs ~2 us
+  static const bool fold = [] {
     const char* e = std::getenv("HIPPS_TOPK_FOLD");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   const float* src = rp ? rp : g.data_ptr<float>();
   if (fold) {

@@ -6,8 +6,12 @@ O=gpurun_out/r4f
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "topk" > $O/ktests.log 2>&1 || { tail -30 $O/ktests.log; exit 1; }
 tail -1 $O/ktests.log
-timeout -k 10 240 python -u bench/codec_bench.py --sizes 10,100,1000,10000,32768 --specs topk:0.01 --no-host --out $O/codec_small.json > $O/codec_small.log 2>&1 || { tail -20 $O/codec_small.log; exit 1; }
-python -c "import json;[print(r['n'], r['codec'], r.get('cache'), r['encode_us']) for r in json.load(open('$O/codec_small.json'))]"
+for f in 0 1 2 3; do
+  HIPPS_TOPK_SMALL=$f timeout -k 10 240 python -u bench/codec_bench.py --sizes 10,1000,10000,32768 --specs topk:0.01 --no-host --out $O/codec_small_f$f.json > $O/codec_small_f$f.log 2>&1 || { tail -20 $O/codec_small_f$f.log; exit 1; }
+  python -c "import json;print('flags $f', [(r['n'], r['encode_us']) for r in json.load(open('$O/codec_small_f$f.json'))])"
+done
+timeout -k 10 240 python -u bench/codec_bench.py --sizes 25557032 --specs topk:0.01,threshold:0.02:0.05 --no-host --out $O/codec_large.json > $O/codec_large.log 2>&1 || { tail -20 $O/codec_large.log; exit 1; }
+python -c "import json;print('large', [(r['codec'], r['encode_us']) for r in json.load(open('$O/codec_large.json'))])"
 export HIPPS_BACKEND=gloo
 for n in 2 4; do
   timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29600+n)) bench.py --gpus $n --steps 10 --warmup 3 --batch 64 --out $O/reh_n$n.json > $O/reh_n$n.log 2>&1 || { echo "n=$n failed"; tail -40 $O/reh_n$n.log; exit 1; }
