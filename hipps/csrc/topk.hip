@@ -78,6 +78,15 @@ struct SelState {        // lives at the head of the workspace
 
 __device__ __forceinline__ uint32_t absbits(float x) { return __float_as_uint(x) & 0x7fffffffu; }
 
+// Workgroup barrier for LDS hand-offs only: __syncthreads() also drains every outstanding global
+// load (s_waitcnt vmcnt(0)), which would retire k_collect's prefetch of the next chunk at each
+// chunk's list barriers.  Only LDS traffic is ordered here.
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // in-launch digit pick (defined with k_topk_pick below)
 __device__ __forceinline__ void pick_body(int lo, int nbits, SelState* __restrict__ st, int flags, uint32_t* wtot);
 __device__ __forceinline__ bool last_arriver(uint32_t* ticket, uint32_t* flag);
@@ -220,7 +229,7 @@ __device__ __forceinline__ uint32_t collect_chunk(const float (&x)[kCompactPer],
     if (lane >= o) { ia += ta; ib += tb; }
   }
   if (lane == 63) { wsum[0][w] = ia & 0xffffu; wsum[1][w] = ia >> 16; wsum[2][w] = ib & 0xffffu; wsum[3][w] = ib >> 16; }
-  __syncthreads();
+  lds_sync();
   const uint32_t incl[4] = {ia & 0xffffu, ia >> 16, ib & 0xffffu, ib >> 16};
   uint32_t off[4], run = 0;
 #pragma unroll
@@ -266,7 +275,7 @@ __device__ __forceinline__ uint32_t collect_chunk(const float (&x)[kCompactPer],
     }
   }
   if (threadIdx.x == 0) { R.coff[c] = base; R.ccnt[c] = run; }
-  __syncthreads();  // wsum / sbase reuse
+  lds_sync();  // wsum / sbase reuse
   return run;
 }
 
