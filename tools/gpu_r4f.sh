@@ -24,11 +24,3 @@ HIPPS_HOST_TIMING=1 timeout -k 10 300 python -u bench.py --steps 30 --warmup 5 -
 grep -i "host" $O/host_timing.log | tail -3
 timeout -k 10 300 python -u tools/host_profile.py --out $O/host_profile.txt --steps 20 --warmup 5 > $O/host_profile.log 2>&1 || { tail -20 $O/host_profile.log; exit 1; }
 head -60 $O/host_profile.txt
-timeout -k 10 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_ps_async_gpu.py tests/test_fused_bn.py > $O/pstests.log 2>&1 || { tail -30 $O/pstests.log; exit 1; }
-tail -1 $O/pstests.log
-for r in 1 2; do
-  for v in 1 0; do
-    timeout -k 10 300 env HIPPS_HOLD_DRAIN=$v python bench.py --steps 30 --warmup 5 --out $O/ab_drain${v}_r$r.json > $O/ab_drain${v}_r$r.log 2>&1 || { tail -20 $O/ab_drain${v}_r$r.log; exit 1; }
-    python -c "import json;d=json.load(open('$O/ab_drain${v}_r$r.json'));print('drain$v r$r', d['value'], d['ms_per_step'], d['final_loss'])"
-  done
-done
