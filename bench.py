@@ -99,6 +99,11 @@ def main():
         print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world.size}; using WORLD_SIZE", file=sys.stderr)
     N = world.size
     dev = torch.device("cuda", torch.cuda.current_device())
+    if os.environ.get("BENCH_HIPRIO") == "1":
+        # the training step on a high-priority stream (the weight-gradient side stream and the
+        # bucket comm stream stay at the default priority): A/B of CU arbitration between the
+        # input-gradient chain and the work beside it
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
     torch.backends.cudnn.benchmark = True
 
     import hipps

@@ -509,7 +509,9 @@ class PSAsyncEngine(Engine):
             self.acc = torch.zeros_like(store.data)
             # high priority: on a co-located PS (rank 0 also trains) the accumulate / update /
             # publish kernels must not queue behind worker 0's forward and backward launches
-            self.ps_stream = torch.cuda.Stream(device=store.device, priority=-1) if self.cuda else None
+            # (HIPPS_PS_PRIORITY=0: same priority as the worker's streams, for A/B)
+            prio = -1 if os.environ.get("HIPPS_PS_PRIORITY", "-1") != "0" else 0
+            self.ps_stream = torch.cuda.Stream(device=store.device, priority=prio) if self.cuda else None
             gs = self.gscale(self.M) / (1 + self.emu)  # emulated copies leave the average unchanged
             self.core = PSCore(self.ctl, C, W, self.nb, self.order, self.SLOTS, self.MAXSLOTS, self.M,
                                cfg.staleness, cfg.staleness_lr, gs, self._stats, bucketwise=self.bucketwise)
