@@ -12,6 +12,8 @@ models stay portable and the CPU test suite exercises the same module.
 """
 from __future__ import annotations
 
+import collections
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -74,12 +76,38 @@ def _same_layout(a, b):
     return a.shape == b.shape and all(sa == sb for n, sa, sb in zip(a.shape, a.stride(), b.stride()) if n > 1)
 
 
+def _joined(idx):
+    """The caller's stream now waits for the side stream: every input held for the side stream's
+    kernels may go back to the allocator (any later reuse of their blocks -- by allocations on the
+    caller's stream, the stream they belong to -- is ordered after those kernels)."""
+    _WG_UNJOINED.discard(idx)
+    h = _WG_HOLD.get(idx)
+    if h:
+        h.clear()
+
+
 def _join_wgrad(idx):
     torch.cuda.current_stream(idx).wait_stream(_WG_STREAMS[idx])
-    _WG_UNJOINED.discard(idx)
+    _joined(idx)
+
+
+def join_wgrad_stream(device):
+    """Make the current stream of ``device`` wait for its weight-gradient side stream."""
+    idx = device.index if isinstance(device, torch.device) else device
+    side = _WG_STREAMS.get(idx)
+    if side is not None:
+        torch.cuda.current_stream(idx).wait_stream(side)
+        _joined(idx)
 
 
 _WG_UNJOINED: set = set()  # devices whose side stream took work after the last backward's join
+# Inputs of in-flight side-stream weight gradients, with an event after each: kept referenced until
+# the event has passed or the caller's stream joined the side stream, then dropped.  This replaces
+# record_stream(): the caching allocator held every such activation-sized block back until a
+# side-stream event it records at free time had passed, and, with the side stream trailing the
+# main stream, kept creating new segments for the blocks still pending (~2.4 per step, 250 MB/step
+# of reserved memory growth with no end, profiles/r4/r4j/alloc_probe_*.txt)
+_WG_HOLD: dict = {}
 
 
 def wgrad_join_pending(device) -> bool:
@@ -105,16 +133,22 @@ def _on_wgrad_stream(param, tensors, fn):
     _WG_UNJOINED.add(idx)
     with torch.cuda.stream(side):
         out = fn()
-    for t in tensors:
-        t.record_stream(side)
+    hold = _WG_HOLD.get(idx)
+    if hold is None:
+        hold = _WG_HOLD[idx] = collections.deque()
+    while hold and hold[0][0].query():  # earlier weight gradients that have finished
+        hold.popleft()
+    ev = torch.cuda.Event()
+    ev.record(side)
+    hold.append((ev, tensors))
     if out.dtype != param.dtype or not _same_layout(out, param):
         cur.wait_stream(side)  # autograd would copy dw on this stream
-        _WG_UNJOINED.discard(idx)
+        _joined(idx)
     else:
         task = torch._C._current_graph_task_id()
         if task < 0:  # not inside an autograd backward pass
             cur.wait_stream(side)
-            _WG_UNJOINED.discard(idx)
+            _joined(idx)
         elif _WG_JOINED.get(idx) != task:
             torch.autograd.Variable._execution_engine.queue_callback(lambda: _join_wgrad(idx))
             _WG_JOINED[idx] = task

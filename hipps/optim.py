@@ -239,7 +239,7 @@ class MPI_PS(torch.optim.Optimizer):
             # so only a side-stream use outside a backward pass needs the join here (one event
             # record less on the host at every step boundary)
             if hnn.wgrad_stream(self.store.device) is not None and hnn.wgrad_join_pending(self.store.device):
-                torch.cuda.current_stream(self.store.device).wait_stream(hnn.wgrad_stream(self.store.device))
+                hnn.join_wgrad_stream(self.store.device)
         data = self.engine.step()
         self._refresh_shadow()
         now = time.perf_counter()

@@ -16,3 +16,13 @@ for r in 1 2; do
     python -c "import json;d=json.load(open('$O/ab_${v}_r$r.json'));print('$v r$r', d['value'], d['ms_per_step'], d['final_loss'], d['ps'].get('drops'), d.get('ps_staleness_mean'))"
   done
 done
+# allocator growth (profiles/r4/r4j: ~2.4 new activation-sized segments per step on the main stream):
+# without the weight-gradient side stream (its record_stream'd inputs), and with expandable segments
+for v in nows expand; do
+  case $v in
+    nows) E="HIPPS_WGRAD_STREAM=0";;
+    expand) E="PYTORCH_HIP_ALLOC_CONF=expandable_segments:True";;
+  esac
+  timeout -k 10 300 env $E python -u tools/alloc_probe.py --out $O/alloc_probe_$v.txt --steps 40 --warmup 5 > $O/alloc_probe_$v.log 2>&1 || { tail -20 $O/alloc_probe_$v.log; exit 1; }
+  echo "== $v"; head -12 $O/alloc_probe_$v.txt
+done
