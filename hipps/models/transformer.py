@@ -8,8 +8,10 @@
   *-tiny      same code, small widths, for CPU tests.
 
 Attention is ``F.scaled_dot_product_attention`` (the ROCm flash / mem-efficient kernels); the
-projections and MLPs are plain ``nn.Linear`` (hipBLASLt).  These models exercise the PS engine's
-bucketing/codec/transport at 100 M - 8 B parameters; they are not a kernel showcase.
+projections and MLPs are ``hipps.ops.nn.Linear`` (hipBLASLt GEMMs that read the engine's bf16
+weight shadow and write fp32 weight gradients directly; plain ``nn.Linear`` behaviour without a
+shadow).  These models exercise the PS engine's bucketing/codec/transport at 100 M - 8 B
+parameters; they are not a kernel showcase.
 """
 from __future__ import annotations
 
@@ -19,6 +21,8 @@ from dataclasses import dataclass
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from hipps.ops import nn as hnn
 
 
 def _ln(mod: nn.LayerNorm, x: torch.Tensor) -> torch.Tensor:
@@ -49,13 +53,13 @@ class BertLayer(nn.Module):
     def __init__(self, c: BertConfig):
         super().__init__()
         self.heads = c.heads
-        self.q = nn.Linear(c.hidden, c.hidden)
-        self.k = nn.Linear(c.hidden, c.hidden)
-        self.v = nn.Linear(c.hidden, c.hidden)
-        self.attn_out = nn.Linear(c.hidden, c.hidden)
+        self.q = hnn.Linear(c.hidden, c.hidden)
+        self.k = hnn.Linear(c.hidden, c.hidden)
+        self.v = hnn.Linear(c.hidden, c.hidden)
+        self.attn_out = hnn.Linear(c.hidden, c.hidden)
         self.attn_ln = nn.LayerNorm(c.hidden, eps=c.eps)
-        self.inter = nn.Linear(c.hidden, c.ffn)
-        self.out = nn.Linear(c.ffn, c.hidden)
+        self.inter = hnn.Linear(c.hidden, c.ffn)
+        self.out = hnn.Linear(c.ffn, c.hidden)
         self.out_ln = nn.LayerNorm(c.hidden, eps=c.eps)
 
     def forward(self, x, mask=None):
@@ -80,10 +84,10 @@ class Bert(nn.Module):
         self.tok_type = nn.Embedding(c.type_vocab, c.hidden)
         self.emb_ln = nn.LayerNorm(c.hidden, eps=c.eps)
         self.layers = nn.ModuleList([BertLayer(c) for _ in range(c.layers)])
-        self.pooler = nn.Linear(c.hidden, c.hidden)
+        self.pooler = hnn.Linear(c.hidden, c.hidden)
         self.mlm = mlm
         if mlm:
-            self.mlm_dense = nn.Linear(c.hidden, c.hidden)
+            self.mlm_dense = hnn.Linear(c.hidden, c.hidden)
             self.mlm_ln = nn.LayerNorm(c.hidden, eps=c.eps)
             self.mlm_bias = nn.Parameter(torch.zeros(c.vocab))
         self.apply(self._init)
@@ -106,7 +110,7 @@ class Bert(nn.Module):
         if not self.mlm:
             return x, pooled
         h = _ln(self.mlm_ln, F.gelu(self.mlm_dense(x)))
-        logits = F.linear(h, self.word.weight, self.mlm_bias)  # tied decoder
+        logits = hnn.linear(h, self.word.weight, self.mlm_bias)  # tied decoder
         if labels is None:
             return logits
         return F.cross_entropy(logits.float().view(-1, logits.shape[-1]), labels.view(-1), ignore_index=-100)
@@ -153,13 +157,13 @@ class LlamaBlock(nn.Module):
         super().__init__()
         self.c = c
         hd = c.dim // c.heads
-        self.wq = nn.Linear(c.dim, c.heads * hd, bias=False)
-        self.wk = nn.Linear(c.dim, c.kv_heads * hd, bias=False)
-        self.wv = nn.Linear(c.dim, c.kv_heads * hd, bias=False)
-        self.wo = nn.Linear(c.heads * hd, c.dim, bias=False)
-        self.w1 = nn.Linear(c.dim, c.ffn, bias=False)
-        self.w3 = nn.Linear(c.dim, c.ffn, bias=False)
-        self.w2 = nn.Linear(c.ffn, c.dim, bias=False)
+        self.wq = hnn.Linear(c.dim, c.heads * hd, bias=False)
+        self.wk = hnn.Linear(c.dim, c.kv_heads * hd, bias=False)
+        self.wv = hnn.Linear(c.dim, c.kv_heads * hd, bias=False)
+        self.wo = hnn.Linear(c.heads * hd, c.dim, bias=False)
+        self.w1 = hnn.Linear(c.dim, c.ffn, bias=False)
+        self.w3 = hnn.Linear(c.dim, c.ffn, bias=False)
+        self.w2 = hnn.Linear(c.ffn, c.dim, bias=False)
         self.attn_norm = RMSNorm(c.dim, c.eps)
         self.ffn_norm = RMSNorm(c.dim, c.eps)
 
@@ -186,7 +190,7 @@ class Llama(nn.Module):
         self.tok = nn.Embedding(c.vocab, c.dim)
         self.blocks = nn.ModuleList([LlamaBlock(c) for _ in range(c.layers)])
         self.norm = RMSNorm(c.dim, c.eps)
-        self.head = nn.Linear(c.dim, c.vocab, bias=False)
+        self.head = hnn.Linear(c.dim, c.vocab, bias=False)
         for m in self.modules():
             if isinstance(m, (nn.Linear, nn.Embedding)):
                 nn.init.normal_(m.weight, std=0.02)

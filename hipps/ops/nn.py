@@ -62,6 +62,8 @@ MASK_NONE, MASK_X, MASK_Y, MASK_BITS = 0, 1, 2, 3
 # hooks, and whose dw has the parameter's layout: autograd then stores dw as is (no accumulate or
 # layout copy on the main stream that would read it early).
 _WGRAD_SIDE = _os.environ.get("HIPPS_WGRAD_STREAM", "1") != "0"
+# nn.Linear on the bf16 weight shadow with an fp32 weight gradient (_ShadowLinear); 0: F.linear
+_SHADOW_LINEAR = _os.environ.get("HIPPS_SHADOW_LINEAR", "1") != "0"
 _WG_STREAMS: dict = {}
 _WG_JOINED: dict = {}  # device -> autograd graph task whose end joins the side stream
 
@@ -108,6 +110,7 @@ _WG_UNJOINED: set = set()  # devices whose side stream took work after the last 
 # main stream, kept creating new segments for the blocks still pending (~2.4 per step, 250 MB/step
 # of reserved memory growth with no end, profiles/r4/r4j/alloc_probe_*.txt)
 _WG_HOLD: dict = {}
+_WG_SEEN: dict = {}  # device -> (graph task id, ids of the parameters whose dw went to the side stream)
 
 
 def wgrad_join_pending(device) -> bool:
@@ -129,6 +132,15 @@ def _on_wgrad_stream(param, tensors, fn):
     if side is None:
         side = _WG_STREAMS[idx] = torch.cuda.Stream(device=dev)
     cur = torch.cuda.current_stream(dev)
+    # a weight used twice in one graph (weight sharing): autograd sums its gradient contributions
+    # on the caller's stream before the single AccumulateGrad, so from the second one on the
+    # caller's stream waits for the side stream (covering the earlier contributions too)
+    task = torch._C._current_graph_task_id()
+    seen = _WG_SEEN.get(idx)
+    if seen is None or seen[0] != task:
+        seen = _WG_SEEN[idx] = (task, set())
+    repeat = id(param) in seen[1]
+    seen[1].add(id(param))
     side.wait_stream(cur)
     _WG_UNJOINED.add(idx)
     with torch.cuda.stream(side):
@@ -141,11 +153,10 @@ def _on_wgrad_stream(param, tensors, fn):
     ev = torch.cuda.Event()
     ev.record(side)
     hold.append((ev, tensors))
-    if out.dtype != param.dtype or not _same_layout(out, param):
-        cur.wait_stream(side)  # autograd would copy dw on this stream
+    if repeat or out.dtype != param.dtype or not _same_layout(out, param):
+        cur.wait_stream(side)  # autograd sums / copies dw on this stream
         _joined(idx)
     else:
-        task = torch._C._current_graph_task_id()
         if task < 0:  # not inside an autograd backward pass
             cur.wait_stream(side)
             _joined(idx)
@@ -646,6 +657,78 @@ def bf16_weight(w: torch.Tensor) -> torch.Tensor:
         if base <= p < base + flat.numel() * 4 and w.device == flat.device:
             return sh.as_strided(w.shape, w.stride(), (p - base) // 4)
     return w.to(torch.bfloat16)
+
+
+def has_weight_shadow(w: torch.Tensor) -> bool:
+    """Is fp32 parameter ``w`` inside a registered bf16 shadow (bf16_weight returns a view)?"""
+    if w.dtype != torch.float32 or not w.is_cuda:
+        return False
+    p = w.data_ptr()
+    return any(flat.data_ptr() <= p < flat.data_ptr() + flat.numel() * 4 and w.device == flat.device
+               for flat, _ in _SHADOWS)
+
+
+class _ShadowLinear(torch.autograd.Function):
+    """y = x W^T + b under bf16 autocast for an fp32 master weight with a bf16 shadow: the GEMM
+    reads the shadow (refreshed once per step by the optimizer) instead of autocast casting W
+    every forward, and the backward writes dW in fp32 straight from the GEMM (hipBLASLt
+    ``mm(..., out_dtype=float32)``) instead of a bf16 dW plus a cast kernel into the fp32 grad.
+    BERT-base spent ~3 ms of a 38.8 ms step in those casts (profiles/r4/r4n/)."""
+
+    @staticmethod
+    def forward(ctx, x, w_master, bias):
+        dt = torch.bfloat16
+        w = bf16_weight(w_master)
+        x2 = x.reshape(-1, x.shape[-1])
+        if x2.dtype != dt:
+            x2 = x2.to(dt)
+        if bias is not None:
+            y = torch.addmm(bf16_weight(bias), x2, w.t())
+        else:
+            y = torch.mm(x2, w.t())
+        ctx.save_for_backward(x2, w_master)
+        ctx.has_bias = bias is not None
+        ctx.xshape, ctx.xdtype = x.shape, x.dtype
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w_master = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if dy2.dtype != torch.bfloat16:
+            dy2 = dy2.to(torch.bfloat16)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.mm(dy2, bf16_weight(w_master)).view(ctx.xshape)
+            if dx.dtype != ctx.xdtype:
+                dx = dx.to(ctx.xdtype)
+        if ctx.needs_input_grad[1]:
+            # (on the caller's stream: a linear weight may be used twice in a graph -- a tied
+            # decoder, a reused module -- and autograd sums such contributions on this stream)
+            dw = torch.mm(dy2.t(), x2, out_dtype=torch.float32)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = torch.sum(dy2, 0, dtype=torch.float32)
+        return dx, dw, db
+
+
+def shadow_linear_ok(x: torch.Tensor, weight: torch.Tensor, bias=None) -> bool:
+    return (_SHADOW_LINEAR and x.is_cuda and torch.is_autocast_enabled() and
+            torch.get_autocast_dtype("cuda") == torch.bfloat16 and has_weight_shadow(weight) and
+            (bias is None or has_weight_shadow(bias)))
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
+    """F.linear, on the bf16 weight shadow when one covers ``weight`` (see _ShadowLinear)."""
+    if shadow_linear_ok(x, weight, bias):
+        return _ShadowLinear.apply(x, weight, bias)
+    return F.linear(x, weight, bias)
+
+
+class Linear(nn.Linear):
+    """nn.Linear that reads the bf16 weight shadow under bf16 autocast (hipps.ops.nn.linear)."""
+
+    def forward(self, x):
+        return linear(x, self.weight, self.bias)
 
 
 class _Conv1x1(torch.autograd.Function):

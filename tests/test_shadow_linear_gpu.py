@@ -1,0 +1,156 @@
+"""hipps.ops.nn.Linear / linear on the bf16 weight shadow (_ShadowLinear) against F.linear under
+bf16 autocast, the transformer models on it, and weight sharing on the weight-gradient side
+stream (a weight used twice in one graph)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _shadowed(*shapes):
+    """fp32 parameters as views of one flat buffer with a registered bf16 shadow."""
+    from hipps.ops import nn as hnn
+
+    n = sum(torch.Size(s).numel() for s in shapes)
+    flat = torch.randn(n, device=DEV) * 0.05
+    shadow = flat.to(torch.bfloat16)
+    hnn.register_weight_shadow(flat, shadow)
+    out, o = [], 0
+    for s in shapes:
+        k = torch.Size(s).numel()
+        out.append(torch.nn.Parameter(flat[o:o + k].view(s)))
+        o += k
+    return flat, shadow, out
+
+
+def test_shadow_linear_matches_autocast_linear():
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(0)
+    flat, shadow, (w, b) = _shadowed((96, 64), (96,))
+    try:
+        x = torch.randn(4, 33, 64, device=DEV, requires_grad=True)
+        x0 = x.detach().clone().requires_grad_(True)
+        w0 = torch.nn.Parameter(w.detach().clone())
+        b0 = torch.nn.Parameter(b.detach().clone())
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            assert hnn.shadow_linear_ok(x, w, b)
+            y = hnn.linear(x, w, b)
+            y0 = F.linear(x0, w0, b0)
+        assert y.dtype == torch.bfloat16 and y.shape == y0.shape
+        torch.testing.assert_close(y.float(), y0.float(), rtol=1e-2, atol=1e-2)
+        g = torch.randn_like(y)
+        y.backward(g)
+        y0.backward(g)
+        assert w.grad.dtype == torch.float32 and x.grad.dtype == torch.float32
+        torch.testing.assert_close(x.grad, x0.grad, rtol=2e-2, atol=2e-2)
+        torch.testing.assert_close(w.grad, w0.grad, rtol=2e-2, atol=2e-2)
+        torch.testing.assert_close(b.grad, b0.grad, rtol=2e-2, atol=2e-2)
+        # fp32 reference of the same op
+        ref = torch.nn.functional.linear(x0.detach().double(), w0.detach().double(), b0.detach().double())
+        torch.testing.assert_close(y.double(), ref, rtol=3e-2, atol=3e-2)
+    finally:
+        hnn.unregister_weight_shadow(shadow)
+
+
+def test_shadow_linear_tied_weight_used_twice():
+    """A weight used twice in one forward (tied decoder): both contributions summed exactly once."""
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(1)
+    flat, shadow, (w,) = _shadowed((80, 48))
+    try:
+        x = torch.randn(16, 48, device=DEV)
+        w0 = torch.nn.Parameter(w.detach().clone())
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            h = hnn.linear(x, w)             # [16, 80]
+            y = hnn.linear(h[:, :48], w)
+            h0 = F.linear(x, w0)
+            y0 = F.linear(h0[:, :48], w0)
+        y.float().sum().backward()
+        y0.float().sum().backward()
+        torch.testing.assert_close(w.grad, w0.grad, rtol=3e-2, atol=3e-2)
+    finally:
+        hnn.unregister_weight_shadow(shadow)
+
+
+def test_conv_weight_shared_twice_on_side_stream():
+    """The same hipps 3x3 conv applied twice in one graph: its two weight-gradient contributions
+    (both on the side stream) are summed by autograd on the caller's stream only after both
+    finished."""
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(2)
+    conv = torch.nn.Conv2d(64, 64, 3, padding=1, bias=False).cuda().to(memory_format=torch.channels_last)
+    ref = torch.nn.Conv2d(64, 64, 3, padding=1, bias=False).cuda().to(memory_format=torch.channels_last)
+    ref.weight.data.copy_(conv.weight.data)
+    x = torch.randn(8, 64, 14, 14, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = hnn.conv2d(conv, hnn.conv2d(conv, x, fuse=True), fuse=True)
+        y0 = ref(ref(x))
+    g = torch.randn_like(y0)
+    y.backward(g)
+    y0.backward(g)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(conv.weight.grad.float(), ref.weight.grad.float(), rtol=5e-2, atol=5e-2)
+
+
+@pytest.mark.parametrize("name", ["bert-tiny", "llama-tiny"])
+def test_transformer_steps_shadow_linear_vs_autocast(name):
+    """Four steps of the tiny transformers with the bf16 shadow on: the Linear layers on
+    _ShadowLinear track plain autocast F.linear (the dW precision differs: fp32 from the GEMM vs
+    a bf16 dW cast up), and the loss goes down."""
+    import hipps
+    from hipps.models.transformer import build
+    from hipps.ops import nn as hnn
+
+    def run(shadow_linear):
+        saved = hnn._SHADOW_LINEAR
+        hnn._SHADOW_LINEAR = shadow_linear
+        torch.manual_seed(3)
+        m = build(name).cuda()
+        opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="local", bf16_weights="on")
+        ids = torch.randint(0, 512, (4, 32), device=DEV, generator=torch.Generator(device=DEV).manual_seed(4))
+        losses = []
+        try:
+            for _ in range(4):
+                opt.zero_grad()
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    loss = m(ids, ids)
+                loss.backward()
+                opt.step()
+                losses.append(loss.item())
+        finally:
+            opt.close()
+            hnn._SHADOW_LINEAR = saved
+        return losses
+
+    on, off = run(True), run(False)
+    assert all(v == v for v in on) and on[-1] < on[0]
+    torch.testing.assert_close(torch.tensor(on), torch.tensor(off), rtol=2e-2, atol=2e-2)
+
+
+def test_transformer_async_step_on_shadow_linear():
+    """The default async path (bf16 shadow auto-on for ps_async on a GPU) with the tiny BERT."""
+    import hipps
+    from hipps.models.transformer import build
+
+    torch.manual_seed(5)
+    m = build("bert-tiny").cuda()
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", max_delay=0)
+    ids = torch.randint(0, 512, (4, 32), device=DEV)
+    losses = []
+    try:
+        for _ in range(6):
+            opt.zero_grad()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = m(ids, ids)
+            loss.backward()
+            opt.step()
+            losses.append(loss.item())
+    finally:
+        opt.close()
+    assert all(v == v for v in losses) and losses[-1] < losses[0]
