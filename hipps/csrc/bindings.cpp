@@ -1,5 +1,6 @@
 // hipps._C — pybind11 bindings for the CDNA4 kernels and the native PS runtime.
 #include <torch/extension.h>
+#include <vector>
 
 namespace hipps {
 // flat.hip
@@ -97,6 +98,9 @@ void bn_finalize_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tensor we
                           at::Tensor mean, at::Tensor invstd, at::Tensor scale, at::Tensor shift, int64_t C, double eps,
                           double momentum);
 void maxpool3s2_backward(at::Tensor dy, at::Tensor code, at::Tensor dx);
+std::vector<at::Tensor> xent_forward(at::Tensor logits, at::Tensor labels, int64_t ignore_index);
+void xent_backward(at::Tensor logits, at::Tensor labels, at::Tensor lse, at::Tensor gout, double scale,
+                   int64_t ignore_index, at::Tensor dx);
 void bn_finalize_bwd_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tensor weight, at::Tensor mean,
                               at::Tensor invstd, at::Tensor dweight, at::Tensor dbias, at::Tensor coef);
 void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64_t Wi, int64_t stride,
@@ -231,6 +235,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("shift") = pybind11::none());
   m.def("bn_finalize_partials", &hipps::bn_finalize_partials,
         "BN train-mode finalize from producer partial sums (mean/invstd/scale/shift + running stats)");
+  m.def("xent_forward", &hipps::xent_forward,
+        "fused softmax cross-entropy over bf16 logits: per-row loss and log-sum-exp (one read of the row)");
+  m.def("xent_backward", &hipps::xent_backward, "cross-entropy gradient (softmax - onehot) * g * scale, bf16");
   m.def("bn_finalize_bwd_partials", &hipps::bn_finalize_bwd_partials,
         "BN backward finalize from partial sums (dweight, dbias, dx coefficients [3, C])");
   m.def("maxpool3s2_backward", &hipps::maxpool3s2_backward, "3x3/s2/p1 max pool backward (gather form, no atomics)");

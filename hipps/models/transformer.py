@@ -113,7 +113,7 @@ class Bert(nn.Module):
         logits = hnn.linear(h, self.word.weight, self.mlm_bias)  # tied decoder
         if labels is None:
             return logits
-        return F.cross_entropy(logits.float().view(-1, logits.shape[-1]), labels.view(-1), ignore_index=-100)
+        return hnn.cross_entropy(logits, labels, ignore_index=-100)
 
 
 # ------------------------------------------------------------------------------------- Llama
@@ -212,7 +212,7 @@ class Llama(nn.Module):
         logits = self.head(self.norm(x))
         if labels is None:
             return logits
-        return F.cross_entropy(logits.float().view(-1, logits.shape[-1]), labels.view(-1))
+        return hnn.cross_entropy(logits, labels)
 
 
 def build(name: str, **kw):

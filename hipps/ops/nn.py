@@ -64,6 +64,8 @@ MASK_NONE, MASK_X, MASK_Y, MASK_BITS = 0, 1, 2, 3
 _WGRAD_SIDE = _os.environ.get("HIPPS_WGRAD_STREAM", "1") != "0"
 # nn.Linear on the bf16 weight shadow with an fp32 weight gradient (_ShadowLinear); 0: F.linear
 _SHADOW_LINEAR = _os.environ.get("HIPPS_SHADOW_LINEAR", "1") != "0"
+# softmax cross-entropy of bf16 logits on csrc/xent.hip (hipps.ops.nn.cross_entropy); 0: PyTorch
+_FUSED_XENT = _os.environ.get("HIPPS_FUSED_XENT", "1") != "0"
 _WG_STREAMS: dict = {}
 _WG_JOINED: dict = {}  # device -> autograd graph task whose end joins the side stream
 
@@ -729,6 +731,38 @@ class Linear(nn.Linear):
 
     def forward(self, x):
         return linear(x, self.weight, self.bias)
+
+
+class _CrossEntropy(torch.autograd.Function):
+    """Mean softmax cross-entropy of bf16 logits [rows, vocab] (csrc/xent.hip): one read of the
+    logits in the forward (online log-sum-exp), one read + one bf16 gradient write in the
+    backward; no fp32 copy of the logits."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index):
+        loss_rows, lse = native().xent_forward(logits, labels, int(ignore_index))
+        n = (labels != ignore_index).sum().clamp_min(1).to(torch.float32)
+        ctx.save_for_backward(logits, labels, lse, n)
+        ctx.ignore = int(ignore_index)
+        return loss_rows.sum() / n
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, labels, lse, n = ctx.saved_tensors
+        dx = torch.empty_like(logits)
+        gs = (g.to(torch.float32) / n).reshape(1).contiguous()
+        native().xent_backward(logits, labels, lse, gs, 1.0, ctx.ignore, dx)
+        return dx, None, None
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
+    """F.cross_entropy(logits.float(), labels, ignore_index=...) (mean over non-ignored rows) on
+    the fused kernel for contiguous bf16 device logits [.., vocab]; the PyTorch route otherwise."""
+    V = logits.shape[-1]
+    if (_FUSED_XENT and logits.is_cuda and logits.dtype == torch.bfloat16 and labels.dtype == torch.int64
+            and labels.numel() * V == logits.numel()):
+        return _CrossEntropy.apply(logits.reshape(-1, V).contiguous(), labels.reshape(-1).contiguous(), ignore_index)
+    return F.cross_entropy(logits.float().reshape(-1, V), labels.reshape(-1), ignore_index=ignore_index)
 
 
 class _Conv1x1(torch.autograd.Function):
