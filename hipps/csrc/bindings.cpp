@@ -99,6 +99,7 @@ void bn_finalize_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tensor we
                           double momentum);
 void maxpool3s2_backward(at::Tensor dy, at::Tensor code, at::Tensor dx);
 std::vector<at::Tensor> xent_forward(at::Tensor logits, at::Tensor labels, int64_t ignore_index);
+void colsum_bf16(at::Tensor x, at::Tensor out);
 void xent_backward(at::Tensor logits, at::Tensor labels, at::Tensor lse, at::Tensor gout, double scale,
                    int64_t ignore_index, at::Tensor dx);
 void bn_finalize_bwd_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tensor weight, at::Tensor mean,
@@ -235,6 +236,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("shift") = pybind11::none());
   m.def("bn_finalize_partials", &hipps::bn_finalize_partials,
         "BN train-mode finalize from producer partial sums (mean/invstd/scale/shift + running stats)");
+  m.def("colsum_bf16", &hipps::colsum_bf16, "fp32 column sums of a bf16 [rows, cols] matrix (bias gradients)");
   m.def("xent_forward", &hipps::xent_forward,
         "fused softmax cross-entropy over bf16 logits: per-row loss and log-sum-exp (one read of the row)");
   m.def("xent_backward", &hipps::xent_backward, "cross-entropy gradient (softmax - onehot) * g * scale, bf16");

@@ -709,8 +709,19 @@ class _ShadowLinear(torch.autograd.Function):
             # decoder, a reused module -- and autograd sums such contributions on this stream)
             dw = torch.mm(dy2.t(), x2, out_dtype=torch.float32)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = torch.sum(dy2, 0, dtype=torch.float32)
+            db = colsum_f32(dy2)
         return dx, dw, db
+
+
+def colsum_f32(t: torch.Tensor) -> torch.Tensor:
+    """t.sum(0) in fp32 for a 2-d bf16 device tensor (csrc/xent.hip k_colsum: deterministic,
+    ~4x PyTorch's reduce on a bias gradient); torch.sum otherwise."""
+    if (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.is_contiguous() and t.shape[1] % 8 == 0
+            and t.data_ptr() % 16 == 0):
+        out = torch.empty(t.shape[1], dtype=torch.float32, device=t.device)
+        native().colsum_bf16(t, out)
+        return out
+    return torch.sum(t, 0, dtype=torch.float32)
 
 
 def shadow_linear_ok(x: torch.Tensor, weight: torch.Tensor, bias=None) -> bool:

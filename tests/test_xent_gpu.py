@@ -42,3 +42,16 @@ def test_fused_cross_entropy_in_3d_lm_head_layout():
     torch.testing.assert_close(loss.float(), loss0, rtol=1e-4, atol=1e-4)
     loss.backward()
     assert x.grad.shape == x.shape and torch.isfinite(x.grad.float()).all()
+
+
+@pytest.mark.parametrize("rows,cols", [(16384, 768), (333, 3072), (5, 8), (1, 64), (4097, 1000)])
+def test_colsum_matches_fp32(rows, cols):
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(rows)
+    t = torch.randn(rows, cols, device="cuda").to(torch.bfloat16)
+    got = hnn.colsum_f32(t)
+    ref = t.double().sum(0)
+    assert got.dtype == torch.float32
+    torch.testing.assert_close(got.double(), ref, rtol=1e-5, atol=1e-3)
+    assert torch.equal(got, hnn.colsum_f32(t))  # deterministic
