@@ -707,10 +707,40 @@ class _ShadowLinear(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             # (on the caller's stream: a linear weight may be used twice in a graph -- a tied
             # decoder, a reused module -- and autograd sums such contributions on this stream)
-            dw = torch.mm(dy2.t(), x2, out_dtype=torch.float32)
+            dw = _linear_wgrad(dy2, x2)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = colsum_f32(dy2)
         return dx, dw, db
+
+
+def _linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+    """dW = dy2^T x2 in fp32 ([N, K] from bf16 [M, N] and [M, K]): the faster, per shape, of
+    hipBLASLt (mm with an fp32 output) and the gemm2 split-M weight-gradient kernels (a Linear's
+    dW is a 1x1 convolution's).  hipBLASLt picked 64x64 macro tiles for BERT-base's 768-wide
+    dW GEMMs (M = 16384 tokens): 186 TFLOP/s (profiles/r4/r4n/)."""
+    M, N = dy2.shape
+    K = x2.shape[1]
+    dw = torch.empty((N, K), dtype=torch.float32, device=dy2.device)
+
+    def mm():
+        torch.ops.aten.mm.dtype_out(dy2.t(), x2, torch.float32, out=dw)
+
+    if not (_GEMM2 and N % 64 == 0 and K % 64 == 0 and M >= 1024 and dy2.is_contiguous() and x2.is_contiguous()
+            and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0):
+        mm()
+        return dw
+    C = native()
+    cands = {"mm": mm}
+    ok = {0: True, 1: N % 256 == 0 and K % 128 == 0, 2: N % 256 == 0 and K % 256 == 0,
+          3: N % 128 == 0 and K % 256 == 0, 4: N % 256 == 0 and K % 128 == 0}
+    for cfg in (0, 1, 2, 3, 4):
+        if ok[cfg]:
+            for ns in ((2, 3) if cfg != 2 else (2, 4)):
+                cands[f"w3_{cfg}" + ("" if ns == 2 else f"s{ns}")] = (
+                    lambda cfg=cfg, ns=ns: C.gemm2_wgrad(dy2, x2, dw, 1, 1, 1, 0, 1, 1, cfg, ns))
+    name = TUNER.pick(("lwgrad", M, N, K), cands)
+    cands[name]()
+    return dw
 
 
 def colsum_f32(t: torch.Tensor) -> torch.Tensor:

@@ -159,3 +159,17 @@ def test_transformer_async_step_on_shadow_linear():
     finally:
         opt.close()
     assert all(v == v for v in losses) and losses[-1] < losses[0]
+
+
+@pytest.mark.parametrize("m,n,k", [(4096, 768, 768), (2048, 3072, 768), (2048, 768, 3072), (1024, 192, 64), (100, 96, 48)])
+def test_linear_wgrad_matches_fp32(m, n, k):
+    """The tuner-picked Linear weight gradient (hipBLASLt or a gemm2 split-M kernel) against fp64."""
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(m + n + k)
+    dy = torch.randn(m, n, device=DEV).to(torch.bfloat16)
+    x = torch.randn(m, k, device=DEV).to(torch.bfloat16)
+    dw = hnn._linear_wgrad(dy, x)
+    ref = dy.double().t() @ x.double()
+    assert dw.dtype == torch.float32 and dw.shape == (n, k)
+    torch.testing.assert_close(dw.double(), ref, rtol=1e-3, atol=1e-2 * (m ** 0.5) / 16)
