@@ -173,3 +173,17 @@ def test_linear_wgrad_matches_fp32(m, n, k):
     ref = dy.double().t() @ x.double()
     assert dw.dtype == torch.float32 and dw.shape == (n, k)
     torch.testing.assert_close(dw.double(), ref, rtol=1e-3, atol=1e-2 * (m ** 0.5) / 16)
+
+
+@pytest.mark.parametrize("m,n,k", [(4096, 768, 768), (2048, 3072, 1024), (1024, 4096, 512), (200, 128, 64)])
+def test_linear_fwd_nobias_matches_fp32(m, n, k):
+    """The tuner-picked bias-free Linear forward (hipBLASLt or a hipps 1x1 GEMM core) against fp64."""
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(m + n)
+    x = torch.randn(m, k, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(n, k, device=DEV) / k ** 0.5).to(torch.bfloat16)
+    y = hnn._linear_fwd_nobias(x, w)
+    ref = x.double() @ w.double().t()
+    assert y.dtype == torch.bfloat16 and y.shape == (m, n)
+    torch.testing.assert_close(y.double(), ref, rtol=1e-2, atol=1e-2)
