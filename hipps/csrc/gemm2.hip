@@ -54,7 +54,10 @@ __device__ __attribute__((aligned(64))) const uint16_t kZero16[32] = {0};
 // per K channel -- every thread transforms the 16-byte chunks it staged, in LDS, after its own
 // DMA landed and before the tile's barrier (rows / taps that read the zero page stay zero), so
 // the BN's output is never written (ResNet bn1 -> conv2, bn2 -> conv3)
-enum Epi : int { kPlain = 0, kStats = 1, kAdd = 2, kBst = 4, kBstBits = 8, kAddS2 = 16, kPar = 32, kPro = 64 };
+// kBias (1x1 only, alone): y = x w^T + bias[col], the fp32 bias added to the fp32 accumulator
+// before the one bf16 rounding (a Linear layer's addmm)
+enum Epi : int { kPlain = 0, kStats = 1, kAdd = 2, kBst = 4, kBstBits = 8, kAddS2 = 16, kPar = 32, kPro = 64,
+                 kBias = 128 };
 
 template <int BM, int BN> struct Cfg;
 template <> struct Cfg<256, 256> { static constexpr int TM = 128, TN = 64; };
@@ -90,6 +93,7 @@ struct Args {
   int ph, pw, Hx, Wx;  // kPar: output parity class and the dx grid
   int tdr[4], tdc[4], tko[4];
   const float *psc, *psh;  // kPro: per-channel scale / shift of the A operand's BN
+  const float* bias;       // kBias: f32 [N]
 };
 
 __device__ __forceinline__ uint32_t add_bf16x2(uint32_t a, uint32_t b) {
@@ -440,16 +444,18 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   float* st = reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(lds) + SCR);
   constexpr bool STATS = (EPI & kStats) != 0, ADD = (EPI & kAdd) != 0;
   constexpr int BST = (EPI & kBstBits) ? 2 : (EPI & kBst) ? 1 : 0;
+  constexpr bool BIAS = (EPI & kBias) != 0;
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int col = wn * TN + j * 16 + (lane & 15);
+    const float bcol = BIAS ? g.bias[n0 + col] : 0.f;
     float s = 0.f, qq = 0.f;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
-        const uint16_t hb = f32_to_bf16(acc[i][j][r]);
+        const uint16_t hb = f32_to_bf16(BIAS ? acc[i][j][r] + bcol : acc[i][j][r]);
         lds[row * EP + col] = hb;
         if (STATS) {  // rows past M hold zeros (zero-page operands)
           const float v = bf16_to_f32(hb);
@@ -1032,7 +1038,8 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
                 c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_bits, c10::optional<at::Tensor> bn_mean,
                 c10::optional<at::Tensor> bn_invstd, c10::optional<at::Tensor> bn_scale,
                 c10::optional<at::Tensor> bn_shift, int64_t stages, bool add_s2,
-                c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift) {
+                c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift,
+                c10::optional<at::Tensor> bias) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "gemm2: device tensors");
   TORCH_CHECK(stages >= 2 && stages <= 4, "gemm2: stages must be 2, 3 or 4 (k-half units)");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
@@ -1128,6 +1135,13 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
     a.psh = pro_shift->data_ptr<float>();
     epi |= g2::kPro;
   }
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(epi == g2::kPlain && !taps, "gemm2: the bias epilogue runs alone on a 1x1 GEMM");
+    TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() == N,
+                "gemm2: bias must be f32 [Cout]");
+    a.bias = bias->data_ptr<float>();
+    epi = g2::kBias;
+  }
   auto stream = c10::hip::getCurrentHIPStream();
   const int grid = (int)(mtiles * ntiles);
 #define HIPPS_G2S(BMc, BNc, EPc, TPc, NSc) \
@@ -1153,6 +1167,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
         case g2::kStats | g2::kPro: HIPPS_G2S(BMc, BNc, (g2::kStats | g2::kPro), false, 2); break;   \
         case g2::kStats: HIPPS_G2(BMc, BNc, g2::kStats, false); break;                              \
         case g2::kAdd: HIPPS_G2(BMc, BNc, g2::kAdd, false); break;                                  \
+        case g2::kBias: HIPPS_G2(BMc, BNc, g2::kBias, false); break;                                \
         case g2::kBst: HIPPS_G2(BMc, BNc, g2::kBst, false); break;                                  \
         case g2::kBst | g2::kAdd: HIPPS_G2(BMc, BNc, (g2::kBst | g2::kAdd), false); break;          \
         case g2::kBstBits: HIPPS_G2(BMc, BNc, g2::kBstBits, false); break;                          \

@@ -13,6 +13,7 @@ models stay portable and the CPU test suite exercises the same module.
 from __future__ import annotations
 
 import collections
+from typing import Optional
 
 import torch
 import torch.nn as nn
@@ -684,10 +685,7 @@ class _ShadowLinear(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         if x2.dtype != dt:
             x2 = x2.to(dt)
-        if bias is not None:
-            y = torch.addmm(bf16_weight(bias), x2, w.t())
-        else:
-            y = _linear_fwd_nobias(x2, w)
+        y = _linear_fwd(x2, w, bias)
         ctx.save_for_backward(x2, w_master)
         ctx.has_bias = bias is not None
         ctx.xshape, ctx.xdtype = x.shape, x.dtype
@@ -713,29 +711,40 @@ class _ShadowLinear(torch.autograd.Function):
         return dx, dw, db
 
 
-def _linear_fwd_nobias(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """y = x2 w^T (bf16 [M, K] x [N, K] -> [M, N]): per shape the faster of hipBLASLt and the
-    hipps 1x1-convolution GEMM cores (a bias-free Linear is a 1x1 convolution over M pixels)."""
+def _linear_fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x2 w^T (+ bias) (bf16 [M, K] x [N, K] -> [M, N]): per shape the faster of hipBLASLt
+    (mm / addmm with the bf16 bias) and the hipps 1x1-convolution GEMM cores (a Linear is a 1x1
+    convolution over M pixels; their kBias epilogue adds the fp32 master bias to the fp32
+    accumulator before the one bf16 rounding)."""
     M, K = x2.shape
     N = w.shape[0]
     y = torch.empty((M, N), dtype=torch.bfloat16, device=x2.device)
 
     def blas():
-        torch.mm(x2, w.t(), out=y)
+        if bias is None:
+            torch.mm(x2, w.t(), out=y)
+        else:
+            torch.addmm(bf16_weight(bias), x2, w.t(), out=y)
 
     if not (_GEMM2 and N % 64 == 0 and K % 64 == 0 and M >= 1024 and x2.is_contiguous() and w.is_contiguous()
-            and x2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and y.data_ptr() % 16 == 0):
+            and x2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and y.data_ptr() % 16 == 0
+            and (bias is None or (bias.dtype == torch.float32 and bias.is_contiguous() and bias.numel() == N))):
         blas()
         return y
     C = native()
     cands = {"blas": blas}
+    b = None if bias is None else bias.detach()
     for name in _g2_names(N):
         bm, bn, ns = _g2_parse(name)
         cands[name] = (lambda bm=bm, bn=bn, ns=ns:
-                       C.gemm2_conv(x2, w, y, None, None, None, 1, 1, 1, 1, 1, 0, bm, bn, stages=ns))
-    pick = TUNER.pick(("lfwd", M, N, K), cands)
+                       C.gemm2_conv(x2, w, y, None, None, None, 1, 1, 1, 1, 1, 0, bm, bn, stages=ns, bias=b))
+    pick = TUNER.pick(("lfwd", M, N, K, bias is not None), cands)
     cands[pick]()
     return y
+
+
+def _linear_fwd_nobias(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    return _linear_fwd(x2, w)
 
 
 def _linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:

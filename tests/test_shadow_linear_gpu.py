@@ -187,3 +187,26 @@ def test_linear_fwd_nobias_matches_fp32(m, n, k):
     ref = x.double() @ w.double().t()
     assert y.dtype == torch.bfloat16 and y.shape == (m, n)
     torch.testing.assert_close(y.double(), ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("m,n,k", [(4096, 768, 768), (2048, 3072, 768), (4096, 768, 3072), (200, 128, 64)])
+def test_linear_fwd_bias_matches_fp32(m, n, k):
+    """The tuner-picked biased Linear forward (hipBLASLt addmm or a hipps 1x1 GEMM core with the
+    fp32 kBias epilogue) against fp64; every gemm2 candidate is also checked on its own."""
+    from hipps.ops import nn as hnn
+    from hipps.ops._native import native
+
+    torch.manual_seed(m + n + 7)
+    x = torch.randn(m, k, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(n, k, device=DEV) / k ** 0.5).to(torch.bfloat16)
+    b = torch.randn(n, device=DEV)
+    y = hnn._linear_fwd(x, w, b)
+    ref = x.double() @ w.double().t() + b.double()
+    assert y.dtype == torch.bfloat16 and y.shape == (m, n)
+    torch.testing.assert_close(y.double(), ref, rtol=1e-2, atol=1e-2)
+    if m >= 1024:
+        for name in hnn._g2_names(n):
+            bm, bn, ns = hnn._g2_parse(name)
+            y2 = torch.full_like(y, float("nan"))
+            native().gemm2_conv(x, w, y2, None, None, None, 1, 1, 1, 1, 1, 0, bm, bn, stages=ns, bias=b)
+            torch.testing.assert_close(y2.double(), ref, rtol=1e-2, atol=1e-2, msg=name)
