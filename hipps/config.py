@@ -98,8 +98,8 @@ class PSConfig:
     param_wire: str = "auto"
     # bf16 weight shadow: one flat bf16 copy of the fp32 params, refreshed by one cast kernel after
     # every step()/irequest_params(), read by the hipps conv kernels instead of one autocast cast
-    # per layer per forward.  'auto' = on for ps_async on a GPU for models with conv weights (the
-    # engine owns the params there:
+    # per layer per forward.  'auto' = on for ps_async on a GPU for models with conv or Linear
+    # weights (hipps.ops.nn.Linear reads it too; the engine owns the params there:
     # any out-of-band edit is overwritten by the next adoption anyway); 'on' | 'off' otherwise.
     # With 'on', call opt.refresh_bf16_weights() after editing params outside step().
     bf16_weights: str = "auto"

@@ -90,6 +90,7 @@ class Bert(nn.Module):
             self.mlm_dense = hnn.Linear(c.hidden, c.hidden)
             self.mlm_ln = nn.LayerNorm(c.hidden, eps=c.eps)
             self.mlm_bias = nn.Parameter(torch.zeros(c.vocab))
+            hnn.mark_shadow_reader(self.word.weight, self.mlm_bias)  # the tied decoder's hnn.linear
         self.apply(self._init)
 
     @staticmethod

@@ -788,6 +788,14 @@ def colsum_f32(t: torch.Tensor) -> torch.Tensor:
     return torch.sum(t, 0, dtype=torch.float32)
 
 
+def mark_shadow_reader(*params) -> None:
+    """Tag parameters read through bf16_weight by hipps ops other than the conv kernels (whose
+    4-D weights the optimizer recognises by shape): bf16_weights='auto' then keeps a shadow."""
+    for p in params:
+        if p is not None:
+            p.reads_bf16_shadow = True
+
+
 def shadow_linear_ok(x: torch.Tensor, weight: torch.Tensor, bias=None) -> bool:
     return (_SHADOW_LINEAR and x.is_cuda and torch.is_autocast_enabled() and
             torch.get_autocast_dtype("cuda") == torch.bfloat16 and has_weight_shadow(weight) and
@@ -802,7 +810,13 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
 
 
 class Linear(nn.Linear):
-    """nn.Linear that reads the bf16 weight shadow under bf16 autocast (hipps.ops.nn.linear)."""
+    """nn.Linear that reads the bf16 weight shadow under bf16 autocast (hipps.ops.nn.linear).
+    Its parameters carry ``reads_bf16_shadow`` so the optimizer's ``bf16_weights='auto'`` knows
+    a reader exists."""
+
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        mark_shadow_reader(self.weight, self.bias)
 
     def forward(self, x):
         return linear(x, self.weight, self.bias)

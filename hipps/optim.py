@@ -102,10 +102,12 @@ class MPI_PS(torch.optim.Optimizer):
         self.steps = 0
         self.engine = self._make_engine()
         bw = self.cfg.bf16_weights
-        # auto: only where a reader exists (the hipps conv kernels read 4-D weights); a transformer
-        # would pay a full bf16 copy of the model (16 GB for Llama-3-8B) for nothing
-        has_conv = any(s.param.dim() == 4 for s in self.store.slots)
-        if bw == "on" or (bw == "auto" and self.mode == "ps_async" and self.store.device.type == "cuda" and has_conv):
+        # auto: where a reader exists -- the hipps conv kernels (4-D weights) and hipps.ops.nn.Linear
+        # (parameters tagged reads_bf16_shadow, _ShadowLinear) read the shadow instead of autocast casting every weight in
+        # every forward; for Llama-3-8B the 16 GB shadow replaces the same 16 GB of per-forward
+        # autocast copies held until backward
+        has_reader = any(s.param.dim() == 4 or getattr(s.param, "reads_bf16_shadow", False) for s in self.store.slots)
+        if bw == "on" or (bw == "auto" and self.mode == "ps_async" and self.store.device.type == "cuda" and has_reader):
             self.store.enable_bf16_shadow()
         self._metrics = None
         if self.cfg.metrics_path:
