@@ -101,6 +101,9 @@ void bn_finalize_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tensor we
 void maxpool3s2_backward(at::Tensor dy, at::Tensor code, at::Tensor dx);
 std::vector<at::Tensor> xent_forward(at::Tensor logits, at::Tensor labels, int64_t ignore_index);
 void colsum_bf16(at::Tensor x, at::Tensor out);
+void swiglu_forward(at::Tensor a, at::Tensor b, at::Tensor c);
+void swiglu_backward(at::Tensor g, at::Tensor a, at::Tensor b, at::Tensor da, at::Tensor db);
+void rope_apply(at::Tensor x, at::Tensor y, at::Tensor cs, at::Tensor sn, int64_t S, int64_t hd, double sign);
 void xent_backward(at::Tensor logits, at::Tensor labels, at::Tensor lse, at::Tensor gout, double scale,
                    int64_t ignore_index, at::Tensor dx);
 void bn_finalize_bwd_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tensor weight, at::Tensor mean,
@@ -238,6 +241,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("shift") = pybind11::none());
   m.def("bn_finalize_partials", &hipps::bn_finalize_partials,
         "BN train-mode finalize from producer partial sums (mean/invstd/scale/shift + running stats)");
+  m.def("swiglu_forward", &hipps::swiglu_forward, "c = silu(a) * b, bf16 (act.hip)");
+  m.def("swiglu_backward", &hipps::swiglu_backward, "gradients of silu(a) * b w.r.t. a and b, bf16 (act.hip)");
+  m.def("rope_apply", &hipps::rope_apply, py::arg("x"), py::arg("y"), py::arg("cos"), py::arg("sin"), py::arg("S"),
+        py::arg("hd"), py::arg("sign") = 1.0, "rotary embedding of interleaved pairs, fp32 tables (act.hip)");
   m.def("colsum_bf16", &hipps::colsum_bf16, "fp32 column sums of a bf16 [rows, cols] matrix (bias gradients)");
   m.def("xent_forward", &hipps::xent_forward,
         "fused softmax cross-entropy over bf16 logits: per-row loss and log-sum-exp (one read of the row)");

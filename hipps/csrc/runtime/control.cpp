@@ -56,7 +56,7 @@ struct alignas(64) RankRec {
   std::atomic<int64_t> stop;               // worker has finished (seq of its last push)
   std::atomic<int64_t> heartbeat_ns;
   std::atomic<int64_t> incl_seq;           // newest own message reflected in the published params
-  std::atomic<int64_t> push_flag[kSlots];  // 1: the slot's step left some parameters without a gradient
+  std::atomic<int64_t> push_flag[kSlots];  // bucket << 1 | 1 if a presence mask follows (a parameter without a gradient)
   std::atomic<int64_t> reading;            // version whose publish buffer this rank is copying (-1 none)
   std::atomic<int64_t> pull_req;           // p2p transport: parameter requests posted by this worker
   std::atomic<int64_t> sent_ver;           // p2p transport: version the PS sent for the last request

@@ -149,8 +149,13 @@ class RMSNorm(nn.Module):
 
 
 def _rope(x, cos, sin):
+    """Rotary embedding of interleaved pairs; cos / sin are fp32 [S, hd/2].  One fused HIP pass
+    (hipps.ops.nn.rope) for bf16 device activations, the eager composition otherwise."""
+    if hnn.rope_ok(x, cos):
+        return hnn.rope(x, cos, sin)
+    c, s_ = cos[None, :x.shape[1], None, :].to(x.dtype), sin[None, :x.shape[1], None, :].to(x.dtype)
     x1, x2 = x[..., ::2], x[..., 1::2]
-    return torch.stack((x1 * cos - x2 * sin, x1 * sin + x2 * cos), dim=-1).flatten(-2)
+    return torch.stack((x1 * c - x2 * s_, x1 * s_ + x2 * c), dim=-1).flatten(-2)
 
 
 class LlamaBlock(nn.Module):
@@ -181,7 +186,7 @@ class LlamaBlock(nn.Module):
         a = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=c.heads != c.kv_heads)
         x = x + self.wo(a.transpose(1, 2).reshape(B, S, D))
         h = self.ffn_norm(x)
-        return x + self.w2(F.silu(self.w1(h)) * self.w3(h))
+        return x + self.w2(hnn.swiglu(self.w1(h), self.w3(h)))
 
 
 class Llama(nn.Module):
@@ -196,18 +201,22 @@ class Llama(nn.Module):
             if isinstance(m, (nn.Linear, nn.Embedding)):
                 nn.init.normal_(m.weight, std=0.02)
 
-    def rope_tables(self, S, device, dtype):
-        hd = self.c.dim // self.c.heads
-        inv = 1.0 / (self.c.theta ** (torch.arange(0, hd, 2, device=device, dtype=torch.float32) / hd))
-        t = torch.arange(S, device=device, dtype=torch.float32)
-        f = torch.outer(t, inv)
-        return f.cos()[None, :, None, :].to(dtype), f.sin()[None, :, None, :].to(dtype)
+    def rope_tables(self, S, device):
+        """fp32 cos / sin [S, hd/2] (cached per length and device: built once, not every forward)."""
+        key = (S, str(device))
+        cache = self.__dict__.setdefault("_rope_cache", {})
+        if key not in cache:
+            hd = self.c.dim // self.c.heads
+            inv = 1.0 / (self.c.theta ** (torch.arange(0, hd, 2, device=device, dtype=torch.float32) / hd))
+            t = torch.arange(S, device=device, dtype=torch.float32)
+            f = torch.outer(t, inv)
+            cache[key] = (f.cos().contiguous(), f.sin().contiguous())
+        return cache[key]
 
     def forward(self, ids, labels=None):
         B, S = ids.shape
         x = self.tok(ids)
-        dt = torch.get_autocast_dtype("cuda") if (x.is_cuda and torch.is_autocast_enabled()) else x.dtype
-        cos, sin = self.rope_tables(S, ids.device, dt)
+        cos, sin = self.rope_tables(S, ids.device)
         for b in self.blocks:
             x = b(x, cos, sin)
         logits = self.head(self.norm(x))

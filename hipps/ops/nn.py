@@ -67,6 +67,8 @@ _WGRAD_SIDE = _os.environ.get("HIPPS_WGRAD_STREAM", "1") != "0"
 _SHADOW_LINEAR = _os.environ.get("HIPPS_SHADOW_LINEAR", "1") != "0"
 # softmax cross-entropy of bf16 logits on csrc/xent.hip (hipps.ops.nn.cross_entropy); 0: PyTorch
 _FUSED_XENT = _os.environ.get("HIPPS_FUSED_XENT", "1") != "0"
+# SwiGLU gate and rotary embedding of the Llama block as one HIP pass each (csrc/act.hip)
+_FUSED_ACT = _os.environ.get("HIPPS_FUSED_ACT", "1") != "0"
 _WG_STREAMS: dict = {}
 _WG_JOINED: dict = {}  # device -> autograd graph task whose end joins the side stream
 
@@ -852,6 +854,72 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int 
             and labels.numel() * V == logits.numel()):
         return _CrossEntropy.apply(logits.reshape(-1, V).contiguous(), labels.reshape(-1).contiguous(), ignore_index)
     return F.cross_entropy(logits.float().reshape(-1, V), labels.reshape(-1), ignore_index=ignore_index)
+
+
+def _flat16_ok(*ts) -> bool:
+    return all(t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous() and t.numel() % 8 == 0
+               and t.data_ptr() % 16 == 0 for t in ts)
+
+
+class _SwiGLU(torch.autograd.Function):
+    """silu(a) * b on bf16 (csrc/act.hip): one pass forward (read a, b; write c), one pass
+    backward (read g, a, b; write da, db) instead of 2 + 4 eager kernels."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        c = torch.empty_like(a)
+        native().swiglu_forward(a, b, c)
+        ctx.save_for_backward(a, b)
+        return c
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g = g.to(torch.bfloat16).contiguous()
+        da, db = torch.empty_like(a), torch.empty_like(b)
+        native().swiglu_backward(g, a, b, da, db)
+        return da, db
+
+
+def swiglu(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """F.silu(a) * b (the Llama MLP gate) on the fused kernel for bf16 device tensors."""
+    if _FUSED_ACT and a.shape == b.shape and _flat16_ok(a, b):
+        return _SwiGLU.apply(a, b)
+    return F.silu(a) * b
+
+
+class _Rope(torch.autograd.Function):
+    """Rotary embedding of interleaved pairs on x [B, S, H, hd] bf16 (csrc/act.hip k_rope, fp32
+    cos / sin tables [S, hd/2]); the backward is the rotation by -theta."""
+
+    @staticmethod
+    def forward(ctx, x, cos, sin):
+        B, S, H, hd = x.shape
+        y = torch.empty_like(x)
+        native().rope_apply(x.view(B * S, H * hd), y.view(B * S, H * hd), cos, sin, S, hd, 1.0)
+        ctx.save_for_backward(cos, sin)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        cos, sin = ctx.saved_tensors
+        B, S, H, hd = g.shape
+        g = g.to(torch.bfloat16).contiguous()
+        dx = torch.empty_like(g)
+        native().rope_apply(g.view(B * S, H * hd), dx.view(B * S, H * hd), cos, sin, S, hd, -1.0)
+        return dx, None, None
+
+
+def rope_ok(x: torch.Tensor, cos: torch.Tensor) -> bool:
+    """Can _Rope rotate x [B, S, H, hd] with fp32 tables cos [S, hd/2]?"""
+    return (_FUSED_ACT and x.dim() == 4 and x.shape[-1] % 8 == 0 and _flat16_ok(x) and cos.dtype == torch.float32
+            and cos.is_cuda and cos.dim() == 2 and cos.shape[0] >= x.shape[1] and cos.shape[1] * 2 == x.shape[-1])
+
+
+def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """x rotated pairwise (x[2i], x[2i+1]) by angle pos * theta_i (cos / sin: fp32 [S, hd/2]) on the
+    fused kernel; callers check rope_ok first."""
+    return _Rope.apply(x, cos, sin)
 
 
 class _Conv1x1(torch.autograd.Function):

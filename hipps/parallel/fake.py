@@ -76,9 +76,10 @@ class FakeAsyncPS:
         self.pub_b = [[0.0] for _ in range(nb)]  # bucketwise: published value of bucket b per version
 
     # ---- worker side ------------------------------------------------------------------------
-    def push_step(self, i: int, grads: Sequence[float], version: Optional[int] = None, partial: bool = False):
-        """Worker i pushes one step (nb bucket messages in ready order) computed on ``version``
-        (default: the version it adopted last)."""
+    def push_step(self, i: int, grads: Sequence[float], version: Optional[int] = None, partial: bool = False,
+                  order: Optional[Sequence[int]] = None):
+        """Worker i pushes one step (nb bucket messages, in ready order or in ``order``) computed on
+        ``version`` (default: the version it adopted last)."""
         F = FIELDS
         assert len(grads) == self.nb
         ver = self.local_ver[i] if version is None else version
@@ -87,11 +88,11 @@ class FakeAsyncPS:
             if s > self.SLOTS and self.ctl.load(F.F_ACK_SEQ, i) < s - self.SLOTS:
                 raise WouldBlock(f"worker {i} message {s}: slot {s % self.SLOTS} not yet consumed")
             slot = s % self.SLOTS
-            bi = self.core.order[pos]
+            bi = (order if order is not None else self.core.order)[pos]
             self.mail[(i, slot)] = float(grads[bi])
             vidx = i * self.MAXSLOTS + slot
             self.ctl.store(F.F_PUSH_VER, vidx, ver)
-            self.ctl.store(F.F_PUSH_FLAG, vidx, 1 if (partial and pos == self.nb - 1) else 0)
+            self.ctl.store(F.F_PUSH_FLAG, vidx, (bi << 1) | (1 if (partial and pos == self.nb - 1) else 0))
             self.ctl.store(F.F_PUSH_SEQ, i, s)
             self.seq[i] = s
         self.steps[i] += 1

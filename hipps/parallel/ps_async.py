@@ -486,6 +486,7 @@ class PSAsyncEngine(Engine):
         self._early = pe != "off" and not self.p2p and cfg.overlap and not self.is_object \
             and self._fault is None and not self.plan.guarded and not self.ps_only
         self._npushed, self._push_wait, self._in_encode_all = 0, 0.0, False
+        self._pushed_b = bytearray(self.nb)  # buckets already pushed this step (any order)
         self._lat = (_LatencyProbe() if self.cuda and self.rank == 0 and not self.dedicated
                      and os.environ.get("HIPPS_PS_LATENCY", "0") == "1" else None)
         self._err: Optional[str] = None
@@ -761,10 +762,11 @@ class PSAsyncEngine(Engine):
                         s = posted[i] + 1
                         slot = s % self.SLOTS
                         pos = (s - 1) % self.nb
-                        b = self.plan.buckets[self.order[pos]]
+                        flag = self.ctl.load(C.F_PUSH_FLAG, i * self.MAXSLOTS + slot)
+                        b = self.plan.buckets[flag >> 1]  # the message names its bucket
                         sbuf = self.slot_buf(i, slot)
                         works = [self._gpg.irecv(sbuf[: b.msg_nbytes], i)]
-                        if pos == self.nb - 1 and self.ctl.load(C.F_PUSH_FLAG, i * self.MAXSLOTS + slot):
+                        if pos == self.nb - 1 and flag & 1:
                             works.append(self._gpg.irecv(sbuf[self.slot_pres:self.slot_pres + ns], i))
                         inflight[i].append((s, _Pending(works, self.cuda or self._gpg.native)))
                         posted[i] = s
@@ -898,7 +900,7 @@ class PSAsyncEngine(Engine):
         """Bucket granularity: OR a kept message's step presence into bucket bi's mask."""
         if not self.cfg.skip_missing_grads or self._pres_full_b[bi]:
             return
-        if not self.ctl.load(self.C.F_PUSH_FLAG, vidx):
+        if not self.ctl.load(self.C.F_PUSH_FLAG, vidx) & 1:
             self._pres_full_b[bi] = True
             self._pres_part_b[bi] = None
             return
@@ -968,7 +970,7 @@ class PSAsyncEngine(Engine):
         """OR the step's presence into this update's mask (skip_missing_grads)."""
         if not self.cfg.skip_missing_grads or self._pres_full:
             return
-        if not self.ctl.load(self.C.F_PUSH_FLAG, vidx):
+        if not self.ctl.load(self.C.F_PUSH_FLAG, vidx) & 1:
             self._pres_full = True  # some accumulated step had every gradient: no mask
             self._pres_part = None
             return
@@ -1089,8 +1091,11 @@ class PSAsyncEngine(Engine):
 
     def _push_one(self, pos: int, bi: int, partial: int) -> float:
         """Push message ``pos`` of this step (bucket ``bi``) into the next mailbox slot: copy on the
-        comm stream (after the bucket's encode), then the GPU doorbell with its version / presence /
-        sequence words.  Returns the host seconds spent waiting for a free slot."""
+        comm stream (after the bucket's encode), then the GPU doorbell with its version / flag /
+        sequence words.  The flag word is ``bi << 1 | presence``: the message names its bucket, so
+        a step's buckets may go in any order (each as soon as its gradients are complete), and
+        bit 0 says a presence mask follows in the slot.  Returns the host seconds spent waiting for
+        a free slot."""
         C = self.C
         t_wait = 0.0
         step = self.step_no + 1
@@ -1111,11 +1116,11 @@ class PSAsyncEngine(Engine):
         vidx = self.rank * self.MAXSLOTS + slot
         last = pos == self.nb - 1 or self.bucketwise  # bucket mode: every message carries presence
         if self.p2p and self.rank != 0:
-            self._push_p2p(src, s, vidx, last and partial)
+            self._push_p2p(src, s, vidx, last and partial, bi)
             return t_wait
         sbuf = self.slot_buf(self.rank, slot)
         dst = sbuf[: b.msg_nbytes]
-        words = [(C.F_PUSH_VER, vidx, self.local_ver), (C.F_PUSH_FLAG, vidx, partial if last else 0),
+        words = [(C.F_PUSH_VER, vidx, self.local_ver), (C.F_PUSH_FLAG, vidx, (bi << 1) | (partial if last else 0)),
                  (C.F_PUSH_SEQ, self.rank, s)]
         if self.cuda:
             cs = self.comm_stream
@@ -1138,19 +1143,20 @@ class PSAsyncEngine(Engine):
         return t_wait
 
     def encode_bucket(self, bi: int):
-        """Hook-time encode; with push_early the encoded prefix of this step's messages (in
-        message order) is pushed right away, during backward: the PS accumulates -- and under
-        ps_granularity='bucket' updates and publishes -- the last layers' buckets while the
-        worker is still computing the first layers' gradients."""
+        """Hook-time encode; with push_early a bucket whose gradients are all in is pushed right
+        away, during backward, in completion order (its message names the bucket): the PS
+        accumulates -- and under ps_granularity='bucket' updates and publishes -- the last layers'
+        buckets while the worker is still computing the first layers' gradients.  A bucket with a
+        parameter that gets no gradient this step (e.g. BERT's pooler under an MLM-only loss) waits
+        for step() without holding back the buckets behind it."""
         super().encode_bucket(bi)
         if not self._early or self._in_encode_all:
             return
-        while self._npushed < self.nb:
-            b = self.order[self._npushed]
-            if not self._encoded[b] or self._bucket_count[b] != len(self.plan.buckets[b].slot_ids):
-                return
+        if (not self._pushed_b[bi] and self._encoded[bi]
+                and self._bucket_count[bi] == len(self.plan.buckets[bi].slot_ids)):
             # every parameter of an early-pushed bucket has its gradient: no presence mask
-            self._push_wait += self._push_one(self._npushed, b, 0)
+            self._push_wait += self._push_one(self._npushed, bi, 0)
+            self._pushed_b[bi] = 1
             self._npushed += 1
 
     def encode_all(self):
@@ -1169,7 +1175,7 @@ class PSAsyncEngine(Engine):
             raise RuntimeError(self._broken)
         data = {}
         early = self._npushed
-        if early and any(self.order[p] in self._late for p in range(early)):
+        if early and any(self._pushed_b[b] for b in self._late):
             # The PS maps message s to bucket order[(s-1) % nb]: the `early` messages already sent
             # moved this worker's sequence, and the step cannot be completed with the gradients
             # the PS expects.  Continuing would shift every later message onto the wrong bucket,
@@ -1179,6 +1185,7 @@ class PSAsyncEngine(Engine):
                             "opt.no_sync(), or set push_early='off'; this ps_async engine cannot continue "
                             "(its message sequence is now out of step with the PS)")
             self._npushed, self._push_wait = 0, 0.0
+            self._pushed_b = bytearray(self.nb)
             self._encoded = [False] * len(self._encoded)
             self._bucket_count = [0] * len(self._bucket_count)
             self._late.clear()
@@ -1197,9 +1204,18 @@ class PSAsyncEngine(Engine):
                 self.enc_event.record(self.comm_stream)
         partial = 0 if (self.step_all_present or not self.cfg.skip_missing_grads) else 1
         t_wait = self._push_wait
-        for pos in range(early, self.nb):
-            t_wait += self._push_one(pos, self.order[pos], partial)
+        pos = early
+        for b in self.order:
+            if self._pushed_b[b]:
+                continue
+            # bucket granularity: the presence mask goes only with a bucket that misses a gradient
+            pb = partial
+            if pb and self.bucketwise:
+                pb = 0 if all(self.step_present[j] for j in self.plan.buckets[b].slot_ids) else 1
+            t_wait += self._push_one(pos, b, pb)
+            pos += 1
         self._npushed, self._push_wait = 0, 0.0
+        self._pushed_b = bytearray(self.nb)
         data["pushed_early"] = float(early)
         self.step_no += 1
         data["slot_wait"] = t_wait
@@ -1223,14 +1239,14 @@ class PSAsyncEngine(Engine):
         return data
 
     # ------------------------------------------------------------------ p2p transport (worker)
-    def _push_p2p(self, msg: torch.Tensor, s: int, vidx: int, partial: bool):
+    def _push_p2p(self, msg: torch.Tensor, s: int, vidx: int, partial: bool, bi: int):
         """Announce message s (version + presence flag, then the sequence word the PS waits on)
         and send it; the PS posts the matching receive when it sees the announcement.  The send
         is ordered after the encode on the comm stream, and the comm stream waits for it before
         the next encode overwrites the wire buffer."""
         C = self.C
         self.ctl.store(C.F_PUSH_VER, vidx, self.local_ver)
-        self.ctl.store(C.F_PUSH_FLAG, vidx, 1 if partial else 0)
+        self.ctl.store(C.F_PUSH_FLAG, vidx, (bi << 1) | (1 if partial else 0))
         self.ctl.store(C.F_PUSH_SEQ, self.rank, s)
         ctx = torch.cuda.stream(self.comm_stream) if self.cuda else contextlib.nullcontext()
         with ctx, self.tracer.phase("push", self.comm_stream):

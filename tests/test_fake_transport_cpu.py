@@ -202,3 +202,24 @@ def test_bucketwise_staleness_drop_counts_whole_steps():
     f.deliver(1)  # computed on version 0, now stale by 1 > 0: the whole step is dropped
     st = f.stats
     assert st["drops"] == 1 and st["accumulated"] == 1 and st["version"] == 1
+
+
+@pytest.mark.parametrize("bucketwise", [False, True])
+def test_messages_name_their_bucket_any_push_order(bucketwise):
+    """A worker pushes a step's buckets in completion order (a bucket with a parameter that got no
+    gradient waits for step() without holding back the others): the PS reads each message's bucket
+    from its flag word, so per-worker push orders that differ give the same update as ready order."""
+    from hipps.parallel.fake import FakeAsyncPS
+
+    def run(orders):
+        f = FakeAsyncPS(W=2, nb=3, M=2, bucketwise=bucketwise)
+        for i in (0, 1):
+            f.push_step(i, grads=[1.0, 2.0, 4.0], order=orders[i])
+        f.deliver_order([1, 0])
+        return f.params, f.stats
+
+    ready = FakeAsyncPS(W=2, nb=3).core.order
+    base_p, base_s = run([ready, ready])
+    p, st = run([[1, 0, 2], [2, 1, 0]])
+    assert p == base_p == [-2.0, -4.0, -8.0]
+    assert st["accumulated"] == base_s["accumulated"] == 2 and st["version"] == base_s["version"] == 1

@@ -347,3 +347,60 @@ def test_async_granularity_auto():
     """ps_granularity='auto': per-bucket versions on the ipc transport, whole-model on p2p."""
     assert run_world(_gran, 2, "ipc")[0]["granularity"] == "bucket"
     assert run_world(_gran, 2, "p2p")[0]["granularity"] == "model"
+
+
+class _HeadPlusUnused(torch.nn.Module):
+    """An MLP whose unused layer sits between two used ones in registration order (BERT's pooler
+    under an MLM-only loss): its bucket comes early in the ready order."""
+
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.fc1 = torch.nn.Linear(784, 64)
+        self.unused = torch.nn.Linear(64, 64)
+        self.fc2 = torch.nn.Linear(64, 10)
+
+    def forward(self, x):
+        return self.fc2(torch.relu(self.fc1(x)))
+
+
+def _early_unused(rank, world, steps, push_early, granularity):
+    import hipps
+
+    m = _HeadPlusUnused()
+    w0 = m.unused.weight.detach().clone()
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", bucket_mb=0.0005,
+                    max_delay=0, accumulate=world, push_early=push_early, ps_granularity=granularity)
+    nb = len(opt.engine.plan.buckets)
+    unused = {id(m.unused.weight), id(m.unused.bias)}
+    n_inc = sum(any(id(opt.store.slots[j].param) in unused for j in b.slot_ids) for b in opt.engine.plan.buckets)
+    early = []
+    for s in range(steps):
+        x, y = _data(rank, s % 4)
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x), y).backward()
+        _, data = opt.step()
+        early.append(data["pushed_early"])
+    opt.close()
+    return {"nb": nb, "n_inc": n_inc, "early": early, "unused_same": torch.equal(m.unused.weight.detach(), w0),
+            "params": [p.detach().clone() for p in m.parameters()]}
+
+
+@pytest.mark.parametrize("granularity", ["model", "bucket"])
+def test_async_push_early_past_a_bucket_without_gradients(granularity):
+    """A bucket holding a parameter with no gradient (skipped, as ps.py:178-179 skips grad None)
+    no longer holds back the buckets behind it in message order: every complete bucket leaves from
+    its backward hook, the incomplete one at step() with its presence mask -- and the parameters
+    are bit-identical to pushing everything at step(); the unused layer never moves."""
+    a = run_world(_early_unused, 2, 4, "on", granularity)
+    b = run_world(_early_unused, 2, 4, "off", granularity)
+    for r in range(2):
+        nb = a[r]["nb"]
+        assert nb >= 3
+        # every bucket but the ones holding the unused layer (which sit early in the ready order)
+        assert 0 < a[r]["n_inc"] < nb - 1
+        assert all(e == nb - a[r]["n_inc"] for e in a[r]["early"]), (a[r]["early"], nb, a[r]["n_inc"])
+        assert all(e == 0 for e in b[r]["early"])
+        assert a[r]["unused_same"] and b[r]["unused_same"]
+        for x, y in zip(a[r]["params"], b[r]["params"]):
+            torch.testing.assert_close(x, y, rtol=0, atol=0)
