@@ -92,6 +92,12 @@ def parse():
 
 def main():
     a = parse()
+    if os.environ.get("BENCH_HANG_DUMP"):
+        # diagnosis of a hung run: every rank prints all its threads' Python stacks after this
+        # many seconds and exits
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["BENCH_HANG_DUMP"]), exit=True)
     from hipps.parallel import dist as hdist
 
     world = hdist.init_from_env()

@@ -102,6 +102,9 @@ void maxpool3s2_backward(at::Tensor dy, at::Tensor code, at::Tensor dx);
 std::vector<at::Tensor> xent_forward(at::Tensor logits, at::Tensor labels, int64_t ignore_index);
 void colsum_bf16(at::Tensor x, at::Tensor out);
 void swiglu_forward(at::Tensor a, at::Tensor b, at::Tensor c);
+void ln_forward(at::Tensor x, at::Tensor w, at::Tensor b, at::Tensor y, at::Tensor mean, at::Tensor rstd, double eps);
+void ln_backward(at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor rstd, at::Tensor w, at::Tensor dx,
+                 at::Tensor dw, at::Tensor db);
 void swiglu_backward(at::Tensor g, at::Tensor a, at::Tensor b, at::Tensor da, at::Tensor db);
 void rope_apply(at::Tensor x, at::Tensor y, at::Tensor cs, at::Tensor sn, int64_t S, int64_t hd, double sign);
 void xent_backward(at::Tensor logits, at::Tensor labels, at::Tensor lse, at::Tensor gout, double scale,
@@ -129,12 +132,12 @@ void pull_params(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t readi
 void pull_select(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, int64_t npub,
                  int64_t tries);
 void pull_copy(at::Tensor sel, at::Tensor pub, int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t lo,
-               int64_t hi);
+               int64_t hi, c10::optional<at::Tensor> shadow);
 void pull_done(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, int64_t ring_slot);
 void pull_select_b(at::Tensor selb, int64_t bpub, int64_t bbuf, int64_t reading_b, int64_t applied, int64_t npub,
                    int64_t tries);
 void pull_copy_b(at::Tensor selb, at::Tensor boff, at::Tensor pub, int64_t stride, int64_t npub, bool bf16,
-                 at::Tensor dst, int64_t lo, int64_t hi);
+                 at::Tensor dst, int64_t lo, int64_t hi, c10::optional<at::Tensor> shadow);
 void pull_done_b(at::Tensor selb, int64_t bpub, int64_t bbuf, int64_t reading_b, int64_t applied, at::Tensor sel,
                  int64_t ring_slot);
 void bind_control(pybind11::module& m);
@@ -241,6 +244,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("shift") = pybind11::none());
   m.def("bn_finalize_partials", &hipps::bn_finalize_partials,
         "BN train-mode finalize from producer partial sums (mean/invstd/scale/shift + running stats)");
+  m.def("ln_forward", &hipps::ln_forward, "LayerNorm forward, bf16 rows, fp32 weight / bias / mean / rstd (ln.hip)");
+  m.def("ln_backward", &hipps::ln_backward, "LayerNorm backward: bf16 dx, fp32 weight / bias gradients (ln.hip)");
   m.def("swiglu_forward", &hipps::swiglu_forward, "c = silu(a) * b, bf16 (act.hip)");
   m.def("swiglu_backward", &hipps::swiglu_backward, "gradients of silu(a) * b w.r.t. a and b, bf16 (act.hip)");
   m.def("rope_apply", &hipps::rope_apply, py::arg("x"), py::arg("y"), py::arg("cos"), py::arg("sin"), py::arg("S"),
@@ -262,10 +267,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pull_params", &hipps::rt::pull_params,
         "GPU-time AsySG-InCon pull: select newest published version, copy it, release the reader word");
   m.def("pull_select", &hipps::rt::pull_select, "GPU-time pull, stage 1: choose the version, announce the reader");
-  m.def("pull_copy", &hipps::rt::pull_copy, "GPU-time pull, stage 2: copy params[lo, hi) of the chosen version");
+  m.def("pull_copy", &hipps::rt::pull_copy, py::arg("sel"), py::arg("pub"), py::arg("stride"), py::arg("npub"),
+        py::arg("bf16"), py::arg("dst"), py::arg("lo"), py::arg("hi"), py::arg("shadow") = py::none(),
+        "GPU-time pull, stage 2: copy params[lo, hi) of the chosen version (+ their bf16 shadow)");
   m.def("pull_done", &hipps::rt::pull_done, "GPU-time pull, stage 3: release the reader word, record the version");
   m.def("pull_select_b", &hipps::rt::pull_select_b, "bucket-granular pull, stage 1: newest version per bucket");
-  m.def("pull_copy_b", &hipps::rt::pull_copy_b, "bucket-granular pull, stage 2: copy each bucket's selected slot");
+  m.def("pull_copy_b", &hipps::rt::pull_copy_b, py::arg("selb"), py::arg("boff"), py::arg("pub"), py::arg("stride"),
+        py::arg("npub"), py::arg("bf16"), py::arg("dst"), py::arg("lo"), py::arg("hi"), py::arg("shadow") = py::none(),
+        "bucket-granular pull, stage 2: copy each bucket's selected slot (+ its bf16 shadow)");
   m.def("pull_done_b", &hipps::rt::pull_done_b, "bucket-granular pull, stage 3: release, record min version");
   hipps::rt::bind_control(m);
   hipps::rt::bind_rccl(m);

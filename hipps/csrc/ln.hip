@@ -1,0 +1,286 @@
+// hipps — LayerNorm over the last dim of a bf16 [rows, D] activation (BERT's 25 norms per step).
+//
+// PyTorch's route under autocast (hipps/models/transformer.py _ln) casts the fp32 weight and bias
+// to bf16 every forward, runs the forward at ~1.7 TB/s, and the backward as an input-gradient
+// kernel (~1.5 TB/s) plus two gamma/beta reduction kernels and the casts of their results.  Here:
+//   forward   one wave per row, the row held in registers (D/8 16-byte chunks over 64 lanes),
+//             two-pass mean / variance in fp32, fp32 weight and bias read directly; writes y
+//             (bf16) and the row's mean / rstd (fp32) for the backward
+//   backward  one wave per row as well: dx = rstd (g - mean(g) - xhat mean(g xhat)), g = dy w;
+//             each workgroup also sums dy xhat and dy over its rows per column into a partial
+//             row, and a second kernel folds the partial rows in a fixed order into the fp32
+//             weight / bias gradients (deterministic)
+#include "common.h"
+
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include <algorithm>
+
+namespace hipps {
+
+namespace {
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kLnWaves = 4;  // rows in flight per workgroup
+
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ void unpack8(const u32x4& v, float* f) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[2 * j] = __uint_as_float(v[j] << 16);
+    f[2 * j + 1] = __uint_as_float(v[j] & 0xffff0000u);
+  }
+}
+
+// NC: 16-byte chunks per lane (D <= 512 * NC; D <= 2048 keeps the backward's LDS at <= 64 KB)
+template <int NC>
+__global__ __launch_bounds__(64 * kLnWaves) void k_ln_fwd(const uint16_t* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ b, uint16_t* __restrict__ y,
+                                                          float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                          int64_t R, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * kLnWaves + (threadIdx.x >> 6);
+  if (row >= R) return;
+  const int nch = D >> 3;
+  const uint16_t* xr = x + row * D;
+  float v[NC][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      unpack8(*reinterpret_cast<const u32x4*>(xr + ch * 8), v[c]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[c][j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+    }
+  }
+  const float mu = wsum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (lane + 64 * c < nch) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[c][j] - mu;
+        q += d * d;
+      }
+    }
+  }
+  const float rs = rsqrtf(wsum(q) / D + eps);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      const float4 w0 = *reinterpret_cast<const float4*>(w + ch * 8), w1 = *reinterpret_cast<const float4*>(w + ch * 8 + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(b + ch * 8), b1 = *reinterpret_cast<const float4*>(b + ch * 8 + 4);
+      const float ww[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        o[j] = pack_bf16x2((v[c][2 * j] - mu) * rs * ww[2 * j] + bb[2 * j],
+                           (v[c][2 * j + 1] - mu) * rs * ww[2 * j + 1] + bb[2 * j + 1]);
+      *reinterpret_cast<u32x4*>(y + row * D + ch * 8) = o;
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mu;
+    rstd_out[row] = rs;
+  }
+}
+
+// rows [blockIdx.x * rpb, +rpb): dx per row; per-column sums of dy * xhat and dy over those rows
+// -> part[blockIdx.x] (2 x D floats: dgamma partial, dbeta partial)
+template <int NC>
+__global__ __launch_bounds__(64 * kLnWaves) void k_ln_bwd(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+                                                          const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                          const float* __restrict__ w, uint16_t* __restrict__ dx,
+                                                          float* __restrict__ part, int64_t R, int D, int rpb) {
+  extern __shared__ float red[];  // [kLnWaves][2][D]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nch = D >> 3;
+  float ww[NC][8];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int ch = lane + 64 * c;
+    const int cc = ch < nch ? ch : 0;
+    const float4 w0 = *reinterpret_cast<const float4*>(w + cc * 8), w1 = *reinterpret_cast<const float4*>(w + cc * 8 + 4);
+    ww[c][0] = w0.x; ww[c][1] = w0.y; ww[c][2] = w0.z; ww[c][3] = w0.w;
+    ww[c][4] = w1.x; ww[c][5] = w1.y; ww[c][6] = w1.z; ww[c][7] = w1.w;
+  }
+  float dg[NC][8], db[NC][8];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dg[c][j] = db[c][j] = 0.f;
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = r0 + rpb < R ? r0 + rpb : R;
+  for (int64_t row = r0 + wv; row < r1; row += kLnWaves) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[NC][8], g[NC][8], gy[NC][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nch) {
+        float xv[8];
+        unpack8(*reinterpret_cast<const u32x4*>(x + row * D + ch * 8), xv);
+        unpack8(*reinterpret_cast<const u32x4*>(dy + row * D + ch * 8), gy[c]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[c][j] = (xv[j] - mu) * rs;
+          g[c][j] = gy[c][j] * ww[c][j];
+          s1 += g[c][j];
+          s2 += g[c][j] * xh[c][j];
+        }
+      }
+    }
+    const float m1 = wsum(s1) / D, m2 = wsum(s2) / D;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nch) {
+        u32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          o[j] = pack_bf16x2(rs * (g[c][2 * j] - m1 - xh[c][2 * j] * m2),
+                             rs * (g[c][2 * j + 1] - m1 - xh[c][2 * j + 1] * m2));
+        *reinterpret_cast<u32x4*>(dx + row * D + ch * 8) = o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          dg[c][j] += gy[c][j] * xh[c][j];
+          db[c][j] += gy[c][j];
+        }
+      }
+    }
+  }
+  // fold the waves' column sums in a fixed order
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[(wv * 2) * D + ch * 8 + j] = dg[c][j];
+        red[(wv * 2 + 1) * D + ch * 8 + j] = db[c][j];
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * D; i += 64 * kLnWaves) {
+    const int k = i / D, col = i - k * D;
+    float a = 0.f;
+#pragma unroll
+    for (int q = 0; q < kLnWaves; ++q) a += red[(q * 2 + k) * D + col];
+    part[(int64_t)blockIdx.x * 2 * D + i] = a;
+  }
+}
+
+// out[k * D + col] = sum_p part[p][k][col] (k = 0: dgamma, 1: dbeta), fixed order
+__global__ __launch_bounds__(256) void k_ln_fold(const float* __restrict__ part, int P, int D, float* __restrict__ dw,
+                                                 float* __restrict__ dbias) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;  // over 2 * D
+  const int ii = i < 2 * D ? i : 0;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  int p = wv;
+  for (; p + 12 < P; p += 16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] += part[(int64_t)(p + 4 * j) * 2 * D + ii];
+  }
+  for (; p < P; p += 4) acc[0] += part[(int64_t)p * 2 * D + ii];
+  red[wv][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  __syncthreads();
+  if (wv == 0 && i < 2 * D) {
+    const float a = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    if (i < D) dw[i] = a;
+    else dbias[i - D] = a;
+  }
+}
+
+void ln_check(const at::Tensor& x, int64_t D) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "layer_norm: contiguous bf16");
+  TORCH_CHECK(D % 8 == 0 && D >= 8 && D <= 2048 && x.numel() % D == 0, "layer_norm: D % 8 == 0, D <= 2048");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "layer_norm: 16-byte aligned");
+}
+
+void ln_param_check(const at::Tensor& p, int64_t D, const char* what) {
+  TORCH_CHECK(p.is_cuda() && p.scalar_type() == at::kFloat && p.is_contiguous() && p.numel() == D &&
+                  reinterpret_cast<uintptr_t>(p.data_ptr()) % 16 == 0,
+              "layer_norm: ", what, " must be a 16-byte aligned fp32 [D]");
+}
+}  // namespace
+
+void ln_forward(at::Tensor x, at::Tensor w, at::Tensor b, at::Tensor y, at::Tensor mean, at::Tensor rstd, double eps) {
+  const int64_t D = x.size(-1);
+  ln_check(x, D);
+  ln_check(y, D);
+  ln_param_check(w, D, "weight");
+  ln_param_check(b, D, "bias");
+  const int64_t R = x.numel() / D;
+  TORCH_CHECK(y.numel() == x.numel() && mean.numel() == R && rstd.numel() == R && mean.scalar_type() == at::kFloat &&
+                  rstd.scalar_type() == at::kFloat,
+              "layer_norm: output sizes");
+  if (R == 0) return;
+  const int grid = (int)((R + kLnWaves - 1) / kLnWaves);
+  auto st = c10::hip::getCurrentHIPStream();
+  const int nc = (int)((D / 8 + 63) / 64);
+#define HIPPS_LNF(NCc)                                                                                              \
+  hipLaunchKernelGGL(k_ln_fwd<NCc>, grid, 64 * kLnWaves, 0, st, (const uint16_t*)x.data_ptr(), w.data_ptr<float>(), \
+                     b.data_ptr<float>(), (uint16_t*)y.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), R,   \
+                     (int)D, (float)eps)
+  if (nc <= 1) HIPPS_LNF(1);
+  else if (nc <= 2) HIPPS_LNF(2);
+  else HIPPS_LNF(4);
+#undef HIPPS_LNF
+}
+
+void ln_backward(at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor rstd, at::Tensor w, at::Tensor dx,
+                 at::Tensor dw, at::Tensor db) {
+  const int64_t D = x.size(-1);
+  ln_check(x, D);
+  ln_check(dy, D);
+  ln_check(dx, D);
+  ln_param_check(w, D, "weight");
+  ln_param_check(dw, D, "weight gradient");
+  ln_param_check(db, D, "bias gradient");
+  const int64_t R = x.numel() / D;
+  TORCH_CHECK(dy.numel() == x.numel() && dx.numel() == x.numel() && mean.numel() == R && rstd.numel() == R,
+              "layer_norm backward: sizes");
+  if (R == 0) {
+    dw.zero_();
+    db.zero_();
+    return;
+  }
+  // partial rows: enough workgroups to fill the chip, >= 16 rows each
+  int64_t P = std::min<int64_t>(1024, std::max<int64_t>(1, R / 16));
+  const int rpb = (int)((R + P - 1) / P);
+  P = (R + rpb - 1) / rpb;
+  at::Tensor part = at::empty({P, 2, D}, dw.options());
+  auto st = c10::hip::getCurrentHIPStream();
+  const size_t lds = (size_t)kLnWaves * 2 * D * sizeof(float);
+  const int nc = (int)((D / 8 + 63) / 64);
+#define HIPPS_LNB(NCc)                                                                                                \
+  hipLaunchKernelGGL(k_ln_bwd<NCc>, (int)P, 64 * kLnWaves, lds, st, (const uint16_t*)dy.data_ptr(),                  \
+                     (const uint16_t*)x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), w.data_ptr<float>(), \
+                     (uint16_t*)dx.data_ptr(), part.data_ptr<float>(), R, (int)D, rpb)
+  if (nc <= 1) HIPPS_LNB(1);
+  else if (nc <= 2) HIPPS_LNB(2);
+  else HIPPS_LNB(4);
+#undef HIPPS_LNB
+  hipLaunchKernelGGL(k_ln_fold, (int)((2 * D + 63) / 64), 256, 0, st, part.data_ptr<float>(), (int)P, (int)D,
+                     dw.data_ptr<float>(), db.data_ptr<float>());
+}
+
+}  // namespace hipps

@@ -65,7 +65,7 @@ __global__ __launch_bounds__(64) void k_pull_select(PullWords w, int64_t* __rest
 template <typename Tin>
 __global__ __launch_bounds__(kBlock) void k_pull_copy(const int64_t* __restrict__ sel, const uint8_t* __restrict__ pub,
                                                       int64_t stride, int npub, float* __restrict__ dst, int64_t n,
-                                                      int fence_mode) {
+                                                      int fence_mode, uint16_t* __restrict__ sh) {
   constexpr int U = 4;
   const int64_t v = sel[0];
   if (v < 0) return;
@@ -87,10 +87,16 @@ __global__ __launch_bounds__(kBlock) void k_pull_copy(const int64_t* __restrict_
       if (i0 + u * step < nv) t[u] = Vec4<Tin>::load(src, (i0 + u * step) << 2);
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (i0 + u * step < nv) Vec4<float>::store(dst, (i0 + u * step) << 2, t[u]);
+      if (i0 + u * step < nv) {
+        Vec4<float>::store(dst, (i0 + u * step) << 2, t[u]);
+        if (sh != nullptr) Vec4<uint16_t>::store(sh, (i0 + u * step) << 2, t[u]);
+      }
   }
   if (blockIdx.x == 0)
-    for (int64_t i = (nv << 2) + threadIdx.x; i < n; i += blockDim.x) dst[i] = Vec4<Tin>::load1(src, i);
+    for (int64_t i = (nv << 2) + threadIdx.x; i < n; i += blockDim.x) {
+      dst[i] = Vec4<Tin>::load1(src, i);
+      if (sh != nullptr) sh[i] = f32_to_bf16(dst[i]);
+    }
 }
 
 __global__ __launch_bounds__(64) void k_pull_done(PullWords w, int64_t* __restrict__ sel, int ring_slot) {
@@ -139,7 +145,7 @@ template <typename Tin>
 __global__ __launch_bounds__(kBlock) void k_pull_copy_b(const int64_t* __restrict__ selb,
                                                         const int64_t* __restrict__ boff, const uint8_t* __restrict__ pub,
                                                         int64_t stride, int npub, float* __restrict__ dst, int64_t lo,
-                                                        int64_t hi, int fence_mode) {
+                                                        int64_t hi, int fence_mode, uint16_t* __restrict__ sh) {
   constexpr int U = 4;
   const int b = blockIdx.y;
   const int64_t v = selb[b];
@@ -160,11 +166,20 @@ __global__ __launch_bounds__(kBlock) void k_pull_copy_b(const int64_t* __restric
       if (i0 + u * step < e4) t[u] = Vec4<Tin>::load(src, (i0 + u * step) << 2);
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (i0 + u * step < e4) Vec4<float>::store(dst, (i0 + u * step) << 2, t[u]);
+      if (i0 + u * step < e4) {
+        Vec4<float>::store(dst, (i0 + u * step) << 2, t[u]);
+        if (sh != nullptr) Vec4<uint16_t>::store(sh, (i0 + u * step) << 2, t[u]);
+      }
   }
   if (blockIdx.x == 0) {  // unaligned head / tail of the range
-    for (int64_t i = a + threadIdx.x; i < min(e, a4 << 2); i += blockDim.x) dst[i] = Vec4<Tin>::load1(src, i);
-    for (int64_t i = max(a, e4 << 2) + threadIdx.x; i < e; i += blockDim.x) dst[i] = Vec4<Tin>::load1(src, i);
+    for (int64_t i = a + threadIdx.x; i < min(e, a4 << 2); i += blockDim.x) {
+      dst[i] = Vec4<Tin>::load1(src, i);
+      if (sh != nullptr) sh[i] = f32_to_bf16(dst[i]);
+    }
+    for (int64_t i = max(a, e4 << 2) + threadIdx.x; i < e; i += blockDim.x) {
+      dst[i] = Vec4<Tin>::load1(src, i);
+      if (sh != nullptr) sh[i] = f32_to_bf16(dst[i]);
+    }
   }
 }
 
@@ -208,8 +223,18 @@ void pull_select(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t readi
                      words_of(pub_ver, buf_ver, reading, applied), sel.data_ptr<int64_t>(), (int)npub, (int)tries);
 }
 
+static uint16_t* shadow_of(const c10::optional<at::Tensor>& shadow, const at::Tensor& dst) {
+  if (!shadow.has_value() || !shadow->defined()) return nullptr;
+  TORCH_CHECK(shadow->is_cuda() && shadow->scalar_type() == at::kBFloat16 && shadow->is_contiguous() &&
+                  shadow->numel() == dst.numel() && reinterpret_cast<uintptr_t>(shadow->data_ptr()) % 16 == 0,
+              "shadow must be a 16-byte aligned bf16 tensor shaped like dst");
+  return reinterpret_cast<uint16_t*>(shadow->data_ptr());
+}
+
+// shadow (optional): the bf16 weight shadow of dst, written in the same pass (RNE of the adopted
+// value; exact for a bf16 publish buffer) -- the separate shadow cast pass goes away
 void pull_copy(at::Tensor sel, at::Tensor pub, int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t lo,
-               int64_t hi) {
+               int64_t hi, c10::optional<at::Tensor> shadow) {
   TORCH_CHECK(sel.is_cuda() && sel.scalar_type() == at::kLong && sel.is_contiguous(), "sel must be int64 device");
   TORCH_CHECK(pub.is_cuda() && pub.scalar_type() == at::kByte, "pub must be a uint8 device view");
   TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kFloat && dst.is_contiguous(), "dst must be f32 device");
@@ -230,12 +255,14 @@ void pull_copy(at::Tensor sel, at::Tensor pub, int64_t stride, int64_t npub, boo
   }();
   const int grid = grid_for((n >> 2) / grid_div + 1);
   const uint8_t* src = pub.data_ptr<uint8_t>() + lo * esz;
+  uint16_t* sh = shadow_of(shadow, dst);
+  if (sh != nullptr) sh += lo;
   if (bf16)
     hipLaunchKernelGGL(k_pull_copy<uint16_t>, grid, kBlock, 0, stream, sel.data_ptr<int64_t>(), src, stride, (int)npub,
-                       dst.data_ptr<float>() + lo, n, fence_mode);
+                       dst.data_ptr<float>() + lo, n, fence_mode, sh);
   else
     hipLaunchKernelGGL(k_pull_copy<float>, grid, kBlock, 0, stream, sel.data_ptr<int64_t>(), src, stride, (int)npub,
-                       dst.data_ptr<float>() + lo, n, fence_mode);
+                       dst.data_ptr<float>() + lo, n, fence_mode, sh);
 }
 
 void pull_done(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, int64_t ring_slot) {
@@ -249,7 +276,7 @@ void pull_done(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading
 void pull_params(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, at::Tensor pub,
                  int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t ring_slot, int64_t tries) {
   pull_select(sel, pub_ver, buf_ver, reading, applied, npub, tries);
-  pull_copy(sel, pub, stride, npub, bf16, dst, 0, dst.numel());
+  pull_copy(sel, pub, stride, npub, bf16, dst, 0, dst.numel(), c10::nullopt);
   pull_done(sel, pub_ver, buf_ver, reading, applied, ring_slot);
 }
 
@@ -269,7 +296,7 @@ void pull_select_b(at::Tensor selb, int64_t bpub, int64_t bbuf, int64_t reading_
 }
 
 void pull_copy_b(at::Tensor selb, at::Tensor boff, at::Tensor pub, int64_t stride, int64_t npub, bool bf16,
-                 at::Tensor dst, int64_t lo, int64_t hi) {
+                 at::Tensor dst, int64_t lo, int64_t hi, c10::optional<at::Tensor> shadow) {
   TORCH_CHECK(selb.is_cuda() && selb.scalar_type() == at::kLong && selb.is_contiguous(), "selb must be int64 device");
   const int64_t nb = selb.numel() / 2;
   TORCH_CHECK(boff.is_cuda() && boff.scalar_type() == at::kLong && boff.numel() == nb + 1, "boff: int64 [nb + 1]");
@@ -282,14 +309,15 @@ void pull_copy_b(at::Tensor selb, at::Tensor boff, at::Tensor pub, int64_t strid
   if (hi == lo || nb == 0) return;
   const int gx = std::max(1, std::min(grid_for(((hi - lo) >> 2) / 16 + 1), (int)(4096 / nb) + 1));
   auto stream = c10::hip::getCurrentHIPStream();
+  uint16_t* sh = shadow_of(shadow, dst);
   if (bf16)
     hipLaunchKernelGGL(k_pull_copy_b<uint16_t>, dim3(gx, nb), kBlock, 0, stream, selb.data_ptr<int64_t>(),
                        boff.data_ptr<int64_t>(), pub.data_ptr<uint8_t>(), stride, (int)npub, dst.data_ptr<float>(), lo,
-                       hi, 1);
+                       hi, 1, sh);
   else
     hipLaunchKernelGGL(k_pull_copy_b<float>, dim3(gx, nb), kBlock, 0, stream, selb.data_ptr<int64_t>(),
                        boff.data_ptr<int64_t>(), pub.data_ptr<uint8_t>(), stride, (int)npub, dst.data_ptr<float>(), lo,
-                       hi, 1);
+                       hi, 1, sh);
 }
 
 void pull_done_b(at::Tensor selb, int64_t bpub, int64_t bbuf, int64_t reading_b, int64_t applied, at::Tensor sel,

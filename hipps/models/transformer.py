@@ -32,7 +32,10 @@ def _ln(mod: nn.LayerNorm, x: torch.Tensor) -> torch.Tensor:
     if x.is_cuda and torch.is_autocast_enabled():
         dt = torch.get_autocast_dtype("cuda")
         with torch.autocast("cuda", enabled=False):
-            return F.layer_norm(x.to(dt), mod.normalized_shape, mod.weight.to(dt), mod.bias.to(dt), mod.eps)
+            xd = x.to(dt)
+            if len(mod.normalized_shape) == 1 and hnn.layer_norm_ok(xd, mod.weight, mod.bias):
+                return hnn.layer_norm(xd, mod.weight, mod.bias, mod.eps)  # csrc/ln.hip
+            return F.layer_norm(xd, mod.normalized_shape, mod.weight.to(dt), mod.bias.to(dt), mod.eps)
     return mod(x)
 
 

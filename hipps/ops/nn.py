@@ -888,6 +888,45 @@ def swiglu(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return F.silu(a) * b
 
 
+class _LayerNorm(torch.autograd.Function):
+    """LayerNorm over the last dim of a bf16 activation with fp32 weight / bias (csrc/ln.hip): no
+    per-forward casts of the parameters, fp32 weight / bias gradients written directly."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        D = x.shape[-1]
+        y = torch.empty_like(x)
+        R = x.numel() // D
+        mean = torch.empty(R, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(R, dtype=torch.float32, device=x.device)
+        native().ln_forward(x, w, b, y, mean, rstd, float(eps))
+        ctx.save_for_backward(x, w, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, mean, rstd = ctx.saved_tensors
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = torch.empty_like(x)
+        dw, db = torch.empty_like(w), torch.empty_like(w)
+        native().ln_backward(dy, x, mean, rstd, w, dx, dw, db)
+        return dx, dw, db, None
+
+
+def layer_norm_ok(x: torch.Tensor, weight, bias) -> bool:
+    """Can _LayerNorm run F.layer_norm(x, (D,), weight, bias) (bf16 x, fp32 affine params)?"""
+    D = x.shape[-1] if x.dim() else 0
+    return (_FUSED_ACT and weight is not None and bias is not None and x.is_cuda and x.dtype == torch.bfloat16
+            and x.is_contiguous() and D % 8 == 0 and 8 <= D <= 2048 and x.data_ptr() % 16 == 0
+            and all(p.dtype == torch.float32 and p.is_contiguous() and p.numel() == D and p.data_ptr() % 16 == 0
+                    for p in (weight, bias)))
+
+
+def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float) -> torch.Tensor:
+    """F.layer_norm over the last dim on the fused kernels (callers check layer_norm_ok)."""
+    return _LayerNorm.apply(x, weight, bias, eps)
+
+
 class _Rope(torch.autograd.Function):
     """Rotary embedding of interleaved pairs on x [B, S, H, hd] bf16 (csrc/act.hip k_rope, fp32
     cos / sin tables [S, hd/2]); the backward is the rotation by -theta."""

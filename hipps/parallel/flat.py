@@ -229,15 +229,17 @@ class FlatStore:
             self.shadow = self.tshadow = self._tiles = None
             self._tile_ranges = {}
 
-    def refresh_shadow(self, lo: int = 0, hi: Optional[int] = None):
+    def refresh_shadow(self, lo: int = 0, hi: Optional[int] = None, cast: bool = True):
         """Re-cast the bf16 shadows of ``data[lo:hi]`` (default: all) on the current stream; a
         range must start and end at slot boundaries (ps_async pull_overlap refreshes the two
-        halves of a split pull on their own streams)."""
+        halves of a split pull on their own streams).  ``cast=False``: the flat shadow was already
+        written (by the pull kernel that adopted ``data``); only the transposed copies are rebuilt."""
         if getattr(self, "shadow", None) is None:
             return
         full = lo == 0 and (hi is None or hi >= self.numel)
         hi = self.numel if hi is None else hi
-        self.shadow[lo:hi].copy_(self.data[lo:hi])  # one vectorized cast kernel
+        if cast:
+            self.shadow[lo:hi].copy_(self.data[lo:hi])  # one vectorized cast kernel
         if getattr(self, "tshadow", None) is not None:
             from ..ops._native import native
 

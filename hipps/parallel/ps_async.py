@@ -35,13 +35,14 @@ CPU runs use the same protocol with POSIX-shm mailboxes and the torch reference 
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import os
 import secrets
 import threading
 import time
 import traceback
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
@@ -78,7 +79,7 @@ def ps_memory_budget(numel: int, W: int, slots: int, slot_bytes: int, npub: int,
     """Bytes the async PS adds on rank 0's GPU, term by term.
 
     PS terms (allocated by the engine):
-      mailbox      W * slots * slot_bytes        every worker's in-flight bucket messages
+      mailbox      W * slots * slot_bytes        every worker's in-flight bucket messages (ring: slots = 1)
       publish      npub * numel * pub_esz        rotating published versions (readers never torn)
       master       numel * 4                     the fp32 master parameters
       accumulator  numel * 4                     the fp32 gradient accumulator
@@ -107,13 +108,31 @@ def ps_memory_budget(numel: int, W: int, slots: int, slot_bytes: int, npub: int,
     return b
 
 
+def mailbox_geometry(msg_nbytes: Sequence[int], pres_bytes: int, mailbox_slots: int, mailbox_mb: float,
+                     max_slots: int):
+    """(word slots per worker, ring bytes per worker) of the PS mailbox: 2 x buckets message
+    slots (at most ``max_slots``) and a byte ring holding two steps' messages, capped by
+    ``mailbox_mb`` but never below two of the largest; an explicit ``mailbox_slots`` sizes the
+    ring for that many of the largest messages."""
+    ext = [_align(n) for n in msg_nbytes]
+    pres_a = _align(pres_bytes)
+    max_ext = max(ext) + pres_a
+    K = mailbox_slots if mailbox_slots > 0 else 2 * len(ext)
+    K = max(1, min(K, max_slots))
+    if mailbox_slots > 0:
+        ring = K * max_ext
+    else:
+        ring = max(2 * max_ext, min(int(mailbox_mb * (1 << 20)), 2 * (sum(ext) + pres_a)))
+    return K, _align(ring)
+
+
 def budget_for_shapes(shapes, W: int, codec="bf16", bucket_mb: float = 64.0, mailbox_mb: float = 4096.0,
                       mailbox_slots: int = 0, param_wire: str = "bf16", opt_floats: int = 1,
                       dedicated: bool = False, shadow: bool = True, npub: Optional[int] = None,
                       max_slots: int = 64) -> Dict[str, int]:
     """:func:`ps_memory_budget` of a model given only its parameter shapes (no allocation: usable
     for an 8B model on a laptop).  Reproduces the engine's bucketing (flat.BucketPlan over
-    16-aligned slots) and mailbox sizing (``mailbox_slots`` or min(2 * buckets, mailbox_mb))."""
+    16-aligned slots) and mailbox sizing (:func:`mailbox_geometry`)."""
     import math
     from types import SimpleNamespace
 
@@ -131,18 +150,16 @@ def budget_for_shapes(shapes, W: int, codec="bf16", bucket_mb: float = 64.0, mai
     plan = BucketPlan(store, c, int(bucket_mb * (1 << 20)))
     nb = len(plan.buckets)
     pres = (len(slots) + 15) // 16 * 16
-    slot_bytes = _align(max(b.msg_nbytes for b in plan.buckets)) + _align(pres)
-    K = mailbox_slots if mailbox_slots > 0 else min(2 * nb, max(2, int(mailbox_mb * (1 << 20)) // slot_bytes))
-    K = max(1, min(K, max_slots))
+    K, ring = mailbox_geometry([b.msg_nbytes for b in plan.buckets], pres, mailbox_slots, mailbox_mb, max_slots)
     if npub is None:
         from hipps.ops._native import available, native
 
         npub = native().ControlBlock.NPUB if available() else 4
     esz = 2 if param_wire == "bf16" else 4
     ef = 1 if getattr(c, "error_feedback", False) else 0
-    b = ps_memory_budget(off, W, K, slot_bytes, npub, esz, opt_floats, colocated=not dedicated,
+    b = ps_memory_budget(off, W, 1, ring, npub, esz, opt_floats, colocated=not dedicated,
                          worker_wire_bytes=plan.wire_nbytes + pres, shadow=shadow, codec_state_floats=ef)
-    b["buckets"], b["mailbox_slots"], b["slot_bytes"] = nb, K, slot_bytes
+    b["buckets"], b["mailbox_slots"], b["slot_bytes"] = nb, K, ring
     return b
 
 
@@ -361,20 +378,26 @@ class PSAsyncEngine(Engine):
         self.timeout_us = int(min(TIMEOUT_US, cfg.comm_timeout_s * 1e6))
         self.pub_dtype = torch.bfloat16 if cfg.param_wire == "bf16" else torch.float32
         esz = torch.empty((), dtype=self.pub_dtype).element_size()
-        # messages are BUCKETS, streamed in ready order; a worker's mailbox holds K of them, so the
-        # PS memory is W*K*max_bucket instead of W*2*model (Llama-3-8B: 8x4x512 MB vs 8x2x16 GB).
-        # Each slot ends with the step's per-parameter presence bytes (used when a step left some
-        # parameters without a gradient; PUSH_FLAG says so).
+        # messages are BUCKETS, pushed as each completes.  A worker's mailbox is a byte ring: a
+        # message takes its own (256-aligned) size -- plus the step's per-parameter presence bytes
+        # when it carries them -- at the next offset, and the PS reads the offset from the
+        # message's flag word.  Before round 4 every message took a slot sized for the LARGEST
+        # bucket (BERT-base: 87 x 47 MB per worker for a 220 MB step -- an 8 GB mailbox whose IPC
+        # mapping never finished on a second rank).  SLOTS per-message control words bound the
+        # messages in flight; the ring holds two steps' messages (capped by mailbox_mb).
         self.nb = len(self.plan.buckets)
         self.order = list(self.plan.ready_order)
-        self.slot_bytes = _align(max(b.msg_nbytes for b in self.plan.buckets)) + _align(self.pres_bytes)
-        self.slot_pres = self.slot_bytes - _align(self.pres_bytes)
-        K = cfg.mailbox_slots if cfg.mailbox_slots > 0 else min(
-            2 * self.nb, max(2, int(cfg.mailbox_mb * (1 << 20)) // self.slot_bytes))
-        self.SLOTS = max(1, min(K, self.MAXSLOTS))
+        if self.nb >= (1 << 20):
+            raise ValueError("ps_async: at most 2**20 buckets")
+        self.msg_ext = [_align(b.msg_nbytes) for b in self.plan.buckets]
+        self.SLOTS, self.ring_bytes = mailbox_geometry([b.msg_nbytes for b in self.plan.buckets], self.pres_bytes,
+                                                       cfg.mailbox_slots, cfg.mailbox_mb, self.MAXSLOTS)
+        self.slot_bytes = self.ring_bytes  # (budget / stats: mailbox bytes per worker)
+        self._ring_off = 0
+        self._inflight = collections.deque()  # (seq, offset, bytes) of this worker's unacked messages
         self.pub_bytes = _align(store.numel * esz)
         self.mail_off = 0
-        self.pub_off = W * self.SLOTS * self.slot_bytes
+        self.pub_off = W * self.ring_bytes
         total = self.pub_off + self.NPUB * self.pub_bytes
         if world.rank == 0:
             self._check_budget(opt, store, esz)
@@ -576,7 +599,7 @@ class PSAsyncEngine(Engine):
         opt, store = self.opt, self.store
         esz = torch.empty((), dtype=self.pub_dtype).element_size()
         cs = sum(1 for st in self.codec_state if "resid" in st)
-        return ps_memory_budget(store.numel, self.W, self.SLOTS, self.slot_bytes, self.NPUB, esz,
+        return ps_memory_budget(store.numel, self.W, 1, self.ring_bytes, self.NPUB, esz,
                                 opt.state_floats(), colocated=not self.dedicated, worker_wire_bytes=self.wire_total,
                                 shadow=getattr(store, "shadow", None) is not None,
                                 codec_state_floats=1 if cs else 0)
@@ -612,7 +635,7 @@ class PSAsyncEngine(Engine):
         tag = torch.full((16,), (self.rank * 7 + 3) % 251, dtype=torch.uint8, device=dev)
         if self.p2p:
             return self._self_test_p2p(tag)
-        dst = self.slot_buf(self.rank, self.SLOTS - 1)[:16]
+        dst = self._ring_buf(self.rank, 0, 16)
         if self.cuda:
             with torch.cuda.stream(self.comm_stream):
                 dst.copy_(tag, non_blocking=True)
@@ -623,7 +646,7 @@ class PSAsyncEngine(Engine):
         ok = True
         if self.rank == 0:
             for r in range(W):
-                got = self._slot_read(r, self.SLOTS - 1, 0, 16).cpu()
+                got = self._ring_read(r, 0, 16).cpu()
                 ok &= bool((got == (r * 7 + 3) % 251).all())
             ck = float(self.pub_buf(0).double().sum())  # what workers actually receive
         else:
@@ -652,7 +675,7 @@ class PSAsyncEngine(Engine):
         ok = True
         if self.rank == 0:
             for r in range(1, W):
-                got = self.slot_buf(r, self.SLOTS - 1)[:16]
+                got = self._ring_buf(r, 0, 16)
                 self._gpg.recv(got, r)
                 ok &= bool((got.cpu() == (r * 7 + 3) % 251).all())
         else:
@@ -669,9 +692,33 @@ class PSAsyncEngine(Engine):
             raise RuntimeError(f"ps_async p2p transport self-test failed (per-rank ok={flags})")
 
     # ------------------------------------------------------------------ memory views
+    def _ring_buf(self, rank: int, off: int, nbytes: int) -> torch.Tensor:
+        o = self.mail_off + rank * self.ring_bytes + off
+        return self.mem[o:o + nbytes]
+
+    def _msg_of(self, rank: int, slot: int):
+        """(bucket, ring offset, carries presence) of worker ``rank``'s message in word slot
+        ``slot``, from its flag word ``offset / 256 << 21 | bucket << 1 | presence``."""
+        f = self.ctl.load(self.C.F_PUSH_FLAG, rank * self.MAXSLOTS + slot)
+        return (f >> 1) & ((1 << 20) - 1), (f >> 21) << 8, f & 1
+
     def slot_buf(self, rank: int, slot: int) -> torch.Tensor:
-        o = self.mail_off + (rank * self.SLOTS + slot) * self.slot_bytes
-        return self.mem[o:o + self.slot_bytes]
+        """The bytes of worker ``rank``'s message in word slot ``slot`` (message, then the presence
+        bytes when it carries them)."""
+        bi, off, pres = self._msg_of(rank, slot)
+        return self._ring_buf(rank, off, self.msg_ext[bi] + (_align(self.pres_bytes) if pres else 0))
+
+    def _pres_range(self, rank: int, slot: int):
+        bi, _, _ = self._msg_of(rank, slot)
+        return self.msg_ext[bi], self.msg_ext[bi] + len(self.store.slots)
+
+    def _ring_read(self, i: int, off: int, nbytes: int) -> torch.Tensor:
+        v = self._ring_buf(i, off, nbytes)
+        if not self._remote(i):
+            return v
+        out = torch.empty(nbytes, dtype=torch.uint8, device=v.device)
+        ops.copy_acquire(v, out)
+        return out
 
     def _bucket_msg(self, bi: int, buf: torch.Tensor):
         b = self.plan.buckets[bi]
@@ -680,7 +727,8 @@ class PSAsyncEngine(Engine):
     def _verify_slot(self, rank: int, slot: int, bi: int, seq: int):
         """debug_canary on the PS: the pushed message must end in its intact 0x29 guard."""
         b = self.plan.buckets[bi]
-        buf = self._slot_read(rank, slot, 0, self.slot_bytes) if self._remote(rank) else self.slot_buf(rank, slot)
+        n = self.msg_ext[bi]
+        buf = self._slot_read(rank, slot, 0, n) if self._remote(rank) else self.slot_buf(rank, slot)
         if bool(self.plan.bad_guard(buf, b.layout.nbytes)):
             raise RuntimeError(f"mailbox canary overwritten: worker {rank} message {seq} (bucket {bi})")
 
@@ -762,12 +810,13 @@ class PSAsyncEngine(Engine):
                         s = posted[i] + 1
                         slot = s % self.SLOTS
                         pos = (s - 1) % self.nb
-                        flag = self.ctl.load(C.F_PUSH_FLAG, i * self.MAXSLOTS + slot)
-                        b = self.plan.buckets[flag >> 1]  # the message names its bucket
+                        bi, _, pres = self._msg_of(i, slot)  # the message names its bucket and offset
+                        b = self.plan.buckets[bi]
                         sbuf = self.slot_buf(i, slot)
                         works = [self._gpg.irecv(sbuf[: b.msg_nbytes], i)]
-                        if pos == self.nb - 1 and flag & 1:
-                            works.append(self._gpg.irecv(sbuf[self.slot_pres:self.slot_pres + ns], i))
+                        if pos == self.nb - 1 and pres:
+                            lo, hi = self._pres_range(i, slot)
+                            works.append(self._gpg.irecv(sbuf[lo:hi], i))
                         inflight[i].append((s, _Pending(works, self.cuda or self._gpg.native)))
                         posted[i] = s
                     while inflight[i] and inflight[i][0][1].done():
@@ -904,8 +953,7 @@ class PSAsyncEngine(Engine):
             self._pres_full_b[bi] = True
             self._pres_part_b[bi] = None
             return
-        ns = len(self.store.slots)
-        p = self._slot_read(i, slot, self.slot_pres, self.slot_pres + ns)
+        p = self._slot_read(i, slot, *self._pres_range(i, slot))
         cur = self._pres_part_b[bi]
         self._pres_part_b[bi] = p.clone() if cur is None else torch.maximum(cur, p)
 
@@ -974,8 +1022,7 @@ class PSAsyncEngine(Engine):
             self._pres_full = True  # some accumulated step had every gradient: no mask
             self._pres_part = None
             return
-        ns = len(self.store.slots)
-        p = self._slot_read(i, slot, self.slot_pres, self.slot_pres + ns)
+        p = self._slot_read(i, slot, *self._pres_range(i, slot))
         self._pres_part = p.clone() if self._pres_part is None else torch.maximum(self._pres_part, p)
 
     def _hold(self):
@@ -1090,12 +1137,13 @@ class PSAsyncEngine(Engine):
         return self.ps_stats()
 
     def _push_one(self, pos: int, bi: int, partial: int) -> float:
-        """Push message ``pos`` of this step (bucket ``bi``) into the next mailbox slot: copy on the
-        comm stream (after the bucket's encode), then the GPU doorbell with its version / flag /
-        sequence words.  The flag word is ``bi << 1 | presence``: the message names its bucket, so
-        a step's buckets may go in any order (each as soon as its gradients are complete), and
-        bit 0 says a presence mask follows in the slot.  Returns the host seconds spent waiting for
-        a free slot."""
+        """Push message ``pos`` of this step (bucket ``bi``) to the next offset of this worker's
+        mailbox ring: copy on the comm stream (after the bucket's encode), then the GPU doorbell
+        with its version / flag / sequence words.  The flag word is
+        ``offset / 256 << 21 | bi << 1 | presence``: the message names its bucket -- a step's
+        buckets may go in any order, each as soon as its gradients are complete -- and where it
+        sits, and bit 0 says the presence bytes follow it.  Returns the host seconds spent waiting
+        for the PS to free a word slot or ring space."""
         C = self.C
         t_wait = 0.0
         step = self.step_no + 1
@@ -1115,30 +1163,34 @@ class PSAsyncEngine(Engine):
         src = self.plan.message(self.wire, bi)  # layout (+ canary guard in debug_canary)
         vidx = self.rank * self.MAXSLOTS + slot
         last = pos == self.nb - 1 or self.bucketwise  # bucket mode: every message carries presence
+        pres = 1 if (last and partial) else 0
+        ext = self.msg_ext[bi] + (_align(self.pres_bytes) if pres else 0)
+        off, tw2 = self._ring_alloc(s, ext)
+        t_wait += tw2
+        flag = ((off >> 8) << 21) | (bi << 1) | pres
         if self.p2p and self.rank != 0:
-            self._push_p2p(src, s, vidx, last and partial, bi)
+            self._push_p2p(src, s, vidx, pres, flag)
             return t_wait
-        sbuf = self.slot_buf(self.rank, slot)
+        sbuf = self._ring_buf(self.rank, off, ext)
         dst = sbuf[: b.msg_nbytes]
-        words = [(C.F_PUSH_VER, vidx, self.local_ver), (C.F_PUSH_FLAG, vidx, (bi << 1) | (partial if last else 0)),
-                 (C.F_PUSH_SEQ, self.rank, s)]
+        words = [(C.F_PUSH_VER, vidx, self.local_ver), (C.F_PUSH_FLAG, vidx, flag), (C.F_PUSH_SEQ, self.rank, s)]
         if self.cuda:
             cs = self.comm_stream
             with torch.cuda.stream(cs), self.tracer.phase("push", cs):
                 # variable-size codes (threshold) move 16 + count * entry bytes, not capacity
                 if self.plan.guarded or not self.codec.push_copy(b.layout, src, dst):
                     dst.copy_(src, non_blocking=True)
-                if last and partial:
+                if pres:
                     ns = len(self.store.slots)
-                    sbuf[self.slot_pres:self.slot_pres + ns].copy_(self.presence_tensor(), non_blocking=True)
+                    sbuf[self.msg_ext[bi]:self.msg_ext[bi] + ns].copy_(self.presence_tensor(), non_blocking=True)
             self._ring(cs, words, ver_src)
             if self._lat is not None:
                 self._lat.pushed(s, cs)
         else:
             dst.copy_(src)
-            if last and partial:
+            if pres:
                 ns = len(self.store.slots)
-                sbuf[self.slot_pres:self.slot_pres + ns].copy_(self.presence_tensor())
+                sbuf[self.msg_ext[bi]:self.msg_ext[bi] + ns].copy_(self.presence_tensor())
             self._ring(None, words)
         return t_wait
 
@@ -1239,14 +1291,40 @@ class PSAsyncEngine(Engine):
         return data
 
     # ------------------------------------------------------------------ p2p transport (worker)
-    def _push_p2p(self, msg: torch.Tensor, s: int, vidx: int, partial: bool, bi: int):
+    def _ring_alloc(self, s: int, nbytes: int):
+        """Ring space for message s: the next offset (back to 0 when the tail is too short), once
+        the PS has acknowledged every in-flight message overlapping it.  Returns (offset, host
+        seconds waited)."""
+        C = self.C
+        off = self._ring_off
+        if off + nbytes > self.ring_bytes:
+            off = 0
+        need = 0
+        for q, o, z in self._inflight:
+            if o < off + nbytes and off < o + z:
+                need = max(need, q)
+        tw = 0.0
+        if need:
+            t0 = time.perf_counter()
+            if not self.ctl.wait_ge(C.F_ACK_SEQ, self.rank, need, self.timeout_us):
+                self._check_error()
+                raise TimeoutError(f"rank {self.rank}: PS did not consume message {need} (mailbox ring full)")
+            tw = time.perf_counter() - t0
+        ack = self.ctl.load(C.F_ACK_SEQ, self.rank)
+        while self._inflight and self._inflight[0][0] <= ack:
+            self._inflight.popleft()
+        self._inflight.append((s, off, nbytes))
+        self._ring_off = off + nbytes
+        return off, tw
+
+    def _push_p2p(self, msg: torch.Tensor, s: int, vidx: int, partial: bool, flag: int):
         """Announce message s (version + presence flag, then the sequence word the PS waits on)
         and send it; the PS posts the matching receive when it sees the announcement.  The send
         is ordered after the encode on the comm stream, and the comm stream waits for it before
         the next encode overwrites the wire buffer."""
         C = self.C
         self.ctl.store(C.F_PUSH_VER, vidx, self.local_ver)
-        self.ctl.store(C.F_PUSH_FLAG, vidx, (bi << 1) | (1 if partial else 0))
+        self.ctl.store(C.F_PUSH_FLAG, vidx, flag)
         self.ctl.store(C.F_PUSH_SEQ, self.rank, s)
         ctx = torch.cuda.stream(self.comm_stream) if self.cuda else contextlib.nullcontext()
         with ctx, self.tracer.phase("push", self.comm_stream):
@@ -1364,23 +1442,27 @@ class PSAsyncEngine(Engine):
         ring = (self.step_no + 1) % RING
         n = self.store.numel
         C.pull_select_b(self._selb, *words, self.NPUB, 64)
+        sh = self._pull_shadow()
         if self._split is None:
-            C.pull_copy_b(self._selb, self._boff, base, self.pub_bytes, self.NPUB, bf16, self.store.data, 0, n)
+            C.pull_copy_b(self._selb, self._boff, base, self.pub_bytes, self.NPUB, bf16, self.store.data, 0, n, sh)
             C.pull_done_b(self._selb, *words, self._sel, ring)
+            if sh is not None:
+                self.store.refresh_shadow(cast=False)
+                self._shadow_done = True
             return True
         dev, s = self.store.device, self._split
         cs = torch.cuda.current_stream(dev)
         ev_sel = torch.cuda.Event()
         ev_sel.record(cs)
-        C.pull_copy_b(self._selb, self._boff, base, self.pub_bytes, self.NPUB, bf16, self.store.data, 0, s)
-        self.store.refresh_shadow(0, s)
+        C.pull_copy_b(self._selb, self._boff, base, self.pub_bytes, self.NPUB, bf16, self.store.data, 0, s, sh)
+        self.store.refresh_shadow(0, s, cast=sh is None)
         ev_early = torch.cuda.Event()
         ev_early.record(cs)
         side = self._late_stream
         with torch.cuda.stream(side):
             side.wait_event(ev_sel)
-            C.pull_copy_b(self._selb, self._boff, base, self.pub_bytes, self.NPUB, bf16, self.store.data, s, n)
-            self.store.refresh_shadow(s, n)
+            C.pull_copy_b(self._selb, self._boff, base, self.pub_bytes, self.NPUB, bf16, self.store.data, s, n, sh)
+            self.store.refresh_shadow(s, n, cast=sh is None)
             side.wait_event(ev_early)
             C.pull_done_b(self._selb, *words, self._sel, ring)
         late = torch.cuda.Event()
@@ -1433,8 +1515,16 @@ class PSAsyncEngine(Engine):
                  self.ctl.device_addr(C.F_READING, self.rank), self.ctl.device_addr(C.F_APPLIED_VER, self.rank))
         bf16 = self.pub_dtype == torch.bfloat16
         ring = (self.step_no + 1) % RING
+        sh = self._pull_shadow()
         if self._split is None:
-            self.C.pull_params(self._sel, *words, base, self.pub_bytes, self.NPUB, bf16, self.store.data, ring, 64)
+            if sh is None:
+                self.C.pull_params(self._sel, *words, base, self.pub_bytes, self.NPUB, bf16, self.store.data, ring, 64)
+                return True
+            self.C.pull_select(self._sel, *words, self.NPUB, 64)
+            self.C.pull_copy(self._sel, base, self.pub_bytes, self.NPUB, bf16, self.store.data, 0, self.store.numel, sh)
+            self.C.pull_done(self._sel, *words, ring)
+            self.store.refresh_shadow(cast=False)
+            self._shadow_done = True
             return True
         # pull_overlap: the early layers' range [0, split) on the compute stream, the late range on
         # a side stream that the late module's forward pre-hook waits for (set_pull_overlap)
@@ -1443,15 +1533,15 @@ class PSAsyncEngine(Engine):
         self.C.pull_select(self._sel, *words, self.NPUB, 64)
         ev_sel = torch.cuda.Event()
         ev_sel.record(cs)
-        self.C.pull_copy(self._sel, base, self.pub_bytes, self.NPUB, bf16, self.store.data, 0, s)
-        self.store.refresh_shadow(0, s)
+        self.C.pull_copy(self._sel, base, self.pub_bytes, self.NPUB, bf16, self.store.data, 0, s, sh)
+        self.store.refresh_shadow(0, s, cast=sh is None)
         ev_early = torch.cuda.Event()
         ev_early.record(cs)
         side = self._late_stream
         with torch.cuda.stream(side):
             side.wait_event(ev_sel)
-            self.C.pull_copy(self._sel, base, self.pub_bytes, self.NPUB, bf16, self.store.data, s, n)
-            self.store.refresh_shadow(s, n)
+            self.C.pull_copy(self._sel, base, self.pub_bytes, self.NPUB, bf16, self.store.data, s, n, sh)
+            self.store.refresh_shadow(s, n, cast=sh is None)
             side.wait_event(ev_early)  # the reader word is released after BOTH halves were read
             self.C.pull_done(self._sel, *words, ring)
         late = torch.cuda.Event()
@@ -1488,6 +1578,13 @@ class PSAsyncEngine(Engine):
         if ev is not None:
             torch.cuda.current_stream(self.store.device).wait_event(ev)
             self._late_ev = None
+
+    def _pull_shadow(self) -> Optional[torch.Tensor]:
+        """The flat bf16 weight shadow for the GPU-time pull to write in the same pass as the fp32
+        parameters (HIPPS_PULL_SHADOW=0: a separate cast pass after the pull, as before)."""
+        if os.environ.get("HIPPS_PULL_SHADOW", "1") == "0":
+            return None
+        return getattr(self.store, "shadow", None)
 
     def take_shadow_done(self) -> bool:
         """True once after a split pull refreshed the bf16 shadows itself."""

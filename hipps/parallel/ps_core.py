@@ -78,9 +78,9 @@ class PSCore:
         slot = s % self.SLOTS
         pos = (s - 1) % nb
         vidx = i * self.MAXSLOTS + slot
-        # the message names its bucket (flag word = bucket << 1 | presence bit): a worker pushes a
-        # step's buckets in completion order, not in a fixed order
-        bi = self.ctl.load(F.F_PUSH_FLAG, vidx) >> 1
+        # the message names its bucket (flag word = ring offset / 256 << 21 | bucket << 1 |
+        # presence bit): a worker pushes a step's buckets in completion order, not a fixed order
+        bi = (self.ctl.load(F.F_PUSH_FLAG, vidx) >> 1) & ((1 << 20) - 1)
         if pos == 0:  # a step's first message carries the version its gradient was computed on
             pv = self.ctl.load(F.F_PUSH_VER, vidx)
             stale = self.ver - pv

@@ -77,3 +77,59 @@ def test_llama_tiny_fused_act_matches_eager():
     (l1, g1), (l0, g0) = run(True), run(False)
     assert abs(l1 - l0) < 2e-2
     torch.testing.assert_close(g1, g0, rtol=5e-2, atol=5e-3)
+
+
+@pytest.mark.parametrize("R,D", [(16384, 768), (33, 64), (100, 2048), (7, 520)])
+def test_layer_norm_matches_fp32(R, D):
+    """csrc/ln.hip LayerNorm (bf16 rows, fp32 affine params) against F.layer_norm in fp32: output,
+    input gradient and the fp32 weight / bias gradients; the backward is deterministic."""
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(R + D)
+    x = (torch.randn(R, D, device=DEV) * 2 + 0.5).to(torch.bfloat16).requires_grad_(True)
+    w = torch.nn.Parameter(torch.randn(D, device=DEV) * 0.2 + 1)
+    b = torch.nn.Parameter(torch.randn(D, device=DEV) * 0.1)
+    assert hnn.layer_norm_ok(x, w, b)
+    y = hnn.layer_norm(x, w, b, 1e-12)
+    xf = x.detach().float().requires_grad_(True)
+    wf, bf = w.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    ref = F.layer_norm(xf, (D,), wf, bf, 1e-12)
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+    g = torch.randn(R, D, device=DEV).to(torch.bfloat16)
+    y.backward(g)
+    ref.backward(g.float())
+    torch.testing.assert_close(x.grad.float(), xf.grad, rtol=3e-2, atol=3e-2)
+    assert w.grad.dtype == torch.float32 and b.grad.dtype == torch.float32
+    tol = 2e-3 * R ** 0.5 + 1e-3
+    torch.testing.assert_close(w.grad, wf.grad, rtol=2e-2, atol=tol)
+    torch.testing.assert_close(b.grad, bf.grad, rtol=2e-2, atol=tol)
+    w.grad = b.grad = x.grad = None
+    hnn.layer_norm(x, w, b, 1e-12).backward(g)
+    dw1 = w.grad.clone()
+    w.grad = None
+    hnn.layer_norm(x, w, b, 1e-12).backward(g)
+    assert torch.equal(dw1, w.grad)
+
+
+def test_bert_tiny_fused_norm_matches_eager():
+    """bert-tiny forward + backward under autocast with the hipps LayerNorm vs F.layer_norm."""
+    from hipps.models.transformer import build
+    from hipps.ops import nn as hnn
+
+    def run(fused):
+        saved = hnn._FUSED_ACT
+        hnn._FUSED_ACT = fused
+        try:
+            torch.manual_seed(9)
+            m = build("bert-tiny").to(DEV)
+            ids = torch.randint(0, 512, (4, 32), device=DEV, generator=torch.Generator(device=DEV).manual_seed(10))
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = m(ids, ids)
+            loss.backward()
+            return loss.item(), torch.cat([p.grad.flatten() for p in m.parameters() if p.grad is not None])
+        finally:
+            hnn._FUSED_ACT = saved
+
+    (l1, g1), (l0, g0) = run(True), run(False)
+    assert abs(l1 - l0) < 2e-2
+    torch.testing.assert_close(g1, g0, rtol=5e-2, atol=5e-3)

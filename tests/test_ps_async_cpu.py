@@ -404,3 +404,34 @@ def test_async_push_early_past_a_bucket_without_gradients(granularity):
         assert a[r]["unused_same"] and b[r]["unused_same"]
         for x, y in zip(a[r]["params"], b[r]["params"]):
             torch.testing.assert_close(x, y, rtol=0, atol=0)
+
+
+def _ring(rank, world, mailbox_mb, granularity):
+    import hipps
+
+    m = _HeadPlusUnused()
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", bucket_mb=0.0005,
+                    max_delay=0, accumulate=world, ps_granularity=granularity, mailbox_mb=mailbox_mb)
+    eng = opt.engine
+    geo = (eng.SLOTS, eng.ring_bytes, max(eng.msg_ext), sum(eng.msg_ext))
+    for s in range(5):
+        x, y = _data(rank, s % 4)
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x), y).backward()
+        opt.step()
+    opt.close()
+    return {"geo": geo, "params": [p.detach().clone() for p in m.parameters()]}
+
+
+@pytest.mark.parametrize("granularity", ["model", "bucket"])
+def test_async_mailbox_ring_wraps(granularity):
+    """The per-worker mailbox is a byte ring of variable-size messages (their offsets ride in the
+    flag word): a ring of two largest messages, which wraps within every two steps, trains bit for
+    bit like a ring holding two whole steps."""
+    small = run_world(_ring, 2, 1e-6, granularity)
+    big = run_world(_ring, 2, 4096.0, granularity)
+    K, ring, mx, tot = small[0]["geo"]
+    assert ring == 2 * (mx + 256) < 2 * tot <= big[0]["geo"][1]
+    for r in range(2):
+        for x, y in zip(small[r]["params"], big[r]["params"]):
+            torch.testing.assert_close(x, y, rtol=0, atol=0)

@@ -126,14 +126,17 @@ def test_gpu_sync_engines_replicas_identical(mode, codec):
         assert torch.equal(a, b)
 
 
-def _tiny_overlap(rank, world, overlap, steps):
+def _tiny_overlap(rank, world, overlap, steps, pull_shadow="1"):
     import hashlib
 
     import torch.nn.functional as F
 
+    import os
+
     import hipps
     from hipps.models import resnet_tiny
 
+    os.environ["HIPPS_PULL_SHADOW"] = pull_shadow
     torch.backends.cudnn.deterministic = True
     torch.backends.cudnn.benchmark = False
     torch.cuda.set_device(0)
@@ -156,7 +159,8 @@ def _tiny_overlap(rank, world, overlap, steps):
     torch.cuda.synchronize()
     out = {"ok": ok, "losses": losses, "ver": opt.engine.adopted_version(),
            "sha": hashlib.sha1(opt.store.data.cpu().numpy().tobytes()).hexdigest(),
-           "shadow": hashlib.sha1(opt.store.shadow.view(torch.int16).cpu().numpy().tobytes()).hexdigest()}
+           "shadow": hashlib.sha1(opt.store.shadow.view(torch.int16).cpu().numpy().tobytes()).hexdigest(),
+           "shadow_is_cast": torch.equal(opt.store.shadow, opt.store.data.to(torch.bfloat16))}
     opt.close()
     return out
 
@@ -342,3 +346,13 @@ def test_gpu_async_memory_budget_refuses_before_allocating():
     assert msg is not None
     for term in ("mailbox", "publish", "master", "accumulator", "optimizer", "ps_dedicated"):
         assert term in msg, msg
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_gpu_async_pull_writes_shadow_bitwise(overlap):
+    """The GPU-time pull writes the bf16 weight shadow in the same pass as the fp32 parameters
+    (HIPPS_PULL_SHADOW, default on): bit for bit the separate cast pass (one-stream and split pull)."""
+    a = run_world(_tiny_overlap, 1, overlap, 6, "1")[0]
+    b = run_world(_tiny_overlap, 1, overlap, 6, "0")[0]
+    assert a["shadow_is_cast"] and b["shadow_is_cast"]
+    assert a["losses"] == b["losses"] and a["sha"] == b["sha"] and a["shadow"] == b["shadow"]
