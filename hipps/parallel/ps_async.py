@@ -108,6 +108,33 @@ def ps_memory_budget(numel: int, W: int, slots: int, slot_bytes: int, npub: int,
     return b
 
 
+def _open_mailbox_bounded(C, handle, total: int, rank: int, limit_s: Optional[float] = None):
+    """hipIpcOpenMemHandle of the PS mailbox, bounded: on the one-GPU rehearsal box (several ranks
+    sharing a device) the call occasionally never returned (profiles/r4/r4u, r4v: 1 of 6 probe
+    launches, any size).  A thread cannot cancel a call stuck in the driver, so past the limit the
+    process reports it and exits with status 3 (the watchdog's abort status) instead of leaving
+    the job hanging until an outer timeout.  HIPPS_IPC_OPEN_TIMEOUT_S sets the limit (default 120)."""
+    if limit_s is None:
+        limit_s = float(os.environ.get("HIPPS_IPC_OPEN_TIMEOUT_S", "120"))
+    done = threading.Event()
+
+    def _guard():
+        if not done.wait(limit_s):
+            import sys
+
+            sys.stderr.write(f"[hipps] rank {rank}: hipIpcOpenMemHandle of the PS mailbox ({total >> 20} MB) did not "
+                             f"return within {limit_s:.0f} s; exiting (status 3)\n")
+            sys.stderr.flush()
+            os._exit(3)
+
+    t = threading.Thread(target=_guard, name="hipps-ipc-open-guard", daemon=True)
+    t.start()
+    try:
+        return C.DeviceMailbox(handle, total)
+    finally:
+        done.set()
+
+
 def mailbox_geometry(msg_nbytes: Sequence[int], pres_bytes: int, mailbox_slots: int, mailbox_mb: float,
                      max_slots: int):
     """(word slots per worker, ring bytes per worker) of the PS mailbox: 2 x buckets message
@@ -452,7 +479,7 @@ class PSAsyncEngine(Engine):
                 if self.p2p:
                     self.mem = None
                 elif self.cuda:
-                    self.mailbox = C.DeviceMailbox(handle, total)
+                    self.mailbox = _open_mailbox_bounded(C, handle, total, self.rank)
                 else:
                     self.mailbox = C.HostMailbox(self.mb_name, total, False)
             except Exception as e:  # e.g. hipIpcOpenMemHandle refused across devices
