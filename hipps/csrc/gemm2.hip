@@ -54,8 +54,9 @@ __device__ __attribute__((aligned(64))) const uint16_t kZero16[32] = {0};
 // per K channel -- every thread transforms the 16-byte chunks it staged, in LDS, after its own
 // DMA landed and before the tile's barrier (rows / taps that read the zero page stay zero), so
 // the BN's output is never written (ResNet bn1 -> conv2, bn2 -> conv3)
-// kBias (1x1 only, alone): y = x w^T + bias[col], the fp32 bias added to the fp32 accumulator
-// before the one bf16 rounding (a Linear layer's addmm)
+// kBias (1x1 only; alone or with a plain kAdd): y = x w^T + bias[col] (+ R), the fp32 bias added
+// to the fp32 accumulator before the bf16 rounding (a Linear layer's addmm; + R: the residual
+// added by the same pass)
 enum Epi : int { kPlain = 0, kStats = 1, kAdd = 2, kBst = 4, kBstBits = 8, kAddS2 = 16, kPar = 32, kPro = 64,
                  kBias = 128 };
 
@@ -1136,11 +1137,12 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
     epi |= g2::kPro;
   }
   if (bias.has_value() && bias->defined()) {
-    TORCH_CHECK(epi == g2::kPlain && !taps, "gemm2: the bias epilogue runs alone on a 1x1 GEMM");
+    TORCH_CHECK((epi == g2::kPlain || epi == g2::kAdd) && !taps,
+                "gemm2: the bias epilogue runs on a 1x1 GEMM, alone or with a plain add (a residual)");
     TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() == N,
                 "gemm2: bias must be f32 [Cout]");
     a.bias = bias->data_ptr<float>();
-    epi = g2::kBias;
+    epi |= g2::kBias;
   }
   auto stream = c10::hip::getCurrentHIPStream();
   const int grid = (int)(mtiles * ntiles);
@@ -1168,6 +1170,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
         case g2::kStats: HIPPS_G2(BMc, BNc, g2::kStats, false); break;                              \
         case g2::kAdd: HIPPS_G2(BMc, BNc, g2::kAdd, false); break;                                  \
         case g2::kBias: HIPPS_G2(BMc, BNc, g2::kBias, false); break;                                \
+        case g2::kBias | g2::kAdd: HIPPS_G2(BMc, BNc, (g2::kBias | g2::kAdd), false); break;        \
         case g2::kBst: HIPPS_G2(BMc, BNc, g2::kBst, false); break;                                  \
         case g2::kBst | g2::kAdd: HIPPS_G2(BMc, BNc, (g2::kBst | g2::kAdd), false); break;          \
         case g2::kBstBits: HIPPS_G2(BMc, BNc, g2::kBstBits, false); break;                          \

@@ -74,8 +74,9 @@ class BertLayer(nn.Module):
 
         a = F.scaled_dot_product_attention(split(self.q(x)), split(self.k(x)), split(self.v(x)), attn_mask=mask)
         a = a.transpose(1, 2).reshape(B, S, D)
-        x = _ln(self.attn_ln, x + self.attn_out(a))
-        return _ln(self.out_ln, x + self.out(F.gelu(self.inter(x))))
+        # residual adds ride in the output projections (GEMM epilogue / hipBLASLt C)
+        x = _ln(self.attn_ln, self.attn_out(a, residual=x))
+        return _ln(self.out_ln, self.out(F.gelu(self.inter(x)), residual=x))
 
 
 class Bert(nn.Module):

@@ -681,16 +681,18 @@ class _ShadowLinear(torch.autograd.Function):
     BERT-base spent ~3 ms of a 38.8 ms step in those casts (profiles/r4/r4n/)."""
 
     @staticmethod
-    def forward(ctx, x, w_master, bias):
+    def forward(ctx, x, w_master, bias, residual=None):
         dt = torch.bfloat16
         w = bf16_weight(w_master)
         x2 = x.reshape(-1, x.shape[-1])
         if x2.dtype != dt:
             x2 = x2.to(dt)
-        y = _linear_fwd(x2, w, bias)
+        r2 = None if residual is None else residual.reshape(-1, w.shape[0])
+        y = _linear_fwd(x2, w, bias, r2)
         ctx.save_for_backward(x2, w_master)
         ctx.has_bias = bias is not None
         ctx.xshape, ctx.xdtype = x.shape, x.dtype
+        ctx.rshape = None if residual is None else residual.shape
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -710,27 +712,35 @@ class _ShadowLinear(torch.autograd.Function):
             dw = _linear_wgrad(dy2, x2)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = colsum_f32(dy2)
-        return dx, dw, db
+        dres = dy.reshape(ctx.rshape) if ctx.rshape is not None and ctx.needs_input_grad[3] else None
+        return dx, dw, db, dres
 
 
-def _linear_fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y = x2 w^T (+ bias) (bf16 [M, K] x [N, K] -> [M, N]): per shape the faster of hipBLASLt
-    (mm / addmm with the bf16 bias) and the hipps 1x1-convolution GEMM cores (a Linear is a 1x1
-    convolution over M pixels; their kBias epilogue adds the fp32 master bias to the fp32
-    accumulator before the one bf16 rounding)."""
+def _linear_fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
+                res: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x2 w^T (+ bias) (+ res) (bf16 [M, K] x [N, K] (+ bf16 [M, N]) -> [M, N]): per shape the
+    faster of hipBLASLt (mm / addmm with the bf16 bias or the residual as C) and the hipps
+    1x1-convolution GEMM cores (a Linear is a 1x1 convolution over M pixels; their kBias epilogue
+    adds the fp32 master bias to the fp32 accumulator before the bf16 rounding, kAdd the residual
+    in the same pass)."""
     M, K = x2.shape
     N = w.shape[0]
     y = torch.empty((M, N), dtype=torch.bfloat16, device=x2.device)
 
     def blas():
-        if bias is None:
+        if res is not None:
+            torch.addmm(res, x2, w.t(), out=y)
+            if bias is not None:
+                y.add_(bf16_weight(bias))
+        elif bias is None:
             torch.mm(x2, w.t(), out=y)
         else:
             torch.addmm(bf16_weight(bias), x2, w.t(), out=y)
 
     if not (_GEMM2 and N % 64 == 0 and K % 64 == 0 and M >= 1024 and x2.is_contiguous() and w.is_contiguous()
             and x2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and y.data_ptr() % 16 == 0
-            and (bias is None or (bias.dtype == torch.float32 and bias.is_contiguous() and bias.numel() == N))):
+            and (bias is None or (bias.dtype == torch.float32 and bias.is_contiguous() and bias.numel() == N))
+            and (res is None or (res.dtype == torch.bfloat16 and res.is_contiguous() and res.data_ptr() % 16 == 0))):
         blas()
         return y
     C = native()
@@ -739,8 +749,8 @@ def _linear_fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] 
     for name in _g2_names(N):
         bm, bn, ns = _g2_parse(name)
         cands[name] = (lambda bm=bm, bn=bn, ns=ns:
-                       C.gemm2_conv(x2, w, y, None, None, None, 1, 1, 1, 1, 1, 0, bm, bn, stages=ns, bias=b))
-    pick = TUNER.pick(("lfwd", M, N, K, bias is not None), cands)
+                       C.gemm2_conv(x2, w, y, None, res, None, 1, 1, 1, 1, 1, 0, bm, bn, stages=ns, bias=b))
+    pick = TUNER.pick(("lfwd", M, N, K, bias is not None, res is not None), cands)
     cands[pick]()
     return y
 
@@ -798,17 +808,21 @@ def mark_shadow_reader(*params) -> None:
             p.reads_bf16_shadow = True
 
 
-def shadow_linear_ok(x: torch.Tensor, weight: torch.Tensor, bias=None) -> bool:
+def shadow_linear_ok(x: torch.Tensor, weight: torch.Tensor, bias=None, residual=None) -> bool:
     return (_SHADOW_LINEAR and x.is_cuda and torch.is_autocast_enabled() and
             torch.get_autocast_dtype("cuda") == torch.bfloat16 and has_weight_shadow(weight) and
-            (bias is None or has_weight_shadow(bias)))
+            (bias is None or has_weight_shadow(bias)) and
+            (residual is None or (residual.dtype == torch.bfloat16 and residual.shape[-1] == weight.shape[0]
+                                  and residual.numel() == x.numel() // x.shape[-1] * weight.shape[0])))
 
 
-def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
-    """F.linear, on the bf16 weight shadow when one covers ``weight`` (see _ShadowLinear)."""
-    if shadow_linear_ok(x, weight, bias):
-        return _ShadowLinear.apply(x, weight, bias)
-    return F.linear(x, weight, bias)
+def linear(x: torch.Tensor, weight: torch.Tensor, bias=None, residual=None) -> torch.Tensor:
+    """F.linear (+ residual), on the bf16 weight shadow when one covers ``weight`` (see
+    _ShadowLinear; a bf16 residual is added in the GEMM's epilogue or as hipBLASLt's C)."""
+    if shadow_linear_ok(x, weight, bias, residual):
+        return _ShadowLinear.apply(x, weight, bias, residual)
+    y = F.linear(x, weight, bias)
+    return y if residual is None else residual + y
 
 
 class Linear(nn.Linear):
@@ -820,8 +834,8 @@ class Linear(nn.Linear):
         super().__init__(*args, **kwargs)
         mark_shadow_reader(self.weight, self.bias)
 
-    def forward(self, x):
-        return linear(x, self.weight, self.bias)
+    def forward(self, x, residual=None):
+        return linear(x, self.weight, self.bias, residual)
 
 
 class _CrossEntropy(torch.autograd.Function):

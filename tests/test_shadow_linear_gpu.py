@@ -210,3 +210,48 @@ def test_linear_fwd_bias_matches_fp32(m, n, k):
             y2 = torch.full_like(y, float("nan"))
             native().gemm2_conv(x, w, y2, None, None, None, 1, 1, 1, 1, 1, 0, bm, bn, stages=ns, bias=b)
             torch.testing.assert_close(y2.double(), ref, rtol=1e-2, atol=1e-2, msg=name)
+
+
+@pytest.mark.parametrize("m,n,k,bias", [(4096, 768, 768, True), (4096, 768, 3072, True), (2048, 1024, 512, False),
+                                        (200, 128, 64, True)])
+def test_linear_fwd_residual_matches_fp32(m, n, k, bias):
+    """y = x w^T (+ b) + r: the tuner-picked route (hipBLASLt with r as C, or a gemm2 core with the
+    kBias | kAdd epilogue) and every gemm2 candidate on its own, against fp64."""
+    from hipps.ops import nn as hnn
+    from hipps.ops._native import native
+
+    torch.manual_seed(m + n + k)
+    x = torch.randn(m, k, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(n, k, device=DEV) / k ** 0.5).to(torch.bfloat16)
+    b = torch.randn(n, device=DEV) if bias else None
+    r = torch.randn(m, n, device=DEV).to(torch.bfloat16)
+    y = hnn._linear_fwd(x, w, b, r)
+    ref = x.double() @ w.double().t() + r.double() + (b.double() if bias else 0)
+    torch.testing.assert_close(y.double(), ref, rtol=2e-2, atol=2e-2)
+    if m >= 1024:
+        for name in hnn._g2_names(n):
+            bm, bn, ns = hnn._g2_parse(name)
+            y2 = torch.full_like(y, float("nan"))
+            native().gemm2_conv(x, w, y2, None, r, None, 1, 1, 1, 1, 1, 0, bm, bn, stages=ns, bias=b)
+            torch.testing.assert_close(y2.double(), ref, rtol=2e-2, atol=2e-2, msg=name)
+
+
+def test_shadow_linear_residual_gradients():
+    """linear(x, w, b, residual=r) under autocast on the shadow: r's gradient is dy itself."""
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(11)
+    flat, shadow, (w, b) = _shadowed((64, 64), (64,))
+    try:
+        x = torch.randn(2, 40, 64, device=DEV, requires_grad=True)
+        r = torch.randn(2, 40, 64, device=DEV).to(torch.bfloat16).requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            assert hnn.shadow_linear_ok(x, w, b, r)
+            y = hnn.linear(x, w, b, residual=r)
+        g = torch.randn_like(y)
+        y.backward(g)
+        assert r.grad.dtype == torch.bfloat16 and torch.equal(r.grad, g)
+        ref = F.linear(x.detach().double(), w.detach().double(), b.detach().double()) + r.detach().double()
+        torch.testing.assert_close(y.double(), ref, rtol=3e-2, atol=3e-2)
+    finally:
+        hnn.unregister_weight_shadow(shadow)
