@@ -105,6 +105,8 @@ void swiglu_forward(at::Tensor a, at::Tensor b, at::Tensor c);
 void ln_forward(at::Tensor x, at::Tensor w, at::Tensor b, at::Tensor y, at::Tensor mean, at::Tensor rstd, double eps);
 void ln_backward(at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor rstd, at::Tensor w, at::Tensor dx,
                  at::Tensor dw, at::Tensor db);
+void rms_forward(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor rstd, double eps);
+void rms_backward(at::Tensor dy, at::Tensor x, at::Tensor rstd, at::Tensor w, at::Tensor dx, at::Tensor dw);
 void swiglu_backward(at::Tensor g, at::Tensor a, at::Tensor b, at::Tensor da, at::Tensor db);
 void rope_apply(at::Tensor x, at::Tensor y, at::Tensor cs, at::Tensor sn, int64_t S, int64_t hd, double sign);
 void xent_backward(at::Tensor logits, at::Tensor labels, at::Tensor lse, at::Tensor gout, double scale,
@@ -244,6 +246,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("shift") = pybind11::none());
   m.def("bn_finalize_partials", &hipps::bn_finalize_partials,
         "BN train-mode finalize from producer partial sums (mean/invstd/scale/shift + running stats)");
+  m.def("rms_forward", &hipps::rms_forward, "RMSNorm forward: fp32 / bf16 rows -> bf16, fp32 rstd (ln.hip)");
+  m.def("rms_backward", &hipps::rms_backward, "RMSNorm backward: dx in x's dtype, fp32 weight gradient (ln.hip)");
   m.def("ln_forward", &hipps::ln_forward, "LayerNorm forward, bf16 rows, fp32 weight / bias / mean / rstd (ln.hip)");
   m.def("ln_backward", &hipps::ln_backward, "LayerNorm backward: bf16 dx, fp32 weight / bias gradients (ln.hip)");
   m.def("swiglu_forward", &hipps::swiglu_forward, "c = silu(a) * b, bf16 (act.hip)");

@@ -1,4 +1,4 @@
-// hipps — LayerNorm over the last dim of a bf16 [rows, D] activation (BERT's 25 norms per step).
+// hipps — LayerNorm (BERT's 25 norms per step) and RMSNorm (Llama) over the last dim of [rows, D].
 //
 // PyTorch's route under autocast (hipps/models/transformer.py _ln) casts the fp32 weight and bias
 // to bf16 every forward, runs the forward at ~1.7 TB/s, and the backward as an input-gradient
@@ -186,26 +186,154 @@ __global__ __launch_bounds__(64 * kLnWaves) void k_ln_bwd(const uint16_t* __rest
   }
 }
 
-// out[k * D + col] = sum_p part[p][k][col] (k = 0: dgamma, 1: dbeta), fixed order
-__global__ __launch_bounds__(256) void k_ln_fold(const float* __restrict__ part, int P, int D, float* __restrict__ dw,
-                                                 float* __restrict__ dbias) {
+// out[k * D + col] = sum_p part[p][k][col] (k = 0: dgamma, 1: dbeta when nk == 2), fixed order
+__global__ __launch_bounds__(256) void k_ln_fold(const float* __restrict__ part, int P, int D, int nk,
+                                                 float* __restrict__ dw, float* __restrict__ dbias) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int i = blockIdx.x * 64 + lane;  // over 2 * D
-  const int ii = i < 2 * D ? i : 0;
+  const int i = blockIdx.x * 64 + lane;  // over nk * D
+  const int ii = i < nk * D ? i : 0;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   int p = wv;
   for (; p + 12 < P; p += 16) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] += part[(int64_t)(p + 4 * j) * 2 * D + ii];
+    for (int j = 0; j < 4; ++j) acc[j] += part[(int64_t)(p + 4 * j) * nk * D + ii];
   }
-  for (; p < P; p += 4) acc[0] += part[(int64_t)p * 2 * D + ii];
+  for (; p < P; p += 4) acc[0] += part[(int64_t)p * nk * D + ii];
   red[wv][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   __syncthreads();
-  if (wv == 0 && i < 2 * D) {
+  if (wv == 0 && i < nk * D) {
     const float a = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
     if (i < D) dw[i] = a;
     else dbias[i - D] = a;
+  }
+}
+
+// ---- RMSNorm (Llama): y = x * rsqrt(mean(x^2) + eps) * w, x fp32 (the residual stream) or bf16 --
+template <typename TX> struct Ld8;
+template <> struct Ld8<float> {
+  __device__ __forceinline__ static void load(const float* p, float* f) {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+  }
+  __device__ __forceinline__ static void store(float* p, const float* f) {
+    *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(f[4], f[5], f[6], f[7]);
+  }
+};
+template <> struct Ld8<uint16_t> {
+  __device__ __forceinline__ static void load(const uint16_t* p, float* f) { unpack8(*reinterpret_cast<const u32x4*>(p), f); }
+  __device__ __forceinline__ static void store(uint16_t* p, const float* f) {
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(f[2 * j], f[2 * j + 1]);
+    *reinterpret_cast<u32x4*>(p) = o;
+  }
+};
+
+__device__ __forceinline__ void load_w8(const float* w, float* f) { Ld8<float>::load(w, f); }
+
+// NC <= 8: D <= 4096
+template <int NC, typename TX>
+__global__ __launch_bounds__(64 * kLnWaves) void k_rms_fwd(const TX* __restrict__ x, const float* __restrict__ w,
+                                                           uint16_t* __restrict__ y, float* __restrict__ rstd_out,
+                                                           int64_t R, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * kLnWaves + (threadIdx.x >> 6);
+  if (row >= R) return;
+  const int nch = D >> 3;
+  float v[NC][8];
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      Ld8<TX>::load(x + row * D + ch * 8, v[c]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q += v[c][j] * v[c][j];
+    }
+  }
+  const float rs = rsqrtf(wsum(q) / D + eps);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      float ww[8], o[8];
+      load_w8(w + ch * 8, ww);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[c][j] * rs * ww[j];
+      Ld8<uint16_t>::store(y + row * D + ch * 8, o);
+    }
+  }
+  if (lane == 0) rstd_out[row] = rs;
+}
+
+// dx = rs (g - xhat mean(g xhat)), g = dy w, xhat = x rs; dw partial = sum_rows dy xhat.  Two
+// passes over each row (the second re-reads it from cache) keep the registers to w + dw sums.
+template <int NC, typename TX>
+__global__ __launch_bounds__(64 * kLnWaves) void k_rms_bwd(const uint16_t* __restrict__ dy, const TX* __restrict__ x,
+                                                           const float* __restrict__ rstd, const float* __restrict__ w,
+                                                           TX* __restrict__ dx, float* __restrict__ part, int64_t R,
+                                                           int D, int rpb) {
+  extern __shared__ float red[];  // [kLnWaves][D]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nch = D >> 3;
+  float ww[NC][8], dg[NC][8];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int ch = lane + 64 * c;
+    load_w8(w + (ch < nch ? ch : 0) * 8, ww[c]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dg[c][j] = 0.f;
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = r0 + rpb < R ? r0 + rpb : R;
+  for (int64_t row = r0 + wv; row < r1; row += kLnWaves) {
+    const float rs = rstd[row];
+    float s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nch) {
+        float xv[8], gy[8];
+        Ld8<TX>::load(x + row * D + ch * 8, xv);
+        unpack8(*reinterpret_cast<const u32x4*>(dy + row * D + ch * 8), gy);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s2 += gy[j] * ww[c][j] * xv[j] * rs;
+      }
+    }
+    const float m2 = wsum(s2) / D;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nch) {
+        float xv[8], gy[8], o[8];
+        Ld8<TX>::load(x + row * D + ch * 8, xv);
+        unpack8(*reinterpret_cast<const u32x4*>(dy + row * D + ch * 8), gy);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = xv[j] * rs;
+          o[j] = rs * (gy[j] * ww[c][j] - xh * m2);
+          dg[c][j] += gy[j] * xh;
+        }
+        Ld8<TX>::store(dx + row * D + ch * 8, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[wv * D + ch * 8 + j] = dg[c][j];
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < D; i += 64 * kLnWaves) {
+    float a = 0.f;
+#pragma unroll
+    for (int q = 0; q < kLnWaves; ++q) a += red[q * D + i];
+    part[(int64_t)blockIdx.x * D + i] = a;
   }
 }
 
@@ -279,8 +407,85 @@ void ln_backward(at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor rstd, 
   else if (nc <= 2) HIPPS_LNB(2);
   else HIPPS_LNB(4);
 #undef HIPPS_LNB
-  hipLaunchKernelGGL(k_ln_fold, (int)((2 * D + 63) / 64), 256, 0, st, part.data_ptr<float>(), (int)P, (int)D,
+  hipLaunchKernelGGL(k_ln_fold, (int)((2 * D + 63) / 64), 256, 0, st, part.data_ptr<float>(), (int)P, (int)D, 2,
                      dw.data_ptr<float>(), db.data_ptr<float>());
+}
+
+// x: fp32 or bf16 [rows, D] (D % 8 == 0, D <= 4096); y bf16; rstd fp32 [rows]
+void rms_forward(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor rstd, double eps) {
+  const int64_t D = x.size(-1);
+  TORCH_CHECK(x.is_cuda() && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16) && x.is_contiguous() &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "rms_norm: x must be a contiguous 16-byte aligned fp32 / bf16 device tensor");
+  TORCH_CHECK(D % 8 == 0 && D >= 8 && D <= 4096, "rms_norm: D % 8 == 0, D <= 4096");
+  ln_check(y, D);
+  ln_param_check(w, D, "weight");
+  const int64_t R = x.numel() / D;
+  TORCH_CHECK(y.numel() == x.numel() && rstd.numel() == R && rstd.scalar_type() == at::kFloat, "rms_norm: sizes");
+  if (R == 0) return;
+  const int grid = (int)((R + kLnWaves - 1) / kLnWaves);
+  auto st = c10::hip::getCurrentHIPStream();
+  const int nc = (int)((D / 8 + 63) / 64);
+  const bool f32 = x.scalar_type() == at::kFloat;
+#define HIPPS_RMSF(NCc)                                                                                                \
+  do {                                                                                                                 \
+    if (f32)                                                                                                           \
+      hipLaunchKernelGGL((k_rms_fwd<NCc, float>), grid, 64 * kLnWaves, 0, st, x.data_ptr<float>(), w.data_ptr<float>(), \
+                         (uint16_t*)y.data_ptr(), rstd.data_ptr<float>(), R, (int)D, (float)eps);                      \
+    else                                                                                                               \
+      hipLaunchKernelGGL((k_rms_fwd<NCc, uint16_t>), grid, 64 * kLnWaves, 0, st, (const uint16_t*)x.data_ptr(),        \
+                         w.data_ptr<float>(), (uint16_t*)y.data_ptr(), rstd.data_ptr<float>(), R, (int)D, (float)eps); \
+  } while (0)
+  if (nc <= 1) HIPPS_RMSF(1);
+  else if (nc <= 2) HIPPS_RMSF(2);
+  else if (nc <= 4) HIPPS_RMSF(4);
+  else HIPPS_RMSF(8);
+#undef HIPPS_RMSF
+}
+
+// dy bf16; x / dx fp32 or bf16 (same dtype); dw fp32 [D]
+void rms_backward(at::Tensor dy, at::Tensor x, at::Tensor rstd, at::Tensor w, at::Tensor dx, at::Tensor dw) {
+  const int64_t D = x.size(-1);
+  TORCH_CHECK(x.is_cuda() && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16) && x.is_contiguous() &&
+                  dx.scalar_type() == x.scalar_type() && dx.is_contiguous() && dx.numel() == x.numel() &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(dx.data_ptr()) % 16 == 0,
+              "rms_norm backward: x / dx");
+  TORCH_CHECK(D % 8 == 0 && D >= 8 && D <= 4096, "rms_norm: D % 8 == 0, D <= 4096");
+  ln_check(dy, D);
+  ln_param_check(w, D, "weight");
+  ln_param_check(dw, D, "weight gradient");
+  const int64_t R = x.numel() / D;
+  TORCH_CHECK(dy.numel() == x.numel() && rstd.numel() == R, "rms_norm backward: sizes");
+  if (R == 0) {
+    dw.zero_();
+    return;
+  }
+  int64_t P = std::min<int64_t>(1024, std::max<int64_t>(1, R / 16));
+  const int rpb = (int)((R + P - 1) / P);
+  P = (R + rpb - 1) / rpb;
+  at::Tensor part = at::empty({P, D}, dw.options());
+  auto st = c10::hip::getCurrentHIPStream();
+  const size_t lds = (size_t)kLnWaves * D * sizeof(float);
+  const int nc = (int)((D / 8 + 63) / 64);
+  const bool f32 = x.scalar_type() == at::kFloat;
+#define HIPPS_RMSB(NCc)                                                                                               \
+  do {                                                                                                                \
+    if (f32)                                                                                                          \
+      hipLaunchKernelGGL((k_rms_bwd<NCc, float>), (int)P, 64 * kLnWaves, lds, st, (const uint16_t*)dy.data_ptr(),     \
+                         x.data_ptr<float>(), rstd.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(),      \
+                         part.data_ptr<float>(), R, (int)D, rpb);                                                     \
+    else                                                                                                              \
+      hipLaunchKernelGGL((k_rms_bwd<NCc, uint16_t>), (int)P, 64 * kLnWaves, lds, st, (const uint16_t*)dy.data_ptr(),  \
+                         (const uint16_t*)x.data_ptr(), rstd.data_ptr<float>(), w.data_ptr<float>(),                  \
+                         (uint16_t*)dx.data_ptr(), part.data_ptr<float>(), R, (int)D, rpb);                            \
+  } while (0)
+  if (nc <= 1) HIPPS_RMSB(1);
+  else if (nc <= 2) HIPPS_RMSB(2);
+  else if (nc <= 4) HIPPS_RMSB(4);
+  else HIPPS_RMSB(8);
+#undef HIPPS_RMSB
+  hipLaunchKernelGGL(k_ln_fold, (int)((D + 63) / 64), 256, 0, st, part.data_ptr<float>(), (int)P, (int)D, 1,
+                     dw.data_ptr<float>(), dw.data_ptr<float>());
 }
 
 }  // namespace hipps

@@ -142,6 +142,9 @@ class RMSNorm(nn.Module):
         self.eps = eps
 
     def forward(self, x):
+        if x.is_cuda and torch.is_autocast_enabled() and hnn.rms_norm_ok(x, self.weight):
+            # csrc/ln.hip: reads the fp32 residual stream directly, writes bf16 (no cast kernels)
+            return hnn.rms_norm(x, self.weight, self.eps)
         if x.is_cuda:
             # one fused kernel (aten._fused_rms_norm, fp32 math) on the activation dtype instead of
             # six eager ops over an fp32 copy

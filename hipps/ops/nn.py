@@ -941,6 +941,44 @@ def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: f
     return _LayerNorm.apply(x, weight, bias, eps)
 
 
+class _RMSNorm(torch.autograd.Function):
+    """RMSNorm over the last dim (csrc/ln.hip): reads the fp32 residual stream (or bf16) directly
+    -- no cast kernel -- writes bf16; the backward writes dx in x's dtype (the fp32 residual
+    gradient, no cast back) and the fp32 weight gradient."""
+
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        D = x.shape[-1]
+        y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+        rstd = torch.empty(x.numel() // D, dtype=torch.float32, device=x.device)
+        native().rms_forward(x, w, y, rstd, float(eps))
+        ctx.save_for_backward(x, w, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, rstd = ctx.saved_tensors
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = torch.empty_like(x)
+        dw = torch.empty_like(w)
+        native().rms_backward(dy, x, rstd, w, dx, dw)
+        return dx, dw, None
+
+
+def rms_norm_ok(x: torch.Tensor, weight) -> bool:
+    """Can _RMSNorm run (fp32 / bf16 contiguous x, D % 8 == 0, D <= 4096, fp32 weight)?"""
+    D = x.shape[-1] if x.dim() else 0
+    return (_FUSED_ACT and weight is not None and x.is_cuda and x.dtype in (torch.float32, torch.bfloat16)
+            and x.is_contiguous() and D % 8 == 0 and 8 <= D <= 4096 and x.data_ptr() % 16 == 0
+            and weight.dtype == torch.float32 and weight.is_contiguous() and weight.numel() == D
+            and weight.data_ptr() % 16 == 0)
+
+
+def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:
+    """bf16 RMSNorm of x over the last dim on the fused kernels (callers check rms_norm_ok)."""
+    return _RMSNorm.apply(x, weight, eps)
+
+
 class _Rope(torch.autograd.Function):
     """Rotary embedding of interleaved pairs on x [B, S, H, hd] bf16 (csrc/act.hip k_rope, fp32
     cos / sin tables [S, hd/2]); the backward is the rotation by -theta."""

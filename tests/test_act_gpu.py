@@ -133,3 +133,34 @@ def test_bert_tiny_fused_norm_matches_eager():
     (l1, g1), (l0, g0) = run(True), run(False)
     assert abs(l1 - l0) < 2e-2
     torch.testing.assert_close(g1, g0, rtol=5e-2, atol=5e-3)
+
+
+@pytest.mark.parametrize("R,D,dtype", [(8192, 2048, torch.float32), (2048, 4096, torch.float32), (33, 64, torch.bfloat16),
+                                       (100, 4096, torch.bfloat16), (7, 1000 // 8 * 8, torch.float32)])
+def test_rms_norm_matches_fp32(R, D, dtype):
+    """csrc/ln.hip RMSNorm (fp32 or bf16 rows -> bf16, fp32 weight) against the fp32 formula: output,
+    input gradient in x's dtype and the fp32 weight gradient; deterministic backward."""
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(R + D)
+    x = (torch.randn(R, D, device=DEV) * 3).to(dtype).requires_grad_(True)
+    w = torch.nn.Parameter(torch.randn(D, device=DEV) * 0.2 + 1)
+    assert hnn.rms_norm_ok(x, w)
+    y = hnn.rms_norm(x, w, 1e-5)
+    assert y.dtype == torch.bfloat16
+    xf = x.detach().float().requires_grad_(True)
+    wf = w.detach().clone().requires_grad_(True)
+    ref = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * wf
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+    g = torch.randn(R, D, device=DEV).to(torch.bfloat16)
+    y.backward(g)
+    ref.backward(g.float())
+    assert x.grad.dtype == dtype and w.grad.dtype == torch.float32
+    torch.testing.assert_close(x.grad.float(), xf.grad, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(w.grad, wf.grad, rtol=2e-2, atol=2e-3 * R ** 0.5 + 1e-3)
+    w.grad = None
+    hnn.rms_norm(x, w, 1e-5).backward(g)
+    dw1 = w.grad.clone()
+    w.grad = None
+    hnn.rms_norm(x, w, 1e-5).backward(g)
+    assert torch.equal(dw1, w.grad)
