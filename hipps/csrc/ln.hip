@@ -337,9 +337,9 @@ __global__ __launch_bounds__(64 * kLnWaves) void k_rms_bwd(const uint16_t* __res
   }
 }
 
-void ln_check(const at::Tensor& x, int64_t D) {
+void ln_check(const at::Tensor& x, int64_t D, int64_t dmax = 2048) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "layer_norm: contiguous bf16");
-  TORCH_CHECK(D % 8 == 0 && D >= 8 && D <= 2048 && x.numel() % D == 0, "layer_norm: D % 8 == 0, D <= 2048");
+  TORCH_CHECK(D % 8 == 0 && D >= 8 && D <= dmax && x.numel() % D == 0, "norm: D % 8 == 0, D <= ", dmax);
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "layer_norm: 16-byte aligned");
 }
 
@@ -418,7 +418,7 @@ void rms_forward(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor rstd, doub
                   reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
               "rms_norm: x must be a contiguous 16-byte aligned fp32 / bf16 device tensor");
   TORCH_CHECK(D % 8 == 0 && D >= 8 && D <= 4096, "rms_norm: D % 8 == 0, D <= 4096");
-  ln_check(y, D);
+  ln_check(y, D, 4096);
   ln_param_check(w, D, "weight");
   const int64_t R = x.numel() / D;
   TORCH_CHECK(y.numel() == x.numel() && rstd.numel() == R && rstd.scalar_type() == at::kFloat, "rms_norm: sizes");
@@ -451,7 +451,7 @@ void rms_backward(at::Tensor dy, at::Tensor x, at::Tensor rstd, at::Tensor w, at
                   reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(dx.data_ptr()) % 16 == 0,
               "rms_norm backward: x / dx");
   TORCH_CHECK(D % 8 == 0 && D >= 8 && D <= 4096, "rms_norm: D % 8 == 0, D <= 4096");
-  ln_check(dy, D);
+  ln_check(dy, D, 4096);
   ln_param_check(w, D, "weight");
   ln_param_check(dw, D, "weight gradient");
   const int64_t R = x.numel() / D;
