@@ -67,6 +67,8 @@ _WGRAD_SIDE = _os.environ.get("HIPPS_WGRAD_STREAM", "1") != "0"
 _SHADOW_LINEAR = _os.environ.get("HIPPS_SHADOW_LINEAR", "1") != "0"
 # softmax cross-entropy of bf16 logits on csrc/xent.hip (hipps.ops.nn.cross_entropy); 0: PyTorch
 _FUSED_XENT = _os.environ.get("HIPPS_FUSED_XENT", "1") != "0"
+# residual adds of the transformer output projections inside the Linear (A/B: 0 = a separate add)
+_LINEAR_RESIDUAL = _os.environ.get("HIPPS_LINEAR_RESIDUAL", "1") != "0"
 # SwiGLU gate and rotary embedding of the Llama block as one HIP pass each (csrc/act.hip)
 _FUSED_ACT = _os.environ.get("HIPPS_FUSED_ACT", "1") != "0"
 _WG_STREAMS: dict = {}
@@ -819,6 +821,8 @@ def shadow_linear_ok(x: torch.Tensor, weight: torch.Tensor, bias=None, residual=
 def linear(x: torch.Tensor, weight: torch.Tensor, bias=None, residual=None) -> torch.Tensor:
     """F.linear (+ residual), on the bf16 weight shadow when one covers ``weight`` (see
     _ShadowLinear; a bf16 residual is added in the GEMM's epilogue or as hipBLASLt's C)."""
+    if residual is not None and not _LINEAR_RESIDUAL:
+        return residual + linear(x, weight, bias)
     if shadow_linear_ok(x, weight, bias, residual):
         return _ShadowLinear.apply(x, weight, bias, residual)
     y = F.linear(x, weight, bias)
