@@ -234,10 +234,13 @@ class Engine:
             C.gather_flat(srcs, table, dst, 1.0)
         return dense
 
-    def encode_bucket(self, bi: int):
+    def encode_bucket(self, bi: int, views=None):
+        """Encode bucket bi's gradient into its message -- in the wire buffer, or into ``views``
+        (ps_async: straight into the bucket's mailbox ring space)."""
         b = self.plan.buckets[bi]
         g = self.store.grad[b.lo:b.hi]
-        views = self.plan.views(self.wire, bi)
+        if views is None:
+            views = self.plan.views(self.wire, bi)
         if self.is_object:  # host codec objects: run on finished gradients (ps.py:94 in a pool)
             if self.cuda:
                 torch.cuda.current_stream(self.store.device).synchronize()

@@ -537,6 +537,14 @@ class PSAsyncEngine(Engine):
             and self._fault is None and not self.plan.guarded and not self.ps_only
         self._npushed, self._push_wait, self._in_encode_all = 0, 0.0, False
         self._pushed_b = bytearray(self.nb)  # buckets already pushed this step (any order)
+        # direct push: a hook-time bucket is encoded straight into its space in the (local) mailbox
+        # ring -- no wire-buffer image and no copy.  Rank 0's own worker only (its mailbox is local
+        # HBM); static-size codecs (the byte accounting reads variable-size counts from the wire)
+        from ..codecs import Codec as _Codec
+
+        self._direct_push = (self._early and self.cuda and self.rank == 0 and not self.plan.guarded
+                             and type(self.codec).used_bytes is _Codec.used_bytes
+                             and os.environ.get("HIPPS_DIRECT_PUSH", "1") != "0")
         self._lat = (_LatencyProbe() if self.cuda and self.rank == 0 and not self.dedicated
                      and os.environ.get("HIPPS_PS_LATENCY", "0") == "1" else None)
         self._err: Optional[str] = None
@@ -1163,7 +1171,7 @@ class PSAsyncEngine(Engine):
         self.close()
         return self.ps_stats()
 
-    def _push_one(self, pos: int, bi: int, partial: int) -> float:
+    def _push_one(self, pos: int, bi: int, partial: int, encode: bool = False) -> float:
         """Push message ``pos`` of this step (bucket ``bi``) to the next offset of this worker's
         mailbox ring: copy on the comm stream (after the bucket's encode), then the GPU doorbell
         with its version / flag / sequence words.  The flag word is
@@ -1201,11 +1209,15 @@ class PSAsyncEngine(Engine):
         sbuf = self._ring_buf(self.rank, off, ext)
         dst = sbuf[: b.msg_nbytes]
         words = [(C.F_PUSH_VER, vidx, self.local_ver), (C.F_PUSH_FLAG, vidx, flag), (C.F_PUSH_SEQ, self.rank, s)]
+        if encode:  # the bucket's encode writes the message here (comm stream); nothing to copy
+            Engine.encode_bucket(self, bi, views=b.layout.views(dst[: b.layout.nbytes]))
         if self.cuda:
             cs = self.comm_stream
             with torch.cuda.stream(cs), self.tracer.phase("push", cs):
                 # variable-size codes (threshold) move 16 + count * entry bytes, not capacity
-                if self.plan.guarded or not self.codec.push_copy(b.layout, src, dst):
+                if encode:
+                    pass
+                elif self.plan.guarded or not self.codec.push_copy(b.layout, src, dst):
                     dst.copy_(src, non_blocking=True)
                 if pres:
                     ns = len(self.store.slots)
@@ -1228,6 +1240,12 @@ class PSAsyncEngine(Engine):
         buckets while the worker is still computing the first layers' gradients.  A bucket with a
         parameter that gets no gradient this step (e.g. BERT's pooler under an MLM-only loss) waits
         for step() without holding back the buckets behind it."""
+        if (self._direct_push and not self._in_encode_all and not self._pushed_b[bi]
+                and self._bucket_count[bi] == len(self.plan.buckets[bi].slot_ids)):
+            self._push_wait += self._push_one(self._npushed, bi, 0, encode=True)
+            self._pushed_b[bi] = 1
+            self._npushed += 1
+            return
         super().encode_bucket(bi)
         if not self._early or self._in_encode_all:
             return

@@ -126,7 +126,7 @@ def test_gpu_sync_engines_replicas_identical(mode, codec):
         assert torch.equal(a, b)
 
 
-def _tiny_overlap(rank, world, overlap, steps, pull_shadow="1"):
+def _tiny_overlap(rank, world, overlap, steps, pull_shadow="1", direct_push="1"):
     import hashlib
 
     import torch.nn.functional as F
@@ -137,6 +137,7 @@ def _tiny_overlap(rank, world, overlap, steps, pull_shadow="1"):
     from hipps.models import resnet_tiny
 
     os.environ["HIPPS_PULL_SHADOW"] = pull_shadow
+    os.environ["HIPPS_DIRECT_PUSH"] = direct_push
     torch.backends.cudnn.deterministic = True
     torch.backends.cudnn.benchmark = False
     torch.cuda.set_device(0)
@@ -160,7 +161,8 @@ def _tiny_overlap(rank, world, overlap, steps, pull_shadow="1"):
     out = {"ok": ok, "losses": losses, "ver": opt.engine.adopted_version(),
            "sha": hashlib.sha1(opt.store.data.cpu().numpy().tobytes()).hexdigest(),
            "shadow": hashlib.sha1(opt.store.shadow.view(torch.int16).cpu().numpy().tobytes()).hexdigest(),
-           "shadow_is_cast": torch.equal(opt.store.shadow, opt.store.data.to(torch.bfloat16))}
+           "shadow_is_cast": torch.equal(opt.store.shadow, opt.store.data.to(torch.bfloat16)),
+           "direct": opt.engine._direct_push}
     opt.close()
     return out
 
@@ -355,4 +357,13 @@ def test_gpu_async_pull_writes_shadow_bitwise(overlap):
     a = run_world(_tiny_overlap, 1, overlap, 6, "1")[0]
     b = run_world(_tiny_overlap, 1, overlap, 6, "0")[0]
     assert a["shadow_is_cast"] and b["shadow_is_cast"]
+    assert a["losses"] == b["losses"] and a["sha"] == b["sha"] and a["shadow"] == b["shadow"]
+
+
+def test_gpu_async_direct_push_bitwise():
+    """Hook-time buckets encoded straight into rank 0's mailbox ring (HIPPS_DIRECT_PUSH, default
+    on) train bit for bit like the encode into the wire buffer plus the push copy."""
+    a = run_world(_tiny_overlap, 1, False, 6, "1", "1")[0]
+    b = run_world(_tiny_overlap, 1, False, 6, "1", "0")[0]
+    assert a["direct"] and not b["direct"]
     assert a["losses"] == b["losses"] and a["sha"] == b["sha"] and a["shadow"] == b["shadow"]
