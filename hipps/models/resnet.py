@@ -14,7 +14,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from hipps.ops.nn import (FusedBatchNorm2d, MaxPool2d, ResidualTap, bn_relu_conv, bn_relu_conv1x1_ok,
+from hipps.ops.nn import (FusedBatchNorm2d, Linear, MaxPool2d, ResidualTap, bn_relu_conv, bn_relu_conv1x1_ok,
                           bn_relu_conv_bn, bn_relu_conv_ok, bn_relu_maxpool, conv1x1_bn_input, conv1x1_ok, conv2d,
                           conv2d_bn, conv2d_stats, conv_bn, dual_bn_relu, dual_bn_relu_ok, global_avg_pool,
                           stem_block, stem_block_ok)
@@ -221,7 +221,7 @@ class ResNet(nn.Module):
         self.num_stages = len(stages)
         for i, st in enumerate(stages):
             setattr(self, f"layer{i + 1}", st)
-        self.fc = nn.Linear(cin, num_classes)
+        self.fc = Linear(cin, num_classes)  # hipps.ops.nn.Linear: reads the bf16 weight shadow
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
