@@ -290,6 +290,7 @@ def main():
         trace = {k: round(v / a.steps, 4) for k, v in tr.totals.items()}
     nbuckets = len(opt.engine.plan.buckets)
     gran_eff = getattr(opt.engine, "granularity", None)
+    ti = opt.engine.transport_info() if hasattr(opt.engine, "transport_info") else {}
     nparams = sum(p.numel() for p in model.parameters())
     opt.close()
     stats = {}
@@ -344,6 +345,9 @@ def main():
                 "ps_granularity": gran_eff if mode == "ps_async" else None,
                 "stale_lookahead": kw.get("stale_lookahead") if mode == "ps_async" else None,
                 "bucket_mb": a.bucket_mb,
+                "mailbox": ({"ring_mb_per_worker": round(ti.get("ring_bytes", 0) / 2**20, 1),
+                             "message_slots": ti.get("mailbox_slots"), "direct_push": ti.get("direct_push")}
+                            if mode == "ps_async" else None),
                 "python_gc": a.gc,
                 "num_params": nparams,
                 "buckets": nbuckets,

@@ -1751,7 +1751,8 @@ class PSAsyncEngine(Engine):
                 "granularity": self.granularity,
                 "ps_dedicated": self.dedicated, "accumulate": self.M,
                 "npub": self.NPUB,
-                "mailbox_slots": self.SLOTS, "slot_bytes": self.slot_bytes}
+                "mailbox_slots": self.SLOTS, "slot_bytes": self.slot_bytes, "ring_bytes": self.ring_bytes,
+                "direct_push": self._direct_push}
 
     def close(self):
         if getattr(self, "_closed", False):
