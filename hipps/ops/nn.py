@@ -650,12 +650,15 @@ def remove_host_idle_task(fn) -> None:
         pass
 
 
-def bf16_weight(w: torch.Tensor) -> torch.Tensor:
+def bf16_weight(w: torch.Tensor, idle: bool = True) -> torch.Tensor:
     """The bf16 view of fp32 master weight ``w`` in a registered shadow (same shape and strides),
     else a fresh cast.  The shadow is refreshed by the optimizer with one cast kernel per step, so
-    a ResNet-50 forward reads its 53 conv weights without 53 autocast cast launches."""
-    for fn in _HOST_IDLE_TASKS:
-        fn()
+    a ResNet-50 forward reads its 53 conv weights without 53 autocast cast launches.  ``idle``:
+    run the registered host idle tasks first (forward: the host leads the GPU there; a backward
+    caller passes False -- at the start of backward the GPU waits for the host)."""
+    if idle:
+        for fn in _HOST_IDLE_TASKS:
+            fn()
     if w.dtype == torch.bfloat16:
         return w
     p = w.data_ptr()
@@ -705,7 +708,7 @@ class _ShadowLinear(torch.autograd.Function):
             dy2 = dy2.to(torch.bfloat16)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dy2, bf16_weight(w_master)).view(ctx.xshape)
+            dx = torch.mm(dy2, bf16_weight(w_master, idle=False)).view(ctx.xshape)
             if dx.dtype != ctx.xdtype:
                 dx = dx.to(ctx.xdtype)
         if ctx.needs_input_grad[1]:
