@@ -8,10 +8,12 @@
   *-tiny      same code, small widths, for CPU tests.
 
 Attention is ``F.scaled_dot_product_attention`` (the ROCm flash / mem-efficient kernels); the
-projections and MLPs are ``hipps.ops.nn.Linear`` (hipBLASLt GEMMs that read the engine's bf16
-weight shadow and write fp32 weight gradients directly; plain ``nn.Linear`` behaviour without a
-shadow).  These models exercise the PS engine's bucketing/codec/transport at 100 M - 8 B
-parameters; they are not a kernel showcase.
+projections and MLPs are ``hipps.ops.nn.Linear`` (per shape hipBLASLt or the hipps gemm2 cores,
+reading the engine's bf16 weight shadow, fp32 weight gradients written directly, the residual add
+in the output projections' epilogue; plain ``nn.Linear`` behaviour without a shadow).  The loss
+is the fused bf16 cross-entropy (csrc/xent.hip), the norms csrc/ln.hip (LayerNorm / RMSNorm), the
+Llama SwiGLU gate and RoPE csrc/act.hip.  These models exercise the PS engine's bucketing /
+codec / transport at 100 M - 8 B parameters (BASELINE configs 4 and 5).
 """
 from __future__ import annotations
 
