@@ -62,8 +62,8 @@ struct SlotPtrs {
 // ---- reading bytes another GPU wrote into this GPU's memory ---------------------------------
 // The async PS's mailbox slots are plain (coarse-grained) hipMalloc memory that remote workers
 // fill over xGMI; the PS learns of a message from a host-polled doorbell, so no HIP-level
-// synchronisation tells this device's caches that the bytes changed.  A slot is rewritten every
-// SLOTS messages, so this XCD's L2 (and the CU's L1) may still hold the previous message's lines.
+// synchronisation tells this device's caches that the bytes changed.  A worker's mailbox ring is
+// rewritten as it wraps, so this XCD's L2 (and the CU's L1) may still hold an older message's lines.
 // The consumer therefore acquires at SYSTEM scope before its first load of the slot
 // (MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility"; cdna_hip_programming.md
 // Guideline 16 consumer recipe): one wave issues the invalidate (buffer_inv sc0 sc1), waits for it
