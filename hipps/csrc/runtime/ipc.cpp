@@ -48,7 +48,13 @@ class DeviceMailbox {
     hipIpcMemHandle_t mh;
     std::memcpy(&mh, h.data(), sizeof(mh));
     hip_check(hipGetDevice(&device_), "hipGetDevice");
-    hip_check(hipIpcOpenMemHandle(&ptr_, mh, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    hipError_t e;
+    {
+      // without the GIL: a Python-side guard can still run if the driver call never returns
+      py::gil_scoped_release nogil;
+      e = hipIpcOpenMemHandle(&ptr_, mh, hipIpcMemLazyEnablePeerAccess);
+    }
+    hip_check(e, "hipIpcOpenMemHandle");
   }
   ~DeviceMailbox() { close(); }
 

@@ -108,31 +108,35 @@ def ps_memory_budget(numel: int, W: int, slots: int, slot_bytes: int, npub: int,
     return b
 
 
-def _open_mailbox_bounded(C, handle, total: int, rank: int, limit_s: Optional[float] = None):
+def _open_mailbox_bounded(C, handle, total: int, rank: int, device=None, limit_s: Optional[float] = None):
     """hipIpcOpenMemHandle of the PS mailbox, bounded: on the one-GPU rehearsal box (several ranks
-    sharing a device) the call occasionally never returned (profiles/r4/r4u, r4v: 1 of 6 probe
-    launches, any size).  A thread cannot cancel a call stuck in the driver, so past the limit the
-    process reports it and exits with status 3 (the watchdog's abort status) instead of leaving
-    the job hanging until an outer timeout.  HIPPS_IPC_OPEN_TIMEOUT_S sets the limit (default 120)."""
+    sharing a device) the call sometimes never returned (profiles/r4/r4u, r4v, r4ac).  The open
+    runs on a helper thread (on this rank's device; the binding drops the GIL inside the driver
+    call); past the limit this raises, every rank learns of it through the setup agreement, and
+    bench.py rebuilds the same async PS on its p2p transport.  A call stuck in the driver cannot be
+    cancelled: the helper thread is left behind.  HIPPS_IPC_OPEN_TIMEOUT_S sets the limit
+    (default 60)."""
     if limit_s is None:
-        limit_s = float(os.environ.get("HIPPS_IPC_OPEN_TIMEOUT_S", "120"))
-    done = threading.Event()
+        limit_s = float(os.environ.get("HIPPS_IPC_OPEN_TIMEOUT_S", "60"))
+    box: dict = {}
 
-    def _guard():
-        if not done.wait(limit_s):
-            import sys
+    def _open():
+        try:
+            if device is not None:
+                torch.cuda.set_device(device)
+            box["mb"] = C.DeviceMailbox(handle, total)
+        except BaseException as e:  # reported to the caller
+            box["err"] = e
 
-            sys.stderr.write(f"[hipps] rank {rank}: hipIpcOpenMemHandle of the PS mailbox ({total >> 20} MB) did not "
-                             f"return within {limit_s:.0f} s; exiting (status 3)\n")
-            sys.stderr.flush()
-            os._exit(3)
-
-    t = threading.Thread(target=_guard, name="hipps-ipc-open-guard", daemon=True)
+    t = threading.Thread(target=_open, name="hipps-ipc-open", daemon=True)
     t.start()
-    try:
-        return C.DeviceMailbox(handle, total)
-    finally:
-        done.set()
+    t.join(limit_s)
+    if t.is_alive():
+        raise TimeoutError(f"rank {rank}: hipIpcOpenMemHandle of the PS mailbox ({total >> 20} MB) did not return "
+                           f"within {limit_s:.0f} s")
+    if "err" in box:
+        raise box["err"]
+    return box["mb"]
 
 
 def mailbox_geometry(msg_nbytes: Sequence[int], pres_bytes: int, mailbox_slots: int, mailbox_mb: float,
@@ -479,7 +483,7 @@ class PSAsyncEngine(Engine):
                 if self.p2p:
                     self.mem = None
                 elif self.cuda:
-                    self.mailbox = _open_mailbox_bounded(C, handle, total, self.rank)
+                    self.mailbox = _open_mailbox_bounded(C, handle, total, self.rank, store.device)
                 else:
                     self.mailbox = C.HostMailbox(self.mb_name, total, False)
             except Exception as e:  # e.g. hipIpcOpenMemHandle refused across devices
