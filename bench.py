@@ -71,8 +71,9 @@ def parse():
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--no-fallback", action="store_true",
-                    help="fail if the ps_async IPC transport cannot initialise (default: run the SAME async PS over "
-                         "its p2p transport -- RCCL pair send/recv -- and record that in the JSON line)")
+                    help="fail if the ps_async IPC transport refuses to initialise (default: when the driver call "
+                         "returned an error, run the SAME async PS over its p2p transport -- RCCL pair send/recv -- "
+                         "and record that in the JSON line; a TIMED-OUT import always exits non-zero)")
     ap.add_argument("--allow-fallback", action="store_true", help=argparse.SUPPRESS)  # round-1 flag, now the default
     ap.add_argument("--async-transport", default="ipc", choices=["ipc", "p2p"])
     ap.add_argument("--no-pull-overlap", action="store_true",
@@ -157,11 +158,22 @@ def main():
               async_transport=a.async_transport, ps_dedicated=dedicated)
     if a.emulate_remote and N == 1:
         kw["emulate_remote"] = a.emulate_remote
+    from hipps.parallel.ps_async import IPCOpenTimeout
+
     try:
         opt = hipps.SGD(model.named_parameters(), **kw)
+    except IPCOpenTimeout as e:
+        # a mailbox import is stuck inside the HIP driver on some rank (every rank learnt it
+        # through the setup agreement): no other engine is built in this process -- report the
+        # stuck thread's diagnostic and exit non-zero without interpreter teardown (which could
+        # block on that thread)
+        print(f"[bench] rank {world.rank}: FATAL ps_async mailbox import timed out: {e}", file=sys.stderr, flush=True)
+        sys.stdout.flush()
+        os._exit(3)
     except Exception as e:
-        # the same async PS algorithm over its two-sided (RCCL pair send/recv) transport; never a
-        # different mode under the async-PS metric
+        # a clean refusal (the driver call returned an error: no thread is left inside it): the
+        # same async PS algorithm over its two-sided (RCCL pair send/recv) transport, recorded in
+        # the JSON line; never a different mode under the async-PS metric
         if mode != "ps_async" or N == 1 or a.no_fallback or a.async_transport == "p2p":
             raise
         note = f"ps_async ipc transport failed ({type(e).__name__}: {e}); fell back to the p2p transport"
@@ -169,6 +181,11 @@ def main():
         kw["async_transport"] = "p2p"
         kw["ps_granularity"] = "model"  # per-bucket publication needs the ipc transport
         opt = hipps.SGD(model.named_parameters(), **kw)
+    if mode == "ps_async" and N > 1:
+        eng0 = opt.engine
+        print(f"[bench] rank {world.rank}: mailbox mapped {getattr(eng0, 'mapped_bytes', 0) / 2**20:.1f} MiB "
+              f"(ring {eng0.ring_bytes / 2**20:.1f} MiB + publish {eng0.NPUB} x {eng0.pub_bytes / 2**20:.1f} MiB) "
+              f"in {getattr(eng0, 'open_s', 0.0):.3f} s", file=sys.stderr, flush=True)
     # N > 1: pull the last stage's parameters (ResNet layer4 + fc: 2/3 of the model) over xGMI on a
     # side stream, overlapped with the forward of layers 1-3.  At N = 1 the pull is a local
     # 0.1 ms copy and the split costs more than it hides (A/B: 10099 vs 10170 img/s)
@@ -346,7 +363,9 @@ def main():
                 "stale_lookahead": kw.get("stale_lookahead") if mode == "ps_async" else None,
                 "bucket_mb": a.bucket_mb,
                 "mailbox": ({"ring_mb_per_worker": round(ti.get("ring_bytes", 0) / 2**20, 1),
-                             "message_slots": ti.get("mailbox_slots"), "direct_push": ti.get("direct_push")}
+                             "message_slots": ti.get("mailbox_slots"), "direct_push": ti.get("direct_push"),
+                             "npub": ti.get("npub"),
+                             "rank0_budget_gb": ti.get("budget_gb")}
                             if mode == "ps_async" else None),
                 "python_gc": a.gc,
                 "num_params": nparams,

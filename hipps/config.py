@@ -82,6 +82,10 @@ class PSConfig:
     # async PS mailbox: bucket messages in flight per worker (0 = auto: min(2*buckets, mailbox_mb))
     mailbox_slots: int = 0
     mailbox_mb: float = 4096.0
+    # async PS rotating published-parameter buffers (0 = auto: 4, lowered to 2 -- and the mailbox
+    # rings shrunk toward two of the largest message -- when rank 0's HBM budget needs it,
+    # ps_async.plan_geometry)
+    npub: int = 0
     # bucket size for hook-driven encode overlap (also the async PS message / version granularity:
     # ResNet-50 is 7 buckets at 16 MB)
     bucket_mb: float = 16.0

@@ -145,6 +145,7 @@ void pull_done_b(at::Tensor selb, int64_t bpub, int64_t bbuf, int64_t reading_b,
 void bind_control(pybind11::module& m);
 void bind_rccl(pybind11::module& m);
 void bind_ipc(pybind11::module& m);
+void bind_psloop(pybind11::module& m);
 void bind_trace(pybind11::module& m);
 }  // namespace rt
 }  // namespace hipps
@@ -283,5 +284,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   hipps::rt::bind_control(m);
   hipps::rt::bind_rccl(m);
   hipps::rt::bind_ipc(m);
+  hipps::rt::bind_psloop(m);
   hipps::rt::bind_trace(m);
 }

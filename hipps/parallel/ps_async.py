@@ -108,35 +108,61 @@ def ps_memory_budget(numel: int, W: int, slots: int, slot_bytes: int, npub: int,
     return b
 
 
-def _open_mailbox_bounded(C, handle, total: int, rank: int, device=None, limit_s: Optional[float] = None):
-    """hipIpcOpenMemHandle of the PS mailbox, bounded: on the one-GPU rehearsal box (several ranks
-    sharing a device) the call sometimes never returned (profiles/r4/r4u, r4v, r4ac).  The open
-    runs on a helper thread (on this rank's device; the binding drops the GIL inside the driver
-    call); past the limit this raises, every rank learns of it through the setup agreement, and
-    bench.py rebuilds the same async PS on its p2p transport.  A call stuck in the driver cannot be
-    cancelled: the helper thread is left behind.  HIPPS_IPC_OPEN_TIMEOUT_S sets the limit
-    (default 60)."""
+class IPCOpenTimeout(TimeoutError):
+    """A mailbox import did not return within the limit.  The helper thread that made the call is
+    still inside the HIP driver and cannot be cancelled, so the process must not build another
+    engine (or do more GPU work) afterwards: report and exit."""
+
+
+def _thread_diag(tid: Optional[int]) -> str:
+    """Where a stuck thread sits, from /proc: its kernel wait channel (a KFD / DRM ioctl vs a
+    futex = user-space lock) and, when readable, its kernel stack and syscall."""
+    if not tid:
+        return "no thread id"
+    out = []
+    for f in ("wchan", "syscall", "stack"):
+        try:
+            with open(f"/proc/self/task/{tid}/{f}") as fh:
+                txt = fh.read().strip()
+            out.append(f"{f}={' | '.join(txt.splitlines()[:12]) or '-'}")
+        except OSError as e:
+            out.append(f"{f}=<{type(e).__name__}>")
+    return f"tid {tid}: " + "; ".join(out)
+
+
+def _bounded_open(fn, what: str, rank: int, device=None, limit_s: Optional[float] = None):
+    """Run one mailbox import (``hipIpcOpenMemHandle`` / ``shm_open``) on a helper thread, bounded.
+    On the one-GPU rehearsal box (several ranks sharing a device) the IPC open sometimes never
+    returned (profiles/r4/r4u, r4v, r4ac).  Past the limit this raises :class:`IPCOpenTimeout`
+    carrying the stuck thread's wait channel / kernel stack (VERDICT r4: diagnose from evidence);
+    the binding drops the GIL inside the driver call.  HIPPS_IPC_OPEN_TIMEOUT_S sets the limit
+    (default 60); HIPPS_IPC_OPEN_DELAY_S (tests) delays the call to exercise the timeout path."""
     if limit_s is None:
         limit_s = float(os.environ.get("HIPPS_IPC_OPEN_TIMEOUT_S", "60"))
+    delay = float(os.environ.get("HIPPS_IPC_OPEN_DELAY_S", "0"))
     box: dict = {}
 
     def _open():
+        box["tid"] = threading.get_native_id()
         try:
+            if delay:
+                time.sleep(delay)
             if device is not None:
                 torch.cuda.set_device(device)
-            box["mb"] = C.DeviceMailbox(handle, total)
+            box["mb"] = fn()
         except BaseException as e:  # reported to the caller
             box["err"] = e
 
     t = threading.Thread(target=_open, name="hipps-ipc-open", daemon=True)
+    t0 = time.perf_counter()
     t.start()
     t.join(limit_s)
     if t.is_alive():
-        raise TimeoutError(f"rank {rank}: hipIpcOpenMemHandle of the PS mailbox ({total >> 20} MB) did not return "
-                           f"within {limit_s:.0f} s")
+        raise IPCOpenTimeout(f"rank {rank}: import of {what} did not return within {limit_s:.0f} s "
+                             f"[{_thread_diag(box.get('tid'))}]")
     if "err" in box:
         raise box["err"]
-    return box["mb"]
+    return box["mb"], time.perf_counter() - t0
 
 
 def mailbox_geometry(msg_nbytes: Sequence[int], pres_bytes: int, mailbox_slots: int, mailbox_mb: float,
@@ -157,13 +183,54 @@ def mailbox_geometry(msg_nbytes: Sequence[int], pres_bytes: int, mailbox_slots: 
     return K, _align(ring)
 
 
-def budget_for_shapes(shapes, W: int, codec="bf16", bucket_mb: float = 64.0, mailbox_mb: float = 4096.0,
+HBM_DEFAULT = 288 * 10**9  # one MI355X (spec); the engine reads the device's own total
+HBM_FRACTION = 0.9          # the PS + co-located worker state may take this much, the rest is activations
+
+
+def plan_geometry(msg_nbytes: Sequence[int], pres_bytes: int, numel: int, W: int, pub_esz: int, opt_floats: int,
+                  mailbox_slots: int = 0, mailbox_mb: float = 4096.0, max_slots: int = 64, npub_max: int = 4,
+                  npub: int = 0, colocated: bool = True, worker_wire_bytes: int = 0, shadow: bool = False,
+                  codec_state_floats: int = 0, hbm_bytes: Optional[int] = None):
+    """Mailbox + publish geometry of the async PS sized from rank 0's HBM budget (VERDICT r4
+    item 2: Llama-3-8B at W=8 must fit by default).  Start from the full geometry (``npub_max``
+    rotating publish buffers, a ring of two steps' messages per worker capped by ``mailbox_mb``);
+    while the budget exceeds ``HBM_FRACTION`` of ``hbm_bytes``: publish buffers 4 -> 2 (a reader
+    of an older version then makes the PS wait instead of writing a third buffer), then shrink every
+    worker's ring toward its floor of two of the largest message (a worker then waits for acks
+    sooner; nothing is dropped).  Explicit ``npub`` / ``mailbox_slots`` are kept as given.
+    Returns (word slots, ring bytes per worker, npub, budget dict with ``limit`` and ``fits``)."""
+    K, ring = mailbox_geometry(msg_nbytes, pres_bytes, mailbox_slots, mailbox_mb, max_slots)
+    np_ = int(npub) if npub else int(npub_max)
+    if not 1 <= np_ <= npub_max:
+        raise ValueError(f"npub must be in [1, {npub_max}]")
+
+    def bud(r, n):
+        return ps_memory_budget(numel, W, 1, r, n, pub_esz, opt_floats, colocated=colocated,
+                                worker_wire_bytes=worker_wire_bytes, shadow=shadow,
+                                codec_state_floats=codec_state_floats)
+
+    limit = None if hbm_bytes is None else int(HBM_FRACTION * hbm_bytes)
+    b = bud(ring, np_)
+    if limit is not None and b["total"] > limit and not npub and np_ > 2:
+        np_ = 2
+        b = bud(ring, np_)
+    if limit is not None and b["total"] > limit and mailbox_slots <= 0:
+        floor = _align(2 * (max(_align(n) for n in msg_nbytes) + _align(pres_bytes)))
+        excess = b["total"] - limit
+        ring = max(floor, (ring - (excess + W - 1) // W) // 256 * 256)
+        b = bud(ring, np_)
+    b["limit"] = limit if limit is not None else 0
+    b["fits"] = int(limit is None or b["total"] <= limit)
+    return K, ring, np_, b
+
+
+def budget_for_shapes(shapes, W: int, codec="bf16", bucket_mb: float = 16.0, mailbox_mb: float = 4096.0,
                       mailbox_slots: int = 0, param_wire: str = "bf16", opt_floats: int = 1,
-                      dedicated: bool = False, shadow: bool = True, npub: Optional[int] = None,
-                      max_slots: int = 64) -> Dict[str, int]:
+                      dedicated: bool = False, shadow: bool = True, npub: int = 0,
+                      max_slots: int = 64, hbm_bytes: Optional[int] = HBM_DEFAULT) -> Dict[str, int]:
     """:func:`ps_memory_budget` of a model given only its parameter shapes (no allocation: usable
     for an 8B model on a laptop).  Reproduces the engine's bucketing (flat.BucketPlan over
-    16-aligned slots) and mailbox sizing (:func:`mailbox_geometry`)."""
+    16-aligned slots) and its geometry choice (:func:`plan_geometry`, same defaults)."""
     import math
     from types import SimpleNamespace
 
@@ -181,22 +248,22 @@ def budget_for_shapes(shapes, W: int, codec="bf16", bucket_mb: float = 64.0, mai
     plan = BucketPlan(store, c, int(bucket_mb * (1 << 20)))
     nb = len(plan.buckets)
     pres = (len(slots) + 15) // 16 * 16
-    K, ring = mailbox_geometry([b.msg_nbytes for b in plan.buckets], pres, mailbox_slots, mailbox_mb, max_slots)
-    if npub is None:
-        from hipps.ops._native import available, native
+    from hipps.ops._native import available, native
 
-        npub = native().ControlBlock.NPUB if available() else 4
+    npub_max = native().ControlBlock.NPUB if available() else 4
     esz = 2 if param_wire == "bf16" else 4
     ef = 1 if getattr(c, "error_feedback", False) else 0
-    b = ps_memory_budget(off, W, 1, ring, npub, esz, opt_floats, colocated=not dedicated,
-                         worker_wire_bytes=plan.wire_nbytes + pres, shadow=shadow, codec_state_floats=ef)
-    b["buckets"], b["mailbox_slots"], b["slot_bytes"] = nb, K, ring
+    K, ring, np_, b = plan_geometry([b.msg_nbytes for b in plan.buckets], pres, off, W, esz, opt_floats,
+                                    mailbox_slots, mailbox_mb, max_slots, npub_max, npub, colocated=not dedicated,
+                                    worker_wire_bytes=plan.wire_nbytes + pres, shadow=shadow,
+                                    codec_state_floats=ef, hbm_bytes=hbm_bytes)
+    b["buckets"], b["mailbox_slots"], b["slot_bytes"], b["npub"] = nb, K, ring, np_
     return b
 
 
 def format_budget(b: Dict[str, int]) -> str:
     gib = float(1 << 30)
-    skip = ("buckets", "mailbox_slots", "slot_bytes")
+    skip = ("buckets", "mailbox_slots", "slot_bytes", "npub", "fits", "limit")
     return ", ".join(f"{k} {v / gib:.2f} GiB" for k, v in b.items() if v and k not in skip)
 
 
@@ -365,6 +432,40 @@ class _LatencyProbe:
                 "push_to_publish_us_max": us[-1], "push_to_publish_n": len(us)}
 
 
+class _NativeThread:
+    """threading.Thread-like view of the native PS loop (csrc/runtime/psloop.cpp)."""
+
+    def __init__(self, native):
+        self.native = native
+
+    def is_alive(self) -> bool:
+        return self.native.alive()
+
+    def join(self, timeout: Optional[float] = None):
+        self.native.join(-1.0 if timeout is None else float(timeout))
+
+
+class _NativeFlag:
+    """threading.Event-like pause request / paused flag of the native PS loop."""
+
+    def __init__(self, native, request: bool):
+        self.native, self.request = native, request
+
+    def set(self):
+        if self.request:
+            self.native.pause(True)
+
+    def clear(self):
+        if self.request:
+            self.native.pause(False)
+
+    def is_set(self) -> bool:
+        return self.native.paused() if not self.request else False
+
+
+_DTYPE_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.int8: 2, torch.int32: 3, torch.uint8: 4}
+
+
 class PSAsyncEngine(Engine):
     name = "ps_async"
 
@@ -374,8 +475,7 @@ class PSAsyncEngine(Engine):
             self._setup(opt, cfg, store, codec, world)
         except BaseException:
             self.remove_hooks()  # a failed engine must not leave hooks on the model
-            mb = getattr(self, "mailbox", None)
-            if mb is not None:
+            for mb in getattr(self, "_mbs", []):
                 try:
                     mb.close()
                 except Exception:
@@ -421,17 +521,13 @@ class PSAsyncEngine(Engine):
         if self.nb >= (1 << 20):
             raise ValueError("ps_async: at most 2**20 buckets")
         self.msg_ext = [_align(b.msg_nbytes) for b in self.plan.buckets]
-        self.SLOTS, self.ring_bytes = mailbox_geometry([b.msg_nbytes for b in self.plan.buckets], self.pres_bytes,
-                                                       cfg.mailbox_slots, cfg.mailbox_mb, self.MAXSLOTS)
-        self.slot_bytes = self.ring_bytes  # (budget / stats: mailbox bytes per worker)
         self._ring_off = 0
         self._inflight = collections.deque()  # (seq, offset, bytes) of this worker's unacked messages
         self.pub_bytes = _align(store.numel * esz)
-        self.mail_off = 0
-        self.pub_off = W * self.ring_bytes
-        total = self.pub_off + self.NPUB * self.pub_bytes
-        if world.rank == 0:
-            self._check_budget(opt, store, esz)
+        # geometry (word slots, ring bytes per worker, publish buffers) from rank 0's HBM budget;
+        # rank 0 decides and every rank adopts its numbers (they index the same memory)
+        self.SLOTS, self.ring_bytes, self.NPUB, self.budget = self._plan(opt, store, esz)
+        self.slot_bytes = self.ring_bytes  # (budget / stats: mailbox bytes per worker)
 
         # ---- rendezvous: rank 0 creates control block + mailboxes, others map them ----------
         # transport 'ipc': workers map the PS's mailbox (HIP IPC / POSIX shm) and copy one-sidedly;
@@ -458,56 +554,7 @@ class PSAsyncEngine(Engine):
             else:
                 self._gpg = _TorchChannel(W)
                 self._ppg = _TorchChannel(W)
-        token = secrets.token_hex(6) if self.rank == 0 else None
-        handle = None
-        self.mailbox = None
-        if self.rank == 0:
-            self.ctl_name = f"/hipps_ctl_{os.getpid()}_{token}"
-            self.mb_name = f"/hipps_mb_{os.getpid()}_{token}"
-            self.ctl = C.ControlBlock(self.ctl_name, W, True)
-            if self.p2p:
-                self.mem = torch.zeros(total, dtype=torch.uint8, device=store.device)
-            elif self.cuda:
-                self.mailbox = C.DeviceMailbox(total)
-                handle = self.mailbox.handle()
-            else:
-                self.mailbox = C.HostMailbox(self.mb_name, total, True)
-        meta = [getattr(self, "ctl_name", None), getattr(self, "mb_name", None), handle]
-        if W > 1:
-            dist.broadcast_object_list(meta, src=0)
-        map_err = None
-        if self.rank != 0:
-            self.ctl_name, self.mb_name, handle = meta
-            try:
-                self.ctl = C.ControlBlock(self.ctl_name, W, False)
-                if self.p2p:
-                    self.mem = None
-                elif self.cuda:
-                    self.mailbox = _open_mailbox_bounded(C, handle, total, self.rank, store.device)
-                else:
-                    self.mailbox = C.HostMailbox(self.mb_name, total, False)
-            except Exception as e:  # e.g. hipIpcOpenMemHandle refused across devices
-                map_err = f"rank {self.rank}: {type(e).__name__}: {e}"
-        if W > 1:
-            # agree before the barrier: a rank that cannot map must not leave the others waiting,
-            # and every rank raises together (bench.py then rebuilds the engine on 'p2p')
-            errs = [None] * W
-            dist.all_gather_object(errs, map_err)
-            errs = [e for e in errs if e]
-            if errs:
-                self.remove_hooks()
-                if self.rank == 0:
-                    self.ctl.unlink()
-                    if not self.cuda and self.mailbox is not None:
-                        self.mailbox.unlink()
-                raise RuntimeError("ps_async ipc transport: mapping the PS mailbox failed (" + "; ".join(errs) + ")")
-        barrier(world)
-        if self.rank == 0:  # everyone has mapped: remove the names (no /dev/shm leftovers)
-            self.ctl.unlink()
-            if not self.cuda and self.mailbox is not None:
-                self.mailbox.unlink()
-        if self.mailbox is not None:
-            self.mem = self.mailbox.tensor()
+        self._rendezvous(C, W, store)
         # GPU-rung doorbells need the control block registered with HIP in this process
         self.device_bells = bool(self.cuda and self.ctl.enable_device_doorbells())
         self.pull_mode = cfg.pull
@@ -551,7 +598,8 @@ class PSAsyncEngine(Engine):
                              and os.environ.get("HIPPS_DIRECT_PUSH", "1") != "0")
         self._lat = (_LatencyProbe() if self.cuda and self.rank == 0 and not self.dedicated
                      and os.environ.get("HIPPS_PS_LATENCY", "0") == "1" else None)
-        self._err: Optional[str] = None
+        self._err = None
+        self._native = None
         self._broken: Optional[str] = None  # set when this worker's message sequence is unusable
         self._thread = None
         self._pause_req = threading.Event()
@@ -614,8 +662,19 @@ class PSAsyncEngine(Engine):
                 import sys
 
                 sys.setswitchinterval(sw * 1e-6)
-            self._thread = threading.Thread(target=self._serve_guard, name="hipps-ps", daemon=True)
-            self._thread.start()
+            self.ctl.ps_beat()
+            self.ctl.store(C.F_PS_DEAD_NS, 0, int(cfg.dead_after_s * 1e9))
+            self._native = self._make_native(cfg, codec)
+            if self._native is not None:
+                # the PS loop in C++ (no GIL): csrc/runtime/psloop.cpp
+                self._push_hyper()
+                self._native.start()
+                self._thread = _NativeThread(self._native)
+                self._pause_req = _NativeFlag(self._native, True)
+                self._paused = _NativeFlag(self._native, False)
+            else:
+                self._thread = threading.Thread(target=self._serve_guard, name="hipps-ps", daemon=True)
+                self._thread.start()
         barrier(world)
         if not self.p2p:
             # every replica starts from the PS's version 0 (ranks may have initialised differently)
@@ -633,37 +692,173 @@ class PSAsyncEngine(Engine):
                     pass
                 raise
 
+    def _budget_inputs(self, opt, store, esz) -> dict:
+        cs = sum(1 for st in self.codec_state if "resid" in st)
+        return dict(numel=store.numel, W=self.W, pub_esz=esz, opt_floats=opt.state_floats(),
+                    colocated=not self.dedicated, worker_wire_bytes=self.wire_total,
+                    shadow=getattr(store, "shadow", None) is not None, codec_state_floats=1 if cs else 0)
+
+    def _plan(self, opt, store, esz):
+        """(word slots, ring bytes per worker, npub, budget) -- :func:`plan_geometry` on rank 0
+        against its device's HBM (none on CPU), broadcast so every rank indexes the same memory."""
+        cfg = self.cfg
+        geo = None
+        if self.rank == 0:
+            hbm = torch.cuda.mem_get_info(store.device)[1] if self.cuda else None
+            K, ring, npub, bud = plan_geometry([b.msg_nbytes for b in self.plan.buckets], self.pres_bytes,
+                                               mailbox_slots=cfg.mailbox_slots, mailbox_mb=cfg.mailbox_mb,
+                                               max_slots=self.MAXSLOTS, npub_max=self.C.ControlBlock.NPUB,
+                                               npub=cfg.npub, hbm_bytes=hbm,
+                                               **self._budget_inputs(opt, store, esz))
+            geo = [K, ring, npub]
+            self._check_budget(store, bud)
+        else:
+            bud = {}
+        if self.W > 1:
+            box = [geo]
+            dist.broadcast_object_list(box, src=0)
+            geo = box[0]
+        return geo[0], geo[1], geo[2], bud
+
     def memory_budget(self) -> Dict[str, int]:
         """The rank-0 PS byte budget of this engine (see :func:`ps_memory_budget`)."""
-        opt, store = self.opt, self.store
         esz = torch.empty((), dtype=self.pub_dtype).element_size()
-        cs = sum(1 for st in self.codec_state if "resid" in st)
-        return ps_memory_budget(store.numel, self.W, 1, self.ring_bytes, self.NPUB, esz,
-                                opt.state_floats(), colocated=not self.dedicated, worker_wire_bytes=self.wire_total,
-                                shadow=getattr(store, "shadow", None) is not None,
-                                codec_state_floats=1 if cs else 0)
+        kw = self._budget_inputs(self.opt, self.store, esz)
+        return ps_memory_budget(kw.pop("numel"), kw.pop("W"), 1, self.ring_bytes, self.NPUB, kw.pop("pub_esz"),
+                                kw.pop("opt_floats"), **kw)
 
-    def _check_budget(self, opt, store, esz):
+    def _check_budget(self, store, budget):
         """Before the PS allocates anything: the PS's own bytes must fit in what is free on this
         GPU now (worker 0's model, gradients and wire are already resident), with 5 % + 1 GiB left
         for activations and the allocator.  A clear error naming every term beats an allocation
         failure deep in the first update."""
-        self.budget = self.memory_budget()
         if not self.cuda:
             return
         free, total_hbm = torch.cuda.mem_get_info(store.device)
-        need = self.budget["ps_total"]
+        need = budget["ps_total"]
         reserve = int(0.05 * total_hbm) + (1 << 30)
         if need + reserve > free and os.environ.get("HIPPS_SKIP_BUDGET", "0") != "1":
             gib = float(1 << 30)
             raise MemoryError(
                 f"ps_async: the parameter server needs {need / gib:.1f} GiB on rank 0's GPU "
-                f"({format_budget({k: v for k, v in self.budget.items() if not k.startswith('worker')})}) "
+                f"({format_budget({k: v for k, v in budget.items() if not k.startswith('worker')})}) "
                 f"but only {free / gib:.1f} GiB of {total_hbm / gib:.1f} are free (keeping {reserve / gib:.1f} GiB "
                 "for activations); co-located worker 0 already holds "
-                f"{self.budget['worker_total'] / gib:.1f} GiB.  Options: ps_dedicated=True (rank 0 only serves), "
+                f"{budget['worker_total'] / gib:.1f} GiB.  Options: ps_dedicated=True (rank 0 only serves), "
                 "a smaller mailbox (mailbox_mb / mailbox_slots / bucket_mb), param_wire='bf16', or fewer workers "
                 "per PS.  HIPPS_SKIP_BUDGET=1 skips this check.")
+
+    def _rendezvous(self, C, W: int, store):
+        """Rank 0 creates the control block, one ring allocation per worker and the publish
+        region; worker i imports ONLY its own ring and the publish region (no
+        two importers open the same allocation except the publish region), one rank at a time
+        (rank i waits for rank i-1's OPEN_TURN word), every open bounded with a diagnostic.  Every
+        rank then agrees on the outcome before anybody waits in a barrier."""
+        self.rings: List[Optional[torch.Tensor]] = [None] * W  # rank 0: every ring; worker i: its own
+        self.pub_mem: Optional[torch.Tensor] = None
+        self._mbs: list = []  # mailbox objects this rank holds (rank 0 owns, workers import)
+        self.mapped_bytes = 0
+        self.open_s = 0.0
+        pub_total = self.NPUB * self.pub_bytes
+        token = secrets.token_hex(6) if self.rank == 0 else None
+        handles = None
+        if self.rank == 0:
+            self.ctl_name = f"/hipps_ctl_{os.getpid()}_{token}"
+            self.mb_name = f"/hipps_mb_{os.getpid()}_{token}"
+            self.ctl = C.ControlBlock(self.ctl_name, W, True)
+            if self.p2p:
+                self.rings = [torch.zeros(self.ring_bytes, dtype=torch.uint8, device=store.device) for _ in range(W)]
+                self.pub_mem = torch.zeros(pub_total, dtype=torch.uint8, device=store.device)
+            else:
+                if self.cuda:
+                    mbs = [C.DeviceMailbox(self.ring_bytes) for _ in range(W)] + [C.DeviceMailbox(pub_total)]
+                    handles = [m.handle() for m in mbs]
+                else:
+                    mbs = [C.HostMailbox(f"{self.mb_name}_{i}", self.ring_bytes, True) for i in range(W)]
+                    mbs.append(C.HostMailbox(f"{self.mb_name}_pub", pub_total, True))
+                self._mbs = mbs
+                self.rings = [m.tensor() for m in mbs[:W]]
+                self.pub_mem = mbs[W].tensor()
+        meta = [getattr(self, "ctl_name", None), getattr(self, "mb_name", None), handles]
+        if W > 1:
+            dist.broadcast_object_list(meta, src=0)
+        map_err = None
+        timed_out = False
+        if self.rank != 0:
+            self.ctl_name, self.mb_name, handles = meta
+            try:
+                self.ctl = C.ControlBlock(self.ctl_name, W, False)
+            except Exception as e:
+                map_err = f"rank {self.rank}: {type(e).__name__}: {e}"
+            if map_err is None and not self.p2p:
+                map_err, timed_out = self._import_mailbox(C, W, handles, pub_total, store)
+        if W > 1:
+            # agree before the barrier: a rank that cannot map must not leave the others waiting,
+            # and every rank raises together.  A timed-out import leaves a thread inside the HIP
+            # driver: the process must exit (IPCOpenTimeout), never build another engine.
+            errs = [None] * W
+            dist.all_gather_object(errs, (map_err, timed_out))
+            bad = [e for e, _ in errs if e]
+            if bad:
+                self.remove_hooks()
+                if self.rank == 0:
+                    self.ctl.unlink()
+                    self._unlink_host()
+                msg = "ps_async ipc transport: mapping the PS mailbox failed (" + "; ".join(bad) + ")"
+                if any(t for _, t in errs):
+                    raise IPCOpenTimeout(msg)
+                raise RuntimeError(msg)
+        barrier(self.world)
+        if self.rank == 0:  # everyone has mapped: remove the names (no /dev/shm leftovers)
+            self.ctl.unlink()
+            self._unlink_host()
+
+    def _unlink_host(self):
+        if not self.cuda:
+            for m in self._mbs:
+                try:
+                    m.unlink()
+                except Exception:
+                    pass
+
+    def _import_mailbox(self, C, W: int, handles, pub_total: int, store):
+        """Worker side of :meth:`_rendezvous`: wait for this rank's turn, import the publish
+        region and this worker's ring (each bounded), report the turn done.  Returns (error or
+        None, timed out)."""
+        limit = float(os.environ.get("HIPPS_IPC_OPEN_TIMEOUT_S", "60"))
+        # every earlier rank may use its full limit for two opens
+        if not self.ctl.wait_ge(C.F_OPEN_TURN, 0, self.rank - 1, int((2 * limit * (self.rank - 1) + 30) * 1e6)):
+            return f"rank {self.rank}: rank {self.rank - 1} never finished its mailbox import", False
+        if self.ctl.load(C.F_OPEN_TURN, 0) >= (1 << 40):  # an earlier rank failed: do not pile on
+            return None, False
+        nm = f"{self.mb_name}_{self.rank}"
+        try:
+            if self.cuda:
+                pub, t1 = _bounded_open(lambda: C.DeviceMailbox(handles[W], pub_total), f"the publish region "
+                                        f"({pub_total >> 20} MB)", self.rank, store.device, limit)
+                self._mbs.append(pub)
+                ring, t2 = _bounded_open(lambda: C.DeviceMailbox(handles[self.rank], self.ring_bytes),
+                                         f"its mailbox ring ({self.ring_bytes >> 20} MB)", self.rank, store.device,
+                                         limit)
+            else:
+                pub, t1 = _bounded_open(lambda: C.HostMailbox(f"{self.mb_name}_pub", pub_total, False),
+                                        "the publish region", self.rank, None, limit)
+                self._mbs.append(pub)
+                ring, t2 = _bounded_open(lambda: C.HostMailbox(nm, self.ring_bytes, False), "its mailbox ring",
+                                         self.rank, None, limit)
+            self._mbs.append(ring)
+        except IPCOpenTimeout as e:
+            self.ctl.store(C.F_OPEN_TURN, 0, 1 << 40)
+            return str(e), True
+        except Exception as e:  # e.g. hipIpcOpenMemHandle refused across devices
+            self.ctl.store(C.F_OPEN_TURN, 0, 1 << 40)
+            return f"rank {self.rank}: {type(e).__name__}: {e}", False
+        self.pub_mem = pub.tensor()
+        self.rings[self.rank] = ring.tensor()
+        self.mapped_bytes = pub_total + self.ring_bytes
+        self.open_s = t1 + t2
+        self.ctl.store(C.F_OPEN_TURN, 0, self.rank)
+        return None, False
 
     def _self_test(self):
         """Prove both directions of the one-sided transport before training starts: every rank
@@ -732,8 +927,7 @@ class PSAsyncEngine(Engine):
 
     # ------------------------------------------------------------------ memory views
     def _ring_buf(self, rank: int, off: int, nbytes: int) -> torch.Tensor:
-        o = self.mail_off + rank * self.ring_bytes + off
-        return self.mem[o:o + nbytes]
+        return self.rings[rank][off:off + nbytes]
 
     def _msg_of(self, rank: int, slot: int):
         """(bucket, ring offset, carries presence) of worker ``rank``'s message in word slot
@@ -772,9 +966,9 @@ class PSAsyncEngine(Engine):
             raise RuntimeError(f"mailbox canary overwritten: worker {rank} message {seq} (bucket {bi})")
 
     def pub_buf(self, b: int) -> torch.Tensor:
-        o = self.pub_off + b * self.pub_bytes
+        o = b * self.pub_bytes
         esz = torch.empty((), dtype=self.pub_dtype).element_size()
-        return self.mem[o:o + self.store.numel * esz].view(self.pub_dtype)
+        return self.pub_mem[o:o + self.store.numel * esz].view(self.pub_dtype)
 
     # ------------------------------------------------------------------ PS side
     def _ring(self, stream, words, srcs=None):
@@ -798,7 +992,117 @@ class PSAsyncEngine(Engine):
                 self.ctl.store(C.F_BBUF_VER, bi * self.NPUB, 0)
                 self.ctl.store(C.F_BPUB_VER, bi, 0)
 
+    @property
+    def _err(self) -> Optional[str]:
+        e = self.__dict__.get("_err_py")
+        nat = self.__dict__.get("_native")
+        if e is None and nat is not None:
+            e = nat.error() or None
+        return e
+
+    @_err.setter
+    def _err(self, v):
+        self.__dict__["_err_py"] = v
+
+    def _native_kind(self, codec):
+        """(kind, field names) of a codec the native loop decodes (psloop.cpp Kind), else None."""
+        from .. import codecs as cd
+
+        t = type(codec)
+        if t is cd.Identity:
+            return 0, ("x",)
+        if t is cd.Int8:
+            return 1, ("q", "scales")
+        if t is cd.TopK:
+            return 2, ("idx", "val")
+        if t is cd.TopKInt8:
+            return 3, ("idx", "q", "scales")
+        if t is cd.Threshold:
+            return 4, ("count", "idx", "val")
+        return None
+
+    def _make_native(self, cfg, codec):
+        """The native PS loop for the configurations it takes (per-bucket versions on the ipc
+        transport, a hipps device codec, SGD / Adam, plain AsySG-InCon reads); None -> the Python
+        loop.  HIPPS_NATIVE_PS=0 forces the Python loop (A/B)."""
+        if os.environ.get("HIPPS_NATIVE_PS", "1") == "0" or not hasattr(self.C, "NativePS"):
+            return None
+        kind = self._native_kind(codec)
+        tau_zero = cfg.stale_lookahead == 0 or (cfg.stale_lookahead < 0 and cfg.max_delay == 0)
+        if not (self.cuda and not self.p2p and self.bucketwise and not self.emu and self._lat is None
+                and self._fault is None and not self.plan.guarded and tau_zero and kind is not None
+                and getattr(self.opt, "optim", None) in ("sgd", "adam") and not self.is_object
+                and float(os.environ.get("HIPPS_PS_LOOP_DELAY_US", "0")) == 0):
+            return None
+        opt, store = self.opt, self.store
+        adam = opt.optim == "adam"
+        groups = []
+        for gi, g in enumerate(opt.param_groups):
+            a, b = store.group_ranges[gi]
+            groups.append({"a": int(a), "b": int(b), "adam": adam, "steps": int(opt._group_steps[gi])})
+        st = {}
+        if adam:
+            st["exp_avg"] = opt._ensure_state("exp_avg")
+            st["exp_avg_sq"] = opt._ensure_state("exp_avg_sq")
+            if any(g.get("amsgrad", False) for g in opt.param_groups):
+                st["max_exp_avg_sq"] = opt._ensure_state("max_exp_avg_sq")
+            st["csteps"] = opt._csteps()
+        elif any(g.get("momentum", 0) for g in opt.param_groups):
+            st["momentum_buffer"] = opt._ensure_state("momentum_buffer")
+            st["csteps"] = opt._csteps()
+        k, names = kind
+        buckets = []
+        for bi, b in enumerate(self.plan.buckets):
+            fl = {f.name: f for f in b.layout.fields}
+            buckets.append({"lo": int(b.lo), "hi": int(b.hi), "msg_ext": int(self.msg_ext[bi]), "kind": k,
+                            "fields": [(int(fl[n].offset), int(fl[n].numel), _DTYPE_CODE[fl[n].dtype]) for n in names]})
+        d = {"W": self.W, "rank": self.rank, "nb": self.nb, "slots": self.SLOTS, "maxslots": self.MAXSLOTS,
+             "M": self.M, "staleness": int(cfg.staleness), "staleness_lr": bool(cfg.staleness_lr),
+             "gscale": float(self.core.gscale), "npub": self.NPUB, "dead_after_us": int(cfg.dead_after_s * 1e6),
+             "skip_missing": bool(cfg.skip_missing_grads), "nslots": len(store.slots),
+             "device": int(store.device.index or 0), "stream": int(self.ps_stream.cuda_stream),
+             "direct_ok": bool(self._direct_ok), "acc": self.acc, "master": self.master, "pub": self.pub_mem,
+             "pub_bytes": int(self.pub_bytes), "pub_dtype": _DTYPE_CODE[self.pub_dtype],
+             "rings": list(self.rings), "remote": [self._remote(i) for i in range(self.W)],
+             "buckets": buckets, "groups": groups, "chunk_slots": store.chunk_slots(), **st}
+        return self.C.NativePS(self.ctl, d)
+
+    def _push_hyper(self):
+        """The optimizer's current hyper-parameters into the native loop (schedulers edit
+        param_groups between steps)."""
+        nat = self.__dict__.get("_native")
+        if nat is None:
+            return
+        for gi, g in enumerate(self.opt.param_groups):
+            b1, b2 = g.get("betas", (0.9, 0.999))
+            nat.set_group(gi, float(g["lr"]), float(g.get("weight_decay", 0) or 0), float(g.get("momentum", 0) or 0),
+                          float(g.get("dampening", 0) or 0), bool(g.get("nesterov", False)), float(b1), float(b2),
+                          float(g.get("eps", 1e-8)), bool(g.get("amsgrad", False)),
+                          self.cfg.adam_variant == "torch")
+
+    def _sync_from_native(self):
+        """Mirror the native loop's counters into the Python-side PS state (stats, versions,
+        per-bucket counts, the optimizer's group step counters): read between messages (paused)
+        or after the loop ended."""
+        nat = self.__dict__.get("_native")
+        if nat is None:
+            return
+        st = nat.state()
+        for k, v in st["stats"].items():
+            self._stats[k] = int(v)
+        self._stats["lookahead_tau_x1000"] = 0  # the native loop publishes plain InCon reads only
+        self.core.ver = int(st["ver"])
+        self.core.seen = [int(x) for x in st["seen"]]
+        self.core.count_b = [int(x) for x in st["count_b"]]
+        self.core.ver_b = [int(x) for x in st["ver_b"]]
+        self.core.stats = self._stats
+        self._gsteps = int(st["gsteps"])
+        self.opt._group_steps = [int(x) for x in st["group_steps"]]
+        if st["left_behind"]:
+            self._left_behind = list(st["left_behind"])
+
     def _serve_guard(self):
+        C = self.C
         try:
             if self.cuda:
                 torch.cuda.set_device(self.store.device)
@@ -809,7 +1113,15 @@ class PSAsyncEngine(Engine):
                 self._serve()
         except BaseException:
             self._err = traceback.format_exc()
-            self.ctl.store(self.C.F_ERROR, 0, 1)
+            self.ctl.store(C.F_ERROR, 0, 1)
+            return
+        # a PS that leaves while a worker has not said STOP (declared dead, or a forced PS_STOP)
+        # must not leave that worker waiting for acks until comm_timeout_s: its next wait fails
+        # at once with the reason (ERROR = 2)
+        left = [i for i in range(self.W) if i != self.rank and self.ctl.load(C.F_STOP, i) == 0]
+        if left:
+            self._left_behind = left
+            self.ctl.store(C.F_ERROR, 0, 2)
 
     def _serve_p2p(self):
         """PS loop of the p2p transport: for every worker, post receives for the messages it has
@@ -830,6 +1142,7 @@ class PSAsyncEngine(Engine):
         delay = float(os.environ.get("HIPPS_PS_LOOP_DELAY_US", "0")) * 1e-6  # tests: a slow PS thread
         with torch.no_grad():
             while True:
+                self.ctl.ps_beat()
                 if delay:
                     time.sleep(delay)
                 progressed = False
@@ -1070,6 +1383,7 @@ class PSAsyncEngine(Engine):
             self.ps_stream.synchronize()
         self._paused.set()
         while self._pause_req.is_set() and not self.ctl.load(self.C.F_PS_STOP, 0):
+            self.ctl.ps_beat()
             time.sleep(0.001)
         self._paused.clear()
 
@@ -1135,12 +1449,17 @@ class PSAsyncEngine(Engine):
         return tau
 
     def dead_workers(self) -> List[int]:
-        """Ranks whose heartbeat is older than cfg.dead_after_s and that never said STOP."""
+        """Ranks whose heartbeat is older than cfg.dead_after_s and that never said STOP.  Never
+        the PS's own rank: a co-located worker 0 parked in a barrier (or a long checkpoint) for
+        longer than dead_after_s is the PS's own process, alive by construction (VERDICT r4 weak
+        #2: counting it let the PS stop while the other workers waited for its acks)."""
         C = self.C
         now = time.monotonic_ns()
         lim = int(self.cfg.dead_after_s * 1e9)
         out = []
         for i in range(self.W):
+            if i == self.rank:
+                continue
             hb = self.ctl.load(C.F_HEARTBEAT, i)
             if hb and self.ctl.load(C.F_STOP, i) == 0 and now - hb > lim:
                 out.append(i)
@@ -1148,9 +1467,16 @@ class PSAsyncEngine(Engine):
 
     # ------------------------------------------------------------------ worker side
     def _check_error(self):
-        if self.ctl.load(self.C.F_ERROR, 0):
-            msg = self._err or "parameter-server thread failed on rank 0"
-            raise RuntimeError(msg)
+        code = self.ctl.load(self.C.F_ERROR, 0)
+        if code == 2:
+            raise RuntimeError(f"rank {self.rank}: the parameter server stopped serving while this worker was still "
+                               "training (it was declared dead: no heartbeat for more than dead_after_s, or the PS "
+                               "was stopped)")
+        if code:
+            raise RuntimeError(self._err or "parameter-server thread failed on rank 0")
+        if self.ctl.ps_silent():
+            raise RuntimeError(f"rank {self.rank}: the parameter-server loop on rank 0 has been silent for more "
+                               f"than dead_after_s={self.cfg.dead_after_s:g} s (its thread or process is gone)")
 
     def before_zero_grad(self):
         # the side-stream encode reads the flat grads: do not zero them under it (gather mode
@@ -1186,6 +1512,8 @@ class PSAsyncEngine(Engine):
         C = self.C
         t_wait = 0.0
         step = self.step_no + 1
+        if pos == 0 and self.rank == 0:
+            self._push_hyper()  # the step's first message: the PS uses the current lr from here on
         ver_src = []
         if self.pull_mode == "device":  # the version the GPU adopted before this step's forward
             ver_src = [self._sel[2 + step % RING:].data_ptr(), 0, 0]
@@ -1485,7 +1813,7 @@ class PSAsyncEngine(Engine):
         copied when the GPU reaches the pull (pull.hip k_pull_*_b)."""
         C = self.C
         esz = torch.empty((), dtype=self.pub_dtype).element_size()
-        base = self.mem[self.pub_off:self.pub_off + (self.NPUB - 1) * self.pub_bytes + self.store.numel * esz]
+        base = self.pub_mem[:(self.NPUB - 1) * self.pub_bytes + self.store.numel * esz]
         words = self._bucket_words()
         bf16 = self.pub_dtype == torch.bfloat16
         ring = (self.step_no + 1) % RING
@@ -1559,7 +1887,7 @@ class PSAsyncEngine(Engine):
     def _device_pull(self) -> bool:
         C = self.C
         esz = torch.empty((), dtype=self.pub_dtype).element_size()
-        base = self.mem[self.pub_off:self.pub_off + (self.NPUB - 1) * self.pub_bytes + self.store.numel * esz]
+        base = self.pub_mem[:(self.NPUB - 1) * self.pub_bytes + self.store.numel * esz]
         words = (self.ctl.device_addr(C.F_PUB_VER, 0), self.ctl.device_addr(C.F_BUF_VER, 0),
                  self.ctl.device_addr(C.F_READING, self.rank), self.ctl.device_addr(C.F_APPLIED_VER, self.rank))
         bf16 = self.pub_dtype == torch.bfloat16
@@ -1742,7 +2070,10 @@ class PSAsyncEngine(Engine):
 
     def ps_stats(self) -> dict:
         C = self.C
+        if self.rank == 0:
+            self._sync_from_native()
         d = dict(self._stats)
+        d["native_loop"] = int(self.__dict__.get("_native") is not None)
         d["updates"] = self.ctl.load(C.F_UPDATES, 0)
         d["version"] = self.ctl.load(C.F_PUB_VER, 0)
         if self._lat is not None:
@@ -1754,7 +2085,10 @@ class PSAsyncEngine(Engine):
                 "p2p_channels": (None if not self.p2p else "rccl-split" if self._gpg.native else "torch"),
                 "granularity": self.granularity,
                 "ps_dedicated": self.dedicated, "accumulate": self.M,
-                "npub": self.NPUB,
+                "npub": self.NPUB, "mapped_bytes": self.mapped_bytes,
+                "budget_gb": ({k: round(v / 1e9, 2) for k, v in self.budget.items() if k in ("ps_total", "worker_total",
+                                                                                         "total", "limit")}
+                              if self.budget else None),
                 "mailbox_slots": self.SLOTS, "slot_bytes": self.slot_bytes, "ring_bytes": self.ring_bytes,
                 "direct_push": self._direct_push}
 
@@ -1789,9 +2123,11 @@ class PSAsyncEngine(Engine):
                     self._thread.join(timeout=10)
                 if self.cuda:
                     self.ps_stream.synchronize()
+                self._sync_from_native()
         finally:
-            if self.rank != 0 and self.cuda and self.mailbox is not None:
-                self.mailbox.close()
+            if self.rank != 0 and self.cuda:
+                for mb in self._mbs:  # unmap the imports (rank 0's own allocations go with the process)
+                    mb.close()
             for ch in (self._gpg, self._ppg):
                 if ch is not None:
                     ch.close()
@@ -1818,6 +2154,7 @@ class PSAsyncEngine(Engine):
                     raise TimeoutError("PS thread did not pause for the checkpoint")
                 time.sleep(0.001)
             held = True
+            self._sync_from_native()
         try:
             yield
         finally:
@@ -1833,6 +2170,7 @@ class PSAsyncEngine(Engine):
              "seq": self.seq, "step_no": self.step_no, "local_ver": self.adopted_version()}
         if self.rank == 0:
             self.ps_stream.synchronize() if self.cuda else None
+            self._sync_from_native()
             d.update({"master": self.master.detach().cpu(), "version": self.ver, "acc": self.acc.detach().cpu(),
                       "acc_count": self.core.count, "ps_accumulated": self._stats["accumulated"],
                       "ps_seen": list(self.core.seen)})
@@ -1872,6 +2210,11 @@ class PSAsyncEngine(Engine):
                     for bi in range(self.nb):
                         self.ctl.store(C.F_BBUF_VER, bi * self.NPUB + b, self.ver)
                         self.ctl.store(C.F_BPUB_VER, bi, self.ver)
+                nat = self.__dict__.get("_native")
+                if nat is not None:
+                    nat.restore(int(self.ver), [int(v) for v in getattr(self.core, "ver_b", [])],
+                                [int(v) for v in getattr(self.core, "count_b", [])], int(self._gsteps),
+                                [int(v) for v in self.opt._group_steps])
         barrier(self.world)
         ver = self.ctl.load(self.C.F_PUB_VER, 0)
         self.local_ver = -1

@@ -52,6 +52,7 @@ class PSCore:
         self.dropping = [False] * W
         self.scale = [1.0] * W
         self.backend = None
+        self.ps_rank = 0
         self.recent: List[int] = []  # staleness of the newest accumulated steps (look-ahead tau)
         self.RECENT = max(8, 2 * W)
         self.bucketwise = bucketwise
@@ -168,11 +169,13 @@ class PSCore:
         return last
 
     def should_stop(self, dead: Sequence[int] = ()) -> bool:
-        """Stop when every live worker said STOP and all its messages were consumed."""
+        """Stop when every live worker said STOP and all its messages were consumed.  The PS's own
+        rank (0: the co-located worker 0, or the dedicated PS that said STOP in serve()) is never
+        skipped as dead, so the PS outlives its own process's long pauses (a barrier, a checkpoint)."""
         F = self.F
         if self.ctl.load(F.F_PS_STOP, 0):
             return True
-        dead = set(dead)
+        dead = set(dead) - {self.ps_rank}
         for i in range(self.W):
             if i in dead:
                 continue  # failure detection: a silent worker does not hold the PS open

@@ -169,9 +169,9 @@ def test_async_checkpoint_quiesce_while_workers_push(tmp_path, monkeypatch):
 
 def test_async_checkpoint_quiesce_bucket_versions(tmp_path, monkeypatch):
     """The same under per-bucket versions (ps_granularity='bucket', the 'auto' choice on the ipc
-    transport): the snapshot is taken between messages, so every bucket has consumed either all
-    accumulated steps or one more (its message of the step in progress arrived before the step's
-    last bucket): ver_b * M + count_b in {accumulated, accumulated + 1}, the global version is the
+    transport): the snapshot is taken between messages, so every bucket has consumed all
+    accumulated steps plus at most one per worker (the message of that worker's step in progress
+    arrived before the step's last bucket): accumulated <= ver_b * M + count_b <= accumulated + W, the global version is the
     slowest bucket's, and after the restore every later step is accounted once."""
     monkeypatch.setenv("HIPPS_PS_LOOP_DELAY_US", "4000")
     ck = str(tmp_path / "ck")
@@ -181,7 +181,8 @@ def test_async_checkpoint_quiesce_bucket_versions(tmp_path, monkeypatch):
     acc = ps["ps_accumulated"]
     es = torch.load(os.path.join(ck, "rank0.pt"), weights_only=True)["engine"]  # per-bucket PS words
     per_bucket = [v * M + c for v, c in zip(es["ver_b"], es["acc_count_b"])]
-    assert all(acc <= n <= acc + 1 for n in per_bucket), (acc, per_bucket)
+    # each of the W=2 workers may have one step in progress whose message for bucket b was consumed
+    assert all(acc <= n <= acc + 2 for n in per_bucket), (acc, per_bucket)
     assert ps["version"] == min(es["ver_b"])
     st = out[0]["stats"]
     assert st["accumulated"] == 2 * 6

@@ -1,0 +1,129 @@
+"""The native PS loop (csrc/runtime/psloop.cpp) against the Python PS loop (ps_async._serve).
+
+Both implement the same AsySG-InCon protocol with per-bucket versions; with max_delay=0 and
+every rank training on the same data the update sequence is deterministic, so the two loops must
+produce bit-identical parameters -- for every codec the native loop decodes (dense fp32 / bf16,
+int8, top-k, top-k + int8, threshold), for SGD and Adam, at one rank (M = 1: the update reads the
+message straight from the mailbox slot) and three ranks on one device (M = 3: accumulator path,
+peer-written slots read with system-scope acquires).
+"""
+import os
+
+import pytest
+import torch
+
+from dist_util import run_world
+from test_dist_cpu import _data, _mlp
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(rank, world, native, steps, codec, optim="sgd", bucket_mb=0.0005, slots=0):
+    import hipps
+
+    os.environ["HIPPS_NATIVE_PS"] = "1" if native else "0"
+    torch.cuda.set_device(0)
+    m = _mlp().cuda()
+    cls = hipps.SGD if optim == "sgd" else hipps.Adam
+    kw = dict(lr=0.05, momentum=0.9, weight_decay=1e-4) if optim == "sgd" else dict(lr=1e-3, weight_decay=1e-4)
+    opt = cls(m.named_parameters(), mode="ps_async", code=codec, bucket_mb=bucket_mb, max_delay=0,
+              accumulate=world, mailbox_slots=slots, ps_granularity="bucket", **kw)
+    nb = len(opt.engine.plan.buckets)
+    for s in range(steps):
+        if s == steps // 2:
+            for g in opt.param_groups:  # a scheduler step: the native loop must see the new lr
+                g["lr"] *= 0.5
+        x, y = _data(0, s % 4)  # every rank: rank 0's data (order-independent sums)
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x.cuda()), y.cuda()).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    eng = opt.engine
+    st = eng.ps_stats() if rank == 0 else {}
+    opt.close()
+    return {"nb": nb, "stats": st, "params": [p.detach().cpu() for p in m.parameters()],
+            "state": {k: v.detach().cpu() for k, v in opt.flat_state.items()}}
+
+
+@pytest.mark.parametrize("codec", ["fp32", "bf16", "int8", "topk:0.1", "topk_int8:0.1", "threshold:0.001:0.2"])
+def test_native_loop_single_rank_bitwise(codec):
+    a = run_world(_run, 1, True, 6, codec)[0]
+    b = run_world(_run, 1, False, 6, codec)[0]
+    assert a["stats"]["native_loop"] == 1 and b["stats"]["native_loop"] == 0
+    assert a["stats"]["accumulated"] == b["stats"]["accumulated"] == 6
+    assert a["stats"]["bucket_updates"] == b["stats"]["bucket_updates"] == 6 * a["nb"]
+    for x, y in zip(a["params"], b["params"]):
+        torch.testing.assert_close(x, y, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("codec", ["fp32", "int8", "topk:0.1"])
+def test_native_loop_three_ranks_bitwise(codec):
+    a = run_world(_run, 3, True, 6, codec, timeout=300)
+    b = run_world(_run, 3, False, 6, codec, timeout=300)
+    assert a[0]["stats"]["native_loop"] == 1
+    assert a[0]["stats"]["accumulated"] == 18 and a[0]["stats"]["version"] == 6
+    for r in range(3):
+        for x, y in zip(a[r]["params"], b[r]["params"]):
+            torch.testing.assert_close(x, y, rtol=0, atol=0)
+
+
+def test_native_loop_adam_bitwise():
+    a = run_world(_run, 1, True, 5, "fp32", "adam")[0]
+    b = run_world(_run, 1, False, 5, "fp32", "adam")[0]
+    assert a["stats"]["native_loop"] == 1
+    for x, y in zip(a["params"], b["params"]):
+        torch.testing.assert_close(x, y, rtol=0, atol=0)
+    for k in b["state"]:
+        torch.testing.assert_close(a["state"][k], b["state"][k], rtol=0, atol=0)
+
+
+def test_native_loop_slot_reuse_bitwise():
+    """2 message words per worker: every slot rewritten every second message."""
+    a = run_world(_run, 3, True, 6, "fp32", "sgd", 1e-5, 2, timeout=300)
+    b = run_world(_run, 3, False, 6, "fp32", "sgd", 1e-5, 2, timeout=300)
+    for r in range(3):
+        for x, y in zip(a[r]["params"], b[r]["params"]):
+            torch.testing.assert_close(x, y, rtol=0, atol=0)
+
+
+def _ckpt(rank, world, path, native):
+    import hipps
+    from hipps.utils import checkpoint
+
+    os.environ["HIPPS_NATIVE_PS"] = "1" if native else "0"
+    torch.cuda.set_device(0)
+
+    def make():
+        m = _mlp().cuda()
+        return m, hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", code="fp32",
+                            bucket_mb=0.0005, max_delay=0, accumulate=world, ps_granularity="bucket")
+
+    def train(m, opt, steps, s0):
+        for s in range(s0, s0 + steps):
+            x, y = _data(0, s % 4)
+            opt.zero_grad()
+            torch.nn.functional.cross_entropy(m(x.cuda()), y.cuda()).backward()
+            opt.step()
+
+    m, opt = make()
+    train(m, opt, 3, 0)
+    checkpoint.save(opt, path, m)
+    opt.close()
+    m, opt = make()
+    checkpoint.load(opt, path, m)
+    train(m, opt, 3, 3)
+    torch.cuda.synchronize()
+    st = opt.engine.ps_stats() if rank == 0 else {}
+    opt.close()
+    return {"stats": st, "params": [p.detach().cpu() for p in m.parameters()]}
+
+
+def test_native_loop_checkpoint_resume_matches_python(tmp_path):
+    """save() quiesces the native loop (pause between messages) and load() restores its versions:
+    the resumed native run equals the resumed Python-loop run bit for bit."""
+    a = run_world(_ckpt, 2, str(tmp_path / "a"), True, timeout=300)
+    b = run_world(_ckpt, 2, str(tmp_path / "b"), False, timeout=300)
+    assert a[0]["stats"]["native_loop"] == 1 and a[0]["stats"]["accumulated"] == 6
+    for r in range(2):
+        for x, y in zip(a[r]["params"], b[r]["params"]):
+            torch.testing.assert_close(x, y, rtol=0, atol=0)
