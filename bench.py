@@ -114,6 +114,7 @@ def main():
     torch.backends.cudnn.benchmark = True
 
     import hipps
+    import hipps.ops.nn as hnn
     from hipps.models import build_model
 
     torch.manual_seed(1234 + world.rank)
@@ -199,7 +200,9 @@ def main():
             t = [time.perf_counter()]
         opt.zero_grad()
         with torch.autocast("cuda", dtype=torch.bfloat16):
-            loss = model(x, y) if is_tf else F.cross_entropy(model(x), y)
+            # (the fused bf16 cross-entropy, csrc/xent.hip: one read of the logits forward, one
+            # read + gradient write backward, instead of PyTorch's log-softmax / nll kernels)
+            loss = model(x, y) if is_tf else hnn.cross_entropy(model(x), y)
         if host_t is not None:
             t.append(time.perf_counter())
         loss.backward()

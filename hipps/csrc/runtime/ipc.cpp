@@ -180,14 +180,19 @@ class VmmRegion {
       int64_t off = 0;
       for (size_t i = 0; i < fds.size() && e == hipSuccess; ++i) {
         hipMemGenericAllocationHandle_t h;
-        e = hipMemImportFromShareableHandle(&h, reinterpret_cast<void*>(static_cast<intptr_t>(fds[i])),
-                                            hipMemHandleTypePosixFileDescriptor);
+        // HIP reads the fd through the pointer (the CUDA form, the fd value cast to a pointer,
+        // dereferenced it as an address: SIGSEGV, profiles/r5/ipc)
+        int fd = fds[i];
+        e = hipMemImportFromShareableHandle(&h, &fd, hipMemHandleTypePosixFileDescriptor);
         if (e != hipSuccess) break;
         handles_.push_back(h);
         e = hipMemMap(reinterpret_cast<char*>(ptr_) + off, (size_t)sizes[i], 0, h, 0);
         off += sizes[i];
       }
-      for (int fd : fds) ::close(fd);
+      // the fds stay open until release(): a chunk's fd number is not handed out again while
+      // its import is mapped (a re-import in the same process once saw another allocation's
+      // pages when the numbers were recycled, profiles/r5/ipc)
+      fds_ = fds;
       if (e != hipSuccess) {
         release();
         hip_check(e, "VmmRegion import");
@@ -253,6 +258,8 @@ class VmmRegion {
       hipMemAddressFree(ptr_, (size_t)total_);
     }
     handles_.clear();
+    for (int fd : fds_) ::close(fd);
+    fds_.clear();
     ptr_ = nullptr;
   }
   void* ptr_ = nullptr;
@@ -261,6 +268,7 @@ class VmmRegion {
   bool owner_;
   std::vector<int64_t> sizes_;
   std::vector<hipMemGenericAllocationHandle_t> handles_;
+  std::vector<int> fds_;  // imported chunks' fds, closed with the mapping
 };
 
 // ---------------------------------------------------------------------------------------------

@@ -56,7 +56,7 @@ struct MsgField {
   at::ScalarType dtype;
 };
 struct BucketDesc {
-  int64_t lo, hi, msg_ext;
+  int64_t lo, hi, msg_ext, wire_off, msg_nbytes;
   int kind;
   std::vector<MsgField> f;
 };
@@ -72,6 +72,7 @@ struct Pend {
   double scale;
   int worker;
   int64_t off;  // message offset in the worker's ring
+  bool emu;     // an emulated remote copy of the preceding message (cfg.emulate_remote)
 };
 
 static at::ScalarType dtype_of(int code) {
@@ -118,6 +119,8 @@ class NativePS {
       b.lo = d["lo"].cast<int64_t>();
       b.hi = d["hi"].cast<int64_t>();
       b.msg_ext = d["msg_ext"].cast<int64_t>();
+      b.wire_off = d["wire_off"].cast<int64_t>();
+      b.msg_nbytes = d["msg_nbytes"].cast<int64_t>();
       b.kind = d["kind"].cast<int>();
       for (auto f : d["fields"].cast<py::list>()) {
         auto t = f.cast<py::tuple>();
@@ -141,6 +144,14 @@ class NativePS {
     max_exp_avg_sq_ = opt_t("max_exp_avg_sq");
     csteps_ = opt_t("csteps");
     chunk_slots_ = opt_t("chunk_slots");
+    // rehearsal: E emulated remote workers' PS load (PSConfig.emulate_remote)
+    emu_ = c.contains("emu") ? c["emu"].cast<int>() : 0;
+    if (emu_ > 0) {
+      emu_in_ = c["emu_in"].cast<at::Tensor>();
+      emu_sink_ = c["emu_sink"].cast<at::Tensor>();
+      emu_stream_ = c["emu_stream"].cast<int64_t>();
+      hip_ok(hipEventCreateWithFlags(&emu_ev_, hipEventDisableTiming), "hipEventCreate");
+    }
     if ((int)rings_.size() != W_ || (int)remote_.size() != W_) throw std::runtime_error("native PS: rings per worker");
     if ((int)buckets_.size() != nb_) throw std::runtime_error("native PS: bucket table");
     seen_.assign(W_, 0);
@@ -160,6 +171,7 @@ class NativePS {
       py::gil_scoped_release nogil;
       th_.join();
     }
+    if (emu_ev_) hipEventDestroy(emu_ev_);
   }
 
   // hyper-parameters of group gi (pushed by Python at every step(): schedulers may change lr)
@@ -387,7 +399,8 @@ class NativePS {
       direct_[bi] = Direct{true, off, i, seq, scale};
       return;
     }
-    pend_.push_back(Pend{bi, scale, i, off});
+    pend_.push_back(Pend{bi, scale, i, off, false});
+    for (int e = 0; e < emu_; ++e) pend_.push_back(Pend{bi, scale, i, off, true});
   }
 
   void ack(int i, int64_t s) {
@@ -451,7 +464,12 @@ class NativePS {
   void flush() {
     if (!pend_.empty()) {
       std::vector<std::pair<std::pair<int, double>, std::vector<const Pend*>>> groups;
+      std::vector<const Pend*> emu;
       for (const Pend& p : pend_) {
+        if (p.emu) {
+          emu.push_back(&p);
+          continue;
+        }
         auto key = std::make_pair(p.bi, p.scale);
         auto it = std::find_if(groups.begin(), groups.end(), [&](auto& g) { return g.first == key; });
         if (it == groups.end()) {
@@ -471,6 +489,11 @@ class NativePS {
           decode_into(part, b, acc, g.first.second, acq);
           bump("acc_launches");
         }
+      }
+      for (const Pend* p : emu) {  // the same bytes once more per emulated worker, one launch each
+        const BucketDesc& b = buckets_[p->bi];
+        decode_into({p}, b, acc_.narrow(0, b.lo, b.hi - b.lo), p->scale, remote_[p->worker]);
+        bump("acc_launches");
       }
       pend_.clear();
     }
@@ -558,8 +581,30 @@ class NativePS {
     for (size_t j = 0; j < words.size(); j += 6)
       ctl_.enqueue(stream_, std::vector<std::tuple<int, int, int64_t>>(
                                 words.begin() + j, words.begin() + std::min(words.size(), j + 6)));
+    if (emu_ > 0) emulate_traffic(k, bi);
     if (gver >= 0) ctl_.fetch_add(UPDATES, 0, 1);
     bump("bucket_updates");
+  }
+
+  // PSAsyncEngine._emulate_remote_traffic: E write sweeps of the bucket's message bytes (their
+  // pushes landing) and E read sweeps of its publish range (their pulls), on a low-priority stream
+  // ordered after the update
+  void emulate_traffic(int k, int bi) {
+    const BucketDesc& b = buckets_[bi];
+    hipStream_t ps = reinterpret_cast<hipStream_t>(stream_), es = reinterpret_cast<hipStream_t>(emu_stream_);
+    hip_ok(hipEventRecord(emu_ev_, ps), "hipEventRecord");
+    hip_ok(hipStreamWaitEvent(es, emu_ev_, 0), "hipStreamWaitEvent");
+    c10::hip::HIPStreamGuard g(c10::hip::getStreamFromExternal(es, device_));
+    at::Tensor win = emu_in_.narrow(0, b.wire_off, b.msg_nbytes);
+    at::Tensor pub = pub_buf(k).narrow(0, b.lo, b.hi - b.lo);
+    for (int e = 0; e < emu_; ++e) {
+      win.fill_(e);
+      at::Tensor out = emu_sink_.narrow(0, e, 1).squeeze(0);
+      at::amax_out(out, pub, {0});
+    }
+  }
+  static void hip_ok(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
   }
 
   ControlBlock& ctl_;
@@ -569,6 +614,10 @@ class NativePS {
   double gscale_;
   at::Tensor acc_, master_, pub_, mom_buf_, exp_avg_, exp_avg_sq_, max_exp_avg_sq_, csteps_, chunk_slots_;
   at::ScalarType pub_dtype_;
+  int emu_ = 0;
+  int64_t emu_stream_ = 0;
+  hipEvent_t emu_ev_ = nullptr;
+  at::Tensor emu_in_, emu_sink_;
   std::vector<at::Tensor> rings_;
   std::vector<bool> remote_;
   std::vector<BucketDesc> buckets_;

@@ -853,7 +853,11 @@ class _CrossEntropy(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, labels, ignore_index):
         loss_rows, lse = native().xent_forward(logits, labels, int(ignore_index))
-        n = (labels != ignore_index).sum().clamp_min(1).to(torch.float32)
+        # the mean runs over the rows that carry a loss: not ignore_index and inside [0, V) (an
+        # out-of-range label contributes no loss -- F.cross_entropy raises on it -- and is not
+        # counted either); every row ignored -> 0 / 0 = NaN, as F.cross_entropy returns
+        V = logits.shape[-1]
+        n = ((labels != ignore_index) & (labels >= 0) & (labels < V)).sum().to(torch.float32)
         ctx.save_for_backward(logits, labels, lse, n)
         ctx.ignore = int(ignore_index)
         return loss_rows.sum() / n

@@ -336,6 +336,13 @@ class MPI_PS(torch.optim.Optimizer):
             self.engine.join_pull()
         self.store.refresh_shadow()
 
+    def watch_module(self, module: torch.nn.Module):
+        """Refresh the bf16 weight shadow whenever ``module.load_state_dict`` writes parameters
+        this optimizer manages (a post-hook: the shadow-reading conv / Linear kernels would
+        otherwise keep reading the pre-load weights until the next step).  ``load_state_dict`` of
+        the optimizer itself and ``hipps.utils.checkpoint.load`` refresh it already."""
+        return module.register_load_state_dict_post_hook(lambda _m, _keys: self.refresh_bf16_weights())
+
     def close(self):
         if getattr(self, "engine", None) is not None:
             self.engine.close()

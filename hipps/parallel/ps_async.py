@@ -554,6 +554,19 @@ class PSAsyncEngine(Engine):
             else:
                 self._gpg = _TorchChannel(W)
                 self._ppg = _TorchChannel(W)
+        # mailbox allocations on a GPU: 'vmm' (hipMemCreate chunks exported as fds, mapped back to
+        # back: no single import larger than one chunk) or 'ipc' (one hipMalloc per region,
+        # hipIpcOpenMemHandle); HIPPS_IPC_ALLOC selects, HIPPS_VMM_CHUNK_MB sizes the chunks
+        # 'auto': hipIpcOpenMemHandle of one allocation of 2 GiB never returned on the rehearsal box
+        # (its thread spinning in user space; 4 x 512 MB allocations imported in 1 ms,
+        # profiles/r5/ipc), so regions from 1 GiB up take the VMM path
+        self.ipc_alloc = os.environ.get("HIPPS_IPC_ALLOC", "auto")
+        if self.ipc_alloc == "auto":
+            big = max(self.ring_bytes, self.NPUB * self.pub_bytes) >= (1 << 30)
+            self.ipc_alloc = "vmm" if big else "ipc"
+        if self.ipc_alloc == "vmm" and not hasattr(C, "VmmRegion"):
+            self.ipc_alloc = "ipc"
+        self.vmm_chunk = int(float(os.environ.get("HIPPS_VMM_CHUNK_MB", "512")) * (1 << 20))
         self._rendezvous(C, W, store)
         # GPU-rung doorbells need the control block registered with HIP in this process
         self.device_bells = bool(self.cuda and self.ctl.enable_device_doorbells())
@@ -770,7 +783,18 @@ class PSAsyncEngine(Engine):
                 self.rings = [torch.zeros(self.ring_bytes, dtype=torch.uint8, device=store.device) for _ in range(W)]
                 self.pub_mem = torch.zeros(pub_total, dtype=torch.uint8, device=store.device)
             else:
-                if self.cuda:
+                if self.cuda and self.ipc_alloc == "vmm":
+                    # hipMemCreate chunks mapped contiguously; their fds go to each worker over a
+                    # Unix socket (SCM_RIGHTS) when its import turn comes (_serve_fds)
+                    ch = self.vmm_chunk
+                    mbs = [C.VmmRegion(self.ring_bytes, ch) for _ in range(W)] + [C.VmmRegion(pub_total, ch)]
+                    fd_name = f"hipps_fd_{os.getpid()}_{token}"
+                    self._fdsrv = C.FdServer(fd_name)
+                    handles = {"vmm": fd_name, "ring_sizes": mbs[0].chunk_sizes(), "pub_sizes": mbs[W].chunk_sizes()}
+                    self._fd_thread = threading.Thread(target=self._serve_fds, args=(mbs,), name="hipps-fds",
+                                                       daemon=True)
+                    self._fd_thread.start()
+                elif self.cuda:
                     mbs = [C.DeviceMailbox(self.ring_bytes) for _ in range(W)] + [C.DeviceMailbox(pub_total)]
                     handles = [m.handle() for m in mbs]
                 else:
@@ -804,6 +828,7 @@ class PSAsyncEngine(Engine):
                 if self.rank == 0:
                     self.ctl.unlink()
                     self._unlink_host()
+                    self._stop_fds()
                 msg = "ps_async ipc transport: mapping the PS mailbox failed (" + "; ".join(bad) + ")"
                 if any(t for _, t in errs):
                     raise IPCOpenTimeout(msg)
@@ -812,6 +837,29 @@ class PSAsyncEngine(Engine):
         if self.rank == 0:  # everyone has mapped: remove the names (no /dev/shm leftovers)
             self.ctl.unlink()
             self._unlink_host()
+            self._stop_fds()
+
+    def _serve_fds(self, mbs):
+        """Rank 0, VMM mailboxes: hand worker i the fds of the publish region's and its ring's
+        chunks when it connects (workers connect in import-turn order); stop when a turn fails."""
+        W, C = self.W, self.C
+        try:
+            for i in range(1, W):
+                while True:
+                    if self.ctl.load(C.F_OPEN_TURN, 0) >= (1 << 40) or getattr(self, "_fds_stop", False):
+                        return
+                    if self._fdsrv.send_one(mbs[W].export_fds() + mbs[i].export_fds(), 500):
+                        break
+        except Exception as e:  # reported by the worker that waits for these fds
+            self._fds_err = f"{type(e).__name__}: {e}"
+
+    def _stop_fds(self):
+        t = getattr(self, "_fd_thread", None)
+        if t is not None:
+            self._fds_stop = True
+            t.join(timeout=5)
+            self._fdsrv.close()
+            self._fd_thread = None
 
     def _unlink_host(self):
         if not self.cuda:
@@ -833,7 +881,19 @@ class PSAsyncEngine(Engine):
             return None, False
         nm = f"{self.mb_name}_{self.rank}"
         try:
-            if self.cuda:
+            if self.cuda and isinstance(handles, dict):  # VMM chunks: fds over the rank-0 socket
+                t0 = time.perf_counter()
+                fds = C.fd_recv(handles["vmm"], int(limit * 1000))
+                npc = len(handles["pub_sizes"])
+                pub, t1 = _bounded_open(lambda: C.VmmRegion(fds[:npc], handles["pub_sizes"], pub_total),
+                                        f"the publish region ({pub_total >> 20} MB, {npc} chunks)", self.rank,
+                                        store.device, limit)
+                self._mbs.append(pub)
+                ring, t2 = _bounded_open(lambda: C.VmmRegion(fds[npc:], handles["ring_sizes"], self.ring_bytes),
+                                         f"its mailbox ring ({self.ring_bytes >> 20} MB)", self.rank, store.device,
+                                         limit)
+                t1 = time.perf_counter() - t0 - t2  # (the fd hand-over counts as the first import)
+            elif self.cuda:
                 pub, t1 = _bounded_open(lambda: C.DeviceMailbox(handles[W], pub_total), f"the publish region "
                                         f"({pub_total >> 20} MB)", self.rank, store.device, limit)
                 self._mbs.append(pub)
@@ -1029,7 +1089,7 @@ class PSAsyncEngine(Engine):
             return None
         kind = self._native_kind(codec)
         tau_zero = cfg.stale_lookahead == 0 or (cfg.stale_lookahead < 0 and cfg.max_delay == 0)
-        if not (self.cuda and not self.p2p and self.bucketwise and not self.emu and self._lat is None
+        if not (self.cuda and not self.p2p and self.bucketwise and self._lat is None
                 and self._fault is None and not self.plan.guarded and tau_zero and kind is not None
                 and getattr(self.opt, "optim", None) in ("sgd", "adam") and not self.is_object
                 and float(os.environ.get("HIPPS_PS_LOOP_DELAY_US", "0")) == 0):
@@ -1055,6 +1115,7 @@ class PSAsyncEngine(Engine):
         for bi, b in enumerate(self.plan.buckets):
             fl = {f.name: f for f in b.layout.fields}
             buckets.append({"lo": int(b.lo), "hi": int(b.hi), "msg_ext": int(self.msg_ext[bi]), "kind": k,
+                            "wire_off": int(b.wire_offset), "msg_nbytes": int(b.msg_nbytes),
                             "fields": [(int(fl[n].offset), int(fl[n].numel), _DTYPE_CODE[fl[n].dtype]) for n in names]})
         d = {"W": self.W, "rank": self.rank, "nb": self.nb, "slots": self.SLOTS, "maxslots": self.MAXSLOTS,
              "M": self.M, "staleness": int(cfg.staleness), "staleness_lr": bool(cfg.staleness_lr),
@@ -1065,6 +1126,9 @@ class PSAsyncEngine(Engine):
              "pub_bytes": int(self.pub_bytes), "pub_dtype": _DTYPE_CODE[self.pub_dtype],
              "rings": list(self.rings), "remote": [self._remote(i) for i in range(self.W)],
              "buckets": buckets, "groups": groups, "chunk_slots": store.chunk_slots(), **st}
+        if self.emu:
+            d.update(emu=int(self.emu), emu_in=self._emu_in, emu_sink=self._emu_sink,
+                     emu_stream=int(self._emu_stream.cuda_stream))
         return self.C.NativePS(self.ctl, d)
 
     def _push_hyper(self):
@@ -2085,7 +2149,7 @@ class PSAsyncEngine(Engine):
                 "p2p_channels": (None if not self.p2p else "rccl-split" if self._gpg.native else "torch"),
                 "granularity": self.granularity,
                 "ps_dedicated": self.dedicated, "accumulate": self.M,
-                "npub": self.NPUB, "mapped_bytes": self.mapped_bytes,
+                "npub": self.NPUB, "mapped_bytes": self.mapped_bytes, "ipc_alloc": self.ipc_alloc,
                 "budget_gb": ({k: round(v / 1e9, 2) for k, v in self.budget.items() if k in ("ps_total", "worker_total",
                                                                                          "total", "limit")}
                               if self.budget else None),

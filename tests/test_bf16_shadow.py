@@ -119,3 +119,19 @@ def test_transposed_shadow_matches_torch_gpu():
     finally:
         opt.close()
     assert not hnn._TSHADOWS
+
+
+def test_watch_module_refreshes_shadow_after_model_load():
+    """a model.load_state_dict after the optimizer exists must reach the bf16 shadow."""
+    import hipps
+
+    m = torch.nn.Sequential(torch.nn.Linear(16, 16), torch.nn.Linear(16, 4))
+    opt = hipps.SGD(m.named_parameters(), lr=0.1, mode="local", bf16_weights="on")
+    if getattr(opt.store, "shadow", None) is None:
+        opt.close()
+        return  # (no shadow on this device)
+    opt.watch_module(m)
+    sd = {k: torch.full_like(v, 0.5) for k, v in m.state_dict().items()}
+    m.load_state_dict(sd)
+    assert torch.equal(opt.store.shadow.float(), opt.store.data.to(torch.bfloat16).float())
+    opt.close()

@@ -55,3 +55,27 @@ def test_colsum_matches_fp32(rows, cols):
     assert got.dtype == torch.float32
     torch.testing.assert_close(got.double(), ref, rtol=1e-5, atol=1e-3)
     assert torch.equal(got, hnn.colsum_f32(t))  # deterministic
+
+
+def test_fused_cross_entropy_label_semantics():
+    """the mean counts only rows that carry a loss.  Ignored rows and out-of-range
+    labels (which F.cross_entropy rejects) are excluded from the denominator; every row ignored
+    gives NaN, as F.cross_entropy does."""
+    from hipps.ops.nn import cross_entropy
+
+    torch.manual_seed(3)
+    logits = torch.randn(8, 64, device="cuda").to(torch.bfloat16)
+    y = torch.randint(0, 64, (8,), device="cuda")
+    y[1] = -100
+    y[5] = -100
+    ref = torch.nn.functional.cross_entropy(logits.float(), y, ignore_index=-100)
+    got = cross_entropy(logits, y)
+    torch.testing.assert_close(got.float(), ref, rtol=1e-3, atol=1e-3)
+    bad = y.clone()
+    bad[2] = 64  # out of range: no loss, not counted
+    keep = (bad != -100) & (bad < 64)
+    ref2 = torch.nn.functional.cross_entropy(logits.float()[keep], bad[keep])
+    torch.testing.assert_close(cross_entropy(logits, bad).float(), ref2, rtol=1e-3, atol=1e-3)
+    allign = torch.full_like(y, -100)
+    assert torch.isnan(cross_entropy(logits, allign)) and torch.isnan(
+        torch.nn.functional.cross_entropy(logits.float(), allign))

@@ -55,16 +55,24 @@ def main():
                 import secrets
 
                 mine = [C.VmmRegion(mb << 20, (a.chunk_mb or mb) << 20)] if rank == 0 else []
+                if rank == 0:
+                    reg = mine[0].tensor()
+                    for c in range(len(mine[0].chunk_sizes())):
+                        reg[c * ((a.chunk_mb or mb) << 20)] = (c % 200) + 1
+                    torch.cuda.synchronize()
                 name = f"hipps_probe_{secrets.token_hex(4)}" if rank == 0 else None
                 srv = C.FdServer(name) if rank == 0 else None
                 meta = [(name, mine[0].chunk_sizes()) if rank == 0 else None]
             else:
                 mine = [C.DeviceMailbox(p << 20) for p in parts] if rank == 0 else []
+                for c, m in enumerate(mine):  # stamp every allocation (checked by the importers)
+                    m.tensor()[0] = (c % 200) + 1
+                torch.cuda.synchronize()
                 meta = [[m.handle() for m in mine] if rank == 0 else None]
             t_alloc = time.perf_counter() - t0
             dist.broadcast_object_list(meta, src=0)
             if a.vmm:
-                parts = [len(meta[0][1])]
+                parts = list(range(len(meta[0][1])))
             res = None
             for r in range(1, W):  # one importer at a time
                 if rank == 0 and a.vmm:
@@ -77,14 +85,23 @@ def main():
                             fds = C.fd_recv(nm, int(a.limit * 1000))
                             mbx, _ = _bounded_open(lambda: C.VmmRegion(fds, sizes, mb << 20), f"{mb} MB (vmm)", rank,
                                                    torch.cuda.current_device(), a.limit)
-                            mbx.tensor()[:16].fill_(rank)
                             mine.append(mbx)
+                            # data check, both directions: the exporter stamped chunk c's first byte
+                            # with (c % 200) + 1; this importer writes its rank at the region's end
+                            t = mbx.tensor()
+                            seen = [int(t[c * ((a.chunk_mb or mb) << 20)]) for c in range(len(sizes))]
+                            want = [(c % 200) + 1 for c in range(len(sizes))]
+                            t[-16:].fill_(rank)
+                            if seen != want:
+                                raise IPCOpenTimeout(f"STALE rank {rank}: saw {seen[:6]} want {want[:6]}")
                         else:
-                            for h, p in zip(meta[0], parts):
+                            for c, (h, p) in enumerate(zip(meta[0], parts)):
                                 mbx, _ = _bounded_open(lambda h=h, p=p: C.DeviceMailbox(h, p << 20), f"{p} MB", rank,
                                                        torch.cuda.current_device(), a.limit)
-                                mbx.tensor()[:16].fill_(rank)
                                 mine.append(mbx)
+                                got = int(mbx.tensor()[0])
+                                if got != (c % 200) + 1:
+                                    raise IPCOpenTimeout(f"STALE rank {rank}: allocation {c} reads {got}")
                         torch.cuda.synchronize()
                         res = round(time.perf_counter() - t1, 4)
                     except IPCOpenTimeout as e:
@@ -92,9 +109,9 @@ def main():
                 dist.barrier()
             if a.vmm and rank == 0:
                 srv.close()
-                # the importers' writes landed in the exporter's memory
-                got = mine[0].tensor()[:16].cpu().tolist()
-                print(f"  vmm first bytes seen by the exporter: {got[:4]}", flush=True)
+            if a.vmm and rank == 0:
+                got = mine[0].tensor()[-16:].cpu().tolist()
+                print(f"  vmm last bytes seen by the exporter: {got[:4]} (want [{W - 1}, ...])", flush=True)
             out = [None] * W
             dist.all_gather_object(out, res)
             if rank == 0:
