@@ -107,11 +107,22 @@ class NativePS {
     direct_ok_ = c["direct_ok"].cast<bool>();
     acc_ = c["acc"].cast<at::Tensor>();
     master_ = c["master"].cast<at::Tensor>();
-    pub_ = c["pub"].cast<at::Tensor>();  // uint8 publish region (npub buffers, pub_bytes apart)
-    pub_bytes_ = c["pub_bytes"].cast<int64_t>();
+    // publish buffers as chunks of pub_chunk elements (each an IPC allocation below 2 GiB), typed
+    for (auto q : c["pub_chunks"].cast<py::list>()) {
+      std::vector<at::Tensor> v;
+      for (auto t : q.cast<py::list>()) v.push_back(t.cast<at::Tensor>());
+      pub_.push_back(std::move(v));
+    }
+    pub_chunk_ = c["pub_chunk"].cast<int64_t>();
     pub_dtype_ = dtype_of(c["pub_dtype"].cast<int>());
     numel_ = master_.numel();
-    for (auto r : c["rings"].cast<py::list>()) rings_.push_back(r.is_none() ? at::Tensor() : r.cast<at::Tensor>());
+    ring_chunk_ = c["ring_chunk"].cast<int64_t>();
+    for (auto r : c["rings"].cast<py::list>()) {
+      std::vector<at::Tensor> v;
+      if (!r.is_none())
+        for (auto t : r.cast<py::list>()) v.push_back(t.cast<at::Tensor>());
+      rings_.push_back(std::move(v));
+    }
     for (auto r : c["remote"].cast<py::list>()) remote_.push_back(r.cast<bool>());
     for (auto o : c["buckets"].cast<py::list>()) {
       auto d = o.cast<py::dict>();
@@ -259,12 +270,26 @@ class NativePS {
     double scale = 1.0;
   };
 
-  at::Tensor view(int worker, int64_t off, const MsgField& f) const {
-    return rings_[worker].narrow(0, off + f.off, f.numel * (int64_t)c10::elementSize(f.dtype)).view(f.dtype);
+  // bytes [off, off + n) of a worker's ring (a message never straddles two ring chunks)
+  at::Tensor ring_bytes(int worker, int64_t off, int64_t n) const {
+    const int64_t c = off / ring_chunk_, o = off - c * ring_chunk_;
+    return rings_[worker].at(c).narrow(0, o, n);
   }
-  at::Tensor pub_buf(int k) const {
-    const int64_t esz = (int64_t)c10::elementSize(pub_dtype_);
-    return pub_.narrow(0, (int64_t)k * pub_bytes_, numel_ * esz).view(pub_dtype_);
+  at::Tensor view(int worker, int64_t off, const MsgField& f) const {
+    return ring_bytes(worker, off + f.off, f.numel * (int64_t)c10::elementSize(f.dtype)).view(f.dtype);
+  }
+  // elements [a, b) of publish buffer k, inside one chunk
+  at::Tensor pub_view(int k, int64_t a, int64_t b) const {
+    const int64_t c = a / pub_chunk_;
+    return pub_[k].at(c).narrow(0, a - c * pub_chunk_, b - a);
+  }
+  template <typename F>
+  void pub_pieces(int64_t lo, int64_t hi, F fn) const {
+    for (int64_t a = lo; a < hi;) {
+      const int64_t b = std::min(hi, (a / pub_chunk_ + 1) * pub_chunk_);
+      fn(a, b);
+      a = b;
+    }
   }
   void bump(const char* k, int64_t v = 1) { stats_[k] += v; }
 
@@ -416,7 +441,7 @@ class NativePS {
       pres_part_b_[bi] = at::Tensor();
       return;
     }
-    at::Tensor p = rings_[i].narrow(0, off + buckets_[bi].msg_ext, ns_);
+    at::Tensor p = ring_bytes(i, off + buckets_[bi].msg_ext, ns_);
     if (remote_[i]) {
       at::Tensor t = at::empty({ns_}, p.options());
       copy_acquire(p, t);
@@ -506,15 +531,16 @@ class NativePS {
     pend_acks_.clear();
   }
 
+  // optimizer step of flat [lo, hi) (inside one publish chunk) publishing into buffer k
   void update_range(const at::Tensor& src, int64_t src_lo, int64_t lo, int64_t hi, double gscale, bool zero_src,
-                    const at::Tensor& pub, const at::Tensor& mask) {
+                    int k, const at::Tensor& mask) {
     std::lock_guard<std::mutex> lk(hp_mu_);
     for (Group& g : groups_) {
       const int64_t a = std::max(g.a, lo), b = std::min(g.b, hi);
       if (b <= a) continue;
       std::vector<at::Tensor> srcs{src.narrow(0, a - src_lo, b - a)};
       at::Tensor tgt = master_.narrow(0, a, b - a);
-      c10::optional<at::Tensor> pb = pub.narrow(0, a, b - a);
+      c10::optional<at::Tensor> pb = pub_view(k, a, b);
       c10::optional<at::Tensor> mk;
       if (mask.defined()) mk = mask.narrow(0, a / 16, (b - a) / 16);
       c10::optional<at::Tensor> cs;
@@ -562,15 +588,16 @@ class NativePS {
         if (g.b > g.a) g.steps += 1;
       gsteps_ = top;
     }
-    at::Tensor pub = pub_buf(k);
     Direct d = direct_[bi];
     direct_[bi] = Direct{};
     if (d.set) {  // straight from the mailbox slot (M = 1)
       at::Tensor msg = view(d.worker, d.off, b.f[0]);
-      update_range(msg, b.lo, b.lo, b.hi, gscale_ * d.scale, false, pub, mask);
+      pub_pieces(b.lo, b.hi, [&](int64_t pa, int64_t pb) {
+        update_range(msg, b.lo, pa, pb, gscale_ * d.scale, false, k, mask);
+      });
       bump("direct_updates");
     } else {
-      update_range(acc_, 0, b.lo, b.hi, gscale_, true, pub, mask);
+      pub_pieces(b.lo, b.hi, [&](int64_t pa, int64_t pb) { update_range(acc_, 0, pa, pb, gscale_, true, k, mask); });
     }
     std::vector<std::tuple<int, int, int64_t>> words;
     if (d.set) words.emplace_back(ACK_SEQ, d.worker, d.seq);  // the slot is free once the update read it
@@ -596,11 +623,10 @@ class NativePS {
     hip_ok(hipStreamWaitEvent(es, emu_ev_, 0), "hipStreamWaitEvent");
     c10::hip::HIPStreamGuard g(c10::hip::getStreamFromExternal(es, device_));
     at::Tensor win = emu_in_.narrow(0, b.wire_off, b.msg_nbytes);
-    at::Tensor pub = pub_buf(k).narrow(0, b.lo, b.hi - b.lo);
     for (int e = 0; e < emu_; ++e) {
       win.fill_(e);
       at::Tensor out = emu_sink_.narrow(0, e, 1).squeeze(0);
-      at::amax_out(out, pub, {0});
+      pub_pieces(b.lo, b.hi, [&](int64_t pa, int64_t pb) { at::amax_out(out, pub_view(k, pa, pb), {0}); });
     }
   }
   static void hip_ok(hipError_t e, const char* what) {
@@ -609,16 +635,18 @@ class NativePS {
 
   ControlBlock& ctl_;
   int W_, rank_, nb_, SLOTS_, MAXSLOTS_, M_, npub_, device_;
-  int64_t staleness_, dead_after_us_, ns_, stream_, pub_bytes_, numel_;
+  int64_t staleness_, dead_after_us_, ns_, stream_, numel_;
   bool staleness_lr_, skip_missing_, direct_ok_;
   double gscale_;
-  at::Tensor acc_, master_, pub_, mom_buf_, exp_avg_, exp_avg_sq_, max_exp_avg_sq_, csteps_, chunk_slots_;
+  at::Tensor acc_, master_, mom_buf_, exp_avg_, exp_avg_sq_, max_exp_avg_sq_, csteps_, chunk_slots_;
+  std::vector<std::vector<at::Tensor>> pub_;  // [npub][chunk]
+  int64_t pub_chunk_ = 0, ring_chunk_ = 0;
   at::ScalarType pub_dtype_;
   int emu_ = 0;
   int64_t emu_stream_ = 0;
   hipEvent_t emu_ev_ = nullptr;
   at::Tensor emu_in_, emu_sink_;
-  std::vector<at::Tensor> rings_;
+  std::vector<std::vector<at::Tensor>> rings_;  // [worker][chunk] (uint8)
   std::vector<bool> remote_;
   std::vector<BucketDesc> buckets_;
   std::vector<Group> groups_;

@@ -29,6 +29,15 @@
 namespace hipps {
 namespace rt {
 
+// where publish buffer k's bytes for the launch's range start (the caller offsets each pointer
+// so that element i of the copied range sits at p[k] + i * esz): the buffers need not be one
+// allocation -- a multi-GB publish region is several IPC allocations (ps_async chunks: one
+// hipIpcOpenMemHandle of a 2 GiB allocation never returned, profiles/r5/ipc)
+constexpr int kMaxPub = 4;
+struct PubPtrs {
+  const uint8_t* p[kMaxPub];
+};
+
 struct PullWords {
   int64_t* pub_ver;
   int64_t* buf_ver;  // [npub]
@@ -63,9 +72,9 @@ __global__ __launch_bounds__(64) void k_pull_select(PullWords w, int64_t* __rest
 // params[lo, hi) <- publish buffer of sel[0]; four 4-element groups per lane in flight (the
 // remote reads cross xGMI, where latency, not the lane count, bounds a one-load-per-lane loop)
 template <typename Tin>
-__global__ __launch_bounds__(kBlock) void k_pull_copy(const int64_t* __restrict__ sel, const uint8_t* __restrict__ pub,
-                                                      int64_t stride, int npub, float* __restrict__ dst, int64_t n,
-                                                      int fence_mode, uint16_t* __restrict__ sh) {
+__global__ __launch_bounds__(kBlock) void k_pull_copy(const int64_t* __restrict__ sel, PubPtrs pub, int npub,
+                                                      float* __restrict__ dst, int64_t n, int fence_mode,
+                                                      uint16_t* __restrict__ sh) {
   constexpr int U = 4;
   const int64_t v = sel[0];
   if (v < 0) return;
@@ -78,7 +87,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_copy(const int64_t* __restrict_
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before any load
   }
   if (fence_mode == 1) __syncthreads();
-  const Tin* src = reinterpret_cast<const Tin*>(pub + (v % npub) * stride);
+  const Tin* src = reinterpret_cast<const Tin*>(pub.p[v % npub]);
   const int64_t nv = n >> 2, step = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < nv; i0 += U * step) {
     float4 t[U];
@@ -143,9 +152,9 @@ __global__ __launch_bounds__(64) void k_pull_select_b(PullWordsB w, int64_t* __r
 // params[lo, hi) <- per bucket (blockIdx.y), the publish slot of that bucket's selected version
 template <typename Tin>
 __global__ __launch_bounds__(kBlock) void k_pull_copy_b(const int64_t* __restrict__ selb,
-                                                        const int64_t* __restrict__ boff, const uint8_t* __restrict__ pub,
-                                                        int64_t stride, int npub, float* __restrict__ dst, int64_t lo,
-                                                        int64_t hi, int fence_mode, uint16_t* __restrict__ sh) {
+                                                        const int64_t* __restrict__ boff, PubPtrs pub, int npub,
+                                                        float* __restrict__ dst, int64_t lo, int64_t hi, int fence_mode,
+                                                        uint16_t* __restrict__ sh) {
   constexpr int U = 4;
   const int b = blockIdx.y;
   const int64_t v = selb[b];
@@ -157,7 +166,7 @@ __global__ __launch_bounds__(kBlock) void k_pull_copy_b(const int64_t* __restric
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before any load
   }
   if (fence_mode == 1) __syncthreads();
-  const Tin* src = reinterpret_cast<const Tin*>(pub + (v % npub) * stride);
+  const Tin* src = reinterpret_cast<const Tin*>(pub.p[v % npub]);  // element i at src[i]
   const int64_t a4 = (a + 3) >> 2, e4 = e >> 2, step = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i0 = a4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < e4; i0 += U * step) {
     float4 t[U];
@@ -231,38 +240,62 @@ static uint16_t* shadow_of(const c10::optional<at::Tensor>& shadow, const at::Te
   return reinterpret_cast<uint16_t*>(shadow->data_ptr());
 }
 
-// shadow (optional): the bf16 weight shadow of dst, written in the same pass (RNE of the adopted
-// value; exact for a bf16 publish buffer) -- the separate shadow cast pass goes away
-void pull_copy(at::Tensor sel, at::Tensor pub, int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t lo,
-               int64_t hi, c10::optional<at::Tensor> shadow) {
-  TORCH_CHECK(sel.is_cuda() && sel.scalar_type() == at::kLong && sel.is_contiguous(), "sel must be int64 device");
-  TORCH_CHECK(pub.is_cuda() && pub.scalar_type() == at::kByte, "pub must be a uint8 device view");
-  TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kFloat && dst.is_contiguous(), "dst must be f32 device");
-  const int64_t esz = bf16 ? 2 : 4;
-  TORCH_CHECK(0 <= lo && lo <= hi && hi <= dst.numel() && lo % 4 == 0, "range [lo, hi) of dst, lo % 4 == 0");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(pub.data_ptr()) % 16 == 0 && stride % 16 == 0, "pub must be 16B aligned");
-  TORCH_CHECK(npub >= 1 && pub.numel() >= (npub - 1) * stride + dst.numel() * esz, "publish view too small");
-  if (hi == lo) return;
-  const int64_t n = hi - lo;
-  auto stream = c10::hip::getCurrentHIPStream();
-  static const int fence_mode = [] {  // A/B knob: 0 every wave fences, 1 one wave per workgroup
+static PubPtrs ptrs_of(const std::vector<int64_t>& ptrs, int64_t npub) {
+  TORCH_CHECK(npub >= 1 && npub <= kMaxPub && (int64_t)ptrs.size() == npub, "one publish pointer per buffer (<= 4)");
+  PubPtrs p{};
+  for (int64_t k = 0; k < npub; ++k) p.p[k] = reinterpret_cast<const uint8_t*>(ptrs[k]);
+  return p;
+}
+
+static int pull_fence_mode() {  // A/B knob: 0 every wave fences, 1 one wave per workgroup
+  static const int v = [] {
     const char* e = std::getenv("HIPPS_PULL_FENCE");
     return e ? std::atoi(e) : 1;
   }();
+  return v;
+}
+
+// dst[lo, hi) <- the selected publish buffer; ptrs[k]: device address of buffer k's element lo
+// (16-byte aligned).  shadow (optional): the bf16 weight shadow of dst, written in the same pass
+// (RNE of the adopted value; exact for a bf16 publish buffer) -- the separate shadow cast pass
+// goes away
+void pull_copy_ptrs(at::Tensor sel, std::vector<int64_t> ptrs, int64_t npub, bool bf16, at::Tensor dst, int64_t lo,
+                    int64_t hi, c10::optional<at::Tensor> shadow) {
+  TORCH_CHECK(sel.is_cuda() && sel.scalar_type() == at::kLong && sel.is_contiguous(), "sel must be int64 device");
+  TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kFloat && dst.is_contiguous(), "dst must be f32 device");
+  TORCH_CHECK(0 <= lo && lo <= hi && hi <= dst.numel() && lo % 4 == 0, "range [lo, hi) of dst, lo % 4 == 0");
+  PubPtrs p = ptrs_of(ptrs, npub);
+  for (int64_t k = 0; k < npub; ++k)
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(p.p[k]) % 16 == 0, "publish pointers must be 16-byte aligned");
+  if (hi == lo) return;
+  const int64_t n = hi - lo;
+  auto stream = c10::hip::getCurrentHIPStream();
   static const int grid_div = [] {  // lanes per 16 elements: fewer workgroups, fewer fences
     const char* e = std::getenv("HIPPS_PULL_GRID_DIV");
     return e ? std::max(1, std::atoi(e)) : 16;
   }();
   const int grid = grid_for((n >> 2) / grid_div + 1);
-  const uint8_t* src = pub.data_ptr<uint8_t>() + lo * esz;
   uint16_t* sh = shadow_of(shadow, dst);
   if (sh != nullptr) sh += lo;
   if (bf16)
-    hipLaunchKernelGGL(k_pull_copy<uint16_t>, grid, kBlock, 0, stream, sel.data_ptr<int64_t>(), src, stride, (int)npub,
-                       dst.data_ptr<float>() + lo, n, fence_mode, sh);
+    hipLaunchKernelGGL(k_pull_copy<uint16_t>, grid, kBlock, 0, stream, sel.data_ptr<int64_t>(), p, (int)npub,
+                       dst.data_ptr<float>() + lo, n, pull_fence_mode(), sh);
   else
-    hipLaunchKernelGGL(k_pull_copy<float>, grid, kBlock, 0, stream, sel.data_ptr<int64_t>(), src, stride, (int)npub,
-                       dst.data_ptr<float>() + lo, n, fence_mode, sh);
+    hipLaunchKernelGGL(k_pull_copy<float>, grid, kBlock, 0, stream, sel.data_ptr<int64_t>(), p, (int)npub,
+                       dst.data_ptr<float>() + lo, n, pull_fence_mode(), sh);
+}
+
+// one-allocation form: buffers 0 .. npub-1 of `pub` (uint8), `stride` bytes apart
+void pull_copy(at::Tensor sel, at::Tensor pub, int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t lo,
+               int64_t hi, c10::optional<at::Tensor> shadow) {
+  TORCH_CHECK(pub.is_cuda() && pub.scalar_type() == at::kByte, "pub must be a uint8 device view");
+  const int64_t esz = bf16 ? 2 : 4;
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(pub.data_ptr()) % 16 == 0 && stride % 16 == 0, "pub must be 16B aligned");
+  TORCH_CHECK(npub >= 1 && pub.numel() >= (npub - 1) * stride + dst.numel() * esz, "publish view too small");
+  std::vector<int64_t> ptrs;
+  for (int64_t k = 0; k < npub; ++k)
+    ptrs.push_back(reinterpret_cast<int64_t>(pub.data_ptr<uint8_t>() + k * stride + lo * esz));
+  pull_copy_ptrs(sel, ptrs, npub, bf16, dst, lo, hi, shadow);
 }
 
 void pull_done(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, int64_t ring_slot) {
@@ -295,29 +328,37 @@ void pull_select_b(at::Tensor selb, int64_t bpub, int64_t bbuf, int64_t reading_
                      (int)npub, (int)tries);
 }
 
-void pull_copy_b(at::Tensor selb, at::Tensor boff, at::Tensor pub, int64_t stride, int64_t npub, bool bf16,
-                 at::Tensor dst, int64_t lo, int64_t hi, c10::optional<at::Tensor> shadow) {
+// bucket granularity: dst[lo, hi) per bucket from that bucket's selected buffer; ptrs[k]: device
+// address such that element i (absolute, lo <= i < hi) of buffer k is at ptrs[k] + i * esz
+void pull_copy_b_ptrs(at::Tensor selb, at::Tensor boff, std::vector<int64_t> ptrs, int64_t npub, bool bf16,
+                      at::Tensor dst, int64_t lo, int64_t hi, c10::optional<at::Tensor> shadow) {
   TORCH_CHECK(selb.is_cuda() && selb.scalar_type() == at::kLong && selb.is_contiguous(), "selb must be int64 device");
   const int64_t nb = selb.numel() / 2;
   TORCH_CHECK(boff.is_cuda() && boff.scalar_type() == at::kLong && boff.numel() == nb + 1, "boff: int64 [nb + 1]");
-  TORCH_CHECK(pub.is_cuda() && pub.scalar_type() == at::kByte, "pub must be a uint8 device view");
   TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kFloat && dst.is_contiguous(), "dst must be f32 device");
-  const int64_t esz = bf16 ? 2 : 4;
   TORCH_CHECK(0 <= lo && lo <= hi && hi <= dst.numel(), "range [lo, hi) of dst");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(pub.data_ptr()) % 16 == 0 && stride % 16 == 0, "pub must be 16B aligned");
-  TORCH_CHECK(npub >= 1 && pub.numel() >= (npub - 1) * stride + dst.numel() * esz, "publish view too small");
+  PubPtrs p = ptrs_of(ptrs, npub);
   if (hi == lo || nb == 0) return;
   const int gx = std::max(1, std::min(grid_for(((hi - lo) >> 2) / 16 + 1), (int)(4096 / nb) + 1));
   auto stream = c10::hip::getCurrentHIPStream();
   uint16_t* sh = shadow_of(shadow, dst);
   if (bf16)
     hipLaunchKernelGGL(k_pull_copy_b<uint16_t>, dim3(gx, nb), kBlock, 0, stream, selb.data_ptr<int64_t>(),
-                       boff.data_ptr<int64_t>(), pub.data_ptr<uint8_t>(), stride, (int)npub, dst.data_ptr<float>(), lo,
-                       hi, 1, sh);
+                       boff.data_ptr<int64_t>(), p, (int)npub, dst.data_ptr<float>(), lo, hi, 1, sh);
   else
     hipLaunchKernelGGL(k_pull_copy_b<float>, dim3(gx, nb), kBlock, 0, stream, selb.data_ptr<int64_t>(),
-                       boff.data_ptr<int64_t>(), pub.data_ptr<uint8_t>(), stride, (int)npub, dst.data_ptr<float>(), lo,
-                       hi, 1, sh);
+                       boff.data_ptr<int64_t>(), p, (int)npub, dst.data_ptr<float>(), lo, hi, 1, sh);
+}
+
+void pull_copy_b(at::Tensor selb, at::Tensor boff, at::Tensor pub, int64_t stride, int64_t npub, bool bf16,
+                 at::Tensor dst, int64_t lo, int64_t hi, c10::optional<at::Tensor> shadow) {
+  TORCH_CHECK(pub.is_cuda() && pub.scalar_type() == at::kByte, "pub must be a uint8 device view");
+  const int64_t esz = bf16 ? 2 : 4;
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(pub.data_ptr()) % 16 == 0 && stride % 16 == 0, "pub must be 16B aligned");
+  TORCH_CHECK(npub >= 1 && pub.numel() >= (npub - 1) * stride + dst.numel() * esz, "publish view too small");
+  std::vector<int64_t> ptrs;
+  for (int64_t k = 0; k < npub; ++k) ptrs.push_back(reinterpret_cast<int64_t>(pub.data_ptr<uint8_t>() + k * stride));
+  pull_copy_b_ptrs(selb, boff, ptrs, npub, bf16, dst, lo, hi, shadow);
 }
 
 void pull_done_b(at::Tensor selb, int64_t bpub, int64_t bbuf, int64_t reading_b, int64_t applied, at::Tensor sel,

@@ -198,9 +198,11 @@ class MPI_PS(torch.optim.Optimizer):
 
     def _update_range(self, sources: List[torch.Tensor], target: torch.Tensor, lo: int, hi: int, gscale: float,
                       zero_src: bool = False, pub: Optional[torch.Tensor] = None,
-                      mask: Optional[torch.Tensor] = None, src_lo: int = 0, lookahead: float = 0.0):
-        """Update flat elements [lo, hi) (16-aligned).  ``target``/``pub``/``mask`` index the whole
-        flat space; ``sources`` start at flat element ``src_lo`` (e.g. one bucket's images)."""
+                      mask: Optional[torch.Tensor] = None, src_lo: int = 0, lookahead: float = 0.0,
+                      pub_lo: int = 0):
+        """Update flat elements [lo, hi) (16-aligned).  ``target``/``mask`` index the whole flat
+        space; ``sources`` start at flat element ``src_lo`` (e.g. one bucket's images), ``pub`` at
+        ``pub_lo`` (one chunk of a publish buffer split over several IPC allocations)."""
         for gi, group in enumerate(self.param_groups):
             a, b = self.store.group_ranges[gi]
             a, b = max(a, lo), min(b, hi)
@@ -208,7 +210,7 @@ class MPI_PS(torch.optim.Optimizer):
                 continue
             cs = self._csteps()
             self._update_group(gi, group, [s[a - src_lo:b - src_lo] for s in sources], target[a:b], gscale,
-                               zero_src, None if pub is None else pub[a:b],
+                               zero_src, None if pub is None else pub[a - pub_lo:b - pub_lo],
                                None if mask is None else mask[a // 16:b // 16], a, b,
                                None if cs is None else cs[a // 16:b // 16], lookahead)
 

@@ -554,20 +554,8 @@ class PSAsyncEngine(Engine):
             else:
                 self._gpg = _TorchChannel(W)
                 self._ppg = _TorchChannel(W)
-        # mailbox allocations on a GPU: 'vmm' (hipMemCreate chunks exported as fds, mapped back to
-        # back: no single import larger than one chunk) or 'ipc' (one hipMalloc per region,
-        # hipIpcOpenMemHandle); HIPPS_IPC_ALLOC selects, HIPPS_VMM_CHUNK_MB sizes the chunks
-        # 'auto': hipIpcOpenMemHandle of one allocation of 2 GiB never returned on the rehearsal box
-        # (its thread spinning in user space; 4 x 512 MB allocations imported in 1 ms,
-        # profiles/r5/ipc), so regions from 1 GiB up take the VMM path
-        self.ipc_alloc = os.environ.get("HIPPS_IPC_ALLOC", "auto")
-        if self.ipc_alloc == "auto":
-            big = max(self.ring_bytes, self.NPUB * self.pub_bytes) >= (1 << 30)
-            self.ipc_alloc = "vmm" if big else "ipc"
-        if self.ipc_alloc == "vmm" and not hasattr(C, "VmmRegion"):
-            self.ipc_alloc = "ipc"
-        self.vmm_chunk = int(float(os.environ.get("HIPPS_VMM_CHUNK_MB", "512")) * (1 << 20))
         self._rendezvous(C, W, store)
+        self.slot_bytes = self.ring_bytes  # (chunk rounding may have grown it)
         # GPU-rung doorbells need the control block registered with HIP in this process
         self.device_bells = bool(self.cuda and self.ctl.enable_device_doorbells())
         self.pull_mode = cfg.pull
@@ -761,48 +749,100 @@ class PSAsyncEngine(Engine):
                 "a smaller mailbox (mailbox_mb / mailbox_slots / bucket_mb), param_wire='bf16', or fewer workers "
                 "per PS.  HIPPS_SKIP_BUDGET=1 skips this check.")
 
+    def _chunking(self, store, esz: int):
+        """Split the mailbox into IPC allocations below 2 GiB: hipIpcOpenMemHandle of ONE 2 GiB
+        allocation never returned on the rehearsal box (its thread spinning in user space), while
+        16 x 512 MB allocations imported in 3 ms with their contents verified
+        (profiles/r5/ipc).  A worker's ring becomes nrc chunks that each hold the largest message
+        (a message never straddles two); every publish buffer becomes npc chunks of pub_chunk
+        elements (256-aligned).  HIPPS_IPC_CHUNK_MB caps a chunk (1024); p2p / CPU: one chunk."""
+        env = os.environ.get("HIPPS_IPC_CHUNK_MB")
+        chunked = not self.p2p and (self.cuda or env is not None)  # (CPU: only when asked, for tests)
+        cap = int(float(env or "1024") * (1 << 20)) if chunked else 1 << 62
+        max_ext = max(self.msg_ext) + _align(self.pres_bytes)
+        nrc = max(1, -(-self.ring_bytes // cap))
+        self.ring_chunk = max(_align(-(-self.ring_bytes // nrc)), _align(max_ext))
+        if self.cuda and chunked and self.ring_chunk >= (2 << 30) - (16 << 20):
+            raise ValueError(f"ps_async: a {max_ext >> 20} MB bucket message does not fit one IPC allocation below "
+                             "2 GiB; use a smaller bucket_mb or async_transport='p2p'")
+        self.nrc = nrc
+        self.ring_bytes = nrc * self.ring_chunk
+        n = store.numel
+        self.pub_chunk = n if n * esz <= cap else max(256, (cap // esz) // 256 * 256)
+        self.npc = -(-n // self.pub_chunk)
+
+    def _pub_chunk_len(self, c: int) -> int:
+        return min(self.pub_chunk, self.store.numel - c * self.pub_chunk)
+
+    def _pub_pieces(self, lo: int, hi: int):
+        """(chunk, a, b): [lo, hi) split at publish-chunk boundaries (multiples of 256)."""
+        P = self.pub_chunk
+        a = lo
+        while a < hi:
+            c = a // P
+            b = min(hi, (c + 1) * P)
+            yield c, a, b
+            a = b
+
+    def pub_view(self, k: int, a: int, b: int) -> torch.Tensor:
+        """Elements [a, b) of publish buffer k (inside one chunk)."""
+        c = a // self.pub_chunk
+        o = c * self.pub_chunk
+        assert b - o <= self._pub_chunk_len(c), "range straddles publish chunks"
+        return self.pub_chunks[k][c][a - o:b - o]
+
+    def _pub_ptrs(self, c: int, lo: int, absolute: bool):
+        """Device address per publish buffer for a pull over chunk c: of element ``lo`` (relative
+        kernel), or the chunk's virtual base so that element i sits at base + i * esz."""
+        esz = torch.empty((), dtype=self.pub_dtype).element_size()
+        o = c * self.pub_chunk
+        return [self.pub_chunks[k][c].data_ptr() + ((-o) if absolute else (lo - o)) * esz for k in range(self.NPUB)]
+
     def _rendezvous(self, C, W: int, store):
-        """Rank 0 creates the control block, one ring allocation per worker and the publish
-        region; worker i imports ONLY its own ring and the publish region (no
-        two importers open the same allocation except the publish region), one rank at a time
-        (rank i waits for rank i-1's OPEN_TURN word), every open bounded with a diagnostic.  Every
-        rank then agrees on the outcome before anybody waits in a barrier."""
-        self.rings: List[Optional[torch.Tensor]] = [None] * W  # rank 0: every ring; worker i: its own
-        self.pub_mem: Optional[torch.Tensor] = None
+        """Rank 0 creates the control block, each worker's ring and the publish buffers (as IPC
+        allocations below 2 GiB, :meth:`_chunking`); worker i imports ONLY its own ring and the
+        publish buffers (no two importers open the same allocation except the
+        publish region), one rank at a time (rank i waits for rank i-1's OPEN_TURN word), every
+        open bounded with a diagnostic.  Every rank then agrees on the outcome before anybody waits
+        in a barrier."""
+        esz = torch.empty((), dtype=self.pub_dtype).element_size()
+        self._chunking(store, esz)
+        # rank 0: every worker's ring; worker i: its own -- a list of chunk tensors (uint8)
+        self.rings: List[Optional[List[torch.Tensor]]] = [None] * W
+        self.pub_chunks: List[List[torch.Tensor]] = []  # [NPUB][npc] views in the publish dtype
         self._mbs: list = []  # mailbox objects this rank holds (rank 0 owns, workers import)
         self.mapped_bytes = 0
         self.open_s = 0.0
-        pub_total = self.NPUB * self.pub_bytes
+        pcb = [_align(self._pub_chunk_len(c) * esz) for c in range(self.npc)]  # publish chunk bytes
         token = secrets.token_hex(6) if self.rank == 0 else None
         handles = None
+
+        def as_pub(t, c):
+            return t[:self._pub_chunk_len(c) * esz].view(self.pub_dtype)
+
         if self.rank == 0:
             self.ctl_name = f"/hipps_ctl_{os.getpid()}_{token}"
             self.mb_name = f"/hipps_mb_{os.getpid()}_{token}"
             self.ctl = C.ControlBlock(self.ctl_name, W, True)
             if self.p2p:
-                self.rings = [torch.zeros(self.ring_bytes, dtype=torch.uint8, device=store.device) for _ in range(W)]
-                self.pub_mem = torch.zeros(pub_total, dtype=torch.uint8, device=store.device)
+                z = dict(dtype=torch.uint8, device=store.device)
+                self.rings = [[torch.zeros(self.ring_chunk, **z) for _ in range(self.nrc)] for _ in range(W)]
+                self.pub_chunks = [[as_pub(torch.zeros(pcb[c], **z), c) for c in range(self.npc)]
+                                   for _ in range(self.NPUB)]
             else:
-                if self.cuda and self.ipc_alloc == "vmm":
-                    # hipMemCreate chunks mapped contiguously; their fds go to each worker over a
-                    # Unix socket (SCM_RIGHTS) when its import turn comes (_serve_fds)
-                    ch = self.vmm_chunk
-                    mbs = [C.VmmRegion(self.ring_bytes, ch) for _ in range(W)] + [C.VmmRegion(pub_total, ch)]
-                    fd_name = f"hipps_fd_{os.getpid()}_{token}"
-                    self._fdsrv = C.FdServer(fd_name)
-                    handles = {"vmm": fd_name, "ring_sizes": mbs[0].chunk_sizes(), "pub_sizes": mbs[W].chunk_sizes()}
-                    self._fd_thread = threading.Thread(target=self._serve_fds, args=(mbs,), name="hipps-fds",
-                                                       daemon=True)
-                    self._fd_thread.start()
-                elif self.cuda:
-                    mbs = [C.DeviceMailbox(self.ring_bytes) for _ in range(W)] + [C.DeviceMailbox(pub_total)]
-                    handles = [m.handle() for m in mbs]
+                if self.cuda:
+                    rmb = [[C.DeviceMailbox(self.ring_chunk) for _ in range(self.nrc)] for _ in range(W)]
+                    pmb = [[C.DeviceMailbox(pcb[c]) for c in range(self.npc)] for _ in range(self.NPUB)]
+                    handles = {"ring": [[m.handle() for m in r] for r in rmb],
+                               "pub": [[m.handle() for m in q] for q in pmb]}
                 else:
-                    mbs = [C.HostMailbox(f"{self.mb_name}_{i}", self.ring_bytes, True) for i in range(W)]
-                    mbs.append(C.HostMailbox(f"{self.mb_name}_pub", pub_total, True))
-                self._mbs = mbs
-                self.rings = [m.tensor() for m in mbs[:W]]
-                self.pub_mem = mbs[W].tensor()
+                    rmb = [[C.HostMailbox(f"{self.mb_name}_{i}_{c}", self.ring_chunk, True) for c in range(self.nrc)]
+                           for i in range(W)]
+                    pmb = [[C.HostMailbox(f"{self.mb_name}_p{k}_{c}", pcb[c], True) for c in range(self.npc)]
+                           for k in range(self.NPUB)]
+                self._mbs = [m for r in rmb for m in r] + [m for q in pmb for m in q]
+                self.rings = [[m.tensor() for m in r] for r in rmb]
+                self.pub_chunks = [[as_pub(m.tensor(), c) for c, m in enumerate(q)] for q in pmb]
         meta = [getattr(self, "ctl_name", None), getattr(self, "mb_name", None), handles]
         if W > 1:
             dist.broadcast_object_list(meta, src=0)
@@ -815,7 +855,7 @@ class PSAsyncEngine(Engine):
             except Exception as e:
                 map_err = f"rank {self.rank}: {type(e).__name__}: {e}"
             if map_err is None and not self.p2p:
-                map_err, timed_out = self._import_mailbox(C, W, handles, pub_total, store)
+                map_err, timed_out = self._import_mailbox(C, W, handles, pcb, store, as_pub)
         if W > 1:
             # agree before the barrier: a rank that cannot map must not leave the others waiting,
             # and every rank raises together.  A timed-out import leaves a thread inside the HIP
@@ -828,7 +868,6 @@ class PSAsyncEngine(Engine):
                 if self.rank == 0:
                     self.ctl.unlink()
                     self._unlink_host()
-                    self._stop_fds()
                 msg = "ps_async ipc transport: mapping the PS mailbox failed (" + "; ".join(bad) + ")"
                 if any(t for _, t in errs):
                     raise IPCOpenTimeout(msg)
@@ -837,29 +876,6 @@ class PSAsyncEngine(Engine):
         if self.rank == 0:  # everyone has mapped: remove the names (no /dev/shm leftovers)
             self.ctl.unlink()
             self._unlink_host()
-            self._stop_fds()
-
-    def _serve_fds(self, mbs):
-        """Rank 0, VMM mailboxes: hand worker i the fds of the publish region's and its ring's
-        chunks when it connects (workers connect in import-turn order); stop when a turn fails."""
-        W, C = self.W, self.C
-        try:
-            for i in range(1, W):
-                while True:
-                    if self.ctl.load(C.F_OPEN_TURN, 0) >= (1 << 40) or getattr(self, "_fds_stop", False):
-                        return
-                    if self._fdsrv.send_one(mbs[W].export_fds() + mbs[i].export_fds(), 500):
-                        break
-        except Exception as e:  # reported by the worker that waits for these fds
-            self._fds_err = f"{type(e).__name__}: {e}"
-
-    def _stop_fds(self):
-        t = getattr(self, "_fd_thread", None)
-        if t is not None:
-            self._fds_stop = True
-            t.join(timeout=5)
-            self._fdsrv.close()
-            self._fd_thread = None
 
     def _unlink_host(self):
         if not self.cuda:
@@ -869,54 +885,56 @@ class PSAsyncEngine(Engine):
                 except Exception:
                     pass
 
-    def _import_mailbox(self, C, W: int, handles, pub_total: int, store):
+    def _import_mailbox(self, C, W: int, handles, pcb, store, as_pub):
         """Worker side of :meth:`_rendezvous`: wait for this rank's turn, import the publish
-        region and this worker's ring (each bounded), report the turn done.  Returns (error or
-        None, timed out)."""
+        buffers' chunks and this worker's ring chunks (each bounded), report the turn done.
+        Returns (error or None, timed out)."""
         limit = float(os.environ.get("HIPPS_IPC_OPEN_TIMEOUT_S", "60"))
-        # every earlier rank may use its full limit for two opens
-        if not self.ctl.wait_ge(C.F_OPEN_TURN, 0, self.rank - 1, int((2 * limit * (self.rank - 1) + 30) * 1e6)):
+        nimp = self.NPUB * self.npc + self.nrc
+        # every earlier rank may use its full limit for each of its opens
+        if not self.ctl.wait_ge(C.F_OPEN_TURN, 0, self.rank - 1, int((nimp * limit * (self.rank - 1) + 30) * 1e6)):
             return f"rank {self.rank}: rank {self.rank - 1} never finished its mailbox import", False
         if self.ctl.load(C.F_OPEN_TURN, 0) >= (1 << 40):  # an earlier rank failed: do not pile on
             return None, False
-        nm = f"{self.mb_name}_{self.rank}"
+        t0 = time.perf_counter()
+        pub = [[None] * self.npc for _ in range(self.NPUB)]
+        ring = [None] * self.nrc
         try:
-            if self.cuda and isinstance(handles, dict):  # VMM chunks: fds over the rank-0 socket
-                t0 = time.perf_counter()
-                fds = C.fd_recv(handles["vmm"], int(limit * 1000))
-                npc = len(handles["pub_sizes"])
-                pub, t1 = _bounded_open(lambda: C.VmmRegion(fds[:npc], handles["pub_sizes"], pub_total),
-                                        f"the publish region ({pub_total >> 20} MB, {npc} chunks)", self.rank,
-                                        store.device, limit)
-                self._mbs.append(pub)
-                ring, t2 = _bounded_open(lambda: C.VmmRegion(fds[npc:], handles["ring_sizes"], self.ring_bytes),
-                                         f"its mailbox ring ({self.ring_bytes >> 20} MB)", self.rank, store.device,
-                                         limit)
-                t1 = time.perf_counter() - t0 - t2  # (the fd hand-over counts as the first import)
-            elif self.cuda:
-                pub, t1 = _bounded_open(lambda: C.DeviceMailbox(handles[W], pub_total), f"the publish region "
-                                        f"({pub_total >> 20} MB)", self.rank, store.device, limit)
-                self._mbs.append(pub)
-                ring, t2 = _bounded_open(lambda: C.DeviceMailbox(handles[self.rank], self.ring_bytes),
-                                         f"its mailbox ring ({self.ring_bytes >> 20} MB)", self.rank, store.device,
-                                         limit)
-            else:
-                pub, t1 = _bounded_open(lambda: C.HostMailbox(f"{self.mb_name}_pub", pub_total, False),
-                                        "the publish region", self.rank, None, limit)
-                self._mbs.append(pub)
-                ring, t2 = _bounded_open(lambda: C.HostMailbox(nm, self.ring_bytes, False), "its mailbox ring",
-                                         self.rank, None, limit)
-            self._mbs.append(ring)
+            for k in range(self.NPUB):
+                for c in range(self.npc):
+                    what = f"publish buffer {k} chunk {c} ({pcb[c] >> 20} MB)"
+                    if self.cuda:
+                        h = handles["pub"][k][c]
+                        m, _ = _bounded_open(lambda h=h, n=pcb[c]: C.DeviceMailbox(h, n), what, self.rank,
+                                             store.device, limit)
+                    else:
+                        nm = f"{self.mb_name}_p{k}_{c}"
+                        m, _ = _bounded_open(lambda nm=nm, n=pcb[c]: C.HostMailbox(nm, n, False), what, self.rank,
+                                             None, limit)
+                    self._mbs.append(m)
+                    pub[k][c] = as_pub(m.tensor(), c)
+            for c in range(self.nrc):
+                what = f"its mailbox ring chunk {c} ({self.ring_chunk >> 20} MB)"
+                if self.cuda:
+                    h = handles["ring"][self.rank][c]
+                    m, _ = _bounded_open(lambda h=h: C.DeviceMailbox(h, self.ring_chunk), what, self.rank,
+                                         store.device, limit)
+                else:
+                    nm = f"{self.mb_name}_{self.rank}_{c}"
+                    m, _ = _bounded_open(lambda nm=nm: C.HostMailbox(nm, self.ring_chunk, False), what, self.rank,
+                                         None, limit)
+                self._mbs.append(m)
+                ring[c] = m.tensor()
         except IPCOpenTimeout as e:
             self.ctl.store(C.F_OPEN_TURN, 0, 1 << 40)
             return str(e), True
         except Exception as e:  # e.g. hipIpcOpenMemHandle refused across devices
             self.ctl.store(C.F_OPEN_TURN, 0, 1 << 40)
             return f"rank {self.rank}: {type(e).__name__}: {e}", False
-        self.pub_mem = pub.tensor()
-        self.rings[self.rank] = ring.tensor()
-        self.mapped_bytes = pub_total + self.ring_bytes
-        self.open_s = t1 + t2
+        self.pub_chunks = pub
+        self.rings[self.rank] = ring
+        self.mapped_bytes = self.NPUB * sum(pcb) + self.nrc * self.ring_chunk
+        self.open_s = time.perf_counter() - t0
         self.ctl.store(C.F_OPEN_TURN, 0, self.rank)
         return None, False
 
@@ -942,7 +960,7 @@ class PSAsyncEngine(Engine):
             for r in range(W):
                 got = self._ring_read(r, 0, 16).cpu()
                 ok &= bool((got == (r * 7 + 3) % 251).all())
-            ck = float(self.pub_buf(0).double().sum())  # what workers actually receive
+            ck = self._pub_sum(0)  # what workers actually receive
         else:
             ck = None
         mine = float(self.store.data.double().sum())
@@ -987,7 +1005,8 @@ class PSAsyncEngine(Engine):
 
     # ------------------------------------------------------------------ memory views
     def _ring_buf(self, rank: int, off: int, nbytes: int) -> torch.Tensor:
-        return self.rings[rank][off:off + nbytes]
+        c, o = divmod(off, self.ring_chunk)
+        return self.rings[rank][c][o:o + nbytes]
 
     def _msg_of(self, rank: int, slot: int):
         """(bucket, ring offset, carries presence) of worker ``rank``'s message in word slot
@@ -1026,9 +1045,14 @@ class PSAsyncEngine(Engine):
             raise RuntimeError(f"mailbox canary overwritten: worker {rank} message {seq} (bucket {bi})")
 
     def pub_buf(self, b: int) -> torch.Tensor:
-        o = b * self.pub_bytes
-        esz = torch.empty((), dtype=self.pub_dtype).element_size()
-        return self.pub_mem[o:o + self.store.numel * esz].view(self.pub_dtype)
+        """The whole publish buffer b as one tensor (one chunk: p2p, CPU, models below the
+        chunk cap); chunked buffers are read and written piecewise (pub_view / _pub_pieces)."""
+        if self.npc != 1:
+            raise RuntimeError("publish buffer spans several IPC allocations: use pub_view per chunk")
+        return self.pub_chunks[b][0]
+
+    def _pub_sum(self, k: int) -> float:
+        return float(sum(self.pub_view(k, a, b).double().sum() for _, a, b in self._pub_pieces(0, self.store.numel)))
 
     # ------------------------------------------------------------------ PS side
     def _ring(self, stream, words, srcs=None):
@@ -1041,8 +1065,8 @@ class PSAsyncEngine(Engine):
 
     def _publish_initial(self):
         C = self.C
-        pub = self.pub_buf(0)
-        ops.convert(self.master, pub)
+        for _, a, b in self._pub_pieces(0, self.store.numel):
+            ops.convert(self.master[a:b], self.pub_view(0, a, b))
         if self.cuda:
             torch.cuda.current_stream(self.store.device).synchronize()
         self.ctl.store(C.F_BUF_VER, 0, 0)
@@ -1094,6 +1118,10 @@ class PSAsyncEngine(Engine):
                 and getattr(self.opt, "optim", None) in ("sgd", "adam") and not self.is_object
                 and float(os.environ.get("HIPPS_PS_LOOP_DELAY_US", "0")) == 0):
             return None
+        return self.C.NativePS(self.ctl, self._native_config(cfg, kind))
+
+    def _native_config(self, cfg, kind) -> dict:
+        """Everything the native loop needs, as one dict (psloop.cpp NativePS)."""
         opt, store = self.opt, self.store
         adam = opt.optim == "adam"
         groups = []
@@ -1121,15 +1149,18 @@ class PSAsyncEngine(Engine):
              "M": self.M, "staleness": int(cfg.staleness), "staleness_lr": bool(cfg.staleness_lr),
              "gscale": float(self.core.gscale), "npub": self.NPUB, "dead_after_us": int(cfg.dead_after_s * 1e6),
              "skip_missing": bool(cfg.skip_missing_grads), "nslots": len(store.slots),
-             "device": int(store.device.index or 0), "stream": int(self.ps_stream.cuda_stream),
-             "direct_ok": bool(self._direct_ok), "acc": self.acc, "master": self.master, "pub": self.pub_mem,
-             "pub_bytes": int(self.pub_bytes), "pub_dtype": _DTYPE_CODE[self.pub_dtype],
-             "rings": list(self.rings), "remote": [self._remote(i) for i in range(self.W)],
+             "device": int(store.device.index or 0),
+             "stream": int(self.ps_stream.cuda_stream) if self.ps_stream is not None else 0,
+             "direct_ok": bool(self._direct_ok), "acc": self.acc, "master": self.master,
+             "pub_chunks": [list(q) for q in self.pub_chunks], "pub_chunk": int(self.pub_chunk),
+             "pub_dtype": _DTYPE_CODE[self.pub_dtype],
+             "rings": [list(r) for r in self.rings], "ring_chunk": int(self.ring_chunk),
+             "remote": [self._remote(i) for i in range(self.W)],
              "buckets": buckets, "groups": groups, "chunk_slots": store.chunk_slots(), **st}
         if self.emu:
             d.update(emu=int(self.emu), emu_in=self._emu_in, emu_sink=self._emu_sink,
                      emu_stream=int(self._emu_stream.cuda_stream))
-        return self.C.NativePS(self.ctl, d)
+        return d
 
     def _push_hyper(self):
         """The optimizer's current hyper-parameters into the native loop (schedulers edit
@@ -1398,14 +1429,17 @@ class PSAsyncEngine(Engine):
         self._stats["lookahead_tau_x1000"] = int(round(tau * 1000))
         direct = self._direct.pop(bi, None)
         with self.tracer.phase("ps_update", self.ps_stream):
-            if direct is not None:  # straight from the mailbox slot (M = 1)
-                msg, scale, (wi, ws) = direct
-                self.opt._update_range([msg], self.master, b.lo, b.hi, gscale * scale, False, self.pub_buf(k), mask,
-                                       b.lo, lookahead=tau)
+            for _, pa, pb in self._pub_pieces(b.lo, b.hi):  # (one piece unless the bucket straddles chunks)
+                if direct is not None:  # straight from the mailbox slot (M = 1)
+                    msg, scale, _ = direct
+                    self.opt._update_range([msg], self.master, pa, pb, gscale * scale, False, self.pub_view(k, pa, pb),
+                                           mask, b.lo, lookahead=tau, pub_lo=pa)
+                else:
+                    self.opt._update_range([self.acc], self.master, pa, pb, gscale, True, self.pub_view(k, pa, pb),
+                                           mask, 0, lookahead=tau, pub_lo=pa)
+            if direct is not None:
+                _, _, (wi, ws) = direct
                 self._stats["direct_updates"] = self._stats.get("direct_updates", 0) + 1
-            else:
-                self.opt._update_range([self.acc], self.master, b.lo, b.hi, gscale, True, self.pub_buf(k), mask, 0,
-                                       lookahead=tau)
         words = [(C.F_BBUF_VER, idx, v), (C.F_BPUB_VER, bi, v)]
         if direct is not None:
             words.insert(0, (C.F_ACK_SEQ, wi, ws))  # the slot is free once the update has read it
@@ -1469,8 +1503,10 @@ class PSAsyncEngine(Engine):
         tau = self.lookahead_tau()
         self._stats["lookahead_tau_x1000"] = int(round(tau * 1000))
         with self.tracer.phase("ps_update", self.ps_stream):
-            self.opt._update_flat([self.acc], self.master, gscale, zero_src=True, pub=self.pub_buf(b), mask=mask,
-                                  lookahead=tau)
+            self.opt._begin_update()
+            for _, pa, pb in self._pub_pieces(0, self.store.numel):
+                self.opt._update_range([self.acc], self.master, pa, pb, gscale, True, self.pub_view(b, pa, pb), mask,
+                                       lookahead=tau, pub_lo=pa)
         st = self.ps_stream
         # order matters: buffer stamp -> version word -> per-worker "included" words, so a worker
         # that sees its message included also sees a version containing it
@@ -1494,13 +1530,14 @@ class PSAsyncEngine(Engine):
         if st is not None:
             st.wait_stream(self.ps_stream)
         with ctx:
-            pub, win = self.pub_buf(b), self._emu_in
+            lo, hi, win = 0, self.store.numel, self._emu_in
             if bi is not None:
                 bk = self.plan.buckets[bi]
-                pub, win = pub[bk.lo:bk.hi], self.plan.message(self._emu_in, bi)
+                lo, hi, win = bk.lo, bk.hi, self.plan.message(self._emu_in, bi)
             for e in range(self.emu):
                 win.fill_(e)
-                torch.amax(pub, dim=0, out=self._emu_sink[e])
+                for _, pa, pb in self._pub_pieces(lo, hi):
+                    torch.amax(self.pub_view(b, pa, pb), dim=0, out=self._emu_sink[e])
 
     def lookahead_tau(self) -> float:
         """Updates to extrapolate the published parameters by (cfg.stale_lookahead): readers'
@@ -1738,6 +1775,9 @@ class PSAsyncEngine(Engine):
         seconds waited)."""
         C = self.C
         off = self._ring_off
+        rc = self.ring_chunk
+        if off // rc != (off + nbytes - 1) // rc:  # a message never straddles two ring allocations
+            off = (off // rc + 1) * rc
         if off + nbytes > self.ring_bytes:
             off = 0
         need = 0
@@ -1872,12 +1912,21 @@ class PSAsyncEngine(Engine):
                 ctl.device_addr(C.F_READING_B, self.rank * C.ControlBlock.MAX_BUCKETS),
                 ctl.device_addr(C.F_APPLIED_VER, self.rank))
 
+    def _copy_b(self, bf16: bool, lo: int, hi: int, sh):
+        """Bucket-granular pull copy of params [lo, hi), one launch per publish chunk."""
+        for c, a, b in self._pub_pieces(lo, hi):
+            self.C.pull_copy_b_ptrs(self._selb, self._boff, self._pub_ptrs(c, a, True), self.NPUB, bf16,
+                                    self.store.data, a, b, sh)
+
+    def _copy(self, bf16: bool, lo: int, hi: int, sh):
+        """Whole-model pull copy of params [lo, hi), one launch per publish chunk."""
+        for c, a, b in self._pub_pieces(lo, hi):
+            self.C.pull_copy_ptrs(self._sel, self._pub_ptrs(c, a, False), self.NPUB, bf16, self.store.data, a, b, sh)
+
     def _device_pull_b(self) -> bool:
         """GPU-time pull, bucket by bucket: each bucket's newest published version is chosen and
         copied when the GPU reaches the pull (pull.hip k_pull_*_b)."""
         C = self.C
-        esz = torch.empty((), dtype=self.pub_dtype).element_size()
-        base = self.pub_mem[:(self.NPUB - 1) * self.pub_bytes + self.store.numel * esz]
         words = self._bucket_words()
         bf16 = self.pub_dtype == torch.bfloat16
         ring = (self.step_no + 1) % RING
@@ -1885,7 +1934,7 @@ class PSAsyncEngine(Engine):
         C.pull_select_b(self._selb, *words, self.NPUB, 64)
         sh = self._pull_shadow()
         if self._split is None:
-            C.pull_copy_b(self._selb, self._boff, base, self.pub_bytes, self.NPUB, bf16, self.store.data, 0, n, sh)
+            self._copy_b(bf16, 0, n, sh)
             C.pull_done_b(self._selb, *words, self._sel, ring)
             if sh is not None:
                 self.store.refresh_shadow(cast=False)
@@ -1895,14 +1944,14 @@ class PSAsyncEngine(Engine):
         cs = torch.cuda.current_stream(dev)
         ev_sel = torch.cuda.Event()
         ev_sel.record(cs)
-        C.pull_copy_b(self._selb, self._boff, base, self.pub_bytes, self.NPUB, bf16, self.store.data, 0, s, sh)
+        self._copy_b(bf16, 0, s, sh)
         self.store.refresh_shadow(0, s, cast=sh is None)
         ev_early = torch.cuda.Event()
         ev_early.record(cs)
         side = self._late_stream
         with torch.cuda.stream(side):
             side.wait_event(ev_sel)
-            C.pull_copy_b(self._selb, self._boff, base, self.pub_bytes, self.NPUB, bf16, self.store.data, s, n, sh)
+            self._copy_b(bf16, s, n, sh)
             self.store.refresh_shadow(s, n, cast=sh is None)
             side.wait_event(ev_early)
             C.pull_done_b(self._selb, *words, self._sel, ring)
@@ -1928,12 +1977,13 @@ class PSAsyncEngine(Engine):
                 ridx = self.rank * MB + bi
                 self.ctl.store(C.F_READING_B, ridx, v)
                 if self.ctl.load(C.F_BBUF_VER, bi * self.NPUB + k) == v:
-                    src = self.pub_buf(k)[b.lo:b.hi]
-                    dst = self.store.data[b.lo:b.hi]
-                    if src.dtype == dst.dtype:
-                        dst.copy_(src, non_blocking=self.cuda)
-                    else:
-                        ops.convert(src if self.cuda else src.clone(), dst)
+                    for _, pa, pb in self._pub_pieces(b.lo, b.hi):
+                        src = self.pub_view(k, pa, pb)
+                        dst = self.store.data[pa:pb]
+                        if src.dtype == dst.dtype:
+                            dst.copy_(src, non_blocking=self.cuda)
+                        else:
+                            ops.convert(src if self.cuda else src.clone(), dst)
                     self._ring(stream, [(C.F_READING_B, ridx, -1)])
                     self._lver_b[bi] = v
                     got = True
@@ -1950,22 +2000,18 @@ class PSAsyncEngine(Engine):
 
     def _device_pull(self) -> bool:
         C = self.C
-        esz = torch.empty((), dtype=self.pub_dtype).element_size()
-        base = self.pub_mem[:(self.NPUB - 1) * self.pub_bytes + self.store.numel * esz]
         words = (self.ctl.device_addr(C.F_PUB_VER, 0), self.ctl.device_addr(C.F_BUF_VER, 0),
                  self.ctl.device_addr(C.F_READING, self.rank), self.ctl.device_addr(C.F_APPLIED_VER, self.rank))
         bf16 = self.pub_dtype == torch.bfloat16
         ring = (self.step_no + 1) % RING
         sh = self._pull_shadow()
         if self._split is None:
-            if sh is None:
-                self.C.pull_params(self._sel, *words, base, self.pub_bytes, self.NPUB, bf16, self.store.data, ring, 64)
-                return True
             self.C.pull_select(self._sel, *words, self.NPUB, 64)
-            self.C.pull_copy(self._sel, base, self.pub_bytes, self.NPUB, bf16, self.store.data, 0, self.store.numel, sh)
+            self._copy(bf16, 0, self.store.numel, sh)
             self.C.pull_done(self._sel, *words, ring)
-            self.store.refresh_shadow(cast=False)
-            self._shadow_done = True
+            if sh is not None:
+                self.store.refresh_shadow(cast=False)
+                self._shadow_done = True
             return True
         # pull_overlap: the early layers' range [0, split) on the compute stream, the late range on
         # a side stream that the late module's forward pre-hook waits for (set_pull_overlap)
@@ -1974,14 +2020,14 @@ class PSAsyncEngine(Engine):
         self.C.pull_select(self._sel, *words, self.NPUB, 64)
         ev_sel = torch.cuda.Event()
         ev_sel.record(cs)
-        self.C.pull_copy(self._sel, base, self.pub_bytes, self.NPUB, bf16, self.store.data, 0, s, sh)
+        self._copy(bf16, 0, s, sh)
         self.store.refresh_shadow(0, s, cast=sh is None)
         ev_early = torch.cuda.Event()
         ev_early.record(cs)
         side = self._late_stream
         with torch.cuda.stream(side):
             side.wait_event(ev_sel)
-            self.C.pull_copy(self._sel, base, self.pub_bytes, self.NPUB, bf16, self.store.data, s, n, sh)
+            self._copy(bf16, s, n, sh)
             self.store.refresh_shadow(s, n, cast=sh is None)
             side.wait_event(ev_early)  # the reader word is released after BOTH halves were read
             self.C.pull_done(self._sel, *words, ring)
@@ -2053,6 +2099,20 @@ class PSAsyncEngine(Engine):
         else:
             self.ctl.store(self.C.F_READING, self.rank, -1)
 
+    def _adopt_pub(self, k: int, v: int):
+        """Adopt publish buffer k (version v) piecewise, chunk by chunk."""
+        for _, a, b in self._pub_pieces(0, self.store.numel):
+            src = self.pub_view(k, a, b)
+            dst = self.store.data[a:b]
+            if src.dtype == dst.dtype:
+                dst.copy_(src, non_blocking=self.cuda)
+            else:
+                ops.convert(src if self.cuda else src.clone(), dst)
+        self.local_ver = v
+        if self.cuda:
+            self._sel[1:].fill_(v)
+        self.ctl.store(self.C.F_APPLIED_VER, self.rank, v)
+
     def _adopt(self, src, v):
         if src.dtype == self.store.data.dtype:
             self.store.data.copy_(src, non_blocking=self.cuda)
@@ -2069,12 +2129,8 @@ class PSAsyncEngine(Engine):
         if got is None:
             return False
         v, b = got
-        if self.cuda:
-            self._adopt(self.pub_buf(b), v)
-            self._release(torch.cuda.current_stream(self.store.device))
-        else:
-            self._adopt(self.pub_buf(b).clone(), v)
-            self._release(None)
+        self._adopt_pub(b, v)
+        self._release(torch.cuda.current_stream(self.store.device) if self.cuda else None)
         return True
 
     def _prefetch_pull(self) -> bool:
@@ -2103,7 +2159,8 @@ class PSAsyncEngine(Engine):
                 if self._stage_ev[k] is not None:
                     ps.wait_event(self._stage_ev[k])
                 with torch.cuda.stream(ps):
-                    self._stage[k].copy_(self.pub_buf(b), non_blocking=True)
+                    for _, pa, pb in self._pub_pieces(0, self.store.numel):
+                        self._stage[k][pa:pb].copy_(self.pub_view(b, pa, pb), non_blocking=True)
                 self._release(ps)
                 ev = torch.cuda.Event()
                 ev.record(ps)
@@ -2149,11 +2206,12 @@ class PSAsyncEngine(Engine):
                 "p2p_channels": (None if not self.p2p else "rccl-split" if self._gpg.native else "torch"),
                 "granularity": self.granularity,
                 "ps_dedicated": self.dedicated, "accumulate": self.M,
-                "npub": self.NPUB, "mapped_bytes": self.mapped_bytes, "ipc_alloc": self.ipc_alloc,
+                "npub": self.NPUB, "mapped_bytes": self.mapped_bytes,
                 "budget_gb": ({k: round(v / 1e9, 2) for k, v in self.budget.items() if k in ("ps_total", "worker_total",
                                                                                          "total", "limit")}
                               if self.budget else None),
                 "mailbox_slots": self.SLOTS, "slot_bytes": self.slot_bytes, "ring_bytes": self.ring_bytes,
+                "ring_chunks": self.nrc, "pub_chunks": self.npc,
                 "direct_push": self._direct_push}
 
     def close(self):
@@ -2260,7 +2318,8 @@ class PSAsyncEngine(Engine):
                     self.core.count = int(d.get("acc_count", 0))
                 self.ver = int(d["version"])
                 b = self.ver % self.NPUB
-                ops.convert(self.master, self.pub_buf(b))
+                for _, pa, pb in self._pub_pieces(0, self.store.numel):
+                    ops.convert(self.master[pa:pb], self.pub_view(b, pa, pb))
                 if self.cuda:
                     torch.cuda.current_stream(self.store.device).synchronize()
                 self.ctl.store(C.F_BUF_VER, b, self.ver)

@@ -215,3 +215,39 @@ def test_small_models_keep_the_full_geometry():
         model = resnet50()
     b = budget_for_shapes([tuple(p.shape) for p in model.parameters()], 8)
     assert b["npub"] == 4 and b["fits"] == 1
+
+
+def _chunked(rank, world, chunk_mb, gran):
+    import os
+
+    import hipps
+
+    if chunk_mb:
+        os.environ["HIPPS_IPC_CHUNK_MB"] = str(chunk_mb)
+    else:
+        os.environ.pop("HIPPS_IPC_CHUNK_MB", None)
+    m = _mlp()
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", bucket_mb=0.0005, max_delay=0,
+                    accumulate=world, ps_granularity=gran, mailbox_slots=3)
+    info = {"npc": opt.engine.npc, "nrc": opt.engine.nrc}
+    for s in range(6):
+        x, y = _data(0, s % 4)
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x), y).backward()
+        opt.step()
+    opt.close()
+    return {"info": info, "params": [p.detach().clone() for p in m.parameters()]}
+
+
+@pytest.mark.parametrize("gran", ["bucket", "model"])
+def test_chunked_mailbox_bitwise(gran):
+    """The mailbox as several allocations (publish buffers in 256-aligned chunks, rings whose
+    messages never straddle a chunk; what a multi-GB mailbox needs on the GPU) trains bit for bit
+    like one allocation per region."""
+    a = run_world(_chunked, 2, 0.25, gran, timeout=180)
+    b = run_world(_chunked, 2, 0, gran, timeout=180)
+    assert a[0]["info"]["npc"] >= 3 and a[0]["info"]["nrc"] >= 2, a[0]["info"]
+    assert b[0]["info"] == {"npc": 1, "nrc": 1}
+    for r in range(2):
+        for x, y in zip(a[r]["params"], b[r]["params"]):
+            torch.testing.assert_close(x, y, rtol=0, atol=0)

@@ -247,3 +247,27 @@ def test_gradient_hold_drain_frees_only_completed_steps():
     assert len(e._held) == Engine.HOLD_MAX
     release(force=True)
     assert not e._held and not e._drain
+
+
+def test_native_ps_config_parses_on_cpu():
+    """The native PS loop's configuration (every key psloop.cpp reads) is built and parsed for
+    every codec kind and both optimizers without a GPU: NativePS's constructor only reads it (the
+    loop itself runs on the GPU, tests/test_native_ps_gpu.py)."""
+    import hipps
+    from test_dist_cpu import _mlp
+
+    for cls, kw in ((hipps.SGD, dict(lr=0.1, momentum=0.9)), (hipps.Adam, dict(lr=1e-3, amsgrad=True))):
+        for code in ("fp32", "bf16", "int8", "topk:0.1", "topk_int8:0.1", "threshold:0.001:0.2"):
+            m = _mlp()
+            opt = cls(m.named_parameters(), mode="ps_async", code=code, bucket_mb=0.0005, ps_granularity="bucket", **kw)
+            eng = opt.engine
+            kind = eng._native_kind(eng.codec)
+            assert kind is not None, code
+            nat = eng.C.NativePS(eng.ctl, eng._native_config(eng.cfg, kind))
+            eng._native = nat  # hyper-parameters and counters round-trip through it
+            eng._push_hyper()
+            st = nat.state()
+            assert st["ver"] == 0 and len(st["ver_b"]) == len(eng.plan.buckets) and not nat.alive()
+            eng._native = None
+            del nat
+            opt.close()

@@ -82,12 +82,6 @@ for step in "$@"; do
         --repeat 2 --chunk-mb "${arg:-0}" > "$OUT/ipc_probe_c${arg:-0}.txt" 2>&1 \
         || fail ipcprobe "$OUT/ipc_probe_c${arg:-0}.txt"
       grep -v "amdgpu.ids\|socket.cpp" "$OUT/ipc_probe_c${arg:-0}.txt" | tail -12 ;;
-    ipcvmm|ipcvmm:*)  # ipcvmm[:chunk_mb] (0 = one chunk) -- the same regions as VmmRegion (POSIX fds)
-      HIPPS_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 3 \
-        --master-addr 127.0.0.1 --master-port 29657 tools/ipc_probe.py --vmm --sizes 256,1024,2048,4096,8192 \
-        --repeat 2 --chunk-mb "${arg:-0}" > "$OUT/ipc_vmm_c${arg:-0}.txt" 2>&1 \
-        || fail ipcvmm "$OUT/ipc_vmm_c${arg:-0}.txt"
-      grep -v "amdgpu.ids\|socket.cpp" "$OUT/ipc_vmm_c${arg:-0}.txt" | tail -14 ;;
     ipclog)  # one importer with AMD_LOG_LEVEL=4 on 4 and 8 GB regions (runtime log of a slow import)
       AMD_LOG_LEVEL=4 HIPPS_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
         --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29656 tools/ipc_probe.py --sizes 4096,8192 \

@@ -1,8 +1,9 @@
 """How long does importing a PS mailbox take, and where does a stuck import sit?
 
 Rank 0 allocates a DeviceMailbox of each size (or, with --chunk-mb, the same bytes as several
-allocations) and exports it; every other rank imports it with hipIpcOpenMemHandle (dmabuf IPC),
-one rank at a time, each import bounded (hipps.parallel.ps_async._bounded_open).  A timed-out
+allocations), stamps each allocation, and exports it; every other rank imports it with
+hipIpcOpenMemHandle (dmabuf IPC), one rank at a time, each import bounded
+(hipps.parallel.ps_async._bounded_open), and checks the stamps.  A timed-out
 import prints the stuck thread's /proc state sampled over a few seconds (wait channel, syscall,
 user / system CPU ticks: a thread burning CPU in user space is a runtime loop, one parked in a
 syscall is the kernel driver) and ends the probe (the thread cannot be cancelled).
@@ -34,8 +35,6 @@ def main():
     ap.add_argument("--chunk-mb", type=int, default=0, help="split every region into allocations of this size")
     ap.add_argument("--limit", type=float, default=20.0)
     ap.add_argument("--repeat", type=int, default=1)
-    ap.add_argument("--vmm", action="store_true", help="VmmRegion (hipMemCreate chunks + POSIX fds over a Unix "
-                    "socket, mapped contiguously) instead of hipIpcOpenMemHandle; --chunk-mb is the chunk size")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -51,71 +50,34 @@ def main():
         for mb in [int(s) for s in a.sizes.split(",")]:
             parts = [mb] if not a.chunk_mb else [min(a.chunk_mb, mb - o) for o in range(0, mb, a.chunk_mb)]
             t0 = time.perf_counter()
-            if a.vmm:
-                import secrets
-
-                mine = [C.VmmRegion(mb << 20, (a.chunk_mb or mb) << 20)] if rank == 0 else []
-                if rank == 0:
-                    reg = mine[0].tensor()
-                    for c in range(len(mine[0].chunk_sizes())):
-                        reg[c * ((a.chunk_mb or mb) << 20)] = (c % 200) + 1
-                    torch.cuda.synchronize()
-                name = f"hipps_probe_{secrets.token_hex(4)}" if rank == 0 else None
-                srv = C.FdServer(name) if rank == 0 else None
-                meta = [(name, mine[0].chunk_sizes()) if rank == 0 else None]
-            else:
-                mine = [C.DeviceMailbox(p << 20) for p in parts] if rank == 0 else []
-                for c, m in enumerate(mine):  # stamp every allocation (checked by the importers)
-                    m.tensor()[0] = (c % 200) + 1
-                torch.cuda.synchronize()
-                meta = [[m.handle() for m in mine] if rank == 0 else None]
+            mine = [C.DeviceMailbox(p << 20) for p in parts] if rank == 0 else []
+            for c, m in enumerate(mine):  # stamp every allocation (checked by the importers)
+                m.tensor()[0] = (c % 200) + 1
+            torch.cuda.synchronize()
+            meta = [[m.handle() for m in mine] if rank == 0 else None]
             t_alloc = time.perf_counter() - t0
             dist.broadcast_object_list(meta, src=0)
-            if a.vmm:
-                parts = list(range(len(meta[0][1])))
             res = None
             for r in range(1, W):  # one importer at a time
-                if rank == 0 and a.vmm:
-                    srv.send_one(mine[0].export_fds(), int(a.limit * 1000))
                 if rank == r:
                     t1 = time.perf_counter()
                     try:
-                        if a.vmm:
-                            nm, sizes = meta[0]
-                            fds = C.fd_recv(nm, int(a.limit * 1000))
-                            mbx, _ = _bounded_open(lambda: C.VmmRegion(fds, sizes, mb << 20), f"{mb} MB (vmm)", rank,
+                        for c, (h, p) in enumerate(zip(meta[0], parts)):
+                            mbx, _ = _bounded_open(lambda h=h, p=p: C.DeviceMailbox(h, p << 20), f"{p} MB", rank,
                                                    torch.cuda.current_device(), a.limit)
                             mine.append(mbx)
-                            # data check, both directions: the exporter stamped chunk c's first byte
-                            # with (c % 200) + 1; this importer writes its rank at the region's end
-                            t = mbx.tensor()
-                            seen = [int(t[c * ((a.chunk_mb or mb) << 20)]) for c in range(len(sizes))]
-                            want = [(c % 200) + 1 for c in range(len(sizes))]
-                            t[-16:].fill_(rank)
-                            if seen != want:
-                                raise IPCOpenTimeout(f"STALE rank {rank}: saw {seen[:6]} want {want[:6]}")
-                        else:
-                            for c, (h, p) in enumerate(zip(meta[0], parts)):
-                                mbx, _ = _bounded_open(lambda h=h, p=p: C.DeviceMailbox(h, p << 20), f"{p} MB", rank,
-                                                       torch.cuda.current_device(), a.limit)
-                                mine.append(mbx)
-                                got = int(mbx.tensor()[0])
-                                if got != (c % 200) + 1:
-                                    raise IPCOpenTimeout(f"STALE rank {rank}: allocation {c} reads {got}")
+                            got = int(mbx.tensor()[0])
+                            if got != (c % 200) + 1:
+                                raise IPCOpenTimeout(f"STALE rank {rank}: allocation {c} reads {got}")
                         torch.cuda.synchronize()
                         res = round(time.perf_counter() - t1, 4)
                     except IPCOpenTimeout as e:
                         res = f"TIMEOUT {e}"
                 dist.barrier()
-            if a.vmm and rank == 0:
-                srv.close()
-            if a.vmm and rank == 0:
-                got = mine[0].tensor()[-16:].cpu().tolist()
-                print(f"  vmm last bytes seen by the exporter: {got[:4]} (want [{W - 1}, ...])", flush=True)
             out = [None] * W
             dist.all_gather_object(out, res)
             if rank == 0:
-                print(f"rep {rep} region {mb} MB as {len(parts)} {'vmm chunk' if a.vmm else 'allocation'}(s): "
+                print(f"rep {rep} region {mb} MB as {len(parts)} allocation(s): "
                       f"alloc+export {t_alloc:.3f} s, "
                       f"import per rank {out[1:]}", flush=True)
             if any(isinstance(o, str) for o in out):
