@@ -69,6 +69,13 @@ def _parse_fault(spec, rank):
     return None
 
 
+def _checksum(t: torch.Tensor, piece: int = 1 << 26) -> float:
+    """float64 sum of a flat tensor in 64 M-element pieces (an 8 B-parameter model's whole-buffer
+    .double() would allocate 64 GB)."""
+    n = t.numel()
+    return float(sum(float(t[a:a + piece].double().sum()) for a in range(0, n, piece))) if n else 0.0
+
+
 def _align(x: int, a: int = 256) -> int:
     return (x + a - 1) // a * a
 
@@ -184,7 +191,7 @@ def mailbox_geometry(msg_nbytes: Sequence[int], pres_bytes: int, mailbox_slots: 
 
 
 HBM_DEFAULT = 288 * 10**9  # one MI355X (spec); the engine reads the device's own total
-HBM_FRACTION = 0.9          # the PS + co-located worker state may take this much, the rest is activations
+HBM_FRACTION = 0.85         # the PS + co-located worker state may take this much, the rest is activations
 
 
 def plan_geometry(msg_nbytes: Sequence[int], pres_bytes: int, numel: int, W: int, pub_esz: int, opt_floats: int,
@@ -713,6 +720,13 @@ class PSAsyncEngine(Engine):
                                                **self._budget_inputs(opt, store, esz))
             geo = [K, ring, npub]
             self._check_budget(store, bud)
+            if not bud.get("fits", 1):
+                import sys
+
+                print(f"[hipps] warning: the async PS state ({bud['total'] / 1e9:.0f} GB with every ring at its floor "
+                      f"and {npub} publish buffers) exceeds {HBM_FRACTION:.0%} of this GPU's HBM; activations may not "
+                      "fit.  Options: param_wire='bf16', ps_dedicated=True, momentum 0 / a smaller optimizer state.",
+                      file=sys.stderr)
         else:
             bud = {}
         if self.W > 1:
@@ -963,7 +977,7 @@ class PSAsyncEngine(Engine):
             ck = self._pub_sum(0)  # what workers actually receive
         else:
             ck = None
-        mine = float(self.store.data.double().sum())
+        mine = _checksum(self.store.data)
         if W > 1:
             box = [ok, ck]
             dist.broadcast_object_list(box, src=0)
@@ -992,11 +1006,11 @@ class PSAsyncEngine(Engine):
                 ok &= bool((got.cpu() == (r * 7 + 3) % 251).all())
         else:
             self._gpg.send(tag, 0)
-        ck = float(self.pub_buf(0).double().sum()) if self.rank == 0 else None
+        ck = _checksum(self.pub_buf(0)) if self.rank == 0 else None
         box = [ok, ck]
         dist.broadcast_object_list(box, src=0)
         ok, ck = box
-        mine = float(self.store.data.double().sum())
+        mine = _checksum(self.store.data)
         good = ok and abs(mine - ck) <= 1e-6 * max(1.0, abs(ck))
         flags = [None] * W
         dist.all_gather_object(flags, good)
@@ -1052,7 +1066,7 @@ class PSAsyncEngine(Engine):
         return self.pub_chunks[b][0]
 
     def _pub_sum(self, k: int) -> float:
-        return float(sum(self.pub_view(k, a, b).double().sum() for _, a, b in self._pub_pieces(0, self.store.numel)))
+        return sum(_checksum(self.pub_view(k, a, b)) for _, a, b in self._pub_pieces(0, self.store.numel))
 
     # ------------------------------------------------------------------ PS side
     def _ring(self, stream, words, srcs=None):

@@ -101,11 +101,13 @@ for step in "$@"; do
         --codec threshold:0.001 --bucket-mb 4 --out "$OUT/bert_thr.json" > "$OUT/bert_thr.log" 2>&1 \
         || fail bert_thr "$OUT/bert_thr.log"
       cut -c1-200 "$OUT/bert_thr.json"
-      timeout -k 10 300 python bench.py --model llama3-1b --batch 4 --seq 2048 --lr 1e-3 --steps 8 --warmup 3 \
+      timeout -k 10 300 python bench.py --model llama3-1b --batch 4 --seq 2048 --param-wire bf16 --lr 1e-3 --steps 8 \
+        --warmup 3 \
         --out "$OUT/llama1b.json" > "$OUT/llama1b.log" 2>&1 || fail llama1b "$OUT/llama1b.log"
       cut -c1-200 "$OUT/llama1b.json" ;;
     llama8b)
-      timeout -k 10 600 python bench.py --model llama3-8b --batch 1 --seq 2048 --lr 1e-4 --steps 6 --warmup 3 \
+      timeout -k 10 600 python bench.py --model llama3-8b --batch 1 --seq 2048 --param-wire bf16 --momentum 0 \
+        --lr 1e-4 --steps 6 --warmup 3 \
         --out "$OUT/llama8b.json" > "$OUT/llama8b.log" 2>&1 || fail llama8b "$OUT/llama8b.log"
       cut -c1-300 "$OUT/llama8b.json" ;;
     emu7)
