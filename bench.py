@@ -263,6 +263,7 @@ def main():
     if host_t is not None:
         host_t[:] = [0.0] * 7
         ms0 = torch.cuda.memory_stats(dev)
+        seq0 = getattr(opt.engine, "seq", 0)
     for hook in TIMED_HOOKS:
         hook(True)
     t0 = time.perf_counter()
@@ -286,6 +287,8 @@ def main():
         print("[bench] host ms/step: forward %.2f backward %.2f step %.2f (wall %.2f); waits: slot %.2f "
               "encode %.2f pull %.2f" % tuple([1e3 * v / host_t[3] for v in host_t[:3]] + [1e3 * elapsed / a.steps]
                                               + [1e3 * v / host_t[3] for v in host_t[4:]]), file=sys.stderr)
+        if hasattr(opt.engine, "wait_summary"):
+            print("[bench] mailbox waits (timed steps): " + opt.engine.wait_summary(seq0), file=sys.stderr)
         ms1 = torch.cuda.memory_stats(dev)
         print("[bench] allocator during timed steps: " + " ".join(
             f"{k}+{ms1.get(k, 0) - ms0.get(k, 0)}" for k in ("num_alloc_retries", "num_device_alloc", "num_device_free",

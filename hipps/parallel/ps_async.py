@@ -595,6 +595,8 @@ class PSAsyncEngine(Engine):
         self._early = pe != "off" and not self.p2p and cfg.overlap and not self.is_object \
             and self._fault is None and not self.plan.guarded and not self.ps_only
         self._npushed, self._push_wait, self._in_encode_all = 0, 0.0, False
+        # HIPPS_WAIT_DIAG=1: every host wait for mailbox space (kind, seq, needed ack, ack at start, s)
+        self._wait_log = [] if os.environ.get("HIPPS_WAIT_DIAG", "0") == "1" else None
         self._pushed_b = bytearray(self.nb)  # buckets already pushed this step (any order)
         # direct push: a hook-time bucket is encoded straight into its space in the (local) mailbox
         # ring -- no wire-buffer image and no copy.  Rank 0's own worker only (its mailbox is local
@@ -1637,10 +1639,14 @@ class PSAsyncEngine(Engine):
         slot = s % self.SLOTS
         if s > self.SLOTS:  # slot reuse: message s - SLOTS must have been consumed
             tw = time.perf_counter()
+            a0 = self.ctl.load(C.F_ACK_SEQ, self.rank) if self._wait_log is not None else 0
             if not self.ctl.wait_ge(C.F_ACK_SEQ, self.rank, s - self.SLOTS, self.timeout_us):
                 self._check_error()
                 raise TimeoutError(f"rank {self.rank}: PS did not consume message {s - self.SLOTS}")
-            t_wait += time.perf_counter() - tw
+            dt = time.perf_counter() - tw
+            t_wait += dt
+            if self._wait_log is not None and a0 < s - self.SLOTS:
+                self._wait_log.append(("slot", s, s - self.SLOTS, a0, dt))
         b = self.plan.buckets[bi]
         src = self.plan.message(self.wire, bi)  # layout (+ canary guard in debug_canary)
         vidx = self.rank * self.MAXSLOTS + slot
@@ -1801,10 +1807,13 @@ class PSAsyncEngine(Engine):
         tw = 0.0
         if need:
             t0 = time.perf_counter()
+            a0 = self.ctl.load(C.F_ACK_SEQ, self.rank) if self._wait_log is not None else 0
             if not self.ctl.wait_ge(C.F_ACK_SEQ, self.rank, need, self.timeout_us):
                 self._check_error()
                 raise TimeoutError(f"rank {self.rank}: PS did not consume message {need} (mailbox ring full)")
             tw = time.perf_counter() - t0
+            if self._wait_log is not None and a0 < need:
+                self._wait_log.append(("ring", s, need, a0, tw))
         ack = self.ctl.load(C.F_ACK_SEQ, self.rank)
         while self._inflight and self._inflight[0][0] <= ack:
             self._inflight.popleft()
@@ -2202,6 +2211,22 @@ class PSAsyncEngine(Engine):
             self.steps += 1
             return True
         return False
+
+    def wait_summary(self, skip_seq: int = 0) -> str:
+        """HIPPS_WAIT_DIAG: the host's mailbox waits after message ``skip_seq``, by kind and by
+        how many messages the PS was behind when the wait began."""
+        log = [w for w in (self._wait_log or []) if w[1] > skip_seq]
+        if not log:
+            return "no mailbox waits"
+        out = []
+        for kind in ("slot", "ring"):
+            ws = [w for w in log if w[0] == kind]
+            if ws:
+                lag = sorted(w[2] - w[3] for w in ws)
+                out.append(f"{kind}: {len(ws)} waits, {1e3 * sum(w[4] for w in ws):.1f} ms, behind by "
+                           f"{lag[len(lag) // 2]} (median) / {lag[-1]} (max) messages; bucket pos of the waiting "
+                           f"message: {sorted(collections.Counter((w[1] - 1) % self.nb for w in ws).items())}")
+        return "; ".join(out)
 
     def ps_stats(self) -> dict:
         C = self.C
