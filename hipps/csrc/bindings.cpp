@@ -110,7 +110,7 @@ void rms_backward(at::Tensor dy, at::Tensor x, at::Tensor rstd, at::Tensor w, at
 void swiglu_backward(at::Tensor g, at::Tensor a, at::Tensor b, at::Tensor da, at::Tensor db);
 void rope_apply(at::Tensor x, at::Tensor y, at::Tensor cs, at::Tensor sn, int64_t S, int64_t hd, double sign);
 void xent_backward(at::Tensor logits, at::Tensor labels, at::Tensor lse, at::Tensor gout, double scale,
-                   int64_t ignore_index, at::Tensor dx);
+                   int64_t ignore_index, at::Tensor dx, c10::optional<at::Tensor> count);
 void bn_finalize_bwd_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tensor weight, at::Tensor mean,
                               at::Tensor invstd, at::Tensor dweight, at::Tensor dbias, at::Tensor coef);
 void conv1x1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t Hi, int64_t Wi, int64_t stride,
@@ -261,8 +261,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("hd"), py::arg("sign") = 1.0, "rotary embedding of interleaved pairs, fp32 tables (act.hip)");
   m.def("colsum_bf16", &hipps::colsum_bf16, "fp32 column sums of a bf16 [rows, cols] matrix (bias gradients)");
   m.def("xent_forward", &hipps::xent_forward,
-        "fused softmax cross-entropy over bf16 logits: per-row loss and log-sum-exp (one read of the row)");
-  m.def("xent_backward", &hipps::xent_backward, "cross-entropy gradient (softmax - onehot) * g * scale, bf16");
+        "fused softmax cross-entropy over bf16 logits: (mean loss, counted rows, per-row log-sum-exp)");
+  m.def("xent_backward", &hipps::xent_backward, py::arg("logits"), py::arg("labels"), py::arg("lse"), py::arg("gout"),
+        py::arg("scale"), py::arg("ignore_index"), py::arg("dx"), py::arg("count") = py::none(),
+        "cross-entropy gradient (softmax - onehot) * g * scale / count, bf16");
   m.def("bn_finalize_bwd_partials", &hipps::bn_finalize_bwd_partials,
         "BN backward finalize from partial sums (dweight, dbias, dx coefficients [3, C])");
   m.def("maxpool3s2_backward", &hipps::maxpool3s2_backward, "3x3/s2/p1 max pool backward (gather form, no atomics)");

@@ -70,7 +70,7 @@ template <> struct Cfg<128, 64> { static constexpr int TM = 64, TN = 32; };
 template <int BM, int BN> constexpr int nthreads() { return 64 * (BM / Cfg<BM, BN>::TM) * (BN / Cfg<BM, BN>::TN); }
 
 template <int BM, int BN, int NS = 2> constexpr int lds_bytes() {
-  constexpr int stage = (NS == 4 ? 2 : NS) * (BM + BN) * BK * 2;
+  constexpr int stage = (NS >= 4 ? 2 : NS) * (BM + BN) * BK * 2;
   constexpr int epi = BM * (BN + 8) * 2;
   constexpr int wm = BM / Cfg<BM, BN>::TM;
   return (stage > epi ? stage : epi) + 2 * 2 * wm * BN * 4;
@@ -130,10 +130,18 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   constexpr int WM = BM / TM, WN = BN / TN, NW = WM * WN, NT = 64 * NW;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr bool KH = NS == 4;
+  // NS == 5: ping-pong (2 LDS stages, 256x256 on 8 waves).  The two row halves of the tile are two
+  // wave groups, one wave of each on every SIMD, one phase apart: while group 0 runs the MFMAs of
+  // tile k, group 1 issues the DMA of tile k+2 and waits on its landing, then they swap -- the
+  // DMA issue and the drains before each barrier sit beside the partner's MFMAs instead of
+  // stalling both waves of the SIMD at the same barrier.  Group 0 stages its own A half (freed
+  // as soon as it finished tile k), group 1 the other A half and all of B (freed one phase later).
+  constexpr bool PP = NS == 5;
   constexpr bool PAR = (EPI & kPar) != 0;
   constexpr bool PRO = (EPI & kPro) != 0;
   static_assert(!PAR || TAPS, "kPar needs the implicit-GEMM loader");
   static_assert(!PRO || NS == 2, "kPro: 2 LDS stages");
+  static_assert(!PP || (BM == 256 && BN == 256), "ping-pong: 256x256 on 8 waves");
   // output row of GEMM row m (kPar: the class's dx position)
   auto orow = [&](int m) -> int64_t {
     if constexpr (PAR) {
@@ -151,11 +159,12 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   constexpr int AI = BM / RPI / NW;       // A wave-instructions per stage (KH: per unit) per wave
   constexpr int BI = BN / RPI / NW;
   constexpr int EP = BN + 8;              // epilogue row pitch (elements)
-  constexpr int NSB = KH ? 2 : NS;        // stage-sized LDS buffers
+  constexpr int NSB = (KH || PP) ? 2 : NS;  // stage-sized LDS buffers
   constexpr int SCR = (NSB * STAGE * 2 > BM * EP * 2 ? NSB * STAGE * 2 : BM * EP * 2);  // bytes before the stats scratch
   static_assert(AI >= 1 && BI >= 1, "tile too small for the wave count");
-  static_assert(NS == 2 || NS == 3 || NS == 4, "stages");
+  static_assert(NS >= 2 && NS <= 5, "stages");
   constexpr int NG = AI + BI;  // glds per tile (KH: per unit) per wave
+  constexpr int BIP = PP ? 2 * BI : BI;  // PP: group 1 stages all of B (group 0 none)
   __shared__ __attribute__((aligned(16))) uint16_t lds[lds_bytes<BM, BN, NS>() / 2];
 
   // bijective XCD-aware block order (cdna_hip_programming.md §5 'XCD swizzle must be bijective'):
@@ -167,6 +176,9 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wm = w / WN, wn = w - (w / WN) * WN;
+  // first row of this wave's i-th A / B wave-instruction (PP: A rows of the wave's own group)
+  auto arb = [&](int i) { return PP ? (BM / 2) * wm + RPI * (i * (NW / 2) + wn) : RPI * (i * NW + w); };
+  auto brb = [&](int i) { return PP ? RPI * (i * (NW / 2) + wn) : RPI * (i * NW + w); };
   // row in the wave-instruction's row group, logical chunk this lane fetches (the LDS slot is
   // lane-linear; the swizzle is applied on the source)
   const int lr = KH ? lane >> 2 : lane >> 3;
@@ -178,7 +190,7 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   bool a_ok[AI];
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
-    const int row = RPI * (i * NW + w) + lr;
+    const int row = arb(i) + lr;
     int m = m0 + row;
     a_ok[i] = m < g.M;
     m = a_ok[i] ? m : g.M - 1;
@@ -200,16 +212,17 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
       a_src[i] = g.X + src * g.K + lc * 8;
     }
   }
-  const uint16_t* b_src[BI];
-#pragma unroll
-  for (int i = 0; i < BI; ++i) b_src[i] = g.W + (int64_t)(n0 + RPI * (i * NW + w) + lr) * g.ldb + lc * 8;
+  // B rows of consecutive wave-instructions are a fixed (wave-uniform) distance apart: one per-lane
+  // base pointer, the rest scalar offsets (no per-instruction VGPR pair)
+  const uint16_t* b_src0 = g.W + (int64_t)(n0 + brb(0) + lr) * g.ldb + lc * 8;
+  auto b_src = [&](int i) { return b_src0 + (int64_t)(brb(i) - brb(0)) * g.ldb; };
 
   // kPro: which of this thread's A chunks of the staged tile hold data (not the zero page), and
   // the BN scale / shift of its 8 channels -- loaded with the tile's DMA, used at the next barrier
   uint32_t pro_ok = 0;
   float pro_sc[PRO ? 8 : 1], pro_sh[PRO ? 8 : 1];
   // stage kt (KH: unit 2*kt + h, k0 = 64*kt + 32*h, rows of 32 elements) into LDS at ``base``
-  auto issue_at = [&](int k0, uint16_t* base, int rowlen) {
+  auto issue_at = [&](int k0, uint16_t* base, int rowlen, bool do_b = true) {
     int bk = k0;  // B column of this K tile
     if constexpr (PRO) {
       const int ch = (TAPS ? k0 - (k0 / g.Cin) * g.Cin : k0) + lc * 8;
@@ -239,18 +252,20 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
         const int hi = a_h[i] + kr, wi = a_w[i] + kc;
         const bool ok = a_ok[i] && hi >= 0 && hi < g.Hi && wi >= 0 && wi < g.Wi;
         const uint16_t* p = ok ? a_src[i] + ((int64_t)hi * g.Wi + wi) * g.Cin + c0 : kZero16;
-        glds16(p, base + RPI * (i * NW + w) * rowlen);
+        glds16(p, base + arb(i) * rowlen);
         if constexpr (PRO) pro_ok |= (ok ? 1u : 0u) << i;
       }
     } else {
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
-        glds16(a_ok[i] ? a_src[i] + k0 : kZero16, base + RPI * (i * NW + w) * rowlen);
+        glds16(a_ok[i] ? a_src[i] + k0 : kZero16, base + arb(i) * rowlen);
         if constexpr (PRO) pro_ok |= (a_ok[i] ? 1u : 0u) << i;
       }
     }
+    if (do_b) {
 #pragma unroll
-    for (int i = 0; i < BI; ++i) glds16(b_src[i] + bk, base + BM * rowlen + RPI * (i * NW + w) * rowlen);
+      for (int i = 0; i < BIP; ++i) glds16(b_src(i) + bk, base + BM * rowlen + brb(i) * rowlen);
+    }
   };
   auto issue = [&](int kt, int s) { issue_at(kt * BK, lds + s * STAGE, BK); };
   auto issue_unit = [&](int u) { issue_at(u * 32, lds + (u & 3) * UNIT, 32); };
@@ -306,7 +321,80 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
         }
     }
   };
-  if constexpr (KH) {
+  if constexpr (PP) {
+    const int KT = g.K / BK;
+    const bool g1 = wm != 0;
+    // MFMAs of tile kt (both k-steps' fragments read up front, the second set in flight while the
+    // first step's MFMAs run)
+    auto compute = [&](int kt) {
+      const uint16_t* As = lds + (kt & 1) * STAGE;
+      const uint16_t* Bs = As + BM * BK;
+      // (TAPS: one fragment set -- the implicit-GEMM loader's per-row state leaves no room for two)
+      constexpr int FS2 = TAPS ? 1 : 2;
+      bf16x8 a[FS2][FM], b[FS2][FN];
+      auto frag = [&](int ks, int slot) {
+        const int c = ks * 4 + (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int row = wn * TN + j * 16 + (lane & 15);
+          b[slot][j] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + ((c ^ (row & 7)) << 3));
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int row = wm * TM + i * 16 + (lane & 15);
+          a[slot][i] = *reinterpret_cast<const bf16x8*>(As + row * BK + ((c ^ (row & 7)) << 3));
+        }
+      };
+      if constexpr (FS2 == 2) {
+        frag(0, 0);
+        frag(1, 1);
+        __builtin_amdgcn_s_waitcnt(waitcnt_lgkm(FM + FN));  // step 0's reads; step 1's in flight
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int slot = FS2 == 2 ? ks : 0;
+        if constexpr (FS2 == 1) frag(ks, 0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[slot][i], b[slot][j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    };
+    // prologue: tiles 0 and 1 (each group its part), drained; group 1 then waits out phase 0
+    issue_at(0, lds, BK, g1);
+    if (KT > 1) issue_at(BK, lds + STAGE, BK, g1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (g1) __builtin_amdgcn_s_barrier();
+    // phase p ends at a barrier; group 0 computes tile kt in phase 2kt, group 1 in phase 2kt+1.
+    // Every wave passes 2 + 2*KT barriers.
+    for (int kt = 0; kt < KT; ++kt) {
+      compute(kt);
+      if (!g1) {
+        __builtin_amdgcn_s_barrier();  // end of phase 2kt: this group's A half of stage kt&1 is free
+        asm volatile("" ::: "memory");
+        if (kt + 2 < KT) {
+          issue_at((kt + 2) * BK, lds + (kt & 1) * STAGE, BK, false);
+          __builtin_amdgcn_s_waitcnt(waitcnt_vm(AI));  // A half of tile kt+1 landed; kt+2's in flight
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();  // end of phase 2kt+1
+        asm volatile("" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this group's part of tile kt+1 landed
+        __builtin_amdgcn_s_barrier();  // end of phase 2kt+1: stage kt&1 fully read
+        asm volatile("" ::: "memory");
+        if (kt + 2 < KT) issue_at((kt + 2) * BK, lds + (kt & 1) * STAGE, BK, true);
+        __builtin_amdgcn_s_barrier();  // end of phase 2kt+2
+        asm volatile("" ::: "memory");
+      }
+    }
+    if (!g1) __builtin_amdgcn_s_barrier();  // pairs group 1's end of phase 2KT
+  } else if constexpr (KH) {
     // k-half units: unit u = K rows [32u, 32u + 32) in LDS slot u & 3
     const int NU = g.K / 32;
     issue_unit(0);
@@ -1042,7 +1130,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
                 c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift,
                 c10::optional<at::Tensor> bias) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "gemm2: device tensors");
-  TORCH_CHECK(stages >= 2 && stages <= 4, "gemm2: stages must be 2, 3 or 4 (k-half units)");
+  TORCH_CHECK(stages >= 2 && stages <= 5, "gemm2: stages must be 2, 3, 4 (k-half units) or 5 (ping-pong)");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
                   y.scalar_type() == at::kBFloat16, "gemm2: bf16 tensors");
   const int64_t N = w.size(0), K = w.numel() / N, Cin = K / (KH * KW);
@@ -1152,6 +1240,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
   do {                                                      \
     if (NS3) HIPPS_G2S(BMc, BNc, EPc, TPc, NS3_OF(BMc, BNc)); \
     else if (NS4) HIPPS_G2S(BMc, BNc, EPc, TPc, 4);          \
+    else if (NS5) HIPPS_G2S(BMc, BNc, EPc, TPc, NS5_OF(BMc, BNc)); \
     else HIPPS_G2S(BMc, BNc, EPc, TPc, 2);                   \
   } while (0)
 #define HIPPS_G2_E(BMc, BNc)                                                                        \
@@ -1186,8 +1275,11 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
   } while (0)
   // 3 stages where they fit the LDS (not 256x256: 3 x 64 KB)
   const bool NS3 = stages == 3, NS4 = stages == 4;  // 4: k-half units (see k_gemm)
+  const bool NS5 = stages == 5;                      // 5: ping-pong wave groups (256x256 only)
   TORCH_CHECK(!NS3 || !(BMv == 256 && BNv == 256), "gemm2: 3 stages do not fit a 256x256 tile");
+  TORCH_CHECK(!NS5 || (BMv == 256 && BNv == 256), "gemm2: the ping-pong schedule (stages 5) is a 256x256 tile");
 #define NS3_OF(BMc, BNc) ((BMc) == 256 && (BNc) == 256 ? 2 : 3)
+#define NS5_OF(BMc, BNc) ((BMc) == 256 && (BNc) == 256 ? 5 : 2)
   if (BMv == 256 && BNv == 256) HIPPS_G2_E(256, 256);
   else if (BMv == 256 && BNv == 128) HIPPS_G2_E(256, 128);
   else if (BMv == 128 && BNv == 128) HIPPS_G2_E(128, 128);
@@ -1198,6 +1290,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
 #undef HIPPS_G2
 #undef HIPPS_G2S
 #undef NS3_OF
+#undef NS5_OF
 }
 
 // Input gradient of a stride-2 3x3 / pad-1 convolution as four output-parity classes (kPar): dx

@@ -89,14 +89,14 @@ __global__ __launch_bounds__(kXBlock) void k_xent_fwd(const uint16_t* __restrict
 __global__ __launch_bounds__(kXBlock) void k_xent_bwd(const uint16_t* __restrict__ x, const int64_t* __restrict__ labels,
                                                       const float* __restrict__ lse, int64_t V, int64_t ignore,
                                                       const float* __restrict__ gscale, float scale,
-                                                      uint16_t* __restrict__ dx) {
+                                                      const float* __restrict__ ndiv, uint16_t* __restrict__ dx) {
   const int64_t r = blockIdx.x;
   const uint16_t* row = x + r * V;
   uint16_t* drow = dx + r * V;
   const int64_t lab = labels[r];
   const bool skip = lab == ignore || lab < 0 || lab >= V;
   const float l = lse[r];
-  const float k = skip ? 0.f : scale * gscale[0];
+  const float k = skip ? 0.f : scale * gscale[0] / (ndiv ? ndiv[0] : 1.f);
   const bool vec = ((reinterpret_cast<uintptr_t>(row) | reinterpret_cast<uintptr_t>(drow)) & 15) == 0;
   const int64_t nv = vec ? V / 8 : 0;
   for (int64_t v = threadIdx.x; v < nv; v += kXBlock) {
@@ -118,37 +118,87 @@ __global__ __launch_bounds__(kXBlock) void k_xent_bwd(const uint16_t* __restrict
     drow[i] = f32_to_bf16((__expf(bf16_to_f32(row[i]) - l) - (i == lab ? 1.f : 0.f)) * k);
 }
 
-// logits: bf16 [R, V] contiguous; labels int64 [R]; returns (per-row loss f32 [R], lse f32 [R])
+// mean over the rows that carry a loss (label not ignored, inside [0, V)): one workgroup sums
+// the per-row losses and counts the rows in a fixed order (deterministic); out = [mean, count].
+// Folds the ~8 PyTorch scalar kernels of "mask, count, sum, divide" (each a host round of
+// dispatch at the forward -> backward turn, where the GPU waits on the host) into one launch.
+__global__ __launch_bounds__(kXBlock) void k_xent_mean(const float* __restrict__ loss, const int64_t* __restrict__ labels,
+                                                       int64_t R, int64_t V, int64_t ignore, float* __restrict__ mean,
+                                                       float* __restrict__ count) {
+  __shared__ float ss[kXBlock / 64];
+  __shared__ int sn[kXBlock / 64];
+  float s = 0.f;
+  int n = 0;
+  for (int64_t r = threadIdx.x; r < R; r += kXBlock) {
+    const int64_t lab = labels[r];
+    if (!(lab == ignore || lab < 0 || lab >= V)) {
+      s += loss[r];
+      ++n;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o, 64);
+    n += __shfl_xor(n, o, 64);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    ss[w] = s;
+    sn[w] = n;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.f;
+    int c = 0;
+#pragma unroll
+    for (int q = 0; q < kXBlock / 64; ++q) {
+      a += ss[q];
+      c += sn[q];
+    }
+    mean[0] = a / (float)c;  // every row ignored -> 0 / 0 = NaN, as F.cross_entropy
+    count[0] = (float)c;
+  }
+}
+
+// logits: bf16 [R, V] contiguous; labels int64 [R]; returns (mean loss f32 [], row count f32 [1],
+// lse f32 [R] for the backward)
 std::vector<at::Tensor> xent_forward(at::Tensor logits, at::Tensor labels, int64_t ignore_index) {
   TORCH_CHECK(logits.is_cuda() && logits.scalar_type() == at::kBFloat16 && logits.dim() == 2 && logits.is_contiguous(),
               "xent: logits must be a contiguous bf16 [rows, vocab] device tensor");
   TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous() &&
                   labels.numel() == logits.size(0), "xent: labels must be int64 [rows] on the device");
   const int64_t R = logits.size(0), V = logits.size(1);
-  TORCH_CHECK(V > 0 && R < (int64_t(1) << 31), "xent: sizes");
+  TORCH_CHECK(V > 0 && R > 0 && R < (int64_t(1) << 24), "xent: sizes");
   auto f32 = logits.options().dtype(at::kFloat);
-  at::Tensor loss = at::empty({R}, f32), lse = at::empty({R}, f32);
-  if (R == 0) return {loss, lse};
-  hipLaunchKernelGGL(k_xent_fwd, (int)R, kXBlock, 0, c10::hip::getCurrentHIPStream(),
-                     (const uint16_t*)logits.data_ptr(), labels.data_ptr<int64_t>(), V, ignore_index,
-                     loss.data_ptr<float>(), lse.data_ptr<float>());
-  return {loss, lse};
+  at::Tensor rows = at::empty({R}, f32), lse = at::empty({R}, f32), mean = at::empty({}, f32), count = at::empty({1}, f32);
+  auto stream = c10::hip::getCurrentHIPStream();
+  hipLaunchKernelGGL(k_xent_fwd, (int)R, kXBlock, 0, stream, (const uint16_t*)logits.data_ptr(),
+                     labels.data_ptr<int64_t>(), V, ignore_index, rows.data_ptr<float>(), lse.data_ptr<float>());
+  hipLaunchKernelGGL(k_xent_mean, 1, kXBlock, 0, stream, rows.data_ptr<float>(), labels.data_ptr<int64_t>(), R, V,
+                     ignore_index, mean.data_ptr<float>(), count.data_ptr<float>());
+  return {mean, count, lse};
 }
 
-// dx = (softmax - onehot) * gout[0] * scale, bf16 like the logits
+// dx = (softmax - onehot) * gout[0] * scale / count[0] (count: xent_forward's row count, or
+// None for 1), bf16 like the logits
 void xent_backward(at::Tensor logits, at::Tensor labels, at::Tensor lse, at::Tensor gout, double scale,
-                   int64_t ignore_index, at::Tensor dx) {
+                   int64_t ignore_index, at::Tensor dx, c10::optional<at::Tensor> count) {
   TORCH_CHECK(logits.is_cuda() && logits.scalar_type() == at::kBFloat16 && logits.dim() == 2 && logits.is_contiguous(),
               "xent: logits must be a contiguous bf16 [rows, vocab] device tensor");
   TORCH_CHECK(dx.sizes() == logits.sizes() && dx.scalar_type() == at::kBFloat16 && dx.is_contiguous(), "xent: dx");
   TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == logits.size(0) && lse.numel() == logits.size(0) &&
                   lse.scalar_type() == at::kFloat, "xent: labels / lse");
   TORCH_CHECK(gout.is_cuda() && gout.scalar_type() == at::kFloat && gout.numel() == 1, "xent: gout f32 scalar");
+  const float* nd = nullptr;
+  if (count.has_value() && count->defined()) {
+    TORCH_CHECK(count->is_cuda() && count->scalar_type() == at::kFloat && count->numel() == 1, "xent: count f32 [1]");
+    nd = count->data_ptr<float>();
+  }
   const int64_t R = logits.size(0), V = logits.size(1);
   if (R == 0) return;
   hipLaunchKernelGGL(k_xent_bwd, (int)R, kXBlock, 0, c10::hip::getCurrentHIPStream(),
                      (const uint16_t*)logits.data_ptr(), labels.data_ptr<int64_t>(), lse.data_ptr<float>(), V,
-                     ignore_index, gout.data_ptr<float>(), (float)scale, (uint16_t*)dx.data_ptr());
+                     ignore_index, gout.data_ptr<float>(), (float)scale, nd, (uint16_t*)dx.data_ptr());
 }
 
 }  // namespace hipps

@@ -14,7 +14,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from hipps.ops.nn import (FusedBatchNorm2d, Linear, MaxPool2d, ResidualTap, bn_relu_conv, bn_relu_conv1x1_ok,
+from hipps.ops.nn import (FusedBatchNorm2d, Linear, MaxPool2d, ResidualTap, bn_pro_pays, bn_relu_conv, bn_relu_conv1x1_ok,
                           bn_relu_conv_bn, bn_relu_conv_ok, bn_relu_maxpool, conv1x1_bn_input, conv1x1_ok, conv2d,
                           conv2d_bn, conv2d_stats, conv_bn, dual_bn_relu, dual_bn_relu_ok, global_avg_pool,
                           stem_block, stem_block_ok)
@@ -158,8 +158,12 @@ class Bottleneck(nn.Module):
             y1, p1, xa = conv1x1_bn_input(self.conv1, x, alias=True, bn_grad=bng)
             y = self.bn1(y1, stats=p1) if self.bn1._fast_ok(y1, None) else self.bn1(y1)
             xd, pd = conv1x1_bn_input(ds[0], xa)
-            y = conv2d_bn(self.conv2, self.bn2, y, fuse=_FUSED_WGRAD, bn_grad=bng)
-            x3, p3 = conv1x1_bn_input(self.conv3, y, bn_grad=bng)
+            x2, p2 = conv2d_stats(self.conv2, y, fuse=_FUSED_WGRAD, bn_grad=bng)
+            if bng and bn_pro_pays(self.bn2, self.conv3, x2, p2):  # measured per layer
+                x3, p3 = bn_relu_conv(self.bn2, self.conv3, x2, p2)
+            else:
+                y = self.bn2(x2, stats=p2) if p2 is not None and self.bn2._fast_ok(x2, None) else self.bn2(x2)
+                x3, p3 = conv1x1_bn_input(self.conv3, y, bn_grad=bng)
             if dual_bn_relu_ok(self.bn3, ds[1], x3, xd):
                 return dual_bn_relu(self.bn3, x3, p3, ds[1], xd, pd)
             return self.bn3(x3, ds[1](xd, stats=pd), stats=p3)
@@ -178,7 +182,16 @@ class Bottleneck(nn.Module):
             y = self.bn2(y)
         else:
             # bn1's output only feeds conv2: its backward reduction rides conv2's input-gradient GEMM
-            y = conv2d_bn(self.conv2, self.bn2, y, fuse=_FUSED_WGRAD, bn_grad=bng)
+            x2, p2 = conv2d_stats(self.conv2, y, fuse=_FUSED_WGRAD, bn_grad=bng)
+            if (bng and self.training and _FUSED_CONV and conv1x1_ok(self.conv3, x2) and
+                    bn_pro_pays(self.bn2, self.conv3, x2, p2)):
+                # bn2 + ReLU in conv3's operand prologue (this layer measured faster that way)
+                x3, p3 = bn_relu_conv(self.bn2, self.conv3, x2, p2)
+                return self.bn3(x3, idt, stats=p3, res_tap=tap) if self.bn3._fast_ok(x3, idt) else self.bn3(x3, idt)
+            if p2 is not None and self.bn2.training and self.bn2._fast_ok(x2, None):
+                y = self.bn2(x2, stats=p2)
+            else:
+                y = self.bn2(x2)
         return conv_bn(self.conv3, self.bn3, y, residual=idt, fuse=_FUSED_CONV, res_tap=tap, bn_grad=bng)
 
 

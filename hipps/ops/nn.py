@@ -71,6 +71,9 @@ _FUSED_XENT = _os.environ.get("HIPPS_FUSED_XENT", "1") != "0"
 _LINEAR_RESIDUAL = _os.environ.get("HIPPS_LINEAR_RESIDUAL", "1") != "0"
 # SwiGLU gate and rotary embedding of the Llama block as one HIP pass each (csrc/act.hip)
 _FUSED_ACT = _os.environ.get("HIPPS_FUSED_ACT", "1") != "0"
+# ResNet bn2 -> conv3: the BN apply + ReLU in conv3's operand prologue per layer, where measured
+# faster than the apply pass + plain GEMMs (bn_pro_pays); 0: always the apply pass
+_BN_PRO_TUNE = _os.environ.get("HIPPS_BN_PRO_TUNE", "1") != "0"
 _WG_STREAMS: dict = {}
 _WG_JOINED: dict = {}  # device -> autograd graph task whose end joins the side stream
 
@@ -213,8 +216,9 @@ class _Tuner:
 TUNER = _Tuner()
 # (block rows, block cols, LDS stages): 3 stages keep one tile's DMA in flight across every
 # K-loop barrier (gemm2.hip k_gemm NS).  Only 128x64 keeps two blocks per CU with 3 stages; the
-# others drop to one wave per SIMD and lose (profiles/gemm2_probe_r3_stages.json)
-_G2_TILES = ((128, 128, 2), (256, 256, 2), (128, 64, 2), (256, 64, 2), (128, 64, 3))
+# others drop to one wave per SIMD and lose (profiles/gemm2_probe_r3_stages.json).  (256, 256, 5):
+# the ping-pong schedule of the 256x256 tile (gemm2.hip k_gemm NS == 5)
+_G2_TILES = ((128, 128, 2), (256, 256, 2), (256, 256, 5), (128, 64, 2), (256, 64, 2), (128, 64, 3))
 
 
 def _g2_names(N: int):
@@ -557,6 +561,51 @@ def bn_relu_conv(bn, conv: nn.Conv2d, x, part):
                              conv.weight, conv.stride[0], conv.padding[0])
 
 
+def bn_pro_pays(bn, conv: nn.Conv2d, x, part) -> bool:
+    """Should conv(relu(bn(x))) for a 1x1 ``conv`` run with the BN applied in the GEMM's operand
+    prologue (_BNReluConv) rather than as its own apply pass?  Measured per layer shape, once (like
+    every tuner pick), on the real operands: the apply pass (finalize + BN + ReLU, output written)
+    + the tuned plain GEMM + the tuned weight gradient against the finalize + the prologue GEMM +
+    the prologue weight gradient (the BN output never written, but every A / X tile transformed in
+    LDS).  Globally the two were a wash (profiles/ab_r2/prologue_*: -0.23 ms of apply passes,
+    +0.10..0.17 ms of GEMM), so the choice is made layer by layer (``tools/tuner_dump.py`` lists
+    it under the key 'bnpro')."""
+    if not _BN_PRO_TUNE or part is None or conv.kernel_size != (1, 1) or not bn_relu_conv_ok(bn, conv, x):
+        return False
+    n, c, h, wd = x.shape
+    cout = conv.out_channels
+    key = ("bnpro", n, c, h, wd, cout)
+    got = TUNER.cache.get(key)
+    if got is None:
+        C = native()
+        cl = torch.channels_last
+        w = bf16_weight(conv.weight)
+        w2 = w.reshape(cout, c)
+        f32 = dict(dtype=torch.float32, device=x.device)
+        rm, rv = bn.running_mean.clone(), bn.running_var.clone()  # (the real buffers stay untouched)
+        mean, invstd, scale, shift = (torch.empty(c, **f32) for _ in range(4))
+        y = torch.empty_like(x, memory_format=cl)
+        out = torch.empty((n, cout, h, wd), dtype=torch.bfloat16, device=x.device, memory_format=cl)
+        dy = torch.randn((n, cout, h, wd), device=x.device).to(torch.bfloat16).contiguous(memory_format=cl)
+        dw = torch.empty((cout, c), **f32)
+        eps, mom = float(bn.eps), float(bn.momentum)
+
+        def apply():
+            C.bn_forward_partials(part, part.shape[2], x, None, y, bn.weight, bn.bias, rm, rv, mean, invstd, scale,
+                                  shift, c, eps, mom, True, None)
+            _conv1x1_gemm(y, w2, out, h, wd, 1, True)
+            _conv_wgrad(dy, y, dw, 1, 1, 1, 0)
+
+        def pro():
+            C.bn_finalize_partials(part, part.shape[2], n * h * wd, bn.weight, bn.bias, rm, rv, mean, invstd, scale,
+                                   shift, c, eps, mom)
+            _conv_pro_fwd(x, w, 1, 0, scale, shift)
+            _conv_wgrad_pro(dy, x, dw, 1, 1, 1, 0, scale, shift)
+
+        got = TUNER.pick(key, {"apply": apply, "pro": pro})
+    return got == "pro"
+
+
 class ResidualTap:
     """Hands a fused BN's residual gradient to the stride-1 1x1 conv that reads the same block
     input (ResNet identity blocks: x feeds conv1 and is bn3's residual).  bn3's backward stores
@@ -852,22 +901,22 @@ class _CrossEntropy(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, logits, labels, ignore_index):
-        loss_rows, lse = native().xent_forward(logits, labels, int(ignore_index))
         # the mean runs over the rows that carry a loss: not ignore_index and inside [0, V) (an
         # out-of-range label contributes no loss -- F.cross_entropy raises on it -- and is not
-        # counted either); every row ignored -> 0 / 0 = NaN, as F.cross_entropy returns
-        V = logits.shape[-1]
-        n = ((labels != ignore_index) & (labels >= 0) & (labels < V)).sum().to(torch.float32)
+        # counted either); every row ignored -> 0 / 0 = NaN, as F.cross_entropy returns.  Loss,
+        # count and mean come out of two launches (k_xent_fwd, k_xent_mean).
+        loss, n, lse = native().xent_forward(logits, labels, int(ignore_index))
         ctx.save_for_backward(logits, labels, lse, n)
         ctx.ignore = int(ignore_index)
-        return loss_rows.sum() / n
+        return loss
 
     @staticmethod
     def backward(ctx, g):
         logits, labels, lse, n = ctx.saved_tensors
         dx = torch.empty_like(logits)
-        gs = (g.to(torch.float32) / n).reshape(1).contiguous()
-        native().xent_backward(logits, labels, lse, gs, 1.0, ctx.ignore, dx)
+        if g.dtype != torch.float32 or g.numel() != 1 or not g.is_contiguous():
+            g = g.to(torch.float32).reshape(1).contiguous()
+        native().xent_backward(logits, labels, lse, g, 1.0, ctx.ignore, dx, n)
         return dx, None, None
 
 

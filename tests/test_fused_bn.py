@@ -124,6 +124,45 @@ def test_gpu_resnet_fused_vs_unfused_step(width, pro, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_gpu_bn_prologue_per_layer_choice(monkeypatch):
+    """bn2 -> conv3 with the BN in conv3's operand prologue (chosen per layer by a measurement,
+    ops.nn.bn_pro_pays) computes the same step as the apply pass + plain GEMMs: loss, every gradient
+    and the BN running statistics agree whichever way each layer goes, and the measured choice is
+    cached under a 'bnpro' tuner key."""
+    import copy
+
+    import hipps.models.resnet as rn
+    from hipps.models.resnet import Bottleneck, ResNet
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(4)
+    cl = torch.channels_last
+    base = ResNet(Bottleneck, [2, 1], num_classes=10, width=64, zero_init_residual=False).cuda().to(memory_format=cl)
+    x = torch.randn(16, 3, 64, 64, device="cuda").contiguous(memory_format=cl)
+    y = torch.randint(0, 10, (16,), device="cuda")
+    res = {}
+    for mode in ("apply", "pro", "tuned"):
+        m = copy.deepcopy(base)
+        if mode == "tuned":
+            monkeypatch.setattr(rn, "bn_pro_pays", hnn.bn_pro_pays)
+        else:
+            monkeypatch.setattr(rn, "bn_pro_pays", lambda *a, _p=(mode == "pro"): _p)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = F.cross_entropy(m(x), y)
+        loss.backward()
+        torch.cuda.synchronize()
+        res[mode] = (loss.item(), [p.grad.clone() for p in m.parameters()],
+                     [b.clone() for n, b in m.named_buffers() if "running" in n])
+    assert any(k[0] == "bnpro" for k in hnn.TUNER.cache)
+    for mode in ("pro", "tuned"):
+        assert abs(res[mode][0] - res["apply"][0]) < 1e-3
+        for a, b in zip(res[mode][1], res["apply"][1]):
+            torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-3 * max(1.0, b.abs().max().item()))
+        for a, b in zip(res[mode][2], res["apply"][2]):
+            torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("with_part3", [False, True])
 def test_gpu_dual_bn_relu_matches_fp32(with_part3):
     """relu(bn3(x3) + bnd(xd)) on _DualBNRelu (statistics from producer partials, the downsample BN

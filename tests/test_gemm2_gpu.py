@@ -206,15 +206,15 @@ def test_gemm2_3x3_bn_backward_epilogue(bm, bn, bits):
 
 
 @pytest.mark.parametrize("bm,bn", [(256, 256), (256, 128), (128, 128), (128, 64), (256, 64)])
-@pytest.mark.parametrize("kind", ["1x1", "1x1_k64", "3x3", "3x3_s2", "dgrad_bst_add"])
+@pytest.mark.parametrize("kind", ["1x1", "1x1_k64", "1x1_k128", "3x3", "3x3_s2", "dgrad_bst_add"])
 def test_gemm2_three_stage_pipeline_bitwise(bm, bn, kind):
-    """3 LDS stages (one tile's DMA in flight across every barrier, counted vmcnt) and the k-half
-    units (stages=4: 32-deep units, two in flight) accumulate in the same order as the 2-stage
-    loop: outputs and partials bit-identical, every K-tile count (1, 2, 3+ tiles: prologue /
-    drain edges)."""
+    """3 LDS stages (one tile's DMA in flight across every barrier, counted vmcnt), the k-half
+    units (stages=4: 32-deep units, two in flight) and the 256x256 ping-pong schedule (stages=5:
+    two wave groups a phase apart) accumulate in the same order as the 2-stage loop: outputs and
+    partials bit-identical, every K-tile count (1, 2, 3+ tiles: prologue / drain edges)."""
     n, h = 2, 11
-    cin, cout, k, st = {"1x1": (320, 256, 1, 1), "1x1_k64": (64, 256, 1, 1), "3x3": (128, 256, 3, 1),
-                        "3x3_s2": (64, 128, 3, 2), "dgrad_bst_add": (256, 256, 1, 1)}[kind]
+    cin, cout, k, st = {"1x1": (320, 256, 1, 1), "1x1_k64": (64, 256, 1, 1), "1x1_k128": (128, 256, 1, 1),
+                        "3x3": (128, 256, 3, 1), "3x3_s2": (64, 128, 3, 2), "dgrad_bst_add": (256, 256, 1, 1)}[kind]
     if cout % bn:
         pytest.skip("tile")
     x = _x(n, cin, h, 21)
@@ -232,7 +232,7 @@ def test_gemm2_three_stage_pipeline_bitwise(bm, bn, kind):
                      bn_invstd=torch.rand(cout, device=DEV) + 0.5, bn_scale=torch.randn(cout, device=DEV),
                      bn_shift=torch.randn(cout, device=DEV) * 0.1)
     outs = []
-    for ns in ((2, 4) if (bm, bn) == (256, 256) else (2, 3, 4)):
+    for ns in ((2, 4, 5) if (bm, bn) == (256, 256) else (2, 3, 4)):
         y = torch.full((n, cout, ho, ho), 3.0, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
         p = torch.empty(2, cout, C().gemm2_mtiles(M, cout, k * k * cin, bm), device=DEV)
         C().gemm2_conv(x, w, y, p, extra.get("add"), None, h, h, st, k, k, pad, bm, bn, extra.get("bn_x"), None,
@@ -246,6 +246,29 @@ def test_gemm2_three_stage_pipeline_bitwise(bm, bn, kind):
     if kind != "dgrad_bst_add":
         ref = F.conv2d(x.float(), w.float().view(cout, cin, k, k), stride=st, padding=pad)
         torch.testing.assert_close(outs[1][0].float(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("M,K,N", [(1000, 512, 512), (4096, 2048, 768), (300, 64, 256)])
+@pytest.mark.parametrize("bias", [False, True])
+def test_gemm2_pingpong_linear_bitwise(M, K, N, bias):
+    """The ping-pong 256x256 schedule (stages=5) on a Linear-shaped GEMM ([M, K] x [N, K]^T, several
+    M tiles, masked tail rows, optional fp32 bias epilogue): bit-identical to the 2-stage loop and
+    close to the fp32 reference."""
+    if N % 256:
+        pytest.skip("tile")
+    g = torch.Generator(device=DEV).manual_seed(M + K)
+    x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV, generator=g) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV, generator=g) if bias else None
+    outs = []
+    for ns in (2, 5):
+        y = torch.full((M, N), 7.0, device=DEV, dtype=torch.bfloat16)
+        C().gemm2_conv(x, w, y, None, None, None, 1, 1, 1, 1, 1, 0, 256, 256, stages=ns, bias=b)
+        outs.append(y)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref = x.float() @ w.float().t() + (b if bias else 0.0)
+    torch.testing.assert_close(outs[1].float(), ref, rtol=2e-2, atol=2e-2)
 
 
 @pytest.mark.parametrize("cfg", [0, 1])

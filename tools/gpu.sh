@@ -19,6 +19,7 @@
 #   emu7             bench.py --emulate-remote 7 and a plain N=1 row on the same box
 #   codec            bench/codec_bench.py
 #   tuner            tools/tuner_dump.py after a bench (which layers chose which kernel)
+#   g2probe          tools/gemm2_probe.py (every gemm2 tile vs the first core / hipBLASLt / MIOpen)
 #
 # Extra bench.py arguments for bench/prof: BENCH_ARGS; env for every step is inherited.
 set -o pipefail
@@ -124,6 +125,19 @@ for step in "$@"; do
       timeout -k 10 300 python tools/tuner_dump.py --out "$OUT/tuner.json" > "$OUT/tuner.txt" 2>&1 \
         || fail tuner "$OUT/tuner.txt"
       tail -20 "$OUT/tuner.txt" ;;
+    g2probe)
+      timeout -k 10 400 python tools/gemm2_probe.py --out "$OUT/gemm2_probe.json" > "$OUT/g2probe.log" 2>&1 \
+        || fail g2probe "$OUT/g2probe.log"
+      python3 - "$OUT/gemm2_probe.json" <<'PY'
+import json, sys
+for r in json.load(open(sys.argv[1])):
+    tf = {k[3:-3]: v for k, v in r.items() if k.startswith("g2_") and k.endswith("_TF") and k != "g2_best_TF"}
+    ref = r.get("hipblaslt_TF") or r.get("miopen_TF")
+    best = max(tf, key=tf.get)
+    print({k: r[k] for k in ("M", "K", "N", "Cin", "H", "Cout", "stride") if k in r}, "best", best, tf[best],
+          "ref", ref, "pp", tf.get("256x256s5"), "s2", tf.get("256x256s2"))
+PY
+      ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
