@@ -872,8 +872,15 @@ void launch_scan_write(hipStream_t stream, const float* src, float* rp, int64_t 
 // writes its selected (index, value) pairs in index order and leaves each element's residual in
 // LDS, and a last coalesced loop stores the residuals.  The multi-pass path above costs ~12
 // launches, which dominates at these sizes.
+// Speculative list (steady state, as P1 of the multi-pass path): with the previous call's
+// threshold T' in the workspace, one atomic-free pass counts the keys >= 0.95 T' per thread range;
+// if there are at least k and at most kCandCap of them, their indices are listed in index order
+// (block scan offsets) and the three digit passes and the selection walk that short list instead
+// of all n keys (the k-th largest key is >= 0.95 T' whenever >= k keys are).  Otherwise (first
+// call, a shrinking gradient) the full passes run.  The final key is stored back as T'.
 constexpr int kSmallMax = 32768;
 constexpr int kSmallThreads = 1024;
+constexpr int kCandCap = 3072;
 
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -923,14 +930,18 @@ __device__ __forceinline__ void wave_hist_add(uint32_t* h, uint32_t bin, bool wa
 template <typename VT>
 __global__ __launch_bounds__(kSmallThreads) void k_topk_small(const float* __restrict__ g, float* __restrict__ resid,
                                                              int n, int k, int32_t* __restrict__ idx,
-                                                             VT* __restrict__ val, int flags) {
+                                                             VT* __restrict__ val, int flags,
+                                                             SelState* __restrict__ st) {
   // flags bit 0: wave-aggregated histogram adds (else one LDS atomic per lane); bit 1: all fold
-  // loads issued before the LDS writes (else a strided loop) -- HIPPS_TOPK_SMALL=<flags> for A/B
+  // loads issued before the LDS writes (else a strided loop); bit 2: no speculative list --
+  // HIPPS_TOPK_SMALL=<flags> for A/B
   __shared__ __attribute__((aligned(16))) float sv[kSmallMax];
   __shared__ uint32_t hist[2][kHistBins];
   __shared__ uint32_t wsum[64];
   __shared__ uint32_t sel[2];  // chosen bin, keys above it
+  __shared__ uint32_t cand[kCandCap];  // speculative list: indices in index order
   const int t = threadIdx.x, wv = t >> 6;
+  const float ptf = __uint_as_float(st->prev_T & 0x7fffffffu);
   // The fold: one CU pulls up to 256 KB, so it is a latency problem -- a strided loop of dependent
   // single loads left one HBM round trip per 1024 elements exposed (~40 us cold at n = 32768).
   // Every lane issues all its 16-byte loads of g and r first (8 + 8 in flight), then writes LDS.
@@ -954,6 +965,26 @@ __global__ __launch_bounds__(kSmallThreads) void k_topk_small(const float* __res
     }
     for (int i = 4 * n4 + t; i < n; i += kSmallThreads) sv[i] = g[i] + (resid ? resid[i] : 0.f);
   }
+  // the walk: all n keys, or the speculative list of the keys >= 0.95 T'
+  int N = n;
+  bool listed = false;
+  const int per0 = ((n + kSmallThreads - 1) / kSmallThreads) | 1;  // odd: bank-conflict-free LDS walks
+  const int lo0 = min(n, t * per0), hi0 = min(n, lo0 + per0);
+  if (!(flags & 4) && ptf > 0.f && ptf < __builtin_inff()) {  // (workgroup-uniform)
+    const uint32_t lo_key = absbits(ptf * kSpecMargin);
+    __syncthreads();  // sv complete
+    uint32_t c = 0;
+    for (int i = lo0; i < hi0; ++i) c += (__float_as_uint(sv[i]) & 0x7fffffffu) >= lo_key;
+    uint32_t tot;
+    uint32_t o = block_excl_scan(c, wsum, tot);
+    if (tot >= (uint32_t)k && tot <= (uint32_t)kCandCap) {
+      for (int i = lo0; i < hi0; ++i)
+        if ((__float_as_uint(sv[i]) & 0x7fffffffu) >= lo_key) cand[o++] = (uint32_t)i;
+      N = (int)tot;
+      listed = true;
+    }
+  }
+  auto at = [&](int j) -> int { return listed ? (int)cand[j] : j; };
   uint32_t prefix = 0, pmask = 0, rem = (uint32_t)k;
 #pragma unroll
   for (int pass = 0; pass < 3; ++pass) {
@@ -961,10 +992,10 @@ __global__ __launch_bounds__(kSmallThreads) void k_topk_small(const float* __res
     for (int b = t; b < 2 * kHistBins; b += kSmallThreads) (&hist[0][0])[b] = 0u;
     __syncthreads();
     uint32_t* h = hist[pass == 0 ? (wv & 1) : 0];
-    for (int i0 = 0; i0 < n; i0 += kSmallThreads) {  // whole waves iterate together (ballots)
+    for (int i0 = 0; i0 < N; i0 += kSmallThreads) {  // whole waves iterate together (ballots)
       const int i = i0 + t;
-      const uint32_t key = i < n ? __float_as_uint(sv[i]) & 0x7fffffffu : 0u;
-      const bool want = i < n && (key & pmask) == prefix;
+      const uint32_t key = i < N ? __float_as_uint(sv[at(i)]) & 0x7fffffffu : 0u;
+      const bool want = i < N && (key & pmask) == prefix;
       if (flags & 1) wave_hist_add(h, (key >> sh) & (nb - 1), want);
       else if (want) atomicAdd(&h[(key >> sh) & (nb - 1)], 1u);
     }
@@ -994,11 +1025,12 @@ __global__ __launch_bounds__(kSmallThreads) void k_topk_small(const float* __res
   }
   // prefix = T (the k-th largest key); admit rem keys == T, lowest index first
   const uint32_t T = prefix;
-  const int per = ((n + kSmallThreads - 1) / kSmallThreads) | 1;  // odd: bank-conflict-free LDS walks
-  const int lo = min(n, t * per), hi = min(n, lo + per);
+  if (t == 0) st->prev_T = T;  // the next call's speculative bound
+  const int per = ((N + kSmallThreads - 1) / kSmallThreads) | 1;  // odd: bank-conflict-free LDS walks
+  const int lo = min(N, t * per), hi = min(N, lo + per);
   uint32_t gt = 0, eq = 0;
-  for (int i = lo; i < hi; ++i) {
-    const uint32_t key = __float_as_uint(sv[i]) & 0x7fffffffu;
+  for (int j = lo; j < hi; ++j) {
+    const uint32_t key = __float_as_uint(sv[at(j)]) & 0x7fffffffu;
     gt += key > T;
     eq += key == T;
   }
@@ -1007,7 +1039,8 @@ __global__ __launch_bounds__(kSmallThreads) void k_topk_small(const float* __res
   const uint32_t adm = eq_before >= rem ? 0u : min(eq, rem - eq_before);
   const uint32_t off = block_excl_scan(gt + adm, wsum, tot);
   uint32_t o = off, taken = 0;
-  for (int i = lo; i < hi; ++i) {
+  for (int j = lo; j < hi; ++j) {
+    const int i = at(j);
     const float v = sv[i];
     const uint32_t key = __float_as_uint(v) & 0x7fffffffu;
     bool take = key > T;
@@ -1055,10 +1088,10 @@ void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::T
     }();
     if (val.scalar_type() == at::kFloat)
       hipLaunchKernelGGL(k_topk_small<float>, 1, kSmallThreads, 0, stream, g.data_ptr<float>(), rp, (int)n, (int)k,
-                         idx.data_ptr<int32_t>(), val.data_ptr<float>(), sflags);
+                         idx.data_ptr<int32_t>(), val.data_ptr<float>(), sflags, w.st);
     else
       hipLaunchKernelGGL(k_topk_small<uint16_t>, 1, kSmallThreads, 0, stream, g.data_ptr<float>(), rp, (int)n,
-                         (int)k, idx.data_ptr<int32_t>(), (uint16_t*)val.data_ptr(), sflags);
+                         (int)k, idx.data_ptr<int32_t>(), (uint16_t*)val.data_ptr(), sflags, w.st);
     return;
   }
   const int nreg = (int)w.g.nreg;

@@ -351,6 +351,36 @@ def test_topk_small_single_workgroup(n, k, vdt, case):
     assert torch.equal(r_dev.cpu(), r_cpu)
 
 
+@pytest.mark.parametrize("n,k", [(32768, 328), (10_000, 100), (32768, 2900), (5000, 4000)])
+@pytest.mark.parametrize("vdt", [torch.float32, torch.bfloat16])
+def test_topk_small_repeated_calls_speculative_list(n, k, vdt):
+    """One workspace across calls on the single-workgroup path: call 1 runs the full digit passes
+    and leaves its threshold; later calls walk the short list of keys >= 0.95 x that threshold; a
+    10x smaller gradient (too few listed keys), an all-equal bucket (more than the list holds) and
+    ties fall back to the full passes.  Every call equals the CPU reference bit for bit."""
+    torch.manual_seed(n + k)
+    ws = torch.zeros(ops.topk_workspace_bytes(n, k), dtype=torch.uint8, device=DEV)
+    r_cpu, r_dev = torch.zeros(n), torch.zeros(n, device=DEV)
+
+    def ties():
+        x = torch.randn(n)
+        x[::3] = 2.0
+        return x
+
+    gens = [lambda: torch.randn(n), lambda: torch.randn(n), lambda: torch.randn(n) * 1.3,
+            lambda: torch.randn(n) * 0.1, lambda: torch.randn(n) * 0.1, ties, lambda: torch.full((n,), 0.5),
+            lambda: torch.randn(n), lambda: torch.randn(n)]
+    for step, gen in enumerate(gens):
+        g = gen()
+        idx, val = torch.empty(k, dtype=torch.int32), torch.empty(k, dtype=vdt)
+        ref.topk_encode(g, r_cpu, k, idx, val)
+        idd, vd = torch.empty(k, dtype=torch.int32, device=DEV), torch.empty(k, dtype=vdt, device=DEV)
+        ops.topk_encode(g.to(DEV), r_dev, k, idd, vd, ws)
+        assert torch.equal(idd.cpu(), idx), step
+        assert torch.equal(vd.cpu(), val), step
+        assert torch.equal(r_dev.cpu(), r_cpu), step
+
+
 @pytest.mark.parametrize("spec", ["fp32", "bf16", "int8", "topk:0.05", "topk_int8:0.05", "threshold:0.5:0.2"])
 def test_codec_accumulate_acquire_path_matches(spec):
     """The PS's acquire path for peer-written mailbox slots (system-scope acquire in every
