@@ -144,6 +144,7 @@ void pull_select_b(at::Tensor selb, int64_t bpub, int64_t bbuf, int64_t reading_
                    int64_t tries);
 void pull_copy_b(at::Tensor selb, at::Tensor boff, at::Tensor pub, int64_t stride, int64_t npub, bool bf16,
                  at::Tensor dst, int64_t lo, int64_t hi, c10::optional<at::Tensor> shadow);
+void emu_sweep(at::Tensor wr, at::Tensor rd, at::Tensor sink, int64_t stamp, int64_t blocks);
 void pull_done_b(at::Tensor selb, int64_t bpub, int64_t bbuf, int64_t reading_b, int64_t applied, at::Tensor sel,
                  int64_t ring_slot);
 void bind_control(pybind11::module& m);
@@ -278,6 +279,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pull_params", &hipps::rt::pull_params,
         "GPU-time AsySG-InCon pull: select newest published version, copy it, release the reader word");
   m.def("pull_select", &hipps::rt::pull_select, "GPU-time pull, stage 1: choose the version, announce the reader");
+  m.def("emu_sweep", &hipps::rt::emu_sweep, py::arg("wr"), py::arg("rd"), py::arg("sink"), py::arg("stamp"),
+        py::arg("blocks") = 8, "emulated remote traffic: write sweep of wr + read sweep of rd from a few workgroups");
   m.def("pull_copy_ptrs", &hipps::rt::pull_copy_ptrs, py::arg("sel"), py::arg("ptrs"), py::arg("npub"),
         py::arg("bf16"), py::arg("dst"), py::arg("lo"), py::arg("hi"), py::arg("shadow") = py::none());
   m.def("pull_copy_b_ptrs", &hipps::rt::pull_copy_b_ptrs, py::arg("selb"), py::arg("boff"), py::arg("ptrs"),

@@ -47,6 +47,7 @@ void thresh_accumulate(at::Tensor count, at::Tensor idx, at::Tensor val, at::Ten
                        bool acquire);
 
 namespace rt {
+void emu_sweep(at::Tensor wr, at::Tensor rd, at::Tensor sink, int64_t stamp, int64_t blocks);
 
 // codec of a bucket's message (hipps/codecs): which fields, in which order
 enum Kind : int { kDense = 0, kQ8 = 1, kTopk = 2, kTopkQ8 = 3, kThresh = 4 };
@@ -161,6 +162,7 @@ class NativePS {
       emu_in_ = c["emu_in"].cast<at::Tensor>();
       emu_sink_ = c["emu_sink"].cast<at::Tensor>();
       emu_stream_ = c["emu_stream"].cast<int64_t>();
+      emu_traffic_ = c.contains("emu_traffic") ? c["emu_traffic"].cast<bool>() : true;
       hip_ok(hipEventCreateWithFlags(&emu_ev_, hipEventDisableTiming), "hipEventCreate");
     }
     if ((int)rings_.size() != W_ || (int)remote_.size() != W_) throw std::runtime_error("native PS: rings per worker");
@@ -488,13 +490,10 @@ class NativePS {
   // per 16 (ps_async.PSAsyncEngine.flush), then the acks in order, 6 words per doorbell
   void flush() {
     if (!pend_.empty()) {
+      // (an emulated remote copy joins its real message's batch: lockstep workers' messages for
+      // a bucket arrive together)
       std::vector<std::pair<std::pair<int, double>, std::vector<const Pend*>>> groups;
-      std::vector<const Pend*> emu;
       for (const Pend& p : pend_) {
-        if (p.emu) {
-          emu.push_back(&p);
-          continue;
-        }
         auto key = std::make_pair(p.bi, p.scale);
         auto it = std::find_if(groups.begin(), groups.end(), [&](auto& g) { return g.first == key; });
         if (it == groups.end()) {
@@ -514,11 +513,6 @@ class NativePS {
           decode_into(part, b, acc, g.first.second, acq);
           bump("acc_launches");
         }
-      }
-      for (const Pend* p : emu) {  // the same bytes once more per emulated worker, one launch each
-        const BucketDesc& b = buckets_[p->bi];
-        decode_into({p}, b, acc_.narrow(0, b.lo, b.hi - b.lo), p->scale, remote_[p->worker]);
-        bump("acc_launches");
       }
       pend_.clear();
     }
@@ -608,7 +602,7 @@ class NativePS {
     for (size_t j = 0; j < words.size(); j += 6)
       ctl_.enqueue(stream_, std::vector<std::tuple<int, int, int64_t>>(
                                 words.begin() + j, words.begin() + std::min(words.size(), j + 6)));
-    if (emu_ > 0) emulate_traffic(k, bi);
+    if (emu_ > 0 && emu_traffic_) emulate_traffic(k, bi);
     if (gver >= 0) ctl_.fetch_add(UPDATES, 0, 1);
     bump("bucket_updates");
   }
@@ -619,14 +613,18 @@ class NativePS {
   void emulate_traffic(int k, int bi) {
     const BucketDesc& b = buckets_[bi];
     hipStream_t ps = reinterpret_cast<hipStream_t>(stream_), es = reinterpret_cast<hipStream_t>(emu_stream_);
-    hip_ok(hipEventRecord(emu_ev_, ps), "hipEventRecord");
-    hip_ok(hipStreamWaitEvent(es, emu_ev_, 0), "hipStreamWaitEvent");
+    if (es != ps) {
+      hip_ok(hipEventRecord(emu_ev_, ps), "hipEventRecord");
+      hip_ok(hipStreamWaitEvent(es, emu_ev_, 0), "hipStreamWaitEvent");
+    }
     c10::hip::HIPStreamGuard g(c10::hip::getStreamFromExternal(es, device_));
     at::Tensor win = emu_in_.narrow(0, b.wire_off, b.msg_nbytes);
-    for (int e = 0; e < emu_; ++e) {
-      win.fill_(e);
-      at::Tensor out = emu_sink_.narrow(0, e, 1).squeeze(0);
-      pub_pieces(b.lo, b.hi, [&](int64_t pa, int64_t pb) { at::amax_out(out, pub_view(k, pa, pb), {0}); });
+    for (int e = 0; e < emu_; ++e) {  // (few workgroups: see rt::emu_sweep)
+      bool first = true;
+      pub_pieces(b.lo, b.hi, [&](int64_t pa, int64_t pb) {
+        emu_sweep(first ? win : win.narrow(0, 0, 0), pub_view(k, pa, pb), emu_sink_, e + 1, 8);
+        first = false;
+      });
     }
   }
   static void hip_ok(hipError_t e, const char* what) {
@@ -643,6 +641,7 @@ class NativePS {
   int64_t pub_chunk_ = 0, ring_chunk_ = 0;
   at::ScalarType pub_dtype_;
   int emu_ = 0;
+  bool emu_traffic_ = true;
   int64_t emu_stream_ = 0;
   hipEvent_t emu_ev_ = nullptr;
   at::Tensor emu_in_, emu_sink_;

@@ -371,5 +371,51 @@ void pull_done_b(at::Tensor selb, int64_t bpub, int64_t bbuf, int64_t reading_b,
                      sel.data_ptr<int64_t>(), (int)ring_slot);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Rehearsal of remote workers' load on the PS's GPU (PSConfig.emulate_remote): their pushes land
+// in this GPU's mailbox over xGMI and their pulls read its publish buffers over xGMI -- HBM
+// traffic on this GPU issued by the OTHER GPUs' compute units (or copy engines), none by this
+// GPU's.  An all-CU PyTorch fill / reduction per emulated worker charged worker 0 for CU time the
+// real run never spends (29 % of its step with the native PS loop); this sweep moves the same bytes
+// from ``blocks`` workgroups (8: one per XCD, 3 % of the CUs), 16-byte stores into ``wr`` (the
+// message bytes) and 16-byte loads of ``rd`` (the published range), folded into sink[0] so the
+// loads stay live.
+__global__ __launch_bounds__(256) void k_emu_sweep(uint4* __restrict__ wr, int64_t nw, const uint4* __restrict__ rd,
+                                                   int64_t nr, uint32_t stamp, uint32_t* __restrict__ sink) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint4 v = make_uint4(stamp, stamp, stamp, stamp);
+  for (int64_t i = t0; i < nw; i += stride) wr[i] = v;
+  uint32_t x = 0;
+  int64_t i = t0;
+  for (; i + 3 * stride < nr; i += 4 * stride) {  // four loads in flight per lane
+    const uint4 a = rd[i], b = rd[i + stride], c = rd[i + 2 * stride], d = rd[i + 3 * stride];
+    x ^= a.x ^ a.w ^ b.y ^ b.z ^ c.x ^ c.w ^ d.y ^ d.z;
+  }
+  for (; i < nr; i += stride) x ^= rd[i].x;
+  if (x == 0x9e3779b9u) sink[0] = x;  // (practically never taken: keeps the loads from being dropped)
+}
+
+void emu_sweep(at::Tensor wr, at::Tensor rd, at::Tensor sink, int64_t stamp, int64_t blocks) {
+  TORCH_CHECK(wr.is_cuda() && rd.is_cuda() && sink.is_cuda() && sink.numel() * sink.element_size() >= 4 &&
+                  reinterpret_cast<uintptr_t>(sink.data_ptr()) % 4 == 0, "emu_sweep: device tensors");
+  TORCH_CHECK(wr.is_contiguous() && rd.is_contiguous(), "emu_sweep: contiguous tensors");
+  TORCH_CHECK(blocks >= 1 && blocks <= 1024, "emu_sweep: blocks");
+  // the 16-byte-aligned interior of each range (a rehearsal load: the few edge bytes do not matter)
+  auto inner = [](const at::Tensor& t, int64_t& n16) -> uintptr_t {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(t.data_ptr());
+    const uintptr_t e = a + (uintptr_t)(t.numel() * t.element_size());
+    const uintptr_t a16 = (a + 15) & ~(uintptr_t)15, e16 = e & ~(uintptr_t)15;
+    n16 = e16 > a16 ? (int64_t)((e16 - a16) / 16) : 0;
+    return a16;
+  };
+  int64_t nw = 0, nr = 0;
+  const uintptr_t w16 = inner(wr, nw), r16 = inner(rd, nr);
+  if (nw == 0 && nr == 0) return;
+  hipLaunchKernelGGL(k_emu_sweep, dim3((unsigned)blocks), dim3(256), 0, c10::hip::getCurrentHIPStream(),
+                     reinterpret_cast<uint4*>(w16), nw, reinterpret_cast<const uint4*>(r16), nr, (uint32_t)stamp,
+                     reinterpret_cast<uint32_t*>(sink.data_ptr()));
+}
+
 }  // namespace rt
 }  // namespace hipps

@@ -63,6 +63,7 @@ MASK_NONE, MASK_X, MASK_Y, MASK_BITS = 0, 1, 2, 3
 # hooks, and whose dw has the parameter's layout: autograd then stores dw as is (no accumulate or
 # layout copy on the main stream that would read it early).
 _WGRAD_SIDE = _os.environ.get("HIPPS_WGRAD_STREAM", "1") != "0"
+_WG_PRIO = int(_os.environ.get("HIPPS_WGRAD_PRIO", "0"))  # (A/B: -1 = the high-priority stream pool)
 # nn.Linear on the bf16 weight shadow with an fp32 weight gradient (_ShadowLinear); 0: F.linear
 _SHADOW_LINEAR = _os.environ.get("HIPPS_SHADOW_LINEAR", "1") != "0"
 # softmax cross-entropy of bf16 logits on csrc/xent.hip (hipps.ops.nn.cross_entropy); 0: PyTorch
@@ -140,7 +141,7 @@ def _on_wgrad_stream(param, tensors, fn):
     idx = dev.index
     side = _WG_STREAMS.get(idx)
     if side is None:
-        side = _WG_STREAMS[idx] = torch.cuda.Stream(device=dev)
+        side = _WG_STREAMS[idx] = torch.cuda.Stream(device=dev, priority=_WG_PRIO)
     cur = torch.cuda.current_stream(dev)
     # a weight used twice in one graph (weight sharing): autograd sums its gradient contributions
     # on the caller's stream before the single AccumulateGrad, so from the second one on the
@@ -176,11 +177,32 @@ def _on_wgrad_stream(param, tensors, fn):
     return out
 
 
+_TUNE_QUIET: list = []  # context-manager factories that keep other GPU work off while timing
+
+
+def add_tune_quiet(fn) -> None:
+    """Register ``fn() -> context manager`` to be entered around every tuner measurement (the
+    co-located async PS registers a pause of its thread: its kernels would otherwise share the GPU
+    with the timed candidates and skew the picks)."""
+    _TUNE_QUIET.append(fn)
+
+
+def remove_tune_quiet(fn) -> None:
+    if fn in _TUNE_QUIET:
+        _TUNE_QUIET.remove(fn)
+
+
 class _Tuner:
     """Per-shape kernel choice by measurement (like cudnn.benchmark): on the first call for a
-    key, every candidate runs once to warm up and then, with the device drained, 3 times between
-    HIP events on the current stream; the fastest name is cached.  Candidates must be side-effect free apart from writing
-    their output (every candidate writes the same values)."""
+    key, every candidate runs once to warm up; then, with the device drained and the registered
+    background work held (add_tune_quiet), ROUNDS rounds each time every candidate (2 calls between
+    HIP events, candidates interleaved) and the fastest by its best round is cached.  Interleaved
+    rounds and the minimum keep a transient neighbour (another stream's kernels) from deciding a
+    pick: with the co-located PS running free a measured 35 % slower set of weight-gradient
+    tilings was once picked (profiles/r5/emu/).  Candidates must be side-effect free apart from
+    writing their output (every candidate writes the same values)."""
+
+    ROUNDS = 3
 
     def __init__(self):
         self.cache: dict = {}
@@ -193,20 +215,30 @@ class _Tuner:
         if len(cands) == 1:
             got = next(iter(cands))
         else:
+            import contextlib
+
             for fn in cands.values():
                 fn()
-            # drain every stream first: kernels still running on another stream (the weight-gradient
-            # side stream, the PS stream) would otherwise share the GPU with the timed candidates
-            torch.cuda.synchronize()
-            t = {}
-            for name, fn in cands.items():
-                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                s.record()
-                for _ in range(3):
-                    fn()
-                e.record()
-                e.synchronize()
-                t[name] = s.elapsed_time(e) / 3
+            with contextlib.ExitStack() as quiet:
+                for q in list(_TUNE_QUIET):
+                    try:
+                        quiet.enter_context(q())
+                    except Exception:  # (a quiet hook that cannot hold: measure anyway)
+                        pass
+                # drain every stream first: kernels still running on another stream (the weight-
+                # gradient side stream, the PS stream) would otherwise share the GPU with the timing
+                torch.cuda.synchronize()
+                evs = {name: [] for name in cands}
+                for _ in range(self.ROUNDS):
+                    for name, fn in cands.items():
+                        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        s.record()
+                        fn()
+                        fn()
+                        e.record()
+                        evs[name].append((s, e))
+                torch.cuda.synchronize()
+            t = {name: min(s.elapsed_time(e) for s, e in pairs) / 2 for name, pairs in evs.items()}
             got = min(t, key=t.get)
             self.times[key] = t
         self.cache[key] = got

@@ -502,6 +502,8 @@ class PSAsyncEngine(Engine):
         self.dedicated = bool(cfg.ps_dedicated) and W > 1
         self.M = cfg.accumulate if cfg.accumulate > 0 else (W - 1 if self.dedicated else W)
         self.emu = int(cfg.emulate_remote) if W == 1 else 0  # emulated remote-worker PS load
+        # (HIPPS_EMU_TRAFFIC=0: the emulated workers' messages only, not their HBM traffic -- A/B)
+        self._emu_traffic = os.environ.get("HIPPS_EMU_TRAFFIC", "1") != "0"
         # 'auto': per-bucket versions wherever they apply (ipc transport, bucket count within the
         # control block's table, device codecs), whole-model versions otherwise
         self.p2p = cfg.async_transport == "p2p" and W > 1
@@ -633,6 +635,8 @@ class PSAsyncEngine(Engine):
             # (HIPPS_PS_PRIORITY=0: same priority as the worker's streams, for A/B)
             prio = -1 if os.environ.get("HIPPS_PS_PRIORITY", "-1") != "0" else 0
             self.ps_stream = torch.cuda.Stream(device=store.device, priority=prio) if self.cuda else None
+            for _ in range(int(os.environ.get("HIPPS_POOL_SKIP", "0")) if self.cuda else 0):
+                torch.cuda.Stream(device=store.device)  # (diagnostic: advance the stream pool)
             gs = self.gscale(self.M) / (1 + self.emu)  # emulated copies leave the average unchanged
             self.core = PSCore(self.ctl, C, W, self.nb, self.order, self.SLOTS, self.MAXSLOTS, self.M,
                                cfg.staleness, cfg.staleness_lr, gs, self._stats, bucketwise=self.bucketwise)
@@ -640,7 +644,11 @@ class PSAsyncEngine(Engine):
             self._pres_part_b = [None] * self.nb
             self._gsteps = 0
             if self.emu:
-                self._emu_stream = torch.cuda.Stream(device=store.device, priority=0) if self.cuda else None
+                # The sweeps go on the PS stream after each update (HIPPS_EMU_STREAM=1: a stream of
+                # their own -- measured 35 % slower for worker 0, profiles/r5/emu/: with that extra
+                # stream and the accumulator path the weight-gradient side stream overlapped badly)
+                own = self.cuda and os.environ.get("HIPPS_EMU_STREAM", "0") != "0"
+                self._emu_stream = torch.cuda.Stream(device=store.device, priority=0) if own else None
                 self._emu_in = torch.empty(self.plan.wire_nbytes, dtype=torch.uint8, device=store.device)
                 self._emu_sink = torch.empty(self.emu, dtype=self.pub_dtype, device=store.device)
             self.core.backend = self
@@ -685,6 +693,10 @@ class PSAsyncEngine(Engine):
             else:
                 self._thread = threading.Thread(target=self._serve_guard, name="hipps-ps", daemon=True)
                 self._thread.start()
+            if self.cuda:  # the kernel tuner holds this PS while it times candidates
+                from hipps.ops import nn as _hnn
+
+                _hnn.add_tune_quiet(self._tune_pause)
         barrier(world)
         if not self.p2p:
             # every replica starts from the PS's version 0 (ranks may have initialised differently)
@@ -1174,8 +1186,9 @@ class PSAsyncEngine(Engine):
              "remote": [self._remote(i) for i in range(self.W)],
              "buckets": buckets, "groups": groups, "chunk_slots": store.chunk_slots(), **st}
         if self.emu:
-            d.update(emu=int(self.emu), emu_in=self._emu_in, emu_sink=self._emu_sink,
-                     emu_stream=int(self._emu_stream.cuda_stream))
+            d.update(emu=int(self.emu), emu_traffic=bool(self._emu_traffic), emu_in=self._emu_in,
+                     emu_sink=self._emu_sink,
+                     emu_stream=int((self._emu_stream or self.ps_stream).cuda_stream))
         return d
 
     def _push_hyper(self):
@@ -1363,8 +1376,8 @@ class PSAsyncEngine(Engine):
         self._pend.append((bi, scale, self._bucket_msg(bi, self.slot_buf(i, slot)), self._remote(i)))
         if self._lat is not None and i == 0:
             self._lat.note(bi, seq)
-        for _ in range(self.emu):  # emulated remote workers: the same bytes, one launch each
-            self._pend.append((bi, scale, None, False))
+        for _ in range(self.emu):  # emulated remote workers: the same bytes (lockstep workers'
+            self._pend.append((bi, scale, None, False))  # messages arrive together: one batch)
 
     def ack(self, i: int, seq: int):
         for d in self._direct.values():
@@ -1376,11 +1389,9 @@ class PSAsyncEngine(Engine):
         if self._pend:
             groups = {}
             remote = {}
-            emu = []
             for bi, scale, msg, rem in self._pend:
                 if msg is None:  # emulated remote copy of the preceding real message
-                    emu.append((bi, scale, groups[(bi, scale)][-1]))
-                    continue
+                    msg = groups[(bi, scale)][-1]
                 groups.setdefault((bi, scale), []).append(msg)
                 remote.setdefault((bi, scale), []).append(rem)
             with self.tracer.phase("ps_accumulate", self.ps_stream):
@@ -1391,10 +1402,7 @@ class PSAsyncEngine(Engine):
                         # a batch holding a peer-written slot acquires at system scope first
                         kw = {"acquire": True} if any(rem[k:k + self.BATCH]) else {}
                         self.codec.accumulate(msgs[k:k + self.BATCH], self.acc[b.lo:b.hi], scale, True, **kw)
-                for bi, scale, msg in emu:
-                    b = self.plan.buckets[bi]
-                    self.codec.accumulate([msg], self.acc[b.lo:b.hi], scale, True)
-            self._stats["acc_launches"] = self._stats.get("acc_launches", 0) + len(emu) + sum(
+            self._stats["acc_launches"] = self._stats.get("acc_launches", 0) + sum(
                 (len(m) + self.BATCH - 1) // self.BATCH for m in groups.values())
             self._pend = []
         acks = self._pend_acks
@@ -1466,7 +1474,7 @@ class PSAsyncEngine(Engine):
             self._ring(self.ps_stream, words[j:j + 6])
         if self._lat is not None:
             self._lat.published(bi, self.ps_stream)
-        if self.emu:
+        if self.emu and self._emu_traffic:
             self._emulate_remote_traffic(k, bi)
         if gver is not None:
             self.ctl.fetch_add(C.F_UPDATES, 0, 1)
@@ -1533,17 +1541,19 @@ class PSAsyncEngine(Engine):
             self._ring(st, words[k:k + 6])
         if self._lat is not None:
             self._lat.published(None, st)
-        if self.emu:
+        if self.emu and self._emu_traffic:
             self._emulate_remote_traffic(b)
         self.ctl.fetch_add(C.F_UPDATES, 0, 1)
 
     def _emulate_remote_traffic(self, b: int, bi: Optional[int] = None):
         """cfg.emulate_remote: E remote workers' pushes (write sweeps of one step's wire bytes)
         and pulls (read sweeps of the new publish buffer) after this update (bucket granularity:
-        of bucket ``bi``'s message and publish range)."""
-        st = self._emu_stream
+        of bucket ``bi``'s message and publish range).  On the GPU the sweeps come from a few
+        workgroups (``emu_sweep``, runtime/pull.hip): the real remote traffic is issued by the
+        other GPUs, so it costs this GPU HBM bandwidth, not compute units."""
+        st = self._emu_stream if self._emu_stream is not None else self.ps_stream
         ctx = torch.cuda.stream(st) if st is not None else contextlib.nullcontext()
-        if st is not None:
+        if st is not None and st is not self.ps_stream:
             st.wait_stream(self.ps_stream)
         with ctx:
             lo, hi, win = 0, self.store.numel, self._emu_in
@@ -1551,6 +1561,10 @@ class PSAsyncEngine(Engine):
                 bk = self.plan.buckets[bi]
                 lo, hi, win = bk.lo, bk.hi, self.plan.message(self._emu_in, bi)
             for e in range(self.emu):
+                if st is not None:
+                    for j, (_, pa, pb) in enumerate(self._pub_pieces(lo, hi)):
+                        self.C.emu_sweep(win if j == 0 else win[:0], self.pub_view(b, pa, pb), self._emu_sink, e + 1)
+                    continue
                 win.fill_(e)
                 for _, pa, pb in self._pub_pieces(lo, hi):
                     torch.amax(self.pub_view(b, pa, pb), dim=0, out=self._emu_sink[e])
@@ -2253,11 +2267,36 @@ class PSAsyncEngine(Engine):
                 "ring_chunks": self.nrc, "pub_chunks": self.npc,
                 "direct_push": self._direct_push}
 
+    @contextlib.contextmanager
+    def _tune_pause(self):
+        """Hold the PS thread between messages (its stream drained) for one tuner measurement;
+        best effort (bounded wait, never raises): a PS that does not pause within 2 s is left
+        running and the measurement proceeds."""
+        held = False
+        th = self._thread
+        if th is not None and th.is_alive() and not self._pause_req.is_set():
+            self._pause_req.set()
+            deadline = time.time() + 2.0
+            while not self._paused.is_set() and th.is_alive() and time.time() < deadline:
+                time.sleep(0.0002)
+            held = self._paused.is_set()
+            if not held:
+                self._pause_req.clear()
+        try:
+            yield
+        finally:
+            if held:
+                self._pause_req.clear()
+
     def close(self):
         if getattr(self, "_closed", False):
             return
         self._closed = True
         super().close()
+        if self.rank == 0 and self.cuda:
+            from hipps.ops import nn as _hnn
+
+            _hnn.remove_tune_quiet(self._tune_pause)
         C = self.C
         if self._late_hook is not None:  # the model outlives the engine: drop the pull-overlap hook
             self._late_hook.remove()

@@ -18,6 +18,8 @@ def _run(rank, world, mode, steps_a, steps_b, ckpt, codec, max_delay, legacy=Non
         kw = dict(mode=mode, code=codec)
         if mode == "ps_async":
             kw["max_delay"] = max_delay
+            if world > 1:  # every update sums all workers' messages in rank order: deterministic
+                kw["accumulate"] = world
         if optim == "Adam":
             return m, hipps.Adam(m.named_parameters(), lr=0.01, **kw)
         return m, hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, **kw)
@@ -61,6 +63,22 @@ def test_resume_is_exact(tmp_path, mode, W, codec, max_delay):
     assert os.path.exists(tmp_path / "ck" / "ps.pt")
     sd = torch.load(tmp_path / "ck" / "ps.pt", weights_only=True)
     assert sd["mode"] == mode
+
+
+@pytest.mark.parametrize("steps_a,steps_b", [(3, 2), (2, 3)])
+def test_resume_is_exact_async_default_granularity(tmp_path, steps_a, steps_b):
+    """the async PS under the library defaults (ps_granularity='auto' -> per-bucket
+    versions, 16 MB buckets, stale_lookahead=0), two workers, odd step counts on either side of
+    the checkpoint: the resumed run equals the straight one bit for bit."""
+    from hipps.config import PSConfig
+
+    d = PSConfig()
+    assert (d.ps_granularity, d.bucket_mb, d.stale_lookahead) == ("auto", 16.0, 0.0)
+    straight = run_world(_run, 2, "ps_async", steps_a, steps_b, None, "fp32", 0)
+    resumed = run_world(_run, 2, "ps_async", steps_a, steps_b, str(tmp_path / "ck"), "fp32", 0)
+    for r in range(2):
+        for a, b in zip(straight[r], resumed[r]):
+            torch.testing.assert_close(a, b, rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("optim,legacy", [("SGD", "mom_started"), ("SGD", "none"), ("Adam", "none")])

@@ -18,7 +18,7 @@ from test_dist_cpu import _data, _mlp
 pytestmark = pytest.mark.gpu
 
 
-def _run(rank, world, native, steps, codec, optim="sgd", bucket_mb=0.0005, slots=0):
+def _run(rank, world, native, steps, codec, optim="sgd", bucket_mb=0.0005, slots=0, emu=0):
     import hipps
 
     os.environ["HIPPS_NATIVE_PS"] = "1" if native else "0"
@@ -26,6 +26,8 @@ def _run(rank, world, native, steps, codec, optim="sgd", bucket_mb=0.0005, slots
     m = _mlp().cuda()
     cls = hipps.SGD if optim == "sgd" else hipps.Adam
     kw = dict(lr=0.05, momentum=0.9, weight_decay=1e-4) if optim == "sgd" else dict(lr=1e-3, weight_decay=1e-4)
+    if emu:
+        kw["emulate_remote"] = emu
     opt = cls(m.named_parameters(), mode="ps_async", code=codec, bucket_mb=bucket_mb, max_delay=0,
               accumulate=world, mailbox_slots=slots, ps_granularity="bucket", **kw)
     nb = len(opt.engine.plan.buckets)
@@ -84,6 +86,22 @@ def test_native_loop_slot_reuse_bitwise():
     for r in range(3):
         for x, y in zip(a[r]["params"], b[r]["params"]):
             torch.testing.assert_close(x, y, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("codec", ["bf16", "int8"])
+def test_native_loop_emulated_remote_load(codec):
+    """emulate_remote=3 (the one-GPU rehearsal of remote workers' PS load: their messages batched
+    with the real one, their traffic as few-workgroup HBM sweeps): the native and Python loops
+    agree bit for bit, and the emulated copies leave the average gradient unchanged (a run with
+    them is close to one without)."""
+    a = run_world(_run, 1, True, 6, codec, "sgd", 0.0005, 0, 3)[0]
+    b = run_world(_run, 1, False, 6, codec, "sgd", 0.0005, 0, 3)[0]
+    c = run_world(_run, 1, True, 6, codec)[0]
+    assert a["stats"]["native_loop"] == 1 and b["stats"]["native_loop"] == 0
+    assert a["stats"]["bucket_updates"] == b["stats"]["bucket_updates"] == 6 * a["nb"]
+    for x, y, z in zip(a["params"], b["params"], c["params"]):
+        torch.testing.assert_close(x, y, rtol=0, atol=0)
+        torch.testing.assert_close(x, z, rtol=1e-3, atol=5e-5)
 
 
 def _ckpt(rank, world, path, native):
