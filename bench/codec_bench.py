@@ -90,7 +90,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--cpu", action="store_true")
-    ap.add_argument("--sizes", default="10,100,1000,10000,1000000,25557032")
+    ap.add_argument("--sizes", default="10,100,1000,10000,32768,1000000,25557032")
     ap.add_argument("--warm", action="store_true", help="do not flush the MALL between iterations")
     ap.add_argument("--specs", default=",".join(SPECS))
     ap.add_argument("--no-host", action="store_true", help="skip the host pickle/msgpack reference rows")

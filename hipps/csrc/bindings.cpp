@@ -136,7 +136,8 @@ void pull_select(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t readi
 void pull_copy_ptrs(at::Tensor sel, std::vector<int64_t> ptrs, int64_t npub, bool bf16, at::Tensor dst, int64_t lo,
                     int64_t hi, c10::optional<at::Tensor> shadow);
 void pull_copy_b_ptrs(at::Tensor selb, at::Tensor boff, std::vector<int64_t> ptrs, int64_t npub, bool bf16,
-                      at::Tensor dst, int64_t lo, int64_t hi, c10::optional<at::Tensor> shadow);
+                      at::Tensor dst, int64_t lo, int64_t hi, c10::optional<at::Tensor> shadow, int64_t b0,
+                      int64_t b1);
 void pull_copy(at::Tensor sel, at::Tensor pub, int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t lo,
                int64_t hi, c10::optional<at::Tensor> shadow);
 void pull_done(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, int64_t ring_slot);
@@ -285,7 +286,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bf16"), py::arg("dst"), py::arg("lo"), py::arg("hi"), py::arg("shadow") = py::none());
   m.def("pull_copy_b_ptrs", &hipps::rt::pull_copy_b_ptrs, py::arg("selb"), py::arg("boff"), py::arg("ptrs"),
         py::arg("npub"), py::arg("bf16"), py::arg("dst"), py::arg("lo"), py::arg("hi"),
-        py::arg("shadow") = py::none());
+        py::arg("shadow") = py::none(), py::arg("b0") = 0, py::arg("b1") = -1);
   m.def("pull_copy", &hipps::rt::pull_copy, py::arg("sel"), py::arg("pub"), py::arg("stride"), py::arg("npub"),
         py::arg("bf16"), py::arg("dst"), py::arg("lo"), py::arg("hi"), py::arg("shadow") = py::none(),
         "GPU-time pull, stage 2: copy params[lo, hi) of the chosen version (+ their bf16 shadow)");

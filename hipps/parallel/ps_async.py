@@ -580,8 +580,8 @@ class PSAsyncEngine(Engine):
         self._lver_b = [-1] * self.nb
         self._boff = self._selb = None
         if self.bucketwise and self.cuda:
-            self._boff = torch.tensor([b.lo for b in self.plan.buckets] + [store.numel], dtype=torch.int64,
-                                      device=store.device)
+            self._boff_host = [b.lo for b in self.plan.buckets] + [store.numel]
+            self._boff = torch.tensor(self._boff_host, dtype=torch.int64, device=store.device)
             self._selb = torch.full((2 * self.nb,), -1, dtype=torch.int64, device=store.device)
         self._p2p_req = None  # worker: (request seq, stage index, [works]) of the posted param recv
         self._p2p_reqs = 0
@@ -630,10 +630,12 @@ class PSAsyncEngine(Engine):
         if self.rank == 0:
             self.master = store.data.detach().clone()
             self.acc = torch.zeros_like(store.data)
-            # high priority: on a co-located PS (rank 0 also trains) the accumulate / update /
-            # publish kernels must not queue behind worker 0's forward and backward launches
-            # (HIPPS_PS_PRIORITY=0: same priority as the worker's streams, for A/B)
-            prio = -1 if os.environ.get("HIPPS_PS_PRIORITY", "-1") != "0" else 0
+            # The PS stream runs at the workers' priority: with the native loop issuing each
+            # bucket's update the moment its message lands, a high-priority stream put those
+            # kernels ahead of worker 0's backward on the co-located GPU and cost Llama-3-8B 15 %
+            # (same box: 11020 vs 12964 tokens/s, profiles/r5/llama8b/); ResNet-50 is neutral to it
+            # (profiles/r4/r4k/).  HIPPS_PS_PRIORITY=1: the high-priority stream (A/B).
+            prio = -1 if os.environ.get("HIPPS_PS_PRIORITY", "0") not in ("0", "") else 0
             self.ps_stream = torch.cuda.Stream(device=store.device, priority=prio) if self.cuda else None
             for _ in range(int(os.environ.get("HIPPS_POOL_SKIP", "0")) if self.cuda else 0):
                 torch.cuda.Stream(device=store.device)  # (diagnostic: advance the stream pool)
@@ -1951,9 +1953,14 @@ class PSAsyncEngine(Engine):
 
     def _copy_b(self, bf16: bool, lo: int, hi: int, sh):
         """Bucket-granular pull copy of params [lo, hi), one launch per publish chunk."""
+        import bisect
+
+        bh = self._boff_host
         for c, a, b in self._pub_pieces(lo, hi):
+            b0 = max(0, bisect.bisect_right(bh, a) - 1)  # the buckets overlapping [a, b): the grid's rows
+            b1 = min(self.nb, bisect.bisect_left(bh, b))
             self.C.pull_copy_b_ptrs(self._selb, self._boff, self._pub_ptrs(c, a, True), self.NPUB, bf16,
-                                    self.store.data, a, b, sh)
+                                    self.store.data, a, b, sh, b0, b1)
 
     def _copy(self, bf16: bool, lo: int, hi: int, sh):
         """Whole-model pull copy of params [lo, hi), one launch per publish chunk."""

@@ -145,3 +145,37 @@ def test_native_loop_checkpoint_resume_matches_python(tmp_path):
     for r in range(2):
         for x, y in zip(a[r]["params"], b[r]["params"]):
             torch.testing.assert_close(x, y, rtol=0, atol=0)
+
+
+def _chunked(rank, world, chunk_mb):
+    import hipps
+
+    if chunk_mb:
+        os.environ["HIPPS_IPC_CHUNK_MB"] = str(chunk_mb)
+    else:
+        os.environ.pop("HIPPS_IPC_CHUNK_MB", None)
+    torch.cuda.set_device(0)
+    m = _mlp().cuda()
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", bucket_mb=0.0005, max_delay=0,
+                    accumulate=world, ps_granularity="bucket", mailbox_slots=3)
+    info = {"npc": opt.engine.npc, "nrc": opt.engine.nrc}
+    for s in range(6):
+        x, y = _data(0, s % 4)
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x.cuda()), y.cuda()).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    opt.close()
+    return {"info": info, "params": [p.detach().cpu() for p in m.parameters()]}
+
+
+def test_chunked_publish_pull_bitwise():
+    """Publish buffers in several allocations (chunks): the GPU-time bucket pull launches once per
+    chunk over only the buckets that overlap it (pull.hip pull_copy_b_ptrs b0 / b1) and adopts the
+    same parameters, bit for bit, as from one allocation."""
+    a = run_world(_chunked, 2, 0.1, timeout=300)
+    b = run_world(_chunked, 2, 0, timeout=300)
+    assert a[0]["info"]["npc"] >= 3, a[0]["info"]  # (several buckets per chunk, buckets across chunks)
+    for r in range(2):
+        for x, y in zip(a[r]["params"], b[r]["params"]):
+            torch.testing.assert_close(x, y, rtol=0, atol=0)
