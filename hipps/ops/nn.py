@@ -64,6 +64,12 @@ MASK_NONE, MASK_X, MASK_Y, MASK_BITS = 0, 1, 2, 3
 # layout copy on the main stream that would read it early).
 _WGRAD_SIDE = _os.environ.get("HIPPS_WGRAD_STREAM", "1") != "0"
 _WG_PRIO = int(_os.environ.get("HIPPS_WGRAD_PRIO", "0"))  # (A/B: -1 = the high-priority stream pool)
+# MIOpen's backward-weights solvers may accumulate with atomics (not bitwise reproducible run to
+# run); the hipps weight-gradient kernels sum their split-M slabs in a fixed order.  MIOpen is a
+# tuner candidate for the 64-channel KxK weight gradients only with HIPPS_MIOPEN_WGRAD=1 (it won
+# no ResNet-50 bs256 shape in round 5, profiles/r5/gemm/tuner_r5n.txt; it did win a tiny test
+# shape and made two bit-identical runs differ)
+_MIOPEN_WGRAD = _os.environ.get("HIPPS_MIOPEN_WGRAD", "0") != "0"
 # nn.Linear on the bf16 weight shadow with an fp32 weight gradient (_ShadowLinear); 0: F.linear
 _SHADOW_LINEAR = _os.environ.get("HIPPS_SHADOW_LINEAR", "1") != "0"
 # softmax cross-entropy of bf16 logits on csrc/xent.hip (hipps.ops.nn.cross_entropy); 0: PyTorch
@@ -342,7 +348,7 @@ def _conv_wgrad(dy, x, dw, kh, kw, stride, pad):
                         lambda cfg=cfg, ns=ns: C.gemm2_wgrad(dy, x, dw, kh, kw, stride, pad, hi, wi, cfg, ns))
         # (fewer, longer M slabs -- gemm2_wgrad sdiv=2, half the fp32 slab traffic -- measured: no
         # shape faster by more than 1 %, profiles/r3b/tuner_sdiv.json; not a candidate)
-        if kh > 1 and cin < 128:
+        if kh > 1 and cin < 128 and _MIOPEN_WGRAD:
             cands["miopen"] = mio
         name = TUNER.pick(("wgrad", tuple(x.shape), cout, kh, kw, stride, pad), cands)
     if name.startswith("w3"):
