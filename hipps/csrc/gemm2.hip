@@ -33,6 +33,7 @@ namespace g2 {
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
@@ -137,11 +138,20 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   // stalling both waves of the SIMD at the same barrier.  Group 0 stages its own A half (freed
   // as soon as it finished tile k), group 1 the other A half and all of B (freed one phase later).
   constexpr bool PP = NS == 5;
+  // NS == 6: the 2-stage loop with v_mfma_f32_32x32x16_bf16 (256x256, 8 waves of 128x64 as 4x2
+  // 32x32 accumulators): half the MFMA instructions of the 16x16x32 form for the same work, so
+  // three times the issue slack per MFMA (24 of 32 cycles vs 8 of 16) for the DMA, LDS reads and
+  // address arithmetic (MI355X_MICROARCH.md cycle constants).  LDS chunk swizzle (row >> 1) & 7:
+  // the 16 lanes of a ds_read_b128 group read 16 different rows of one 32-row fragment at the
+  // same logical chunk, which row & 7 would pair 2-way on the 128-byte rows.
+  constexpr bool M32 = NS == 6;
+  constexpr int NSX = M32 ? 2 : NS;  // LDS stages of the generic loop
   constexpr bool PAR = (EPI & kPar) != 0;
   constexpr bool PRO = (EPI & kPro) != 0;
   static_assert(!PAR || TAPS, "kPar needs the implicit-GEMM loader");
   static_assert(!PRO || NS == 2, "kPro: 2 LDS stages");
   static_assert(!PP || (BM == 256 && BN == 256), "ping-pong: 256x256 on 8 waves");
+  static_assert(!M32 || (BM == 256 && BN == 256 && !PRO), "32x32x16 MFMA: the 256x256 tile");
   // output row of GEMM row m (kPar: the class's dx position)
   auto orow = [&](int m) -> int64_t {
     if constexpr (PAR) {
@@ -159,10 +169,10 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   constexpr int AI = BM / RPI / NW;       // A wave-instructions per stage (KH: per unit) per wave
   constexpr int BI = BN / RPI / NW;
   constexpr int EP = BN + 8;              // epilogue row pitch (elements)
-  constexpr int NSB = (KH || PP) ? 2 : NS;  // stage-sized LDS buffers
+  constexpr int NSB = (KH || PP || M32) ? 2 : NS;  // stage-sized LDS buffers
   constexpr int SCR = (NSB * STAGE * 2 > BM * EP * 2 ? NSB * STAGE * 2 : BM * EP * 2);  // bytes before the stats scratch
   static_assert(AI >= 1 && BI >= 1, "tile too small for the wave count");
-  static_assert(NS >= 2 && NS <= 5, "stages");
+  static_assert(NS >= 2 && NS <= 6, "stages");
   constexpr int NG = AI + BI;  // glds per tile (KH: per unit) per wave
   constexpr int BIP = PP ? 2 * BI : BI;  // PP: group 1 stages all of B (group 0 none)
   __shared__ __attribute__((aligned(16))) uint16_t lds[lds_bytes<BM, BN, NS>() / 2];
@@ -182,7 +192,10 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   // row in the wave-instruction's row group, logical chunk this lane fetches (the LDS slot is
   // lane-linear; the swizzle is applied on the source)
   const int lr = KH ? lane >> 2 : lane >> 3;
-  const int lc = KH ? (lane & 3) ^ khalf_swz(lr) : (lane & 7) ^ lr;
+  // (M32: the swizzle (row >> 1) & 7 of row 8m + lr is (lr >> 1) | (m & 1) << 2, and m = i*NW + w
+  // has the parity of w for every wave-instruction i of this wave)
+  const int lc = KH ? (lane & 3) ^ khalf_swz(lr)
+                    : M32 ? (lane & 7) ^ (((lr >> 1) | ((w & 1) << 2)) & 7) : (lane & 7) ^ lr;
 
   // ---- per-lane sources (fixed over the K loop) ----
   const uint16_t* a_src[AI];  // 1x1: row base + chunk; TAPS: image base
@@ -275,6 +288,16 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int FM2 = M32 ? TM / 32 : 1, FN2 = M32 ? TN / 32 : 1;  // M32: 32x32 accumulators
+  f32x16 acc32[FM2][FN2];
+  if constexpr (M32) {
+#pragma unroll
+    for (int i = 0; i < FM2; ++i)
+#pragma unroll
+      for (int j = 0; j < FN2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc32[i][j][r] = 0.f;
+  }
 
   // epilogue operands (residual-gradient addend, BN-backward x and bits) are loaded during the
   // MFMAs of the last K tile, when no DMA is in flight, if they fit the register budget
@@ -436,12 +459,12 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   } else {
     const int KT = g.K / BK;
     issue(0, 0);
-    if (NS == 3 && KT > 1) issue(1, 1);
+    if (NSX == 3 && KT > 1) issue(1, 1);
     int cur = 0;
     for (int kt = 0; kt < KT; ++kt) {
       // this wave's DMA of tile kt has landed and its reads of tile kt-1 are retired; after the
       // barrier every wave's have, so tile kt is readable and tile kt-1's buffer is free to refill
-      if (NS == 3 && kt + 1 < KT) {
+      if (NSX == 3 && kt + 1 < KT) {
         __builtin_amdgcn_s_waitcnt(waitcnt_vm(NG));  // tile kt+1 stays in flight
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       } else {
@@ -470,18 +493,54 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
       }
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (kt + NS - 1 < KT) {
-        int nxt = cur + NS - 1;
-        nxt = nxt >= NS ? nxt - NS : nxt;
-        issue(kt + NS - 1, nxt);
+      if (kt + NSX - 1 < KT) {
+        int nxt = cur + NSX - 1;
+        nxt = nxt >= NSX ? nxt - NSX : nxt;
+        issue(kt + NSX - 1, nxt);
       } else if (kt + 1 < KT) {
         // NS == 3, second-to-last tile: nothing left to issue
       } else {
         prefetch_epi();
       }
       const uint16_t* As = lds + cur * STAGE;
-      cur = cur + 1 == NS ? 0 : cur + 1;
+      cur = cur + 1 == NSX ? 0 : cur + 1;
       const uint16_t* Bs = As + BM * BK;
+      if constexpr (M32) {
+        // four 16-deep k-steps per 64-deep tile; step s+1's fragments are read while step s's
+        // MFMAs run (counted lgkmcnt)
+        bf16x8 a2[2][FM2], b2[2][FN2];
+        auto frag32 = [&](int ks, int slot) {
+          const int c = 2 * ks + (lane >> 5);
+#pragma unroll
+          for (int j = 0; j < FN2; ++j) {
+            const int row = wn * TN + j * 32 + (lane & 31);
+            b2[slot][j] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + ((c ^ ((row >> 1) & 7)) << 3));
+          }
+#pragma unroll
+          for (int i = 0; i < FM2; ++i) {
+            const int row = wm * TM + i * 32 + (lane & 31);
+            a2[slot][i] = *reinterpret_cast<const bf16x8*>(As + row * BK + ((c ^ ((row >> 1) & 7)) << 3));
+          }
+        };
+        frag32(0, 0);
+#pragma unroll
+        for (int ks = 0; ks < BK / 16; ++ks) {
+          if (ks + 1 < BK / 16) {
+            frag32(ks + 1, (ks + 1) & 1);
+            __builtin_amdgcn_s_waitcnt(waitcnt_lgkm(FM2 + FN2));
+          } else {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          }
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int i = 0; i < FM2; ++i)
+#pragma unroll
+            for (int j = 0; j < FN2; ++j)
+              acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2[ks & 1][i], b2[ks & 1][j], acc32[i][j], 0, 0, 0);
+          __builtin_amdgcn_s_setprio(0);
+        }
+        continue;
+      }
       // FPF (one wave per SIMD): both k-steps' fragments are read up front, so the second step's
       // reads are in flight while the first step's MFMAs run (counted lgkmcnt) instead of a
       // read-wait-MFMA round per step; at two waves per SIMD (256x256) the other wave covers the
@@ -534,8 +593,38 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   constexpr bool STATS = (EPI & kStats) != 0, ADD = (EPI & kAdd) != 0;
   constexpr int BST = (EPI & kBstBits) ? 2 : (EPI & kBst) ? 1 : 0;
   constexpr bool BIAS = (EPI & kBias) != 0;
+  if constexpr (M32) {  // C/D map (32x32x16): column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
 #pragma unroll
-  for (int j = 0; j < FN; ++j) {
+    for (int j = 0; j < FN2; ++j) {
+      const int col = wn * TN + j * 32 + (lane & 31);
+      const float bcol = BIAS ? g.bias[n0 + col] : 0.f;
+      float s = 0.f, qq = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM2; ++i) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const uint16_t hb = f32_to_bf16(BIAS ? acc32[i][j][r] + bcol : acc32[i][j][r]);
+          lds[row * EP + col] = hb;
+          if (STATS) {
+            const float v = bf16_to_f32(hb);
+            s += v;
+            qq = fmaf(v, v, qq);
+          }
+        }
+      }
+      if (STATS) {
+        s += __shfl_xor(s, 32, 64);
+        qq += __shfl_xor(qq, 32, 64);
+        if (lane < 32) {
+          st[(wm * BN + col) * 2] = s;
+          st[(wm * BN + col) * 2 + 1] = qq;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < (M32 ? 0 : FN); ++j) {
     const int col = wn * TN + j * 16 + (lane & 15);
     const float bcol = BIAS ? g.bias[n0 + col] : 0.f;
     float s = 0.f, qq = 0.f;
@@ -1130,7 +1219,8 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
                 c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift,
                 c10::optional<at::Tensor> bias) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "gemm2: device tensors");
-  TORCH_CHECK(stages >= 2 && stages <= 5, "gemm2: stages must be 2, 3, 4 (k-half units) or 5 (ping-pong)");
+  TORCH_CHECK(stages >= 2 && stages <= 6,
+              "gemm2: stages must be 2, 3, 4 (k-half units), 5 (ping-pong) or 6 (32x32x16 MFMA)");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
                   y.scalar_type() == at::kBFloat16, "gemm2: bf16 tensors");
   const int64_t N = w.size(0), K = w.numel() / N, Cin = K / (KH * KW);
@@ -1241,6 +1331,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
     if (NS3) HIPPS_G2S(BMc, BNc, EPc, TPc, NS3_OF(BMc, BNc)); \
     else if (NS4) HIPPS_G2S(BMc, BNc, EPc, TPc, 4);          \
     else if (NS5) HIPPS_G2S(BMc, BNc, EPc, TPc, NS5_OF(BMc, BNc)); \
+    else if (NS6) HIPPS_G2S(BMc, BNc, EPc, TPc, NS6_OF(BMc, BNc)); \
     else HIPPS_G2S(BMc, BNc, EPc, TPc, 2);                   \
   } while (0)
 #define HIPPS_G2_E(BMc, BNc)                                                                        \
@@ -1276,10 +1367,13 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
   // 3 stages where they fit the LDS (not 256x256: 3 x 64 KB)
   const bool NS3 = stages == 3, NS4 = stages == 4;  // 4: k-half units (see k_gemm)
   const bool NS5 = stages == 5;                      // 5: ping-pong wave groups (256x256 only)
+  const bool NS6 = stages == 6;                      // 6: 32x32x16 MFMA (256x256 only)
   TORCH_CHECK(!NS3 || !(BMv == 256 && BNv == 256), "gemm2: 3 stages do not fit a 256x256 tile");
   TORCH_CHECK(!NS5 || (BMv == 256 && BNv == 256), "gemm2: the ping-pong schedule (stages 5) is a 256x256 tile");
+  TORCH_CHECK(!NS6 || (BMv == 256 && BNv == 256), "gemm2: the 32x32x16 MFMA loop (stages 6) is a 256x256 tile");
 #define NS3_OF(BMc, BNc) ((BMc) == 256 && (BNc) == 256 ? 2 : 3)
 #define NS5_OF(BMc, BNc) ((BMc) == 256 && (BNc) == 256 ? 5 : 2)
+#define NS6_OF(BMc, BNc) ((BMc) == 256 && (BNc) == 256 ? 6 : 2)
   if (BMv == 256 && BNv == 256) HIPPS_G2_E(256, 256);
   else if (BMv == 256 && BNv == 128) HIPPS_G2_E(256, 128);
   else if (BMv == 128 && BNv == 128) HIPPS_G2_E(128, 128);
@@ -1291,6 +1385,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
 #undef HIPPS_G2S
 #undef NS3_OF
 #undef NS5_OF
+#undef NS6_OF
 }
 
 // Input gradient of a stride-2 3x3 / pad-1 convolution as four output-parity classes (kPar): dx

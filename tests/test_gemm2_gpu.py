@@ -232,7 +232,7 @@ def test_gemm2_three_stage_pipeline_bitwise(bm, bn, kind):
                      bn_invstd=torch.rand(cout, device=DEV) + 0.5, bn_scale=torch.randn(cout, device=DEV),
                      bn_shift=torch.randn(cout, device=DEV) * 0.1)
     outs = []
-    for ns in ((2, 4, 5) if (bm, bn) == (256, 256) else (2, 3, 4)):
+    for ns in ((2, 4, 5, 6) if (bm, bn) == (256, 256) else (2, 3, 4)):
         y = torch.full((n, cout, ho, ho), 3.0, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
         p = torch.empty(2, cout, C().gemm2_mtiles(M, cout, k * k * cin, bm), device=DEV)
         C().gemm2_conv(x, w, y, p, extra.get("add"), None, h, h, st, k, k, pad, bm, bn, extra.get("bn_x"), None,
@@ -240,9 +240,13 @@ def test_gemm2_three_stage_pipeline_bitwise(bm, bn, kind):
                        stages=ns)
         outs.append((y, p))
     torch.cuda.synchronize()
+    m32 = outs.pop() if (bm, bn) == (256, 256) else None  # stages 6: 32x32x16 MFMAs, another k order
     for o in outs[1:]:
         assert torch.equal(outs[0][0], o[0])
         assert torch.equal(outs[0][1], o[1])
+    if m32 is not None:
+        torch.testing.assert_close(m32[0].float(), outs[0][0].float(), rtol=2e-2, atol=2e-2)
+        torch.testing.assert_close(m32[1], outs[0][1], rtol=2e-2, atol=2e-1)
     if kind != "dgrad_bst_add":
         ref = F.conv2d(x.float(), w.float().view(cout, cin, k, k), stride=st, padding=pad)
         torch.testing.assert_close(outs[1][0].float(), ref, rtol=2e-2, atol=2e-2)
@@ -261,7 +265,7 @@ def test_gemm2_pingpong_linear_bitwise(M, K, N, bias):
     w = (torch.randn(N, K, device=DEV, generator=g) / K ** 0.5).to(torch.bfloat16)
     b = torch.randn(N, device=DEV, generator=g) if bias else None
     outs = []
-    for ns in (2, 5):
+    for ns in (2, 5, 6):
         y = torch.full((M, N), 7.0, device=DEV, dtype=torch.bfloat16)
         C().gemm2_conv(x, w, y, None, None, None, 1, 1, 1, 1, 1, 0, 256, 256, stages=ns, bias=b)
         outs.append(y)
@@ -269,6 +273,7 @@ def test_gemm2_pingpong_linear_bitwise(M, K, N, bias):
     assert torch.equal(outs[0], outs[1])
     ref = x.float() @ w.float().t() + (b if bias else 0.0)
     torch.testing.assert_close(outs[1].float(), ref, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(outs[2].float(), ref, rtol=2e-2, atol=2e-2)  # (32x32x16: another k order)
 
 
 @pytest.mark.parametrize("cfg", [0, 1])

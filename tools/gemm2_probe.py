@@ -26,8 +26,8 @@ GEMMS = [  # (M, K, N): ResNet-50 bs256 1x1 convolutions + large steady-state pr
 CONVS = [  # (Cin, H, Cout, stride): ResNet-50 bs256 3x3 convolutions (pad 1)
     (64, 56, 64, 1), (128, 56, 128, 2), (128, 28, 128, 1), (256, 28, 256, 2), (256, 14, 256, 1),
     (512, 14, 512, 2), (512, 7, 512, 1)]
-TILES = [(256, 256, 2), (256, 256, 5), (256, 128, 2), (256, 128, 3), (128, 128, 2), (256, 64, 2), (128, 64, 2),
-         (128, 64, 3)]  # (bm, bn, LDS stages; 4 = k-half units, 5 = ping-pong wave groups)
+TILES = [(256, 256, 2), (256, 256, 5), (256, 256, 6), (256, 128, 2), (256, 128, 3), (128, 128, 2), (256, 64, 2), (128, 64, 2),
+         (128, 64, 3)]  # (bm, bn, LDS stages; 4 = k-half units, 5 = ping-pong wave groups, 6 = 32x32x16 MFMA)
 
 
 def timeit(fn, it):

@@ -135,7 +135,7 @@ for r in json.load(open(sys.argv[1])):
     ref = r.get("hipblaslt_TF") or r.get("miopen_TF")
     best = max(tf, key=tf.get)
     print({k: r[k] for k in ("M", "K", "N", "Cin", "H", "Cout", "stride") if k in r}, "best", best, tf[best],
-          "ref", ref, "pp", tf.get("256x256s5"), "s2", tf.get("256x256s2"))
+          "ref", ref, "pp", tf.get("256x256s5"), "m32", tf.get("256x256s6"), "s2", tf.get("256x256s2"))
 PY
       ;;
     *) echo "unknown step $step"; exit 2 ;;
