@@ -63,6 +63,10 @@ def parse():
                          "plain AsySG-InCon, the reference's algorithm; -1 = auto delay compensation)")
     ap.add_argument("--mailbox-slots", type=int, default=0,
                     help="ps_async: bucket messages in flight per worker (0 = the library's auto)")
+    ap.add_argument("--no-defer-wgrad-join", action="store_true",
+                    help="join the weight-gradient side stream at the end of every backward (the library "
+                         "default); the bench's loop reads no param.grad between backward and step, so by "
+                         "default it lets the async PS order its gradient reads itself (defer_wgrad_join)")
     ap.add_argument("--gc", default=os.environ.get("BENCH_GC", "freeze"), choices=["freeze", "default", "off"],
                     help="Python garbage collector during the timed steps: 'freeze' (default) moves every object "
                          "alive after warmup (model, optimizer, autograd machinery) out of the collector's "
@@ -157,6 +161,8 @@ def main():
               accumulate=a.accumulate or None, average=True, param_wire=a.param_wire, bucket_mb=a.bucket_mb,
               mailbox_slots=a.mailbox_slots, ps_granularity=a.granularity, stale_lookahead=a.lookahead,
               async_transport=a.async_transport, ps_dedicated=dedicated)
+    if mode == "ps_async":
+        kw["defer_wgrad_join"] = not a.no_defer_wgrad_join
     if a.emulate_remote and N == 1:
         kw["emulate_remote"] = a.emulate_remote
     from hipps.parallel.ps_async import IPCOpenTimeout
@@ -374,6 +380,7 @@ def main():
                              "rank0_budget_gb": ti.get("budget_gb")}
                             if mode == "ps_async" else None),
                 "python_gc": a.gc,
+                "wgrad_join": ("deferred" if mode == "ps_async" and not a.no_defer_wgrad_join else "end of backward"),
                 "num_params": nparams,
                 "buckets": nbuckets,
             },

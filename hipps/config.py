@@ -72,9 +72,16 @@ class PSConfig:
     # emulated remote workers -- every message of worker 0 is accumulated 1 + E times (one launch
     # each; the update scales by 1/(1+E), so the math is unchanged) and every update is followed by
     # E write sweeps of the step's wire bytes (their pushes landing in HBM) and E read sweeps of the
-    # published parameters (their pulls) on a low-priority stream.  Pessimistic: on a real node
-    # that traffic moves over xGMI without running on this GPU's CUs
+    # published parameters (their pulls), from 8 workgroups on the PS stream (on a real node that
+    # traffic moves over xGMI without running on this GPU's CUs)
     emulate_remote: int = 0
+    # ps_async on GPUs: no end-of-backward join of the weight-gradient side stream into the caller's
+    # stream -- every gradient the engine reads is ordered after that stream by its per-bucket
+    # encode, so the next step's pull and forward run beside the last weight gradients (ResNet-50:
+    # the stem and layer 1, +0.7 %, profiles/r5/defer/).  Only for loops that do not read
+    # param.grad between backward() and step() (gradient clipping, logging): call
+    # opt.join_grads() before such a read
+    defer_wgrad_join: bool = False
     # samples per worker step (e.g. the batch size): adds samples_per_sec to step() data
     samples_per_step: int = 0
     # async PS failure detection: a worker silent for this long (no heartbeat, no STOP) is dead

@@ -120,6 +120,23 @@ def join_wgrad_stream(device):
 
 
 _WG_UNJOINED: set = set()  # devices whose side stream took work after the last backward's join
+# devices whose gradient consumer orders itself after the side stream (the async PS engine's
+# bucket encode waits for it per bucket): no end-of-backward join into the caller's stream, so
+# the next step's pull and forward run beside the last weight gradients (stem, layer 1)
+_WG_DEFER: set = set()
+
+
+def set_wgrad_join_deferred(device, on: bool) -> None:
+    idx = device.index if isinstance(device, torch.device) else device
+    if on:
+        _WG_DEFER.add(idx)
+    else:
+        _WG_DEFER.discard(idx)
+
+
+def wgrad_join_deferred(device) -> bool:
+    idx = device.index if isinstance(device, torch.device) else device
+    return idx in _WG_DEFER
 # Inputs of in-flight side-stream weight gradients, with an event after each: kept referenced until
 # the event has passed or the caller's stream joined the side stream, then dropped.  This replaces
 # record_stream(): the caching allocator held every such activation-sized block back until a
@@ -142,6 +159,13 @@ def _on_wgrad_stream(param, tensors, fn):
     ``param`` takes dw as is; ``tensors`` (its inputs) are recorded on that stream."""
     if not (_WGRAD_SIDE and param is not None and param.grad is None and tensors[0].is_cuda
             and not param._backward_hooks):
+        if param is not None and param.grad is not None and tensors[0].is_cuda:
+            # autograd will add this dw to the existing .grad on the caller's stream: with the
+            # end-of-backward join deferred, that .grad may still be in flight on the side stream
+            idx = tensors[0].device.index
+            if idx in _WG_DEFER and idx in _WG_UNJOINED:
+                torch.cuda.current_stream(tensors[0].device).wait_stream(_WG_STREAMS[idx])
+                _joined(idx)
         return fn()
     dev = tensors[0].device
     idx = dev.index
@@ -177,7 +201,7 @@ def _on_wgrad_stream(param, tensors, fn):
         if task < 0:  # not inside an autograd backward pass
             cur.wait_stream(side)
             _joined(idx)
-        elif _WG_JOINED.get(idx) != task:
+        elif _WG_JOINED.get(idx) != task and idx not in _WG_DEFER:
             torch.autograd.Variable._execution_engine.queue_callback(lambda: _join_wgrad(idx))
             _WG_JOINED[idx] = task
     return out

@@ -242,7 +242,8 @@ class MPI_PS(torch.optim.Optimizer):
             # joining it into the caller's stream (an autograd final callback, ops.nn._join_wgrad),
             # so only a side-stream use outside a backward pass needs the join here (one event
             # record less on the host at every step boundary)
-            if hnn.wgrad_stream(self.store.device) is not None and hnn.wgrad_join_pending(self.store.device):
+            if (hnn.wgrad_stream(self.store.device) is not None and hnn.wgrad_join_pending(self.store.device)
+                    and not hnn.wgrad_join_deferred(self.store.device)):
                 hnn.join_wgrad_stream(self.store.device)
         data = self.engine.step()
         self._refresh_shadow()
@@ -331,6 +332,15 @@ class MPI_PS(torch.optim.Optimizer):
         """Order the current stream after any parameter copy still in flight (split pull)."""
         if hasattr(self.engine, "join_pull"):
             self.engine.join_pull()
+
+    def join_grads(self):
+        """Order the current stream after every gradient still being computed on the
+        weight-gradient side stream (needed before reading ``param.grad`` between ``backward()``
+        and ``step()`` when ``defer_wgrad_join`` is on; a no-op otherwise)."""
+        if self.store.device.type == "cuda":
+            from .ops import nn as hnn
+
+            hnn.join_wgrad_stream(self.store.device)
 
     def refresh_bf16_weights(self):
         """Re-cast the bf16 weight shadow after editing parameters outside ``step()``."""

@@ -699,6 +699,13 @@ class PSAsyncEngine(Engine):
                 from hipps.ops import nn as _hnn
 
                 _hnn.add_tune_quiet(self._tune_pause)
+        if self.cuda and cfg.defer_wgrad_join:
+            # every gradient this engine reads is ordered after the weight-gradient side stream by
+            # the bucket encode itself: no end-of-backward join (PSConfig.defer_wgrad_join)
+            from hipps.ops import nn as _hnn
+
+            _hnn.set_wgrad_join_deferred(store.device, True)
+            self._deferred_join = True
         barrier(world)
         if not self.p2p:
             # every replica starts from the PS's version 0 (ranks may have initialised differently)
@@ -2300,10 +2307,14 @@ class PSAsyncEngine(Engine):
             return
         self._closed = True
         super().close()
-        if self.rank == 0 and self.cuda:
+        if self.cuda:
             from hipps.ops import nn as _hnn
 
-            _hnn.remove_tune_quiet(self._tune_pause)
+            if self.rank == 0:
+                _hnn.remove_tune_quiet(self._tune_pause)
+            if getattr(self, "_deferred_join", False):
+                _hnn.join_wgrad_stream(self.store.device)
+                _hnn.set_wgrad_join_deferred(self.store.device, False)
         C = self.C
         if self._late_hook is not None:  # the model outlives the engine: drop the pull-overlap hook
             self._late_hook.remove()

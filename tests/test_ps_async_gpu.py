@@ -367,3 +367,48 @@ def test_gpu_async_direct_push_bitwise():
     b = run_world(_tiny_overlap, 1, False, 6, "1", "0")[0]
     assert a["direct"] and not b["direct"]
     assert a["losses"] == b["losses"] and a["sha"] == b["sha"] and a["shadow"] == b["shadow"]
+
+
+def _resnet_defer(rank, world, defer, read_grads):
+    import copy  # noqa: F401
+
+    import torch.nn.functional as F
+
+    import hipps
+    from hipps.models.resnet import Bottleneck, ResNet
+
+    torch.cuda.set_device(0)
+    torch.manual_seed(7)
+    m = ResNet(Bottleneck, [1, 1], num_classes=10, width=64, zero_init_residual=False).cuda()
+    m = m.to(memory_format=torch.channels_last)
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", code="bf16", max_delay=0,
+                    defer_wgrad_join=defer)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    norms = []
+    for s in range(4):
+        x = torch.randn(16, 3, 64, 64, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
+        y = torch.randint(0, 10, (16,), device="cuda", generator=g)
+        opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = F.cross_entropy(m(x), y)
+        loss.backward()
+        if read_grads:  # a gradient read between backward and step (clipping, logging)
+            opt.join_grads()
+            norms.append(torch.stack([p.grad.float().norm() for p in m.parameters() if p.grad is not None]).sum().item())
+        opt.step()
+    torch.cuda.synchronize()
+    opt.close()
+    return {"params": [p.detach().cpu() for p in m.parameters()], "norms": norms}
+
+
+@pytest.mark.parametrize("read_grads", [False, True])
+def test_gpu_deferred_wgrad_join_bitwise(read_grads):
+    """defer_wgrad_join: no end-of-backward join of the weight-gradient side stream; the async PS's
+    per-bucket encode orders every gradient read itself, so training is bit-identical to the
+    joined default, and opt.join_grads() makes a read of param.grad between backward and step see
+    the finished gradients."""
+    a = run_world(_resnet_defer, 1, True, read_grads)[0]
+    b = run_world(_resnet_defer, 1, False, read_grads)[0]
+    for x, y in zip(a["params"], b["params"]):
+        torch.testing.assert_close(x, y, rtol=0, atol=0)
+    assert a["norms"] == b["norms"]
