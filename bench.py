@@ -73,6 +73,9 @@ def parse():
                          "generations, so periodic full collections no longer stall the host at step boundaries; "
                          "'off' disables it for the timed steps; 'default' leaves it alone")
     ap.add_argument("--no-channels-last", action="store_true")
+    ap.add_argument("--nondeterministic", action="store_true",
+                    help="let MIOpen use its non-deterministic convolution algorithms (default: "
+                         "hipps.set_deterministic, bit-for-bit repeatable steps at no measured cost)")
     ap.add_argument("--out", default=None, help="also write the JSON line to this file")
     ap.add_argument("--no-fallback", action="store_true",
                     help="fail if the ps_async IPC transport refuses to initialise (default: when the driver call "
@@ -120,6 +123,8 @@ def main():
     import hipps
     import hipps.ops.nn as hnn
     from hipps.models import build_model
+
+    hipps.set_deterministic(not a.nondeterministic)
 
     torch.manual_seed(1234 + world.rank)
     is_tf = a.model in TRANSFORMERS
@@ -380,6 +385,7 @@ def main():
                              "rank0_budget_gb": ti.get("budget_gb")}
                             if mode == "ps_async" else None),
                 "python_gc": a.gc,
+                "deterministic": not a.nondeterministic,
                 "wgrad_join": ("deferred" if mode == "ps_async" and not a.no_defer_wgrad_join else "end of backward"),
                 "num_params": nparams,
                 "buckets": nbuckets,

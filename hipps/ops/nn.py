@@ -137,6 +137,19 @@ def set_wgrad_join_deferred(device, on: bool) -> None:
 def wgrad_join_deferred(device) -> bool:
     idx = device.index if isinstance(device, torch.device) else device
     return idx in _WG_DEFER
+
+
+def set_deterministic(on: bool = True) -> None:
+    """Bit-for-bit repeatable training steps.  hipps' own kernels already reduce in a fixed order
+    once the tuner has picked (its picks -- e.g. a weight gradient's slab count -- are made once per
+    process and shape), and the MIOpen weight-gradient candidate stays out of the tuner unless
+    HIPPS_MIOPEN_WGRAD=1; what remains are the MIOpen convolutions the tuner still measures against
+    the hipps kernels (forward / input gradient of some KxK layers, the strided input gradients),
+    whose default algorithms are not run-to-run deterministic (two runs of a ResNet differed in
+    every parameter, tools/diag/determinism_probe.py).  This restricts them to MIOpen's
+    deterministic algorithms (torch.backends.cudnn.deterministic); no measurable cost on the
+    ResNet-50 bs256 headline (profiles/r5/det)."""
+    torch.backends.cudnn.deterministic = bool(on)
 # Inputs of in-flight side-stream weight gradients, with an event after each: kept referenced until
 # the event has passed or the caller's stream joined the side stream, then dropped.  This replaces
 # record_stream(): the caching allocator held every such activation-sized block back until a
