@@ -24,7 +24,11 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from hipps import codecs  # noqa: E402
 
-SPECS = ["fp32", "bf16", "int8", "int8_sr", "topk:0.01", "topk_bf16:0.01", "topk_int8:0.01", "threshold:0.02:0.05"]
+# threshold:0.02:0.05 saturates on this data (x ~ 0.01 randn with error feedback: the message is at its
+# 5 % cap from the second call on and most of the residual exceeds tau, profiles/codec/r5/ab_topk.txt);
+# threshold:0.1:0.05 stays below its cap (~1 % sent per call)
+SPECS = ["fp32", "bf16", "int8", "int8_sr", "topk:0.01", "topk_bf16:0.01", "topk_int8:0.01", "threshold:0.02:0.05",
+         "threshold:0.1:0.05"]
 
 
 _FLUSH = None

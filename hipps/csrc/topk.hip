@@ -191,7 +191,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* red4, 
   return wb + incl - v;
 }
 
-struct Regions {       // region r = chunks [r*cpw, min((r+1)*cpw, nchunks))
+struct Regions {       // region r = chunks [first(r), first(r + 1)) = [r*cpw, min((r+1)*cpw, nchunks))
   uint32_t* lval;      // list entries: raw f32 bits
   uint32_t* lidx;      //               element index
   uint32_t* coff;      // per chunk: first list entry (slot or pool)
@@ -202,6 +202,9 @@ struct Regions {       // region r = chunks [r*cpw, min((r+1)*cpw, nchunks))
   int64_t nchunks;
   int64_t cpw;         // chunks per region
   int64_t pool_off;    // first pool entry (after nreg * capw slot entries)
+  // (an even split, 1024 regions of 6-7 chunks at 25.6 M instead of 892 of 7, measured no faster:
+  // 183.8 / 184.1 vs 182.6 / 181.2 us, profiles/codec/r5/ab_topk.txt)
+  __device__ __forceinline__ int64_t first(int64_t r) const { return std::min<int64_t>(r * cpw, nchunks); }
 };
 
 constexpr uint32_t kNoBase = 0xffffffffu;
@@ -302,7 +305,7 @@ __global__ __launch_bounds__(kBlock) void k_collect(const float* __restrict__ sr
   uint32_t slot_pos = blockIdx.x * capw;
   const uint32_t slot_end = slot_pos + capw;
   uint32_t total = 0;
-  const int64_t c0 = blockIdx.x * R.cpw, c1 = std::min<int64_t>(c0 + R.cpw, R.nchunks);
+  const int64_t c0 = R.first(blockIdx.x), c1 = R.first(blockIdx.x + 1);
   float gx[PF ? kCompactPer : 1], rx[PF ? kCompactPer : 1];
   if constexpr (PF) {
     if (c0 < c1) {
@@ -384,8 +387,8 @@ constexpr int kListU = 8;  // list entries per lane per step: 8 independent load
 
 __device__ __forceinline__ RegionView load_region(const Regions& R, uint32_t* s_off, uint32_t* s_pre, uint32_t* red4) {
   RegionView v;
-  const int64_t c0 = blockIdx.x * R.cpw;
-  v.nc = (int)(std::min<int64_t>(c0 + R.cpw, R.nchunks) - c0);
+  const int64_t c0 = R.first(blockIdx.x);
+  v.nc = (int)(R.first(blockIdx.x + 1) - c0);
   // two chunks per thread (cpw <= 512)
   const int t = threadIdx.x;
   uint32_t a = 0, b = 0;
@@ -576,48 +579,41 @@ __global__ __launch_bounds__(kBlock) void k_hist_list(const float* __restrict__ 
   }
 }
 
-// P5a (top-k): per region, the counts of keys > T and == T, from its list (the full-mode twin
-// below re-reads the region's chunks instead)
-__global__ __launch_bounds__(kBlock) void k_count_list(const SelState* __restrict__ st, Regions R) {
-  __shared__ uint32_t red[4], s_off[kMaxCpw], s_pre[kMaxCpw];
-  if (st->full) return;
-  const uint32_t T = st->prefix;
-  uint32_t gt = 0, eq = 0;
-  const RegionView v = load_region(R, s_off, s_pre, red);
-  for (uint32_t j0 = threadIdx.x * kListU; j0 < v.total; j0 += blockDim.x * kListU) {
-    uint32_t e[kListU], k[kListU];
-    v.entries<kListU>(j0, e);
-#pragma unroll
-    for (int u = 0; u < kListU; ++u) k[u] = j0 + u < v.total ? (R.lval[e[u]] & 0x7fffffffu) : 0u;
-#pragma unroll
-    for (int u = 0; u < kListU; ++u) {
-      gt += k[u] > T;
-      eq += j0 + u < v.total && k[u] == T;
-    }
-  }
-  gt = block_sum(gt, red);
-  eq = block_sum(eq, red);
-  if (threadIdx.x == 0) { R.cgt[blockIdx.x] = gt; R.ceq[blockIdx.x] = eq; }
-}
-
-__global__ __launch_bounds__(kBlock) void k_count_full(const float* __restrict__ src, int64_t n,
+// P5a (top-k): per region, the counts of keys > T and == T, from its list -- or, when a pool
+// shard ran out (full mode), from the region's chunks of the bucket (one launch for both: a
+// separate full-mode twin cost an empty 1024-workgroup launch per call)
+__global__ __launch_bounds__(kBlock) void k_count_list(const float* __restrict__ src, int64_t n,
                                                        const SelState* __restrict__ st, Regions R) {
-  __shared__ uint32_t red[4];
-  if (!st->full) return;
+  __shared__ uint32_t red[4], s_off[kMaxCpw], s_pre[kMaxCpw];
   const uint32_t T = st->prefix;
   uint32_t gt = 0, eq = 0;
-  const int64_t c0 = blockIdx.x * R.cpw, c1 = std::min<int64_t>(c0 + R.cpw, R.nchunks);
-  for (int64_t c = c0; c < c1; ++c) {
-    float x[kCompactPer];
-    chunk_load(src, n, c, x);
+  if (!st->full) {
+    const RegionView v = load_region(R, s_off, s_pre, red);
+    for (uint32_t j0 = threadIdx.x * kListU; j0 < v.total; j0 += blockDim.x * kListU) {
+      uint32_t e[kListU], k[kListU];
+      v.entries<kListU>(j0, e);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t i = seg_index(c, j);
+      for (int u = 0; u < kListU; ++u) k[u] = j0 + u < v.total ? (R.lval[e[u]] & 0x7fffffffu) : 0u;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const uint32_t k = absbits(x[4 * j + e]);
-        gt += (i + e < n) && k > T;
-        eq += (i + e < n) && k == T;
+      for (int u = 0; u < kListU; ++u) {
+        gt += k[u] > T;
+        eq += j0 + u < v.total && k[u] == T;
+      }
+    }
+  } else {
+    const int64_t c0 = R.first(blockIdx.x), c1 = R.first(blockIdx.x + 1);
+    for (int64_t c = c0; c < c1; ++c) {
+      float x[kCompactPer];
+      chunk_load(src, n, c, x);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t i = seg_index(c, j);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t k = absbits(x[4 * j + e]);
+          gt += (i + e < n) && k > T;
+          eq += (i + e < n) && k == T;
+        }
       }
     }
   }
@@ -709,7 +705,7 @@ __global__ __launch_bounds__(kBlock) void k_write_regions(const float* __restric
   }
   // full mode: the region's chunks in order, ordered positions within each chunk
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t c0 = blockIdx.x * R.cpw, c1 = std::min<int64_t>(c0 + R.cpw, R.nchunks);
+  const int64_t c0 = R.first(blockIdx.x), c1 = R.first(blockIdx.x + 1);
   for (int64_t c = c0; c < c1; ++c) {
     float x[kCompactPer];
     chunk_load(src, n, c, x);
@@ -1137,8 +1133,7 @@ void topk_encode(at::Tensor g, c10::optional<at::Tensor> resid, int64_t k, at::T
     hipLaunchKernelGGL(k_topk_pick, 1, kBlock, 0, stream, 0, 9, w.st, kPickFinal);
   }
   // P5: region counts, scan, ordered write
-  hipLaunchKernelGGL(k_count_list, nreg, kBlock, 0, stream, w.st, w.R);
-  hipLaunchKernelGGL(k_count_full, nreg, kBlock, 0, stream, src, n, w.st, w.R);
+  hipLaunchKernelGGL(k_count_list, nreg, kBlock, 0, stream, src, n, w.st, w.R);
   if (val.scalar_type() == at::kFloat)
     launch_scan_write<float>(stream, src, rp, n, w, idx.data_ptr<int32_t>(), val.data_ptr<float>(), (uint32_t)k,
                              nullptr);
