@@ -371,20 +371,34 @@ __global__ __launch_bounds__(256) void k_stem_pool_bwd_reduce(StemBnPoolBwd f, c
     sa[j] = sb[j] = 0.f;
   }
   const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t v = (int64_t)blockIdx.x * 256 + t; v < total; v += stride) {
-    // 32-bit index decomposition (the host checks total < 2^32); int64 div/mod dominated
-    const uint32_t px = (uint32_t)v / G;
-    const uint32_t r = px / (uint32_t)Wo;
-    const int w = (int)(px - r * (uint32_t)Wo);
-    const int img = (int)(r / (uint32_t)Ho), h = (int)(r - (uint32_t)img * (uint32_t)Ho);
-    float dz[8], yv[8];
-    pool_dz8(f, img, h, w, g, dz);
-    ld8f(f.y + v * 8, yv);
+  // kU items per trip, every item's gathers and y loads issued before any is reduced (one item per
+  // trip left the loop latency-bound: 368 us per batch-256 stem, 1.5 TB/s; two: 274 us; four: 311)
+  constexpr int kU = 2;
+  for (int64_t v0 = (int64_t)blockIdx.x * 256 + t; v0 < total; v0 += kU * stride) {
+    float dz[kU][8], yv[kU][8];
+    bool ok[kU];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float d = fmaf(yv[j], sc[j], sh[j]) > 0.f ? dz[j] : 0.f;
-      sa[j] += d;
-      sb[j] = fmaf(d, (yv[j] - mu[j]) * is[j], sb[j]);
+    for (int u = 0; u < kU; ++u) {
+      const int64_t v = v0 + u * stride;
+      ok[u] = v < total;
+      const int64_t vc = ok[u] ? v : v0;  // (a clamped, valid item; its values are not used)
+      // 32-bit index decomposition (the host checks total < 2^32); int64 div/mod dominated
+      const uint32_t px = (uint32_t)vc / G;
+      const uint32_t r = px / (uint32_t)Wo;
+      const int w = (int)(px - r * (uint32_t)Wo);
+      const int img = (int)(r / (uint32_t)Ho), h = (int)(r - (uint32_t)img * (uint32_t)Ho);
+      pool_dz8(f, img, h, w, g, dz[u]);
+      ld8f(f.y + vc * 8, yv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (!ok[u]) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = fmaf(yv[u][j], sc[j], sh[j]) > 0.f ? dz[u][j] : 0.f;
+        sa[j] += d;
+        sb[j] = fmaf(d, (yv[u][j] - mu[j]) * is[j], sb[j]);
+      }
     }
   }
 #pragma unroll
@@ -418,6 +432,20 @@ __device__ __forceinline__ u32x4 bnpool_dy8(const StemBnPoolBwd& f, int img, int
     o[j] = fmaf(f.ca[c], d, fmaf(f.ck1[c], yv[j], f.ck0[c]));
   }
   return u32x4{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]), pack_bf16x2(o[6], o[7])};
+}
+
+// dy = BN-backward(pool-backward(dp)) written out (mode 2 of stem_bnpool_backward): one lane = 8
+// channels of one stem-output pixel, the same bits the weight gradient's fused staging computes
+__global__ __launch_bounds__(256) void k_stem_bnpool_dy(StemBnPoolBwd f, int Ho, int Wo, int64_t total,
+                                                        uint16_t* __restrict__ dy) {
+  constexpr int G = kCout / 8;
+  const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= total) return;
+  const uint32_t px = (uint32_t)v / G, g = (uint32_t)v - px * G;  // (the host checks total < 2^32)
+  const uint32_t r = px / (uint32_t)Wo;
+  const int w = (int)(px - r * (uint32_t)Wo);
+  const int img = (int)(r / (uint32_t)Ho), h = (int)(r - (uint32_t)img * (uint32_t)Ho);
+  *reinterpret_cast<u32x4*>(dy + v * 8) = bnpool_dy8(f, img, h, w, (int)g, Ho, Wo);
 }
 
 template <bool PRO>
@@ -694,13 +722,16 @@ void stem_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw) {
   launch_stem_wgrad(dy, x, dw, nullptr);
 }
 
-// Backward of pool(relu(bn(stem(x)))) without materialising the pool or BN input gradients:
+// Backward of pool(relu(bn(stem(x)))) without materialising the pool gradient (nor, with
+// materialize_dy = false, the BN input gradient):
 // dp [imgs, 64, Hp, Wp] bf16 + code (max pool tap codes) + y (stem output, BN input); BN vectors
 // f32 [64] (weight, mean, invstd, scale, shift).  Writes dbn_w, dbn_b (BN parameter gradients) and
-// dw (stem weight gradient, f32 channels-last [64, 3, 7, 7]).
+// dw (stem weight gradient, f32 channels-last [64, 3, 7, 7]).  materialize_dy: the BN input
+// gradient is written by one elementwise pass and the plain weight gradient reads it (the gather
+// inside the weight gradient's staging is latency-bound); otherwise the staging recomputes it.
 void stem_bnpool_backward(at::Tensor dp, at::Tensor code, at::Tensor y, at::Tensor x, at::Tensor bn_weight,
                           at::Tensor mean, at::Tensor invstd, at::Tensor scale, at::Tensor shift, at::Tensor dbn_w,
-                          at::Tensor dbn_b, at::Tensor dw) {
+                          at::Tensor dbn_b, at::Tensor dw, bool materialize_dy) {
   int64_t Hi, Wi, Ho, Wo;
   check_geom(x, Hi, Wi, Ho, Wo);
   const int64_t imgs = x.size(0), Hp = (Ho - 1) / 2 + 1, Wp = (Wo - 1) / 2 + 1;
@@ -722,7 +753,8 @@ void stem_bnpool_backward(at::Tensor dp, at::Tensor code, at::Tensor y, at::Tens
                    scale.data_ptr<float>(), shift.data_ptr<float>(), nullptr, nullptr, nullptr, (int)Hp, (int)Wp};
   const int64_t total = imgs * Ho * Wo * (kCout / 8);
   TORCH_CHECK(total < (int64_t(1) << 32), "stem_bnpool_backward: size");
-  const int nrb = (int)std::max<int64_t>(1, std::min<int64_t>(256 * 4, (total + 255) / 256));
+  // 8 resident blocks per CU (18 KB of LDS each): twice the loads in flight of 4
+  const int nrb = (int)std::max<int64_t>(1, std::min<int64_t>(256 * 8, (total + 255) / 256));
   auto part = at::empty({2, kCout, (int64_t)nrb}, scale.options());
   hipLaunchKernelGGL(k_stem_pool_bwd_reduce, nrb, 256, 0, stream, fb, mean.data_ptr<float>(), invstd.data_ptr<float>(),
                      (int)Ho, (int)Wo, total, part[0].data_ptr<float>(), part[1].data_ptr<float>());
@@ -731,7 +763,14 @@ void stem_bnpool_backward(at::Tensor dp, at::Tensor code, at::Tensor y, at::Tens
   fb.ca = coef[0].data_ptr<float>();
   fb.ck1 = coef[1].data_ptr<float>();
   fb.ck0 = coef[2].data_ptr<float>();
-  launch_stem_wgrad(y, x, dw, &fb);
+  if (materialize_dy) {
+    auto dy = at::empty_like(y, y.options(), at::MemoryFormat::ChannelsLast);
+    hipLaunchKernelGGL(k_stem_bnpool_dy, (unsigned)((total + 255) / 256), 256, 0, stream, fb, (int)Ho, (int)Wo, total,
+                       (uint16_t*)dy.data_ptr());
+    launch_stem_wgrad(dy, x, dw, nullptr);
+  } else {
+    launch_stem_wgrad(y, x, dw, &fb);
+  }
 }
 
 }  // namespace hipps

@@ -42,10 +42,12 @@ _FUSED_WGRAD = _os.environ.get("HIPPS_FUSED_WGRAD", "1") != "0"
 _FUSED_STEM = _FUSED
 # stem BN apply + ReLU folded into the max pool's load (the BN output is never materialised)
 _FUSED_STEM_POOL = _FUSED_STEM and _os.environ.get("HIPPS_FUSED_STEMPOOL", "1") != "0"
-# ... and the stem's backward as one pass pair (no pool / BN input gradients materialised).
-# Opt-in: it moves 1.9 GB/step less, but the recomputed pool gather in the weight gradient's dy
-# staging is latency-bound (A/B on one box: 10308 on / 10342 off img/s, profiles/ab_r2/stembwd_*)
-_FUSED_STEM_BWD = _FUSED_STEM_POOL and _os.environ.get("HIPPS_FUSED_STEMBWD", "0") != "0"
+# ... and the stem's backward as one node (_StemBlock): the pool gradient is never materialised; 2 (default)
+# writes the BN input gradient in one pass for the plain weight gradient, 1 recomputes it inside the
+# weight gradient's staging (latency-bound there: 10308 vs 10342 img/s in round 2,
+# profiles/ab_r2/stembwd_*; 12020 / 12037 vs 12171 / 12089 in round 5, profiles/r5/stem/), 0 = pool backward + BN
+# backward kernels
+_FUSED_STEM_BWD = _FUSED_STEM_POOL and _os.environ.get("HIPPS_FUSED_STEMBWD", "2") != "0"
 _FUSED_PRO = _FUSED_CONV and _os.environ.get("HIPPS_FUSED_PRO", "0") != "0"
 # downsample blocks: the downsample BN applied inside bn3's apply pass (its output, the residual,
 # is never materialised) and both BNs' backward in two passes (ops.nn._DualBNRelu)

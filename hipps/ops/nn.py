@@ -81,6 +81,11 @@ _FUSED_ACT = _os.environ.get("HIPPS_FUSED_ACT", "1") != "0"
 # ResNet bn2 -> conv3: the BN apply + ReLU in conv3's operand prologue per layer, where measured
 # faster than the apply pass + plain GEMMs (bn_pro_pays); 0: always the apply pass
 _BN_PRO_TUNE = _os.environ.get("HIPPS_BN_PRO_TUNE", "1") != "0"
+# _StemBlock backward (HIPPS_FUSED_STEMBWD=2, the default): the BN input gradient written by one
+# elementwise pass on the recomputed pool gradient, read by the plain stem weight gradient (=1:
+# recomputed inside the weight gradient's staging instead; 0: no _StemBlock, the pool gradient and
+# the BN backward materialised)
+_STEM_BWD_DY = _os.environ.get("HIPPS_FUSED_STEMBWD", "2") == "2"
 _WG_STREAMS: dict = {}
 _WG_JOINED: dict = {}  # device -> autograd graph task whose end joins the side stream
 
@@ -1922,7 +1927,8 @@ class _StemBlock(torch.autograd.Function):
         dout = dout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dbw, dbb = torch.empty_like(bn_w), torch.empty_like(bn_w)
         dw = torch.empty((64, 3, 7, 7), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
-        native().stem_bnpool_backward(dout, code, y, x, bn_w, mean, invstd, scale, shift, dbw, dbb, dw)
+        native().stem_bnpool_backward(dout, code, y, x, bn_w, mean, invstd, scale, shift, dbw, dbb, dw,
+                                      materialize_dy=_STEM_BWD_DY)
         if ctx.wdtype != torch.float32:
             dw = dw.to(ctx.wdtype)
         return None, dw, dbw, dbb, None, None, None, None

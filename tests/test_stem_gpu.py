@@ -132,7 +132,8 @@ def test_bn_relu_pool_bit_identical_to_bn_then_pool(shape):
 
 @pytest.mark.parametrize("fused_bwd", [True, False])
 def test_resnet_stem_route(fused_bwd, monkeypatch):
-    """The ResNet stem runs _StemBlock (HIPPS_FUSED_STEMBWD=1) or _StemConv + _BNReluPool (default)."""
+    """The ResNet stem runs _StemBlock (default, HIPPS_FUSED_STEMBWD=2 or 1) or _StemConv +
+    _BNReluPool (HIPPS_FUSED_STEMBWD=0)."""
     from hipps.models import resnet as R
     from hipps.models import resnet50
 
@@ -149,11 +150,15 @@ def test_resnet_stem_route(fused_bwd, monkeypatch):
     assert m.bn1.weight.grad is not None and torch.isfinite(m.conv1.weight.grad).all()
 
 
+@pytest.mark.parametrize("materialize_dy", [False, True])
 @pytest.mark.parametrize("n", [4, 2])
-def test_stem_block_matches_unfused_ops(n):
+def test_stem_block_matches_unfused_ops(n, materialize_dy, monkeypatch):
     """_StemBlock (fused stem backward: BN reductions on a recomputed pool gradient, dy staged into
-    the weight gradient) vs _StemConv -> FusedBatchNorm2d -> MaxPool2d on the hipps kernels:
-    identical forward and running statistics; gradients equal up to the BN reduction order."""
+    the weight gradient -- or, materialize_dy (HIPPS_FUSED_STEMBWD=2), written by one elementwise
+    pass and read by the plain weight gradient) vs _StemConv -> FusedBatchNorm2d -> MaxPool2d on the
+    hipps kernels: identical forward and running statistics; gradients equal up to the BN
+    reduction order."""
+    monkeypatch.setattr(hnn, "_STEM_BWD_DY", materialize_dy)
     torch.manual_seed(n)
     x = _cl(torch.randn(n, 3, 224 if n == 4 else 96, 224 if n == 4 else 64, device=DEV).to(torch.bfloat16))
     res = []
