@@ -127,7 +127,7 @@ void stem_forward(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Te
 void stem_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw);
 void stem_bnpool_backward(at::Tensor dp, at::Tensor code, at::Tensor y, at::Tensor x, at::Tensor bn_weight,
                           at::Tensor mean, at::Tensor invstd, at::Tensor scale, at::Tensor shift, at::Tensor dbn_w,
-                          at::Tensor dbn_b, at::Tensor dw, bool materialize_dy);
+                          at::Tensor dbn_b, at::Tensor dw, bool materialize_dy, bool quad);
 namespace rt {
 void pull_params(at::Tensor sel, int64_t pub_ver, int64_t buf_ver, int64_t reading, int64_t applied, at::Tensor pub,
                  int64_t stride, int64_t npub, bool bf16, at::Tensor dst, int64_t ring_slot, int64_t tries);
@@ -247,7 +247,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "materialised (the BN input gradient only with materialize_dy)",
         py::arg("dp"), py::arg("code"), py::arg("y"), py::arg("x"), py::arg("bn_weight"), py::arg("mean"),
         py::arg("invstd"), py::arg("scale"), py::arg("shift"), py::arg("dbn_w"), py::arg("dbn_b"), py::arg("dw"),
-        py::arg("materialize_dy") = false);
+        py::arg("materialize_dy") = false, py::arg("quad") = true);
   m.def("stem_wgrad", &hipps::stem_wgrad, "ResNet stem 7x7/s2/p3 weight gradient on MFMA (fp32 dW, deterministic)");
   m.def("conv_wgrad", &hipps::conv_wgrad, "MFMA KxK conv weight gradient (implicit GEMM, split-M, fp32 dW)");
   m.def("maxpool3s2_forward", &hipps::maxpool3s2_forward,

@@ -351,6 +351,48 @@ __device__ __forceinline__ void pool_dz8(const StemBnPoolBwd& f, int img, int h,
   for (int j = 0; j < 8; ++j) dz[j] = bf16_to_f32(f32_to_bf16(acc[j]));
 }
 
+// dz (bf16-rounded) of the 2x2 block of input pixels (2kb + a, 2jb + b), a, b in {0, 1}, channels
+// 8g .. 8g+7 (pixel p = 2a + b).  All four lie in the same four windows (kb | kb+1) x (jb | jb+1) --
+// the odd-odd pixel's candidates -- so the block loads 4 codes + 4 dp vectors instead of up to 16.
+// Each pixel sums its windows in pool_dz8's order, adding +0 for the others (a window of the
+// next row / column covers only the block's odd rows / columns): bit-identical dz.
+__device__ __forceinline__ void pool_dz8_quad(const StemBnPoolBwd& f, int img, int kb, int jb, int g,
+                                              float dz[4][8]) {
+  uint32_t c[4];
+  u32x4 d[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int oh = kb + (r >> 1), ow = jb + (r & 1);
+    const bool ok = oh < f.Hp && ow < f.Wp;
+    const int64_t o = ok ? ((int64_t)(img * f.Hp + oh) * f.Wp + ow) * (kCout / 8) + g : 0;
+    const uint32_t cv = f.code[o];
+    const u32x4 dv = *reinterpret_cast<const u32x4*>(f.dp + o * 8);
+    c[r] = ok ? cv : 0xffffffffu;
+    d[r] = dv;
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int a = p >> 1, b = p & 1;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      // a window of the next row (column) holds only odd-row (odd-column) pixels of the block
+      const bool in = (r >> 1) <= a && (r & 1) <= b;
+      const uint32_t tap = in ? (uint32_t)((a - 2 * (r >> 1) + 1) * 3 + (b - 2 * (r & 1) + 1)) : 0xffffffffu;
+      const uint32_t dw[4] = {d[r].x, d[r].y, d[r].z, d[r].w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = __uint_as_float(j & 1 ? dw[j >> 1] & 0xffff0000u : dw[j >> 1] << 16);
+        acc[j] += ((c[r] >> (4 * j)) & 15u) == tap ? v : 0.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dz[p][j] = bf16_to_f32(f32_to_bf16(acc[j]));
+  }
+}
+
 // BN backward reductions over dz * relu'(y): a[c] = sum dz', b[c] = sum dz' * (y - mean) * invstd,
 // per block partials pa/pb[c][block] (the format k_bn_finalize_bwd combines).  Lane = 8 channels of
 // one pixel; the grid stride is a multiple of the 8 channel groups, so each lane keeps its group.
@@ -419,6 +461,70 @@ __global__ __launch_bounds__(256) void k_stem_pool_bwd_reduce(StemBnPoolBwd f, c
   }
 }
 
+// k_stem_pool_bwd_reduce over 2x2 pixel blocks (pool_dz8_quad): item = (block, channel group),
+// total = imgs * Hb * Wb * 8 with Hb = ceil(Ho / 2); the four pixels accumulate in row-major order
+__global__ __launch_bounds__(256) void k_stem_pool_bwd_reduce_q(StemBnPoolBwd f, const float* __restrict__ mean,
+                                                                const float* __restrict__ invstd, int Ho, int Wo,
+                                                                int64_t total, float* __restrict__ pa,
+                                                                float* __restrict__ pb) {
+  __shared__ float red[2][256][9];  // +1 pad
+  constexpr int G = kCout / 8;
+  const int t = threadIdx.x, g = t % G;
+  const int Hb = (Ho + 1) >> 1, Wb = (Wo + 1) >> 1;
+  float sc[8], sh[8], mu[8], is[8], sa[8], sb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = f.scale[8 * g + j];
+    sh[j] = f.shift[8 * g + j];
+    mu[j] = mean[8 * g + j];
+    is[j] = invstd[8 * g + j];
+    sa[j] = sb[j] = 0.f;
+  }
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + t; v < total; v += stride) {
+    const uint32_t q = (uint32_t)v / G;  // (the host checks total < 2^32)
+    const uint32_t r = q / (uint32_t)Wb;
+    const int jb = (int)(q - r * (uint32_t)Wb);
+    const int img = (int)(r / (uint32_t)Hb), kb = (int)(r - (uint32_t)img * (uint32_t)Hb);
+    float dz[4][8], yv[4][8];
+    bool ok[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int h = 2 * kb + (p >> 1), w = 2 * jb + (p & 1);
+      ok[p] = h < Ho && w < Wo;
+      const int hc = ok[p] ? h : 2 * kb, wc = ok[p] ? w : 2 * jb;  // (a valid pixel; values unused)
+      ld8f(f.y + (((int64_t)img * Ho + hc) * Wo + wc) * kCout + 8 * g, yv[p]);
+    }
+    pool_dz8_quad(f, img, kb, jb, g, dz);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      if (!ok[p]) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = fmaf(yv[p][j], sc[j], sh[j]) > 0.f ? dz[p][j] : 0.f;
+        sa[j] += d;
+        sb[j] = fmaf(d, (yv[p][j] - mu[j]) * is[j], sb[j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][t][j] = sa[j];
+    red[1][t][j] = sb[j];
+  }
+  __syncthreads();
+  if (t < kCout) {
+    const int gg = t >> 3, j = t & 7;
+    float a = 0.f, c = 0.f;
+    for (int l = gg; l < 256; l += G) {
+      a += red[0][l][j];
+      c += red[1][l][j];
+    }
+    pa[(int64_t)t * gridDim.x + blockIdx.x] = a;
+    pb[(int64_t)t * gridDim.x + blockIdx.x] = c;
+  }
+}
+
 // staged dy chunk (bf16 x 8) of pixel (img, h, w), channel group g: the BN backward apply on the
 // recomputed dz, bit-for-bit the expression of k_bn_apply_bwd<MASK_X>
 __device__ __forceinline__ u32x4 bnpool_dy8(const StemBnPoolBwd& f, int img, int h, int w, int g, int Ho, int Wo) {
@@ -446,6 +552,43 @@ __global__ __launch_bounds__(256) void k_stem_bnpool_dy(StemBnPoolBwd f, int Ho,
   const int w = (int)(px - r * (uint32_t)Wo);
   const int img = (int)(r / (uint32_t)Ho), h = (int)(r - (uint32_t)img * (uint32_t)Ho);
   *reinterpret_cast<u32x4*>(dy + v * 8) = bnpool_dy8(f, img, h, w, (int)g, Ho, Wo);
+}
+
+// k_stem_bnpool_dy over 2x2 pixel blocks (pool_dz8_quad): the same bits per pixel
+__global__ __launch_bounds__(256) void k_stem_bnpool_dy_q(StemBnPoolBwd f, int Ho, int Wo, int64_t total,
+                                                          uint16_t* __restrict__ dy) {
+  constexpr int G = kCout / 8;
+  const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= total) return;
+  const int Hb = (Ho + 1) >> 1, Wb = (Wo + 1) >> 1;
+  const uint32_t q = (uint32_t)v / G, g = (uint32_t)v - q * G;
+  const uint32_t r = q / (uint32_t)Wb;
+  const int jb = (int)(q - r * (uint32_t)Wb);
+  const int img = (int)(r / (uint32_t)Hb), kb = (int)(r - (uint32_t)img * (uint32_t)Hb);
+  float dz[4][8], yv[4][8];
+  bool ok[4];
+  int64_t off[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int h = 2 * kb + (p >> 1), w = 2 * jb + (p & 1);
+    ok[p] = h < Ho && w < Wo;
+    off[p] = (((int64_t)img * Ho + (ok[p] ? h : 2 * kb)) * Wo + (ok[p] ? w : 2 * jb)) * kCout + 8 * g;
+    ld8f(f.y + off[p], yv[p]);
+  }
+  pool_dz8_quad(f, img, kb, jb, (int)g, dz);
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    if (!ok[p]) continue;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = 8 * g + j;
+      const float d = fmaf(yv[p][j], f.scale[c], f.shift[c]) > 0.f ? dz[p][j] : 0.f;
+      o[j] = fmaf(f.ca[c], d, fmaf(f.ck1[c], yv[p][j], f.ck0[c]));
+    }
+    *reinterpret_cast<u32x4*>(dy + off[p]) =
+        u32x4{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]), pack_bf16x2(o[6], o[7])};
+  }
 }
 
 template <bool PRO>
@@ -731,7 +874,7 @@ void stem_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw) {
 // inside the weight gradient's staging is latency-bound); otherwise the staging recomputes it.
 void stem_bnpool_backward(at::Tensor dp, at::Tensor code, at::Tensor y, at::Tensor x, at::Tensor bn_weight,
                           at::Tensor mean, at::Tensor invstd, at::Tensor scale, at::Tensor shift, at::Tensor dbn_w,
-                          at::Tensor dbn_b, at::Tensor dw, bool materialize_dy) {
+                          at::Tensor dbn_b, at::Tensor dw, bool materialize_dy, bool quad) {
   int64_t Hi, Wi, Ho, Wo;
   check_geom(x, Hi, Wi, Ho, Wo);
   const int64_t imgs = x.size(0), Hp = (Ho - 1) / 2 + 1, Wp = (Wo - 1) / 2 + 1;
@@ -756,8 +899,16 @@ void stem_bnpool_backward(at::Tensor dp, at::Tensor code, at::Tensor y, at::Tens
   // 8 resident blocks per CU (18 KB of LDS each): twice the loads in flight of 4
   const int nrb = (int)std::max<int64_t>(1, std::min<int64_t>(256 * 8, (total + 255) / 256));
   auto part = at::empty({2, kCout, (int64_t)nrb}, scale.options());
-  hipLaunchKernelGGL(k_stem_pool_bwd_reduce, nrb, 256, 0, stream, fb, mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                     (int)Ho, (int)Wo, total, part[0].data_ptr<float>(), part[1].data_ptr<float>());
+  // quad: 2x2 pixel blocks per item (one window gather shared by four pixels); else per pixel
+  const int64_t qtotal = imgs * ((Ho + 1) / 2) * ((Wo + 1) / 2) * (kCout / 8);
+  if (quad)
+    hipLaunchKernelGGL(k_stem_pool_bwd_reduce_q, nrb, 256, 0, stream, fb, mean.data_ptr<float>(),
+                       invstd.data_ptr<float>(), (int)Ho, (int)Wo, qtotal, part[0].data_ptr<float>(),
+                       part[1].data_ptr<float>());
+  else
+    hipLaunchKernelGGL(k_stem_pool_bwd_reduce, nrb, 256, 0, stream, fb, mean.data_ptr<float>(),
+                       invstd.data_ptr<float>(), (int)Ho, (int)Wo, total, part[0].data_ptr<float>(),
+                       part[1].data_ptr<float>());
   auto coef = at::empty({3, kCout}, scale.options());
   bn_finalize_bwd_partials(part, nrb, imgs * Ho * Wo, bn_weight, mean, invstd, dbn_w, dbn_b, coef);
   fb.ca = coef[0].data_ptr<float>();
@@ -765,8 +916,12 @@ void stem_bnpool_backward(at::Tensor dp, at::Tensor code, at::Tensor y, at::Tens
   fb.ck0 = coef[2].data_ptr<float>();
   if (materialize_dy) {
     auto dy = at::empty_like(y, y.options(), at::MemoryFormat::ChannelsLast);
-    hipLaunchKernelGGL(k_stem_bnpool_dy, (unsigned)((total + 255) / 256), 256, 0, stream, fb, (int)Ho, (int)Wo, total,
-                       (uint16_t*)dy.data_ptr());
+    if (quad)
+      hipLaunchKernelGGL(k_stem_bnpool_dy_q, (unsigned)((qtotal + 255) / 256), 256, 0, stream, fb, (int)Ho, (int)Wo,
+                         qtotal, (uint16_t*)dy.data_ptr());
+    else
+      hipLaunchKernelGGL(k_stem_bnpool_dy, (unsigned)((total + 255) / 256), 256, 0, stream, fb, (int)Ho, (int)Wo,
+                         total, (uint16_t*)dy.data_ptr());
     launch_stem_wgrad(dy, x, dw, nullptr);
   } else {
     launch_stem_wgrad(y, x, dw, &fb);

@@ -86,6 +86,8 @@ _BN_PRO_TUNE = _os.environ.get("HIPPS_BN_PRO_TUNE", "1") != "0"
 # recomputed inside the weight gradient's staging instead; 0: no _StemBlock, the pool gradient and
 # the BN backward materialised)
 _STEM_BWD_DY = _os.environ.get("HIPPS_FUSED_STEMBWD", "2") == "2"
+# ... its pool-gradient recompute over 2x2 pixel blocks (one window gather per four pixels); 0: per pixel
+_STEM_QUAD = _os.environ.get("HIPPS_STEM_QUAD", "1") != "0"
 _WG_STREAMS: dict = {}
 _WG_JOINED: dict = {}  # device -> autograd graph task whose end joins the side stream
 
@@ -1928,7 +1930,7 @@ class _StemBlock(torch.autograd.Function):
         dbw, dbb = torch.empty_like(bn_w), torch.empty_like(bn_w)
         dw = torch.empty((64, 3, 7, 7), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
         native().stem_bnpool_backward(dout, code, y, x, bn_w, mean, invstd, scale, shift, dbw, dbb, dw,
-                                      materialize_dy=_STEM_BWD_DY)
+                                      materialize_dy=_STEM_BWD_DY, quad=_STEM_QUAD)
         if ctx.wdtype != torch.float32:
             dw = dw.to(ctx.wdtype)
         return None, dw, dbw, dbb, None, None, None, None

@@ -150,17 +150,22 @@ def test_resnet_stem_route(fused_bwd, monkeypatch):
     assert m.bn1.weight.grad is not None and torch.isfinite(m.conv1.weight.grad).all()
 
 
+@pytest.mark.parametrize("quad", [True, False])
 @pytest.mark.parametrize("materialize_dy", [False, True])
-@pytest.mark.parametrize("n", [4, 2])
-def test_stem_block_matches_unfused_ops(n, materialize_dy, monkeypatch):
+@pytest.mark.parametrize("n", [4, 2, 3])
+def test_stem_block_matches_unfused_ops(n, materialize_dy, quad, monkeypatch):
     """_StemBlock (fused stem backward: BN reductions on a recomputed pool gradient, dy staged into
     the weight gradient -- or, materialize_dy (HIPPS_FUSED_STEMBWD=2), written by one elementwise
     pass and read by the plain weight gradient) vs _StemConv -> FusedBatchNorm2d -> MaxPool2d on the
     hipps kernels: identical forward and running statistics; gradients equal up to the BN
     reduction order."""
     monkeypatch.setattr(hnn, "_STEM_BWD_DY", materialize_dy)
+    monkeypatch.setattr(hnn, "_STEM_QUAD", quad)
     torch.manual_seed(n)
-    x = _cl(torch.randn(n, 3, 224 if n == 4 else 96, 224 if n == 4 else 64, device=DEV).to(torch.bfloat16))
+    # n = 3: an odd number of stem output rows (98 x 72 -> 49 x 36; pooled 25 x 18), so the 2x2 blocks
+    # of the quad kernels have missing pixels and missing windows at the edges
+    hw = {4: (224, 224), 2: (96, 64), 3: (98, 72)}[n]
+    x = _cl(torch.randn(n, 3, hw[0], hw[1], device=DEV).to(torch.bfloat16))
     res = []
     for fused in (True, False):
         torch.manual_seed(1)
