@@ -21,6 +21,8 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
+#include <cstdlib>
+
 namespace hipps {
 
 namespace {
@@ -93,6 +95,85 @@ __global__ __launch_bounds__(kBlock) void k_maxpool3s2_fwd(const uint16_t* __res
   }
   st8(y + v * 8, m);
   code[v] = c;
+}
+
+// Two horizontally adjacent outputs per lane (wo = 2 wp, 2 wp + 1): their windows share the middle
+// input column, so 3 x 5 taps are loaded (and, BN variant, normalised) instead of 2 x 9.  Per
+// output the same scan order, ties and NaN rule as k_maxpool3s2_fwd, so values and codes are equal.
+template <typename I, bool BN = false>
+__global__ __launch_bounds__(kBlock) void k_maxpool3s2_fwd2(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                            uint32_t* __restrict__ code, int64_t total, int H, int W,
+                                                            int Ho, int Wo, int G, const float* __restrict__ scale,
+                                                            const float* __restrict__ shift) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= total) return;
+  const int Wp = (Wo + 1) >> 1;
+  I p = (I)v;
+  const int g = (int)(p % (I)G);
+  p /= (I)G;
+  const int wp = (int)(p % (I)Wp);
+  p /= (I)Wp;
+  const int ho = (int)(p % (I)Ho);
+  const int64_t n = (int64_t)(p / (I)Ho);
+  const int wo0 = 2 * wp;
+  const bool two = wo0 + 1 < Wo;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = BN ? scale[g * 8 + j] : 1.f;
+    sh[j] = BN ? shift[g * 8 + j] : 0.f;
+  }
+  float xv[3][5][8];
+  bool okr[3], okc[5];
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const int h = 2 * ho - 1 + kh;
+    okr[kh] = h >= 0 && h < H;
+    const int hc = min(max(h, 0), H - 1);
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      const int w = 2 * wo0 - 1 + c;
+      okc[c] = w >= 0 && w < W;
+      const int wc = min(max(w, 0), W - 1);
+      ld8(x + (((n * H + hc) * W + wc) * G + g) * 8, xv[kh][c]);
+    }
+  }
+  if (BN) {
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int c = 0; c < 5; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          xv[kh][c][j] = bf16_to_f32(f32_to_bf16(fmaxf(fmaf(xv[kh][c][j], sc[j], sh[j]), 0.f)));
+  }
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+    if (o == 1 && !two) break;
+    float m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+    uint32_t cd = 0;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int c = 2 * o + kw;
+        const bool ok = okr[kh] && okc[c];
+        const uint32_t t = kh * 3 + kw;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (ok && (xv[kh][c][j] > m[j] || __builtin_isnan(xv[kh][c][j]))) {
+            m[j] = xv[kh][c][j];
+            cd = (cd & ~(15u << (4 * j))) | (t << (4 * j));
+          }
+        }
+      }
+    }
+    const int64_t out = ((n * Ho + ho) * Wo + wo0 + o) * G + g;
+    st8(y + out * 8, m);
+    code[out] = cd;
+  }
 }
 
 template <typename I>
@@ -171,16 +252,27 @@ void maxpool3s2_forward(at::Tensor x, at::Tensor y, at::Tensor code, c10::option
     sh = shift->data_ptr<float>();
   }
   if (total == 0) return;
-  const int grid = (int)((total + kBlock - 1) / kBlock);
   auto stream = c10::hip::getCurrentHIPStream();
-#define HIPPS_MP(I, B)                                                                                        \
-  hipLaunchKernelGGL((k_maxpool3s2_fwd<I, B>), grid, kBlock, 0, stream, (const uint16_t*)x.data_ptr(),          \
-                     (uint16_t*)y.data_ptr(), (uint32_t*)code.data_ptr(), total, (int)H, (int)W, (int)Ho, (int)Wo, \
-                     (int)(C / 8), sc, sh)
-  if (total < (int64_t(1) << 31)) {
-    if (bn) HIPPS_MP(uint32_t, true); else HIPPS_MP(uint32_t, false);
+  // two outputs per lane (k_maxpool3s2_fwd2); HIPPS_POOL_PAIR=0: one per lane
+  static const bool pair = [] {
+    const char* e = std::getenv("HIPPS_POOL_PAIR");
+    return !(e && e[0] == '0');
+  }();
+  const int64_t items = pair ? N * Ho * ((Wo + 1) / 2) * (C / 8) : total;
+  const int grid = (int)((items + kBlock - 1) / kBlock);
+#define HIPPS_MP(K, I, B)                                                                                     \
+  hipLaunchKernelGGL((K<I, B>), grid, kBlock, 0, stream, (const uint16_t*)x.data_ptr(), (uint16_t*)y.data_ptr(), \
+                     (uint32_t*)code.data_ptr(), items, (int)H, (int)W, (int)Ho, (int)Wo, (int)(C / 8), sc, sh)
+  if (pair) {
+    if (total < (int64_t(1) << 31)) {
+      if (bn) HIPPS_MP(k_maxpool3s2_fwd2, uint32_t, true); else HIPPS_MP(k_maxpool3s2_fwd2, uint32_t, false);
+    } else {
+      if (bn) HIPPS_MP(k_maxpool3s2_fwd2, int64_t, true); else HIPPS_MP(k_maxpool3s2_fwd2, int64_t, false);
+    }
+  } else if (total < (int64_t(1) << 31)) {
+    if (bn) HIPPS_MP(k_maxpool3s2_fwd, uint32_t, true); else HIPPS_MP(k_maxpool3s2_fwd, uint32_t, false);
   } else {
-    if (bn) HIPPS_MP(int64_t, true); else HIPPS_MP(int64_t, false);
+    if (bn) HIPPS_MP(k_maxpool3s2_fwd, int64_t, true); else HIPPS_MP(k_maxpool3s2_fwd, int64_t, false);
   }
 #undef HIPPS_MP
 }
