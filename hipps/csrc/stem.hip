@@ -462,7 +462,8 @@ __global__ __launch_bounds__(256) void k_stem_pool_bwd_reduce(StemBnPoolBwd f, c
 }
 
 // k_stem_pool_bwd_reduce over 2x2 pixel blocks (pool_dz8_quad): item = (block, channel group),
-// total = imgs * Hb * Wb * 8 with Hb = ceil(Ho / 2); the four pixels accumulate in row-major order
+// total = imgs * Hb * Wb * 8 with Hb = ceil(Ho / 2); the four pixels accumulate in row-major order.
+// One block per trip (178 us per batch-256 stem; two per trip measured 204 us)
 __global__ __launch_bounds__(256) void k_stem_pool_bwd_reduce_q(StemBnPoolBwd f, const float* __restrict__ mean,
                                                                 const float* __restrict__ invstd, int Ho, int Wo,
                                                                 int64_t total, float* __restrict__ pa,
