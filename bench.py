@@ -55,9 +55,7 @@ def parse():
                          "xGMI pull; the PS keeps the fp32 master, workers compute in bf16 anyway)")
     ap.add_argument("--momentum", type=float, default=0.9)
     ap.add_argument("--bucket-mb", type=float, default=None,
-                    help="bucket size in MB (default: 8 for ResNet-50 -- same-box A/Bs +0.35 %% on average over "
-                         "16 and 32, 4 slower, the emulated N=8 PS load no worse: profiles/r5/bucket/ -- else the "
-                         "library's, PSConfig.bucket_mb)")
+                    help="bucket size in MB (default: the library's, PSConfig.bucket_mb)")
     ap.add_argument("--granularity", default=None, choices=["model", "bucket", "auto"],
                     help="ps_async update/publication granularity (default: the library's, PSConfig.ps_granularity)")
     ap.add_argument("--lookahead", type=float, default=None,
@@ -163,7 +161,7 @@ def main():
     if a.lookahead is None:
         a.lookahead = dflt.stale_lookahead
     if a.bucket_mb is None:
-        a.bucket_mb = 8.0 if a.model == "resnet50" and "HIPPS_BUCKET_MB" not in os.environ else dflt.bucket_mb
+        a.bucket_mb = dflt.bucket_mb
     kw = dict(lr=a.lr, momentum=a.momentum, weight_decay=5e-5, mode=mode, code=a.codec,
               accumulate=a.accumulate or None, average=True, param_wire=a.param_wire, bucket_mb=a.bucket_mb,
               mailbox_slots=a.mailbox_slots, ps_granularity=a.granularity, stale_lookahead=a.lookahead,
