@@ -101,6 +101,10 @@ void bn_finalize_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tensor we
 void maxpool3s2_backward(at::Tensor dy, at::Tensor code, at::Tensor dx);
 std::vector<at::Tensor> xent_forward(at::Tensor logits, at::Tensor labels, int64_t ignore_index);
 void colsum_bf16(at::Tensor x, at::Tensor out);
+std::vector<at::Tensor> attn_forward(at::Tensor q, at::Tensor k, at::Tensor v, bool causal, double scale,
+                                     c10::optional<at::Tensor> kvlen);
+std::vector<at::Tensor> attn_backward(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o,
+                                      at::Tensor lse, bool causal, double scale, c10::optional<at::Tensor> kvlen);
 void swiglu_forward(at::Tensor a, at::Tensor b, at::Tensor c);
 void ln_forward(at::Tensor x, at::Tensor w, at::Tensor b, at::Tensor y, at::Tensor mean, at::Tensor rstd, double eps);
 void ln_backward(at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor rstd, at::Tensor w, at::Tensor dx,
@@ -265,6 +269,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_apply", &hipps::rope_apply, py::arg("x"), py::arg("y"), py::arg("cos"), py::arg("sin"), py::arg("S"),
         py::arg("hd"), py::arg("sign") = 1.0, "rotary embedding of interleaved pairs, fp32 tables (act.hip)");
   m.def("colsum_bf16", &hipps::colsum_bf16, "fp32 column sums of a bf16 [rows, cols] matrix (bias gradients)");
+  m.def("attn_forward", &hipps::attn_forward, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"),
+        py::arg("scale"), py::arg("kv_len") = py::none(),
+        "flash attention forward on MFMA: q [B,Sq,Hq,D], k/v [B,Sk,Hkv,D] bf16 -> (o, lse) (attn.hip)");
+  m.def("attn_backward", &hipps::attn_backward, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),
+        py::arg("o"), py::arg("lse"), py::arg("causal"), py::arg("scale"), py::arg("kv_len") = py::none(),
+        "flash attention backward (deterministic dQ and dK/dV kernels) -> (dq, dk, dv) (attn.hip)");
   m.def("xent_forward", &hipps::xent_forward,
         "fused softmax cross-entropy over bf16 logits: (mean loss, counted rows, per-row log-sum-exp)");
   m.def("xent_backward", &hipps::xent_backward, py::arg("logits"), py::arg("labels"), py::arg("lse"), py::arg("gout"),

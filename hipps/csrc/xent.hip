@@ -57,6 +57,35 @@ __device__ __forceinline__ void block_lse(float& m, float& s) {
 }
 }  // namespace
 
+// one 16-byte chunk (8 bf16) into the running (max, sum-exp): one rescale per chunk, not per element
+__device__ __forceinline__ void online8(float& m, float& s, const uint4 u) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+  float x[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    x[2 * j] = __uint_as_float(w[j] << 16);
+    x[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+  }
+  const float cm = fmaxf(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])), fmaxf(fmaxf(x[4], x[5]), fmaxf(x[6], x[7])));
+  if (cm == -INFINITY) return;  // (all masked)
+  if (cm > m) {
+    s *= __expf(m - cm);  // m == -inf: s == 0 stays 0
+    m = cm;
+  }
+  float a = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a += __expf(x[j] - m);
+  s += a;
+}
+
+// elements before a row's first 16-byte boundary (rows of an odd-sized vocab start at any 2-byte
+// offset: BERT's V = 30522 puts 3 of every 4 rows off the boundary, which used to send the whole
+// row down the 2-byte scalar path)
+__device__ __forceinline__ int64_t head_elems(const uint16_t* row, int64_t V) {
+  const int64_t h = ((16 - (reinterpret_cast<uintptr_t>(row) & 15)) & 15) >> 1;
+  return h < V ? h : V;
+}
+
 // loss[r] = lse(x_r) - x_r[label_r] (0 for ignored rows), lse[r] kept for the backward
 __global__ __launch_bounds__(kXBlock) void k_xent_fwd(const uint16_t* __restrict__ x, const int64_t* __restrict__ labels,
                                                       int64_t V, int64_t ignore, float* __restrict__ loss,
@@ -64,18 +93,18 @@ __global__ __launch_bounds__(kXBlock) void k_xent_fwd(const uint16_t* __restrict
   const int64_t r = blockIdx.x;
   const uint16_t* row = x + r * V;
   float m = -INFINITY, s = 0.f;
-  const bool vec = ((reinterpret_cast<uintptr_t>(row) & 15) == 0);
-  const int64_t nv = vec ? V / 8 : 0;
-  for (int64_t v = threadIdx.x; v < nv; v += kXBlock) {
-    const uint4 u = reinterpret_cast<const uint4*>(row)[v];
-    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      online(m, s, __uint_as_float(w[j] << 16));
-      online(m, s, __uint_as_float(w[j] & 0xffff0000u));
-    }
+  const int64_t h = head_elems(row, V);
+  if (threadIdx.x < h) online(m, s, bf16_to_f32(row[threadIdx.x]));
+  const uint4* vrow = reinterpret_cast<const uint4*>(row + h);
+  const int64_t nv = (V - h) >> 3;
+  int64_t v = threadIdx.x;
+  for (; v + kXBlock < nv; v += 2 * kXBlock) {  // two chunks in flight per lane
+    const uint4 a = vrow[v], b = vrow[v + kXBlock];
+    online8(m, s, a);
+    online8(m, s, b);
   }
-  for (int64_t i = nv * 8 + threadIdx.x; i < V; i += kXBlock) online(m, s, bf16_to_f32(row[i]));
+  if (v < nv) online8(m, s, vrow[v]);
+  for (int64_t i = h + nv * 8 + threadIdx.x; i < V; i += kXBlock) online(m, s, bf16_to_f32(row[i]));
   block_lse(m, s);
   if (threadIdx.x == 0) {
     const float l = m + __logf(s);
@@ -97,10 +126,17 @@ __global__ __launch_bounds__(kXBlock) void k_xent_bwd(const uint16_t* __restrict
   const bool skip = lab == ignore || lab < 0 || lab >= V;
   const float l = lse[r];
   const float k = skip ? 0.f : scale * gscale[0] / (ndiv ? ndiv[0] : 1.f);
-  const bool vec = ((reinterpret_cast<uintptr_t>(row) | reinterpret_cast<uintptr_t>(drow)) & 15) == 0;
-  const int64_t nv = vec ? V / 8 : 0;
-  for (int64_t v = threadIdx.x; v < nv; v += kXBlock) {
-    const uint4 u = reinterpret_cast<const uint4*>(row)[v];
+  // the vector loop needs x and dx rows at the same offset from a 16-byte boundary (true for
+  // tensors of one shape allocated by the caching allocator); then peel the head elements
+  const bool vec = ((reinterpret_cast<uintptr_t>(row) ^ reinterpret_cast<uintptr_t>(drow)) & 15) == 0;
+  const int64_t h = vec ? head_elems(row, V) : V;
+  for (int64_t i = threadIdx.x; i < h; i += kXBlock)
+    drow[i] = f32_to_bf16((__expf(bf16_to_f32(row[i]) - l) - (i == lab ? 1.f : 0.f)) * k);
+  if (!vec) return;
+  const int64_t nv = (V - h) >> 3;
+  const uint4* vrow = reinterpret_cast<const uint4*>(row + h);
+  uint4* vd = reinterpret_cast<uint4*>(drow + h);
+  auto one = [&](int64_t v, const uint4 u) {
     const uint32_t w[4] = {u.x, u.y, u.z, u.w};
     float g[8];
 #pragma unroll
@@ -108,13 +144,19 @@ __global__ __launch_bounds__(kXBlock) void k_xent_bwd(const uint16_t* __restrict
       g[2 * j] = __expf(__uint_as_float(w[j] << 16) - l);
       g[2 * j + 1] = __expf(__uint_as_float(w[j] & 0xffff0000u) - l);
     }
-    const int64_t i0 = v * 8;
+    const int64_t i0 = h + v * 8;
 #pragma unroll
     for (int j = 0; j < 8; ++j) g[j] = (g[j] - (i0 + j == lab ? 1.f : 0.f)) * k;
-    reinterpret_cast<uint4*>(drow)[v] =
-        make_uint4(pack_bf16x2(g[0], g[1]), pack_bf16x2(g[2], g[3]), pack_bf16x2(g[4], g[5]), pack_bf16x2(g[6], g[7]));
+    vd[v] = make_uint4(pack_bf16x2(g[0], g[1]), pack_bf16x2(g[2], g[3]), pack_bf16x2(g[4], g[5]), pack_bf16x2(g[6], g[7]));
+  };
+  int64_t v = threadIdx.x;
+  for (; v + kXBlock < nv; v += 2 * kXBlock) {
+    const uint4 a = vrow[v], b = vrow[v + kXBlock];
+    one(v, a);
+    one(v + kXBlock, b);
   }
-  for (int64_t i = nv * 8 + threadIdx.x; i < V; i += kXBlock)
+  if (v < nv) one(v, vrow[v]);
+  for (int64_t i = h + nv * 8 + threadIdx.x; i < V; i += kXBlock)
     drow[i] = f32_to_bf16((__expf(bf16_to_f32(row[i]) - l) - (i == lab ? 1.f : 0.f)) * k);
 }
 

@@ -7,7 +7,9 @@
               vocab 128256) = 8.03 B params.  Config 5 ("Llama-3 8B pure-DP async PS").
   *-tiny      same code, small widths, for CPU tests.
 
-Attention is ``F.scaled_dot_product_attention`` (the ROCm flash / mem-efficient kernels); the
+Attention is ``hipps.ops.nn.attention`` (csrc/attn.hip: MFMA flash attention, forward and a
+deterministic backward, causal + grouped-query heads for Llama, key padding for BERT) on the
+[B, S, H, hd] views of the projection outputs (no transposes); the
 projections and MLPs are ``hipps.ops.nn.Linear`` (per shape hipBLASLt or the hipps gemm2 cores,
 reading the engine's bf16 weight shadow, fp32 weight gradients written directly, the residual add
 in the output projections' epilogue; plain ``nn.Linear`` behaviour without a shadow).  The loss
@@ -72,10 +74,16 @@ class BertLayer(nn.Module):
         h = self.heads
 
         def split(t):
-            return t.view(B, S, h, D // h).transpose(1, 2)
+            return t.view(B, S, h, D // h)
 
-        a = F.scaled_dot_product_attention(split(self.q(x)), split(self.k(x)), split(self.v(x)), attn_mask=mask)
-        a = a.transpose(1, 2).reshape(B, S, D)
+        if mask is None or (torch.is_tensor(mask) and mask.dtype == torch.int32 and mask.dim() == 1):
+            # [B, S, H, hd] views of the projections straight into the hipps flash-attention kernels
+            # (csrc/attn.hip); ``mask`` may be the int32 [B] key lengths of a padded batch
+            a = hnn.attention(split(self.q(x)), split(self.k(x)), split(self.v(x)), kv_len=mask)
+        else:
+            a = F.scaled_dot_product_attention(split(self.q(x)).transpose(1, 2), split(self.k(x)).transpose(1, 2),
+                                               split(self.v(x)).transpose(1, 2), attn_mask=mask).transpose(1, 2)
+        a = a.reshape(B, S, D)
         # residual adds ride in the output projections (GEMM epilogue / hipBLASLt C)
         x = _ln(self.attn_ln, self.attn_out(a, residual=x))
         return _ln(self.out_ln, self.out(F.gelu(self.inter(x)), residual=x))
@@ -106,13 +114,14 @@ class Bert(nn.Module):
         if isinstance(m, nn.Linear) and m.bias is not None:
             nn.init.zeros_(m.bias)
 
-    def forward(self, ids, labels=None):
+    def forward(self, ids, labels=None, kv_len=None):
+        """``kv_len``: optional int32 [B] valid lengths of a right-padded batch (key padding mask)."""
         B, S = ids.shape
         pos = torch.arange(S, device=ids.device)
         x = self.word(ids) + self.pos(pos)[None] + self.tok_type(torch.zeros_like(ids))
         x = _ln(self.emb_ln, x)
         for layer in self.layers:
-            x = layer(x)
+            x = layer(x, kv_len)
         pooled = torch.tanh(self.pooler(x[:, 0]))
         if not self.mlm:
             return x, pooled
@@ -191,9 +200,8 @@ class LlamaBlock(nn.Module):
         k = self.wk(h).view(B, S, c.kv_heads, hd)
         v = self.wv(h).view(B, S, c.kv_heads, hd)
         q, k = _rope(q, cos, sin), _rope(k, cos, sin)
-        q, k, v = (t.transpose(1, 2) for t in (q, k, v))
-        a = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=c.heads != c.kv_heads)
-        x = x + self.wo(a.transpose(1, 2).reshape(B, S, D))
+        a = hnn.attention(q, k, v, causal=True)  # [B, S, H, hd]; causal + GQA in csrc/attn.hip
+        x = x + self.wo(a.reshape(B, S, D))
         h = self.ffn_norm(x)
         return x + self.w2(hnn.swiglu(self.w1(h), self.w3(h)))
 

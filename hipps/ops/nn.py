@@ -1007,9 +1007,82 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, ignore_index: int 
     the fused kernel for contiguous bf16 device logits [.., vocab]; the PyTorch route otherwise."""
     V = logits.shape[-1]
     if (_FUSED_XENT and logits.is_cuda and logits.dtype == torch.bfloat16 and labels.dtype == torch.int64
-            and labels.numel() * V == logits.numel()):
+            and labels.numel() * V == logits.numel() and 0 < labels.numel() < (1 << 24) and V > 0):
+        # (the kernel's row count limits; empty batches and larger ones take the PyTorch route)
         return _CrossEntropy.apply(logits.reshape(-1, V).contiguous(), labels.reshape(-1).contiguous(), ignore_index)
     return F.cross_entropy(logits.float().reshape(-1, V), labels.reshape(-1), ignore_index=ignore_index)
+
+
+# ---------------------------------------------------------------------------------- attention
+# flash attention on the hipps MFMA kernels (csrc/attn.hip) instead of PyTorch SDPA (whose ROCm
+# route is aotriton, Triton-generated code); HIPPS_FUSED_ATTN=0 keeps SDPA for A/B runs
+_FUSED_ATTN = _os.environ.get("HIPPS_FUSED_ATTN", "1") != "0"
+
+
+def _attn_rows_ok(t: torch.Tensor) -> bool:
+    return (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 4 and t.stride(3) == 1
+            and all(x % 8 == 0 for x in t.stride()[:3]) and t.data_ptr() % 16 == 0)
+
+
+def attention_ok(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = False) -> bool:
+    """Whether :func:`attention` runs on the hipps kernels for these operands."""
+    return (_FUSED_ATTN and _attn_rows_ok(q) and _attn_rows_ok(k) and _attn_rows_ok(v) and q.shape[3] in (64, 128)
+            and k.shape == v.shape and k.shape[3] == q.shape[3] and k.shape[0] == q.shape[0]
+            and q.shape[2] % k.shape[2] == 0 and (not causal or q.shape[1] == k.shape[1])
+            and 0 < q.shape[1] < (1 << 24) and 0 < k.shape[1] < (1 << 24))
+
+
+class _FlashAttention(torch.autograd.Function):
+    """o = softmax(q k^T * scale [+ causal / key-padding mask]) v on [B, S, H, D] bf16 operands
+    (csrc/attn.hip): forward keeps only o and the per-row log-sum-exp; backward recomputes P in
+    the dQ and the dK/dV kernels (deterministic: no float atomics)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale, kv_len):
+        o, lse = native().attn_forward(q, k, v, causal, scale, kv_len)
+        ctx.save_for_backward(q, k, v, o, lse, kv_len)
+        ctx.causal, ctx.scale = causal, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, kv_len = ctx.saved_tensors
+        do = do.to(torch.bfloat16)
+        if not _attn_rows_ok(do):
+            do = do.contiguous()
+        dq, dk, dv = native().attn_backward(do, q, k, v, o, lse, ctx.causal, ctx.scale, kv_len)
+        return dq, dk, dv, None, None, None
+
+
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = False,
+              scale: Optional[float] = None, kv_len: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Scaled dot-product attention on the [batch, seq, heads, head_dim] layout (the projection
+    outputs viewed per head, no transposes): q [B, Sq, Hq, D], k / v [B, Sk, Hkv, D] with Hq a
+    multiple of Hkv (grouped-query attention), optional causal mask (Sq == Sk) and key padding
+    (``kv_len`` int32 [B]: keys >= kv_len[b] are masked).  Returns [B, Sq, Hq, D].
+
+    bf16 device operands with head dim 64 / 128 run the hipps flash-attention kernels; anything
+    else runs ``F.scaled_dot_product_attention`` on the transposed views."""
+    D = q.shape[-1]
+    sc = float(scale) if scale is not None else 1.0 / (D ** 0.5)
+    if attention_ok(q, k, v, causal):
+        kl = None
+        if kv_len is not None:
+            kl = kv_len.to(device=q.device, dtype=torch.int32).contiguous()
+        return _FlashAttention.apply(q, k, v, bool(causal), sc, kl)
+    qt, kt, vt = (t.transpose(1, 2) for t in (q, k, v))
+    if k.shape[2] != q.shape[2]:
+        rep = q.shape[2] // k.shape[2]
+        kt, vt = kt.repeat_interleave(rep, dim=1), vt.repeat_interleave(rep, dim=1)
+    mask = None
+    if kv_len is not None:
+        keys = torch.arange(k.shape[1], device=q.device)
+        mask = (keys[None, :] < kv_len.to(q.device).view(-1, 1))[:, None, None, :]
+        if causal:
+            mask = mask & torch.ones(q.shape[1], k.shape[1], dtype=torch.bool, device=q.device).tril()
+            causal = False
+    o = F.scaled_dot_product_attention(qt, kt, vt, attn_mask=mask, is_causal=causal, scale=sc)
+    return o.transpose(1, 2)
 
 
 def _flat16_ok(*ts) -> bool:

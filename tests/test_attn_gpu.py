@@ -1,0 +1,168 @@
+"""hipps flash attention (csrc/attn.hip, hipps.ops.nn.attention) against an fp32
+softmax(Q K^T / sqrt(d) + mask) V reference: forward output, log-sum-exp and all three
+gradients, for the transformer configs' shapes (BERT head dim 64, Llama head dim 128 with
+causal masking and grouped-query heads), odd sequence lengths and key padding.
+
+The bf16 error is also compared with PyTorch SDPA's own bf16 error against the same fp32
+reference, so the bound is not a loose absolute number."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(q, k, v, causal, kv_len, scale):
+    """fp32 reference on [B, S, H, D] inputs (GQA by repetition)."""
+    qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))
+    rep = qf.shape[1] // kf.shape[1]
+    kf, vf = kf.repeat_interleave(rep, 1), vf.repeat_interleave(rep, 1)
+    s = (qf @ kf.transpose(-1, -2)) * scale
+    Sq, Sk = s.shape[-2], s.shape[-1]
+    mask = torch.ones(Sq, Sk, dtype=torch.bool, device=q.device)[None, None].expand(q.shape[0], 1, Sq, Sk).clone()
+    if causal:
+        mask &= torch.ones(Sq, Sk, dtype=torch.bool, device=q.device).tril()
+    if kv_len is not None:
+        mask &= (torch.arange(Sk, device=q.device)[None, :] < kv_len.view(-1, 1))[:, None, None, :]
+    s = s.masked_fill(~mask, float("-inf"))
+    lse = torch.logsumexp(s, -1)
+    p = torch.softmax(s, -1).nan_to_num(0.0)
+    return (p @ vf).transpose(1, 2), lse
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
+
+
+CASES = [
+    # B, S, Hq, Hkv, D, causal, padded
+    (2, 128, 4, 4, 64, False, False),
+    (2, 512, 4, 4, 64, False, False),
+    (1, 1000, 4, 4, 64, False, False),
+    (2, 512, 4, 4, 64, False, True),
+    (1, 2048, 4, 4, 64, True, False),
+    (2, 128, 8, 2, 128, True, False),
+    (1, 512, 8, 2, 128, True, False),
+    (1, 1000, 8, 2, 128, True, False),
+    (1, 2048, 8, 2, 128, True, False),
+    (1, 512, 4, 4, 128, False, False),
+    (1, 1000, 4, 1, 128, False, True),
+    (2, 333, 8, 2, 64, True, False),
+    (1, 2048, 8, 8, 128, False, False),
+]
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv,D,causal,padded", CASES)
+def test_flash_attention_forward_backward(B, S, Hq, Hkv, D, causal, padded):
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(S * 7 + Hq + D + int(causal))
+    dev = "cuda"
+    q = torch.randn(B, S, Hq, D, device=dev).to(torch.bfloat16)
+    k = torch.randn(B, S, Hkv, D, device=dev).to(torch.bfloat16)
+    v = torch.randn(B, S, Hkv, D, device=dev).to(torch.bfloat16)
+    kv_len = None
+    if padded:
+        kv_len = torch.tensor([S - 37 - 50 * i for i in range(B)], device=dev, dtype=torch.int32)
+    scale = 1.0 / D ** 0.5
+    assert hnn.attention_ok(q, k, v, causal)
+    qa, ka, va = (t.clone().requires_grad_(True) for t in (q, k, v))
+    o = hnn.attention(qa, ka, va, causal=causal, kv_len=kv_len)
+    assert o.shape == q.shape and o.dtype == torch.bfloat16
+    qr, kr, vr = (t.float().requires_grad_(True) for t in (q, k, v))
+    ref, lse_ref = _ref(qr, kr, vr, causal, kv_len, scale)
+    # forward
+    assert _rel(o, ref) < 1.5e-2, _rel(o, ref)
+    _, lse = hnn.native().attn_forward(q, k, v, causal, scale, kv_len)
+    ok = torch.isfinite(lse_ref)
+    torch.testing.assert_close(lse[ok], lse_ref[ok], rtol=1e-3, atol=2e-3)
+    # backward
+    g = torch.randn_like(o)
+    o.backward(g)
+    ref.backward(g.float())
+    for got, want, name in ((qa.grad, qr.grad, "dq"), (ka.grad, kr.grad, "dk"), (va.grad, vr.grad, "dv")):
+        assert got.shape == want.shape and got.dtype == torch.bfloat16, name
+        assert torch.isfinite(got.float()).all(), name
+        assert _rel(got, want) < 3e-2, (name, _rel(got, want))
+    if padded:  # masked keys get no gradient
+        for i in range(B):
+            assert torch.count_nonzero(ka.grad[i, int(kv_len[i]):]) == 0
+            assert torch.count_nonzero(va.grad[i, int(kv_len[i]):]) == 0
+
+
+@pytest.mark.parametrize("causal,Hkv,D", [(False, 4, 64), (True, 2, 128)])
+def test_flash_attention_error_vs_sdpa(causal, Hkv, D):
+    """hipps' bf16 error against fp32 is no worse than 1.5x PyTorch SDPA's bf16 error."""
+    from hipps.ops import nn as hnn
+    import torch.nn.functional as F
+
+    torch.manual_seed(11)
+    B, S, Hq = 2, 512, 8
+    q = torch.randn(B, S, Hq, D, device="cuda").to(torch.bfloat16)
+    k = torch.randn(B, S, Hkv, D, device="cuda").to(torch.bfloat16)
+    v = torch.randn(B, S, Hkv, D, device="cuda").to(torch.bfloat16)
+    ref, _ = _ref(q, k, v, causal, None, D ** -0.5)
+    rep = Hq // Hkv
+    sd = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2).repeat_interleave(rep, 1),
+                                        v.transpose(1, 2).repeat_interleave(rep, 1), is_causal=causal).transpose(1, 2)
+    ours = hnn.attention(q, k, v, causal=causal)
+    assert _rel(ours, ref) <= 1.5 * _rel(sd, ref) + 1e-3, (_rel(ours, ref), _rel(sd, ref))
+
+
+def test_flash_attention_deterministic_and_strided_inputs():
+    """Backward is bitwise repeatable (no atomics), and q / k / v may be strided views of a fused
+    [B, S, 3, H, D] projection."""
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(5)
+    B, S, H, D = 2, 384, 6, 64
+    qkv = torch.randn(B, S, 3, H, D, device="cuda").to(torch.bfloat16)
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    assert not q.is_contiguous() and hnn.attention_ok(q, k, v)
+    g = torch.randn(B, S, H, D, device="cuda").to(torch.bfloat16)
+    grads = []
+    for _ in range(2):
+        x = qkv.clone().requires_grad_(True)
+        o = hnn.attention(x[:, :, 0], x[:, :, 1], x[:, :, 2])
+        o.backward(g)
+        grads.append((o.detach(), x.grad))
+    assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
+    ref, _ = _ref(q, k, v, False, None, D ** -0.5)
+    assert _rel(grads[0][0], ref) < 1.5e-2
+
+
+def test_flash_attention_in_models(monkeypatch):
+    """BERT and Llama blocks (head dims 64 / 128, Llama causal + GQA) route attention to the hipps
+    kernels and match their SDPA route's loss and gradients."""
+    from hipps.ops import nn as hnn
+    from hipps.models import transformer as tf
+
+    calls = []
+    fwd = hnn._FlashAttention.forward
+
+    def counted(ctx, *a):
+        calls.append(1)
+        return fwd(ctx, *a)
+
+    monkeypatch.setattr(hnn._FlashAttention, "forward", staticmethod(counted))
+    torch.manual_seed(0)
+    models = [(tf.Bert(tf.BertConfig(vocab=512, hidden=128, layers=2, heads=2, ffn=256, max_pos=128)), 2),
+              (tf.Llama(tf.LlamaConfig(vocab=512, dim=256, layers=2, heads=2, kv_heads=1, ffn=256, max_seq=128)), 2)]
+    for m, nlayers in models:
+        m = m.cuda()
+        ids = torch.randint(0, 512, (2, 96), device="cuda")
+        outs = []
+        for fused in (True, False):
+            monkeypatch.setattr(hnn, "_FUSED_ATTN", fused)
+            calls.clear()
+            m.zero_grad()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = m(ids, labels=ids)
+            loss.backward()
+            assert len(calls) == (nlayers if fused else 0)
+            outs.append((loss.detach().float(), [p.grad.detach().float().clone() for p in m.parameters()
+                                                  if p.grad is not None]))
+        (l1, g1), (l0, g0) = outs
+        torch.testing.assert_close(l1, l0, rtol=2e-2, atol=2e-2)
+        num = sum((a - b).norm() ** 2 for a, b in zip(g1, g0)) ** 0.5
+        den = sum(b.norm() ** 2 for b in g0) ** 0.5
+        assert num / den < 5e-2, num / den
