@@ -54,6 +54,8 @@ def parse():
                     help="published-parameter dtype: auto = fp32 at N=1 (local pull), bf16 at N>1 (halves the "
                          "xGMI pull; the PS keeps the fp32 master, workers compute in bf16 anyway)")
     ap.add_argument("--momentum", type=float, default=0.9)
+    ap.add_argument("--optim", default="sgd", choices=["sgd", "adam"],
+                    help="the PS optimizer: the reference's SGD (ps.py:195-214) or Adam (ps.py:217-261)")
     ap.add_argument("--bucket-mb", type=float, default=None,
                     help="bucket size in MB (default: the library's, PSConfig.bucket_mb)")
     ap.add_argument("--granularity", default=None, choices=["model", "bucket", "auto"],
@@ -172,8 +174,12 @@ def main():
         kw["emulate_remote"] = a.emulate_remote
     from hipps.parallel.ps_async import IPCOpenTimeout
 
+    ocls = hipps.SGD
+    if a.optim == "adam":  # (betas / eps: the reference's defaults; no momentum argument)
+        ocls = hipps.Adam
+        kw.pop("momentum")
     try:
-        opt = hipps.SGD(model.named_parameters(), **kw)
+        opt = ocls(model.named_parameters(), **kw)
     except IPCOpenTimeout as e:
         # a mailbox import is stuck inside the HIP driver on some rank (every rank learnt it
         # through the setup agreement): no other engine is built in this process -- report the
@@ -192,7 +198,7 @@ def main():
         print("[bench] " + note, file=sys.stderr)
         kw["async_transport"] = "p2p"
         kw["ps_granularity"] = "model"  # per-bucket publication needs the ipc transport
-        opt = hipps.SGD(model.named_parameters(), **kw)
+        opt = ocls(model.named_parameters(), **kw)
     if mode == "ps_async" and N > 1:
         eng0 = opt.engine
         print(f"[bench] rank {world.rank}: mailbox mapped {getattr(eng0, 'mapped_bytes', 0) / 2**20:.1f} MiB "
@@ -366,6 +372,7 @@ def main():
                                 else f"1 worker + PS, {a.emulate_workers} emulated workers on the same GPU"),
                 "global_batch": a.batch * trainers,
                 "codec": a.codec,
+                "optimizer": a.optim if a.optim == "adam" else f"sgd(momentum={a.momentum})",
                 "accumulate": a.accumulate or N,
                 "grad_bytes_per_step_per_worker": grad_bytes,
                 "grad_bytes_per_step_used": int(grad_used),

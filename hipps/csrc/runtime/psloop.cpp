@@ -107,6 +107,8 @@ class NativePS {
     stream_ = c["stream"].cast<int64_t>();
     direct_ok_ = c["direct_ok"].cast<bool>();
     acc_ = c["acc"].cast<at::Tensor>();
+    // per-bucket versions at M = 1: acc_ is one bucket-sized scratch (ps_async._acc_scratch)
+    acc_scratch_ = c.contains("acc_scratch") && c["acc_scratch"].cast<bool>();
     master_ = c["master"].cast<at::Tensor>();
     // publish buffers as chunks of pub_chunk elements (each an IPC allocation below 2 GiB), typed
     for (auto q : c["pub_chunks"].cast<py::list>()) {
@@ -229,6 +231,7 @@ class NativePS {
   bool alive() const { return th_.joinable() && !done_.load(); }
   void pause(bool on) { pause_req_ = on; }
   bool paused() const { return paused_.load(); }
+  bool pause_requested() const { return pause_req_.load(); }
   std::string error() {
     std::lock_guard<std::mutex> lk(err_mu_);
     return err_;
@@ -504,7 +507,7 @@ class NativePS {
       }
       for (auto& g : groups) {
         const BucketDesc& b = buckets_[g.first.first];
-        at::Tensor acc = acc_.narrow(0, b.lo, b.hi - b.lo);
+        at::Tensor acc = acc_.narrow(0, acc_scratch_ ? 0 : b.lo, b.hi - b.lo);
         auto& ms = g.second;
         for (size_t k = 0; k < ms.size(); k += 16) {
           std::vector<const Pend*> part(ms.begin() + k, ms.begin() + std::min(ms.size(), k + 16));
@@ -591,7 +594,9 @@ class NativePS {
       });
       bump("direct_updates");
     } else {
-      pub_pieces(b.lo, b.hi, [&](int64_t pa, int64_t pb) { update_range(acc_, 0, pa, pb, gscale_, true, k, mask); });
+      pub_pieces(b.lo, b.hi, [&](int64_t pa, int64_t pb) {
+        update_range(acc_, acc_scratch_ ? b.lo : 0, pa, pb, gscale_, true, k, mask);
+      });
     }
     std::vector<std::tuple<int, int, int64_t>> words;
     if (d.set) words.emplace_back(ACK_SEQ, d.worker, d.seq);  // the slot is free once the update read it
@@ -634,7 +639,7 @@ class NativePS {
   ControlBlock& ctl_;
   int W_, rank_, nb_, SLOTS_, MAXSLOTS_, M_, npub_, device_;
   int64_t staleness_, dead_after_us_, ns_, stream_, numel_;
-  bool staleness_lr_, skip_missing_, direct_ok_;
+  bool staleness_lr_, skip_missing_, direct_ok_, acc_scratch_ = false;
   double gscale_;
   at::Tensor acc_, master_, mom_buf_, exp_avg_, exp_avg_sq_, max_exp_avg_sq_, csteps_, chunk_slots_;
   std::vector<std::vector<at::Tensor>> pub_;  // [npub][chunk]
@@ -680,6 +685,7 @@ void bind_psloop(py::module& m) {
       .def("alive", &NativePS::alive)
       .def("pause", &NativePS::pause)
       .def("paused", &NativePS::paused)
+      .def("pause_requested", &NativePS::pause_requested)
       .def("error", &NativePS::error)
       .def("state", &NativePS::state)
       .def("restore", &NativePS::restore);

@@ -97,13 +97,18 @@ __global__ __launch_bounds__(kXBlock) void k_xent_fwd(const uint16_t* __restrict
   if (threadIdx.x < h) online(m, s, bf16_to_f32(row[threadIdx.x]));
   const uint4* vrow = reinterpret_cast<const uint4*>(row + h);
   const int64_t nv = (V - h) >> 3;
+  // software pipeline: the next two chunks are in flight while the current two are reduced
+  const uint4 z = make_uint4(0xff80ff80u, 0xff80ff80u, 0xff80ff80u, 0xff80ff80u);  // -inf x 8
   int64_t v = threadIdx.x;
-  for (; v + kXBlock < nv; v += 2 * kXBlock) {  // two chunks in flight per lane
-    const uint4 a = vrow[v], b = vrow[v + kXBlock];
+  uint4 a = v < nv ? vrow[v] : z, b = v + kXBlock < nv ? vrow[v + kXBlock] : z;
+  for (; v < nv; v += 2 * kXBlock) {
+    const int64_t n0 = v + 2 * kXBlock, n1 = v + 3 * kXBlock;
+    const uint4 na = n0 < nv ? vrow[n0] : z, nb = n1 < nv ? vrow[n1] : z;
     online8(m, s, a);
     online8(m, s, b);
+    a = na;
+    b = nb;
   }
-  if (v < nv) online8(m, s, vrow[v]);
   for (int64_t i = h + nv * 8 + threadIdx.x; i < V; i += kXBlock) online(m, s, bf16_to_f32(row[i]));
   block_lse(m, s);
   if (threadIdx.x == 0) {
@@ -149,13 +154,18 @@ __global__ __launch_bounds__(kXBlock) void k_xent_bwd(const uint16_t* __restrict
     for (int j = 0; j < 8; ++j) g[j] = (g[j] - (i0 + j == lab ? 1.f : 0.f)) * k;
     vd[v] = make_uint4(pack_bf16x2(g[0], g[1]), pack_bf16x2(g[2], g[3]), pack_bf16x2(g[4], g[5]), pack_bf16x2(g[6], g[7]));
   };
+  // software pipeline: the next two chunks' loads are issued before this pair's stores, so the
+  // wait for them (vmcnt counts stores too) does not wait for the stores' completion
   int64_t v = threadIdx.x;
-  for (; v + kXBlock < nv; v += 2 * kXBlock) {
-    const uint4 a = vrow[v], b = vrow[v + kXBlock];
+  uint4 a = v < nv ? vrow[v] : uint4{}, b = v + kXBlock < nv ? vrow[v + kXBlock] : uint4{};
+  for (; v < nv; v += 2 * kXBlock) {
+    const int64_t n0 = v + 2 * kXBlock, n1 = v + 3 * kXBlock;
+    const uint4 na = n0 < nv ? vrow[n0] : uint4{}, nb = n1 < nv ? vrow[n1] : uint4{};
     one(v, a);
-    one(v + kXBlock, b);
+    if (v + kXBlock < nv) one(v + kXBlock, b);
+    a = na;
+    b = nb;
   }
-  if (v < nv) one(v, vrow[v]);
   for (int64_t i = h + nv * 8 + threadIdx.x; i < V; i += kXBlock)
     drow[i] = f32_to_bf16((__expf(bf16_to_f32(row[i]) - l) - (i == lab ? 1.f : 0.f)) * k);
 }

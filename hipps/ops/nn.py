@@ -155,7 +155,13 @@ def set_deterministic(on: bool = True) -> None:
     whose default algorithms are not run-to-run deterministic (two runs of a ResNet differed in
     every parameter, tools/diag/determinism_probe.py).  This restricts them to MIOpen's
     deterministic algorithms (torch.backends.cudnn.deterministic); no measurable cost on the
-    ResNet-50 bs256 headline (profiles/r5/det)."""
+    ResNet-50 bs256 headline (profiles/r5/det).
+
+    Scope: a step is repeatable for a given set of tuner picks.  The picks are timed per process,
+    and some candidates are not bitwise equal to each other (weight-gradient slab counts, the BN
+    operand-prologue route ``bnpro``), so two processes can choose differently on a near tie.  For
+    bit-for-bit runs across processes or ranks, record the picks once (``TUNER.save(path)``) and
+    load them everywhere (``TUNER.load(path)`` or ``HIPPS_TUNER_CACHE=path``)."""
     torch.backends.cudnn.deterministic = bool(on)
 # Inputs of in-flight side-stream weight gradients, with an event after each: kept referenced until
 # the event has passed or the caller's stream joined the side stream, then dropped.  This replaces
@@ -294,8 +300,30 @@ class _Tuner:
         self.cache[key] = got
         return got
 
+    def save(self, path: str) -> None:
+        """Write every pick (key -> candidate name) as JSON."""
+        import json
+
+        with open(path, "w") as f:
+            json.dump([[list(k), v] for k, v in self.cache.items()], f)
+
+    def load(self, path: str) -> int:
+        """Adopt recorded picks (they win over measuring): runs that load the same file make the
+        same choices, so choices between candidates that are not bitwise equal (weight-gradient
+        slab counts, the BN prologue route) cannot differ between runs or ranks.  Returns the
+        number of picks loaded."""
+        import json
+
+        with open(path) as f:
+            for k, v in json.load(f):
+                self.cache[tuple(k)] = v
+        return len(self.cache)
+
 
 TUNER = _Tuner()
+# HIPPS_TUNER_CACHE=<file>: picks recorded by TUNER.save are loaded at import (set_deterministic)
+if _os.environ.get("HIPPS_TUNER_CACHE") and _os.path.exists(_os.environ["HIPPS_TUNER_CACHE"]):
+    TUNER.load(_os.environ["HIPPS_TUNER_CACHE"])
 # (block rows, block cols, LDS stages): 3 stages keep one tile's DMA in flight across every
 # K-loop barrier (gemm2.hip k_gemm NS).  Only 128x64 keeps two blocks per CU with 3 stages; the
 # others drop to one wave per SIMD and lose (profiles/gemm2_probe_r3_stages.json).  (256, 256, 5):

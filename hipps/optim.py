@@ -32,6 +32,25 @@ from .parallel import dist as hdist
 from .parallel.flat import FlatStore
 
 
+class _HyperGroup(dict):
+    """A param group (dict) that calls ``notify()`` when a hyper-parameter changes value."""
+
+    _KEYS = frozenset(("lr", "weight_decay", "momentum", "dampening", "nesterov", "betas", "eps", "amsgrad"))
+
+    def __init__(self, d, notify):
+        super().__init__(d)
+        self._notify = notify
+
+    def __setitem__(self, k, v):
+        changed = k in self._KEYS and (k not in self or self[k] != v)
+        super().__setitem__(k, v)
+        if changed:
+            self._notify()
+
+    def __reduce__(self):  # (pickles / deep-copies as the plain dict torch expects)
+        return (dict, (dict(self),))
+
+
 class MPI_PS(torch.optim.Optimizer):
     """Base PS optimizer (ps.py:53).  Subclasses provide ``_update_group``."""
 
@@ -101,6 +120,7 @@ class MPI_PS(torch.optim.Optimizer):
         self._init_state()
         self.steps = 0
         self.engine = self._make_engine()
+        self._watch_hyper()
         bw = self.cfg.bf16_weights
         # auto: where a reader exists -- the hipps conv kernels (4-D weights) and hipps.ops.nn.Linear
         # (parameters tagged reads_bf16_shadow, _ShadowLinear) read the shadow instead of autocast casting every weight in
@@ -393,6 +413,24 @@ class MPI_PS(torch.optim.Optimizer):
                 sd["hipps"]["chunk_steps"] = self.chunk_steps.detach().cpu()
         return sd
 
+    def _watch_hyper(self):
+        """Make every param group notify the engine when a hyper-parameter is written (an LR
+        scheduler's ``group['lr'] = ...``): the native PS loop (ps_async, C++ without the GIL)
+        cannot read ``param_groups`` at each update the way the Python loop does, so the new value
+        is pushed into it at once -- both loops then use the same lr from the same moment on
+        (ADVICE r5)."""
+        if getattr(self.engine, "_push_hyper", None) is None:
+            return
+
+        def push():
+            eng = getattr(self, "engine", None)
+            if eng is not None and hasattr(eng, "_push_hyper"):
+                eng._push_hyper()
+
+        for i, g in enumerate(self.param_groups):
+            if not isinstance(g, _HyperGroup):
+                self.param_groups[i] = _HyperGroup(g, push)
+
     def _sync_param_state(self):
         """Refresh host-side per-parameter state entries derived from device state."""
 
@@ -419,6 +457,12 @@ class MPI_PS(torch.optim.Optimizer):
                 cs.copy_(extra["chunk_steps"].to(cs.device))
             else:  # a plain torch state dict: per-parameter counts from its own entries
                 self._csteps_from_state(cs)
+        # torch rebuilt param_groups as plain dicts: watch them again, and hand the loaded
+        # hyper-parameters and group step counts to a native PS loop
+        self._watch_hyper()
+        eng = getattr(self, "engine", None)
+        if eng is not None and hasattr(eng, "reload_hyper"):
+            eng.reload_hyper()
         self.store.refresh_shadow()
 
     def _csteps_from_state(self, cs: torch.Tensor):

@@ -82,14 +82,15 @@ def _align(x: int, a: int = 256) -> int:
 
 def ps_memory_budget(numel: int, W: int, slots: int, slot_bytes: int, npub: int, pub_esz: int, opt_floats: int,
                      colocated: bool = True, worker_wire_bytes: int = 0, shadow: bool = False,
-                     codec_state_floats: int = 0) -> Dict[str, int]:
+                     codec_state_floats: int = 0, acc_floats: Optional[int] = None) -> Dict[str, int]:
     """Bytes the async PS adds on rank 0's GPU, term by term.
 
     PS terms (allocated by the engine):
       mailbox      W * slots * slot_bytes        every worker's in-flight bucket messages (ring: slots = 1)
       publish      npub * numel * pub_esz        rotating published versions (readers never torn)
       master       numel * 4                     the fp32 master parameters
-      accumulator  numel * 4                     the fp32 gradient accumulator
+      accumulator  acc_floats * 4                the fp32 gradient accumulator (numel; one bucket at
+                                                 M = 1 with per-bucket versions)
       optimizer    opt_floats * numel * 4        momentum (SGD) / moments (Adam) on the master
       chunk_steps  numel / 16 * 4                per-parameter step counters
     Co-located worker 0 (rank 0 also trains, ``colocated``): its fp32 parameters and gradients,
@@ -99,7 +100,7 @@ def ps_memory_budget(numel: int, W: int, slots: int, slot_bytes: int, npub: int,
         "mailbox": W * slots * slot_bytes,
         "publish": npub * numel * pub_esz,
         "master": numel * 4,
-        "accumulator": numel * 4,
+        "accumulator": (numel if acc_floats is None else acc_floats) * 4,
         "optimizer": opt_floats * numel * 4,
         "chunk_steps": (numel + 15) // 16 * 4,
     }
@@ -197,7 +198,7 @@ HBM_FRACTION = 0.85         # the PS + co-located worker state may take this muc
 def plan_geometry(msg_nbytes: Sequence[int], pres_bytes: int, numel: int, W: int, pub_esz: int, opt_floats: int,
                   mailbox_slots: int = 0, mailbox_mb: float = 4096.0, max_slots: int = 64, npub_max: int = 4,
                   npub: int = 0, colocated: bool = True, worker_wire_bytes: int = 0, shadow: bool = False,
-                  codec_state_floats: int = 0, hbm_bytes: Optional[int] = None):
+                  codec_state_floats: int = 0, hbm_bytes: Optional[int] = None, acc_floats: Optional[int] = None):
     """Mailbox + publish geometry of the async PS sized from rank 0's HBM budget (VERDICT r4
     item 2: Llama-3-8B at W=8 must fit by default).  Start from the full geometry (``npub_max``
     rotating publish buffers, a ring of two steps' messages per worker capped by ``mailbox_mb``);
@@ -214,7 +215,7 @@ def plan_geometry(msg_nbytes: Sequence[int], pres_bytes: int, numel: int, W: int
     def bud(r, n):
         return ps_memory_budget(numel, W, 1, r, n, pub_esz, opt_floats, colocated=colocated,
                                 worker_wire_bytes=worker_wire_bytes, shadow=shadow,
-                                codec_state_floats=codec_state_floats)
+                                codec_state_floats=codec_state_floats, acc_floats=acc_floats)
 
     limit = None if hbm_bytes is None else int(HBM_FRACTION * hbm_bytes)
     b = bud(ring, np_)
@@ -234,7 +235,8 @@ def plan_geometry(msg_nbytes: Sequence[int], pres_bytes: int, numel: int, W: int
 def budget_for_shapes(shapes, W: int, codec="bf16", bucket_mb: float = 16.0, mailbox_mb: float = 4096.0,
                       mailbox_slots: int = 0, param_wire: str = "bf16", opt_floats: int = 1,
                       dedicated: bool = False, shadow: bool = True, npub: int = 0,
-                      max_slots: int = 64, hbm_bytes: Optional[int] = HBM_DEFAULT) -> Dict[str, int]:
+                      max_slots: int = 64, hbm_bytes: Optional[int] = HBM_DEFAULT, accumulate: int = 1,
+                      bucketwise: bool = True, direct_push: Optional[bool] = None) -> Dict[str, int]:
     """:func:`ps_memory_budget` of a model given only its parameter shapes (no allocation: usable
     for an 8B model on a laptop).  Reproduces the engine's bucketing (flat.BucketPlan over
     16-aligned slots) and its geometry choice (:func:`plan_geometry`, same defaults)."""
@@ -260,12 +262,26 @@ def budget_for_shapes(shapes, W: int, codec="bf16", bucket_mb: float = 16.0, mai
     npub_max = native().ControlBlock.NPUB if available() else 4
     esz = 2 if param_wire == "bf16" else 4
     ef = 1 if getattr(c, "error_feedback", False) else 0
+    from hipps.codecs import Codec
+
+    # rank 0's worker pushes hook-time buckets straight into its ring (PSAsyncEngine._direct_push):
+    # no wire image for static-size codecs
+    direct = type(c).used_bytes is Codec.used_bytes if direct_push is None else bool(direct_push)
     K, ring, np_, b = plan_geometry([b.msg_nbytes for b in plan.buckets], pres, off, W, esz, opt_floats,
                                     mailbox_slots, mailbox_mb, max_slots, npub_max, npub, colocated=not dedicated,
-                                    worker_wire_bytes=plan.wire_nbytes + pres, shadow=shadow,
-                                    codec_state_floats=ef, hbm_bytes=hbm_bytes)
+                                    worker_wire_bytes=pres if direct else plan.wire_nbytes + pres, shadow=shadow,
+                                    codec_state_floats=ef, hbm_bytes=hbm_bytes,
+                                    acc_floats=_acc_floats(plan, off, accumulate, bucketwise))
     b["buckets"], b["mailbox_slots"], b["slot_bytes"], b["npub"] = nb, K, ring, np_
     return b
+
+
+def _acc_floats(plan, numel: int, M: int, bucketwise: bool) -> int:
+    """fp32 accumulator elements the PS allocates (PSAsyncEngine._acc_scratch): one bucket-sized
+    scratch at M = 1 with per-bucket versions, the whole model otherwise."""
+    if bucketwise and M == 1 and plan.buckets:
+        return _align(max(b.hi - b.lo for b in plan.buckets), 16)
+    return numel
 
 
 def format_budget(b: Dict[str, int]) -> str:
@@ -467,13 +483,14 @@ class _NativeFlag:
             self.native.pause(False)
 
     def is_set(self) -> bool:
-        return self.native.paused() if not self.request else False
+        return self.native.pause_requested() if self.request else self.native.paused()
 
 
 _DTYPE_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.int8: 2, torch.int32: 3, torch.uint8: 4}
 
 
 class PSAsyncEngine(Engine):
+    _lazy_wire = True  # (rank 0 with direct push never allocates its wire image)
     name = "ps_async"
 
     def __init__(self, opt, cfg, store, codec, world):
@@ -533,6 +550,20 @@ class PSAsyncEngine(Engine):
         self._ring_off = 0
         self._inflight = collections.deque()  # (seq, offset, bytes) of this worker's unacked messages
         self.pub_bytes = _align(store.numel * esz)
+        # push_early: push each bucket's message from its backward hook (see encode_bucket)
+        pe = cfg.push_early
+        self._early = pe != "off" and not self.p2p and cfg.overlap and not self.is_object \
+            and self._fault is None and not self.plan.guarded and not self.ps_only
+        # direct push: a hook-time bucket is encoded straight into its space in the (local) mailbox
+        # ring -- no wire-buffer image and no copy.  Rank 0's own worker only (its mailbox is local
+        # HBM); static-size codecs (the byte accounting reads variable-size counts from the wire).
+        # Its wire image is then never allocated (Engine.wire) unless a bucket falls back to the
+        # step-time encode (a parameter without a gradient, backward twice before step())
+        from ..codecs import Codec as _Codec
+
+        self._direct_push = (self._early and self.cuda and self.rank == 0 and not self.plan.guarded
+                             and type(self.codec).used_bytes is _Codec.used_bytes
+                             and os.environ.get("HIPPS_DIRECT_PUSH", "1") != "0")
         # geometry (word slots, ring bytes per worker, publish buffers) from rank 0's HBM budget;
         # rank 0 decides and every rank adopts its numbers (they index the same memory)
         self.SLOTS, self.ring_bytes, self.NPUB, self.budget = self._plan(opt, store, esz)
@@ -592,22 +623,10 @@ class PSAsyncEngine(Engine):
         self.step_no = 0
         self.local_ver = -1
         self._stats = {"drops": 0, "staleness_sum": 0, "accumulated": 0, "reader_waits": 0}
-        # push_early: push each bucket's message from its backward hook (see encode_bucket)
-        pe = cfg.push_early
-        self._early = pe != "off" and not self.p2p and cfg.overlap and not self.is_object \
-            and self._fault is None and not self.plan.guarded and not self.ps_only
         self._npushed, self._push_wait, self._in_encode_all = 0, 0.0, False
         # HIPPS_WAIT_DIAG=1: every host wait for mailbox space (kind, seq, needed ack, ack at start, s)
         self._wait_log = [] if os.environ.get("HIPPS_WAIT_DIAG", "0") == "1" else None
         self._pushed_b = bytearray(self.nb)  # buckets already pushed this step (any order)
-        # direct push: a hook-time bucket is encoded straight into its space in the (local) mailbox
-        # ring -- no wire-buffer image and no copy.  Rank 0's own worker only (its mailbox is local
-        # HBM); static-size codecs (the byte accounting reads variable-size counts from the wire)
-        from ..codecs import Codec as _Codec
-
-        self._direct_push = (self._early and self.cuda and self.rank == 0 and not self.plan.guarded
-                             and type(self.codec).used_bytes is _Codec.used_bytes
-                             and os.environ.get("HIPPS_DIRECT_PUSH", "1") != "0")
         self._lat = (_LatencyProbe() if self.cuda and self.rank == 0 and not self.dedicated
                      and os.environ.get("HIPPS_PS_LATENCY", "0") == "1" else None)
         self._err = None
@@ -629,7 +648,17 @@ class PSAsyncEngine(Engine):
             self._sel = torch.full((2 + RING,), -1, dtype=torch.int64, device=store.device)
         if self.rank == 0:
             self.master = store.data.detach().clone()
-            self.acc = torch.zeros_like(store.data)
+            # Per-bucket versions at M = 1: every kept message is accumulated and applied before
+            # the next one is looked at (ps_core._one_bucket: accumulate -> flush -> update_bucket,
+            # all on the PS stream), so one bucket-sized scratch replaces the model-sized fp32
+            # accumulator (Llama-3-8B: 32 GB of rank 0's HBM).  The update
+            # zeroes the scratch as it reads it (zero_src), re-arming it for the next bucket.
+            self._acc_scratch = self.bucketwise and self.M == 1
+            if self._acc_scratch:
+                big = max(b.hi - b.lo for b in self.plan.buckets)
+                self.acc = torch.zeros((big + 15) // 16 * 16, dtype=store.data.dtype, device=store.device)
+            else:
+                self.acc = torch.zeros_like(store.data)
             # The PS stream runs at the workers' priority: with the native loop issuing each
             # bucket's update the moment its message lands, a high-priority stream put those
             # kernels ahead of worker 0's backward on the co-located GPU and cost Llama-3-8B 15 %
@@ -726,8 +755,10 @@ class PSAsyncEngine(Engine):
     def _budget_inputs(self, opt, store, esz) -> dict:
         cs = sum(1 for st in self.codec_state if "resid" in st)
         return dict(numel=store.numel, W=self.W, pub_esz=esz, opt_floats=opt.state_floats(),
-                    colocated=not self.dedicated, worker_wire_bytes=self.wire_total,
-                    shadow=getattr(store, "shadow", None) is not None, codec_state_floats=1 if cs else 0)
+                    colocated=not self.dedicated,
+                    worker_wire_bytes=self.pres_bytes if self._direct_push else self.wire_total,
+                    shadow=getattr(store, "shadow", None) is not None, codec_state_floats=1 if cs else 0,
+                    acc_floats=_acc_floats(self.plan, store.numel, self.M, self.bucketwise))
 
     def _plan(self, opt, store, esz):
         """(word slots, ring bytes per worker, npub, budget) -- :func:`plan_geometry` on rank 0
@@ -928,8 +959,15 @@ class PSAsyncEngine(Engine):
         Returns (error or None, timed out)."""
         limit = float(os.environ.get("HIPPS_IPC_OPEN_TIMEOUT_S", "60"))
         nimp = self.NPUB * self.npc + self.nrc
-        # every earlier rank may use its full limit for each of its opens
-        if not self.ctl.wait_ge(C.F_OPEN_TURN, 0, self.rank - 1, int((nimp * limit * (self.rank - 1) + 30) * 1e6)):
+        # every earlier rank may use its full limit for each of its opens, but the wait is capped
+        # (HIPPS_IPC_TURN_WAIT_S, default 600 s): an earlier rank that could not even map the
+        # control block cannot post the failure marker, and uncapped the W=8 Llama-3-8B worst
+        # case was hours of silence (ADVICE r5)
+        cap = float(os.environ.get("HIPPS_IPC_TURN_WAIT_S", "600"))
+        wait_s = min(nimp * limit * (self.rank - 1) + 30, cap)
+        if not self.ctl.wait_ge(C.F_OPEN_TURN, 0, self.rank - 1, int(wait_s * 1e6)):
+            # mark the failure so the ranks after this one stop waiting too
+            self.ctl.store(C.F_OPEN_TURN, 0, 1 << 40)
             return f"rank {self.rank}: rank {self.rank - 1} never finished its mailbox import", False
         if self.ctl.load(C.F_OPEN_TURN, 0) >= (1 << 40):  # an earlier rank failed: do not pile on
             return None, False
@@ -1188,7 +1226,8 @@ class PSAsyncEngine(Engine):
              "skip_missing": bool(cfg.skip_missing_grads), "nslots": len(store.slots),
              "device": int(store.device.index or 0),
              "stream": int(self.ps_stream.cuda_stream) if self.ps_stream is not None else 0,
-             "direct_ok": bool(self._direct_ok), "acc": self.acc, "master": self.master,
+             "direct_ok": bool(self._direct_ok), "acc": self.acc, "acc_scratch": bool(self._acc_scratch),
+             "master": self.master,
              "pub_chunks": [list(q) for q in self.pub_chunks], "pub_chunk": int(self.pub_chunk),
              "pub_dtype": _DTYPE_CODE[self.pub_dtype],
              "rings": [list(r) for r in self.rings], "ring_chunk": int(self.ring_chunk),
@@ -1212,6 +1251,19 @@ class PSAsyncEngine(Engine):
                           float(g.get("dampening", 0) or 0), bool(g.get("nesterov", False)), float(b1), float(b2),
                           float(g.get("eps", 1e-8)), bool(g.get("amsgrad", False)),
                           self.cfg.adam_variant == "torch")
+
+    def reload_hyper(self):
+        """After ``opt.load_state_dict``: the optimizer's hyper-parameters and group step counts
+        into the native loop (held between messages while the counts change)."""
+        nat = self.__dict__.get("_native")
+        if nat is None:
+            return
+        self._push_hyper()
+        gs = [int(v) for v in self.opt._group_steps]  # (the loaded counts: quiesced() re-reads the loop's)
+        with self.quiesced():
+            self.opt._group_steps = list(gs)
+            nat.restore(int(self.ver), [int(v) for v in getattr(self.core, "ver_b", [])],
+                        [int(v) for v in getattr(self.core, "count_b", [])], int(self._gsteps), gs)
 
     def _sync_from_native(self):
         """Mirror the native loop's counters into the Python-side PS state (stats, versions,
@@ -1388,6 +1440,10 @@ class PSAsyncEngine(Engine):
         for _ in range(self.emu):  # emulated remote workers: the same bytes (lockstep workers'
             self._pend.append((bi, scale, None, False))  # messages arrive together: one batch)
 
+    def _acc_of(self, b) -> torch.Tensor:
+        """The accumulator image of bucket ``b`` (the shared scratch at M = 1 per-bucket)."""
+        return self.acc[:b.hi - b.lo] if self._acc_scratch else self.acc[b.lo:b.hi]
+
     def ack(self, i: int, seq: int):
         for d in self._direct.values():
             if d[2] == (i, seq):  # rung by update_bucket, after the update kernel that reads the slot
@@ -1410,7 +1466,7 @@ class PSAsyncEngine(Engine):
                     for k in range(0, len(msgs), self.BATCH):
                         # a batch holding a peer-written slot acquires at system scope first
                         kw = {"acquire": True} if any(rem[k:k + self.BATCH]) else {}
-                        self.codec.accumulate(msgs[k:k + self.BATCH], self.acc[b.lo:b.hi], scale, True, **kw)
+                        self.codec.accumulate(msgs[k:k + self.BATCH], self._acc_of(b), scale, True, **kw)
             self._stats["acc_launches"] = self._stats.get("acc_launches", 0) + sum(
                 (len(m) + self.BATCH - 1) // self.BATCH for m in groups.values())
             self._pend = []
@@ -1469,7 +1525,7 @@ class PSAsyncEngine(Engine):
                                            mask, b.lo, lookahead=tau, pub_lo=pa)
                 else:
                     self.opt._update_range([self.acc], self.master, pa, pb, gscale, True, self.pub_view(k, pa, pb),
-                                           mask, 0, lookahead=tau, pub_lo=pa)
+                                           mask, b.lo if self._acc_scratch else 0, lookahead=tau, pub_lo=pa)
             if direct is not None:
                 _, _, (wi, ws) = direct
                 self._stats["direct_updates"] = self._stats.get("direct_updates", 0) + 1
@@ -1766,7 +1822,8 @@ class PSAsyncEngine(Engine):
             self.remove_hooks()
             raise RuntimeError(self._broken)
         data["code_wait"] = self.encode_all()
-        self.verify_guards([self.wire], "encode")
+        if self.plan.guarded:
+            self.verify_guards([self.wire], "encode")
         self._check_error()
         if self._fault is not None and self._inject(data):
             return data
@@ -2410,7 +2467,13 @@ class PSAsyncEngine(Engine):
             with self.quiesced():
                 self.master.copy_(d["master"].to(self.master.device))
                 if "acc" in d:
-                    self.acc.copy_(d["acc"].to(self.acc.device))
+                    a = d["acc"]
+                    if a.numel() == self.acc.numel():
+                        self.acc.copy_(a.to(self.acc.device))
+                    elif a.numel() and bool(a.abs().max() > 0):
+                        raise RuntimeError("saved accumulator holds a pending sum this configuration cannot take")
+                    else:  # (an M = 1 per-bucket run's scratch holds nothing between updates)
+                        self.acc.zero_()
                     self.core.count = int(d.get("acc_count", 0))
                 self.ver = int(d["version"])
                 b = self.ver % self.NPUB

@@ -179,3 +179,50 @@ def test_chunked_publish_pull_bitwise():
     for r in range(2):
         for x, y in zip(a[r]["params"], b[r]["params"]):
             torch.testing.assert_close(x, y, rtol=0, atol=0)
+
+
+def _scratch(rank, world, native):
+    import hipps
+
+    os.environ["HIPPS_NATIVE_PS"] = "1" if native else "0"
+    torch.cuda.set_device(0)
+    m = _mlp().cuda()
+    opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="ps_async", code="bf16", bucket_mb=0.0005,
+                    max_delay=0, accumulate=1, ps_granularity="bucket")
+    eng = opt.engine
+    info = {}
+    if rank == 0:
+        info = {"acc": eng.acc.numel(), "big": max(b.hi - b.lo for b in eng.plan.buckets),
+                "numel": eng.store.numel, "scratch": eng._acc_scratch, "nb": len(eng.plan.buckets)}
+    losses = []
+    for s in range(6):
+        x, y = _data(0, s % 4)
+        opt.zero_grad()
+        loss = torch.nn.functional.cross_entropy(m(x.cuda()), y.cuda())
+        loss.backward()
+        opt.step()
+        losses.append(float(loss))
+    torch.cuda.synchronize()
+    st = eng.ps_stats() if rank == 0 else {}
+    wire_alloc = eng._wire is not None
+    opt.close()
+    return {"info": info, "stats": st, "losses": losses, "wire_alloc": wire_alloc,
+            "params": [p.detach().cpu() for p in m.parameters()]}
+
+
+@pytest.mark.parametrize("native", [True, False])
+def test_m1_accumulator_scratch_with_remote_workers(native):
+    """accumulate=1 with per-bucket versions and three ranks: the peer-written messages go through
+    ONE bucket-sized accumulator scratch (not a model-sized fp32 buffer), each applied before the
+    next is accumulated; every message is counted and applied, training stays finite and close to
+    the Python loop's, and rank 0 (direct push) never allocates its wire image."""
+    res = run_world(_scratch, 3, native, timeout=300)
+    info, st = res[0]["info"], res[0]["stats"]
+    assert info["scratch"] and info["acc"] < info["numel"] and info["acc"] >= info["big"]
+    assert st["native_loop"] == (1 if native else 0)
+    assert st["accumulated"] == 18 and st["bucket_updates"] == 18 * info["nb"]
+    assert st.get("direct_updates", 0) == 6 * info["nb"]  # rank 0's own messages
+    assert not res[0]["wire_alloc"]
+    for r in res:
+        assert all(torch.isfinite(p).all() for p in r["params"])
+        assert r["losses"][-1] < r["losses"][0]

@@ -9,6 +9,7 @@
 * worker i maps only its own ring and the publish region;
 * the default geometry of Llama-3-8B at W=8 fits rank 0's HBM budget (config 5).
 """
+import math
 import time
 
 import pytest
@@ -251,3 +252,23 @@ def test_chunked_mailbox_bitwise(gran):
     for r in range(2):
         for x, y in zip(a[r]["params"], b[r]["params"]):
             torch.testing.assert_close(x, y, rtol=0, atol=0)
+
+
+def test_llama8b_w8_adam_fits():
+    """Config 5 at W=8 with the reference's Adam (two fp32 moments on the PS, ps.py:217-261):
+    rank 0 fits within 85 % of 288 GB -- the M = 1 per-bucket accumulator is one bucket-sized
+    scratch (not a model-sized fp32 buffer) and rank 0's worker pushes its buckets straight into
+    its ring (no 16 GB wire image)."""
+    from hipps.models import transformer
+    from hipps.parallel.ps_async import HBM_FRACTION, budget_for_shapes
+
+    with torch.device("meta"):
+        model = transformer.build("llama3-8b")
+    shapes = [tuple(p.shape) for p in model.parameters()]
+    b = budget_for_shapes(shapes, 8, opt_floats=2)
+    assert b["fits"] == 1, b
+    assert b["total"] <= HBM_FRACTION * 288e9
+    assert b["accumulator"] < 3e9 and b["worker_wire"] < 1e6
+    # M > 1 (or whole-model versions) needs the full accumulator again
+    full = budget_for_shapes(shapes, 8, opt_floats=2, accumulate=4, hbm_bytes=None)
+    assert full["accumulator"] >= 4 * sum(math.prod(s) for s in shapes)

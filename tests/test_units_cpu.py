@@ -192,7 +192,7 @@ def test_ps_memory_budget_terms_and_engine_agree():
     opt = hipps.SGD(m.named_parameters(), lr=0.1, momentum=0.9, mode="ps_async", bucket_mb=0.05, code="int8")
     live = opt.engine.memory_budget()
     shp = budget_for_shapes([tuple(p.shape) for p in m.parameters()], W=1, codec="int8", bucket_mb=0.05,
-                            param_wire="fp32", opt_floats=1, shadow=False)
+                            param_wire="fp32", opt_floats=1, shadow=False, direct_push=False)  # (CPU: no direct push)
     opt.close()
     for k in ("mailbox", "publish", "master", "accumulator", "optimizer", "chunk_steps", "worker_wire",
               "worker_codec_state"):
@@ -271,3 +271,46 @@ def test_native_ps_config_parses_on_cpu():
             eng._native = None
             del nat
             opt.close()
+
+
+def test_lr_schedule_reaches_the_ps_loop_at_once(tmp_path):
+    """a scheduler writing group['lr'] notifies the engine immediately (the native PS
+    loop cannot read param_groups itself), and opt.load_state_dict re-arms the watch and reloads
+    the hyper-parameters."""
+    import hipps
+    from test_dist_cpu import _mlp
+
+    m = _mlp()
+    opt = hipps.SGD(m.named_parameters(), lr=0.1, momentum=0.9, mode="ps_async", bucket_mb=0.05)
+    calls = []
+    opt.engine._push_hyper = lambda: calls.append(opt.param_groups[0]["lr"])
+    reloads = []
+    opt.engine.reload_hyper = lambda: reloads.append(1)
+    sched = torch.optim.lr_scheduler.StepLR(opt, step_size=1, gamma=0.5)
+    opt.step()
+    sched.step()
+    assert calls and calls[-1] == pytest.approx(0.05)
+    n = len(calls)
+    opt.param_groups[0]["lr"] = 0.05  # same value: no push
+    assert len(calls) == n
+    sd = opt.state_dict()
+    assert type(sd["param_groups"][0]) is dict
+    opt.load_state_dict(sd)
+    assert reloads == [1]
+    opt.param_groups[0]["momentum"] = 0.5
+    assert len(calls) == n + 1
+    opt.close()
+
+
+def test_tuner_picks_round_trip(tmp_path):
+    """Recorded kernel picks load back (set_deterministic across processes)."""
+    from hipps.ops.nn import _Tuner
+
+    t = _Tuner()
+    t.cache[("lfwd", 1024, 768, 768, True, False)] = "g2_256x256"
+    t.cache[("bnpro", 256, 64, 56, 56, 256)] = False
+    f = str(tmp_path / "picks.json")
+    t.save(f)
+    u = _Tuner()
+    assert u.load(f) == 2 and u.cache == t.cache
+    assert u.pick(("lfwd", 1024, 768, 768, True, False), {"x": None, "y": None}) == "g2_256x256"
