@@ -242,14 +242,13 @@ class Engine:
         """Encode bucket bi's gradient into its message -- in the wire buffer, or into ``views``
         (ps_async: straight into the bucket's mailbox ring space)."""
         b = self.plan.buckets[bi]
-        g = self.store.grad[b.lo:b.hi]
         if views is None:
             views = self.plan.views(self.wire, bi)
         if self.is_object:  # host codec objects: run on finished gradients (ps.py:94 in a pool)
             if self.cuda:
                 torch.cuda.current_stream(self.store.device).synchronize()
             with self.tracer.phase("encode"):
-                self.codec.encode_into(g, views, self.codec_state[bi])
+                self.codec.encode_into(self.store.grad[b.lo:b.hi], views, self.codec_state[bi])
             self._encoded[bi] = True
             return
         if self.cuda:
@@ -266,10 +265,10 @@ class Engine:
                     if self.grad_mode == "gather" and self._gather_bucket(bi, views):
                         pass  # dense codec: the gather already wrote the wire image
                     else:
-                        self.codec.encode_into(g, views, self.codec_state[bi])
+                        self.codec.encode_into(self.store.grad[b.lo:b.hi], views, self.codec_state[bi])
         else:
             with self.tracer.phase("encode"):
-                self.codec.encode_into(g, views, self.codec_state[bi])
+                self.codec.encode_into(self.store.grad[b.lo:b.hi], views, self.codec_state[bi])
         self._encoded[bi] = True
         if self.cfg.debug_check_order:
             self._order_log.append(f"{bi}:{b.numel}:{self.codec.name}")

@@ -74,7 +74,10 @@ class FlatStore:
         self.device = torch.device(device)
         self.dtype = dtype
         self.data = torch.zeros(self.numel, dtype=dtype, device=self.device)
-        self.grad = torch.zeros(self.numel, dtype=dtype, device=self.device)
+        # the flat gradient buffer is allocated on first use (``grad``): engines in 'gather' mode
+        # with a dense codec gather autograd's gradients straight into the bucket messages and
+        # never read it (Llama-3-8B: 32 GB per worker)
+        self._grad: Optional[torch.Tensor] = None
         self.grad_mode = "flat"
         self._force_present = False
         self._stale = [False] * len(self.slots)  # flat grad view holds data from an earlier step
@@ -95,6 +98,16 @@ class FlatStore:
                 gv = self._view(self.grad, s, p.data)
                 gv.copy_(g)
                 p.grad = gv
+
+    @property
+    def grad(self) -> torch.Tensor:
+        if self._grad is None:
+            self._grad = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
+        return self._grad
+
+    @property
+    def grad_allocated(self) -> bool:
+        return self._grad is not None
 
     @staticmethod
     def _view(buf: torch.Tensor, s: Slot, like: torch.Tensor) -> torch.Tensor:

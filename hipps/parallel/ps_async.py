@@ -82,7 +82,8 @@ def _align(x: int, a: int = 256) -> int:
 
 def ps_memory_budget(numel: int, W: int, slots: int, slot_bytes: int, npub: int, pub_esz: int, opt_floats: int,
                      colocated: bool = True, worker_wire_bytes: int = 0, shadow: bool = False,
-                     codec_state_floats: int = 0, acc_floats: Optional[int] = None) -> Dict[str, int]:
+                     codec_state_floats: int = 0, acc_floats: Optional[int] = None,
+                     grad_floats: Optional[int] = None) -> Dict[str, int]:
     """Bytes the async PS adds on rank 0's GPU, term by term.
 
     PS terms (allocated by the engine):
@@ -93,7 +94,9 @@ def ps_memory_budget(numel: int, W: int, slots: int, slot_bytes: int, npub: int,
                                                  M = 1 with per-bucket versions)
       optimizer    opt_floats * numel * 4        momentum (SGD) / moments (Adam) on the master
       chunk_steps  numel / 16 * 4                per-parameter step counters
-    Co-located worker 0 (rank 0 also trains, ``colocated``): its fp32 parameters and gradients,
+    Co-located worker 0 (rank 0 also trains, ``colocated``): its fp32 parameters and gradients
+    (the flat buffer, or -- gather mode -- the autograd-owned tensors the bucket gathers read,
+    alive until the next zero_grad: the flat buffer is then never allocated, FlatStore.grad),
     the bf16 weight shadow, its wire image and codec state (error-feedback residuals).  Its
     activations are the model's own and are not counted."""
     b = {
@@ -106,7 +109,8 @@ def ps_memory_budget(numel: int, W: int, slots: int, slot_bytes: int, npub: int,
     }
     b["ps_total"] = sum(b.values())
     if colocated:
-        w = {"worker_params": numel * 4, "worker_grads": numel * 4, "worker_shadow": numel * 2 if shadow else 0,
+        w = {"worker_params": numel * 4, "worker_grads": (numel if grad_floats is None else grad_floats) * 4,
+             "worker_shadow": numel * 2 if shadow else 0,
              "worker_wire": worker_wire_bytes, "worker_codec_state": codec_state_floats * numel * 4}
         b.update(w)
         b["worker_total"] = sum(w.values())
@@ -198,7 +202,8 @@ HBM_FRACTION = 0.85         # the PS + co-located worker state may take this muc
 def plan_geometry(msg_nbytes: Sequence[int], pres_bytes: int, numel: int, W: int, pub_esz: int, opt_floats: int,
                   mailbox_slots: int = 0, mailbox_mb: float = 4096.0, max_slots: int = 64, npub_max: int = 4,
                   npub: int = 0, colocated: bool = True, worker_wire_bytes: int = 0, shadow: bool = False,
-                  codec_state_floats: int = 0, hbm_bytes: Optional[int] = None, acc_floats: Optional[int] = None):
+                  codec_state_floats: int = 0, hbm_bytes: Optional[int] = None, acc_floats: Optional[int] = None,
+                  grad_floats: Optional[int] = None):
     """Mailbox + publish geometry of the async PS sized from rank 0's HBM budget (VERDICT r4
     item 2: Llama-3-8B at W=8 must fit by default).  Start from the full geometry (``npub_max``
     rotating publish buffers, a ring of two steps' messages per worker capped by ``mailbox_mb``);
@@ -215,7 +220,8 @@ def plan_geometry(msg_nbytes: Sequence[int], pres_bytes: int, numel: int, W: int
     def bud(r, n):
         return ps_memory_budget(numel, W, 1, r, n, pub_esz, opt_floats, colocated=colocated,
                                 worker_wire_bytes=worker_wire_bytes, shadow=shadow,
-                                codec_state_floats=codec_state_floats, acc_floats=acc_floats)
+                                codec_state_floats=codec_state_floats, acc_floats=acc_floats,
+                                grad_floats=grad_floats)
 
     limit = None if hbm_bytes is None else int(HBM_FRACTION * hbm_bytes)
     b = bud(ring, np_)
@@ -1727,7 +1733,9 @@ class PSAsyncEngine(Engine):
             if self._wait_log is not None and a0 < s - self.SLOTS:
                 self._wait_log.append(("slot", s, s - self.SLOTS, a0, dt))
         b = self.plan.buckets[bi]
-        src = self.plan.message(self.wire, bi)  # layout (+ canary guard in debug_canary)
+        # the wire image (layout + canary guard in debug_canary) -- not touched by a direct push,
+        # which encodes into the ring itself (rank 0 then never allocates the image)
+        src = None if encode else self.plan.message(self.wire, bi)
         vidx = self.rank * self.MAXSLOTS + slot
         last = pos == self.nb - 1 or self.bucketwise  # bucket mode: every message carries presence
         pres = 1 if (last and partial) else 0

@@ -203,10 +203,12 @@ def _scratch(rank, world, native):
         opt.step()
         losses.append(float(loss))
     torch.cuda.synchronize()
-    st = eng.ps_stats() if rank == 0 else {}
     wire_alloc = eng._wire is not None
+    grad_alloc = eng.store.grad_allocated
+    torch.distributed.barrier()  # every worker pushed its last message; close() drains the PS
     opt.close()
-    return {"info": info, "stats": st, "losses": losses, "wire_alloc": wire_alloc,
+    st = opt._last_engine_stats if rank == 0 else {}
+    return {"info": info, "stats": st, "losses": losses, "wire_alloc": wire_alloc, "grad_alloc": grad_alloc,
             "params": [p.detach().cpu() for p in m.parameters()]}
 
 
@@ -215,7 +217,8 @@ def test_m1_accumulator_scratch_with_remote_workers(native):
     """accumulate=1 with per-bucket versions and three ranks: the peer-written messages go through
     ONE bucket-sized accumulator scratch (not a model-sized fp32 buffer), each applied before the
     next is accumulated; every message is counted and applied, training stays finite and close to
-    the Python loop's, and rank 0 (direct push) never allocates its wire image."""
+    the Python loop's, rank 0 (direct push) never allocates its wire image and no rank allocates
+    the flat gradient buffer."""
     res = run_world(_scratch, 3, native, timeout=300)
     info, st = res[0]["info"], res[0]["stats"]
     assert info["scratch"] and info["acc"] < info["numel"] and info["acc"] >= info["big"]
@@ -223,6 +226,8 @@ def test_m1_accumulator_scratch_with_remote_workers(native):
     assert st["accumulated"] == 18 and st["bucket_updates"] == 18 * info["nb"]
     assert st.get("direct_updates", 0) == 6 * info["nb"]  # rank 0's own messages
     assert not res[0]["wire_alloc"]
+    # bf16 codec, gather mode: autograd's gradients go straight into the messages on every rank
+    assert not any(r["grad_alloc"] for r in res)
     for r in res:
         assert all(torch.isfinite(p).all() for p in r["params"])
         assert r["losses"][-1] < r["losses"][0]

@@ -20,6 +20,10 @@
 #   codec            bench/codec_bench.py
 #   tuner            tools/tuner_dump.py after a bench (which layers chose which kernel)
 #   g2probe          tools/gemm2_probe.py (every gemm2 tile vs the first core / hipBLASLt / MIOpen)
+#   scale8           ONLY on an 8-GPU node (never on the one-GPU pool): tests/test_multigpu.py with
+#                    one rank per device (W = every device; the cross-device bitwise parity, chunked
+#                    mailbox and W=8-geometry cases), then bench.py at N = 2, 4, 8 under
+#                    torch.distributed.run -> scale_n{2,4,8}.json
 #
 # Extra bench.py arguments for bench/prof: BENCH_ARGS; env for every step is inherited.
 set -o pipefail
@@ -51,6 +55,18 @@ for step in "$@"; do
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread "${K[@]}" \
         > "$OUT/gpu_tests.log" 2>&1 || fail tests "$OUT/gpu_tests.log"
       tail -1 "$OUT/gpu_tests.log" ;;
+    scale8)
+      ndev=$(python -c "import torch; print(torch.cuda.device_count())")
+      if [ "$ndev" -lt 8 ]; then echo "scale8: needs an 8-GPU node (found $ndev devices)"; exit 2; fi
+      timeout -k 10 1800 python -u -m pytest tests/test_multigpu.py -v --timeout 600 --timeout-method thread \
+        > "$OUT/multigpu_tests.log" 2>&1 || fail multigpu "$OUT/multigpu_tests.log"
+      tail -1 "$OUT/multigpu_tests.log"
+      for n in 2 4 8; do
+        timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 \
+          --master-port $((29700 + n)) bench.py --gpus "$n" --steps 20 --warmup 5 --out "$OUT/scale_n$n.json" \
+          > "$OUT/scale_n$n.log" 2>&1 || fail "scale n=$n" "$OUT/scale_n$n.log"
+        cut -c1-200 "$OUT/scale_n$n.json"
+      done ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
         || fail smoke "$OUT/smoke.log"
