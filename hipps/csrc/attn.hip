@@ -68,6 +68,7 @@ struct Args {
   int64_t qsb, ksb, vsb, osb, dosb;       // batch strides (elements)
   int64_t qss, qsh, kss, ksh, vss, vsh;   // sequence / head strides
   int64_t oss, osh, doss, dosh;
+  int64_t gqb, gqs, gqh, gkb, gks, gkh;  // dq / (dk, dv) output strides (packed QKV gradients)
   int B, Hq, Hkv, Sq, Sk;
   float scale;
   int nblk;    // query blocks (forward / dQ) or key blocks (dK/dV) of QB rows
@@ -353,7 +354,7 @@ __global__ __launch_bounds__(256) void k_attn_dq(Args a) {
       }
   }
   if (qok) {
-    uint16_t* gp = a.dq + ((int64_t)b * a.Sq + qrow) * a.Hq * D + (int64_t)hq * D;
+    uint16_t* gp = a.dq + b * a.gqb + (int64_t)qrow * a.gqs + hq * a.gqh;
     const float sc = a.scale;
 #pragma unroll
     for (int db = 0; db < DB; ++db)
@@ -459,7 +460,7 @@ __global__ __launch_bounds__(256) void k_attn_dkdv(Args a) {
   const bool kok = key < kv_end;  // padded keys: zero gradient
   const float sc = a.scale;
   if (a.gsplit == 1) {
-    const int64_t off = (((int64_t)b * a.Sk + key) * a.Hkv + hk) * D;
+    const int64_t off = b * a.gkb + (int64_t)key * a.gks + hk * a.gkh;
 #pragma unroll
     for (int db = 0; db < DB; ++db)
 #pragma unroll
@@ -489,8 +490,10 @@ __global__ __launch_bounds__(256) void k_attn_dkdv(Args a) {
   }
 }
 
-// dK / dV of a split GQA group: sum the slices in order (deterministic), cast to bf16
-__global__ __launch_bounds__(256) void k_attn_gsum(const float* __restrict__ part, int gsplit, int64_t n,
+// dK / dV of a split GQA group: sum the slices in order (deterministic), cast to bf16 into the
+// (possibly strided) outputs; the partials are contiguous [B, Sk, Hkv, D]
+__global__ __launch_bounds__(256) void k_attn_gsum(const float* __restrict__ part, int gsplit, int64_t n, int D,
+                                                   int Hkv, int Sk, int64_t sb, int64_t ss, int64_t sh,
                                                    uint16_t* __restrict__ dk, uint16_t* __restrict__ dv) {
   for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < 2 * n; i += (int64_t)gridDim.x * 1024) {
     float4 s = *reinterpret_cast<const float4*>(part + i);
@@ -498,7 +501,14 @@ __global__ __launch_bounds__(256) void k_attn_gsum(const float* __restrict__ par
       const float4 x = *reinterpret_cast<const float4*>(part + (int64_t)g * 2 * n + i);
       s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
     }
-    uint16_t* o = i < n ? dk + i : dv + (i - n);
+    const int64_t j = i < n ? i : i - n;
+    const int d = (int)(j % D);
+    int64_t r = j / D;
+    const int hk = (int)(r % Hkv);
+    r /= Hkv;
+    const int key = (int)(r % Sk);
+    const int64_t b = r / Sk;
+    uint16_t* o = (i < n ? dk : dv) + b * sb + (int64_t)key * ss + hk * sh + d;
     store4(o, s.x, s.y, s.z, s.w);
   }
 }
@@ -581,7 +591,9 @@ std::vector<at::Tensor> attn_forward(at::Tensor q, at::Tensor k, at::Tensor v, b
 
 // gradients of attn_forward: returns (dq, dk, dv) contiguous in the layouts of q, k, v
 std::vector<at::Tensor> attn_backward(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o,
-                                      at::Tensor lse, bool causal, double scale, c10::optional<at::Tensor> kvlen) {
+                                      at::Tensor lse, bool causal, double scale, c10::optional<at::Tensor> kvlen,
+                                      c10::optional<at::Tensor> dq_out, c10::optional<at::Tensor> dk_out,
+                                      c10::optional<at::Tensor> dv_out) {
   attn::Args a = attn::make_args(q, k, v, causal, scale, kvlen);
   attn::check_qkv(dout, "dout");
   attn::check_qkv(o, "o");
@@ -594,23 +606,40 @@ std::vector<at::Tensor> attn_backward(at::Tensor dout, at::Tensor q, at::Tensor 
   a.dout = (const uint16_t*)dout.data_ptr();
   a.dosb = dout.stride(0); a.doss = dout.stride(1); a.dosh = dout.stride(2);
   a.lse = lse.data_ptr<float>();
-  at::Tensor dq = at::empty(q.sizes(), q.options());
-  at::Tensor dk = at::empty({k.size(0), k.size(1), k.size(2), D}, k.options());
-  at::Tensor dv = at::empty({k.size(0), k.size(1), k.size(2), D}, k.options());
+  // outputs: contiguous, or caller-provided views (a packed [B, S, 3, H, D] QKV gradient: the
+  // kernels write dq / dk / dv straight into it, no concatenation pass)
+  auto out_or = [&](const c10::optional<at::Tensor>& t, const at::Tensor& like, const char* name) {
+    if (t.has_value() && t->defined()) {
+      attn::check_qkv(*t, name);
+      TORCH_CHECK(t->sizes() == like.sizes(), "attn: ", name, " shape");
+      return *t;
+    }
+    return at::empty(like.sizes(), like.options());
+  };
+  at::Tensor dq = out_or(dq_out, q, "dq_out");
+  at::Tensor dk = out_or(dk_out, k, "dk_out");
+  at::Tensor dv = out_or(dv_out, k, "dv_out");
+  TORCH_CHECK(dk.strides() == dv.strides(), "attn: dk_out / dv_out must share strides");
   a.dq = (uint16_t*)dq.data_ptr();
   a.dk = (uint16_t*)dk.data_ptr();
   a.dv = (uint16_t*)dv.data_ptr();
+  a.gqb = dq.stride(0); a.gqs = dq.stride(1); a.gqh = dq.stride(2);
+  a.gkb = dk.stride(0); a.gks = dk.stride(1); a.gkh = dk.stride(2);
   a.nblk = a.nqblk = (a.Sq + attn::QB - 1) / attn::QB;
   at::Tensor rowstat = at::empty({(int64_t)a.B * a.Hq * 2 * a.nblk * 128}, q.options().dtype(at::kFloat));
   a.rowstat = rowstat.data_ptr<float>();
   const int64_t gq = (int64_t)a.nblk * a.B * a.Hq;
   ATTN_DISPATCH(attn::k_attn_dq, D, causal, (unsigned)gq, a);
-  // dK / dV: split the GQA group over workgroups when the (batch, kv head, key block) grid would
-  // leave CUs idle; the slices' fp32 partials are summed in a fixed order
+  // dK / dV: split the GQA group over workgroups when the (batch, kv head, key block) grid is
+  // small: under the causal mask the first key block of a sequence sweeps every query tile and
+  // the last one a single tile, so a grid that fits the GPU in one wave runs as long as its
+  // heaviest workgroup (Llama-3-1B, 512 workgroups: 2x the mean); more, lighter workgroups
+  // launched heaviest-first balance.  The slices' fp32 partials are summed in a fixed order.
   const int nkb = (a.Sk + attn::QB - 1) / attn::QB;
   const int G = a.Hq / a.Hkv;
+  const int64_t want = causal ? 2048 : 512;
   int gsplit = 1;
-  while (gsplit < G && (int64_t)nkb * a.B * a.Hkv * gsplit < 512 && G % (gsplit * 2) == 0) gsplit *= 2;
+  while (gsplit < G && (int64_t)nkb * a.B * a.Hkv * gsplit < want && G % (gsplit * 2) == 0) gsplit *= 2;
   a.gsplit = gsplit;
   at::Tensor part;
   if (gsplit > 1) {
@@ -623,8 +652,8 @@ std::vector<at::Tensor> attn_backward(at::Tensor dout, at::Tensor q, at::Tensor 
   if (gsplit > 1) {
     const int64_t n = dk.numel();
     const int grid = (int)std::min<int64_t>(2048, (2 * n / 4 + 255) / 256);
-    hipLaunchKernelGGL(attn::k_attn_gsum, grid, 256, 0, c10::hip::getCurrentHIPStream(), a.part, gsplit, n,
-                       (uint16_t*)dk.data_ptr(), (uint16_t*)dv.data_ptr());
+    hipLaunchKernelGGL(attn::k_attn_gsum, grid, 256, 0, c10::hip::getCurrentHIPStream(), a.part, gsplit, n, (int)D,
+                       a.Hkv, a.Sk, a.gkb, a.gks, a.gkh, (uint16_t*)dk.data_ptr(), (uint16_t*)dv.data_ptr());
   }
   return {dq, dk, dv};
 }

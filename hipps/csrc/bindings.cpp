@@ -104,7 +104,9 @@ void colsum_bf16(at::Tensor x, at::Tensor out);
 std::vector<at::Tensor> attn_forward(at::Tensor q, at::Tensor k, at::Tensor v, bool causal, double scale,
                                      c10::optional<at::Tensor> kvlen);
 std::vector<at::Tensor> attn_backward(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o,
-                                      at::Tensor lse, bool causal, double scale, c10::optional<at::Tensor> kvlen);
+                                      at::Tensor lse, bool causal, double scale, c10::optional<at::Tensor> kvlen,
+                                      c10::optional<at::Tensor> dq_out, c10::optional<at::Tensor> dk_out,
+                                      c10::optional<at::Tensor> dv_out);
 void swiglu_forward(at::Tensor a, at::Tensor b, at::Tensor c);
 void ln_forward(at::Tensor x, at::Tensor w, at::Tensor b, at::Tensor y, at::Tensor mean, at::Tensor rstd, double eps);
 void ln_backward(at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor rstd, at::Tensor w, at::Tensor dx,
@@ -274,6 +276,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "flash attention forward on MFMA: q [B,Sq,Hq,D], k/v [B,Sk,Hkv,D] bf16 -> (o, lse) (attn.hip)");
   m.def("attn_backward", &hipps::attn_backward, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),
         py::arg("o"), py::arg("lse"), py::arg("causal"), py::arg("scale"), py::arg("kv_len") = py::none(),
+        py::arg("dq_out") = py::none(), py::arg("dk_out") = py::none(), py::arg("dv_out") = py::none(),
         "flash attention backward (deterministic dQ and dK/dV kernels) -> (dq, dk, dv) (attn.hip)");
   m.def("xent_forward", &hipps::xent_forward,
         "fused softmax cross-entropy over bf16 logits: (mean loss, counted rows, per-row log-sum-exp)");

@@ -328,7 +328,31 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_fwd(const uint16_t* __restr
     }
   };
   int64_t v = v0;
-  if constexpr (UNR > 1) {
+  if constexpr (UNR == 3) {
+    // software pipeline: the next vector's loads are issued before this one's stores, so the
+    // wait for them (vmcnt counts stores too, in issue order) never waits for a store to land
+    float xa[8], ra[8];
+    if (v < V) {
+      load8(x + v * 8, xa);
+      if (res) load8(res + v * 8, ra);
+    }
+    for (; v < V; v += stride) {
+      const int64_t vn = v + stride;
+      float xb[8], rb[8];
+      if (vn < V) {
+        load8(x + vn * 8, xb);
+        if (res) load8(res + vn * 8, rb);
+      }
+      body(xa, ra, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        xa[j] = xb[j];
+        ra[j] = rb[j];
+      }
+    }
+    return;
+  }
+  if constexpr (UNR == 2) {
     for (; v + (UNR - 1) * stride < V; v += UNR * stride) {
       float xv[UNR][8], rv[UNR][8];
 #pragma unroll
@@ -389,11 +413,44 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_bwd(const uint16_t* __restr
   };
   constexpr bool need_y = mask_mode == MASK_Y, need_b = mask_mode == MASK_BITS;
   int64_t v = v0;
-  for (; v + (UNR - 1) * stride < V; v += UNR * stride) {  // UNR vectors in flight per lane
-    float d[UNR][8], xv[UNR][8], yv[need_y ? UNR : 1][8];
-    uint32_t mb[UNR];
+  if constexpr (UNR == 0) {
+    // software pipeline (HIPPS_BN_PIPE=1): the next vector's loads go out before this vector's
+    // stores, so waiting for them never waits on a store (vmcnt counts both, in issue order)
+    float d0[8], x0[8], y0[8];
+    uint32_t m0 = 0;
+    if (v < V) {
+      load8(dy + v * 8, d0);
+      load8(x + v * 8, x0);
+      if (need_y) load8(y + v * 8, y0);
+      m0 = need_b ? (uint32_t)mbits[v] : 0u;
+    }
+    for (; v < V; v += stride) {
+      const int64_t vn = v + stride;
+      float d1[8], x1[8], y1[8];
+      uint32_t m1 = 0;
+      if (vn < V) {
+        load8(dy + vn * 8, d1);
+        load8(x + vn * 8, x1);
+        if (need_y) load8(y + vn * 8, y1);
+        m1 = need_b ? (uint32_t)mbits[vn] : 0u;
+      }
+      body(d0, x0, y0, m0, v * 8);
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
+      for (int j = 0; j < 8; ++j) {
+        d0[j] = d1[j];
+        x0[j] = x1[j];
+        y0[j] = y1[j];
+      }
+      m0 = m1;
+    }
+    return;
+  }
+  constexpr int UN = UNR > 0 ? UNR : 1;  // (UNR == 0 returned above)
+  for (; v + (UN - 1) * stride < V; v += UN * stride) {  // UNR vectors in flight per lane
+    float d[UN][8], xv[UN][8], yv[need_y ? UN : 1][8];
+    uint32_t mb[UN];
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
       const int64_t o = (v + u * stride) * 8;
       load8(dy + o, d[u]);
       load8(x + o, xv[u]);
@@ -401,7 +458,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_bwd(const uint16_t* __restr
       mb[u] = need_b ? (uint32_t)mbits[v + u * stride] : 0u;
     }
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) body(d[u], xv[u], yv[need_y ? u : 0], mb[u], (v + u * stride) * 8);
+    for (int u = 0; u < UN; ++u) body(d[u], xv[u], yv[need_y ? u : 0], mb[u], (v + u * stride) * 8);
   }
   for (; v < V; v += stride) {
     float d0[8], x0[8], y0[8];
@@ -522,7 +579,16 @@ ApplyFwdFn apply_fwd_kernel(int64_t M, int C) {
     return e ? std::atoi(e) : 1;
   }();
   if (unr == 2 && M * (C / 8) >= (int64_t(4) << 20)) return k_bn_apply_fwd<2>;
+  if (unr == 3) return k_bn_apply_fwd<3>;  // software-pipelined (A/B)
   return k_bn_apply_fwd<1>;
+}
+// HIPPS_BN_PIPE=1: the software-pipelined backward apply (k_bn_apply_bwd<MODE, 0>) -- A/B
+bool bn_pipe() {
+  static const bool on = [] {
+    const char* e = std::getenv("HIPPS_BN_PIPE");
+    return e != nullptr && std::atoi(e) != 0;
+  }();
+  return on;
 }
 }  // namespace
 
@@ -735,6 +801,15 @@ void bn_backward(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> y, int64
                        coef[0].data_ptr<float>(), coef[1].data_ptr<float>(), coef[2].data_ptr<float>(),
                        (uint16_t*)dx.data_ptr(), drp, M, (int)C);
   };
+  if (bn_pipe()) {
+    switch (mask_mode) {
+      case MASK_NONE: app(k_bn_apply_bwd<MASK_NONE, 0>); break;
+      case MASK_X: app(k_bn_apply_bwd<MASK_X, 0>); break;
+      case MASK_Y: app(k_bn_apply_bwd<MASK_Y, 0>); break;
+      default: app(k_bn_apply_bwd<MASK_BITS, 0>); break;
+    }
+    return;
+  }
   switch (mask_mode) {
     case MASK_NONE: app(k_bn_apply_bwd<MASK_NONE>); break;
     case MASK_X: app(k_bn_apply_bwd<MASK_X>); break;
@@ -829,7 +904,13 @@ void bn_backward_partials(at::Tensor part, int64_t nrb, at::Tensor dy, at::Tenso
                        coef[0].data_ptr<float>(), coef[1].data_ptr<float>(), coef[2].data_ptr<float>(),
                        (uint16_t*)dx.data_ptr(), drp, M, (int)C);
   };
-  if (unr == 4) {
+  if (bn_pipe()) {
+    switch (mask_mode) {
+      case MASK_NONE: app(k_bn_apply_bwd<MASK_NONE, 0>); break;
+      case MASK_X: app(k_bn_apply_bwd<MASK_X, 0>); break;
+      default: app(k_bn_apply_bwd<MASK_BITS, 0>); break;
+    }
+  } else if (unr == 4) {
     switch (mask_mode) {
       case MASK_NONE: app(k_bn_apply_bwd<MASK_NONE, 4>); break;
       case MASK_X: app(k_bn_apply_bwd<MASK_X, 4>); break;
@@ -938,7 +1019,8 @@ void bn_dual_backward(c10::optional<at::Tensor> part3, int64_t nrb3, at::Tensor 
   else if (unr == 8) dual(k_bn_bwd_dual<8>);
   else dual(k_bn_bwd_dual<4>);
   finb(pd.data_ptr<float>(), nrb, wd, meand, invstdd, dwd, dbd, coefd);
-  hipLaunchKernelGGL(k_bn_apply_bwd<MASK_BITS>, apply_grid(M, (int)C), kBlock, 0, stream,
+  auto appk = bn_pipe() ? k_bn_apply_bwd<MASK_BITS, 0> : k_bn_apply_bwd<MASK_BITS>;
+  hipLaunchKernelGGL(appk, apply_grid(M, (int)C), kBlock, 0, stream,
                      (const uint16_t*)dz.data_ptr(), (const uint16_t*)xd.data_ptr(), nullptr, mbp, nullptr, nullptr,
                      coefd[0].data_ptr<float>(), coefd[1].data_ptr<float>(), coefd[2].data_ptr<float>(),
                      (uint16_t*)dxd.data_ptr(), nullptr, M, (int)C);

@@ -1,7 +1,9 @@
 """Transformer models for BASELINE configs 4 and 5 (random init, synthetic tokens).
 
   bert-base   BertModel layout (12 x 768, 12 heads, FFN 3072, vocab 30522, 512 positions, pooler)
-              = 109,482,240 params in 199 tensors + a tied-decoder MLM head.
+              = 109,482,240 params + a tied-decoder MLM head; the query / key /
+              value projections are one fused [2304, 768] Linear per layer (175 tensors instead
+              of the 199 of separate q / k / v -- same parameter count and math).
               Config 4 ("BERT-base async PS, variable-size per-layer grad buckets").
   llama3-8b   Llama-3 8B (32 x 4096, 32 q / 8 kv heads, SwiGLU 14336, RMSNorm, RoPE theta 5e5,
               vocab 128256) = 8.03 B params.  Config 5 ("Llama-3 8B pure-DP async PS").
@@ -60,9 +62,10 @@ class BertLayer(nn.Module):
     def __init__(self, c: BertConfig):
         super().__init__()
         self.heads = c.heads
-        self.q = hnn.Linear(c.hidden, c.hidden)
-        self.k = hnn.Linear(c.hidden, c.hidden)
-        self.v = hnn.Linear(c.hidden, c.hidden)
+        # the query / key / value projections as ONE [3 * hidden, hidden] weight (+ [3 * hidden]
+        # bias): same parameters and math as three Linears, one GEMM each way instead of three,
+        # and the input gradient comes out of one GEMM (no two autograd adds per layer)
+        self.qkv = hnn.Linear(c.hidden, 3 * c.hidden)
         self.attn_out = hnn.Linear(c.hidden, c.hidden)
         self.attn_ln = nn.LayerNorm(c.hidden, eps=c.eps)
         self.inter = hnn.Linear(c.hidden, c.ffn)
@@ -73,16 +76,14 @@ class BertLayer(nn.Module):
         B, S, D = x.shape
         h = self.heads
 
-        def split(t):
-            return t.view(B, S, h, D // h)
-
+        qkv = self.qkv(x).view(B, S, 3, h, D // h)
         if mask is None or (torch.is_tensor(mask) and mask.dtype == torch.int32 and mask.dim() == 1):
-            # [B, S, H, hd] views of the projections straight into the hipps flash-attention kernels
-            # (csrc/attn.hip); ``mask`` may be the int32 [B] key lengths of a padded batch
-            a = hnn.attention(split(self.q(x)), split(self.k(x)), split(self.v(x)), kv_len=mask)
+            # the packed [B, S, 3, H, hd] projection straight into the hipps flash-attention
+            # kernels (csrc/attn.hip); ``mask`` may be the int32 [B] key lengths of a padded batch
+            a = hnn.attention_qkv(qkv, kv_len=mask)
         else:
-            a = F.scaled_dot_product_attention(split(self.q(x)).transpose(1, 2), split(self.k(x)).transpose(1, 2),
-                                               split(self.v(x)).transpose(1, 2), attn_mask=mask).transpose(1, 2)
+            q, k, v = (t.transpose(1, 2) for t in qkv.unbind(2))
+            a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask).transpose(1, 2)
         a = a.reshape(B, S, D)
         # residual adds ride in the output projections (GEMM epilogue / hipBLASLt C)
         x = _ln(self.attn_ln, self.attn_out(a, residual=x))

@@ -1082,6 +1082,46 @@ class _FlashAttention(torch.autograd.Function):
         return dq, dk, dv, None, None, None
 
 
+class _FlashAttentionQKV(torch.autograd.Function):
+    """Attention over q / k / v packed in one [B, S, 3, H, D] tensor (a fused QKV projection's
+    output viewed per head).  The backward writes dq, dk and dv straight into ONE packed gradient
+    of the same layout (attn_backward's strided outputs), so the projection's backward reads a
+    single [B*S, 3*H*D] gradient -- no per-slice zero-fill / copy / sum that autograd would run for
+    three separate views."""
+
+    @staticmethod
+    def forward(ctx, qkv, causal, scale, kv_len):
+        q, k, v = qkv.unbind(2)
+        o, lse = native().attn_forward(q, k, v, causal, scale, kv_len)
+        ctx.save_for_backward(qkv, o, lse, kv_len)
+        ctx.causal, ctx.scale = causal, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse, kv_len = ctx.saved_tensors
+        do = do.to(torch.bfloat16)
+        if not _attn_rows_ok(do):
+            do = do.contiguous()
+        g = torch.empty(qkv.shape, dtype=torch.bfloat16, device=qkv.device)
+        q, k, v = qkv.unbind(2)
+        gq, gk, gv = g.unbind(2)
+        native().attn_backward(do, q, k, v, o, lse, ctx.causal, ctx.scale, kv_len, gq, gk, gv)
+        return g, None, None, None
+
+
+def attention_qkv(qkv: torch.Tensor, causal: bool = False, scale: Optional[float] = None,
+                  kv_len: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """:func:`attention` of q, k, v packed as ``qkv`` [B, S, 3, H, D] (e.g. ``linear(x, W_qkv)
+    .view(B, S, 3, H, D)``); returns [B, S, H, D]."""
+    q, k, v = qkv.unbind(2)
+    if attention_ok(q, k, v, causal) and qkv.dtype == torch.bfloat16:
+        sc = float(scale) if scale is not None else 1.0 / (qkv.shape[-1] ** 0.5)
+        kl = None if kv_len is None else kv_len.to(device=qkv.device, dtype=torch.int32).contiguous()
+        return _FlashAttentionQKV.apply(qkv, bool(causal), sc, kl)
+    return attention(q, k, v, causal=causal, scale=scale, kv_len=kv_len)
+
+
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = False,
               scale: Optional[float] = None, kv_len: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Scaled dot-product attention on the [batch, seq, heads, head_dim] layout (the projection

@@ -137,13 +137,12 @@ def test_flash_attention_in_models(monkeypatch):
     from hipps.models import transformer as tf
 
     calls = []
-    fwd = hnn._FlashAttention.forward
+    for cls in (hnn._FlashAttention, hnn._FlashAttentionQKV):  # Llama: separate q / k / v; BERT: packed
+        def counted(ctx, *a, _fwd=cls.forward):
+            calls.append(1)
+            return _fwd(ctx, *a)
 
-    def counted(ctx, *a):
-        calls.append(1)
-        return fwd(ctx, *a)
-
-    monkeypatch.setattr(hnn._FlashAttention, "forward", staticmethod(counted))
+        monkeypatch.setattr(cls, "forward", staticmethod(counted))
     torch.manual_seed(0)
     models = [(tf.Bert(tf.BertConfig(vocab=512, hidden=128, layers=2, heads=2, ffn=256, max_pos=128)), 2),
               (tf.Llama(tf.LlamaConfig(vocab=512, dim=256, layers=2, heads=2, kv_heads=1, ffn=256, max_seq=128)), 2)]
@@ -166,3 +165,25 @@ def test_flash_attention_in_models(monkeypatch):
         num = sum((a - b).norm() ** 2 for a, b in zip(g1, g0)) ** 0.5
         den = sum(b.norm() ** 2 for b in g0) ** 0.5
         assert num / den < 5e-2, num / den
+
+
+@pytest.mark.parametrize("padded", [False, True])
+def test_packed_qkv_attention_matches_separate(padded):
+    """attention_qkv (one packed [B, S, 3, H, D] input, its gradient written packed by the kernels)
+    equals attention on the three views, forward and backward, bit for bit."""
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(21)
+    B, S, H, D = 2, 320, 4, 64
+    base = torch.randn(B, S, 3 * H * D, device="cuda").to(torch.bfloat16)
+    kv_len = torch.tensor([S, S - 77], device="cuda", dtype=torch.int32) if padded else None
+    g = torch.randn(B, S, H, D, device="cuda").to(torch.bfloat16)
+    x1 = base.clone().requires_grad_(True)
+    o1 = hnn.attention_qkv(x1.view(B, S, 3, H, D), kv_len=kv_len)
+    o1.backward(g)
+    x2 = base.clone().requires_grad_(True)
+    q, k, v = x2.view(B, S, 3, H, D).unbind(2)
+    o2 = hnn.attention(q, k, v, kv_len=kv_len)
+    o2.backward(g)
+    assert torch.equal(o1, o2)
+    assert torch.equal(x1.grad, x2.grad)
