@@ -42,6 +42,12 @@ constexpr int BK = 64;  // k per stage = 8 chunks of 16 bytes per row
 
 // 16-byte zero source for out-of-range rows and zero-padding taps (global memory, read-only)
 __device__ __attribute__((aligned(64))) const uint16_t kZero16[32] = {0};
+// the residual-mask byte of an unmasked add (kAdd without RM): every bit set
+__device__ __attribute__((aligned(64))) const uint8_t kOnes8[64] = {
+    0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+    0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+    0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+    0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff};
 
 // epilogue flags: kStats = forward BN statistics of Y; kAdd = Y += R (* mask bits); kBst =
 // backward BN statistics of the BN whose output gradient Y is (relu' recomputed from x * scale +
@@ -96,6 +102,7 @@ struct Args {
   int tdr[4], tdc[4], tko[4];
   const float *psc, *psh;  // kPro: per-channel scale / shift of the A operand's BN
   const float* bias;       // kBias: f32 [N]
+  int epf;                 // EPF allowed (HIPPS_G2_EPF, default 1)
 };
 
 __device__ __forceinline__ uint32_t add_bf16x2(uint32_t a, uint32_t b) {
@@ -320,9 +327,22 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   constexpr int RCH = BN / 8;             // 16-byte chunks per output row
   constexpr int NOUT = BM * RCH / NT;     // output chunks per thread
   constexpr int NSTR = (ADDE ? 1 : 0) + (BSTE ? 1 : 0);       // epilogue operand streams
-  constexpr bool PF = NSTR > 0 && NOUT * 5 * NSTR <= 40;     // <= 40 registers
+  // EPF: a 1x1 GEMM with a short K (<= 2 tiles: the memory-bound dgrad passes with a residual
+  // add and a BN-backward reduction, K = 64..128) whose prefetched operands fit (PF) issues them
+  // right after the first tile's DMA, so their HBM latency overlaps the DMA and the MFMAs
+  // instead of following them.  (A larger PF budget for the 128x128 tile measured 138 -> 256
+  // VGPRs: one wave per SIMD.)
+  constexpr bool EPF_OK = !TAPS && !S2 && !PP && !KH && !M32 && !PRO && NSX == 2;
+  constexpr bool PF = NSTR > 0 && NOUT * 5 * NSTR <= 40;  // <= 40 registers
+  // vector-memory instructions of one prefetch (16-byte operand + mask byte per stream and chunk)
+  constexpr int NPFL = PF ? NOUT * ((ADDE ? 2 : 0) + (BSTE == 2 ? 2 : BSTE ? 1 : 0)) : 0;
+  static_assert(NPFL < 64, "vmcnt immediate");
   u32x4 pr[PF && ADDE ? NOUT : 1], px[PF && BSTE ? NOUT : 1];
   uint32_t prm[PF && ADDE ? NOUT : 1], pxm[PF && BSTE ? NOUT : 1];
+  const uint8_t* rm_src = g.RM;  // (no mask: a byte of ones, so every prefetch issues the same loads)
+  if constexpr (ADDE) {
+    if (rm_src == nullptr) rm_src = kOnes8;
+  }
 
   // epilogue operands loaded during the MFMAs of the last K step (no DMA in flight then)
   auto prefetch_epi = [&]() {
@@ -335,7 +355,7 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
           if constexpr (ADDE) {
             const int64_t ro = r_off(m0 + row < g.M ? m0 + row : m0, n0 + c * 8);
             pr[i] = ro >= 0 ? *reinterpret_cast<const u32x4*>(g.R + ro) : u32x4{0u, 0u, 0u, 0u};
-            prm[i] = g.RM != nullptr ? g.RM[o >> 3] : 0xffu;
+            prm[i] = rm_src[rm_src == kOnes8 ? 0 : (o >> 3)];
           }
           if constexpr (BSTE) {
             px[i] = *reinterpret_cast<const u32x4*>(g.bx + o);
@@ -460,12 +480,21 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
     const int KT = g.K / BK;
     issue(0, 0);
     if (NSX == 3 && KT > 1) issue(1, 1);
+    const bool early = EPF_OK && PF && KT <= 2 && g.epf;
+    if (early) {
+      asm volatile("" ::: "memory");  // (the prefetch's loads issue after tile 0's DMA)
+      prefetch_epi();
+      asm volatile("" ::: "memory");
+    }
     int cur = 0;
     for (int kt = 0; kt < KT; ++kt) {
       // this wave's DMA of tile kt has landed and its reads of tile kt-1 are retired; after the
       // barrier every wave's have, so tile kt is readable and tile kt-1's buffer is free to refill
       if (NSX == 3 && kt + 1 < KT) {
         __builtin_amdgcn_s_waitcnt(waitcnt_vm(NG));  // tile kt+1 stays in flight
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      } else if (early && kt == 0) {
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(NPFL));  // tile 0 landed; the epilogue loads stay in flight
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -499,7 +528,7 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
         issue(kt + NSX - 1, nxt);
       } else if (kt + 1 < KT) {
         // NS == 3, second-to-last tile: nothing left to issue
-      } else {
+      } else if (!early) {
         prefetch_epi();
       }
       const uint16_t* As = lds + cur * STAGE;
@@ -1322,6 +1351,11 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
     a.bias = bias->data_ptr<float>();
     epi |= g2::kBias;
   }
+  static const int epf_env = [] {
+    const char* e = std::getenv("HIPPS_G2_EPF");
+    return e ? std::atoi(e) : 1;
+  }();
+  a.epf = epf_env;
   auto stream = c10::hip::getCurrentHIPStream();
   const int grid = (int)(mtiles * ntiles);
 #define HIPPS_G2S(BMc, BNc, EPc, TPc, NSc) \
