@@ -148,7 +148,7 @@ __device__ __forceinline__ void store4(uint16_t* p, float a, float b, float c, f
 
 // ------------------------------------------------------------------------------------ forward
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256) void k_attn_fwd(Args a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_attn_fwd(Args a) {
   constexpr int DK = D / 16, DB = D / 32, TILE = KT * 2 * D;
   __shared__ __attribute__((aligned(16))) char lds[2][2 * TILE];
   const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(Args a) {
 // Also computes delta = rowsum(dO * O) and publishes the per-row constants the dK/dV kernel
 // initialises its accumulators with (rowstat), so no separate preprocess pass reads dO and O.
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256) void k_attn_dq(Args a) {
+__device__ __forceinline__ void attn_dq_body(const Args& a) {
   constexpr int DK = D / 16, DB = D / 32, TILE = KT * 2 * D;
   __shared__ __attribute__((aligned(16))) char lds[2][2 * TILE];
   const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -367,7 +367,7 @@ __global__ __launch_bounds__(256) void k_attn_dq(Args a) {
 
 // ---------------------------------------------------------------------------- backward: dK, dV
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256) void k_attn_dkdv(Args a) {
+__device__ __forceinline__ void attn_dkdv_body(const Args& a) {
   constexpr int DK = D / 16, DB = D / 32, TILE = KT * 2 * D, STG = 2 * TILE + 512;
   __shared__ __attribute__((aligned(16))) char lds[2][STG];
   const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -490,6 +490,25 @@ __global__ __launch_bounds__(256) void k_attn_dkdv(Args a) {
   }
 }
 
+// Register budgets: the head-dim-64 backward kernels fit two waves per SIMD (<= 256 registers);
+// the head-dim-128 ones would spill there, so they keep one wave per SIMD and every register.
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_attn_dq(Args a) {
+  attn_dq_body<D, CAUSAL>(a);
+}
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256) void k_attn_dq_wide(Args a) {
+  attn_dq_body<D, CAUSAL>(a);
+}
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_attn_dkdv(Args a) {
+  attn_dkdv_body<D, CAUSAL>(a);
+}
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256) void k_attn_dkdv_wide(Args a) {
+  attn_dkdv_body<D, CAUSAL>(a);
+}
+
 // dK / dV of a split GQA group: sum the slices in order (deterministic), cast to bf16 into the
 // (possibly strided) outputs; the partials are contiguous [B, Sk, Hkv, D]
 __global__ __launch_bounds__(256) void k_attn_gsum(const float* __restrict__ part, int gsplit, int64_t n, int D,
@@ -557,17 +576,18 @@ Args make_args(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, bo
 
 }  // namespace
 
-#define ATTN_DISPATCH(KER, D_, CAUSAL_, GRID, A)                                                   \
+#define ATTN_DISPATCH2(KER64, KER128, D_, CAUSAL_, GRID, A)                                       \
   do {                                                                                             \
     auto st = c10::hip::getCurrentHIPStream();                                                     \
     if ((D_) == 64) {                                                                              \
-      if (CAUSAL_) hipLaunchKernelGGL((KER<64, true>), dim3(GRID), dim3(256), 0, st, A);            \
-      else hipLaunchKernelGGL((KER<64, false>), dim3(GRID), dim3(256), 0, st, A);                   \
+      if (CAUSAL_) hipLaunchKernelGGL((KER64<64, true>), dim3(GRID), dim3(256), 0, st, A);          \
+      else hipLaunchKernelGGL((KER64<64, false>), dim3(GRID), dim3(256), 0, st, A);                 \
     } else {                                                                                       \
-      if (CAUSAL_) hipLaunchKernelGGL((KER<128, true>), dim3(GRID), dim3(256), 0, st, A);           \
-      else hipLaunchKernelGGL((KER<128, false>), dim3(GRID), dim3(256), 0, st, A);                  \
+      if (CAUSAL_) hipLaunchKernelGGL((KER128<128, true>), dim3(GRID), dim3(256), 0, st, A);        \
+      else hipLaunchKernelGGL((KER128<128, false>), dim3(GRID), dim3(256), 0, st, A);               \
     }                                                                                              \
   } while (0)
+#define ATTN_DISPATCH(KER, D_, CAUSAL_, GRID, A) ATTN_DISPATCH2(KER, KER, D_, CAUSAL_, GRID, A)
 
 }  // namespace attn
 
@@ -629,7 +649,7 @@ std::vector<at::Tensor> attn_backward(at::Tensor dout, at::Tensor q, at::Tensor 
   at::Tensor rowstat = at::empty({(int64_t)a.B * a.Hq * 2 * a.nblk * 128}, q.options().dtype(at::kFloat));
   a.rowstat = rowstat.data_ptr<float>();
   const int64_t gq = (int64_t)a.nblk * a.B * a.Hq;
-  ATTN_DISPATCH(attn::k_attn_dq, D, causal, (unsigned)gq, a);
+  ATTN_DISPATCH2(attn::k_attn_dq, attn::k_attn_dq_wide, D, causal, (unsigned)gq, a);
   // dK / dV: split the GQA group over workgroups when the (batch, kv head, key block) grid is
   // small: under the causal mask the first key block of a sequence sweeps every query tile and
   // the last one a single tile, so a grid that fits the GPU in one wave runs as long as its
@@ -648,7 +668,7 @@ std::vector<at::Tensor> attn_backward(at::Tensor dout, at::Tensor q, at::Tensor 
   }
   a.nblk = nkb;
   const int64_t gk = (int64_t)nkb * a.B * a.Hkv * gsplit;
-  ATTN_DISPATCH(attn::k_attn_dkdv, D, causal, (unsigned)gk, a);
+  ATTN_DISPATCH2(attn::k_attn_dkdv, attn::k_attn_dkdv_wide, D, causal, (unsigned)gk, a);
   if (gsplit > 1) {
     const int64_t n = dk.numel();
     const int grid = (int)std::min<int64_t>(2048, (2 * n / 4 + 255) / 256);
