@@ -136,6 +136,17 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& a, int s) {
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// lane l and lane l ^ 32 hold the two halves of one query row: combine them with
+// v_permlane32_swap (a VALU lane swap) instead of a ds_bpermute round trip through the LDS unit
+__device__ __forceinline__ float half_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float half_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 #define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
 
 // row of accumulator register r for lane half h (32x32 C layout)
@@ -212,7 +223,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kk][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = half_max(mx);
     const float mn = fmaxf(m, mx * c);
     const float mu = mn == -INFINITY ? 0.f : mn;
     const float alpha = fast_exp2(m - mu);
@@ -242,7 +253,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         for (int db = 0; db < DB; ++db) o[db] = MFMA32(tr_frag<D>(Vt, 32 * kk + 16 * s2, db, lane), pf, o[db]);
       }
   }
-  const float lt = lsum + __shfl_xor(lsum, 32, 64);
+  const float lt = half_sum(lsum);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
   if (qrow < a.Sq) {
     uint16_t* op = a.out + b * a.osb + hq * a.osh + (int64_t)qrow * a.oss;
@@ -290,7 +301,7 @@ __device__ __forceinline__ void attn_dq_body(const Args& a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) dl += bf16_to_f32((uint16_t)df[dk][j]) * bf16_to_f32((uint16_t)of[j]);
   }
-  const float delta = qok ? dl + __shfl_xor(dl, 32, 64) : 0.f;
+  const float delta = qok ? half_sum(dl) : 0.f;
   const float c = a.scale * kLog2e;
   const float lse2 = qok ? a.lse[((int64_t)b * a.Hq + hq) * a.Sq + qrow] * kLog2e : INFINITY;
   if (h == 0) {

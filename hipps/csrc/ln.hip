@@ -186,24 +186,34 @@ __global__ __launch_bounds__(64 * kLnWaves) void k_ln_bwd(const uint16_t* __rest
   }
 }
 
-// out[k * D + col] = sum_p part[p][k][col] (k = 0: dgamma, 1: dbeta when nk == 2), fixed order
-__global__ __launch_bounds__(256) void k_ln_fold(const float* __restrict__ part, int P, int D, int nk,
-                                                 float* __restrict__ dw, float* __restrict__ dbias) {
-  __shared__ float red[4][64];
+// out[k * D + col] = sum_p part[p][k][col] (k = 0: dgamma, 1: dbeta when nk == 2), fixed order.
+// 64 columns per workgroup of 16 waves; wave w sums partial rows w, w + 16, ... with 8 loads in
+// flight (D = 768 gives only 24 workgroups: with 4 waves of 4 loads each the fold was a chain of
+// dependent HBM round trips, 24 us per call on BERT-base)
+constexpr int kFoldWaves = 16;
+__global__ __launch_bounds__(64 * kFoldWaves) void k_ln_fold(const float* __restrict__ part, int P, int D, int nk,
+                                                             float* __restrict__ dw, float* __restrict__ dbias) {
+  __shared__ float red[kFoldWaves][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + lane;  // over nk * D
   const int ii = i < nk * D ? i : 0;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t rs = (int64_t)nk * D;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   int p = wv;
-  for (; p + 12 < P; p += 16) {
+  for (; p + 7 * kFoldWaves < P; p += 8 * kFoldWaves) {
+    float v[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] += part[(int64_t)(p + 4 * j) * nk * D + ii];
+    for (int j = 0; j < 8; ++j) v[j] = part[(int64_t)(p + kFoldWaves * j) * rs + ii];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += v[j];
   }
-  for (; p < P; p += 4) acc[0] += part[(int64_t)p * nk * D + ii];
-  red[wv][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  for (; p < P; p += kFoldWaves) acc[0] += part[(int64_t)p * rs + ii];
+  red[wv][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   __syncthreads();
   if (wv == 0 && i < nk * D) {
-    const float a = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    float a = 0.f;
+#pragma unroll
+    for (int q = 0; q < kFoldWaves; ++q) a += red[q][lane];
     if (i < D) dw[i] = a;
     else dbias[i - D] = a;
   }
@@ -407,7 +417,7 @@ void ln_backward(at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor rstd, 
   else if (nc <= 2) HIPPS_LNB(2);
   else HIPPS_LNB(4);
 #undef HIPPS_LNB
-  hipLaunchKernelGGL(k_ln_fold, (int)((2 * D + 63) / 64), 256, 0, st, part.data_ptr<float>(), (int)P, (int)D, 2,
+  hipLaunchKernelGGL(k_ln_fold, (int)((2 * D + 63) / 64), 64 * kFoldWaves, 0, st, part.data_ptr<float>(), (int)P, (int)D, 2,
                      dw.data_ptr<float>(), db.data_ptr<float>());
 }
 
@@ -484,7 +494,7 @@ void rms_backward(at::Tensor dy, at::Tensor x, at::Tensor rstd, at::Tensor w, at
   else if (nc <= 4) HIPPS_RMSB(4);
   else HIPPS_RMSB(8);
 #undef HIPPS_RMSB
-  hipLaunchKernelGGL(k_ln_fold, (int)((D + 63) / 64), 256, 0, st, part.data_ptr<float>(), (int)P, (int)D, 1,
+  hipLaunchKernelGGL(k_ln_fold, (int)((D + 63) / 64), 64 * kFoldWaves, 0, st, part.data_ptr<float>(), (int)P, (int)D, 1,
                      dw.data_ptr<float>(), dw.data_ptr<float>());
 }
 
