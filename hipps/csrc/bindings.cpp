@@ -115,6 +115,8 @@ void rms_forward(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor rstd, doub
 void rms_backward(at::Tensor dy, at::Tensor x, at::Tensor rstd, at::Tensor w, at::Tensor dx, at::Tensor dw);
 void swiglu_backward(at::Tensor g, at::Tensor a, at::Tensor b, at::Tensor da, at::Tensor db);
 void rope_apply(at::Tensor x, at::Tensor y, at::Tensor cs, at::Tensor sn, int64_t S, int64_t hd, double sign);
+void swiglu_rows_forward(at::Tensor y, at::Tensor c);
+void swiglu_rows_backward(at::Tensor g, at::Tensor y, at::Tensor dy);
 void xent_backward(at::Tensor logits, at::Tensor labels, at::Tensor lse, at::Tensor gout, double scale,
                    int64_t ignore_index, at::Tensor dx, c10::optional<at::Tensor> count);
 void bn_finalize_bwd_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tensor weight, at::Tensor mean,
@@ -270,6 +272,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("swiglu_backward", &hipps::swiglu_backward, "gradients of silu(a) * b w.r.t. a and b, bf16 (act.hip)");
   m.def("rope_apply", &hipps::rope_apply, py::arg("x"), py::arg("y"), py::arg("cos"), py::arg("sin"), py::arg("S"),
         py::arg("hd"), py::arg("sign") = 1.0, "rotary embedding of interleaved pairs, fp32 tables (act.hip)");
+  m.def("swiglu_rows_forward", &hipps::swiglu_rows_forward,
+        "c = silu(y[:, :F]) * y[:, F:] for a packed [rows, 2F] gate/up projection (act.hip)");
+  m.def("swiglu_rows_backward", &hipps::swiglu_rows_backward,
+        "packed [rows, 2F] gradient (da | db) of swiglu_rows_forward (act.hip)");
   m.def("colsum_bf16", &hipps::colsum_bf16, "fp32 column sums of a bf16 [rows, cols] matrix (bias gradients)");
   m.def("attn_forward", &hipps::attn_forward, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"),
         py::arg("scale"), py::arg("kv_len") = py::none(),

@@ -6,7 +6,8 @@
               of the 199 of separate q / k / v -- same parameter count and math).
               Config 4 ("BERT-base async PS, variable-size per-layer grad buckets").
   llama3-8b   Llama-3 8B (32 x 4096, 32 q / 8 kv heads, SwiGLU 14336, RMSNorm, RoPE theta 5e5,
-              vocab 128256) = 8.03 B params.  Config 5 ("Llama-3 8B pure-DP async PS").
+              vocab 128256) = 8.03 B params.  Config 5 ("Llama-3 8B pure-DP async PS").  The
+              q / k / v and gate / up projections are fused Linears (same parameters and math).
   *-tiny      same code, small widths, for CPU tests.
 
 Attention is ``hipps.ops.nn.attention`` (csrc/attn.hip: MFMA flash attention, forward and a
@@ -182,12 +183,13 @@ class LlamaBlock(nn.Module):
         super().__init__()
         self.c = c
         hd = c.dim // c.heads
-        self.wq = hnn.Linear(c.dim, c.heads * hd, bias=False)
-        self.wk = hnn.Linear(c.dim, c.kv_heads * hd, bias=False)
-        self.wv = hnn.Linear(c.dim, c.kv_heads * hd, bias=False)
+        # q | k | v as ONE [(heads + 2 kv_heads) * hd, dim] projection and the SwiGLU gate | up as
+        # ONE [2 ffn, dim] projection: the same parameters and math as wq / wk / wv and w1 / w3,
+        # one GEMM each way instead of three (two), and their input gradients come out of one
+        # GEMM (no autograd adds of the slices' gradients)
+        self.wqkv = hnn.Linear(c.dim, (c.heads + 2 * c.kv_heads) * hd, bias=False)
         self.wo = hnn.Linear(c.heads * hd, c.dim, bias=False)
-        self.w1 = hnn.Linear(c.dim, c.ffn, bias=False)
-        self.w3 = hnn.Linear(c.dim, c.ffn, bias=False)
+        self.w13 = hnn.Linear(c.dim, 2 * c.ffn, bias=False)
         self.w2 = hnn.Linear(c.ffn, c.dim, bias=False)
         self.attn_norm = RMSNorm(c.dim, c.eps)
         self.ffn_norm = RMSNorm(c.dim, c.eps)
@@ -197,14 +199,18 @@ class LlamaBlock(nn.Module):
         c = self.c
         hd = D // c.heads
         h = self.attn_norm(x)
-        q = self.wq(h).view(B, S, c.heads, hd)
-        k = self.wk(h).view(B, S, c.kv_heads, hd)
-        v = self.wv(h).view(B, S, c.kv_heads, hd)
-        q, k = _rope(q, cos, sin), _rope(k, cos, sin)
-        a = hnn.attention(q, k, v, causal=True)  # [B, S, H, hd]; causal + GQA in csrc/attn.hip
+        y = self.wqkv(h)  # [B, S, (heads + 2 kv_heads) * hd]
+        if hnn.rope_attention_packed_ok(y, cos, c.heads, c.kv_heads):
+            # RoPE + causal GQA flash attention on the packed projection (csrc/act.hip, attn.hip)
+            a = hnn.rope_attention_packed(y, cos, sin, c.heads, c.kv_heads)
+        else:
+            q, k, v = y.split([c.heads * hd, c.kv_heads * hd, c.kv_heads * hd], dim=-1)
+            q = _rope(q.reshape(B, S, c.heads, hd).contiguous(), cos, sin)
+            k = _rope(k.reshape(B, S, c.kv_heads, hd).contiguous(), cos, sin)
+            a = hnn.attention(q, k, v.reshape(B, S, c.kv_heads, hd), causal=True)
         x = x + self.wo(a.reshape(B, S, D))
         h = self.ffn_norm(x)
-        return x + self.w2(hnn.swiglu(self.w1(h), self.w3(h)))
+        return x + self.w2(hnn.swiglu_packed(self.w13(h)))
 
 
 class Llama(nn.Module):

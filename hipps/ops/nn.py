@@ -1122,6 +1122,70 @@ def attention_qkv(qkv: torch.Tensor, causal: bool = False, scale: Optional[float
     return attention(q, k, v, causal=causal, scale=scale, kv_len=kv_len)
 
 
+class _RopeAttentionPacked(torch.autograd.Function):
+    """Llama's attention from ONE packed projection y [B, S, (Hq + 2 Hkv) * D] (q | k | v column
+    blocks): RoPE on q and k (csrc/act.hip k_rope, strided reads), causal GQA flash attention with v
+    read in place.  The backward writes dq, dk and dv straight into one packed gradient of y's
+    layout and rotates its q / k blocks back in place -- the fused projection's backward then
+    runs one GEMM each way, with no per-slice zero-fill / copy / add that autograd would run for
+    three views of y."""
+
+    @staticmethod
+    def forward(ctx, y, cos, sin, hq, hkv, causal, scale):
+        B, S, W = y.shape
+        D = W // (hq + 2 * hkv)
+        y2 = y.view(B * S, W)
+        q = torch.empty(B, S, hq, D, dtype=y.dtype, device=y.device)
+        k = torch.empty(B, S, hkv, D, dtype=y.dtype, device=y.device)
+        C = native()
+        C.rope_apply(y2[:, :hq * D], q.view(B * S, hq * D), cos, sin, S, D, 1.0)
+        C.rope_apply(y2[:, hq * D:(hq + hkv) * D], k.view(B * S, hkv * D), cos, sin, S, D, 1.0)
+        v = y[:, :, (hq + hkv) * D:].view(B, S, hkv, D)
+        o, lse = C.attn_forward(q, k, v, causal, scale, None)
+        ctx.save_for_backward(q, k, y, o, lse, cos, sin)
+        ctx.meta = (hq, hkv, D, causal, scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, y, o, lse, cos, sin = ctx.saved_tensors
+        hq, hkv, D, causal, scale = ctx.meta
+        B, S, W = y.shape
+        do = do.to(torch.bfloat16)
+        if not _attn_rows_ok(do):
+            do = do.contiguous()
+        g = torch.empty(B, S, W, dtype=torch.bfloat16, device=y.device)
+        v = y[:, :, (hq + hkv) * D:].view(B, S, hkv, D)
+        gq = g[:, :, :hq * D].view(B, S, hq, D)
+        gk = g[:, :, hq * D:(hq + hkv) * D].view(B, S, hkv, D)
+        gv = g[:, :, (hq + hkv) * D:].view(B, S, hkv, D)
+        C = native()
+        C.attn_backward(do, q, k, v, o, lse, causal, scale, None, gq, gk, gv)
+        g2 = g.view(B * S, W)
+        for a, b in ((0, hq * D), (hq * D, (hq + hkv) * D)):  # rotate back in place (the backward of RoPE)
+            C.rope_apply(g2[:, a:b], g2[:, a:b], cos, sin, S, D, -1.0)
+        return g, None, None, None, None, None, None
+
+
+def rope_attention_packed_ok(y: torch.Tensor, cos: torch.Tensor, hq: int, hkv: int) -> bool:
+    W = y.shape[-1]
+    if y.dim() != 3 or W % (hq + 2 * hkv):
+        return False
+    D = W // (hq + 2 * hkv)
+    return (_FUSED_ATTN and _FUSED_ACT and D in (64, 128) and y.is_cuda and y.dtype == torch.bfloat16
+            and y.is_contiguous() and y.data_ptr() % 16 == 0 and cos.dtype == torch.float32 and cos.is_cuda
+            and cos.dim() == 2 and cos.shape[0] >= y.shape[1] and cos.shape[1] * 2 == D and hq % hkv == 0)
+
+
+def rope_attention_packed(y: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, hq: int, hkv: int,
+                          causal: bool = True, scale: Optional[float] = None) -> torch.Tensor:
+    """Rotary embedding + (causal, grouped-query) attention of a packed q | k | v projection
+    y [B, S, (hq + 2 hkv) * D]; returns [B, S, hq, D].  Callers check rope_attention_packed_ok."""
+    D = y.shape[-1] // (hq + 2 * hkv)
+    sc = float(scale) if scale is not None else 1.0 / (D ** 0.5)
+    return _RopeAttentionPacked.apply(y, cos, sin, int(hq), int(hkv), bool(causal), sc)
+
+
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = False,
               scale: Optional[float] = None, kv_len: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Scaled dot-product attention on the [batch, seq, heads, head_dim] layout (the projection
@@ -1176,6 +1240,41 @@ class _SwiGLU(torch.autograd.Function):
         da, db = torch.empty_like(a), torch.empty_like(b)
         native().swiglu_backward(g, a, b, da, db)
         return da, db
+
+
+class _SwiGLUPacked(torch.autograd.Function):
+    """silu(y[:, :F]) * y[:, F:] of ONE packed gate / up projection y [.., 2F] (csrc/act.hip
+    k_swiglu_*_rows): the backward writes the packed [.., 2F] gradient directly."""
+
+    @staticmethod
+    def forward(ctx, y):
+        F2 = y.shape[-1]
+        y2 = y.reshape(-1, F2)
+        c = torch.empty(y2.shape[0], F2 // 2, dtype=y.dtype, device=y.device)
+        native().swiglu_rows_forward(y2, c)
+        ctx.save_for_backward(y)
+        return c.view(*y.shape[:-1], F2 // 2)
+
+    @staticmethod
+    def backward(ctx, g):
+        (y,) = ctx.saved_tensors
+        F2 = y.shape[-1]
+        g2 = g.to(torch.bfloat16).reshape(-1, F2 // 2)
+        if g2.stride(-1) != 1 or g2.stride(0) % 8 or g2.data_ptr() % 16:
+            g2 = g2.contiguous()
+        dy = torch.empty_like(y)
+        native().swiglu_rows_backward(g2, y.reshape(-1, F2), dy.view(-1, F2))
+        return dy
+
+
+def swiglu_packed(y: torch.Tensor) -> torch.Tensor:
+    """F.silu(a) * b for a, b = the two halves of y's last dimension (a fused gate / up GEMM)."""
+    F2 = y.shape[-1]
+    if (_FUSED_ACT and y.is_cuda and y.dtype == torch.bfloat16 and y.is_contiguous() and F2 % 16 == 0
+            and y.data_ptr() % 16 == 0):
+        return _SwiGLUPacked.apply(y)
+    a, b = y.split(F2 // 2, dim=-1)
+    return F.silu(a) * b
 
 
 def swiglu(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:

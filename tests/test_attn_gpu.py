@@ -137,7 +137,7 @@ def test_flash_attention_in_models(monkeypatch):
     from hipps.models import transformer as tf
 
     calls = []
-    for cls in (hnn._FlashAttention, hnn._FlashAttentionQKV):  # Llama: separate q / k / v; BERT: packed
+    for cls in (hnn._FlashAttention, hnn._FlashAttentionQKV, hnn._RopeAttentionPacked):  # BERT / Llama packed
         def counted(ctx, *a, _fwd=cls.forward):
             calls.append(1)
             return _fwd(ctx, *a)
@@ -187,3 +187,56 @@ def test_packed_qkv_attention_matches_separate(padded):
     o2.backward(g)
     assert torch.equal(o1, o2)
     assert torch.equal(x1.grad, x2.grad)
+
+
+@pytest.mark.parametrize("D,hq,hkv", [(64, 8, 2), (128, 4, 1)])
+def test_rope_attention_packed_matches_separate_path(D, hq, hkv):
+    """Llama's packed q | k | v projection: RoPE + causal GQA attention with the gradient written
+    packed and rotated back in place equals rope() + attention() on the three slices, bit for bit."""
+    from hipps.ops import nn as hnn
+    from hipps.models.transformer import _rope
+
+    torch.manual_seed(D + hq)
+    B, S = 2, 256
+    W = (hq + 2 * hkv) * D
+    base = (torch.randn(B, S, W, device="cuda") * 0.5).to(torch.bfloat16)
+    inv = 1.0 / (5e5 ** (torch.arange(0, D, 2, device="cuda", dtype=torch.float32) / D))
+    f = torch.outer(torch.arange(S, device="cuda", dtype=torch.float32), inv)
+    cos, sin = f.cos().contiguous(), f.sin().contiguous()
+    g = torch.randn(B, S, hq, D, device="cuda").to(torch.bfloat16)
+    y1 = base.clone().requires_grad_(True)
+    assert hnn.rope_attention_packed_ok(y1, cos, hq, hkv)
+    o1 = hnn.rope_attention_packed(y1, cos, sin, hq, hkv)
+    o1.backward(g)
+    y2 = base.clone().requires_grad_(True)
+    q, k, v = y2.split([hq * D, hkv * D, hkv * D], dim=-1)
+    q, k = q.reshape(B, S, hq, D).contiguous(), k.reshape(B, S, hkv, D).contiguous()
+    assert hnn.rope_ok(q, cos) and hnn.rope_ok(k, cos)  # (the same RoPE kernel on both paths)
+    q, k = _rope(q, cos, sin), _rope(k, cos, sin)
+    o2 = hnn.attention(q, k, v.reshape(B, S, hkv, D), causal=True)
+    o2.backward(g)
+    assert torch.equal(o1, o2)
+    assert torch.equal(y1.grad, y2.grad)
+
+
+def test_swiglu_packed_matches_fp32_and_unpacked():
+    from hipps.ops import nn as hnn
+    import torch.nn.functional as F
+
+    torch.manual_seed(2)
+    y = (torch.randn(3, 77, 2 * 384, device="cuda") * 2).to(torch.bfloat16)
+    g = torch.randn(3, 77, 384, device="cuda").to(torch.bfloat16)
+    yp = y.clone().requires_grad_(True)
+    c = hnn.swiglu_packed(yp)
+    c.backward(g)
+    a, b = y.float().split(384, dim=-1)
+    a.requires_grad_(True)
+    b.requires_grad_(True)
+    ref = F.silu(a) * b
+    ref.backward(g.float())
+    torch.testing.assert_close(c.float(), ref, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(yp.grad.float(), torch.cat([a.grad, b.grad], -1), rtol=2e-2, atol=2e-2)
+    a2, b2 = (t.contiguous().requires_grad_(True) for t in y.split(384, dim=-1))
+    c2 = hnn.swiglu(a2, b2)
+    c2.backward(g)
+    assert torch.equal(c, c2) and torch.equal(yp.grad, torch.cat([a2.grad, b2.grad], -1))
