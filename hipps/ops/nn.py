@@ -889,6 +889,11 @@ def _linear_fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] 
     in the same pass)."""
     M, K = x2.shape
     N = w.shape[0]
+    if res is not None and res.dtype == torch.float32:
+        # an fp32 residual stream (Llama: x + wo(a), x + w2(.)): one hipBLASLt GEMM with the fp32
+        # residual as C and an fp32 output (aten addmm.dtype) instead of a bf16 GEMM output plus a
+        # mixed-dtype add pass over the residual stream
+        return torch.ops.aten.addmm.dtype(res, x2, w.t(), torch.float32)
     y = torch.empty((M, N), dtype=torch.bfloat16, device=x2.device)
 
     def blas():
@@ -976,8 +981,9 @@ def shadow_linear_ok(x: torch.Tensor, weight: torch.Tensor, bias=None, residual=
     return (_SHADOW_LINEAR and x.is_cuda and torch.is_autocast_enabled() and
             torch.get_autocast_dtype("cuda") == torch.bfloat16 and has_weight_shadow(weight) and
             (bias is None or has_weight_shadow(bias)) and
-            (residual is None or (residual.dtype == torch.bfloat16 and residual.shape[-1] == weight.shape[0]
-                                  and residual.numel() == x.numel() // x.shape[-1] * weight.shape[0])))
+            (residual is None or (residual.dtype in (torch.bfloat16, torch.float32) and residual.shape[-1] == weight.shape[0]
+                                  and residual.numel() == x.numel() // x.shape[-1] * weight.shape[0]
+                                  and (residual.dtype == torch.bfloat16 or (bias is None and residual.is_contiguous())))))
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias=None, residual=None) -> torch.Tensor:

@@ -255,3 +255,34 @@ def test_shadow_linear_residual_gradients():
         torch.testing.assert_close(y.double(), ref, rtol=3e-2, atol=3e-2)
     finally:
         hnn.unregister_weight_shadow(shadow)
+
+
+def test_shadow_linear_fp32_residual():
+    """An fp32 residual stream (Llama: x + wo(a)) is added by the GEMM itself (hipBLASLt C, fp32
+    output): y is fp32 and equals residual + x w^T; the residual's gradient is dy (fp32), and the
+    input / weight gradients match autocast's F.linear."""
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(12)
+    flat, shadow, (w,) = _shadowed((128, 64))
+    try:
+        x = torch.randn(2, 48, 64, device=DEV).to(torch.bfloat16).requires_grad_(True)
+        r = torch.randn(2, 48, 128, device=DEV, requires_grad=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            assert hnn.shadow_linear_ok(x, w, None, r)
+            y = hnn.linear(x, w, residual=r)
+        assert y.dtype == torch.float32
+        ref = F.linear(x.detach().double(), w.detach().to(torch.bfloat16).double()) + r.detach().double()
+        torch.testing.assert_close(y.double(), ref, rtol=1e-3, atol=5e-3)
+        g = torch.randn_like(y)
+        y.backward(g)
+        assert r.grad.dtype == torch.float32 and torch.equal(r.grad, g)
+        x0 = x.detach().clone().requires_grad_(True)
+        w0 = torch.nn.Parameter(w.detach().clone())
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y0 = F.linear(x0, w0)
+        y0.backward(g.to(torch.bfloat16))
+        torch.testing.assert_close(x.grad.float(), x0.grad.float(), rtol=2e-2, atol=2e-2)
+        torch.testing.assert_close(w.grad, w0.grad, rtol=2e-2, atol=2e-2)
+    finally:
+        hnn.unregister_weight_shadow(shadow)

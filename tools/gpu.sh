@@ -86,7 +86,7 @@ for step in "$@"; do
         -- python3 "$ROOT/bench.py" --steps 12 --warmup 5 $BENCH_ARGS) > "$OUT/bench_prof.log" 2>&1 \
         || fail prof "$OUT/bench_prof.log"
       T=$(find /tmp/hprof -name "bench_kernel_trace.csv" | head -1)
-      python3 tools/steady_profile.py "$T" "$OUT/steady.txt" --skip 5 --title "ResNet-50 bs256 ps_async bf16 N=1 $BENCH_ARGS"
+      python3 tools/steady_profile.py "$T" "$OUT/steady.txt" --skip 5 --title "ResNet-50 bs256 ps_async bf16 N=1 $BENCH_ARGS" ${PROF_DETAIL:+--detail "$PROF_DETAIL"}
       head -12 "$OUT/steady.txt" ;;
     reh_r50:*) reh "r50_n$arg" "$arg" $((29610 + arg)) --batch 64 --steps 10 --warmup 3 ;;
     reh_bert:*) reh "bert_n$arg" "$arg" $((29620 + arg)) --model bert-base --batch 4 --seq 512 --bucket-mb 4 \

@@ -16,6 +16,8 @@ def main():
     ap.add_argument("--marker", default="k_pull_select")
     ap.add_argument("--skip", type=int, default=5)
     ap.add_argument("--title", default="")
+    ap.add_argument("--detail", default=None,
+                    help="regex: list every call of the matching kernels in the last steady step (grid, us)")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -97,6 +99,20 @@ def main():
     lines.append("")
     for k, (d, c) in sorted(agg.items(), key=lambda x: -x[1][0])[:60]:
         lines.append(f"{d / n / 1e3:9.1f} us/step calls/step={c / n:6.1f}  {k[:140]}")
+    if a.detail:
+        import re
+
+        pat = re.compile(a.detail)
+        last = [r for r in rows if marks[-2] <= int(r["Start_Timestamp"]) < marks[-1]]
+        gkey = next((k for k in ("Grid_Size_X", "Grid_Size", "grid_size_x") if rows and k in rows[0]), None)
+        lines.append("")
+        lines.append(f"calls of /{a.detail}/ in the last steady step (start us, grid, us):")
+        for r in last:
+            if pat.search(r["Kernel_Name"]):
+                st = (int(r["Start_Timestamp"]) - marks[-2]) / 1e3
+                du = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+                lines.append(f"  {st:9.1f} {('s' + str(r[sid])) if sid else ''} grid={r.get(gkey, '?') if gkey else '?':>9} "
+                             f"{du:8.1f}  {r['Kernel_Name'][:90]}")
     open(a.out, "w").write("\n".join(lines) + "\n")
     print("\n".join(lines[:24]))
 
