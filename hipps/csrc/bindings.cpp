@@ -111,8 +111,10 @@ void swiglu_forward(at::Tensor a, at::Tensor b, at::Tensor c);
 void ln_forward(at::Tensor x, at::Tensor w, at::Tensor b, at::Tensor y, at::Tensor mean, at::Tensor rstd, double eps);
 void ln_backward(at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor rstd, at::Tensor w, at::Tensor dx,
                  at::Tensor dw, at::Tensor db);
-void rms_forward(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor rstd, double eps);
-void rms_backward(at::Tensor dy, at::Tensor x, at::Tensor rstd, at::Tensor w, at::Tensor dx, at::Tensor dw);
+void rms_forward(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor rstd, double eps, c10::optional<at::Tensor> add,
+                 c10::optional<at::Tensor> xsum);
+void rms_backward(at::Tensor dy, at::Tensor x, at::Tensor rstd, at::Tensor w, at::Tensor dx, at::Tensor dw,
+                  c10::optional<at::Tensor> dres, c10::optional<at::Tensor> dx16);
 void swiglu_backward(at::Tensor g, at::Tensor a, at::Tensor b, at::Tensor da, at::Tensor db);
 void rope_apply(at::Tensor x, at::Tensor y, at::Tensor cs, at::Tensor sn, int64_t S, int64_t hd, double sign);
 void swiglu_rows_forward(at::Tensor y, at::Tensor c);
@@ -264,8 +266,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("shift") = pybind11::none());
   m.def("bn_finalize_partials", &hipps::bn_finalize_partials,
         "BN train-mode finalize from producer partial sums (mean/invstd/scale/shift + running stats)");
-  m.def("rms_forward", &hipps::rms_forward, "RMSNorm forward: fp32 / bf16 rows -> bf16, fp32 rstd (ln.hip)");
-  m.def("rms_backward", &hipps::rms_backward, "RMSNorm backward: dx in x's dtype, fp32 weight gradient (ln.hip)");
+  m.def("rms_forward", &hipps::rms_forward,
+        "RMSNorm forward: fp32 / bf16 rows -> bf16, fp32 rstd; optional fused residual add (ln.hip)", py::arg("x"),
+        py::arg("w"), py::arg("y"), py::arg("rstd"), py::arg("eps"), py::arg("add") = py::none(),
+        py::arg("xsum") = py::none());
+  m.def("rms_backward", &hipps::rms_backward,
+        "RMSNorm backward: dx in x's dtype, fp32 weight gradient; optional residual gradient in, bf16 twin out "
+        "(ln.hip)",
+        py::arg("dy"), py::arg("x"), py::arg("rstd"), py::arg("w"), py::arg("dx"), py::arg("dw"),
+        py::arg("dres") = py::none(), py::arg("dx16") = py::none());
   m.def("ln_forward", &hipps::ln_forward, "LayerNorm forward, bf16 rows, fp32 weight / bias / mean / rstd (ln.hip)");
   m.def("ln_backward", &hipps::ln_backward, "LayerNorm backward: bf16 dx, fp32 weight / bias gradients (ln.hip)");
   m.def("swiglu_forward", &hipps::swiglu_forward, "c = silu(a) * b, bf16 (act.hip)");

@@ -247,7 +247,9 @@ __device__ __forceinline__ void load_w8(const float* w, float* f) { Ld8<float>::
 template <int NC, typename TX>
 __global__ __launch_bounds__(64 * kLnWaves) void k_rms_fwd(const TX* __restrict__ x, const float* __restrict__ w,
                                                            uint16_t* __restrict__ y, float* __restrict__ rstd_out,
-                                                           int64_t R, int D, float eps) {
+                                                           int64_t R, int D, float eps,
+                                                           const uint16_t* __restrict__ addy,
+                                                           float* __restrict__ xsum) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * kLnWaves + (threadIdx.x >> 6);
   if (row >= R) return;
@@ -259,6 +261,13 @@ __global__ __launch_bounds__(64 * kLnWaves) void k_rms_fwd(const TX* __restrict_
     const int ch = lane + 64 * c;
     if (ch < nch) {
       Ld8<TX>::load(x + row * D + ch * 8, v[c]);
+      if (addy) {  // fused residual add: x + addy (bf16) is normalised and written out (fp32)
+        float a[8];
+        unpack8(*reinterpret_cast<const u32x4*>(addy + row * D + ch * 8), a);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] += a[j];
+        Ld8<float>::store(xsum + row * D + ch * 8, v[c]);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) q += v[c][j] * v[c][j];
     }
@@ -284,7 +293,8 @@ template <int NC, typename TX>
 __global__ __launch_bounds__(64 * kLnWaves) void k_rms_bwd(const uint16_t* __restrict__ dy, const TX* __restrict__ x,
                                                            const float* __restrict__ rstd, const float* __restrict__ w,
                                                            TX* __restrict__ dx, float* __restrict__ part, int64_t R,
-                                                           int D, int rpb) {
+                                                           int D, int rpb, const float* __restrict__ dres,
+                                                           uint16_t* __restrict__ dx16) {
   extern __shared__ float red[];  // [kLnWaves][D]
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nch = D >> 3;
@@ -326,7 +336,14 @@ __global__ __launch_bounds__(64 * kLnWaves) void k_rms_bwd(const uint16_t* __res
           o[j] = rs * (gy[j] * ww[c][j] - xh * m2);
           dg[c][j] += gy[j] * xh;
         }
+        if (dres) {  // the residual stream's own gradient joins here (fused residual add backward)
+          float g[8];
+          Ld8<float>::load(dres + row * D + ch * 8, g);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += g[j];
+        }
         Ld8<TX>::store(dx + row * D + ch * 8, o);
+        if (dx16) Ld8<uint16_t>::store(dx16 + row * D + ch * 8, o);  // bf16 twin for the bf16 branch
       }
     }
   }
@@ -422,7 +439,9 @@ void ln_backward(at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor rstd, 
 }
 
 // x: fp32 or bf16 [rows, D] (D % 8 == 0, D <= 4096); y bf16; rstd fp32 [rows]
-void rms_forward(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor rstd, double eps) {
+// add (optional): bf16 [rows, D] added to x (fp32) first; the sum is written to xsum (fp32)
+void rms_forward(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor rstd, double eps, c10::optional<at::Tensor> add,
+                 c10::optional<at::Tensor> xsum) {
   const int64_t D = x.size(-1);
   TORCH_CHECK(x.is_cuda() && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16) && x.is_contiguous() &&
                   reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
@@ -432,6 +451,17 @@ void rms_forward(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor rstd, doub
   ln_param_check(w, D, "weight");
   const int64_t R = x.numel() / D;
   TORCH_CHECK(y.numel() == x.numel() && rstd.numel() == R && rstd.scalar_type() == at::kFloat, "rms_norm: sizes");
+  const uint16_t* addp = nullptr;
+  float* xsp = nullptr;
+  if (add.has_value()) {
+    TORCH_CHECK(x.scalar_type() == at::kFloat && xsum.has_value(), "rms_norm(add): fp32 x and an xsum output");
+    ln_check(*add, D, 4096);
+    TORCH_CHECK(add->numel() == x.numel() && xsum->numel() == x.numel() && xsum->scalar_type() == at::kFloat &&
+                    xsum->is_contiguous() && reinterpret_cast<uintptr_t>(xsum->data_ptr()) % 16 == 0,
+                "rms_norm(add): add / xsum sizes");
+    addp = (const uint16_t*)add->data_ptr();
+    xsp = xsum->data_ptr<float>();
+  }
   if (R == 0) return;
   const int grid = (int)((R + kLnWaves - 1) / kLnWaves);
   auto st = c10::hip::getCurrentHIPStream();
@@ -441,10 +471,11 @@ void rms_forward(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor rstd, doub
   do {                                                                                                                 \
     if (f32)                                                                                                           \
       hipLaunchKernelGGL((k_rms_fwd<NCc, float>), grid, 64 * kLnWaves, 0, st, x.data_ptr<float>(), w.data_ptr<float>(), \
-                         (uint16_t*)y.data_ptr(), rstd.data_ptr<float>(), R, (int)D, (float)eps);                      \
+                         (uint16_t*)y.data_ptr(), rstd.data_ptr<float>(), R, (int)D, (float)eps, addp, xsp);        \
     else                                                                                                               \
       hipLaunchKernelGGL((k_rms_fwd<NCc, uint16_t>), grid, 64 * kLnWaves, 0, st, (const uint16_t*)x.data_ptr(),        \
-                         w.data_ptr<float>(), (uint16_t*)y.data_ptr(), rstd.data_ptr<float>(), R, (int)D, (float)eps); \
+                         w.data_ptr<float>(), (uint16_t*)y.data_ptr(), rstd.data_ptr<float>(), R, (int)D, (float)eps,   \
+                         nullptr, nullptr);                                                                            \
   } while (0)
   if (nc <= 1) HIPPS_RMSF(1);
   else if (nc <= 2) HIPPS_RMSF(2);
@@ -454,7 +485,9 @@ void rms_forward(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor rstd, doub
 }
 
 // dy bf16; x / dx fp32 or bf16 (same dtype); dw fp32 [D]
-void rms_backward(at::Tensor dy, at::Tensor x, at::Tensor rstd, at::Tensor w, at::Tensor dx, at::Tensor dw) {
+// dres (optional, fp32 x only): added to dx; dx16 (optional): a bf16 copy of the final dx
+void rms_backward(at::Tensor dy, at::Tensor x, at::Tensor rstd, at::Tensor w, at::Tensor dx, at::Tensor dw,
+                  c10::optional<at::Tensor> dres, c10::optional<at::Tensor> dx16) {
   const int64_t D = x.size(-1);
   TORCH_CHECK(x.is_cuda() && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16) && x.is_contiguous() &&
                   dx.scalar_type() == x.scalar_type() && dx.is_contiguous() && dx.numel() == x.numel() &&
@@ -466,6 +499,20 @@ void rms_backward(at::Tensor dy, at::Tensor x, at::Tensor rstd, at::Tensor w, at
   ln_param_check(dw, D, "weight gradient");
   const int64_t R = x.numel() / D;
   TORCH_CHECK(dy.numel() == x.numel() && rstd.numel() == R, "rms_norm backward: sizes");
+  const float* dresp = nullptr;
+  uint16_t* dx16p = nullptr;
+  if (dres.has_value()) {
+    TORCH_CHECK(x.scalar_type() == at::kFloat && dres->scalar_type() == at::kFloat && dres->is_contiguous() &&
+                    dres->numel() == x.numel() && reinterpret_cast<uintptr_t>(dres->data_ptr()) % 16 == 0,
+                "rms_norm backward: dres must be fp32 contiguous, aligned, x's size (fp32 x)");
+    dresp = dres->data_ptr<float>();
+  }
+  if (dx16.has_value()) {
+    TORCH_CHECK(x.scalar_type() == at::kFloat, "rms_norm backward: dx16 needs fp32 x");
+    ln_check(*dx16, D, 4096);
+    TORCH_CHECK(dx16->numel() == x.numel(), "rms_norm backward: dx16 size");
+    dx16p = (uint16_t*)dx16->data_ptr();
+  }
   if (R == 0) {
     dw.zero_();
     return;
@@ -483,11 +530,11 @@ void rms_backward(at::Tensor dy, at::Tensor x, at::Tensor rstd, at::Tensor w, at
     if (f32)                                                                                                          \
       hipLaunchKernelGGL((k_rms_bwd<NCc, float>), (int)P, 64 * kLnWaves, lds, st, (const uint16_t*)dy.data_ptr(),     \
                          x.data_ptr<float>(), rstd.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(),      \
-                         part.data_ptr<float>(), R, (int)D, rpb);                                                     \
+                         part.data_ptr<float>(), R, (int)D, rpb, dresp, dx16p);                                       \
     else                                                                                                              \
       hipLaunchKernelGGL((k_rms_bwd<NCc, uint16_t>), (int)P, 64 * kLnWaves, lds, st, (const uint16_t*)dy.data_ptr(),  \
                          (const uint16_t*)x.data_ptr(), rstd.data_ptr<float>(), w.data_ptr<float>(),                  \
-                         (uint16_t*)dx.data_ptr(), part.data_ptr<float>(), R, (int)D, rpb);                            \
+                         (uint16_t*)dx.data_ptr(), part.data_ptr<float>(), R, (int)D, rpb, nullptr, nullptr);          \
   } while (0)
   if (nc <= 1) HIPPS_RMSB(1);
   else if (nc <= 2) HIPPS_RMSB(2);

@@ -154,7 +154,14 @@ class RMSNorm(nn.Module):
         self.weight = nn.Parameter(torch.ones(d))
         self.eps = eps
 
-    def forward(self, x):
+    def forward(self, x, add=None):
+        """RMSNorm(x); with ``add``, returns (x + add, RMSNorm(x + add)) -- the residual add of the
+        block before folded into this norm (one fused pass each way on the device)."""
+        if add is not None:
+            if x.is_cuda and torch.is_autocast_enabled() and hnn.add_rms_norm_ok(x, add, self.weight):
+                return hnn.add_rms_norm(x, add, self.weight, self.eps)
+            x = x + add
+            return x, self(x)
         if x.is_cuda and torch.is_autocast_enabled() and hnn.rms_norm_ok(x, self.weight):
             # csrc/ln.hip: reads the fp32 residual stream directly, writes bf16 (no cast kernels)
             return hnn.rms_norm(x, self.weight, self.eps)
@@ -194,11 +201,17 @@ class LlamaBlock(nn.Module):
         self.attn_norm = RMSNorm(c.dim, c.eps)
         self.ffn_norm = RMSNorm(c.dim, c.eps)
 
-    def forward(self, x, cos, sin):
+    def forward(self, x, cos, sin, y=None):
+        """Returns (x', y') with the block's output = x' + y': the residual add of each branch is
+        deferred into the norm that reads it next (RMSNorm(x, add=...)), so ``y`` is the previous
+        block's pending branch output (None for the first block)."""
         B, S, D = x.shape
         c = self.c
         hd = D // c.heads
-        h = self.attn_norm(x)
+        if y is None:
+            h = self.attn_norm(x)
+        else:
+            x, h = self.attn_norm(x, add=y)
         y = self.wqkv(h)  # [B, S, (heads + 2 kv_heads) * hd]
         if hnn.rope_attention_packed_ok(y, cos, c.heads, c.kv_heads):
             # RoPE + causal GQA flash attention on the packed projection (csrc/act.hip, attn.hip)
@@ -208,9 +221,8 @@ class LlamaBlock(nn.Module):
             q = _rope(q.reshape(B, S, c.heads, hd).contiguous(), cos, sin)
             k = _rope(k.reshape(B, S, c.kv_heads, hd).contiguous(), cos, sin)
             a = hnn.attention(q, k, v.reshape(B, S, c.kv_heads, hd), causal=True)
-        x = x + self.wo(a.reshape(B, S, D))
-        h = self.ffn_norm(x)
-        return x + self.w2(hnn.swiglu_packed(self.w13(h)))
+        x, h = self.ffn_norm(x, add=self.wo(a.reshape(B, S, D)))
+        return x, self.w2(hnn.swiglu_packed(self.w13(h)))
 
 
 class Llama(nn.Module):
@@ -241,9 +253,10 @@ class Llama(nn.Module):
         B, S = ids.shape
         x = self.tok(ids)
         cos, sin = self.rope_tables(S, ids.device)
+        y = None
         for b in self.blocks:
-            x = b(x, cos, sin)
-        logits = self.head(self.norm(x))
+            x, y = b(x, cos, sin, y)
+        logits = self.head(self.norm(x) if y is None else self.norm(x, add=y)[1])
         if labels is None:
             return logits
         return hnn.cross_entropy(logits, labels)

@@ -1367,6 +1367,53 @@ def rms_norm(x: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:
     return _RMSNorm.apply(x, weight, eps)
 
 
+def _aligned(t: torch.Tensor) -> torch.Tensor:
+    t = t.contiguous()
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
+class _AddRMSNorm(torch.autograd.Function):
+    """Residual add + RMSNorm in one pass (csrc/ln.hip k_rms_fwd with ``addy``): s = x + y (x the
+    fp32 residual stream, y a block's bf16 output) is written once and normalised from registers
+    -- no separate add kernel that writes s and a norm that reads it back.  The backward folds the
+    residual stream's own gradient into the norm's dx (k_rms_bwd with ``dres``) and emits its bf16
+    twin for y: one pass instead of norm backward + autograd's fp32 add + a bf16 cast."""
+
+    @staticmethod
+    def forward(ctx, x, y, w, eps):
+        D = x.shape[-1]
+        s = torch.empty_like(x)
+        h = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+        rstd = torch.empty(x.numel() // D, dtype=torch.float32, device=x.device)
+        native().rms_forward(x, w, h, rstd, float(eps), y, s)
+        ctx.save_for_backward(s, w, rstd)
+        ctx.set_materialize_grads(False)
+        return s, h
+
+    @staticmethod
+    def backward(ctx, ds, dh):
+        s, w, rstd = ctx.saved_tensors
+        dh = torch.zeros(s.shape, dtype=torch.bfloat16, device=s.device) if dh is None else \
+            _aligned(dh.to(torch.bfloat16))
+        dres = None if ds is None else _aligned(ds.to(torch.float32))
+        dx = torch.empty_like(s)
+        dy = torch.empty(s.shape, dtype=torch.bfloat16, device=s.device) if ctx.needs_input_grad[1] else None
+        dw = torch.empty_like(w)
+        native().rms_backward(dh, s, rstd, w, dx, dw, dres, dy)
+        return dx, dy, dw, None
+
+
+def add_rms_norm_ok(x: torch.Tensor, y: torch.Tensor, weight) -> bool:
+    """Can _AddRMSNorm run: fp32 residual x and bf16 y of x's shape, both contiguous and aligned?"""
+    return (rms_norm_ok(x, weight) and x.dtype == torch.float32 and y.dtype == torch.bfloat16
+            and y.shape == x.shape and y.is_contiguous() and y.data_ptr() % 16 == 0 and y.device == x.device)
+
+
+def add_rms_norm(x: torch.Tensor, y: torch.Tensor, weight: torch.Tensor, eps: float):
+    """(x + y, bf16 RMSNorm(x + y)) in one fused pass each way (callers check add_rms_norm_ok)."""
+    return _AddRMSNorm.apply(x, y, weight, eps)
+
+
 class _Rope(torch.autograd.Function):
     """Rotary embedding of interleaved pairs on x [B, S, H, hd] bf16 (csrc/act.hip k_rope, fp32
     cos / sin tables [S, hd/2]); the backward is the rotation by -theta."""

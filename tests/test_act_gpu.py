@@ -164,3 +164,38 @@ def test_rms_norm_matches_fp32(R, D, dtype):
     w.grad = None
     hnn.rms_norm(x, w, 1e-5).backward(g)
     assert torch.equal(dw1, w.grad)
+
+
+@pytest.mark.parametrize("R,D,with_dres", [(8192, 2048, True), (2048, 4096, True), (33, 64, False), (7, 1000 // 8 * 8, True)])
+def test_add_rms_norm_matches_fp32(R, D, with_dres):
+    """csrc/ln.hip fused residual add + RMSNorm: s = x + y (fp32 x, bf16 y), bf16 norm(s); the
+    backward returns the fp32 residual gradient (incoming ds + norm backward, one pass) for x and
+    its bf16 twin for y, against the fp32 formula."""
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(R + D + 1)
+    x = (torch.randn(R, D, device=DEV) * 3).requires_grad_(True)
+    y = torch.randn(R, D, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    w = torch.nn.Parameter(torch.randn(D, device=DEV) * 0.2 + 1)
+    assert hnn.add_rms_norm_ok(x, y, w)
+    s, h = hnn.add_rms_norm(x, y, w, 1e-5)
+    assert s.dtype == torch.float32 and h.dtype == torch.bfloat16
+    xf, yf = x.detach().clone().requires_grad_(True), y.detach().float().requires_grad_(True)
+    wf = w.detach().clone().requires_grad_(True)
+    sf = xf + yf
+    ref = sf * torch.rsqrt(sf.pow(2).mean(-1, keepdim=True) + 1e-5) * wf
+    torch.testing.assert_close(s, sf, rtol=0, atol=0)
+    torch.testing.assert_close(h.float(), ref, rtol=2e-2, atol=2e-2)
+    g = torch.randn(R, D, device=DEV).to(torch.bfloat16)
+    gs = torch.randn(R, D, device=DEV) if with_dres else None
+    if with_dres:
+        torch.autograd.backward((s, h), (gs, g))
+        torch.autograd.backward((sf, ref), (gs, g.float()))
+    else:
+        h.backward(g)
+        ref.backward(g.float())
+    assert x.grad.dtype == torch.float32 and y.grad.dtype == torch.bfloat16
+    torch.testing.assert_close(x.grad, xf.grad, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(y.grad.float(), xf.grad.to(torch.bfloat16).float(), rtol=1e-2, atol=1e-2)
+    assert torch.equal(y.grad, x.grad.to(torch.bfloat16))
+    torch.testing.assert_close(w.grad, wf.grad, rtol=2e-2, atol=2e-3 * R ** 0.5 + 1e-3)
