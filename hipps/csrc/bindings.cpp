@@ -87,7 +87,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
                 c10::optional<at::Tensor> bn_invstd, c10::optional<at::Tensor> bn_scale,
                 c10::optional<at::Tensor> bn_shift, int64_t stages, bool add_s2,
                 c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift,
-                c10::optional<at::Tensor> bias);
+                c10::optional<at::Tensor> bias, c10::optional<at::Tensor> gelu_pre, int64_t gelu);
 void gemm2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
                  int64_t Hi, int64_t Wi, int64_t cfg, int64_t stages,
                  c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift, int64_t sdiv);
@@ -225,7 +225,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bn_bits") = py::none(), py::arg("bn_mean") = py::none(), py::arg("bn_invstd") = py::none(),
         py::arg("bn_scale") = py::none(), py::arg("bn_shift") = py::none(), py::arg("stages") = 2,
         py::arg("add_s2") = false, py::arg("pro_scale") = py::none(), py::arg("pro_shift") = py::none(),
-        py::arg("bias") = py::none());
+        py::arg("bias") = py::none(), py::arg("gelu_pre") = py::none(), py::arg("gelu") = 0);
   m.def("gemm2_dgrad_s2", &hipps::gemm2_dgrad_s2,
         "stride-2 3x3 input gradient as four output-parity implicit GEMMs (+ BN-backward reduction)",
         py::arg("dy"), py::arg("wf"), py::arg("dx"), py::arg("bm") = 128, py::arg("bn") = 128,

@@ -64,8 +64,39 @@ __device__ __attribute__((aligned(64))) const uint8_t kOnes8[64] = {
 // kBias (1x1 only; alone or with a plain kAdd): y = x w^T + bias[col] (+ R), the fp32 bias added
 // to the fp32 accumulator before the bf16 rounding (a Linear layer's addmm; + R: the residual
 // added by the same pass)
+// kGelu (1x1, with kBias or alone): the Linear + GELU of a transformer MLP -- Y2 = bf16(acc + bias)
+// (the pre-activation the backward needs) and Y = bf16(gelu(Y2)), exact erf form, as F.gelu on
+// the bf16 pre-activation rounds it: one pass instead of the GEMM, a GELU read and its write
+// kGeluB (1x1): the next Linear's input gradient with the GELU backward in its epilogue: Y =
+// bf16(gelu'(x) * bf16(acc)), x the saved bf16 pre-activation (read like kBst's BN input)
 enum Epi : int { kPlain = 0, kStats = 1, kAdd = 2, kBst = 4, kBstBits = 8, kAddS2 = 16, kPar = 32, kPro = 64,
-                 kBias = 128 };
+                 kBias = 128, kGelu = 256, kGeluB = 512 };
+
+// Branch-free erf for the epilogues: erf(z) = 1 - poly(t) e^{-z^2}, t = 1 / (1 + p |z|)
+// (Abramowitz & Stegun 7.1.26, |error| < 1.5e-7 -- far below the bf16 rounding of the result);
+// ocml's erff branches on |z| and the divergent lanes of a 64-wide wave ran both of its paths (the
+// GELU epilogue cost 48 us on BERT's 16384 x 3072 pre-activation with it).  e^{-z^2} is returned
+// too: GELU's backward reuses it as its density term.
+__device__ __forceinline__ float erf_fast(float z, float& ez2) {
+  const float az = fabsf(z);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, az, 1.f));
+  ez2 = __expf(-az * az);
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = fmaf(-p * t, ez2, 1.f);
+  return copysignf(e, z);
+}
+__device__ __forceinline__ float gelu_f(float x) {
+  float ez2;
+  return x * 0.5f * (1.f + erf_fast(x * 0.70710678118654752f, ez2));
+}
+__device__ __forceinline__ float gelu_bwd_f(float dy, float x) {
+  float ez2;  // = e^{-x^2 / 2}
+  const float cdf = 0.5f * (1.f + erf_fast(x * 0.70710678118654752f, ez2));
+  return dy * fmaf(x, 0.3989422804014327f * ez2, cdf);
+}
 
 template <int BM, int BN> struct Cfg;
 template <> struct Cfg<256, 256> { static constexpr int TM = 128, TN = 64; };
@@ -102,6 +133,7 @@ struct Args {
   int tdr[4], tdc[4], tko[4];
   const float *psc, *psh;  // kPro: per-channel scale / shift of the A operand's BN
   const float* bias;       // kBias: f32 [N]
+  uint16_t* Y2;            // kGelu: the bf16 pre-activation [M, N]
   int epf;                 // EPF allowed (HIPPS_G2_EPF, default 1)
 };
 
@@ -311,6 +343,8 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   constexpr bool ADDE = (EPI & kAdd) != 0;
   constexpr bool S2 = (EPI & kAddS2) != 0;
   constexpr int BSTE = (EPI & kBstBits) ? 2 : (EPI & kBst) ? 1 : 0;
+  constexpr bool GELUB = (EPI & kGeluB) != 0;
+  constexpr bool XS = BSTE || GELUB;  // the bx operand stream (BN input, or GELU pre-activation)
   // element offset in R of output row m's chunk (col), or -1 for a row that gets no addend (S2)
   auto r_off = [&](int m, int col) -> int64_t {
     if constexpr (S2) {
@@ -326,7 +360,7 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   };
   constexpr int RCH = BN / 8;             // 16-byte chunks per output row
   constexpr int NOUT = BM * RCH / NT;     // output chunks per thread
-  constexpr int NSTR = (ADDE ? 1 : 0) + (BSTE ? 1 : 0);       // epilogue operand streams
+  constexpr int NSTR = (ADDE ? 1 : 0) + (XS ? 1 : 0);       // epilogue operand streams
   // EPF: a 1x1 GEMM with a short K (<= 2 tiles: the memory-bound dgrad passes with a residual
   // add and a BN-backward reduction, K = 64..128) whose prefetched operands fit (PF) issues them
   // right after the first tile's DMA, so their HBM latency overlaps the DMA and the MFMAs
@@ -335,10 +369,10 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   constexpr bool EPF_OK = !TAPS && !S2 && !PP && !KH && !M32 && !PRO && NSX == 2;
   constexpr bool PF = NSTR > 0 && NOUT * 5 * NSTR <= 40;  // <= 40 registers
   // vector-memory instructions of one prefetch (16-byte operand + mask byte per stream and chunk)
-  constexpr int NPFL = PF ? NOUT * ((ADDE ? 2 : 0) + (BSTE == 2 ? 2 : BSTE ? 1 : 0)) : 0;
+  constexpr int NPFL = PF ? NOUT * ((ADDE ? 2 : 0) + (BSTE == 2 ? 2 : XS ? 1 : 0)) : 0;
   static_assert(NPFL < 64, "vmcnt immediate");
-  u32x4 pr[PF && ADDE ? NOUT : 1], px[PF && BSTE ? NOUT : 1];
-  uint32_t prm[PF && ADDE ? NOUT : 1], pxm[PF && BSTE ? NOUT : 1];
+  u32x4 pr[PF && ADDE ? NOUT : 1], px[PF && XS ? NOUT : 1];
+  uint32_t prm[PF && ADDE ? NOUT : 1], pxm[PF && XS ? NOUT : 1];
   const uint8_t* rm_src = g.RM;  // (no mask: a byte of ones, so every prefetch issues the same loads)
   if constexpr (ADDE) {
     if (rm_src == nullptr) rm_src = kOnes8;
@@ -357,7 +391,7 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
             pr[i] = ro >= 0 ? *reinterpret_cast<const u32x4*>(g.R + ro) : u32x4{0u, 0u, 0u, 0u};
             prm[i] = rm_src[rm_src == kOnes8 ? 0 : (o >> 3)];
           }
-          if constexpr (BSTE) {
+          if constexpr (XS) {
             px[i] = *reinterpret_cast<const u32x4*>(g.bx + o);
             pxm[i] = BSTE == 2 ? g.bbits[o >> 3] : 0u;
           }
@@ -725,7 +759,7 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
           }
           lrm[b] = g.RM != nullptr ? g.RM[o >> 3] : 0xffu;
         }
-        if constexpr (BSTE) {
+        if constexpr (XS) {
           lx[b] = *reinterpret_cast<const u32x4*>(g.bx + o);
           lxm[b] = BSTE == 2 ? g.bbits[o >> 3] : 0u;
         }
@@ -759,6 +793,26 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
         v.y = add_bf16x2(v.y, r.y);
         v.z = add_bf16x2(v.z, r.z);
         v.w = add_bf16x2(v.w, r.w);
+      }
+      if constexpr ((EPI & kGelu) != 0) {  // v = pre-activation: kept for the backward, GELU stored
+        *reinterpret_cast<uint4*>(g.Y2 + o) = v;
+        uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          vw[j] = pack_bf16x2(gelu_f(__uint_as_float(vw[j] << 16)), gelu_f(__uint_as_float(vw[j] & 0xffff0000u)));
+        v = uint4{vw[0], vw[1], vw[2], vw[3]};
+      }
+      if constexpr (GELUB) {  // v = bf16 input gradient of the GELU output -> of its input
+        u32x4 xu;
+        if constexpr (PF) xu = px[i];
+        else xu = lx[b];
+        const uint32_t xw[4] = {xu.x, xu.y, xu.z, xu.w};
+        uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          vw[j] = pack_bf16x2(gelu_bwd_f(__uint_as_float(vw[j] << 16), __uint_as_float(xw[j] << 16)),
+                              gelu_bwd_f(__uint_as_float(vw[j] & 0xffff0000u), __uint_as_float(xw[j] & 0xffff0000u)));
+        v = uint4{vw[0], vw[1], vw[2], vw[3]};
       }
       *reinterpret_cast<uint4*>(g.Y + o) = v;
       if (BST) {  // dz = dy * relu'(.) on the stored bf16 dy; x-hat from the BN input
@@ -1239,6 +1293,9 @@ int64_t gemm2_mtiles(int64_t M, int64_t N, int64_t K, int64_t bm) {
 //     [img, ceil(Ho/2), ceil(Wo/2), Cout] input gradient of a stride-2 1x1 conv over the same
 //     tensor, added on the even (h, w) rows only (ResNet downsample branch)
 //   bm / bn: block tile (0 = default per shape); stages: LDS stages (2, or 3 below 256x256)
+//   gelu_pre + gelu (1x1, no other epilogue): gelu=1 -> y = gelu(x w^T + bias), gelu_pre = the
+//     bf16 pre-activation; gelu=2 -> y = gelu'(gelu_pre) * (x w^T), the GELU backward folded
+//     into an input-gradient GEMM (x = the output gradient, w = the next layer's weight^T)
 void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part,
                 c10::optional<at::Tensor> add, c10::optional<at::Tensor> add_mask, int64_t Hi, int64_t Wi,
                 int64_t stride, int64_t KH, int64_t KW, int64_t pad, int64_t bm, int64_t bn,
@@ -1246,7 +1303,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
                 c10::optional<at::Tensor> bn_invstd, c10::optional<at::Tensor> bn_scale,
                 c10::optional<at::Tensor> bn_shift, int64_t stages, bool add_s2,
                 c10::optional<at::Tensor> pro_scale, c10::optional<at::Tensor> pro_shift,
-                c10::optional<at::Tensor> bias) {
+                c10::optional<at::Tensor> bias, c10::optional<at::Tensor> gelu_pre, int64_t gelu) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "gemm2: device tensors");
   TORCH_CHECK(stages >= 2 && stages <= 6,
               "gemm2: stages must be 2, 3, 4 (k-half units), 5 (ping-pong) or 6 (32x32x16 MFMA)");
@@ -1343,8 +1400,25 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
     a.psh = pro_shift->data_ptr<float>();
     epi |= g2::kPro;
   }
+  if (gelu_pre.has_value() && gelu_pre->defined()) {
+    TORCH_CHECK(epi == g2::kPlain && !taps && (gelu == 1 || gelu == 2),
+                "gemm2: the GELU epilogues run on a plain 1x1 GEMM (gelu=1 forward, 2 backward)");
+    TORCH_CHECK(gelu_pre->is_cuda() && gelu_pre->scalar_type() == at::kBFloat16 && gelu_pre->numel() == M * N &&
+                    gelu_pre->is_contiguous() && reinterpret_cast<uintptr_t>(gelu_pre->data_ptr()) % 16 == 0,
+                "gemm2: gelu_pre must be a 16-byte aligned contiguous bf16 tensor shaped like y");
+    if (gelu == 1) {
+      a.Y2 = (uint16_t*)gelu_pre->data_ptr();
+      epi |= g2::kGelu;
+    } else {
+      TORCH_CHECK(!(bias.has_value() && bias->defined()), "gemm2: the GELU backward epilogue takes no bias");
+      a.bx = (const uint16_t*)gelu_pre->data_ptr();
+      epi |= g2::kGeluB;
+    }
+  } else {
+    TORCH_CHECK(gelu == 0, "gemm2: gelu needs gelu_pre");
+  }
   if (bias.has_value() && bias->defined()) {
-    TORCH_CHECK((epi == g2::kPlain || epi == g2::kAdd) && !taps,
+    TORCH_CHECK((epi == g2::kPlain || epi == g2::kAdd || epi == g2::kGelu) && !taps,
                 "gemm2: the bias epilogue runs on a 1x1 GEMM, alone or with a plain add (a residual)");
     TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() == N,
                 "gemm2: bias must be f32 [Cout]");
@@ -1385,6 +1459,9 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
         case g2::kAdd: HIPPS_G2(BMc, BNc, g2::kAdd, false); break;                                  \
         case g2::kBias: HIPPS_G2(BMc, BNc, g2::kBias, false); break;                                \
         case g2::kBias | g2::kAdd: HIPPS_G2(BMc, BNc, (g2::kBias | g2::kAdd), false); break;        \
+        case g2::kGelu: HIPPS_G2(BMc, BNc, g2::kGelu, false); break;                                \
+        case g2::kBias | g2::kGelu: HIPPS_G2(BMc, BNc, (g2::kBias | g2::kGelu), false); break;      \
+        case g2::kGeluB: HIPPS_G2(BMc, BNc, g2::kGeluB, false); break;                              \
         case g2::kBst: HIPPS_G2(BMc, BNc, g2::kBst, false); break;                                  \
         case g2::kBst | g2::kAdd: HIPPS_G2(BMc, BNc, (g2::kBst | g2::kAdd), false); break;          \
         case g2::kBstBits: HIPPS_G2(BMc, BNc, g2::kBstBits, false); break;                          \

@@ -72,12 +72,16 @@ class BertLayer(nn.Module):
         self.inter = hnn.Linear(c.hidden, c.ffn)
         self.out = hnn.Linear(c.ffn, c.hidden)
         self.out_ln = nn.LayerNorm(c.hidden, eps=c.eps)
+        # bf16 W^T copies (refreshed with the shadow) for the input-gradient GEMMs that carry an
+        # epilogue: qkv's and inter's add the residual's gradient, out's the GELU backward
+        hnn.mark_transposed_reader(self.qkv.weight, self.inter.weight, self.out.weight)
 
     def forward(self, x, mask=None):
         B, S, D = x.shape
         h = self.heads
 
-        qkv = self.qkv(x).view(B, S, 3, h, D // h)
+        link = hnn.ResidualLink()  # x's gradient from attn_out's residual joins qkv's input-gradient GEMM
+        qkv = self.qkv(x, link=link).view(B, S, 3, h, D // h)
         if mask is None or (torch.is_tensor(mask) and mask.dtype == torch.int32 and mask.dim() == 1):
             # the packed [B, S, 3, H, hd] projection straight into the hipps flash-attention
             # kernels (csrc/attn.hip); ``mask`` may be the int32 [B] key lengths of a padded batch
@@ -87,8 +91,9 @@ class BertLayer(nn.Module):
             a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask).transpose(1, 2)
         a = a.reshape(B, S, D)
         # residual adds ride in the output projections (GEMM epilogue / hipBLASLt C)
-        x = _ln(self.attn_ln, self.attn_out(a, residual=x))
-        return _ln(self.out_ln, self.out(F.gelu(self.inter(x)), residual=x))
+        x = _ln(self.attn_ln, self.attn_out(a, residual=x, link=link))
+        # intermediate -> GELU -> output (+ x) as one node: GELU in the GEMM epilogues both ways
+        return _ln(self.out_ln, hnn.gelu_mlp(x, self.inter, self.out, residual_x=True))
 
 
 class Bert(nn.Module):

@@ -78,6 +78,10 @@ _FUSED_XENT = _os.environ.get("HIPPS_FUSED_XENT", "1") != "0"
 _LINEAR_RESIDUAL = _os.environ.get("HIPPS_LINEAR_RESIDUAL", "1") != "0"
 # SwiGLU gate and rotary embedding of the Llama block as one HIP pass each (csrc/act.hip)
 _FUSED_ACT = _os.environ.get("HIPPS_FUSED_ACT", "1") != "0"
+# the fused GELU MLP node (_GeluMLP: GELU in the GEMM epilogues) and the residual-gradient links
+# (ResidualLink); HIPPS_GELU_MLP=0 / HIPPS_RES_LINK=0 restore the module compositions for A/B runs
+_GELU_MLP = _os.environ.get("HIPPS_GELU_MLP", "1") != "0"
+_RES_LINK = _os.environ.get("HIPPS_RES_LINK", "1") != "0"
 # ResNet bn2 -> conv3: the BN apply + ReLU in conv3's operand prologue per layer, where measured
 # faster than the apply pass + plain GEMMs (bn_pro_pays); 0: always the apply pass
 _BN_PRO_TUNE = _os.environ.get("HIPPS_BN_PRO_TUNE", "1") != "0"
@@ -787,6 +791,23 @@ def register_transposed_weight(p: torch.Tensor, view: torch.Tensor):
     _TSHADOWS[p.data_ptr()] = view
 
 
+def mark_transposed_reader(*params) -> None:
+    """Ask the optimizer's flat store for a bf16 W^T copy of these Linear weights, refreshed with the
+    shadow (one transpose-cast kernel per step for all of them): the gemm2 input-gradient GEMMs
+    with an epilogue (GELU backward, a residual gradient) read it as their B operand."""
+    if not (_GELU_MLP or _RES_LINK):
+        return
+    for p in params:
+        if p is not None and p.dim() == 2:
+            p.reads_bf16_shadow_t = True
+
+
+def transposed_weight(w: torch.Tensor):
+    """The registered bf16 W^T of fp32 weight ``w`` (mark_transposed_reader), or None."""
+    t = _TSHADOWS.get(w.data_ptr())
+    return t if t is not None and w.dim() == 2 and tuple(t.shape) == (w.shape[1], w.shape[0]) else None
+
+
 def unregister_transposed_weight(p: torch.Tensor):
     _TSHADOWS.pop(p.data_ptr(), None)
 
@@ -845,7 +866,7 @@ class _ShadowLinear(torch.autograd.Function):
     BERT-base spent ~3 ms of a 38.8 ms step in those casts (profiles/r4/r4n/)."""
 
     @staticmethod
-    def forward(ctx, x, w_master, bias, residual=None):
+    def forward(ctx, x, w_master, bias, residual=None, link=None):
         dt = torch.bfloat16
         w = bf16_weight(w_master)
         x2 = x.reshape(-1, x.shape[-1])
@@ -857,6 +878,16 @@ class _ShadowLinear(torch.autograd.Function):
         ctx.has_bias = bias is not None
         ctx.xshape, ctx.xdtype = x.shape, x.dtype
         ctx.rshape = None if residual is None else residual.shape
+        # ResidualLink: the consumer side (this Linear reads x, a later one adds x as its residual)
+        # arms the link; the residual side hands its gradient over instead of returning it
+        ctx.link_in = ctx.link_out = None
+        if link is not None and _RES_LINK:
+            if residual is None and x.dtype == dt and x.dim() >= 2:
+                link.armed, link.x = True, x
+                ctx.link_in = link
+            elif residual is not None and link.armed and link.x is residual:
+                ctx.link_out = link
+                link.armed, link.x = False, None
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -867,7 +898,12 @@ class _ShadowLinear(torch.autograd.Function):
             dy2 = dy2.to(torch.bfloat16)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dy2, bf16_weight(w_master, idle=False)).view(ctx.xshape)
+            g = ctx.link_in.take() if ctx.link_in is not None else None
+            if g is not None:
+                # the residual's gradient (handed over by the Linear that added x) joins in the GEMM
+                dx = _dgrad(dy2, w_master, g.reshape(dy2.shape[0], -1)).view(ctx.xshape)
+            else:
+                dx = torch.mm(dy2, bf16_weight(w_master, idle=False)).view(ctx.xshape)
             if dx.dtype != ctx.xdtype:
                 dx = dx.to(ctx.xdtype)
         if ctx.needs_input_grad[1]:
@@ -877,7 +913,31 @@ class _ShadowLinear(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = colsum_f32(dy2)
         dres = dy.reshape(ctx.rshape) if ctx.rshape is not None and ctx.needs_input_grad[3] else None
-        return dx, dw, db, dres
+        if dres is not None and ctx.link_out is not None:
+            ctx.link_out.give(dres if dres.dtype == torch.bfloat16 else dres.to(torch.bfloat16))
+            dres = None
+        return dx, dw, db, dres, None
+
+
+class ResidualLink:
+    """Pairs the Linear that reads x with the later Linear that adds x back as its residual
+    (BERT: qkv(x) ... attn_out(a, residual=x)), so x's two gradients meet in ONE GEMM: the
+    residual side's backward (which runs first) hands dy over, and the reader's input gradient is
+    addmm(dy, d_out, W) instead of mm + an autograd add.  The reader's forward arms the link (its
+    _ShadowLinear path only, for the same tensor); a residual side that finds it unarmed returns its
+    gradient normally.  One link per use, created in the forward."""
+
+    __slots__ = ("armed", "x", "g")
+
+    def __init__(self):
+        self.armed, self.x, self.g = False, None, None
+
+    def give(self, g):
+        self.g = g if self.g is None else self.g + g
+
+    def take(self):
+        g, self.g = self.g, None
+        return g
 
 
 def _linear_fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
@@ -958,6 +1018,161 @@ def _linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     return dw
 
 
+def _g2_ok(*ts) -> bool:
+    return all(t.is_contiguous() and t.data_ptr() % 16 == 0 for t in ts)
+
+
+def _gelu_linear_fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor]):
+    """(gelu(x2 w^T + bias), x2 w^T + bias), both bf16 [M, N]: per shape the faster of hipBLASLt
+    addmm + PyTorch's GELU and the gemm2 kGelu epilogue (gemm2.hip: the pre-activation and the
+    GELU written by the GEMM's own epilogue -- no GELU pass re-reading the pre-activation)."""
+    M, K = x2.shape
+    N = w.shape[0]
+    pre = torch.empty((M, N), dtype=torch.bfloat16, device=x2.device)
+    post = torch.empty_like(pre)
+
+    def blas():
+        if bias is None:
+            torch.mm(x2, w.t(), out=pre)
+        else:
+            torch.addmm(bf16_weight(bias), x2, w.t(), out=pre)
+        torch._C._nn.gelu(pre, out=post)
+
+    if not (_GEMM2 and N % 64 == 0 and K % 64 == 0 and M >= 1024 and _g2_ok(x2, w)
+            and (bias is None or (bias.dtype == torch.float32 and bias.is_contiguous() and bias.numel() == N))):
+        blas()
+        return post, pre
+    C = native()
+    b = None if bias is None else bias.detach()
+    cands = {"blas": blas}
+    for name in _g2_names(N):
+        bm, bn, ns = _g2_parse(name)
+        cands[name] = (lambda bm=bm, bn=bn, ns=ns:
+                       C.gemm2_conv(x2, w, post, None, None, None, 1, 1, 1, 1, 1, 0, bm, bn, stages=ns, bias=b,
+                                    gelu_pre=pre, gelu=1))
+    cands[TUNER.pick(("gelu_fwd", M, N, K, bias is not None), cands)]()
+    return post, pre
+
+
+def _gelu_dgrad(dy2: torch.Tensor, w: torch.Tensor, pre: torch.Tensor, wt=None) -> torch.Tensor:
+    """d pre = gelu'(pre) * (dy2 w) (bf16 [M, K] from dy2 [M, N], w [N, K]: the input gradient of
+    the Linear after a GELU, through the GELU): per shape the faster of hipBLASLt mm + PyTorch's
+    GELU backward and the gemm2 kGeluB epilogue over ``wt`` = w^T [K, N] (the flat store's
+    transposed shadow, mark_transposed_reader; without one, no gemm2 candidate)."""
+    M, N = dy2.shape
+    K = w.shape[1]
+
+    def blas():
+        return torch.ops.aten.gelu_backward(torch.mm(dy2, w), pre)
+
+    if not (_GEMM2 and wt is not None and N % 64 == 0 and K % 64 == 0 and M >= 1024 and _g2_ok(dy2, wt, pre)):
+        return blas()
+    C = native()
+    out = torch.empty((M, K), dtype=torch.bfloat16, device=dy2.device)
+
+    def g2(bm, bn, ns):
+        C.gemm2_conv(dy2, wt, out, None, None, None, 1, 1, 1, 1, 1, 0, bm, bn, stages=ns, gelu_pre=pre, gelu=2)
+        return out
+
+    cands = {"blas": blas}
+    for name in _g2_names(K):
+        bm, bn, ns = _g2_parse(name)
+        cands[name] = (lambda bm=bm, bn=bn, ns=ns: g2(bm, bn, ns))
+    return cands[TUNER.pick(("gelu_dgrad", M, N, K), cands)]()
+
+
+def _dgrad(dy2: torch.Tensor, w_master: torch.Tensor, add: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dx = dy2 W (+ add) in bf16 ([M, K] from dy2 [M, N] and the weight's [N, K] shadow; ``add``
+    bf16 [M, K], a residual's gradient): hipBLASLt (mm, or addmm with ``add`` as C -- which
+    PyTorch first copies into the output), or with a registered W^T (mark_transposed_reader) the
+    gemm2 tiles with ``add`` in the kAdd epilogue, the faster per shape."""
+    w = bf16_weight(w_master, idle=False)
+    M, N = dy2.shape
+    K = w.shape[1]
+
+    def blas():
+        return torch.mm(dy2, w) if add is None else torch.addmm(add, dy2, w)
+
+    wt = transposed_weight(w_master)
+    if not (_GEMM2 and wt is not None and add is not None and N % 64 == 0 and K % 64 == 0 and M >= 1024
+            and add.dtype == torch.bfloat16 and tuple(add.shape) == (M, K) and _g2_ok(dy2, wt, add)):
+        return blas()
+    C = native()
+    out = torch.empty((M, K), dtype=torch.bfloat16, device=dy2.device)
+
+    def g2(bm, bn, ns):
+        C.gemm2_conv(dy2, wt, out, None, add, None, 1, 1, 1, 1, 1, 0, bm, bn, stages=ns)
+        return out
+
+    cands = {"blas": blas}
+    for name in _g2_names(K):
+        bm, bn, ns = _g2_parse(name)
+        cands[name] = (lambda bm=bm, bn=bn, ns=ns: g2(bm, bn, ns))
+    return cands[TUNER.pick(("dgrad_add", M, N, K), cands)]()
+
+
+class _GeluMLP(torch.autograd.Function):
+    """y = gelu(x W1^T + b1) W2^T + b2 (+ x): a transformer MLP (BERT's intermediate / output
+    Linear pair, exact-erf GELU, optionally with its own input as the residual) as ONE autograd
+    node on the bf16 weight shadows (see _ShadowLinear):
+
+    * forward: the first GEMM writes the pre-activation AND the GELU in its epilogue
+      (_gelu_linear_fwd), the second adds b2 and the residual in its own (_linear_fwd);
+    * backward: the second Linear's input gradient carries the GELU backward in its epilogue
+      (_gelu_dgrad), and with the residual the first Linear's input gradient is one hipBLASLt
+      addmm with dy as C -- the residual's gradient joins there instead of in an autograd add.
+
+    Same math as hnn.Linear -> F.gelu -> hnn.Linear(residual=x) (which hipps.models used before)."""
+
+    @staticmethod
+    def forward(ctx, x, w1m, b1, w2m, b2, res_x):
+        dt = torch.bfloat16
+        x2 = x.reshape(-1, x.shape[-1])
+        if x2.dtype != dt:
+            x2 = x2.to(dt)
+        post, pre = _gelu_linear_fwd(x2, bf16_weight(w1m), b1)
+        w2 = bf16_weight(w2m)
+        y = _linear_fwd(post, w2, b2, x2 if res_x else None)
+        ctx.save_for_backward(x2, pre, post, w1m, w2m)
+        ctx.has_b1, ctx.has_b2, ctx.res_x = b1 is not None, b2 is not None, bool(res_x)
+        ctx.xshape, ctx.xdtype = x.shape, x.dtype
+        return y.view(*x.shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, pre, post, w1m, w2m = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if dy2.dtype != torch.bfloat16:
+            dy2 = dy2.to(torch.bfloat16)
+        dy2 = dy2.contiguous()
+        dpre = _gelu_dgrad(dy2, bf16_weight(w2m, idle=False), pre, transposed_weight(w2m))
+        dx = dw1 = db1 = dw2 = db2 = None
+        if ctx.needs_input_grad[0]:
+            dx = _dgrad(dpre, w1m, dy2 if ctx.res_x else None).view(ctx.xshape)
+            if dx.dtype != ctx.xdtype:
+                dx = dx.to(ctx.xdtype)
+        if ctx.needs_input_grad[3]:
+            dw2 = _linear_wgrad(dy2, post)
+        if ctx.has_b2 and ctx.needs_input_grad[4]:
+            db2 = colsum_f32(dy2)
+        if ctx.needs_input_grad[1]:
+            dw1 = _linear_wgrad(dpre, x2)
+        if ctx.has_b1 and ctx.needs_input_grad[2]:
+            db1 = colsum_f32(dpre)
+        return dx, dw1, db1, dw2, db2, None
+
+
+def gelu_mlp(x: torch.Tensor, l1: nn.Linear, l2: nn.Linear, residual_x: bool = False) -> torch.Tensor:
+    """l2(gelu(l1(x))) (+ x with ``residual_x``): one _GeluMLP node under bf16 autocast when weight
+    shadows cover both Linears (the fused GEMM epilogues), the module composition otherwise."""
+    if (_GELU_MLP and _SHADOW_LINEAR and shadow_linear_ok(x, l1.weight, l1.bias) and shadow_linear_ok(x, l2.weight, l2.bias)
+            and x.shape[-1] == l1.weight.shape[1] and l2.weight.shape[1] == l1.weight.shape[0]
+            and (not residual_x or (l2.weight.shape[0] == x.shape[-1] and x.dtype == torch.bfloat16))):
+        return _GeluMLP.apply(x, l1.weight, l1.bias, l2.weight, l2.bias, residual_x)
+    h = F.gelu(l1(x))
+    return l2(h, residual=x) if residual_x and isinstance(l2, Linear) else (l2(h) + x if residual_x else l2(h))
+
+
 def colsum_f32(t: torch.Tensor) -> torch.Tensor:
     """t.sum(0) in fp32 for a 2-d bf16 device tensor (csrc/xent.hip k_colsum: deterministic,
     ~4x PyTorch's reduce on a bias gradient); torch.sum otherwise."""
@@ -986,13 +1201,14 @@ def shadow_linear_ok(x: torch.Tensor, weight: torch.Tensor, bias=None, residual=
                                   and (residual.dtype == torch.bfloat16 or (bias is None and residual.is_contiguous())))))
 
 
-def linear(x: torch.Tensor, weight: torch.Tensor, bias=None, residual=None) -> torch.Tensor:
+def linear(x: torch.Tensor, weight: torch.Tensor, bias=None, residual=None, link=None) -> torch.Tensor:
     """F.linear (+ residual), on the bf16 weight shadow when one covers ``weight`` (see
-    _ShadowLinear; a bf16 residual is added in the GEMM's epilogue or as hipBLASLt's C)."""
+    _ShadowLinear; a bf16 residual is added in the GEMM's epilogue or as hipBLASLt's C).
+    ``link``: a ResidualLink shared with the Linear that reads (or adds) the same x."""
     if residual is not None and not _LINEAR_RESIDUAL:
         return residual + linear(x, weight, bias)
     if shadow_linear_ok(x, weight, bias, residual):
-        return _ShadowLinear.apply(x, weight, bias, residual)
+        return _ShadowLinear.apply(x, weight, bias, residual, link)
     y = F.linear(x, weight, bias)
     return y if residual is None else residual + y
 
@@ -1006,8 +1222,8 @@ class Linear(nn.Linear):
         super().__init__(*args, **kwargs)
         mark_shadow_reader(self.weight, self.bias)
 
-    def forward(self, x, residual=None):
-        return linear(x, self.weight, self.bias, residual)
+    def forward(self, x, residual=None, link=None):
+        return linear(x, self.weight, self.bias, residual, link)
 
 
 class _CrossEntropy(torch.autograd.Function):

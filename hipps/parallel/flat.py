@@ -198,8 +198,9 @@ class FlatStore:
     def _build_transposed_shadow(self):
         """Backward-operand bf16 copies refreshed with the shadow by one multi-matrix transpose
         kernel (flat.hip k_transpose_cast): [Cin, Cout] for every 1x1-conv weight (the input-
-        gradient GEMM's B operand) and rot180(W)^T as a channels-last [Cin, Cout, KH, KW] weight for
-        every square KxK conv (stride-1 input gradient as a forward convolution, ops.nn._ConvKxK)."""
+        gradient GEMM's B operand), rot180(W)^T as a channels-last [Cin, Cout, KH, KW] weight for
+        every square KxK conv (stride-1 input gradient as a forward convolution, ops.nn._ConvKxK)
+        and W^T [in, out] for each Linear weight marked by ops.nn.mark_transposed_reader."""
         from ..ops import _native
         from ..ops import nn as hnn
 
@@ -214,12 +215,17 @@ class FlatStore:
                     (p.shape[2] == 1 or p.is_contiguous(memory_format=torch.channels_last)):
                 mats.append((s, off))
                 off += s.numel
+            elif p.dim() == 2 and getattr(p, "reads_bf16_shadow_t", False) and p.is_contiguous():
+                # a Linear weight [out, in] whose input-gradient GEMM runs on gemm2 (ops.nn
+                # mark_transposed_reader): [in, out]
+                mats.append((s, off))
+                off += s.numel
         if not mats:
             return
         self.tshadow = torch.empty(off, dtype=torch.bfloat16, device=self.device)
         rows = []
         for s, toff in mats:
-            R, C, KH, KW = s.param.shape
+            R, C, KH, KW = s.param.shape if s.param.dim() == 4 else (*s.param.shape, 1, 1)
             T = KH * KW
             for kh in range(KH):
                 for kw in range(KW):

@@ -286,3 +286,107 @@ def test_shadow_linear_fp32_residual():
         torch.testing.assert_close(w.grad, w0.grad, rtol=2e-2, atol=2e-2)
     finally:
         hnn.unregister_weight_shadow(shadow)
+
+
+@pytest.mark.parametrize("name", ["g2_256x256", "g2_256x256s5", "g2_256x256s6", "g2_256x128", "g2_256x128s3",
+                                  "g2_128x128", "g2_128x128s3", "g2_256x64", "g2_128x64", "g2_128x64s3"])
+def test_gemm2_gelu_epilogues_every_tile(name):
+    """gemm2.hip kGelu (y = gelu(x w^T + b), pre kept) and kGeluB (gelu'(pre) * (dy w)) on every
+    tile against the fp32 formula over the same bf16 operands (M not a tile multiple)."""
+    from hipps.ops import _native
+    from hipps.ops import nn as hnn
+
+    C = _native.native()
+    bm, bn, ns = hnn._g2_parse(name)
+    torch.manual_seed(bm + bn + ns)
+    M, K, N = 1000, 256, 512
+    x = (torch.randn(M, K, device=DEV) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.1).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV) * 0.5
+    pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    post = torch.empty_like(pre)
+    C.gemm2_conv(x, w, post, None, None, None, 1, 1, 1, 1, 1, 0, bm, bn, stages=ns, bias=b, gelu_pre=pre, gelu=1)
+    ref_pre = x.float() @ w.float().t() + b
+    torch.testing.assert_close(pre.float(), ref_pre, rtol=1e-2, atol=1e-2)
+    # the GELU of the stored bf16 pre-activation, as F.gelu on it rounds it
+    torch.testing.assert_close(post.float(), F.gelu(pre.float()).to(torch.bfloat16).float(), rtol=0, atol=1e-2)
+    # backward: dy [M, K2] through w2 [K2, N] (the next Linear, transposed for the kernel)
+    K2 = 256
+    dy = torch.randn(M, K2, device=DEV).to(torch.bfloat16)
+    w2 = (torch.randn(K2, N, device=DEV) * 0.1).to(torch.bfloat16)
+    dpre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    C.gemm2_conv(dy, w2.t().contiguous(), dpre, None, None, None, 1, 1, 1, 1, 1, 0, bm, bn, stages=ns,
+                 gelu_pre=pre, gelu=2)
+    dpost = (dy.float() @ w2.float())
+    prf = pre.float()
+    ref = dpost * (0.5 * (1 + torch.erf(prf * 0.7071067811865476)) + prf * torch.exp(-0.5 * prf * prf) * 0.3989422804014327)
+    torch.testing.assert_close(dpre.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+def test_gelu_mlp_matches_fp32_and_composition():
+    """hnn.gelu_mlp (one _GeluMLP node: kGelu / kGeluB epilogues, the residual gradient folded
+    into the input-gradient addmm) against the fp32 formula over the bf16 shadows, forward and
+    every gradient; the tuner runs (M >= 1024)."""
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(3)
+    D, F4 = 256, 1024
+    flat, shadow, (w1, b1, w2, b2) = _shadowed((F4, D), (F4,), (D, F4), (D,))
+    try:
+        l1 = hnn.Linear(D, F4).to(DEV)
+        l2 = hnn.Linear(F4, D).to(DEV)
+        l1.weight, l1.bias, l2.weight, l2.bias = w1, b1, w2, b2
+        # the W^T copies the flat store keeps for marked Linears (gemm2 input-gradient epilogues)
+        for w in (w1, w2):
+            hnn.register_transposed_weight(w, w.detach().t().contiguous().to(torch.bfloat16))
+        x = (torch.randn(4, 512, D, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = hnn.gelu_mlp(x, l1, l2, residual_x=True)
+        assert y.grad_fn is not None and "GeluMLP" in type(y.grad_fn).__name__
+        g = torch.randn_like(y)
+        y.backward(g)
+        xs = x.detach().double().requires_grad_(True)
+        sw = [t.detach().to(torch.bfloat16).double().requires_grad_(True) for t in (w1, b1, w2, b2)]
+        ref = F.linear(F.gelu(F.linear(xs, sw[0], sw[1])), sw[2], sw[3]) + xs
+        ref.backward(g.double())
+        torch.testing.assert_close(y.double(), ref, rtol=3e-2, atol=3e-2)
+        torch.testing.assert_close(x.grad.double(), xs.grad, rtol=3e-2, atol=3e-2)
+        for p, r in zip((w1, b1, w2, b2), sw):
+            assert p.grad.dtype == torch.float32
+            tol = 2e-2 * r.grad.abs().max().item() + 1e-3
+            torch.testing.assert_close(p.grad.double(), r.grad, rtol=3e-2, atol=tol)
+    finally:
+        hnn.unregister_weight_shadow(shadow)
+        for w in (w1, w2):
+            hnn.unregister_transposed_weight(w)
+
+
+def test_residual_link_folds_the_residual_gradient():
+    """ResidualLink: qkv(x, link) ... out(a, residual=x, link) gives x the same gradient as the
+    unlinked pair (the residual's gradient added inside qkv's input-gradient addmm), and an
+    unarmed link (reader off the shadow path) leaves the residual's gradient to autograd."""
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(5)
+    D = 128
+    flat, shadow, (w1, w2) = _shadowed((D, D), (D, D))
+    hnn.register_transposed_weight(w1, w1.detach().t().contiguous().to(torch.bfloat16))
+    try:
+        x0 = torch.randn(8, 256, D, device=DEV).to(torch.bfloat16)
+        g = torch.randn(8, 256, D, device=DEV).to(torch.bfloat16)
+
+        def run(use_link, arm=True):
+            x = x0.clone().requires_grad_(True)
+            link = hnn.ResidualLink() if use_link else None
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                h = hnn.linear(x, w1, None, link=link if arm else None)
+                y = hnn.linear(torch.tanh(h), w2, None, residual=x, link=link)
+            y.backward(g)
+            return x.grad.float()
+
+        ref = run(False)
+        torch.testing.assert_close(run(True), ref, rtol=2e-2, atol=2e-2)
+        torch.testing.assert_close(run(True, arm=False), ref, rtol=0, atol=0)
+    finally:
+        hnn.unregister_weight_shadow(shadow)
+        hnn.unregister_transposed_weight(w1)
