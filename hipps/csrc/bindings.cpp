@@ -111,6 +111,10 @@ void swiglu_forward(at::Tensor a, at::Tensor b, at::Tensor c);
 void ln_forward(at::Tensor x, at::Tensor w, at::Tensor b, at::Tensor y, at::Tensor mean, at::Tensor rstd, double eps);
 void ln_backward(at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor rstd, at::Tensor w, at::Tensor dx,
                  at::Tensor dw, at::Tensor db);
+void embed_forward(at::Tensor ids, c10::optional<at::Tensor> tt, at::Tensor word, at::Tensor pos, at::Tensor typ,
+                   at::Tensor out);
+void embed_pos_backward(at::Tensor dout, at::Tensor dpos, int64_t B, int64_t S);
+void embed_seg_backward(at::Tensor dout, at::Tensor sid, at::Tensor perm, at::Tensor dtab);
 void rms_forward(at::Tensor x, at::Tensor w, at::Tensor y, at::Tensor rstd, double eps, c10::optional<at::Tensor> add,
                  c10::optional<at::Tensor> xsum);
 void rms_backward(at::Tensor dy, at::Tensor x, at::Tensor rstd, at::Tensor w, at::Tensor dx, at::Tensor dw,
@@ -266,6 +270,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("shift") = pybind11::none());
   m.def("bn_finalize_partials", &hipps::bn_finalize_partials,
         "BN train-mode finalize from producer partial sums (mean/invstd/scale/shift + running stats)");
+  m.def("embed_forward", &hipps::embed_forward, "word + position + type embedding -> bf16 rows (embed.hip)");
+  m.def("embed_pos_backward", &hipps::embed_pos_backward, "position-table gradient: fixed-order batch sum");
+  m.def("embed_seg_backward", &hipps::embed_seg_backward, "table gradient over id-sorted rows, one wave per id");
   m.def("rms_forward", &hipps::rms_forward,
         "RMSNorm forward: fp32 / bf16 rows -> bf16, fp32 rstd; optional fused residual add (ln.hip)", py::arg("x"),
         py::arg("w"), py::arg("y"), py::arg("rstd"), py::arg("eps"), py::arg("add") = py::none(),

@@ -124,8 +124,12 @@ class Bert(nn.Module):
     def forward(self, ids, labels=None, kv_len=None):
         """``kv_len``: optional int32 [B] valid lengths of a right-padded batch (key padding mask)."""
         B, S = ids.shape
-        pos = torch.arange(S, device=ids.device)
-        x = self.word(ids) + self.pos(pos)[None] + self.tok_type(torch.zeros_like(ids))
+        if hnn.bert_embed_ok(ids, self.word.weight, self.pos.weight, self.tok_type.weight):
+            # one gather-add pass, deterministic table gradients (csrc/embed.hip); type ids all 0
+            x = hnn.bert_embed(ids, self.word.weight, self.pos.weight, self.tok_type.weight)
+        else:
+            pos = torch.arange(S, device=ids.device)
+            x = self.word(ids) + self.pos(pos)[None] + self.tok_type(torch.zeros_like(ids))
         x = _ln(self.emb_ln, x)
         for layer in self.layers:
             x = layer(x, kv_len)
