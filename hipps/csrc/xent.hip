@@ -9,6 +9,9 @@
 // (softmax - onehot) * g / n.  One workgroup per row, 16-byte loads, fp32 accumulation.
 #include "common.h"
 
+#include <mutex>
+#include <unordered_map>
+
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
@@ -263,9 +266,39 @@ void xent_backward(at::Tensor logits, at::Tensor labels, at::Tensor lse, at::Ten
 // -> partial[chunk][col]; pass 2 sums the chunks in order (deterministic).
 namespace hipps {
 
+// fixed-order sum of the P partial rows of 64 columns (4 waves, 8 loads in flight per lane)
+__device__ __forceinline__ void colsum_fold(const float* __restrict__ part, int64_t P, int64_t N, int64_t c,
+                                            float* __restrict__ out, float (*red)[64]) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t cc = c < N ? c : N - 1;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  int64_t p = wv;
+  for (; p + 28 < P; p += 32) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = part[(p + 4 * j) * N + cc];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+  }
+  for (; p < P; p += 4) acc[0] += part[p * N + cc];
+  float a = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  red[wv][lane] = a;
+  __syncthreads();
+  if (wv == 0 && c < N) out[c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+// tickets (optional, opt-in: see colsum_bf16): one arrival counter per 64-column tile, zero on
+// entry; the block of a tile that arrives last (agent-scope release / acquire, correct for any
+// placement over the XCDs) folds the tile's P partial rows into out and re-arms the counter --
+// one launch instead of a part + fin pair
 __global__ __launch_bounds__(256) void k_colsum_part(const uint16_t* __restrict__ x, int64_t R, int64_t N,
-                                                     int64_t rows_per, float* __restrict__ part) {
+                                                     int64_t rows_per, float* __restrict__ part,
+                                                     uint32_t* __restrict__ tickets, float* __restrict__ out) {
   __shared__ float red[32][65];
+  __shared__ float red4[4][64];
+  __shared__ uint32_t lastf;
   const int t = threadIdx.x, g = t & 7, rl = t >> 3;
   const int64_t c0 = (int64_t)blockIdx.x * 64 + g * 8;
   const int64_t r0 = (int64_t)blockIdx.y * rows_per, r1 = min(R, r0 + rows_per);
@@ -303,6 +336,24 @@ __global__ __launch_bounds__(256) void k_colsum_part(const uint16_t* __restrict_
     const int64_t c = (int64_t)blockIdx.x * 64 + t;
     if (c < N) part[(int64_t)blockIdx.y * N + c] = a;
   }
+  if (tickets == nullptr) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(tickets + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t last = old == gridDim.y - 1 ? 1u : 0u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(tickets + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+    }
+    lastf = last;
+  }
+  __syncthreads();
+  if (lastf == 0u) return;
+  colsum_fold(part, gridDim.y, N, (int64_t)blockIdx.x * 64 + (t & 63), out, red4);
 }
 
 // 64 columns per block: lane (t & 63) owns a column, the 4 waves take every 4th partial row with
@@ -311,26 +362,24 @@ __global__ __launch_bounds__(256) void k_colsum_part(const uint16_t* __restrict_
 __global__ __launch_bounds__(256) void k_colsum_fin(const float* __restrict__ part, int64_t P, int64_t N,
                                                     float* __restrict__ out) {
   __shared__ float red[4][64];
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
-  const int64_t cc = c < N ? c : N - 1;
-  float acc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-  int64_t p = wv;
-  for (; p + 28 < P; p += 32) {
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = part[(p + 4 * j) * N + cc];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += v[j];
-  }
-  for (; p < P; p += 4) acc[0] += part[p * N + cc];
-  float a = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-  red[wv][lane] = a;
-  __syncthreads();
-  if (wv == 0 && c < N) out[c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  colsum_fold(part, P, N, (int64_t)blockIdx.x * 64 + (threadIdx.x & 63), out, red);
 }
+
+namespace {
+// per-stream arrival counters of the one-launch column sum (zeroed once; each fold re-arms its own)
+constexpr int64_t kColsumTickets = 4096;
+uint32_t* colsum_tickets(hipStream_t s, const at::Tensor& like) {
+  static std::mutex mu;
+  static std::unordered_map<hipStream_t, at::Tensor> bufs;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = bufs.find(s);
+  if (it == bufs.end()) {
+    at::Tensor t = at::zeros({kColsumTickets}, like.options().dtype(at::kInt));
+    it = bufs.emplace(s, t).first;
+  }
+  return reinterpret_cast<uint32_t*>(it->second.data_ptr());
+}
+}  // namespace
 
 // out[N] (f32) = x.sum(0) for a contiguous bf16 [R, N], N % 8 == 0, 16-byte aligned
 void colsum_bf16(at::Tensor x, at::Tensor out) {
@@ -346,8 +395,21 @@ void colsum_bf16(at::Tensor x, at::Tensor out) {
   P = std::max<int64_t>(1, (R + rows_per - 1) / rows_per);
   auto stream = c10::hip::getCurrentHIPStream();
   at::Tensor part = at::empty({P, N}, out.options());
+  // opt-in (HIPPS_COLSUM_ONE=1): measured SLOWER in the BERT-base step, 735 k vs 794 k tokens/s on
+  // one box (profiles/r6/bert_mlp/colsum_one_*.json) -- each of the ~2000 blocks' agent-scope
+  // release writes back its XCD's dirty L2 lines, which costs the neighbouring kernels far more
+  // than the fin launch it saves
+  static const bool one = [] {
+    const char* e = std::getenv("HIPPS_COLSUM_ONE");
+    return e && e[0] == '1';
+  }();
+  if (one && ct <= kColsumTickets) {
+    hipLaunchKernelGGL(k_colsum_part, dim3((unsigned)ct, (unsigned)P), 256, 0, stream, (const uint16_t*)x.data_ptr(),
+                       R, N, rows_per, part.data_ptr<float>(), colsum_tickets(stream, out), out.data_ptr<float>());
+    return;
+  }
   hipLaunchKernelGGL(k_colsum_part, dim3((unsigned)ct, (unsigned)P), 256, 0, stream, (const uint16_t*)x.data_ptr(), R,
-                     N, rows_per, part.data_ptr<float>());
+                     N, rows_per, part.data_ptr<float>(), nullptr, nullptr);
   hipLaunchKernelGGL(k_colsum_fin, (int)ct, 256, 0, stream, part.data_ptr<float>(), P, N,
                      out.data_ptr<float>());
 }

@@ -57,6 +57,28 @@ def test_colsum_matches_fp32(rows, cols):
     assert torch.equal(got, hnn.colsum_f32(t))  # deterministic
 
 
+def test_colsum_one_launch_tickets_rearm():
+    """The column sum (two launches by default; with HIPPS_COLSUM_ONE=1 the one-launch form whose
+    last-arriving block per column tile folds, xent.hip): many calls of different shapes on two
+    streams, each right and bitwise repeatable (the one-launch form's counters re-arm)."""
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(1)
+    ts = [torch.randn(r, c, device="cuda").to(torch.bfloat16) for r, c in
+          ((16384, 768), (16384, 3072), (100, 64), (4097, 2304), (1, 8))]
+    refs = [t.double().sum(0) for t in ts]
+    first = [hnn.colsum_f32(t) for t in ts]
+    side = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    for i in range(40):
+        k = i % len(ts)
+        with torch.cuda.stream(side if i % 3 == 0 else torch.cuda.current_stream()):
+            got = hnn.colsum_f32(ts[k])
+        torch.cuda.synchronize()
+        torch.testing.assert_close(got.double(), refs[k], rtol=1e-5, atol=1e-3)
+        assert torch.equal(got, first[k])
+
+
 def test_fused_cross_entropy_label_semantics():
     """the mean counts only rows that carry a loss.  Ignored rows and out-of-range
     labels (which F.cross_entropy rejects) are excluded from the denominator; every row ignored
