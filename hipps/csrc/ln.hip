@@ -544,9 +544,10 @@ void rms_backward(at::Tensor dy, at::Tensor x, at::Tensor rstd, at::Tensor w, at
     dw.zero_();
     return;
   }
-  int64_t P = std::min<int64_t>(1024, std::max<int64_t>(1, R / 16));
-  const int rpb = (int)((R + P - 1) / P);
-  P = (R + rpb - 1) / rpb;
+  // 4..16 rows per workgroup: >= 2 workgroups per CU at 2048 rows (Llama-3-8B, D 4096), where
+  // 16-row blocks left 128 workgroups for 256 CUs (144 us per call, < 1 TB/s)
+  const int rpb = (int)std::min<int64_t>(16, std::max<int64_t>(4, R / 1024));
+  const int64_t P = (R + rpb - 1) / rpb;
   at::Tensor part = at::empty({P, D}, dw.options());
   auto st = c10::hip::getCurrentHIPStream();
   const size_t lds = (size_t)kLnWaves * D * sizeof(float);
