@@ -297,10 +297,18 @@ __global__ __launch_bounds__(kBlock) void k_gather(GatherPtrs src, const int64_t
     const int64_t len = row[3];
     const bool vec = ((reinterpret_cast<uintptr_t>(s) & 15) == 0);
     const int64_t nv = vec ? (len >> 2) : 0;
-    for (int64_t v = threadIdx.x; v < nv; v += blockDim.x) {
-      float4 x = Vec4<float>::load(s, v << 2);
-      if (scale != 1.f) { x.x *= scale; x.y *= scale; x.z *= scale; x.w *= scale; }
-      Vec4<Tout>::store(d, v << 2, x);
+    constexpr int U = 4;  // four 16-byte loads in flight per lane before any store
+    for (int64_t v0 = threadIdx.x; v0 < nv; v0 += U * (int64_t)blockDim.x) {
+      float4 x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (v0 + u * (int64_t)blockDim.x < nv) x[u] = Vec4<float>::load(s, (v0 + u * (int64_t)blockDim.x) << 2);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (v0 + u * (int64_t)blockDim.x < nv) {
+          if (scale != 1.f) { x[u].x *= scale; x[u].y *= scale; x[u].z *= scale; x[u].w *= scale; }
+          Vec4<Tout>::store(d, (v0 + u * (int64_t)blockDim.x) << 2, x[u]);
+        }
     }
     for (int64_t i = (nv << 2) + threadIdx.x; i < len; i += blockDim.x) Vec4<Tout>::store1(d, i, s[i] * scale);
   }
