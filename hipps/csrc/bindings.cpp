@@ -100,6 +100,7 @@ void bn_finalize_partials(at::Tensor part, int64_t nrb, int64_t M, at::Tensor we
                           double momentum);
 void maxpool3s2_backward(at::Tensor dy, at::Tensor code, at::Tensor dx);
 std::vector<at::Tensor> xent_forward(at::Tensor logits, at::Tensor labels, int64_t ignore_index);
+void colsum_fold(at::Tensor part, at::Tensor out);
 void colsum_bf16(at::Tensor x, at::Tensor out);
 std::vector<at::Tensor> attn_forward(at::Tensor q, at::Tensor k, at::Tensor v, bool causal, double scale,
                                      c10::optional<at::Tensor> kvlen);
@@ -110,7 +111,7 @@ std::vector<at::Tensor> attn_backward(at::Tensor dout, at::Tensor q, at::Tensor 
 void swiglu_forward(at::Tensor a, at::Tensor b, at::Tensor c);
 void ln_forward(at::Tensor x, at::Tensor w, at::Tensor b, at::Tensor y, at::Tensor mean, at::Tensor rstd, double eps);
 void ln_backward(at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor rstd, at::Tensor w, at::Tensor dx,
-                 at::Tensor dw, at::Tensor db);
+                 at::Tensor dw, at::Tensor db, c10::optional<at::Tensor> dxsum);
 void embed_forward(at::Tensor ids, c10::optional<at::Tensor> tt, at::Tensor word, at::Tensor pos, at::Tensor typ,
                    at::Tensor out);
 void embed_pos_backward(at::Tensor dout, at::Tensor dpos, int64_t B, int64_t S);
@@ -283,7 +284,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dy"), py::arg("x"), py::arg("rstd"), py::arg("w"), py::arg("dx"), py::arg("dw"),
         py::arg("dres") = py::none(), py::arg("dx16") = py::none());
   m.def("ln_forward", &hipps::ln_forward, "LayerNorm forward, bf16 rows, fp32 weight / bias / mean / rstd (ln.hip)");
-  m.def("ln_backward", &hipps::ln_backward, "LayerNorm backward: bf16 dx, fp32 weight / bias gradients (ln.hip)");
+  m.def("ln_backward", &hipps::ln_backward,
+        "LayerNorm backward: bf16 dx, fp32 weight / bias gradients, optional column sum of dx (ln.hip)",
+        py::arg("dy"), py::arg("x"), py::arg("mean"), py::arg("rstd"), py::arg("w"), py::arg("dx"), py::arg("dw"),
+        py::arg("db"), py::arg("dxsum") = py::none());
   m.def("swiglu_forward", &hipps::swiglu_forward, "c = silu(a) * b, bf16 (act.hip)");
   m.def("swiglu_backward", &hipps::swiglu_backward, "gradients of silu(a) * b w.r.t. a and b, bf16 (act.hip)");
   m.def("rope_apply", &hipps::rope_apply, py::arg("x"), py::arg("y"), py::arg("cos"), py::arg("sin"), py::arg("S"),
@@ -292,6 +296,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "c = silu(y[:, :F]) * y[:, F:] for a packed [rows, 2F] gate/up projection (act.hip)");
   m.def("swiglu_rows_backward", &hipps::swiglu_rows_backward,
         "packed [rows, 2F] gradient (da | db) of swiglu_rows_forward (act.hip)");
+  m.def("colsum_fold", &hipps::colsum_fold, "fixed-order sum of fp32 partial rows [P, N] -> [N]");
   m.def("colsum_bf16", &hipps::colsum_bf16, "fp32 column sums of a bf16 [rows, cols] matrix (bias gradients)");
   m.def("attn_forward", &hipps::attn_forward, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"),
         py::arg("scale"), py::arg("kv_len") = py::none(),

@@ -69,8 +69,10 @@ __device__ __attribute__((aligned(64))) const uint8_t kOnes8[64] = {
 // the bf16 pre-activation rounds it: one pass instead of the GEMM, a GELU read and its write
 // kGeluB (1x1): the next Linear's input gradient with the GELU backward in its epilogue: Y =
 // bf16(gelu'(x) * bf16(acc)), x the saved bf16 pre-activation (read like kBst's BN input)
+// kGeluBS (with kGeluB): also the column sums of the bf16 Y written (the bias gradient of the
+// Linear before the GELU), per m-tile into pa[mt][N] (a fixed-order fold sums the tiles)
 enum Epi : int { kPlain = 0, kStats = 1, kAdd = 2, kBst = 4, kBstBits = 8, kAddS2 = 16, kPar = 32, kPro = 64,
-                 kBias = 128, kGelu = 256, kGeluB = 512 };
+                 kBias = 128, kGelu = 256, kGeluB = 512, kGeluBS = 1024 };
 
 // Branch-free erf for the epilogues: erf(z) = 1 - poly(t) e^{-z^2}, t = 1 / (1 + p |z|)
 // (Abramowitz & Stegun 7.1.26, |error| < 1.5e-7 -- far below the bf16 rounding of the result);
@@ -656,6 +658,7 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   constexpr bool STATS = (EPI & kStats) != 0, ADD = (EPI & kAdd) != 0;
   constexpr int BST = (EPI & kBstBits) ? 2 : (EPI & kBst) ? 1 : 0;
   constexpr bool BIAS = (EPI & kBias) != 0;
+  constexpr bool GBS = (EPI & kGeluBS) != 0;
   if constexpr (M32) {  // C/D map (32x32x16): column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
 #pragma unroll
     for (int j = 0; j < FN2; ++j) {
@@ -721,6 +724,10 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
   // BST: this thread's 8 channels are fixed (NT % RCH == 0): per-channel BN constants in registers
   const int cc = (t % RCH) * 8;
   float bmu[8], bis[8], bsc[8], bsh[8], bsa[8], bsb[8];
+  if (GBS) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bsa[j] = bsb[j] = 0.f;
+  }
   if (BST) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -813,6 +820,13 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
           vw[j] = pack_bf16x2(gelu_bwd_f(__uint_as_float(vw[j] << 16), __uint_as_float(xw[j] << 16)),
                               gelu_bwd_f(__uint_as_float(vw[j] & 0xffff0000u), __uint_as_float(xw[j] & 0xffff0000u)));
         v = uint4{vw[0], vw[1], vw[2], vw[3]};
+        if constexpr (GBS) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            bsa[2 * j] += __uint_as_float(vw[j] << 16);
+            bsa[2 * j + 1] += __uint_as_float(vw[j] & 0xffff0000u);
+          }
+        }
       }
       *reinterpret_cast<uint4*>(g.Y + o) = v;
       if (BST) {  // dz = dy * relu'(.) on the stored bf16 dy; x-hat from the BN input
@@ -840,7 +854,7 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
     }
   }
   }
-  if (BST) {  // combine the NT/RCH row lanes of each channel chunk through LDS, fixed order
+  if (BST || GBS) {  // combine the NT/RCH row lanes of each channel chunk through LDS, fixed order
     constexpr int RL = NT / RCH;
     static_assert(2 * RL * BN * 4 <= lds_bytes<BM, BN, NS>(), "BST scratch");
     float* red = reinterpret_cast<float*>(lds);
@@ -857,8 +871,12 @@ __global__ __launch_bounds__((nthreads<BM, BN>())) void k_gemm(Args g) {
         sa += red[r * BN + t];
         sb += red[RL * BN + r * BN + t];
       }
-      g.pa[(int64_t)(n0 + t) * g.pstride + g.pcol0 + mt] = sa;
-      g.pb[(int64_t)(n0 + t) * g.pstride + g.pcol0 + mt] = sb;
+      if constexpr (GBS) {
+        g.pa[(int64_t)mt * g.N + n0 + t] = sa;  // [mtiles][N]: rows of column partial sums
+      } else {
+        g.pa[(int64_t)(n0 + t) * g.pstride + g.pcol0 + mt] = sa;
+        g.pb[(int64_t)(n0 + t) * g.pstride + g.pcol0 + mt] = sb;
+      }
     }
   }
   if (STATS && t < BN) {
@@ -1339,7 +1357,8 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
   int epi = g2::kPlain;
   if (part.has_value() && part->defined()) {
     TORCH_CHECK(part->is_cuda() && part->scalar_type() == at::kFloat && part->is_contiguous() &&
-                    part->numel() == 2 * N * mtiles, "gemm2: part must be f32 [2, Cout, mtiles]");
+                    part->numel() == (gelu == 2 ? 1 : 2) * N * mtiles,
+                "gemm2: part must be f32 [2, Cout, mtiles] ([mtiles, Cout] with the GELU backward)");
     a.pa = part->data_ptr<float>();
     a.pb = a.pa + N * mtiles;
   }
@@ -1385,7 +1404,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
     } else {
       epi |= g2::kBst;
     }
-  } else if (a.pa != nullptr) {
+  } else if (a.pa != nullptr && gelu != 2) {
     TORCH_CHECK(!(epi & g2::kAdd), "gemm2: forward statistics and the add epilogue are exclusive");
     epi |= g2::kStats;
   }
@@ -1413,6 +1432,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
       TORCH_CHECK(!(bias.has_value() && bias->defined()), "gemm2: the GELU backward epilogue takes no bias");
       a.bx = (const uint16_t*)gelu_pre->data_ptr();
       epi |= g2::kGeluB;
+      if (a.pa != nullptr) epi |= g2::kGeluBS;  // + the column sums of y, per m-tile
     }
   } else {
     TORCH_CHECK(gelu == 0, "gemm2: gelu needs gelu_pre");
@@ -1462,6 +1482,7 @@ void gemm2_conv(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tens
         case g2::kGelu: HIPPS_G2(BMc, BNc, g2::kGelu, false); break;                                \
         case g2::kBias | g2::kGelu: HIPPS_G2(BMc, BNc, (g2::kBias | g2::kGelu), false); break;      \
         case g2::kGeluB: HIPPS_G2(BMc, BNc, g2::kGeluB, false); break;                              \
+        case g2::kGeluB | g2::kGeluBS: HIPPS_G2(BMc, BNc, (g2::kGeluB | g2::kGeluBS), false); break;  \
         case g2::kBst: HIPPS_G2(BMc, BNc, g2::kBst, false); break;                                  \
         case g2::kBst | g2::kAdd: HIPPS_G2(BMc, BNc, (g2::kBst | g2::kAdd), false); break;          \
         case g2::kBstBits: HIPPS_G2(BMc, BNc, g2::kBstBits, false); break;                          \

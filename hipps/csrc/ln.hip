@@ -101,12 +101,15 @@ __global__ __launch_bounds__(64 * kLnWaves) void k_ln_fwd(const uint16_t* __rest
 
 // rows [blockIdx.x * rpb, +rpb): dx per row; per-column sums of dy * xhat and dy over those rows
 // -> part[blockIdx.x] (2 x D floats: dgamma partial, dbeta partial)
-template <int NC>
+// DXS: a third column sum, of the bf16 dx written (the bias gradient of the Linear whose output
+// this LayerNorm normalised -- BERT's attn_out / out: their colsum pass over dx is saved)
+template <int NC, bool DXS = false>
 __global__ __launch_bounds__(64 * kLnWaves) void k_ln_bwd(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
                                                           const float* __restrict__ mean, const float* __restrict__ rstd,
                                                           const float* __restrict__ w, uint16_t* __restrict__ dx,
                                                           float* __restrict__ part, int64_t R, int D, int rpb) {
-  extern __shared__ float red[];  // [kLnWaves][2][D]
+  constexpr int NK = DXS ? 3 : 2;
+  extern __shared__ float red[];  // [kLnWaves][NK][D]
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nch = D >> 3;
   float ww[NC][8];
@@ -118,11 +121,15 @@ __global__ __launch_bounds__(64 * kLnWaves) void k_ln_bwd(const uint16_t* __rest
     ww[c][0] = w0.x; ww[c][1] = w0.y; ww[c][2] = w0.z; ww[c][3] = w0.w;
     ww[c][4] = w1.x; ww[c][5] = w1.y; ww[c][6] = w1.z; ww[c][7] = w1.w;
   }
-  float dg[NC][8], db[NC][8];
+  float dg[NC][8], db[NC][8], dsx[DXS ? NC : 1][8];
 #pragma unroll
   for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int j = 0; j < 8; ++j) dg[c][j] = db[c][j] = 0.f;
+#pragma unroll
+  for (int c = 0; c < (DXS ? NC : 1); ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dsx[c][j] = 0.f;
   const int64_t r0 = (int64_t)blockIdx.x * rpb;
   const int64_t r1 = r0 + rpb < R ? r0 + rpb : R;
   // software pipelined: the next row's x / dy / statistics are in flight while this row is
@@ -183,6 +190,13 @@ __global__ __launch_bounds__(64 * kLnWaves) void k_ln_bwd(const uint16_t* __rest
           o[j] = pack_bf16x2(rs * (g[c][2 * j] - m1 - xh[c][2 * j] * m2),
                              rs * (g[c][2 * j + 1] - m1 - xh[c][2 * j + 1] * m2));
         *reinterpret_cast<u32x4*>(dx + row * D + ch * 8) = o;
+        if constexpr (DXS) {  // the stored (bf16-rounded) values, as a colsum over dx would read them
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            dsx[DXS ? c : 0][2 * j] += __uint_as_float(o[j] << 16);
+            dsx[DXS ? c : 0][2 * j + 1] += __uint_as_float(o[j] & 0xffff0000u);
+          }
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           dg[c][j] += gy[c][j] * xh[c][j];
@@ -198,18 +212,19 @@ __global__ __launch_bounds__(64 * kLnWaves) void k_ln_bwd(const uint16_t* __rest
     if (ch < nch) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        red[(wv * 2) * D + ch * 8 + j] = dg[c][j];
-        red[(wv * 2 + 1) * D + ch * 8 + j] = db[c][j];
+        red[(wv * NK) * D + ch * 8 + j] = dg[c][j];
+        red[(wv * NK + 1) * D + ch * 8 + j] = db[c][j];
+        if constexpr (DXS) red[(wv * NK + 2) * D + ch * 8 + j] = dsx[DXS ? c : 0][j];
       }
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 2 * D; i += 64 * kLnWaves) {
+  for (int i = threadIdx.x; i < NK * D; i += 64 * kLnWaves) {
     const int k = i / D, col = i - k * D;
     float a = 0.f;
 #pragma unroll
-    for (int q = 0; q < kLnWaves; ++q) a += red[(q * 2 + k) * D + col];
-    part[(int64_t)blockIdx.x * 2 * D + i] = a;
+    for (int q = 0; q < kLnWaves; ++q) a += red[(q * NK + k) * D + col];
+    part[(int64_t)blockIdx.x * NK * D + i] = a;
   }
 }
 
@@ -219,7 +234,8 @@ __global__ __launch_bounds__(64 * kLnWaves) void k_ln_bwd(const uint16_t* __rest
 // dependent HBM round trips, 24 us per call on BERT-base)
 constexpr int kFoldWaves = 16;
 __global__ __launch_bounds__(64 * kFoldWaves) void k_ln_fold(const float* __restrict__ part, int P, int D, int nk,
-                                                             float* __restrict__ dw, float* __restrict__ dbias) {
+                                                             float* __restrict__ dw, float* __restrict__ dbias,
+                                                             float* __restrict__ dsum = nullptr) {
   __shared__ float red[kFoldWaves][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + lane;  // over nk * D
@@ -242,7 +258,8 @@ __global__ __launch_bounds__(64 * kFoldWaves) void k_ln_fold(const float* __rest
 #pragma unroll
     for (int q = 0; q < kFoldWaves; ++q) a += red[q][lane];
     if (i < D) dw[i] = a;
-    else dbias[i - D] = a;
+    else if (i < 2 * D) dbias[i - D] = a;
+    else dsum[i - 2 * D] = a;
   }
 }
 
@@ -428,8 +445,9 @@ void ln_forward(at::Tensor x, at::Tensor w, at::Tensor b, at::Tensor y, at::Tens
 #undef HIPPS_LNF
 }
 
+// dxsum (optional): fp32 [D] column sum of the bf16 dx written (a Linear's bias gradient)
 void ln_backward(at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor rstd, at::Tensor w, at::Tensor dx,
-                 at::Tensor dw, at::Tensor db) {
+                 at::Tensor dw, at::Tensor db, c10::optional<at::Tensor> dxsum) {
   const int64_t D = x.size(-1);
   ln_check(x, D);
   ln_check(dy, D);
@@ -449,20 +467,29 @@ void ln_backward(at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor rstd, 
   int64_t P = std::min<int64_t>(1024, std::max<int64_t>(1, R / 16));
   const int rpb = (int)((R + P - 1) / P);
   P = (R + rpb - 1) / rpb;
-  at::Tensor part = at::empty({P, 2, D}, dw.options());
+  const bool dxs = dxsum.has_value() && dxsum->defined();
+  if (dxs) ln_param_check(*dxsum, D, "dx column sum");
+  const int nk = dxs ? 3 : 2;
+  at::Tensor part = at::empty({P, nk, D}, dw.options());
   auto st = c10::hip::getCurrentHIPStream();
-  const size_t lds = (size_t)kLnWaves * 2 * D * sizeof(float);
+  const size_t lds = (size_t)kLnWaves * nk * D * sizeof(float);
   const int nc = (int)((D / 8 + 63) / 64);
-#define HIPPS_LNB(NCc)                                                                                                \
-  hipLaunchKernelGGL(k_ln_bwd<NCc>, (int)P, 64 * kLnWaves, lds, st, (const uint16_t*)dy.data_ptr(),                  \
+#define HIPPS_LNB(NCc, DX)                                                                                            \
+  hipLaunchKernelGGL((k_ln_bwd<NCc, DX>), (int)P, 64 * kLnWaves, lds, st, (const uint16_t*)dy.data_ptr(),            \
                      (const uint16_t*)x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), w.data_ptr<float>(), \
                      (uint16_t*)dx.data_ptr(), part.data_ptr<float>(), R, (int)D, rpb)
-  if (nc <= 1) HIPPS_LNB(1);
-  else if (nc <= 2) HIPPS_LNB(2);
-  else HIPPS_LNB(4);
+  if (dxs) {
+    if (nc <= 1) HIPPS_LNB(1, true);
+    else if (nc <= 2) HIPPS_LNB(2, true);
+    else HIPPS_LNB(4, true);
+  } else {
+    if (nc <= 1) HIPPS_LNB(1, false);
+    else if (nc <= 2) HIPPS_LNB(2, false);
+    else HIPPS_LNB(4, false);
+  }
 #undef HIPPS_LNB
-  hipLaunchKernelGGL(k_ln_fold, (int)((2 * D + 63) / 64), 64 * kFoldWaves, 0, st, part.data_ptr<float>(), (int)P, (int)D, 2,
-                     dw.data_ptr<float>(), db.data_ptr<float>());
+  hipLaunchKernelGGL(k_ln_fold, (int)((nk * D + 63) / 64), 64 * kFoldWaves, 0, st, part.data_ptr<float>(), (int)P, (int)D,
+                     nk, dw.data_ptr<float>(), db.data_ptr<float>(), dxs ? dxsum->data_ptr<float>() : nullptr);
 }
 
 // x: fp32 or bf16 [rows, D] (D % 8 == 0, D <= 4096); y bf16; rstd fp32 [rows]
@@ -570,7 +597,7 @@ void rms_backward(at::Tensor dy, at::Tensor x, at::Tensor rstd, at::Tensor w, at
   else HIPPS_RMSB(8);
 #undef HIPPS_RMSB
   hipLaunchKernelGGL(k_ln_fold, (int)((D + 63) / 64), 64 * kFoldWaves, 0, st, part.data_ptr<float>(), (int)P, (int)D, 1,
-                     dw.data_ptr<float>(), dw.data_ptr<float>());
+                     dw.data_ptr<float>(), dw.data_ptr<float>(), nullptr);
 }
 
 }  // namespace hipps

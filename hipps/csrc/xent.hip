@@ -381,6 +381,19 @@ uint32_t* colsum_tickets(hipStream_t s, const at::Tensor& like) {
 }
 }  // namespace
 
+// out[N] (f32) = part.sum(0), fixed order, for fp32 partial rows [P, N] (a producing kernel's
+// per-tile column sums, e.g. gemm2's kGeluBS)
+void colsum_fold(at::Tensor part, at::Tensor out) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.dim() == 2 && part.is_contiguous(),
+              "colsum_fold: part must be a contiguous fp32 [P, N] device tensor");
+  const int64_t P = part.size(0), N = part.size(1);
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() == N,
+              "colsum_fold: out");
+  if (N == 0) return;
+  hipLaunchKernelGGL(k_colsum_fin, (int)((N + 63) / 64), 256, 0, c10::hip::getCurrentHIPStream(),
+                     part.data_ptr<float>(), P, N, out.data_ptr<float>());
+}
+
 // out[N] (f32) = x.sum(0) for a contiguous bf16 [R, N], N % 8 == 0, 16-byte aligned
 void colsum_bf16(at::Tensor x, at::Tensor out) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous(),

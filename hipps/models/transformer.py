@@ -32,7 +32,7 @@ import torch.nn.functional as F
 from hipps.ops import nn as hnn
 
 
-def _ln(mod: nn.LayerNorm, x: torch.Tensor) -> torch.Tensor:
+def _ln(mod: nn.LayerNorm, x: torch.Tensor, colsum_dx: bool = False) -> torch.Tensor:
     """LayerNorm on the autocast dtype: PyTorch's kernel reads bf16, computes in fp32 and writes
     bf16, where autocast's fp32 policy for layer_norm would cast the activation up, write fp32 and
     cast it back down for the next GEMM (two extra passes per norm, fp32 residual adds)."""
@@ -41,7 +41,7 @@ def _ln(mod: nn.LayerNorm, x: torch.Tensor) -> torch.Tensor:
         with torch.autocast("cuda", enabled=False):
             xd = x.to(dt)
             if len(mod.normalized_shape) == 1 and hnn.layer_norm_ok(xd, mod.weight, mod.bias):
-                return hnn.layer_norm(xd, mod.weight, mod.bias, mod.eps)  # csrc/ln.hip
+                return hnn.layer_norm(xd, mod.weight, mod.bias, mod.eps, colsum_dx)  # csrc/ln.hip
             return F.layer_norm(xd, mod.normalized_shape, mod.weight.to(dt), mod.bias.to(dt), mod.eps)
     return mod(x)
 
@@ -91,9 +91,10 @@ class BertLayer(nn.Module):
             a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask).transpose(1, 2)
         a = a.reshape(B, S, D)
         # residual adds ride in the output projections (GEMM epilogue / hipBLASLt C)
-        x = _ln(self.attn_ln, self.attn_out(a, residual=x, link=link))
+        # (colsum_dx: the LayerNorm backward also sums its dx -- attn_out's / out's bias gradient)
+        x = _ln(self.attn_ln, self.attn_out(a, residual=x, link=link), colsum_dx=True)
         # intermediate -> GELU -> output (+ x) as one node: GELU in the GEMM epilogues both ways
-        return _ln(self.out_ln, hnn.gelu_mlp(x, self.inter, self.out, residual_x=True))
+        return _ln(self.out_ln, hnn.gelu_mlp(x, self.inter, self.out, residual_x=True), colsum_dx=True)
 
 
 class Bert(nn.Module):

@@ -1054,16 +1054,21 @@ def _gelu_linear_fwd(x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Ten
     return post, pre
 
 
-def _gelu_dgrad(dy2: torch.Tensor, w: torch.Tensor, pre: torch.Tensor, wt=None) -> torch.Tensor:
+def _gelu_dgrad(dy2: torch.Tensor, w: torch.Tensor, pre: torch.Tensor, wt=None, bias_grad: bool = False) -> torch.Tensor:
     """d pre = gelu'(pre) * (dy2 w) (bf16 [M, K] from dy2 [M, N], w [N, K]: the input gradient of
     the Linear after a GELU, through the GELU): per shape the faster of hipBLASLt mm + PyTorch's
     GELU backward and the gemm2 kGeluB epilogue over ``wt`` = w^T [K, N] (the flat store's
-    transposed shadow, mark_transposed_reader; without one, no gemm2 candidate)."""
+    transposed shadow, mark_transposed_reader; without one, no gemm2 candidate).  ``bias_grad``:
+    the column sum of d pre (the first Linear's bias gradient) is left for colsum_f32 -- the gemm2
+    epilogue sums its own output tiles (kGeluBS), so no pass re-reads d pre."""
     M, N = dy2.shape
     K = w.shape[1]
 
     def blas():
-        return torch.ops.aten.gelu_backward(torch.mm(dy2, w), pre)
+        out = torch.ops.aten.gelu_backward(torch.mm(dy2, w), pre)
+        if bias_grad:
+            stash_colsum(out, colsum_f32(out))
+        return out
 
     if not (_GEMM2 and wt is not None and N % 64 == 0 and K % 64 == 0 and M >= 1024 and _g2_ok(dy2, wt, pre)):
         return blas()
@@ -1071,14 +1076,21 @@ def _gelu_dgrad(dy2: torch.Tensor, w: torch.Tensor, pre: torch.Tensor, wt=None) 
     out = torch.empty((M, K), dtype=torch.bfloat16, device=dy2.device)
 
     def g2(bm, bn, ns):
-        C.gemm2_conv(dy2, wt, out, None, None, None, 1, 1, 1, 1, 1, 0, bm, bn, stages=ns, gelu_pre=pre, gelu=2)
+        part = None
+        if bias_grad:
+            part = torch.empty((C.gemm2_mtiles(M, K, N, bm), K), dtype=torch.float32, device=dy2.device)
+        C.gemm2_conv(dy2, wt, out, part, None, None, 1, 1, 1, 1, 1, 0, bm, bn, stages=ns, gelu_pre=pre, gelu=2)
+        if bias_grad:
+            db = torch.empty(K, dtype=torch.float32, device=dy2.device)
+            C.colsum_fold(part, db)
+            stash_colsum(out, db)
         return out
 
     cands = {"blas": blas}
     for name in _g2_names(K):
         bm, bn, ns = _g2_parse(name)
         cands[name] = (lambda bm=bm, bn=bn, ns=ns: g2(bm, bn, ns))
-    return cands[TUNER.pick(("gelu_dgrad", M, N, K), cands)]()
+    return cands[TUNER.pick(("gelu_dgrad", M, N, K, bias_grad), cands)]()
 
 
 def _dgrad(dy2: torch.Tensor, w_master: torch.Tensor, add: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -1145,7 +1157,8 @@ class _GeluMLP(torch.autograd.Function):
         if dy2.dtype != torch.bfloat16:
             dy2 = dy2.to(torch.bfloat16)
         dy2 = dy2.contiguous()
-        dpre = _gelu_dgrad(dy2, bf16_weight(w2m, idle=False), pre, transposed_weight(w2m))
+        dpre = _gelu_dgrad(dy2, bf16_weight(w2m, idle=False), pre, transposed_weight(w2m),
+                           bias_grad=ctx.has_b1 and ctx.needs_input_grad[2])
         dx = dw1 = db1 = dw2 = db2 = None
         if ctx.needs_input_grad[0]:
             dx = _dgrad(dpre, w1m, dy2 if ctx.res_x else None).view(ctx.xshape)
@@ -1173,9 +1186,31 @@ def gelu_mlp(x: torch.Tensor, l1: nn.Linear, l2: nn.Linear, residual_x: bool = F
     return l2(h, residual=x) if residual_x and isinstance(l2, Linear) else (l2(h) + x if residual_x else l2(h))
 
 
+# column sums computed as a by-product of the kernel that wrote a gradient (LayerNorm backward
+# over its dx: the bias gradient of the Linear before it), keyed by data pointer; each entry holds
+# its tensor (the pointer cannot be reused while it waits) and the tensor's version (an in-place
+# change voids it).  Bounded: an entry nobody consumes is dropped after 4 newer ones.
+_COLSUM_STASH: "collections.OrderedDict" = collections.OrderedDict()
+
+
+def stash_colsum(t: torch.Tensor, cs: torch.Tensor) -> None:
+    """Record cs = t.reshape(-1, t.shape[-1]).sum(0) (fp32) for colsum_f32 to return for t."""
+    _COLSUM_STASH[t.data_ptr()] = (t, t._version, cs)
+    while len(_COLSUM_STASH) > 4:
+        _COLSUM_STASH.popitem(last=False)
+
+
 def colsum_f32(t: torch.Tensor) -> torch.Tensor:
     """t.sum(0) in fp32 for a 2-d bf16 device tensor (csrc/xent.hip k_colsum: deterministic,
-    ~4x PyTorch's reduce on a bias gradient); torch.sum otherwise."""
+    ~4x PyTorch's reduce on a bias gradient); torch.sum otherwise.  A sum the producing kernel
+    already computed (stash_colsum) is returned without a pass over t."""
+    if _COLSUM_STASH and t.dim() == 2:
+        hit = _COLSUM_STASH.pop(t.data_ptr(), None)
+        if hit is not None:
+            src, ver, cs = hit
+            if (src._version == ver and src.dtype == t.dtype and src.numel() == t.numel()
+                    and src.shape[-1] == t.shape[1] and src.is_contiguous() and t.is_contiguous()):
+                return cs
     if (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.is_contiguous() and t.shape[1] % 8 == 0
             and t.data_ptr() % 16 == 0):
         out = torch.empty(t.shape[1], dtype=torch.float32, device=t.device)
@@ -1511,7 +1546,7 @@ class _LayerNorm(torch.autograd.Function):
     per-forward casts of the parameters, fp32 weight / bias gradients written directly."""
 
     @staticmethod
-    def forward(ctx, x, w, b, eps):
+    def forward(ctx, x, w, b, eps, colsum_dx=False):
         D = x.shape[-1]
         y = torch.empty_like(x)
         R = x.numel() // D
@@ -1519,6 +1554,7 @@ class _LayerNorm(torch.autograd.Function):
         rstd = torch.empty(R, dtype=torch.float32, device=x.device)
         native().ln_forward(x, w, b, y, mean, rstd, float(eps))
         ctx.save_for_backward(x, w, mean, rstd)
+        ctx.colsum_dx = bool(colsum_dx)
         return y
 
     @staticmethod
@@ -1527,8 +1563,11 @@ class _LayerNorm(torch.autograd.Function):
         dy = dy.to(torch.bfloat16).contiguous()
         dx = torch.empty_like(x)
         dw, db = torch.empty_like(w), torch.empty_like(w)
-        native().ln_backward(dy, x, mean, rstd, w, dx, dw, db)
-        return dx, dw, db, None
+        cs = torch.empty_like(w) if ctx.colsum_dx else None
+        native().ln_backward(dy, x, mean, rstd, w, dx, dw, db, cs)
+        if cs is not None:
+            stash_colsum(dx, cs)
+        return dx, dw, db, None, None
 
 
 def layer_norm_ok(x: torch.Tensor, weight, bias) -> bool:
@@ -1540,9 +1579,12 @@ def layer_norm_ok(x: torch.Tensor, weight, bias) -> bool:
                     for p in (weight, bias)))
 
 
-def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float) -> torch.Tensor:
-    """F.layer_norm over the last dim on the fused kernels (callers check layer_norm_ok)."""
-    return _LayerNorm.apply(x, weight, bias, eps)
+def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float,
+               colsum_dx: bool = False) -> torch.Tensor:
+    """F.layer_norm over the last dim on the fused kernels (callers check layer_norm_ok).
+    ``colsum_dx``: x is a biased Linear's output -- the backward also sums dx over the rows and
+    leaves it for that Linear's bias gradient (stash_colsum / colsum_f32)."""
+    return _LayerNorm.apply(x, weight, bias, eps, colsum_dx)
 
 
 class _RMSNorm(torch.autograd.Function):

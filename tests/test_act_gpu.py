@@ -199,3 +199,35 @@ def test_add_rms_norm_matches_fp32(R, D, with_dres):
     torch.testing.assert_close(y.grad.float(), xf.grad.to(torch.bfloat16).float(), rtol=1e-2, atol=1e-2)
     assert torch.equal(y.grad, x.grad.to(torch.bfloat16))
     torch.testing.assert_close(w.grad, wf.grad, rtol=2e-2, atol=2e-3 * R ** 0.5 + 1e-3)
+
+
+def test_layer_norm_dx_colsum_stash():
+    """LayerNorm backward with colsum_dx: the column sum of the bf16 dx it wrote is left for
+    colsum_f32 (the bias gradient of the Linear before the norm) -- equal to summing dx itself,
+    consumed once, and voided by an in-place change of dx.  (dx is caught by a hook on a non-leaf
+    input, as the Linear's backward receives it: a leaf's .grad may be a copy.)"""
+    from hipps.ops import nn as hnn
+
+    torch.manual_seed(4)
+    R, D = 4096, 768
+    x0 = torch.randn(R, D, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    w = torch.randn(D, device=DEV) * 0.2 + 1
+    b = torch.randn(D, device=DEV) * 0.1
+    g = torch.randn(R, D, device=DEV).to(torch.bfloat16)
+
+    def run():
+        got = []
+        x = x0 * 1.0
+        x.register_hook(lambda t: got.append(t))
+        hnn.layer_norm(x, w, b, 1e-12, colsum_dx=True).backward(g)
+        return got[0]
+
+    dx = run()
+    assert dx.data_ptr() in hnn._COLSUM_STASH
+    ref = dx.double().sum(0)
+    got = hnn.colsum_f32(dx)
+    torch.testing.assert_close(got.double(), ref, rtol=1e-5, atol=1e-3)
+    assert dx.data_ptr() not in hnn._COLSUM_STASH  # consumed
+    dx = run()
+    dx.mul_(2)  # in-place change: the stashed sum is void
+    torch.testing.assert_close(hnn.colsum_f32(dx).double(), dx.double().sum(0), rtol=1e-5, atol=1e-3)

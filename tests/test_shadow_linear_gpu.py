@@ -321,6 +321,15 @@ def test_gemm2_gelu_epilogues_every_tile(name):
     prf = pre.float()
     ref = dpost * (0.5 * (1 + torch.erf(prf * 0.7071067811865476)) + prf * torch.exp(-0.5 * prf * prf) * 0.3989422804014327)
     torch.testing.assert_close(dpre.float(), ref, rtol=2e-2, atol=2e-2)
+    # kGeluBS: the same output plus per-m-tile column sums of it (the first Linear's bias gradient)
+    part = torch.empty((C.gemm2_mtiles(M, N, K2, bm), N), device=DEV, dtype=torch.float32)
+    dpre2 = torch.empty_like(dpre)
+    C.gemm2_conv(dy, w2.t().contiguous(), dpre2, part, None, None, 1, 1, 1, 1, 1, 0, bm, bn, stages=ns,
+                 gelu_pre=pre, gelu=2)
+    assert torch.equal(dpre2, dpre)
+    db = torch.empty(N, device=DEV, dtype=torch.float32)
+    C.colsum_fold(part, db)
+    torch.testing.assert_close(db.double(), dpre.double().sum(0), rtol=1e-5, atol=1e-3)
 
 
 def test_gelu_mlp_matches_fp32_and_composition():
