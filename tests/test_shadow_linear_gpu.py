@@ -399,3 +399,43 @@ def test_residual_link_folds_the_residual_gradient():
     finally:
         hnn.unregister_weight_shadow(shadow)
         hnn.unregister_transposed_weight(w1)
+
+
+def test_bert_fused_tail_matches_compositions_at_gemm2_sizes(monkeypatch):
+    """A small BERT (1024 tokens: the gemm2 candidates are live) with the round-6 transformer tail
+    -- GELU MLP node (kGelu / kGeluB / kGeluBS over the W^T shadows), residual links, LayerNorm dx
+    column sums, fused embedding -- against the same model on the module compositions: the first
+    step's gradients agree and three steps' losses track each other."""
+    import hipps
+    from hipps.models.transformer import Bert, BertConfig
+    from hipps.ops import nn as hnn
+
+    def run(fused):
+        for flag in ("_GELU_MLP", "_RES_LINK", "_FUSED_EMBED"):
+            monkeypatch.setattr(hnn, flag, fused)
+        torch.manual_seed(21)
+        m = Bert(BertConfig(vocab=1000, hidden=128, layers=2, heads=2, ffn=512, max_pos=128)).cuda()
+        opt = hipps.SGD(m.named_parameters(), lr=0.05, momentum=0.9, mode="local", bf16_weights="on")
+        ids = torch.randint(0, 1000, (8, 128), device=DEV, generator=torch.Generator(device=DEV).manual_seed(22))
+        losses, grads = [], None
+        try:
+            for i in range(3):
+                opt.zero_grad()
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    loss = m(ids, ids)
+                loss.backward()
+                if i == 0:
+                    grads = {n: p.grad.detach().float().clone() for n, p in m.named_parameters() if p.grad is not None}
+                opt.step()
+                losses.append(loss.item())
+        finally:
+            opt.close()
+        return losses, grads
+
+    (l1, g1), (l0, g0) = run(True), run(False)
+    assert g1.keys() == g0.keys()
+    for n in g0:
+        scale = g0[n].abs().max().item() + 1e-6
+        assert (g1[n] - g0[n]).abs().max().item() <= 5e-2 * scale + 1e-4, n
+    torch.testing.assert_close(torch.tensor(l1), torch.tensor(l0), rtol=2e-2, atol=2e-2)
+    assert l1[-1] < l1[0]
