@@ -12,6 +12,8 @@
 //             weight / bias gradients (deterministic)
 #include "common.h"
 
+#include <type_traits>
+
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
@@ -352,7 +354,79 @@ __global__ __launch_bounds__(64 * kLnWaves) void k_rms_bwd(const uint16_t* __res
   }
   const int64_t r0 = (int64_t)blockIdx.x * rpb;
   const int64_t r1 = r0 + rpb < R ? r0 + rpb : R;
-  for (int64_t row = r0 + wv; row < r1; row += kLnWaves) {
+  // fp32 rows of D <= 2048 (Llama-3-1B): the row stays in registers between the two passes and
+  // the next row's x / dy / rstd are in flight while this one is reduced and written (the
+  // two-pass re-read form ran ~2.9 TB/s); D = 4096 keeps the re-read form (register budget)
+  constexpr bool REG = NC <= 4 && std::is_same<TX, float>::value;
+  if constexpr (REG) {
+    float4 nx[NC][2];
+    u32x4 ndy[NC];
+    float nrs = 0.f;
+    auto fetch = [&](int64_t row) {
+      if (row < r1) {
+        nrs = rstd[row];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          const int ch = lane + 64 * c;
+          if (ch < nch) {
+            const float* xp = reinterpret_cast<const float*>(x) + row * D + ch * 8;
+            nx[c][0] = *reinterpret_cast<const float4*>(xp);
+            nx[c][1] = *reinterpret_cast<const float4*>(xp + 4);
+            ndy[c] = *reinterpret_cast<const u32x4*>(dy + row * D + ch * 8);
+          }
+        }
+      }
+    };
+    fetch(r0 + wv);
+    for (int64_t row = r0 + wv; row < r1; row += kLnWaves) {
+      const float rs = nrs;
+      float xv[NC][8], gy[NC][8];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        xv[c][0] = nx[c][0].x; xv[c][1] = nx[c][0].y; xv[c][2] = nx[c][0].z; xv[c][3] = nx[c][0].w;
+        xv[c][4] = nx[c][1].x; xv[c][5] = nx[c][1].y; xv[c][6] = nx[c][1].z; xv[c][7] = nx[c][1].w;
+        unpack8(ndy[c], gy[c]);
+      }
+      fetch(row + kLnWaves);
+      float gr[NC][8];
+      if (dres) {  // this row's residual gradient, issued before the reduction
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          const int ch = lane + 64 * c;
+          if (ch < nch) Ld8<float>::load(dres + row * D + ch * 8, gr[c]);
+        }
+      }
+      float s2 = 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if (lane + 64 * c < nch) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s2 += gy[c][j] * ww[c][j] * xv[c][j] * rs;
+        }
+      }
+      const float m2 = wsum(s2) / D;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int ch = lane + 64 * c;
+        if (ch < nch) {
+          float o[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float xh = xv[c][j] * rs;
+            o[j] = rs * (gy[c][j] * ww[c][j] - xh * m2);
+            dg[c][j] += gy[c][j] * xh;
+          }
+          if (dres) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] += gr[c][j];
+          }
+          Ld8<TX>::store(dx + row * D + ch * 8, o);
+          if (dx16) Ld8<uint16_t>::store(dx16 + row * D + ch * 8, o);
+        }
+      }
+    }
+  }
+  for (int64_t row = r0 + wv; !REG && row < r1; row += kLnWaves) {
     const float rs = rstd[row];
     float s2 = 0.f;
 #pragma unroll
