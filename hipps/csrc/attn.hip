@@ -149,6 +149,28 @@ __device__ __forceinline__ float half_sum(float x) {
 
 #define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
 
+// vmcnt-only s_waitcnt immediate (gfx9 encoding; expcnt / lgkmcnt at their maxima)
+constexpr int waitcnt_vm(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
+// LDS-DMA instructions per wave for one KT-row tile
+template <int D> constexpr int tile_glds() { return KT * (D / 8) / (64 * NW); }
+
+// NS: LDS stages of the streamed tiles.  2: the DMA of tile it+1 is issued after the barrier of
+// tile it and drained before the next barrier -- one tile's compute (~1 us at D = 64) to cover
+// the HBM latency.  3: tile it+2 is issued instead and each wait leaves the younger tile in
+// flight (cdna_hip_programming.md 'Pipelining across barriers').
+template <int NS> __device__ __forceinline__ void wait_tile(bool younger, int n_younger) {
+  if (NS == 3 && younger) {
+    // n_younger is one of two wave-uniform counts (the rowstat DMA of wave 0): immediates only
+    if (n_younger == 5) __builtin_amdgcn_s_waitcnt(waitcnt_vm(5));
+    else if (n_younger == 4) __builtin_amdgcn_s_waitcnt(waitcnt_vm(4));
+    else if (n_younger == 9) __builtin_amdgcn_s_waitcnt(waitcnt_vm(9));
+    else if (n_younger == 8) __builtin_amdgcn_s_waitcnt(waitcnt_vm(8));
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
 // row of accumulator register r for lane half h (32x32 C layout)
 __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
@@ -158,10 +180,10 @@ __device__ __forceinline__ void store4(uint16_t* p, float a, float b, float c, f
 }
 
 // ------------------------------------------------------------------------------------ forward
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int NS = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_attn_fwd(Args a) {
   constexpr int DK = D / 16, DB = D / 32, TILE = KT * 2 * D;
-  __shared__ __attribute__((aligned(16))) char lds[2][2 * TILE];
+  __shared__ __attribute__((aligned(16))) char lds[NS][2 * TILE];
   const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int h = lane >> 5;
   const int nbh = a.B * a.Hq, bid = blockIdx.x;
@@ -185,21 +207,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
   float m = -INFINITY, lsum = 0.f;
   const float c = a.scale * kLog2e;
-  if (ntile > 0) {
-    stage_tile<D>(lds[0], kb, a.kss, 0, kv_end, w, lane);
-    stage_tile<D>(lds[0] + TILE, vb, a.vss, 0, kv_end, w, lane);
+  for (int p = 0; p < NS - 1 && p < ntile; ++p) {
+    stage_tile<D>(lds[p], kb, a.kss, p * KT, kv_end, w, lane);
+    stage_tile<D>(lds[p] + TILE, vb, a.vss, p * KT, kv_end, w, lane);
   }
   for (int it = 0; it < ntile; ++it) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // tile it landed for every wave; the other buffer is free
-    if (it + 1 < ntile) {
-      char* nb = lds[(it + 1) & 1];
-      stage_tile<D>(nb, kb, a.kss, (it + 1) * KT, kv_end, w, lane);
-      stage_tile<D>(nb + TILE, vb, a.vss, (it + 1) * KT, kv_end, w, lane);
+    wait_tile<NS>(it + 1 < ntile, 2 * tile_glds<D>());
+    __syncthreads();  // tile it landed for every wave; the slot of tile it-1 is free
+    if (it + NS - 1 < ntile) {
+      char* nb = lds[(it + NS - 1) % NS];
+      stage_tile<D>(nb, kb, a.kss, (it + NS - 1) * KT, kv_end, w, lane);
+      stage_tile<D>(nb + TILE, vb, a.vss, (it + NS - 1) * KT, kv_end, w, lane);
     }
     const int k0 = it * KT;
     if (CAUSAL && k0 > qw0 + 31) continue;  // (wave-uniform) every key above this wave's rows
-    const char* Kt = lds[it & 1];
+    const char* Kt = lds[it % NS];
     const char* Vt = Kt + TILE;
     f32x16 s[2];
 #pragma unroll
@@ -270,10 +292,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 // ------------------------------------------------------------------------------- backward: dQ
 // Also computes delta = rowsum(dO * O) and publishes the per-row constants the dK/dV kernel
 // initialises its accumulators with (rowstat), so no separate preprocess pass reads dO and O.
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int NS>
 __device__ __forceinline__ void attn_dq_body(const Args& a) {
   constexpr int DK = D / 16, DB = D / 32, TILE = KT * 2 * D;
-  __shared__ __attribute__((aligned(16))) char lds[2][2 * TILE];
+  __shared__ __attribute__((aligned(16))) char lds[NS][2 * TILE];
   const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int h = lane >> 5;
   const int nbh = a.B * a.Hq, bid = blockIdx.x;
@@ -314,21 +336,21 @@ __device__ __forceinline__ void attn_dq_body(const Args& a) {
   for (int db = 0; db < DB; ++db)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dq[db][r] = 0.f;
-  if (ntile > 0) {
-    stage_tile<D>(lds[0], kb, a.kss, 0, kv_end, w, lane);
-    stage_tile<D>(lds[0] + TILE, vb, a.vss, 0, kv_end, w, lane);
+  for (int p = 0; p < NS - 1 && p < ntile; ++p) {
+    stage_tile<D>(lds[p], kb, a.kss, p * KT, kv_end, w, lane);
+    stage_tile<D>(lds[p] + TILE, vb, a.vss, p * KT, kv_end, w, lane);
   }
   for (int it = 0; it < ntile; ++it) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wait_tile<NS>(it + 1 < ntile, 2 * tile_glds<D>());
     __syncthreads();
-    if (it + 1 < ntile) {
-      char* nb = lds[(it + 1) & 1];
-      stage_tile<D>(nb, kb, a.kss, (it + 1) * KT, kv_end, w, lane);
-      stage_tile<D>(nb + TILE, vb, a.vss, (it + 1) * KT, kv_end, w, lane);
+    if (it + NS - 1 < ntile) {
+      char* nb = lds[(it + NS - 1) % NS];
+      stage_tile<D>(nb, kb, a.kss, (it + NS - 1) * KT, kv_end, w, lane);
+      stage_tile<D>(nb + TILE, vb, a.vss, (it + NS - 1) * KT, kv_end, w, lane);
     }
     const int k0 = it * KT;
     if (CAUSAL && k0 > qw0 + 31) continue;
-    const char* Kt = lds[it & 1];
+    const char* Kt = lds[it % NS];
     const char* Vt = Kt + TILE;
     f32x16 s[2], dp[2];
 #pragma unroll
@@ -377,10 +399,10 @@ __device__ __forceinline__ void attn_dq_body(const Args& a) {
 }
 
 // ---------------------------------------------------------------------------- backward: dK, dV
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int NS>
 __device__ __forceinline__ void attn_dkdv_body(const Args& a) {
   constexpr int DK = D / 16, DB = D / 32, TILE = KT * 2 * D, STG = 2 * TILE + 512;
-  __shared__ __attribute__((aligned(16))) char lds[2][STG];
+  __shared__ __attribute__((aligned(16))) char lds[NS][STG];
   const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int h = lane >> 5;
   const int G = a.Hq / a.Hkv, gper = G / a.gsplit;
@@ -423,14 +445,15 @@ __device__ __forceinline__ void attn_dkdv_body(const Args& a) {
     if (w == 0 && lane < 32)
       glds16(a.rowstat + (((int64_t)b * a.Hq + hq) * ntq64 + qt) * 128 + 4 * lane, buf + 2 * TILE);
   };
-  if (niter > 0) stage(0, lds[0]);
+  for (int p = 0; p < NS - 1 && p < niter; ++p) stage(p, lds[p]);
   for (int it = 0; it < niter; ++it) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // wave 0 also issues the rowstat DMA of each stage
+    wait_tile<NS>(it + 1 < niter, 2 * tile_glds<D>() + (w == 0 ? 1 : 0));
     __syncthreads();
-    if (it + 1 < niter) stage(it + 1, lds[(it + 1) & 1]);
+    if (it + NS - 1 < niter) stage(it + NS - 1, lds[(it + NS - 1) % NS]);
     const int qt = qt0 + it % per, qs0 = qt * KT;
     if (!wave_live || (CAUSAL && qs0 + KT - 1 < kw0)) continue;  // every query row before the wave's keys
-    const char* Qt = lds[it & 1];
+    const char* Qt = lds[it % NS];
     const char* Ot = Qt + TILE;  // dO
     const float* rs = reinterpret_cast<const float*>(Qt + 2 * TILE);
 #pragma unroll
@@ -503,21 +526,21 @@ __device__ __forceinline__ void attn_dkdv_body(const Args& a) {
 
 // Register budgets: the head-dim-64 backward kernels fit two waves per SIMD (<= 256 registers);
 // the head-dim-128 ones would spill there, so they keep one wave per SIMD and every register.
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int NS = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_attn_dq(Args a) {
-  attn_dq_body<D, CAUSAL>(a);
+  attn_dq_body<D, CAUSAL, NS>(a);
 }
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int NS = 2>
 __global__ __launch_bounds__(256) void k_attn_dq_wide(Args a) {
-  attn_dq_body<D, CAUSAL>(a);
+  attn_dq_body<D, CAUSAL, NS>(a);
 }
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int NS = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_attn_dkdv(Args a) {
-  attn_dkdv_body<D, CAUSAL>(a);
+  attn_dkdv_body<D, CAUSAL, NS>(a);
 }
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int NS = 2>
 __global__ __launch_bounds__(256) void k_attn_dkdv_wide(Args a) {
-  attn_dkdv_body<D, CAUSAL>(a);
+  attn_dkdv_body<D, CAUSAL, NS>(a);
 }
 
 // dK / dV of a split GQA group: sum the slices in order (deterministic), cast to bf16 into the
@@ -587,18 +610,44 @@ Args make_args(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, bo
 
 }  // namespace
 
-#define ATTN_DISPATCH2(KER64, KER128, D_, CAUSAL_, GRID, A)                                       \
+// LDS stages of the streamed tiles: 2 (HIPPS_ATTN_STAGES=3: the three-stage form, A/B).  Measured
+// same-box (profiles/r6/attn/attn_stages_ab.txt): 3 stages cost the forward and the BERT backward
+// (the LDS of a third stage takes the second workgroup per CU) and did not help the causal
+// backward either (Llama-3-1B 0.462 / 0.467 ms with 2 vs 0.488 / 0.501 with 3) -- the kernels are
+// not waiting on the tile DMA
+int attn_stages(bool causal, bool backward) {
+  static const int env = [] {
+    const char* e = std::getenv("HIPPS_ATTN_STAGES");
+    return e ? std::atoi(e) : 0;
+  }();
+  (void)causal;
+  (void)backward;
+  return env == 3 ? 3 : 2;
+}
+
+#define ATTN_DISPATCH2(KER64, KER128, D_, CAUSAL_, BWD_, GRID, A)                                 \
   do {                                                                                             \
     auto st = c10::hip::getCurrentHIPStream();                                                     \
+    const bool s3 = attn::attn_stages(CAUSAL_, BWD_) == 3;                                         \
     if ((D_) == 64) {                                                                              \
-      if (CAUSAL_) hipLaunchKernelGGL((KER64<64, true>), dim3(GRID), dim3(256), 0, st, A);          \
-      else hipLaunchKernelGGL((KER64<64, false>), dim3(GRID), dim3(256), 0, st, A);                 \
+      if (CAUSAL_) {                                                                               \
+        if (s3) hipLaunchKernelGGL((KER64<64, true, 3>), dim3(GRID), dim3(256), 0, st, A);          \
+        else hipLaunchKernelGGL((KER64<64, true, 2>), dim3(GRID), dim3(256), 0, st, A);             \
+      } else {                                                                                     \
+        if (s3) hipLaunchKernelGGL((KER64<64, false, 3>), dim3(GRID), dim3(256), 0, st, A);         \
+        else hipLaunchKernelGGL((KER64<64, false, 2>), dim3(GRID), dim3(256), 0, st, A);            \
+      }                                                                                            \
     } else {                                                                                       \
-      if (CAUSAL_) hipLaunchKernelGGL((KER128<128, true>), dim3(GRID), dim3(256), 0, st, A);        \
-      else hipLaunchKernelGGL((KER128<128, false>), dim3(GRID), dim3(256), 0, st, A);               \
+      if (CAUSAL_) {                                                                               \
+        if (s3) hipLaunchKernelGGL((KER128<128, true, 3>), dim3(GRID), dim3(256), 0, st, A);        \
+        else hipLaunchKernelGGL((KER128<128, true, 2>), dim3(GRID), dim3(256), 0, st, A);           \
+      } else {                                                                                     \
+        if (s3) hipLaunchKernelGGL((KER128<128, false, 3>), dim3(GRID), dim3(256), 0, st, A);       \
+        else hipLaunchKernelGGL((KER128<128, false, 2>), dim3(GRID), dim3(256), 0, st, A);          \
+      }                                                                                            \
     }                                                                                              \
   } while (0)
-#define ATTN_DISPATCH(KER, D_, CAUSAL_, GRID, A) ATTN_DISPATCH2(KER, KER, D_, CAUSAL_, GRID, A)
+#define ATTN_DISPATCH(KER, D_, CAUSAL_, GRID, A) ATTN_DISPATCH2(KER, KER, D_, CAUSAL_, false, GRID, A)
 
 }  // namespace attn
 
@@ -660,7 +709,7 @@ std::vector<at::Tensor> attn_backward(at::Tensor dout, at::Tensor q, at::Tensor 
   at::Tensor rowstat = at::empty({(int64_t)a.B * a.Hq * 2 * a.nblk * 128}, q.options().dtype(at::kFloat));
   a.rowstat = rowstat.data_ptr<float>();
   const int64_t gq = (int64_t)a.nblk * a.B * a.Hq;
-  ATTN_DISPATCH2(attn::k_attn_dq, attn::k_attn_dq_wide, D, causal, (unsigned)gq, a);
+  ATTN_DISPATCH2(attn::k_attn_dq, attn::k_attn_dq_wide, D, causal, true, (unsigned)gq, a);
   // dK / dV: split the GQA group over workgroups when the (batch, kv head, key block) grid is
   // small: under the causal mask the first key block of a sequence sweeps every query tile and
   // the last one a single tile, so a grid that fits the GPU in one wave runs as long as its
@@ -679,7 +728,7 @@ std::vector<at::Tensor> attn_backward(at::Tensor dout, at::Tensor q, at::Tensor 
   }
   a.nblk = nkb;
   const int64_t gk = (int64_t)nkb * a.B * a.Hkv * gsplit;
-  ATTN_DISPATCH2(attn::k_attn_dkdv, attn::k_attn_dkdv_wide, D, causal, (unsigned)gk, a);
+  ATTN_DISPATCH2(attn::k_attn_dkdv, attn::k_attn_dkdv_wide, D, causal, true, (unsigned)gk, a);
   if (gsplit > 1) {
     const int64_t n = dk.numel();
     const int grid = (int)std::min<int64_t>(2048, (2 * n / 4 + 255) / 256);
