@@ -292,7 +292,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_fwd(const uint16_t* __restr
                                                          const float* __restrict__ scale,
                                                          const float* __restrict__ shift, int64_t M, int C, int relu,
                                                          const float* __restrict__ rsc = nullptr,
-                                                         const float* __restrict__ rsh = nullptr) {
+                                                         const float* __restrict__ rsh = nullptr, int pack_bits = 1) {
   const int G = C >> 3;
   const int64_t V = M * (int64_t)G, stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -324,7 +324,16 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply_fwd(const uint16_t* __restr
       uint32_t b = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) b |= (xv[j] > 0.f ? 1u : 0u) << j;
-      mbits[v] = (uint8_t)b;
+      // a full wave's 64 bytes as 16 dword stores (4 lanes' bytes gathered by DPP-free shuffles)
+      // instead of 64 byte stores; the last, partial wave of the tensor stores bytes
+      const int lane = threadIdx.x & 63;
+      // (UNR == 2 splits a wave between its paired and remainder loops: bytes only)
+      if (pack_bits && UNR != 2 && v - lane + 63 < V) {
+        const uint32_t b1 = __shfl_down(b, 1, 64), b2 = __shfl_down(b, 2, 64), b3 = __shfl_down(b, 3, 64);
+        if ((lane & 3) == 0) *reinterpret_cast<uint32_t*>(mbits + v) = b | (b1 << 8) | (b2 << 16) | (b3 << 24);
+      } else {
+        mbits[v] = (uint8_t)b;
+      }
     }
   };
   int64_t v = v0;
@@ -572,7 +581,15 @@ int apply_grid(int64_t M, int C) {
 // forward apply: UNR vectors in flight per lane on the large (>= 4 M-vector, layer-1/2) tensors
 // when HIPPS_BN_APPLY_UNR=2 (A/B; 1 measured no slower on the layer-3/4 sizes)
 typedef void (*ApplyFwdFn)(const uint16_t*, const uint16_t*, uint16_t*, uint8_t*, const float*, const float*, int64_t,
-                           int, int, const float*, const float*);
+                           int, int, const float*, const float*, int);
+// the ReLU mask bytes of a full wave as 16 dword stores (HIPPS_BN_BITS_PACK=0: 64 byte stores, A/B)
+int bits_pack() {
+  static const int on = [] {
+    const char* e = std::getenv("HIPPS_BN_BITS_PACK");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return on;
+}
 ApplyFwdFn apply_fwd_kernel(int64_t M, int C) {
   static const int unr = [] {
     const char* e = std::getenv("HIPPS_BN_APPLY_UNR");
@@ -606,7 +623,7 @@ void finalize_apply_fwd(const at::Tensor& part, int nrb, const at::Tensor& x, co
                      shift.data_ptr<float>());
   hipLaunchKernelGGL(apply_fwd_kernel(M, (int)C), apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)x.data_ptr(), rp,
                      (uint16_t*)y.data_ptr(), mo, scale.data_ptr<float>(), shift.data_ptr<float>(), M, (int)C,
-                     (int)relu, nullptr, nullptr);
+                     (int)relu, nullptr, nullptr, bits_pack());
 }
 }  // namespace
 
@@ -742,7 +759,7 @@ void bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, at::Ten
   check_vec(shift, "shift", (int)C);
   hipLaunchKernelGGL(apply_fwd_kernel(M, (int)C), apply_grid(M, (int)C), kBlock, 0, c10::hip::getCurrentHIPStream(),
                      (const uint16_t*)x.data_ptr(), rp, (uint16_t*)y.data_ptr(), nullptr, scale.data_ptr<float>(),
-                     shift.data_ptr<float>(), M, (int)C, (int)relu, nullptr, nullptr);
+                     shift.data_ptr<float>(), M, (int)C, (int)relu, nullptr, nullptr, bits_pack());
 }
 
 // returns nothing; writes dx (and dres), dweight, dbias
@@ -963,7 +980,7 @@ void bn_dual_forward(at::Tensor part3, int64_t nrb3, at::Tensor partd, int64_t n
   hipLaunchKernelGGL(apply_fwd_kernel(M, (int)C), apply_grid(M, (int)C), kBlock, 0, stream, (const uint16_t*)x3.data_ptr(),
                      (const uint16_t*)xd.data_ptr(), (uint16_t*)z.data_ptr(), (uint8_t*)mask.data_ptr(),
                      scale3.data_ptr<float>(), shift3.data_ptr<float>(), M, (int)C, 1, scaled.data_ptr<float>(),
-                     shiftd.data_ptr<float>());
+                     shiftd.data_ptr<float>(), bits_pack());
 }
 
 // Backward of bn_dual_forward: dx3 (bn3's input gradient), dxd (the downsample BN's), the four
