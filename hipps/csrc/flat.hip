@@ -100,7 +100,11 @@ __device__ __forceinline__ void pub_store1(void* pub, int pub_mode, int64_t i, f
 }
 
 // ------------------------------------------------------------------------------------------
-// k_aggregate: acc = (accumulate ? acc : 0) + gscale * sum_w slot_w
+// k_aggregate: acc = gscale * sum_w slot_w (rank order), or with ``accumulate`` (the async PS
+// adding the messages that arrived) acc = (((acc + g*slot_0) + g*slot_1) + ...) -- each message
+// added on its own, without contraction, so the result does not depend on how arriving messages
+// were batched into launches (it did: identical messages summed as {a, a, a} or {a}, {a, a}
+// rounded differently -- tests/test_multigpu.py's same-device determinism case failed once)
 // ------------------------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_aggregate(SlotPtrs g, int W, float gscale, float* __restrict__ acc,
@@ -109,17 +113,31 @@ __global__ __launch_bounds__(kBlock) void k_aggregate(SlotPtrs g, int W, float g
   const int64_t nv = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
     const int64_t i = v << 2;
-    float4 d = sum_slots4<T>(g, W, i, gscale);
+    float4 d;
     if (accumulate) {
-      float4 a = Vec4<float>::load(acc, i);
-      d.x += a.x; d.y += a.y; d.z += a.z; d.w += a.w;
+      d = Vec4<float>::load(acc, i);
+      for (int w = 0; w < W; ++w) {
+        const float4 s = Vec4<T>::load(reinterpret_cast<const T*>(g.p[w]), i);
+        d.x = __fadd_rn(d.x, __fmul_rn(s.x, gscale));
+        d.y = __fadd_rn(d.y, __fmul_rn(s.y, gscale));
+        d.z = __fadd_rn(d.z, __fmul_rn(s.z, gscale));
+        d.w = __fadd_rn(d.w, __fmul_rn(s.w, gscale));
+      }
+    } else {
+      d = sum_slots4<T>(g, W, i, gscale);
     }
     Vec4<float>::store(acc, i, d);
   }
   if (blockIdx.x == 0) {
     for (int64_t i = (nv << 2) + threadIdx.x; i < n; i += blockDim.x) {
-      float d = sum_slots1<T>(g, W, i, gscale);
-      acc[i] = accumulate ? acc[i] + d : d;
+      if (accumulate) {
+        float d = acc[i];
+        for (int w = 0; w < W; ++w)
+          d = __fadd_rn(d, __fmul_rn(Vec4<T>::load1(reinterpret_cast<const T*>(g.p[w]), i), gscale));
+        acc[i] = d;
+      } else {
+        acc[i] = sum_slots1<T>(g, W, i, gscale);
+      }
     }
   }
 }

@@ -191,7 +191,9 @@ __global__ __launch_bounds__(kBlock) void k_q8_encode_rows(const float* __restri
   }
 }
 
-// acc (+)= gscale * sum_w deq(q_w, s_w)   — rank-ordered, 4 elements per lane
+// acc = gscale * sum_w deq(q_w, s_w) (rank order, 4 elements per lane), or with ``accumulate``
+// acc = ((acc + g*deq_0) + g*deq_1) + ... -- each message on its own, no contraction: batch-
+// invariant, as flat.hip k_aggregate
 __global__ __launch_bounds__(kBlock) void k_q8_aggregate(SlotPtrs qs, SlotPtrs ss, int W, float gscale,
                                                          float* __restrict__ acc, int64_t n, int accumulate,
                                                          int acquire) {
@@ -200,6 +202,31 @@ __global__ __launch_bounds__(kBlock) void k_q8_aggregate(SlotPtrs qs, SlotPtrs s
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
     const int64_t i = v << 2;
     const int64_t blk = i / kQBlock;
+    if (accumulate) {
+      if (i + 4 <= n) {
+        float4 a = *reinterpret_cast<const float4*>(acc + i);
+        for (int w = 0; w < W; ++w) {
+          const char4 c = *reinterpret_cast<const char4*>(reinterpret_cast<const int8_t*>(qs.p[w]) + i);
+          const float s = reinterpret_cast<const float*>(ss.p[w])[blk];
+          a.x = __fadd_rn(a.x, __fmul_rn(__fmul_rn((float)c.x, s), gscale));
+          a.y = __fadd_rn(a.y, __fmul_rn(__fmul_rn((float)c.y, s), gscale));
+          a.z = __fadd_rn(a.z, __fmul_rn(__fmul_rn((float)c.z, s), gscale));
+          a.w = __fadd_rn(a.w, __fmul_rn(__fmul_rn((float)c.w, s), gscale));
+        }
+        *reinterpret_cast<float4*>(acc + i) = a;
+      } else {
+        for (int j = 0; j < 4 && i + j < n; ++j) {
+          float a = acc[i + j];
+          for (int w = 0; w < W; ++w) {
+            const int8_t* q = reinterpret_cast<const int8_t*>(qs.p[w]);
+            const float s = reinterpret_cast<const float*>(ss.p[w])[blk];
+            a = __fadd_rn(a, __fmul_rn(__fmul_rn((float)q[i + j], s), gscale));
+          }
+          acc[i + j] = a;
+        }
+      }
+      continue;
+    }
     float d[4] = {0.f, 0.f, 0.f, 0.f};
     const bool full = i + 4 <= n;
     for (int w = 0; w < W; ++w) {

@@ -24,6 +24,10 @@ def _f32(t: torch.Tensor) -> torch.Tensor:
 
 
 def aggregate(slots: Sequence[torch.Tensor], acc: torch.Tensor, gscale: float = 1.0, accumulate: bool = False):
+    if accumulate:  # each message added on its own (batch-invariant; csrc/flat.hip k_aggregate)
+        for s in slots:
+            acc.add_(_f32(s) * gscale if gscale != 1.0 else _f32(s))
+        return
     d = _f32(slots[0]).clone()
     for s in slots[1:]:  # rank order (ps.py:176 `sum(grads)`)
         d += _f32(s)
@@ -218,6 +222,10 @@ def q8_dequant(q, scales):
 
 
 def q8_aggregate(qs, ss, acc, gscale=1.0, accumulate=False):
+    if accumulate:  # each message added on its own (batch-invariant; csrc/quant.hip k_q8_aggregate)
+        for q, s in zip(qs, ss):
+            acc.add_(q8_dequant(q, s) * gscale)
+        return
     d = q8_dequant(qs[0], ss[0])
     for q, s in zip(qs[1:], ss[1:]):
         d += q8_dequant(q, s)

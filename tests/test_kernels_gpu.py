@@ -408,3 +408,45 @@ def test_copy_acquire(n):
     dst = torch.zeros(n, dtype=torch.uint8, device=DEV)
     ops.copy_acquire(src, dst)
     assert torch.equal(src, dst)
+
+
+@pytest.mark.parametrize("codec", ["dense_f32", "dense_bf16", "int8"])
+def test_ps_accumulate_is_batch_invariant(codec):
+    """The async PS adds arriving messages in launches of whatever arrived together: the result
+    must not depend on that batching (one launch of [a, b, c] == [a] then [b, c], bitwise), and it
+    matches the reference's per-message sequence."""
+    torch.manual_seed(7)
+    n = 5000
+    acc0 = torch.randn(n, device=DEV)
+    if codec == "int8":
+        msgs = []
+        for _ in range(3):
+            x = torch.randn(n, device=DEV)
+            q = torch.empty(n, dtype=torch.int8, device=DEV)
+            s = torch.empty((n + 255) // 256, device=DEV)
+            ops.q8_encode(x, None, q, s, False, 0)
+            msgs.append((q, s))
+
+        def add(ms, acc):
+            ops.q8_aggregate([m[0] for m in ms], [m[1] for m in ms], acc, 1 / 3, True)
+        want = acc0.cpu().clone()
+        ref.q8_aggregate([m[0].cpu() for m in msgs], [m[1].cpu() for m in msgs], want, 1 / 3, True)
+    else:
+        dt = torch.float32 if codec == "dense_f32" else torch.bfloat16
+        msgs = [torch.randn(n, device=DEV).to(dt) for _ in range(3)]
+
+        def add(ms, acc):
+            ops.aggregate(ms, acc, 1 / 3, True)
+        want = acc0.cpu().clone()
+        ref.aggregate([m.cpu() for m in msgs], want, 1 / 3, True)
+    one = acc0.clone()
+    add(msgs, one)
+    two = acc0.clone()
+    add(msgs[:1], two)
+    add(msgs[1:], two)
+    three = acc0.clone()
+    for m in msgs:
+        add([m], three)
+    assert torch.equal(one, two) and torch.equal(one, three)
+    # (the CPU reference scales by the Python double 1/3; the kernel by its float rounding)
+    torch.testing.assert_close(one.cpu(), want, rtol=1e-6, atol=1e-6)
