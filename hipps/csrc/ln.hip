@@ -27,6 +27,12 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kLnWaves = 4;  // rows in flight per workgroup
 
+template <int N> __device__ __forceinline__ float wsum_n(float v) {  // sum over aligned groups of N lanes
+#pragma unroll
+  for (int o = N / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
 __device__ __forceinline__ float wsum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -105,19 +111,23 @@ __global__ __launch_bounds__(64 * kLnWaves) void k_ln_fwd(const uint16_t* __rest
 // -> part[blockIdx.x] (2 x D floats: dgamma partial, dbeta partial)
 // DXS: a third column sum, of the bf16 dx written (the bias gradient of the Linear whose output
 // this LayerNorm normalised -- BERT's attn_out / out: their colsum pass over dx is saved)
-template <int NC, bool DXS = false>
+// LPR (lanes per row) 32: each half-wave takes a row -- D = 768's 96 chunks as 3 per lane on
+// 32 lanes instead of 2 on half of 64 (half the lanes idle in the second chunk)
+template <int NC, bool DXS = false, int LPR = 64>
 __global__ __launch_bounds__(64 * kLnWaves) void k_ln_bwd(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
                                                           const float* __restrict__ mean, const float* __restrict__ rstd,
                                                           const float* __restrict__ w, uint16_t* __restrict__ dx,
                                                           float* __restrict__ part, int64_t R, int D, int rpb) {
   constexpr int NK = DXS ? 3 : 2;
   extern __shared__ float red[];  // [kLnWaves][NK][D]
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane64 = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  constexpr int RPW = 64 / LPR;                 // rows per wave at a time
+  const int lane = lane64 & (LPR - 1), hrow = lane64 / LPR;
   const int nch = D >> 3;
   float ww[NC][8];
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    const int ch = lane + 64 * c;
+    const int ch = lane + LPR * c;
     const int cc = ch < nch ? ch : 0;
     const float4 w0 = *reinterpret_cast<const float4*>(w + cc * 8), w1 = *reinterpret_cast<const float4*>(w + cc * 8 + 4);
     ww[c][0] = w0.x; ww[c][1] = w0.y; ww[c][2] = w0.z; ww[c][3] = w0.w;
@@ -145,7 +155,7 @@ __global__ __launch_bounds__(64 * kLnWaves) void k_ln_bwd(const uint16_t* __rest
       nrs = rstd[row];
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        const int ch = lane + 64 * c;
+        const int ch = lane + LPR * c;
         if (ch < nch) {
           nx[c] = *reinterpret_cast<const u32x4*>(x + row * D + ch * 8);
           ndy[c] = *reinterpret_cast<const u32x4*>(dy + row * D + ch * 8);
@@ -153,8 +163,8 @@ __global__ __launch_bounds__(64 * kLnWaves) void k_ln_bwd(const uint16_t* __rest
       }
     }
   };
-  fetch(r0 + wv);
-  for (int64_t row = r0 + wv; row < r1; row += kLnWaves) {
+  fetch(r0 + wv * RPW + hrow);
+  for (int64_t row = r0 + wv * RPW + hrow; row < r1; row += kLnWaves * RPW) {
     const float mu = nmu, rs = nrs;
     u32x4 cx[NC], cdy[NC];
 #pragma unroll
@@ -162,12 +172,12 @@ __global__ __launch_bounds__(64 * kLnWaves) void k_ln_bwd(const uint16_t* __rest
       cx[c] = nx[c];
       cdy[c] = ndy[c];
     }
-    fetch(row + kLnWaves);
+    fetch(row + kLnWaves * RPW);
     float xh[NC][8], g[NC][8], gy[NC][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      const int ch = lane + 64 * c;
+      const int ch = lane + LPR * c;
       if (ch < nch) {
         float xv[8];
         unpack8(cx[c], xv);
@@ -181,10 +191,10 @@ __global__ __launch_bounds__(64 * kLnWaves) void k_ln_bwd(const uint16_t* __rest
         }
       }
     }
-    const float m1 = wsum(s1) / D, m2 = wsum(s2) / D;
+    const float m1 = wsum_n<LPR>(s1) / D, m2 = wsum_n<LPR>(s2) / D;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      const int ch = lane + 64 * c;
+      const int ch = lane + LPR * c;
       if (ch < nch) {
         u32x4 o;
 #pragma unroll
@@ -207,11 +217,21 @@ __global__ __launch_bounds__(64 * kLnWaves) void k_ln_bwd(const uint16_t* __rest
       }
     }
   }
-  // fold the waves' column sums in a fixed order
+  // fold the waves' column sums in a fixed order (LPR 32: the two half-waves' first, lane l + l^32)
+  if constexpr (LPR == 32) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        dg[c][j] += __shfl_xor(dg[c][j], 32, 64);
+        db[c][j] += __shfl_xor(db[c][j], 32, 64);
+        if constexpr (DXS) dsx[DXS ? c : 0][j] += __shfl_xor(dsx[DXS ? c : 0][j], 32, 64);
+      }
+  }
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    const int ch = lane + 64 * c;
-    if (ch < nch) {
+    const int ch = lane + LPR * c;
+    if (ch < nch && hrow == 0) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         red[(wv * NK) * D + ch * 8 + j] = dg[c][j];
@@ -552,7 +572,24 @@ void ln_backward(at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor rstd, 
   hipLaunchKernelGGL((k_ln_bwd<NCc, DX>), (int)P, 64 * kLnWaves, lds, st, (const uint16_t*)dy.data_ptr(),            \
                      (const uint16_t*)x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), w.data_ptr<float>(), \
                      (uint16_t*)dx.data_ptr(), part.data_ptr<float>(), R, (int)D, rpb)
-  if (dxs) {
+  // opt-in (HIPPS_LN_HALF=1): a row per half-wave, 3 chunks per lane for D 520..768 -- measured
+  // slower in the BERT-base step (803.4 / 804.0 k vs 813.4 / 813.8 k tokens/s, same box,
+  // profiles/r6/ab_ln_half/): the 64-lane form's idle half-chunk costs less than the half-wave
+  // form's extra row state and cross-half fold
+  static const bool half = [] {
+    const char* e = std::getenv("HIPPS_LN_HALF");
+    return e && e[0] == '1';
+  }();
+  if (half && D / 8 > 64 && D / 8 <= 96) {  // D 520..768: a row per half-wave, 3 chunks per lane
+    if (dxs)
+      hipLaunchKernelGGL((k_ln_bwd<3, true, 32>), (int)P, 64 * kLnWaves, lds, st, (const uint16_t*)dy.data_ptr(),
+                         (const uint16_t*)x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                         w.data_ptr<float>(), (uint16_t*)dx.data_ptr(), part.data_ptr<float>(), R, (int)D, rpb);
+    else
+      hipLaunchKernelGGL((k_ln_bwd<3, false, 32>), (int)P, 64 * kLnWaves, lds, st, (const uint16_t*)dy.data_ptr(),
+                         (const uint16_t*)x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                         w.data_ptr<float>(), (uint16_t*)dx.data_ptr(), part.data_ptr<float>(), R, (int)D, rpb);
+  } else if (dxs) {
     if (nc <= 1) HIPPS_LNB(1, true);
     else if (nc <= 2) HIPPS_LNB(2, true);
     else HIPPS_LNB(4, true);
